@@ -1,0 +1,137 @@
+/*
+ * imagekit_hip.h -- C ABI of libimagekit_hip.so, the MI355X-native drop-in for
+ * the reference's transform hot path (Shreyas2409/Rust-Image-Transform,
+ * crate `imagekit`, module `imagekit::transform`).
+ *
+ * The reference has no plugin registry: its "operator API" is three free Rust
+ * functions (src/transform.rs) called by the /img and /upload handlers
+ * (src/lib.rs:175,180,188 and :281,286,294).  Each entry point below names the
+ * reference item it replaces.  Plain pointers and sizes only; images are
+ * device-resident handles (ik_image) so a decode -> resize -> encode chain
+ * keeps pixels in HBM.  All functions are thread-safe; errors are reported as
+ * an ik_status plus a thread-local message (ik_last_error), never a panic or
+ * abort across the ABI (reference: every failure maps to
+ * ImageKitError::TransformError, src/lib.rs:34-52).
+ */
+#ifndef IMAGEKIT_HIP_H
+#define IMAGEKIT_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ImageFormat (reference src/config.rs:11-17): jpeg, webp, avif */
+typedef enum { IK_FORMAT_JPEG = 0, IK_FORMAT_WEBP = 1, IK_FORMAT_AVIF = 2 } ik_format;
+
+/* image::imageops::FilterType (image 0.25.8).  The reference always uses
+ * Lanczos3 (src/transform.rs:88); the others are extensions. */
+typedef enum {
+    IK_FILTER_NEAREST = 0,
+    IK_FILTER_TRIANGLE = 1,
+    IK_FILTER_CATMULLROM = 2,
+    IK_FILTER_GAUSSIAN = 3,
+    IK_FILTER_LANCZOS3 = 4
+} ik_filter;
+
+typedef enum {
+    IK_OK = 0,
+    IK_ERR_TRANSFORM = 1,   /* ImageKitError::TransformError (decode/encode failure) */
+    IK_ERR_INVALID = 2,     /* bad argument (null pointer, zero size, bad enum)    */
+    IK_ERR_DEVICE = 3,      /* HIP runtime failure                                  */
+    IK_ERR_UNSUPPORTED = 4, /* recognised but not compiled in (e.g. AVIF decode)    */
+    IK_ERR_NOMEM = 5
+} ik_status;
+
+/* DynamicImage (image 0.25.8): 8-bit, 1..4 interleaved channels
+ * (Luma8, LumaA8, Rgb8, Rgba8), pixels resident in device memory. */
+typedef struct ik_image ik_image;
+
+/* ---- runtime ---------------------------------------------------------- */
+int ik_init(int device);                /* select the HIP device for this thread; -1 = keep */
+int ik_device_count(void);
+size_t ik_last_error(char *buf, size_t cap); /* thread-local message of the last failure */
+const char *ik_version(void);
+
+/* ---- image handles ---------------------------------------------------- */
+/* ImageBuffer::from_raw: copy a tightly packed host buffer to the device */
+int ik_image_from_host(const uint8_t *pixels, uint32_t width, uint32_t height, uint32_t channels,
+                       ik_image **out);
+/* wrap an existing device buffer (not owned; must outlive the handle) */
+int ik_image_wrap_device(uint8_t *dev_pixels, uint32_t width, uint32_t height, uint32_t channels,
+                         size_t pitch, ik_image **out);
+int ik_image_info(const ik_image *img, uint32_t *width, uint32_t *height, uint32_t *channels);
+int ik_image_to_host(const ik_image *img, uint8_t *dst, size_t cap); /* tightly packed */
+void ik_image_free(ik_image *img);
+void ik_buf_free(uint8_t *buf);
+
+/* ---- the three reference functions ------------------------------------ */
+/* decode_image (src/transform.rs:27-43): guess_format + load_from_memory_with_format.
+ * *fmt_out = IK_FORMAT_* for webp/jpeg/avif, -1 (None) for other formats. */
+int ik_decode(const uint8_t *bytes, size_t len, ik_image **out, int *fmt_out);
+
+/* resize_image (src/transform.rs:62-90).  w/h < 0 mean None.  Both None returns
+ * the input unchanged (*out == img); otherwise a new image (img is not freed:
+ * the Rust shim drops its by-value argument).  filter: IK_FILTER_* (Lanczos3 in
+ * the reference). */
+int ik_resize(ik_image *img, int64_t w, int64_t h, int filter, ik_image **out);
+
+/* imageops::resize to exact dimensions (the resampler under resize_image) */
+int ik_resize_exact(const ik_image *img, uint32_t nw, uint32_t nh, int filter, ik_image **out);
+
+/* encode_image (src/transform.rs:113-150): quality clamped to [1,100].
+ * *out is allocated by the library; release with ik_buf_free. */
+int ik_encode(const ik_image *img, int fmt, int quality, uint8_t **out, size_t *out_len);
+
+/* ---- fused / batched entry points (pixels stay in HBM) ----------------- */
+/* decode -> resize_image -> encode_image in one call (handler src/lib.rs:175-191) */
+int ik_transform(const uint8_t *bytes, size_t len, int64_t w, int64_t h, int fmt, int quality,
+                 int filter, uint8_t **out, size_t *out_len);
+
+/* A batch of n same-geometry 8-bit images already resident in device memory
+ * (image i at dev_src + i*src_image_stride, rows src_pitch bytes apart) ->
+ * resize to nw x nh -> encode.  Encoded bytes are written into the caller's
+ * host buffer `out` (capacity out_cap) back to back; out_sizes[i] receives each
+ * size.  threads = host entropy-coder threads (0 = default). */
+typedef struct ik_pipeline ik_pipeline;
+int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t nh, int filter,
+                       int fmt, int quality, uint32_t max_batch, int threads, ik_pipeline **out);
+int ik_pipeline_run(ik_pipeline *p, const uint8_t *dev_src, size_t src_pitch,
+                    size_t src_image_stride, uint32_t n, uint8_t *out, size_t out_cap,
+                    size_t *out_sizes);
+/* device-only part (resize + colour convert/FDCT) for n images, no host stage */
+int ik_pipeline_run_device(ik_pipeline *p, const uint8_t *dev_src, size_t src_pitch,
+                           size_t src_image_stride, uint32_t n);
+/* average device time (ms) per launch of kernel `which` (0 = resize, 1 = colour
+ * convert) over the last run, from HIP events on the pipeline's stream */
+double ik_pipeline_kernel_ms(const ik_pipeline *p, int which);
+/* resized pixels of image i of the last run (tightly packed nw*nh*C) */
+int ik_pipeline_fetch_resized(ik_pipeline *p, uint32_t i, uint8_t *dst, size_t cap);
+void ik_pipeline_destroy(ik_pipeline *p);
+
+/* raw device kernels, for parity tests and the bench (dev_* = device pointers) */
+int ik_resize_batch_device(const uint8_t *dev_src, uint32_t W, uint32_t H, uint32_t C,
+                           size_t src_pitch, size_t src_image_stride, uint32_t n, uint32_t nw,
+                           uint32_t nh, int filter, uint8_t *dev_dst, size_t dst_pitch,
+                           size_t dst_image_stride, void *hip_stream);
+/* the WebP colour conversion (to_rgb8 + libwebp RGB->YUV420) on the device;
+ * dev_yuv receives the Y (w*h), U and V ((w+1)/2 * (h+1)/2) planes back to back */
+int ik_webp_yuv420_device(const uint8_t *dev_src, uint32_t w, uint32_t h, uint32_t C,
+                          size_t pitch, uint8_t *dev_yuv, void *hip_stream);
+/* the JPEG front end (to_rgb8 + RGB->YCbCr + FDCT + quantise) on the device:
+ * int16 coefficients, MCU-major, Y/Cb/Cr, natural order */
+int ik_jpeg_coeffs_device(const uint8_t *dev_src, uint32_t w, uint32_t h, uint32_t C,
+                          size_t pitch, int quality, int16_t *dev_coef, void *hip_stream);
+
+/* device memory helpers (so callers need no HIP headers) */
+int ik_dev_alloc(size_t bytes, void **dev_ptr);
+int ik_dev_free(void *dev_ptr);
+int ik_memcpy_h2d(void *dev_dst, const void *host_src, size_t bytes);
+int ik_memcpy_d2h(void *host_dst, const void *dev_src, size_t bytes);
+int ik_dev_synchronize(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,438 @@
+// ik_host.cpp -- the C ABI of libimagekit_hip.so (include/imagekit_hip.h).
+//
+// Mirrors reference src/transform.rs: decode_image (:27-43), resize_image
+// (:62-90), encode_image (:113-150) with the error mapping of src/lib.rs:34-52
+// (every failure is a status + thread-local message, never a panic).  Pixels
+// stay device-resident between the three calls; only compressed bytes cross
+// PCIe (plus the small planes/coefficients handed to the host entropy coders).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+
+#include "../../include/imagekit_hip.h"
+#include "ik_runtime.h"
+
+namespace ik {
+
+static thread_local std::string t_err;
+static thread_local int t_device = -1;
+
+int fail(int status, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    t_err = buf;
+    return status;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(IK_ERR_DEVICE, "HIP error %d (%s) in %s", (int)e, hipGetErrorString(e), what);
+}
+
+int current_device() {
+    if (t_device < 0) {
+        int d = 0;
+        if (hipGetDevice(&d) != hipSuccess) d = 0;
+        t_device = d;
+    }
+    return t_device;
+}
+
+hipStream_t thread_stream() {
+    static thread_local std::map<int, hipStream_t> streams;
+    const int d = current_device();
+    auto it = streams.find(d);
+    if (it != streams.end()) return it->second;
+    (void)hipSetDevice(d);
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    streams[d] = s;
+    return s;
+}
+
+size_t pitch_for(uint32_t w, uint32_t c) { return ((size_t)w * c + 255) & ~size_t(255); }
+
+int alloc_image(uint32_t w, uint32_t h, uint32_t c, ik_image** out) {
+    auto* img = new ik_image();
+    img->w = w; img->h = h; img->c = c;
+    img->pitch = pitch_for(w, c);
+    img->device = current_device();
+    (void)hipSetDevice(img->device);
+    // + 16 bytes: the fused kernel's 8-byte lane loads may touch the pitch tail
+    hipError_t e = hipMalloc(&img->d, img->pitch * (size_t)(h ? h : 1) + 16);
+    if (e != hipSuccess) { delete img; return hip_fail(e, "hipMalloc(image)"); }
+    *out = img;
+    return IK_OK;
+}
+
+void webp_gamma_tables(uint16_t g2l[256], int l2g[33]) {
+    // libwebp picture_csp_enc.c InitGammaTables: kGamma 0.80, kGammaFix 12, kGammaTabFix 7
+    const double scale = (double)(1 << 7) / ((1 << 12) - 1);
+    const double norm = 1. / 255.;
+    for (int v = 0; v <= 255; ++v) g2l[v] = (uint16_t)(pow(norm * v, 0.80) * ((1 << 12) - 1) + .5);
+    for (int v = 0; v <= 32; ++v) l2g[v] = (int)(255. * pow(scale * v, 1. / 0.80) + .5);
+}
+
+const DeviceConsts* device_consts(int device) {
+    static std::mutex mu;
+    static std::map<int, DeviceConsts*> m;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = m.find(device);
+    if (it != m.end()) return it->second;
+    uint16_t g2l[256];
+    int l2g[33];
+    webp_gamma_tables(g2l, l2g);
+    auto* dc = new DeviceConsts();
+    (void)hipSetDevice(device);
+    if (hipMalloc(&dc->gamma_to_lin, sizeof(g2l)) != hipSuccess ||
+        hipMalloc(&dc->lin_to_gamma, sizeof(l2g)) != hipSuccess ||
+        hipMemcpy(dc->gamma_to_lin, g2l, sizeof(g2l), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(dc->lin_to_gamma, l2g, sizeof(l2g), hipMemcpyHostToDevice) != hipSuccess) {
+        delete dc;
+        return nullptr;
+    }
+    m[device] = dc;
+    return dc;
+}
+
+// Run the device front end of encode_image and hand its output to the host
+// entropy stage.  WebP: to_rgb8 + RGB->YUV420 on the GPU, libwebp VP8 coding of
+// those planes on the host.  JPEG: to_rgb8 + YCbCr + FDCT + quantise on the GPU,
+// baseline Huffman coding on the host.
+int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, size_t pitch,
+                        int fmt, int quality, std::vector<uint8_t>& out) {
+    const int q = quality < 1 ? 1 : (quality > 100 ? 100 : quality);
+    hipStream_t s = thread_stream();
+    if (!s) return fail(IK_ERR_DEVICE, "cannot create HIP stream");
+    if (fmt == IK_FORMAT_WEBP) {
+        if (w > 16383 || h > 16383) return fail(IK_ERR_TRANSFORM, "WebP dimensions %ux%u exceed 16383", w, h);
+        const DeviceConsts* dc = device_consts(current_device());
+        if (!dc) return fail(IK_ERR_DEVICE, "cannot upload WebP tables");
+        const size_t uvw = (w + 1) / 2, uvh = (h + 1) / 2;
+        const size_t bytes = (size_t)w * h + 2 * uvw * uvh;
+        uint8_t* dyuv = nullptr;
+        IK_HIP(hipMallocAsync((void**)&dyuv, bytes, s));
+        std::vector<uint8_t> yuv(bytes);
+        hipError_t e = launch_webp_yuv420(dev, (int)w, (int)h, (int)c, pitch, 0, dyuv, 0, 1,
+                                          dc->gamma_to_lin, dc->lin_to_gamma, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(yuv.data(), dyuv, bytes, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipFreeAsync(dyuv, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return hip_fail(e, "webp yuv420");
+        const uint8_t* Y = yuv.data();
+        return webp_encode_yuv420(Y, Y + (size_t)w * h, Y + (size_t)w * h + uvw * uvh, (int)w, (int)h,
+                                  (float)q, out);
+    }
+    if (fmt == IK_FORMAT_JPEG) {
+        if (w > 65535 || h > 65535) return fail(IK_ERR_TRANSFORM, "JPEG dimensions %ux%u exceed 65535", w, h);
+        uint8_t qt[128];
+        jpeg_quant_tables(q, qt);
+        const size_t nmcu = (size_t)((w + 7) / 8) * ((h + 7) / 8);
+        const size_t cbytes = nmcu * 3 * 64 * sizeof(int16_t);
+        uint8_t* dq = nullptr;
+        int16_t* dcoef = nullptr;
+        IK_HIP(hipMallocAsync((void**)&dq, 128, s));
+        IK_HIP(hipMallocAsync((void**)&dcoef, cbytes, s));
+        std::vector<int16_t> coef(nmcu * 3 * 64);
+        hipError_t e = hipMemcpyAsync(dq, qt, 128, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = launch_jpeg_coeffs(dev, (int)w, (int)h, (int)c, pitch, 0, dq, dcoef, 0, 1, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(coef.data(), dcoef, cbytes, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipFreeAsync(dcoef, s);
+        if (e == hipSuccess) e = hipFreeAsync(dq, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return hip_fail(e, "jpeg coefficients");
+        jpeg_write(coef.data(), (int)w, (int)h, qt, out);
+        return IK_OK;
+    }
+    if (fmt == IK_FORMAT_AVIF)
+        return fail(IK_ERR_UNSUPPORTED,
+                    "AVIF encoding (ravif/rav1e in the reference) is not implemented in this build");
+    return fail(IK_ERR_INVALID, "unknown ImageFormat %d", fmt);
+}
+
+}  // namespace ik
+
+using namespace ik;
+
+extern "C" {
+
+const char* ik_version(void) { return "imagekit-hip 0.1.0 (gfx950)"; }
+
+size_t ik_last_error(char* buf, size_t cap) {
+    const std::string& e = t_err;
+    if (buf && cap) {
+        size_t n = e.size() < cap - 1 ? e.size() : cap - 1;
+        std::memcpy(buf, e.data(), n);
+        buf[n] = 0;
+    }
+    return e.size();
+}
+
+int ik_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int ik_init(int device) {
+    int n = 0;
+    IK_HIP(hipGetDeviceCount(&n));
+    if (device >= n) return fail(IK_ERR_INVALID, "device %d out of range (%d devices)", device, n);
+    if (device >= 0) t_device = device;
+    IK_HIP(hipSetDevice(current_device()));
+    if (!thread_stream()) return fail(IK_ERR_DEVICE, "cannot create HIP stream");
+    return IK_OK;
+}
+
+int ik_image_from_host(const uint8_t* pixels, uint32_t width, uint32_t height, uint32_t channels,
+                       ik_image** out) {
+    if (!out || (!pixels && width && height)) return fail(IK_ERR_INVALID, "null pointer");
+    if (channels < 1 || channels > 4) return fail(IK_ERR_INVALID, "channels must be 1..4");
+    ik_image* img = nullptr;
+    int st = alloc_image(width, height, channels, &img);
+    if (st) return st;
+    if (width && height) {
+        hipStream_t s = thread_stream();
+        hipError_t e = hipMemcpy2DAsync(img->d, img->pitch, pixels, (size_t)width * channels,
+                                        (size_t)width * channels, height, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) { ik_image_free(img); return hip_fail(e, "upload image"); }
+    }
+    *out = img;
+    return IK_OK;
+}
+
+int ik_image_wrap_device(uint8_t* dev_pixels, uint32_t width, uint32_t height, uint32_t channels,
+                         size_t pitch, ik_image** out) {
+    if (!out || !dev_pixels) return fail(IK_ERR_INVALID, "null pointer");
+    if (channels < 1 || channels > 4) return fail(IK_ERR_INVALID, "channels must be 1..4");
+    if (pitch < (size_t)width * channels) return fail(IK_ERR_INVALID, "pitch smaller than a row");
+    auto* img = new ik_image();
+    img->w = width; img->h = height; img->c = channels; img->pitch = pitch;
+    img->d = dev_pixels; img->owned = false; img->device = current_device();
+    *out = img;
+    return IK_OK;
+}
+
+int ik_image_info(const ik_image* img, uint32_t* w, uint32_t* h, uint32_t* c) {
+    if (!img) return fail(IK_ERR_INVALID, "null image");
+    if (w) *w = img->w;
+    if (h) *h = img->h;
+    if (c) *c = img->c;
+    return IK_OK;
+}
+
+int ik_image_to_host(const ik_image* img, uint8_t* dst, size_t cap) {
+    if (!img || !dst) return fail(IK_ERR_INVALID, "null pointer");
+    const size_t row = (size_t)img->w * img->c;
+    if (cap < row * img->h) return fail(IK_ERR_INVALID, "destination too small");
+    if (!row || !img->h) return IK_OK;
+    hipStream_t s = thread_stream();
+    IK_HIP(hipMemcpy2DAsync(dst, row, img->d, img->pitch, row, img->h, hipMemcpyDeviceToHost, s));
+    IK_HIP(hipStreamSynchronize(s));
+    return IK_OK;
+}
+
+void ik_image_free(ik_image* img) {
+    if (!img) return;
+    if (img->owned && img->d) (void)hipFree(img->d);
+    delete img;
+}
+
+void ik_buf_free(uint8_t* buf) { free(buf); }
+
+// imageops::resize(image, nw, nh, filter)
+int ik_resize_exact(const ik_image* img, uint32_t nw, uint32_t nh, int filter, ik_image** out) {
+    if (!img || !out) return fail(IK_ERR_INVALID, "null pointer");
+    if (filter < 0 || filter > 4) return fail(IK_ERR_INVALID, "unknown filter %d", filter);
+    if (nw == 0 || nh == 0) return fail(IK_ERR_INVALID, "zero output dimension");
+    ik_image* o = nullptr;
+    int st = alloc_image(nw, nh, img->c, &o);
+    if (st) return st;
+    hipStream_t s = thread_stream();
+    const size_t orow = (size_t)nw * img->c;
+    if (img->w == 0 || img->h == 0) {  // "nothing to sample from": blank image
+        hipError_t e = hipMemset2DAsync(o->d, o->pitch, 0, orow, nh, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) { ik_image_free(o); return hip_fail(e, "blank image"); }
+        *out = o;
+        return IK_OK;
+    }
+    if (nw == img->w && nh == img->h) {  // copy instead of resampling
+        hipError_t e = hipMemcpy2DAsync(o->d, o->pitch, img->d, img->pitch, orow, nh, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) { ik_image_free(o); return hip_fail(e, "copy image"); }
+        *out = o;
+        return IK_OK;
+    }
+    int rc = ik_resize_batch_device(img->d, img->w, img->h, img->c, img->pitch, 0, 1, nw, nh, filter,
+                                    o->d, o->pitch, 0, s);
+    if (rc == IK_OK) {
+        hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "resize");
+    }
+    if (rc) { ik_image_free(o); return rc; }
+    *out = o;
+    return IK_OK;
+}
+
+static uint32_t f32_as_u32(float v) {
+    if (!(v > 0.0f)) return 0;
+    if (v >= 4294967296.0f) return 0xFFFFFFFFu;
+    return (uint32_t)v;
+}
+
+// src/transform.rs:62-90 then DynamicImage::resize (image 0.25.8):
+// (nw,nh) == dims -> clone; else resize_dimensions(..., fill=false) (aspect FIT,
+// f64, round, max 1) -> imageops::resize.
+int ik_resize(ik_image* img, int64_t w, int64_t h, int filter, ik_image** out) {
+    if (!img || !out) return fail(IK_ERR_INVALID, "null pointer");
+    if (w < 0 && h < 0) { *out = img; return IK_OK; }
+    if (w > 0xFFFFFFFFll || h > 0xFFFFFFFFll) return fail(IK_ERR_INVALID, "dimension exceeds u32");
+    uint32_t tw, th;
+    if (w >= 0) tw = (uint32_t)w;
+    else tw = f32_as_u32(roundf((float)img->w * ((float)(uint32_t)h / (float)img->h)));
+    if (h >= 0) th = (uint32_t)h;
+    else th = f32_as_u32(roundf((float)img->h * ((float)(uint32_t)w / (float)img->w)));
+    if (tw < 1) tw = 1;
+    if (th < 1) th = 1;
+    uint32_t nw = tw, nh = th;
+    if (!(tw == img->w && th == img->h)) {
+        const double wr = (double)tw / (double)img->w, hr = (double)th / (double)img->h;
+        const double r = wr < hr ? wr : hr;
+        double fw = std::round((double)img->w * r), fh = std::round((double)img->h * r);
+        unsigned long long rw = fw < 1 ? 1 : (unsigned long long)fw;
+        unsigned long long rh = fh < 1 ? 1 : (unsigned long long)fh;
+        if (rw > 0xFFFFFFFFull || rh > 0xFFFFFFFFull) return fail(IK_ERR_INVALID, "dimension overflow");
+        nw = (uint32_t)rw; nh = (uint32_t)rh;
+    }
+    return ik_resize_exact(img, nw, nh, filter, out);
+}
+
+int ik_encode(const ik_image* img, int fmt, int quality, uint8_t** out, size_t* out_len) {
+    if (!img || !out || !out_len) return fail(IK_ERR_INVALID, "null pointer");
+    if (img->w == 0 || img->h == 0) return fail(IK_ERR_TRANSFORM, "cannot encode an empty image");
+    std::vector<uint8_t> bytes;
+    int st = encode_device_image(img->d, img->w, img->h, img->c, img->pitch, fmt, quality, bytes);
+    if (st) return st;
+    *out = (uint8_t*)malloc(bytes.size() ? bytes.size() : 1);
+    if (!*out) return fail(IK_ERR_NOMEM, "out of host memory");
+    std::memcpy(*out, bytes.data(), bytes.size());
+    *out_len = bytes.size();
+    return IK_OK;
+}
+
+// decode_image: image::guess_format + load_from_memory_with_format; formats the
+// reference build compiles in (Cargo.toml:20: jpeg, png, webp; avif = encoder only)
+int ik_decode(const uint8_t* bytes, size_t len, ik_image** out, int* fmt_out) {
+    if (!out) return fail(IK_ERR_INVALID, "null pointer");
+    if (!bytes && len) return fail(IK_ERR_INVALID, "null bytes");
+    const Sniffed f = guess_format(bytes, len);
+    if (f == Sniffed::Unknown) return fail(IK_ERR_TRANSFORM, "The image format could not be determined");
+    uint32_t w = 0, h = 0, c = 0;
+    std::vector<uint8_t> px;
+    int st;
+    switch (f) {
+    case Sniffed::Png: st = decode_png(bytes, len, w, h, c, px); break;
+    case Sniffed::Jpeg: st = decode_jpeg(bytes, len, w, h, c, px); break;
+    case Sniffed::WebP: st = decode_webp(bytes, len, w, h, c, px); break;
+    default:
+        return fail(IK_ERR_TRANSFORM, "The image format %s is not supported", format_name(f));
+    }
+    if (st) return st;
+    ik_image* img = nullptr;
+    st = ik_image_from_host(px.data(), w, h, c, &img);
+    if (st) return st;
+    *out = img;
+    if (fmt_out) {
+        *fmt_out = f == Sniffed::WebP ? IK_FORMAT_WEBP
+                 : f == Sniffed::Jpeg ? IK_FORMAT_JPEG
+                 : f == Sniffed::Avif ? IK_FORMAT_AVIF : -1;
+    }
+    return IK_OK;
+}
+
+int ik_transform(const uint8_t* bytes, size_t len, int64_t w, int64_t h, int fmt, int quality,
+                 int filter, uint8_t** out, size_t* out_len) {
+    ik_image* img = nullptr;
+    int st = ik_decode(bytes, len, &img, nullptr);
+    if (st) return st;
+    ik_image* rs = nullptr;
+    st = ik_resize(img, w, h, filter, &rs);
+    if (st) { ik_image_free(img); return st; }
+    st = ik_encode(rs, fmt, quality, out, out_len);
+    if (rs != img) ik_image_free(rs);
+    ik_image_free(img);
+    return st;
+}
+
+int ik_resize_batch_device(const uint8_t* dev_src, uint32_t W, uint32_t H, uint32_t C,
+                           size_t src_pitch, size_t src_image_stride, uint32_t n, uint32_t nw,
+                           uint32_t nh, int filter, uint8_t* dev_dst, size_t dst_pitch,
+                           size_t dst_image_stride, void* hip_stream) {
+    if (!dev_src || !dev_dst) return fail(IK_ERR_INVALID, "null device pointer");
+    if (C < 1 || C > 4 || !W || !H || !nw || !nh || !n) return fail(IK_ERR_INVALID, "bad geometry");
+    if (filter < 0 || filter > 4) return fail(IK_ERR_INVALID, "unknown filter %d", filter);
+    if (src_pitch < (size_t)W * C || dst_pitch < (size_t)nw * C) return fail(IK_ERR_INVALID, "pitch too small");
+    if ((src_pitch & 7) || ((uintptr_t)dev_src & 7)) return fail(IK_ERR_INVALID, "source rows must be 8-byte aligned");
+    if (n > 1 && (src_image_stride < src_pitch * H || dst_image_stride < dst_pitch * nh))
+        return fail(IK_ERR_INVALID, "image stride too small");
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : thread_stream();
+    ResizePlan* plan = get_resize_plan(current_device(), (int)W, (int)H, (int)C, (int)nw, (int)nh, filter, (int)n);
+    if (!plan) return fail(IK_ERR_DEVICE, "cannot build resize plan");
+    float* tmp = nullptr;
+    if (plan->slots == 0) {
+        IK_HIP(hipMallocAsync((void**)&tmp, sizeof(float) * (size_t)n * nh * W * C, s));
+    }
+    hipError_t e = launch_resize(*plan, dev_src, src_pitch, src_image_stride, dev_dst, dst_pitch,
+                                 dst_image_stride, (int)n, tmp, s);
+    if (tmp) (void)hipFreeAsync(tmp, s);
+    if (e != hipSuccess) return hip_fail(e, "resize kernel launch");
+    return IK_OK;
+}
+
+int ik_webp_yuv420_device(const uint8_t* dev_src, uint32_t w, uint32_t h, uint32_t C, size_t pitch,
+                          uint8_t* dev_yuv, void* hip_stream) {
+    if (!dev_src || !dev_yuv || !w || !h || C < 1 || C > 4) return fail(IK_ERR_INVALID, "bad arguments");
+    const DeviceConsts* dc = device_consts(current_device());
+    if (!dc) return fail(IK_ERR_DEVICE, "cannot upload WebP tables");
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : thread_stream();
+    IK_HIP(launch_webp_yuv420(dev_src, (int)w, (int)h, (int)C, pitch, 0, dev_yuv, 0, 1,
+                              dc->gamma_to_lin, dc->lin_to_gamma, s));
+    return IK_OK;
+}
+
+int ik_jpeg_coeffs_device(const uint8_t* dev_src, uint32_t w, uint32_t h, uint32_t C, size_t pitch,
+                          int quality, int16_t* dev_coef, void* hip_stream) {
+    if (!dev_src || !dev_coef || !w || !h || C < 1 || C > 4) return fail(IK_ERR_INVALID, "bad arguments");
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : thread_stream();
+    uint8_t qt[128];
+    jpeg_quant_tables(quality < 1 ? 1 : quality > 100 ? 100 : quality, qt);
+    uint8_t* dq = nullptr;
+    IK_HIP(hipMallocAsync((void**)&dq, 128, s));
+    IK_HIP(hipMemcpyAsync(dq, qt, 128, hipMemcpyHostToDevice, s));
+    IK_HIP(launch_jpeg_coeffs(dev_src, (int)w, (int)h, (int)C, pitch, 0, dq, dev_coef, 0, 1, s));
+    IK_HIP(hipFreeAsync(dq, s));
+    IK_HIP(hipStreamSynchronize(s));
+    return IK_OK;
+}
+
+int ik_dev_alloc(size_t bytes, void** dev_ptr) {
+    if (!dev_ptr) return fail(IK_ERR_INVALID, "null pointer");
+    (void)hipSetDevice(current_device());
+    IK_HIP(hipMalloc(dev_ptr, bytes ? bytes : 1));
+    return IK_OK;
+}
+int ik_dev_free(void* p) { IK_HIP(hipFree(p)); return IK_OK; }
+int ik_memcpy_h2d(void* d, const void* h, size_t n) { IK_HIP(hipMemcpy(d, h, n, hipMemcpyHostToDevice)); return IK_OK; }
+int ik_memcpy_d2h(void* h, const void* d, size_t n) { IK_HIP(hipMemcpy(h, d, n, hipMemcpyDeviceToHost)); return IK_OK; }
+int ik_dev_synchronize(void) { IK_HIP(hipDeviceSynchronize()); return IK_OK; }
+
+}  // extern "C"

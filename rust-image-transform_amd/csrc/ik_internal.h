@@ -1,0 +1,71 @@
+// ik_internal.h -- shared declarations between the HIP kernels (ik_kernels.hip)
+// and the host runtime (ik_*.cpp) of libimagekit_hip.so.  Not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace ik {
+
+constexpr int kThreads = 256;            // workgroup size (4 wave64s)
+constexpr int kBytesPerLane = 8;         // vertical pass: bytes of a source row per lane
+constexpr int kStripBytes = kBytesPerLane * kThreads;  // 2048 source bytes per strip
+constexpr int kRowWords = kStripBytes + kStripBytes / 8;  // LDS f32 row, +4 words per 32
+constexpr int kRowsPerFlush = 4;         // vertical rows staged in LDS per horizontal pass
+
+// Everything the resize kernels read.  Weight tables follow image 0.25.8
+// sample.rs (see ik_plan.cpp); tables live in one device allocation per plan.
+struct ResizeArgs {
+    const uint8_t* src;
+    size_t src_pitch, src_img_stride;
+    uint8_t* dst;
+    size_t dst_pitch, dst_img_stride;
+    int W, H, C, nw, nh, row_bytes;
+    const int* ly;     // [nh]   first source row of each output row
+    const int* ny;     // [nh]   tap count
+    const float* wy;   // [nh*Ty] normalised weights, zero padded
+    int Ty;
+    const int* lx;     // [nw]
+    const int* nx;     // [nw]
+    const float* wx;   // [nw*Tx]
+    int Tx;
+    const int* strips; // [NS*3] (ox0, ox1, first source byte)
+    int NS;
+    const int* bands;  // [NB*2] (oy0, oy1)
+    int NB;
+    float* tmp;        // naive path only: f32 vertical intermediate [n][nh][row_bytes]
+};
+
+// Host-side plan for one (W,H,C,nw,nh,filter,band height) geometry.
+struct ResizePlan {
+    int W = 0, H = 0, C = 0, nw = 0, nh = 0, filter = 0;
+    int slots = 0;        // accumulator slots the fused kernel needs (0 = naive path)
+    int NS = 0, NB = 0;
+    size_t table_bytes = 0;
+    void* dev_tables = nullptr;
+    ResizeArgs args{};    // pointers into dev_tables; src/dst/tmp filled per launch
+};
+
+// ---- launchers (ik_kernels.hip) ----
+hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_pitch,
+                         size_t src_img_stride, uint8_t* dst, size_t dst_pitch,
+                         size_t dst_img_stride, int n, float* naive_tmp, hipStream_t s);
+hipError_t launch_webp_yuv420(const uint8_t* src, int w, int h, int C, size_t pitch,
+                              size_t img_stride, uint8_t* yuv /* Y, U, V planes per image */,
+                              size_t yuv_img_stride, int n, const uint16_t* gamma_to_lin,
+                              const int* lin_to_gamma, hipStream_t s);
+hipError_t launch_jpeg_coeffs(const uint8_t* src, int w, int h, int C, size_t pitch,
+                              size_t img_stride, const uint8_t* qtables /*dev, 128 B*/,
+                              int16_t* coef, size_t coef_img_stride, int n, hipStream_t s);
+
+// ---- plans (ik_plan.cpp) ----
+// sample.rs weights for one axis; returns the tap count T (row stride of w).
+int axis_weights(int in, int out, int filter, std::vector<int>& left, std::vector<int>& cnt,
+                 std::vector<float>& w);
+int required_slots(const std::vector<int>& left, const std::vector<int>& cnt);
+ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int filter, int n);
+
+}  // namespace ik

@@ -1,0 +1,411 @@
+// ik_kernels.hip -- hand-written gfx950 (CDNA4, wave64) kernels of the transform
+// hot path (reference src/transform.rs:62-150):
+//
+//   k_resize_fused<A>  resize_image's resampler (image 0.25.8 imageops::resize:
+//                      vertical_sample then horizontal_sample) fused in one pass:
+//                      source rows stream HBM -> VGPRs once per column strip, the
+//                      f32 vertical intermediate lives only in LDS.
+//   k_vert_naive / k_horz_naive   general fallback (huge ratios, extreme upscales)
+//   k_webp_yuv420      encode_image webp branch front end: to_rgb8 + libwebp's
+//                      RGB -> YUV420 (gamma-corrected chroma averaging)
+//   k_jpeg_coeffs      encode_image jpeg branch front end: to_rgb8 + f32 RGB->YCbCr
+//                      + libjpeg-islow FDCT + quantise (image JpegEncoder)
+//
+// Bit-exactness with the reference's f32 arithmetic: no FMA contraction in this
+// file (rustc never contracts), sequential tap order, host-computed weights,
+// correctly rounded division, Rust round-half-away-from-zero.
+#include "ik_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace ik {
+
+__device__ __forceinline__ int lds_idx(int i) { return i + ((i >> 5) << 2); }
+
+// clamp(t, 0, 255) then f32::round (half away from zero) -> u8   (sample.rs FloatNearest)
+__device__ __forceinline__ uint8_t float_nearest_u8(float t) {
+    t = t < 0.0f ? 0.0f : (t > 255.0f ? 255.0f : t);
+    return (uint8_t)roundf(t);
+}
+
+// Horizontal pass over `nrows` completed vertical rows staged in LDS.
+// out(r, ox, c) = round(sum_k tmp[r][(lx[ox]+k)*C + c] * wx[ox][k]), sequential k.
+__device__ __forceinline__ void horizontal_rows(const ResizeArgs& a, const float* __restrict__ lds,
+                                                int r0, int nrows, int ox0, int ox1, int sb,
+                                                uint8_t* __restrict__ dst) {
+    const int C = a.C;
+    const int per_row = (ox1 - ox0) * C;
+    const int total = nrows * per_row;
+    for (int v = threadIdx.x; v < total; v += kThreads) {
+        const int row = v / per_row;
+        const int rem = v - row * per_row;
+        const int oxl = rem / C;
+        const int c = rem - oxl * C;
+        const int ox = ox0 + oxl;
+        const int n = a.nx[ox];
+        const float* __restrict__ w = a.wx + (size_t)ox * a.Tx;
+        const float* __restrict__ t = lds + row * kRowWords;
+        int idx = a.lx[ox] * C + c - sb;
+        float acc = 0.0f;
+        for (int k = 0; k < n; ++k, idx += C) {
+            const float prod = t[lds_idx(idx)] * w[k];
+            acc = acc + prod;
+        }
+        dst[(size_t)(r0 + row) * a.dst_pitch + (size_t)ox * C + c] = float_nearest_u8(acc);
+    }
+}
+
+// Fused resampler.  Workgroup = (column strip, band of output rows, image).
+// Each lane owns kBytesPerLane consecutive bytes of the strip (the vertical pass
+// is channel-agnostic), sweeps the band's source rows top to bottom exactly once
+// and scatters every converted source row into the A rolling accumulators of the
+// output rows whose tap window contains it (A >= max rows open at once, checked
+// on the host).  Completed rows go to LDS; every kRowsPerFlush rows the workgroup
+// runs the horizontal pass on them.  All per-row scalars are wave-uniform.
+template <int A>
+__global__ __launch_bounds__(kThreads) void k_resize_fused(ResizeArgs a) {
+    __shared__ __attribute__((aligned(16))) float lds[kRowsPerFlush * kRowWords];
+    static_assert(A % kRowsPerFlush == 0, "flush points must be compile-time");
+
+    const int tile = blockIdx.x;
+    const int img = blockIdx.y;
+    const int strip = tile % a.NS;
+    const int band = tile / a.NS;
+    const int ox0 = a.strips[3 * strip], ox1 = a.strips[3 * strip + 1], sb = a.strips[3 * strip + 2];
+    const int oy0 = a.bands[2 * band], oy1 = a.bands[2 * band + 1];
+    const uint8_t* __restrict__ src = a.src + (size_t)img * a.src_img_stride;
+    uint8_t* __restrict__ dst = a.dst + (size_t)img * a.dst_img_stride;
+
+    const int mybyte = sb + kBytesPerLane * (int)threadIdx.x;
+    const bool active = mybyte < a.row_bytes;
+    const uint8_t* __restrict__ colp = src + (active ? mybyte : 0);
+    float* __restrict__ my_lds = lds + lds_idx(kBytesPerLane * (int)threadIdx.x);
+
+    float acc[A][kBytesPerLane];
+#pragma unroll
+    for (int s = 0; s < A; ++s)
+#pragma unroll
+        for (int j = 0; j < kBytesPerLane; ++j) acc[s][j] = 0.0f;
+
+    int i = a.ly[oy0];
+    for (int rbase = oy0; rbase < oy1; rbase += A) {
+        // per-slot row scalars for this round (wave-uniform)
+        int ly_[2 * A], ny_[2 * A];
+#pragma unroll
+        for (int d = 0; d < 2 * A; ++d) {
+            const int rr = rbase + d;
+            const bool ok = rr < oy1;
+            ly_[d] = ok ? a.ly[rr] : 0x7fffffff;
+            ny_[d] = ok ? a.ny[rr] : 0;
+        }
+#pragma unroll
+        for (int s = 0; s < A; ++s) {
+            const int r = rbase + s;
+            if (r < oy1) {
+                const int iend = ly_[s] + ny_[s];
+                i = i > ly_[s] ? i : ly_[s];
+                for (; i < iend; ++i) {
+                    uint2 raw = make_uint2(0u, 0u);
+                    if (active) raw = *reinterpret_cast<const uint2*>(colp + (size_t)i * a.src_pitch);
+                    float p[kBytesPerLane];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        p[j] = (float)((raw.x >> (8 * j)) & 0xffu);
+                        p[4 + j] = (float)((raw.y >> (8 * j)) & 0xffu);
+                    }
+#pragma unroll
+                    for (int d = 0; d < A; ++d) {
+                        const int kk = i - ly_[s + d];
+                        if (kk >= 0 && kk < ny_[s + d]) {
+                            const float w = a.wy[(size_t)(r + d) * a.Ty + kk];
+#pragma unroll
+                            for (int j = 0; j < kBytesPerLane; ++j) {
+                                const float prod = p[j] * w;
+                                acc[(s + d) % A][j] = acc[(s + d) % A][j] + prod;
+                            }
+                        }
+                    }
+                }
+                // row r complete -> LDS slot (r - oy0) % kRowsPerFlush
+                float* o = my_lds + (s % kRowsPerFlush) * kRowWords;
+                *reinterpret_cast<float4*>(o) = make_float4(acc[s][0], acc[s][1], acc[s][2], acc[s][3]);
+                *reinterpret_cast<float4*>(o + 4) = make_float4(acc[s][4], acc[s][5], acc[s][6], acc[s][7]);
+#pragma unroll
+                for (int j = 0; j < kBytesPerLane; ++j) acc[s][j] = 0.0f;
+                if ((s % kRowsPerFlush) == kRowsPerFlush - 1 || r == oy1 - 1) {
+                    __syncthreads();
+                    const int nrows = (s % kRowsPerFlush) + 1;
+                    horizontal_rows(a, lds, r - (nrows - 1), nrows, ox0, ox1, sb, dst);
+                    __syncthreads();
+                }
+            }
+        }
+    }
+}
+
+// Fallback vertical pass: one thread per (byte column, output row, image).
+__global__ __launch_bounds__(kThreads) void k_vert_naive(ResizeArgs a) {
+    const int b = blockIdx.x * kThreads + threadIdx.x;
+    const int r = blockIdx.y;
+    const int img = blockIdx.z;
+    if (b >= a.row_bytes) return;
+    const uint8_t* __restrict__ src = a.src + (size_t)img * a.src_img_stride + b;
+    const int l = a.ly[r], n = a.ny[r];
+    const float* __restrict__ w = a.wy + (size_t)r * a.Ty;
+    float t = 0.0f;
+    for (int k = 0; k < n; ++k) {
+        const float prod = (float)src[(size_t)(l + k) * a.src_pitch] * w[k];
+        t = t + prod;
+    }
+    a.tmp[((size_t)img * a.nh + r) * a.row_bytes + b] = t;
+}
+
+// Fallback horizontal pass: one thread per (output byte, output row, image).
+__global__ __launch_bounds__(kThreads) void k_horz_naive(ResizeArgs a) {
+    const int v = blockIdx.x * kThreads + threadIdx.x;
+    const int r = blockIdx.y;
+    const int img = blockIdx.z;
+    if (v >= a.nw * a.C) return;
+    const int ox = v / a.C, c = v - ox * a.C;
+    const float* __restrict__ t = a.tmp + ((size_t)img * a.nh + r) * a.row_bytes;
+    const int n = a.nx[ox];
+    const float* __restrict__ w = a.wx + (size_t)ox * a.Tx;
+    int idx = a.lx[ox] * a.C + c;
+    float acc = 0.0f;
+    for (int k = 0; k < n; ++k, idx += a.C) {
+        const float prod = t[idx] * w[k];
+        acc = acc + prod;
+    }
+    a.dst[(size_t)img * a.dst_img_stride + (size_t)r * a.dst_pitch + v] = float_nearest_u8(acc);
+}
+
+hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_pitch,
+                         size_t src_img_stride, uint8_t* dst, size_t dst_pitch,
+                         size_t dst_img_stride, int n, float* naive_tmp, hipStream_t s) {
+    ResizeArgs a = plan.args;
+    a.src = src; a.src_pitch = src_pitch; a.src_img_stride = src_img_stride;
+    a.dst = dst; a.dst_pitch = dst_pitch; a.dst_img_stride = dst_img_stride;
+    a.tmp = naive_tmp;
+    if (plan.slots > 0) {
+        dim3 grid(plan.NS * plan.NB, n);
+        switch (plan.slots) {
+        case 4: hipLaunchKernelGGL(k_resize_fused<4>, grid, dim3(kThreads), 0, s, a); break;
+        case 8: hipLaunchKernelGGL(k_resize_fused<8>, grid, dim3(kThreads), 0, s, a); break;
+        case 16: hipLaunchKernelGGL(k_resize_fused<16>, grid, dim3(kThreads), 0, s, a); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+    if (!naive_tmp) return hipErrorInvalidValue;
+    dim3 g1((a.row_bytes + kThreads - 1) / kThreads, a.nh, n);
+    hipLaunchKernelGGL(k_vert_naive, g1, dim3(kThreads), 0, s, a);
+    dim3 g2((a.nw * a.C + kThreads - 1) / kThreads, a.nh, n);
+    hipLaunchKernelGGL(k_horz_naive, g2, dim3(kThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// WebP front end: to_rgb8 (image 0.25.8: Rgba drops alpha, Luma replicates) then
+// libwebp ImportYUVAFromRGBA for opaque input (src/enc/picture_csp_enc.c):
+//   Y = (16839 r + 33059 g + 6420 b + 2^15 + (16 << 16)) >> 16
+//   U/V from gamma-linearised 2x2 sums (SUM4 / SUM2 on odd edges), rounding 2^17.
+// One thread per chroma sample (2x2 luma block).
+__device__ __forceinline__ void load_rgb(const uint8_t* __restrict__ row, int x, int C, int& r,
+                                         int& g, int& b) {
+    const uint8_t* p = row + x * C;
+    if (C >= 3) { r = p[0]; g = p[1]; b = p[2]; }
+    else { r = g = b = p[0]; }
+}
+
+__device__ __forceinline__ int webp_y(int r, int g, int b) {
+    return (16839 * r + 33059 * g + 6420 * b + (1 << 15) + (16 << 16)) >> 16;
+}
+
+__device__ __forceinline__ int webp_clip_uv(int uv) {
+    uv = (uv + (1 << 17) + (128 << 18)) >> 18;
+    return ((uv & ~0xff) == 0) ? uv : (uv < 0) ? 0 : 255;
+}
+
+__device__ __forceinline__ int lin_to_gamma(const int* __restrict__ tab, uint32_t base, int shift) {
+    const int v = (int)(base << shift);
+    const int pos = v >> 9;
+    const int x = v & 511;
+    const int y = tab[pos + 1] * x + tab[pos] * (512 - x);
+    return (y + 64) >> 7;
+}
+
+__global__ __launch_bounds__(kThreads) void k_webp_yuv420(const uint8_t* __restrict__ src, int w,
+                                                          int h, int C, size_t pitch,
+                                                          size_t img_stride, uint8_t* __restrict__ Y,
+                                                          size_t yuv_img_stride,
+                                                          const uint16_t* __restrict__ g2l,
+                                                          const int* __restrict__ l2g) {
+    __shared__ uint16_t s_g2l[256];
+    __shared__ int s_l2g[33];
+    for (int t = threadIdx.x; t < 256; t += kThreads) s_g2l[t] = g2l[t];
+    if (threadIdx.x < 33) s_l2g[threadIdx.x] = l2g[threadIdx.x];
+    __syncthreads();
+    const int uvw = (w + 1) >> 1, uvh = (h + 1) >> 1;
+    const int cx = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int cy = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int img = blockIdx.z;
+    if (cx >= uvw || cy >= uvh) return;
+    const uint8_t* __restrict__ base = src + (size_t)img * img_stride;
+    uint8_t* __restrict__ y_img = Y + (size_t)img * yuv_img_stride;
+    uint8_t* __restrict__ u_img = y_img + (size_t)w * h;
+    uint8_t* __restrict__ v_img = u_img + (size_t)uvw * uvh;
+    const int x0 = 2 * cx, y0 = 2 * cy;
+    const bool has_x1 = x0 + 1 < w, has_y1 = y0 + 1 < h;
+    int R[4], G[4], B[4];
+    const uint8_t* row0 = base + (size_t)y0 * pitch;
+    const uint8_t* row1 = base + (size_t)(has_y1 ? y0 + 1 : y0) * pitch;  // rgb_stride = 0 on odd last row
+    load_rgb(row0, x0, C, R[0], G[0], B[0]);
+    load_rgb(row1, x0, C, R[2], G[2], B[2]);
+    if (has_x1) {
+        load_rgb(row0, x0 + 1, C, R[1], G[1], B[1]);
+        load_rgb(row1, x0 + 1, C, R[3], G[3], B[3]);
+    } else {
+        R[1] = R[0]; G[1] = G[0]; B[1] = B[0];
+        R[3] = R[2]; G[3] = G[2]; B[3] = B[2];
+    }
+    y_img[(size_t)y0 * w + x0] = (uint8_t)webp_y(R[0], G[0], B[0]);
+    if (has_x1) y_img[(size_t)y0 * w + x0 + 1] = (uint8_t)webp_y(R[1], G[1], B[1]);
+    if (has_y1) {
+        y_img[(size_t)(y0 + 1) * w + x0] = (uint8_t)webp_y(R[2], G[2], B[2]);
+        if (has_x1) y_img[(size_t)(y0 + 1) * w + x0 + 1] = (uint8_t)webp_y(R[3], G[3], B[3]);
+    }
+    int sum[3];
+    const int* comp[3] = {R, G, B};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const int* q = comp[c];
+        if (has_x1) {
+            const uint32_t s4 = s_g2l[q[0]] + s_g2l[q[1]] + s_g2l[q[2]] + s_g2l[q[3]];
+            sum[c] = lin_to_gamma(s_l2g, s4, 0);
+        } else {
+            const uint32_t s2 = s_g2l[q[0]] + s_g2l[q[2]];
+            sum[c] = lin_to_gamma(s_l2g, s2, 1);
+        }
+    }
+    u_img[(size_t)cy * uvw + cx] = (uint8_t)webp_clip_uv(-9719 * sum[0] - 19081 * sum[1] + 28800 * sum[2]);
+    v_img[(size_t)cy * uvw + cx] = (uint8_t)webp_clip_uv(28800 * sum[0] - 24116 * sum[1] - 4684 * sum[2]);
+}
+
+hipError_t launch_webp_yuv420(const uint8_t* src, int w, int h, int C, size_t pitch,
+                              size_t img_stride, uint8_t* yuv, size_t yuv_img_stride, int n, const uint16_t* gamma_to_lin,
+                              const int* lin_to_gamma_tab, hipStream_t s) {
+    const int uvw = (w + 1) >> 1, uvh = (h + 1) >> 1;
+    dim3 grid((uvw + 63) / 64, (uvh + 3) / 4, n);
+    hipLaunchKernelGGL(k_webp_yuv420, grid, dim3(kThreads), 0, s, src, w, h, C, pitch, img_stride,
+                       yuv, yuv_img_stride, gamma_to_lin, lin_to_gamma_tab);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// JPEG front end (image 0.25.8 JpegEncoder::encode_rgb, 4:4:4): per 8x8 block
+// and component: pixel_at_or_near -> rgb_to_ycbcr (f32, `as u8`) -> fdct (libjpeg
+// 9a islow, integer) -> ((c / 8) as f32 / q).round().  Workgroup = 8 MCUs x 3
+// components x 8 lines; pass 1 (rows) and pass 2 (columns) meet in LDS.
+constexpr int CB = 13, P1 = 2;
+
+__device__ __forceinline__ uint8_t f32_as_u8(float v) {
+    if (!(v > 0.0f)) return 0;
+    if (v >= 255.0f) return 255;
+    return (uint8_t)v;
+}
+
+__device__ __forceinline__ void dct8(int s0, int s1, int s2, int s3, int s4, int s5, int s6, int s7,
+                                     int out[8], bool pass1) {
+    int t0 = s0 + s7, t1 = s1 + s6, t2 = s2 + s5, t3 = s3 + s4;
+    int t10 = t0 + t3, t12 = t0 - t3, t11 = t1 + t2, t13 = t1 - t2;
+    if (!pass1) t10 += 1 << (P1 - 1);
+    t0 = s0 - s7; t1 = s1 - s6; t2 = s2 - s5; t3 = s3 - s4;
+    const int sh = pass1 ? CB - P1 : CB + P1;
+    if (pass1) {
+        out[0] = (t10 + t11 - 8 * 128) << P1;
+        out[4] = (t10 - t11) << P1;
+    } else {
+        out[0] = (t10 + t11) >> P1;
+        out[4] = (t10 - t11) >> P1;
+    }
+    int z1 = (t12 + t13) * 4433;
+    z1 += 1 << (sh - 1);
+    out[2] = (z1 + t12 * 6270) >> sh;
+    out[6] = (z1 - t13 * 15137) >> sh;
+    t12 = t0 + t2; t13 = t1 + t3;
+    z1 = (t12 + t13) * 9633;
+    z1 += 1 << (sh - 1);
+    t12 = t12 * (-3196); t13 = t13 * (-16069);
+    t12 += z1; t13 += z1;
+    z1 = (t0 + t3) * (-7373);
+    t0 = t0 * 12299; t3 = t3 * 2446;
+    t0 += z1 + t12; t3 += z1 + t13;
+    z1 = (t1 + t2) * (-20995);
+    t1 = t1 * 25172; t2 = t2 * 16819;
+    t1 += z1 + t13; t2 += z1 + t12;
+    out[1] = t0 >> sh; out[3] = t1 >> sh; out[5] = t2 >> sh; out[7] = t3 >> sh;
+}
+
+__global__ __launch_bounds__(192) void k_jpeg_coeffs(const uint8_t* __restrict__ src, int w, int h,
+                                                     int C, size_t pitch, size_t img_stride,
+                                                     const uint8_t* __restrict__ qt,
+                                                     int16_t* __restrict__ coef,
+                                                     size_t coef_img_stride, int nmcu) {
+    __shared__ int rows[24][8][9];
+    const int t = threadIdx.x;
+    const int blk = t >> 3, line = t & 7;
+    const int m = blockIdx.x * 8 + blk / 3, comp = blk % 3;
+    const int img = blockIdx.y;
+    const int nbx = (w + 7) >> 3;
+    const bool ok = m < nmcu;
+    if (ok) {
+        const int bx = m % nbx, by = m / nbx;
+        int py = by * 8 + line;
+        if (py >= h) py = h - 1;
+        const uint8_t* row = src + (size_t)img * img_stride + (size_t)py * pitch;
+        int smp[8];
+        const float mx = 255.0f;
+#pragma unroll
+        for (int x = 0; x < 8; ++x) {
+            int px = bx * 8 + x;
+            if (px >= w) px = w - 1;
+            int ri, gi, bi;
+            load_rgb(row, px, C, ri, gi, bi);
+            const float r = (float)ri, g = (float)gi, b = (float)bi;
+            float v;
+            if (comp == 0) v = 76.245f / mx * r + 149.685f / mx * g + 29.07f / mx * b;
+            else if (comp == 1) v = -43.0185f / mx * r - 84.4815f / mx * g + 127.5f / mx * b + 128.0f;
+            else v = 127.5f / mx * r - 106.7685f / mx * g - 20.7315f / mx * b + 128.0f;
+            smp[x] = f32_as_u8(v);
+        }
+        int o[8];
+        dct8(smp[0], smp[1], smp[2], smp[3], smp[4], smp[5], smp[6], smp[7], o, true);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) rows[blk][line][k] = o[k];
+    }
+    __syncthreads();
+    if (!ok) return;
+    const int x = line;  // column
+    int o[8];
+    dct8(rows[blk][0][x], rows[blk][1][x], rows[blk][2][x], rows[blk][3][x], rows[blk][4][x],
+         rows[blk][5][x], rows[blk][6][x], rows[blk][7][x], o, false);
+    const uint8_t* q = qt + (comp ? 64 : 0);
+    int16_t* out = coef + (size_t)img * coef_img_stride + ((size_t)m * 3 + comp) * 64;
+#pragma unroll
+    for (int y = 0; y < 8; ++y) {
+        const int d = o[y];
+        out[y * 8 + x] = (int16_t)(int)roundf((float)(d / 8) / (float)q[y * 8 + x]);
+    }
+}
+
+hipError_t launch_jpeg_coeffs(const uint8_t* src, int w, int h, int C, size_t pitch,
+                              size_t img_stride, const uint8_t* qtables, int16_t* coef,
+                              size_t coef_img_stride, int n, hipStream_t s) {
+    const int nmcu = ((w + 7) >> 3) * ((h + 7) >> 3);
+    dim3 grid((nmcu + 7) / 8, n);
+    hipLaunchKernelGGL(k_jpeg_coeffs, grid, dim3(192), 0, s, src, w, h, C, pitch, img_stride,
+                       qtables, coef, coef_img_stride, nmcu);
+    return hipGetLastError();
+}
+
+}  // namespace ik

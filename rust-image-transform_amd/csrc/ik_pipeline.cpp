@@ -1,0 +1,260 @@
+// ik_pipeline.cpp -- batched transform over device-resident images (the
+// throughput path behind the /img and /upload handlers, src/lib.rs:175-191 and
+// :281-297, when many requests are in flight).
+//
+// Per run: ONE resize launch over the whole batch (k_resize_fused, pixels HBM ->
+// LDS -> HBM), ONE colour-convert launch (WebP YUV420 planes or JPEG quantised
+// coefficients), one D2H copy of those small planes into pinned memory, then the
+// host entropy coders (libwebp VP8 / baseline Huffman) over a persistent thread
+// pool, one image per task -- the reference runs one synchronous transform per
+// tokio worker (src/main.rs:20), so per-image serial entropy coding across cores
+// is the same structure.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
+
+#include "../../include/imagekit_hip.h"
+#include "ik_runtime.h"
+
+namespace ik {
+namespace {
+
+class Pool {
+public:
+    explicit Pool(int n) {
+        for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+    // run fn(i) for i in [0, n) on the workers (and the caller), wait for all
+    void run(int n, const std::function<void(int)>& fn) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            fn_ = &fn;
+            n_ = n;
+            next_.store(0);
+            done_ = 0;
+            ++gen_;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [&] { return done_ == n_; });
+        fn_ = nullptr;
+    }
+
+private:
+    void work() {
+        for (;;) {
+            const int i = next_.fetch_add(1);
+            if (i >= n_) return;
+            (*fn_)(i);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (++done_ == n_) done_cv_.notify_all();
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || (gen_ != seen && fn_ != nullptr); });
+                if (stop_) return;
+                seen = gen_;
+            }
+            work();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(int)>* fn_ = nullptr;
+    int n_ = 0, done_ = 0;
+    std::atomic<int> next_{0};
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+}  // namespace
+}  // namespace ik
+
+struct ik_pipeline {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t W = 0, H = 0, C = 0, nw = 0, nh = 0, max_batch = 0;
+    int filter = 4, fmt = 1, quality = 80;
+    uint8_t* d_resized = nullptr;
+    size_t r_pitch = 0, r_img_stride = 0;
+    uint8_t* d_stage = nullptr;  // YUV planes or int16 coefficients, per image
+    size_t stage_bytes = 0;
+    uint8_t* h_stage = nullptr;  // pinned
+    uint8_t* d_qt = nullptr;
+    uint8_t qt[128];
+    float* d_tmp = nullptr;      // naive resize path only
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    double ms[2] = {0, 0};
+    uint32_t last_n = 0;
+    ik::Pool* pool = nullptr;
+    std::vector<std::vector<uint8_t>> outs;
+    std::vector<int> status;
+};
+
+using namespace ik;
+
+extern "C" {
+
+int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t nh, int filter,
+                       int fmt, int quality, uint32_t max_batch, int threads, ik_pipeline** out) {
+    if (!out || !W || !H || !nw || !nh || !max_batch || C < 1 || C > 4) return fail(IK_ERR_INVALID, "bad geometry");
+    if (fmt != IK_FORMAT_WEBP && fmt != IK_FORMAT_JPEG)
+        return fail(IK_ERR_UNSUPPORTED, "pipeline supports jpeg and webp output");
+    auto* p = new ik_pipeline();
+    p->device = current_device();
+    IK_HIP(hipSetDevice(p->device));
+    p->W = W; p->H = H; p->C = C; p->nw = nw; p->nh = nh; p->max_batch = max_batch;
+    p->filter = filter; p->fmt = fmt;
+    p->quality = quality < 1 ? 1 : quality > 100 ? 100 : quality;
+    IK_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    for (auto& e : p->ev) IK_HIP(hipEventCreate(&e));
+    p->r_pitch = pitch_for(nw, C);
+    p->r_img_stride = p->r_pitch * nh;
+    IK_HIP(hipMalloc(&p->d_resized, p->r_img_stride * max_batch + 16));
+    if (fmt == IK_FORMAT_WEBP) {
+        const size_t uvw = (nw + 1) / 2, uvh = (nh + 1) / 2;
+        p->stage_bytes = (size_t)nw * nh + 2 * uvw * uvh;
+    } else {
+        p->stage_bytes = (size_t)((nw + 7) / 8) * ((nh + 7) / 8) * 3 * 64 * sizeof(int16_t);
+        jpeg_quant_tables(p->quality, p->qt);
+        IK_HIP(hipMalloc(&p->d_qt, 128));
+        IK_HIP(hipMemcpy(p->d_qt, p->qt, 128, hipMemcpyHostToDevice));
+    }
+    IK_HIP(hipMalloc(&p->d_stage, p->stage_bytes * max_batch));
+    IK_HIP(hipHostMalloc(&p->h_stage, p->stage_bytes * max_batch, hipHostMallocDefault));
+    ResizePlan* plan = get_resize_plan(p->device, (int)W, (int)H, (int)C, (int)nw, (int)nh, filter, (int)max_batch);
+    if (!plan) return fail(IK_ERR_DEVICE, "cannot build resize plan");
+    if (plan->slots == 0) IK_HIP(hipMalloc(&p->d_tmp, sizeof(float) * (size_t)max_batch * nh * W * C));
+    if (threads <= 0) {
+        threads = (int)std::thread::hardware_concurrency();
+        if (threads > 16) threads = 16;
+        if (threads < 1) threads = 1;
+    }
+    p->pool = new Pool(threads - 1);  // the calling thread works too
+    if (fmt == IK_FORMAT_WEBP && !device_consts(p->device)) return fail(IK_ERR_DEVICE, "cannot upload WebP tables");
+    *out = p;
+    return IK_OK;
+}
+
+int ik_pipeline_run_device(ik_pipeline* p, const uint8_t* dev_src, size_t src_pitch,
+                           size_t src_image_stride, uint32_t n) {
+    if (!p || !dev_src || !n || n > p->max_batch) return fail(IK_ERR_INVALID, "bad batch");
+    if (src_pitch < (size_t)p->W * p->C || (src_pitch & 7) || ((uintptr_t)dev_src & 7))
+        return fail(IK_ERR_INVALID, "source rows must be 8-byte aligned and >= W*C");
+    if (n > 1 && src_image_stride < src_pitch * p->H) return fail(IK_ERR_INVALID, "image stride too small");
+    IK_HIP(hipSetDevice(p->device));
+    ResizePlan* plan = get_resize_plan(p->device, (int)p->W, (int)p->H, (int)p->C, (int)p->nw, (int)p->nh,
+                                       p->filter, (int)p->max_batch);
+    if (!plan) return fail(IK_ERR_DEVICE, "cannot build resize plan");
+    IK_HIP(hipEventRecord(p->ev[0], p->stream));
+    IK_HIP(launch_resize(*plan, dev_src, src_pitch, src_image_stride, p->d_resized, p->r_pitch,
+                         p->r_img_stride, (int)n, p->d_tmp, p->stream));
+    IK_HIP(hipEventRecord(p->ev[1], p->stream));
+    if (p->fmt == IK_FORMAT_WEBP) {
+        const DeviceConsts* dc = device_consts(p->device);
+        IK_HIP(launch_webp_yuv420(p->d_resized, (int)p->nw, (int)p->nh, (int)p->C, p->r_pitch,
+                                  p->r_img_stride, p->d_stage, p->stage_bytes, (int)n,
+                                  dc->gamma_to_lin, dc->lin_to_gamma, p->stream));
+    } else {
+        IK_HIP(launch_jpeg_coeffs(p->d_resized, (int)p->nw, (int)p->nh, (int)p->C, p->r_pitch,
+                                  p->r_img_stride, p->d_qt, (int16_t*)p->d_stage,
+                                  p->stage_bytes / sizeof(int16_t), (int)n, p->stream));
+    }
+    IK_HIP(hipEventRecord(p->ev[2], p->stream));
+    IK_HIP(hipEventSynchronize(p->ev[2]));
+    float a = 0, b = 0;
+    IK_HIP(hipEventElapsedTime(&a, p->ev[0], p->ev[1]));
+    IK_HIP(hipEventElapsedTime(&b, p->ev[1], p->ev[2]));
+    p->ms[0] = a;
+    p->ms[1] = b;
+    p->last_n = n;
+    return IK_OK;
+}
+
+int ik_pipeline_run(ik_pipeline* p, const uint8_t* dev_src, size_t src_pitch, size_t src_image_stride,
+                    uint32_t n, uint8_t* out, size_t out_cap, size_t* out_sizes) {
+    int st = ik_pipeline_run_device(p, dev_src, src_pitch, src_image_stride, n);
+    if (st) return st;
+    IK_HIP(hipMemcpyAsync(p->h_stage, p->d_stage, p->stage_bytes * n, hipMemcpyDeviceToHost, p->stream));
+    IK_HIP(hipStreamSynchronize(p->stream));
+    p->outs.resize(n);
+    p->status.assign(n, 0);
+    std::vector<std::string> errs(n);
+    p->pool->run((int)n, [&](int i) {
+        const uint8_t* s = p->h_stage + p->stage_bytes * (size_t)i;
+        if (p->fmt == IK_FORMAT_WEBP) {
+            const size_t ys = (size_t)p->nw * p->nh, uvs = (size_t)((p->nw + 1) / 2) * ((p->nh + 1) / 2);
+            p->status[i] = webp_encode_yuv420(s, s + ys, s + ys + uvs, (int)p->nw, (int)p->nh,
+                                              (float)p->quality, p->outs[i]);
+            if (p->status[i]) {
+                char buf[256];
+                ik_last_error(buf, sizeof(buf));
+                errs[i] = buf;
+            }
+        } else {
+            jpeg_write((const int16_t*)s, (int)p->nw, (int)p->nh, p->qt, p->outs[i]);
+        }
+    });
+    size_t off = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (p->status[i]) return fail(p->status[i], "image %u: %s", i, errs[i].c_str());
+        if (out_sizes) out_sizes[i] = p->outs[i].size();
+        if (out) {
+            if (off + p->outs[i].size() > out_cap) return fail(IK_ERR_INVALID, "output buffer too small");
+            std::memcpy(out + off, p->outs[i].data(), p->outs[i].size());
+        }
+        off += p->outs[i].size();
+    }
+    return IK_OK;
+}
+
+double ik_pipeline_kernel_ms(const ik_pipeline* p, int which) {
+    if (!p || which < 0 || which > 1) return -1.0;
+    return p->ms[which];
+}
+
+int ik_pipeline_fetch_resized(ik_pipeline* p, uint32_t i, uint8_t* dst, size_t cap) {
+    if (!p || !dst || i >= p->last_n) return fail(IK_ERR_INVALID, "bad image index");
+    const size_t row = (size_t)p->nw * p->C;
+    if (cap < row * p->nh) return fail(IK_ERR_INVALID, "destination too small");
+    IK_HIP(hipMemcpy2DAsync(dst, row, p->d_resized + p->r_img_stride * i, p->r_pitch, row, p->nh,
+                            hipMemcpyDeviceToHost, p->stream));
+    IK_HIP(hipStreamSynchronize(p->stream));
+    return IK_OK;
+}
+
+void ik_pipeline_destroy(ik_pipeline* p) {
+    if (!p) return;
+    (void)hipSetDevice(p->device);
+    delete p->pool;
+    if (p->d_resized) (void)hipFree(p->d_resized);
+    if (p->d_stage) (void)hipFree(p->d_stage);
+    if (p->h_stage) (void)hipHostFree(p->h_stage);
+    if (p->d_qt) (void)hipFree(p->d_qt);
+    if (p->d_tmp) (void)hipFree(p->d_tmp);
+    for (auto& e : p->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (p->stream) (void)hipStreamDestroy(p->stream);
+    delete p;
+}
+
+}  // extern "C"

@@ -1,0 +1,199 @@
+// ik_plan.cpp -- resize plans: the host half of resize_image's resampler.
+//
+// Weights follow image 0.25.8 src/imageops/sample.rs (vertical_sample /
+// horizontal_sample, called from reference src/transform.rs:85-89): per output
+// index, centre (o + 0.5) * ratio, support * max(ratio, 1), window
+// [floor(c - s), ceil(c + s)) clamped, kernel((i - (c - 0.5)) / sratio),
+// normalised by the sequential f32 sum (w /= sum).  They are computed once per
+// geometry on the host -- with glibc sinf/expf, as rustc's f32::sin/exp are --
+// and uploaded, so the device kernels only multiply and add.
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
+
+#include "ik_internal.h"
+
+
+namespace ik {
+namespace {
+
+constexpr float kPi = 3.14159265358979323846264338327950288f;
+
+float sinc(float t) {
+    const float a = t * kPi;
+    if (t == 0.0f) return 1.0f;
+    return sinf(a) / a;
+}
+
+float kernel_eval(int filter, float x) {
+    const float ax = fabsf(x);
+    switch (filter) {
+    case 0: return 1.0f;                                   // box_kernel (Nearest)
+    case 1: return ax < 1.0f ? 1.0f - ax : 0.0f;           // triangle_kernel
+    case 2: {                                              // catmullrom = bc_cubic_spline(x, 0, 0.5)
+        const float b = 0.0f, c = 0.5f;
+        float k;
+        if (ax < 1.0f) {
+            const float a2 = ax * ax, a3 = a2 * ax;
+            k = (12.0f - 9.0f * b - 6.0f * c) * a3 + (-18.0f + 12.0f * b + 6.0f * c) * a2 +
+                (6.0f - 2.0f * b);
+        } else if (ax < 2.0f) {
+            const float a2 = ax * ax, a3 = a2 * ax;
+            k = (-b - 6.0f * c) * a3 + (6.0f * b + 30.0f * c) * a2 + (-12.0f * b - 48.0f * c) * ax +
+                (8.0f * b + 24.0f * c);
+        } else {
+            k = 0.0f;
+        }
+        return k / 6.0f;
+    }
+    case 3: {                                              // gaussian_kernel = gaussian(x, 0.5)
+        const float r = 0.5f;
+        const float cst = 1.0f / (sqrtf(2.0f * kPi) * r);
+        return cst * expf(-(x * x) / (2.0f * (r * r)));
+    }
+    default:                                               // lanczos3_kernel
+        return ax < 3.0f ? sinc(x) * sinc(x / 3.0f) : 0.0f;
+    }
+}
+
+float support_of(int filter) {
+    switch (filter) {
+    case 0: return 0.0f;
+    case 1: return 1.0f;
+    case 2: return 2.0f;
+    default: return 3.0f;
+    }
+}
+
+}  // namespace
+
+int axis_weights(int in, int out, int filter, std::vector<int>& left, std::vector<int>& cnt,
+                 std::vector<float>& w) {
+    const float ratio = (float)in / (float)out;
+    const float sratio = ratio < 1.0f ? 1.0f : ratio;
+    const float src_support = support_of(filter) * sratio;
+    left.assign(out, 0);
+    cnt.assign(out, 0);
+    std::vector<std::vector<float>> rows(out);
+    int T = 1;
+    for (int o = 0; o < out; ++o) {
+        float c = ((float)o + 0.5f) * ratio;
+        long long l = (long long)floorf(c - src_support);
+        l = l < 0 ? 0 : (l > in - 1 ? in - 1 : l);
+        long long r = (long long)ceilf(c + src_support);
+        r = r < l + 1 ? l + 1 : (r > in ? in : r);
+        c = c - 0.5f;
+        std::vector<float>& ws = rows[o];
+        float sum = 0.0f;
+        for (long long i = l; i < r; ++i) {
+            const float wv = kernel_eval(filter, ((float)i - c) / sratio);
+            ws.push_back(wv);
+            sum = sum + wv;
+        }
+        for (float& wv : ws) wv = wv / sum;
+        left[o] = (int)l;
+        cnt[o] = (int)(r - l);
+        if (cnt[o] > T) T = cnt[o];
+    }
+    w.assign((size_t)out * T, 0.0f);
+    for (int o = 0; o < out; ++o) std::memcpy(&w[(size_t)o * T], rows[o].data(), sizeof(float) * cnt[o]);
+    return T;
+}
+
+// smallest A with left[r + A] >= left[r] + cnt[r] for every r: no more than A
+// output rows are ever open at once in a top-to-bottom sweep
+int required_slots(const std::vector<int>& left, const std::vector<int>& cnt) {
+    const int n = (int)left.size();
+    int A = 1;
+    for (int r = 0; r < n; ++r) {
+        const int end = left[r] + cnt[r];
+        while (r + A < n && left[r + A] < end) ++A;
+    }
+    return A;
+}
+
+namespace {
+
+std::mutex g_plan_mu;
+std::map<std::tuple<int, int, int, int, int, int, int, int>, ResizePlan*> g_plans;
+
+template <typename T>
+size_t put(std::vector<char>& blob, const std::vector<T>& v) {
+    size_t off = (blob.size() + 255) & ~size_t(255);
+    blob.resize(off + v.size() * sizeof(T));
+    if (!v.empty()) std::memcpy(blob.data() + off, v.data(), v.size() * sizeof(T));
+    return off;
+}
+
+}  // namespace
+
+ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int filter, int n) {
+    // band height depends on how many images share the launch: aim for >= 2048
+    // workgroups (8 per CU) without cutting bands below 32 rows
+    std::vector<int> lx, cx, ly, cy;
+    std::vector<float> wx, wy;
+    const int Tx = axis_weights(W, nw, filter, lx, cx, wx);
+    const int Ty = axis_weights(H, nh, filter, ly, cy, wy);
+    int A = required_slots(ly, cy);
+    int slots = A <= 4 ? 4 : A <= 8 ? 8 : A <= 16 ? 16 : 0;
+
+    // column strips: as many output columns as fit kStripBytes source bytes
+    std::vector<int> strips;
+    for (int ox0 = 0; ox0 < nw && slots;) {
+        const int sb = (lx[ox0] * C) & ~15;
+        int ox1 = ox0;
+        while (ox1 < nw && (lx[ox1] + cx[ox1]) * C - sb <= kStripBytes) ++ox1;
+        if (ox1 == ox0) { slots = 0; break; }  // one output column wider than a strip
+        strips.push_back(ox0); strips.push_back(ox1); strips.push_back(sb);
+        ox0 = ox1;
+    }
+    const int NS = slots ? (int)strips.size() / 3 : 0;
+    int band_h = nh;
+    if (slots) {
+        const long target = 2048;
+        long per_img = (target + n - 1) / n;
+        long nb = (per_img + NS - 1) / NS;
+        if (nb < 1) nb = 1;
+        band_h = (int)((nh + nb - 1) / nb);
+        if (band_h < 32) band_h = 32;
+        band_h = ((band_h + slots - 1) / slots) * slots;
+        if (band_h > nh) band_h = nh;
+    }
+    const auto key = std::make_tuple(device, W, H, C, nw, nh, filter, band_h);
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    auto it = g_plans.find(key);
+    if (it != g_plans.end()) return it->second;
+
+    std::vector<int> bands;
+    for (int y = 0; y < nh; y += band_h) { bands.push_back(y); bands.push_back(y + band_h < nh ? y + band_h : nh); }
+
+    std::vector<char> blob;
+    const size_t o_ly = put(blob, ly), o_cy = put(blob, cy), o_wy = put(blob, wy);
+    const size_t o_lx = put(blob, lx), o_cx = put(blob, cx), o_wx = put(blob, wx);
+    const size_t o_st = put(blob, strips), o_bd = put(blob, bands);
+
+    auto* p = new ResizePlan();
+    p->W = W; p->H = H; p->C = C; p->nw = nw; p->nh = nh; p->filter = filter;
+    p->slots = slots;
+    p->NS = NS;
+    p->NB = (int)bands.size() / 2;
+    p->table_bytes = blob.size();
+    if (hipMalloc(&p->dev_tables, blob.size()) != hipSuccess ||
+        hipMemcpy(p->dev_tables, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        delete p;
+        return nullptr;
+    }
+    char* d = static_cast<char*>(p->dev_tables);
+    ResizeArgs& a = p->args;
+    a.W = W; a.H = H; a.C = C; a.nw = nw; a.nh = nh; a.row_bytes = W * C;
+    a.ly = (const int*)(d + o_ly); a.ny = (const int*)(d + o_cy); a.wy = (const float*)(d + o_wy); a.Ty = Ty;
+    a.lx = (const int*)(d + o_lx); a.nx = (const int*)(d + o_cx); a.wx = (const float*)(d + o_wx); a.Tx = Tx;
+    a.strips = (const int*)(d + o_st); a.NS = p->NS;
+    a.bands = (const int*)(d + o_bd); a.NB = p->NB;
+    g_plans[key] = p;
+    return p;
+}
+
+}  // namespace ik

@@ -1,0 +1,60 @@
+// ik_runtime.h -- host runtime internals of libimagekit_hip.so (not part of the ABI).
+#pragma once
+#include <cstdarg>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "ik_internal.h"
+
+struct ik_image {
+    uint32_t w = 0, h = 0, c = 0;  // 8-bit, c interleaved channels
+    size_t pitch = 0;              // bytes between rows on the device (multiple of 256)
+    uint8_t* d = nullptr;          // device pixels
+    bool owned = true;
+    int device = 0;
+};
+
+namespace ik {
+
+// thread-local error message + status (ik_last_error)
+int fail(int status, const char* fmt, ...);
+int hip_fail(hipError_t e, const char* what);
+#define IK_HIP(call)                                    \
+    do {                                                \
+        hipError_t _e = (call);                         \
+        if (_e != hipSuccess) return hip_fail(_e, #call); \
+    } while (0)
+
+int current_device();
+hipStream_t thread_stream();  // per-thread, per-device non-blocking stream
+size_t pitch_for(uint32_t w, uint32_t c);
+int alloc_image(uint32_t w, uint32_t h, uint32_t c, ik_image** out);
+
+// per-device constant tables (WebP gamma tables)
+struct DeviceConsts {
+    uint16_t* gamma_to_lin = nullptr;  // [256]
+    int* lin_to_gamma = nullptr;       // [33]
+};
+const DeviceConsts* device_consts(int device);
+void webp_gamma_tables(uint16_t g2l[256], int l2g[33]);
+
+// host entropy stages (ik_codec.cpp)
+int webp_encode_yuv420(const uint8_t* y, const uint8_t* u, const uint8_t* v, int w, int h,
+                       float quality, std::vector<uint8_t>& out);
+void jpeg_quant_tables(int quality, uint8_t qt[128]);
+void jpeg_write(const int16_t* coef, int w, int h, const uint8_t qt[128], std::vector<uint8_t>& out);
+
+// host decoders (ik_decode.cpp): tightly packed 8-bit pixels
+enum class Sniffed { Png, Jpeg, Gif, WebP, Tiff, Bmp, Ico, Hdr, Avif, OpenExr, Qoi, Farbfeld, Pnm, Dds, Unknown };
+Sniffed guess_format(const uint8_t* b, size_t n);
+const char* format_name(Sniffed f);
+int decode_png(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& c, std::vector<uint8_t>& px);
+int decode_jpeg(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& c, std::vector<uint8_t>& px);
+int decode_webp(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& c, std::vector<uint8_t>& px);
+
+// device-side stage helpers used by ik_encode and the pipeline
+int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, size_t pitch,
+                        int fmt, int quality, std::vector<uint8_t>& out);
+
+}  // namespace ik

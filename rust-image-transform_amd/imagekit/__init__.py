@@ -1,0 +1,15 @@
+"""imagekit (MI355X-native): drop-in for the reference crate's transform hot path.
+
+Layout mirrors the crate: `imagekit.transform` (src/transform.rs),
+`imagekit.config` (src/config.rs), `imagekit.ImageKitError` (src/lib.rs:34-52).
+"""
+from . import config, transform
+from .config import DEFAULT_QUALITY, MAX_QUALITY, MIN_QUALITY, ImageFormat, ImageKitConfig
+from .errors import ImageKitError, InvalidArgument, TransformError
+from .transform import DynamicImage, FilterType, decode_image, encode_image, resize_image
+
+__all__ = [
+    "config", "transform", "ImageFormat", "ImageKitConfig", "DEFAULT_QUALITY", "MIN_QUALITY",
+    "MAX_QUALITY", "ImageKitError", "TransformError", "InvalidArgument", "DynamicImage",
+    "FilterType", "decode_image", "encode_image", "resize_image",
+]

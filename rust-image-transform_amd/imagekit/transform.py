@@ -1,0 +1,197 @@
+"""Host-side mirror of reference `imagekit::transform` (src/transform.rs).
+
+The same three functions with the same argument meaning and error behaviour:
+
+    decode_image(bytes) -> (DynamicImage, Optional[ImageFormat])       :27-43
+    resize_image(img, w: Optional[int], h: Optional[int]) -> DynamicImage  :62-90
+    encode_image(img, fmt: ImageFormat, quality: int) -> bytes          :113-150
+
+Every call goes through libimagekit_hip.so (include/imagekit_hip.h): pixels live
+in HBM as a device-resident `DynamicImage`; the resampler, the colour
+conversions and the FDCT/quantiser are gfx950 kernels.  Failures raise
+`TransformError`, as the reference maps every decode/encode failure to
+`ImageKitError::TransformError`.  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+from .config import ImageFormat
+from .errors import InvalidArgument, TransformError
+
+
+class FilterType(enum.IntEnum):
+    """image::imageops::FilterType (image 0.25.8).  resize_image uses Lanczos3."""
+
+    Nearest = 0
+    Triangle = 1
+    CatmullRom = 2
+    Gaussian = 3
+    Lanczos3 = 4
+
+
+_COLOR = {1: "L8", 2: "La8", 3: "Rgb8", 4: "Rgba8"}
+
+
+def _raise(status: int, what: str):
+    msg = _lib.last_error()
+    if status == 2:
+        raise InvalidArgument(f"{what}: {msg}")
+    raise TransformError(msg)
+
+
+class DynamicImage:
+    """An 8-bit image (L8 / La8 / Rgb8 / Rgba8) resident in device memory."""
+
+    __slots__ = ("_h", "__weakref__")
+
+    def __init__(self, handle: int):
+        self._h = ctypes.c_void_p(handle)
+
+    @classmethod
+    def from_array(cls, pixels: np.ndarray) -> "DynamicImage":
+        """ImageBuffer::from_raw on an (H, W) or (H, W, C) uint8 array."""
+        a = np.ascontiguousarray(pixels, dtype=np.uint8)
+        if a.ndim == 2:
+            a = a[:, :, None]
+        if a.ndim != 3 or not 1 <= a.shape[2] <= 4:
+            raise InvalidArgument("expected (H, W, C) uint8 with C in 1..4")
+        h, w, c = a.shape
+        lib = _lib.load()
+        out = ctypes.c_void_p()
+        st = lib.ik_image_from_host(a.ctypes.data, w, h, c, ctypes.byref(out))
+        if st:
+            _raise(st, "from_array")
+        return cls(out.value)
+
+    @classmethod
+    def new_rgb8(cls, w: int, h: int) -> "DynamicImage":
+        """DynamicImage::new_rgb8 (all-zero pixels), as tests/transform.rs builds inputs."""
+        return cls.from_array(np.zeros((h, w, 3), np.uint8))
+
+    @classmethod
+    def new_rgba8(cls, w: int, h: int) -> "DynamicImage":
+        return cls.from_array(np.zeros((h, w, 4), np.uint8))
+
+    def dimensions(self) -> Tuple[int, int]:
+        w, h, c = self._info()
+        return (w, h)
+
+    def width(self) -> int:
+        return self._info()[0]
+
+    def height(self) -> int:
+        return self._info()[1]
+
+    @property
+    def channels(self) -> int:
+        return self._info()[2]
+
+    def color(self) -> str:
+        return _COLOR[self._info()[2]]
+
+    def _info(self):
+        lib = _lib.load()
+        w, h, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        st = lib.ik_image_info(self._h, ctypes.byref(w), ctypes.byref(h), ctypes.byref(c))
+        if st:
+            _raise(st, "image_info")
+        return w.value, h.value, c.value
+
+    def to_array(self) -> np.ndarray:
+        """Copy the pixels back to the host as an (H, W, C) uint8 array."""
+        w, h, c = self._info()
+        out = np.empty((h, w, c), np.uint8)
+        st = _lib.load().ik_image_to_host(self._h, out.ctypes.data, out.nbytes)
+        if st:
+            _raise(st, "to_array")
+        return out
+
+    def resize(self, nw: int, nh: int, filter: FilterType = FilterType.Lanczos3) -> "DynamicImage":
+        """imageops::resize to exactly nw x nh (the resampler under resize_image)."""
+        out = ctypes.c_void_p()
+        st = _lib.load().ik_resize_exact(self._h, nw, nh, int(filter), ctypes.byref(out))
+        if st:
+            _raise(st, "resize")
+        return DynamicImage(out.value)
+
+    def clone(self) -> "DynamicImage":
+        return DynamicImage.from_array(self.to_array())
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.ik_image_free(h)
+            self._h = ctypes.c_void_p(0)
+
+    def __repr__(self) -> str:
+        w, h, c = self._info()
+        return f"DynamicImage({_COLOR[c]}, {w}x{h}, device)"
+
+
+def decode_image(data: bytes) -> Tuple[DynamicImage, Optional[ImageFormat]]:
+    """src/transform.rs:27-43 -- guess_format + load_from_memory_with_format."""
+    lib = _lib.load()
+    b = bytes(data)
+    out = ctypes.c_void_p()
+    fmt = ctypes.c_int(-1)
+    st = lib.ik_decode(b, len(b), ctypes.byref(out), ctypes.byref(fmt))
+    if st:
+        raise TransformError(_lib.last_error())
+    f = None if fmt.value < 0 else ImageFormat(fmt.value)
+    return DynamicImage(out.value), f
+
+
+def resize_image(img: DynamicImage, w: Optional[int], h: Optional[int],
+                 filter: FilterType = FilterType.Lanczos3) -> DynamicImage:
+    """src/transform.rs:62-90 (Lanczos3; `filter` is an extension)."""
+    if w is None and h is None:
+        return img
+    for v in (w, h):
+        if v is not None and not 0 <= v <= 0xFFFFFFFF:
+            raise InvalidArgument("dimension must be a u32")
+    out = ctypes.c_void_p()
+    st = _lib.load().ik_resize(img._h, -1 if w is None else int(w), -1 if h is None else int(h),
+                               int(filter), ctypes.byref(out))
+    if st:
+        _raise(st, "resize_image")
+    return DynamicImage(out.value)
+
+
+def encode_image(img: DynamicImage, fmt: ImageFormat, quality: int) -> bytes:
+    """src/transform.rs:113-150.  quality is a u8, clamped to [1, 100]."""
+    if not 0 <= int(quality) <= 255:
+        raise InvalidArgument("quality must be a u8")
+    lib = _lib.load()
+    buf = _lib.u8p()
+    n = ctypes.c_size_t()
+    st = lib.ik_encode(img._h, ImageFormat(fmt).value, int(quality), ctypes.byref(buf), ctypes.byref(n))
+    if st:
+        raise TransformError(_lib.last_error())
+    try:
+        return ctypes.string_at(buf, n.value)
+    finally:
+        lib.ik_buf_free(buf)
+
+
+def transform(data: bytes, w: Optional[int], h: Optional[int], fmt: ImageFormat, quality: int,
+              filter: FilterType = FilterType.Lanczos3) -> bytes:
+    """decode -> resize_image -> encode_image in one device-resident call."""
+    lib = _lib.load()
+    b = bytes(data)
+    buf = _lib.u8p()
+    n = ctypes.c_size_t()
+    st = lib.ik_transform(b, len(b), -1 if w is None else int(w), -1 if h is None else int(h),
+                          ImageFormat(fmt).value, int(quality), int(filter), ctypes.byref(buf),
+                          ctypes.byref(n))
+    if st:
+        raise TransformError(_lib.last_error())
+    try:
+        return ctypes.string_at(buf, n.value)
+    finally:
+        lib.ik_buf_free(buf)
