@@ -57,6 +57,71 @@ hipStream_t thread_stream() {
     return s;
 }
 
+// Host <-> device copies of pageable memory go through a per-thread pinned
+// staging buffer with stream-ordered async copies on the thread's stream.  (A
+// synchronous hipMemcpy* from pageable memory is issued on the null stream, and
+// a non-blocking stream is not ordered after its DMA.)
+static uint8_t* staging(size_t bytes) {
+    static thread_local uint8_t* buf = nullptr;
+    static thread_local size_t cap = 0;
+    if (bytes <= cap) return buf;
+    if (buf) (void)hipHostFree(buf);
+    buf = nullptr;
+    cap = 0;
+    size_t want = bytes < (1u << 20) ? (1u << 20) : bytes;
+    if (hipHostMalloc((void**)&buf, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+    cap = want;
+    return buf;
+}
+
+int copy_h2d_2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,
+                size_t height, hipStream_t s) {
+    const size_t chunk_rows = height ? (size_t)((64u << 20) / (width ? width : 1)) + 1 : 1;
+    for (size_t y0 = 0; y0 < height; y0 += chunk_rows) {
+        const size_t rows = height - y0 < chunk_rows ? height - y0 : chunk_rows;
+        uint8_t* st = staging(rows * width);
+        if (!st) return fail(IK_ERR_NOMEM, "cannot allocate pinned staging");
+        for (size_t y = 0; y < rows; ++y) std::memcpy(st + y * width, src + (y0 + y) * spitch, width);
+        IK_HIP(hipMemcpy2DAsync(dst + y0 * dpitch, dpitch, st, width, width, rows, hipMemcpyHostToDevice, s));
+        IK_HIP(hipStreamSynchronize(s));
+    }
+    return IK_OK;
+}
+
+int copy_d2h_2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,
+                size_t height, hipStream_t s) {
+    const size_t chunk_rows = height ? (size_t)((64u << 20) / (width ? width : 1)) + 1 : 1;
+    for (size_t y0 = 0; y0 < height; y0 += chunk_rows) {
+        const size_t rows = height - y0 < chunk_rows ? height - y0 : chunk_rows;
+        uint8_t* st = staging(rows * width);
+        if (!st) return fail(IK_ERR_NOMEM, "cannot allocate pinned staging");
+        IK_HIP(hipMemcpy2DAsync(st, width, src + y0 * spitch, spitch, width, rows, hipMemcpyDeviceToHost, s));
+        IK_HIP(hipStreamSynchronize(s));
+        for (size_t y = 0; y < rows; ++y) std::memcpy(dst + (y0 + y) * dpitch, st + y * width, width);
+    }
+    return IK_OK;
+}
+
+// Per-thread, per-device device scratch (grown with hipMalloc; never the
+// stream-ordered allocator).  Valid until the next scratch() call on this thread.
+uint8_t* scratch(size_t bytes) {
+    struct Arena { uint8_t* p = nullptr; size_t cap = 0; };
+    static thread_local std::map<int, Arena> arenas;
+    Arena& a = arenas[current_device()];
+    if (bytes <= a.cap) return a.p;
+    if (a.p) {
+        (void)hipStreamSynchronize(thread_stream());
+        (void)hipFree(a.p);
+    }
+    a.p = nullptr;
+    a.cap = 0;
+    const size_t want = bytes < (4u << 20) ? (4u << 20) : bytes;
+    (void)hipSetDevice(current_device());
+    if (hipMalloc((void**)&a.p, want) != hipSuccess) return nullptr;
+    a.cap = want;
+    return a.p;
+}
+
 size_t pitch_for(uint32_t w, uint32_t c) { return ((size_t)w * c + 255) & ~size_t(255); }
 
 int alloc_image(uint32_t w, uint32_t h, uint32_t c, ik_image** out) {
@@ -94,7 +159,8 @@ const DeviceConsts* device_consts(int device) {
     if (hipMalloc(&dc->gamma_to_lin, sizeof(g2l)) != hipSuccess ||
         hipMalloc(&dc->lin_to_gamma, sizeof(l2g)) != hipSuccess ||
         hipMemcpy(dc->gamma_to_lin, g2l, sizeof(g2l), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(dc->lin_to_gamma, l2g, sizeof(l2g), hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(dc->lin_to_gamma, l2g, sizeof(l2g), hipMemcpyHostToDevice) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {  // order before non-blocking streams
         delete dc;
         return nullptr;
     }
@@ -117,15 +183,14 @@ int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, 
         if (!dc) return fail(IK_ERR_DEVICE, "cannot upload WebP tables");
         const size_t uvw = (w + 1) / 2, uvh = (h + 1) / 2;
         const size_t bytes = (size_t)w * h + 2 * uvw * uvh;
-        uint8_t* dyuv = nullptr;
-        IK_HIP(hipMallocAsync((void**)&dyuv, bytes, s));
+        uint8_t* dyuv = scratch(bytes);
+        if (!dyuv) return fail(IK_ERR_DEVICE, "cannot allocate device scratch");
         std::vector<uint8_t> yuv(bytes);
         hipError_t e = launch_webp_yuv420(dev, (int)w, (int)h, (int)c, pitch, 0, dyuv, 0, 1,
                                           dc->gamma_to_lin, dc->lin_to_gamma, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(yuv.data(), dyuv, bytes, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipFreeAsync(dyuv, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_fail(e, "webp yuv420");
+        int rc = copy_d2h_2d(yuv.data(), bytes, dyuv, bytes, bytes, 1, s);
+        if (rc) return rc;
         const uint8_t* Y = yuv.data();
         return webp_encode_yuv420(Y, Y + (size_t)w * h, Y + (size_t)w * h + uvw * uvh, (int)w, (int)h,
                                   (float)q, out);
@@ -136,18 +201,16 @@ int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, 
         jpeg_quant_tables(q, qt);
         const size_t nmcu = (size_t)((w + 7) / 8) * ((h + 7) / 8);
         const size_t cbytes = nmcu * 3 * 64 * sizeof(int16_t);
-        uint8_t* dq = nullptr;
-        int16_t* dcoef = nullptr;
-        IK_HIP(hipMallocAsync((void**)&dq, 128, s));
-        IK_HIP(hipMallocAsync((void**)&dcoef, cbytes, s));
+        uint8_t* dq = scratch(cbytes + 256);
+        if (!dq) return fail(IK_ERR_DEVICE, "cannot allocate device scratch");
+        int16_t* dcoef = (int16_t*)(dq + 256);
         std::vector<int16_t> coef(nmcu * 3 * 64);
-        hipError_t e = hipMemcpyAsync(dq, qt, 128, hipMemcpyHostToDevice, s);
-        if (e == hipSuccess) e = launch_jpeg_coeffs(dev, (int)w, (int)h, (int)c, pitch, 0, dq, dcoef, 0, 1, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(coef.data(), dcoef, cbytes, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipFreeAsync(dcoef, s);
-        if (e == hipSuccess) e = hipFreeAsync(dq, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        int rc = copy_h2d_2d(dq, 128, qt, 128, 128, 1, s);
+        if (rc) return rc;
+        hipError_t e = launch_jpeg_coeffs(dev, (int)w, (int)h, (int)c, pitch, 0, dq, dcoef, 0, 1, s);
         if (e != hipSuccess) return hip_fail(e, "jpeg coefficients");
+        rc = copy_d2h_2d((uint8_t*)coef.data(), cbytes, (const uint8_t*)dcoef, cbytes, cbytes, 1, s);
+        if (rc) return rc;
         jpeg_write(coef.data(), (int)w, (int)h, qt, out);
         return IK_OK;
     }
@@ -199,11 +262,9 @@ int ik_image_from_host(const uint8_t* pixels, uint32_t width, uint32_t height, u
     int st = alloc_image(width, height, channels, &img);
     if (st) return st;
     if (width && height) {
-        hipStream_t s = thread_stream();
-        hipError_t e = hipMemcpy2DAsync(img->d, img->pitch, pixels, (size_t)width * channels,
-                                        (size_t)width * channels, height, hipMemcpyHostToDevice, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) { ik_image_free(img); return hip_fail(e, "upload image"); }
+        const size_t row = (size_t)width * channels;
+        int rc = copy_h2d_2d(img->d, img->pitch, pixels, row, row, height, thread_stream());
+        if (rc) { ik_image_free(img); return rc; }
     }
     *out = img;
     return IK_OK;
@@ -234,10 +295,7 @@ int ik_image_to_host(const ik_image* img, uint8_t* dst, size_t cap) {
     const size_t row = (size_t)img->w * img->c;
     if (cap < row * img->h) return fail(IK_ERR_INVALID, "destination too small");
     if (!row || !img->h) return IK_OK;
-    hipStream_t s = thread_stream();
-    IK_HIP(hipMemcpy2DAsync(dst, row, img->d, img->pitch, row, img->h, hipMemcpyDeviceToHost, s));
-    IK_HIP(hipStreamSynchronize(s));
-    return IK_OK;
+    return copy_d2h_2d(dst, row, img->d, img->pitch, row, img->h, thread_stream());
 }
 
 void ik_image_free(ik_image* img) {
@@ -389,11 +447,11 @@ int ik_resize_batch_device(const uint8_t* dev_src, uint32_t W, uint32_t H, uint3
     if (!plan) return fail(IK_ERR_DEVICE, "cannot build resize plan");
     float* tmp = nullptr;
     if (plan->slots == 0) {
-        IK_HIP(hipMallocAsync((void**)&tmp, sizeof(float) * (size_t)n * nh * W * C, s));
+        tmp = (float*)scratch(sizeof(float) * (size_t)n * nh * W * C);
+        if (!tmp) return fail(IK_ERR_DEVICE, "cannot allocate device scratch");
     }
     hipError_t e = launch_resize(*plan, dev_src, src_pitch, src_image_stride, dev_dst, dst_pitch,
                                  dst_image_stride, (int)n, tmp, s);
-    if (tmp) (void)hipFreeAsync(tmp, s);
     if (e != hipSuccess) return hip_fail(e, "resize kernel launch");
     return IK_OK;
 }
@@ -415,11 +473,10 @@ int ik_jpeg_coeffs_device(const uint8_t* dev_src, uint32_t w, uint32_t h, uint32
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : thread_stream();
     uint8_t qt[128];
     jpeg_quant_tables(quality < 1 ? 1 : quality > 100 ? 100 : quality, qt);
-    uint8_t* dq = nullptr;
-    IK_HIP(hipMallocAsync((void**)&dq, 128, s));
-    IK_HIP(hipMemcpyAsync(dq, qt, 128, hipMemcpyHostToDevice, s));
+    uint8_t* dq = scratch(128);
+    if (!dq) return fail(IK_ERR_DEVICE, "cannot allocate device scratch");
+    if (int rc = copy_h2d_2d(dq, 128, qt, 128, 128, 1, s)) return rc;
     IK_HIP(launch_jpeg_coeffs(dev_src, (int)w, (int)h, (int)C, pitch, 0, dq, dev_coef, 0, 1, s));
-    IK_HIP(hipFreeAsync(dq, s));
     IK_HIP(hipStreamSynchronize(s));
     return IK_OK;
 }
@@ -431,8 +488,14 @@ int ik_dev_alloc(size_t bytes, void** dev_ptr) {
     return IK_OK;
 }
 int ik_dev_free(void* p) { IK_HIP(hipFree(p)); return IK_OK; }
-int ik_memcpy_h2d(void* d, const void* h, size_t n) { IK_HIP(hipMemcpy(d, h, n, hipMemcpyHostToDevice)); return IK_OK; }
-int ik_memcpy_d2h(void* h, const void* d, size_t n) { IK_HIP(hipMemcpy(h, d, n, hipMemcpyDeviceToHost)); return IK_OK; }
+int ik_memcpy_h2d(void* d, const void* h, size_t n) {
+    IK_HIP(hipDeviceSynchronize());
+    return copy_h2d_2d((uint8_t*)d, n, (const uint8_t*)h, n, n, n ? 1 : 0, thread_stream());
+}
+int ik_memcpy_d2h(void* h, const void* d, size_t n) {
+    IK_HIP(hipDeviceSynchronize());
+    return copy_d2h_2d((uint8_t*)h, n, (const uint8_t*)d, n, n, n ? 1 : 0, thread_stream());
+}
 int ik_dev_synchronize(void) { IK_HIP(hipDeviceSynchronize()); return IK_OK; }
 
 }  // extern "C"

@@ -137,7 +137,7 @@ int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t
         p->stage_bytes = (size_t)((nw + 7) / 8) * ((nh + 7) / 8) * 3 * 64 * sizeof(int16_t);
         jpeg_quant_tables(p->quality, p->qt);
         IK_HIP(hipMalloc(&p->d_qt, 128));
-        IK_HIP(hipMemcpy(p->d_qt, p->qt, 128, hipMemcpyHostToDevice));
+        if (int rc = copy_h2d_2d(p->d_qt, 128, p->qt, 128, 128, 1, p->stream)) return rc;
     }
     IK_HIP(hipMalloc(&p->d_stage, p->stage_bytes * max_batch));
     IK_HIP(hipHostMalloc(&p->h_stage, p->stage_bytes * max_batch, hipHostMallocDefault));
@@ -236,10 +236,7 @@ int ik_pipeline_fetch_resized(ik_pipeline* p, uint32_t i, uint8_t* dst, size_t c
     if (!p || !dst || i >= p->last_n) return fail(IK_ERR_INVALID, "bad image index");
     const size_t row = (size_t)p->nw * p->C;
     if (cap < row * p->nh) return fail(IK_ERR_INVALID, "destination too small");
-    IK_HIP(hipMemcpy2DAsync(dst, row, p->d_resized + p->r_img_stride * i, p->r_pitch, row, p->nh,
-                            hipMemcpyDeviceToHost, p->stream));
-    IK_HIP(hipStreamSynchronize(p->stream));
-    return IK_OK;
+    return copy_d2h_2d(dst, row, p->d_resized + p->r_img_stride * i, p->r_pitch, row, p->nh, p->stream);
 }
 
 void ik_pipeline_destroy(ik_pipeline* p) {

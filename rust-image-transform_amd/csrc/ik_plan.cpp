@@ -181,7 +181,8 @@ ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int
     p->NB = (int)bands.size() / 2;
     p->table_bytes = blob.size();
     if (hipMalloc(&p->dev_tables, blob.size()) != hipSuccess ||
-        hipMemcpy(p->dev_tables, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(p->dev_tables, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {  // order before non-blocking streams
         delete p;
         return nullptr;
     }

@@ -29,6 +29,11 @@ int hip_fail(hipError_t e, const char* what);
 int current_device();
 hipStream_t thread_stream();  // per-thread, per-device non-blocking stream
 size_t pitch_for(uint32_t w, uint32_t c);
+uint8_t* scratch(size_t bytes);  // per-thread device scratch, valid until the next call
+int copy_h2d_2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,
+                size_t height, hipStream_t s);
+int copy_d2h_2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,
+                size_t height, hipStream_t s);
 int alloc_image(uint32_t w, uint32_t h, uint32_t c, ik_image** out);
 
 // per-device constant tables (WebP gamma tables)
