@@ -1,0 +1,255 @@
+#!/usr/bin/env python3
+"""bench.py -- transform MPix/s (decode+resize+encode) 4096^2 -> 512^2 WebP q80.
+
+Workload (BASELINE.json configs[1]): synthetic 4096x4096 RGBA8 images already
+resident in HBM ("RGBA8 synthetic": the decoded DynamicImage the reference's
+resize_image receives; raw frames need no entropy decode) -> resize_image to
+512x512 (Triangle = "bilinear" per configs[1]; --filter lanczos3 for the
+reference's own filter) -> encode_image WebP q80.  One step = one batch through
+libimagekit_hip.so's pipeline: ONE resize launch over the batch, ONE WebP
+colour-convert launch, D2H of the YUV planes, libwebp VP8 coding of every image
+on the host thread pool.  Encoded bytes end in host memory.
+
+value = input pixels of all images of all ranks / max-over-ranks wall time of
+the K timed steps.  roofline = the resize kernel (the dominant device kernel):
+algorithmic bytes per launch (4*W*H + 4*w*h per image) /
+its average duration from HIP events on the pipeline's stream.  cpu_baseline =
+the oracle restatement of the reference CPU path (image 0.25.8 resize + libwebp
+WebPEncodeRGB) timed on this host's cores on a bounded sample.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under
+torch.distributed.run (one rank per GPU, RCCL only for barrier/max).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "rust-image-transform_amd"), os.path.join(ROOT, "tests")]
+
+METRIC = "transform MPix/s (decode+resize+encode) 4096²→512² WebP q80; 1/2/4/8 GPU"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+FILTERS = {"nearest": 0, "triangle": 1, "catmullrom": 2, "gaussian": 3, "lanczos3": 4}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
+    ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--out", type=int, default=512)
+    ap.add_argument("--filter", default="triangle", choices=sorted(FILTERS))
+    ap.add_argument("--quality", type=int, default=80)
+    ap.add_argument("--threads", type=int, default=16, help="host entropy-coder threads per rank")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--device-only", action="store_true", help="time resize+colour kernels only")
+    return ap.parse_args()
+
+
+def synth_rgba(w, h, seed):
+    import ikutil
+    return ikutil.synth(w, h, 4, seed=seed, pattern="S")
+
+
+def cpu_baseline(args, img: np.ndarray):
+    """Reference CPU transform restated (oracle/, test infrastructure) on a bounded sample."""
+    import ikutil
+    orc = ikutil.Oracle()
+    threads = max(1, min(args.threads, os.cpu_count() or 1))
+    H, W, C = img.shape
+    f = FILTERS[args.filter]
+    done = [0]
+    lock = threading.Lock()
+
+    def one():
+        b, dims = orc.transform(img, args.out, args.out, f, 1, args.quality)
+        assert dims == (args.out, args.out) and b[:4] == b"RIFF"
+        with lock:
+            done[0] += 1
+
+    # single-thread time of one image sizes the sample (10-30 s of CPU work in all)
+    t0 = time.perf_counter()
+    one()
+    t1 = time.perf_counter() - t0
+    rounds = max(1, int(args.cpu_seconds / max(t1, 1e-3)))
+    rounds = min(rounds, 8)
+    done[0] = 0
+    t0 = time.perf_counter()
+    for _ in range(rounds):
+        ts = [threading.Thread(target=one) for _ in range(threads)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    wall = time.perf_counter() - t0
+    n = done[0]
+    return {
+        "value": round(n * W * H / wall / 1e6, 3),
+        "unit": "MPix/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{n} x {W}x{H} RGBA8 -> {args.out}x{args.out} {args.filter} + libwebp q{args.quality}, "
+                  f"one image per thread, {threads} threads, {wall:.1f}s wall",
+        "value_1core": round(W * H / t1 / 1e6, 3),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    import torch
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    from imagekit import _lib
+    lib = _lib.load()
+    if lib.ik_init(local) != 0:
+        raise SystemExit(f"ik_init({local}) failed: {_lib.last_error()}")
+
+    S, O, B = args.size, args.out, args.batch
+    f = FILTERS[args.filter]
+    pitch = S * 4
+    # inputs resident in HBM before the timed region: 4 distinct synthetic frames tiled over the batch
+    distinct = [synth_rgba(S, S, seed=1000 * rank + i) for i in range(min(B, 4))]
+    src = torch.empty((B, S, pitch), dtype=torch.uint8, device=f"cuda:{local}")
+    for i in range(B):
+        src[i].copy_(torch.from_numpy(distinct[i % len(distinct)].reshape(S, pitch)))
+    torch.cuda.synchronize()
+
+    pipe = ctypes.c_void_p()
+    if lib.ik_pipeline_create(S, S, 4, O, O, f, 1, args.quality, B, args.threads, ctypes.byref(pipe)):
+        raise SystemExit(f"pipeline: {_lib.last_error()}")
+    out_cap = B * O * O * 4 + (1 << 20)
+    out = np.empty(out_cap, np.uint8)
+    sizes = (ctypes.c_size_t * B)()
+
+    def step():
+        if args.device_only:
+            rc = lib.ik_pipeline_run_device(pipe, ctypes.c_void_p(src.data_ptr()), pitch, S * pitch, B)
+        else:
+            rc = lib.ik_pipeline_run(pipe, ctypes.c_void_p(src.data_ptr()), pitch, S * pitch, B,
+                                     out.ctypes.data, out_cap, sizes)
+        if rc:
+            raise SystemExit(f"pipeline run: {_lib.last_error()}")
+        return lib.ik_pipeline_kernel_ms(pipe, 0), lib.ik_pipeline_kernel_ms(pipe, 1)
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(args.steps):
+        kms.append(step())
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    barrier()
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if not args.device_only:
+        assert bytes(out[:4]) == b"RIFF" and all(s > 0 for s in sizes)
+    resize_ms = float(np.mean([k[0] for k in kms]))
+    colour_ms = float(np.mean([k[1] for k in kms]))
+    bytes_per_img = 4 * S * S + 4 * O * O
+    achieved = B * bytes_per_img / (resize_ms * 1e-3) / 1e9
+    total_px = world * B * args.steps * S * S
+    value = total_px / elapsed / 1e6
+
+    # the other filter's kernel on the same batch (device-only), for DESIGN.md
+    alt = {}
+    alt_name = "lanczos3" if args.filter != "lanczos3" else "triangle"
+    p2 = ctypes.c_void_p()
+    if lib.ik_pipeline_create(S, S, 4, O, O, FILTERS[alt_name], 1, args.quality, B, 1, ctypes.byref(p2)) == 0:
+        ms = []
+        for i in range(6):
+            lib.ik_pipeline_run_device(p2, ctypes.c_void_p(src.data_ptr()), pitch, S * pitch, B)
+            if i >= 2:
+                ms.append(lib.ik_pipeline_kernel_ms(p2, 0))
+        m = float(np.mean(ms))
+        alt = {"filter": alt_name, "resize_ms": round(m, 4),
+               "achieved_GBps": round(B * bytes_per_img / (m * 1e-3) / 1e9, 1)}
+        lib.ik_pipeline_destroy(p2)
+    lib.ik_pipeline_destroy(pipe)
+
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_resize.json")
+    if os.path.exists(pmc):
+        try:
+            d = json.load(open(pmc))
+            key = f"{args.filter}_{S}_{O}_b{B}"
+            if key in d:
+                traffic = d[key]["hbm_bytes_per_launch"]
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, distinct[0])
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "MPix/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{S}x{S} RGBA8 frames resident in HBM -> resize_image {O}x{O} "
+                            f"({args.filter}) -> encode_image webp q{args.quality}; bytes to host",
+                "batch_per_gpu": B, "filter": args.filter, "format": "webp",
+                "quality": args.quality, "host_threads_per_gpu": args.threads,
+                "device_only": bool(args.device_only), "parallelism": f"images sharded, {world} rank(s)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": traffic,
+                "kernel": "k_resize_fused",
+                "kernel_ms": round(resize_ms, 4),
+                "bytes_per_launch": B * bytes_per_img,
+            },
+            "colour_kernel_ms": round(colour_ms, 4),
+            "alt_filter_kernel": alt,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -15,6 +15,8 @@ constexpr int kBytesPerLane = 8;         // vertical pass: bytes of a source row
 constexpr int kStripBytes = kBytesPerLane * kThreads;  // 2048 source bytes per strip
 constexpr int kRowWords = kStripBytes + kStripBytes / 8;  // LDS f32 row, +4 words per 32
 constexpr int kRowsPerFlush = 4;         // vertical rows staged in LDS per horizontal pass
+constexpr int kMaxStripCols = 512;       // output columns per strip (LDS offset/count tables)
+constexpr int kMaxStripWeights = 3072;   // horizontal weights per strip kept in LDS (12 KB)
 
 // Everything the resize kernels read.  Weight tables follow image 0.25.8
 // sample.rs (see ik_plan.cpp); tables live in one device allocation per plan.
@@ -36,6 +38,11 @@ struct ResizeArgs {
     int NS;
     const int* bands;  // [NB*2] (oy0, oy1)
     int NB;
+    // steady-state block tables of the fused kernel (output row r, r not first in its band):
+    const int* bs;              // [nh] first source row of r's block = max(end(r-1), ly[r])
+    const int* bn;              // [nh] rows in the block
+    const unsigned long long* bmask;  // [nh] bit j*A+d: source row bs+j is in row r+d's window
+    const float* bw;            // [nh][R][A] weight of source row bs+j for output row r+d (0 if not)
     float* tmp;        // naive path only: f32 vertical intermediate [n][nh][row_bytes]
 };
 
@@ -43,6 +50,8 @@ struct ResizeArgs {
 struct ResizePlan {
     int W = 0, H = 0, C = 0, nw = 0, nh = 0, filter = 0;
     int slots = 0;        // accumulator slots the fused kernel needs (0 = naive path)
+    int rows = 0;         // prefetch depth: max source rows consumed per output row
+    bool weights_in_lds = false;
     int NS = 0, NB = 0;
     size_t table_bytes = 0;
     void* dev_tables = nullptr;

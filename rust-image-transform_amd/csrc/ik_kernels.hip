@@ -22,123 +22,228 @@ namespace ik {
 
 __device__ __forceinline__ int lds_idx(int i) { return i + ((i >> 5) << 2); }
 
+// Read-only plan tables through the constant address space: wave-uniform
+// addresses then compile to scalar (SMEM) loads instead of vector loads +
+// v_readfirstlane (the tables are never written by a kernel).
+template <typename T>
+using cptr = const __attribute__((address_space(4))) T*;
+template <typename T>
+__device__ __forceinline__ cptr<T> as_const(const T* p) { return (cptr<T>)p; }
+
 // clamp(t, 0, 255) then f32::round (half away from zero) -> u8   (sample.rs FloatNearest)
 __device__ __forceinline__ uint8_t float_nearest_u8(float t) {
     t = t < 0.0f ? 0.0f : (t > 255.0f ? 255.0f : t);
     return (uint8_t)roundf(t);
 }
 
-// Horizontal pass over `nrows` completed vertical rows staged in LDS.
+// Horizontal pass over `nrows` (<= kRowsPerFlush) completed vertical rows staged
+// in LDS.  Lane = (output column, channel) of the strip; each lane computes the
+// rows together so every weight read feeds nrows taps.
 // out(r, ox, c) = round(sum_k tmp[r][(lx[ox]+k)*C + c] * wx[ox][k]), sequential k.
 __device__ __forceinline__ void horizontal_rows(const ResizeArgs& a, const float* __restrict__ lds,
-                                                int r0, int nrows, int ox0, int ox1, int sb,
-                                                uint8_t* __restrict__ dst) {
+                                                const float* __restrict__ sw, const int* __restrict__ soff,
+                                                const int* __restrict__ sn, int r0, int nrows, int ox0,
+                                                int nox, uint8_t* __restrict__ dst) {
     const int C = a.C;
-    const int per_row = (ox1 - ox0) * C;
-    const int total = nrows * per_row;
+    const int total = nox * C;
     for (int v = threadIdx.x; v < total; v += kThreads) {
-        const int row = v / per_row;
-        const int rem = v - row * per_row;
-        const int oxl = rem / C;
-        const int c = rem - oxl * C;
-        const int ox = ox0 + oxl;
-        const int n = a.nx[ox];
-        const float* __restrict__ w = a.wx + (size_t)ox * a.Tx;
-        const float* __restrict__ t = lds + row * kRowWords;
-        int idx = a.lx[ox] * C + c - sb;
-        float acc = 0.0f;
+        const int oxl = v / C;
+        const int c = v - oxl * C;
+        const int n = sn[oxl];
+        const float* __restrict__ w = sw + oxl * a.Tx;
+        int idx = soff[oxl] + c;
+        float acc[kRowsPerFlush];
+#pragma unroll
+        for (int q = 0; q < kRowsPerFlush; ++q) acc[q] = 0.0f;
         for (int k = 0; k < n; ++k, idx += C) {
-            const float prod = t[lds_idx(idx)] * w[k];
-            acc = acc + prod;
+            const float wk = w[k];
+            const int li = lds_idx(idx);
+#pragma unroll
+            for (int q = 0; q < kRowsPerFlush; ++q) {
+                const float prod = lds[q * kRowWords + li] * wk;
+                acc[q] = acc[q] + prod;
+            }
         }
-        dst[(size_t)(r0 + row) * a.dst_pitch + (size_t)ox * C + c] = float_nearest_u8(acc);
+        uint8_t* o = dst + (size_t)r0 * a.dst_pitch + (size_t)(ox0 + oxl) * C + c;
+#pragma unroll
+        for (int q = 0; q < kRowsPerFlush; ++q)
+            if (q < nrows) o[(size_t)q * a.dst_pitch] = float_nearest_u8(acc[q]);
     }
 }
 
 // Fused resampler.  Workgroup = (column strip, band of output rows, image).
 // Each lane owns kBytesPerLane consecutive bytes of the strip (the vertical pass
-// is channel-agnostic), sweeps the band's source rows top to bottom exactly once
-// and scatters every converted source row into the A rolling accumulators of the
-// output rows whose tap window contains it (A >= max rows open at once, checked
-// on the host).  Completed rows go to LDS; every kRowsPerFlush rows the workgroup
-// runs the horizontal pass on them.  All per-row scalars are wave-uniform.
-template <int A>
+// is channel-agnostic) and sweeps the band's source rows top to bottom once.
+// Output row r's tap window is consumed as "block" [end(r-1), end(r)); the rows
+// of block r+1 are prefetched into registers (R loads in flight per lane) while
+// block r is scattered into the A rolling accumulators acc[d] = output row r+d
+// (A >= rows open at once, checked on the host).  When row r completes, acc[0]
+// goes to LDS and the accumulators shift down one slot.  Every kRowsPerFlush
+// rows the workgroup runs the horizontal pass from LDS.  Row scalars and
+// weights are wave-uniform (scalar loads); the weights of the strip's output
+// columns sit in LDS when they fit (WL).
+template <int A, int R, bool WL>
 __global__ __launch_bounds__(kThreads) void k_resize_fused(ResizeArgs a) {
     __shared__ __attribute__((aligned(16))) float lds[kRowsPerFlush * kRowWords];
-    static_assert(A % kRowsPerFlush == 0, "flush points must be compile-time");
+    __shared__ float s_w[WL ? kMaxStripWeights : 1];
+    __shared__ int s_off[kMaxStripCols];
+    __shared__ int s_n[kMaxStripCols];
 
     const int tile = blockIdx.x;
     const int img = blockIdx.y;
     const int strip = tile % a.NS;
     const int band = tile / a.NS;
-    const int ox0 = a.strips[3 * strip], ox1 = a.strips[3 * strip + 1], sb = a.strips[3 * strip + 2];
-    const int oy0 = a.bands[2 * band], oy1 = a.bands[2 * band + 1];
+    const cptr<int> strips = as_const(a.strips);
+    const cptr<int> bands = as_const(a.bands);
+    const cptr<int> cly = as_const(a.ly);
+    const cptr<int> cny = as_const(a.ny);
+    const cptr<float> cwy = as_const(a.wy);
+    const int ox0 = strips[3 * strip], ox1 = strips[3 * strip + 1], sb = strips[3 * strip + 2];
+    const int nox = ox1 - ox0;
+    const int oy0 = bands[2 * band], oy1 = bands[2 * band + 1];
     const uint8_t* __restrict__ src = a.src + (size_t)img * a.src_img_stride;
     uint8_t* __restrict__ dst = a.dst + (size_t)img * a.dst_img_stride;
 
+    for (int t = threadIdx.x; t < nox; t += kThreads) {
+        s_off[t] = a.lx[ox0 + t] * a.C - sb;
+        s_n[t] = a.nx[ox0 + t];
+    }
+    if (WL) {
+        const float* __restrict__ gw = a.wx + (size_t)ox0 * a.Tx;
+        for (int t = threadIdx.x; t < nox * a.Tx; t += kThreads) s_w[t] = gw[t];
+    }
+    const float* __restrict__ hw = WL ? s_w : a.wx + (size_t)ox0 * a.Tx;
+
     const int mybyte = sb + kBytesPerLane * (int)threadIdx.x;
-    const bool active = mybyte < a.row_bytes;
-    const uint8_t* __restrict__ colp = src + (active ? mybyte : 0);
+    const uint8_t* __restrict__ colp = src + (mybyte < a.row_bytes ? mybyte : 0);
     float* __restrict__ my_lds = lds + lds_idx(kBytesPerLane * (int)threadIdx.x);
+    const int Hm1 = a.H - 1;
+    const size_t pitch = a.src_pitch;
+    auto ld = [&](int row) -> uint2 {
+        row = row < Hm1 ? row : Hm1;
+        return *reinterpret_cast<const uint2*>(colp + (size_t)row * pitch);
+    };
 
     float acc[A][kBytesPerLane];
 #pragma unroll
-    for (int s = 0; s < A; ++s)
+    for (int d = 0; d < A; ++d)
 #pragma unroll
-        for (int j = 0; j < kBytesPerLane; ++j) acc[s][j] = 0.0f;
+        for (int j = 0; j < kBytesPerLane; ++j) acc[d][j] = 0.0f;
 
-    int i = a.ly[oy0];
-    for (int rbase = oy0; rbase < oy1; rbase += A) {
-        // per-slot row scalars for this round (wave-uniform)
-        int ly_[2 * A], ny_[2 * A];
+    uint2 buf0[R], buf1[R];
+    int cs = cly[oy0];
+    int ce = cs + cny[oy0];
+    bool cpf = ce - cs <= R;
+    if (cpf) {
 #pragma unroll
-        for (int d = 0; d < 2 * A; ++d) {
-            const int rr = rbase + d;
-            const bool ok = rr < oy1;
-            ly_[d] = ok ? a.ly[rr] : 0x7fffffff;
-            ny_[d] = ok ? a.ny[rr] : 0;
+        for (int j = 0; j < R; ++j) buf0[j] = ld(cs + j);
+    }
+    __syncthreads();  // s_w / s_off / s_n ready
+
+    const cptr<int> cbs = as_const(a.bs);
+    const cptr<int> cbn = as_const(a.bn);
+    const cptr<unsigned long long> cbm = as_const(a.bmask);
+    const cptr<float> cbw = as_const(a.bw);
+
+    auto cvt8 = [](uint2 raw, float (&p)[kBytesPerLane]) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            p[j] = (float)((raw.x >> (8 * j)) & 0xffu);
+            p[4 + j] = (float)((raw.y >> (8 * j)) & 0xffu);
         }
+    };
+    auto mac = [&](float (&dst)[kBytesPerLane], const float (&p)[kBytesPerLane], float w) {
 #pragma unroll
-        for (int s = 0; s < A; ++s) {
-            const int r = rbase + s;
-            if (r < oy1) {
-                const int iend = ly_[s] + ny_[s];
-                i = i > ly_[s] ? i : ly_[s];
-                for (; i < iend; ++i) {
-                    uint2 raw = make_uint2(0u, 0u);
-                    if (active) raw = *reinterpret_cast<const uint2*>(colp + (size_t)i * a.src_pitch);
+        for (int j = 0; j < kBytesPerLane; ++j) {
+            const float prod = p[j] * w;
+            dst[j] = dst[j] + prod;
+        }
+    };
+
+    // one output row r: consume its block [cs, ce) (prefetched in `cur` when cpf),
+    // prefetch the next row's block into `nxt`
+    auto body = [&](int r, uint2 (&cur)[R], uint2 (&nxt)[R]) {
+        const bool has_next = r + 1 < oy1;
+        const int ns = has_next ? cbs[r + 1] : ce;
+        const int ne = has_next ? ns + cbn[r + 1] : ce;
+        const bool npf = has_next && ne - ns <= R;
+        if (npf) {
+#pragma unroll
+            for (int j = 0; j < R; ++j) nxt[j] = ld(ns + j);
+        }
+        if (cpf && r != oy0) {
+            // steady state: A*R weights and the activity mask from the block tables
+            const unsigned long long m = cbm[r];
+            const cptr<float> w = cbw + (size_t)r * (R * A);
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                if ((m >> (j * A)) & ((1ull << A) - 1ull)) {
                     float p[kBytesPerLane];
+                    cvt8(cur[j], p);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        p[j] = (float)((raw.x >> (8 * j)) & 0xffu);
-                        p[4 + j] = (float)((raw.y >> (8 * j)) & 0xffu);
-                    }
-#pragma unroll
-                    for (int d = 0; d < A; ++d) {
-                        const int kk = i - ly_[s + d];
-                        if (kk >= 0 && kk < ny_[s + d]) {
-                            const float w = a.wy[(size_t)(r + d) * a.Ty + kk];
-#pragma unroll
-                            for (int j = 0; j < kBytesPerLane; ++j) {
-                                const float prod = p[j] * w;
-                                acc[(s + d) % A][j] = acc[(s + d) % A][j] + prod;
-                            }
-                        }
-                    }
-                }
-                // row r complete -> LDS slot (r - oy0) % kRowsPerFlush
-                float* o = my_lds + (s % kRowsPerFlush) * kRowWords;
-                *reinterpret_cast<float4*>(o) = make_float4(acc[s][0], acc[s][1], acc[s][2], acc[s][3]);
-                *reinterpret_cast<float4*>(o + 4) = make_float4(acc[s][4], acc[s][5], acc[s][6], acc[s][7]);
-#pragma unroll
-                for (int j = 0; j < kBytesPerLane; ++j) acc[s][j] = 0.0f;
-                if ((s % kRowsPerFlush) == kRowsPerFlush - 1 || r == oy1 - 1) {
-                    __syncthreads();
-                    const int nrows = (s % kRowsPerFlush) + 1;
-                    horizontal_rows(a, lds, r - (nrows - 1), nrows, ox0, ox1, sb, dst);
-                    __syncthreads();
+                    for (int d = 0; d < A; ++d)
+                        if ((m >> (j * A + d)) & 1ull) mac(acc[d], p, w[j * A + d]);
                 }
             }
+        } else {
+            // first row of the band (its whole window) or an oversized block
+            int lyv[A], nyv[A];
+#pragma unroll
+            for (int d = 0; d < A; ++d) {
+                const int rr = r + d;
+                const bool ok = rr < oy1;
+                lyv[d] = ok ? cly[rr] : 0x3fffffff;
+                nyv[d] = ok ? cny[rr] : 0;
+            }
+            auto scatter = [&](uint2 raw, int i) {
+                float p[kBytesPerLane];
+                cvt8(raw, p);
+#pragma unroll
+                for (int d = 0; d < A; ++d) {
+                    const int kk = i - lyv[d];
+                    if (kk >= 0 && kk < nyv[d]) mac(acc[d], p, cwy[(size_t)(r + d) * a.Ty + kk]);
+                }
+            };
+            if (cpf) {
+#pragma unroll
+                for (int j = 0; j < R; ++j)
+                    if (cs + j < ce) scatter(cur[j], cs + j);
+            } else {
+                for (int c0 = cs; c0 < ce; c0 += R) {
+                    uint2 t[R];
+#pragma unroll
+                    for (int j = 0; j < R; ++j) t[j] = ld(c0 + j);
+#pragma unroll
+                    for (int j = 0; j < R; ++j)
+                        if (c0 + j < ce) scatter(t[j], c0 + j);
+                }
+            }
+        }
+        // row r complete -> LDS slot, shift the accumulators down
+        float* o = my_lds + ((r - oy0) % kRowsPerFlush) * kRowWords;
+        *reinterpret_cast<float4*>(o) = make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
+        *reinterpret_cast<float4*>(o + 4) = make_float4(acc[0][4], acc[0][5], acc[0][6], acc[0][7]);
+#pragma unroll
+        for (int d = 0; d + 1 < A; ++d)
+#pragma unroll
+            for (int j = 0; j < kBytesPerLane; ++j) acc[d][j] = acc[d + 1][j];
+#pragma unroll
+        for (int j = 0; j < kBytesPerLane; ++j) acc[A - 1][j] = 0.0f;
+        cs = ns;
+        ce = ne;
+        cpf = npf;
+    };
+
+    int fbase = oy0;  // first row not yet flushed
+    for (int r = oy0; r < oy1; r += 2) {
+        body(r, buf0, buf1);
+        if (r + 1 < oy1) body(r + 1, buf1, buf0);
+        const int last = r + 1 < oy1 ? r + 1 : r;
+        if (last - fbase + 1 == kRowsPerFlush || last == oy1 - 1) {
+            __syncthreads();
+            horizontal_rows(a, lds, hw, s_off, s_n, fbase, last - fbase + 1, ox0, nox, dst);
+            __syncthreads();
+            fbase = last + 1;
         }
     }
 }
@@ -188,13 +293,19 @@ hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_
     a.tmp = naive_tmp;
     if (plan.slots > 0) {
         dim3 grid(plan.NS * plan.NB, n);
-        switch (plan.slots) {
-        case 4: hipLaunchKernelGGL(k_resize_fused<4>, grid, dim3(kThreads), 0, s, a); break;
-        case 8: hipLaunchKernelGGL(k_resize_fused<8>, grid, dim3(kThreads), 0, s, a); break;
-        case 16: hipLaunchKernelGGL(k_resize_fused<16>, grid, dim3(kThreads), 0, s, a); break;
-        default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
+        const bool wl = plan.weights_in_lds;
+#define IK_LAUNCH(A_, R_)                                                                         \
+    if (plan.slots == A_ && plan.rows == R_) {                                                    \
+        if (wl) hipLaunchKernelGGL((k_resize_fused<A_, R_, true>), grid, dim3(kThreads), 0, s, a); \
+        else hipLaunchKernelGGL((k_resize_fused<A_, R_, false>), grid, dim3(kThreads), 0, s, a);   \
+        return hipGetLastError();                                                                 \
+    }
+        // instances that fit the register file without spilling (ik_plan.cpp picks)
+        IK_LAUNCH(4, 4) IK_LAUNCH(4, 8)
+        IK_LAUNCH(8, 4) IK_LAUNCH(8, 8)
+        IK_LAUNCH(16, 4)
+#undef IK_LAUNCH
+        return hipErrorInvalidValue;
     }
     if (!naive_tmp) return hipErrorInvalidValue;
     dim3 g1((a.row_bytes + kThreads - 1) / kThreads, a.nh, n);

@@ -7,7 +7,9 @@
 // normalised by the sequential f32 sum (w /= sum).  They are computed once per
 // geometry on the host -- with glibc sinf/expf, as rustc's f32::sin/exp are --
 // and uploaded, so the device kernels only multiply and add.
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -139,20 +141,59 @@ ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int
     int A = required_slots(ly, cy);
     int slots = A <= 4 ? 4 : A <= 8 ? 8 : A <= 16 ? 16 : 0;
 
-    // column strips: as many output columns as fit kStripBytes source bytes
+    // prefetch depth: source rows consumed per output row after the first
+    int maxblk = 1;
+    for (int r = 1; r < nh; ++r) {
+        const int b = ly[r] + cy[r] - std::max(ly[r - 1] + cy[r - 1], ly[r]);
+        maxblk = std::max(maxblk, b);
+    }
+    int rows = maxblk <= 4 ? 4 : maxblk <= 8 ? 8 : 16;
+    // non-spilling instances: A=4,8 -> R<=8, A=16 -> R=4 (larger blocks
+    // take the kernel's chunked path)
+    if (slots <= 8 && rows > 8) rows = 8;
+    if (slots == 16) rows = 4;
+    // column strips: as many output columns as fit kStripBytes source bytes (and,
+    // when possible, kMaxStripWeights horizontal weights in LDS)
+    bool wl = (long)Tx <= kMaxStripWeights;
     std::vector<int> strips;
-    for (int ox0 = 0; ox0 < nw && slots;) {
-        const int sb = (lx[ox0] * C) & ~15;
-        int ox1 = ox0;
-        while (ox1 < nw && (lx[ox1] + cx[ox1]) * C - sb <= kStripBytes) ++ox1;
-        if (ox1 == ox0) { slots = 0; break; }  // one output column wider than a strip
-        strips.push_back(ox0); strips.push_back(ox1); strips.push_back(sb);
-        ox0 = ox1;
+    for (int pass = 0; pass < 2 && slots; ++pass) {
+        strips.clear();
+        bool ok = true;
+        for (int ox0 = 0; ox0 < nw;) {
+            const int sb = (lx[ox0] * C) & ~15;
+            int ox1 = ox0;
+            while (ox1 < nw && (lx[ox1] + cx[ox1]) * C - sb <= kStripBytes && ox1 - ox0 < kMaxStripCols &&
+                   (!wl || (long)(ox1 - ox0 + 1) * Tx <= kMaxStripWeights))
+                ++ox1;
+            if (ox1 == ox0) { ok = false; break; }  // one output column wider than a strip
+            strips.push_back(ox0); strips.push_back(ox1); strips.push_back(sb);
+            ox0 = ox1;
+        }
+        if (!ok) { slots = 0; break; }
+        // weights in LDS only when that costs at most ~10% more strips
+        if (wl && pass == 0) {
+            std::vector<int> keep = strips;
+            int ns_wl = (int)strips.size() / 3;
+            wl = false;
+            strips.clear();
+            int ns_gl = 0;
+            for (int ox0 = 0; ox0 < nw;) {
+                const int sb = (lx[ox0] * C) & ~15;
+                int ox1 = ox0;
+                while (ox1 < nw && (lx[ox1] + cx[ox1]) * C - sb <= kStripBytes && ox1 - ox0 < kMaxStripCols) ++ox1;
+                ++ns_gl;
+                ox0 = ox1 > ox0 ? ox1 : ox0 + 1;
+            }
+            if (ns_wl * 10 <= ns_gl * 11) { wl = true; strips = keep; break; }
+            continue;  // second pass without the LDS-weights limit
+        }
+        break;
     }
     const int NS = slots ? (int)strips.size() / 3 : 0;
     int band_h = nh;
     if (slots) {
-        const long target = 2048;
+        long target = 2048;
+        if (const char* e = getenv("IK_TARGET_WG")) target = atol(e);
         long per_img = (target + n - 1) / n;
         long nb = (per_img + NS - 1) / NS;
         if (nb < 1) nb = 1;
@@ -161,6 +202,7 @@ ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int
         band_h = ((band_h + slots - 1) / slots) * slots;
         if (band_h > nh) band_h = nh;
     }
+    if (const char* e = getenv("IK_BAND_ROWS")) band_h = std::max(1, std::min(nh, atoi(e)));
     const auto key = std::make_tuple(device, W, H, C, nw, nh, filter, band_h);
     std::lock_guard<std::mutex> lk(g_plan_mu);
     auto it = g_plans.find(key);
@@ -169,14 +211,39 @@ ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int
     std::vector<int> bands;
     for (int y = 0; y < nh; y += band_h) { bands.push_back(y); bands.push_back(y + band_h < nh ? y + band_h : nh); }
 
+    // steady-state block tables (see ResizeArgs)
+    std::vector<int> bsv(nh, 0), bnv(nh, 0);
+    std::vector<unsigned long long> bmv(nh, 0);
+    std::vector<float> bwv;
+    if (slots) {
+        bwv.assign((size_t)nh * rows * slots, 0.0f);
+        for (int r = 1; r < nh; ++r) {
+            const int st = std::max(ly[r - 1] + cy[r - 1], ly[r]);
+            const int en = ly[r] + cy[r];
+            bsv[r] = st;
+            bnv[r] = en - st;
+            for (int j = 0; j < rows && st + j < en; ++j)
+                for (int d = 0; d < slots && r + d < nh; ++d) {
+                    const int kk = st + j - ly[r + d];
+                    if (kk >= 0 && kk < cy[r + d]) {
+                        bmv[r] |= 1ull << (j * slots + d);
+                        bwv[((size_t)r * rows + j) * slots + d] = wy[(size_t)(r + d) * Ty + kk];
+                    }
+                }
+        }
+    }
+
     std::vector<char> blob;
     const size_t o_ly = put(blob, ly), o_cy = put(blob, cy), o_wy = put(blob, wy);
     const size_t o_lx = put(blob, lx), o_cx = put(blob, cx), o_wx = put(blob, wx);
     const size_t o_st = put(blob, strips), o_bd = put(blob, bands);
+    const size_t o_bs = put(blob, bsv), o_bn = put(blob, bnv), o_bm = put(blob, bmv), o_bw = put(blob, bwv);
 
     auto* p = new ResizePlan();
     p->W = W; p->H = H; p->C = C; p->nw = nw; p->nh = nh; p->filter = filter;
     p->slots = slots;
+    p->rows = rows;
+    p->weights_in_lds = wl;
     p->NS = NS;
     p->NB = (int)bands.size() / 2;
     p->table_bytes = blob.size();
@@ -193,6 +260,8 @@ ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int
     a.lx = (const int*)(d + o_lx); a.nx = (const int*)(d + o_cx); a.wx = (const float*)(d + o_wx); a.Tx = Tx;
     a.strips = (const int*)(d + o_st); a.NS = p->NS;
     a.bands = (const int*)(d + o_bd); a.NB = p->NB;
+    a.bs = (const int*)(d + o_bs); a.bn = (const int*)(d + o_bn);
+    a.bmask = (const unsigned long long*)(d + o_bm); a.bw = (const float*)(d + o_bw);
     g_plans[key] = p;
     return p;
 }
