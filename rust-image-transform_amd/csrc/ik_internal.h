@@ -14,7 +14,7 @@ constexpr int kThreads = 256;            // workgroup size (4 wave64s)
 constexpr int kBytesPerLane = 8;         // vertical pass: bytes of a source row per lane
 constexpr int kStripBytes = kBytesPerLane * kThreads;  // 2048 source bytes per strip
 constexpr int kRowWords = kStripBytes + kStripBytes / 8;  // LDS f32 row, +4 words per 32
-constexpr int kRowsPerFlush = 4;         // vertical rows staged in LDS per horizontal pass
+constexpr int kRowsPerFlush = 3;         // vertical rows staged in LDS per horizontal pass
 constexpr int kMaxStripCols = 512;       // output columns per strip (LDS offset/count tables)
 constexpr int kMaxStripWeights = 3072;   // horizontal weights per strip kept in LDS (12 KB)
 
@@ -38,11 +38,15 @@ struct ResizeArgs {
     int NS;
     const int* bands;  // [NB*2] (oy0, oy1)
     int NB;
-    // steady-state block tables of the fused kernel (output row r, r not first in its band):
-    const int* bs;              // [nh] first source row of r's block = max(end(r-1), ly[r])
-    const int* bn;              // [nh] rows in the block
-    const unsigned long long* bmask;  // [nh] bit j*A+d: source row bs+j is in row r+d's window
-    const float* bw;            // [nh][R][A] weight of source row bs+j for output row r+d (0 if not)
+    // fused-kernel step tables.  A band is a sequence of steps; a step brings in
+    // up to R new source rows [start, start+count) and scatters them into the A
+    // rolling accumulators (acc[d] = output row next+d); `emit` completes row next.
+    const int* step_hdr;        // [nsteps][4] (start, count, emit, 0)
+    const unsigned long long* step_mask;  // [nsteps] bit j*A+d: row start+j feeds acc[d]
+    const float* step_w;        // [nsteps][R][A] the matching weights (0 elsewhere)
+    const int* band_step;       // [NB+1] first step of each band
+    int max_strip_cols;      // max output columns of a strip (LDS table size)
+    int max_strip_weights;   // max nox*Tx of a strip (LDS weights size when in LDS)
     float* tmp;        // naive path only: f32 vertical intermediate [n][nh][row_bytes]
 };
 

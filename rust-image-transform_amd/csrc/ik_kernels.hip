@@ -71,23 +71,26 @@ __device__ __forceinline__ void horizontal_rows(const ResizeArgs& a, const float
     }
 }
 
+// waves per SIMD to ask the register allocator for (A=8 fits 168 VGPRs at 3)
+template <int A>
+struct FusedOcc { static constexpr int value = A <= 4 ? 4 : (A <= 8 ? 3 : 1); };
+
 // Fused resampler.  Workgroup = (column strip, band of output rows, image).
 // Each lane owns kBytesPerLane consecutive bytes of the strip (the vertical pass
-// is channel-agnostic) and sweeps the band's source rows top to bottom once.
-// Output row r's tap window is consumed as "block" [end(r-1), end(r)); the rows
-// of block r+1 are prefetched into registers (R loads in flight per lane) while
-// block r is scattered into the A rolling accumulators acc[d] = output row r+d
-// (A >= rows open at once, checked on the host).  When row r completes, acc[0]
-// goes to LDS and the accumulators shift down one slot.  Every kRowsPerFlush
-// rows the workgroup runs the horizontal pass from LDS.  Row scalars and
-// weights are wave-uniform (scalar loads); the weights of the strip's output
-// columns sit in LDS when they fit (WL).
+// is channel-agnostic) and sweeps the band's source rows top to bottom once, as
+// a host-built sequence of steps: step k brings in up to R new source rows and
+// scatters each converted row into the A rolling accumulators acc[d] = output
+// row next+d (host-computed activity mask + weights, wave-uniform scalar loads);
+// an `emit` step completes row `next`: acc[0] goes to LDS and the accumulators
+// shift down.  Prefetch is a rolling two-step register ring: step k sits in
+// buf[k&1]; as soon as row j of step k is converted its registers are refilled
+// (unconditionally, so the compiler's vmcnt bookkeeping stays exact) with row j
+// of step k+2, keeping ~2R loads per lane in flight.  Every kRowsPerFlush
+// completed rows the workgroup runs the horizontal pass from LDS.  LDS is
+// dynamic: [kRowsPerFlush rows of f32 tmp][strip weights if WL][offsets][taps].
 template <int A, int R, bool WL>
-__global__ __launch_bounds__(kThreads) void k_resize_fused(ResizeArgs a) {
-    __shared__ __attribute__((aligned(16))) float lds[kRowsPerFlush * kRowWords];
-    __shared__ float s_w[WL ? kMaxStripWeights : 1];
-    __shared__ int s_off[kMaxStripCols];
-    __shared__ int s_n[kMaxStripCols];
+__global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(ResizeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
 
     const int tile = blockIdx.x;
     const int img = blockIdx.y;
@@ -95,15 +98,20 @@ __global__ __launch_bounds__(kThreads) void k_resize_fused(ResizeArgs a) {
     const int band = tile / a.NS;
     const cptr<int> strips = as_const(a.strips);
     const cptr<int> bands = as_const(a.bands);
-    const cptr<int> cly = as_const(a.ly);
-    const cptr<int> cny = as_const(a.ny);
-    const cptr<float> cwy = as_const(a.wy);
+    const cptr<int> shdr = as_const(a.step_hdr);
+    const cptr<unsigned long long> smask = as_const(a.step_mask);
+    const cptr<float> sw = as_const(a.step_w);
+    const cptr<int> bstep = as_const(a.band_step);
     const int ox0 = strips[3 * strip], ox1 = strips[3 * strip + 1], sb = strips[3 * strip + 2];
     const int nox = ox1 - ox0;
     const int oy0 = bands[2 * band], oy1 = bands[2 * band + 1];
+    const int kb = bstep[band], ke = bstep[band + 1];
     const uint8_t* __restrict__ src = a.src + (size_t)img * a.src_img_stride;
     uint8_t* __restrict__ dst = a.dst + (size_t)img * a.dst_img_stride;
 
+    float* __restrict__ s_w = lds + kRowsPerFlush * kRowWords;
+    int* __restrict__ s_off = reinterpret_cast<int*>(s_w + (WL ? a.max_strip_weights : 0));
+    int* __restrict__ s_n = s_off + a.max_strip_cols;
     for (int t = threadIdx.x; t < nox; t += kThreads) {
         s_off[t] = a.lx[ox0 + t] * a.C - sb;
         s_n[t] = a.nx[ox0 + t];
@@ -114,14 +122,22 @@ __global__ __launch_bounds__(kThreads) void k_resize_fused(ResizeArgs a) {
     }
     const float* __restrict__ hw = WL ? s_w : a.wx + (size_t)ox0 * a.Tx;
 
+    // Source rows through a buffer descriptor over this image: per-lane byte
+    // offset in voffset (constant), row * pitch in soffset (scalar).
     const int mybyte = sb + kBytesPerLane * (int)threadIdx.x;
-    const uint8_t* __restrict__ colp = src + (mybyte < a.row_bytes ? mybyte : 0);
+    const int voff = mybyte < a.row_bytes ? mybyte : 0;
+    const unsigned long long base = (unsigned long long)src;
+    const unsigned blo = __builtin_amdgcn_readfirstlane((unsigned)base);
+    const unsigned bhi = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((unsigned long long)bhi << 32) | blo), (short)0, (int)(a.src_pitch * a.H), 0x00020000);
     float* __restrict__ my_lds = lds + lds_idx(kBytesPerLane * (int)threadIdx.x);
     const int Hm1 = a.H - 1;
-    const size_t pitch = a.src_pitch;
+    const int pitch = (int)a.src_pitch;
     auto ld = [&](int row) -> uint2 {
         row = row < Hm1 ? row : Hm1;
-        return *reinterpret_cast<const uint2*>(colp + (size_t)row * pitch);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, voff, row * pitch, 0);
+        return make_uint2(v[0], v[1]);
     };
 
     float acc[A][kBytesPerLane];
@@ -131,120 +147,70 @@ __global__ __launch_bounds__(kThreads) void k_resize_fused(ResizeArgs a) {
         for (int j = 0; j < kBytesPerLane; ++j) acc[d][j] = 0.0f;
 
     uint2 buf0[R], buf1[R];
-    int cs = cly[oy0];
-    int ce = cs + cny[oy0];
-    bool cpf = ce - cs <= R;
-    if (cpf) {
+    {
+        const int s0 = shdr[4 * kb];
+        const int s1 = kb + 1 < ke ? shdr[4 * (kb + 1)] : s0;
 #pragma unroll
-        for (int j = 0; j < R; ++j) buf0[j] = ld(cs + j);
+        for (int j = 0; j < R; ++j) buf0[j] = ld(s0 + j);
+#pragma unroll
+        for (int j = 0; j < R; ++j) buf1[j] = ld(s1 + j);
     }
     __syncthreads();  // s_w / s_off / s_n ready
 
-    const cptr<int> cbs = as_const(a.bs);
-    const cptr<int> cbn = as_const(a.bn);
-    const cptr<unsigned long long> cbm = as_const(a.bmask);
-    const cptr<float> cbw = as_const(a.bw);
-
-    auto cvt8 = [](uint2 raw, float (&p)[kBytesPerLane]) {
+    int next = oy0;  // next output row to complete
+    auto body = [&](int k, uint2 (&cur)[R]) {
+        const int hstart = shdr[4 * k], hemit = shdr[4 * k + 2];
+        const unsigned long long m = smask[k];
+        const cptr<float> w = sw + (size_t)k * (R * A);
+        const int s2 = k + 2 < ke ? shdr[4 * (k + 2)] : hstart;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            p[j] = (float)((raw.x >> (8 * j)) & 0xffu);
-            p[4 + j] = (float)((raw.y >> (8 * j)) & 0xffu);
-        }
-    };
-    auto mac = [&](float (&dst)[kBytesPerLane], const float (&p)[kBytesPerLane], float w) {
-#pragma unroll
-        for (int j = 0; j < kBytesPerLane; ++j) {
-            const float prod = p[j] * w;
-            dst[j] = dst[j] + prod;
-        }
-    };
-
-    // one output row r: consume its block [cs, ce) (prefetched in `cur` when cpf),
-    // prefetch the next row's block into `nxt`
-    auto body = [&](int r, uint2 (&cur)[R], uint2 (&nxt)[R]) {
-        const bool has_next = r + 1 < oy1;
-        const int ns = has_next ? cbs[r + 1] : ce;
-        const int ne = has_next ? ns + cbn[r + 1] : ce;
-        const bool npf = has_next && ne - ns <= R;
-        if (npf) {
-#pragma unroll
-            for (int j = 0; j < R; ++j) nxt[j] = ld(ns + j);
-        }
-        if (cpf && r != oy0) {
-            // steady state: A*R weights and the activity mask from the block tables
-            const unsigned long long m = cbm[r];
-            const cptr<float> w = cbw + (size_t)r * (R * A);
-#pragma unroll
-            for (int j = 0; j < R; ++j) {
-                if ((m >> (j * A)) & ((1ull << A) - 1ull)) {
-                    float p[kBytesPerLane];
-                    cvt8(cur[j], p);
-#pragma unroll
-                    for (int d = 0; d < A; ++d)
-                        if ((m >> (j * A + d)) & 1ull) mac(acc[d], p, w[j * A + d]);
-                }
-            }
-        } else {
-            // first row of the band (its whole window) or an oversized block
-            int lyv[A], nyv[A];
-#pragma unroll
-            for (int d = 0; d < A; ++d) {
-                const int rr = r + d;
-                const bool ok = rr < oy1;
-                lyv[d] = ok ? cly[rr] : 0x3fffffff;
-                nyv[d] = ok ? cny[rr] : 0;
-            }
-            auto scatter = [&](uint2 raw, int i) {
+        for (int j = 0; j < R; ++j) {
+            if ((m >> (j * A)) & ((1ull << A) - 1ull)) {
+                const uint2 raw = cur[j];
                 float p[kBytesPerLane];
-                cvt8(raw, p);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    p[q] = (float)((raw.x >> (8 * q)) & 0xffu);
+                    p[4 + q] = (float)((raw.y >> (8 * q)) & 0xffu);
+                }
 #pragma unroll
                 for (int d = 0; d < A; ++d) {
-                    const int kk = i - lyv[d];
-                    if (kk >= 0 && kk < nyv[d]) mac(acc[d], p, cwy[(size_t)(r + d) * a.Ty + kk]);
-                }
-            };
-            if (cpf) {
+                    if ((m >> (j * A + d)) & 1ull) {
+                        const float wt = w[j * A + d];
 #pragma unroll
-                for (int j = 0; j < R; ++j)
-                    if (cs + j < ce) scatter(cur[j], cs + j);
-            } else {
-                for (int c0 = cs; c0 < ce; c0 += R) {
-                    uint2 t[R];
-#pragma unroll
-                    for (int j = 0; j < R; ++j) t[j] = ld(c0 + j);
-#pragma unroll
-                    for (int j = 0; j < R; ++j)
-                        if (c0 + j < ce) scatter(t[j], c0 + j);
+                        for (int q = 0; q < kBytesPerLane; ++q) {
+                            const float prod = p[q] * wt;
+                            acc[d][q] = acc[d][q] + prod;
+                        }
+                    }
                 }
             }
+            cur[j] = ld(s2 + j);  // refill: row j of step k+2 (a valid re-read at the end)
         }
-        // row r complete -> LDS slot, shift the accumulators down
-        float* o = my_lds + ((r - oy0) % kRowsPerFlush) * kRowWords;
-        *reinterpret_cast<float4*>(o) = make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
-        *reinterpret_cast<float4*>(o + 4) = make_float4(acc[0][4], acc[0][5], acc[0][6], acc[0][7]);
+        if (hemit) {
+            // row `next` complete -> LDS slot, shift the accumulators down
+            float* o = my_lds + ((next - oy0) % kRowsPerFlush) * kRowWords;
+            *reinterpret_cast<float4*>(o) = make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
+            *reinterpret_cast<float4*>(o + 4) = make_float4(acc[0][4], acc[0][5], acc[0][6], acc[0][7]);
 #pragma unroll
-        for (int d = 0; d + 1 < A; ++d)
+            for (int d = 0; d + 1 < A; ++d)
 #pragma unroll
-            for (int j = 0; j < kBytesPerLane; ++j) acc[d][j] = acc[d + 1][j];
+                for (int q = 0; q < kBytesPerLane; ++q) acc[d][q] = acc[d + 1][q];
 #pragma unroll
-        for (int j = 0; j < kBytesPerLane; ++j) acc[A - 1][j] = 0.0f;
-        cs = ns;
-        ce = ne;
-        cpf = npf;
+            for (int q = 0; q < kBytesPerLane; ++q) acc[A - 1][q] = 0.0f;
+            const int nrows = (next - oy0) % kRowsPerFlush + 1;
+            if (nrows == kRowsPerFlush || next == oy1 - 1) {
+                __syncthreads();
+                horizontal_rows(a, lds, hw, s_off, s_n, next - nrows + 1, nrows, ox0, nox, dst);
+                __syncthreads();
+            }
+            ++next;
+        }
     };
 
-    int fbase = oy0;  // first row not yet flushed
-    for (int r = oy0; r < oy1; r += 2) {
-        body(r, buf0, buf1);
-        if (r + 1 < oy1) body(r + 1, buf1, buf0);
-        const int last = r + 1 < oy1 ? r + 1 : r;
-        if (last - fbase + 1 == kRowsPerFlush || last == oy1 - 1) {
-            __syncthreads();
-            horizontal_rows(a, lds, hw, s_off, s_n, fbase, last - fbase + 1, ox0, nox, dst);
-            __syncthreads();
-            fbase = last + 1;
-        }
+    for (int k = kb; k < ke; k += 2) {
+        body(k, buf0);
+        if (k + 1 < ke) body(k + 1, buf1);
     }
 }
 
@@ -294,10 +260,12 @@ hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_
     if (plan.slots > 0) {
         dim3 grid(plan.NS * plan.NB, n);
         const bool wl = plan.weights_in_lds;
+        const size_t lds = sizeof(float) * ((size_t)kRowsPerFlush * kRowWords +
+                                            (wl ? (size_t)a.max_strip_weights : 0) + 2 * (size_t)a.max_strip_cols);
 #define IK_LAUNCH(A_, R_)                                                                         \
     if (plan.slots == A_ && plan.rows == R_) {                                                    \
-        if (wl) hipLaunchKernelGGL((k_resize_fused<A_, R_, true>), grid, dim3(kThreads), 0, s, a); \
-        else hipLaunchKernelGGL((k_resize_fused<A_, R_, false>), grid, dim3(kThreads), 0, s, a);   \
+        if (wl) hipLaunchKernelGGL((k_resize_fused<A_, R_, true>), grid, dim3(kThreads), lds, s, a); \
+        else hipLaunchKernelGGL((k_resize_fused<A_, R_, false>), grid, dim3(kThreads), lds, s, a);   \
         return hipGetLastError();                                                                 \
     }
         // instances that fit the register file without spilling (ik_plan.cpp picks)

@@ -211,33 +211,50 @@ ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int
     std::vector<int> bands;
     for (int y = 0; y < nh; y += band_h) { bands.push_back(y); bands.push_back(y + band_h < nh ? y + band_h : nh); }
 
-    // steady-state block tables (see ResizeArgs)
-    std::vector<int> bsv(nh, 0), bnv(nh, 0);
-    std::vector<unsigned long long> bmv(nh, 0);
-    std::vector<float> bwv;
+    // step tables (see ResizeArgs): per band, output row r needs source rows
+    // [max(consumed, ly[r]), ly[r]+cy[r]); cut into steps of <= rows rows, the last
+    // step of r emits it.
+    std::vector<int> hdr, band_step;
+    std::vector<unsigned long long> smask;
+    std::vector<float> sw;
     if (slots) {
-        bwv.assign((size_t)nh * rows * slots, 0.0f);
-        for (int r = 1; r < nh; ++r) {
-            const int st = std::max(ly[r - 1] + cy[r - 1], ly[r]);
-            const int en = ly[r] + cy[r];
-            bsv[r] = st;
-            bnv[r] = en - st;
-            for (int j = 0; j < rows && st + j < en; ++j)
-                for (int d = 0; d < slots && r + d < nh; ++d) {
-                    const int kk = st + j - ly[r + d];
-                    if (kk >= 0 && kk < cy[r + d]) {
-                        bmv[r] |= 1ull << (j * slots + d);
-                        bwv[((size_t)r * rows + j) * slots + d] = wy[(size_t)(r + d) * Ty + kk];
-                    }
-                }
+        for (size_t bi = 0; bi < bands.size(); bi += 2) {
+            const int oy0 = bands[bi], oy1 = bands[bi + 1];
+            band_step.push_back((int)smask.size());
+            int consumed = ly[oy0];
+            for (int r = oy0; r < oy1; ++r) {
+                const int end = ly[r] + cy[r];
+                int st = std::max(consumed, ly[r]);
+                do {
+                    const int cnt = std::min(rows, std::max(0, end - st));
+                    unsigned long long m = 0;
+                    std::vector<float> w((size_t)rows * slots, 0.0f);
+                    for (int j = 0; j < cnt; ++j)
+                        for (int d = 0; d < slots && r + d < oy1; ++d) {
+                            const int kk = st + j - ly[r + d];
+                            if (kk >= 0 && kk < cy[r + d]) {
+                                m |= 1ull << (j * slots + d);
+                                w[(size_t)j * slots + d] = wy[(size_t)(r + d) * Ty + kk];
+                            }
+                        }
+                    st += cnt;
+                    const int emit = st >= end ? 1 : 0;
+                    hdr.push_back(st - cnt); hdr.push_back(cnt); hdr.push_back(emit); hdr.push_back(0);
+                    smask.push_back(m);
+                    sw.insert(sw.end(), w.begin(), w.end());
+                    if (emit) break;
+                } while (true);
+                consumed = std::max(consumed, end);
+            }
         }
+        band_step.push_back((int)smask.size());
     }
 
     std::vector<char> blob;
     const size_t o_ly = put(blob, ly), o_cy = put(blob, cy), o_wy = put(blob, wy);
     const size_t o_lx = put(blob, lx), o_cx = put(blob, cx), o_wx = put(blob, wx);
     const size_t o_st = put(blob, strips), o_bd = put(blob, bands);
-    const size_t o_bs = put(blob, bsv), o_bn = put(blob, bnv), o_bm = put(blob, bmv), o_bw = put(blob, bwv);
+    const size_t o_sh = put(blob, hdr), o_sm = put(blob, smask), o_sw = put(blob, sw), o_bst = put(blob, band_step);
 
     auto* p = new ResizePlan();
     p->W = W; p->H = H; p->C = C; p->nw = nw; p->nh = nh; p->filter = filter;
@@ -259,9 +276,15 @@ ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int
     a.ly = (const int*)(d + o_ly); a.ny = (const int*)(d + o_cy); a.wy = (const float*)(d + o_wy); a.Ty = Ty;
     a.lx = (const int*)(d + o_lx); a.nx = (const int*)(d + o_cx); a.wx = (const float*)(d + o_wx); a.Tx = Tx;
     a.strips = (const int*)(d + o_st); a.NS = p->NS;
+    a.max_strip_cols = 0;
+    for (int k = 0; k < p->NS; ++k) a.max_strip_cols = std::max(a.max_strip_cols, strips[3 * k + 1] - strips[3 * k]);
+    a.max_strip_cols = (a.max_strip_cols + 3) & ~3;
+    a.max_strip_weights = (a.max_strip_cols * Tx + 3) & ~3;
     a.bands = (const int*)(d + o_bd); a.NB = p->NB;
-    a.bs = (const int*)(d + o_bs); a.bn = (const int*)(d + o_bn);
-    a.bmask = (const unsigned long long*)(d + o_bm); a.bw = (const float*)(d + o_bw);
+    a.step_hdr = (const int*)(d + o_sh);
+    a.step_mask = (const unsigned long long*)(d + o_sm);
+    a.step_w = (const float*)(d + o_sw);
+    a.band_step = (const int*)(d + o_bst);
     g_plans[key] = p;
     return p;
 }
