@@ -83,7 +83,7 @@ def cpu_baseline(args, img: np.ndarray):
     one()
     t1 = time.perf_counter() - t0
     rounds = max(1, int(args.cpu_seconds / max(t1, 1e-3)))
-    rounds = min(rounds, 8)
+    rounds = min(rounds, 96)
     done[0] = 0
     t0 = time.perf_counter()
     for _ in range(rounds):

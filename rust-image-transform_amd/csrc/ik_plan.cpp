@@ -192,7 +192,7 @@ ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int
     const int NS = slots ? (int)strips.size() / 3 : 0;
     int band_h = nh;
     if (slots) {
-        long target = 2048;
+        long target = 8192;  // measured best on MI355X for 4096^2->512^2 batches (tools/sweep_resize.py)
         if (const char* e = getenv("IK_TARGET_WG")) target = atol(e);
         long per_img = (target + n - 1) / n;
         long nb = (per_img + NS - 1) / NS;
