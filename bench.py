@@ -57,6 +57,26 @@ def parse():
     return ap.parse_args()
 
 
+def shard_seeds(rank: int, batch: int, distinct: int = 4):
+    """Synthetic frames of rank `rank`: disjoint seed ranges, so ranks never share work."""
+    return [1000 * rank + i for i in range(min(batch, distinct))]
+
+
+def reduce_max(value: float, dist, device) -> float:
+    """Max over ranks (the slowest rank defines the job's wall time)."""
+    if dist is None:
+        return value
+    import torch
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def aggregate_mpix(world: int, batch: int, steps: int, size: int, elapsed: float) -> float:
+    """Whole-job throughput: input pixels of all ranks / max-over-ranks wall time."""
+    return world * batch * steps * size * size / elapsed / 1e6
+
+
 def synth_rgba(w, h, seed):
     import ikutil
     return ikutil.synth(w, h, 4, seed=seed, pattern="S")
@@ -126,7 +146,7 @@ def main():
     f = FILTERS[args.filter]
     pitch = S * 4
     # inputs resident in HBM before the timed region: 4 distinct synthetic frames tiled over the batch
-    distinct = [synth_rgba(S, S, seed=1000 * rank + i) for i in range(min(B, 4))]
+    distinct = [synth_rgba(S, S, seed=sd) for sd in shard_seeds(rank, B)]
     src = torch.empty((B, S, pitch), dtype=torch.uint8, device=f"cuda:{local}")
     for i in range(B):
         src[i].copy_(torch.from_numpy(distinct[i % len(distinct)].reshape(S, pitch)))
@@ -165,10 +185,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     barrier()
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = reduce_max(elapsed, dist, f"cuda:{local}")
 
     if not args.device_only:
         assert bytes(out[:4]) == b"RIFF" and all(s > 0 for s in sizes)
@@ -176,8 +193,7 @@ def main():
     colour_ms = float(np.mean([k[1] for k in kms]))
     bytes_per_img = 4 * S * S + 4 * O * O
     achieved = B * bytes_per_img / (resize_ms * 1e-3) / 1e9
-    total_px = world * B * args.steps * S * S
-    value = total_px / elapsed / 1e6
+    value = aggregate_mpix(world, B, args.steps, S, elapsed)
 
     # the other filter's kernel on the same batch (device-only), for DESIGN.md
     alt = {}
