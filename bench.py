@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--filter", default="triangle", choices=sorted(FILTERS))
     ap.add_argument("--quality", type=int, default=80)
     ap.add_argument("--threads", type=int, default=16, help="host entropy-coder threads per rank")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline sample budget")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample wall-time budget (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--device-only", action="store_true", help="time resize+colour kernels only")
     return ap.parse_args()
@@ -98,12 +98,14 @@ def cpu_baseline(args, img: np.ndarray):
         with lock:
             done[0] += 1
 
-    # single-thread time of one image sizes the sample (10-30 s of CPU work in all)
+    # single-thread time of one warm image sizes the sample: `rounds` rounds of one
+    # image per thread ~ args.cpu_seconds of wall time (10-30 s of CPU work in all)
+    one()
     t0 = time.perf_counter()
     one()
     t1 = time.perf_counter() - t0
     rounds = max(1, int(args.cpu_seconds / max(t1, 1e-3)))
-    rounds = min(rounds, 96)
+    rounds = min(rounds, 400)
     done[0] = 0
     t0 = time.perf_counter()
     for _ in range(rounds):

@@ -440,6 +440,8 @@ int ik_resize_batch_device(const uint8_t* dev_src, uint32_t W, uint32_t H, uint3
     if (filter < 0 || filter > 4) return fail(IK_ERR_INVALID, "unknown filter %d", filter);
     if (src_pitch < (size_t)W * C || dst_pitch < (size_t)nw * C) return fail(IK_ERR_INVALID, "pitch too small");
     if ((src_pitch & 7) || ((uintptr_t)dev_src & 7)) return fail(IK_ERR_INVALID, "source rows must be 8-byte aligned");
+    if (C == 4 && (((uintptr_t)dev_dst & 3) || (dst_pitch & 3) || (dst_image_stride & 3)))
+        return fail(IK_ERR_INVALID, "RGBA destination rows must be 4-byte aligned");
     if (n > 1 && (src_image_stride < src_pitch * H || dst_image_stride < dst_pitch * nh))
         return fail(IK_ERR_INVALID, "image stride too small");
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : thread_stream();

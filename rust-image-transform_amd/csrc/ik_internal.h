@@ -14,7 +14,7 @@ constexpr int kThreads = 256;            // workgroup size (4 wave64s)
 constexpr int kBytesPerLane = 8;         // vertical pass: bytes of a source row per lane
 constexpr int kStripBytes = kBytesPerLane * kThreads;  // 2048 source bytes per strip
 constexpr int kRowWords = kStripBytes + kStripBytes / 8;  // LDS f32 row, +4 words per 32
-constexpr int kRowsPerFlush = 3;         // vertical rows staged in LDS per horizontal pass
+constexpr int kMaxFlushRows = 4;         // vertical rows staged in LDS per horizontal pass (plan: 2..4)
 constexpr int kMaxStripCols = 512;       // output columns per strip (LDS offset/count tables)
 constexpr int kMaxStripWeights = 3072;   // horizontal weights per strip kept in LDS (12 KB)
 
@@ -56,6 +56,7 @@ struct ResizePlan {
     int slots = 0;        // accumulator slots the fused kernel needs (0 = naive path)
     int rows = 0;         // prefetch depth: max source rows consumed per output row
     bool weights_in_lds = false;
+    int flush = 3;        // completed vertical rows staged in LDS per horizontal pass
     int NS = 0, NB = 0;
     size_t table_bytes = 0;
     void* dev_tables = nullptr;
@@ -66,6 +67,9 @@ struct ResizePlan {
 hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_pitch,
                          size_t src_img_stride, uint8_t* dst, size_t dst_pitch,
                          size_t dst_img_stride, int n, float* naive_tmp, hipStream_t s);
+// dynamic LDS bytes and resident workgroups per CU of the fused kernel
+size_t resize_lds_bytes(const ResizeArgs& a, bool wl, int flush);
+int resize_blocks_per_cu(int slots, int rows, int flush, bool wl, size_t lds);
 hipError_t launch_webp_yuv420(const uint8_t* src, int w, int h, int C, size_t pitch,
                               size_t img_stride, uint8_t* yuv /* Y, U, V planes per image */,
                               size_t yuv_img_stride, int n, const uint16_t* gamma_to_lin,

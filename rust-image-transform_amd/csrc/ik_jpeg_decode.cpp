@@ -28,13 +28,13 @@ const uint8_t kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18,
 struct HuffTable {
     bool present = false;
     // canonical decode: maxcode[l], valptr[l], mincode[l]; plus a 9-bit lookahead
-    int maxcode[18], valptr[17], mincode[17];
-    uint8_t vals[256];
-    uint8_t look_len[512], look_val[512];
+    int maxcode[18] = {}, valptr[17] = {}, mincode[17] = {};
+    uint8_t vals[256] = {};
+    uint8_t look_len[512] = {}, look_val[512] = {};
 };
 
 bool build_huff(const uint8_t* bits, const uint8_t* vals, int nvals, HuffTable& t) {
-    std::memset(&t, 0, sizeof(t));
+    t = HuffTable();
     std::memcpy(t.vals, vals, nvals);
     int code = 0, k = 0;
     for (int l = 1; l <= 16; ++l) {

@@ -36,38 +36,70 @@ __device__ __forceinline__ uint8_t float_nearest_u8(float t) {
     return (uint8_t)roundf(t);
 }
 
-// Horizontal pass over `nrows` (<= kRowsPerFlush) completed vertical rows staged
-// in LDS.  Lane = (output column, channel) of the strip; each lane computes the
-// rows together so every weight read feeds nrows taps.
+// Horizontal pass over `nrows` (<= F) completed vertical rows staged
+// in LDS.  Lane = (row, output column) of the strip, all C channels per lane:
+// one LDS read of C consecutive f32 per tap (ds_read_b128 for RGBA; the 4-per-32
+// word padding makes the 36-word column stride bank-conflict free), C separate
+// sequential sums, one C-byte store.
 // out(r, ox, c) = round(sum_k tmp[r][(lx[ox]+k)*C + c] * wx[ox][k]), sequential k.
+template <int C>
+__device__ __forceinline__ void horizontal_rows_c(const ResizeArgs& a, const float* __restrict__ lds,
+                                                  const float* __restrict__ sw, const int* __restrict__ soff,
+                                                  const int* __restrict__ sn, int r0, int nrows, int ox0,
+                                                  int nox, uint8_t* __restrict__ dst) {
+    const int total = nox * nrows;
+    for (int v = threadIdx.x; v < total; v += kThreads) {
+        const int q = v / nox;
+        const int oxl = v - q * nox;
+        const int n = sn[oxl];
+        const float* __restrict__ w = sw + oxl * a.Tx;
+        const float* __restrict__ row = lds + q * kRowWords;
+        int idx = soff[oxl];
+        float acc[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = 0.0f;
+        for (int k = 0; k < n; ++k, idx += C) {
+            const float wk = w[k];
+            const int li = lds_idx(idx);
+            float t[C];
+            if constexpr (C == 4) {
+                const float4 t4 = *reinterpret_cast<const float4*>(row + li);
+                t[0] = t4.x; t[1] = t4.y; t[2] = t4.z; t[3] = t4.w;
+            } else if constexpr (C == 2) {
+                const float2 t2 = *reinterpret_cast<const float2*>(row + li);
+                t[0] = t2.x; t[1] = t2.y;
+            } else {
+                // C = 3 / 1: channels may straddle a 32-word pad boundary
+#pragma unroll
+                for (int c = 0; c < C; ++c) t[c] = row[lds_idx(idx + c)];
+            }
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const float prod = t[c] * wk;
+                acc[c] = acc[c] + prod;
+            }
+        }
+        uint8_t* o = dst + (size_t)(r0 + q) * a.dst_pitch + (size_t)(ox0 + oxl) * C;
+        if constexpr (C == 4) {
+            const unsigned u = (unsigned)float_nearest_u8(acc[0]) | ((unsigned)float_nearest_u8(acc[1]) << 8) |
+                               ((unsigned)float_nearest_u8(acc[2]) << 16) | ((unsigned)float_nearest_u8(acc[3]) << 24);
+            *reinterpret_cast<unsigned*>(o) = u;  // dst rows are 256-B pitched, columns 4-B aligned
+        } else {
+#pragma unroll
+            for (int c = 0; c < C; ++c) o[c] = float_nearest_u8(acc[c]);
+        }
+    }
+}
+
 __device__ __forceinline__ void horizontal_rows(const ResizeArgs& a, const float* __restrict__ lds,
                                                 const float* __restrict__ sw, const int* __restrict__ soff,
                                                 const int* __restrict__ sn, int r0, int nrows, int ox0,
                                                 int nox, uint8_t* __restrict__ dst) {
-    const int C = a.C;
-    const int total = nox * C;
-    for (int v = threadIdx.x; v < total; v += kThreads) {
-        const int oxl = v / C;
-        const int c = v - oxl * C;
-        const int n = sn[oxl];
-        const float* __restrict__ w = sw + oxl * a.Tx;
-        int idx = soff[oxl] + c;
-        float acc[kRowsPerFlush];
-#pragma unroll
-        for (int q = 0; q < kRowsPerFlush; ++q) acc[q] = 0.0f;
-        for (int k = 0; k < n; ++k, idx += C) {
-            const float wk = w[k];
-            const int li = lds_idx(idx);
-#pragma unroll
-            for (int q = 0; q < kRowsPerFlush; ++q) {
-                const float prod = lds[q * kRowWords + li] * wk;
-                acc[q] = acc[q] + prod;
-            }
-        }
-        uint8_t* o = dst + (size_t)r0 * a.dst_pitch + (size_t)(ox0 + oxl) * C + c;
-#pragma unroll
-        for (int q = 0; q < kRowsPerFlush; ++q)
-            if (q < nrows) o[(size_t)q * a.dst_pitch] = float_nearest_u8(acc[q]);
+    switch (a.C) {
+    case 4: horizontal_rows_c<4>(a, lds, sw, soff, sn, r0, nrows, ox0, nox, dst); break;
+    case 3: horizontal_rows_c<3>(a, lds, sw, soff, sn, r0, nrows, ox0, nox, dst); break;
+    case 2: horizontal_rows_c<2>(a, lds, sw, soff, sn, r0, nrows, ox0, nox, dst); break;
+    default: horizontal_rows_c<1>(a, lds, sw, soff, sn, r0, nrows, ox0, nox, dst); break;
     }
 }
 
@@ -85,15 +117,24 @@ struct FusedOcc { static constexpr int value = A <= 4 ? 4 : (A <= 8 ? 3 : 1); };
 // shift down.  Prefetch is a rolling two-step register ring: step k sits in
 // buf[k&1]; as soon as row j of step k is converted its registers are refilled
 // (unconditionally, so the compiler's vmcnt bookkeeping stays exact) with row j
-// of step k+2, keeping ~2R loads per lane in flight.  Every kRowsPerFlush
+// of step k+2, keeping ~2R loads per lane in flight.  Every F
 // completed rows the workgroup runs the horizontal pass from LDS.  LDS is
-// dynamic: [kRowsPerFlush rows of f32 tmp][strip weights if WL][offsets][taps].
-template <int A, int R, bool WL>
+// dynamic: [F rows of f32 tmp][strip weights if WL][offsets][taps].
+template <int A, int R, int F, bool WL>
 __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(ResizeArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
 
-    const int tile = blockIdx.x;
-    const int img = blockIdx.y;
+    // XCD-aware order: hardware deals workgroup h to XCD h % 8, so logical tile L
+    // = (h % 8)-th eighth of the grid + h / 8 gives each XCD a contiguous run of
+    // (strip, band, image) tiles; neighbouring strips (which share the 128-B lines
+    // at their edges) and neighbouring bands then meet in the same L2.
+    const int G = (int)gridDim.x;
+    const int h = (int)blockIdx.x;
+    const int per = G >> 3, rem = G & 7, x = h & 7;
+    const int L = x * per + (x < rem ? x : rem) + (h >> 3);
+    const int tiles = a.NS * a.NB;
+    const int img = L / tiles;
+    const int tile = L - img * tiles;
     const int strip = tile % a.NS;
     const int band = tile / a.NS;
     const cptr<int> strips = as_const(a.strips);
@@ -109,7 +150,7 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
     const uint8_t* __restrict__ src = a.src + (size_t)img * a.src_img_stride;
     uint8_t* __restrict__ dst = a.dst + (size_t)img * a.dst_img_stride;
 
-    float* __restrict__ s_w = lds + kRowsPerFlush * kRowWords;
+    float* __restrict__ s_w = lds + F * kRowWords;
     int* __restrict__ s_off = reinterpret_cast<int*>(s_w + (WL ? a.max_strip_weights : 0));
     int* __restrict__ s_n = s_off + a.max_strip_cols;
     for (int t = threadIdx.x; t < nox; t += kThreads) {
@@ -163,6 +204,14 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
         const unsigned long long m = smask[k];
         const cptr<float> w = sw + (size_t)k * (R * A);
         const int s2 = k + 2 < ke ? shdr[4 * (k + 2)] : hstart;
+        // all of the step's weights in SGPRs up front (a few wide scalar loads and
+        // one wait, instead of one dependent load per active tap)
+        constexpr int kWregs = R * A <= 64 ? R * A : 1;
+        float wv[kWregs];
+        if constexpr (R * A <= 64) {
+#pragma unroll
+            for (int i = 0; i < kWregs; ++i) wv[i] = w[i];
+        }
 #pragma unroll
         for (int j = 0; j < R; ++j) {
             if ((m >> (j * A)) & ((1ull << A) - 1ull)) {
@@ -176,7 +225,9 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
 #pragma unroll
                 for (int d = 0; d < A; ++d) {
                     if ((m >> (j * A + d)) & 1ull) {
-                        const float wt = w[j * A + d];
+                        float wt;
+                        if constexpr (R * A <= 64) wt = wv[j * A + d];
+                        else wt = w[j * A + d];
 #pragma unroll
                         for (int q = 0; q < kBytesPerLane; ++q) {
                             const float prod = p[q] * wt;
@@ -189,7 +240,7 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
         }
         if (hemit) {
             // row `next` complete -> LDS slot, shift the accumulators down
-            float* o = my_lds + ((next - oy0) % kRowsPerFlush) * kRowWords;
+            float* o = my_lds + ((next - oy0) % F) * kRowWords;
             *reinterpret_cast<float4*>(o) = make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
             *reinterpret_cast<float4*>(o + 4) = make_float4(acc[0][4], acc[0][5], acc[0][6], acc[0][7]);
 #pragma unroll
@@ -198,8 +249,8 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
                 for (int q = 0; q < kBytesPerLane; ++q) acc[d][q] = acc[d + 1][q];
 #pragma unroll
             for (int q = 0; q < kBytesPerLane; ++q) acc[A - 1][q] = 0.0f;
-            const int nrows = (next - oy0) % kRowsPerFlush + 1;
-            if (nrows == kRowsPerFlush || next == oy1 - 1) {
+            const int nrows = (next - oy0) % F + 1;
+            if (nrows == F || next == oy1 - 1) {
                 __syncthreads();
                 horizontal_rows(a, lds, hw, s_off, s_n, next - nrows + 1, nrows, ox0, nox, dst);
                 __syncthreads();
@@ -208,9 +259,11 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
         }
     };
 
+    // bands hold an even number of steps (ik_plan.cpp pads with a no-op step), so
+    // both halves run unconditionally and the vmcnt accounting stays at 2R
     for (int k = kb; k < ke; k += 2) {
         body(k, buf0);
-        if (k + 1 < ke) body(k + 1, buf1);
+        body(k + 1, buf1);
     }
 }
 
@@ -250,6 +303,35 @@ __global__ __launch_bounds__(kThreads) void k_horz_naive(ResizeArgs a) {
     a.dst[(size_t)img * a.dst_img_stride + (size_t)r * a.dst_pitch + v] = float_nearest_u8(acc);
 }
 
+size_t resize_lds_bytes(const ResizeArgs& a, bool wl, int flush) {
+    return sizeof(float) * ((size_t)flush * kRowWords + (wl ? (size_t)a.max_strip_weights : 0) +
+                            2 * (size_t)a.max_strip_cols);
+}
+
+// Instances that fit the register file without spilling (ik_plan.cpp picks A, R);
+// X(A, R, F) for every flush depth F the plan may choose.
+#define IK_FUSED_INSTANCES(X)                                               \
+    X(4, 4, 2) X(4, 4, 3) X(4, 4, 4) X(4, 8, 2) X(4, 8, 3) X(4, 8, 4)       \
+    X(8, 4, 2) X(8, 4, 3) X(8, 4, 4) X(8, 8, 2) X(8, 8, 3) X(8, 8, 4)       \
+    X(16, 4, 2) X(16, 4, 3) X(16, 4, 4)
+
+static const void* fused_fn(int A, int R, int F, bool wl) {
+#define IK_PICK(A_, R_, F_)                                                              \
+    if (A == A_ && R == R_ && F == F_)                                                   \
+        return wl ? reinterpret_cast<const void*>(&k_resize_fused<A_, R_, F_, true>)     \
+                  : reinterpret_cast<const void*>(&k_resize_fused<A_, R_, F_, false>);
+    IK_FUSED_INSTANCES(IK_PICK)
+#undef IK_PICK
+    return nullptr;
+}
+
+int resize_blocks_per_cu(int slots, int rows, int flush, bool wl, size_t lds) {
+    const void* fn = fused_fn(slots, rows, flush, wl);
+    int blocks = 0;
+    if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, kThreads, lds) != hipSuccess) return 0;
+    return blocks;
+}
+
 hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_pitch,
                          size_t src_img_stride, uint8_t* dst, size_t dst_pitch,
                          size_t dst_img_stride, int n, float* naive_tmp, hipStream_t s) {
@@ -258,20 +340,16 @@ hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_
     a.dst = dst; a.dst_pitch = dst_pitch; a.dst_img_stride = dst_img_stride;
     a.tmp = naive_tmp;
     if (plan.slots > 0) {
-        dim3 grid(plan.NS * plan.NB, n);
+        dim3 grid(plan.NS * plan.NB * n);  // 1-D: the kernel maps it XCD-aware
         const bool wl = plan.weights_in_lds;
-        const size_t lds = sizeof(float) * ((size_t)kRowsPerFlush * kRowWords +
-                                            (wl ? (size_t)a.max_strip_weights : 0) + 2 * (size_t)a.max_strip_cols);
-#define IK_LAUNCH(A_, R_)                                                                         \
-    if (plan.slots == A_ && plan.rows == R_) {                                                    \
-        if (wl) hipLaunchKernelGGL((k_resize_fused<A_, R_, true>), grid, dim3(kThreads), lds, s, a); \
-        else hipLaunchKernelGGL((k_resize_fused<A_, R_, false>), grid, dim3(kThreads), lds, s, a);   \
-        return hipGetLastError();                                                                 \
+        const size_t lds = resize_lds_bytes(a, wl, plan.flush);
+#define IK_LAUNCH(A_, R_, F_)                                                                          \
+    if (plan.slots == A_ && plan.rows == R_ && plan.flush == F_) {                                     \
+        if (wl) hipLaunchKernelGGL((k_resize_fused<A_, R_, F_, true>), grid, dim3(kThreads), lds, s, a); \
+        else hipLaunchKernelGGL((k_resize_fused<A_, R_, F_, false>), grid, dim3(kThreads), lds, s, a);   \
+        return hipGetLastError();                                                                      \
     }
-        // instances that fit the register file without spilling (ik_plan.cpp picks)
-        IK_LAUNCH(4, 4) IK_LAUNCH(4, 8)
-        IK_LAUNCH(8, 4) IK_LAUNCH(8, 8)
-        IK_LAUNCH(16, 4)
+        IK_FUSED_INSTANCES(IK_LAUNCH)
 #undef IK_LAUNCH
         return hipErrorInvalidValue;
     }

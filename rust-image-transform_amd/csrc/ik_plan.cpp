@@ -119,7 +119,7 @@ int required_slots(const std::vector<int>& left, const std::vector<int>& cnt) {
 namespace {
 
 std::mutex g_plan_mu;
-std::map<std::tuple<int, int, int, int, int, int, int, int>, ResizePlan*> g_plans;
+std::map<std::tuple<int, int, int, int, int, int, int, int, int>, ResizePlan*> g_plans;
 
 template <typename T>
 size_t put(std::vector<char>& blob, const std::vector<T>& v) {
@@ -160,7 +160,7 @@ ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int
         strips.clear();
         bool ok = true;
         for (int ox0 = 0; ox0 < nw;) {
-            const int sb = (lx[ox0] * C) & ~15;
+            const int sb = (lx[ox0] * C) & ~127;  // strip rows start on a 128-B line
             int ox1 = ox0;
             while (ox1 < nw && (lx[ox1] + cx[ox1]) * C - sb <= kStripBytes && ox1 - ox0 < kMaxStripCols &&
                    (!wl || (long)(ox1 - ox0 + 1) * Tx <= kMaxStripWeights))
@@ -178,7 +178,7 @@ ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int
             strips.clear();
             int ns_gl = 0;
             for (int ox0 = 0; ox0 < nw;) {
-                const int sb = (lx[ox0] * C) & ~15;
+                const int sb = (lx[ox0] * C) & ~127;  // strip rows start on a 128-B line
                 int ox1 = ox0;
                 while (ox1 < nw && (lx[ox1] + cx[ox1]) * C - sb <= kStripBytes && ox1 - ox0 < kMaxStripCols) ++ox1;
                 ++ns_gl;
@@ -203,7 +203,24 @@ ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int
         if (band_h > nh) band_h = nh;
     }
     if (const char* e = getenv("IK_BAND_ROWS")) band_h = std::max(1, std::min(nh, atoi(e)));
-    const auto key = std::make_tuple(device, W, H, C, nw, nh, filter, band_h);
+    // flush depth F (vertical rows staged in LDS per horizontal pass): LDS per
+    // workgroup grows with F, so take the deepest F that keeps the most
+    // workgroups resident per CU (more waves = more source loads in flight).
+    int flush = 3;
+    if (slots) {
+        int msc = 0;
+        for (int k = 0; k < NS; ++k) msc = std::max(msc, strips[3 * k + 1] - strips[3 * k]);
+        ResizeArgs probe{};
+        probe.max_strip_cols = (msc + 3) & ~3;
+        probe.max_strip_weights = (probe.max_strip_cols * Tx + 3) & ~3;
+        int best = -1;
+        for (int f = kMaxFlushRows; f >= 2; --f) {
+            const int b = resize_blocks_per_cu(slots, rows, f, wl, resize_lds_bytes(probe, wl, f));
+            if (b > best) { best = b; flush = f; }
+        }
+        if (const char* e = getenv("IK_FLUSH_ROWS")) flush = std::max(2, std::min(kMaxFlushRows, atoi(e)));
+    }
+    const auto key = std::make_tuple(device, W, H, C, nw, nh, filter, band_h, flush);
     std::lock_guard<std::mutex> lk(g_plan_mu);
     auto it = g_plans.find(key);
     if (it != g_plans.end()) return it->second;
@@ -246,6 +263,14 @@ ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int
                 } while (true);
                 consumed = std::max(consumed, end);
             }
+            // the kernel runs steps in pairs: pad an odd band with a no-op step
+            // (no rows, no taps, no emit; its prefetch re-reads a valid row)
+            if ((smask.size() - band_step.back()) & 1) {
+                const int last = hdr[hdr.size() - 4];
+                hdr.push_back(last); hdr.push_back(0); hdr.push_back(0); hdr.push_back(0);
+                smask.push_back(0);
+                sw.insert(sw.end(), (size_t)rows * slots, 0.0f);
+            }
         }
         band_step.push_back((int)smask.size());
     }
@@ -261,6 +286,7 @@ ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int
     p->slots = slots;
     p->rows = rows;
     p->weights_in_lds = wl;
+    p->flush = flush;
     p->NS = NS;
     p->NB = (int)bands.size() / 2;
     p->table_bytes = blob.size();

@@ -186,11 +186,14 @@ def test_webp_decode_and_format(ik):
     Image.fromarray(ikutil.synth(33, 21, 3, seed=4)).save(buf, format="WEBP", quality=80)
     img, fmt = decode_image(buf.getvalue())
     assert fmt is ImageFormat.webp and img.dimensions() == (33, 21) and img.channels == 3
+    # lossless with real alpha -> Rgba8 (an all-opaque lossless file has alpha_is_used = 0 -> Rgb8)
+    px = ikutil.synth(33, 21, 4, seed=4)
+    px[..., 3] = np.arange(33 * 21, dtype=np.uint32).reshape(21, 33) % 256
     buf = io.BytesIO()
-    Image.fromarray(ikutil.synth(33, 21, 4, seed=4)).save(buf, format="WEBP", lossless=True)
+    Image.fromarray(px).save(buf, format="WEBP", lossless=True, exact=True)
     img, fmt = decode_image(buf.getvalue())
     assert img.channels == 4
-    np.testing.assert_array_equal(img.to_array(), ikutil.synth(33, 21, 4, seed=4))
+    np.testing.assert_array_equal(img.to_array(), px)
 
 
 def test_config1_jpeg_to_webp(ik, oracle):

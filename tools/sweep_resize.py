@@ -18,8 +18,13 @@ for i in range(B):
 torch.cuda.synchronize()
 res = {}
 for f in [int(x) for x in os.environ.get("FILTERS", "1,4").split(",")]:
-    for tgt in os.environ.get("TARGETS", "2048").split(","):
+    for tgt, fl, br in [(t, fl, br) for t in os.environ.get("TARGETS", "8192").split(",")
+                        for fl in os.environ.get("FLUSH", "").split(",")
+                        for br in os.environ.get("BANDS", "").split(",")]:
         os.environ["IK_TARGET_WG"] = tgt
+        for k, v in (("IK_FLUSH_ROWS", fl), ("IK_BAND_ROWS", br)):
+            if v: os.environ[k] = v
+            else: os.environ.pop(k, None)
         p = ctypes.c_void_p()
         assert lib.ik_pipeline_create(S, S, 4, O, O, f, 1, 80, B, 1, ctypes.byref(p)) == 0, _lib.last_error()
         ms = []
@@ -30,4 +35,4 @@ for f in [int(x) for x in os.environ.get("FILTERS", "1,4").split(",")]:
         lib.ik_pipeline_destroy(p)
         m = float(np.median(ms))
         gbs = B * (4 * S * S + 4 * O * O) / (m * 1e-3) / 1e9
-        print(f"filter={f} target_wg={tgt} resize_ms={m:.4f} ({m/B*1e3:.1f} us/img) GB/s={gbs:.0f} frac={gbs/8000:.3f}", flush=True)
+        print(f"filter={f} target_wg={tgt} flush={fl or 'auto'} band={br or 'auto'} resize_ms={m:.4f} ({m/B*1e3:.1f} us/img) GB/s={gbs:.0f} frac={gbs/8000:.3f}", flush=True)
