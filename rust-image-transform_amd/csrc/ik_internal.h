@@ -67,9 +67,8 @@ struct ResizePlan {
 hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_pitch,
                          size_t src_img_stride, uint8_t* dst, size_t dst_pitch,
                          size_t dst_img_stride, int n, float* naive_tmp, hipStream_t s);
-// dynamic LDS bytes and resident workgroups per CU of the fused kernel
+// dynamic LDS bytes of the fused kernel
 size_t resize_lds_bytes(const ResizeArgs& a, bool wl, int flush);
-int resize_blocks_per_cu(int slots, int rows, int flush, bool wl, size_t lds);
 hipError_t launch_webp_yuv420(const uint8_t* src, int w, int h, int C, size_t pitch,
                               size_t img_stride, uint8_t* yuv /* Y, U, V planes per image */,
                               size_t yuv_img_stride, int n, const uint16_t* gamma_to_lin,

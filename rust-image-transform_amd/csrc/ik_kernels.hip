@@ -40,44 +40,61 @@ __device__ __forceinline__ uint8_t float_nearest_u8(float t) {
 // in LDS.  Lane = (row, output column) of the strip, all C channels per lane:
 // one LDS read of C consecutive f32 per tap (ds_read_b128 for RGBA; the 4-per-32
 // word padding makes the 36-word column stride bank-conflict free), C separate
-// sequential sums, one C-byte store.
+// sequential sums, one C-byte store.  Taps run over the plan's Tx (a multiple of
+// 4; zero weights past the column's own count), kHTaps at a time so their LDS
+// reads are in flight together.  A zero-weight tap past the strip reads finite
+// data (the next LDS row or the tables after the rows; the rows are zeroed at the
+// start) and adds +-0, which leaves the sum bit-identical.
 // out(r, ox, c) = round(sum_k tmp[r][(lx[ox]+k)*C + c] * wx[ox][k]), sequential k.
-template <int C>
+template <int C, int kHTaps = 2>
 __device__ __forceinline__ void horizontal_rows_c(const ResizeArgs& a, const float* __restrict__ lds,
                                                   const float* __restrict__ sw, const int* __restrict__ soff,
-                                                  const int* __restrict__ sn, int r0, int nrows, int ox0,
-                                                  int nox, uint8_t* __restrict__ dst) {
+                                                  int r0, int nrows, int ox0, int nox, int hq, int hox,
+                                                  uint8_t* __restrict__ dst) {
     const int total = nox * nrows;
+    const int Tx = a.Tx;
     for (int v = threadIdx.x; v < total; v += kThreads) {
-        const int q = v / nox;
-        const int oxl = v - q * nox;
-        const int n = sn[oxl];
-        const float* __restrict__ w = sw + oxl * a.Tx;
+        int q = hq, oxl = hox;  // (v / nox, v % nox) for v = threadIdx.x, precomputed
+        if (v != (int)threadIdx.x) { q = v / nox; oxl = v - q * nox; }
+        const float* __restrict__ w = sw + oxl * Tx;
         const float* __restrict__ row = lds + q * kRowWords;
-        int idx = soff[oxl];
+        const int base = soff[oxl];
         float acc[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) acc[c] = 0.0f;
-        for (int k = 0; k < n; ++k, idx += C) {
-            const float wk = w[k];
-            const int li = lds_idx(idx);
-            float t[C];
-            if constexpr (C == 4) {
-                const float4 t4 = *reinterpret_cast<const float4*>(row + li);
-                t[0] = t4.x; t[1] = t4.y; t[2] = t4.z; t[3] = t4.w;
-            } else if constexpr (C == 2) {
-                const float2 t2 = *reinterpret_cast<const float2*>(row + li);
-                t[0] = t2.x; t[1] = t2.y;
+#pragma unroll 1
+        for (int k = 0; k < Tx; k += kHTaps) {
+            float wk[kHTaps];
+            if constexpr (kHTaps == 4) {
+                const float4 w4 = *reinterpret_cast<const float4*>(w + k);
+                wk[0] = w4.x; wk[1] = w4.y; wk[2] = w4.z; wk[3] = w4.w;
             } else {
-                // C = 3 / 1: channels may straddle a 32-word pad boundary
+                const float2 w2 = *reinterpret_cast<const float2*>(w + k);
+                wk[0] = w2.x; wk[1] = w2.y;
+            }
+            float t[kHTaps][C];
 #pragma unroll
-                for (int c = 0; c < C; ++c) t[c] = row[lds_idx(idx + c)];
+            for (int u = 0; u < kHTaps; ++u) {
+                const int idx = base + (k + u) * C;
+                if constexpr (C == 4) {
+                    const float4 t4 = *reinterpret_cast<const float4*>(row + lds_idx(idx));
+                    t[u][0] = t4.x; t[u][1] = t4.y; t[u][2] = t4.z; t[u][3] = t4.w;
+                } else if constexpr (C == 2) {
+                    const float2 t2 = *reinterpret_cast<const float2*>(row + lds_idx(idx));
+                    t[u][0] = t2.x; t[u][1] = t2.y;
+                } else {
+                    // C = 3 / 1: channels may straddle a 32-word pad boundary
+#pragma unroll
+                    for (int c = 0; c < C; ++c) t[u][c] = row[lds_idx(idx + c)];
+                }
             }
 #pragma unroll
-            for (int c = 0; c < C; ++c) {
-                const float prod = t[c] * wk;
-                acc[c] = acc[c] + prod;
-            }
+            for (int u = 0; u < kHTaps; ++u)
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    const float prod = t[u][c] * wk[u];
+                    acc[c] = acc[c] + prod;
+                }
         }
         uint8_t* o = dst + (size_t)(r0 + q) * a.dst_pitch + (size_t)(ox0 + oxl) * C;
         if constexpr (C == 4) {
@@ -93,13 +110,13 @@ __device__ __forceinline__ void horizontal_rows_c(const ResizeArgs& a, const flo
 
 __device__ __forceinline__ void horizontal_rows(const ResizeArgs& a, const float* __restrict__ lds,
                                                 const float* __restrict__ sw, const int* __restrict__ soff,
-                                                const int* __restrict__ sn, int r0, int nrows, int ox0,
-                                                int nox, uint8_t* __restrict__ dst) {
+                                                int r0, int nrows, int ox0, int nox, int hq, int hox,
+                                                uint8_t* __restrict__ dst) {
     switch (a.C) {
-    case 4: horizontal_rows_c<4>(a, lds, sw, soff, sn, r0, nrows, ox0, nox, dst); break;
-    case 3: horizontal_rows_c<3>(a, lds, sw, soff, sn, r0, nrows, ox0, nox, dst); break;
-    case 2: horizontal_rows_c<2>(a, lds, sw, soff, sn, r0, nrows, ox0, nox, dst); break;
-    default: horizontal_rows_c<1>(a, lds, sw, soff, sn, r0, nrows, ox0, nox, dst); break;
+    case 4: horizontal_rows_c<4>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
+    case 3: horizontal_rows_c<3>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
+    case 2: horizontal_rows_c<2>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
+    default: horizontal_rows_c<1>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
     }
 }
 
@@ -119,7 +136,7 @@ struct FusedOcc { static constexpr int value = A <= 4 ? 4 : (A <= 8 ? 3 : 1); };
 // (unconditionally, so the compiler's vmcnt bookkeeping stays exact) with row j
 // of step k+2, keeping ~2R loads per lane in flight.  Every F
 // completed rows the workgroup runs the horizontal pass from LDS.  LDS is
-// dynamic: [F rows of f32 tmp][strip weights if WL][offsets][taps].
+// dynamic: [F rows of f32 tmp][strip weights if WL][column offsets].
 template <int A, int R, int F, bool WL>
 __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(ResizeArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -152,11 +169,10 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
 
     float* __restrict__ s_w = lds + F * kRowWords;
     int* __restrict__ s_off = reinterpret_cast<int*>(s_w + (WL ? a.max_strip_weights : 0));
-    int* __restrict__ s_n = s_off + a.max_strip_cols;
-    for (int t = threadIdx.x; t < nox; t += kThreads) {
-        s_off[t] = a.lx[ox0 + t] * a.C - sb;
-        s_n[t] = a.nx[ox0 + t];
-    }
+    for (int t = threadIdx.x; t < nox; t += kThreads) s_off[t] = a.lx[ox0 + t] * a.C - sb;
+    for (int t = threadIdx.x; t < F * kRowWords / 4; t += kThreads)
+        reinterpret_cast<float4*>(lds)[t] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const int hq = (int)threadIdx.x / nox, hox = (int)threadIdx.x - hq * nox;
     if (WL) {
         const float* __restrict__ gw = a.wx + (size_t)ox0 * a.Tx;
         for (int t = threadIdx.x; t < nox * a.Tx; t += kThreads) s_w[t] = gw[t];
@@ -252,7 +268,7 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
             const int nrows = (next - oy0) % F + 1;
             if (nrows == F || next == oy1 - 1) {
                 __syncthreads();
-                horizontal_rows(a, lds, hw, s_off, s_n, next - nrows + 1, nrows, ox0, nox, dst);
+                horizontal_rows(a, lds, hw, s_off, next - nrows + 1, nrows, ox0, nox, hq, hox, dst);
                 __syncthreads();
             }
             ++next;
@@ -305,32 +321,16 @@ __global__ __launch_bounds__(kThreads) void k_horz_naive(ResizeArgs a) {
 
 size_t resize_lds_bytes(const ResizeArgs& a, bool wl, int flush) {
     return sizeof(float) * ((size_t)flush * kRowWords + (wl ? (size_t)a.max_strip_weights : 0) +
-                            2 * (size_t)a.max_strip_cols);
+                            (size_t)a.max_strip_cols);
 }
 
 // Instances that fit the register file without spilling (ik_plan.cpp picks A, R);
 // X(A, R, F) for every flush depth F the plan may choose.
 #define IK_FUSED_INSTANCES(X)                                               \
+    X(2, 4, 2) X(2, 4, 3) X(2, 4, 4) X(2, 8, 2) X(2, 8, 3) X(2, 8, 4)       \
     X(4, 4, 2) X(4, 4, 3) X(4, 4, 4) X(4, 8, 2) X(4, 8, 3) X(4, 8, 4)       \
     X(8, 4, 2) X(8, 4, 3) X(8, 4, 4) X(8, 8, 2) X(8, 8, 3) X(8, 8, 4)       \
     X(16, 4, 2) X(16, 4, 3) X(16, 4, 4)
-
-static const void* fused_fn(int A, int R, int F, bool wl) {
-#define IK_PICK(A_, R_, F_)                                                              \
-    if (A == A_ && R == R_ && F == F_)                                                   \
-        return wl ? reinterpret_cast<const void*>(&k_resize_fused<A_, R_, F_, true>)     \
-                  : reinterpret_cast<const void*>(&k_resize_fused<A_, R_, F_, false>);
-    IK_FUSED_INSTANCES(IK_PICK)
-#undef IK_PICK
-    return nullptr;
-}
-
-int resize_blocks_per_cu(int slots, int rows, int flush, bool wl, size_t lds) {
-    const void* fn = fused_fn(slots, rows, flush, wl);
-    int blocks = 0;
-    if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, kThreads, lds) != hipSuccess) return 0;
-    return blocks;
-}
 
 hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_pitch,
                          size_t src_img_stride, uint8_t* dst, size_t dst_pitch,

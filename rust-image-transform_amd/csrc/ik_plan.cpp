@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -99,6 +100,7 @@ int axis_weights(int in, int out, int filter, std::vector<int>& left, std::vecto
         cnt[o] = (int)(r - l);
         if (cnt[o] > T) T = cnt[o];
     }
+    T = (T + 3) & ~3;  // the fused kernel's horizontal pass runs taps in groups
     w.assign((size_t)out * T, 0.0f);
     for (int o = 0; o < out; ++o) std::memcpy(&w[(size_t)o * T], rows[o].data(), sizeof(float) * cnt[o]);
     return T;
@@ -139,7 +141,7 @@ ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int
     const int Tx = axis_weights(W, nw, filter, lx, cx, wx);
     const int Ty = axis_weights(H, nh, filter, ly, cy, wy);
     int A = required_slots(ly, cy);
-    int slots = A <= 4 ? 4 : A <= 8 ? 8 : A <= 16 ? 16 : 0;
+    int slots = A <= 2 ? 2 : A <= 4 ? 4 : A <= 8 ? 8 : A <= 16 ? 16 : 0;
 
     // prefetch depth: source rows consumed per output row after the first
     int maxblk = 1;
@@ -198,28 +200,22 @@ ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int
         long nb = (per_img + NS - 1) / NS;
         if (nb < 1) nb = 1;
         band_h = (int)((nh + nb - 1) / nb);
-        if (band_h < 32) band_h = 32;
+        // halo rows re-read per band ~ taps - ratio: short filters afford short bands
+        const int min_band = Ty <= 20 ? 16 : 32;
+        if (band_h < min_band) band_h = min_band;
         band_h = ((band_h + slots - 1) / slots) * slots;
         if (band_h > nh) band_h = nh;
     }
     if (const char* e = getenv("IK_BAND_ROWS")) band_h = std::max(1, std::min(nh, atoi(e)));
-    // flush depth F (vertical rows staged in LDS per horizontal pass): LDS per
-    // workgroup grows with F, so take the deepest F that keeps the most
-    // workgroups resident per CU (more waves = more source loads in flight).
+    // flush depth F (vertical rows staged in LDS per horizontal pass): 3 measured
+    // best on MI355X for both triangle and lanczos3 8x downscales (deeper costs
+    // resident workgroups, shallower runs the barrier-bound horizontal pass more
+    // often; tools/sweep_resize.py FLUSH=2,3,4)
     int flush = 3;
-    if (slots) {
-        int msc = 0;
-        for (int k = 0; k < NS; ++k) msc = std::max(msc, strips[3 * k + 1] - strips[3 * k]);
-        ResizeArgs probe{};
-        probe.max_strip_cols = (msc + 3) & ~3;
-        probe.max_strip_weights = (probe.max_strip_cols * Tx + 3) & ~3;
-        int best = -1;
-        for (int f = kMaxFlushRows; f >= 2; --f) {
-            const int b = resize_blocks_per_cu(slots, rows, f, wl, resize_lds_bytes(probe, wl, f));
-            if (b > best) { best = b; flush = f; }
-        }
-        if (const char* e = getenv("IK_FLUSH_ROWS")) flush = std::max(2, std::min(kMaxFlushRows, atoi(e)));
-    }
+    if (const char* e = getenv("IK_FLUSH_ROWS")) flush = std::max(2, std::min(kMaxFlushRows, atoi(e)));
+    if (getenv("IK_DEBUG_PLAN"))
+        fprintf(stderr, "[ik plan] %dx%dx%d -> %dx%d f%d: A=%d R=%d NS=%d band_h=%d wl=%d flush=%d Tx=%d\n",
+                W, H, C, nw, nh, filter, slots, rows, NS, band_h, (int)wl, flush, Tx);
     const auto key = std::make_tuple(device, W, H, C, nw, nh, filter, band_h, flush);
     std::lock_guard<std::mutex> lk(g_plan_mu);
     auto it = g_plans.find(key);

@@ -11,7 +11,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libimagekit_hip.so")
+LIB_PATH = os.environ.get("IK_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "lib", "libimagekit_hip.so")
 
 _lock = threading.Lock()
 _lib = None
