@@ -397,17 +397,19 @@ int ik_decode(const uint8_t* bytes, size_t len, ik_image** out, int* fmt_out) {
     uint32_t w = 0, h = 0, c = 0;
     std::vector<uint8_t> px;
     int st;
+    ik_image* img = nullptr;
     switch (f) {
     case Sniffed::Png: st = decode_png(bytes, len, w, h, c, px); break;
-    case Sniffed::Jpeg: st = decode_jpeg(bytes, len, w, h, c, px); break;
+    case Sniffed::Jpeg: st = decode_jpeg_device(bytes, len, &img); break;
     case Sniffed::WebP: st = decode_webp(bytes, len, w, h, c, px); break;
     default:
         return fail(IK_ERR_TRANSFORM, "The image format %s is not supported", format_name(f));
     }
     if (st) return st;
-    ik_image* img = nullptr;
-    st = ik_image_from_host(px.data(), w, h, c, &img);
-    if (st) return st;
+    if (!img) {
+        st = ik_image_from_host(px.data(), w, h, c, &img);
+        if (st) return st;
+    }
     *out = img;
     if (fmt_out) {
         *fmt_out = f == Sniffed::WebP ? IK_FORMAT_WEBP

@@ -77,6 +77,22 @@ hipError_t launch_jpeg_coeffs(const uint8_t* src, int w, int h, int C, size_t pi
                               size_t img_stride, const uint8_t* qtables /*dev, 128 B*/,
                               int16_t* coef, size_t coef_img_stride, int n, hipStream_t s);
 
+// JPEG reconstruction (ik_jpeg.hip): dequantise + islow IDCT every 8x8 block of
+// the coefficient image into per-component sample planes, then fancy-upsample +
+// colour-convert into the device image.
+struct JpegGeom {
+    int ncomp, W, H, hmax, vmax;
+    int colorspace;                 // 0 gray, 1 YCbCr, 2 RGB
+    int h[4], v[4], bw[4], bh[4], dw[4], dh[4];
+    long long blk0[4];              // first block of each component in coef
+    long long plane0[4];            // byte offset of each component plane (bw*8 x bh*8)
+    long long nblocks;
+    const uint16_t* qt;             // [component][64] natural order
+    const int16_t* coef;            // [block][64] natural order, quantised
+    uint8_t* planes;
+};
+hipError_t launch_jpeg_reconstruct(const JpegGeom& g, uint8_t* dst, size_t dst_pitch, hipStream_t s);
+
 // ---- plans (ik_plan.cpp) ----
 // sample.rs weights for one axis; returns the tap count T (row stride of w).
 int axis_weights(int in, int out, int filter, std::vector<int>& left, std::vector<int>& cnt,

@@ -1,15 +1,18 @@
 // ik_jpeg_decode.cpp -- JPEG branch of decode_image (reference src/transform.rs:31 ->
-// image 0.25.8 -> zune-jpeg 0.4.21, Cargo.lock:3106).
+// image 0.25.8 -> zune-jpeg 0.4.21, Cargo.lock:3106), host half.
 //
-// Baseline sequential Huffman JPEG (SOF0/SOF1, 8-bit), any sampling factors,
-// restart intervals, 1 (gray -> L8) or 3 (YCbCr -> Rgb8) components.
-// zune-jpeg's output cannot be checked offline (no crate sources), so the
-// reconstruction follows the libjpeg decode pipeline that zune-jpeg aims to
-// match: jidctint islow IDCT with the range-limit table, "fancy" h2v1 / h2v2 /
-// h1v2 chroma upsampling with replicated edge context rows, and jdcolor's
-// fixed-point YCbCr->RGB tables.  Parity is pinned against libjpeg-turbo
-// (Pillow) in tests/test_gpu_decode.py.  Progressive, arithmetic-coded, 12-bit
-// and CMYK JPEGs report IK_ERR_UNSUPPORTED.
+// The host parses the markers and runs the Huffman entropy decoder into a dense
+// block-coefficient image (quantised int16, natural order, one plane of 8x8
+// blocks per component): baseline sequential (SOF0/SOF1, interleaved or not) and
+// progressive (SOF2: DC first/refine, AC first/refine with EOB runs), restart
+// intervals, 8-bit, 1 (gray -> L8) or 3 components (YCbCr -> Rgb8, or RGB for
+// Adobe transform 0).  Reconstruction -- dequantise, islow IDCT, fancy chroma
+// upsampling, YCbCr->RGB -- runs on the GPU (ik_jpeg.hip) straight into the
+// device image.  zune-jpeg's output cannot be checked offline (no crate
+// sources), so reconstruction follows the libjpeg pipeline zune-jpeg aims to
+// match; parity is pinned against libjpeg-turbo (Pillow) in tests/test_gpu_decode.py.
+// Arithmetic-coded, lossless, hierarchical, 12-bit and CMYK JPEGs report
+// IK_ERR_UNSUPPORTED.
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -64,14 +67,6 @@ bool build_huff(const uint8_t* bits, const uint8_t* vals, int nvals, HuffTable& 
     return true;
 }
 
-struct Component {
-    int id = 0, h = 1, v = 1, tq = 0, td = 0, ta = 0;
-    int bw = 0, bh = 0;          // blocks across/down (padded to MCUs)
-    int dw = 0, dh = 0;          // downsampled width/height (libjpeg downsampled_width/height)
-    std::vector<uint8_t> plane;  // bw*8 x bh*8 samples after IDCT
-    int pred = 0;
-};
-
 struct BitReader {
     const uint8_t* p;
     const uint8_t* end;
@@ -118,343 +113,362 @@ int decode_symbol(BitReader& br, const HuffTable& t) {
     return -1;
 }
 
-// jidctint.c jpeg_idct_islow (libjpeg / libjpeg-turbo), dequantised input
-#define CB 13
-#define P1 2
-void idct_islow(const int* in, uint8_t* out, int stride) {
-    int ws[64];
-    auto descale = [](long long x, int n) { return (int)((x + (1ll << (n - 1))) >> n); };
-    auto clamp = [](int x) -> uint8_t { x += 128; return (uint8_t)(x < 0 ? 0 : x > 255 ? 255 : x); };
-    for (int c = 0; c < 8; ++c) {
-        const int* ip = in + c;
-        if (!ip[8] && !ip[16] && !ip[24] && !ip[32] && !ip[40] && !ip[48] && !ip[56]) {
-            const int dc = ip[0] * (1 << P1);
-            for (int r = 0; r < 8; ++r) ws[r * 8 + c] = dc;
-            continue;
-        }
-        long long z2 = ip[16], z3 = ip[48];
-        long long z1 = (z2 + z3) * 4433;
-        long long tmp2 = z1 + z3 * -15137, tmp3 = z1 + z2 * 6270;
-        z2 = ip[0]; z3 = ip[32];
-        long long tmp0 = (z2 + z3) * (1ll << CB), tmp1 = (z2 - z3) * (1ll << CB);
-        long long t10 = tmp0 + tmp3, t13 = tmp0 - tmp3, t11 = tmp1 + tmp2, t12 = tmp1 - tmp2;
-        tmp0 = ip[56]; tmp1 = ip[40]; tmp2 = ip[24]; tmp3 = ip[8];
-        z1 = tmp0 + tmp3; z2 = tmp1 + tmp2; z3 = tmp0 + tmp2;
-        long long z4 = tmp1 + tmp3, z5 = (z3 + z4) * 9633;
-        tmp0 *= 2446; tmp1 *= 16819; tmp2 *= 25172; tmp3 *= 12299;
-        z1 *= -7373; z2 *= -20995; z3 *= -16069; z4 *= -3196;
-        z3 += z5; z4 += z5;
-        tmp0 += z1 + z3; tmp1 += z2 + z4; tmp2 += z2 + z3; tmp3 += z1 + z4;
-        ws[0 * 8 + c] = descale(t10 + tmp3, CB - P1);
-        ws[7 * 8 + c] = descale(t10 - tmp3, CB - P1);
-        ws[1 * 8 + c] = descale(t11 + tmp2, CB - P1);
-        ws[6 * 8 + c] = descale(t11 - tmp2, CB - P1);
-        ws[2 * 8 + c] = descale(t12 + tmp1, CB - P1);
-        ws[5 * 8 + c] = descale(t12 - tmp1, CB - P1);
-        ws[3 * 8 + c] = descale(t13 + tmp0, CB - P1);
-        ws[4 * 8 + c] = descale(t13 - tmp0, CB - P1);
-    }
-    for (int r = 0; r < 8; ++r) {
-        const int* w = ws + r * 8;
-        uint8_t* o = out + (size_t)r * stride;
-        if (!w[1] && !w[2] && !w[3] && !w[4] && !w[5] && !w[6] && !w[7]) {
-            const uint8_t dc = clamp(descale(w[0], P1 + 3));
-            for (int k = 0; k < 8; ++k) o[k] = dc;
-            continue;
-        }
-        long long z2 = w[2], z3 = w[6];
-        long long z1 = (z2 + z3) * 4433;
-        long long tmp2 = z1 + z3 * -15137, tmp3 = z1 + z2 * 6270;
-        long long tmp0 = ((long long)w[0] + w[4]) * (1ll << CB), tmp1 = ((long long)w[0] - w[4]) * (1ll << CB);
-        long long t10 = tmp0 + tmp3, t13 = tmp0 - tmp3, t11 = tmp1 + tmp2, t12 = tmp1 - tmp2;
-        tmp0 = w[7]; tmp1 = w[5]; tmp2 = w[3]; tmp3 = w[1];
-        z1 = tmp0 + tmp3; z2 = tmp1 + tmp2; z3 = tmp0 + tmp2;
-        long long z4 = tmp1 + tmp3, z5 = (z3 + z4) * 9633;
-        tmp0 *= 2446; tmp1 *= 16819; tmp2 *= 25172; tmp3 *= 12299;
-        z1 *= -7373; z2 *= -20995; z3 *= -16069; z4 *= -3196;
-        z3 += z5; z4 += z5;
-        tmp0 += z1 + z3; tmp1 += z2 + z4; tmp2 += z2 + z3; tmp3 += z1 + z4;
-        const int sh = CB + P1 + 3;
-        o[0] = clamp(descale(t10 + tmp3, sh)); o[7] = clamp(descale(t10 - tmp3, sh));
-        o[1] = clamp(descale(t11 + tmp2, sh)); o[6] = clamp(descale(t11 - tmp2, sh));
-        o[2] = clamp(descale(t12 + tmp1, sh)); o[5] = clamp(descale(t12 - tmp1, sh));
-        o[3] = clamp(descale(t13 + tmp0, sh)); o[4] = clamp(descale(t13 - tmp0, sh));
-    }
-}
-#undef CB
-#undef P1
+struct Component {
+    int id = 0, h = 1, v = 1, tq = 0, td = 0, ta = 0;
+    int bw = 0, bh = 0;    // blocks across/down, padded to whole MCUs
+    int dw = 0, dh = 0;    // downsampled width/height (libjpeg downsampled_width/height)
+    size_t blk0 = 0;       // first block in the coefficient image
+    int pred = 0;
+};
 
-// jdcolor.c ycc_rgb_convert tables (SCALEBITS 16)
-struct YccTables {
-    int cr_r[256], cb_b[256];
-    long long cr_g[256], cb_g[256];
-    YccTables() {
-        const long long half = 1ll << 15;
-        auto fix = [](double x) { return (long long)(x * 65536.0 + 0.5); };
-        for (int i = 0; i < 256; ++i) {
-            const long long x = i - 128;
-            cr_r[i] = (int)((fix(1.40200) * x + half) >> 16);
-            cb_b[i] = (int)((fix(1.77200) * x + half) >> 16);
-            cr_g[i] = -fix(0.71414) * x;
-            cb_g[i] = -fix(0.34414) * x + half;
+const char* const kFmtErr = "Format error decoding Jpeg";
+
+struct Decoder {
+    const uint8_t* b;
+    const uint8_t* end;
+    uint16_t qt[4][64] = {};
+    HuffTable dc[4], ac[4];
+    std::vector<Component> comps;
+    int width = 0, height = 0, restart = 0, hmax = 1, vmax = 1, mcux = 0, mcuy = 0;
+    bool have_frame = false, progressive = false, adobe = false;
+    int adobe_transform = -1;
+    std::vector<int16_t> coef;  // [block][64], natural order, quantised
+    int eobrun = 0;
+
+    int16_t* block(const Component& c, int bx, int by) { return &coef[(c.blk0 + (size_t)by * c.bw + bx) * 64]; }
+
+    int frame(const uint8_t* s, int m) {
+        if (have_frame) return fail(IK_ERR_TRANSFORM, "%s: duplicate SOF", kFmtErr);
+        if (s[0] != 8) return fail(IK_ERR_UNSUPPORTED, "%d-bit JPEG is not supported", s[0]);
+        progressive = m == 0xC2;
+        height = (int)s[1] << 8 | s[2];
+        width = (int)s[3] << 8 | s[4];
+        const int nc = s[5];
+        if (!width || !height) return fail(IK_ERR_TRANSFORM, "%s: zero dimension", kFmtErr);
+        if (nc != 1 && nc != 3) return fail(IK_ERR_UNSUPPORTED, "JPEG with %d components is not supported", nc);
+        if ((uint64_t)width * height > (512ull << 20) / 3) return fail(IK_ERR_TRANSFORM, "Limits are exceeded");
+        comps.resize(nc);
+        for (int i = 0; i < nc; ++i) {
+            comps[i].id = s[6 + 3 * i];
+            comps[i].h = s[7 + 3 * i] >> 4;
+            comps[i].v = s[7 + 3 * i] & 15;
+            comps[i].tq = s[8 + 3 * i] & 3;
+            if (comps[i].h < 1 || comps[i].h > 4 || comps[i].v < 1 || comps[i].v > 4)
+                return fail(IK_ERR_TRANSFORM, "%s: bad sampling factors", kFmtErr);
+            hmax = std::max(hmax, comps[i].h);
+            vmax = std::max(vmax, comps[i].v);
+        }
+        for (auto& c : comps)
+            if (hmax % c.h || vmax % c.v)
+                return fail(IK_ERR_UNSUPPORTED, "fractional JPEG chroma sampling is not supported");
+        mcux = (width + 8 * hmax - 1) / (8 * hmax);
+        mcuy = (height + 8 * vmax - 1) / (8 * vmax);
+        size_t blocks = 0;
+        for (auto& c : comps) {
+            c.bw = mcux * c.h;
+            c.bh = mcuy * c.v;
+            c.dw = (width * c.h + hmax - 1) / hmax;
+            c.dh = (height * c.v + vmax - 1) / vmax;
+            c.blk0 = blocks;
+            blocks += (size_t)c.bw * c.bh;
+        }
+        coef.assign(blocks * 64, 0);
+        have_frame = true;
+        return IK_OK;
+    }
+
+    // one block of one scan (ITU T.81 F.2.2 / G.1.2; libjpeg jdhuff.c / jdphuff.c)
+    int block_baseline(BitReader& br, Component& c, int16_t* blk) {
+        const int t = decode_symbol(br, dc[c.td]);
+        if (t < 0 || t > 11) return fail(IK_ERR_TRANSFORM, "%s: bad DC code", kFmtErr);
+        c.pred += t ? extend(br.get(t), t) : 0;
+        blk[0] = (int16_t)c.pred;
+        for (int k = 1; k < 64;) {
+            const int rs = decode_symbol(br, ac[c.ta]);
+            if (rs < 0) return fail(IK_ERR_TRANSFORM, "%s: bad AC code", kFmtErr);
+            const int r = rs >> 4, sz = rs & 15;
+            if (!sz) {
+                if (r != 15) break;  // EOB
+                k += 16;
+                continue;
+            }
+            k += r;
+            if (k > 63) return fail(IK_ERR_TRANSFORM, "%s: AC overflow", kFmtErr);
+            blk[kZigzag[k]] = (int16_t)extend(br.get(sz), sz);
+            ++k;
+        }
+        return IK_OK;
+    }
+    int block_dc_first(BitReader& br, Component& c, int16_t* blk, int Al) {
+        const int t = decode_symbol(br, dc[c.td]);
+        if (t < 0 || t > 11) return fail(IK_ERR_TRANSFORM, "%s: bad DC code", kFmtErr);
+        c.pred += t ? extend(br.get(t), t) : 0;
+        blk[0] = (int16_t)(c.pred * (1 << Al));
+        return IK_OK;
+    }
+    void block_dc_refine(BitReader& br, int16_t* blk, int Al) {
+        if (br.get(1)) blk[0] = (int16_t)(blk[0] | (1 << Al));
+    }
+    int block_ac_first(BitReader& br, const Component& c, int16_t* blk, int Ss, int Se, int Al) {
+        if (eobrun > 0) { --eobrun; return IK_OK; }
+        for (int k = Ss; k <= Se; ++k) {
+            const int rs = decode_symbol(br, ac[c.ta]);
+            if (rs < 0) return fail(IK_ERR_TRANSFORM, "%s: bad AC code", kFmtErr);
+            const int r = rs >> 4, sz = rs & 15;
+            if (sz) {
+                k += r;
+                if (k > Se) return fail(IK_ERR_TRANSFORM, "%s: AC overflow", kFmtErr);
+                blk[kZigzag[k]] = (int16_t)(extend(br.get(sz), sz) * (1 << Al));
+            } else if (r == 15) {
+                k += 15;
+            } else {
+                eobrun = 1 << r;
+                if (r) eobrun += br.get(r);
+                --eobrun;
+                break;
+            }
+        }
+        return IK_OK;
+    }
+    int block_ac_refine(BitReader& br, const Component& c, int16_t* blk, int Ss, int Se, int Al) {
+        const int p1 = 1 << Al, m1 = -1 * (1 << Al);
+        auto refine = [&](int16_t* co) {
+            if (br.get(1) && (*co & p1) == 0) *co = (int16_t)(*co >= 0 ? *co + p1 : *co + m1);
+        };
+        int k = Ss;
+        if (eobrun == 0) {
+            for (; k <= Se; ++k) {
+                const int rs = decode_symbol(br, ac[c.ta]);
+                if (rs < 0) return fail(IK_ERR_TRANSFORM, "%s: bad AC code", kFmtErr);
+                int r = rs >> 4, sz = rs & 15, val = 0;
+                if (sz) {
+                    if (sz != 1) return fail(IK_ERR_TRANSFORM, "%s: bad AC refinement", kFmtErr);
+                    val = br.get(1) ? p1 : m1;
+                } else if (r != 15) {
+                    eobrun = 1 << r;
+                    if (r) eobrun += br.get(r);
+                    break;  // the rest of the band goes to the EOB-run pass below
+                }
+                // skip r zero-history coefficients, refining the nonzero ones passed
+                do {
+                    int16_t* co = blk + kZigzag[k];
+                    if (*co != 0) refine(co);
+                    else if (--r < 0) break;
+                    ++k;
+                } while (k <= Se);
+                if (val) {
+                    if (k > Se) return fail(IK_ERR_TRANSFORM, "%s: AC overflow", kFmtErr);
+                    blk[kZigzag[k]] = (int16_t)val;
+                }
+            }
+        }
+        if (eobrun > 0) {
+            for (; k <= Se; ++k) {
+                int16_t* co = blk + kZigzag[k];
+                if (*co != 0) refine(co);
+            }
+            --eobrun;
+        }
+        return IK_OK;
+    }
+
+    int scan(const uint8_t* s, const uint8_t* se, const uint8_t*& next) {
+        if (!have_frame) return fail(IK_ERR_TRANSFORM, "%s: SOS before SOF", kFmtErr);
+        const int ns = s[0];
+        if (ns < 1 || ns > (int)comps.size() || se - s < 1 + 2 * ns + 3)
+            return fail(IK_ERR_TRANSFORM, "%s: bad SOS", kFmtErr);
+        std::vector<int> order(ns);
+        for (int i = 0; i < ns; ++i) {
+            const int cid = s[1 + 2 * i];
+            int k = -1;
+            for (int j = 0; j < (int)comps.size(); ++j) if (comps[j].id == cid) k = j;
+            if (k < 0) return fail(IK_ERR_TRANSFORM, "%s: bad scan component", kFmtErr);
+            comps[k].td = s[2 + 2 * i] >> 4;
+            comps[k].ta = s[2 + 2 * i] & 15;
+            if (comps[k].td > 3 || comps[k].ta > 3) return fail(IK_ERR_TRANSFORM, "%s: bad table id", kFmtErr);
+            order[i] = k;
+        }
+        const int Ss = s[1 + 2 * ns], Se = s[2 + 2 * ns], Ah = s[3 + 2 * ns] >> 4, Al = s[3 + 2 * ns] & 15;
+        // kind: 0 baseline, 1 DC first, 2 DC refine, 3 AC first, 4 AC refine
+        int kind = 0;
+        if (progressive) {
+            if (Ss == 0) {
+                if (Se != 0) return fail(IK_ERR_TRANSFORM, "%s: bad progressive DC scan", kFmtErr);
+                kind = Ah ? 2 : 1;
+            } else {
+                if (Se < Ss || Se > 63 || ns != 1) return fail(IK_ERR_TRANSFORM, "%s: bad progressive AC scan", kFmtErr);
+                kind = Ah ? 4 : 3;
+            }
+            if (Al > 13) return fail(IK_ERR_TRANSFORM, "%s: bad successive approximation", kFmtErr);
+        }
+        for (int i = 0; i < ns; ++i) {
+            const Component& c = comps[order[i]];
+            const bool need_dc = kind == 0 || kind == 1, need_ac = kind == 0 || kind >= 3;
+            if ((need_dc && !dc[c.td].present) || (need_ac && !ac[c.ta].present))
+                return fail(IK_ERR_TRANSFORM, "%s: missing Huffman table", kFmtErr);
+        }
+        for (auto& c : comps) c.pred = 0;
+        eobrun = 0;
+        BitReader br{se, end};
+        const bool single = ns == 1;
+        const Component& c0 = comps[order[0]];
+        const int single_bw = (c0.dw + 7) / 8, single_bh = (c0.dh + 7) / 8;
+        const long total_mcu = single ? (long)single_bw * single_bh : (long)mcux * mcuy;
+        auto do_block = [&](Component& c, int16_t* blk) -> int {
+            switch (kind) {
+            case 0: return block_baseline(br, c, blk);
+            case 1: return block_dc_first(br, c, blk, Al);
+            case 2: block_dc_refine(br, blk, Al); return IK_OK;
+            case 3: return block_ac_first(br, c, blk, Ss, Se, Al);
+            default: return block_ac_refine(br, c, blk, Ss, Se, Al);
+            }
+        };
+        for (long mcu = 0; mcu < total_mcu; ++mcu) {
+            if (restart && mcu > 0 && mcu % restart == 0) {
+                // expect RSTn: realign to the marker, reset predictors and EOB run
+                const uint8_t* q = br.p;
+                while (q + 1 < end && !(q[0] == 0xFF && q[1] >= 0xD0 && q[1] <= 0xD7)) ++q;
+                if (q + 1 >= end) return fail(IK_ERR_TRANSFORM, "%s: missing restart marker", kFmtErr);
+                br.p = q + 2;
+                br.reset_at_marker();
+                for (auto& c : comps) c.pred = 0;
+                eobrun = 0;
+            }
+            if (single) {
+                Component& c = comps[order[0]];
+                const int st = do_block(c, block(c, (int)(mcu % single_bw), (int)(mcu / single_bw)));
+                if (st) return st;
+                continue;
+            }
+            const int mx = (int)(mcu % mcux), my = (int)(mcu / mcux);
+            for (int oi = 0; oi < ns; ++oi) {
+                Component& c = comps[order[oi]];
+                for (int by = 0; by < c.v; ++by)
+                    for (int bx = 0; bx < c.h; ++bx) {
+                        const int st = do_block(c, block(c, mx * c.h + bx, my * c.v + by));
+                        if (st) return st;
+                    }
+            }
+        }
+        next = br.p;
+        return IK_OK;
+    }
+
+    int parse() {
+        const uint8_t* p = b + 2;
+        auto be16 = [](const uint8_t* q) { return (int)q[0] << 8 | q[1]; };
+        bool scanned = false;
+        for (;;) {
+            while (p < end && *p != 0xFF) ++p;  // tolerate garbage between segments
+            while (p < end && *p == 0xFF) ++p;
+            if (p >= end || *p == 0xD9) {
+                if (scanned) return IK_OK;  // EOI (or a stream cut after its last scan)
+                return fail(IK_ERR_TRANSFORM, "%s: no SOS", kFmtErr);
+            }
+            const uint8_t m = *p++;
+            if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
+            if (p + 2 > end) return fail(IK_ERR_TRANSFORM, "%s: truncated", kFmtErr);
+            const int len = be16(p);
+            if (len < 2 || p + len > end) return fail(IK_ERR_TRANSFORM, "%s: bad segment length", kFmtErr);
+            const uint8_t* s = p + 2;
+            const uint8_t* se = p + len;
+            if (m == 0xDB) {  // DQT
+                while (s < se) {
+                    const int pq = s[0] >> 4, tq = s[0] & 15;
+                    if (tq > 3 || s + 1 + (pq ? 128 : 64) > se) return fail(IK_ERR_TRANSFORM, "%s: bad DQT", kFmtErr);
+                    ++s;
+                    for (int i = 0; i < 64; ++i) qt[tq][kZigzag[i]] = pq ? (uint16_t)be16(s + 2 * i) : s[i];
+                    s += pq ? 128 : 64;
+                }
+            } else if (m == 0xC4) {  // DHT
+                while (s < se) {
+                    const int tc = s[0] >> 4, th = s[0] & 15;
+                    if (th > 3 || tc > 1 || s + 17 > se) return fail(IK_ERR_TRANSFORM, "%s: bad DHT", kFmtErr);
+                    int total = 0;
+                    for (int i = 0; i < 16; ++i) total += s[1 + i];
+                    if (total > 256 || s + 17 + total > se) return fail(IK_ERR_TRANSFORM, "%s: bad DHT", kFmtErr);
+                    if (!build_huff(s + 1, s + 17, total, tc ? ac[th] : dc[th]))
+                        return fail(IK_ERR_TRANSFORM, "%s: bad Huffman table", kFmtErr);
+                    s += 17 + total;
+                }
+            } else if (m == 0xDD) {  // DRI
+                if (len < 4) return fail(IK_ERR_TRANSFORM, "%s: bad DRI", kFmtErr);
+                restart = be16(s);
+            } else if (m == 0xEE) {  // APP14 Adobe
+                if (len >= 14 && !std::memcmp(s, "Adobe", 5)) { adobe = true; adobe_transform = s[11]; }
+            } else if (m == 0xC0 || m == 0xC1 || m == 0xC2) {  // SOF0 / SOF1 / SOF2
+                if (len < 8) return fail(IK_ERR_TRANSFORM, "%s: bad SOF", kFmtErr);
+                const int st = frame(s, m);
+                if (st) return st;
+            } else if (m >= 0xC3 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+                return fail(IK_ERR_UNSUPPORTED, "arithmetic / lossless / hierarchical JPEG (SOF%d) is not supported",
+                            m - 0xC0);
+            } else if (m == 0xDA) {  // SOS: entropy-coded data follows the header
+                const uint8_t* next = se;
+                const int st = scan(s, se, next);
+                if (st) return st;
+                scanned = true;
+                p = next;
+                continue;
+            }
+            p += len;
         }
     }
 };
 
-inline uint8_t clamp255(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
-
-// upsample one component plane (dw x dh valid samples) to the full image size
-void upsample(const Component& c, int hmax, int vmax, int W, int H, std::vector<uint8_t>& out) {
-    const int pw = c.bw * 8;  // plane stride
-    const int fh = hmax / c.h, fv = vmax / c.v;
-    const int ow = c.dw * fh, oh = c.dh * fv;
-    std::vector<uint8_t> full((size_t)ow * oh);
-    auto in = [&](int y) { return c.plane.data() + (size_t)(y < 0 ? 0 : y >= c.dh ? c.dh - 1 : y) * pw; };
-    if (fh == 1 && fv == 1) {
-        for (int y = 0; y < oh; ++y) std::memcpy(&full[(size_t)y * ow], in(y), ow);
-    } else if (fh == 2 && fv == 1) {  // h2v1_fancy_upsample
-        for (int y = 0; y < c.dh; ++y) {
-            const uint8_t* ip = in(y);
-            uint8_t* op = &full[(size_t)y * ow];
-            if (c.dw == 1) { op[0] = op[1] = ip[0]; continue; }
-            op[0] = ip[0];
-            op[1] = (uint8_t)((ip[0] * 3 + ip[1] + 2) >> 2);
-            for (int x = 1; x < c.dw - 1; ++x) {
-                const int v3 = ip[x] * 3;
-                op[2 * x] = (uint8_t)((v3 + ip[x - 1] + 1) >> 2);
-                op[2 * x + 1] = (uint8_t)((v3 + ip[x + 1] + 2) >> 2);
-            }
-            const int x = c.dw - 1;
-            op[2 * x] = (uint8_t)((ip[x] * 3 + ip[x - 1] + 1) >> 2);
-            op[2 * x + 1] = ip[x];
-        }
-    } else if (fh == 2 && fv == 2) {  // h2v2_fancy_upsample
-        for (int y = 0; y < c.dh; ++y) {
-            for (int v = 0; v < 2; ++v) {
-                const uint8_t* i0 = in(y);
-                const uint8_t* i1 = in(v == 0 ? y - 1 : y + 1);
-                uint8_t* op = &full[(size_t)(2 * y + v) * ow];
-                if (c.dw == 1) {
-                    const int s = i0[0] * 3 + i1[0];
-                    op[0] = (uint8_t)((s * 4 + 8) >> 4);
-                    op[1] = (uint8_t)((s * 4 + 7) >> 4);
-                    continue;
-                }
-                int thiss = i0[0] * 3 + i1[0];
-                int nexts = i0[1] * 3 + i1[1];
-                op[0] = (uint8_t)((thiss * 4 + 8) >> 4);
-                op[1] = (uint8_t)((thiss * 3 + nexts + 7) >> 4);
-                int lasts = thiss;
-                thiss = nexts;
-                for (int x = 1; x < c.dw - 1; ++x) {
-                    nexts = i0[x + 1] * 3 + i1[x + 1];
-                    op[2 * x] = (uint8_t)((thiss * 3 + lasts + 8) >> 4);
-                    op[2 * x + 1] = (uint8_t)((thiss * 3 + nexts + 7) >> 4);
-                    lasts = thiss;
-                    thiss = nexts;
-                }
-                const int x = c.dw - 1;
-                op[2 * x] = (uint8_t)((thiss * 3 + lasts + 8) >> 4);
-                op[2 * x + 1] = (uint8_t)((thiss * 4 + 7) >> 4);
-            }
-        }
-    } else if (fh == 1 && fv == 2) {  // h1v2_fancy_upsample (libjpeg-turbo)
-        for (int y = 0; y < c.dh; ++y)
-            for (int v = 0; v < 2; ++v) {
-                const uint8_t* i0 = in(y);
-                const uint8_t* i1 = in(v == 0 ? y - 1 : y + 1);
-                const int bias = v == 0 ? 1 : 2;
-                uint8_t* op = &full[(size_t)(2 * y + v) * ow];
-                for (int x = 0; x < c.dw; ++x) op[x] = (uint8_t)((i0[x] * 3 + i1[x] + bias) >> 2);
-            }
-    } else {  // int_upsample: replication
-        for (int y = 0; y < oh; ++y)
-            for (int x = 0; x < ow; ++x) full[(size_t)y * ow + x] = in(y / fv)[x / fh];
-    }
-    out.assign((size_t)W * H, 0);
-    for (int y = 0; y < H; ++y) {
-        const int sy = y < oh ? y : oh - 1;
-        for (int x = 0; x < W; ++x) out[(size_t)y * W + x] = full[(size_t)sy * ow + (x < ow ? x : ow - 1)];
-    }
-}
-
 }  // namespace
 
-int decode_jpeg(const uint8_t* b, size_t n, uint32_t& W, uint32_t& H, uint32_t& C, std::vector<uint8_t>& px) {
-    const uint8_t* p = b + 2;
-    const uint8_t* end = b + n;
-    uint16_t qt[4][64] = {};
-    HuffTable dc[4], ac[4];
-    std::vector<Component> comps;
-    int width = 0, height = 0, restart = 0;
-    bool have_frame = false, adobe = false;
-    int adobe_transform = -1;
-    auto be16 = [](const uint8_t* q) { return (int)q[0] << 8 | q[1]; };
-    const char* fmt_err = "Format error decoding Jpeg";
-    for (;;) {
-        while (p < end && *p != 0xFF) ++p;  // tolerate garbage between segments
-        while (p < end && *p == 0xFF) ++p;
-        if (p >= end) return fail(IK_ERR_TRANSFORM, "%s: no SOS", fmt_err);
-        const uint8_t m = *p++;
-        if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
-        if (m == 0xD9) return fail(IK_ERR_TRANSFORM, "%s: no SOS", fmt_err);
-        if (p + 2 > end) return fail(IK_ERR_TRANSFORM, "%s: truncated", fmt_err);
-        const int len = be16(p);
-        if (len < 2 || p + len > end) return fail(IK_ERR_TRANSFORM, "%s: bad segment length", fmt_err);
-        const uint8_t* s = p + 2;
-        const uint8_t* se = p + len;
-        if (m == 0xDB) {  // DQT
-            while (s < se) {
-                const int pq = s[0] >> 4, tq = s[0] & 15;
-                if (tq > 3) return fail(IK_ERR_TRANSFORM, "%s: bad DQT", fmt_err);
-                ++s;
-                for (int i = 0; i < 64; ++i) {
-                    qt[tq][kZigzag[i]] = pq ? (uint16_t)be16(s + 2 * i) : s[i];
-                }
-                s += pq ? 128 : 64;
-            }
-        } else if (m == 0xC4) {  // DHT
-            while (s < se) {
-                const int tc = s[0] >> 4, th = s[0] & 15;
-                if (th > 3 || tc > 1 || s + 17 > se) return fail(IK_ERR_TRANSFORM, "%s: bad DHT", fmt_err);
-                int total = 0;
-                for (int i = 0; i < 16; ++i) total += s[1 + i];
-                if (total > 256 || s + 17 + total > se) return fail(IK_ERR_TRANSFORM, "%s: bad DHT", fmt_err);
-                if (!build_huff(s + 1, s + 17, total, tc ? ac[th] : dc[th]))
-                    return fail(IK_ERR_TRANSFORM, "%s: bad Huffman table", fmt_err);
-                s += 17 + total;
-            }
-        } else if (m == 0xDD) {  // DRI
-            restart = be16(s);
-        } else if (m == 0xEE) {  // APP14 Adobe
-            if (len >= 14 && !std::memcmp(s, "Adobe", 5)) { adobe = true; adobe_transform = s[11]; }
-        } else if (m == 0xC0 || m == 0xC1) {  // SOF0 / SOF1 baseline
-            if (s[0] != 8) return fail(IK_ERR_UNSUPPORTED, "12-bit JPEG is not supported");
-            height = be16(s + 1);
-            width = be16(s + 3);
-            const int nc = s[5];
-            if (!width || !height) return fail(IK_ERR_TRANSFORM, "%s: zero dimension", fmt_err);
-            if (nc != 1 && nc != 3) return fail(IK_ERR_UNSUPPORTED, "JPEG with %d components is not supported", nc);
-            comps.resize(nc);
-            for (int i = 0; i < nc; ++i) {
-                comps[i].id = s[6 + 3 * i];
-                comps[i].h = s[7 + 3 * i] >> 4;
-                comps[i].v = s[7 + 3 * i] & 15;
-                comps[i].tq = s[8 + 3 * i] & 3;
-                if (comps[i].h < 1 || comps[i].h > 4 || comps[i].v < 1 || comps[i].v > 4)
-                    return fail(IK_ERR_TRANSFORM, "%s: bad sampling factors", fmt_err);
-            }
-            have_frame = true;
-        } else if ((m >= 0xC2 && m <= 0xCF) && m != 0xC4 && m != 0xC8 && m != 0xCC) {
-            return fail(IK_ERR_UNSUPPORTED, "progressive / arithmetic / lossless JPEG (SOF%d) is not supported",
-                        m - 0xC0);
-        } else if (m == 0xDA) {  // SOS
-            if (!have_frame) return fail(IK_ERR_TRANSFORM, "%s: SOS before SOF", fmt_err);
-            const int ns = s[0];
-            if (ns != (int)comps.size()) return fail(IK_ERR_UNSUPPORTED, "non-interleaved baseline scans are not supported");
-            std::vector<int> order(ns);
-            for (int i = 0; i < ns; ++i) {
-                const int cid = s[1 + 2 * i];
-                int k = -1;
-                for (int j = 0; j < (int)comps.size(); ++j) if (comps[j].id == cid) k = j;
-                if (k < 0) return fail(IK_ERR_TRANSFORM, "%s: bad scan component", fmt_err);
-                comps[k].td = s[2 + 2 * i] >> 4;
-                comps[k].ta = s[2 + 2 * i] & 15;
-                if (comps[k].td > 3 || comps[k].ta > 3 || !dc[comps[k].td].present || !ac[comps[k].ta].present)
-                    return fail(IK_ERR_TRANSFORM, "%s: missing Huffman table", fmt_err);
-                order[i] = k;
-            }
-            // geometry
-            int hmax = 1, vmax = 1;
-            for (auto& c : comps) { hmax = std::max(hmax, c.h); vmax = std::max(vmax, c.v); }
-            const int mcux = (width + 8 * hmax - 1) / (8 * hmax), mcuy = (height + 8 * vmax - 1) / (8 * vmax);
-            if ((uint64_t)width * height > (512ull << 20) / 3) return fail(IK_ERR_TRANSFORM, "Limits are exceeded");
-            for (auto& c : comps) {
-                c.bw = mcux * c.h;
-                c.bh = mcuy * c.v;
-                c.dw = (width * c.h + hmax - 1) / hmax;
-                c.dh = (height * c.v + vmax - 1) / vmax;
-                c.plane.assign((size_t)c.bw * 8 * c.bh * 8, 0);
-                c.pred = 0;
-            }
-            BitReader br{se, end};
-            int blk[64];
-            const bool single = ns == 1;
-            const int total_mcu = single ? ((comps[0].dw + 7) / 8) * ((comps[0].dh + 7) / 8) : mcux * mcuy;
-            const int single_bw = single ? (comps[0].dw + 7) / 8 : 0;
-            for (int mcu = 0; mcu < total_mcu; ++mcu) {
-                if (restart && mcu > 0 && mcu % restart == 0) {
-                    // expect RSTn: realign to the marker and reset predictors
-                    const uint8_t* q = br.p;
-                    while (q + 1 < end && !(q[0] == 0xFF && q[1] >= 0xD0 && q[1] <= 0xD7)) ++q;
-                    if (q + 1 >= end) return fail(IK_ERR_TRANSFORM, "%s: missing restart marker", fmt_err);
-                    br.p = q + 2;
-                    br.reset_at_marker();
-                    for (auto& c : comps) c.pred = 0;
-                }
-                for (int oi = 0; oi < ns; ++oi) {
-                    Component& c = comps[order[oi]];
-                    const int nby = single ? 1 : c.v, nbx = single ? 1 : c.h;
-                    for (int by = 0; by < nby; ++by)
-                        for (int bx = 0; bx < nbx; ++bx) {
-                            std::memset(blk, 0, sizeof(blk));
-                            const int t = decode_symbol(br, dc[c.td]);
-                            if (t < 0 || t > 11) return fail(IK_ERR_TRANSFORM, "%s: bad DC code", fmt_err);
-                            const int diff = t ? extend(br.get(t), t) : 0;
-                            c.pred += diff;
-                            blk[0] = c.pred * qt[c.tq][0];
-                            for (int k = 1; k < 64;) {
-                                const int rs = decode_symbol(br, ac[c.ta]);
-                                if (rs < 0) return fail(IK_ERR_TRANSFORM, "%s: bad AC code", fmt_err);
-                                const int r = rs >> 4, sz = rs & 15;
-                                if (!sz) {
-                                    if (r != 15) break;  // EOB
-                                    k += 16;
-                                    continue;
-                                }
-                                k += r;
-                                if (k > 63) return fail(IK_ERR_TRANSFORM, "%s: AC overflow", fmt_err);
-                                const int zz = kZigzag[k];
-                                blk[zz] = extend(br.get(sz), sz) * qt[c.tq][zz];
-                                ++k;
-                            }
-                            int bxx, byy;
-                            if (single) { bxx = mcu % single_bw; byy = mcu / single_bw; }
-                            else { bxx = (mcu % mcux) * c.h + bx; byy = (mcu / mcux) * c.v + by; }
-                            idct_islow(blk, c.plane.data() + (size_t)byy * 8 * (c.bw * 8) + bxx * 8, c.bw * 8);
-                        }
-                }
-            }
-            // upsample + colour convert
-            W = (uint32_t)width;
-            H = (uint32_t)height;
-            if (comps.size() == 1) {
-                C = 1;
-                px.resize((size_t)width * height);
-                const Component& c = comps[0];
-                for (int y = 0; y < height; ++y)
-                    std::memcpy(&px[(size_t)y * width], c.plane.data() + (size_t)y * c.bw * 8, width);
-                return IK_OK;
-            }
-            if (adobe && adobe_transform == 0)
-                return fail(IK_ERR_UNSUPPORTED, "JPEG in RGB colour space (Adobe transform 0) is not supported");
-            std::vector<uint8_t> Y, Cb, Cr;
-            upsample(comps[0], hmax, vmax, width, height, Y);
-            upsample(comps[1], hmax, vmax, width, height, Cb);
-            upsample(comps[2], hmax, vmax, width, height, Cr);
-            static const YccTables T;
-            C = 3;
-            px.resize((size_t)width * height * 3);
-            for (size_t i = 0; i < (size_t)width * height; ++i) {
-                const int y = Y[i], cb = Cb[i], cr = Cr[i];
-                px[3 * i] = clamp255(y + T.cr_r[cr]);
-                px[3 * i + 1] = clamp255(y + (int)((T.cb_g[cb] + T.cr_g[cr]) >> 16));
-                px[3 * i + 2] = clamp255(y + T.cb_b[cb]);
-            }
-            return IK_OK;
-        }
-        p += len;
+int decode_jpeg_device(const uint8_t* bytes, size_t n, ik_image** out) {
+    Decoder d;
+    d.b = bytes;
+    d.end = bytes + n;
+    int st = d.parse();
+    if (st) return st;
+    const int nc = (int)d.comps.size();
+    int colorspace = nc == 1 ? 0 : 1;  // gray / YCbCr
+    if (nc == 3 && d.adobe && d.adobe_transform == 0) colorspace = 2;  // Adobe RGB-coded
+    if (nc == 3 && !d.adobe && d.comps[0].id == 'R' && d.comps[1].id == 'G' && d.comps[2].id == 'B') colorspace = 2;
+
+    JpegGeom g{};
+    g.ncomp = nc;
+    g.W = d.width;
+    g.H = d.height;
+    g.hmax = d.hmax;
+    g.vmax = d.vmax;
+    g.colorspace = colorspace;
+    size_t plane_bytes = 0;
+    for (int i = 0; i < nc; ++i) {
+        const Component& c = d.comps[i];
+        g.h[i] = c.h; g.v[i] = c.v; g.bw[i] = c.bw; g.bh[i] = c.bh; g.dw[i] = c.dw; g.dh[i] = c.dh;
+        g.blk0[i] = (long long)c.blk0;
+        g.plane0[i] = (long long)plane_bytes;
+        plane_bytes += (size_t)c.bw * 8 * c.bh * 8;
     }
+    g.nblocks = (long long)(d.coef.size() / 64);
+
+    // one upload: [qtables 4x64 u16 per component][coefficients][planes (device only)]
+    const size_t qbytes = 256 * sizeof(uint16_t);
+    const size_t cbytes = d.coef.size() * sizeof(int16_t);
+    std::vector<uint16_t> q(256, 0);
+    for (int i = 0; i < nc; ++i) std::memcpy(&q[i * 64], d.qt[d.comps[i].tq], 64 * sizeof(uint16_t));
+    ik_image* img = nullptr;
+    st = alloc_image((uint32_t)d.width, (uint32_t)d.height, nc == 1 ? 1u : 3u, &img);
+    if (st) return st;
+    uint8_t* dev = scratch(qbytes + cbytes + plane_bytes + 256);
+    if (!dev) { ik_image_free(img); return fail(IK_ERR_DEVICE, "cannot allocate device scratch"); }
+    hipStream_t s = thread_stream();
+    st = copy_h2d_2d(dev, qbytes, reinterpret_cast<const uint8_t*>(q.data()), qbytes, qbytes, 1, s);
+    if (!st && cbytes)
+        st = copy_h2d_2d(dev + qbytes, cbytes, reinterpret_cast<const uint8_t*>(d.coef.data()), cbytes, cbytes, 1, s);
+    if (st) { ik_image_free(img); return st; }
+    g.qt = reinterpret_cast<const uint16_t*>(dev);
+    g.coef = reinterpret_cast<const int16_t*>(dev + qbytes);
+    g.planes = dev + qbytes + cbytes;
+    hipError_t e = launch_jpeg_reconstruct(g, img->d, img->pitch, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) { ik_image_free(img); return hip_fail(e, "jpeg reconstruct"); }
+    *out = img;
+    return IK_OK;
 }
 
 }  // namespace ik

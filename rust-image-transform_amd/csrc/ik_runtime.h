@@ -55,8 +55,11 @@ enum class Sniffed { Png, Jpeg, Gif, WebP, Tiff, Bmp, Ico, Hdr, Avif, OpenExr, Q
 Sniffed guess_format(const uint8_t* b, size_t n);
 const char* format_name(Sniffed f);
 int decode_png(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& c, std::vector<uint8_t>& px);
-int decode_jpeg(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& c, std::vector<uint8_t>& px);
 int decode_webp(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& c, std::vector<uint8_t>& px);
+
+// JPEG: host entropy decode + GPU reconstruction straight into a new device image
+// (ik_jpeg_decode.cpp + ik_jpeg.hip)
+int decode_jpeg_device(const uint8_t* b, size_t n, ik_image** out);
 
 // device-side stage helpers used by ik_encode and the pipeline
 int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, size_t pitch,

@@ -13,7 +13,7 @@ import zlib
 
 import numpy as np
 import pytest
-from PIL import Image
+from PIL import Image, ImageFile
 
 import ikutil
 from imagekit import ImageFormat, TransformError, decode_image
@@ -22,6 +22,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _jpeg(img, **kw):
+    ImageFile.MAXBLOCK = max(ImageFile.MAXBLOCK, 1 << 24)  # progressive noise needs a big buffer
     buf = io.BytesIO()
     Image.fromarray(img).save(buf, format="JPEG", **kw)
     return buf.getvalue()
@@ -49,10 +50,43 @@ def test_jpeg_gray_and_restart_markers(ik):
     np.testing.assert_array_equal(img.to_array(), np.asarray(Image.open(io.BytesIO(b))))
 
 
-def test_jpeg_progressive_is_reported(ik):
-    b = _jpeg(ikutil.synth(64, 64, 3, seed=2), quality=80, progressive=True)
-    with pytest.raises(TransformError, match="progressive"):
-        decode_image(b)
+@pytest.mark.parametrize("wh", [(64, 64), (1, 1), (37, 19), (641, 479)])
+@pytest.mark.parametrize("sub", [0, 2])
+@pytest.mark.parametrize("q", [30, 95])
+def test_jpeg_progressive_matches_libjpeg_turbo(ik, wh, sub, q):
+    # SOF2: DC first + refine, spectral-selection AC first, successive-approximation
+    # AC refine with EOB runs (libjpeg's default progression script)
+    w, h = wh
+    b = _jpeg(ikutil.synth(w, h, 3, seed=w * h + q, pattern="N" if q == 95 else "S"), quality=q,
+              subsampling=sub, progressive=True)
+    assert b"\xff\xc2" in b
+    img, fmt = decode_image(b)
+    assert fmt is ImageFormat.jpeg
+    np.testing.assert_array_equal(img.to_array(), np.asarray(Image.open(io.BytesIO(b))))
+
+
+def test_jpeg_progressive_gray_and_restarts(ik):
+    g = ikutil.synth(129, 70, 1, seed=5)[..., 0]
+    b = _jpeg(g, quality=75, progressive=True)
+    img, _ = decode_image(b)
+    np.testing.assert_array_equal(img.to_array()[..., 0], np.asarray(Image.open(io.BytesIO(b))))
+    b = _jpeg(ikutil.synth(200, 150, 3, seed=6), quality=85, subsampling=1, progressive=True,
+              restart_marker_blocks=3)
+    assert b"\xff\xdd" in b
+    img, _ = decode_image(b)
+    np.testing.assert_array_equal(img.to_array(), np.asarray(Image.open(io.BytesIO(b))))
+
+
+def test_jpeg_truncated_progressive_is_an_error_or_partial(ik):
+    # a stream cut inside its entropy data decodes like libjpeg (missing bits read as
+    # zeros) or fails with the reference's error string, never crashes
+    b = _jpeg(ikutil.synth(96, 96, 3, seed=7), quality=80, progressive=True)
+    for cut in (len(b) // 2, len(b) - 3):
+        try:
+            img, _ = decode_image(b[:cut])
+            assert img.dimensions() == (96, 96)
+        except TransformError as e:
+            assert "Jpeg" in str(e) or "jpeg" in str(e)
 
 
 # ---- PNG writer for the test (all filter types, Adam7, any colour type) ------

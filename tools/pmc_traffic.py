@@ -30,7 +30,8 @@ def main():
     fetch = fetch_kb * 1024.0 * calib
     write = write_kb * 1024.0
     algo = B * (4 * S * S + 4 * O * O)
-    out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_resize.json")
+    out_path = os.environ.get("IK_PMC_OUT") or os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_resize.json")
     d = json.load(open(out_path)) if os.path.exists(out_path) else {}
     d[key] = {
         "hbm_bytes_per_launch": int(fetch + write),
