@@ -14,7 +14,17 @@
 // order, the four standard DHT tables, one scan, BitWriter with 0xFF stuffing
 // and the pad_byte() = write_bits(0x7F, 7) tail.  The quantised coefficients come
 // from the GPU (k_jpeg_coeffs).
+//
+// AVIF: the reference uses image's AvifEncoder (ravif 0.11.20 -> rav1e 0.7.1,
+// speed 4, quality q; Cargo.lock:1796, 1761).  rav1e is not available here, so
+// the AV1 coding is libavif 1.x with its aom encoder (the copy bundled with the
+// image's Pillow, or a system libavif.so.16), fed BT.601 full-range 4:4:4 planes
+// (+ alpha when not opaque) from the GPU (k_avif_yuv444), speed 4, quality q.
+// Output bytes differ from rav1e's; parity is a decoded-PSNR bound
+// (tests/test_gpu_encode.py).  The avifImage / avifEncoder field offsets are those
+// of libavif 1.x and are checked against the library's defaults before use.
 #include <dlfcn.h>
+#include <glob.h>
 
 #include <cstring>
 #include <mutex>
@@ -296,6 +306,133 @@ void jpeg_write(const int16_t* coef, int w, int h, const uint8_t qt[128], std::v
     }
     b.put(0x7F, 7);  // pad_byte(); leftover bits (< 8) are dropped, as in BitWriter
     out.push_back(0xFF); out.push_back(0xD9);
+}
+
+// ---- AVIF through libavif (dlopen) ---------------------------------------------
+namespace {
+
+struct AvifApi {
+    void* lib = nullptr;
+    void* (*image_create)(uint32_t, uint32_t, uint32_t, int) = nullptr;
+    int (*image_alloc)(void*, int) = nullptr;
+    void (*image_destroy)(void*) = nullptr;
+    void* (*encoder_create)() = nullptr;
+    void (*encoder_destroy)(void*) = nullptr;
+    int (*encoder_write)(void*, const void*, void*) = nullptr;
+    void (*rwdata_free)(void*) = nullptr;
+    bool ok = false;
+    std::string err;
+};
+
+// libavif 1.x layouts (include/avif/avif.h)
+constexpr size_t kImgRange = 16, kImgPlanes = 24, kImgRowBytes = 48, kImgAlpha = 64, kImgAlphaRowBytes = 72;
+constexpr size_t kImgCicp = 104;  // colorPrimaries, transferCharacteristics, matrixCoefficients (u16 each)
+constexpr size_t kEncMaxThreads = 4, kEncSpeed = 8, kEncQuality = 32, kEncQualityAlpha = 36;
+constexpr int kYuv444 = 1, kPlanesYuv = 1, kPlanesAll = 0xff;
+
+const AvifApi& avif_api() {
+    static AvifApi api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        std::vector<std::string> cands;
+        if (const char* e = getenv("IK_LIBAVIF")) cands.push_back(e);
+        cands.push_back("libavif.so.16");
+        for (const char* pat : {"/usr/local/lib/python3*/dist-packages/pillow.libs/libavif-*.so*",
+                                "/usr/lib/python3*/dist-packages/pillow.libs/libavif-*.so*",
+                                "/usr/local/lib/python3*/site-packages/pillow.libs/libavif-*.so*"}) {
+            glob_t g{};
+            if (glob(pat, 0, nullptr, &g) == 0)
+                for (size_t i = 0; i < g.gl_pathc; ++i) cands.push_back(g.gl_pathv[i]);
+            globfree(&g);
+        }
+        for (const auto& c : cands)
+            if ((api.lib = dlopen(c.c_str(), RTLD_NOW | RTLD_LOCAL))) break;
+        if (!api.lib) { api.err = "libavif (with an AV1 encoder) not found"; return; }
+        api.image_create = (void* (*)(uint32_t, uint32_t, uint32_t, int))dlsym(api.lib, "avifImageCreate");
+        api.image_alloc = (int (*)(void*, int))dlsym(api.lib, "avifImageAllocatePlanes");
+        api.image_destroy = (void (*)(void*))dlsym(api.lib, "avifImageDestroy");
+        api.encoder_create = (void* (*)())dlsym(api.lib, "avifEncoderCreate");
+        api.encoder_destroy = (void (*)(void*))dlsym(api.lib, "avifEncoderDestroy");
+        api.encoder_write = (int (*)(void*, const void*, void*))dlsym(api.lib, "avifEncoderWrite");
+        api.rwdata_free = (void (*)(void*))dlsym(api.lib, "avifRWDataFree");
+        auto version = (const char* (*)())dlsym(api.lib, "avifVersion");
+        if (!api.image_create || !api.image_alloc || !api.image_destroy || !api.encoder_create ||
+            !api.encoder_destroy || !api.encoder_write || !api.rwdata_free || !version || version()[0] != '1') {
+            api.err = "libavif 1.x encoder API not found";
+            return;
+        }
+        // layout check against the documented defaults of a fresh image / encoder
+        void* img = api.image_create(291, 69, 8, kYuv444);
+        void* enc = api.encoder_create();
+        bool ok = img && enc;
+        if (ok) {
+            uint32_t whd[3]; int fmt_range[2]; uint16_t cicp[3]; int e[4];
+            std::memcpy(whd, img, 12);
+            std::memcpy(fmt_range, (char*)img + 12, 8);
+            std::memcpy(cicp, (char*)img + kImgCicp, 6);
+            std::memcpy(e, enc, 16);
+            ok = whd[0] == 291 && whd[1] == 69 && whd[2] == 8 && fmt_range[0] == kYuv444 && fmt_range[1] == 1 &&
+                 cicp[0] == 2 && cicp[1] == 2 && cicp[2] == 2 && e[1] == 1 && e[2] == -1;
+            int qa[2];
+            std::memcpy(qa, (char*)enc + kEncQuality, 8);
+            ok = ok && qa[0] == -1 && qa[1] == -1;
+        }
+        if (img) api.image_destroy(img);
+        if (enc) api.encoder_destroy(enc);
+        if (!ok) { api.err = "unexpected libavif struct layout"; return; }
+        api.ok = true;
+    });
+    return api;
+}
+
+}  // namespace
+
+int avif_encode_yuv444(const uint8_t* planes, bool has_alpha, int w, int h, int quality, int speed,
+                       std::vector<uint8_t>& out) {
+    const AvifApi& api = avif_api();
+    if (!api.ok) return fail(IK_ERR_UNSUPPORTED, "AVIF encoding unavailable: %s", api.err.c_str());
+    void* img = api.image_create((uint32_t)w, (uint32_t)h, 8, kYuv444);
+    void* enc = api.encoder_create();
+    auto cleanup = [&] { if (img) api.image_destroy(img); if (enc) api.encoder_destroy(enc); };
+    if (!img || !enc) { cleanup(); return fail(IK_ERR_NOMEM, "avif: out of memory"); }
+    const int full = 1;
+    const uint16_t cicp[3] = {1, 13, 6};  // BT.709 primaries, sRGB transfer, BT.601 matrix
+    std::memcpy((char*)img + kImgRange, &full, 4);
+    std::memcpy((char*)img + kImgCicp, cicp, 6);
+    if (api.image_alloc(img, has_alpha ? kPlanesAll : kPlanesYuv) != 0) {
+        cleanup();
+        return fail(IK_ERR_NOMEM, "avif: cannot allocate planes");
+    }
+    const size_t n = (size_t)w * h;
+    for (int pl = 0; pl < 4; ++pl) {
+        if (pl == 3 && !has_alpha) break;
+        uint8_t* dst;
+        uint32_t rb;
+        if (pl < 3) {
+            std::memcpy(&dst, (char*)img + kImgPlanes + 8 * pl, 8);
+            std::memcpy(&rb, (char*)img + kImgRowBytes + 4 * pl, 4);
+        } else {
+            std::memcpy(&dst, (char*)img + kImgAlpha, 8);
+            std::memcpy(&rb, (char*)img + kImgAlphaRowBytes, 4);
+        }
+        if (!dst || rb < (uint32_t)w) { cleanup(); return fail(IK_ERR_TRANSFORM, "avif: bad plane layout"); }
+        for (int y = 0; y < h; ++y) std::memcpy(dst + (size_t)y * rb, planes + pl * n + (size_t)y * w, (size_t)w);
+    }
+    const int threads = 1, q2[2] = {quality, quality};
+    std::memcpy((char*)enc + kEncMaxThreads, &threads, 4);
+    std::memcpy((char*)enc + kEncSpeed, &speed, 4);
+    std::memcpy((char*)enc + kEncQuality, q2, 8);
+    struct { uint8_t* data; size_t size; } rw{nullptr, 0};
+    const int r = api.encoder_write(enc, img, &rw);
+    if (r != 0 || !rw.data) {
+        if (rw.data) api.rwdata_free(&rw);
+        cleanup();
+        return fail(IK_ERR_TRANSFORM, "Encoding error: avifEncoderWrite failed (%d)", r);
+    }
+    out.assign(rw.data, rw.data + rw.size);
+    api.rwdata_free(&rw);
+    cleanup();
+    return IK_OK;
 }
 
 }  // namespace ik

@@ -171,7 +171,8 @@ const DeviceConsts* device_consts(int device) {
 // Run the device front end of encode_image and hand its output to the host
 // entropy stage.  WebP: to_rgb8 + RGB->YUV420 on the GPU, libwebp VP8 coding of
 // those planes on the host.  JPEG: to_rgb8 + YCbCr + FDCT + quantise on the GPU,
-// baseline Huffman coding on the host.
+// baseline Huffman coding on the host.  AVIF: to_rgba8 + YCbCr 4:4:4 on the GPU,
+// AV1 coding by libavif/aom on the host.
 int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, size_t pitch,
                         int fmt, int quality, std::vector<uint8_t>& out) {
     const int q = quality < 1 ? 1 : (quality > 100 ? 100 : quality);
@@ -214,9 +215,24 @@ int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, 
         jpeg_write(coef.data(), (int)w, (int)h, qt, out);
         return IK_OK;
     }
-    if (fmt == IK_FORMAT_AVIF)
-        return fail(IK_ERR_UNSUPPORTED,
-                    "AVIF encoding (ravif/rav1e in the reference) is not implemented in this build");
+    if (fmt == IK_FORMAT_AVIF) {
+        // image 0.25.8 AvifEncoder::new_with_speed_quality(out, 4, q) (src/transform.rs:140-145)
+        const size_t n = (size_t)w * h;
+        uint8_t* dp = scratch(4 * n + 256);
+        if (!dp) return fail(IK_ERR_DEVICE, "cannot allocate device scratch");
+        int* dflag = reinterpret_cast<int*>(dp + 4 * n + 128 - ((4 * n) & 127));
+        const int one = 1;
+        int rc = copy_h2d_2d(reinterpret_cast<uint8_t*>(dflag), 4, reinterpret_cast<const uint8_t*>(&one), 4, 4, 1, s);
+        if (rc) return rc;
+        hipError_t e = launch_avif_yuv444(dev, (int)w, (int)h, (int)c, pitch, dp, dflag, s);
+        if (e != hipSuccess) return hip_fail(e, "avif yuv444");
+        std::vector<uint8_t> planes(4 * n);
+        int opaque = 1;
+        rc = copy_d2h_2d(planes.data(), 4 * n, dp, 4 * n, 4 * n, 1, s);
+        if (!rc) rc = copy_d2h_2d(reinterpret_cast<uint8_t*>(&opaque), 4, reinterpret_cast<const uint8_t*>(dflag), 4, 4, 1, s);
+        if (rc) return rc;
+        return avif_encode_yuv444(planes.data(), !opaque, (int)w, (int)h, q, 4, out);
+    }
     return fail(IK_ERR_INVALID, "unknown ImageFormat %d", fmt);
 }
 

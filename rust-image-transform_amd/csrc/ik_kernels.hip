@@ -459,6 +459,38 @@ hipError_t launch_webp_yuv420(const uint8_t* src, int w, int h, int C, size_t pi
 }
 
 // ---------------------------------------------------------------------------
+// AVIF front end (image 0.25.8 AvifEncoder: to_rgba8 -> ravif RGB->YCbCr): BT.601
+// full-range 4:4:4 planes plus the alpha plane; `opaque` drops to 0 when any
+// alpha < 255 (ravif then codes an alpha plane).  One lane per pixel.
+__global__ __launch_bounds__(kThreads) void k_avif_yuv444(const uint8_t* __restrict__ src, int w, int h, int C,
+                                                          size_t pitch, uint8_t* __restrict__ planes,
+                                                          int* __restrict__ opaque) {
+    const int x = blockIdx.x * kThreads + threadIdx.x, y = blockIdx.y;
+    if (x >= w) return;
+    const uint8_t* p = src + (size_t)y * pitch + (size_t)x * C;
+    int r, g, b, al = 255;
+    if (C >= 3) { r = p[0]; g = p[1]; b = p[2]; if (C == 4) al = p[3]; }
+    else { r = g = b = p[0]; if (C == 2) al = p[1]; }
+    const float Y = 0.299f * r + 0.587f * g + 0.114f * b;
+    const float U = (b - Y) * (0.5f / 0.886f) + 128.0f;
+    const float V = (r - Y) * (0.5f / 0.701f) + 128.0f;
+    auto q8 = [](float v) -> uint8_t { v = floorf(v + 0.5f); return (uint8_t)(v < 0.f ? 0.f : (v > 255.f ? 255.f : v)); };
+    const size_t n = (size_t)w * h, i = (size_t)y * w + x;
+    planes[i] = q8(Y);
+    planes[n + i] = q8(U);
+    planes[2 * n + i] = q8(V);
+    planes[3 * n + i] = (uint8_t)al;
+    if (al != 255) atomicAnd(opaque, 0);
+}
+
+hipError_t launch_avif_yuv444(const uint8_t* src, int w, int h, int C, size_t pitch, uint8_t* planes,
+                              int* opaque, hipStream_t s) {
+    hipLaunchKernelGGL(k_avif_yuv444, dim3((w + kThreads - 1) / kThreads, h), dim3(kThreads), 0, s, src, w, h, C,
+                       pitch, planes, opaque);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // JPEG front end (image 0.25.8 JpegEncoder::encode_rgb, 4:4:4): per 8x8 block
 // and component: pixel_at_or_near -> rgb_to_ycbcr (f32, `as u8`) -> fdct (libjpeg
 // 9a islow, integer) -> ((c / 8) as f32 / q).round().  Workgroup = 8 MCUs x 3

@@ -48,6 +48,8 @@ void webp_gamma_tables(uint16_t g2l[256], int l2g[33]);
 int webp_encode_yuv420(const uint8_t* y, const uint8_t* u, const uint8_t* v, int w, int h,
                        float quality, std::vector<uint8_t>& out);
 void jpeg_quant_tables(int quality, uint8_t qt[128]);
+int avif_encode_yuv444(const uint8_t* planes /* Y, U, V, A */, bool has_alpha, int w, int h, int quality,
+                       int speed, std::vector<uint8_t>& out);
 void jpeg_write(const int16_t* coef, int w, int h, const uint8_t qt[128], std::vector<uint8_t>& out);
 
 // host decoders (ik_decode.cpp): tightly packed 8-bit pixels

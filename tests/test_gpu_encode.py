@@ -4,7 +4,9 @@ WebP: the device YUV420 planes must equal libwebp 1.2.2's own import (and the
 oracle restatement); the WebP bytes must equal WebPEncodeRGB(to_rgb8(img), q)
 byte for byte -- i.e. webp 0.3.1 Encoder::from_rgb(..).encode(q) on the same
 libwebp.  JPEG: device coefficients and bytes must equal the image 0.25.8
-JpegEncoder restatement byte for byte."""
+JpegEncoder restatement byte for byte.  AVIF: rav1e (the reference's AV1 encoder)
+is absent, the build codes AV1 with libavif/aom: parity unpinned, checked as a
+decoded-PSNR bound (Pillow/dav1d), dimensions, alpha handling and q-monotone size."""
 import ctypes
 import io
 
@@ -91,3 +93,41 @@ def test_quality_clamp(ik, oracle):
     assert encode_image(d, ImageFormat.jpeg, 0) == oracle.jpeg_encode_rgb(img, 1)
     assert encode_image(d, ImageFormat.jpeg, 101) == oracle.jpeg_encode_rgb(img, 100)
     assert encode_image(d, ImageFormat.webp, 0) == oracle.webp_encode_rgb(img, 1.0)
+
+
+# ---- AVIF (image AvifEncoder -> ravif/rav1e in the reference; libavif/aom here) ----
+def _psnr(a, b):
+    mse = np.mean((a.astype(np.float64) - b.astype(np.float64)) ** 2)
+    return 99.0 if mse == 0 else 10 * np.log10(255.0 ** 2 / mse)
+
+
+@pytest.mark.parametrize("wh", [(1, 1), (17, 9), (320, 240), (512, 512)])
+def test_avif_encode_decodes_close_to_source(ik, wh):
+    from PIL import Image
+    w, h = wh
+    src = ikutil.synth(w, h, 4, seed=w + h, pattern="S")
+    b = encode_image(DynamicImage.from_array(src), ImageFormat.avif, 80)
+    assert b[4:12] == b"ftypavif"
+    im = Image.open(io.BytesIO(b))
+    assert im.size == (w, h) and im.mode == "RGB"  # opaque source: no alpha plane
+    if w * h >= 64:
+        assert _psnr(np.asarray(im), src[..., :3]) > 30.0
+
+
+def test_avif_alpha_and_gray(ik):
+    from PIL import Image
+    src = ikutil.synth(96, 64, 4, seed=3, pattern="S").copy()
+    src[..., 3] = np.linspace(0, 255, 96, dtype=np.uint8)[None, :]
+    im = Image.open(io.BytesIO(encode_image(DynamicImage.from_array(src), ImageFormat.avif, 90)))
+    assert im.mode == "RGBA"
+    a = np.asarray(im)
+    assert np.abs(a[..., 3].astype(int) - src[..., 3]).max() <= 8
+    g = ikutil.synth(40, 30, 1, seed=4, pattern="S")
+    im = Image.open(io.BytesIO(encode_image(DynamicImage.from_array(g), ImageFormat.avif, 90)))
+    rgb = np.asarray(im.convert("RGB")).astype(int)
+    assert np.abs(rgb - g.repeat(3, axis=2)).mean() < 3.0
+
+
+def test_avif_quality_orders_size(ik):
+    img = DynamicImage.from_array(ikutil.synth(256, 256, 3, seed=9, pattern="N"))
+    assert len(encode_image(img, ImageFormat.avif, 10)) < len(encode_image(img, ImageFormat.avif, 95))

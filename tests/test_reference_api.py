@@ -1,8 +1,9 @@
 """GPU: the reference's own hot-path tests (tests/transform.rs, 20 #[test]s) run
 against the MI355X implementation through the Python mirror of imagekit::transform.
 Inputs are built the way the reference builds them (DynamicImage::new_rgb8 =
-all-zero pixels; PNG fixtures from a blank RGBA image).  AVIF encoding is not
-implemented in this build, so the AVIF assertions are xfail."""
+all-zero pixels; PNG fixtures from a blank RGBA image).  AVIF goes through
+libavif/aom instead of ravif/rav1e, so AVIF bytes differ from
+the reference's; the reference's AVIF assertions (non-empty output) hold."""
 import io
 
 import pytest
@@ -79,7 +80,6 @@ def test_all_format_encodings(ik):                                # :137-154 (jp
     assert len(encode_image(img, ImageFormat.webp, 80)) > 0
 
 
-@pytest.mark.xfail(raises=TransformError, strict=True, reason="AVIF encoder (ravif/rav1e) not implemented")
 def test_all_format_encodings_avif(ik):                           # :151-153
     assert len(encode_image(rgb8(100, 100), ImageFormat.avif, 80)) > 0
 
@@ -122,7 +122,6 @@ def test_full_pipeline_webp(ik):                                  # :238-257
     assert decoded.dimensions() == (640, 360) and fmt is ImageFormat.webp
 
 
-@pytest.mark.xfail(raises=TransformError, strict=True, reason="AVIF encoder (ravif/rav1e) not implemented")
 def test_full_pipeline_avif(ik):                                  # :259-269
     resized = resize_image(rgb8(800, 600), 400, None)
     assert resized.dimensions() == (400, 300)
