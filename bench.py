@@ -38,6 +38,7 @@ sys.path[:0] = [os.path.join(ROOT, "rust-image-transform_amd"), os.path.join(ROO
 METRIC = "transform MPix/s (decode+resize+encode) 4096²→512² WebP q80; 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FILTERS = {"nearest": 0, "triangle": 1, "catmullrom": 2, "gaussian": 3, "lanczos3": 4}
+ENCODERS = {"libwebp": 0, "gpu": 1}
 
 
 def parse():
@@ -54,6 +55,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample wall-time budget (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--device-only", action="store_true", help="time resize+colour kernels only")
+    ap.add_argument("--webp-encoder", default="libwebp", choices=["libwebp", "gpu"],
+                    help="libwebp: host VP8 coder, bytes identical to the reference; gpu: gfx950 VP8 encoder")
+    ap.add_argument("--no-alt-encoder", action="store_true", help="skip timing the other WebP encoder")
     return ap.parse_args()
 
 
@@ -157,6 +161,8 @@ def main():
     pipe = ctypes.c_void_p()
     if lib.ik_pipeline_create(S, S, 4, O, O, f, 1, args.quality, B, args.threads, ctypes.byref(pipe)):
         raise SystemExit(f"pipeline: {_lib.last_error()}")
+    if lib.ik_pipeline_set_webp_encoder(pipe, ENCODERS[args.webp_encoder]):
+        raise SystemExit(f"webp encoder: {_lib.last_error()}")
     out_cap = B * O * O * 4 + (1 << 20)
     out = np.empty(out_cap, np.uint8)
     sizes = (ctypes.c_size_t * B)()
@@ -169,7 +175,8 @@ def main():
                                      out.ctypes.data, out_cap, sizes)
         if rc:
             raise SystemExit(f"pipeline run: {_lib.last_error()}")
-        return lib.ik_pipeline_kernel_ms(pipe, 0), lib.ik_pipeline_kernel_ms(pipe, 1)
+        return (lib.ik_pipeline_kernel_ms(pipe, 0), lib.ik_pipeline_kernel_ms(pipe, 1),
+                lib.ik_pipeline_kernel_ms(pipe, 2))
 
     for _ in range(args.warmup):
         step()
@@ -193,6 +200,25 @@ def main():
         assert bytes(out[:4]) == b"RIFF" and all(s > 0 for s in sizes)
     resize_ms = float(np.mean([k[0] for k in kms]))
     colour_ms = float(np.mean([k[1] for k in kms]))
+    vp8_ms = float(np.mean([k[2] for k in kms]))
+    out_bytes = int(sum(sizes))
+
+    # the other WebP encoder end to end on the same batch (a few steps)
+    alt_enc = {}
+    if not args.device_only and not args.no_alt_encoder:
+        other = "gpu" if args.webp_encoder == "libwebp" else "libwebp"
+        if lib.ik_pipeline_set_webp_encoder(pipe, ENCODERS[other]) == 0:
+            step()
+            barrier()
+            t1 = time.perf_counter()
+            ak = [step() for _ in range(3)]
+            barrier()
+            te = reduce_max(time.perf_counter() - t1, dist, f"cuda:{local}")
+            alt_enc = {"encoder": other, "value": round(aggregate_mpix(world, B, 3, S, te), 2),
+                       "ms_per_step": round(te / 3 * 1e3, 3),
+                       "vp8_kernel_ms": round(float(np.mean([k[2] for k in ak])), 4),
+                       "output_bytes_per_step": int(sum(sizes))}
+            lib.ik_pipeline_set_webp_encoder(pipe, ENCODERS[args.webp_encoder])
     bytes_per_img = 4 * S * S + 4 * O * O
     achieved = B * bytes_per_img / (resize_ms * 1e-3) / 1e9
     value = aggregate_mpix(world, B, args.steps, S, elapsed)
@@ -247,6 +273,7 @@ def main():
                             f"({args.filter}) -> encode_image webp q{args.quality}; bytes to host",
                 "batch_per_gpu": B, "filter": args.filter, "format": "webp",
                 "quality": args.quality, "host_threads_per_gpu": args.threads,
+                "webp_encoder": args.webp_encoder,
                 "device_only": bool(args.device_only), "parallelism": f"images sharded, {world} rank(s)",
             },
             "roofline": {
@@ -261,6 +288,9 @@ def main():
                 "bytes_per_launch": B * bytes_per_img,
             },
             "colour_kernel_ms": round(colour_ms, 4),
+            "vp8_kernel_ms": round(vp8_ms, 4),
+            "output_bytes_per_step": out_bytes,
+            "alt_webp_encoder": alt_enc,
             "alt_filter_kernel": alt,
             "cpu_baseline": cpu,
         }

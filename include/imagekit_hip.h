@@ -84,6 +84,17 @@ int ik_resize_exact(const ik_image *img, uint32_t nw, uint32_t nh, int filter, i
  * *out is allocated by the library; release with ik_buf_free. */
 int ik_encode(const ik_image *img, int fmt, int quality, uint8_t **out, size_t *out_len);
 
+/* WebP encoder behind encode_image (src/transform.rs:129-137).
+ * IK_WEBP_LIBWEBP (default): libwebp's VP8 coder on the host over device-made
+ *   YUV420 planes -- bytes identical to the reference's webp 0.3.1 / libwebp.
+ * IK_WEBP_GPU: the gfx950 VP8 macroblock encoder (RD mode search, transforms,
+ *   quantisation on the GPU; boolean coding on the host) -- a different encoder
+ *   with libwebp-level size and PSNR, not byte-identical to libwebp.
+ * The process default comes from IK_WEBP_ENCODER=gpu|libwebp when first used. */
+typedef enum { IK_WEBP_LIBWEBP = 0, IK_WEBP_GPU = 1 } ik_webp_encoder;
+int ik_set_webp_encoder(int encoder); /* process-wide, for ik_encode / ik_transform */
+int ik_get_webp_encoder(void);
+
 /* ---- fused / batched entry points (pixels stay in HBM) ----------------- */
 /* decode -> resize_image -> encode_image in one call (handler src/lib.rs:175-191) */
 int ik_transform(const uint8_t *bytes, size_t len, int64_t w, int64_t h, int fmt, int quality,
@@ -100,11 +111,13 @@ int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t
 int ik_pipeline_run(ik_pipeline *p, const uint8_t *dev_src, size_t src_pitch,
                     size_t src_image_stride, uint32_t n, uint8_t *out, size_t out_cap,
                     size_t *out_sizes);
-/* device-only part (resize + colour convert/FDCT) for n images, no host stage */
+/* WebP encoder of this pipeline (IK_WEBP_*; default: the process default) */
+int ik_pipeline_set_webp_encoder(ik_pipeline *p, int encoder);
+/* device-only part (resize + colour convert/FDCT [+ GPU VP8]) for n images, no host stage */
 int ik_pipeline_run_device(ik_pipeline *p, const uint8_t *dev_src, size_t src_pitch,
                            size_t src_image_stride, uint32_t n);
-/* average device time (ms) per launch of kernel `which` (0 = resize, 1 = colour
- * convert) over the last run, from HIP events on the pipeline's stream */
+/* device time (ms) of stage `which` (0 = resize, 1 = colour convert, 2 = GPU VP8
+ * wavefront) in the last run, from HIP events on the pipeline's stream */
 double ik_pipeline_kernel_ms(const ik_pipeline *p, int which);
 /* resized pixels of image i of the last run (tightly packed nw*nh*C) */
 int ik_pipeline_fetch_resized(ik_pipeline *p, uint32_t i, uint8_t *dst, size_t cap);
@@ -119,6 +132,10 @@ int ik_resize_batch_device(const uint8_t *dev_src, uint32_t W, uint32_t H, uint3
  * dev_yuv receives the Y (w*h), U and V ((w+1)/2 * (h+1)/2) planes back to back */
 int ik_webp_yuv420_device(const uint8_t *dev_src, uint32_t w, uint32_t h, uint32_t C,
                           size_t pitch, uint8_t *dev_yuv, void *hip_stream);
+/* the GPU WebP encoder on device YUV420 planes (the layout ik_webp_yuv420_device
+ * writes); *out is allocated by the library (ik_buf_free) */
+int ik_webp_encode_gpu_device(const uint8_t *dev_yuv, uint32_t w, uint32_t h, int quality,
+                              uint8_t **out, size_t *out_len);
 /* the JPEG front end (to_rgb8 + RGB->YCbCr + FDCT + quantise) on the device:
  * int16 coefficients, MCU-major, Y/Cb/Cr, natural order */
 int ik_jpeg_coeffs_device(const uint8_t *dev_src, uint32_t w, uint32_t h, uint32_t C,

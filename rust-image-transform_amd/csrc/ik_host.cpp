@@ -190,6 +190,7 @@ int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, 
         hipError_t e = launch_webp_yuv420(dev, (int)w, (int)h, (int)c, pitch, 0, dyuv, 0, 1,
                                           dc->gamma_to_lin, dc->lin_to_gamma, s);
         if (e != hipSuccess) return hip_fail(e, "webp yuv420");
+        if (default_webp_encoder() == IK_WEBP_GPU) return webp_encode_gpu(dyuv, (int)w, (int)h, q, out);
         int rc = copy_d2h_2d(yuv.data(), bytes, dyuv, bytes, bytes, 1, s);
         if (rc) return rc;
         const uint8_t* Y = yuv.data();

@@ -102,8 +102,10 @@ struct ik_pipeline {
     uint8_t* d_qt = nullptr;
     uint8_t qt[128];
     float* d_tmp = nullptr;      // naive resize path only
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-    double ms[2] = {0, 0};
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    double ms[3] = {0, 0, 0};
+    int webp_enc = IK_WEBP_LIBWEBP;  // IK_WEBP_GPU: k_vp8_diag wavefront + host bitstream
+    ik::Vp8Work vp8;
     uint32_t last_n = 0;
     ik::Pool* pool = nullptr;
     std::vector<std::vector<uint8_t>> outs;
@@ -152,6 +154,21 @@ int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t
     p->pool = new Pool(threads - 1);  // the calling thread works too
     if (fmt == IK_FORMAT_WEBP && !device_consts(p->device)) return fail(IK_ERR_DEVICE, "cannot upload WebP tables");
     *out = p;
+    if (fmt == IK_FORMAT_WEBP && default_webp_encoder() == IK_WEBP_GPU)
+        return ik_pipeline_set_webp_encoder(p, IK_WEBP_GPU);
+    return IK_OK;
+}
+
+int ik_pipeline_set_webp_encoder(ik_pipeline* p, int encoder) {
+    if (!p) return fail(IK_ERR_INVALID, "null pipeline");
+    if (encoder != IK_WEBP_LIBWEBP && encoder != IK_WEBP_GPU) return fail(IK_ERR_INVALID, "bad WebP encoder %d", encoder);
+    if (p->fmt != IK_FORMAT_WEBP) return fail(IK_ERR_INVALID, "not a WebP pipeline");
+    IK_HIP(hipSetDevice(p->device));
+    if (encoder == IK_WEBP_GPU) {
+        if (p->nw > 16383 || p->nh > 16383) return fail(IK_ERR_TRANSFORM, "WebP dimensions exceed 16383");
+        if (int rc = p->vp8.reserve((int)p->nw, (int)p->nh, (int)p->max_batch)) return rc;
+    }
+    p->webp_enc = encoder;
     return IK_OK;
 }
 
@@ -180,12 +197,19 @@ int ik_pipeline_run_device(ik_pipeline* p, const uint8_t* dev_src, size_t src_pi
                                   p->stage_bytes / sizeof(int16_t), (int)n, p->stream));
     }
     IK_HIP(hipEventRecord(p->ev[2], p->stream));
-    IK_HIP(hipEventSynchronize(p->ev[2]));
-    float a = 0, b = 0;
+    const bool gpu_vp8 = p->fmt == IK_FORMAT_WEBP && p->webp_enc == IK_WEBP_GPU;
+    if (gpu_vp8) {
+        if (int rc = p->vp8.launch(p->d_stage, p->stage_bytes, (int)n, p->quality, p->stream)) return rc;
+    }
+    IK_HIP(hipEventRecord(p->ev[3], p->stream));
+    IK_HIP(hipEventSynchronize(p->ev[3]));
+    float a = 0, b = 0, c = 0;
     IK_HIP(hipEventElapsedTime(&a, p->ev[0], p->ev[1]));
     IK_HIP(hipEventElapsedTime(&b, p->ev[1], p->ev[2]));
+    IK_HIP(hipEventElapsedTime(&c, p->ev[2], p->ev[3]));
     p->ms[0] = a;
     p->ms[1] = b;
+    p->ms[2] = gpu_vp8 ? c : 0.0;
     p->last_n = n;
     return IK_OK;
 }
@@ -194,14 +218,21 @@ int ik_pipeline_run(ik_pipeline* p, const uint8_t* dev_src, size_t src_pitch, si
                     uint32_t n, uint8_t* out, size_t out_cap, size_t* out_sizes) {
     int st = ik_pipeline_run_device(p, dev_src, src_pitch, src_image_stride, n);
     if (st) return st;
-    IK_HIP(hipMemcpyAsync(p->h_stage, p->d_stage, p->stage_bytes * n, hipMemcpyDeviceToHost, p->stream));
+    const bool gpu_vp8 = p->fmt == IK_FORMAT_WEBP && p->webp_enc == IK_WEBP_GPU;
+    if (gpu_vp8) {
+        if (int rc = p->vp8.fetch((int)n, p->stream)) return rc;
+    } else {
+        IK_HIP(hipMemcpyAsync(p->h_stage, p->d_stage, p->stage_bytes * n, hipMemcpyDeviceToHost, p->stream));
+    }
     IK_HIP(hipStreamSynchronize(p->stream));
     p->outs.resize(n);
     p->status.assign(n, 0);
     std::vector<std::string> errs(n);
     p->pool->run((int)n, [&](int i) {
         const uint8_t* s = p->h_stage + p->stage_bytes * (size_t)i;
-        if (p->fmt == IK_FORMAT_WEBP) {
+        if (gpu_vp8) {
+            p->vp8.write(i, p->quality, p->outs[i]);
+        } else if (p->fmt == IK_FORMAT_WEBP) {
             const size_t ys = (size_t)p->nw * p->nh, uvs = (size_t)((p->nw + 1) / 2) * ((p->nh + 1) / 2);
             p->status[i] = webp_encode_yuv420(s, s + ys, s + ys + uvs, (int)p->nw, (int)p->nh,
                                               (float)p->quality, p->outs[i]);
@@ -228,7 +259,7 @@ int ik_pipeline_run(ik_pipeline* p, const uint8_t* dev_src, size_t src_pitch, si
 }
 
 double ik_pipeline_kernel_ms(const ik_pipeline* p, int which) {
-    if (!p || which < 0 || which > 1) return -1.0;
+    if (!p || which < 0 || which > 2) return -1.0;
     return p->ms[which];
 }
 
@@ -243,6 +274,7 @@ void ik_pipeline_destroy(ik_pipeline* p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
     delete p->pool;
+    p->vp8.release();
     if (p->d_resized) (void)hipFree(p->d_resized);
     if (p->d_stage) (void)hipFree(p->d_stage);
     if (p->h_stage) (void)hipHostFree(p->h_stage);

@@ -52,6 +52,26 @@ int avif_encode_yuv444(const uint8_t* planes /* Y, U, V, A */, bool has_alpha, i
                        int speed, std::vector<uint8_t>& out);
 void jpeg_write(const int16_t* coef, int w, int h, const uint8_t qt[128], std::vector<uint8_t>& out);
 
+// GPU WebP encoder (ik_webp_gpu.cpp + ik_vp8.hip): reusable device / pinned
+// buffers for n images of one geometry
+namespace vp8 { struct MBOut; }
+struct Vp8Work {
+    int w = 0, h = 0, cap_n = 0;
+    uint8_t* d_rec = nullptr;        // reconstruction planes (prediction context)
+    vp8::MBOut* d_mbs = nullptr;     // per-MB decisions + levels
+    uint8_t* d_nz = nullptr;         // per-MB outgoing non-zero contexts
+    vp8::MBOut* h_mbs = nullptr;     // pinned mirror of d_mbs
+    int reserve(int w, int h, int n);
+    void release();
+    size_t mb_count() const;
+    // the wavefront launches for n images (YUV420 planes yuv_stride apart), async on s
+    int launch(const uint8_t* d_yuv, size_t yuv_stride, int n, int quality, hipStream_t s);
+    int fetch(int n, hipStream_t s);  // async D2H of the MB records
+    void write(int i, int quality, std::vector<uint8_t>& out) const;  // bitstream of image i (host)
+};
+int default_webp_encoder();  // IK_WEBP_LIBWEBP unless ik_set_webp_encoder / IK_WEBP_ENCODER=gpu
+int webp_encode_gpu(const uint8_t* d_yuv, int w, int h, int quality, std::vector<uint8_t>& out);
+
 // host decoders (ik_decode.cpp): tightly packed 8-bit pixels
 enum class Sniffed { Png, Jpeg, Gif, WebP, Tiff, Bmp, Ico, Hdr, Avif, OpenExr, Qoi, Farbfeld, Pnm, Dds, Unknown };
 Sniffed guess_format(const uint8_t* b, size_t n);

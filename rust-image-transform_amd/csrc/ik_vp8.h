@@ -404,6 +404,39 @@ IK_HD void pred_nxn(int m, int N, const uint8_t* d, int mb_x, int mb_y, uint8_t*
         }
 }
 
+// One 4x4 block (bx, by) of the NxN prediction pred_nxn(m, N, ...) would write:
+// the same values, computed for that block only (the GPU kernel's lanes each own
+// one block of one mode).
+IK_HD void pred_blk(int m, int N, const uint8_t* d, int mb_x, int mb_y, int bx, int by, uint8_t* pr) {
+    if (m == DC_PRED) {
+        int s = 0, v;
+        const int sh = N == 16 ? 4 : 3;
+        if (mb_x > 0 && mb_y > 0) {
+            for (int i = 0; i < N; ++i) s += d[i - kBps] + d[-1 + i * kBps];
+            v = (s + N) >> (sh + 1);
+        } else if (mb_y > 0) {
+            for (int i = 0; i < N; ++i) s += d[i - kBps];
+            v = (s + (N >> 1)) >> sh;
+        } else if (mb_x > 0) {
+            for (int i = 0; i < N; ++i) s += d[-1 + i * kBps];
+            v = (s + (N >> 1)) >> sh;
+        } else {
+            v = 0x80;
+        }
+        for (int i = 0; i < 16; ++i) pr[i] = (uint8_t)v;
+        return;
+    }
+    const int x0 = bx * 4, y0 = by * 4;
+    for (int y = 0; y < 4; ++y)
+        for (int x = 0; x < 4; ++x) {
+            int v;
+            if (m == V_PRED) v = d[x0 + x - kBps];
+            else if (m == H_PRED) v = d[-1 + (y0 + y) * kBps];
+            else v = clip8(d[x0 + x - kBps] + d[-1 + (y0 + y) * kBps] - d[-1 - kBps]);
+            pr[y * 4 + x] = (uint8_t)v;
+        }
+}
+
 // ---- one macroblock, scalar (the reference encoder; the GPU kernel runs it per lane) ----
 struct MBOut {
     uint8_t ymode, uvmode, skip, pad;

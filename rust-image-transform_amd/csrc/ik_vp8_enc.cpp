@@ -216,6 +216,8 @@ int quality_to_qindex(float quality) {
     return q < 0 ? 0 : (q > 127 ? 127 : q);
 }
 
+QParams qparams_for_quality(float quality) { return make_qparams(quality_to_qindex(quality), -2); }
+
 void write_webp(int width, int height, const QParams& q, const MBOut* mbs, int filter_level,
                 std::vector<uint8_t>& out) {
     const int mb_w = (width + 15) >> 4, mb_h = (height + 15) >> 4;

@@ -14,6 +14,10 @@ namespace vp8 {
 // mid susceptibility): c = QualityToCompression(q/100), qindex = 127 * (1 - c)
 int quality_to_qindex(float quality);
 
+// the quantiser / lambda / filter parameters the encoder uses for `quality`
+// (chroma DC delta -4 * sns_strength / 100 = -2 at libwebp's default sns 50)
+QParams qparams_for_quality(float quality);
+
 // Bitstream for one frame of mb_w x mb_h macroblocks (raster order) with the
 // decisions in `mbs`.  `filter_level` < 0 uses q.filter_level.
 void write_webp(int width, int height, const QParams& q, const MBOut* mbs, int filter_level,

@@ -1,0 +1,32 @@
+// ik_vp8_gpu.h -- launcher of the GPU VP8 macroblock encoder (ik_vp8.hip).
+// Host code (ik_pipeline.cpp, ik_host.cpp) drives it; the bitstream is written on
+// the host from the MBOut records (ik_vp8_enc.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "ik_vp8.h"
+
+namespace ik {
+namespace vp8 {
+
+struct Vp8Args {
+    const uint8_t* yuv;  // per image: Y (w*h), U, V ((w+1)/2 * (h+1)/2), back to back
+    size_t yuv_stride;   // bytes between images
+    int w, h, mb_w, mb_h;
+    uint8_t* rec;        // per image: reconstruction Y (mb_w*16 x mb_h*16), U, V (mb_w*8 x mb_h*8)
+    size_t rec_stride;
+    MBOut* mbs;          // per image: mb_w*mb_h records, raster order
+    uint8_t* nz;         // per image: mb_w*mb_h x 18 outgoing non-zero contexts (top[9], left[9])
+    QParams q;
+};
+
+inline size_t vp8_rec_bytes(int w, int h) {
+    const size_t mw = (size_t)((w + 15) >> 4), mh = (size_t)((h + 15) >> 4);
+    return mw * 16 * mh * 16 + 2 * mw * 8 * mh * 8;
+}
+
+// the whole wavefront for n images: (mb_w-1) + 2*(mb_h-1) + 1 launches on stream s
+hipError_t launch_vp8_encode(const Vp8Args& a, int n, hipStream_t s);
+
+}  // namespace vp8
+}  // namespace ik

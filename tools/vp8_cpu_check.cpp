@@ -101,7 +101,7 @@ void encode_frame_scalar(const uint8_t* Y, const uint8_t* U, const uint8_t* V, i
 extern "C" int vp8_dev_encode(const uint8_t* y, const uint8_t* u, const uint8_t* v, int w, int h, float quality,
                               int filter_level, uint8_t* out, size_t cap, size_t* n, uint8_t* recon) {
     using namespace ik::vp8;
-    const QParams q = make_qparams(quality_to_qindex(quality), -2);
+    const QParams q = qparams_for_quality(quality);
     std::vector<MBOut> mbs;
     std::vector<uint8_t> rec;
     encode_frame_scalar(y, u, v, w, h, q, mbs, &rec);
