@@ -33,14 +33,18 @@ IK_HD int zigzag(int n) {
     constexpr uint8_t z[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
     return z[n];
 }
+IK_HD int izigzag(int j) {  // raster position -> zigzag index
+    constexpr uint8_t iz[16] = {0, 1, 5, 6, 2, 4, 7, 12, 3, 8, 11, 13, 9, 10, 14, 15};
+    return iz[j];
+}
 IK_HD int band(int n) {
     constexpr uint8_t b[17] = {0, 1, 2, 3, 6, 4, 5, 6, 6, 6, 6, 6, 6, 6, 6, 7, 0};
     return b[n];
 }
 IK_HD int clip8(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
-IK_HD int cost0(int p) { return kBitCost[p]; }         // 1/256 bit, coding 0 with P(0)=p/256
-IK_HD int cost1(int p) { return kBitCost[256 - p]; }   // coding 1
-IK_HD int costb(int p, int b) { return b ? cost1(p) : cost0(p); }
+IK_HD constexpr int cost0(int p) { return kBitCost[p]; }         // 1/256 bit, coding 0 with P(0)=p/256
+IK_HD constexpr int cost1(int p) { return kBitCost[256 - p]; }   // coding 1
+IK_HD constexpr int costb(int p, int b) { return b ? cost1(p) : cost0(p); }
 IK_HD const uint8_t* coef_probs(const uint8_t* probs, int type, int bnd, int ctx) {
     return probs + ((type * 8 + bnd) * 3 + ctx) * 11;
 }
@@ -237,7 +241,102 @@ IK_HD int block_cost(const int16_t* lv, int first, int last, int ctx, int type, 
     }
 }
 
-IK_HD int bmode_cost(int mode, int top, int left) {
+// block_cost(lv, FIRST, last, ctx0, TYPE, kCoeffProbs0), restated position by
+// position for levels held in registers: the cost of zigzag position n depends
+// only on lv[n-1] (its context and whether an end-of-block flag precedes it) and
+// lv[n], and with the default probabilities every probability is a compile-time
+// constant once the loop is unrolled -- the three contexts become selects, no
+// table loads.  Same value as block_cost (tests/test_vp8_host.py).
+IK_HD int sel3(int c, int a0, int a1, int a2) { return c == 0 ? a0 : (c == 1 ? a1 : a2); }
+template <int TYPE>
+IK_HD int pc0(int b, int c, int k) { return cost0(kCoeffProbs0[((TYPE * 8 + b) * 3 + c) * 11 + k]); }
+template <int TYPE>
+IK_HD int pc1(int b, int c, int k) { return cost1(kCoeffProbs0[((TYPE * 8 + b) * 3 + c) * 11 + k]); }
+template <int TYPE>
+IK_HD int large_cost_fixed(int v, int b, int c) {
+#define IK_C0(k) sel3(c, pc0<TYPE>(b, 0, k), pc0<TYPE>(b, 1, k), pc0<TYPE>(b, 2, k))
+#define IK_C1(k) sel3(c, pc1<TYPE>(b, 0, k), pc1<TYPE>(b, 1, k), pc1<TYPE>(b, 2, k))
+    if (v <= 4) {
+        if (v == 2) return IK_C0(3) + IK_C0(4);
+        return IK_C0(3) + IK_C1(4) + (v == 4 ? IK_C1(5) : IK_C0(5));
+    }
+    if (v <= 10) {
+        if (v <= 6) return IK_C1(3) + IK_C0(6) + IK_C0(7) + costb(159, v - 5);
+        return IK_C1(3) + IK_C0(6) + IK_C1(7) + costb(165, (v - 7) >> 1) + costb(145, (v - 7) & 1);
+    }
+    const int cat = v <= 18 ? 0 : (v <= 34 ? 1 : (v <= 66 ? 2 : 3));
+    const int c8 = (cat >> 1) ? IK_C1(8) : IK_C0(8);
+    const int c9 = (cat >> 1) ? ((cat & 1) ? IK_C1(10) : IK_C0(10)) : ((cat & 1) ? IK_C1(9) : IK_C0(9));
+    const int nb = cat == 3 ? 11 : 3 + cat;
+    return IK_C1(3) + IK_C1(6) + c8 + c9 + nb * 256;
+#undef IK_C0
+#undef IK_C1
+}
+template <int TYPE, int FIRST>
+IK_HD int block_cost_fixed(const int16_t* lv, int last, int ctx0) {
+    if (last <= FIRST)
+        return sel3(ctx0, pc0<TYPE>(band(FIRST), 0, 0), pc0<TYPE>(band(FIRST), 1, 0), pc0<TYPE>(band(FIRST), 2, 0));
+    int cost = 0, pc = ctx0;
+    bool chk = true;  // an end-of-block flag is coded before this position
+#pragma unroll
+    for (int n = FIRST; n < 16; ++n) {
+        const int b = band(n);
+        const int v = lv[n] < 0 ? -lv[n] : lv[n];
+        if (n < last) {
+            int c = chk ? sel3(pc, pc1<TYPE>(b, 0, 0), pc1<TYPE>(b, 1, 0), pc1<TYPE>(b, 2, 0)) : 0;
+            if (v == 0) {
+                c += sel3(pc, pc0<TYPE>(b, 0, 1), pc0<TYPE>(b, 1, 1), pc0<TYPE>(b, 2, 1));
+            } else {
+                c += sel3(pc, pc1<TYPE>(b, 0, 1), pc1<TYPE>(b, 1, 1), pc1<TYPE>(b, 2, 1)) + 256;
+                if (v == 1) c += sel3(pc, pc0<TYPE>(b, 0, 2), pc0<TYPE>(b, 1, 2), pc0<TYPE>(b, 2, 2));
+                else c += sel3(pc, pc1<TYPE>(b, 0, 2), pc1<TYPE>(b, 1, 2), pc1<TYPE>(b, 2, 2)) + large_cost_fixed<TYPE>(v, b, pc);
+            }
+            cost += c;
+        } else if (n == last) {
+            cost += sel3(pc, pc0<TYPE>(b, 0, 0), pc0<TYPE>(b, 1, 0), pc0<TYPE>(b, 2, 0));  // end of block
+        }
+        pc = v == 0 ? 0 : (v == 1 ? 1 : 2);
+        chk = v != 0;
+    }
+    return cost;
+}
+
+// Token-cost rows for one block type under the default probabilities, per
+// (band, ctx): {c1(p0), c0(p0), c0(p1), c1(p1) + 256 (sign), c0(p2), c1(p2), 0, 0,
+// then c0(pk), c1(pk) for k = 3..10} -- what block_cost reads, as a table the
+// GPU's position-parallel token cost gathers from LDS.
+struct TokCostTab { uint16_t v[8][3][24]; };
+constexpr TokCostTab make_tok_cost(int type) {
+    TokCostTab t{};
+    for (int b = 0; b < 8; ++b)
+        for (int c = 0; c < 3; ++c) {
+            const uint8_t* p = kCoeffProbs0 + ((type * 8 + b) * 3 + c) * 11;
+            uint16_t* r = t.v[b][c];
+            r[0] = (uint16_t)cost1(p[0]); r[1] = (uint16_t)cost0(p[0]); r[2] = (uint16_t)cost0(p[1]);
+            r[3] = (uint16_t)(cost1(p[1]) + 256); r[4] = (uint16_t)cost0(p[2]); r[5] = (uint16_t)cost1(p[2]);
+            for (int k = 3; k <= 10; ++k) { r[8 + 2 * (k - 3)] = (uint16_t)cost0(p[k]); r[9 + 2 * (k - 3)] = (uint16_t)cost1(p[k]); }
+        }
+    return t;
+}
+constexpr TokCostTab kTokCostI4 = make_tok_cost(3);
+// large_cost(v, p) from a row's c0/c1 of p3..p10 (r16[2*(k-3) + bit])
+IK_HD int large_cost_row(int v, const uint16_t* r16) {
+#define IK_R(k, bit) (int)r16[2 * ((k) - 3) + (bit)]
+    if (v <= 4) {
+        if (v == 2) return IK_R(3, 0) + IK_R(4, 0);
+        return IK_R(3, 0) + IK_R(4, 1) + IK_R(5, v == 4);
+    }
+    if (v <= 10) {
+        if (v <= 6) return IK_R(3, 1) + IK_R(6, 0) + IK_R(7, 0) + costb(159, v - 5);
+        return IK_R(3, 1) + IK_R(6, 0) + IK_R(7, 1) + costb(165, (v - 7) >> 1) + costb(145, (v - 7) & 1);
+    }
+    const int cat = v <= 18 ? 0 : (v <= 34 ? 1 : (v <= 66 ? 2 : 3));
+    const int nb = cat == 3 ? 11 : 3 + cat;
+    return IK_R(3, 1) + IK_R(6, 1) + IK_R(8, cat >> 1) + IK_R(9 + (cat >> 1), cat & 1) + nb * 256;
+#undef IK_R
+}
+
+IK_HD constexpr int bmode_cost(int mode, int top, int left) {
     const uint8_t* p = kBModeProbs + (top * 10 + left) * 9;
     // libwebp kYModesIntra4 tree
     switch (mode) {
@@ -257,6 +356,16 @@ IK_HD int bmode_cost(int mode, int top, int left) {
     default: return c + cost1(p[3]) + cost1(p[6]) + cost1(p[7]) + cost1(p[8]);
     }
 }
+struct BModeCostTab { uint16_t v[NUM_BMODES][NUM_BMODES][NUM_BMODES]; };  // [top][left][mode]
+constexpr BModeCostTab make_bmode_cost() {
+    BModeCostTab t{};
+    for (int a = 0; a < NUM_BMODES; ++a)
+        for (int l = 0; l < NUM_BMODES; ++l)
+            for (int m = 0; m < NUM_BMODES; ++m) t.v[a][l][m] = (uint16_t)bmode_cost(m, a, l);
+    return t;
+}
+constexpr BModeCostTab kBModeCost = make_bmode_cost();
+
 IK_HD int ymode_cost(int m) {  // key-frame y mode: B_PRED / DC / V / H / TM
     if (m == B_PRED) return cost0(145);
     const int c = cost1(145);
@@ -372,6 +481,74 @@ IK_HD void pred4(int m, const uint8_t* d, uint8_t* pr) {
         break;
     }
 #undef P
+}
+
+// pred4 restated as one tap descriptor per (mode, pixel) over the 13 context
+// samples 0:X 1..8:A..H 9..12:I..L -- so lanes predicting different modes run the
+// same instructions (the GPU kernel's lane = (mode, row)).  kind<<12 | i0<<8 | i1<<4 | i2.
+enum { P4_CP = 0, P4_A2, P4_A3, P4_TM, P4_DC };
+constexpr uint16_t p4d(int kind, int a, int b = 0, int c = 0) {
+    return (uint16_t)(kind << 12 | a << 8 | b << 4 | c);
+}
+#define CP(a) p4d(P4_CP, a)
+#define A2(a, b) p4d(P4_A2, a, b)
+#define A3(a, b, c) p4d(P4_A3, a, b, c)
+#define TM(x, y) p4d(P4_TM, 1 + (x), 9 + (y), 0)
+#define DC p4d(P4_DC, 0)
+constexpr uint16_t kPred4Tab[NUM_BMODES][16] = {
+    // B_DC
+    {DC, DC, DC, DC, DC, DC, DC, DC, DC, DC, DC, DC, DC, DC, DC, DC},
+    // B_TM
+    {TM(0, 0), TM(1, 0), TM(2, 0), TM(3, 0), TM(0, 1), TM(1, 1), TM(2, 1), TM(3, 1),
+     TM(0, 2), TM(1, 2), TM(2, 2), TM(3, 2), TM(0, 3), TM(1, 3), TM(2, 3), TM(3, 3)},
+    // B_VE: avg3 of the top row around column x (X left of A)
+    {A3(0, 1, 2), A3(1, 2, 3), A3(2, 3, 4), A3(3, 4, 5), A3(0, 1, 2), A3(1, 2, 3), A3(2, 3, 4), A3(3, 4, 5),
+     A3(0, 1, 2), A3(1, 2, 3), A3(2, 3, 4), A3(3, 4, 5), A3(0, 1, 2), A3(1, 2, 3), A3(2, 3, 4), A3(3, 4, 5)},
+    // B_HE
+    {A3(0, 9, 10), A3(0, 9, 10), A3(0, 9, 10), A3(0, 9, 10), A3(9, 10, 11), A3(9, 10, 11), A3(9, 10, 11),
+     A3(9, 10, 11), A3(10, 11, 12), A3(10, 11, 12), A3(10, 11, 12), A3(10, 11, 12), A3(11, 12, 12),
+     A3(11, 12, 12), A3(11, 12, 12), A3(11, 12, 12)},
+    // B_RD: avg3 along the down-right diagonal of L K J I X A B C D
+    {A3(9, 0, 1), A3(0, 1, 2), A3(1, 2, 3), A3(2, 3, 4), A3(10, 9, 0), A3(9, 0, 1), A3(0, 1, 2), A3(1, 2, 3),
+     A3(11, 10, 9), A3(10, 9, 0), A3(9, 0, 1), A3(0, 1, 2), A3(12, 11, 10), A3(11, 10, 9), A3(10, 9, 0), A3(9, 0, 1)},
+    // B_VR
+    {A2(0, 1), A2(1, 2), A2(2, 3), A2(3, 4), A3(9, 0, 1), A3(0, 1, 2), A3(1, 2, 3), A3(2, 3, 4),
+     A3(10, 9, 0), A2(0, 1), A2(1, 2), A2(2, 3), A3(11, 10, 9), A3(9, 0, 1), A3(0, 1, 2), A3(1, 2, 3)},
+    // B_LD: avg3 along the down-left diagonal (H repeated)
+    {A3(1, 2, 3), A3(2, 3, 4), A3(3, 4, 5), A3(4, 5, 6), A3(2, 3, 4), A3(3, 4, 5), A3(4, 5, 6), A3(5, 6, 7),
+     A3(3, 4, 5), A3(4, 5, 6), A3(5, 6, 7), A3(6, 7, 8), A3(4, 5, 6), A3(5, 6, 7), A3(6, 7, 8), A3(7, 8, 8)},
+    // B_VL
+    {A2(1, 2), A2(2, 3), A2(3, 4), A2(4, 5), A3(1, 2, 3), A3(2, 3, 4), A3(3, 4, 5), A3(4, 5, 6),
+     A2(2, 3), A2(3, 4), A2(4, 5), A3(5, 6, 7), A3(2, 3, 4), A3(3, 4, 5), A3(4, 5, 6), A3(6, 7, 8)},
+    // B_HD
+    {A2(9, 0), A3(9, 0, 1), A3(0, 1, 2), A3(1, 2, 3), A2(10, 9), A3(10, 9, 0), A2(9, 0), A3(9, 0, 1),
+     A2(11, 10), A3(11, 10, 9), A2(10, 9), A3(10, 9, 0), A2(12, 11), A3(12, 11, 10), A2(11, 10), A3(11, 10, 9)},
+    // B_HU
+    {A2(9, 10), A3(9, 10, 11), A2(10, 11), A3(10, 11, 12), A2(10, 11), A3(10, 11, 12), A2(11, 12), A3(11, 12, 12),
+     A2(11, 12), A3(11, 12, 12), CP(12), CP(12), CP(12), CP(12), CP(12), CP(12)},
+};
+#undef CP
+#undef A2
+#undef A3
+#undef TM
+#undef DC
+IK_HD int p4_off(int i) { return i == 0 ? -1 - kBps : (i <= 8 ? i - 1 - kBps : -1 + (i - 9) * kBps); }
+// pixel p (= y*4 + x) of pred4(m, d, .); dcv = the block's B_DC value
+IK_HD int pred4_px(int m, int p, const uint8_t* d, int dcv) {
+    const int t = kPred4Tab[m][p];
+    const int kind = t >> 12;
+    const int a = d[p4_off((t >> 8) & 15)], b = d[p4_off((t >> 4) & 15)], c = d[p4_off(t & 15)];
+    switch (kind) {
+    case P4_CP: return a;
+    case P4_A2: return avg2(a, b);
+    case P4_A3: return avg3(a, b, c);
+    case P4_TM: return clip8(a + b - c);
+    default: return dcv;
+    }
+}
+IK_HD int pred4_dc(const uint8_t* d) {
+    return (d[-kBps] + d[1 - kBps] + d[2 - kBps] + d[3 - kBps] + d[-1] + d[-1 + kBps] + d[-1 + 2 * kBps] +
+            d[-1 + 3 * kBps] + 4) >> 3;
 }
 
 // NxN (16 luma / 8 chroma) prediction; mb_x/mb_y select libwebp's DC variants

@@ -18,6 +18,7 @@ struct Vp8Args {
     MBOut* mbs;          // per image: mb_w*mb_h records, raster order
     uint8_t* nz;         // per image: mb_w*mb_h x 18 outgoing non-zero contexts (top[9], left[9])
     QParams q;
+    unsigned long long* stamps;  // dev tool (IK_VP8_STAMPS): per diagonal, 8 phase clocks of image 0's first MB
 };
 
 inline size_t vp8_rec_bytes(int w, int h) {

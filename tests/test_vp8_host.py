@@ -58,3 +58,27 @@ def test_quality_orders_size():
     Y, U, V = vp8.yuv_of(ikutil.synth(128, 96, 3, seed=5, pattern="S"))
     sizes = [len(vp8.encode(Y, U, V, q, -1)[0]) for q in (10.0, 50.0, 80.0, 100.0)]
     assert sizes == sorted(sizes) and sizes[0] < sizes[-1]
+
+
+@pytest.mark.parametrize("typ,first", [(0, 1), (0, 0), (1, 0), (2, 0), (3, 0)])
+def test_register_token_cost_equals_scan(typ, first):
+    """block_cost_fixed (the GPU kernel's unrolled, compile-time-probability form)
+    == block_cost's scan, over sparse/dense/large levels and all three contexts."""
+    rng = np.random.default_rng(typ * 2 + first)
+    for trial in range(1500):
+        lv = np.zeros(16, np.int16)
+        k = rng.integers(0, 17)
+        pos = rng.choice(16, size=k, replace=False)
+        mag = rng.choice([1, 1, 1, 2, 3, 4, 5, 6, 7, 9, 10, 11, 18, 19, 34, 35, 66, 67, 200, 2047], size=k)
+        lv[pos] = mag * rng.choice([-1, 1], size=k)
+        if first:
+            lv[0] = 0
+        for ctx in range(3):
+            g, f = vp8.cost_pair(lv, typ, first, ctx)
+            assert g == f, (lv.tolist(), typ, first, ctx, g, f)
+
+
+def test_pred4_tap_table_equals_pred4():
+    """kPred4Tab / pred4_px (the GPU's lane-per-(mode,row) predictor) == pred4 for all
+    10 modes and 16 pixels on random contexts."""
+    assert vp8.lib.vp8_dev_pred4_mismatches(7, 20000) == 0

@@ -113,3 +113,38 @@ extern "C" int vp8_dev_encode(const uint8_t* y, const uint8_t* u, const uint8_t*
     if (recon) std::memcpy(recon, rec.data(), rec.size());
     return 0;
 }
+
+// block_cost_fixed (the GPU kernel's register form) against the generic scan
+extern "C" int vp8_dev_cost_pair(const int16_t* lv, int type, int first, int ctx, int* generic, int* fixed) {
+    using namespace ik::vp8;
+    const int last = last_nz(lv, first);
+    *generic = block_cost(lv, first, last, ctx, type, kCoeffProbs0);
+    switch (type * 2 + first) {
+    case 0: *fixed = block_cost_fixed<0, 0>(lv, last, ctx); break;
+    case 1: *fixed = block_cost_fixed<0, 1>(lv, last, ctx); break;
+    case 2: *fixed = block_cost_fixed<1, 0>(lv, last, ctx); break;
+    case 4: *fixed = block_cost_fixed<2, 0>(lv, last, ctx); break;
+    case 6: *fixed = block_cost_fixed<3, 0>(lv, last, ctx); break;
+    default: return 1;
+    }
+    return 0;
+}
+
+// pred4_px (the GPU kernel's per-pixel tap table) against pred4, on random contexts
+extern "C" int vp8_dev_pred4_mismatches(unsigned seed, int trials) {
+    using namespace ik::vp8;
+    unsigned s = seed * 2654435761u + 1;
+    int bad = 0;
+    for (int t = 0; t < trials; ++t) {
+        uint8_t buf[6 * kBps];
+        for (auto& v : buf) { s = s * 1664525u + 1013904223u; v = (uint8_t)(s >> 24); }
+        const uint8_t* d = buf + kBps + 1;
+        for (int m = 0; m < NUM_BMODES; ++m) {
+            uint8_t pr[16];
+            pred4(m, d, pr);
+            const int dcv = pred4_dc(d);
+            for (int p = 0; p < 16; ++p) bad += pred4_px(m, p, d, dcv) != pr[p];
+        }
+    }
+    return bad;
+}

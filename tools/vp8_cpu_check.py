@@ -14,6 +14,9 @@ subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", so,
 lib = ctypes.CDLL(so)
 lib.vp8_dev_encode.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_int,
                                ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), ctypes.c_void_p]
+lib.vp8_dev_cost_pair.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+lib.vp8_dev_pred4_mismatches.argtypes = [ctypes.c_uint, ctypes.c_int]
 webp = ctypes.CDLL("libwebp.so.7")
 webp.WebPDecodeYUV.restype = ctypes.POINTER(ctypes.c_uint8)
 webp.WebPDecodeYUV.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
@@ -59,6 +62,13 @@ def encode(Y, U, V, q, filt):
                               np.ascontiguousarray(V).ctypes.data, w, h, q, filt, out.ctypes.data, out.size,
                               ctypes.byref(n), rec.ctypes.data) == 0
     return bytes(out[:n.value]), rec
+
+
+def cost_pair(lv, typ, first, ctx):
+    lv = np.ascontiguousarray(lv, dtype=np.int16)
+    g, f = ctypes.c_int(), ctypes.c_int()
+    assert lib.vp8_dev_cost_pair(lv.ctypes.data, typ, first, ctx, ctypes.byref(g), ctypes.byref(f)) == 0
+    return g.value, f.value
 
 
 def psnr(a, b):
