@@ -104,7 +104,7 @@ __global__ __launch_bounds__(kThreadsMB) void k_vp8_diag(Vp8Args a, int t) {
     __shared__ uint8_t s_nzb16[64], s_nzbuv[32], s_bm4[16], s_bnz[16];
     __shared__ uint8_t s_ctx[26];  // top_nz[9], left_nz[9], top_bmodes[4], left_bmodes[4]
 
-    // ---- load: every global read of the MB issued at once, one barrier ----
+    // ---- load: every global read of the MB formed first and issued at once ----
     const uint8_t* Y = a.yuv + (size_t)img * a.yuv_stride;
     const int uvw = (a.w + 1) >> 1, uvh = (a.h + 1) >> 1;
     const uint8_t* U = Y + (size_t)a.w * a.h;
@@ -128,39 +128,61 @@ __global__ __launch_bounds__(kThreadsMB) void k_vp8_diag(Vp8Args a, int t) {
         s_src_y[i] = Y[(size_t)sy * a.w + sx];
     }
     {
-        const int sx = min(mx * 8 + (lane & 7), uvw - 1), sy = min(my * 8 + (lane >> 3), uvh - 1);
-        if (wv == 0) s_src_u[lane] = U[(size_t)sy * uvw + sx];
-        else s_src_v[lane] = V[(size_t)sy * uvw + sx];
+        const int cx = min(mx * 8 + (lane & 7), uvw - 1), cy = min(my * 8 + (lane >> 3), uvh - 1);
+        (wv == 0 ? s_src_u : s_src_v)[lane] = (wv == 0 ? U : V)[(size_t)cy * uvw + cx];
     }
-    // work buffers: context row 0 (top-left, top, top-right) and column 0 (left)
+    // Work buffers: context row 0 (top-left, top, top-right) and column 0 (left)
     // with libwebp's frame-edge 127 / 129 fills, the 4x4 top-right copies of the
-    // MB's top-right samples in block rows 1..3, zero elsewhere
-    auto ctx_px = [&](const uint8_t* rec, int stride, int n, int extra, int row, int col) -> int {
+    // MB's top-right samples in block rows 1..3, zero elsewhere.  Each byte is a
+    // constant or one reconstructed sample: addresses first, then every load
+    // unconditionally (one memory round trip), then the selects.
+    auto ctx_src = [&](const uint8_t* rec, int stride, int n, int extra, int row, int col, int& cval) -> const uint8_t* {
         const int x0 = mx * n, y0 = my * n;
+        cval = 0;
         if (row == 0 || (n == 16 && (row == 4 || row == 8 || row == 12) && col >= 17 && col <= 20)) {
             const int x = col - 1;
-            if (x >= n + extra) return 0;
-            if (my == 0) return 127;
-            if (x < 0) return mx == 0 ? 129 : rec[(size_t)(y0 - 1) * stride + x0 - 1];
-            if (x < n) return rec[(size_t)(y0 - 1) * stride + x0 + x];
-            return mx == mb_w - 1 ? rec[(size_t)(y0 - 1) * stride + x0 + n - 1] : rec[(size_t)(y0 - 1) * stride + x0 + x];
+            if (x >= n + extra) return nullptr;
+            if (my == 0) { cval = 127; return nullptr; }
+            if (x < 0) {
+                if (mx == 0) { cval = 129; return nullptr; }
+                return rec + (size_t)(y0 - 1) * stride + x0 - 1;
+            }
+            return rec + (size_t)(y0 - 1) * stride + x0 + (x >= n && mx == mb_w - 1 ? n - 1 : x);
         }
-        if (col == 0 && row <= n) return mx == 0 ? 129 : rec[(size_t)(y0 + row - 1) * stride + x0 - 1];
-        return 0;
+        if (col == 0 && row >= 1 && row <= n) {
+            if (mx == 0) { cval = 129; return nullptr; }
+            return rec + (size_t)(y0 + row - 1) * stride + x0 - 1;
+        }
+        return nullptr;
     };
-    for (int wd = tid; wd < 17 * kBps / 4; wd += kThreadsMB) {
-        const int row = (wd * 4) / kBps, col = (wd * 4) % kBps;
-        uint32_t v = 0;
-        for (int k = 0; k < 4; ++k) v |= (uint32_t)ctx_px(RY, rw, 16, 4, row, col + k) << (8 * k);
-        reinterpret_cast<uint32_t*>(s_y)[wd] = v;
-        reinterpret_cast<uint32_t*>(s_y4)[wd] = v;
-    }
-    for (int wd = tid; wd < 2 * 9 * kBps / 4; wd += kThreadsMB) {
-        const int ch = wd >= 9 * kBps / 4, w2 = wd - ch * (9 * kBps / 4);
-        const int row = (w2 * 4) / kBps, col = (w2 * 4) % kBps;
-        uint32_t v = 0;
-        for (int k = 0; k < 4; ++k) v |= (uint32_t)ctx_px(ch ? RV : RU, cw, 8, 0, row, col + k) << (8 * k);
-        reinterpret_cast<uint32_t*>(ch ? s_v : s_u)[w2] = v;
+    auto ctx_word = [&](const uint8_t* rec, int stride, int n, int extra, int row, int col) -> uint32_t {
+        const uint8_t* p[4];
+        int cv[4], v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) p[k] = ctx_src(rec, stride, n, extra, row, col + k, cv[k]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = *(p[k] ? p[k] : rec);  // rec: a valid dummy address
+        uint32_t w = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w |= (uint32_t)(p[k] ? v[k] : cv[k]) << (8 * k);
+        return w;
+    };
+    // 136 luma words + 144 chroma words over the 128 threads, loads of all rounds
+    // issued before any select (the loop is unrolled)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int wd = tid + k * kThreadsMB;
+        if (wd < 17 * kBps / 4) {
+            const int row = (wd * 4) / kBps, col = (wd * 4) % kBps;
+            const uint32_t w = ctx_word(RY, rw, 16, 4, row, col);
+            reinterpret_cast<uint32_t*>(s_y)[wd] = w;
+            reinterpret_cast<uint32_t*>(s_y4)[wd] = w;
+        } else if (wd < 17 * kBps / 4 + 2 * 9 * kBps / 4) {
+            const int w1 = wd - 17 * kBps / 4;
+            const int ch = w1 >= 9 * kBps / 4, w2 = w1 - ch * (9 * kBps / 4);
+            const int row = (w2 * 4) / kBps, col = (w2 * 4) % kBps;
+            reinterpret_cast<uint32_t*>(ch ? s_v : s_u)[w2] = ctx_word(ch ? RV : RU, cw, 8, 0, row, col);
+        }
     }
     if (tid < 9) {
         s_ctx[tid] = my ? nzs[(size_t)(mbi - mb_w) * 18 + tid] : 0;       // above MB's outgoing top

@@ -80,11 +80,11 @@ int Vp8Work::launch(const uint8_t* d_yuv, size_t yuv_stride, int n, int quality,
         std::vector<unsigned long long> st((size_t)8 * T);
         IK_HIP(hipStreamSynchronize(s));
         IK_HIP(hipMemcpy(st.data(), a.stamps, st.size() * 8, hipMemcpyDeviceToHost));
-        double ph[5] = {0, 0, 0, 0, 0};
+        double ph[4] = {0, 0, 0, 0};
         for (int t = 0; t < T; ++t)
-            for (int k = 0; k < 5; ++k) ph[k] += (double)(st[8 * t + k + 1] - st[8 * t + k]) / T;
-        fprintf(stderr, "[vp8 stamps] per MB (memtime ticks): load %.0f i16 %.0f i4 %.0f uv %.0f out %.0f; diag span %.0f\n",
-                ph[0], ph[1], ph[2], ph[3], ph[4], (double)(st[8 * (T - 1)] - st[0]) / (T - 1));
+            for (int k = 0; k < 4; ++k) ph[k] += (double)(st[8 * t + k + 1] - st[8 * t + k]) / T;
+        fprintf(stderr, "[vp8 stamps] per MB (memtime ticks): load %.0f search %.0f decide %.0f out %.0f; diag span %.0f\n",
+                ph[0], ph[1], ph[2], ph[3], (double)(st[8 * (T - 1)] - st[0]) / (T - 1));
         (void)hipFree(a.stamps);
     }
     return IK_OK;
