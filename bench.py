@@ -8,7 +8,9 @@ resize_image receives; raw frames need no entropy decode) -> resize_image to
 reference's own filter) -> encode_image WebP q80.  One step = one batch through
 libimagekit_hip.so's pipeline: ONE resize launch over the batch, ONE WebP
 colour-convert launch, D2H of the YUV planes, libwebp VP8 coding of every image
-on the host thread pool.  Encoded bytes end in host memory.
+on the host thread pool.  Encoded bytes end in host memory.  Batches go through
+ik_pipeline_submit / ik_pipeline_collect with two in flight, so the host coding
+of batch i overlaps the device stage of batch i+1 (--sync: one at a time).
 
 value = input pixels of all images of all ranks / max-over-ranks wall time of
 the K timed steps.  roofline = the resize kernel (the dominant device kernel):
@@ -57,6 +59,7 @@ def parse():
     ap.add_argument("--device-only", action="store_true", help="time resize+colour kernels only")
     ap.add_argument("--webp-encoder", default="libwebp", choices=["libwebp", "gpu"],
                     help="libwebp: host VP8 coder, bytes identical to the reference; gpu: gfx950 VP8 encoder")
+    ap.add_argument("--sync", action="store_true", help="one batch in flight (ik_pipeline_run per step)")
     ap.add_argument("--no-alt-encoder", action="store_true", help="skip timing the other WebP encoder")
     return ap.parse_args()
 
@@ -167,19 +170,49 @@ def main():
     out = np.empty(out_cap, np.uint8)
     sizes = (ctypes.c_size_t * B)()
 
-    def step():
-        if args.device_only:
-            rc = lib.ik_pipeline_run_device(pipe, ctypes.c_void_p(src.data_ptr()), pitch, S * pitch, B)
-        else:
-            rc = lib.ik_pipeline_run(pipe, ctypes.c_void_p(src.data_ptr()), pitch, S * pitch, B,
-                                     out.ctypes.data, out_cap, sizes)
-        if rc:
-            raise SystemExit(f"pipeline run: {_lib.last_error()}")
+    src_ptr = ctypes.c_void_p(src.data_ptr())
+    n_done = ctypes.c_uint32()
+
+    def kernel_ms():
         return (lib.ik_pipeline_kernel_ms(pipe, 0), lib.ik_pipeline_kernel_ms(pipe, 1),
                 lib.ik_pipeline_kernel_ms(pipe, 2))
 
-    for _ in range(args.warmup):
-        step()
+    def submit():
+        if lib.ik_pipeline_submit(pipe, src_ptr, pitch, S * pitch, B):
+            raise SystemExit(f"pipeline submit: {_lib.last_error()}")
+
+    def collect():
+        if lib.ik_pipeline_collect(pipe, out.ctypes.data, out_cap, sizes, ctypes.byref(n_done)):
+            raise SystemExit(f"pipeline collect: {_lib.last_error()}")
+        assert n_done.value == B
+        return kernel_ms()
+
+    def run_steps(k):
+        """k batches; with --sync one run per batch, else two in flight (the host
+        stage of batch i overlaps the device stage of batch i+1)"""
+        if args.device_only:
+            res = []
+            for _ in range(k):
+                if lib.ik_pipeline_run_device(pipe, src_ptr, pitch, S * pitch, B):
+                    raise SystemExit(f"pipeline run: {_lib.last_error()}")
+                res.append(kernel_ms())
+            return res
+        if args.sync:
+            res = []
+            for _ in range(k):
+                submit()
+                res.append(collect())
+            return res
+        res = []
+        submit()
+        for _ in range(k - 1):
+            submit()
+            res.append(collect())
+        res.append(collect())
+        return res
+
+    if args.warmup:
+        run_steps(args.warmup)
 
     def barrier():
         if dist is not None:
@@ -188,9 +221,7 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    kms = []
-    for _ in range(args.steps):
-        kms.append(step())
+    kms = run_steps(args.steps)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     barrier()
@@ -208,10 +239,10 @@ def main():
     if not args.device_only and not args.no_alt_encoder:
         other = "gpu" if args.webp_encoder == "libwebp" else "libwebp"
         if lib.ik_pipeline_set_webp_encoder(pipe, ENCODERS[other]) == 0:
-            step()
+            run_steps(1)
             barrier()
             t1 = time.perf_counter()
-            ak = [step() for _ in range(3)]
+            ak = run_steps(3)
             barrier()
             te = reduce_max(time.perf_counter() - t1, dist, f"cuda:{local}")
             alt_enc = {"encoder": other, "value": round(aggregate_mpix(world, B, 3, S, te), 2),
@@ -274,7 +305,7 @@ def main():
                 "batch_per_gpu": B, "filter": args.filter, "format": "webp",
                 "quality": args.quality, "host_threads_per_gpu": args.threads,
                 "webp_encoder": args.webp_encoder,
-                "device_only": bool(args.device_only), "parallelism": f"images sharded, {world} rank(s)",
+                "device_only": bool(args.device_only), "batches_in_flight": 1 if args.sync else 2, "parallelism": f"images sharded, {world} rank(s)",
             },
             "roofline": {
                 "bound": "hbm",

@@ -111,6 +111,16 @@ int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t
 int ik_pipeline_run(ik_pipeline *p, const uint8_t *dev_src, size_t src_pitch,
                     size_t src_image_stride, uint32_t n, uint8_t *out, size_t out_cap,
                     size_t *out_sizes);
+/* Streaming form of ik_pipeline_run: submit enqueues the device stage of a batch
+ * (and the copy of what the host stage needs) and returns; collect finishes the
+ * oldest submitted batch -- its host entropy stage -- and writes its bytes like
+ * ik_pipeline_run (*n_out = its image count).  At most two batches are in flight,
+ * so the host stage of batch k overlaps the device stage of batch k+1.  The
+ * source frames of a submitted batch must stay valid until it is collected. */
+int ik_pipeline_submit(ik_pipeline *p, const uint8_t *dev_src, size_t src_pitch,
+                       size_t src_image_stride, uint32_t n);
+int ik_pipeline_collect(ik_pipeline *p, uint8_t *out, size_t out_cap, size_t *out_sizes,
+                        uint32_t *n_out);
 /* WebP encoder of this pipeline (IK_WEBP_*; default: the process default) */
 int ik_pipeline_set_webp_encoder(ik_pipeline *p, int encoder);
 /* device-only part (resize + colour convert/FDCT [+ GPU VP8]) for n images, no host stage */

@@ -2,13 +2,16 @@
 // throughput path behind the /img and /upload handlers, src/lib.rs:175-191 and
 // :281-297, when many requests are in flight).
 //
-// Per run: ONE resize launch over the whole batch (k_resize_fused, pixels HBM ->
+// Per batch: ONE resize launch over the whole batch (k_resize_fused, pixels HBM ->
 // LDS -> HBM), ONE colour-convert launch (WebP YUV420 planes or JPEG quantised
-// coefficients), one D2H copy of those small planes into pinned memory, then the
-// host entropy coders (libwebp VP8 / baseline Huffman) over a persistent thread
-// pool, one image per task -- the reference runs one synchronous transform per
-// tokio worker (src/main.rs:20), so per-image serial entropy coding across cores
-// is the same structure.
+// coefficients), with the GPU WebP encoder the VP8 wavefront (ik_vp8.hip), one
+// D2H copy of the small planes / MB records into pinned memory, then the host
+// entropy stage (libwebp VP8 / VP8 boolean coder / baseline Huffman) over a
+// persistent thread pool, one image per task -- the reference runs one
+// synchronous transform per tokio worker (src/main.rs:20), so per-image serial
+// entropy coding across cores is the same structure.  submit / collect keep two
+// batches in flight, so the host stage of one overlaps the device stage of the
+// next; run = submit + collect.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -98,14 +101,24 @@ struct ik_pipeline {
     size_t r_pitch = 0, r_img_stride = 0;
     uint8_t* d_stage = nullptr;  // YUV planes or int16 coefficients, per image
     size_t stage_bytes = 0;
-    uint8_t* h_stage = nullptr;  // pinned
     uint8_t* d_qt = nullptr;
     uint8_t qt[128];
     float* d_tmp = nullptr;      // naive resize path only
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    double ms[3] = {0, 0, 0};
     int webp_enc = IK_WEBP_LIBWEBP;  // IK_WEBP_GPU: k_vp8_diag wavefront + host bitstream
     ik::Vp8Work vp8;
+    // Two host slots: the device stage of batch k+1 (enqueued by submit) runs
+    // while the host entropy stage of batch k (collect) works from its slot.
+    // Device buffers are shared: the stream orders batch k+1's kernels after
+    // batch k's copies out.
+    struct Slot {
+        uint8_t* h_stage = nullptr;       // pinned planes / coefficients
+        ik::vp8::MBOut* h_mbs = nullptr;  // pinned MB records (GPU VP8)
+        hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // resize, colour, vp8, copy boundaries
+        uint32_t n = 0;
+        bool gpu_vp8 = false;
+    } slot[2];
+    int head = 0, inflight = 0;
+    double ms[3] = {0, 0, 0};
     uint32_t last_n = 0;
     ik::Pool* pool = nullptr;
     std::vector<std::vector<uint8_t>> outs;
@@ -113,6 +126,107 @@ struct ik_pipeline {
 };
 
 using namespace ik;
+
+namespace {
+
+int check_batch(const ik_pipeline* p, const uint8_t* dev_src, size_t src_pitch, size_t src_image_stride, uint32_t n) {
+    if (!p || !dev_src || !n || n > p->max_batch) return fail(IK_ERR_INVALID, "bad batch");
+    if (src_pitch < (size_t)p->W * p->C || (src_pitch & 7) || ((uintptr_t)dev_src & 7))
+        return fail(IK_ERR_INVALID, "source rows must be 8-byte aligned and >= W*C");
+    if (n > 1 && src_image_stride < src_pitch * p->H) return fail(IK_ERR_INVALID, "image stride too small");
+    return IK_OK;
+}
+
+// device stage of one batch on the pipeline's stream, events into slot s; with
+// copy_out, also the D2H of what the host stage needs (no synchronisation)
+int enqueue(ik_pipeline* p, ik_pipeline::Slot& s, const uint8_t* dev_src, size_t src_pitch, size_t src_image_stride,
+            uint32_t n, bool copy_out) {
+    IK_HIP(hipSetDevice(p->device));
+    ResizePlan* plan = get_resize_plan(p->device, (int)p->W, (int)p->H, (int)p->C, (int)p->nw, (int)p->nh,
+                                       p->filter, (int)p->max_batch);
+    if (!plan) return fail(IK_ERR_DEVICE, "cannot build resize plan");
+    s.gpu_vp8 = p->fmt == IK_FORMAT_WEBP && p->webp_enc == IK_WEBP_GPU;
+    s.n = n;
+    IK_HIP(hipEventRecord(s.ev[0], p->stream));
+    IK_HIP(launch_resize(*plan, dev_src, src_pitch, src_image_stride, p->d_resized, p->r_pitch,
+                         p->r_img_stride, (int)n, p->d_tmp, p->stream));
+    IK_HIP(hipEventRecord(s.ev[1], p->stream));
+    if (p->fmt == IK_FORMAT_WEBP) {
+        const DeviceConsts* dc = device_consts(p->device);
+        IK_HIP(launch_webp_yuv420(p->d_resized, (int)p->nw, (int)p->nh, (int)p->C, p->r_pitch,
+                                  p->r_img_stride, p->d_stage, p->stage_bytes, (int)n,
+                                  dc->gamma_to_lin, dc->lin_to_gamma, p->stream));
+    } else {
+        IK_HIP(launch_jpeg_coeffs(p->d_resized, (int)p->nw, (int)p->nh, (int)p->C, p->r_pitch,
+                                  p->r_img_stride, p->d_qt, (int16_t*)p->d_stage,
+                                  p->stage_bytes / sizeof(int16_t), (int)n, p->stream));
+    }
+    IK_HIP(hipEventRecord(s.ev[2], p->stream));
+    if (s.gpu_vp8) {
+        if (int rc = p->vp8.launch(p->d_stage, p->stage_bytes, (int)n, p->quality, p->stream)) return rc;
+    }
+    IK_HIP(hipEventRecord(s.ev[3], p->stream));
+    if (copy_out) {
+        if (s.gpu_vp8) {
+            if (int rc = p->vp8.fetch_to(s.h_mbs, (int)n, p->stream)) return rc;
+        } else {
+            IK_HIP(hipMemcpyAsync(s.h_stage, p->d_stage, p->stage_bytes * n, hipMemcpyDeviceToHost, p->stream));
+        }
+    }
+    IK_HIP(hipEventRecord(s.ev[4], p->stream));
+    return IK_OK;
+}
+
+int finish_device(ik_pipeline* p, ik_pipeline::Slot& s) {
+    IK_HIP(hipEventSynchronize(s.ev[4]));
+    float a = 0, b = 0, c = 0;
+    IK_HIP(hipEventElapsedTime(&a, s.ev[0], s.ev[1]));
+    IK_HIP(hipEventElapsedTime(&b, s.ev[1], s.ev[2]));
+    IK_HIP(hipEventElapsedTime(&c, s.ev[2], s.ev[3]));
+    p->ms[0] = a;
+    p->ms[1] = b;
+    p->ms[2] = s.gpu_vp8 ? c : 0.0;
+    p->last_n = s.n;
+    return IK_OK;
+}
+
+// host entropy stage of a finished slot; bytes back to back into out
+int host_stage(ik_pipeline* p, const ik_pipeline::Slot& s, uint8_t* out, size_t out_cap, size_t* out_sizes) {
+    const uint32_t n = s.n;
+    p->outs.resize(n);
+    p->status.assign(n, 0);
+    std::vector<std::string> errs(n);
+    p->pool->run((int)n, [&](int i) {
+        const uint8_t* st = s.h_stage + p->stage_bytes * (size_t)i;
+        if (s.gpu_vp8) {
+            p->vp8.write_from(s.h_mbs, i, p->quality, p->outs[i]);
+        } else if (p->fmt == IK_FORMAT_WEBP) {
+            const size_t ys = (size_t)p->nw * p->nh, uvs = (size_t)((p->nw + 1) / 2) * ((p->nh + 1) / 2);
+            p->status[i] = webp_encode_yuv420(st, st + ys, st + ys + uvs, (int)p->nw, (int)p->nh,
+                                              (float)p->quality, p->outs[i]);
+            if (p->status[i]) {
+                char buf[256];
+                ik_last_error(buf, sizeof(buf));
+                errs[i] = buf;
+            }
+        } else {
+            jpeg_write((const int16_t*)st, (int)p->nw, (int)p->nh, p->qt, p->outs[i]);
+        }
+    });
+    size_t off = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (p->status[i]) return fail(p->status[i], "image %u: %s", i, errs[i].c_str());
+        if (out_sizes) out_sizes[i] = p->outs[i].size();
+        if (out) {
+            if (off + p->outs[i].size() > out_cap) return fail(IK_ERR_INVALID, "output buffer too small");
+            std::memcpy(out + off, p->outs[i].data(), p->outs[i].size());
+        }
+        off += p->outs[i].size();
+    }
+    return IK_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -128,7 +242,8 @@ int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t
     p->filter = filter; p->fmt = fmt;
     p->quality = quality < 1 ? 1 : quality > 100 ? 100 : quality;
     IK_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
-    for (auto& e : p->ev) IK_HIP(hipEventCreate(&e));
+    for (auto& sl : p->slot)
+        for (auto& e : sl.ev) IK_HIP(hipEventCreate(&e));
     p->r_pitch = pitch_for(nw, C);
     p->r_img_stride = p->r_pitch * nh;
     IK_HIP(hipMalloc(&p->d_resized, p->r_img_stride * max_batch + 16));
@@ -142,7 +257,7 @@ int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t
         if (int rc = copy_h2d_2d(p->d_qt, 128, p->qt, 128, 128, 1, p->stream)) return rc;
     }
     IK_HIP(hipMalloc(&p->d_stage, p->stage_bytes * max_batch));
-    IK_HIP(hipHostMalloc(&p->h_stage, p->stage_bytes * max_batch, hipHostMallocDefault));
+    for (auto& sl : p->slot) IK_HIP(hipHostMalloc(&sl.h_stage, p->stage_bytes * max_batch, hipHostMallocDefault));
     ResizePlan* plan = get_resize_plan(p->device, (int)W, (int)H, (int)C, (int)nw, (int)nh, filter, (int)max_batch);
     if (!plan) return fail(IK_ERR_DEVICE, "cannot build resize plan");
     if (plan->slots == 0) IK_HIP(hipMalloc(&p->d_tmp, sizeof(float) * (size_t)max_batch * nh * W * C));
@@ -163,10 +278,14 @@ int ik_pipeline_set_webp_encoder(ik_pipeline* p, int encoder) {
     if (!p) return fail(IK_ERR_INVALID, "null pipeline");
     if (encoder != IK_WEBP_LIBWEBP && encoder != IK_WEBP_GPU) return fail(IK_ERR_INVALID, "bad WebP encoder %d", encoder);
     if (p->fmt != IK_FORMAT_WEBP) return fail(IK_ERR_INVALID, "not a WebP pipeline");
+    if (p->inflight) return fail(IK_ERR_INVALID, "batches in flight: collect them first");
     IK_HIP(hipSetDevice(p->device));
     if (encoder == IK_WEBP_GPU) {
         if (p->nw > 16383 || p->nh > 16383) return fail(IK_ERR_TRANSFORM, "WebP dimensions exceed 16383");
         if (int rc = p->vp8.reserve((int)p->nw, (int)p->nh, (int)p->max_batch)) return rc;
+        const size_t recs = p->vp8.record_bytes((int)p->max_batch);
+        for (auto& sl : p->slot)
+            if (!sl.h_mbs) IK_HIP(hipHostMalloc(&sl.h_mbs, recs, hipHostMallocDefault));
     }
     p->webp_enc = encoder;
     return IK_OK;
@@ -174,88 +293,38 @@ int ik_pipeline_set_webp_encoder(ik_pipeline* p, int encoder) {
 
 int ik_pipeline_run_device(ik_pipeline* p, const uint8_t* dev_src, size_t src_pitch,
                            size_t src_image_stride, uint32_t n) {
-    if (!p || !dev_src || !n || n > p->max_batch) return fail(IK_ERR_INVALID, "bad batch");
-    if (src_pitch < (size_t)p->W * p->C || (src_pitch & 7) || ((uintptr_t)dev_src & 7))
-        return fail(IK_ERR_INVALID, "source rows must be 8-byte aligned and >= W*C");
-    if (n > 1 && src_image_stride < src_pitch * p->H) return fail(IK_ERR_INVALID, "image stride too small");
-    IK_HIP(hipSetDevice(p->device));
-    ResizePlan* plan = get_resize_plan(p->device, (int)p->W, (int)p->H, (int)p->C, (int)p->nw, (int)p->nh,
-                                       p->filter, (int)p->max_batch);
-    if (!plan) return fail(IK_ERR_DEVICE, "cannot build resize plan");
-    IK_HIP(hipEventRecord(p->ev[0], p->stream));
-    IK_HIP(launch_resize(*plan, dev_src, src_pitch, src_image_stride, p->d_resized, p->r_pitch,
-                         p->r_img_stride, (int)n, p->d_tmp, p->stream));
-    IK_HIP(hipEventRecord(p->ev[1], p->stream));
-    if (p->fmt == IK_FORMAT_WEBP) {
-        const DeviceConsts* dc = device_consts(p->device);
-        IK_HIP(launch_webp_yuv420(p->d_resized, (int)p->nw, (int)p->nh, (int)p->C, p->r_pitch,
-                                  p->r_img_stride, p->d_stage, p->stage_bytes, (int)n,
-                                  dc->gamma_to_lin, dc->lin_to_gamma, p->stream));
-    } else {
-        IK_HIP(launch_jpeg_coeffs(p->d_resized, (int)p->nw, (int)p->nh, (int)p->C, p->r_pitch,
-                                  p->r_img_stride, p->d_qt, (int16_t*)p->d_stage,
-                                  p->stage_bytes / sizeof(int16_t), (int)n, p->stream));
-    }
-    IK_HIP(hipEventRecord(p->ev[2], p->stream));
-    const bool gpu_vp8 = p->fmt == IK_FORMAT_WEBP && p->webp_enc == IK_WEBP_GPU;
-    if (gpu_vp8) {
-        if (int rc = p->vp8.launch(p->d_stage, p->stage_bytes, (int)n, p->quality, p->stream)) return rc;
-    }
-    IK_HIP(hipEventRecord(p->ev[3], p->stream));
-    IK_HIP(hipEventSynchronize(p->ev[3]));
-    float a = 0, b = 0, c = 0;
-    IK_HIP(hipEventElapsedTime(&a, p->ev[0], p->ev[1]));
-    IK_HIP(hipEventElapsedTime(&b, p->ev[1], p->ev[2]));
-    IK_HIP(hipEventElapsedTime(&c, p->ev[2], p->ev[3]));
-    p->ms[0] = a;
-    p->ms[1] = b;
-    p->ms[2] = gpu_vp8 ? c : 0.0;
-    p->last_n = n;
+    if (int rc = check_batch(p, dev_src, src_pitch, src_image_stride, n)) return rc;
+    if (p->inflight) return fail(IK_ERR_INVALID, "batches in flight: collect them first");
+    if (int rc = enqueue(p, p->slot[0], dev_src, src_pitch, src_image_stride, n, false)) return rc;
+    return finish_device(p, p->slot[0]);
+}
+
+int ik_pipeline_submit(ik_pipeline* p, const uint8_t* dev_src, size_t src_pitch, size_t src_image_stride,
+                       uint32_t n) {
+    if (int rc = check_batch(p, dev_src, src_pitch, src_image_stride, n)) return rc;
+    if (p->inflight >= 2) return fail(IK_ERR_INVALID, "two batches already in flight: collect one first");
+    ik_pipeline::Slot& s = p->slot[p->head & 1];
+    if (int rc = enqueue(p, s, dev_src, src_pitch, src_image_stride, n, true)) return rc;
+    ++p->head;
+    ++p->inflight;
     return IK_OK;
+}
+
+int ik_pipeline_collect(ik_pipeline* p, uint8_t* out, size_t out_cap, size_t* out_sizes, uint32_t* n_out) {
+    if (!p) return fail(IK_ERR_INVALID, "null pipeline");
+    if (!p->inflight) return fail(IK_ERR_INVALID, "no batch in flight");
+    ik_pipeline::Slot& s = p->slot[(p->head - p->inflight) & 1];
+    --p->inflight;  // the slot is free again whatever happens below
+    if (n_out) *n_out = s.n;
+    if (int rc = finish_device(p, s)) return rc;
+    return host_stage(p, s, out, out_cap, out_sizes);
 }
 
 int ik_pipeline_run(ik_pipeline* p, const uint8_t* dev_src, size_t src_pitch, size_t src_image_stride,
                     uint32_t n, uint8_t* out, size_t out_cap, size_t* out_sizes) {
-    int st = ik_pipeline_run_device(p, dev_src, src_pitch, src_image_stride, n);
-    if (st) return st;
-    const bool gpu_vp8 = p->fmt == IK_FORMAT_WEBP && p->webp_enc == IK_WEBP_GPU;
-    if (gpu_vp8) {
-        if (int rc = p->vp8.fetch((int)n, p->stream)) return rc;
-    } else {
-        IK_HIP(hipMemcpyAsync(p->h_stage, p->d_stage, p->stage_bytes * n, hipMemcpyDeviceToHost, p->stream));
-    }
-    IK_HIP(hipStreamSynchronize(p->stream));
-    p->outs.resize(n);
-    p->status.assign(n, 0);
-    std::vector<std::string> errs(n);
-    p->pool->run((int)n, [&](int i) {
-        const uint8_t* s = p->h_stage + p->stage_bytes * (size_t)i;
-        if (gpu_vp8) {
-            p->vp8.write(i, p->quality, p->outs[i]);
-        } else if (p->fmt == IK_FORMAT_WEBP) {
-            const size_t ys = (size_t)p->nw * p->nh, uvs = (size_t)((p->nw + 1) / 2) * ((p->nh + 1) / 2);
-            p->status[i] = webp_encode_yuv420(s, s + ys, s + ys + uvs, (int)p->nw, (int)p->nh,
-                                              (float)p->quality, p->outs[i]);
-            if (p->status[i]) {
-                char buf[256];
-                ik_last_error(buf, sizeof(buf));
-                errs[i] = buf;
-            }
-        } else {
-            jpeg_write((const int16_t*)s, (int)p->nw, (int)p->nh, p->qt, p->outs[i]);
-        }
-    });
-    size_t off = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        if (p->status[i]) return fail(p->status[i], "image %u: %s", i, errs[i].c_str());
-        if (out_sizes) out_sizes[i] = p->outs[i].size();
-        if (out) {
-            if (off + p->outs[i].size() > out_cap) return fail(IK_ERR_INVALID, "output buffer too small");
-            std::memcpy(out + off, p->outs[i].data(), p->outs[i].size());
-        }
-        off += p->outs[i].size();
-    }
-    return IK_OK;
+    if (p && p->inflight) return fail(IK_ERR_INVALID, "batches in flight: collect them first");
+    if (int rc = ik_pipeline_submit(p, dev_src, src_pitch, src_image_stride, n)) return rc;
+    return ik_pipeline_collect(p, out, out_cap, out_sizes, nullptr);
 }
 
 double ik_pipeline_kernel_ms(const ik_pipeline* p, int which) {
@@ -273,15 +342,19 @@ int ik_pipeline_fetch_resized(ik_pipeline* p, uint32_t i, uint8_t* dst, size_t c
 void ik_pipeline_destroy(ik_pipeline* p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
+    if (p->stream) (void)hipStreamSynchronize(p->stream);
     delete p->pool;
     p->vp8.release();
     if (p->d_resized) (void)hipFree(p->d_resized);
     if (p->d_stage) (void)hipFree(p->d_stage);
-    if (p->h_stage) (void)hipHostFree(p->h_stage);
     if (p->d_qt) (void)hipFree(p->d_qt);
     if (p->d_tmp) (void)hipFree(p->d_tmp);
-    for (auto& e : p->ev)
-        if (e) (void)hipEventDestroy(e);
+    for (auto& sl : p->slot) {
+        if (sl.h_stage) (void)hipHostFree(sl.h_stage);
+        if (sl.h_mbs) (void)hipHostFree(sl.h_mbs);
+        for (auto& e : sl.ev)
+            if (e) (void)hipEventDestroy(e);
+    }
     if (p->stream) (void)hipStreamDestroy(p->stream);
     delete p;
 }

@@ -64,10 +64,13 @@ struct Vp8Work {
     int reserve(int w, int h, int n);
     void release();
     size_t mb_count() const;
+    size_t record_bytes(int n) const;  // MB records of n images
     // the wavefront launches for n images (YUV420 planes yuv_stride apart), async on s
     int launch(const uint8_t* d_yuv, size_t yuv_stride, int n, int quality, hipStream_t s);
-    int fetch(int n, hipStream_t s);  // async D2H of the MB records
-    void write(int i, int quality, std::vector<uint8_t>& out) const;  // bitstream of image i (host)
+    int fetch(int n, hipStream_t s) { return fetch_to(h_mbs, n, s); }  // async D2H of the MB records
+    int fetch_to(vp8::MBOut* dst, int n, hipStream_t s);
+    void write(int i, int quality, std::vector<uint8_t>& out) const { write_from(h_mbs, i, quality, out); }
+    void write_from(const vp8::MBOut* recs, int i, int quality, std::vector<uint8_t>& out) const;  // host bitstream
 };
 int default_webp_encoder();  // IK_WEBP_LIBWEBP unless ik_set_webp_encoder / IK_WEBP_ENCODER=gpu
 int webp_encode_gpu(const uint8_t* d_yuv, int w, int h, int quality, std::vector<uint8_t>& out);

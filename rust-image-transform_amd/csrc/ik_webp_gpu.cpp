@@ -90,14 +90,16 @@ int Vp8Work::launch(const uint8_t* d_yuv, size_t yuv_stride, int n, int quality,
     return IK_OK;
 }
 
-int Vp8Work::fetch(int n, hipStream_t s) {
-    IK_HIP(hipMemcpyAsync(h_mbs, d_mbs, sizeof(vp8::MBOut) * mb_count() * n, hipMemcpyDeviceToHost, s));
+size_t Vp8Work::record_bytes(int n) const { return sizeof(vp8::MBOut) * mb_count() * (size_t)n; }
+
+int Vp8Work::fetch_to(vp8::MBOut* dst, int n, hipStream_t s) {
+    IK_HIP(hipMemcpyAsync(dst, d_mbs, sizeof(vp8::MBOut) * mb_count() * n, hipMemcpyDeviceToHost, s));
     return IK_OK;
 }
 
-void Vp8Work::write(int i, int quality, std::vector<uint8_t>& out) const {
+void Vp8Work::write_from(const vp8::MBOut* recs, int i, int quality, std::vector<uint8_t>& out) const {
     const vp8::QParams q = vp8::qparams_for_quality((float)quality);
-    vp8::write_webp(w, h, q, h_mbs + mb_count() * (size_t)i, -1, out);
+    vp8::write_webp(w, h, q, recs + mb_count() * (size_t)i, -1, out);
 }
 
 // one image from device YUV420 planes, on the calling thread's stream
