@@ -48,7 +48,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
+    ap.add_argument("--batch", type=int, default=64, help="images per GPU per step")
+    ap.add_argument("--alt-batch", type=int, default=128, help="images per GPU per step for the other WebP encoder")
+    ap.add_argument("--alt-steps", type=int, default=4)
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--out", type=int, default=512)
     ap.add_argument("--filter", default="triangle", choices=sorted(FILTERS))
@@ -155,9 +157,10 @@ def main():
     f = FILTERS[args.filter]
     pitch = S * 4
     # inputs resident in HBM before the timed region: 4 distinct synthetic frames tiled over the batch
-    distinct = [synth_rgba(S, S, seed=sd) for sd in shard_seeds(rank, B)]
-    src = torch.empty((B, S, pitch), dtype=torch.uint8, device=f"cuda:{local}")
-    for i in range(B):
+    NB = max(B, 0 if (args.device_only or args.no_alt_encoder) else args.alt_batch)
+    distinct = [synth_rgba(S, S, seed=sd) for sd in shard_seeds(rank, NB)]
+    src = torch.empty((NB, S, pitch), dtype=torch.uint8, device=f"cuda:{local}")
+    for i in range(NB):
         src[i].copy_(torch.from_numpy(distinct[i % len(distinct)].reshape(S, pitch)))
     torch.cuda.synchronize()
 
@@ -174,8 +177,7 @@ def main():
     n_done = ctypes.c_uint32()
 
     def kernel_ms():
-        return (lib.ik_pipeline_kernel_ms(pipe, 0), lib.ik_pipeline_kernel_ms(pipe, 1),
-                lib.ik_pipeline_kernel_ms(pipe, 2))
+        return tuple(lib.ik_pipeline_kernel_ms(pipe, k) for k in range(4))
 
     def submit():
         if lib.ik_pipeline_submit(pipe, src_ptr, pitch, S * pitch, B):
@@ -232,24 +234,51 @@ def main():
     resize_ms = float(np.mean([k[0] for k in kms]))
     colour_ms = float(np.mean([k[1] for k in kms]))
     vp8_ms = float(np.mean([k[2] for k in kms]))
+    host_ms = float(np.mean([k[3] for k in kms]))
     out_bytes = int(sum(sizes))
 
-    # the other WebP encoder end to end on the same batch (a few steps)
+    # the other WebP encoder end to end on frames of the same batch (a few steps,
+    # its own batch size: the GPU VP8 wavefront is latency-bound, so it wants more
+    # images per launch)
     alt_enc = {}
     if not args.device_only and not args.no_alt_encoder:
         other = "gpu" if args.webp_encoder == "libwebp" else "libwebp"
-        if lib.ik_pipeline_set_webp_encoder(pipe, ENCODERS[other]) == 0:
-            run_steps(1)
-            barrier()
-            t1 = time.perf_counter()
-            ak = run_steps(3)
-            barrier()
-            te = reduce_max(time.perf_counter() - t1, dist, f"cuda:{local}")
-            alt_enc = {"encoder": other, "value": round(aggregate_mpix(world, B, 3, S, te), 2),
-                       "ms_per_step": round(te / 3 * 1e3, 3),
-                       "vp8_kernel_ms": round(float(np.mean([k[2] for k in ak])), 4),
-                       "output_bytes_per_step": int(sum(sizes))}
-            lib.ik_pipeline_set_webp_encoder(pipe, ENCODERS[args.webp_encoder])
+        AB = args.alt_batch
+        p3 = ctypes.c_void_p()
+        if lib.ik_pipeline_create(S, S, 4, O, O, f, 1, args.quality, AB, args.threads, ctypes.byref(p3)) == 0:
+            if lib.ik_pipeline_set_webp_encoder(p3, ENCODERS[other]) == 0:
+                acap = AB * O * O * 4 + (1 << 20)
+                aout = np.empty(acap, np.uint8)
+                asz = (ctypes.c_size_t * AB)()
+                nd = ctypes.c_uint32()
+
+                def asub():
+                    assert lib.ik_pipeline_submit(p3, src_ptr, pitch, S * pitch, AB) == 0, _lib.last_error()
+
+                def acol():
+                    assert lib.ik_pipeline_collect(p3, aout.ctypes.data, acap, asz, ctypes.byref(nd)) == 0, \
+                        _lib.last_error()
+                    return lib.ik_pipeline_kernel_ms(p3, 2), lib.ik_pipeline_kernel_ms(p3, 3)
+
+                asub()
+                acol()
+                barrier()
+                t1 = time.perf_counter()
+                asub()
+                ak = []
+                for _ in range(args.alt_steps - 1):
+                    asub()
+                    ak.append(acol())
+                ak.append(acol())
+                barrier()
+                te = reduce_max(time.perf_counter() - t1, dist, f"cuda:{local}")
+                alt_enc = {"encoder": other, "batch_per_gpu": AB, "steps": args.alt_steps,
+                           "value": round(aggregate_mpix(world, AB, args.alt_steps, S, te), 2),
+                           "ms_per_step": round(te / args.alt_steps * 1e3, 3),
+                           "vp8_kernel_ms": round(float(np.mean([k[0] for k in ak])), 4),
+                           "host_stage_ms": round(float(np.mean([k[1] for k in ak])), 3),
+                           "output_bytes_per_image": int(sum(asz)) // AB}
+            lib.ik_pipeline_destroy(p3)
     bytes_per_img = 4 * S * S + 4 * O * O
     achieved = B * bytes_per_img / (resize_ms * 1e-3) / 1e9
     value = aggregate_mpix(world, B, args.steps, S, elapsed)
@@ -320,7 +349,8 @@ def main():
             },
             "colour_kernel_ms": round(colour_ms, 4),
             "vp8_kernel_ms": round(vp8_ms, 4),
-            "output_bytes_per_step": out_bytes,
+            "host_stage_ms": round(host_ms, 3),
+            "output_bytes_per_image": out_bytes // B,
             "alt_webp_encoder": alt_enc,
             "alt_filter_kernel": alt,
             "cpu_baseline": cpu,

@@ -127,7 +127,8 @@ int ik_pipeline_set_webp_encoder(ik_pipeline *p, int encoder);
 int ik_pipeline_run_device(ik_pipeline *p, const uint8_t *dev_src, size_t src_pitch,
                            size_t src_image_stride, uint32_t n);
 /* device time (ms) of stage `which` (0 = resize, 1 = colour convert, 2 = GPU VP8
- * wavefront) in the last run, from HIP events on the pipeline's stream */
+ * wavefront) in the last run, from HIP events on the pipeline's stream;
+ * 3 = wall time (ms) of the last collected batch's host entropy stage */
 double ik_pipeline_kernel_ms(const ik_pipeline *p, int which);
 /* resized pixels of image i of the last run (tightly packed nw*nh*C) */
 int ik_pipeline_fetch_resized(ik_pipeline *p, uint32_t i, uint8_t *dst, size_t cap);

@@ -16,6 +16,7 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <chrono>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -94,31 +95,36 @@ private:
 
 struct ik_pipeline {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;   // resize + colour convert (+ host copies)
+    hipStream_t stream2 = nullptr;  // GPU VP8 wavefront + packer: overlaps the next batch's resize
     uint32_t W = 0, H = 0, C = 0, nw = 0, nh = 0, max_batch = 0;
     int filter = 4, fmt = 1, quality = 80;
     uint8_t* d_resized = nullptr;
     size_t r_pitch = 0, r_img_stride = 0;
-    uint8_t* d_stage = nullptr;  // YUV planes or int16 coefficients, per image
+    uint8_t* d_stage = nullptr;  // per slot: YUV planes or int16 coefficients, per image
     size_t stage_bytes = 0;
     uint8_t* d_qt = nullptr;
     uint8_t qt[128];
     float* d_tmp = nullptr;      // naive resize path only
     int webp_enc = IK_WEBP_LIBWEBP;  // IK_WEBP_GPU: k_vp8_diag wavefront + host bitstream
     ik::Vp8Work vp8;
-    // Two host slots: the device stage of batch k+1 (enqueued by submit) runs
-    // while the host entropy stage of batch k (collect) works from its slot.
-    // Device buffers are shared: the stream orders batch k+1's kernels after
-    // batch k's copies out.
+    // Two slots: the device stage of batch k+1 (enqueued by submit) runs while
+    // the host entropy stage of batch k (collect) works from its slot.  The
+    // resized images are shared (stream order); each slot has its own stage
+    // planes on the device, so with the GPU VP8 encoder the resize of batch k+1
+    // (stream) runs beside the wavefront of batch k (stream2).
     struct Slot {
         uint8_t* h_stage = nullptr;       // pinned planes / coefficients
-        ik::vp8::MBOut* h_mbs = nullptr;  // pinned MB records (GPU VP8)
-        hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // resize, colour, vp8, copy boundaries
+        ik::vp8::MBOut* h_mbs = nullptr;  // pinned MB records (GPU VP8, frames too big to pack)
+        uint8_t* h_pack = nullptr;        // pinned compact MB streams (GPU VP8, k_vp8_pack)
+        // resize start / end, colour end, vp8 end, copies end, vp8 start (stream2)
+        hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+        uint8_t* d_stage = nullptr;       // this slot's part of ik_pipeline::d_stage
         uint32_t n = 0;
-        bool gpu_vp8 = false;
+        bool gpu_vp8 = false, packed = false;
     } slot[2];
     int head = 0, inflight = 0;
-    double ms[3] = {0, 0, 0};
+    double ms[4] = {0, 0, 0, 0};
     uint32_t last_n = 0;
     ik::Pool* pool = nullptr;
     std::vector<std::vector<uint8_t>> outs;
@@ -151,29 +157,40 @@ int enqueue(ik_pipeline* p, ik_pipeline::Slot& s, const uint8_t* dev_src, size_t
     IK_HIP(launch_resize(*plan, dev_src, src_pitch, src_image_stride, p->d_resized, p->r_pitch,
                          p->r_img_stride, (int)n, p->d_tmp, p->stream));
     IK_HIP(hipEventRecord(s.ev[1], p->stream));
+    // the slot's stage planes were last read by the wavefront of the batch two
+    // back (stream2): its end event is still in s.ev[3] (a no-op wait if never recorded)
+    IK_HIP(hipStreamWaitEvent(p->stream, s.ev[3], 0));
     if (p->fmt == IK_FORMAT_WEBP) {
         const DeviceConsts* dc = device_consts(p->device);
         IK_HIP(launch_webp_yuv420(p->d_resized, (int)p->nw, (int)p->nh, (int)p->C, p->r_pitch,
-                                  p->r_img_stride, p->d_stage, p->stage_bytes, (int)n,
+                                  p->r_img_stride, s.d_stage, p->stage_bytes, (int)n,
                                   dc->gamma_to_lin, dc->lin_to_gamma, p->stream));
     } else {
         IK_HIP(launch_jpeg_coeffs(p->d_resized, (int)p->nw, (int)p->nh, (int)p->C, p->r_pitch,
-                                  p->r_img_stride, p->d_qt, (int16_t*)p->d_stage,
+                                  p->r_img_stride, p->d_qt, (int16_t*)s.d_stage,
                                   p->stage_bytes / sizeof(int16_t), (int)n, p->stream));
     }
     IK_HIP(hipEventRecord(s.ev[2], p->stream));
+    s.packed = false;
     if (s.gpu_vp8) {
-        if (int rc = p->vp8.launch(p->d_stage, p->stage_bytes, (int)n, p->quality, p->stream)) return rc;
-    }
-    IK_HIP(hipEventRecord(s.ev[3], p->stream));
-    if (copy_out) {
-        if (s.gpu_vp8) {
-            if (int rc = p->vp8.fetch_to(s.h_mbs, (int)n, p->stream)) return rc;
-        } else {
-            IK_HIP(hipMemcpyAsync(s.h_stage, p->d_stage, p->stage_bytes * n, hipMemcpyDeviceToHost, p->stream));
+        IK_HIP(hipStreamWaitEvent(p->stream2, s.ev[2], 0));
+        IK_HIP(hipEventRecord(s.ev[5], p->stream2));
+        if (int rc = p->vp8.launch(s.d_stage, p->stage_bytes, (int)n, p->quality, p->stream2)) return rc;
+        IK_HIP(hipEventRecord(s.ev[3], p->stream2));
+        if (copy_out && p->vp8.packable()) {
+            if (int rc = p->vp8.pack_to(s.h_pack, (int)n, p->stream2)) return rc;
+            s.packed = true;
+        } else if (copy_out) {
+            if (int rc = p->vp8.fetch_to(s.h_mbs, (int)n, p->stream2)) return rc;
         }
+        IK_HIP(hipEventRecord(s.ev[4], p->stream2));
+    } else {
+        IK_HIP(hipEventRecord(s.ev[5], p->stream));
+        IK_HIP(hipEventRecord(s.ev[3], p->stream));
+        if (copy_out)
+            IK_HIP(hipMemcpyAsync(s.h_stage, s.d_stage, p->stage_bytes * n, hipMemcpyDeviceToHost, p->stream));
+        IK_HIP(hipEventRecord(s.ev[4], p->stream));
     }
-    IK_HIP(hipEventRecord(s.ev[4], p->stream));
     return IK_OK;
 }
 
@@ -182,7 +199,7 @@ int finish_device(ik_pipeline* p, ik_pipeline::Slot& s) {
     float a = 0, b = 0, c = 0;
     IK_HIP(hipEventElapsedTime(&a, s.ev[0], s.ev[1]));
     IK_HIP(hipEventElapsedTime(&b, s.ev[1], s.ev[2]));
-    IK_HIP(hipEventElapsedTime(&c, s.ev[2], s.ev[3]));
+    IK_HIP(hipEventElapsedTime(&c, s.ev[5], s.ev[3]));
     p->ms[0] = a;
     p->ms[1] = b;
     p->ms[2] = s.gpu_vp8 ? c : 0.0;
@@ -193,12 +210,20 @@ int finish_device(ik_pipeline* p, ik_pipeline::Slot& s) {
 // host entropy stage of a finished slot; bytes back to back into out
 int host_stage(ik_pipeline* p, const ik_pipeline::Slot& s, uint8_t* out, size_t out_cap, size_t* out_sizes) {
     const uint32_t n = s.n;
+    const auto t0 = std::chrono::steady_clock::now();
     p->outs.resize(n);
     p->status.assign(n, 0);
     std::vector<std::string> errs(n);
     p->pool->run((int)n, [&](int i) {
         const uint8_t* st = s.h_stage + p->stage_bytes * (size_t)i;
-        if (s.gpu_vp8) {
+        if (s.packed) {
+            p->status[i] = p->vp8.write_packed(s.h_pack + p->vp8.pack_cap() * (size_t)i, p->quality, p->outs[i]);
+            if (p->status[i]) {
+                char buf[256];
+                ik_last_error(buf, sizeof(buf));
+                errs[i] = buf;
+            }
+        } else if (s.gpu_vp8) {
             p->vp8.write_from(s.h_mbs, i, p->quality, p->outs[i]);
         } else if (p->fmt == IK_FORMAT_WEBP) {
             const size_t ys = (size_t)p->nw * p->nh, uvs = (size_t)((p->nw + 1) / 2) * ((p->nh + 1) / 2);
@@ -213,6 +238,7 @@ int host_stage(ik_pipeline* p, const ik_pipeline::Slot& s, uint8_t* out, size_t 
             jpeg_write((const int16_t*)st, (int)p->nw, (int)p->nh, p->qt, p->outs[i]);
         }
     });
+    p->ms[3] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     size_t off = 0;
     for (uint32_t i = 0; i < n; ++i) {
         if (p->status[i]) return fail(p->status[i], "image %u: %s", i, errs[i].c_str());
@@ -242,6 +268,7 @@ int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t
     p->filter = filter; p->fmt = fmt;
     p->quality = quality < 1 ? 1 : quality > 100 ? 100 : quality;
     IK_HIP(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    IK_HIP(hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking));
     for (auto& sl : p->slot)
         for (auto& e : sl.ev) IK_HIP(hipEventCreate(&e));
     p->r_pitch = pitch_for(nw, C);
@@ -256,7 +283,9 @@ int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t
         IK_HIP(hipMalloc(&p->d_qt, 128));
         if (int rc = copy_h2d_2d(p->d_qt, 128, p->qt, 128, 128, 1, p->stream)) return rc;
     }
-    IK_HIP(hipMalloc(&p->d_stage, p->stage_bytes * max_batch));
+    IK_HIP(hipMalloc(&p->d_stage, 2 * p->stage_bytes * max_batch));
+    p->slot[0].d_stage = p->d_stage;
+    p->slot[1].d_stage = p->d_stage + p->stage_bytes * max_batch;
     for (auto& sl : p->slot) IK_HIP(hipHostMalloc(&sl.h_stage, p->stage_bytes * max_batch, hipHostMallocDefault));
     ResizePlan* plan = get_resize_plan(p->device, (int)W, (int)H, (int)C, (int)nw, (int)nh, filter, (int)max_batch);
     if (!plan) return fail(IK_ERR_DEVICE, "cannot build resize plan");
@@ -283,9 +312,13 @@ int ik_pipeline_set_webp_encoder(ik_pipeline* p, int encoder) {
     if (encoder == IK_WEBP_GPU) {
         if (p->nw > 16383 || p->nh > 16383) return fail(IK_ERR_TRANSFORM, "WebP dimensions exceed 16383");
         if (int rc = p->vp8.reserve((int)p->nw, (int)p->nh, (int)p->max_batch)) return rc;
-        const size_t recs = p->vp8.record_bytes((int)p->max_batch);
-        for (auto& sl : p->slot)
-            if (!sl.h_mbs) IK_HIP(hipHostMalloc(&sl.h_mbs, recs, hipHostMallocDefault));
+        for (auto& sl : p->slot) {
+            if (p->vp8.packable()) {
+                if (!sl.h_pack) IK_HIP(hipHostMalloc(&sl.h_pack, p->vp8.pack_cap() * p->max_batch, hipHostMallocDefault));
+            } else if (!sl.h_mbs) {
+                IK_HIP(hipHostMalloc(&sl.h_mbs, p->vp8.record_bytes((int)p->max_batch), hipHostMallocDefault));
+            }
+        }
     }
     p->webp_enc = encoder;
     return IK_OK;
@@ -328,7 +361,7 @@ int ik_pipeline_run(ik_pipeline* p, const uint8_t* dev_src, size_t src_pitch, si
 }
 
 double ik_pipeline_kernel_ms(const ik_pipeline* p, int which) {
-    if (!p || which < 0 || which > 2) return -1.0;
+    if (!p || which < 0 || which > 3) return -1.0;
     return p->ms[which];
 }
 
@@ -343,6 +376,7 @@ void ik_pipeline_destroy(ik_pipeline* p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
     if (p->stream) (void)hipStreamSynchronize(p->stream);
+    if (p->stream2) (void)hipStreamSynchronize(p->stream2);
     delete p->pool;
     p->vp8.release();
     if (p->d_resized) (void)hipFree(p->d_resized);
@@ -352,10 +386,12 @@ void ik_pipeline_destroy(ik_pipeline* p) {
     for (auto& sl : p->slot) {
         if (sl.h_stage) (void)hipHostFree(sl.h_stage);
         if (sl.h_mbs) (void)hipHostFree(sl.h_mbs);
+        if (sl.h_pack) (void)hipHostFree(sl.h_pack);
         for (auto& e : sl.ev)
             if (e) (void)hipEventDestroy(e);
     }
     if (p->stream) (void)hipStreamDestroy(p->stream);
+    if (p->stream2) (void)hipStreamDestroy(p->stream2);
     delete p;
 }
 

@@ -61,6 +61,8 @@ struct Vp8Work {
     vp8::MBOut* d_mbs = nullptr;     // per-MB decisions + levels
     uint8_t* d_nz = nullptr;         // per-MB outgoing non-zero contexts
     vp8::MBOut* h_mbs = nullptr;     // pinned mirror of d_mbs
+    uint8_t* d_pack = nullptr;       // k_vp8_pack scratch (pack_cap() bytes per image)
+    uint8_t* h_pack = nullptr;       // pinned compact streams (single-image path)
     int reserve(int w, int h, int n);
     void release();
     size_t mb_count() const;
@@ -71,6 +73,12 @@ struct Vp8Work {
     int fetch_to(vp8::MBOut* dst, int n, hipStream_t s);
     void write(int i, int quality, std::vector<uint8_t>& out) const { write_from(h_mbs, i, quality, out); }
     void write_from(const vp8::MBOut* recs, int i, int quality, std::vector<uint8_t>& out) const;  // host bitstream
+    // compact records (k_vp8_pack) of n images straight into pinned host memory,
+    // pack_cap() bytes apart; packable() = the frame fits the packer
+    bool packable() const;
+    size_t pack_cap() const;
+    int pack_to(uint8_t* host_dst, int n, hipStream_t s);
+    int write_packed(const uint8_t* pack_img, int quality, std::vector<uint8_t>& out) const;
 };
 int default_webp_encoder();  // IK_WEBP_LIBWEBP unless ik_set_webp_encoder / IK_WEBP_ENCODER=gpu
 int webp_encode_gpu(const uint8_t* d_yuv, int w, int h, int quality, std::vector<uint8_t>& out);

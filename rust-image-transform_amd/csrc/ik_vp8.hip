@@ -504,6 +504,143 @@ __global__ __launch_bounds__(kThreadsMB) void k_vp8_diag(Vp8Args a, int t) {
     if (stamp) stamp[4] = __builtin_amdgcn_s_memtime();
 }
 
+// ---- compact MB records for the host ------------------------------------------
+// One workgroup per image.  The records of k_vp8_diag (820 B per MB, mostly zero
+// levels) are rewritten as a byte stream (layout in ik_vp8_gpu.h) in a device
+// scratch image, then copied with 16-byte stores straight into the caller's pinned
+// host buffer: a small fraction of the bytes of a plain D2H of the records, and no
+// copy-engine pass on the stream.
+namespace {
+
+constexpr int kPackThreads = 1024;  // 16 waves: MB loads of an image in flight together
+
+__device__ __forceinline__ int wave_sum(int v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ int wave_excl_scan(int v) {
+    const int lane = threadIdx.x & 63;
+    int inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(inc, o);
+        if (lane >= o) inc += u;
+    }
+    return inc - v;
+}
+// lane = (block b = lane >> 1, half = lane & 1): its 8 levels, their nonzero mask,
+// and the whole block's 16-bit mask
+struct PackLane {
+    int16_t v[8];
+    int m8, cm;
+};
+__device__ __forceinline__ PackLane pack_load(const MBOut& o, int lane) {
+    PackLane p;
+    uint32_t w[4] = {0, 0, 0, 0};
+    if (lane < 50) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(&o.lv[0][0]) + lane * 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = src[k];
+    }
+    p.m8 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        p.v[2 * k] = (int16_t)(w[k] & 0xffff);
+        p.v[2 * k + 1] = (int16_t)(w[k] >> 16);
+        p.m8 |= (p.v[2 * k] != 0 ? 1 : 0) << (2 * k);
+        p.m8 |= (p.v[2 * k + 1] != 0 ? 1 : 0) << (2 * k + 1);
+    }
+    const int other = __shfl_xor(p.m8, 1);
+    p.cm = (lane & 1) ? (other | (p.m8 << 8)) : (p.m8 | (other << 8));
+    return p;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kPackThreads) void k_vp8_pack(const MBOut* __restrict__ mbs, int nmb,
+                                                          uint8_t* __restrict__ scratch, uint8_t* __restrict__ dst,
+                                                          size_t cap_img) {
+    __shared__ uint32_t s_off[kMaxPackMBs];
+    __shared__ uint32_t s_part[kPackThreads / 64];
+    const int img = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const MBOut* m0 = mbs + (size_t)img * nmb;
+    uint8_t* sc = scratch + (size_t)img * cap_img;
+    // 1. record sizes
+    for (int m = wv; m < nmb; m += kPackThreads / 64) {
+        const MBOut& o = m0[m];
+        const PackLane p = pack_load(o, lane);
+        const int bsz = ((lane & 1) == 0 && p.cm) ? 2 + 2 * __popc(p.cm) : 0;
+        const int tot = wave_sum(bsz);
+        if (lane == 0) s_off[m] = 8 + (o.ymode == B_PRED ? 16 : 0) + tot;
+    }
+    __syncthreads();
+    // 2. exclusive scan of the sizes (each thread: a run of consecutive MBs)
+    const int per = (nmb + kPackThreads - 1) / kPackThreads;
+    const int lo = min(tid * per, nmb), hi = min(lo + per, nmb);
+    uint32_t run = 0;
+    for (int m = lo; m < hi; ++m) run += s_off[m];
+    const uint32_t wex = (uint32_t)wave_excl_scan((int)run);
+    if (lane == 63) s_part[wv] = wex + run;
+    __syncthreads();
+    uint32_t base = kPackHeaderBytes + wex;
+    for (int k = 0; k < wv; ++k) base += s_part[k];
+    uint32_t total = kPackHeaderBytes;
+    for (int k = 0; k < kPackThreads / 64; ++k) total += s_part[k];
+    for (int m = lo; m < hi; ++m) {  // each thread rewrites only its own run
+        const uint32_t sz = s_off[m];
+        s_off[m] = base;
+        base += sz;
+    }
+    __syncthreads();
+    // 3. the records
+    for (int m = wv; m < nmb; m += kPackThreads / 64) {
+        const MBOut& o = m0[m];
+        const PackLane p = pack_load(o, lane);
+        const bool i4 = o.ymode == B_PRED;
+        const int bsz = ((lane & 1) == 0 && p.cm) ? 2 + 2 * __popc(p.cm) : 0;
+        const int boff = wave_excl_scan(bsz);  // block offsets in record order (= lane order)
+        const unsigned long long nzl = __ballot((lane & 1) == 0 && p.cm != 0);
+        uint8_t* r = sc + s_off[m];
+        if (lane == 0) {
+            uint32_t nzmask = 0;
+            for (int b = 0; b < 25; ++b) nzmask |= (uint32_t)((nzl >> (2 * b)) & 1) << b;
+            r[0] = o.ymode;
+            r[1] = o.uvmode;
+            r[2] = o.skip;
+            r[3] = 0;
+            *reinterpret_cast<uint32_t*>(r + 4) = nzmask;
+        }
+        if (i4 && lane < 16) r[8 + lane] = o.bmodes[lane];
+        const int blk = __shfl(boff, lane & ~1) + 8 + (i4 ? 16 : 0);  // the block's start (even lane)
+        if (lane < 50 && p.cm) {
+            int16_t* vals = reinterpret_cast<int16_t*>(r + blk + 2);
+            if ((lane & 1) == 0) *reinterpret_cast<uint16_t*>(r + blk) = (uint16_t)p.cm;
+            int rank = (lane & 1) ? __popc(p.cm & 0xff) : 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if ((p.m8 >> j) & 1) vals[rank++] = p.v[j];
+        }
+    }
+    if (tid == 0) {
+        uint32_t* h = reinterpret_cast<uint32_t*>(sc);
+        h[0] = total;
+        h[1] = (uint32_t)nmb;
+        h[2] = kPackMagic;
+        h[3] = 0;
+    }
+    __syncthreads();
+    // 4. to the host, 16 bytes per store
+    const uint4* s4 = reinterpret_cast<const uint4*>(sc);
+    uint4* d4 = reinterpret_cast<uint4*>(dst + (size_t)img * cap_img);
+    for (uint32_t i = tid; i < (total + 15) / 16; i += kPackThreads) d4[i] = s4[i];
+}
+
+hipError_t launch_vp8_pack(const MBOut* mbs, int nmb, int n, uint8_t* scratch, uint8_t* host_dst, size_t cap_img,
+                           hipStream_t s) {
+    if (nmb > kMaxPackMBs || (cap_img & 15)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_vp8_pack, dim3(n), dim3(kPackThreads), 0, s, mbs, nmb, scratch, host_dst, cap_img);
+    return hipGetLastError();
+}
+
 hipError_t launch_vp8_encode(const Vp8Args& a, int n, hipStream_t s) {
     const int per_diag = a.mb_h < (a.mb_w + 1) / 2 ? a.mb_h : (a.mb_w + 1) / 2;
     const int T = (a.mb_w - 1) + 2 * (a.mb_h - 1) + 1;

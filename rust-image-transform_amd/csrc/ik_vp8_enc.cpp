@@ -6,6 +6,7 @@
 // libwebp's decoder without a GPU.
 #include "ik_vp8_enc.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -13,58 +14,79 @@ namespace ik {
 namespace vp8 {
 namespace {
 
-// RFC 6386 section 7.3 boolean encoder
+constexpr size_t kPackHeader = 16;
+constexpr uint32_t kPackMagicHost = 0x4b503856u;  // ik_vp8_gpu.h kPackMagic
+
+// RFC 6386 section 7.3 boolean encoder, normalising a whole shift at a time.
+// `range` holds range-1 (the split is then (range*prob)>>8); bytes whose value is
+// 0xff are held back as a run until the next byte settles whether a carry
+// ripples through them.
 struct BoolEnc {
     std::vector<uint8_t> out;
-    uint32_t range = 255, bottom = 0;
-    int bit_count = 24;
-    void carry() {
-        size_t i = out.size();
-        while (i > 0 && out[i - 1] == 255) out[--i] = 0;
-        if (i > 0) ++out[i - 1];
-    }
-    void put(int bit, int prob) {
-        const uint32_t split = 1 + (((range - 1) * (uint32_t)prob) >> 8);
-        if (bit) { bottom += split; range -= split; }
-        else range = split;
-        while (range < 128) {
-            range <<= 1;
-            if (bottom & (1u << 31)) carry();
-            bottom <<= 1;
-            if (!--bit_count) {
-                out.push_back((uint8_t)(bottom >> 24));
-                bottom &= (1u << 24) - 1;
-                bit_count = 8;
+    int32_t range = 254, value = 0;
+    int nb_bits = -8, run = 0;
+    void emit() {
+        const int s = 8 + nb_bits;
+        const int32_t bits = value >> s;
+        value -= bits << s;
+        nb_bits -= 8;
+        if ((bits & 0xff) != 0xff) {
+            if ((bits & 0x100) && !out.empty()) ++out.back();
+            if (run) {
+                out.insert(out.end(), (size_t)run, (bits & 0x100) ? 0x00 : 0xff);
+                run = 0;
             }
+            out.push_back((uint8_t)bits);
+        } else {
+            ++run;
         }
+    }
+    inline void put(int bit, int prob) {  // branch-free but for the byte emit
+        const int32_t split = (range * prob) >> 8;
+        value += (split + 1) & -bit;
+        range = bit ? range - (split + 1) : split;
+        // renormalise: shift so that range+1 >= 128 (shift 0 when it already is)
+        const int shift = __builtin_clz((uint32_t)range + 1) - 24;
+        range = ((range + 1) << shift) - 1;
+        value <<= shift;
+        nb_bits += shift;
+        if (nb_bits > 0) emit();
     }
     void literal(int v, int n) {
         for (int i = n - 1; i >= 0; --i) put((v >> i) & 1, 128);
     }
-    void flush() {
-        int c = bit_count;
-        uint32_t v = bottom;
-        if (v & (1u << (32 - c))) carry();
-        v <<= c & 7;
-        c >>= 3;
-        while (--c >= 0) v <<= 8;
-        c = 4;
-        while (--c >= 0) {
-            out.push_back((uint8_t)(v >> 24));
-            v <<= 8;
-        }
+    void flush() {  // pad with zero bits until every coded bit is in a byte
+        const int pad = 9 - nb_bits;
+        for (int i = 0; i < pad; ++i) put(0, 128);
+        nb_bits = 0;
+        emit();
     }
 };
 
-// token sink: either counts node decisions (for probability adaptation) or codes them
+// Recorded token decisions: bit 15 = the bit, bits 0..10 = index into a 1312-entry
+// probability table: 0..1055 the adapted node probabilities, 1056 + p the fixed
+// probability p (extra bits, sign).
+// Pass 1 builds this and the node counts in one walk of the residuals; the coding
+// pass then only runs the boolean coder over it.
 struct TokenSink {
-    BoolEnc* enc = nullptr;           // coding when non-null
-    uint32_t (*counts)[2] = nullptr;  // [1056][2] when counting
-    const uint8_t* probs = nullptr;
-    void bit(int idx /* flat node index or -1 */, int prob, int b) {
-        if (counts && idx >= 0) ++counts[idx][b];
-        if (enc) enc->put(b, prob);
+    std::vector<uint16_t> toks;
+    uint16_t* w = nullptr;            // write cursor into toks
+    uint32_t (*counts)[2] = nullptr;  // [1056][2]
+    // room for one more macroblock: 25 blocks x 16 coefficients x <= 24 decisions
+    void reserve_mb() {
+        const size_t used = w ? (size_t)(w - toks.data()) : 0, need = used + 25 * 16 * 24;
+        if (toks.size() < need) {
+            toks.resize(need * 2);
+        }
+        w = toks.data() + used;
     }
+    size_t size() const { return (size_t)(w - toks.data()); }
+    std::vector<size_t> row_end;  // token count at the end of each MB row
+    inline void node(int idx, int b) {
+        ++counts[idx][b];
+        *w++ = (uint16_t)(idx | (b << 15));
+    }
+    inline void fixed(int prob, int b) { *w++ = (uint16_t)((1056 + prob) | (b << 15)); }
 };
 
 }  // namespace
@@ -77,83 +99,136 @@ int last_nz(const int16_t* lv, int first) {
 
 namespace {
 
-// one block's tokens (libwebp GetCoeffs in reverse); returns nz (any nonzero)
-int write_block(TokenSink& s, const int16_t* lv, int first, int ctx, int type) {
-    const int last = last_nz(lv, first);
+// one block's tokens (libwebp GetCoeffs in reverse) from its compact form (u16
+// nonzero mask + the nonzero levels; null = all zero); returns nz (any nonzero
+// level at or after `first`)
+int write_block(TokenSink& s, const uint8_t* blk, int first, int ctx, int type) {
+    uint32_t cm = 0;
+    const uint8_t* v = nullptr;
+    if (blk) {
+        uint16_t c;
+        std::memcpy(&c, blk, 2);
+        cm = c;
+        v = blk + 2 + 2 * __builtin_popcount(cm & ((1u << first) - 1));  // levels before `first` are not coded
+        cm &= ~((1u << first) - 1);
+    }
     int n = first;
     auto base = [&](int nn, int c) { return ((type * 8 + band(nn)) * 3 + c) * 11; };
     int b = base(n, ctx);
-    if (last <= first) {
-        s.bit(b + 0, s.probs[b + 0], 0);
+    if (!cm) {
+        s.node(b + 0, 0);
         return 0;
     }
+    const int last = 32 - __builtin_clz(cm);
     for (;;) {
-        s.bit(b + 0, s.probs[b + 0], 1);
-        while (lv[n] == 0) {
-            s.bit(b + 1, s.probs[b + 1], 0);
+        s.node(b + 0, 1);
+        while (!((cm >> n) & 1)) {
+            s.node(b + 1, 0);
             ++n;
             b = base(n, 0);
         }
-        s.bit(b + 1, s.probs[b + 1], 1);
-        const int v = lv[n] < 0 ? -lv[n] : lv[n];
+        s.node(b + 1, 1);
+        int16_t lvn;
+        std::memcpy(&lvn, v, 2);
+        v += 2;
+        const int val = lvn < 0 ? -lvn : lvn;
         int nctx;
-        if (v == 1) {
-            s.bit(b + 2, s.probs[b + 2], 0);
+        if (val == 1) {
+            s.node(b + 2, 0);
             nctx = 1;
         } else {
-            s.bit(b + 2, s.probs[b + 2], 1);
-            if (v <= 4) {
-                s.bit(b + 3, s.probs[b + 3], 0);
-                if (v == 2) s.bit(b + 4, s.probs[b + 4], 0);
-                else { s.bit(b + 4, s.probs[b + 4], 1); s.bit(b + 5, s.probs[b + 5], v == 4); }
-            } else if (v <= 10) {
-                s.bit(b + 3, s.probs[b + 3], 1);
-                s.bit(b + 6, s.probs[b + 6], 0);
-                if (v <= 6) {
-                    s.bit(b + 7, s.probs[b + 7], 0);
-                    s.bit(-1, 159, v - 5);
+            s.node(b + 2, 1);
+            if (val <= 4) {
+                s.node(b + 3, 0);
+                if (val == 2) s.node(b + 4, 0);
+                else { s.node(b + 4, 1); s.node(b + 5, val == 4); }
+            } else if (val <= 10) {
+                s.node(b + 3, 1);
+                s.node(b + 6, 0);
+                if (val <= 6) {
+                    s.node(b + 7, 0);
+                    s.fixed(159, val - 5);
                 } else {
-                    s.bit(b + 7, s.probs[b + 7], 1);
-                    s.bit(-1, 165, (v - 7) >> 1);
-                    s.bit(-1, 145, (v - 7) & 1);
+                    s.node(b + 7, 1);
+                    s.fixed(165, (val - 7) >> 1);
+                    s.fixed(145, (val - 7) & 1);
                 }
             } else {
-                s.bit(b + 3, s.probs[b + 3], 1);
-                s.bit(b + 6, s.probs[b + 6], 1);
+                s.node(b + 3, 1);
+                s.node(b + 6, 1);
                 static const uint8_t kCat3[] = {173, 148, 140, 0};
                 static const uint8_t kCat4[] = {176, 155, 140, 135, 0};
                 static const uint8_t kCat5[] = {180, 157, 141, 134, 130, 0};
                 static const uint8_t kCat6[] = {254, 254, 243, 230, 196, 177, 153, 140, 133, 130, 129, 0};
                 static const uint8_t* const kCat[4] = {kCat3, kCat4, kCat5, kCat6};
-                const int cat = v <= 18 ? 0 : (v <= 34 ? 1 : (v <= 66 ? 2 : 3));
-                s.bit(b + 8, s.probs[b + 8], cat >> 1);
-                s.bit(b + 9 + (cat >> 1), s.probs[b + 9 + (cat >> 1)], cat & 1);
-                const int extra = v - (3 + (8 << cat));
+                const int cat = val <= 18 ? 0 : (val <= 34 ? 1 : (val <= 66 ? 2 : 3));
+                s.node(b + 8, cat >> 1);
+                s.node(b + 9 + (cat >> 1), cat & 1);
+                const int extra = val - (3 + (8 << cat));
                 const int nb = cat == 3 ? 11 : 3 + cat;
-                for (int i = 0; i < nb; ++i) s.bit(-1, kCat[cat][i], (extra >> (nb - 1 - i)) & 1);
+                for (int i = 0; i < nb; ++i) s.fixed(kCat[cat][i], (extra >> (nb - 1 - i)) & 1);
             }
             nctx = 2;
         }
-        if (s.enc) s.enc->put(lv[n] < 0, 128);  // sign
+        s.fixed(128, lvn < 0);  // sign
         ++n;
         if (n == 16) return 1;
         b = base(n, nctx);
         if (n >= last) {
-            s.bit(b + 0, s.probs[b + 0], 0);
+            s.node(b + 0, 0);
             return 1;
         }
     }
 }
 
+// One MB of a compact stream (layout in ik_vp8_gpu.h): modes, and per block a
+// pointer to its u16 coefficient mask + nonzero levels (null: all zero).
+struct PackedMB {
+    uint8_t ymode, uvmode, skip;
+    const uint8_t* bmodes;  // 16 (B_PRED only)
+    const uint8_t* blk[25];
+};
+
+// parse the record at p (bounded by end); returns the next record or null
+const uint8_t* parse_mb(const uint8_t* p, const uint8_t* end, PackedMB& m) {
+    if (end - p < 8) return nullptr;
+    m.ymode = p[0];
+    m.uvmode = p[1];
+    m.skip = p[2];
+    uint32_t nzmask;
+    std::memcpy(&nzmask, p + 4, 4);
+    p += 8;
+    m.bmodes = nullptr;
+    if (m.ymode == B_PRED) {
+        if (end - p < 16) return nullptr;
+        m.bmodes = p;
+        p += 16;
+    }
+    for (int b = 0; b < 25; ++b) {
+        m.blk[b] = nullptr;
+        if (!((nzmask >> b) & 1)) continue;
+        if (end - p < 2) return nullptr;
+        uint16_t cm;
+        std::memcpy(&cm, p, 2);
+        const long n = 2 + 2 * __builtin_popcount(cm);
+        if (end - p < n) return nullptr;
+        m.blk[b] = p;
+        p += n;
+    }
+    return p;
+}
+
 // all residual tokens of the frame, with the decoder's non-zero contexts
-void write_tokens(TokenSink& s, int mb_w, int mb_h, const MBOut* mbs, bool use_skip) {
+void write_tokens(TokenSink& s, int mb_w, int mb_h, const uint8_t* const* recs, const uint8_t* end, bool use_skip) {
     std::vector<uint8_t> top((size_t)mb_w * 9, 0);
+    PackedMB m;
     for (int my = 0; my < mb_h; ++my) {
         uint8_t left[9] = {0};
         for (int mx = 0; mx < mb_w; ++mx) {
-            const MBOut& m = mbs[(size_t)my * mb_w + mx];
+            parse_mb(recs[(size_t)my * mb_w + mx], end, m);  // validated by index_records
             uint8_t* t = &top[(size_t)mx * 9];
             const bool i4 = m.ymode == B_PRED;
+            s.reserve_mb();
             if (use_skip && m.skip) {
                 for (int i = 0; i < 8; ++i) t[i] = left[i] = 0;
                 if (!i4) t[8] = left[8] = 0;
@@ -161,28 +236,81 @@ void write_tokens(TokenSink& s, int mb_w, int mb_h, const MBOut* mbs, bool use_s
             }
             int first = 0, ytype = 3;
             if (!i4) {
-                const int nz = write_block(s, m.lv[24], 0, t[8] + left[8], 1);
+                const int nz = write_block(s, m.blk[24], 0, t[8] + left[8], 1);
                 t[8] = left[8] = (uint8_t)nz;
                 first = 1;
                 ytype = 0;
             }
             for (int y = 0; y < 4; ++y)
                 for (int x = 0; x < 4; ++x) {
-                    const int nz = write_block(s, m.lv[y * 4 + x], first, t[x] + left[y], ytype);
+                    const int nz = write_block(s, m.blk[y * 4 + x], first, t[x] + left[y], ytype);
                     t[x] = left[y] = (uint8_t)nz;
                 }
             for (int ch = 0; ch < 2; ++ch)
                 for (int y = 0; y < 2; ++y)
                     for (int x = 0; x < 2; ++x) {
-                        const int nz = write_block(s, m.lv[16 + 4 * ch + y * 2 + x], 0,
+                        const int nz = write_block(s, m.blk[16 + 4 * ch + y * 2 + x], 0,
                                                    t[4 + 2 * ch + x] + left[4 + 2 * ch + y], 2);
                         t[4 + 2 * ch + x] = left[4 + 2 * ch + y] = (uint8_t)nz;
                     }
         }
+        s.row_end.push_back(s.size());
     }
 }
 
-void put_bmode(BoolEnc& e, int mode, int top, int left) {
+// Code the token streams (the first partition, then the token partitions: MB row
+// r -> partition r % K) with their boolean coders interleaved: each coder is one
+// long dependency chain, so several side by side keep the core busy.  Streams
+// are taken shortest first: positions [from, to) run on the A that are still
+// that long.
+struct Strm {
+    const uint16_t* p;
+    size_t n;
+    BoolEnc* e;
+};
+
+template <int A>
+void code_span(const Strm* st, size_t from, size_t to, const uint8_t* ptab) {
+    BoolEnc e[A];  // coder state in locals (registers) for the span
+    const uint16_t* p[A];
+    for (int k = 0; k < A; ++k) { e[k] = std::move(*st[k].e); p[k] = st[k].p; }
+    for (size_t i = from; i < to; ++i)
+#pragma GCC unroll 8
+        for (int k = 0; k < A; ++k) e[k].put(p[k][i] >> 15, ptab[p[k][i] & 0x7ff]);
+    for (int k = 0; k < A; ++k) *st[k].e = std::move(e[k]);
+}
+
+void code_streams(Strm* st, int S, const uint8_t* ptab) {
+    std::sort(st, st + S, [](const Strm& a, const Strm& b) { return a.n < b.n; });
+    size_t done = 0;
+    for (int j = 0; j < S; ++j) {
+        const int A = S - j;
+        const size_t to = st[j].n;
+        if (to > done) {
+            switch (A) {
+            case 5: code_span<5>(st + j, done, to, ptab); break;
+            case 4: code_span<4>(st + j, done, to, ptab); break;
+            case 3: code_span<3>(st + j, done, to, ptab); break;
+            case 2: code_span<2>(st + j, done, to, ptab); break;
+            default: code_span<1>(st + j, done, to, ptab); break;
+            }
+            done = to;
+        }
+    }
+}
+
+// records first-partition decisions as fixed-probability tokens, so the header
+// is coded side by side with the token partitions
+struct RecEnc {
+    std::vector<uint16_t> toks;
+    void put(int bit, int prob) { toks.push_back((uint16_t)((1056 + prob) | (bit << 15))); }
+    void literal(int v, int n) {
+        for (int i = n - 1; i >= 0; --i) put((v >> i) & 1, 128);
+    }
+};
+
+template <class E>
+void put_bmode(E& e, int mode, int top, int left) {
     const uint8_t* p = kBModeProbs + (top * 10 + left) * 9;
     switch (mode) {
     case B_DC: e.put(0, p[0]); return;
@@ -216,25 +344,72 @@ int quality_to_qindex(float quality) {
     return q < 0 ? 0 : (q > 127 ? 127 : q);
 }
 
+void pack_mbs(const MBOut* mbs, size_t nmb, std::vector<uint8_t>& out) {
+    out.assign(kPackHeader, 0);
+    for (size_t i = 0; i < nmb; ++i) {
+        const MBOut& o = mbs[i];
+        uint32_t nzmask = 0;
+        for (int b = 0; b < 25; ++b)
+            for (int n = 0; n < 16; ++n)
+                if (o.lv[b][n]) nzmask |= 1u << b;
+        const uint8_t hdr[4] = {o.ymode, o.uvmode, o.skip, 0};
+        out.insert(out.end(), hdr, hdr + 4);
+        out.insert(out.end(), (const uint8_t*)&nzmask, (const uint8_t*)&nzmask + 4);
+        if (o.ymode == B_PRED) out.insert(out.end(), o.bmodes, o.bmodes + 16);
+        for (int b = 0; b < 25; ++b) {
+            if (!((nzmask >> b) & 1)) continue;
+            uint16_t cm = 0;
+            for (int n = 0; n < 16; ++n) cm |= (uint16_t)((o.lv[b][n] != 0) << n);
+            out.insert(out.end(), (const uint8_t*)&cm, (const uint8_t*)&cm + 2);
+            for (int n = 0; n < 16; ++n)
+                if (o.lv[b][n]) out.insert(out.end(), (const uint8_t*)&o.lv[b][n], (const uint8_t*)&o.lv[b][n] + 2);
+        }
+    }
+    const uint32_t h[4] = {(uint32_t)out.size(), (uint32_t)nmb, kPackMagicHost, 0};
+    std::memcpy(out.data(), h, sizeof(h));
+}
+
 QParams qparams_for_quality(float quality) { return make_qparams(quality_to_qindex(quality), -2); }
 
-void write_webp(int width, int height, const QParams& q, const MBOut* mbs, int filter_level,
-                std::vector<uint8_t>& out) {
+bool write_webp_packed(int width, int height, const QParams& q, const uint8_t* pack, size_t cap, int filter_level,
+                       std::vector<uint8_t>& out) {
     const int mb_w = (width + 15) >> 4, mb_h = (height + 15) >> 4;
     const size_t nmb = (size_t)mb_w * mb_h;
+    // 0. the records: validate the stream once, keep each MB's start
+    uint32_t hdr[4];
+    if (cap < sizeof(hdr)) return false;
+    std::memcpy(hdr, pack, sizeof(hdr));
+    if (hdr[2] != kPackMagicHost || hdr[1] != nmb || hdr[0] > cap || hdr[0] < sizeof(hdr)) return false;
+    const uint8_t* end = pack + hdr[0];
+    static thread_local std::vector<const uint8_t*> recs;
+    recs.resize(nmb);
+    size_t nskip = 0;
+    {
+        const uint8_t* r = pack + sizeof(hdr);
+        PackedMB m;
+        for (size_t i = 0; i < nmb; ++i) {
+            recs[i] = r;
+            r = parse_mb(r, end, m);
+            if (!r) return false;
+            // y: DC/TM/V/H (0..3) or B_PRED; uv: DC/TM/V/H
+            if ((m.ymode > 3 && m.ymode != B_PRED) || m.uvmode > 3) return false;
+            if (m.bmodes)
+                for (int b = 0; b < 16; ++b)
+                    if (m.bmodes[b] >= NUM_BMODES) return false;
+            nskip += m.skip;
+        }
+        if (r != end) return false;
+    }
     // 1. token statistics under the frame's structure -> adapted probabilities
     std::vector<uint32_t> cnt(1056 * 2, 0);
-    size_t nskip = 0;
-    for (size_t i = 0; i < nmb; ++i) nskip += mbs[i].skip;
     const bool use_skip = nskip > 0;
     uint8_t probs[1056];
     std::memcpy(probs, kCoeffProbs0, sizeof(probs));
-    {
-        TokenSink s;
-        s.counts = reinterpret_cast<uint32_t(*)[2]>(cnt.data());
-        s.probs = probs;
-        write_tokens(s, mb_w, mb_h, mbs, use_skip);
-    }
+    TokenSink s;
+    s.counts = reinterpret_cast<uint32_t(*)[2]>(cnt.data());
+    s.toks.resize(nmb * 128);
+    s.w = s.toks.data();
+    write_tokens(s, mb_w, mb_h, recs.data(), end, use_skip);
     bool upd[1056];
     for (int i = 0; i < 1056; ++i) {
         upd[i] = false;
@@ -252,8 +427,8 @@ void write_webp(int width, int height, const QParams& q, const MBOut* mbs, int f
         skip_prob = (int)((nmb - nskip) * 255 / nmb);
         skip_prob = skip_prob < 1 ? 1 : (skip_prob > 254 ? 254 : skip_prob);
     }
-    // 2. first partition: header + per-MB modes
-    BoolEnc h;
+    // 2. first partition: header + per-MB modes (recorded, coded in step 3)
+    RecEnc h;
     h.literal(0, 1);  // color_space
     h.literal(0, 1);  // clamping_type
     h.literal(0, 1);  // segmentation_enabled
@@ -261,7 +436,9 @@ void write_webp(int width, int height, const QParams& q, const MBOut* mbs, int f
     h.literal(filter_level < 0 ? q.filter_level : filter_level, 6);
     h.literal(0, 3);  // sharpness
     h.literal(0, 1);  // loop_filter_adj_enable
-    h.literal(0, 2);  // one token partition
+    // token partitions: 4 (2, 1 for frames of fewer MB rows)
+    const int log2k = mb_h >= 4 ? 2 : (mb_h >= 2 ? 1 : 0), K = 1 << log2k;
+    h.literal(log2k, 2);
     h.literal(q.qindex, 7);
     const int deltas[5] = {0, 0, 0, q.dq_uv_dc, 0};  // y_dc, y2_dc, y2_ac, uv_dc, uv_ac
     for (int d : deltas) {
@@ -281,7 +458,8 @@ void write_webp(int width, int height, const QParams& q, const MBOut* mbs, int f
     for (int my = 0; my < mb_h; ++my) {
         uint8_t left_modes[4] = {B_DC, B_DC, B_DC, B_DC};
         for (int mx = 0; mx < mb_w; ++mx) {
-            const MBOut& m = mbs[(size_t)my * mb_w + mx];
+            PackedMB m;
+            parse_mb(recs[(size_t)my * mb_w + mx], end, m);
             uint8_t* tm = &top_modes[(size_t)mx * 4];
             if (use_skip) h.put(m.skip, skip_prob);
             if (m.ymode == B_PRED) {
@@ -311,26 +489,36 @@ void write_webp(int width, int height, const QParams& q, const MBOut* mbs, int f
             }
         }
     }
-    h.flush();
-    // 3. token partition
-    BoolEnc t;
-    {
-        TokenSink s;
-        s.enc = &t;
-        s.probs = probs;
-        write_tokens(s, mb_w, mb_h, mbs, use_skip);
+    // 3. the first partition and the token partitions, coded together
+    std::vector<uint16_t> part[5];
+    part[0].swap(h.toks);
+    for (int r = 0; r < mb_h; ++r) {
+        const size_t b0 = r ? s.row_end[r - 1] : 0, b1 = s.row_end[r];
+        part[1 + r % K].insert(part[1 + r % K].end(), s.toks.data() + b0, s.toks.data() + b1);
     }
-    t.flush();
+    BoolEnc t[5];
+    for (int k = 0; k <= K; ++k) t[k].out.reserve(part[k].size() / 4 + 64);
+    uint8_t ptab[1056 + 256];
+    std::memcpy(ptab, probs, 1056);
+    for (int i = 0; i < 256; ++i) ptab[1056 + i] = (uint8_t)i;
+    Strm st[5];
+    for (int k = 0; k <= K; ++k) st[k] = Strm{part[k].data(), part[k].size(), &t[k]};
+    code_streams(st, K + 1, ptab);
+    for (int k = 0; k <= K; ++k) t[k].flush();
     // 4. frame + container
     std::vector<uint8_t> vp8;
-    const uint32_t first = (uint32_t)h.out.size();
+    const uint32_t first = (uint32_t)t[0].out.size();
     const uint32_t tag = 0u | (0u << 1) | (1u << 4) | (first << 5);  // key frame, v0, shown
     vp8.push_back((uint8_t)tag); vp8.push_back((uint8_t)(tag >> 8)); vp8.push_back((uint8_t)(tag >> 16));
     vp8.push_back(0x9d); vp8.push_back(0x01); vp8.push_back(0x2a);
     vp8.push_back((uint8_t)width); vp8.push_back((uint8_t)(width >> 8));
     vp8.push_back((uint8_t)height); vp8.push_back((uint8_t)(height >> 8));
-    vp8.insert(vp8.end(), h.out.begin(), h.out.end());
-    vp8.insert(vp8.end(), t.out.begin(), t.out.end());
+    vp8.insert(vp8.end(), t[0].out.begin(), t[0].out.end());
+    for (int k = 1; k < K; ++k) {  // sizes of all token partitions but the last, 3 bytes LE
+        const uint32_t sz = (uint32_t)t[k].out.size();
+        vp8.push_back((uint8_t)sz); vp8.push_back((uint8_t)(sz >> 8)); vp8.push_back((uint8_t)(sz >> 16));
+    }
+    for (int k = 1; k <= K; ++k) vp8.insert(vp8.end(), t[k].out.begin(), t[k].out.end());
     const uint32_t vsize = (uint32_t)vp8.size(), pad = vsize & 1;
     out.clear();
     out.reserve(20 + vsize + pad);
@@ -340,6 +528,15 @@ void write_webp(int width, int height, const QParams& q, const MBOut* mbs, int f
     le32(out, vsize);
     out.insert(out.end(), vp8.begin(), vp8.end());
     if (pad) out.push_back(0);
+    return true;
+}
+
+void write_webp(int width, int height, const QParams& q, const MBOut* mbs, int filter_level,
+                std::vector<uint8_t>& out) {
+    const size_t nmb = (size_t)((width + 15) >> 4) * ((height + 15) >> 4);
+    std::vector<uint8_t> pack;
+    pack_mbs(mbs, nmb, pack);
+    write_webp_packed(width, height, q, pack.data(), pack.size(), filter_level, out);
 }
 
 }  // namespace vp8

@@ -2,6 +2,7 @@
 // after the macroblock decisions -- coefficient-probability adaptation, the
 // boolean entropy coder, the frame header and the RIFF/WEBP container.
 #pragma once
+#include <cstddef>
 #include <cstdint>
 #include <vector>
 
@@ -22,6 +23,14 @@ QParams qparams_for_quality(float quality);
 // decisions in `mbs`.  `filter_level` < 0 uses q.filter_level.
 void write_webp(int width, int height, const QParams& q, const MBOut* mbs, int filter_level,
                 std::vector<uint8_t>& out);
+
+// The same bitstream from the compact MB stream k_vp8_pack writes (layout in
+// ik_vp8_gpu.h; at most cap bytes): false, and no output, when it is malformed.
+bool write_webp_packed(int width, int height, const QParams& q, const uint8_t* pack, size_t cap, int filter_level,
+                       std::vector<uint8_t>& out);
+
+// the host form of k_vp8_pack (same bytes) for records already on the host
+void pack_mbs(const MBOut* mbs, size_t nmb, std::vector<uint8_t>& out);
 
 // zigzag index after the last nonzero level of a block (== first when none)
 int last_nz(const int16_t* lv, int first);

@@ -26,6 +26,20 @@ inline size_t vp8_rec_bytes(int w, int h) {
     return mw * 16 * mh * 16 + 2 * mw * 8 * mh * 8;
 }
 
+// Compact MB stream of one image (k_vp8_pack -> host), cap bytes per image:
+//   PackHeader {u32 bytes (header included), u32 mb count, u32 kPackMagic, u32 0}
+//   per MB, raster order: u8 ymode, u8 uvmode, u8 skip, u8 0, u32 nzmask (bit b:
+//   block b of MBOut.lv has a nonzero level); if ymode == B_PRED u8 bmodes[16];
+//   then per set bit of nzmask, in block order: u16 coefficient mask (bit n:
+//   lv[b][n] != 0), then the nonzero levels as int16, in coefficient order.
+constexpr int kPackHeaderBytes = 16;
+constexpr uint32_t kPackMagic = 0x4b503856u;  // "V8PK"
+constexpr int kMaxPackMBs = 4096;             // one image's MBs (scan in LDS): 1024x1024
+constexpr size_t kPackMaxMBBytes = 8 + 16 + 25 * (2 + 32);
+inline size_t vp8_pack_cap(size_t nmb) { return (kPackHeaderBytes + nmb * kPackMaxMBBytes + 15) & ~(size_t)15; }
+hipError_t launch_vp8_pack(const MBOut* mbs, int nmb, int n, uint8_t* scratch, uint8_t* host_dst, size_t cap_img,
+                           hipStream_t s);
+
 // the whole wavefront for n images: (mb_w-1) + 2*(mb_h-1) + 1 launches on stream s
 hipError_t launch_vp8_encode(const Vp8Args& a, int n, hipStream_t s);
 

@@ -1,7 +1,8 @@
 // ik_webp_gpu.cpp -- driver of the GPU WebP encoder (encode_image's WebP branch,
 // reference src/transform.rs:129-137, as an alternative to libwebp on the host):
-// device YUV420 planes -> k_vp8_diag wavefront (ik_vp8.hip) -> MB records D2H ->
-// bitstream + RIFF on the host (ik_vp8_enc.cpp).
+// device YUV420 planes -> k_vp8_diag wavefront (ik_vp8.hip) -> k_vp8_pack (compact
+// MB records written into pinned host memory; a plain D2H of the records for
+// frames over 4096 MBs) -> bitstream + RIFF on the host (ik_vp8_enc.cpp).
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -45,6 +46,10 @@ int Vp8Work::reserve(int w_, int h_, int n_) {
     IK_HIP(hipMalloc(&d_mbs, sizeof(vp8::MBOut) * nmb * n_ + 256));
     IK_HIP(hipMalloc(&d_nz, 18 * nmb * n_ + 256));
     IK_HIP(hipHostMalloc(&h_mbs, sizeof(vp8::MBOut) * nmb * n_, hipHostMallocDefault));
+    if (nmb <= (size_t)vp8::kMaxPackMBs) {
+        IK_HIP(hipMalloc(&d_pack, vp8::vp8_pack_cap(nmb) * n_));
+        IK_HIP(hipHostMalloc(&h_pack, vp8::vp8_pack_cap(nmb) * n_, hipHostMallocDefault));
+    }
     w = w_; h = h_; cap_n = n_;
     return IK_OK;
 }
@@ -54,7 +59,9 @@ void Vp8Work::release() {
     if (d_mbs) (void)hipFree(d_mbs);
     if (d_nz) (void)hipFree(d_nz);
     if (h_mbs) (void)hipHostFree(h_mbs);
-    d_rec = nullptr; d_mbs = nullptr; d_nz = nullptr; h_mbs = nullptr;
+    if (d_pack) (void)hipFree(d_pack);
+    if (h_pack) (void)hipHostFree(h_pack);
+    d_rec = nullptr; d_mbs = nullptr; d_nz = nullptr; h_mbs = nullptr; d_pack = nullptr; h_pack = nullptr;
     w = h = cap_n = 0;
 }
 
@@ -102,6 +109,23 @@ void Vp8Work::write_from(const vp8::MBOut* recs, int i, int quality, std::vector
     vp8::write_webp(w, h, q, recs + mb_count() * (size_t)i, -1, out);
 }
 
+bool Vp8Work::packable() const { return d_pack != nullptr; }
+
+size_t Vp8Work::pack_cap() const { return vp8::vp8_pack_cap(mb_count()); }
+
+int Vp8Work::pack_to(uint8_t* host_dst, int n, hipStream_t s) {
+    if (!d_pack || n > cap_n) return fail(IK_ERR_INVALID, "VP8 pack buffers not reserved");
+    IK_HIP(vp8::launch_vp8_pack(d_mbs, (int)mb_count(), n, d_pack, host_dst, pack_cap(), s));
+    return IK_OK;
+}
+
+int Vp8Work::write_packed(const uint8_t* pack_img, int quality, std::vector<uint8_t>& out) const {
+    const vp8::QParams q = vp8::qparams_for_quality((float)quality);
+    if (!vp8::write_webp_packed(w, h, q, pack_img, pack_cap(), -1, out))
+        return fail(IK_ERR_DEVICE, "malformed VP8 macroblock stream from the device");
+    return IK_OK;
+}
+
 // one image from device YUV420 planes, on the calling thread's stream
 int webp_encode_gpu(const uint8_t* d_yuv, int w, int h, int quality, std::vector<uint8_t>& out) {
     if (w < 1 || h < 1 || w > 16383 || h > 16383) return fail(IK_ERR_TRANSFORM, "WebP dimensions %dx%d out of range", w, h);
@@ -111,6 +135,11 @@ int webp_encode_gpu(const uint8_t* d_yuv, int w, int h, int quality, std::vector
     if (!s) return fail(IK_ERR_DEVICE, "cannot create HIP stream");
     if (int rc = wk.reserve(w, h, 1)) return rc;
     if (int rc = wk.launch(d_yuv, 0, 1, quality, s)) return rc;
+    if (wk.packable()) {
+        if (int rc = wk.pack_to(wk.h_pack, 1, s)) return rc;
+        IK_HIP(hipStreamSynchronize(s));
+        return wk.write_packed(wk.h_pack, quality, out);
+    }
     if (int rc = wk.fetch(1, s)) return rc;
     IK_HIP(hipStreamSynchronize(s));
     wk.write(0, quality, out);

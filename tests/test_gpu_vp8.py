@@ -133,3 +133,12 @@ def test_pipeline_gpu_encoder_batch(ik, oracle):
         off += sizes[i]
         Y, U, V = oracle.webp_yuv420(oracle.to_rgb8(oracle.resize(im, nw, nh, 4)))
         assert b == vp8.encode(Y, U, V, 80.0, -1)[0]
+
+
+def test_gpu_large_frame_unpacked_records(ik, oracle):
+    """Frames over 4096 MBs (here 65 x 65) skip the compact-record packer and copy
+    the full MB records: same bytes as the scalar encoder."""
+    rgb = ikutil.synth(1040, 1040, 3, seed=5, pattern="S")
+    Y, U, V = oracle.webp_yuv420(rgb)
+    want, _ = vp8.encode(Y, U, V, 80.0, -1)
+    assert _gpu_encode_planes(ik, Y, U, V, 80) == want

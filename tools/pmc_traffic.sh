@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out && cp profiles/pmc_resize.json gpurun_out/pmc_resize.json
 export IK_PMC_OUT=gpurun_out/pmc_resize.json
 B=${B:-32}
-args="bench.py --no-cpu-baseline --warmup 2 --steps 2 --batch $B"
+args="bench.py --no-cpu-baseline --no-alt-encoder --warmup 2 --steps 2 --batch $B"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcF -o run -f csv -- python $args > gpurun_out/pmcF.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcW -o run -f csv -- python $args > gpurun_out/pmcW.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcC -o run -f csv -- python tools/bw_probe.py 0 > gpurun_out/pmcC.log 2>&1 && \

@@ -5,6 +5,7 @@
 #include <cstring>
 
 #include <algorithm>
+#include <chrono>
 
 #include "../rust-image-transform_amd/csrc/ik_vp8_enc.h"
 
@@ -147,4 +148,20 @@ extern "C" int vp8_dev_pred4_mismatches(unsigned seed, int trials) {
         }
     }
     return bad;
+}
+
+// host bitstream cost: mean seconds of write_webp_packed over `reps` runs on the
+// scalar encoder's MB records (the host stage of the GPU WebP encoder)
+extern "C" double vp8_dev_write_seconds(const uint8_t* y, const uint8_t* u, const uint8_t* v, int w, int h,
+                                        float quality, int reps) {
+    using namespace ik::vp8;
+    const QParams q = qparams_for_quality(quality);
+    std::vector<MBOut> mbs;
+    encode_frame_scalar(y, u, v, w, h, q, mbs, nullptr);
+    std::vector<uint8_t> bytes, pack;
+    pack_mbs(mbs.data(), mbs.size(), pack);
+    write_webp_packed(w, h, q, pack.data(), pack.size(), -1, bytes);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < reps; ++i) write_webp_packed(w, h, q, pack.data(), pack.size(), -1, bytes);
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / reps;
 }

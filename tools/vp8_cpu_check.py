@@ -8,7 +8,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import ikutil
 so = "/tmp/vp8_cpu_check.so"
-subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", so,
+subprocess.check_call(["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-o", so,
                        os.path.join(ROOT, "tools/vp8_cpu_check.cpp"),
                        os.path.join(ROOT, "rust-image-transform_amd/csrc/ik_vp8_enc.cpp")])
 lib = ctypes.CDLL(so)
