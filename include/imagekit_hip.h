@@ -71,6 +71,14 @@ void ik_buf_free(uint8_t *buf);
  * *fmt_out = IK_FORMAT_* for webp/jpeg/avif, -1 (None) for other formats. */
 int ik_decode(const uint8_t *bytes, size_t len, ik_image **out, int *fmt_out);
 
+/* decode_image over n inputs at once (the /img handler under load).  JPEGs whose
+ * scan has restart intervals are entropy-decoded by ONE GPU launch (one lane per
+ * interval, all images together) and reconstructed on the GPU; other inputs go
+ * through ik_decode.  outs[i] / fmts[i] / status[i] per input (outs[i] NULL on
+ * failure; fmts and status may be NULL); returns the first failure or IK_OK. */
+int ik_decode_batch(const uint8_t *const *bytes, const size_t *lens, uint32_t n, ik_image **outs,
+                    int *fmts, int *status);
+
 /* resize_image (src/transform.rs:62-90).  w/h < 0 mean None.  Both None returns
  * the input unchanged (*out == img); otherwise a new image (img is not freed:
  * the Rust shim drops its by-value argument).  filter: IK_FILTER_* (Lanczos3 in

@@ -436,6 +436,43 @@ int ik_decode(const uint8_t* bytes, size_t len, ik_image** out, int* fmt_out) {
     return IK_OK;
 }
 
+int ik_decode_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t n, ik_image** outs, int* fmts,
+                    int* status) {
+    if (!bytes || !lens || !outs || !n) return fail(IK_ERR_INVALID, "bad batch");
+    std::vector<const uint8_t*> jb;
+    std::vector<size_t> jl;
+    std::vector<uint32_t> ji;
+    std::vector<int> st(n, IK_OK);
+    for (uint32_t i = 0; i < n; ++i) {
+        outs[i] = nullptr;
+        if (fmts) fmts[i] = -1;
+        if (!bytes[i] && lens[i]) { st[i] = fail(IK_ERR_INVALID, "null bytes"); continue; }
+        if (guess_format(bytes[i], lens[i]) == Sniffed::Jpeg) {
+            jb.push_back(bytes[i]);
+            jl.push_back(lens[i]);
+            ji.push_back(i);
+            if (fmts) fmts[i] = IK_FORMAT_JPEG;
+        } else {
+            st[i] = ik_decode(bytes[i], lens[i], &outs[i], fmts ? &fmts[i] : nullptr);
+        }
+    }
+    if (!ji.empty()) {
+        std::vector<ik_image*> jo(ji.size(), nullptr);
+        std::vector<int> js(ji.size(), IK_OK);
+        decode_jpeg_batch(jb.data(), jl.data(), (int)ji.size(), jo.data(), js.data());
+        for (size_t k = 0; k < ji.size(); ++k) {
+            outs[ji[k]] = jo[k];
+            st[ji[k]] = js[k];
+        }
+    }
+    int first = IK_OK;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (status) status[i] = st[i];
+        if (st[i] && !first) first = st[i];
+    }
+    return first;
+}
+
 int ik_transform(const uint8_t* bytes, size_t len, int64_t w, int64_t h, int fmt, int quality,
                  int filter, uint8_t** out, size_t* out_len) {
     ik_image* img = nullptr;

@@ -95,6 +95,35 @@ struct JpegGeom {
 };
 hipError_t launch_jpeg_reconstruct(const JpegGeom& g, uint8_t* dst, size_t dst_pitch, hipStream_t s);
 
+// Baseline Huffman decoding on the GPU, one thread per restart interval
+// (ik_jpeg.hip k_jpeg_huff).  Tables: 4 DC then 4 AC, canonical form plus a 9-bit
+// lookahead (look = length << 8 | value, length 0 = longer code).
+struct JpegHuffTables {
+    uint16_t look[8][512];
+    int maxcode[8][18], valptr[8][17], mincode[8][17];
+    int lj[8][17];  // left-justified 16-bit bound of the codes up to each length (carried over empty lengths)
+    uint8_t vals[8][256];
+};
+struct JpegScanArgs {
+    const uint8_t* data;          // the scan's entropy-coded bytes (stuffed, with RST markers)
+    long long size;
+    const unsigned* seg;          // first byte of each restart interval (n_seg entries)
+    int n_seg, restart;           // intervals, MCUs per interval
+    long long total_mcu;
+    int mcux;                     // MCUs per row (interleaved scans)
+    int single, single_bw;        // one-component scan: an MCU is one block, single_bw per row
+    int ns;                       // components in the scan, in scan order:
+    int h[4], v[4], bw[4], td[4], ta[4];
+    long long blk0[4];
+    const JpegHuffTables* tabs;
+    int16_t* coef;                // [block][64] natural order, pre-zeroed
+    int* err;                     // set non-zero on a bad code (the host then redoes the scan)
+    int lanes;                    // intervals per 64-lane workgroup (64, or fewer to cut divergence)
+};
+hipError_t launch_jpeg_huff(const JpegScanArgs& a, hipStream_t s);
+// n scans in one launch (dev_scans: device array of n JpegScanArgs; max_seg = most intervals)
+hipError_t launch_jpeg_huff_batch(const JpegScanArgs* dev_scans, int n, int max_seg, hipStream_t s);
+
 // ---- plans (ik_plan.cpp) ----
 // sample.rs weights for one axis; returns the tap count T (row stride of w).
 int axis_weights(int in, int out, int filter, std::vector<int>& left, std::vector<int>& cnt,

@@ -188,6 +188,220 @@ __global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restr
 
 }  // namespace
 
+// ---- baseline Huffman decoding, one thread per restart interval ---------------
+// A restart interval is self-contained: the DC predictors reset and the bit
+// stream realigns at its RSTn marker, so the host only has to find the markers
+// (a byte scan) and each lane decodes its interval's MCUs into the dense
+// coefficient image with the same rules as the host decoder (ITU T.81 F.2.2,
+// libjpeg jdhuff.c): byte-stuffed 0xFF 0x00, zeros fed past a marker, 9-bit
+// lookahead then the canonical maxcode walk.  Tables live in LDS.
+namespace {
+
+constexpr int kHuffThreads = 64;
+
+__device__ const uint8_t kZz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                    12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                    35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                    58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+// Bit reader over a per-lane LDS ring of the scan bytes.  Global memory is only
+// touched in 64-byte chunks (16 independent dword loads); at every block start
+// all lanes of the wave top their rings up together (a wave vote), so the wave
+// waits for memory once per many blocks instead of once per symbol.
+constexpr int kRingDw = 64;  // 256 bytes per lane
+
+struct GpuBits {
+    const uint32_t* g;  // the scan bytes as dwords (256-B aligned base, padded past the end)
+    uint32_t* ring;     // this lane's ring
+    uint32_t pos, fetched, size;  // next byte, ring filled up to (multiple of 4), scan end
+    unsigned long long acc;
+    int n;
+    bool marker;
+    __device__ void chunk() {
+        uint32_t v[16];
+        const uint32_t d0 = fetched >> 2;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = g[d0 + i];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ring[(d0 + i) & (kRingDw - 1)] = v[i];
+        fetched += 64;
+    }
+    __device__ void top_up() {  // uniform point: every lane ends with >= 128 bytes ahead
+        while (__any((int)(fetched - pos) < 128))  // signed: the ring starts at pos rounded down
+            if ((int)(fetched - pos) < 128) chunk();
+    }
+    __device__ uint32_t byte_at(uint32_t o) const { return (ring[(o >> 2) & (kRingDw - 1)] >> ((o & 3) * 8)) & 0xffu; }
+    __device__ void fill() {
+        while (n <= 56) {
+            uint32_t v = 0;
+            if (!marker && pos < size) {
+                if ((int)(fetched - pos) < 2) chunk();  // a block longer than the lookahead (rare)
+                v = byte_at(pos);
+                if (v == 0xFF) {
+                    const uint32_t nx = pos + 1 < size ? byte_at(pos + 1) : 0;  // 0 past the end, as on the host
+                    if (nx == 0) pos += 2;
+                    else { marker = true; v = 0; }
+                } else {
+                    ++pos;
+                }
+            }
+            acc |= (unsigned long long)v << (56 - n);
+            n += 8;
+        }
+    }
+    __device__ int peek(int k) {
+        if (n < k) fill();
+        return (int)(acc >> (64 - k));
+    }
+    __device__ void skip(int k) { acc <<= k; n -= k; }
+    __device__ int get(int k) {
+        if (!k) return 0;
+        const int v = peek(k);
+        skip(k);
+        return v;
+    }
+};
+
+__device__ __forceinline__ int extend_dev(int v, int t) { return v < (1 << (t - 1)) ? v - (1 << t) + 1 : v; }
+
+__device__ int decode_sym(GpuBits& br, const JpegHuffTables& T, int t) {
+    const int look = br.peek(9);
+    const int lv = T.look[t][look];
+    if (lv >> 8) {
+        br.skip(lv >> 8);
+        return lv & 0xff;
+    }
+    // longer codes: the length is 10 + the number of left-justified bounds the
+    // 16-bit window reaches (canonical codes; one round of LDS reads, no loop)
+    const int code = br.peek(16);
+    int len = 10;
+#pragma unroll
+    for (int l = 10; l <= 16; ++l) len += code >= T.lj[t][l];
+    if (len > 16) return -1;
+    br.skip(len);
+    const int c = code >> (16 - len);
+    return T.vals[t][T.valptr[t][len] + c - T.mincode[t][len]];
+}
+
+}  // namespace
+
+// the whole interval `seg` of scan `a` (tables already in LDS)
+__device__ void huff_interval(const JpegScanArgs& a, const JpegHuffTables& T, const uint8_t* s_zz, uint32_t* ring,
+                              int seg) {
+    GpuBits br;
+    br.g = reinterpret_cast<const uint32_t*>(a.data);
+    br.ring = ring;
+    br.pos = a.seg[seg];
+    br.fetched = br.pos & ~3u;
+    br.size = (uint32_t)a.size;
+    br.acc = 0;
+    br.n = 0;
+    br.marker = false;
+    int pred[4] = {0, 0, 0, 0};
+    const long long m0 = (long long)seg * a.restart;
+    const int nm = (int)min((long long)a.restart, a.total_mcu - m0);
+    // MCU position, advanced incrementally (no 64-bit divisions per block)
+    const int row_len = a.single ? a.single_bw : a.mcux;
+    int mx = (int)(m0 % row_len), my = (int)(m0 / row_len);
+    for (int i = 0; i < nm; ++i) {
+        for (int ci = 0; ci < a.ns; ++ci) {
+            const int nby = a.single ? 1 : a.v[ci], nbx = a.single ? 1 : a.h[ci];
+            for (int by = 0; by < nby; ++by)
+                for (int bx = 0; bx < nbx; ++bx) {
+                    const long long bi = a.single ? a.blk0[ci] + (long long)my * a.bw[ci] + mx
+                                                  : a.blk0[ci] + (long long)(my * a.v[ci] + by) * a.bw[ci] + mx * a.h[ci] + bx;
+                    int16_t* blk = a.coef + bi * 64;
+                    br.top_up();
+                    const int t = decode_sym(br, T, a.td[ci]);
+                    if (t < 0 || t > 11) { atomicOr(a.err, 1); return; }
+                    pred[ci] += t ? extend_dev(br.get(t), t) : 0;
+                    blk[0] = (int16_t)pred[ci];
+                    for (int k = 1; k < 64;) {
+                        const int rs = decode_sym(br, T, 4 + a.ta[ci]);
+                        if (rs < 0) { atomicOr(a.err, 2); return; }
+                        const int r = rs >> 4, sz = rs & 15;
+                        if (!sz) {
+                            if (r != 15) break;  // EOB
+                            k += 16;
+                            continue;
+                        }
+                        k += r;
+                        if (k > 63) { atomicOr(a.err, 4); return; }
+                        blk[s_zz[k]] = (int16_t)extend_dev(br.get(sz), sz);
+                        ++k;
+                    }
+                }
+        }
+        if (++mx == row_len) { mx = 0; ++my; }
+    }
+}
+
+__device__ __forceinline__ void load_tables(const JpegHuffTables* g, JpegHuffTables& T, uint8_t* s_zz) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(g);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&T);
+    for (int i = threadIdx.x; i < (int)(sizeof(JpegHuffTables) / 4); i += kHuffThreads) dst[i] = src[i];
+    if (threadIdx.x < 64) s_zz[threadIdx.x] = kZz[threadIdx.x];
+}
+
+__global__ __launch_bounds__(kHuffThreads) void k_jpeg_huff(JpegScanArgs a) {
+    __shared__ JpegHuffTables T;
+    __shared__ uint8_t s_zz[64];
+    __shared__ uint32_t s_ring[kHuffThreads][kRingDw + 1];  // +1: lanes' rings start in different banks
+    load_tables(a.tabs, T, s_zz);
+    __syncthreads();
+    const int seg = blockIdx.x * a.lanes + threadIdx.x;
+    if ((int)threadIdx.x < a.lanes && seg < a.n_seg) huff_interval(a, T, s_zz, s_ring[threadIdx.x], seg);
+}
+
+// a batch of scans: grid.y = scan, each with its own tables; `lanes` intervals per workgroup
+__global__ __launch_bounds__(kHuffThreads) void k_jpeg_huff_batch(const JpegScanArgs* __restrict__ scans, int lanes) {
+    __shared__ JpegHuffTables T;
+    __shared__ uint8_t s_zz[64];
+    __shared__ uint32_t s_ring[kHuffThreads][kRingDw + 1];  // +1: lanes' rings start in different banks
+    const JpegScanArgs a = scans[blockIdx.y];
+    if ((int)blockIdx.x * lanes >= a.n_seg) return;  // whole workgroup past this scan's intervals
+    load_tables(a.tabs, T, s_zz);
+    __syncthreads();
+    const int seg = blockIdx.x * lanes + threadIdx.x;
+    if ((int)threadIdx.x < lanes && seg < a.n_seg) huff_interval(a, T, s_zz, s_ring[threadIdx.x], seg);
+}
+
+namespace {
+int huff_lanes(int dflt) {
+    static const int forced = [] {
+        const char* e = getenv("IK_HUFF_LANES");
+        return e ? atoi(e) : 0;
+    }();
+    const int v = forced > 0 ? forced : dflt;
+    return v < 1 ? 1 : (v > kHuffThreads ? kHuffThreads : v);
+}
+}  // namespace
+
+hipError_t launch_jpeg_huff(const JpegScanArgs& a, hipStream_t s) {
+    if (a.n_seg <= 0 || a.restart <= 0 || a.ns < 1 || a.ns > 4) return hipErrorInvalidValue;
+    // Lanes of a wave decode different intervals and diverge on every symbol, so a
+    // lone image runs one interval per wave (its waves spread over the CUs);
+    // IK_HUFF_LANES overrides (dev)
+    JpegScanArgs b = a;
+    const int lanes = huff_lanes(1);
+    b.lanes = lanes;
+    hipLaunchKernelGGL(k_jpeg_huff, dim3((a.n_seg + lanes - 1) / lanes), dim3(kHuffThreads), 0, s, b);
+    return hipGetLastError();
+}
+
+hipError_t launch_jpeg_huff_batch(const JpegScanArgs* dev_scans, int n, int max_seg, hipStream_t s) {
+    if (n <= 0 || max_seg <= 0 || n > 65535) return hipErrorInvalidValue;
+    // many intervals: pack total/1024 per wave (about a thousand waves in flight;
+    // measured on 32 x 256 intervals: 1 -> 97 ms, 2 -> 72, 4 -> 59, 8 -> 51 ms)
+    const long long total = (long long)n * max_seg;
+    int want = 1;
+    while (want < 16 && (long long)want * 2 * 1024 <= total) want *= 2;
+    const int lanes = huff_lanes(want);
+    hipLaunchKernelGGL(k_jpeg_huff_batch, dim3((max_seg + lanes - 1) / lanes, n), dim3(kHuffThreads), 0,
+                       s, dev_scans, lanes);
+    return hipGetLastError();
+}
+
 hipError_t launch_jpeg_reconstruct(const JpegGeom& g, uint8_t* dst, size_t dst_pitch, hipStream_t s) {
     if (g.nblocks <= 0 || g.W <= 0 || g.H <= 0) return hipErrorInvalidValue;
     const unsigned nb = (unsigned)((g.nblocks + 255) / 256);

@@ -14,6 +14,12 @@
 // Arithmetic-coded, lossless, hierarchical, 12-bit and CMYK JPEGs report
 // IK_ERR_UNSUPPORTED.
 #include <algorithm>
+#include <thread>
+#include <memory>
+#include <atomic>
+#include <cstdlib>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -132,8 +138,19 @@ struct Decoder {
     int width = 0, height = 0, restart = 0, hmax = 1, vmax = 1, mcux = 0, mcuy = 0;
     bool have_frame = false, progressive = false, adobe = false;
     int adobe_transform = -1;
-    std::vector<int16_t> coef;  // [block][64], natural order, quantised
+    std::vector<int16_t> coef;  // [block][64], natural order, quantised (host-decoded scans only)
+    size_t nblocks = 0;
     int eobrun = 0;
+    // GPU entropy decoding of a baseline scan with restart intervals: the scan is
+    // recorded here (segment starts = first byte after each RSTn) instead of decoded
+    bool try_gpu = false, deferred = false, need_host = false, scanned = false;
+    const uint8_t* gpu_data = nullptr;
+    std::vector<unsigned> gpu_segs;
+    JpegScanArgs gpu_scan{};
+
+    void ensure_coef() {
+        if (coef.empty()) coef.assign(nblocks * 64, 0);
+    }
 
     int16_t* block(const Component& c, int bx, int by) { return &coef[(c.blk0 + (size_t)by * c.bw + bx) * 64]; }
 
@@ -172,7 +189,7 @@ struct Decoder {
             c.blk0 = blocks;
             blocks += (size_t)c.bw * c.bh;
         }
-        coef.assign(blocks * 64, 0);
+        nblocks = blocks;
         have_frame = true;
         return IK_OK;
     }
@@ -272,6 +289,69 @@ struct Decoder {
         return IK_OK;
     }
 
+    // Record a baseline scan for k_jpeg_huff: find its restart markers (the end of
+    // the scan is the first other marker).  False (decode on the host) when the
+    // marker count does not match the MCU count.
+    bool defer_scan(const std::vector<int>& order, const uint8_t* data, const uint8_t*& next) {
+        const bool single = order.size() == 1;
+        const Component& c0 = comps[order[0]];
+        const int single_bw = (c0.dw + 7) / 8, single_bh = (c0.dh + 7) / 8;
+        const long long total_mcu = single ? (long long)single_bw * single_bh : (long long)mcux * mcuy;
+        const long long want = (total_mcu + restart - 1) / restart;
+        gpu_segs.assign(1, 0u);
+        const uint8_t* q = data;
+        while (q + 1 < end) {
+            if (q[0] != 0xFF) { ++q; continue; }
+            const uint8_t m = q[1];
+            if (m == 0x00) { q += 2; continue; }
+            if (m == 0xFF) { ++q; continue; }
+            if (m >= 0xD0 && m <= 0xD7) {
+                if ((long long)gpu_segs.size() >= want) break;  // a marker past the last interval: let the host judge
+                gpu_segs.push_back((unsigned)(q + 2 - data));
+                q += 2;
+                continue;
+            }
+            break;
+        }
+        if ((long long)gpu_segs.size() != want || (size_t)(end - data) > 0xffffffffu) return false;
+        JpegScanArgs& a = gpu_scan;
+        a = JpegScanArgs{};
+        a.size = (long long)(end - data);
+        a.n_seg = (int)want;
+        a.restart = restart;
+        a.total_mcu = total_mcu;
+        a.mcux = mcux;
+        a.single = single ? 1 : 0;
+        a.single_bw = single_bw;
+        a.ns = (int)order.size();
+        for (int i = 0; i < a.ns; ++i) {
+            const Component& c = comps[order[i]];
+            a.h[i] = c.h; a.v[i] = c.v; a.bw[i] = c.bw; a.td[i] = c.td; a.ta[i] = c.ta;
+            a.blk0[i] = (long long)c.blk0;
+        }
+        gpu_data = data;
+        deferred = true;
+        next = q;
+        return true;
+    }
+
+    void tables(JpegHuffTables& t) const {
+        std::memset(&t, 0, sizeof(t));
+        for (int k = 0; k < 8; ++k) {
+            const HuffTable& h = k < 4 ? dc[k] : ac[k - 4];
+            for (int i = 0; i < 512; ++i) t.look[k][i] = (uint16_t)(h.look_len[i] << 8 | h.look_val[i]);
+            std::memcpy(t.maxcode[k], h.maxcode, sizeof(h.maxcode));
+            std::memcpy(t.valptr[k], h.valptr, sizeof(h.valptr));
+            std::memcpy(t.mincode[k], h.mincode, sizeof(h.mincode));
+            std::memcpy(t.vals[k], h.vals, sizeof(h.vals));
+            int carry = 0;
+            for (int l = 1; l <= 16; ++l) {
+                if (h.maxcode[l] >= 0) carry = (h.maxcode[l] + 1) << (16 - l);
+                t.lj[k][l] = carry;
+            }
+        }
+    }
+
     int scan(const uint8_t* s, const uint8_t* se, const uint8_t*& next) {
         if (!have_frame) return fail(IK_ERR_TRANSFORM, "%s: SOS before SOF", kFmtErr);
         const int ns = s[0];
@@ -307,6 +387,15 @@ struct Decoder {
             if ((need_dc && !dc[c.td].present) || (need_ac && !ac[c.ta].present))
                 return fail(IK_ERR_TRANSFORM, "%s: missing Huffman table", kFmtErr);
         }
+        if (deferred) {  // a second scan: the whole image goes through the host decoder
+            need_host = true;
+            return IK_OK;
+        }
+        const bool first_scan = !scanned;
+        scanned = true;
+        if (try_gpu && first_scan && kind == 0 && restart > 0 && ns == (int)comps.size() && defer_scan(order, se, next))
+            return IK_OK;
+        ensure_coef();
         for (auto& c : comps) c.pred = 0;
         eobrun = 0;
         BitReader br{se, end};
@@ -357,7 +446,6 @@ struct Decoder {
     int parse() {
         const uint8_t* p = b + 2;
         auto be16 = [](const uint8_t* q) { return (int)q[0] << 8 | q[1]; };
-        bool scanned = false;
         for (;;) {
             while (p < end && *p != 0xFF) ++p;  // tolerate garbage between segments
             while (p < end && *p == 0xFF) ++p;
@@ -407,7 +495,7 @@ struct Decoder {
                 const uint8_t* next = se;
                 const int st = scan(s, se, next);
                 if (st) return st;
-                scanned = true;
+                if (need_host) return IK_OK;
                 p = next;
                 continue;
             }
@@ -418,18 +506,15 @@ struct Decoder {
 
 }  // namespace
 
-int decode_jpeg_device(const uint8_t* bytes, size_t n, ik_image** out) {
-    Decoder d;
-    d.b = bytes;
-    d.end = bytes + n;
-    int st = d.parse();
-    if (st) return st;
+namespace {
+
+// reconstruction geometry of a parsed stream; returns the plane bytes it needs
+size_t make_geom(const Decoder& d, JpegGeom& g) {
     const int nc = (int)d.comps.size();
     int colorspace = nc == 1 ? 0 : 1;  // gray / YCbCr
     if (nc == 3 && d.adobe && d.adobe_transform == 0) colorspace = 2;  // Adobe RGB-coded
     if (nc == 3 && !d.adobe && d.comps[0].id == 'R' && d.comps[1].id == 'G' && d.comps[2].id == 'B') colorspace = 2;
-
-    JpegGeom g{};
+    g = JpegGeom{};
     g.ncomp = nc;
     g.W = d.width;
     g.H = d.height;
@@ -444,31 +529,243 @@ int decode_jpeg_device(const uint8_t* bytes, size_t n, ik_image** out) {
         g.plane0[i] = (long long)plane_bytes;
         plane_bytes += (size_t)c.bw * 8 * c.bh * 8;
     }
-    g.nblocks = (long long)(d.coef.size() / 64);
+    g.nblocks = (long long)d.nblocks;
+    return plane_bytes;
+}
 
-    // one upload: [qtables 4x64 u16 per component][coefficients][planes (device only)]
+void qtables(const Decoder& d, uint16_t q[256]) {
+    std::memset(q, 0, 256 * sizeof(uint16_t));
+    for (int i = 0; i < (int)d.comps.size(); ++i) std::memcpy(&q[i * 64], d.qt[d.comps[i].tq], 64 * sizeof(uint16_t));
+}
+
+inline size_t up256(size_t x) { return (x + 255) / 256 * 256; }
+
+// try_gpu: baseline scans with restart intervals are entropy-decoded on the GPU
+// (k_jpeg_huff); anything else, and any stream the GPU finds a bad code in, goes
+// through the host decoder
+int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gpu) {
+    static const bool timing = getenv("IK_JPEG_TIMING") != nullptr;  // dev: phase times to stderr
+    auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t0 = timing ? now() : 0;
+    Decoder d;
+    d.b = bytes;
+    d.end = bytes + n;
+    d.try_gpu = try_gpu;
+    int st = d.parse();
+    if (st) return st;
+    if (d.need_host) return decode_jpeg_impl(bytes, n, out, false);  // several scans: all on the host
+    const int nc = (int)d.comps.size();
+    JpegGeom g;
+    const size_t plane_bytes = make_geom(d, g);
+
+    // device scratch: [qtables 4x64 u16][coefficients][planes][GPU entropy decoding:
+    // tables, error flag, segment starts, scan bytes]
     const size_t qbytes = 256 * sizeof(uint16_t);
-    const size_t cbytes = d.coef.size() * sizeof(int16_t);
+    const size_t cbytes = d.nblocks * 64 * sizeof(int16_t);
+    const bool gpu = d.deferred;
+    const size_t tbytes = gpu ? (sizeof(JpegHuffTables) + 255) / 256 * 256 : 0;
+    const size_t sbytes = gpu ? (d.gpu_segs.size() * sizeof(unsigned) + 255) / 256 * 256 : 0;
+    const size_t dbytes = gpu ? (size_t)d.gpu_scan.size : 0;
     std::vector<uint16_t> q(256, 0);
-    for (int i = 0; i < nc; ++i) std::memcpy(&q[i * 64], d.qt[d.comps[i].tq], 64 * sizeof(uint16_t));
+    qtables(d, q.data());
+    const double t1 = timing ? now() : 0;
     ik_image* img = nullptr;
     st = alloc_image((uint32_t)d.width, (uint32_t)d.height, nc == 1 ? 1u : 3u, &img);
     if (st) return st;
-    uint8_t* dev = scratch(qbytes + cbytes + plane_bytes + 256);
+    const double t2 = timing ? now() : 0;
+    const size_t pl_off = qbytes + (cbytes + 255) / 256 * 256;
+    const size_t t_off = pl_off + (plane_bytes + 255) / 256 * 256;
+    const size_t e_off = t_off + tbytes, s_off = e_off + 256, d_off = s_off + sbytes;
+    uint8_t* dev = scratch(d_off + dbytes + 1024);  // the GPU bit reader fetches 64-B chunks past the end
     if (!dev) { ik_image_free(img); return fail(IK_ERR_DEVICE, "cannot allocate device scratch"); }
     hipStream_t s = thread_stream();
     st = copy_h2d_2d(dev, qbytes, reinterpret_cast<const uint8_t*>(q.data()), qbytes, qbytes, 1, s);
-    if (!st && cbytes)
+    if (!st && gpu) {
+        JpegHuffTables tabs;
+        d.tables(tabs);
+        st = copy_h2d_2d(dev + t_off, sizeof(tabs), reinterpret_cast<const uint8_t*>(&tabs), sizeof(tabs),
+                         sizeof(tabs), 1, s);
+        if (!st)
+            st = copy_h2d_2d(dev + s_off, sbytes, reinterpret_cast<const uint8_t*>(d.gpu_segs.data()),
+                             d.gpu_segs.size() * sizeof(unsigned), d.gpu_segs.size() * sizeof(unsigned), 1, s);
+        if (!st && dbytes) st = copy_h2d_2d(dev + d_off, dbytes, d.gpu_data, dbytes, dbytes, 1, s);
+        if (!st) {
+            hipError_t e = hipMemsetAsync(dev + qbytes, 0, cbytes, s);
+            if (e == hipSuccess) e = hipMemsetAsync(dev + e_off, 0, sizeof(int), s);
+            JpegScanArgs a = d.gpu_scan;
+            a.data = dev + d_off;
+            a.seg = reinterpret_cast<const unsigned*>(dev + s_off);
+            a.tabs = reinterpret_cast<const JpegHuffTables*>(dev + t_off);
+            a.coef = reinterpret_cast<int16_t*>(dev + qbytes);
+            a.err = reinterpret_cast<int*>(dev + e_off);
+            if (e == hipSuccess) e = launch_jpeg_huff(a, s);
+            int err = 0;
+            if (e == hipSuccess) e = hipMemcpyAsync(&err, dev + e_off, sizeof(int), hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) { ik_image_free(img); return hip_fail(e, "jpeg entropy decode"); }
+            if (err) {  // a bad code somewhere: the host decoder reports it
+                ik_image_free(img);
+                return decode_jpeg_impl(bytes, n, out, false);
+            }
+        }
+    } else if (!st && cbytes) {
         st = copy_h2d_2d(dev + qbytes, cbytes, reinterpret_cast<const uint8_t*>(d.coef.data()), cbytes, cbytes, 1, s);
+    }
     if (st) { ik_image_free(img); return st; }
+    const double t3 = timing ? now() : 0;
     g.qt = reinterpret_cast<const uint16_t*>(dev);
     g.coef = reinterpret_cast<const int16_t*>(dev + qbytes);
-    g.planes = dev + qbytes + cbytes;
+    g.planes = dev + pl_off;
     hipError_t e = launch_jpeg_reconstruct(g, img->d, img->pitch, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) { ik_image_free(img); return hip_fail(e, "jpeg reconstruct"); }
+    if (timing)
+        fprintf(stderr, "[jpeg] %s: parse %.2f alloc %.2f entropy/upload %.2f reconstruct %.2f ms\n",
+                gpu ? "gpu entropy" : "host entropy", t1 - t0, t2 - t1, t3 - t2, now() - t3);
     *out = img;
     return IK_OK;
+}
+
+}  // namespace
+
+int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_image** outs, int* status) {
+    // 1. parse every stream (host threads); restart-interval baseline scans are deferred
+    std::vector<std::unique_ptr<Decoder>> ds(n);
+    std::vector<int> st(n, IK_OK);
+    {
+        std::atomic<int> next{0};
+        auto work = [&] {
+            for (int i; (i = next.fetch_add(1)) < n;) {
+                ds[i].reset(new Decoder());
+                ds[i]->b = bytes[i];
+                ds[i]->end = bytes[i] + lens[i];
+                ds[i]->try_gpu = true;
+                st[i] = ds[i]->parse();
+            }
+        };
+        const int nt = std::max(1, std::min(n, std::min(16, (int)std::thread::hardware_concurrency())));
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+    }
+    std::vector<int> gpu_idx, host_idx;
+    for (int i = 0; i < n; ++i) {
+        outs[i] = nullptr;
+        if (st[i]) continue;
+        if (ds[i]->deferred && !ds[i]->need_host) gpu_idx.push_back(i);
+        else host_idx.push_back(i);
+    }
+    // 2. the deferred scans: one device allocation, one Huffman launch over all of them
+    const int m = (int)gpu_idx.size();
+    if (m) {
+        struct Lay { size_t q, t, sg, dt, coef, pl, end; JpegGeom g; };
+        std::vector<Lay> lay(m);
+        size_t total = 256 + up256(sizeof(JpegScanArgs) * m) + up256(sizeof(int) * m);
+        const size_t hdr = total;
+        for (int k = 0; k < m; ++k) {
+            const Decoder& d = *ds[gpu_idx[k]];
+            Lay& L = lay[k];
+            const size_t pb = make_geom(d, L.g);
+            L.q = total;
+            L.t = L.q + 512;
+            L.sg = L.t + up256(sizeof(JpegHuffTables));
+            L.dt = L.sg + up256(d.gpu_segs.size() * sizeof(unsigned));
+            L.coef = L.dt + up256((size_t)d.gpu_scan.size + 1024);  // 64-B chunk fetches past the end
+            L.pl = L.coef + up256(d.nblocks * 64 * sizeof(int16_t));
+            L.end = L.pl + up256(pb);
+            total = L.end;
+        }
+        uint8_t* dev = nullptr;
+        IK_HIP(hipMalloc(&dev, total));
+        hipStream_t s = thread_stream();
+        int rc = IK_OK;
+        std::vector<JpegScanArgs> args(m);
+        int max_seg = 0;
+        for (int k = 0; k < m && !rc; ++k) {
+            const Decoder& d = *ds[gpu_idx[k]];
+            const Lay& L = lay[k];
+            uint16_t q[256];
+            qtables(d, q);
+            JpegHuffTables tabs;
+            d.tables(tabs);
+            rc = copy_h2d_2d(dev + L.q, 512, reinterpret_cast<const uint8_t*>(q), 512, 512, 1, s);
+            if (!rc) rc = copy_h2d_2d(dev + L.t, sizeof(tabs), reinterpret_cast<const uint8_t*>(&tabs), sizeof(tabs),
+                                      sizeof(tabs), 1, s);
+            const size_t sb = d.gpu_segs.size() * sizeof(unsigned);
+            if (!rc) rc = copy_h2d_2d(dev + L.sg, sb, reinterpret_cast<const uint8_t*>(d.gpu_segs.data()), sb, sb, 1, s);
+            const size_t db = (size_t)d.gpu_scan.size;
+            if (!rc && db) rc = copy_h2d_2d(dev + L.dt, db, d.gpu_data, db, db, 1, s);
+            JpegScanArgs& a = args[k];
+            a = d.gpu_scan;
+            a.data = dev + L.dt;
+            a.seg = reinterpret_cast<const unsigned*>(dev + L.sg);
+            a.tabs = reinterpret_cast<const JpegHuffTables*>(dev + L.t);
+            a.coef = reinterpret_cast<int16_t*>(dev + L.coef);
+            a.err = reinterpret_cast<int*>(dev + 256 + up256(sizeof(JpegScanArgs) * m)) + k;
+            max_seg = std::max(max_seg, a.n_seg);
+        }
+        std::vector<int> errs(m, 0);
+        if (!rc) {
+            rc = copy_h2d_2d(dev + 256, sizeof(JpegScanArgs) * m, reinterpret_cast<const uint8_t*>(args.data()),
+                             sizeof(JpegScanArgs) * m, sizeof(JpegScanArgs) * m, 1, s);
+        }
+        if (!rc) {
+            hipError_t e = hipMemsetAsync(dev + 256 + up256(sizeof(JpegScanArgs) * m), 0, sizeof(int) * m, s);
+            for (int k = 0; k < m && e == hipSuccess; ++k)
+                e = hipMemsetAsync(dev + lay[k].coef, 0, lay[k].pl - lay[k].coef, s);
+            if (e == hipSuccess)
+                e = launch_jpeg_huff_batch(reinterpret_cast<const JpegScanArgs*>(dev + 256), m, max_seg, s);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(errs.data(), dev + 256 + up256(sizeof(JpegScanArgs) * m), sizeof(int) * m,
+                                   hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) rc = hip_fail(e, "jpeg batch entropy decode");
+        }
+        // 3. reconstruction of every image the GPU decoded cleanly
+        for (int k = 0; k < m && !rc; ++k) {
+            const int i = gpu_idx[k];
+            if (errs[k]) { host_idx.push_back(i); continue; }
+            const Decoder& d = *ds[i];
+            JpegGeom g = lay[k].g;
+            g.qt = reinterpret_cast<const uint16_t*>(dev + lay[k].q);
+            g.coef = reinterpret_cast<const int16_t*>(dev + lay[k].coef);
+            g.planes = dev + lay[k].pl;
+            ik_image* img = nullptr;
+            st[i] = alloc_image((uint32_t)d.width, (uint32_t)d.height, d.comps.size() == 1 ? 1u : 3u, &img);
+            if (st[i]) continue;
+            hipError_t e = launch_jpeg_reconstruct(g, img->d, img->pitch, s);
+            if (e != hipSuccess) { ik_image_free(img); st[i] = hip_fail(e, "jpeg reconstruct"); continue; }
+            outs[i] = img;
+        }
+        hipError_t e = hipStreamSynchronize(s);
+        (void)hipFree(dev);
+        if (rc || e != hipSuccess) {
+            for (int k = 0; k < m; ++k) {
+                const int i = gpu_idx[k];
+                if (outs[i]) { ik_image_free(outs[i]); outs[i] = nullptr; }
+            }
+            if (rc) return rc;
+            return hip_fail(e, "jpeg batch reconstruct");
+        }
+        (void)hdr;
+    }
+    // 4. everything else: the single-image path with host entropy decoding
+    for (int i : host_idx) st[i] = decode_jpeg_impl(bytes[i], lens[i], &outs[i], false);
+    int first = IK_OK;
+    for (int i = 0; i < n; ++i) {
+        if (status) status[i] = st[i];
+        if (st[i] && !first) first = st[i];
+    }
+    return first;
+}
+
+int decode_jpeg_device(const uint8_t* bytes, size_t n, ik_image** out) {
+    static const bool gpu = [] {
+        const char* e = getenv("IK_JPEG_GPU_ENTROPY");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return decode_jpeg_impl(bytes, n, out, gpu);
 }
 
 }  // namespace ik

@@ -93,6 +93,9 @@ int decode_webp(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& 
 // JPEG: host entropy decode + GPU reconstruction straight into a new device image
 // (ik_jpeg_decode.cpp + ik_jpeg.hip)
 int decode_jpeg_device(const uint8_t* b, size_t n, ik_image** out);
+// n streams at once: restart-interval baseline scans entropy-decoded in one GPU
+// launch; per-stream status (outs[i] null on failure); returns the first failure
+int decode_jpeg_batch(const uint8_t* const* b, const size_t* lens, int n, ik_image** outs, int* status);
 
 // device-side stage helpers used by ik_encode and the pipeline
 int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, size_t pitch,

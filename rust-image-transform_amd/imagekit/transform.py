@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import ctypes
 import enum
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 import numpy as np
 
@@ -145,6 +145,26 @@ def decode_image(data: bytes) -> Tuple[DynamicImage, Optional[ImageFormat]]:
         raise TransformError(_lib.last_error())
     f = None if fmt.value < 0 else ImageFormat(fmt.value)
     return DynamicImage(out.value), f
+
+
+def decode_image_batch(datas) -> List[Tuple[DynamicImage, Optional[ImageFormat]]]:
+    """decode_image over many inputs with one GPU entropy-decoding launch for the
+    restart-interval JPEGs among them (ik_decode_batch).  Raises the first failure."""
+    lib = _lib.load()
+    bufs = [bytes(d) for d in datas]
+    n = len(bufs)
+    if n == 0:
+        return []
+    ptrs = (ctypes.c_void_p * n)(*[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p) for b in bufs])
+    lens = (ctypes.c_size_t * n)(*[len(b) for b in bufs])
+    outs = (ctypes.c_void_p * n)()
+    fmts = (ctypes.c_int * n)()
+    status = (ctypes.c_int * n)()
+    st = lib.ik_decode_batch(ptrs, lens, n, outs, fmts, status)
+    imgs = [DynamicImage(outs[i]) if outs[i] else None for i in range(n)]
+    if st:
+        raise TransformError(_lib.last_error())
+    return [(imgs[i], None if fmts[i] < 0 else ImageFormat(fmts[i])) for i in range(n)]
 
 
 def resize_image(img: DynamicImage, w: Optional[int], h: Optional[int],

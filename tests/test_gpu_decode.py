@@ -240,3 +240,86 @@ def test_config1_jpeg_to_webp(ik, oracle):
     assert out.dimensions() == (320, 240)
     want, dims = oracle.transform(np.asarray(Image.open(io.BytesIO(b))), 320, None, 4, 1, 80)
     assert encode_image(out, ImageFormat.webp, 80) == want
+
+
+# ---- GPU entropy decoding (k_jpeg_huff): baseline scans with restart intervals ----
+@pytest.mark.parametrize("wh", [(16, 16), (300, 200), (1023, 767), (17, 9)])
+@pytest.mark.parametrize("sub", [0, 1, 2])
+@pytest.mark.parametrize("rst", [("rows", 1), ("rows", 3), ("blocks", 1), ("blocks", 7)])
+def test_jpeg_restart_intervals_gpu_entropy(ik, wh, sub, rst):
+    """One GPU lane per restart interval; pixels equal libjpeg-turbo's."""
+    w, h = wh
+    kw = {"restart_marker_rows" if rst[0] == "rows" else "restart_marker_blocks": rst[1]}
+    pat = "N" if (w * h) % 2 else "S"
+    b = _jpeg(ikutil.synth(w, h, 3, seed=w + h + sub, pattern=pat), quality=85, subsampling=sub, **kw)
+    img, fmt = decode_image(b)
+    assert fmt is ImageFormat.jpeg
+    np.testing.assert_array_equal(img.to_array(), np.asarray(Image.open(io.BytesIO(b))))
+
+
+@pytest.mark.parametrize("q", [10, 100])
+def test_jpeg_restart_gray_and_extreme_quality(ik, q):
+    g = ikutil.synth(257, 131, 1, seed=q, pattern="N")[..., 0]
+    b = _jpeg(g, quality=q, restart_marker_blocks=5)
+    img, _ = decode_image(b)
+    np.testing.assert_array_equal(img.to_array()[..., 0], np.asarray(Image.open(io.BytesIO(b))))
+
+
+def test_jpeg_restart_large_4096(ik):
+    """A configs[2]-sized frame (4096 x 4096, 4:2:0, one restart per MCU row)."""
+    b = _jpeg(ikutil.synth(4096, 4096, 3, seed=9, pattern="S"), quality=90, subsampling=2, restart_marker_rows=1)
+    img, _ = decode_image(b)
+    np.testing.assert_array_equal(img.to_array(), np.asarray(Image.open(io.BytesIO(b))))
+
+
+def test_jpeg_restart_corrupt_interval_is_handled_like_the_host(ik):
+    """A bad code inside one interval: the GPU flags it and the host decoder
+    decides (an error, or libjpeg-style tolerant output) -- never a crash."""
+    b = bytearray(_jpeg(ikutil.synth(320, 240, 3, seed=4, pattern="N"), quality=90, restart_marker_rows=1))
+    sos = b.index(b"\xff\xda")
+    mid = sos + (len(b) - sos) // 2
+    for i in range(mid, mid + 64):
+        if b[i] not in (0xFF, 0x00) and b[i - 1] != 0xFF:
+            b[i] = 0xFF ^ b[i] if b[i] != 0xFF else b[i]
+    try:
+        img, _ = decode_image(bytes(b))
+        assert img.to_array().shape == (240, 320, 3)
+    except TransformError:
+        pass
+
+
+def test_decode_batch_one_launch_matches_libjpeg_turbo(ik):
+    """ik_decode_batch: restart JPEGs of mixed geometry/subsampling entropy-decoded
+    in one GPU launch, plus inputs that take the single-image paths (no restarts,
+    progressive, PNG); every result equals its own decoder's answer."""
+    from imagekit import decode_image_batch
+    blobs, want = [], []
+    for k, (w, h, sub) in enumerate([(640, 480, 2), (333, 211, 0), (96, 64, 1), (1024, 768, 2), (17, 9, 2)]):
+        b = _jpeg(ikutil.synth(w, h, 3, seed=50 + k, pattern="S" if k % 2 else "N"), quality=80 + k,
+                  subsampling=sub, restart_marker_rows=1 + k % 2)
+        blobs.append(b)
+        want.append(np.asarray(Image.open(io.BytesIO(b))))
+    b = _jpeg(ikutil.synth(200, 100, 3, seed=60), quality=75)  # no restart markers: host entropy path
+    blobs.append(b)
+    want.append(np.asarray(Image.open(io.BytesIO(b))))
+    b = _jpeg(ikutil.synth(120, 90, 3, seed=61), quality=75, progressive=True, restart_marker_blocks=2)
+    blobs.append(b)
+    want.append(np.asarray(Image.open(io.BytesIO(b))))
+    px = ikutil.synth(40, 30, 4, seed=62)
+    buf = io.BytesIO()
+    Image.fromarray(px).save(buf, format="PNG")
+    blobs.append(buf.getvalue())
+    want.append(px)
+    out = decode_image_batch(blobs)
+    assert len(out) == len(blobs)
+    for (img, fmt), w_ in zip(out, want):
+        a = img.to_array()
+        np.testing.assert_array_equal(a.reshape(w_.shape), w_)
+    assert [f for _, f in out][:7] == [ImageFormat.jpeg] * 7 and out[7][1] is None
+
+
+def test_decode_batch_reports_failures(ik):
+    from imagekit import decode_image_batch
+    good = _jpeg(ikutil.synth(64, 48, 3, seed=1), quality=80, restart_marker_rows=1)
+    with pytest.raises(TransformError):
+        decode_image_batch([good, b"\x00" * 10, good])
