@@ -267,11 +267,15 @@ void jpeg_quant_tables(int quality, uint8_t qt[128]) {
     }
 }
 
-void jpeg_write(const int16_t* coef, int w, int h, const uint8_t qt[128], std::vector<uint8_t>& out) {
+void jpeg_huff_u32(uint32_t t[4 * 256]) {
     const Tables& T = tables();
-    const size_t nmcu = (size_t)((w + 7) / 8) * ((h + 7) / 8);
+    const Huff* hs[4] = {&T.ldc, &T.lac, &T.cdc, &T.cac};
+    for (int k = 0; k < 4; ++k)
+        for (int i = 0; i < 256; ++i) t[k * 256 + i] = (uint32_t)hs[k]->code[i] << 8 | hs[k]->size[i];
+}
+
+void jpeg_header(int w, int h, const uint8_t qt[128], std::vector<uint8_t>& out) {
     out.clear();
-    out.reserve(1024 + nmcu * 64);
     out.push_back(0xFF); out.push_back(0xD8);
     const uint8_t jfif[14] = {'J', 'F', 'I', 'F', 0, 1, 2, 0, 0, 1, 0, 1, 0, 0};
     segment(out, 0xE0, jfif, sizeof(jfif));
@@ -296,6 +300,13 @@ void jpeg_write(const int16_t* coef, int w, int h, const uint8_t qt[128], std::v
     }
     const uint8_t sos[10] = {3, 1, 0x00, 2, 0x11, 3, 0x11, 0, 63, 0};
     segment(out, 0xDA, sos, sizeof(sos));
+}
+
+void jpeg_write(const int16_t* coef, int w, int h, const uint8_t qt[128], std::vector<uint8_t>& out) {
+    const Tables& T = tables();
+    const size_t nmcu = (size_t)((w + 7) / 8) * ((h + 7) / 8);
+    jpeg_header(w, h, qt, out);
+    out.reserve(out.size() + nmcu * 64);
     Bits b(out);
     int pdc[3] = {0, 0, 0};
     for (size_t m = 0; m < nmcu; ++m) {

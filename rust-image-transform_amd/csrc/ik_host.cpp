@@ -154,12 +154,16 @@ const DeviceConsts* device_consts(int device) {
     uint16_t g2l[256];
     int l2g[33];
     webp_gamma_tables(g2l, l2g);
+    uint32_t hf[4 * 256];
+    jpeg_huff_u32(hf);
     auto* dc = new DeviceConsts();
     (void)hipSetDevice(device);
     if (hipMalloc(&dc->gamma_to_lin, sizeof(g2l)) != hipSuccess ||
         hipMalloc(&dc->lin_to_gamma, sizeof(l2g)) != hipSuccess ||
+        hipMalloc(&dc->jpeg_huff, sizeof(hf)) != hipSuccess ||
         hipMemcpy(dc->gamma_to_lin, g2l, sizeof(g2l), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(dc->lin_to_gamma, l2g, sizeof(l2g), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(dc->jpeg_huff, hf, sizeof(hf), hipMemcpyHostToDevice) != hipSuccess ||
         hipDeviceSynchronize() != hipSuccess) {  // order before non-blocking streams
         delete dc;
         return nullptr;
@@ -203,17 +207,50 @@ int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, 
         jpeg_quant_tables(q, qt);
         const size_t nmcu = (size_t)((w + 7) / 8) * ((h + 7) / 8);
         const size_t cbytes = nmcu * 3 * 64 * sizeof(int16_t);
-        uint8_t* dq = scratch(cbytes + 256);
+        const DeviceConsts* dc = device_consts(current_device());
+        if (!dc) return fail(IK_ERR_DEVICE, "cannot upload JPEG tables");
+        // [qtables 256][coefficients][Huffman work: words + staging][stuffed stream][length]
+        const size_t cap = jpeg_enc_cap((int)w, (int)h);
+        const size_t c_off = 256, w_off = c_off + (cbytes + 255) / 256 * 256;
+        const size_t o_off = w_off + 2 * cap, l_off = o_off + cap;
+        uint8_t* dq = scratch(l_off + 256);
         if (!dq) return fail(IK_ERR_DEVICE, "cannot allocate device scratch");
-        int16_t* dcoef = (int16_t*)(dq + 256);
-        std::vector<int16_t> coef(nmcu * 3 * 64);
+        int16_t* dcoef = (int16_t*)(dq + c_off);
         int rc = copy_h2d_2d(dq, 128, qt, 128, 128, 1, s);
         if (rc) return rc;
         hipError_t e = launch_jpeg_coeffs(dev, (int)w, (int)h, (int)c, pitch, 0, dq, dcoef, 0, 1, s);
         if (e != hipSuccess) return hip_fail(e, "jpeg coefficients");
-        rc = copy_d2h_2d((uint8_t*)coef.data(), cbytes, (const uint8_t*)dcoef, cbytes, cbytes, 1, s);
+        JpegEncArgs a{};
+        a.coef = dcoef;
+        a.coef_img_stride = 0;
+        a.nmcu = (int)nmcu;
+        a.huff = dc->jpeg_huff;
+        a.work = dq + w_off;
+        a.work_img_bytes = 2 * cap;
+        a.words_bytes = cap;
+        a.out = dq + o_off;
+        a.out_img_stride = cap;
+        a.out_cap = cap;
+        a.out_len = reinterpret_cast<uint32_t*>(dq + l_off);
+        e = launch_jpeg_huff_enc(a, 1, s);
+        if (e != hipSuccess) return hip_fail(e, "jpeg huffman");
+        uint32_t len = 0;
+        rc = copy_d2h_2d(reinterpret_cast<uint8_t*>(&len), 4, dq + l_off, 4, 4, 1, s);
         if (rc) return rc;
-        jpeg_write(coef.data(), (int)w, (int)h, qt, out);
+        if (len == 0xffffffffu) {  // does not fit the GPU coder's buffer: host coder
+            std::vector<int16_t> coef(nmcu * 3 * 64);
+            rc = copy_d2h_2d((uint8_t*)coef.data(), cbytes, (const uint8_t*)dcoef, cbytes, cbytes, 1, s);
+            if (rc) return rc;
+            jpeg_write(coef.data(), (int)w, (int)h, qt, out);
+            return IK_OK;
+        }
+        jpeg_header((int)w, (int)h, qt, out);
+        const size_t hdr = out.size();
+        out.resize(hdr + len + 2);
+        if (len) rc = copy_d2h_2d(out.data() + hdr, len, dq + o_off, len, len, 1, s);
+        if (rc) return rc;
+        out[hdr + len] = 0xFF;
+        out[hdr + len + 1] = 0xD9;
         return IK_OK;
     }
     if (fmt == IK_FORMAT_AVIF) {

@@ -124,6 +124,26 @@ hipError_t launch_jpeg_huff(const JpegScanArgs& a, hipStream_t s);
 // n scans in one launch (dev_scans: device array of n JpegScanArgs; max_seg = most intervals)
 hipError_t launch_jpeg_huff_batch(const JpegScanArgs* dev_scans, int n, int max_seg, hipStream_t s);
 
+// Baseline Huffman coding of k_jpeg_coeffs' output on the GPU (ik_jpeg_enc.hip),
+// the same bytes as ik_codec.cpp's host coder.  Per image: entropy-coded segment
+// (stuffed, with pad_byte) in out + i*out_img_stride, its length in out_len[i]
+// (0xffffffff: does not fit out_cap -> code it on the host).
+struct JpegEncArgs {
+    const int16_t* coef;       // [mcu][Y,Cb,Cr][64] natural order per image
+    size_t coef_img_stride;    // int16 elements between images
+    int nmcu;
+    const uint32_t* huff;      // [ldc, lac, cdc, cac][256]: code << 8 | size
+    uint8_t* work;             // per image: words_bytes of bit words, then out_cap staging bytes
+    size_t work_img_bytes, words_bytes;
+    uint8_t* out;              // device or pinned host memory
+    size_t out_img_stride, out_cap;
+    uint32_t* out_len;
+};
+hipError_t launch_jpeg_huff_enc(const JpegEncArgs& a, int n, hipStream_t s);
+inline size_t jpeg_enc_cap(int w, int h) {  // stuffed-stream capacity per image
+    return ((size_t)3 * w * h + 4096 + 15) & ~(size_t)15;
+}
+
 // ---- plans (ik_plan.cpp) ----
 // sample.rs weights for one axis; returns the tap count T (row stride of w).
 int axis_weights(int in, int out, int filter, std::vector<int>& left, std::vector<int>& cnt,

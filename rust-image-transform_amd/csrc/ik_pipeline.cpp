@@ -107,6 +107,9 @@ struct ik_pipeline {
     uint8_t qt[128];
     float* d_tmp = nullptr;      // naive resize path only
     int webp_enc = IK_WEBP_LIBWEBP;  // IK_WEBP_GPU: k_vp8_diag wavefront + host bitstream
+    uint8_t* d_jwork = nullptr;      // JPEG: k_jpeg_huff_enc work (2 * jcap per image)
+    size_t jcap = 0;
+    std::vector<uint8_t> jpeg_hdr;   // SOI .. SOS for this geometry and quality
     ik::Vp8Work vp8;
     // Two slots: the device stage of batch k+1 (enqueued by submit) runs while
     // the host entropy stage of batch k (collect) works from its slot.  The
@@ -117,6 +120,8 @@ struct ik_pipeline {
         uint8_t* h_stage = nullptr;       // pinned planes / coefficients
         ik::vp8::MBOut* h_mbs = nullptr;  // pinned MB records (GPU VP8, frames too big to pack)
         uint8_t* h_pack = nullptr;        // pinned compact MB streams (GPU VP8, k_vp8_pack)
+        uint8_t* h_jpeg = nullptr;        // pinned entropy-coded JPEG segments (k_jpeg_huff_enc), jcap apart
+        uint32_t* h_jlen = nullptr;       // their lengths
         // resize start / end, colour end, vp8 end, copies end, vp8 start (stream2)
         hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
         uint8_t* d_stage = nullptr;       // this slot's part of ik_pipeline::d_stage
@@ -186,8 +191,23 @@ int enqueue(ik_pipeline* p, ik_pipeline::Slot& s, const uint8_t* dev_src, size_t
         IK_HIP(hipEventRecord(s.ev[4], p->stream2));
     } else {
         IK_HIP(hipEventRecord(s.ev[5], p->stream));
+        if (copy_out && p->fmt == IK_FORMAT_JPEG) {  // Huffman coding on the GPU, straight into pinned memory
+            JpegEncArgs ja{};
+            ja.coef = reinterpret_cast<const int16_t*>(s.d_stage);
+            ja.coef_img_stride = p->stage_bytes / sizeof(int16_t);
+            ja.nmcu = (int)(((p->nw + 7) / 8) * ((p->nh + 7) / 8));
+            ja.huff = device_consts(p->device)->jpeg_huff;
+            ja.work = p->d_jwork;
+            ja.work_img_bytes = 2 * p->jcap;
+            ja.words_bytes = p->jcap;
+            ja.out = s.h_jpeg;
+            ja.out_img_stride = p->jcap;
+            ja.out_cap = p->jcap;
+            ja.out_len = s.h_jlen;
+            IK_HIP(launch_jpeg_huff_enc(ja, (int)n, p->stream));
+        }
         IK_HIP(hipEventRecord(s.ev[3], p->stream));
-        if (copy_out)
+        if (copy_out && p->fmt != IK_FORMAT_JPEG)
             IK_HIP(hipMemcpyAsync(s.h_stage, s.d_stage, p->stage_bytes * n, hipMemcpyDeviceToHost, p->stream));
         IK_HIP(hipEventRecord(s.ev[4], p->stream));
     }
@@ -234,8 +254,23 @@ int host_stage(ik_pipeline* p, const ik_pipeline::Slot& s, uint8_t* out, size_t 
                 ik_last_error(buf, sizeof(buf));
                 errs[i] = buf;
             }
-        } else {
-            jpeg_write((const int16_t*)st, (int)p->nw, (int)p->nh, p->qt, p->outs[i]);
+        } else if (s.h_jlen[i] != 0xffffffffu) {  // GPU-coded segment: header + bytes + EOI
+            const uint32_t len = s.h_jlen[i];
+            std::vector<uint8_t>& o = p->outs[i];
+            o.resize(p->jpeg_hdr.size() + len + 2);
+            std::memcpy(o.data(), p->jpeg_hdr.data(), p->jpeg_hdr.size());
+            std::memcpy(o.data() + p->jpeg_hdr.size(), s.h_jpeg + p->jcap * (size_t)i, len);
+            o[o.size() - 2] = 0xFF;
+            o[o.size() - 1] = 0xD9;
+        } else {  // did not fit the GPU coder's buffer: coefficients back, host coder
+            std::vector<int16_t> coef(p->stage_bytes / sizeof(int16_t));
+            if (hipMemcpy(coef.data(), s.d_stage + p->stage_bytes * (size_t)i, p->stage_bytes,
+                          hipMemcpyDeviceToHost) != hipSuccess) {
+                p->status[i] = IK_ERR_DEVICE;
+                errs[i] = "coefficient copy failed";
+                return;
+            }
+            jpeg_write(coef.data(), (int)p->nw, (int)p->nh, p->qt, p->outs[i]);
         }
     });
     p->ms[3] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -280,6 +315,14 @@ int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t
     } else {
         p->stage_bytes = (size_t)((nw + 7) / 8) * ((nh + 7) / 8) * 3 * 64 * sizeof(int16_t);
         jpeg_quant_tables(p->quality, p->qt);
+        jpeg_header((int)nw, (int)nh, p->qt, p->jpeg_hdr);
+        p->jcap = jpeg_enc_cap((int)nw, (int)nh);
+        IK_HIP(hipMalloc(&p->d_jwork, 2 * p->jcap * max_batch));
+        for (auto& sl : p->slot) {
+            IK_HIP(hipHostMalloc(&sl.h_jpeg, p->jcap * max_batch, hipHostMallocDefault));
+            IK_HIP(hipHostMalloc(&sl.h_jlen, sizeof(uint32_t) * max_batch, hipHostMallocDefault));
+        }
+        if (!device_consts(p->device)) return fail(IK_ERR_DEVICE, "cannot upload JPEG tables");
         IK_HIP(hipMalloc(&p->d_qt, 128));
         if (int rc = copy_h2d_2d(p->d_qt, 128, p->qt, 128, 128, 1, p->stream)) return rc;
     }
@@ -383,10 +426,13 @@ void ik_pipeline_destroy(ik_pipeline* p) {
     if (p->d_stage) (void)hipFree(p->d_stage);
     if (p->d_qt) (void)hipFree(p->d_qt);
     if (p->d_tmp) (void)hipFree(p->d_tmp);
+    if (p->d_jwork) (void)hipFree(p->d_jwork);
     for (auto& sl : p->slot) {
         if (sl.h_stage) (void)hipHostFree(sl.h_stage);
         if (sl.h_mbs) (void)hipHostFree(sl.h_mbs);
         if (sl.h_pack) (void)hipHostFree(sl.h_pack);
+        if (sl.h_jpeg) (void)hipHostFree(sl.h_jpeg);
+        if (sl.h_jlen) (void)hipHostFree(sl.h_jlen);
         for (auto& e : sl.ev)
             if (e) (void)hipEventDestroy(e);
     }

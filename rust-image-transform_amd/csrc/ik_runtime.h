@@ -40,6 +40,7 @@ int alloc_image(uint32_t w, uint32_t h, uint32_t c, ik_image** out);
 struct DeviceConsts {
     uint16_t* gamma_to_lin = nullptr;  // [256]
     int* lin_to_gamma = nullptr;       // [33]
+    uint32_t* jpeg_huff = nullptr;     // [4][256] standard Huffman tables (k_jpeg_huff_enc)
 };
 const DeviceConsts* device_consts(int device);
 void webp_gamma_tables(uint16_t g2l[256], int l2g[33]);
@@ -51,6 +52,8 @@ void jpeg_quant_tables(int quality, uint8_t qt[128]);
 int avif_encode_yuv444(const uint8_t* planes /* Y, U, V, A */, bool has_alpha, int w, int h, int quality,
                        int speed, std::vector<uint8_t>& out);
 void jpeg_write(const int16_t* coef, int w, int h, const uint8_t qt[128], std::vector<uint8_t>& out);
+void jpeg_header(int w, int h, const uint8_t qt[128], std::vector<uint8_t>& out);  // SOI .. SOS
+void jpeg_huff_u32(uint32_t t[4 * 256]);  // ldc, lac, cdc, cac: code << 8 | size
 
 // GPU WebP encoder (ik_webp_gpu.cpp + ik_vp8.hip): reusable device / pinned
 // buffers for n images of one geometry
