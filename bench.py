@@ -41,6 +41,7 @@ METRIC = "transform MPix/s (decode+resize+encode) 4096²→512² WebP q80; 1/2/4
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FILTERS = {"nearest": 0, "triangle": 1, "catmullrom": 2, "gaussian": 3, "lanczos3": 4}
 ENCODERS = {"libwebp": 0, "gpu": 1}
+FORMATS = {"jpeg": 0, "webp": 1}
 
 
 def parse():
@@ -55,6 +56,8 @@ def parse():
     ap.add_argument("--out", type=int, default=512)
     ap.add_argument("--filter", default="triangle", choices=sorted(FILTERS))
     ap.add_argument("--quality", type=int, default=80)
+    ap.add_argument("--format", default="webp", choices=["webp", "jpeg"],
+                    help="webp: the headline (configs[1]); jpeg: configs[2]-style runs (GPU Huffman coding)")
     ap.add_argument("--threads", type=int, default=16, help="host entropy-coder threads per rank")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample wall-time budget (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -102,8 +105,8 @@ def cpu_baseline(args, img: np.ndarray):
     lock = threading.Lock()
 
     def one():
-        b, dims = orc.transform(img, args.out, args.out, f, 1, args.quality)
-        assert dims == (args.out, args.out) and b[:4] == b"RIFF"
+        b, dims = orc.transform(img, args.out, args.out, f, FORMATS[args.format], args.quality)
+        assert dims == (args.out, args.out) and b[:2] in (b"RI", b"\xff\xd8")
         with lock:
             done[0] += 1
 
@@ -130,7 +133,8 @@ def cpu_baseline(args, img: np.ndarray):
         "unit": "MPix/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{n} x {W}x{H} RGBA8 -> {args.out}x{args.out} {args.filter} + libwebp q{args.quality}, "
+        "sample": f"{n} x {W}x{H} RGBA8 -> {args.out}x{args.out} {args.filter} + "
+                  f"{'libwebp' if args.format == 'webp' else 'image-crate JPEG'} q{args.quality}, "
                   f"one image per thread, {threads} threads, {wall:.1f}s wall",
         "value_1core": round(W * H / t1 / 1e6, 3),
     }
@@ -157,17 +161,21 @@ def main():
     f = FILTERS[args.filter]
     pitch = S * 4
     # inputs resident in HBM before the timed region: 4 distinct synthetic frames tiled over the batch
-    NB = max(B, 0 if (args.device_only or args.no_alt_encoder) else args.alt_batch)
+    NB = max(B, 0 if (args.device_only or args.no_alt_encoder or args.format != "webp") else args.alt_batch)
     distinct = [synth_rgba(S, S, seed=sd) for sd in shard_seeds(rank, NB)]
     src = torch.empty((NB, S, pitch), dtype=torch.uint8, device=f"cuda:{local}")
-    for i in range(NB):
-        src[i].copy_(torch.from_numpy(distinct[i % len(distinct)].reshape(S, pitch)))
+    for i in range(NB):  # distinct frames over PCIe once, the rest device to device
+        if i < len(distinct):
+            src[i].copy_(torch.from_numpy(distinct[i].reshape(S, pitch)))
+        else:
+            src[i].copy_(src[i % len(distinct)])
     torch.cuda.synchronize()
 
     pipe = ctypes.c_void_p()
-    if lib.ik_pipeline_create(S, S, 4, O, O, f, 1, args.quality, B, args.threads, ctypes.byref(pipe)):
+    fmt = FORMATS[args.format]
+    if lib.ik_pipeline_create(S, S, 4, O, O, f, fmt, args.quality, B, args.threads, ctypes.byref(pipe)):
         raise SystemExit(f"pipeline: {_lib.last_error()}")
-    if lib.ik_pipeline_set_webp_encoder(pipe, ENCODERS[args.webp_encoder]):
+    if fmt == 1 and lib.ik_pipeline_set_webp_encoder(pipe, ENCODERS[args.webp_encoder]):
         raise SystemExit(f"webp encoder: {_lib.last_error()}")
     out_cap = B * O * O * 4 + (1 << 20)
     out = np.empty(out_cap, np.uint8)
@@ -230,7 +238,7 @@ def main():
     elapsed = reduce_max(elapsed, dist, f"cuda:{local}")
 
     if not args.device_only:
-        assert bytes(out[:4]) == b"RIFF" and all(s > 0 for s in sizes)
+        assert bytes(out[:2]) in (b"RI", b"\xff\xd8") and all(s > 0 for s in sizes)
     resize_ms = float(np.mean([k[0] for k in kms]))
     colour_ms = float(np.mean([k[1] for k in kms]))
     vp8_ms = float(np.mean([k[2] for k in kms]))
@@ -241,7 +249,7 @@ def main():
     # its own batch size: the GPU VP8 wavefront is latency-bound, so it wants more
     # images per launch)
     alt_enc = {}
-    if not args.device_only and not args.no_alt_encoder:
+    if not args.device_only and not args.no_alt_encoder and fmt == 1:
         other = "gpu" if args.webp_encoder == "libwebp" else "libwebp"
         AB = args.alt_batch
         p3 = ctypes.c_void_p()
@@ -316,7 +324,8 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": METRIC,
+            "metric": METRIC if args.format == "webp" else
+                      f"transform MPix/s (resize+encode) {S}²→{O}² {args.filter} JPEG q{args.quality} (configs[2] shape)",
             "value": round(value, 2),
             "unit": "MPix/s",
             "n_gpus": world,
@@ -330,8 +339,8 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": f"{S}x{S} RGBA8 frames resident in HBM -> resize_image {O}x{O} "
-                            f"({args.filter}) -> encode_image webp q{args.quality}; bytes to host",
-                "batch_per_gpu": B, "filter": args.filter, "format": "webp",
+                            f"({args.filter}) -> encode_image {args.format} q{args.quality}; bytes to host",
+                "batch_per_gpu": B, "filter": args.filter, "format": args.format,
                 "quality": args.quality, "host_threads_per_gpu": args.threads,
                 "webp_encoder": args.webp_encoder,
                 "device_only": bool(args.device_only), "batches_in_flight": 1 if args.sync else 2, "parallelism": f"images sharded, {world} rank(s)",
