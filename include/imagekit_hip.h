@@ -108,6 +108,16 @@ int ik_get_webp_encoder(void);
 int ik_transform(const uint8_t *bytes, size_t len, int64_t w, int64_t h, int fmt, int quality,
                  int filter, uint8_t **out, size_t *out_len);
 
+/* ik_transform over n requests at once (the /img handler under load, loadtest C4
+ * mix): ik_decode_batch (one GPU entropy launch for the restart-interval JPEGs),
+ * then resize_image + encode_image per request on `threads` host threads (0 =
+ * default), each with its own HIP stream.  w/h (-1 = None), fmt and quality per
+ * request; outs[i] (ik_buf_free) / out_lens[i] / status[i] per request (status
+ * may be NULL); returns the first failure or IK_OK. */
+int ik_transform_batch(const uint8_t *const *bytes, const size_t *lens, uint32_t n, const int64_t *w,
+                       const int64_t *h, const int *fmt, const int *quality, int filter, int threads,
+                       uint8_t **outs, size_t *out_lens, int *status);
+
 /* A batch of n same-geometry 8-bit images already resident in device memory
  * (image i at dev_src + i*src_image_stride, rows src_pitch bytes apart) ->
  * resize to nw x nh -> encode.  Encoded bytes are written into the caller's

@@ -7,12 +7,16 @@
 // PCIe (plus the small planes/coefficients handed to the host entropy coders).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <string>
+#include <thread>
 
 #include "../../include/imagekit_hip.h"
 #include "ik_runtime.h"
@@ -508,6 +512,57 @@ int ik_decode_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t n,
         if (st[i] && !first) first = st[i];
     }
     return first;
+}
+
+int ik_transform_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t n, const int64_t* w,
+                       const int64_t* h, const int* fmt, const int* quality, int filter, int threads, uint8_t** outs,
+                       size_t* out_lens, int* status) {
+    if (!bytes || !lens || !w || !h || !fmt || !quality || !outs || !out_lens || !n)
+        return fail(IK_ERR_INVALID, "bad batch");
+    std::vector<ik_image*> imgs(n, nullptr);
+    std::vector<int> st(n, IK_OK);
+    for (uint32_t i = 0; i < n; ++i) { outs[i] = nullptr; out_lens[i] = 0; }
+    ik_decode_batch(bytes, lens, n, imgs.data(), nullptr, st.data());
+    // resize + encode per image on host threads, each with its own HIP stream
+    const int dev = current_device();
+    if (threads <= 0) threads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    threads = (int)std::min<uint32_t>((uint32_t)threads, n);
+    std::vector<std::string> errs(n);
+    std::atomic<uint32_t> next{0};
+    auto work = [&](bool own_thread) {
+        if (own_thread) ik_init(dev);
+        for (uint32_t i; (i = next.fetch_add(1)) < n;) {
+            if (st[i]) {
+                char buf[256];
+                if (!errs[i].size()) { ik_last_error(buf, sizeof(buf)); errs[i] = buf; }
+                continue;
+            }
+            ik_image* rs = nullptr;
+            int r = ik_resize(imgs[i], w[i], h[i], filter, &rs);
+            if (!r) r = ik_encode(rs, fmt[i], quality[i], &outs[i], &out_lens[i]);
+            if (r) {
+                char buf[256];
+                ik_last_error(buf, sizeof(buf));
+                errs[i] = buf;
+                st[i] = r;
+            }
+            if (rs && rs != imgs[i]) ik_image_free(rs);
+            ik_image_free(imgs[i]);
+            imgs[i] = nullptr;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; ++t) th.emplace_back(work, true);
+    work(false);
+    for (auto& t : th) t.join();
+    int first = IK_OK;
+    uint32_t first_i = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (status) status[i] = st[i];
+        if (st[i] && !first) { first = st[i]; first_i = i; }
+    }
+    if (first) return fail(first, "item %u: %s", first_i, errs[first_i].c_str());
+    return IK_OK;
 }
 
 int ik_transform(const uint8_t* bytes, size_t len, int64_t w, int64_t h, int fmt, int quality,

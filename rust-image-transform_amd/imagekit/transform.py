@@ -167,6 +167,35 @@ def decode_image_batch(datas) -> List[Tuple[DynamicImage, Optional[ImageFormat]]
     return [(imgs[i], None if fmts[i] < 0 else ImageFormat(fmts[i])) for i in range(n)]
 
 
+def transform_batch(datas, sizes, fmts, qualities, filter: "FilterType" = None, threads: int = 0) -> List[bytes]:
+    """ik_transform_batch: decode -> resize_image -> encode_image for many requests
+    (sizes: (w, h) per request, None = unset; fmts: ImageFormat per request)."""
+    lib = _lib.load()
+    bufs = [bytes(d) for d in datas]
+    n = len(bufs)
+    if n == 0:
+        return []
+    filt = int(FilterType.Lanczos3 if filter is None else filter)
+    ptrs = (ctypes.c_void_p * n)(*[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p) for b in bufs])
+    lens = (ctypes.c_size_t * n)(*[len(b) for b in bufs])
+    ws = (ctypes.c_int64 * n)(*[-1 if s[0] is None else int(s[0]) for s in sizes])
+    hs = (ctypes.c_int64 * n)(*[-1 if s[1] is None else int(s[1]) for s in sizes])
+    fs = (ctypes.c_int * n)(*[int(f.value if isinstance(f, ImageFormat) else f) for f in fmts])
+    qs = (ctypes.c_int * n)(*[int(q) for q in qualities])
+    outs = (ctypes.c_void_p * n)()
+    olens = (ctypes.c_size_t * n)()
+    status = (ctypes.c_int * n)()
+    st = lib.ik_transform_batch(ptrs, lens, n, ws, hs, fs, qs, filt, threads, outs, olens, status)
+    res = []
+    for i in range(n):
+        res.append(ctypes.string_at(outs[i], olens[i]) if outs[i] else None)
+        if outs[i]:
+            lib.ik_buf_free(outs[i])
+    if st:
+        raise TransformError(_lib.last_error())
+    return res
+
+
 def resize_image(img: DynamicImage, w: Optional[int], h: Optional[int],
                  filter: FilterType = FilterType.Lanczos3) -> DynamicImage:
     """src/transform.rs:62-90 (Lanczos3; `filter` is an extension)."""
