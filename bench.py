@@ -137,7 +137,22 @@ def cpu_baseline(args, img: np.ndarray):
                   f"{'libwebp' if args.format == 'webp' else 'image-crate JPEG'} q{args.quality}, "
                   f"one image per thread, {threads} threads, {wall:.1f}s wall",
         "value_1core": round(W * H / t1 / 1e6, 3),
+        "host": host_info(),
     }
+
+
+def host_info():
+    """the GPU box host's CPU model and core count beside the CPU number."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(),
+            "affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
 
 
 def main():

@@ -15,8 +15,10 @@
 
 #if defined(__HIPCC__)
 #define IK_HD __host__ __device__ inline
+#define IK_UNROLL _Pragma("unroll")
 #else
 #define IK_HD inline
+#define IK_UNROLL _Pragma("GCC unroll 16")
 #endif
 
 namespace ik {
@@ -278,7 +280,7 @@ IK_HD int block_cost_fixed(const int16_t* lv, int last, int ctx0) {
         return sel3(ctx0, pc0<TYPE>(band(FIRST), 0, 0), pc0<TYPE>(band(FIRST), 1, 0), pc0<TYPE>(band(FIRST), 2, 0));
     int cost = 0, pc = ctx0;
     bool chk = true;  // an end-of-block flag is coded before this position
-#pragma unroll
+IK_UNROLL
     for (int n = FIRST; n < 16; ++n) {
         const int b = band(n);
         const int v = lv[n] < 0 ? -lv[n] : lv[n];
