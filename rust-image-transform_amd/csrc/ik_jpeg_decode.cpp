@@ -677,9 +677,8 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
             total = L.end;
         }
         uint8_t* dev = nullptr;
-        IK_HIP(hipMalloc(&dev, total));
         hipStream_t s = thread_stream();
-        int rc = IK_OK;
+        int rc = hipMalloc(&dev, total) == hipSuccess ? IK_OK : fail(IK_ERR_DEVICE, "hipMalloc(jpeg batch)");
         std::vector<JpegScanArgs> args(m);
         int max_seg = 0;
         for (int k = 0; k < m && !rc; ++k) {
@@ -738,15 +737,15 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
             if (e != hipSuccess) { ik_image_free(img); st[i] = hip_fail(e, "jpeg reconstruct"); continue; }
             outs[i] = img;
         }
-        hipError_t e = hipStreamSynchronize(s);
-        (void)hipFree(dev);
-        if (rc || e != hipSuccess) {
+        hipError_t e = rc ? hipSuccess : hipStreamSynchronize(s);
+        if (dev) (void)hipFree(dev);
+        if (rc || e != hipSuccess) {  // the batch as a whole failed on the device: each image on its own path
             for (int k = 0; k < m; ++k) {
                 const int i = gpu_idx[k];
                 if (outs[i]) { ik_image_free(outs[i]); outs[i] = nullptr; }
+                if (!errs[k]) host_idx.push_back(i);
+                st[i] = IK_OK;
             }
-            if (rc) return rc;
-            return hip_fail(e, "jpeg batch reconstruct");
         }
         (void)hdr;
     }

@@ -291,12 +291,32 @@ int host_stage(ik_pipeline* p, const ik_pipeline::Slot& s, uint8_t* out, size_t 
 
 extern "C" {
 
+namespace {
+int pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t nh, int filter, int fmt, int quality,
+                    uint32_t max_batch, int threads, ik_pipeline* p);
+}  // namespace
+
 int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t nh, int filter,
                        int fmt, int quality, uint32_t max_batch, int threads, ik_pipeline** out) {
     if (!out || !W || !H || !nw || !nh || !max_batch || C < 1 || C > 4) return fail(IK_ERR_INVALID, "bad geometry");
     if (fmt != IK_FORMAT_WEBP && fmt != IK_FORMAT_JPEG)
         return fail(IK_ERR_UNSUPPORTED, "pipeline supports jpeg and webp output");
     auto* p = new ik_pipeline();
+    const int rc = pipeline_create(W, H, C, nw, nh, filter, fmt, quality, max_batch, threads, p);
+    if (rc) {  // release whatever was allocated before the failure
+        ik_pipeline_destroy(p);
+        return rc;
+    }
+    *out = p;
+    if (fmt == IK_FORMAT_WEBP && default_webp_encoder() == IK_WEBP_GPU) return ik_pipeline_set_webp_encoder(p, IK_WEBP_GPU);
+    return IK_OK;
+}
+
+}  // extern "C"
+
+namespace {
+int pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t nh, int filter, int fmt, int quality,
+                    uint32_t max_batch, int threads, ik_pipeline* p) {
     p->device = current_device();
     IK_HIP(hipSetDevice(p->device));
     p->W = W; p->H = H; p->C = C; p->nw = nw; p->nh = nh; p->max_batch = max_batch;
@@ -340,11 +360,11 @@ int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t
     }
     p->pool = new Pool(threads - 1);  // the calling thread works too
     if (fmt == IK_FORMAT_WEBP && !device_consts(p->device)) return fail(IK_ERR_DEVICE, "cannot upload WebP tables");
-    *out = p;
-    if (fmt == IK_FORMAT_WEBP && default_webp_encoder() == IK_WEBP_GPU)
-        return ik_pipeline_set_webp_encoder(p, IK_WEBP_GPU);
     return IK_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int ik_pipeline_set_webp_encoder(ik_pipeline* p, int encoder) {
     if (!p) return fail(IK_ERR_INVALID, "null pipeline");
