@@ -320,6 +320,21 @@ def main():
         alt = {"filter": alt_name, "resize_ms": round(m, 4),
                "achieved_GBps": round(B * bytes_per_img / (m * 1e-3) / 1e9, 1)}
         lib.ik_pipeline_destroy(p2)
+    # the FMA resize mode (within 1 LSB; the default stays bit-exact) on both filters, device-only
+    fma = {}
+    if lib.ik_set_resize_mode(1) == 0:
+        for name in (args.filter, alt_name):
+            p4 = ctypes.c_void_p()
+            if lib.ik_pipeline_create(S, S, 4, O, O, FILTERS[name], 1, args.quality, B, 1, ctypes.byref(p4)) == 0:
+                ms = []
+                for i in range(6):
+                    lib.ik_pipeline_run_device(p4, ctypes.c_void_p(src.data_ptr()), pitch, S * pitch, B)
+                    if i >= 2:
+                        ms.append(lib.ik_pipeline_kernel_ms(p4, 0))
+                m = float(np.mean(ms))
+                fma[name] = {"resize_ms": round(m, 4), "achieved_GBps": round(B * bytes_per_img / (m * 1e-3) / 1e9, 1)}
+                lib.ik_pipeline_destroy(p4)
+        lib.ik_set_resize_mode(0)
     lib.ik_pipeline_destroy(pipe)
 
     traffic = None
@@ -377,6 +392,7 @@ def main():
             "output_bytes_per_image": out_bytes // B,
             "alt_webp_encoder": alt_enc,
             "alt_filter_kernel": alt,
+            "resize_fma_mode": fma,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))

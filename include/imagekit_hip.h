@@ -85,6 +85,15 @@ int ik_decode_batch(const uint8_t *const *bytes, const size_t *lens, uint32_t n,
  * the reference). */
 int ik_resize(ik_image *img, int64_t w, int64_t h, int filter, ik_image **out);
 
+/* Resampler arithmetic.  IK_RESIZE_EXACT (default): image 0.25.8's f32 sequence,
+ * separately rounded multiply and add per tap -- bit-exact.  IK_RESIZE_FMA: one
+ * fused multiply-add per tap -- within +-1 LSB per channel (the north star's
+ * tolerance for bilinear/Lanczos), fewer vector instructions.  Process-wide; the
+ * default also comes from IK_RESIZE_MODE=exact|fma when first used. */
+typedef enum { IK_RESIZE_EXACT = 0, IK_RESIZE_FMA = 1 } ik_resize_mode;
+int ik_set_resize_mode(int mode);
+int ik_get_resize_mode(void);
+
 /* imageops::resize to exact dimensions (the resampler under resize_image) */
 int ik_resize_exact(const ik_image *img, uint32_t nw, uint32_t nh, int filter, ik_image **out);
 

@@ -149,6 +149,22 @@ void webp_gamma_tables(uint16_t g2l[256], int l2g[33]) {
     for (int v = 0; v <= 32; ++v) l2g[v] = (int)(255. * pow(scale * v, 1. / 0.80) + .5);
 }
 
+namespace {
+std::atomic<int> g_resize_mode{-1};  // -1 = not yet read from IK_RESIZE_MODE
+}  // namespace
+
+int resize_mode() {
+    int m = g_resize_mode.load();
+    if (m < 0) {
+        const char* e = getenv("IK_RESIZE_MODE");
+        m = (e && (!strcmp(e, "fma") || !strcmp(e, "1"))) ? IK_RESIZE_FMA : IK_RESIZE_EXACT;
+        int expected = -1;
+        g_resize_mode.compare_exchange_strong(expected, m);
+        m = g_resize_mode.load();
+    }
+    return m;
+}
+
 const DeviceConsts* device_consts(int device) {
     static std::mutex mu;
     static std::map<int, DeviceConsts*> m;
@@ -513,6 +529,15 @@ int ik_decode_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t n,
     }
     return first;
 }
+
+int ik_set_resize_mode(int mode) {
+    if (mode != IK_RESIZE_EXACT && mode != IK_RESIZE_FMA) return fail(IK_ERR_INVALID, "bad resize mode %d", mode);
+    (void)resize_mode();
+    g_resize_mode.store(mode);
+    return IK_OK;
+}
+
+int ik_get_resize_mode(void) { return resize_mode(); }
 
 int ik_transform_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t n, const int64_t* w,
                        const int64_t* h, const int* fmt, const int* quality, int filter, int threads, uint8_t** outs,

@@ -8,7 +8,13 @@
 #include <string>
 #include <vector>
 
+#include "../../include/imagekit_hip.h"
+
 namespace ik {
+
+// resize arithmetic (ik_set_resize_mode): IK_RESIZE_EXACT (the reference's f32
+// sequence, bit-exact) or IK_RESIZE_FMA (fused multiply-add, within 1 LSB)
+int resize_mode();
 
 constexpr int kThreads = 256;            // workgroup size (4 wave64s)
 constexpr int kBytesPerLane = 8;         // vertical pass: bytes of a source row per lane

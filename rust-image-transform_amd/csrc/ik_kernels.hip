@@ -46,7 +46,7 @@ __device__ __forceinline__ uint8_t float_nearest_u8(float t) {
 // data (the next LDS row or the tables after the rows; the rows are zeroed at the
 // start) and adds +-0, which leaves the sum bit-identical.
 // out(r, ox, c) = round(sum_k tmp[r][(lx[ox]+k)*C + c] * wx[ox][k]), sequential k.
-template <int C, int kHTaps = 2>
+template <int C, bool FMA, int kHTaps = 2>
 __device__ __forceinline__ void horizontal_rows_c(const ResizeArgs& a, const float* __restrict__ lds,
                                                   const float* __restrict__ sw, const int* __restrict__ soff,
                                                   int r0, int nrows, int ox0, int nox, int hq, int hox,
@@ -92,8 +92,12 @@ __device__ __forceinline__ void horizontal_rows_c(const ResizeArgs& a, const flo
             for (int u = 0; u < kHTaps; ++u)
 #pragma unroll
                 for (int c = 0; c < C; ++c) {
-                    const float prod = t[u][c] * wk[u];
-                    acc[c] = acc[c] + prod;
+                    if constexpr (FMA) {
+                        acc[c] = __builtin_fmaf(t[u][c], wk[u], acc[c]);
+                    } else {
+                        const float prod = t[u][c] * wk[u];
+                        acc[c] = acc[c] + prod;
+                    }
                 }
         }
         uint8_t* o = dst + (size_t)(r0 + q) * a.dst_pitch + (size_t)(ox0 + oxl) * C;
@@ -108,15 +112,16 @@ __device__ __forceinline__ void horizontal_rows_c(const ResizeArgs& a, const flo
     }
 }
 
+template <bool FMA>
 __device__ __forceinline__ void horizontal_rows(const ResizeArgs& a, const float* __restrict__ lds,
                                                 const float* __restrict__ sw, const int* __restrict__ soff,
                                                 int r0, int nrows, int ox0, int nox, int hq, int hox,
                                                 uint8_t* __restrict__ dst) {
     switch (a.C) {
-    case 4: horizontal_rows_c<4>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
-    case 3: horizontal_rows_c<3>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
-    case 2: horizontal_rows_c<2>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
-    default: horizontal_rows_c<1>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
+    case 4: horizontal_rows_c<4, FMA>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
+    case 3: horizontal_rows_c<3, FMA>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
+    case 2: horizontal_rows_c<2, FMA>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
+    default: horizontal_rows_c<1, FMA>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
     }
 }
 
@@ -137,7 +142,7 @@ struct FusedOcc { static constexpr int value = A <= 4 ? 4 : (A <= 8 ? 3 : 1); };
 // of step k+2, keeping ~2R loads per lane in flight.  Every F
 // completed rows the workgroup runs the horizontal pass from LDS.  LDS is
 // dynamic: [F rows of f32 tmp][strip weights if WL][column offsets].
-template <int A, int R, int F, bool WL>
+template <int A, int R, int F, bool WL, bool FMA>
 __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(ResizeArgs a) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
 
@@ -246,8 +251,12 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
                         else wt = w[j * A + d];
 #pragma unroll
                         for (int q = 0; q < kBytesPerLane; ++q) {
-                            const float prod = p[q] * wt;
-                            acc[d][q] = acc[d][q] + prod;
+                            if constexpr (FMA) {
+                                acc[d][q] = __builtin_fmaf(p[q], wt, acc[d][q]);
+                            } else {
+                                const float prod = p[q] * wt;
+                                acc[d][q] = acc[d][q] + prod;
+                            }
                         }
                     }
                 }
@@ -268,7 +277,7 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
             const int nrows = (next - oy0) % F + 1;
             if (nrows == F || next == oy1 - 1) {
                 __syncthreads();
-                horizontal_rows(a, lds, hw, s_off, next - nrows + 1, nrows, ox0, nox, hq, hox, dst);
+                horizontal_rows<FMA>(a, lds, hw, s_off, next - nrows + 1, nrows, ox0, nox, hq, hox, dst);
                 __syncthreads();
             }
             ++next;
@@ -343,11 +352,17 @@ hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_
         dim3 grid(plan.NS * plan.NB * n);  // 1-D: the kernel maps it XCD-aware
         const bool wl = plan.weights_in_lds;
         const size_t lds = resize_lds_bytes(a, wl, plan.flush);
-#define IK_LAUNCH(A_, R_, F_)                                                                          \
-    if (plan.slots == A_ && plan.rows == R_ && plan.flush == F_) {                                     \
-        if (wl) hipLaunchKernelGGL((k_resize_fused<A_, R_, F_, true>), grid, dim3(kThreads), lds, s, a); \
-        else hipLaunchKernelGGL((k_resize_fused<A_, R_, F_, false>), grid, dim3(kThreads), lds, s, a);   \
-        return hipGetLastError();                                                                      \
+        const bool fma = resize_mode() == IK_RESIZE_FMA;
+#define IK_LAUNCH(A_, R_, F_)                                                                                 \
+    if (plan.slots == A_ && plan.rows == R_ && plan.flush == F_) {                                            \
+        if (fma) {                                                                                            \
+            if (wl) hipLaunchKernelGGL((k_resize_fused<A_, R_, F_, true, true>), grid, dim3(kThreads), lds, s, a); \
+            else hipLaunchKernelGGL((k_resize_fused<A_, R_, F_, false, true>), grid, dim3(kThreads), lds, s, a);   \
+        } else {                                                                                              \
+            if (wl) hipLaunchKernelGGL((k_resize_fused<A_, R_, F_, true, false>), grid, dim3(kThreads), lds, s, a); \
+            else hipLaunchKernelGGL((k_resize_fused<A_, R_, F_, false, false>), grid, dim3(kThreads), lds, s, a);   \
+        }                                                                                                     \
+        return hipGetLastError();                                                                             \
     }
         IK_FUSED_INSTANCES(IK_LAUNCH)
 #undef IK_LAUNCH
