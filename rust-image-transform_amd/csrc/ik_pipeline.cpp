@@ -374,7 +374,7 @@ int ik_pipeline_set_webp_encoder(ik_pipeline* p, int encoder) {
     IK_HIP(hipSetDevice(p->device));
     if (encoder == IK_WEBP_GPU) {
         if (p->nw > 16383 || p->nh > 16383) return fail(IK_ERR_TRANSFORM, "WebP dimensions exceed 16383");
-        if (int rc = p->vp8.reserve((int)p->nw, (int)p->nh, (int)p->max_batch)) return rc;
+        if (int rc = p->vp8.reserve((int)p->nw, (int)p->nh, (int)p->max_batch, false)) return rc;
         for (auto& sl : p->slot) {
             if (p->vp8.packable()) {
                 if (!sl.h_pack) IK_HIP(hipHostMalloc(&sl.h_pack, p->vp8.pack_cap() * p->max_batch, hipHostMallocDefault));

@@ -63,10 +63,10 @@ struct Vp8Work {
     uint8_t* d_rec = nullptr;        // reconstruction planes (prediction context)
     vp8::MBOut* d_mbs = nullptr;     // per-MB decisions + levels
     uint8_t* d_nz = nullptr;         // per-MB outgoing non-zero contexts
-    vp8::MBOut* h_mbs = nullptr;     // pinned mirror of d_mbs
+    vp8::MBOut* h_mbs = nullptr;     // pinned mirror of d_mbs (host_buffers, frames too big to pack)
     uint8_t* d_pack = nullptr;       // k_vp8_pack scratch (pack_cap() bytes per image)
     uint8_t* h_pack = nullptr;       // pinned compact streams (single-image path)
-    int reserve(int w, int h, int n);
+    int reserve(int w, int h, int n, bool host_buffers);
     void release();
     size_t mb_count() const;
     size_t record_bytes(int n) const;  // MB records of n images

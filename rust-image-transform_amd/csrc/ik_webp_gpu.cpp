@@ -36,7 +36,7 @@ int default_webp_encoder() {
     return e;
 }
 
-int Vp8Work::reserve(int w_, int h_, int n_) {
+int Vp8Work::reserve(int w_, int h_, int n_, bool host_buffers) {
     const int mbw = (w_ + 15) >> 4, mbh = (h_ + 15) >> 4;
     const size_t nmb = (size_t)mbw * mbh;
     const size_t rec = vp8::vp8_rec_bytes(w_, h_);
@@ -45,11 +45,13 @@ int Vp8Work::reserve(int w_, int h_, int n_) {
     IK_HIP(hipMalloc(&d_rec, rec * n_ + 256));
     IK_HIP(hipMalloc(&d_mbs, sizeof(vp8::MBOut) * nmb * n_ + 256));
     IK_HIP(hipMalloc(&d_nz, 18 * nmb * n_ + 256));
-    IK_HIP(hipHostMalloc(&h_mbs, sizeof(vp8::MBOut) * nmb * n_, hipHostMallocDefault));
-    if (nmb <= (size_t)vp8::kMaxPackMBs) {
-        IK_HIP(hipMalloc(&d_pack, vp8::vp8_pack_cap(nmb) * n_));
-        IK_HIP(hipHostMalloc(&h_pack, vp8::vp8_pack_cap(nmb) * n_, hipHostMallocDefault));
-    }
+    const bool pack = nmb <= (size_t)vp8::kMaxPackMBs;
+    if (pack) IK_HIP(hipMalloc(&d_pack, vp8::vp8_pack_cap(nmb) * n_));
+    // pinned mirrors only for callers that copy through this object (the
+    // pipeline keeps its own per-slot buffers): compact streams, or full
+    // records for frames too big to pack
+    if (host_buffers && pack) IK_HIP(hipHostMalloc(&h_pack, vp8::vp8_pack_cap(nmb) * n_, hipHostMallocDefault));
+    if (host_buffers && !pack) IK_HIP(hipHostMalloc(&h_mbs, sizeof(vp8::MBOut) * nmb * n_, hipHostMallocDefault));
     w = w_; h = h_; cap_n = n_;
     return IK_OK;
 }
@@ -133,7 +135,7 @@ int webp_encode_gpu(const uint8_t* d_yuv, int w, int h, int quality, std::vector
     Vp8Work& wk = works[current_device()];
     hipStream_t s = thread_stream();
     if (!s) return fail(IK_ERR_DEVICE, "cannot create HIP stream");
-    if (int rc = wk.reserve(w, h, 1)) return rc;
+    if (int rc = wk.reserve(w, h, 1, true)) return rc;
     if (int rc = wk.launch(d_yuv, 0, 1, quality, s)) return rc;
     if (wk.packable()) {
         if (int rc = wk.pack_to(wk.h_pack, 1, s)) return rc;
