@@ -149,6 +149,22 @@ void webp_gamma_tables(uint16_t g2l[256], int l2g[33]) {
     for (int v = 0; v <= 32; ++v) l2g[v] = (int)(255. * pow(scale * v, 1. / 0.80) + .5);
 }
 
+void parallel_for(int n, int threads, const std::function<void(int)>& fn) {
+    if (n <= 0) return;
+    if (threads <= 0) threads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    threads = std::min(threads, n);
+    const int dev = current_device();
+    std::atomic<int> next{0};
+    auto work = [&](bool own) {
+        if (own) ik_init(dev);
+        for (int i; (i = next.fetch_add(1)) < n;) fn(i);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; ++t) th.emplace_back(work, true);
+    work(false);
+    for (auto& t : th) t.join();
+}
+
 namespace {
 std::atomic<int> g_resize_mode{-1};  // -1 = not yet read from IK_RESIZE_MODE
 }  // namespace
@@ -500,6 +516,7 @@ int ik_decode_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t n,
     std::vector<size_t> jl;
     std::vector<uint32_t> ji;
     std::vector<int> st(n, IK_OK);
+    std::vector<uint32_t> other;
     for (uint32_t i = 0; i < n; ++i) {
         outs[i] = nullptr;
         if (fmts) fmts[i] = -1;
@@ -510,9 +527,19 @@ int ik_decode_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t n,
             ji.push_back(i);
             if (fmts) fmts[i] = IK_FORMAT_JPEG;
         } else {
-            st[i] = ik_decode(bytes[i], lens[i], &outs[i], fmts ? &fmts[i] : nullptr);
+            other.push_back(i);
         }
     }
+    std::vector<std::string> msg(n);
+    parallel_for((int)other.size(), 0, [&](int k) {  // PNG / WebP / unknown: host decoders, in parallel
+        const uint32_t i = other[k];
+        st[i] = ik_decode(bytes[i], lens[i], &outs[i], fmts ? &fmts[i] : nullptr);
+        if (st[i]) {
+            char buf[256];
+            ik_last_error(buf, sizeof(buf));
+            msg[i] = buf;
+        }
+    });
     if (!ji.empty()) {
         std::vector<ik_image*> jo(ji.size(), nullptr);
         std::vector<int> js(ji.size(), IK_OK);
@@ -523,11 +550,13 @@ int ik_decode_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t n,
         }
     }
     int first = IK_OK;
+    uint32_t fi = 0;
     for (uint32_t i = 0; i < n; ++i) {
         if (status) status[i] = st[i];
-        if (st[i] && !first) first = st[i];
+        if (st[i] && !first) { first = st[i]; fi = i; }
     }
-    return first;
+    if (first) return fail(first, "input %u: %s", fi, msg[fi].empty() ? "JPEG decode failed" : msg[fi].c_str());
+    return IK_OK;
 }
 
 int ik_set_resize_mode(int mode) {

@@ -750,7 +750,10 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
         (void)hdr;
     }
     // 4. everything else: the single-image path with host entropy decoding
-    for (int i : host_idx) st[i] = decode_jpeg_impl(bytes[i], lens[i], &outs[i], false);
+    parallel_for((int)host_idx.size(), 0, [&](int k) {
+        const int i = host_idx[k];
+        st[i] = decode_jpeg_impl(bytes[i], lens[i], &outs[i], false);
+    });
     int first = IK_OK;
     for (int i = 0; i < n; ++i) {
         if (status) status[i] = st[i];

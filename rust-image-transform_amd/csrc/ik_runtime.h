@@ -2,6 +2,7 @@
 #pragma once
 #include <cstdarg>
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -27,6 +28,9 @@ int hip_fail(hipError_t e, const char* what);
     } while (0)
 
 int current_device();
+// fn(i) for i in [0, n) on up to `threads` host threads (0 = min(16, cores)); the
+// extra threads select the caller's HIP device first
+void parallel_for(int n, int threads, const std::function<void(int)>& fn);
 hipStream_t thread_stream();  // per-thread, per-device non-blocking stream
 size_t pitch_for(uint32_t w, uint32_t c);
 uint8_t* scratch(size_t bytes);  // per-thread device scratch, valid until the next call
