@@ -366,6 +366,157 @@ __global__ __launch_bounds__(kHuffThreads) void k_jpeg_huff_batch(const JpegScan
     if ((int)threadIdx.x < lanes && seg < a.n_seg) huff_interval(a, T, s_zz, s_ring[threadIdx.x], seg);
 }
 
+// ---- baseline scans without restart markers: self-synchronising decoding ------
+namespace {
+
+// MSB-first reader over the unstuffed scan (no markers, no stuffing), keeping
+// two words in registers: a load only when the position crosses a word
+struct SeqBits {
+    const uint32_t* w;
+    unsigned long long pos;
+    unsigned long long buf;  // words [idx, idx+1]
+    long long idx;
+    __device__ uint32_t peek32() {
+        const long long i = (long long)(pos >> 5);
+        if (i != idx) {
+            const uint32_t hi = (i == idx + 1) ? (uint32_t)buf : w[i];
+            buf = ((unsigned long long)hi << 32) | w[i + 1];
+            idx = i;
+        }
+        return (uint32_t)((buf << (pos & 31)) >> 32);
+    }
+};
+
+__device__ __forceinline__ int seq_sym(SeqBits& br, const JpegHuffTables& T, int t) {
+    const uint32_t win = br.peek32();
+    const int lv = T.look[t][win >> 23];
+    if (lv >> 8) {
+        br.pos += lv >> 8;
+        return lv & 0xff;
+    }
+    const int code = (int)(win >> 16);
+    int len = 10;
+#pragma unroll
+    for (int l = 10; l <= 16; ++l) len += code >= T.lj[t][l];
+    if (len > 16) return -1;
+    br.pos += len;
+    const int c = code >> (16 - len);
+    return T.vals[t][T.valptr[t][len] + c - T.mincode[t][len]];
+}
+
+__device__ __forceinline__ int seq_get(SeqBits& br, int n) {
+    if (!n) return 0;
+    const uint32_t v = br.peek32() >> (32 - n);
+    br.pos += n;
+    return (int)v;
+}
+
+// one block: DC difference into *dcdiff, AC levels into blk (natural order) when
+// blk != null; false on a bad code
+__device__ bool seq_block(SeqBits& br, const JpegHuffTables& T, const uint8_t* zz, int td, int ta, int* dcdiff,
+                          int16_t* blk) {
+    const int t = seq_sym(br, T, td);
+    if (t < 0 || t > 11) return false;
+    *dcdiff = t ? extend_dev(seq_get(br, t), t) : 0;
+    for (int k = 1; k < 64;) {
+        const int rs = seq_sym(br, T, 4 + ta);
+        if (rs < 0) return false;
+        const int r = rs >> 4, sz = rs & 15;
+        if (!sz) {
+            if (r != 15) break;
+            k += 16;
+            continue;
+        }
+        k += r;
+        if (k > 63) return false;
+        const int val = extend_dev(seq_get(br, sz), sz);
+        if (blk) blk[zz[k]] = (int16_t)val;
+        ++k;
+    }
+    return true;
+}
+
+}  // namespace
+
+// one sync round: lane t decodes from its guessed first block start to the
+// first block start at or past its subsequence end, which becomes lane t+1's guess
+__global__ __launch_bounds__(kHuffThreads) void k_jpeg_seq_sync(JpegSeqArgs a) {
+    __shared__ JpegHuffTables T;
+    __shared__ uint8_t s_zz[64];
+    load_tables(a.tabs, T, s_zz);
+    __syncthreads();
+    const int t = blockIdx.x * a.lanes + threadIdx.x;
+    if ((int)threadIdx.x >= a.lanes || t >= a.nsub) return;
+    SeqBits br{a.words, a.start_bit[t], 0, -2};
+    int j = a.start_j[t];
+    const unsigned long long end = (unsigned long long)(t + 1) * (unsigned long long)a.L;
+    int n = 0, dc[4] = {0, 0, 0, 0};
+    bool ok = true;
+    while (br.pos < end && br.pos < (unsigned long long)a.nbits) {
+        const int c = a.comp_of[j];
+        int diff;
+        if (!seq_block(br, T, s_zz, a.td[c], a.ta[c], &diff, nullptr)) { ok = false; break; }
+        dc[c] += diff;
+        ++n;
+        j = j + 1 == a.bpm ? 0 : j + 1;
+        if (n > (1 << 24)) { ok = false; break; }  // runaway guard
+    }
+    a.nblocks[t] = n;
+    for (int c = 0; c < 4; ++c) a.dcsum[t * 4 + c] = dc[c];
+    if (t + 1 < a.nsub) {
+        const unsigned long long nb = ok ? br.pos : ~0ull;  // a bad code: this guess is wrong, keep iterating
+        if (nb != a.start_bit[t + 1] || (ok ? j : 0) != a.start_j[t + 1]) atomicAdd(a.changed, 1);
+        a.next_bit[t + 1] = nb;
+        a.next_j[t + 1] = ok ? j : 0;
+    }
+    // the last lane runs into the scan's padding bits past the final block: what
+    // it decodes (or fails on) there is cut off by the host at the known block count
+}
+
+// the decode pass: converged starts, block and DC bases from prefix sums
+__global__ __launch_bounds__(kHuffThreads) void k_jpeg_seq_decode(JpegSeqArgs a) {
+    __shared__ JpegHuffTables T;
+    __shared__ uint8_t s_zz[64];
+    load_tables(a.tabs, T, s_zz);
+    __syncthreads();
+    const int t = blockIdx.x * a.lanes + threadIdx.x;
+    if ((int)threadIdx.x >= a.lanes || t >= a.nsub) return;
+    SeqBits br{a.words, a.start_bit[t], 0, -2};
+    const unsigned long long end = (unsigned long long)(t + 1) * (unsigned long long)a.L;
+    long long b = a.block_base[t];
+    int pred[4];
+    for (int c = 0; c < 4; ++c) pred[c] = a.dc_base[t * 4 + c];
+    const int nb = a.nblocks[t];
+    long long mcu = b / a.bpm;
+    int j = (int)(b - mcu * a.bpm);
+    int mx = (int)(mcu % a.mcux), my = (int)(mcu / a.mcux);
+    for (int i = 0; i < nb && br.pos < end; ++i, ++b) {
+        const int c = a.comp_of[j];
+        long long bi;
+        if (a.single) bi = a.blk0[c] + (b / a.single_bw) * a.bw[c] + (b % a.single_bw);
+        else bi = a.blk0[c] + (long long)(my * a.v[c] + a.by_of[j]) * a.bw[c] + mx * a.h[c] + a.bx_of[j];
+        int16_t* blk = a.coef + bi * 64;
+        int diff;
+        if (!seq_block(br, T, s_zz, a.td[c], a.ta[c], &diff, blk)) { atomicOr(a.err, 1); return; }
+        pred[c] += diff;
+        blk[0] = (int16_t)pred[c];
+        if (++j == a.bpm) {
+            j = 0;
+            if (++mx == a.mcux) { mx = 0; ++my; }
+        }
+    }
+}
+
+hipError_t launch_jpeg_seq_sync(const JpegSeqArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_jpeg_seq_sync, dim3((a.nsub + a.lanes - 1) / a.lanes), dim3(kHuffThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_jpeg_seq_decode(const JpegSeqArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_jpeg_seq_decode, dim3((a.nsub + a.lanes - 1) / a.lanes), dim3(kHuffThreads), 0, s, a);
+    return hipGetLastError();
+}
+
 namespace {
 int huff_lanes(int dflt) {
     static const int forced = [] {
@@ -376,6 +527,12 @@ int huff_lanes(int dflt) {
     return v < 1 ? 1 : (v > kHuffThreads ? kHuffThreads : v);
 }
 }  // namespace
+
+int jpeg_lanes_for(long long total) {
+    int want = 1;
+    while (want < 16 && (long long)want * 2 * 1024 <= total) want *= 2;
+    return huff_lanes(want);
+}
 
 hipError_t launch_jpeg_huff(const JpegScanArgs& a, hipStream_t s) {
     if (a.n_seg <= 0 || a.restart <= 0 || a.ns < 1 || a.ns > 4) return hipErrorInvalidValue;

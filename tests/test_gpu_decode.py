@@ -323,3 +323,23 @@ def test_decode_batch_reports_failures(ik):
     good = _jpeg(ikutil.synth(64, 48, 3, seed=1), quality=80, restart_marker_rows=1)
     with pytest.raises(TransformError):
         decode_image_batch([good, b"\x00" * 10, good])
+
+
+def test_jpeg_seq_opt_in_is_correct():
+    """IK_JPEG_SEQ=1 (self-synchronising GPU decoding of restart-free scans, opt-in):
+    pixels still equal libjpeg-turbo's, through the GPU or through the fallback."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import io,sys,numpy as np; sys.path[:0]=['rust-image-transform_amd','tests']\n"
+        "from PIL import Image; import ikutil; from imagekit import decode_image\n"
+        "for k,(w,h,sub) in enumerate([(640,480,2),(300,200,0),(97,61,1)]):\n"
+        "    buf=io.BytesIO(); Image.fromarray(ikutil.synth(w,h,3,seed=k,pattern='S')).save(buf,format='JPEG',quality=85,subsampling=sub)\n"
+        "    b=buf.getvalue(); img,_=decode_image(b)\n"
+        "    assert np.array_equal(img.to_array(), np.asarray(Image.open(io.BytesIO(b)))), k\n"
+        "print('ok')\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, IK_JPEG_SEQ="1"),
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]

@@ -13,7 +13,8 @@ def blobs(S, n):
     for i in range(n):
         buf = io.BytesIO()
         Image.fromarray(ikutil.synth(S, S, 3, seed=9 + i, pattern="S")).save(
-            buf, format="JPEG", quality=90, subsampling=2, restart_marker_rows=1)
+            buf, format="JPEG", quality=90, subsampling=2,
+            **({} if os.environ.get("NORST") else {"restart_marker_rows": 1}))
         out.append(buf.getvalue())
     return out
 
@@ -22,7 +23,8 @@ def run(mode):
     from imagekit import decode_image, decode_image_batch
     S, N = int(os.environ.get("S", "4096")), int(os.environ.get("N", "16"))
     bs = blobs(S, N)
-    tag = f"{S}x{S} q90 4:2:0 rst/row, {sum(map(len, bs)) / N / 1e6:.2f} MB each"
+    tag = (f"{S}x{S} q90 4:2:0 {'no restarts' if os.environ.get('NORST') else 'rst/row'}, "
+           f"{sum(map(len, bs)) / N / 1e6:.2f} MB each")
     if mode == "batch":
         decode_image_batch(bs[:2])
         t0 = time.perf_counter()
