@@ -153,6 +153,7 @@ struct JpegSeqArgs {
     int* nblocks;                         // [nsub]
     int* dcsum;                           // [nsub][4]
     int* changed;
+    int* flags;                           // [nsub] lane t+1's guess changed this round (lane 0: 0)
     const long long* block_base;          // decode pass: [nsub]
     const int* dc_base;                   // [nsub][4]
     int16_t* coef;

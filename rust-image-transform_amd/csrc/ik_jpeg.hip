@@ -465,7 +465,9 @@ __global__ __launch_bounds__(kHuffThreads) void k_jpeg_seq_sync(JpegSeqArgs a) {
     for (int c = 0; c < 4; ++c) a.dcsum[t * 4 + c] = dc[c];
     if (t + 1 < a.nsub) {
         const unsigned long long nb = ok ? br.pos : ~0ull;  // a bad code: this guess is wrong, keep iterating
-        if (nb != a.start_bit[t + 1] || (ok ? j : 0) != a.start_j[t + 1]) atomicAdd(a.changed, 1);
+        const int ch = nb != a.start_bit[t + 1] || (ok ? j : 0) != a.start_j[t + 1];
+        a.flags[t + 1] = ch;
+        if (ch) atomicAdd(a.changed, 1);
         a.next_bit[t + 1] = nb;
         a.next_j[t + 1] = ok ? j : 0;
     }

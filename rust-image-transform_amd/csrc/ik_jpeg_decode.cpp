@@ -129,19 +129,16 @@ struct Component {
 
 const char* const kFmtErr = "Format error decoding Jpeg";
 
-// Restart-free baseline scans on the GPU (self-synchronising decoding): opt-in
-// with IK_JPEG_SEQ=1.  Measured on 4:2:0 q90 scans, ~90 % of the 1-KiB lanes
-// synchronise in the first round but chains of lanes whose guessed MCU phase never
-// resynchronises within a lane remain, so the Jacobi rounds do not converge in
-// the budget and the image falls back to the host decoder (slower than host
-// decoding alone).  Off by default until the rounds propagate further.
+// Restart-free baseline scans on the GPU (self-synchronising decoding, run_seq);
+// IK_JPEG_SEQ=0 keeps them on the host entropy decoder.
 bool seq_enabled() {
     static const bool on = [] {
         const char* e = getenv("IK_JPEG_SEQ");
-        return e && !strcmp(e, "1");
+        return !(e && !strcmp(e, "0"));
     }();
     return on;
 }
+constexpr size_t kSeqMinBytes = 32 << 10;  // smaller scans: the host decoder is faster
 
 struct Decoder {
     const uint8_t* b;
@@ -384,6 +381,7 @@ struct Decoder {
             if (q + 1 >= end) { clean.push_back(0xFF); ++q; continue; }  // a lone 0xFF at the end: stuffed, as on the host
             break;  // a marker: the scan ends (the host feeds zeros from here)
         }
+        if (clean.size() < kSeqMinBytes) return false;
         const size_t nw = (clean.size() + 3) / 4 + 4;  // zero words past the end
         seq_words.assign(nw, 0u);
         for (size_t i = 0; i < clean.size(); ++i) seq_words[i >> 2] |= (uint32_t)clean[i] << (24 - 8 * (i & 3));
@@ -610,79 +608,188 @@ void qtables(const Decoder& d, uint16_t q[256]) {
 
 inline size_t up256(size_t x) { return (x + 255) / 256 * 256; }
 
+// Host decoder over the unstuffed words from an arbitrary (bit, MCU phase) state:
+// the frontier walk below uses it on the few lanes the GPU rounds leave unsynced.
+struct HostSeq {
+    const Decoder& d;
+    const JpegSeqArgs& a;
+    const uint32_t* w;
+    uint32_t peek32(unsigned long long pos) const {
+        const size_t i = (size_t)(pos >> 5);
+        const uint64_t buf = ((uint64_t)w[i] << 32) | w[i + 1];
+        return (uint32_t)((buf << (pos & 31)) >> 32);
+    }
+    int sym(unsigned long long& pos, const HuffTable& t) const {
+        const uint32_t win = peek32(pos);
+        const int look = (int)(win >> 23);
+        if (t.look_len[look]) { pos += t.look_len[look]; return t.look_val[look]; }
+        const int code = (int)(win >> 16);
+        for (int len = 10; len <= 16; ++len) {
+            const int c = code >> (16 - len);
+            if (t.maxcode[len] >= 0 && c <= t.maxcode[len] && c >= t.mincode[len]) {
+                pos += len;
+                return t.vals[t.valptr[len] + c - t.mincode[len]];
+            }
+        }
+        return -1;
+    }
+    int get(unsigned long long& pos, int n) const {
+        if (!n) return 0;
+        const int v = (int)(peek32(pos) >> (32 - n));
+        pos += n;
+        return v;
+    }
+    bool block(unsigned long long& pos, int c) const {
+        const int t = sym(pos, d.dc[a.td[c]]);
+        if (t < 0 || t > 11) return false;
+        (void)get(pos, t);
+        for (int k = 1; k < 64;) {
+            const int rs = sym(pos, d.ac[a.ta[c]]);
+            if (rs < 0) return false;
+            const int r = rs >> 4, sz = rs & 15;
+            if (!sz) {
+                if (r != 15) break;
+                k += 16;
+                continue;
+            }
+            k += r;
+            if (k > 63) return false;
+            (void)get(pos, sz);
+            ++k;
+        }
+        return true;
+    }
+    // lane u from (bit, j): the first block start at or past its end; false on a bad code
+    bool lane(int u, unsigned long long& bit, int& j) const {
+        const unsigned long long end = (unsigned long long)(u + 1) * (unsigned long long)a.L;
+        while (bit < end && bit < (unsigned long long)a.nbits) {
+            if (!block(bit, a.comp_of[j])) return false;
+            j = j + 1 == a.bpm ? 0 : j + 1;
+        }
+        return true;
+    }
+};
+
 // Self-synchronising GPU decoding of a scan recorded by defer_seq into the
-// coefficient image dcoef (pre-zeroed): sync rounds until no lane's guessed first
-// block start changes, prefix sums of the per-lane block counts / DC sums, then
-// the decode pass.  IK_OK, or 1: did not converge / inconsistent -> host decoder.
+// coefficient image dcoef (pre-zeroed).
+//  1. GPU rounds: every lane decodes from its guessed first block start (bit, MCU
+//     phase) to its end; the state there is the next lane's new guess.  Most lanes
+//     synchronise in the first round.
+//  2. Frontier walk on the host: from the first lane whose guess changed (its new
+//     guess is exact), decode lane by lane until the walk meets the GPU's chain
+//     again, then jump to the next changed lane -- only the unsynchronised stretches
+//     are decoded serially.
+//  3. A GPU round on the corrected starts must change nothing; its block counts and
+//     DC sums give the bases (host prefix sums) for the decode pass.
+// IK_OK, or 1: inconsistent (bad data) -> host decoder.
 int run_seq(const Decoder& d, const uint8_t* dtabs, int16_t* dcoef, hipStream_t s) {
     const JpegSeqArgs& base = d.seq_args;
     const int ns = base.nsub;
     const size_t wbytes = d.seq_words.size() * 4;
-    const size_t o_bitA = up256(wbytes), o_bitB = o_bitA + up256(8ull * ns), o_jA = o_bitB + up256(8ull * ns);
-    const size_t o_jB = o_jA + up256(4ull * ns), o_nb = o_jB + up256(4ull * ns), o_dc = o_nb + up256(4ull * ns);
-    const size_t o_bb = o_dc + up256(16ull * ns), o_db = o_bb + up256(8ull * ns), o_fl = o_db + up256(16ull * ns);
+    const size_t o_sb = up256(wbytes), o_nbit = o_sb + up256(8ull * ns), o_sj = o_nbit + up256(8ull * ns);
+    const size_t o_nj = o_sj + up256(4ull * ns), o_nb = o_nj + up256(4ull * ns), o_dc = o_nb + up256(4ull * ns);
+    const size_t o_bb = o_dc + up256(16ull * ns), o_db = o_bb + up256(8ull * ns), o_fg = o_db + up256(16ull * ns);
+    const size_t o_fl = o_fg + up256(4ull * ns);
     const size_t total = o_fl + 256;
     uint8_t* dev = nullptr;
     if (hipMalloc(&dev, total) != hipSuccess) return fail(IK_ERR_DEVICE, "hipMalloc(jpeg seq)");
     struct Free { uint8_t* p; ~Free() { if (p) (void)hipFree(p); } } guard{dev};
-    std::vector<unsigned long long> bit0(ns);
-    std::vector<int> j0(ns, 0);
-    for (int t = 0; t < ns; ++t) bit0[t] = (unsigned long long)t * base.L;  // guess: a block starts at each cut
+    static const bool timing = getenv("IK_JPEG_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<unsigned long long> S(ns), G(ns);
+    std::vector<int> Sj(ns, 0), Gj(ns, 0), flags(ns, 0);
+    for (int t = 0; t < ns; ++t) S[t] = (unsigned long long)t * base.L;  // guess: a block starts at each cut
     int rc = copy_h2d_2d(dev, wbytes, reinterpret_cast<const uint8_t*>(d.seq_words.data()), wbytes, wbytes, 1, s);
-    for (const size_t o : {o_bitA, o_bitB})
-        if (!rc) rc = copy_h2d_2d(dev + o, 8ull * ns, reinterpret_cast<const uint8_t*>(bit0.data()), 8ull * ns, 8ull * ns, 1, s);
-    for (const size_t o : {o_jA, o_jB})
-        if (!rc) rc = copy_h2d_2d(dev + o, 4ull * ns, reinterpret_cast<const uint8_t*>(j0.data()), 4ull * ns, 4ull * ns, 1, s);
     if (rc) return rc;
     JpegSeqArgs a = base;
     a.words = reinterpret_cast<const uint32_t*>(dev);
     a.tabs = reinterpret_cast<const JpegHuffTables*>(dtabs);
+    a.start_bit = reinterpret_cast<const unsigned long long*>(dev + o_sb);
+    a.start_j = reinterpret_cast<const int*>(dev + o_sj);
+    a.next_bit = reinterpret_cast<unsigned long long*>(dev + o_nbit);
+    a.next_j = reinterpret_cast<int*>(dev + o_nj);
     a.nblocks = reinterpret_cast<int*>(dev + o_nb);
     a.dcsum = reinterpret_cast<int*>(dev + o_dc);
+    a.flags = reinterpret_cast<int*>(dev + o_fg);
     a.changed = reinterpret_cast<int*>(dev + o_fl);
     a.err = reinterpret_cast<int*>(dev + o_fl + 4);
     a.coef = dcoef;
     a.lanes = jpeg_lanes_for(ns);
-    bool cur_a = true, converged = false;
-    int rounds = 0;
-    static const bool timing = getenv("IK_JPEG_TIMING") != nullptr;
-    const auto t0 = std::chrono::steady_clock::now();
-    for (int round = 0; round < 16 && !converged; ++round) {
-        ++rounds;
-        a.start_bit = reinterpret_cast<const unsigned long long*>(dev + (cur_a ? o_bitA : o_bitB));
-        a.start_j = reinterpret_cast<const int*>(dev + (cur_a ? o_jA : o_jB));
-        a.next_bit = reinterpret_cast<unsigned long long*>(dev + (cur_a ? o_bitB : o_bitA));
-        a.next_j = reinterpret_cast<int*>(dev + (cur_a ? o_jB : o_jA));
+    // one GPU round on the starts S: new guesses into G, flags; returns the changed count or < 0
+    auto round = [&]() -> int {
         int changed = 0;
+        int r = copy_h2d_2d(dev + o_sb, 8ull * ns, reinterpret_cast<const uint8_t*>(S.data()), 8ull * ns, 8ull * ns, 1, s);
+        if (!r) r = copy_h2d_2d(dev + o_sj, 4ull * ns, reinterpret_cast<const uint8_t*>(Sj.data()), 4ull * ns, 4ull * ns, 1, s);
+        if (r) return -1;
         hipError_t e = hipMemsetAsync(a.changed, 0, 4, s);
+        if (e == hipSuccess) e = hipMemsetAsync(a.flags, 0, 4ull * ns, s);
         if (e == hipSuccess) e = launch_jpeg_seq_sync(a, s);
         if (e == hipSuccess) e = hipMemcpyAsync(&changed, a.changed, 4, hipMemcpyDeviceToHost, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) return hip_fail(e, "jpeg seq sync");
-        converged = changed == 0;
-        if (timing && (round < 8 || round % 8 == 0)) fprintf(stderr, "[jpeg seq] round %d: %d lanes changed\n", round, changed);
-        if (!converged) cur_a = !cur_a;  // the guesses just written become the next round's starts
+        if (e != hipSuccess) { hip_fail(e, "jpeg seq sync"); return -1; }
+        if (changed) {
+            r = copy_d2h_2d(reinterpret_cast<uint8_t*>(G.data()), 8ull * ns, dev + o_nbit, 8ull * ns, 8ull * ns, 1, s);
+            if (!r) r = copy_d2h_2d(reinterpret_cast<uint8_t*>(Gj.data()), 4ull * ns, dev + o_nj, 4ull * ns, 4ull * ns, 1, s);
+            if (!r) r = copy_d2h_2d(reinterpret_cast<uint8_t*>(flags.data()), 4ull * ns, dev + o_fg, 4ull * ns, 4ull * ns, 1, s);
+            if (r) return -1;
+            G[0] = 0;
+            Gj[0] = 0;
+            flags[0] = 0;
+        }
+        return changed;
+    };
+    // round 1 from the naive guesses; round 2 from its results (most already exact),
+    // so that the walk below meets a chain whose starts are mostly right
+    int changed = round();
+    int walked = 0;
+    if (changed < 0) return 1;
+    if (changed > 0) {
+        S = G;
+        Sj = Gj;
+        changed = round();
+        if (changed < 0) return 1;
+    }
+    if (changed > 0) {
+        // lanes before the first changed one are consistent from lane 0, so that
+        // lane's new guess is exact; walk from there
+        const HostSeq hs{d, base, d.seq_words.data()};
+        std::vector<unsigned long long> T = S;
+        std::vector<int> Tj = Sj;
+        int u = 1;
+        while (u < ns && !flags[u]) ++u;
+        while (u < ns) {
+            unsigned long long bit = G[u];
+            int j = Gj[u];
+            T[u] = bit;
+            Tj[u] = j;
+            // walk until the walked state equals the GPU's guess for a lane whose own
+            // guess did not change (from there the GPU chain is consistent)
+            for (;;) {
+                if (!hs.lane(u, bit, j)) return 1;
+                ++walked;
+                ++u;
+                if (u >= ns) break;
+                T[u] = bit;
+                Tj[u] = j;
+                if (!flags[u] && bit == S[u] && j == Sj[u]) break;
+            }
+            while (u < ns && !flags[u]) ++u;  // consistent stretch: keep the GPU's starts
+        }
+        S = T;
+        Sj = Tj;
+        changed = round();  // verification: nothing may change now
+        if (changed != 0) return 1;
     }
     if (timing)
-        fprintf(stderr, "[jpeg seq] %d lanes, %d per wave, %d rounds, %s, %.2f ms\n", ns, a.lanes, rounds,
-                converged ? "converged" : "NOT converged",
+        fprintf(stderr, "[jpeg seq] %d lanes, %d per wave, %d lanes walked on the host, %.2f ms\n", ns, a.lanes, walked,
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-    if (!converged) return 1;
     // prefix sums on the host (a few thousand lanes)
     std::vector<int> nb(ns), dc(4ull * ns);
     rc = copy_d2h_2d(reinterpret_cast<uint8_t*>(nb.data()), 4ull * ns, dev + o_nb, 4ull * ns, 4ull * ns, 1, s);
     if (!rc) rc = copy_d2h_2d(reinterpret_cast<uint8_t*>(dc.data()), 16ull * ns, dev + o_dc, 16ull * ns, 16ull * ns, 1, s);
     if (rc) return rc;
-    std::vector<long long> bb(ns);
-    std::vector<int> db(4ull * ns);
     long long acc = 0;
-    int dacc[4] = {0, 0, 0, 0};
-    for (int t = 0; t < ns; ++t) {
-        bb[t] = acc;
-        acc += nb[t];
-        for (int c = 0; c < 4; ++c) { db[4 * t + c] = dacc[c]; dacc[c] += dc[4 * t + c]; }
-    }
-    if (timing) fprintf(stderr, "[jpeg seq] blocks %lld of %lld\n", acc, base.total_blocks);
+    for (int t = 0; t < ns; ++t) acc += nb[t];
     if (acc < base.total_blocks) return 1;  // a real block failed to decode: the host decoder decides
     if (acc > base.total_blocks) {  // blocks decoded from the padding past the final block: drop them
         long long excess = acc - base.total_blocks;
@@ -693,6 +800,15 @@ int run_seq(const Decoder& d, const uint8_t* dtabs, int16_t* dcoef, hipStream_t 
         }
         rc = copy_h2d_2d(dev + o_nb, 4ull * ns, reinterpret_cast<const uint8_t*>(nb.data()), 4ull * ns, 4ull * ns, 1, s);
         if (rc) return rc;
+    }
+    std::vector<long long> bb(ns);
+    std::vector<int> db(4ull * ns);
+    acc = 0;
+    int dacc[4] = {0, 0, 0, 0};
+    for (int t = 0; t < ns; ++t) {
+        bb[t] = acc;
+        acc += nb[t];
+        for (int c = 0; c < 4; ++c) { db[4 * t + c] = dacc[c]; dacc[c] += dc[4 * t + c]; }
     }
     rc = copy_h2d_2d(dev + o_bb, 8ull * ns, reinterpret_cast<const uint8_t*>(bb.data()), 8ull * ns, 8ull * ns, 1, s);
     if (!rc) rc = copy_h2d_2d(dev + o_db, 16ull * ns, reinterpret_cast<const uint8_t*>(db.data()), 16ull * ns, 16ull * ns, 1, s);

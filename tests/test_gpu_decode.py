@@ -343,3 +343,23 @@ def test_jpeg_seq_opt_in_is_correct():
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, IK_JPEG_SEQ="1"),
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("wh", [(1500, 1100), (2048, 1536), (1001, 999)])
+@pytest.mark.parametrize("sub", [0, 1, 2])
+@pytest.mark.parametrize("pat", ["S", "N"])
+def test_jpeg_no_restart_self_sync_gpu(ik, wh, sub, pat):
+    """Restart-free baseline scans >= 32 KB go through self-synchronising GPU
+    decoding (GPU rounds + host frontier walk + GPU decode pass): pixels equal
+    libjpeg-turbo's."""
+    w, h = wh
+    b = _jpeg(ikutil.synth(w, h, 3, seed=w + sub, pattern=pat), quality=92 if pat == "S" else 60, subsampling=sub)
+    img, _ = decode_image(b)
+    np.testing.assert_array_equal(img.to_array(), np.asarray(Image.open(io.BytesIO(b))))
+
+
+def test_jpeg_no_restart_gray_self_sync(ik):
+    g = ikutil.synth(1800, 1200, 1, seed=4, pattern="N")[..., 0]
+    b = _jpeg(g, quality=75)
+    img, _ = decode_image(b)
+    np.testing.assert_array_equal(img.to_array()[..., 0], np.asarray(Image.open(io.BytesIO(b))))
