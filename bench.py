@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=64, help="images per GPU per step")
-    ap.add_argument("--alt-batch", type=int, default=128, help="images per GPU per step for the other WebP encoder")
+    ap.add_argument("--alt-batch", type=int, default=256, help="images per GPU per step for the other WebP encoder")
     ap.add_argument("--alt-steps", type=int, default=4)
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--out", type=int, default=512)

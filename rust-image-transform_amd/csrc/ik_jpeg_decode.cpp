@@ -682,7 +682,15 @@ struct HostSeq {
 //  3. A GPU round on the corrected starts must change nothing; its block counts and
 //     DC sums give the bases (host prefix sums) for the decode pass.
 // IK_OK, or 1: inconsistent (bad data) -> host decoder.
-int run_seq(const Decoder& d, const uint8_t* dtabs, int16_t* dcoef, hipStream_t s) {
+// device bytes run_seq needs (part of the caller's scratch: no hipMalloc/hipFree,
+// which would synchronise the device under concurrent decodes)
+size_t seq_bytes(const Decoder& d) {
+    const size_t ns = (size_t)d.seq_args.nsub;
+    return up256(d.seq_words.size() * 4) + 2 * up256(8 * ns) + 3 * up256(4 * ns) + up256(16 * ns) + up256(8 * ns) +
+           up256(16 * ns) + up256(4 * ns) + 256;
+}
+
+int run_seq(const Decoder& d, const uint8_t* dtabs, int16_t* dcoef, uint8_t* dev, hipStream_t s) {
     const JpegSeqArgs& base = d.seq_args;
     const int ns = base.nsub;
     const size_t wbytes = d.seq_words.size() * 4;
@@ -690,10 +698,6 @@ int run_seq(const Decoder& d, const uint8_t* dtabs, int16_t* dcoef, hipStream_t 
     const size_t o_nj = o_sj + up256(4ull * ns), o_nb = o_nj + up256(4ull * ns), o_dc = o_nb + up256(4ull * ns);
     const size_t o_bb = o_dc + up256(16ull * ns), o_db = o_bb + up256(8ull * ns), o_fg = o_db + up256(16ull * ns);
     const size_t o_fl = o_fg + up256(4ull * ns);
-    const size_t total = o_fl + 256;
-    uint8_t* dev = nullptr;
-    if (hipMalloc(&dev, total) != hipSuccess) return fail(IK_ERR_DEVICE, "hipMalloc(jpeg seq)");
-    struct Free { uint8_t* p; ~Free() { if (p) (void)hipFree(p); } } guard{dev};
     static const bool timing = getenv("IK_JPEG_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<unsigned long long> S(ns), G(ns);
@@ -861,7 +865,8 @@ int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gp
     const size_t pl_off = qbytes + (cbytes + 255) / 256 * 256;
     const size_t t_off = pl_off + (plane_bytes + 255) / 256 * 256;
     const size_t e_off = t_off + tbytes, s_off = e_off + 256, d_off = s_off + sbytes;
-    uint8_t* dev = scratch(d_off + dbytes + 1024);  // the GPU bit reader fetches 64-B chunks past the end
+    const size_t q_off = up256(d_off + dbytes + 1024);  // the restart bit reader fetches 64-B chunks past the end
+    uint8_t* dev = scratch(q_off + (gpu && seq ? seq_bytes(d) : 0));
     if (!dev) { ik_image_free(img); return fail(IK_ERR_DEVICE, "cannot allocate device scratch"); }
     hipStream_t s = thread_stream();
     st = copy_h2d_2d(dev, qbytes, reinterpret_cast<const uint8_t*>(q.data()), qbytes, qbytes, 1, s);
@@ -871,7 +876,7 @@ int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gp
         st = copy_h2d_2d(dev + t_off, sizeof(tabs), reinterpret_cast<const uint8_t*>(&tabs), sizeof(tabs),
                          sizeof(tabs), 1, s);
         if (!st && hipMemsetAsync(dev + qbytes, 0, cbytes, s) != hipSuccess) st = fail(IK_ERR_DEVICE, "memset");
-        if (!st) st = run_seq(d, dev + t_off, reinterpret_cast<int16_t*>(dev + qbytes), s);
+        if (!st) st = run_seq(d, dev + t_off, reinterpret_cast<int16_t*>(dev + qbytes), dev + q_off, s);
         if (st == 1) {  // not resolved on the GPU: the host decoder decides
             ik_image_free(img);
             return decode_jpeg_impl(bytes, n, out, false);
