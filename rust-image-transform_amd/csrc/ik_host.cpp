@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -128,6 +129,31 @@ uint8_t* scratch(size_t bytes) {
 
 size_t pitch_for(uint32_t w, uint32_t c) { return ((size_t)w * c + 255) & ~size_t(255); }
 
+// Device image blocks are recycled per device: hipFree synchronises the whole
+// device, which would serialise every thread's stream under request load.  A
+// freed block is kept (up to kPoolBytes per device) and handed to the next image
+// that fits in it; every API call has synchronised its own stream before it
+// returns, so a block is idle when it comes back.
+namespace {
+constexpr size_t kPoolBytes = size_t(4) << 30;
+struct ImagePool {
+    std::mutex mu;
+    std::multimap<size_t, uint8_t*> free_blocks;
+    size_t held = 0;
+};
+ImagePool& image_pool(int device) {
+    static std::mutex mu;
+    static std::map<int, ImagePool*> pools;
+    std::lock_guard<std::mutex> lk(mu);
+    ImagePool*& p = pools[device];
+    if (!p) p = new ImagePool();
+    return *p;
+}
+size_t block_size(size_t bytes) {  // 64 KiB granules: images of similar sizes share blocks
+    return (bytes + (size_t(64) << 10) - 1) & ~((size_t(64) << 10) - 1);
+}
+}  // namespace
+
 int alloc_image(uint32_t w, uint32_t h, uint32_t c, ik_image** out) {
     auto* img = new ik_image();
     img->w = w; img->h = h; img->c = c;
@@ -135,8 +161,23 @@ int alloc_image(uint32_t w, uint32_t h, uint32_t c, ik_image** out) {
     img->device = current_device();
     (void)hipSetDevice(img->device);
     // + 16 bytes: the fused kernel's 8-byte lane loads may touch the pitch tail
-    hipError_t e = hipMalloc(&img->d, img->pitch * (size_t)(h ? h : 1) + 16);
-    if (e != hipSuccess) { delete img; return hip_fail(e, "hipMalloc(image)"); }
+    const size_t need = block_size(img->pitch * (size_t)(h ? h : 1) + 16);
+    ImagePool& pool = image_pool(img->device);
+    {
+        std::lock_guard<std::mutex> lk(pool.mu);
+        auto it = pool.free_blocks.lower_bound(need);
+        if (it != pool.free_blocks.end() && it->first <= 2 * need) {  // reuse a block at most twice the size
+            img->d = it->second;
+            img->block = it->first;
+            pool.held -= it->first;
+            pool.free_blocks.erase(it);
+        }
+    }
+    if (!img->d) {
+        hipError_t e = hipMalloc(&img->d, need);
+        if (e != hipSuccess) { delete img; return hip_fail(e, "hipMalloc(image)"); }
+        img->block = need;
+    }
     *out = img;
     return IK_OK;
 }
@@ -390,7 +431,19 @@ int ik_image_to_host(const ik_image* img, uint8_t* dst, size_t cap) {
 
 void ik_image_free(ik_image* img) {
     if (!img) return;
-    if (img->owned && img->d) (void)hipFree(img->d);
+    if (img->owned && img->d) {
+        ImagePool& pool = image_pool(img->device);
+        bool kept = false;
+        if (img->block) {
+            std::lock_guard<std::mutex> lk(pool.mu);
+            if (pool.held + img->block <= kPoolBytes) {
+                pool.free_blocks.emplace(img->block, img->d);
+                pool.held += img->block;
+                kept = true;
+            }
+        }
+        if (!kept) (void)hipFree(img->d);
+    }
     delete img;
 }
 
@@ -583,6 +636,9 @@ int ik_transform_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t
     threads = (int)std::min<uint32_t>((uint32_t)threads, n);
     std::vector<std::string> errs(n);
     std::atomic<uint32_t> next{0};
+    static const bool timing = getenv("IK_TIMING") != nullptr;  // dev: per-stage sums to stderr
+    std::mutex tmu;
+    double t_resize = 0, t_encode = 0;
     auto work = [&](bool own_thread) {
         if (own_thread) ik_init(dev);
         for (uint32_t i; (i = next.fetch_add(1)) < n;) {
@@ -592,8 +648,16 @@ int ik_transform_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t
                 continue;
             }
             ik_image* rs = nullptr;
+            const auto t0 = std::chrono::steady_clock::now();
             int r = ik_resize(imgs[i], w[i], h[i], filter, &rs);
+            const auto t1 = std::chrono::steady_clock::now();
             if (!r) r = ik_encode(rs, fmt[i], quality[i], &outs[i], &out_lens[i]);
+            if (timing) {
+                const auto t2 = std::chrono::steady_clock::now();
+                std::lock_guard<std::mutex> lk(tmu);
+                t_resize += std::chrono::duration<double, std::milli>(t1 - t0).count();
+                t_encode += std::chrono::duration<double, std::milli>(t2 - t1).count();
+            }
             if (r) {
                 char buf[256];
                 ik_last_error(buf, sizeof(buf));
@@ -609,6 +673,8 @@ int ik_transform_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t
     for (int t = 1; t < threads; ++t) th.emplace_back(work, true);
     work(false);
     for (auto& t : th) t.join();
+    if (timing) fprintf(stderr, "[transform_batch] %u requests, %d threads: resize %.1f ms, encode %.1f ms (summed)\n",
+                        n, threads, t_resize, t_encode);
     int first = IK_OK;
     uint32_t first_i = 0;
     for (uint32_t i = 0; i < n; ++i) {

@@ -17,6 +17,7 @@
 #include <tuple>
 
 #include "ik_internal.h"
+#include "ik_runtime.h"
 
 
 namespace ik {
@@ -122,6 +123,8 @@ namespace {
 
 std::mutex g_plan_mu;
 std::map<std::tuple<int, int, int, int, int, int, int, int, int>, ResizePlan*> g_plans;
+// request -> plan (several requests can share one plan in g_plans)
+std::map<std::tuple<int, int, int, int, int, int, int, int, int, int, int>, ResizePlan*> g_front;
 
 template <typename T>
 size_t put(std::vector<char>& blob, const std::vector<T>& v) {
@@ -133,7 +136,28 @@ size_t put(std::vector<char>& blob, const std::vector<T>& v) {
 
 }  // namespace
 
+ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, int filter, int n);
+
 ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int filter, int n) {
+    // front cache on the request itself (plus the dev overrides), so a repeated
+    // geometry costs a map lookup, not a recomputation of the weights
+    auto env_i = [](const char* k) { const char* e = getenv(k); return e ? atoi(e) : -1; };
+    const auto fkey = std::make_tuple(device, W, H, C, nw, nh, filter, n, env_i("IK_TARGET_WG"),
+                                      env_i("IK_BAND_ROWS"), env_i("IK_FLUSH_ROWS"));
+    {
+        std::lock_guard<std::mutex> lk(g_plan_mu);
+        auto it = g_front.find(fkey);
+        if (it != g_front.end()) return it->second;
+    }
+    ResizePlan* p = build_resize_plan(device, W, H, C, nw, nh, filter, n);
+    if (p) {
+        std::lock_guard<std::mutex> lk(g_plan_mu);
+        g_front[fkey] = p;
+    }
+    return p;
+}
+
+ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, int filter, int n) {
     // band height depends on how many images share the launch: aim for >= 2048
     // workgroups (8 per CU) without cutting bands below 32 rows
     std::vector<int> lx, cx, ly, cy;
@@ -286,9 +310,12 @@ ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int
     p->NS = NS;
     p->NB = (int)bands.size() / 2;
     p->table_bytes = blob.size();
+    // upload on this thread's stream, synchronised there (copy_h2d_2d): done
+    // before any stream launches with the plan, without a device-wide sync
     if (hipMalloc(&p->dev_tables, blob.size()) != hipSuccess ||
-        hipMemcpy(p->dev_tables, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess ||
-        hipDeviceSynchronize() != hipSuccess) {  // order before non-blocking streams
+        copy_h2d_2d(static_cast<uint8_t*>(p->dev_tables), blob.size(), reinterpret_cast<const uint8_t*>(blob.data()),
+                    blob.size(), blob.size(), 1,
+                    thread_stream()) != IK_OK) {
         delete p;
         return nullptr;
     }

@@ -14,6 +14,7 @@ struct ik_image {
     uint8_t* d = nullptr;          // device pixels
     bool owned = true;
     int device = 0;
+    size_t block = 0;              // bytes of the pooled allocation behind d (owned images)
 };
 
 namespace ik {
