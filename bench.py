@@ -41,7 +41,8 @@ METRIC = "transform MPix/s (decode+resize+encode) 4096²→512² WebP q80; 1/2/4
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FILTERS = {"nearest": 0, "triangle": 1, "catmullrom": 2, "gaussian": 3, "lanczos3": 4}
 ENCODERS = {"libwebp": 0, "gpu": 1}
-FORMATS = {"jpeg": 0, "webp": 1}
+CPU_CODER = {"webp": "libwebp", "jpeg": "image-crate JPEG", "avif": "libavif/aom speed 4 (Pillow, rav1e absent)"}
+FORMATS = {"jpeg": 0, "webp": 1, "avif": 2}
 
 
 def parse():
@@ -56,8 +57,9 @@ def parse():
     ap.add_argument("--out", type=int, default=512)
     ap.add_argument("--filter", default="triangle", choices=sorted(FILTERS))
     ap.add_argument("--quality", type=int, default=80)
-    ap.add_argument("--format", default="webp", choices=["webp", "jpeg"],
-                    help="webp: the headline (configs[1]); jpeg: configs[2]-style runs (GPU Huffman coding)")
+    ap.add_argument("--format", default="webp", choices=["webp", "jpeg", "avif"],
+                    help="webp: the headline (configs[1]); jpeg: configs[2]-style runs (GPU Huffman coding); "
+                         "avif: configs[4]-style runs (--size 8192 --out 1024 --filter lanczos3 --quality 60)")
     ap.add_argument("--threads", type=int, default=16, help="host entropy-coder threads per rank")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample wall-time budget (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -105,8 +107,17 @@ def cpu_baseline(args, img: np.ndarray):
     lock = threading.Lock()
 
     def one():
-        b, dims = orc.transform(img, args.out, args.out, f, FORMATS[args.format], args.quality)
-        assert dims == (args.out, args.out) and b[:2] in (b"RI", b"\xff\xd8")
+        if args.format == "avif":  # oracle resize + libavif/aom (Pillow's, one thread), speed 4 as ravif's
+            import io
+
+            from PIL import Image
+            px = orc.resize(img, args.out, args.out, f)
+            bio = io.BytesIO()
+            Image.fromarray(px[..., :3]).save(bio, format="AVIF", quality=args.quality, speed=4, max_threads=1)
+            assert bio.getvalue()[4:8] == b"ftyp"
+        else:
+            b, dims = orc.transform(img, args.out, args.out, f, FORMATS[args.format], args.quality)
+            assert dims == (args.out, args.out) and b[:2] in (b"RI", b"\xff\xd8")
         with lock:
             done[0] += 1
 
@@ -134,7 +145,7 @@ def cpu_baseline(args, img: np.ndarray):
         "cores": threads,
         "kind": "port",
         "sample": f"{n} x {W}x{H} RGBA8 -> {args.out}x{args.out} {args.filter} + "
-                  f"{'libwebp' if args.format == 'webp' else 'image-crate JPEG'} q{args.quality}, "
+                  f"{CPU_CODER[args.format]} q{args.quality}, "
                   f"one image per thread, {threads} threads, {wall:.1f}s wall",
         "value_1core": round(W * H / t1 / 1e6, 3),
         "host": host_info(),
@@ -253,7 +264,7 @@ def main():
     elapsed = reduce_max(elapsed, dist, f"cuda:{local}")
 
     if not args.device_only:
-        assert bytes(out[:2]) in (b"RI", b"\xff\xd8") and all(s > 0 for s in sizes)
+        assert (bytes(out[:2]) in (b"RI", b"\xff\xd8") or bytes(out[4:8]) == b"ftyp") and all(s > 0 for s in sizes)
     resize_ms = float(np.mean([k[0] for k in kms]))
     colour_ms = float(np.mean([k[1] for k in kms]))
     vp8_ms = float(np.mean([k[2] for k in kms]))
@@ -355,7 +366,8 @@ def main():
     if rank == 0:
         line = {
             "metric": METRIC if args.format == "webp" else
-                      f"transform MPix/s (resize+encode) {S}²→{O}² {args.filter} JPEG q{args.quality} (configs[2] shape)",
+                      f"transform MPix/s (resize+encode) {S}²→{O}² {args.filter} {args.format.upper()} q{args.quality} "
+                      f"(configs[{2 if args.format == 'jpeg' else 4}] shape)",
             "value": round(value, 2),
             "unit": "MPix/s",
             "n_gpus": world,

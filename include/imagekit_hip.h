@@ -131,7 +131,10 @@ int ik_transform_batch(const uint8_t *const *bytes, const size_t *lens, uint32_t
  * (image i at dev_src + i*src_image_stride, rows src_pitch bytes apart) ->
  * resize to nw x nh -> encode.  Encoded bytes are written into the caller's
  * host buffer `out` (capacity out_cap) back to back; out_sizes[i] receives each
- * size.  threads = host entropy-coder threads (0 = default). */
+ * size.  threads = host entropy-coder threads (0 = default).  fmt: any
+ * IK_FORMAT_*; JPEG is coded on the GPU, WebP by libwebp (or the GPU VP8
+ * encoder) and AVIF by libavif/aom on the host threads, from planes the GPU
+ * converted (the encode_image branches, src/transform.rs:121-146). */
 typedef struct ik_pipeline ik_pipeline;
 int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t nh, int filter,
                        int fmt, int quality, uint32_t max_batch, int threads, ik_pipeline **out);

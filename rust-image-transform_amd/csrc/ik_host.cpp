@@ -336,17 +336,14 @@ int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, 
         uint8_t* dp = scratch(4 * n + 256);
         if (!dp) return fail(IK_ERR_DEVICE, "cannot allocate device scratch");
         int* dflag = reinterpret_cast<int*>(dp + 4 * n + 128 - ((4 * n) & 127));
-        const int one = 1;
-        int rc = copy_h2d_2d(reinterpret_cast<uint8_t*>(dflag), 4, reinterpret_cast<const uint8_t*>(&one), 4, 4, 1, s);
-        if (rc) return rc;
-        hipError_t e = launch_avif_yuv444(dev, (int)w, (int)h, (int)c, pitch, dp, dflag, s);
+        hipError_t e = launch_avif_yuv444(dev, (int)w, (int)h, (int)c, pitch, 0, dp, 0, dflag, 1, s);
         if (e != hipSuccess) return hip_fail(e, "avif yuv444");
         std::vector<uint8_t> planes(4 * n);
-        int opaque = 1;
-        rc = copy_d2h_2d(planes.data(), 4 * n, dp, 4 * n, 4 * n, 1, s);
-        if (!rc) rc = copy_d2h_2d(reinterpret_cast<uint8_t*>(&opaque), 4, reinterpret_cast<const uint8_t*>(dflag), 4, 4, 1, s);
+        int transparent = 0;
+        int rc = copy_d2h_2d(planes.data(), 4 * n, dp, 4 * n, 4 * n, 1, s);
+        if (!rc) rc = copy_d2h_2d(reinterpret_cast<uint8_t*>(&transparent), 4, reinterpret_cast<const uint8_t*>(dflag), 4, 4, 1, s);
         if (rc) return rc;
-        return avif_encode_yuv444(planes.data(), !opaque, (int)w, (int)h, q, 4, out);
+        return avif_encode_yuv444(planes.data(), transparent != 0, (int)w, (int)h, q, 4, out);
     }
     return fail(IK_ERR_INVALID, "unknown ImageFormat %d", fmt);
 }

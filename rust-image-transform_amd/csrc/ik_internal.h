@@ -79,8 +79,10 @@ hipError_t launch_webp_yuv420(const uint8_t* src, int w, int h, int C, size_t pi
                               size_t img_stride, uint8_t* yuv /* Y, U, V planes per image */,
                               size_t yuv_img_stride, int n, const uint16_t* gamma_to_lin,
                               const int* lin_to_gamma, hipStream_t s);
-hipError_t launch_avif_yuv444(const uint8_t* src, int w, int h, int C, size_t pitch,
-                              uint8_t* planes /* Y, U, V, A: w*h each */, int* opaque, hipStream_t s);
+// n images; planes (Y, U, V, A: w*h each) plane_img_stride apart; transparent[n]
+// zeroed here, then set to 1 for every image with an alpha < 255
+hipError_t launch_avif_yuv444(const uint8_t* src, int w, int h, int C, size_t pitch, size_t img_stride,
+                              uint8_t* planes, size_t plane_img_stride, int* transparent, int n, hipStream_t s);
 hipError_t launch_jpeg_coeffs(const uint8_t* src, int w, int h, int C, size_t pitch,
                               size_t img_stride, const uint8_t* qtables /*dev, 128 B*/,
                               int16_t* coef, size_t coef_img_stride, int n, hipStream_t s);

@@ -475,14 +475,17 @@ hipError_t launch_webp_yuv420(const uint8_t* src, int w, int h, int C, size_t pi
 
 // ---------------------------------------------------------------------------
 // AVIF front end (image 0.25.8 AvifEncoder: to_rgba8 -> ravif RGB->YCbCr): BT.601
-// full-range 4:4:4 planes plus the alpha plane; `opaque` drops to 0 when any
-// alpha < 255 (ravif then codes an alpha plane).  One lane per pixel.
+// full-range 4:4:4 planes plus the alpha plane; transparent[z] becomes 1 when any
+// alpha of image z is < 255 (ravif then codes an alpha plane; the caller zeroes
+// the flags).  One lane per pixel, grid.z = image of the batch.
 __global__ __launch_bounds__(kThreads) void k_avif_yuv444(const uint8_t* __restrict__ src, int w, int h, int C,
-                                                          size_t pitch, uint8_t* __restrict__ planes,
-                                                          int* __restrict__ opaque) {
-    const int x = blockIdx.x * kThreads + threadIdx.x, y = blockIdx.y;
+                                                          size_t pitch, size_t img_stride,
+                                                          uint8_t* __restrict__ planes, size_t plane_img_stride,
+                                                          int* __restrict__ transparent) {
+    const int x = blockIdx.x * kThreads + threadIdx.x, y = blockIdx.y, z = blockIdx.z;
     if (x >= w) return;
-    const uint8_t* p = src + (size_t)y * pitch + (size_t)x * C;
+    const uint8_t* p = src + img_stride * z + (size_t)y * pitch + (size_t)x * C;
+    planes += plane_img_stride * z;
     int r, g, b, al = 255;
     if (C >= 3) { r = p[0]; g = p[1]; b = p[2]; if (C == 4) al = p[3]; }
     else { r = g = b = p[0]; if (C == 2) al = p[1]; }
@@ -495,13 +498,16 @@ __global__ __launch_bounds__(kThreads) void k_avif_yuv444(const uint8_t* __restr
     planes[n + i] = q8(U);
     planes[2 * n + i] = q8(V);
     planes[3 * n + i] = (uint8_t)al;
-    if (al != 255) atomicAnd(opaque, 0);
+    // one atomic per wave at most: the first lane that sees a translucent pixel
+    const uint64_t m = __ballot(al != 255);
+    if (m && (threadIdx.x & 63) == (int)__builtin_ctzll(m)) atomicOr(transparent + z, 1);
 }
 
-hipError_t launch_avif_yuv444(const uint8_t* src, int w, int h, int C, size_t pitch, uint8_t* planes,
-                              int* opaque, hipStream_t s) {
-    hipLaunchKernelGGL(k_avif_yuv444, dim3((w + kThreads - 1) / kThreads, h), dim3(kThreads), 0, s, src, w, h, C,
-                       pitch, planes, opaque);
+hipError_t launch_avif_yuv444(const uint8_t* src, int w, int h, int C, size_t pitch, size_t img_stride,
+                              uint8_t* planes, size_t plane_img_stride, int* transparent, int n, hipStream_t s) {
+    if (hipError_t e = hipMemsetAsync(transparent, 0, sizeof(int) * (size_t)n, s)) return e;
+    hipLaunchKernelGGL(k_avif_yuv444, dim3((w + kThreads - 1) / kThreads, h, n), dim3(kThreads), 0, s, src, w, h, C,
+                       pitch, img_stride, planes, plane_img_stride, transparent);
     return hipGetLastError();
 }
 

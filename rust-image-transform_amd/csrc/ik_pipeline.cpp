@@ -122,6 +122,8 @@ struct ik_pipeline {
         uint8_t* h_pack = nullptr;        // pinned compact MB streams (GPU VP8, k_vp8_pack)
         uint8_t* h_jpeg = nullptr;        // pinned entropy-coded JPEG segments (k_jpeg_huff_enc), jcap apart
         uint32_t* h_jlen = nullptr;       // their lengths
+        int* d_aflag = nullptr;           // AVIF: per image, 1 when any alpha < 255 (k_avif_yuv444)
+        int* h_aflag = nullptr;           // their pinned copies
         // resize start / end, colour end, vp8 end, copies end, vp8 start (stream2)
         hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
         uint8_t* d_stage = nullptr;       // this slot's part of ik_pipeline::d_stage
@@ -165,7 +167,10 @@ int enqueue(ik_pipeline* p, ik_pipeline::Slot& s, const uint8_t* dev_src, size_t
     // the slot's stage planes were last read by the wavefront of the batch two
     // back (stream2): its end event is still in s.ev[3] (a no-op wait if never recorded)
     IK_HIP(hipStreamWaitEvent(p->stream, s.ev[3], 0));
-    if (p->fmt == IK_FORMAT_WEBP) {
+    if (p->fmt == IK_FORMAT_AVIF) {
+        IK_HIP(launch_avif_yuv444(p->d_resized, (int)p->nw, (int)p->nh, (int)p->C, p->r_pitch, p->r_img_stride,
+                                  s.d_stage, p->stage_bytes, s.d_aflag, (int)n, p->stream));
+    } else if (p->fmt == IK_FORMAT_WEBP) {
         const DeviceConsts* dc = device_consts(p->device);
         IK_HIP(launch_webp_yuv420(p->d_resized, (int)p->nw, (int)p->nh, (int)p->C, p->r_pitch,
                                   p->r_img_stride, s.d_stage, p->stage_bytes, (int)n,
@@ -209,6 +214,8 @@ int enqueue(ik_pipeline* p, ik_pipeline::Slot& s, const uint8_t* dev_src, size_t
         IK_HIP(hipEventRecord(s.ev[3], p->stream));
         if (copy_out && p->fmt != IK_FORMAT_JPEG)
             IK_HIP(hipMemcpyAsync(s.h_stage, s.d_stage, p->stage_bytes * n, hipMemcpyDeviceToHost, p->stream));
+        if (copy_out && p->fmt == IK_FORMAT_AVIF)
+            IK_HIP(hipMemcpyAsync(s.h_aflag, s.d_aflag, sizeof(int) * n, hipMemcpyDeviceToHost, p->stream));
         IK_HIP(hipEventRecord(s.ev[4], p->stream));
     }
     return IK_OK;
@@ -245,6 +252,15 @@ int host_stage(ik_pipeline* p, const ik_pipeline::Slot& s, uint8_t* out, size_t 
             }
         } else if (s.gpu_vp8) {
             p->vp8.write_from(s.h_mbs, i, p->quality, p->outs[i]);
+        } else if (p->fmt == IK_FORMAT_AVIF) {
+            // image 0.25.8 AvifEncoder::new_with_speed_quality(out, 4, q) (src/transform.rs:140-145)
+            p->status[i] = avif_encode_yuv444(st, s.h_aflag[i] != 0, (int)p->nw, (int)p->nh, p->quality, 4,
+                                              p->outs[i]);
+            if (p->status[i]) {
+                char buf[256];
+                ik_last_error(buf, sizeof(buf));
+                errs[i] = buf;
+            }
         } else if (p->fmt == IK_FORMAT_WEBP) {
             const size_t ys = (size_t)p->nw * p->nh, uvs = (size_t)((p->nw + 1) / 2) * ((p->nh + 1) / 2);
             p->status[i] = webp_encode_yuv420(st, st + ys, st + ys + uvs, (int)p->nw, (int)p->nh,
@@ -299,8 +315,8 @@ int pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t nh
 int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t nh, int filter,
                        int fmt, int quality, uint32_t max_batch, int threads, ik_pipeline** out) {
     if (!out || !W || !H || !nw || !nh || !max_batch || C < 1 || C > 4) return fail(IK_ERR_INVALID, "bad geometry");
-    if (fmt != IK_FORMAT_WEBP && fmt != IK_FORMAT_JPEG)
-        return fail(IK_ERR_UNSUPPORTED, "pipeline supports jpeg and webp output");
+    if (fmt != IK_FORMAT_WEBP && fmt != IK_FORMAT_JPEG && fmt != IK_FORMAT_AVIF)
+        return fail(IK_ERR_INVALID, "unknown ImageFormat %d", fmt);
     auto* p = new ik_pipeline();
     const int rc = pipeline_create(W, H, C, nw, nh, filter, fmt, quality, max_batch, threads, p);
     if (rc) {  // release whatever was allocated before the failure
@@ -332,6 +348,12 @@ int pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t nh
     if (fmt == IK_FORMAT_WEBP) {
         const size_t uvw = (nw + 1) / 2, uvh = (nh + 1) / 2;
         p->stage_bytes = (size_t)nw * nh + 2 * uvw * uvh;
+    } else if (fmt == IK_FORMAT_AVIF) {  // Y, U, V, A planes (4:4:4), 256-B aligned per image
+        p->stage_bytes = (4 * (size_t)nw * nh + 255) & ~(size_t)255;
+        for (auto& sl : p->slot) {
+            IK_HIP(hipMalloc(&sl.d_aflag, sizeof(int) * max_batch));
+            IK_HIP(hipHostMalloc(&sl.h_aflag, sizeof(int) * max_batch, hipHostMallocDefault));
+        }
     } else {
         p->stage_bytes = (size_t)((nw + 7) / 8) * ((nh + 7) / 8) * 3 * 64 * sizeof(int16_t);
         jpeg_quant_tables(p->quality, p->qt);
@@ -453,6 +475,8 @@ void ik_pipeline_destroy(ik_pipeline* p) {
         if (sl.h_pack) (void)hipHostFree(sl.h_pack);
         if (sl.h_jpeg) (void)hipHostFree(sl.h_jpeg);
         if (sl.h_jlen) (void)hipHostFree(sl.h_jlen);
+        if (sl.d_aflag) (void)hipFree(sl.d_aflag);
+        if (sl.h_aflag) (void)hipHostFree(sl.h_aflag);
         for (auto& e : sl.ev)
             if (e) (void)hipEventDestroy(e);
     }

@@ -71,3 +71,68 @@ def test_pipeline_config2_shape(ik, oracle):
     for im, b in zip(imgs, got):
         assert b[:2] == b"\xff\xd8" and b[-2:] == b"\xff\xd9"
         assert b == oracle.jpeg_encode_rgb(oracle.to_rgb8(oracle.resize(im, 512, 512, 4)), 85)
+
+
+# ---- AVIF (image AvifEncoder -> ravif/rav1e in the reference; libavif/aom here) ----
+# rav1e is absent, so AVIF bytes are parity-unpinned against the reference (DESIGN
+# section 8).  The bar here: the pipeline's batched GPU colour conversion hands
+# libavif exactly the planes the single-image encode_image path does, so the
+# bytes are identical to encode_image on the oracle-resized pixels, and they
+# decode (Pillow/dav1d) close to those pixels.
+IK_AVIF = 2
+
+
+def _psnr(a, b):
+    mse = np.mean((a.astype(np.float64) - b.astype(np.float64)) ** 2)
+    return 99.0 if mse == 0 else 10 * np.log10(255.0 ** 2 / mse)
+
+
+def _decode_rgba(b):
+    import io
+
+    from PIL import Image
+    return np.asarray(Image.open(io.BytesIO(b)).convert("RGBA"))
+
+
+def test_pipeline_avif_matches_encode_image(ik, oracle):
+    from imagekit import DynamicImage, ImageFormat, encode_image
+    imgs = [ikutil.synth(200, 150, 4, seed=90 + s, pattern="S") for s in range(3)]
+    imgs[1][..., 3] = np.uint8(128)  # one translucent frame: only it gets an alpha plane
+    got = _run(ik, imgs, 100, 75, 4, IK_AVIF, 60)
+    for i, (im, b) in enumerate(zip(imgs, got)):
+        ref = oracle.resize(im, 100, 75, 4)
+        assert b[4:12] == b"ftypavif"
+        assert b == encode_image(DynamicImage.from_array(ref), ImageFormat.avif, 60)
+        dec = _decode_rgba(b)
+        assert dec.shape == (75, 100, 4)
+        assert (dec[..., 3] == 255).all() == (i != 1)
+        assert _psnr(dec[..., :3], ref[..., :3]) > 30
+
+
+def test_pipeline_config4_shape(ik, oracle):
+    """configs[4]: 8192^2 RGBA8 -> 1024^2 (Lanczos3, the reference's filter) -> AVIF q60."""
+    im = ikutil.synth(8192, 8192, 4, seed=4, pattern="S")
+    n = 1
+    H, W, C = im.shape
+    d = ctypes.c_void_p()
+    assert ik.ik_dev_alloc(im.nbytes, ctypes.byref(d)) == 0
+    p = ctypes.c_void_p()
+    try:
+        assert ik.ik_memcpy_h2d(d, im.ctypes.data, im.nbytes) == 0
+        assert ik.ik_pipeline_create(W, H, C, 1024, 1024, 4, IK_AVIF, 60, n, 1, ctypes.byref(p)) == 0, _lib.last_error()
+        cap = 4 << 20
+        out = np.zeros(cap, np.uint8)
+        sizes = (ctypes.c_size_t * n)()
+        assert ik.ik_pipeline_run(p, d, W * C, H * W * C, n, out.ctypes.data, cap, sizes) == 0, _lib.last_error()
+        px = np.zeros((1024, 1024, 4), np.uint8)
+        assert ik.ik_pipeline_fetch_resized(p, 0, px.ctypes.data, px.nbytes) == 0
+    finally:
+        if p:
+            ik.ik_pipeline_destroy(p)
+        ik.ik_dev_free(d)
+    ref = oracle.resize(im, 1024, 1024, 4)
+    np.testing.assert_array_equal(px, ref)  # the resize is bit-exact at full size
+    b = bytes(out[:sizes[0]])
+    dec = _decode_rgba(b)
+    assert dec.shape == (1024, 1024, 4) and (dec[..., 3] == 255).all()
+    assert _psnr(dec[..., :3], ref[..., :3]) > 30

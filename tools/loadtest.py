@@ -28,6 +28,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "rust-image-transform_amd"), os.path.join(ROOT, "tests")]
 
 
+def make_requests(n, sources, fmts, seed):
+    """The /img mix of loadtest/src/main.rs:80-100: (source, w, h, format) with w, h
+    drawn from [200, 800) (:84-85) and the format from the allowed list (:59-60)."""
+    rng = np.random.default_rng(seed)
+    return [(int(rng.integers(0, sources)), int(rng.integers(200, 800)), int(rng.integers(200, 800)),
+             fmts[int(rng.integers(0, len(fmts)))]) for _ in range(n)]
+
+
+def shard(reqs, rank, world):
+    """Round-robin: rank r serves requests r, r + world, ... (independent requests)."""
+    return reqs[rank::world]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--requests", type=int, default=1024)
@@ -64,11 +77,8 @@ def main():
         kw = {"restart_marker_rows": 1} if args.restart else {}
         Image.fromarray(ikutil.synth(S, S, 3, seed=100 + k, pattern="S")).save(buf, format="JPEG", quality=85, **kw)
         srcs.append(buf.getvalue())
-    rng = np.random.default_rng(args.seed)
     fmts = [ImageFormat[f] for f in args.formats.split(",")]
-    reqs = [(int(rng.integers(0, args.sources)), int(rng.integers(200, 800)), int(rng.integers(200, 800)),
-             fmts[int(rng.integers(0, len(fmts)))]) for _ in range(args.requests)]
-    mine = reqs[rank::world]
+    mine = shard(make_requests(args.requests, args.sources, fmts, args.seed), rank, world)
 
     def run_batch(chunk):
         return transform_batch([srcs[s] for s, _, _, _ in chunk], [(w, h) for _, w, h, _ in chunk],

@@ -25,7 +25,7 @@ def main():
     fetch_kb, nf = per_dispatch(fdir, "FETCH_SIZE", "k_resize_fused", first, count)
     write_kb, nw = per_dispatch(wdir, "WRITE_SIZE", "k_resize_fused", first, count)
     cal_kb, nc = per_dispatch(cdir, "FETCH_SIZE", "k_strip")
-    known = 32 * S * S * 4  # tools/bw_probe.py: 32 images of S^2 RGBA8, each byte read once
+    known = 32 * 4096 * 4096 * 4  # tools/bw_probe.py: 32 images of 4096^2 RGBA8 (fixed), each byte read once
     calib = known / (cal_kb * 1024.0)
     fetch = fetch_kb * 1024.0 * calib
     write = write_kb * 1024.0
