@@ -68,6 +68,8 @@ def parse():
                     help="libwebp: host VP8 coder, bytes identical to the reference; gpu: gfx950 VP8 encoder")
     ap.add_argument("--sync", action="store_true", help="one batch in flight (ik_pipeline_run per step)")
     ap.add_argument("--no-alt-encoder", action="store_true", help="skip timing the other WebP encoder")
+    ap.add_argument("--png-images", type=int, default=64,
+                    help="images per rank for the decode-inclusive leg (PNG sources through ik_transform_batch; 0 = skip)")
     return ap.parse_args()
 
 
@@ -94,6 +96,66 @@ def aggregate_mpix(world: int, batch: int, steps: int, size: int, elapsed: float
 def synth_rgba(w, h, seed):
     import ikutil
     return ikutil.synth(w, h, 4, seed=seed, pattern="S")
+
+
+def png_leg(args, frames, world, dist, device, barrier):
+    """Decode-inclusive figure beside `value`: the same frames as PNG files (RGBA8,
+    Pillow's zlib level 6; SURVEY 8(d) D-2's container for configs[1]) through
+    ik_transform_batch -- host inflate + unfilter (png 0.18 via image), device
+    resize, encode -- with encoded input and output bytes in host memory."""
+    import io
+
+    from PIL import Image
+
+    from imagekit import transform_batch
+    pngs = []
+    for im in frames[:2]:
+        b = io.BytesIO()
+        Image.fromarray(im, "RGBA").save(b, format="PNG")
+        pngs.append(b.getvalue())
+    n, O, fmt, f = args.png_images, args.out, FORMATS[args.format], FILTERS[args.filter]
+
+    def run(k):
+        res = transform_batch([pngs[i % len(pngs)] for i in range(k)], [(O, O)] * k, [fmt] * k,
+                              [args.quality] * k, filter=f, threads=args.threads)
+        assert all(r for r in res)
+
+    run(2)
+    barrier()
+    t0 = time.perf_counter()
+    run(n)
+    el = time.perf_counter() - t0
+    barrier()
+    el = reduce_max(el, dist, device)
+    res = {"source": "PNG RGBA8 (zlib level 6), host inflate + unfilter", "images_per_gpu": n,
+           "png_bytes_per_image": sum(len(p) for p in pngs) // len(pngs),
+           "value": round(aggregate_mpix(world, n, 1, args.size, el), 2), "unit": "MPix/s",
+           "ms_per_image_per_gpu": round(el / n * 1e3, 3)}
+    if world == 1 and not args.no_cpu_baseline and args.format != "avif":
+        # CPU proxy of the same decode-inclusive transform: Pillow's PNG decoder (zlib +
+        # libpng-style unfilter, standing in for png 0.18) + the oracle resize + encode,
+        # one image per thread, two rounds of args.threads images
+        import ikutil
+        orc = ikutil.Oracle()
+        threads = max(1, min(args.threads, os.cpu_count() or 1))
+
+        def one(k):
+            px = np.asarray(Image.open(io.BytesIO(pngs[k % len(pngs)])).convert("RGBA"))
+            b, _ = orc.transform(px, O, O, f, fmt, args.quality)
+            assert b
+
+        t0 = time.perf_counter()
+        for r in range(2):
+            ts = [threading.Thread(target=one, args=(r * threads + i,)) for i in range(threads)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
+        cw = time.perf_counter() - t0
+        res["cpu_proxy"] = {"value": round(2 * threads * args.size * args.size / cw / 1e6, 2), "unit": "MPix/s",
+                            "cores": threads, "sample": f"{2 * threads} PNG images, Pillow decode + oracle "
+                                                        f"resize + {CPU_CODER[args.format]}, {cw:.1f}s wall"}
+    return res
 
 
 def cpu_baseline(args, img: np.ndarray):
@@ -359,6 +421,10 @@ def main():
         except Exception:
             traffic = None
 
+    png = {}
+    if args.png_images > 0 and not args.device_only and args.format != "avif":
+        png = png_leg(args, distinct, world, dist, f"cuda:{local}", barrier)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, distinct[0])
@@ -405,6 +471,7 @@ def main():
             "alt_webp_encoder": alt_enc,
             "alt_filter_kernel": alt,
             "resize_fma_mode": fma,
+            "decode_inclusive_png": png,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))

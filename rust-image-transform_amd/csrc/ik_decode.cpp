@@ -72,9 +72,68 @@ inline int paeth(int a, int b, int c) {
     return c;
 }
 
+// libdeflate (system libdeflate.so.0, dlopen'd; about twice zlib's inflate rate on
+// image data).  Only its one-shot zlib decompressor is used, and only when the
+// stream inflates to exactly the expected size; anything else goes through zlib
+// so that error and trailing-data behaviour stay those of the zlib path.
+struct Deflate {
+    void* (*alloc)() = nullptr;
+    int (*zlib_decompress)(void*, const void*, size_t, void*, size_t, size_t*) = nullptr;
+    void (*release)(void*) = nullptr;
+    uint32_t (*crc32)(uint32_t, const void*, size_t) = nullptr;  // same convention as zlib's crc32
+    bool ok = false;
+};
+const Deflate& deflate_api() {
+    static Deflate d;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* lib = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!lib) return;
+        d.alloc = (void* (*)())dlsym(lib, "libdeflate_alloc_decompressor");
+        d.zlib_decompress = (int (*)(void*, const void*, size_t, void*, size_t, size_t*))dlsym(lib, "libdeflate_zlib_decompress");
+        d.release = (void (*)(void*))dlsym(lib, "libdeflate_free_decompressor");
+        d.crc32 = (uint32_t (*)(uint32_t, const void*, size_t))dlsym(lib, "libdeflate_crc32");
+        d.ok = d.alloc && d.zlib_decompress && d.release && !getenv("IK_PNG_ZLIB");
+    });
+    return d;
+}
+
+bool inflate_exact_libdeflate(const std::vector<uint8_t>& in, std::vector<uint8_t>& out) {
+    const Deflate& d = deflate_api();
+    if (!d.ok) return false;
+    thread_local struct Holder {
+        void* p = nullptr;
+        ~Holder() { if (p) deflate_api().release(p); }
+    } h;
+    if (!h.p) h.p = d.alloc();
+    if (!h.p) return false;
+    size_t got = 0;
+    return d.zlib_decompress(h.p, in.data(), in.size(), out.data(), out.size(), &got) == 0 && got == out.size();
+}
+
+uint32_t chunk_crc(const uint8_t* type, const uint8_t* data, size_t len) {
+    const Deflate& d = deflate_api();
+    if (d.ok && d.crc32) return d.crc32(d.crc32(0, type, 4), data, len);
+    return (uint32_t)crc32(crc32(0, type, 4), data, len);
+}
+
+// Per-thread compressed/filtered buffers, kept between decodes (first-touch page
+// faults cost as much as the unfiltering); released after images over 128 MiB.
+struct PngScratch {
+    std::vector<uint8_t> idat, raw;
+};
+struct PngScratchGuard {
+    PngScratch& s;
+    ~PngScratchGuard() {
+        s.idat.clear();
+        if (s.idat.capacity() > (128u << 20)) std::vector<uint8_t>().swap(s.idat);
+        if (s.raw.capacity() > (128u << 20)) std::vector<uint8_t>().swap(s.raw);
+    }
+};
+
 // unfilter one (sub)image of `h` rows of `rowbytes` bytes, bpp = bytes per complete pixel
 bool unfilter(uint8_t* data, size_t h, size_t rowbytes, size_t bpp, std::vector<uint8_t>& out) {
-    out.assign(h * rowbytes, 0);
+    out.resize(h * rowbytes);
     std::vector<uint8_t> zero(rowbytes, 0);
     for (size_t y = 0; y < h; ++y) {
         const uint8_t ft = data[y * (rowbytes + 1)];
@@ -83,9 +142,12 @@ bool unfilter(uint8_t* data, size_t h, size_t rowbytes, size_t bpp, std::vector<
         const uint8_t* prev = y ? out.data() + (y - 1) * rowbytes : zero.data();
         switch (ft) {
         case 0: std::memcpy(cur, in, rowbytes); break;
-        case 1:
-            for (size_t i = 0; i < rowbytes; ++i) cur[i] = (uint8_t)(in[i] + (i >= bpp ? cur[i - bpp] : 0));
+        case 1: {
+            const size_t b0 = bpp < rowbytes ? bpp : rowbytes;
+            for (size_t i = 0; i < b0; ++i) cur[i] = in[i];
+            for (size_t i = b0; i < rowbytes; ++i) cur[i] = (uint8_t)(in[i] + cur[i - bpp]);
             break;
+        }
         case 2:
             for (size_t i = 0; i < rowbytes; ++i) cur[i] = (uint8_t)(in[i] + prev[i]);
             break;
@@ -109,7 +171,11 @@ int decode_png(const uint8_t* b, size_t n, uint32_t& W, uint32_t& H, uint32_t& C
     size_t pos = 8;
     uint32_t w = 0, h = 0;
     int depth = 0, ctype = -1, interlace = 0;
-    std::vector<uint8_t> idat, plte, trns;
+    thread_local PngScratch scratch;
+    PngScratchGuard guard{scratch};
+    std::vector<uint8_t>& idat = scratch.idat;
+    idat.clear();
+    std::vector<uint8_t> plte, trns;
     bool seen_ihdr = false, seen_iend = false;
     while (pos + 12 <= n) {
         const uint32_t len = be32(b + pos);
@@ -117,7 +183,7 @@ int decode_png(const uint8_t* b, size_t n, uint32_t& W, uint32_t& H, uint32_t& C
         const uint8_t* type = b + pos + 4;
         const uint8_t* data = b + pos + 8;
         const uint32_t crc = be32(data + len);
-        if ((uint32_t)crc32(crc32(0, type, 4), data, len) != crc)
+        if (chunk_crc(type, data, len) != crc)
             return fail(IK_ERR_TRANSFORM, "Format error decoding Png: CRC error");
         if (!std::memcmp(type, "IHDR", 4)) {
             if (len != 13) return fail(IK_ERR_TRANSFORM, "Format error decoding Png: bad IHDR");
@@ -169,24 +235,33 @@ int decode_png(const uint8_t* b, size_t n, uint32_t& W, uint32_t& H, uint32_t& C
         if (passes[p].x0 >= w || passes[p].y0 >= h) continue;
         raw_total += ph * (rowbytes_of(pw) + 1);
     }
-    std::vector<uint8_t> raw(raw_total);
-    z_stream zs{};
-    if (inflateInit(&zs) != Z_OK) return fail(IK_ERR_TRANSFORM, "zlib init failed");
-    zs.next_in = idat.data();
-    zs.avail_in = (uInt)idat.size();
-    zs.next_out = raw.data();
-    zs.avail_out = (uInt)raw.size();
-    int zr = inflate(&zs, Z_FINISH);
-    const size_t got = raw.size() - zs.avail_out;
-    inflateEnd(&zs);
-    if (got != raw.size() || (zr != Z_STREAM_END && zr != Z_BUF_ERROR && zr != Z_OK))
-        return fail(IK_ERR_TRANSFORM, "Format error decoding Png: corrupt deflate stream");
+    std::vector<uint8_t>& raw = scratch.raw;
+    raw.resize(raw_total);  // contents are overwritten by the inflate (or the decode fails)
+    if (!inflate_exact_libdeflate(idat, raw)) {
+        z_stream zs{};
+        if (inflateInit(&zs) != Z_OK) return fail(IK_ERR_TRANSFORM, "zlib init failed");
+        zs.next_in = idat.data();
+        zs.avail_in = (uInt)idat.size();
+        zs.next_out = raw.data();
+        zs.avail_out = (uInt)raw.size();
+        int zr = inflate(&zs, Z_FINISH);
+        const size_t got = raw.size() - zs.avail_out;
+        inflateEnd(&zs);
+        if (got != raw.size() || (zr != Z_STREAM_END && zr != Z_BUF_ERROR && zr != Z_OK))
+            return fail(IK_ERR_TRANSFORM, "Format error decoding Png: corrupt deflate stream");
+    }
 
     // samples at 8 bits per sample (expanded), spp per pixel, full image
-    std::vector<uint8_t> samp((size_t)w * h * spp);
+    std::vector<uint8_t> samp;
     size_t off = 0;
     std::vector<uint8_t> rows;
-    for (int p = 0; p < npass; ++p) {
+    if (depth == 8 && !interlace) {  // the unfiltered rows are the samples: no repacking
+        if (!unfilter(raw.data(), h, rowbytes_of(w), bpp, samp))
+            return fail(IK_ERR_TRANSFORM, "Format error decoding Png: unknown filter method");
+    } else {
+        samp.resize((size_t)w * h * spp);
+    }
+    for (int p = 0; p < (depth == 8 && !interlace ? 0 : npass); ++p) {
         if (passes[p].x0 >= w || passes[p].y0 >= h) continue;
         const size_t pw = (w - passes[p].x0 + passes[p].dx - 1) / passes[p].dx;
         const size_t ph = (h - passes[p].y0 + passes[p].dy - 1) / passes[p].dy;

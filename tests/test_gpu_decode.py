@@ -208,6 +208,32 @@ def test_png_corruption_is_an_error(ik):
         decode_image(b[:30])
 
 
+def _png_from_stream(w, h, stream, split=1):
+    """RGB8 PNG whose IDAT data is `stream` (a zlib stream), cut into `split` chunks."""
+    out = b"\x89PNG\r\n\x1a\n" + _chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, 2, 0, 0, 0))
+    step = -(-len(stream) // split)
+    for i in range(0, len(stream), step):
+        out += _chunk(b"IDAT", stream[i:i + step])
+    return out + _chunk(b"IEND", b"")
+
+
+def test_png_inflate_paths(ik):
+    """The one-shot inflate (libdeflate) and the zlib path agree on what is an image:
+    many IDAT chunks; extra data after the image rows (accepted, as the zlib path
+    does); a short stream (an error)."""
+    w, h = 300, 97
+    px = ikutil.synth(w, h, 3, seed=5, pattern="S")
+    raw = b"".join(_filter_row(px[y].tobytes(), px[y - 1].tobytes() if y else None, 3, 2 if y % 3 else 4)
+                   for y in range(h))
+    for split in (1, 7, 64):
+        img, _ = decode_image(_png_from_stream(w, h, zlib.compress(raw, 9), split))
+        np.testing.assert_array_equal(img.to_array(), px)
+    img, _ = decode_image(_png_from_stream(w, h, zlib.compress(raw + bytes(50), 6)))
+    np.testing.assert_array_equal(img.to_array(), px)
+    with pytest.raises(TransformError):
+        decode_image(_png_from_stream(w, h, zlib.compress(raw[:-10], 6)))
+
+
 @pytest.mark.parametrize("blob", [b"GIF89a" + bytes(20), b"BM" + bytes(40),
                                   b"\x00\x00\x00\x1cftypavif" + bytes(20), bytes(100), b""])
 def test_unsupported_or_unknown_formats(ik, blob):
