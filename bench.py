@@ -451,6 +451,8 @@ def main():
                 "batch_per_gpu": B, "filter": args.filter, "format": args.format,
                 "quality": args.quality, "host_threads_per_gpu": args.threads,
                 "webp_encoder": args.webp_encoder,
+                "libwebp": "%d.%d.%d" % (lib.ik_libwebp_version() >> 16, (lib.ik_libwebp_version() >> 8) & 255,
+                                         lib.ik_libwebp_version() & 255),
                 "device_only": bool(args.device_only), "batches_in_flight": 1 if args.sync else 2, "parallelism": f"images sharded, {world} rank(s)",
             },
             "roofline": {

@@ -110,6 +110,9 @@ int ik_encode(const ik_image *img, int fmt, int quality, uint8_t **out, size_t *
  * The process default comes from IK_WEBP_ENCODER=gpu|libwebp when first used. */
 typedef enum { IK_WEBP_LIBWEBP = 0, IK_WEBP_GPU = 1 } ik_webp_encoder;
 int ik_set_webp_encoder(int encoder); /* process-wide, for ik_encode / ik_transform */
+/* version of the libwebp that codes WebP (WebPGetEncoderVersion, e.g. 0x010600),
+ * -1 when none could be loaded; IK_LIBWEBP=<path> picks a specific copy */
+int ik_libwebp_version(void);
 int ik_get_webp_encoder(void);
 
 /* ---- fused / batched entry points (pixels stay in HBM) ----------------- */

@@ -37,6 +37,7 @@ SIGNATURES = [
     ("ik_encode", ctypes.c_int, [c_img_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]),
     ("ik_transform", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]),
     ("ik_set_webp_encoder", ctypes.c_int, [ctypes.c_int]),
+    ("ik_libwebp_version", ctypes.c_int, []),
     ("ik_get_webp_encoder", ctypes.c_int, []),
     ("ik_pipeline_set_webp_encoder", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("ik_webp_encode_gpu_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]),
