@@ -120,7 +120,7 @@ uint32_t chunk_crc(const uint8_t* type, const uint8_t* data, size_t len) {
 // Per-thread compressed/filtered buffers, kept between decodes (first-touch page
 // faults cost as much as the unfiltering); released after images over 128 MiB.
 struct PngScratch {
-    std::vector<uint8_t> idat, raw;
+    std::vector<uint8_t> idat, raw, samp;  // samp trades buffers with the caller's px (swap)
 };
 struct PngScratchGuard {
     PngScratch& s;
@@ -128,6 +128,7 @@ struct PngScratchGuard {
         s.idat.clear();
         if (s.idat.capacity() > (128u << 20)) std::vector<uint8_t>().swap(s.idat);
         if (s.raw.capacity() > (128u << 20)) std::vector<uint8_t>().swap(s.raw);
+        if (s.samp.capacity() > (128u << 20)) std::vector<uint8_t>().swap(s.samp);
     }
 };
 
@@ -252,7 +253,7 @@ int decode_png(const uint8_t* b, size_t n, uint32_t& W, uint32_t& H, uint32_t& C
     }
 
     // samples at 8 bits per sample (expanded), spp per pixel, full image
-    std::vector<uint8_t> samp;
+    std::vector<uint8_t>& samp = scratch.samp;  // every sample is written below
     size_t off = 0;
     std::vector<uint8_t> rows;
     if (depth == 8 && !interlace) {  // the unfiltered rows are the samples: no repacking

@@ -535,7 +535,13 @@ int ik_decode(const uint8_t* bytes, size_t len, ik_image** out, int* fmt_out) {
     const Sniffed f = guess_format(bytes, len);
     if (f == Sniffed::Unknown) return fail(IK_ERR_TRANSFORM, "The image format could not be determined");
     uint32_t w = 0, h = 0, c = 0;
-    std::vector<uint8_t> px;
+    // host-decoded pixels: a per-thread buffer (with the PNG decoder's own it
+    // trades places, so neither is page-faulted in again per image); released
+    // after images over 128 MiB
+    thread_local std::vector<uint8_t> px;
+    struct Trim {
+        ~Trim() { if (px.capacity() > (128u << 20)) std::vector<uint8_t>().swap(px); }
+    } trim;
     int st;
     ik_image* img = nullptr;
     switch (f) {
