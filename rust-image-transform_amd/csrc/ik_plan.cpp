@@ -181,6 +181,7 @@ ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, i
     // column strips: as many output columns as fit kStripBytes source bytes (and,
     // when possible, kMaxStripWeights horizontal weights in LDS)
     bool wl = (long)Tx <= kMaxStripWeights;
+    if (const char* e = getenv("IK_WEIGHTS_LDS")) wl = wl && atoi(e) != 0;  // tuning experiments
     std::vector<int> strips;
     for (int pass = 0; pass < 2 && slots; ++pass) {
         strips.clear();
