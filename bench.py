@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--sync", action="store_true", help="one batch in flight (ik_pipeline_run per step)")
     ap.add_argument("--no-alt-encoder", action="store_true", help="skip timing the other WebP encoder")
     ap.add_argument("--png-images", type=int, default=64,
-                    help="images per rank for the decode-inclusive leg (PNG sources through ik_transform_batch; 0 = skip)")
+                    help="images per rank for each decode-inclusive leg (PNG and JPEG sources through ik_transform_batch; 0 = skip)")
     return ap.parse_args()
 
 
@@ -98,11 +98,13 @@ def synth_rgba(w, h, seed):
     return ikutil.synth(w, h, 4, seed=seed, pattern="S")
 
 
-def png_leg(args, frames, world, dist, device, barrier):
-    """Decode-inclusive figure beside `value`: the same frames as PNG files (RGBA8,
-    Pillow's zlib level 6; SURVEY 8(d) D-2's container for configs[1]) through
-    ik_transform_batch -- host inflate + unfilter (png 0.18 via image), device
-    resize, encode -- with encoded input and output bytes in host memory."""
+def png_leg(args, frames, world, dist, device, barrier, kind="png"):
+    """Decode-inclusive figure beside `value`: the same frames as encoded files through
+    ik_transform_batch, with encoded input and output bytes in host memory.
+    kind "png": PNG RGBA8 (Pillow's zlib level 6; SURVEY 8(d) D-2's container for
+    configs[1]) -- host inflate + unfilter (png 0.18 via image), device resize, encode.
+    kind "jpeg": baseline JPEG q90 4:2:0 with a restart marker per MCU row (D-2's
+    container for configs[2]) -- GPU entropy decoding, IDCT, upsampling and colour."""
     import io
 
     from PIL import Image
@@ -111,7 +113,11 @@ def png_leg(args, frames, world, dist, device, barrier):
     pngs = []
     for im in frames[:2]:
         b = io.BytesIO()
-        Image.fromarray(im, "RGBA").save(b, format="PNG")
+        if kind == "png":
+            Image.fromarray(im, "RGBA").save(b, format="PNG")
+        else:
+            Image.fromarray(np.ascontiguousarray(im[..., :3]), "RGB").save(b, format="JPEG", quality=90,
+                                                                         restart_marker_rows=1)
         pngs.append(b.getvalue())
     n, O, fmt, f = args.png_images, args.out, FORMATS[args.format], FILTERS[args.filter]
 
@@ -127,8 +133,9 @@ def png_leg(args, frames, world, dist, device, barrier):
     el = time.perf_counter() - t0
     barrier()
     el = reduce_max(el, dist, device)
-    res = {"source": "PNG RGBA8 (zlib level 6), host inflate + unfilter", "images_per_gpu": n,
-           "png_bytes_per_image": sum(len(p) for p in pngs) // len(pngs),
+    res = {"source": "PNG RGBA8 (zlib level 6), host inflate + unfilter" if kind == "png" else
+                     "JPEG q90 4:2:0, RSTn per MCU row, GPU entropy decoding", "images_per_gpu": n,
+           "bytes_per_source_image": sum(len(p) for p in pngs) // len(pngs),
            "value": round(aggregate_mpix(world, n, 1, args.size, el), 2), "unit": "MPix/s",
            "ms_per_image_per_gpu": round(el / n * 1e3, 3)}
     if world == 1 and not args.no_cpu_baseline and args.format != "avif":
@@ -140,7 +147,7 @@ def png_leg(args, frames, world, dist, device, barrier):
         threads = max(1, min(args.threads, os.cpu_count() or 1))
 
         def one(k):
-            px = np.asarray(Image.open(io.BytesIO(pngs[k % len(pngs)])).convert("RGBA"))
+            px = np.asarray(Image.open(io.BytesIO(pngs[k % len(pngs)])).convert("RGBA" if kind == "png" else "RGB"))
             b, _ = orc.transform(px, O, O, f, fmt, args.quality)
             assert b
 
@@ -153,7 +160,7 @@ def png_leg(args, frames, world, dist, device, barrier):
                 t.join()
         cw = time.perf_counter() - t0
         res["cpu_proxy"] = {"value": round(2 * threads * args.size * args.size / cw / 1e6, 2), "unit": "MPix/s",
-                            "cores": threads, "sample": f"{2 * threads} PNG images, Pillow decode + oracle "
+                            "cores": threads, "sample": f"{2 * threads} {kind.upper()} images, Pillow decode + oracle "
                                                         f"resize + {CPU_CODER[args.format]}, {cw:.1f}s wall"}
     return res
 
@@ -432,9 +439,10 @@ def main():
         except Exception:
             traffic = None
 
-    png = {}
+    png = jpg = {}
     if args.png_images > 0 and not args.device_only and args.format != "avif":
         png = png_leg(args, distinct, world, dist, f"cuda:{local}", barrier)
+        jpg = png_leg(args, distinct, world, dist, f"cuda:{local}", barrier, kind="jpeg")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -485,6 +493,7 @@ def main():
             "alt_filter_kernel": alt,
             "resize_fma_mode": fma,
             "decode_inclusive_png": png,
+            "decode_inclusive_jpeg": jpg,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
