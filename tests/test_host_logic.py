@@ -32,3 +32,19 @@ def test_error_display_matches_thiserror():
     assert str(errors.TransformError("bad")) == "Transformation error: bad"
     assert str(errors.InvalidArgument("q")) == "Invalid argument: q"
     assert issubclass(errors.TransformError, errors.ImageKitError)
+
+
+def test_bench_cli_formats_match_image_format(monkeypatch):
+    """bench.py's --format values are the ImageFormat discriminants the C ABI takes
+    (include/imagekit_hip.h ik_format), incl. the configs[4] AVIF runs."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    for f in ImageFormat:
+        assert bench.FORMATS[str(f)] == f.value
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--size", "8192", "--out", "1024", "--filter", "lanczos3",
+                                      "--format", "avif", "--quality", "60", "--batch", "32"])
+    a = bench.parse()
+    assert (a.size, a.out, a.filter, a.format, a.quality, a.batch, a.gpus) == (8192, 1024, "lanczos3", "avif", 60, 32, 1)
+    assert set(bench.CPU_CODER) == set(bench.FORMATS)
