@@ -22,7 +22,7 @@ namespace {
 
 constexpr int kEncThreads = 1024;
 
-__device__ const uint8_t kZigE[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+constexpr uint8_t kZigE[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
                                       12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
                                       35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
                                       58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
@@ -43,7 +43,7 @@ struct BitSink {
     int n;                   // pending bit count (< 32 after a flush)
     unsigned long long first_word, last_word;  // shared words of this run: atomics
     bool count_only;
-    __device__ void flush_word() {
+    __device__ __forceinline__ void flush_word() {
         const unsigned long long w = (pos - (unsigned long long)n) >> 5;  // word of the oldest pending bit
         const uint32_t v = (uint32_t)(acc >> 32);
         if (w == first_word || w == last_word) atomicOr(&words[w], v);
@@ -51,7 +51,7 @@ struct BitSink {
         acc <<= 32;
         n -= 32;
     }
-    __device__ void put(uint32_t bits, int size) {
+    __device__ __forceinline__ void put(uint32_t bits, int size) {
         if (count_only) {
             pos += (unsigned)size;
             return;
@@ -62,7 +62,7 @@ struct BitSink {
         pos += (unsigned)size;
         if (n >= 32) flush_word();
     }
-    __device__ void finish() {
+    __device__ __forceinline__ void finish() {
         if (count_only || n <= 0) return;
         const unsigned long long w = (pos - (unsigned long long)n) >> 5;
         atomicOr(&words[w], (uint32_t)(acc >> 32));
@@ -71,23 +71,34 @@ struct BitSink {
     }
 };
 
-// one block of MCU m, component c (coef: [mcu][3][64] natural order)
-__device__ void code_block(BitSink& b, const int16_t* __restrict__ coef, long long blk, const uint32_t* __restrict__ huff,
-                           const uint8_t* __restrict__ zz) {
+// one block of MCU m, component c (coef: [mcu][3][64] natural order, 128-B blocks,
+// 16-B aligned).  The block comes in with eight 16-byte loads and the zigzag walk
+// is unrolled, so every coefficient is a register with a compile-time index (one
+// scattered 2-byte load per coefficient was the kernel's cost).
+__device__ __forceinline__ void code_block(BitSink& b, const int16_t* __restrict__ coef, long long blk, const uint32_t* __restrict__ huff) {
     const long long m = blk / 3;
     const int c = (int)(blk - m * 3);
     const int16_t* p = coef + (m * 3 + c) * 64;
     const int prev = m ? coef[((m - 1) * 3 + c) * 64] : 0;
+    uint32_t wv[32];
+    const uint4* p4 = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const uint4 t = p4[j];
+        wv[4 * j] = t.x; wv[4 * j + 1] = t.y; wv[4 * j + 2] = t.z; wv[4 * j + 3] = t.w;
+    }
+    auto coefk = [&](int k) -> int { return (int)(int16_t)(wv[k >> 1] >> (16 * (k & 1))); };
     const uint32_t* dc = huff + (c ? 2 : 0) * 256;
     const uint32_t* ac = huff + (c ? 3 : 1) * 256;
     int nb;
     uint32_t v;
-    coef_bits_dev(p[0] - prev, nb, v);
+    coef_bits_dev(coefk(0) - prev, nb, v);
     b.put(dc[nb] >> 8, dc[nb] & 0xff);
     b.put(v, nb);
     int zr = 0;
+#pragma unroll
     for (int i = 1; i < 64; ++i) {
-        const int x = p[zz[i]];
+        const int x = coefk(kZigE[i]);
         if (x == 0) { ++zr; continue; }
         while (zr > 15) { b.put(ac[0xF0] >> 8, ac[0xF0] & 0xff); zr -= 16; }
         coef_bits_dev(x, nb, v);
@@ -96,10 +107,10 @@ __device__ void code_block(BitSink& b, const int16_t* __restrict__ coef, long lo
         b.put(v, nb);
         zr = 0;
     }
-    if (p[zz[63]] == 0) b.put(ac[0] >> 8, ac[0] & 0xff);
+    if (coefk(kZigE[63]) == 0) b.put(ac[0] >> 8, ac[0] & 0xff);
 }
 
-__device__ unsigned long long block_scan_excl(unsigned long long v, unsigned long long* s_tmp, unsigned long long& total) {
+__device__ __forceinline__ unsigned long long block_scan_excl(unsigned long long v, unsigned long long* s_tmp, unsigned long long& total) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     unsigned long long inc = v;
     for (int o = 1; o < 64; o <<= 1) {
@@ -121,12 +132,10 @@ __device__ unsigned long long block_scan_excl(unsigned long long v, unsigned lon
 }  // namespace
 
 __global__ __launch_bounds__(kEncThreads) void k_jpeg_huff_enc(JpegEncArgs a) {
-    __shared__ uint8_t s_zz[64];
     __shared__ uint32_t s_huff[4 * 256];
     __shared__ unsigned long long s_tmp[kEncThreads / 64];
     const int img = blockIdx.x, tid = threadIdx.x;
     for (int i = tid; i < 4 * 256; i += kEncThreads) s_huff[i] = a.huff[i];
-    if (tid < 64) s_zz[tid] = kZigE[tid];
     const int16_t* coef = a.coef + (size_t)img * a.coef_img_stride;
     uint32_t* words = reinterpret_cast<uint32_t*>(a.work + (size_t)img * a.work_img_bytes);
     uint8_t* stage = a.work + (size_t)img * a.work_img_bytes + a.words_bytes;
@@ -136,7 +145,7 @@ __global__ __launch_bounds__(kEncThreads) void k_jpeg_huff_enc(JpegEncArgs a) {
     const long long b0 = min((long long)tid * per, nblk), b1 = min(b0 + per, nblk);
     // 1. bit lengths
     BitSink cnt{words, 0, 0, 0, 0, 0, true};
-    for (long long k = b0; k < b1; ++k) code_block(cnt, coef, k, s_huff, s_zz);
+    for (long long k = b0; k < b1; ++k) code_block(cnt, coef, k, s_huff);
     unsigned long long total_bits;
     const unsigned long long off = block_scan_excl(cnt.pos, s_tmp, total_bits);
     const unsigned long long T = total_bits + 7;  // + pad_byte's 7 one-bits
@@ -152,7 +161,7 @@ __global__ __launch_bounds__(kEncThreads) void k_jpeg_huff_enc(JpegEncArgs a) {
     BitSink w{words, off, 0, 0, off >> 5, (off + cnt.pos) >> 5, false};
     w.n = (int)(off & 31);  // align the accumulator to word boundaries: leading zero bits
     w.acc = 0;
-    for (long long k = b0; k < b1; ++k) code_block(w, coef, k, s_huff, s_zz);
+    for (long long k = b0; k < b1; ++k) code_block(w, coef, k, s_huff);
     w.finish();
     if (tid == 0) {  // pad_byte: seven one-bits at the end
         BitSink pb{words, total_bits, 0, (int)(total_bits & 31), total_bits >> 5, (total_bits + 7) >> 5, false};
@@ -185,7 +194,9 @@ __global__ __launch_bounds__(kEncThreads) void k_jpeg_huff_enc(JpegEncArgs a) {
 }
 
 hipError_t launch_jpeg_huff_enc(const JpegEncArgs& a, int n, hipStream_t s) {
-    if (n <= 0 || (a.out_img_stride & 15) || (a.work_img_bytes & 15) || (a.words_bytes & 15)) return hipErrorInvalidValue;
+    if (n <= 0 || (a.out_img_stride & 15) || (a.work_img_bytes & 15) || (a.words_bytes & 15) ||
+        ((uintptr_t)a.coef & 15) || (a.coef_img_stride & 7))  // code_block's 16-byte loads
+        return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_jpeg_huff_enc, dim3(n), dim3(kEncThreads), 0, s, a);
     return hipGetLastError();
 }
