@@ -49,8 +49,29 @@ typedef enum {
 typedef struct ik_image ik_image;
 
 /* ---- runtime ---------------------------------------------------------- */
-int ik_init(int device);                /* select the HIP device for this thread; -1 = keep */
+/* ik_init(d >= 0): select HIP device d for the calling thread.
+ * ik_init(-1): one process drives every visible GPU (or the list in IK_DEVICES,
+ *   e.g. "0,1,2,3"; a device may repeat, "0,0" = two logical devices on GPU 0).
+ *   From then on ik_transform / ik_transform_batch / ik_decode called from any
+ *   number of threads feed a host work queue: each request goes to the logical
+ *   device with the least outstanding cost (ik_request_cost), and runs there on
+ *   that device's persistent workers.  The reference's analogue is tokio's
+ *   multi-thread runtime calling the transform from every worker
+ *   (src/main.rs:20, src/lib.rs:175-191). */
+int ik_init(int device);
+int ik_init_devices(const int *devices, int n); /* ik_init(-1) with an explicit list */
 int ik_device_count(void);
+int ik_logical_device_count(void);  /* 0 unless multi-device dispatch is on */
+/* per logical device: requests taken, cost completed, cost still outstanding */
+int ik_logical_device_stats(uint32_t logical, uint64_t *jobs, uint64_t *cost_done, uint64_t *outstanding);
+/* the scheduler's cost of one request, in bytes-equivalent: encoded input +
+ * decoded pixels (from the header) + an encoder weight per output pixel */
+uint64_t ik_request_cost(const uint8_t *bytes, size_t len, int64_t w, int64_t h, int fmt);
+/* the batch placement policy on its own (no device work): n requests with
+ * costs[i] over ndev devices already carrying outstanding[d] (may be NULL) ->
+ * assign[i]; largest request first to the least-loaded device */
+void ik_schedule_plan(const uint64_t *costs, uint32_t n, uint32_t ndev, const uint64_t *outstanding,
+                      uint32_t *assign);
 size_t ik_last_error(char *buf, size_t cap); /* thread-local message of the last failure */
 const char *ik_version(void);
 

@@ -50,34 +50,84 @@ int current_device() {
     return t_device;
 }
 
+DeviceGuard::DeviceGuard(int device) : prev(current_device()) {
+    if (device != prev) {
+        t_device = device;
+        (void)hipSetDevice(device);
+    }
+}
+DeviceGuard::~DeviceGuard() {
+    if (t_device != prev) {
+        t_device = prev;
+        (void)hipSetDevice(prev);
+    }
+}
+
+// Per-thread HIP resources: a non-blocking stream per device, pinned staging
+// arenas and grow-only device arenas.  Worker threads are persistent (ik_pool.cpp),
+// so these live as long as the process; a caller's own thread releases its set
+// when it exits.
+namespace {
+struct Arena {
+    uint8_t* p = nullptr;
+    size_t cap = 0;
+    int device = 0;
+};
+struct ThreadRes {
+    std::map<int, hipStream_t> streams;
+    std::map<std::pair<int, int>, Arena> dev;  // (device, slot)
+    Arena pinned[4];
+    ~ThreadRes() {
+        for (auto& kv : dev) {
+            if (!kv.second.p) continue;
+            (void)hipSetDevice(kv.second.device);
+            auto s = streams.find(kv.second.device);
+            if (s != streams.end()) (void)hipStreamSynchronize(s->second);
+            (void)hipFree(kv.second.p);
+        }
+        for (Arena& a : pinned)
+            if (a.p) (void)hipHostFree(a.p);
+        for (auto& kv : streams) (void)hipStreamDestroy(kv.second);
+    }
+};
+ThreadRes& tres() {
+    static thread_local ThreadRes r;
+    return r;
+}
+}  // namespace
+
 hipStream_t thread_stream() {
-    static thread_local std::map<int, hipStream_t> streams;
+    ThreadRes& r = tres();
     const int d = current_device();
-    auto it = streams.find(d);
-    if (it != streams.end()) return it->second;
+    auto it = r.streams.find(d);
+    if (it != r.streams.end()) return it->second;
     (void)hipSetDevice(d);
     hipStream_t s = nullptr;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    streams[d] = s;
+    r.streams[d] = s;
     return s;
+}
+
+uint8_t* pinned_slot(int slot, size_t bytes) {
+    Arena& a = tres().pinned[slot];
+    if (bytes <= a.cap) return a.p;
+    if (a.p) {
+        (void)hipStreamSynchronize(thread_stream());  // no copy may still read the old buffer
+        (void)hipHostFree(a.p);
+    }
+    a.p = nullptr;
+    a.cap = 0;
+    size_t want = bytes < (1u << 20) ? (1u << 20) : bytes;
+    if (hipHostMalloc((void**)&a.p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+    a.cap = want;
+    return a.p;
 }
 
 // Host <-> device copies of pageable memory go through a per-thread pinned
 // staging buffer with stream-ordered async copies on the thread's stream.  (A
 // synchronous hipMemcpy* from pageable memory is issued on the null stream, and
 // a non-blocking stream is not ordered after its DMA.)
-static uint8_t* staging(size_t bytes) {
-    static thread_local uint8_t* buf = nullptr;
-    static thread_local size_t cap = 0;
-    if (bytes <= cap) return buf;
-    if (buf) (void)hipHostFree(buf);
-    buf = nullptr;
-    cap = 0;
-    size_t want = bytes < (1u << 20) ? (1u << 20) : bytes;
-    if (hipHostMalloc((void**)&buf, want, hipHostMallocDefault) != hipSuccess) return nullptr;
-    cap = want;
-    return buf;
-}
+static uint8_t* staging(size_t bytes) { return pinned_slot(0, bytes); }
 
 int copy_h2d_2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,
                 size_t height, hipStream_t s) {
@@ -109,10 +159,10 @@ int copy_d2h_2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, 
 
 // Per-thread, per-device device scratch (grown with hipMalloc; never the
 // stream-ordered allocator).  Valid until the next scratch() call on this thread.
-uint8_t* scratch(size_t bytes) {
-    struct Arena { uint8_t* p = nullptr; size_t cap = 0; };
-    static thread_local std::map<int, Arena> arenas;
-    Arena& a = arenas[current_device()];
+uint8_t* scratch_slot(int slot, size_t bytes) {
+    const int d = current_device();
+    Arena& a = tres().dev[{d, slot}];
+    a.device = d;
     if (bytes <= a.cap) return a.p;
     if (a.p) {
         (void)hipStreamSynchronize(thread_stream());
@@ -120,12 +170,15 @@ uint8_t* scratch(size_t bytes) {
     }
     a.p = nullptr;
     a.cap = 0;
-    const size_t want = bytes < (4u << 20) ? (4u << 20) : bytes;
-    (void)hipSetDevice(current_device());
+    // grow geometrically so a run of slightly larger requests does not re-allocate each time
+    size_t want = bytes < (4u << 20) ? (4u << 20) : bytes + bytes / 8;
+    (void)hipSetDevice(d);
     if (hipMalloc((void**)&a.p, want) != hipSuccess) return nullptr;
     a.cap = want;
     return a.p;
 }
+
+uint8_t* scratch(size_t bytes) { return scratch_slot(0, bytes); }
 
 size_t pitch_for(uint32_t w, uint32_t c) { return ((size_t)w * c + 255) & ~size_t(255); }
 
@@ -188,22 +241,6 @@ void webp_gamma_tables(uint16_t g2l[256], int l2g[33]) {
     const double norm = 1. / 255.;
     for (int v = 0; v <= 255; ++v) g2l[v] = (uint16_t)(pow(norm * v, 0.80) * ((1 << 12) - 1) + .5);
     for (int v = 0; v <= 32; ++v) l2g[v] = (int)(255. * pow(scale * v, 1. / 0.80) + .5);
-}
-
-void parallel_for(int n, int threads, const std::function<void(int)>& fn) {
-    if (n <= 0) return;
-    if (threads <= 0) threads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-    threads = std::min(threads, n);
-    const int dev = current_device();
-    std::atomic<int> next{0};
-    auto work = [&](bool own) {
-        if (own) ik_init(dev);
-        for (int i; (i = next.fetch_add(1)) < n;) fn(i);
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < threads; ++t) th.emplace_back(work, true);
-    work(false);
-    for (auto& t : th) t.join();
 }
 
 namespace {
@@ -376,10 +413,37 @@ int ik_init(int device) {
     int n = 0;
     IK_HIP(hipGetDeviceCount(&n));
     if (device >= n) return fail(IK_ERR_INVALID, "device %d out of range (%d devices)", device, n);
-    if (device >= 0) t_device = device;
+    if (device < 0) {  // every visible GPU (or IK_DEVICES): one process, many devices
+        if (int rc = sched_configure(nullptr, 0)) return rc;
+        device = sched_phys(0);
+    }
+    t_device = device;
     IK_HIP(hipSetDevice(current_device()));
     if (!thread_stream()) return fail(IK_ERR_DEVICE, "cannot create HIP stream");
     return IK_OK;
+}
+
+int ik_init_devices(const int* devices, int n) {
+    if (!devices || n <= 0) return fail(IK_ERR_INVALID, "empty device list");
+    if (int rc = sched_configure(devices, n)) return rc;
+    return ik_init(sched_phys(0));
+}
+
+int ik_logical_device_count(void) { return sched_multi() ? sched_count() : 0; }
+
+int ik_logical_device_stats(uint32_t logical, uint64_t* jobs, uint64_t* cost_done, uint64_t* outstanding) {
+    if (!sched_multi()) return fail(IK_ERR_INVALID, "multi-device dispatch is not enabled");
+    return sched_stats(logical, jobs, cost_done, outstanding);
+}
+
+uint64_t ik_request_cost(const uint8_t* bytes, size_t len, int64_t w, int64_t h, int fmt) {
+    return request_cost(bytes, len, w, h, fmt);
+}
+
+void ik_schedule_plan(const uint64_t* costs, uint32_t n, uint32_t ndev, const uint64_t* outstanding,
+                      uint32_t* assign) {
+    if (!costs || !assign || !ndev) return;
+    sched_plan(costs, n, ndev, outstanding, assign);
 }
 
 int ik_image_from_host(const uint8_t* pixels, uint32_t width, uint32_t height, uint32_t channels,
@@ -423,6 +487,7 @@ int ik_image_to_host(const ik_image* img, uint8_t* dst, size_t cap) {
     const size_t row = (size_t)img->w * img->c;
     if (cap < row * img->h) return fail(IK_ERR_INVALID, "destination too small");
     if (!row || !img->h) return IK_OK;
+    DeviceGuard g(img->device);
     return copy_d2h_2d(dst, row, img->d, img->pitch, row, img->h, thread_stream());
 }
 
@@ -439,7 +504,10 @@ void ik_image_free(ik_image* img) {
                 kept = true;
             }
         }
-        if (!kept) (void)hipFree(img->d);
+        if (!kept) {
+            DeviceGuard g(img->device);
+            (void)hipFree(img->d);
+        }
     }
     delete img;
 }
@@ -451,6 +519,7 @@ int ik_resize_exact(const ik_image* img, uint32_t nw, uint32_t nh, int filter, i
     if (!img || !out) return fail(IK_ERR_INVALID, "null pointer");
     if (filter < 0 || filter > 4) return fail(IK_ERR_INVALID, "unknown filter %d", filter);
     if (nw == 0 || nh == 0) return fail(IK_ERR_INVALID, "zero output dimension");
+    DeviceGuard g(img->device);
     ik_image* o = nullptr;
     int st = alloc_image(nw, nh, img->c, &o);
     if (st) return st;
@@ -517,6 +586,7 @@ int ik_resize(ik_image* img, int64_t w, int64_t h, int filter, ik_image** out) {
 int ik_encode(const ik_image* img, int fmt, int quality, uint8_t** out, size_t* out_len) {
     if (!img || !out || !out_len) return fail(IK_ERR_INVALID, "null pointer");
     if (img->w == 0 || img->h == 0) return fail(IK_ERR_TRANSFORM, "cannot encode an empty image");
+    DeviceGuard g(img->device);
     std::vector<uint8_t> bytes;
     int st = encode_device_image(img->d, img->w, img->h, img->c, img->pitch, fmt, quality, bytes);
     if (st) return st;
@@ -527,9 +597,13 @@ int ik_encode(const ik_image* img, int fmt, int quality, uint8_t** out, size_t* 
     return IK_OK;
 }
 
+}  // extern "C"
+
+namespace ik {
+
 // decode_image: image::guess_format + load_from_memory_with_format; formats the
 // reference build compiles in (Cargo.toml:20: jpeg, png, webp; avif = encoder only)
-int ik_decode(const uint8_t* bytes, size_t len, ik_image** out, int* fmt_out) {
+static int decode_one(const uint8_t* bytes, size_t len, ik_image** out, int* fmt_out) {
     if (!out) return fail(IK_ERR_INVALID, "null pointer");
     if (!bytes && len) return fail(IK_ERR_INVALID, "null bytes");
     const Sniffed f = guess_format(bytes, len);
@@ -565,18 +639,20 @@ int ik_decode(const uint8_t* bytes, size_t len, ik_image** out, int* fmt_out) {
     return IK_OK;
 }
 
-int ik_decode_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t n, ik_image** outs, int* fmts,
-                    int* status) {
-    if (!bytes || !lens || !outs || !n) return fail(IK_ERR_INVALID, "bad batch");
+static std::string last_error_str() { return t_err; }
+
+// decode_image over a batch on the calling thread's device; per-item status and
+// message (the decoder's own, as TransformError(e.to_string()) carries it)
+int decode_batch_dev(const uint8_t* const* bytes, const size_t* lens, uint32_t n, ik_image** outs, int* fmts,
+                     int* st, std::string* msg, int threads) {
     std::vector<const uint8_t*> jb;
     std::vector<size_t> jl;
-    std::vector<uint32_t> ji;
-    std::vector<int> st(n, IK_OK);
-    std::vector<uint32_t> other;
+    std::vector<uint32_t> ji, other;
     for (uint32_t i = 0; i < n; ++i) {
         outs[i] = nullptr;
+        st[i] = IK_OK;
         if (fmts) fmts[i] = -1;
-        if (!bytes[i] && lens[i]) { st[i] = fail(IK_ERR_INVALID, "null bytes"); continue; }
+        if (!bytes[i] && lens[i]) { st[i] = fail(IK_ERR_INVALID, "null bytes"); msg[i] = t_err; continue; }
         if (guess_format(bytes[i], lens[i]) == Sniffed::Jpeg) {
             jb.push_back(bytes[i]);
             jl.push_back(lens[i]);
@@ -586,32 +662,72 @@ int ik_decode_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t n,
             other.push_back(i);
         }
     }
-    std::vector<std::string> msg(n);
-    parallel_for((int)other.size(), 0, [&](int k) {  // PNG / WebP / unknown: host decoders, in parallel
+    parallel_for((int)other.size(), threads, [&](int k) {  // PNG / WebP / unknown: host decoders, in parallel
         const uint32_t i = other[k];
-        st[i] = ik_decode(bytes[i], lens[i], &outs[i], fmts ? &fmts[i] : nullptr);
-        if (st[i]) {
-            char buf[256];
-            ik_last_error(buf, sizeof(buf));
-            msg[i] = buf;
-        }
+        st[i] = decode_one(bytes[i], lens[i], &outs[i], fmts ? &fmts[i] : nullptr);
+        if (st[i]) msg[i] = t_err;
     });
     if (!ji.empty()) {
         std::vector<ik_image*> jo(ji.size(), nullptr);
         std::vector<int> js(ji.size(), IK_OK);
-        decode_jpeg_batch(jb.data(), jl.data(), (int)ji.size(), jo.data(), js.data());
+        std::vector<std::string> jm(ji.size());
+        decode_jpeg_batch(jb.data(), jl.data(), (int)ji.size(), jo.data(), js.data(), jm.data());
         for (size_t k = 0; k < ji.size(); ++k) {
             outs[ji[k]] = jo[k];
             st[ji[k]] = js[k];
+            msg[ji[k]] = jm[k];
         }
     }
     int first = IK_OK;
+    for (uint32_t i = 0; i < n; ++i)
+        if (st[i] && !first) first = st[i];
+    return first;
+}
+
+}  // namespace ik (reopened for the ABI below)
+extern "C" {
+
+int ik_decode(const uint8_t* bytes, size_t len, ik_image** out, int* fmt_out) {
+    if (!sched_multi()) return decode_one(bytes, len, out, fmt_out);
+    // several devices: the least-loaded one decodes (the image stays there)
+    const uint64_t cost = request_cost(bytes, len, -1, -1, IK_FORMAT_JPEG);
+    const int ld = sched_acquire(cost);
+    int st;
+    {
+        DeviceGuard g(sched_phys(ld));
+        st = decode_one(bytes, len, out, fmt_out);
+    }
+    sched_release(ld, cost);
+    return st;
+}
+
+int ik_decode_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t n, ik_image** outs, int* fmts,
+                    int* status) {
+    if (!bytes || !lens || !outs || !n) return fail(IK_ERR_INVALID, "bad batch");
+    std::vector<int> st(n, IK_OK);
+    std::vector<std::string> msg(n);
+    int first;
+    if (sched_multi()) {
+        uint64_t cost = 0;
+        for (uint32_t i = 0; i < n; ++i) cost += request_cost(bytes[i], lens[i], -1, -1, IK_FORMAT_JPEG);
+        const int ld = sched_acquire(cost);
+        {
+            DeviceGuard g(sched_phys(ld));
+            first = decode_batch_dev(bytes, lens, n, outs, fmts, st.data(), msg.data(), 0);
+        }
+        sched_release(ld, cost);
+    } else {
+        first = decode_batch_dev(bytes, lens, n, outs, fmts, st.data(), msg.data(), 0);
+    }
     uint32_t fi = 0;
     for (uint32_t i = 0; i < n; ++i) {
         if (status) status[i] = st[i];
-        if (st[i] && !first) { first = st[i]; fi = i; }
+        if (st[i] && fi == 0 && first && st[fi] == IK_OK) fi = i;
     }
-    if (first) return fail(first, "input %u: %s", fi, msg[fi].empty() ? "JPEG decode failed" : msg[fi].c_str());
+    if (first) {
+        for (fi = 0; fi < n && !st[fi]; ++fi) {}
+        return fail(first, "input %u: %s", fi, msg[fi].c_str());
+    }
     return IK_OK;
 }
 
@@ -624,60 +740,98 @@ int ik_set_resize_mode(int mode) {
 
 int ik_get_resize_mode(void) { return resize_mode(); }
 
+}  // extern "C"
+
+namespace ik {
+
+// ik_transform_batch over the items idx[] of a batch, on the calling thread's
+// device: one batched decode (GPU entropy decoding where the stream allows), then
+// resize_image + encode_image per item on the device's persistent workers.
+static void transform_batch_dev(const uint8_t* const* bytes, const size_t* lens, const std::vector<uint32_t>& idx,
+                                const int64_t* w, const int64_t* h, const int* fmt, const int* quality, int filter,
+                                int threads, uint8_t** outs, size_t* out_lens, int* st, std::string* errs) {
+    const uint32_t m = (uint32_t)idx.size();
+    if (!m) return;
+    std::vector<const uint8_t*> b(m);
+    std::vector<size_t> l(m);
+    for (uint32_t k = 0; k < m; ++k) { b[k] = bytes[idx[k]]; l[k] = lens[idx[k]]; }
+    std::vector<ik_image*> imgs(m, nullptr);
+    std::vector<int> ds(m, IK_OK);
+    std::vector<std::string> dm(m);
+    decode_batch_dev(b.data(), l.data(), m, imgs.data(), nullptr, ds.data(), dm.data(), threads);
+    static const bool timing = getenv("IK_TIMING") != nullptr;  // dev: per-stage sums to stderr
+    std::mutex tmu;
+    double t_resize = 0, t_encode = 0;
+    parallel_for((int)m, threads, [&](int k) {
+        const uint32_t i = idx[k];
+        if (ds[k]) { st[i] = ds[k]; errs[i] = dm[k]; return; }
+        ik_image* rs = nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
+        int r = ik_resize(imgs[k], w[i], h[i], filter, &rs);
+        const auto t1 = std::chrono::steady_clock::now();
+        if (!r) r = ik_encode(rs, fmt[i], quality[i], &outs[i], &out_lens[i]);
+        if (timing) {
+            const auto t2 = std::chrono::steady_clock::now();
+            std::lock_guard<std::mutex> lk(tmu);
+            t_resize += std::chrono::duration<double, std::milli>(t1 - t0).count();
+            t_encode += std::chrono::duration<double, std::milli>(t2 - t1).count();
+        }
+        if (r) { errs[i] = last_error_str(); st[i] = r; }
+        if (rs && rs != imgs[k]) ik_image_free(rs);
+        ik_image_free(imgs[k]);
+        imgs[k] = nullptr;
+    });
+    if (timing)
+        fprintf(stderr, "[transform_batch] %u requests on device %d: resize %.1f ms, encode %.1f ms (summed)\n", m,
+                current_device(), t_resize, t_encode);
+}
+
+}  // namespace ik
+
+extern "C" {
+
 int ik_transform_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t n, const int64_t* w,
                        const int64_t* h, const int* fmt, const int* quality, int filter, int threads, uint8_t** outs,
                        size_t* out_lens, int* status) {
     if (!bytes || !lens || !w || !h || !fmt || !quality || !outs || !out_lens || !n)
         return fail(IK_ERR_INVALID, "bad batch");
-    std::vector<ik_image*> imgs(n, nullptr);
     std::vector<int> st(n, IK_OK);
-    for (uint32_t i = 0; i < n; ++i) { outs[i] = nullptr; out_lens[i] = 0; }
-    ik_decode_batch(bytes, lens, n, imgs.data(), nullptr, st.data());
-    // resize + encode per image on host threads, each with its own HIP stream
-    const int dev = current_device();
-    if (threads <= 0) threads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-    threads = (int)std::min<uint32_t>((uint32_t)threads, n);
     std::vector<std::string> errs(n);
-    std::atomic<uint32_t> next{0};
-    static const bool timing = getenv("IK_TIMING") != nullptr;  // dev: per-stage sums to stderr
-    std::mutex tmu;
-    double t_resize = 0, t_encode = 0;
-    auto work = [&](bool own_thread) {
-        if (own_thread) ik_init(dev);
-        for (uint32_t i; (i = next.fetch_add(1)) < n;) {
-            if (st[i]) {
-                char buf[256];
-                if (!errs[i].size()) { ik_last_error(buf, sizeof(buf)); errs[i] = buf; }
-                continue;
-            }
-            ik_image* rs = nullptr;
-            const auto t0 = std::chrono::steady_clock::now();
-            int r = ik_resize(imgs[i], w[i], h[i], filter, &rs);
-            const auto t1 = std::chrono::steady_clock::now();
-            if (!r) r = ik_encode(rs, fmt[i], quality[i], &outs[i], &out_lens[i]);
-            if (timing) {
-                const auto t2 = std::chrono::steady_clock::now();
-                std::lock_guard<std::mutex> lk(tmu);
-                t_resize += std::chrono::duration<double, std::milli>(t1 - t0).count();
-                t_encode += std::chrono::duration<double, std::milli>(t2 - t1).count();
-            }
-            if (r) {
-                char buf[256];
-                ik_last_error(buf, sizeof(buf));
-                errs[i] = buf;
-                st[i] = r;
-            }
-            if (rs && rs != imgs[i]) ik_image_free(rs);
-            ik_image_free(imgs[i]);
-            imgs[i] = nullptr;
+    for (uint32_t i = 0; i < n; ++i) { outs[i] = nullptr; out_lens[i] = 0; }
+    if (!sched_multi()) {
+        std::vector<uint32_t> all(n);
+        for (uint32_t i = 0; i < n; ++i) all[i] = i;
+        transform_batch_dev(bytes, lens, all, w, h, fmt, quality, filter, threads, outs, out_lens, st.data(),
+                            errs.data());
+    } else {
+        // several devices: the requests are split by least outstanding cost (largest
+        // first) and each device's share runs on that device's own workers
+        std::vector<uint64_t> cost(n);
+        for (uint32_t i = 0; i < n; ++i) cost[i] = request_cost(bytes[i], lens[i], w[i], h[i], fmt[i]);
+        std::vector<uint32_t> assign(n);
+        sched_acquire_batch(cost.data(), n, assign.data());
+        const int nd = sched_count();
+        std::vector<std::vector<uint32_t>> part(nd);
+        for (uint32_t i = 0; i < n; ++i) part[assign[i]].push_back(i);
+        std::mutex mu;
+        std::condition_variable cv;
+        int pending = 0;
+        for (int d = 0; d < nd; ++d) {
+            if (part[d].empty()) continue;
+            ++pending;
+            sched_pool(d).post([&, d] {
+                transform_batch_dev(bytes, lens, part[d], w, h, fmt, quality, filter, threads, outs, out_lens,
+                                    st.data(), errs.data());
+                uint64_t c = 0;
+                for (uint32_t i : part[d]) c += cost[i];
+                sched_release(d, c);
+                std::lock_guard<std::mutex> lk(mu);
+                if (--pending == 0) cv.notify_all();
+            });
         }
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < threads; ++t) th.emplace_back(work, true);
-    work(false);
-    for (auto& t : th) t.join();
-    if (timing) fprintf(stderr, "[transform_batch] %u requests, %d threads: resize %.1f ms, encode %.1f ms (summed)\n",
-                        n, threads, t_resize, t_encode);
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return pending == 0; });
+    }
     int first = IK_OK;
     uint32_t first_i = 0;
     for (uint32_t i = 0; i < n; ++i) {
@@ -688,10 +842,10 @@ int ik_transform_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t
     return IK_OK;
 }
 
-int ik_transform(const uint8_t* bytes, size_t len, int64_t w, int64_t h, int fmt, int quality,
-                 int filter, uint8_t** out, size_t* out_len) {
+static int transform_here(const uint8_t* bytes, size_t len, int64_t w, int64_t h, int fmt, int quality,
+                          int filter, uint8_t** out, size_t* out_len) {
     ik_image* img = nullptr;
-    int st = ik_decode(bytes, len, &img, nullptr);
+    int st = decode_one(bytes, len, &img, nullptr);
     if (st) return st;
     ik_image* rs = nullptr;
     st = ik_resize(img, w, h, filter, &rs);
@@ -700,6 +854,35 @@ int ik_transform(const uint8_t* bytes, size_t len, int64_t w, int64_t h, int fmt
     if (rs != img) ik_image_free(rs);
     ik_image_free(img);
     return st;
+}
+
+int ik_transform(const uint8_t* bytes, size_t len, int64_t w, int64_t h, int fmt, int quality,
+                 int filter, uint8_t** out, size_t* out_len) {
+    if (!sched_multi()) return transform_here(bytes, len, w, h, fmt, quality, filter, out, out_len);
+    // several devices: queue the request to the least-loaded device's workers
+    const uint64_t cost = request_cost(bytes, len, w, h, fmt);
+    const int ld = sched_acquire(cost);
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+    int st = IK_OK;
+    std::string msg;
+    sched_pool(ld).post([&] {
+        const int r = transform_here(bytes, len, w, h, fmt, quality, filter, out, out_len);
+        std::string m = r ? last_error_str() : std::string();
+        std::lock_guard<std::mutex> lk(mu);
+        st = r;
+        msg.swap(m);
+        done = true;
+        cv.notify_all();
+    });
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return done; });
+    }
+    sched_release(ld, cost);
+    if (st) return fail(st, "%s", msg.c_str());
+    return IK_OK;
 }
 
 int ik_resize_batch_device(const uint8_t* dev_src, uint32_t W, uint32_t H, uint32_t C,

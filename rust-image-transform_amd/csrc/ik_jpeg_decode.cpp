@@ -929,27 +929,26 @@ int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gp
 
 }  // namespace
 
-int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_image** outs, int* status) {
+int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_image** outs, int* status,
+                      std::string* msgs) {
     // 1. parse every stream (host threads); restart-interval baseline scans are deferred
     std::vector<std::unique_ptr<Decoder>> ds(n);
     std::vector<int> st(n, IK_OK);
-    {
-        std::atomic<int> next{0};
-        auto work = [&] {
-            for (int i; (i = next.fetch_add(1)) < n;) {
-                ds[i].reset(new Decoder());
-                ds[i]->b = bytes[i];
-                ds[i]->end = bytes[i] + lens[i];
-                ds[i]->try_gpu = true;
-                st[i] = ds[i]->parse();
-            }
-        };
-        const int nt = std::max(1, std::min(n, std::min(16, (int)std::thread::hardware_concurrency())));
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; ++t) th.emplace_back(work);
-        work();
-        for (auto& t : th) t.join();
-    }
+    auto note = [&](int i) {
+        if (st[i] && msgs) {
+            char buf[512];
+            ik_last_error(buf, sizeof(buf));
+            msgs[i] = buf;
+        }
+    };
+    parallel_for(n, 0, [&](int i) {
+        ds[i].reset(new Decoder());
+        ds[i]->b = bytes[i];
+        ds[i]->end = bytes[i] + lens[i];
+        ds[i]->try_gpu = true;
+        st[i] = ds[i]->parse();
+        note(i);
+    });
     std::vector<int> gpu_idx, host_idx, seq_idx;
     for (int i = 0; i < n; ++i) {
         outs[i] = nullptr;
@@ -978,9 +977,11 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
             L.end = L.pl + up256(pb);
             total = L.end;
         }
-        uint8_t* dev = nullptr;
+        // the batch's device work area: a grow-only per-thread arena (hipFree would
+        // synchronise the whole device under concurrent batches)
         hipStream_t s = thread_stream();
-        int rc = hipMalloc(&dev, total) == hipSuccess ? IK_OK : fail(IK_ERR_DEVICE, "hipMalloc(jpeg batch)");
+        uint8_t* dev = scratch_slot(1, total);
+        int rc = dev ? IK_OK : fail(IK_ERR_DEVICE, "cannot allocate the JPEG batch work area");
         std::vector<JpegScanArgs> args(m);
         int max_seg = 0;
         for (int k = 0; k < m && !rc; ++k) {
@@ -1040,7 +1041,6 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
             outs[i] = img;
         }
         hipError_t e = rc ? hipSuccess : hipStreamSynchronize(s);
-        if (dev) (void)hipFree(dev);
         if (rc || e != hipSuccess) {  // the batch as a whole failed on the device: each image on its own path
             for (int k = 0; k < m; ++k) {
                 const int i = gpu_idx[k];
@@ -1058,6 +1058,7 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
     parallel_for((int)host_idx.size(), 0, [&](int k) {
         const int i = host_idx[k];
         st[i] = decode_jpeg_impl(bytes[i], lens[i], &outs[i], k >= nh);
+        note(i);
     });
     int first = IK_OK;
     for (int i = 0; i < n; ++i) {

@@ -28,12 +28,12 @@
 namespace ik {
 namespace {
 
-class Pool {
+class CoderPool {
 public:
-    explicit Pool(int n) {
+    explicit CoderPool(int n) {
         for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
     }
-    ~Pool() {
+    ~CoderPool() {
         {
             std::lock_guard<std::mutex> lk(mu_);
             stop_ = true;
@@ -133,7 +133,7 @@ struct ik_pipeline {
     int head = 0, inflight = 0;
     double ms[4] = {0, 0, 0, 0};
     uint32_t last_n = 0;
-    ik::Pool* pool = nullptr;
+    ik::CoderPool* pool = nullptr;
     std::vector<std::vector<uint8_t>> outs;
     std::vector<int> status;
 };
@@ -380,7 +380,7 @@ int pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t nh
         if (threads > 16) threads = 16;
         if (threads < 1) threads = 1;
     }
-    p->pool = new Pool(threads - 1);  // the calling thread works too
+    p->pool = new CoderPool(threads - 1);  // the calling thread works too
     if (fmt == IK_FORMAT_WEBP && !device_consts(p->device)) return fail(IK_ERR_DEVICE, "cannot upload WebP tables");
     return IK_OK;
 }

@@ -1,8 +1,11 @@
 // ik_runtime.h -- host runtime internals of libimagekit_hip.so (not part of the ABI).
 #pragma once
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdint>
+#include <deque>
 #include <functional>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -29,12 +32,60 @@ int hip_fail(hipError_t e, const char* what);
     } while (0)
 
 int current_device();
-// fn(i) for i in [0, n) on up to `threads` host threads (0 = min(16, cores)); the
-// extra threads select the caller's HIP device first
+// make `device` the calling thread's device for the guard's lifetime (an image's
+// stages run on the device that holds its pixels)
+struct DeviceGuard {
+    int prev;
+    explicit DeviceGuard(int device);
+    ~DeviceGuard();
+};
+
+// ---- persistent host workers (ik_pool.cpp) ----
+int default_threads();  // IK_THREADS, else min(16, cores)
+class Pool {
+public:
+    Pool(int device, int max_threads);
+    // fn(i) for i in [0, n) on up to `threads` threads (the caller included; 0 =
+    // default_threads()); returns when every call has returned
+    void parallel_for(int n, int threads, const std::function<void(int)>& fn);
+    void post(std::function<void()> task);  // run on a worker (device already selected)
+    int device() const { return device_; }
+
+private:
+    void ensure(int nthreads);
+    void loop();
+    int device_, max_threads_;
+    int nthreads_ = 0, busy_ = 0;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+};
+Pool& device_pool(int device);  // the persistent workers of a physical device
+// fn(i) for i in [0, n) on the calling thread's device pool (and the caller)
 void parallel_for(int n, int threads, const std::function<void(int)>& fn);
+
+// multi-device dispatch (ik_init(-1) / IK_DEVICES): logical devices, least outstanding cost
+int sched_configure(const int* devices, int n);
+bool sched_multi();
+int sched_count();
+int sched_phys(int logical);
+Pool& sched_pool(int logical);
+int sched_acquire(uint64_t cost);
+void sched_release(int logical, uint64_t cost);
+void sched_acquire_batch(const uint64_t* costs, uint32_t n, uint32_t* assign);
+void sched_plan(const uint64_t* costs, uint32_t n, uint32_t ndev, const uint64_t* outstanding, uint32_t* assign);
+int sched_stats(uint32_t logical, uint64_t* jobs, uint64_t* cost_done, uint64_t* outstanding);
+// header-only dimension sniff (PNG IHDR, JPEG SOFn, WebP VP8/VP8L/VP8X); c = bytes per pixel
+bool sniff_dims(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& c);
+uint64_t request_cost(const uint8_t* b, size_t n, int64_t w, int64_t h, int fmt);
+
 hipStream_t thread_stream();  // per-thread, per-device non-blocking stream
 size_t pitch_for(uint32_t w, uint32_t c);
 uint8_t* scratch(size_t bytes);  // per-thread device scratch, valid until the next call
+// per-thread, per-device grow-only device arenas for batch work (slot 1: JPEG
+// batch decode, slot 2: PNG batch decode); valid until the next call with that slot
+uint8_t* scratch_slot(int slot, size_t bytes);
+uint8_t* pinned_slot(int slot, size_t bytes);  // per-thread grow-only pinned host arenas
 int copy_h2d_2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,
                 size_t height, hipStream_t s);
 int copy_d2h_2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,
@@ -103,7 +154,8 @@ int decode_webp(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& 
 int decode_jpeg_device(const uint8_t* b, size_t n, ik_image** out);
 // n streams at once: restart-interval baseline scans entropy-decoded in one GPU
 // launch; per-stream status (outs[i] null on failure); returns the first failure
-int decode_jpeg_batch(const uint8_t* const* b, const size_t* lens, int n, ik_image** outs, int* status);
+int decode_jpeg_batch(const uint8_t* const* b, const size_t* lens, int n, ik_image** outs, int* status,
+                      std::string* msgs /* [n] or null: per-stream error message */);
 
 // device-side stage helpers used by ik_encode and the pipeline
 int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, size_t pitch,

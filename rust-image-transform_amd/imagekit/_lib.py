@@ -23,6 +23,11 @@ c_img_p = ctypes.c_void_p
 SIGNATURES = [
     ("ik_init", ctypes.c_int, [ctypes.c_int]),
     ("ik_device_count", ctypes.c_int, []),
+    ("ik_init_devices", ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    ("ik_logical_device_count", ctypes.c_int, []),
+    ("ik_logical_device_stats", ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    ("ik_request_cost", ctypes.c_uint64, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int64, ctypes.c_int]),
+    ("ik_schedule_plan", None, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
     ("ik_last_error", ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_size_t]),
     ("ik_version", ctypes.c_char_p, []),
     ("ik_image_from_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(c_img_p)]),

@@ -60,3 +60,107 @@ def test_transform_batch_avif_and_errors(ik):
         assert im.size == (w, h)
     with pytest.raises(TransformError):
         transform_batch([blobs[0], b"not an image"], [(10, None), (10, None)], [ImageFormat.jpeg] * 2, [80, 80])
+
+
+def test_batch_error_message_is_the_decoders_own(ik):
+    """The failing item carries its own decoder's message (TransformError(e.to_string()),
+    src/transform.rs:29,32), not another request's or an empty one."""
+    blobs = _inputs()
+    bad_png = blobs[4][:60]  # truncated chunk
+    with pytest.raises(TransformError) as ei:
+        transform_batch([blobs[0], bad_png, blobs[1]], [(10, None)] * 3, [ImageFormat.jpeg] * 3, [80] * 3)
+    assert "item 1" in str(ei.value) and "Png" in str(ei.value)
+
+
+def test_repeated_batches_do_not_grow_device_memory(ik):
+    """per-call threads leaked a HIP stream, pinned staging and
+    device scratch each.  Batch work now runs on persistent workers: after a warm-up
+    the free device memory stays flat over repeated calls."""
+    import torch
+    blobs = _inputs()
+    sizes = [(320, None), (None, 240), (None, None), (400, 400), (150, 100), (512, None)] * 3
+    fmts = [ImageFormat.webp, ImageFormat.jpeg] * 9
+    datas = blobs * 3
+
+    def run():
+        transform_batch(datas, sizes, fmts, [80] * len(datas), threads=8)
+        torch.cuda.synchronize()
+        return torch.cuda.mem_get_info()[0]
+
+    run()
+    run()
+    f0 = run()
+    for _ in range(6):
+        f1 = run()
+    assert f0 - f1 < (32 << 20), f"device memory fell by {(f0 - f1) >> 20} MiB over 6 batches"
+
+
+MULTI_SCRIPT = r'''
+import ctypes, io, json, os, sys, threading
+sys.path[:0] = [os.environ["IK_PKG"], os.environ["IK_TESTS"]]
+import numpy as np
+from PIL import Image
+import ikutil
+from imagekit import ImageFormat, _lib, transform_batch
+lib = _lib.load()
+blobs = []
+for k, (w, h) in enumerate([(640, 480), (1000, 700), (333, 222), (800, 600)]):
+    b = io.BytesIO()
+    Image.fromarray(ikutil.synth(w, h, 3, seed=k)).save(b, format="JPEG", quality=90, **({"restart_marker_rows": 1} if k % 2 == 0 else {}))
+    blobs.append(b.getvalue())
+b = io.BytesIO(); Image.fromarray(ikutil.synth(300, 200, 4, seed=9)).save(b, format="PNG"); blobs.append(b.getvalue())
+sizes = [(320, None), (None, 240), (200, 200), (400, 400), (150, 100)] * 4
+fmts = [ImageFormat.webp, ImageFormat.jpeg] * 10
+datas = blobs * 4
+def single():
+    res = []
+    for d, (w, h), f in zip(datas, sizes, fmts):
+        out, n = _lib.u8p(), ctypes.c_size_t()
+        assert lib.ik_transform(d, len(d), -1 if w is None else w, -1 if h is None else h, f.value, 80, 4,
+                                ctypes.byref(out), ctypes.byref(n)) == 0, _lib.last_error()
+        res.append(ctypes.string_at(out, n.value)); lib.ik_buf_free(out)
+    return res
+assert lib.ik_init(0) == 0
+ref_batch = transform_batch(datas, sizes, fmts, [80] * len(datas), threads=4)
+ref_single = single()
+assert lib.ik_init(-1) == 0, _lib.last_error()          # IK_DEVICES=0,0: two logical devices on GPU 0
+assert lib.ik_logical_device_count() == 2
+got_batch = transform_batch(datas, sizes, fmts, [80] * len(datas), threads=4)
+got = [None] * len(datas)
+def worker(t):
+    for i in range(t, len(datas), 4):
+        d, (w, h), f = datas[i], sizes[i], fmts[i]
+        out, n = _lib.u8p(), ctypes.c_size_t()
+        assert lib.ik_transform(d, len(d), -1 if w is None else w, -1 if h is None else h, f.value, 80, 4,
+                                ctypes.byref(out), ctypes.byref(n)) == 0, _lib.last_error()
+        got[i] = ctypes.string_at(out, n.value); lib.ik_buf_free(out)
+ts = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+[t.start() for t in ts]; [t.join() for t in ts]
+jobs = []
+for d in range(2):
+    j, c, o = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    assert lib.ik_logical_device_stats(d, ctypes.byref(j), ctypes.byref(c), ctypes.byref(o)) == 0
+    jobs.append((j.value, c.value, o.value))
+print(json.dumps({"batch_equal": got_batch == ref_batch, "single_equal": got == ref_single,
+                  "batch_vs_single": ref_batch == ref_single, "jobs": jobs}))
+'''
+
+
+def test_two_logical_devices_match_single_device(ik):
+    """SURVEY 8(e) E-2: one process, a work queue over logical devices.  IK_DEVICES=0,0
+    maps two logical devices onto GPU 0; the bytes equal single-device output and
+    both devices take work.  (Own process: multi-device dispatch is process-wide.)"""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, IK_DEVICES="0,0", IK_PKG=os.path.join(root, "rust-image-transform_amd"),
+               IK_TESTS=os.path.join(root, "tests"))
+    r = subprocess.run([sys.executable, "-c", MULTI_SCRIPT], env=env, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["batch_vs_single"] and res["batch_equal"] and res["single_equal"], res
+    (j0, c0, o0), (j1, c1, o1) = res["jobs"]
+    assert j0 > 0 and j1 > 0 and o0 == 0 and o1 == 0
+    assert max(c0, c1) < 3 * min(c0, c1)  # least-outstanding keeps the two within reach
