@@ -1,31 +1,39 @@
 #!/usr/bin/env python3
 """bench.py -- transform MPix/s (decode+resize+encode) 4096^2 -> 512^2 WebP q80.
 
-Workload (BASELINE.json configs[1]): synthetic 4096x4096 RGBA8 images already
-resident in HBM ("RGBA8 synthetic": the decoded DynamicImage the reference's
-resize_image receives; raw frames need no entropy decode) -> resize_image to
-512x512 (Triangle = "bilinear" per configs[1]; --filter lanczos3 for the
-reference's own filter) -> encode_image WebP q80.  One step = one batch through
-libimagekit_hip.so's pipeline: ONE resize launch over the batch, ONE WebP
-colour-convert launch, D2H of the YUV planes, libwebp VP8 coding of every image
-on the host thread pool.  Encoded bytes end in host memory.  Batches go through
-ik_pipeline_submit / ik_pipeline_collect with two in flight, so the host coding
-of batch i overlaps the device stage of batch i+1 (--sync: one at a time).
+Headline `value` (BASELINE.json metric): synthetic 4096x4096
+RGBA8 frames as PNG files (Pillow, zlib level 6, adaptive filters; the configs[1]
+frame in the container SURVEY D-2 names) sit in HOST memory; one step is one
+ik_transform_batch call over a batch of them -- decode_image (GPU inflate +
+unfilter, ik_png.hip), resize_image to 512x512 (Triangle = configs[1]'s
+"bilinear"), encode_image WebP q80 (libwebp, byte-identical to the reference's
+webp 0.3.1 path) -- and ends with the WebP bytes in host memory.  value = input
+pixels of all ranks / max-over-ranks wall time of the K timed steps.  The host
+threads the GPU path may use are stated (--threads, default 32 = an 8-GPU node's
+256 cores / 8).
 
-value = input pixels of all images of all ranks / max-over-ranks wall time of
-the K timed steps.  roofline = the resize kernel (the dominant device kernel):
-algorithmic bytes per launch (4*W*H + 4*w*h per image) /
-its average duration from HIP events on the pipeline's stream.  cpu_baseline =
-the oracle restatement of the reference CPU path (image 0.25.8 resize + libwebp
-WebPEncodeRGB) timed on this host's cores on a bounded sample.
+Beside it, in the same JSON line:
+  cpu_baseline   the same PNG bytes through the reference CPU path restated
+                 (oracle/: png decode + image 0.25.8 resize + libwebp), one image
+                 per thread, at 1 thread and at nproc threads (SURVEY D-6; the
+                 reference runs one synchronous transform per tokio worker).
+  roofline       the dominant device kernel of the step by HIP-event time, its
+                 algorithmic bytes per launch / its duration vs 8 TB/s; the
+                 resize kernel's own roofline in roofline_resize.
+  hbm_resident   the old headline: the same frames already decoded in HBM ->
+                 ik_pipeline (one resize launch per batch, WebP colour kernel,
+                 libwebp on the host threads), two batches in flight.
+  decode_inclusive_jpeg   the same frames as JPEG q90 4:2:0 with restart markers
+                 (configs[2]'s container) through ik_transform_batch.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N>1 under
-torch.distributed.run (one rank per GPU, RCCL only for barrier/max).
+torch.distributed.run (one rank per GPU; RCCL only for barrier / max).
 """
 from __future__ import annotations
 
 import argparse
 import ctypes
+import io
 import json
 import os
 import sys
@@ -40,42 +48,34 @@ sys.path[:0] = [os.path.join(ROOT, "rust-image-transform_amd"), os.path.join(ROO
 METRIC = "transform MPix/s (decode+resize+encode) 4096²→512² WebP q80; 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FILTERS = {"nearest": 0, "triangle": 1, "catmullrom": 2, "gaussian": 3, "lanczos3": 4}
-ENCODERS = {"libwebp": 0, "gpu": 1}
-CPU_CODER = {"webp": "libwebp", "jpeg": "image-crate JPEG", "avif": "libavif/aom speed 4 (Pillow, rav1e absent)"}
 FORMATS = {"jpeg": 0, "webp": 1, "avif": 2}
+PNG_STAGES = ["host_parse_stage", "find", "count", "emit", "resolve", "unfilter"]
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=64, help="images per GPU per step")
-    ap.add_argument("--alt-batch", type=int, default=256, help="images per GPU per step for the other WebP encoder")
-    ap.add_argument("--alt-steps", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=64, help="PNG requests per GPU per step")
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--out", type=int, default=512)
     ap.add_argument("--filter", default="triangle", choices=sorted(FILTERS))
     ap.add_argument("--quality", type=int, default=80)
-    ap.add_argument("--format", default="webp", choices=["webp", "jpeg", "avif"],
-                    help="webp: the headline (configs[1]); jpeg: configs[2]-style runs (GPU Huffman coding); "
-                         "avif: configs[4]-style runs (--size 8192 --out 1024 --filter lanczos3 --quality 60)")
-    ap.add_argument("--threads", type=int, default=16, help="host entropy-coder threads per rank")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample wall-time budget (s)")
+    ap.add_argument("--distinct", type=int, default=4, help="distinct PNG frames per rank (tiled over the batch)")
+    ap.add_argument("--threads", type=int, default=32, help="host threads per GPU (stated budget)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of each cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--device-only", action="store_true", help="time resize+colour kernels only")
-    ap.add_argument("--webp-encoder", default="libwebp", choices=["libwebp", "gpu"],
-                    help="libwebp: host VP8 coder, bytes identical to the reference; gpu: gfx950 VP8 encoder")
-    ap.add_argument("--sync", action="store_true", help="one batch in flight (ik_pipeline_run per step)")
-    ap.add_argument("--no-alt-encoder", action="store_true", help="skip timing the other WebP encoder")
-    ap.add_argument("--png-images", type=int, default=64,
-                    help="images per rank for each decode-inclusive leg (PNG and JPEG sources through ik_transform_batch; 0 = skip)")
+    ap.add_argument("--no-extras", action="store_true", help="skip the hbm_resident / JPEG legs")
+    ap.add_argument("--hbm-batch", type=int, default=64)
+    ap.add_argument("--hbm-steps", type=int, default=6)
+    ap.add_argument("--jpeg-images", type=int, default=64)
     return ap.parse_args()
 
 
-def shard_seeds(rank: int, batch: int, distinct: int = 4):
+def shard_seeds(rank: int, n: int):
     """Synthetic frames of rank `rank`: disjoint seed ranges, so ranks never share work."""
-    return [1000 * rank + i for i in range(min(batch, distinct))]
+    return [1000 * rank + i for i in range(n)]
 
 
 def reduce_max(value: float, dist, device) -> float:
@@ -88,137 +88,9 @@ def reduce_max(value: float, dist, device) -> float:
     return float(t.item())
 
 
-def aggregate_mpix(world: int, batch: int, steps: int, size: int, elapsed: float) -> float:
+def aggregate_mpix(world: int, per_rank_images: int, size: int, elapsed: float) -> float:
     """Whole-job throughput: input pixels of all ranks / max-over-ranks wall time."""
-    return world * batch * steps * size * size / elapsed / 1e6
-
-
-def synth_rgba(w, h, seed):
-    import ikutil
-    return ikutil.synth(w, h, 4, seed=seed, pattern="S")
-
-
-def png_leg(args, frames, world, dist, device, barrier, kind="png"):
-    """Decode-inclusive figure beside `value`: the same frames as encoded files through
-    ik_transform_batch, with encoded input and output bytes in host memory.
-    kind "png": PNG RGBA8 (Pillow's zlib level 6; SURVEY 8(d) D-2's container for
-    configs[1]) -- host inflate + unfilter (png 0.18 via image), device resize, encode.
-    kind "jpeg": baseline JPEG q90 4:2:0 with a restart marker per MCU row (D-2's
-    container for configs[2]) -- GPU entropy decoding, IDCT, upsampling and colour."""
-    import io
-
-    from PIL import Image
-
-    from imagekit import transform_batch
-    pngs = []
-    for im in frames[:2]:
-        b = io.BytesIO()
-        if kind == "png":
-            Image.fromarray(im, "RGBA").save(b, format="PNG")
-        else:
-            Image.fromarray(np.ascontiguousarray(im[..., :3]), "RGB").save(b, format="JPEG", quality=90,
-                                                                         restart_marker_rows=1)
-        pngs.append(b.getvalue())
-    n, O, fmt, f = args.png_images, args.out, FORMATS[args.format], FILTERS[args.filter]
-
-    def run(k):
-        res = transform_batch([pngs[i % len(pngs)] for i in range(k)], [(O, O)] * k, [fmt] * k,
-                              [args.quality] * k, filter=f, threads=args.threads)
-        assert all(r for r in res)
-
-    run(2)
-    barrier()
-    t0 = time.perf_counter()
-    run(n)
-    el = time.perf_counter() - t0
-    barrier()
-    el = reduce_max(el, dist, device)
-    res = {"source": "PNG RGBA8 (zlib level 6), host inflate + unfilter" if kind == "png" else
-                     "JPEG q90 4:2:0, RSTn per MCU row, GPU entropy decoding", "images_per_gpu": n,
-           "bytes_per_source_image": sum(len(p) for p in pngs) // len(pngs),
-           "value": round(aggregate_mpix(world, n, 1, args.size, el), 2), "unit": "MPix/s",
-           "ms_per_image_per_gpu": round(el / n * 1e3, 3)}
-    if world == 1 and not args.no_cpu_baseline and args.format != "avif":
-        # CPU proxy of the same decode-inclusive transform: Pillow's PNG decoder (zlib +
-        # libpng-style unfilter, standing in for png 0.18) + the oracle resize + encode,
-        # one image per thread, two rounds of args.threads images
-        import ikutil
-        orc = ikutil.Oracle()
-        threads = max(1, min(args.threads, os.cpu_count() or 1))
-
-        def one(k):
-            px = np.asarray(Image.open(io.BytesIO(pngs[k % len(pngs)])).convert("RGBA" if kind == "png" else "RGB"))
-            b, _ = orc.transform(px, O, O, f, fmt, args.quality)
-            assert b
-
-        t0 = time.perf_counter()
-        for r in range(2):
-            ts = [threading.Thread(target=one, args=(r * threads + i,)) for i in range(threads)]
-            for t in ts:
-                t.start()
-            for t in ts:
-                t.join()
-        cw = time.perf_counter() - t0
-        res["cpu_proxy"] = {"value": round(2 * threads * args.size * args.size / cw / 1e6, 2), "unit": "MPix/s",
-                            "cores": threads, "sample": f"{2 * threads} {kind.upper()} images, Pillow decode + oracle "
-                                                        f"resize + {CPU_CODER[args.format]}, {cw:.1f}s wall"}
-    return res
-
-
-def cpu_baseline(args, img: np.ndarray):
-    """Reference CPU transform restated (oracle/, test infrastructure) on a bounded sample."""
-    import ikutil
-    orc = ikutil.Oracle()
-    threads = max(1, min(args.threads, os.cpu_count() or 1))
-    H, W, C = img.shape
-    f = FILTERS[args.filter]
-    done = [0]
-    lock = threading.Lock()
-
-    def one():
-        if args.format == "avif":  # oracle resize + libavif/aom (Pillow's, one thread), speed 4 as ravif's
-            import io
-
-            from PIL import Image
-            px = orc.resize(img, args.out, args.out, f)
-            bio = io.BytesIO()
-            Image.fromarray(px[..., :3]).save(bio, format="AVIF", quality=args.quality, speed=4, max_threads=1)
-            assert bio.getvalue()[4:8] == b"ftyp"
-        else:
-            b, dims = orc.transform(img, args.out, args.out, f, FORMATS[args.format], args.quality)
-            assert dims == (args.out, args.out) and b[:2] in (b"RI", b"\xff\xd8")
-        with lock:
-            done[0] += 1
-
-    # single-thread time of one warm image sizes the sample: `rounds` rounds of one
-    # image per thread ~ args.cpu_seconds of wall time (10-30 s of CPU work in all)
-    one()
-    t0 = time.perf_counter()
-    one()
-    t1 = time.perf_counter() - t0
-    rounds = max(1, int(args.cpu_seconds / max(t1, 1e-3)))
-    rounds = min(rounds, 400)
-    done[0] = 0
-    t0 = time.perf_counter()
-    for _ in range(rounds):
-        ts = [threading.Thread(target=one) for _ in range(threads)]
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
-    wall = time.perf_counter() - t0
-    n = done[0]
-    return {
-        "value": round(n * W * H / wall / 1e6, 3),
-        "unit": "MPix/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"{n} x {W}x{H} RGBA8 -> {args.out}x{args.out} {args.filter} + "
-                  f"{CPU_CODER[args.format]} q{args.quality}, "
-                  f"one image per thread, {threads} threads, {wall:.1f}s wall",
-        "value_1core": round(W * H / t1 / 1e6, 3),
-        "host": host_info(),
-    }
+    return world * per_rank_images * size * size / elapsed / 1e6
 
 
 def host_info():
@@ -233,6 +105,87 @@ def host_info():
         pass
     return {"cpu_model": model, "nproc": os.cpu_count(),
             "affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
+
+
+def make_pngs(frames):
+    from PIL import Image
+    out = []
+    for im in frames:
+        b = io.BytesIO()
+        Image.fromarray(im, "RGBA").save(b, format="PNG")  # zlib level 6, adaptive filters
+        out.append(b.getvalue())
+    return out
+
+
+def cpu_baseline(args, pngs):
+    """The reference CPU path restated (oracle/: PNG decode + image 0.25.8 resize +
+    libwebp WebPEncodeRGB) on the same PNG bytes, one image per thread, at 1 thread
+    and at nproc threads; each sample sized to about args.cpu_seconds of wall."""
+    import ikutil
+    orc = ikutil.Oracle()
+    L = orc.lib
+    L.iko_png_decode.restype = ctypes.c_long
+    L.iko_png_decode.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ikutil.u8p),
+                                 ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                 ctypes.POINTER(ctypes.c_uint32)]
+    f, fmt, O = FILTERS[args.filter], FORMATS["webp"], args.out
+
+    def one(k):
+        data = pngs[k % len(pngs)]
+        px = ikutil.u8p()
+        w, h, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        n = L.iko_png_decode(data, len(data), ctypes.byref(px), ctypes.byref(w), ctypes.byref(h), ctypes.byref(c))
+        assert n > 0, n
+        out = ikutil.u8p()
+        ow, oh = ctypes.c_uint32(), ctypes.c_uint32()
+        m = L.iko_transform_u8(px, w.value, h.value, c.value, O, O, f, fmt, args.quality, ctypes.byref(out),
+                               ctypes.byref(ow), ctypes.byref(oh))
+        L.iko_free(px)
+        assert m > 0 and (ow.value, oh.value) == (O, O)
+        L.iko_free(out)
+
+    one(0)
+    t0 = time.perf_counter()
+    one(1)
+    t1 = time.perf_counter() - t0
+    n1 = max(2, int(args.cpu_seconds / max(t1, 1e-3)))
+    t0 = time.perf_counter()
+    for k in range(n1):
+        one(k)
+    w1 = time.perf_counter() - t0
+    nproc = os.cpu_count() or 1
+    # nproc threads, each doing `per` images: ~cpu_seconds if the cores scaled perfectly
+    per = max(1, int(round(args.cpu_seconds / max(t1, 1e-3))))
+    per = min(per, 4)
+    done = [0]
+    lock = threading.Lock()
+
+    def worker(t):
+        for k in range(per):
+            one(t * per + k)
+            with lock:
+                done[0] += 1
+
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(nproc)]
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    wn = time.perf_counter() - t0
+    S = args.size
+    return {
+        "value": round(done[0] * S * S / wn / 1e6, 2),
+        "unit": "MPix/s",
+        "cores": nproc,
+        "kind": "port",
+        "sample": f"{done[0]} x {S}x{S} RGBA8 PNG (host memory) -> oracle PNG decode (CRC, libdeflate inflate, "
+                  f"unfilter) -> image 0.25.8 resize {O}x{O} {args.filter} -> libwebp q{args.quality}; one image per "
+                  f"thread, {nproc} threads, {wn:.1f}s wall",
+        "value_1core": round(n1 * S * S / w1 / 1e6, 2),
+        "sample_1core": f"{n1} images on 1 thread, {w1:.1f}s wall",
+        "host": host_info(),
+    }
 
 
 def main():
@@ -258,201 +211,170 @@ def main():
         dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
-    from imagekit import _lib
+    import ikutil
+    from imagekit import _lib, transform_batch
     lib = _lib.load()
     if lib.ik_init(local) != 0:
         raise SystemExit(f"ik_init({local}) failed: {_lib.last_error()}")
-
-    S, O, B = args.size, args.out, args.batch
-    f = FILTERS[args.filter]
-    pitch = S * 4
-    # inputs resident in HBM before the timed region: 4 distinct synthetic frames tiled over the batch
-    NB = max(B, 0 if (args.device_only or args.no_alt_encoder or args.format != "webp") else args.alt_batch)
-    distinct = [synth_rgba(S, S, seed=sd) for sd in shard_seeds(rank, NB)]
-    src = torch.empty((NB, S, pitch), dtype=torch.uint8, device=f"cuda:{local}")
-    for i in range(NB):  # distinct frames over PCIe once, the rest device to device
-        if i < len(distinct):
-            src[i].copy_(torch.from_numpy(distinct[i].reshape(S, pitch)))
-        else:
-            src[i].copy_(src[i % len(distinct)])
-    torch.cuda.synchronize()
-
-    pipe = ctypes.c_void_p()
-    fmt = FORMATS[args.format]
-    if lib.ik_pipeline_create(S, S, 4, O, O, f, fmt, args.quality, B, args.threads, ctypes.byref(pipe)):
-        raise SystemExit(f"pipeline: {_lib.last_error()}")
-    if fmt == 1 and lib.ik_pipeline_set_webp_encoder(pipe, ENCODERS[args.webp_encoder]):
-        raise SystemExit(f"webp encoder: {_lib.last_error()}")
-    out_cap = B * O * O * 4 + (1 << 20)
-    out = np.empty(out_cap, np.uint8)
-    sizes = (ctypes.c_size_t * B)()
-
-    src_ptr = ctypes.c_void_p(src.data_ptr())
-    n_done = ctypes.c_uint32()
-
-    def kernel_ms():
-        return tuple(lib.ik_pipeline_kernel_ms(pipe, k) for k in range(4))
-
-    def submit():
-        if lib.ik_pipeline_submit(pipe, src_ptr, pitch, S * pitch, B):
-            raise SystemExit(f"pipeline submit: {_lib.last_error()}")
-
-    def collect():
-        if lib.ik_pipeline_collect(pipe, out.ctypes.data, out_cap, sizes, ctypes.byref(n_done)):
-            raise SystemExit(f"pipeline collect: {_lib.last_error()}")
-        assert n_done.value == B
-        return kernel_ms()
-
-    def run_steps(k):
-        """k batches; with --sync one run per batch, else two in flight (the host
-        stage of batch i overlaps the device stage of batch i+1)"""
-        if args.device_only:
-            res = []
-            for _ in range(k):
-                if lib.ik_pipeline_run_device(pipe, src_ptr, pitch, S * pitch, B):
-                    raise SystemExit(f"pipeline run: {_lib.last_error()}")
-                res.append(kernel_ms())
-            return res
-        if args.sync:
-            res = []
-            for _ in range(k):
-                submit()
-                res.append(collect())
-            return res
-        res = []
-        submit()
-        for _ in range(k - 1):
-            submit()
-            res.append(collect())
-        res.append(collect())
-        return res
-
-    if args.warmup:
-        run_steps(args.warmup)
+    dev = f"cuda:{local}"
 
     def barrier():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
 
+    S, O, B = args.size, args.out, args.batch
+    f = FILTERS[args.filter]
+    frames = [ikutil.synth(S, S, 4, seed=sd, pattern="S") for sd in shard_seeds(rank, args.distinct)]
+    pngs = make_pngs(frames)
+    reqs = [pngs[i % len(pngs)] for i in range(B)]
+
+    # ---- headline: PNG bytes in host memory -> WebP bytes in host memory ----
+    timing = (ctypes.c_double * 10)()
+    stage_ms = []
+
+    def step():
+        res = transform_batch(reqs, [(O, O)] * B, [FORMATS["webp"]] * B, [args.quality] * B, filter=f,
+                              threads=args.threads)
+        lib.ik_png_last_timing(timing, 10)
+        stage_ms.append(list(timing))
+        return res
+
+    for _ in range(args.warmup):
+        step()
+    stage_ms.clear()
     barrier()
     t0 = time.perf_counter()
-    kms = run_steps(args.steps)
+    for _ in range(args.steps):
+        res = step()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     barrier()
-    elapsed = reduce_max(elapsed, dist, f"cuda:{local}")
+    elapsed = reduce_max(elapsed, dist, dev)
+    assert all(r is not None and r[:4] == b"RIFF" for r in res)
+    value = aggregate_mpix(world, B * args.steps, S, elapsed)
+    st = np.mean(np.array(stage_ms), axis=0)
+    png_stages = {k: round(float(v), 3) for k, v in zip(PNG_STAGES, st[:6])}
+    png_stages.update({"decode_wall_ms": round(float(st[6]), 3), "count_rounds": float(st[7]),
+                       "decoder_lanes": int(st[8]), "streams_on_gpu": int(st[9])})
+    out_bytes = sum(len(r) for r in res) // B
+    in_bytes = sum(len(p) for p in reqs) // B
 
-    if not args.device_only:
-        assert (bytes(out[:2]) in (b"RI", b"\xff\xd8") or bytes(out[4:8]) == b"ftyp") and all(s > 0 for s in sizes)
-    resize_ms = float(np.mean([k[0] for k in kms]))
-    colour_ms = float(np.mean([k[1] for k in kms]))
-    vp8_ms = float(np.mean([k[2] for k in kms]))
-    host_ms = float(np.mean([k[3] for k in kms]))
-    out_bytes = int(sum(sizes))
+    # ---- device kernels of the step: algorithmic bytes per launch ----
+    raw = (S * 4 + 1) * S
+    kern = {
+        # compressed stream read, u16 symbols written (count: read only)
+        "k_png_inflate<emit>": (png_stages["emit"], B * (in_bytes + 2 * raw)),
+        "k_png_inflate<count>": (png_stages["count"], B * in_bytes),
+        "k_png_resolve": (png_stages["resolve"], B * (2 * raw + 4 * S * S)),
+        "k_png_unfilter": (png_stages["unfilter"], B * (2 * 4 * S * S)),
+        "k_png_find": (png_stages["find"], B * in_bytes),
+    }
+    dom = max(kern, key=lambda k: kern[k][0])
+    dms, dbytes = kern[dom]
+    roof = {"bound": "hbm", "achieved": round(dbytes / (dms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(dbytes / (dms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None, "kernel": dom,
+            "kernel_ms": round(dms, 4), "bytes_per_launch": dbytes,
+            "note": "entropy decoding is bound by serial per-lane decode latency, not HBM; bytes = compressed in "
+                    "+ u16 symbols out"}
+    kernels = {k: {"ms": round(v[0], 4), "GBps": round(v[1] / max(v[0], 1e-6) / 1e6, 1)} for k, v in kern.items()}
 
-    # the other WebP encoder end to end on frames of the same batch (a few steps,
-    # its own batch size: the GPU VP8 wavefront is latency-bound, so it wants more
-    # images per launch)
-    alt_enc = {}
-    if not args.device_only and not args.no_alt_encoder and fmt == 1:
-        other = "gpu" if args.webp_encoder == "libwebp" else "libwebp"
-        AB = args.alt_batch
-        p3 = ctypes.c_void_p()
-        if lib.ik_pipeline_create(S, S, 4, O, O, f, 1, args.quality, AB, args.threads, ctypes.byref(p3)) == 0:
-            if lib.ik_pipeline_set_webp_encoder(p3, ENCODERS[other]) == 0:
-                acap = AB * O * O * 4 + (1 << 20)
-                aout = np.empty(acap, np.uint8)
-                asz = (ctypes.c_size_t * AB)()
-                nd = ctypes.c_uint32()
+    # ---- extras: HBM-resident pipeline (old headline) and JPEG-source leg ----
+    hbm = {}
+    roof_resize = None
+    jpg = {}
+    if not args.no_extras:
+        HB = args.hbm_batch
+        pitch = S * 4
+        src = torch.empty((HB, S, pitch), dtype=torch.uint8, device=dev)
+        for i in range(HB):
+            if i < len(frames):
+                src[i].copy_(torch.from_numpy(frames[i].reshape(S, pitch)))
+            else:
+                src[i].copy_(src[i % len(frames)])
+        torch.cuda.synchronize()
+        pipe = ctypes.c_void_p()
+        if lib.ik_pipeline_create(S, S, 4, O, O, f, FORMATS["webp"], args.quality, HB, args.threads,
+                                  ctypes.byref(pipe)):
+            raise SystemExit(f"pipeline: {_lib.last_error()}")
+        cap = HB * O * O * 4 + (1 << 20)
+        out = np.empty(cap, np.uint8)
+        sizes = (ctypes.c_size_t * HB)()
+        nd = ctypes.c_uint32()
+        sp = ctypes.c_void_p(src.data_ptr())
+        km = []
 
-                def asub():
-                    assert lib.ik_pipeline_submit(p3, src_ptr, pitch, S * pitch, AB) == 0, _lib.last_error()
+        def sub():
+            assert lib.ik_pipeline_submit(pipe, sp, pitch, S * pitch, HB) == 0, _lib.last_error()
 
-                def acol():
-                    assert lib.ik_pipeline_collect(p3, aout.ctypes.data, acap, asz, ctypes.byref(nd)) == 0, \
-                        _lib.last_error()
-                    return lib.ik_pipeline_kernel_ms(p3, 2), lib.ik_pipeline_kernel_ms(p3, 3)
+        def col():
+            assert lib.ik_pipeline_collect(pipe, out.ctypes.data, cap, sizes, ctypes.byref(nd)) == 0, _lib.last_error()
+            km.append([lib.ik_pipeline_kernel_ms(pipe, k) for k in range(4)])
 
-                asub()
-                acol()
-                barrier()
-                t1 = time.perf_counter()
-                asub()
-                ak = []
-                for _ in range(args.alt_steps - 1):
-                    asub()
-                    ak.append(acol())
-                ak.append(acol())
-                barrier()
-                te = reduce_max(time.perf_counter() - t1, dist, f"cuda:{local}")
-                alt_enc = {"encoder": other, "batch_per_gpu": AB, "steps": args.alt_steps,
-                           "value": round(aggregate_mpix(world, AB, args.alt_steps, S, te), 2),
-                           "ms_per_step": round(te / args.alt_steps * 1e3, 3),
-                           "vp8_kernel_ms": round(float(np.mean([k[0] for k in ak])), 4),
-                           "host_stage_ms": round(float(np.mean([k[1] for k in ak])), 3),
-                           "output_bytes_per_image": int(sum(asz)) // AB}
-            lib.ik_pipeline_destroy(p3)
-    bytes_per_img = 4 * S * S + 4 * O * O
-    achieved = B * bytes_per_img / (resize_ms * 1e-3) / 1e9
-    value = aggregate_mpix(world, B, args.steps, S, elapsed)
-
-    # the other filter's kernel on the same batch (device-only), for DESIGN.md
-    alt = {}
-    alt_name = "lanczos3" if args.filter != "lanczos3" else "triangle"
-    p2 = ctypes.c_void_p()
-    if lib.ik_pipeline_create(S, S, 4, O, O, FILTERS[alt_name], 1, args.quality, B, 1, ctypes.byref(p2)) == 0:
-        ms = []
-        for i in range(6):
-            lib.ik_pipeline_run_device(p2, ctypes.c_void_p(src.data_ptr()), pitch, S * pitch, B)
-            if i >= 2:
-                ms.append(lib.ik_pipeline_kernel_ms(p2, 0))
-        m = float(np.mean(ms))
-        alt = {"filter": alt_name, "resize_ms": round(m, 4),
-               "achieved_GBps": round(B * bytes_per_img / (m * 1e-3) / 1e9, 1)}
-        lib.ik_pipeline_destroy(p2)
-    # the FMA resize mode (within 1 LSB; the default stays bit-exact) on both filters, device-only
-    fma = {}
-    if lib.ik_set_resize_mode(1) == 0:
-        for name in (args.filter, alt_name):
-            p4 = ctypes.c_void_p()
-            if lib.ik_pipeline_create(S, S, 4, O, O, FILTERS[name], 1, args.quality, B, 1, ctypes.byref(p4)) == 0:
-                ms = []
-                for i in range(6):
-                    lib.ik_pipeline_run_device(p4, ctypes.c_void_p(src.data_ptr()), pitch, S * pitch, B)
-                    if i >= 2:
-                        ms.append(lib.ik_pipeline_kernel_ms(p4, 0))
-                m = float(np.mean(ms))
-                fma[name] = {"resize_ms": round(m, 4), "achieved_GBps": round(B * bytes_per_img / (m * 1e-3) / 1e9, 1)}
-                lib.ik_pipeline_destroy(p4)
-        lib.ik_set_resize_mode(0)
-    lib.ik_pipeline_destroy(pipe)
-
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_resize.json")
-    if os.path.exists(pmc):
-        try:
-            d = json.load(open(pmc))
-            key = f"{args.filter}_{S}_{O}_b{B}"
-            if key in d:
-                traffic = d[key]["hbm_bytes_per_launch"]
-        except Exception:
-            traffic = None
-
-    png = jpg = {}
-    if args.png_images > 0 and not args.device_only and args.format != "avif":
-        png = png_leg(args, distinct, world, dist, f"cuda:{local}", barrier)
-        jpg = png_leg(args, distinct, world, dist, f"cuda:{local}", barrier, kind="jpeg")
+        sub()
+        col()
+        km.clear()
+        barrier()
+        t1 = time.perf_counter()
+        sub()
+        for _ in range(args.hbm_steps - 1):
+            sub()
+            col()
+        col()
+        barrier()
+        te = reduce_max(time.perf_counter() - t1, dist, dev)
+        lib.ik_pipeline_destroy(pipe)
+        kmm = np.mean(np.array(km), axis=0)
+        rb = HB * (4 * S * S + 4 * O * O)
+        hbm = {"workload": f"{S}x{S} RGBA8 frames already in HBM -> resize {O}x{O} {args.filter} -> WebP q{args.quality} "
+                           "(libwebp), bytes to host; two batches in flight",
+               "value": round(aggregate_mpix(world, HB * args.hbm_steps, S, te), 2), "unit": "MPix/s",
+               "ms_per_step": round(te / args.hbm_steps * 1e3, 3), "batch_per_gpu": HB,
+               "resize_ms": round(float(kmm[0]), 4), "colour_ms": round(float(kmm[1]), 4),
+               "host_stage_ms": round(float(kmm[3]), 3)}
+        achieved = rb / (kmm[0] * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_resize.json")
+        if os.path.exists(pmc):
+            try:
+                d = json.load(open(pmc))
+                key = f"{args.filter}_{S}_{O}_b{HB}"
+                traffic = d[key]["hbm_bytes_per_launch"] if key in d else None
+            except Exception:
+                traffic = None
+        roof_resize = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                       "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "kernel": "k_resize_fused",
+                       "kernel_ms": round(float(kmm[0]), 4), "bytes_per_launch": rb, "batch": HB}
+        del src
+        torch.cuda.empty_cache()
+        # JPEG sources (restart marker per MCU row) through the same batch call
+        if args.jpeg_images > 0:
+            from PIL import Image
+            jp = []
+            for im in frames[:2]:
+                b = io.BytesIO()
+                Image.fromarray(np.ascontiguousarray(im[..., :3]), "RGB").save(b, format="JPEG", quality=90,
+                                                                             restart_marker_rows=1)
+                jp.append(b.getvalue())
+            n = args.jpeg_images
+            run = lambda k: transform_batch([jp[i % 2] for i in range(k)], [(O, O)] * k, [1] * k,
+                                            [args.quality] * k, filter=f, threads=args.threads)
+            run(4)
+            barrier()
+            t1 = time.perf_counter()
+            run(n)
+            te = reduce_max(time.perf_counter() - t1, dist, dev)
+            jpg = {"source": "JPEG q90 4:2:0, RSTn per MCU row (GPU entropy decoding)", "images_per_gpu": n,
+                   "bytes_per_source_image": sum(len(p) for p in jp) // 2,
+                   "value": round(aggregate_mpix(world, n, S, te), 2), "unit": "MPix/s"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, distinct[0])
+        cpu = cpu_baseline(args, pngs)
 
     if rank == 0:
         line = {
-            "metric": METRIC if args.format == "webp" else
-                      f"transform MPix/s (resize+encode) {S}²→{O}² {args.filter} {args.format.upper()} q{args.quality} "
-                      f"(configs[{2 if args.format == 'jpeg' else 4}] shape)",
+            "metric": METRIC,
             "value": round(value, 2),
             "unit": "MPix/s",
             "n_gpus": world,
@@ -462,40 +384,30 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": f"{S}x{S} RGBA8 frames resident in HBM -> resize_image {O}x{O} "
-                            f"({args.filter}) -> encode_image {args.format} q{args.quality}; bytes to host",
-                "batch_per_gpu": B, "filter": args.filter, "format": args.format,
-                "quality": args.quality, "host_threads_per_gpu": args.threads,
-                "webp_encoder": args.webp_encoder,
+                "workload": f"{S}x{S} RGBA8 synthetic frames as PNG (zlib level 6) in host memory -> "
+                            f"ik_transform_batch: decode_image (GPU inflate + unfilter) -> resize_image {O}x{O} "
+                            f"({args.filter}) -> encode_image webp q{args.quality} (libwebp) -> WebP bytes in host memory",
+                "batch_per_gpu": B, "filter": args.filter, "format": "webp", "quality": args.quality,
+                "host_threads_per_gpu": args.threads, "png_bytes_per_image": in_bytes,
+                "webp_bytes_per_image": out_bytes,
                 "libwebp": "%d.%d.%d" % (lib.ik_libwebp_version() >> 16, (lib.ik_libwebp_version() >> 8) & 255,
                                          lib.ik_libwebp_version() & 255),
-                "device_only": bool(args.device_only), "batches_in_flight": 1 if args.sync else 2, "parallelism": f"images sharded, {world} rank(s)",
+                "parallelism": f"images sharded, {world} rank(s)",
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": traffic,
-                "kernel": "k_resize_fused",
-                "kernel_ms": round(resize_ms, 4),
-                "bytes_per_launch": B * bytes_per_img,
-            },
-            "colour_kernel_ms": round(colour_ms, 4),
-            "vp8_kernel_ms": round(vp8_ms, 4),
-            "host_stage_ms": round(host_ms, 3),
-            "output_bytes_per_image": out_bytes // B,
-            "alt_webp_encoder": alt_enc,
-            "alt_filter_kernel": alt,
-            "resize_fma_mode": fma,
-            "decode_inclusive_png": png,
+            "roofline": roof,
+            "roofline_resize": roof_resize,
+            "png_decode_stages_ms": png_stages,
+            "kernels": kernels,
+            "hbm_resident": hbm,
             "decode_inclusive_jpeg": jpg,
             "cpu_baseline": cpu,
         }
+        if cpu:
+            line["ratio_vs_cpu_allcore"] = round(value / cpu["value"], 2)
+            line["ratio_vs_cpu_1core"] = round(value / cpu["value_1core"], 2)
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()

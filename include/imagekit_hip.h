@@ -100,6 +100,18 @@ int ik_decode(const uint8_t *bytes, size_t len, ik_image **out, int *fmt_out);
 int ik_decode_batch(const uint8_t *const *bytes, const size_t *lens, uint32_t n, ik_image **outs,
                     int *fmts, int *status);
 
+/* PNG decoding on the GPU (ik_decode / ik_decode_batch / ik_transform*): streams
+ * whose filtered image data is at least min_raw_bytes are inflated and unfiltered
+ * on the GPU (parallel DEFLATE over block-start candidates, row-wavefront
+ * unfilter); smaller ones, palette / tRNS / interlaced / 16-bit streams and any
+ * the GPU finds inconsistent use the host decoder.  -1 = host decoder only.
+ * Default 256 KiB (IK_PNG_GPU_MIN; IK_PNG_GPU=0 = off). */
+int ik_set_png_gpu_min(long long min_raw_bytes);
+/* the calling thread's last GPU PNG batch: [0] host parse + staging ms, device ms
+ * of [1] block search [2] count passes [3] emit pass [4] resolve [5] unfilter,
+ * [6] wall ms, [7] count rounds, [8] decoder lanes, [9] streams on the GPU */
+int ik_png_last_timing(double *out, int n);
+
 /* resize_image (src/transform.rs:62-90).  w/h < 0 mean None.  Both None returns
  * the input unchanged (*out == img); otherwise a new image (img is not freed:
  * the Rust shim drops its by-value argument).  filter: IK_FILTER_* (Lanczos3 in

@@ -88,6 +88,11 @@ long iko_transform_u8(const uint8_t *src, uint32_t W, uint32_t H, uint32_t C, in
                       int64_t h_opt, int filter, int fmt, int quality, uint8_t **out,
                       uint32_t *ow, uint32_t *oh);
 
+/* decode_image on a PNG (image 0.25.8 -> png 0.18, EXPAND) for non-interlaced
+ * 8-bit colour types 0/2/4/6: CRC-checked chunks, inflate, unfilter.  Returns the
+ * pixel byte count (pixels in *out, iko_free) or < 0.  png_dec.c. */
+long iko_png_decode(const uint8_t *png, size_t n, uint8_t **out, uint32_t *w, uint32_t *h, uint32_t *c);
+
 void iko_free(void *p);
 
 #ifdef __cplusplus

@@ -111,11 +111,15 @@ bool inflate_exact_libdeflate(const std::vector<uint8_t>& in, std::vector<uint8_
     return d.zlib_decompress(h.p, in.data(), in.size(), out.data(), out.size(), &got) == 0 && got == out.size();
 }
 
-uint32_t chunk_crc(const uint8_t* type, const uint8_t* data, size_t len) {
+}  // namespace
+
+uint32_t png_chunk_crc(const uint8_t* type, const uint8_t* data, size_t len) {
     const Deflate& d = deflate_api();
     if (d.ok && d.crc32) return d.crc32(d.crc32(0, type, 4), data, len);
     return (uint32_t)crc32(crc32(0, type, 4), data, len);
 }
+
+namespace {
 
 // Per-thread compressed/filtered buffers, kept between decodes (first-touch page
 // faults cost as much as the unfiltering); released after images over 128 MiB.
@@ -184,7 +188,7 @@ int decode_png(const uint8_t* b, size_t n, uint32_t& W, uint32_t& H, uint32_t& C
         const uint8_t* type = b + pos + 4;
         const uint8_t* data = b + pos + 8;
         const uint32_t crc = be32(data + len);
-        if (chunk_crc(type, data, len) != crc)
+        if (png_chunk_crc(type, data, len) != crc)
             return fail(IK_ERR_TRANSFORM, "Format error decoding Png: CRC error");
         if (!std::memcmp(type, "IHDR", 4)) {
             if (len != 13) return fail(IK_ERR_TRANSFORM, "Format error decoding Png: bad IHDR");

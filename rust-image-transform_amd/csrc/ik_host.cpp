@@ -619,7 +619,13 @@ static int decode_one(const uint8_t* bytes, size_t len, ik_image** out, int* fmt
     int st;
     ik_image* img = nullptr;
     switch (f) {
-    case Sniffed::Png: st = decode_png(bytes, len, w, h, c, px); break;
+    case Sniffed::Png: {  // GPU inflate + unfilter when the stream allows, else the host decoder
+        std::string msg;
+        const uint8_t* const bp[1] = {bytes};
+        st = decode_png_batch(bp, &len, 1, &img, &st, &msg);
+        if (st) return fail(st, "%s", msg.c_str());
+        break;
+    }
     case Sniffed::Jpeg: st = decode_jpeg_device(bytes, len, &img); break;
     case Sniffed::WebP: st = decode_webp(bytes, len, w, h, c, px); break;
     default:
@@ -645,21 +651,37 @@ static std::string last_error_str() { return t_err; }
 // message (the decoder's own, as TransformError(e.to_string()) carries it)
 int decode_batch_dev(const uint8_t* const* bytes, const size_t* lens, uint32_t n, ik_image** outs, int* fmts,
                      int* st, std::string* msg, int threads) {
-    std::vector<const uint8_t*> jb;
-    std::vector<size_t> jl;
-    std::vector<uint32_t> ji, other;
+    std::vector<const uint8_t*> jb, pb;
+    std::vector<size_t> jl, pl;
+    std::vector<uint32_t> ji, pi, other;
     for (uint32_t i = 0; i < n; ++i) {
         outs[i] = nullptr;
         st[i] = IK_OK;
         if (fmts) fmts[i] = -1;
         if (!bytes[i] && lens[i]) { st[i] = fail(IK_ERR_INVALID, "null bytes"); msg[i] = t_err; continue; }
-        if (guess_format(bytes[i], lens[i]) == Sniffed::Jpeg) {
+        const Sniffed f = guess_format(bytes[i], lens[i]);
+        if (f == Sniffed::Jpeg) {
             jb.push_back(bytes[i]);
             jl.push_back(lens[i]);
             ji.push_back(i);
             if (fmts) fmts[i] = IK_FORMAT_JPEG;
+        } else if (f == Sniffed::Png) {
+            pb.push_back(bytes[i]);
+            pl.push_back(lens[i]);
+            pi.push_back(i);
         } else {
             other.push_back(i);
+        }
+    }
+    if (!pi.empty()) {  // every PNG of the batch through one set of GPU launches
+        std::vector<ik_image*> po(pi.size(), nullptr);
+        std::vector<int> ps(pi.size(), IK_OK);
+        std::vector<std::string> pm(pi.size());
+        decode_png_batch(pb.data(), pl.data(), (int)pi.size(), po.data(), ps.data(), pm.data());
+        for (size_t k = 0; k < pi.size(); ++k) {
+            outs[pi[k]] = po[k];
+            st[pi[k]] = ps[k];
+            msg[pi[k]] = pm[k];
         }
     }
     parallel_for((int)other.size(), threads, [&](int k) {  // PNG / WebP / unknown: host decoders, in parallel

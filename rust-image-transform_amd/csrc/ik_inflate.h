@@ -1,0 +1,548 @@
+// ik_inflate.h -- DEFLATE (RFC 1951) decoding core shared by the GPU PNG decoder
+// (ik_png.hip) and its host-side model (ik_png_model.cpp, CPU tests only).
+//
+// decode_image on a PNG (reference src/transform.rs:31 -> png 0.18 via image
+// 0.25.8) spends nearly all its time in zlib inflate of the IDAT stream.  The
+// stream is one serial bit sequence, so the GPU decoder cuts it into chunks and
+// decodes them in parallel, rapidgzip-style:
+//
+//  1. find:  in every chunk, the first bit offset where a *dynamic* block header
+//            parses and builds valid Huffman codes (a strong filter: BTYPE, HLIT/
+//            HDIST ranges, a complete code-length code, code lengths that decode
+//            to exactly HLIT+HDIST entries, complete literal/distance codes with an
+//            end-of-block code).
+//  2. count: one decoder per candidate start decodes whole blocks until it
+//            reaches the next candidate; it must land exactly on it (else the
+//            candidate was not a real block start and is dropped).  Output
+//            lengths -> prefix sums -> each decoder's output offset.
+//  3. emit:  decode again, writing u16 symbols: a literal byte (< 256), or for a
+//            back-reference into bytes before the decoder's own output (written
+//            by its predecessor) a marker 0x8000 | index into the 32 KiB window
+//            that precedes the decoder's first output byte.  Markers copied
+//            within a decoder keep their value (they name an absolute position).
+//  4. resolve (in the PNG unfilter pass): a marker is replaced by the byte at its
+//            window position, following chains through earlier decoders.
+//
+// Everything here is written once for both compilers: IK_HD functions run in the
+// HIP kernels and in the CPU model that the CPU test suite checks against zlib.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define IK_HD __host__ __device__ __forceinline__
+#define IK_HD_COLD __host__ __device__ __attribute__((noinline))
+#else
+#define IK_HD inline
+#define IK_HD_COLD inline
+#endif
+
+namespace ik {
+namespace infl {
+
+constexpr int kLitRoot = 9;    // root bits of the literal/length table
+constexpr int kDistRoot = 7;   // root bits of the distance table
+constexpr int kLitRootN = 1 << kLitRoot;
+constexpr int kDistRootN = 1 << kDistRoot;
+constexpr int kLitSub = 512;   // subtable entries for codes longer than the root (zlib's bound: 852 - 512)
+constexpr int kDistSub = 512;
+constexpr int kWindow = 32768;
+
+// table entry (u16): bit 15 = 0: symbol in bits 0..8, code length in bits 9..12
+//                    bit 15 = 1: subtable at index bits 0..10, index bits in 11..14
+IK_HD uint16_t ent(int sym, int len) { return (uint16_t)(sym | (len << 9)); }
+
+// 32-bit little-endian words of the stream; pos = absolute bit position of the
+// next bit.  The buffer must hold >= 4 zero words past the last stream word.
+struct Bits {
+    const uint32_t* w;
+    uint64_t buf;
+    int n;          // valid bits in buf
+    uint64_t wi;    // next word index to load
+    uint64_t wend;  // words that may be read (the stream and its zero padding)
+    uint32_t nxt;   // prefetched word wi
+    IK_HD void init(const uint32_t* words, uint64_t bit, uint64_t nwords) {
+        w = words;
+        wend = nwords;
+        wi = bit >> 5;
+        const uint32_t first = wi < wend ? w[wi] : 0u;
+        n = 32 - (int)(bit & 31);
+        buf = (uint64_t)(first >> (bit & 31));
+        ++wi;
+        nxt = wi < wend ? w[wi] : 0u;
+    }
+    IK_HD uint64_t pos() const { return (wi << 5) - (uint64_t)n; }
+    IK_HD void refill() {
+        if (n < 32) {
+            buf |= (uint64_t)nxt << n;
+            n += 32;
+            ++wi;
+            nxt = wi < wend ? w[wi] : 0u;  // never past the buffer, whatever a corrupt stream says
+        }
+    }
+    IK_HD uint32_t peek(int k) const { return (uint32_t)buf & ((1u << k) - 1u); }
+    IK_HD void drop(int k) {
+        buf >>= k;
+        n -= k;
+    }
+    IK_HD uint32_t get(int k) {  // k <= 25 after a refill
+        refill();
+        const uint32_t v = peek(k);
+        drop(k);
+        return v;
+    }
+};
+
+// canonical-code bookkeeping of one code (lengths 0..15)
+struct CodeInfo {
+    uint16_t count[16];
+    int max;
+};
+
+// RFC 1951 3.2.2 / zlib inftrees: 0 = ok, -1 = oversubscribed or incomplete
+// (incomplete is accepted only for a code of at most one length-1... i.e. max <= 1
+// as zlib does for literal/distance codes; `codes` = the code-length code, which
+// must be complete)
+IK_HD_COLD int code_check(const uint8_t* lens, int n, bool codes, CodeInfo& ci) {
+    for (int i = 0; i < 16; ++i) ci.count[i] = 0;
+    for (int i = 0; i < n; ++i) ci.count[lens[i]]++;
+    ci.max = 0;
+    for (int l = 15; l >= 1; --l)
+        if (ci.count[l]) { ci.max = l; break; }
+    if (ci.max == 0) return codes ? -1 : 0;  // no codes: only allowed for literal/distance (distance-free block)
+    int left = 1;
+    for (int l = 1; l <= 15; ++l) {
+        left <<= 1;
+        left -= ci.count[l];
+        if (left < 0) return -1;  // oversubscribed
+    }
+    if (left > 0 && (codes || ci.max != 1)) return -1;  // incomplete
+    return 0;
+}
+
+IK_HD uint32_t rev_bits(uint32_t v, int k) {
+    uint32_t r = 0;
+    for (int i = 0; i < k; ++i) {
+        r = (r << 1) | (v & 1u);
+        v >>= 1;
+    }
+    return r;
+}
+
+// Build the two-level lookup of a canonical code (lengths[n]).  root: 2^rb
+// entries; sub: subtables (capacity sub_cap).  Returns 0, or -1 if the
+// subtables would not fit.  Entries for unused root slots (incomplete code) are
+// set to length 0, which the decoder treats as an invalid code.
+template <class RootT, class SubT>
+IK_HD_COLD int build_table(const uint8_t* lens, int n, const CodeInfo& ci, int rb, RootT root, SubT sub, int sub_cap) {
+    const int rootn = 1 << rb;
+    for (int i = 0; i < rootn; ++i) root[i] = 0;
+    if (ci.max == 0) return 0;
+    // first canonical code of each length (RFC 1951 3.2.2; bl_count[0] counts as 0)
+    uint32_t next[16];
+    uint32_t code = 0;
+    next[0] = 0;
+    for (int l = 1; l <= 15; ++l) {
+        code = (code + (l > 1 ? ci.count[l - 1] : 0)) << 1;
+        next[l] = code;
+    }
+    // remaining codes per length (for subtable sizing, zlib's rule)
+    int remain[16];
+    for (int l = 0; l < 16; ++l) remain[l] = ci.count[l];
+    int sub_used = 0;
+    int cur_prefix = -1, cur_base = 0, cur_bits = 0;
+    // walk codes in canonical order: by length, then symbol
+    for (int l = 1; l <= 15; ++l) {
+        if (!ci.count[l]) continue;
+        for (int s = 0; s < n; ++s) {
+            if (lens[s] != l) continue;
+            const uint32_t c = next[l]++;
+            const uint32_t r = rev_bits(c, l);
+            if (l <= rb) {
+                const uint16_t e = ent(s, l);
+                for (uint32_t i = r; i < (uint32_t)rootn; i += (1u << l)) root[i] = e;
+            } else {
+                const int prefix = (int)(r & (uint32_t)(rootn - 1));
+                if (prefix != cur_prefix) {
+                    // new subtable: smallest size covering the codes that share this
+                    // prefix (zlib inftrees' `curr` computation)
+                    int curr = l - rb;
+                    int left = 1 << curr;
+                    while (curr + rb < ci.max) {
+                        left -= remain[curr + rb];
+                        if (left <= 0) break;
+                        ++curr;
+                        left <<= 1;
+                    }
+                    if (sub_used + (1 << curr) > sub_cap) return -1;
+                    cur_prefix = prefix;
+                    cur_base = sub_used;
+                    cur_bits = curr;
+                    for (int i = 0; i < (1 << curr); ++i) sub[cur_base + i] = 0;
+                    sub_used += 1 << curr;
+                    root[prefix] = (uint16_t)(0x8000 | (cur_bits << 11) | cur_base);
+                }
+                const int sl = l - rb;
+                const uint32_t hi = r >> rb;
+                const uint16_t e = ent(s, sl);
+                for (uint32_t i = hi; i < (1u << cur_bits); i += (1u << sl)) sub[cur_base + i] = e;
+            }
+            remain[l]--;
+        }
+    }
+    return 0;
+}
+
+// decode one symbol with a two-level table; returns the symbol or -1 (invalid code)
+template <class RootT, class SubT>
+IK_HD int decode_sym(Bits& b, RootT root, SubT sub, int rb) {
+    b.refill();
+    uint32_t e = root[b.peek(rb)];
+    if (e & 0x8000u) {
+        const int bits = (int)((e >> 11) & 15u);
+        const uint32_t idx = (e & 0x7FFu) + ((uint32_t)(b.buf >> rb) & ((1u << bits) - 1u));
+        const uint32_t e2 = sub[idx];
+        const int len = (int)((e2 >> 9) & 15u);
+        if (!len) return -1;
+        b.drop(rb + len);
+        return (int)(e2 & 0x1FFu);
+    }
+    const int len = (int)((e >> 9) & 15u);
+    if (!len) return -1;
+    b.drop(len);
+    return (int)(e & 0x1FFu);
+}
+
+IK_HD int len_base(int s) {  // length symbols 257..285
+    // RFC 1951 3.2.5
+    const int i = s - 257;
+    if (i < 8) return 3 + i;
+    if (i == 28) return 258;
+    const int e = (i - 4) >> 2;
+    return ((4 + ((i - 4) & 3)) << e) + 3;
+}
+IK_HD int len_extra(int s) {
+    const int i = s - 257;
+    if (i < 8 || i == 28) return 0;
+    return (i - 4) >> 2;
+}
+IK_HD int dist_base(int d) {  // distance symbols 0..29
+    if (d < 4) return 1 + d;
+    const int e = (d - 2) >> 1;
+    return ((2 + (d & 1)) << e) + 1;
+}
+IK_HD int dist_extra(int d) { return d < 4 ? 0 : (d - 2) >> 1; }
+
+// Parse a dynamic block header at b (after BFINAL/BTYPE) into code lengths,
+// validating like zlib.  lens: 286 + 30 entries (literal/length then distance).
+// Returns 0 or -1.
+IK_HD_COLD int parse_dynamic(Bits& b, uint8_t* lens, int& nlen, int& ndist, CodeInfo& lci, CodeInfo& dci) {
+    const int hlit = (int)b.get(5), hdist = (int)b.get(5), hclen = (int)b.get(4);
+    nlen = hlit + 257;
+    ndist = hdist + 1;
+    if (nlen > 286 || ndist > 30) return -1;
+    const int ncode = hclen + 4;
+    const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+    uint8_t cl[19];
+    for (int i = 0; i < 19; ++i) cl[i] = 0;
+    for (int i = 0; i < ncode; ++i) cl[order[i]] = (uint8_t)b.get(3);
+    CodeInfo cci;
+    if (code_check(cl, 19, true, cci)) return -1;
+    // code-length code: lengths <= 7, decode with a direct 7-bit table
+    uint8_t ctab_sym[128], ctab_len[128];
+    {
+        uint32_t next[8];
+        uint32_t c = 0;
+        for (int l = 1; l <= 7; ++l) {
+            c = (c + (l > 1 ? cci.count[l - 1] : 0)) << 1;
+            next[l] = c;
+        }
+        for (int i = 0; i < 128; ++i) ctab_len[i] = 0;
+        for (int l = 1; l <= 7; ++l)
+            for (int s = 0; s < 19; ++s) {
+                if (cl[s] != l) continue;
+                const uint32_t r = rev_bits(next[l]++, l);
+                for (uint32_t i = r; i < 128; i += (1u << l)) { ctab_sym[i] = (uint8_t)s; ctab_len[i] = (uint8_t)l; }
+            }
+    }
+    const int total = nlen + ndist;
+    int i = 0;
+    while (i < total) {
+        b.refill();
+        const uint32_t k = b.peek(7);
+        const int l = ctab_len[k];
+        if (!l) return -1;
+        const int s = ctab_sym[k];
+        b.drop(l);
+        if (s < 16) {
+            lens[i++] = (uint8_t)s;
+        } else {
+            int rep;
+            uint8_t v = 0;
+            if (s == 16) {
+                if (i == 0) return -1;
+                v = lens[i - 1];
+                rep = 3 + (int)b.get(2);
+            } else if (s == 17) {
+                rep = 3 + (int)b.get(3);
+            } else {
+                rep = 11 + (int)b.get(7);
+            }
+            if (i + rep > total) return -1;
+            while (rep--) lens[i++] = v;
+        }
+    }
+    if (lens[256] == 0) return -1;  // no end-of-block code
+    if (code_check(lens, nlen, false, lci)) return -1;
+    if (code_check(lens + nlen, ndist, false, dci)) return -1;
+    return 0;
+}
+
+// Fixed Huffman code lengths (RFC 1951 3.2.6)
+IK_HD_COLD void fixed_lens(uint8_t* lens) {
+    for (int i = 0; i < 144; ++i) lens[i] = 8;
+    for (int i = 144; i < 256; ++i) lens[i] = 9;
+    for (int i = 256; i < 280; ++i) lens[i] = 7;
+    for (int i = 280; i < 288; ++i) lens[i] = 8;
+    for (int i = 0; i < 30; ++i) lens[288 + i] = 5;
+}
+
+// The finder's full header check, streaming: decodes the code lengths with the
+// caller's 128-entry code-length-code table (LDS; entry = symbol | length << 5)
+// and keeps only running sums -- no length arrays -- rejecting as soon as the
+// literal/length code is oversubscribed.  Accepts exactly what parse_dynamic
+// accepts (complete codes, or a single length-1 code; an end-of-block code).
+// `bits` = the 57 bits after the 17 header bits (the code-length code lengths).
+template <class Tab>
+IK_HD bool dynamic_header_ok(const uint32_t* words, uint64_t nbits, uint64_t bit, uint32_t hdr17, uint64_t bits,
+                             Tab tab) {
+    const int nlen = (int)((hdr17 >> 3) & 31u) + 257, ndist = (int)((hdr17 >> 8) & 31u) + 1;
+    const int ncode = (int)((hdr17 >> 13) & 15u) + 4;
+    const uint8_t order[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+    uint32_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint8_t cl[19];
+    for (int i = 0; i < 19; ++i) cl[i] = 0;
+    for (int i = 0; i < ncode; ++i) {
+        cl[order[i]] = (uint8_t)((bits >> (3 * i)) & 7u);
+        cnt[cl[order[i]]]++;
+    }
+    uint32_t next[8];
+    uint32_t c = 0;
+    for (int l = 1; l <= 7; ++l) {
+        c = (c + (l > 1 ? cnt[l - 1] : 0)) << 1;
+        next[l] = c;
+    }
+    for (int l = 1; l <= 7; ++l)
+        for (int sym = 0; sym < 19; ++sym) {
+            if (cl[sym] != l) continue;
+            const uint32_t r = rev_bits(next[l]++, l);
+            for (uint32_t i = r; i < 128; i += (1u << l)) tab[i] = (uint8_t)(sym | (l << 5));
+        }
+    Bits b;
+    b.init(words, bit + 17 + 3 * (uint64_t)ncode, (nbits >> 5) + 4);
+    const int total = nlen + ndist;
+    int i = 0, prev = -1;
+    uint32_t kl = 0, kd = 0;
+    int maxl = 0, maxd = 0;
+    bool eob = false;
+    while (i < total) {
+        b.refill();
+        const uint32_t e = tab[b.peek(7)];
+        const int l = (int)(e >> 5), sym = (int)(e & 31u);
+        b.drop(l);
+        int rep = 1, val = sym;
+        if (sym == 16) {
+            if (prev < 0) return false;
+            val = prev;
+            rep = 3 + (int)b.get(2);
+        } else if (sym == 17) {
+            val = 0;
+            rep = 3 + (int)b.get(3);
+        } else if (sym == 18) {
+            val = 0;
+            rep = 11 + (int)b.get(7);
+        }
+        if (i + rep > total) return false;
+        if (val) {
+            // the run's lengths split between the literal/length and distance codes
+            const int nl = i < nlen ? (i + rep <= nlen ? rep : nlen - i) : 0;
+            const int nd = rep - nl;
+            if (nl) {
+                kl += (uint32_t)nl << (15 - val);
+                if (kl > 32768u) return false;
+                if (val > maxl) maxl = val;
+                if (i <= 256 && 256 < i + nl) eob = true;
+            }
+            if (nd) {
+                kd += (uint32_t)nd << (15 - val);
+                if (kd > 32768u) return false;
+                if (val > maxd) maxd = val;
+            }
+        }
+        i += rep;
+        prev = val;
+    }
+    if (!eob) return false;
+    if (kl != 32768u && !(maxl == 1 && kl == 16384u)) return false;
+    if (kd != 0u && kd != 32768u && !(maxd == 1 && kd == 16384u)) return false;
+    return true;
+}
+
+// Is there a plausible dynamic block header at absolute bit `bit`?  (step 1)
+IK_HD_COLD bool plausible_dynamic(const uint32_t* words, uint64_t nbits, uint64_t bit) {
+    Bits b;
+    b.init(words, bit, (nbits >> 5) + 4);
+    b.refill();
+    const uint32_t h = b.peek(17);  // BFINAL, BTYPE(2), HLIT(5), HDIST(5), HCLEN(4)
+    if (((h >> 1) & 3u) != 2u) return false;
+    if (((h >> 3) & 31u) > 29u || ((h >> 8) & 31u) > 29u) return false;
+    b.drop(3);
+    uint8_t lens[286 + 30];
+    int nlen, ndist;
+    CodeInfo lci, dci;
+    return parse_dynamic(b, lens, nlen, ndist, lci, dci) == 0;
+}
+
+
+// ---- one decoder ("lane") ------------------------------------------------------
+enum LaneStatus { kLaneOk = 0, kLaneMismatch = 1, kLaneCorrupt = 2 };
+struct LaneResult {
+    uint64_t end_bit;   // block boundary where the decoder stopped
+    uint64_t out_len;   // bytes it decoded
+    int status;         // LaneStatus
+    int final_block;    // it decoded the BFINAL block
+};
+
+// Decode whole blocks from `start` (a block boundary) until a block boundary >=
+// `stop` (exact hit: kLaneOk; passing it, or the final block before it:
+// kLaneMismatch), or through the final block when stop == ~0.  EMIT: write u16
+// symbols at out[obase + k] (literal bytes, or window markers for bytes before
+// obase, see the file comment); obase < 0 = unknown (count pass).  out_cap
+// bounds the lane's output (corrupt past it).
+template <bool EMIT, class LRoot, class LSub, class DRoot, class DSub, class Out>
+IK_HD void decode_lane(const uint32_t* words, uint64_t nbits, uint64_t start, uint64_t stop, LRoot lroot, LSub lsub,
+                       DRoot droot, DSub dsub, Out out, int64_t obase, uint64_t out_cap, LaneResult& r) {
+    Bits b;
+    b.init(words, start, (nbits >> 5) + 4);
+    const uint64_t wlimit = (nbits >> 5) + 3;  // past the stream: corrupt
+    uint64_t cnt = 0;
+    r.status = kLaneCorrupt;
+    r.final_block = 0;
+    uint8_t lens[288 + 32];
+    for (;;) {
+        const uint64_t p = b.pos();
+        if (p >= stop) {
+            r.status = p == stop ? kLaneOk : kLaneMismatch;
+            break;
+        }
+        if (p + 3 > nbits) break;  // ran off the stream without a final block
+        b.refill();
+        const uint32_t hdr = b.peek(3);
+        b.drop(3);
+        const int bfinal = (int)(hdr & 1u), btype = (int)(hdr >> 1);
+        if (btype == 0) {  // stored
+            b.drop(b.n & 7);  // to the byte boundary
+            const uint32_t len = b.get(16), nlen = b.get(16);
+            if ((len ^ 0xFFFFu) != nlen) break;
+            if (cnt + len > out_cap) break;
+            if (b.pos() + 8ull * len > nbits) break;
+            for (uint32_t i = 0; i < len; ++i) {
+                const uint32_t v = b.get(8);
+                if (EMIT) out[obase + (int64_t)cnt] = (uint16_t)v;
+                ++cnt;
+            }
+        } else if (btype == 3) {
+            break;
+        } else {
+            int nlen, ndist;
+            CodeInfo lci, dci;
+            if (btype == 2) {
+                // the header parser is out of line: hand it a copy, so the hot loop's
+                // reader stays in registers (an escaping reference would put it in scratch)
+                Bits hb = b;
+                const int prc = parse_dynamic(hb, lens, nlen, ndist, lci, dci);
+                b = hb;
+                if (prc) break;
+                // the distance lengths follow the literal/length ones: move them to
+                // 288.. (backwards: the ranges overlap when nlen + ndist > 288)
+                for (int i = ndist - 1; i >= 0; --i) lens[288 + i] = lens[nlen + i];
+            } else {
+                fixed_lens(lens);
+                nlen = 288;
+                ndist = 30;
+                code_check(lens, 288, false, lci);
+                code_check(lens + 288, 30, false, dci);
+            }
+            if (build_table(lens, nlen, lci, kLitRoot, lroot, lsub, kLitSub)) break;
+            if (build_table(lens + 288, ndist, dci, kDistRoot, droot, dsub, kDistSub)) break;
+            bool bad = false;
+            for (;;) {
+                if (b.wi > wlimit) { bad = true; break; }
+                const int sym = decode_sym(b, lroot, lsub, kLitRoot);
+                if (sym < 256) {
+                    if (sym < 0 || cnt >= out_cap) { bad = true; break; }
+                    if (EMIT) out[obase + (int64_t)cnt] = (uint16_t)sym;
+                    ++cnt;
+                    continue;
+                }
+                if (sym == 256) break;
+                if (sym > 285) { bad = true; break; }
+                const int len = len_base(sym) + (int)b.get(len_extra(sym));
+                const int ds = decode_sym(b, droot, dsub, kDistRoot);
+                if (ds < 0 || ds > 29) { bad = true; break; }
+                const int de = dist_extra(ds);
+                const int dist = dist_base(ds) + (int)(de ? b.get(de) : 0u);
+                if (cnt + (uint64_t)len > out_cap) { bad = true; break; }
+                if (obase >= 0 && (int64_t)cnt + obase < dist) { bad = true; break; }  // before the stream start
+                if (EMIT) {
+                    int64_t src = (int64_t)cnt - dist;
+                    int64_t dst = (int64_t)cnt;
+                    for (int i = 0; i < len; ++i, ++src, ++dst) {
+                        // before this decoder's first byte: a window marker (the
+                        // predecessor's byte); else a copy, markers included
+                        out[obase + dst] = src < 0 ? (uint16_t)(0x8000 | (uint32_t)(kWindow + src))
+                                                   : (uint16_t)out[obase + src];
+                    }
+                }
+                cnt += (uint64_t)len;
+            }
+            if (bad) break;
+        }
+        if (b.pos() > nbits + 64) break;  // decoded zero padding
+        if (bfinal) {
+            r.final_block = 1;
+            r.status = stop == ~0ull ? kLaneOk : kLaneMismatch;
+            break;
+        }
+    }
+    r.end_bit = b.pos();
+    r.out_len = cnt;
+}
+
+// value of the u16 stream at absolute position q after following window markers.
+// lane_obase: output offsets of the image's decoders (ascending), n of them;
+// page_lane[q >> page_shift] = the decoder that holds the page's first byte.
+// Returns -1 on a malformed chain.
+template <class U16, class Off, class Pages>
+IK_HD int resolve_at(U16 u16, Off lane_obase, int n, Pages page_lane, int page_shift, int64_t q) {
+    int lane = -1;
+    for (int guard = 0; guard < 64; ++guard) {
+        const uint32_t v = u16[q];
+        if (v < 256u) return (int)v;
+        if (!(v & 0x8000u)) return -1;
+        // the decoder that wrote position q (the first hop: its page's decoder or a
+        // later one; later hops: the same decoder or an earlier one)
+        if (lane < 0) {
+            lane = page_lane[q >> page_shift];
+            while (lane + 1 < n && (int64_t)lane_obase[lane + 1] <= q) ++lane;
+        } else {
+            while (lane > 0 && (int64_t)lane_obase[lane] > q) --lane;
+        }
+        q = (int64_t)lane_obase[lane] - kWindow + (int64_t)(v & 0x7FFFu);
+        if (q < 0) return -1;
+    }
+    return -1;
+}
+
+}  // namespace infl
+}  // namespace ik

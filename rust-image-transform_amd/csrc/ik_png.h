@@ -1,0 +1,49 @@
+// ik_png.h -- device-side descriptors and launchers of the GPU PNG decoder
+// (kernels: ik_png.hip; host orchestration: ik_png_decode.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "ik_inflate.h"
+
+namespace ik {
+
+constexpr int kPngInflateThreads = 64;     // decoder lanes per workgroup (LDS: 1280 B each)
+constexpr int kPngUnfilterThreads = 1024;  // 16 waves: 16 bands in flight per image
+constexpr uint64_t kPngChunkBytes = 16384; // candidate-search chunk of the compressed stream
+constexpr int kPngPageShift = 12;          // resolve: output page -> decoder table
+
+// one image of a batch, as the kernels see it
+struct PngImgDev {
+    const uint32_t* words;   // zlib stream (little-endian words, zero padded)
+    uint64_t bit0;           // first DEFLATE bit (after the 2-byte zlib header)
+    uint64_t nbits;          // stream length in bits
+    uint16_t* u16;           // emit pass output: raw_total symbols (+ padding)
+    uint64_t raw_total;      // bytes of the filtered image (H rows of 1 + rowbytes)
+    const int64_t* obase;    // output offset of each decoder lane (ascending)
+    const int* page_lane;    // decoder holding the first byte of each output page
+    int nlanes;
+    int rowbytes, H, bpp;
+    uint8_t* ft;             // filter type of every row
+    uint8_t* dst;            // the image (pitched); filtered rows, then pixels in place
+    size_t pitch;
+};
+
+struct PngLaneDev {
+    uint64_t start, stop;    // block boundary to start at; next lane's start (~0 = last)
+    int64_t obase;           // emit pass: output offset
+    uint32_t img;            // image of the batch
+    uint32_t slot;           // subtable work area index
+    uint32_t first;          // lane 0 of its image (output offset 0 is known)
+    uint32_t pad;
+};
+
+hipError_t launch_png_find(const PngImgDev* imgs, const int* chunk_img, const int* chunk_idx, int n,
+                           uint64_t chunk_bits, int64_t* cand, hipStream_t s);
+hipError_t launch_png_inflate(bool emit, const PngImgDev* imgs, const PngLaneDev* lanes, int n, uint16_t* sub_ws,
+                              infl::LaneResult* res, hipStream_t s);
+hipError_t launch_png_resolve(const PngImgDev* imgs, const int2* rows, int nrows, int* err, hipStream_t s);
+hipError_t launch_png_unfilter(const PngImgDev* imgs, int n, int bpp, hipStream_t s);
+
+}  // namespace ik

@@ -1,0 +1,543 @@
+// ik_png_decode.cpp -- decode_image on PNG streams with the GPU doing the inflate
+// and the unfiltering (reference src/transform.rs:31 -> image 0.25.8 ->
+// png 0.18).  Kernels: ik_png.hip; algorithm: ik_inflate.h / ik_png_plan.h.
+//
+// Per batch of streams:
+//   host   chunk walk + CRC check of every chunk (png verifies CRCs), IHDR;
+//          the IDAT payloads of all streams -> one pinned buffer -> one H2D copy
+//   GPU    k_png_find (block-start candidates per 16 KiB chunk)
+//   GPU    k_png_inflate count rounds; the host checks the lane chain after each
+//          (a false candidate is dropped and its predecessor decodes on)
+//   GPU    k_png_inflate emit (u16 symbols + window markers), k_png_resolve
+//          (filtered rows into the image, markers followed), k_png_unfilter
+// The GPU path covers 8- and 16-bit, non-interlaced, non-palette streams
+// without tRNS (png's EXPAND leaves those samples as they are); everything else,
+// and any stream the GPU finds inconsistent, goes through the host decoder, whose
+// error messages are png's.  The zlib Adler-32 is not verified, as png 0.18 does
+// not by default (CRCs cover the data).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/imagekit_hip.h"
+#include "ik_png.h"
+#include "ik_png_plan.h"
+#include "ik_runtime.h"
+
+namespace ik {
+
+namespace {
+
+inline uint32_t be32(const uint8_t* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
+size_t up256(size_t v) { return (v + 255) & ~size_t(255); }
+
+struct PngJob {
+    int idx = -1;                                   // stream index in the batch
+    uint32_t w = 0, h = 0;
+    int depth = 0, ctype = 0, bpp = 0, ch = 0;       // bytes per pixel, image channels
+    std::vector<std::pair<const uint8_t*, uint32_t>> idat;
+    size_t zlen = 0;                                 // IDAT payload bytes (zlib stream)
+    uint64_t raw_total = 0;
+    int rowbytes = 0;
+    // device layout (offsets into the batch work area)
+    size_t o_words = 0, o_u16 = 0, o_ft = 0;
+    size_t z_off = 0;                                // offset of the stream in the pinned buffer
+    uint64_t nbits = 0;
+    int chunk0 = 0, nchunks = 0;                     // its chunks in the batch chunk table
+    pngplan::Lanes lanes;
+    int state = 0;                                   // 0 running, 1 verified, -1 host fallback
+    ik_image* img = nullptr;
+};
+
+// png 0.18 + image's EXPAND: which streams the GPU path decodes.  Returns false
+// for streams that must go to the host decoder (which also produces png's
+// errors for malformed ones).
+bool parse_png(const uint8_t* b, size_t n, PngJob& J) {
+    if (n < 8 || std::memcmp(b, "\x89PNG\r\n\x1a\n", 8)) return false;
+    size_t pos = 8;
+    bool ihdr = false, trns = false;
+    int interlace = 0;
+    while (pos + 12 <= n) {
+        const uint32_t len = be32(b + pos);
+        if (len > n - pos - 12) return false;
+        const uint8_t* type = b + pos + 4;
+        const uint8_t* data = b + pos + 8;
+        if (png_chunk_crc(type, data, len) != be32(data + len)) return false;
+        if (!std::memcmp(type, "IHDR", 4)) {
+            if (len != 13 || ihdr) return false;
+            J.w = be32(data);
+            J.h = be32(data + 4);
+            J.depth = data[8];
+            J.ctype = data[9];
+            interlace = data[12];
+            ihdr = true;
+        } else if (!std::memcmp(type, "tRNS", 4)) {
+            trns = true;
+        } else if (!std::memcmp(type, "IDAT", 4)) {
+            if (len) J.idat.emplace_back(data, len);
+            J.zlen += len;
+        } else if (!std::memcmp(type, "IEND", 4)) {
+            break;
+        }
+        pos += 12 + len;
+    }
+    if (!ihdr || J.idat.empty() || !J.w || !J.h || interlace || trns) return false;
+    if (J.depth != 8 && J.depth != 16) return false;
+    int spp;
+    switch (J.ctype) {
+    case 0: spp = 1; break;
+    case 2: spp = 3; break;
+    case 4: spp = 2; break;
+    case 6: spp = 4; break;
+    default: return false;  // palette: host
+    }
+    J.ch = spp;
+    J.bpp = spp * J.depth / 8;
+    if (J.depth == 16) return false;  // 16-bit samples: host (see decode_png)
+    const uint64_t rb = (uint64_t)J.w * J.bpp;
+    // image's default limit: 512 MiB of decoded pixels
+    if (rb * J.h > (512ull << 20) || rb > 0x7FFFFFF0ull) return false;
+    J.rowbytes = (int)rb;
+    J.raw_total = (rb + 1) * J.h;
+    // zlib header: CM 8, window <= 32 KiB, FCHECK, no preset dictionary
+    const uint8_t* z0 = J.idat[0].first;
+    uint8_t cmf, flg;
+    if (J.idat[0].second >= 2) { cmf = z0[0]; flg = z0[1]; }
+    else if (J.idat.size() > 1) { cmf = z0[0]; flg = J.idat[1].first[0]; }
+    else return false;
+    if ((cmf & 15) != 8 || (cmf >> 4) > 7 || ((cmf << 8) | flg) % 31 || (flg & 0x20)) return false;
+    return true;
+}
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// the last batch's stage times on this thread (ik_png_last_timing): host parse +
+// staging, then device ms of find / count (all rounds) / emit / resolve / unfilter
+// from HIP events on the thread's stream, wall ms, rounds, lanes, GPU streams
+thread_local double t_png_timing[10];
+struct Events {
+    hipEvent_t e[12] = {};
+    bool ok = false;
+    Events() {
+        ok = true;
+        for (auto& x : e) ok = ok && hipEventCreate(&x) == hipSuccess;
+    }
+};
+Events& events() {
+    static thread_local Events ev;
+    return ev;
+}
+float ev_ms(int a, int b) {
+    float ms = 0;
+    if (!events().ok || hipEventElapsedTime(&ms, events().e[a], events().e[b]) != hipSuccess) return 0;
+    return ms;
+}
+
+}  // namespace
+
+namespace {
+std::atomic<long long> g_png_gpu_min{-2};  // -2: not read yet; -1: GPU path off
+long long png_gpu_min() {
+    long long v = g_png_gpu_min.load();
+    if (v == -2) {
+        const char* e = getenv("IK_PNG_GPU");
+        const char* m = getenv("IK_PNG_GPU_MIN");
+        v = (e && !strcmp(e, "0")) ? -1 : (m ? (long long)strtoull(m, nullptr, 10) : (256ll << 10));
+        long long expect = -2;
+        g_png_gpu_min.compare_exchange_strong(expect, v);
+        v = g_png_gpu_min.load();
+    }
+    return v;
+}
+}  // namespace
+
+bool png_gpu_enabled(size_t raw_bytes) {
+    const long long v = png_gpu_min();
+    return v >= 0 && (long long)raw_bytes >= v;
+}
+
+int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_image** outs, int* status,
+                     std::string* msgs) {
+    static const bool timing = getenv("IK_PNG_TIMING") != nullptr;
+    const double t0 = now_ms();
+    for (double& v : t_png_timing) v = 0;
+    Events& ev = events();
+    auto rec = [&](int k, hipStream_t st) { if (ev.ok) (void)hipEventRecord(ev.e[k], st); };
+    double count_dev = 0;
+    std::vector<PngJob> jobs(n);
+    std::vector<char> gpu(n, 0);
+    parallel_for(n, 0, [&](int i) {
+        outs[i] = nullptr;
+        status[i] = IK_OK;
+        jobs[i].idx = i;
+        gpu[i] = parse_png(bytes[i], lens[i], jobs[i]) && png_gpu_enabled(jobs[i].raw_total);
+    });
+    std::vector<PngJob*> J;
+    for (int i = 0; i < n; ++i)
+        if (gpu[i]) J.push_back(&jobs[i]);
+    const int m = (int)J.size();
+    hipStream_t s = thread_stream();
+    int rc = IK_OK;
+    const uint64_t cbits = kPngChunkBytes * 8;
+    if (m) {
+        // ---- device layout ----
+        size_t total = 0, zbytes = 0;
+        int nchunks = 0;
+        for (PngJob* j : J) {
+            j->z_off = zbytes;
+            zbytes += (j->zlen + 3) & ~size_t(3);
+            j->nbits = (uint64_t)j->zlen * 8;
+            j->nchunks = (int)((j->nbits - 16 + cbits - 1) / cbits);
+            j->chunk0 = nchunks;
+            nchunks += j->nchunks;
+            j->o_words = total;
+            total += up256(((j->zlen + 3) & ~size_t(3)) + 64);  // 4 zero words past the end (Bits::wend)
+            j->o_u16 = total;
+            total += up256(2 * (j->raw_total + 64));
+            j->o_ft = total;
+            total += up256(j->h);
+        }
+        const size_t o_imgs = total;
+        total += up256(sizeof(PngImgDev) * m);
+        const size_t o_ctab = total;
+        total += up256(sizeof(int) * 2 * nchunks);
+        const size_t o_cand = total;
+        total += up256(sizeof(int64_t) * nchunks);
+        const size_t o_err = total;
+        total += up256(sizeof(int) * m);
+        const size_t o_dyn = total;  // lane tables, results, obase, rows, subtables: sized per round below
+        uint8_t* pin = pinned_slot(1, zbytes + 64);
+        if (!pin) rc = fail(IK_ERR_NOMEM, "cannot allocate pinned PNG staging");
+        // IDAT payloads -> pinned (host threads), word-padded
+        if (!rc)
+            parallel_for(m, 0, [&](int k) {
+                PngJob& j = *J[k];
+                uint8_t* d = pin + j.z_off;
+                for (auto& seg : j.idat) {
+                    std::memcpy(d, seg.first, seg.second);
+                    d += seg.second;
+                }
+                while ((size_t)(d - (pin + j.z_off)) & 3) *d++ = 0;
+            });
+        const double t1 = now_ms();
+        // the work area: grows with the largest round's lane tables (bounded below)
+        size_t max_lanes = 0;
+        for (PngJob* j : J) max_lanes += (size_t)j->nchunks;
+        size_t dyn = up256(sizeof(PngLaneDev) * max_lanes) + up256(sizeof(infl::LaneResult) * max_lanes) +
+                     up256(sizeof(int64_t) * max_lanes) + (size_t)max_lanes * (infl::kLitSub + infl::kDistSub) * 2;
+        size_t nrows = 0, npages = 0;
+        for (PngJob* j : J) {
+            nrows += j->h;
+            npages += (j->raw_total >> kPngPageShift) + 1;
+        }
+        dyn += up256(sizeof(int2) * nrows) + up256(sizeof(int) * npages);
+        uint8_t* dev = rc ? nullptr : scratch_slot(2, o_dyn + dyn);
+        if (!rc && !dev) rc = fail(IK_ERR_DEVICE, "cannot allocate the PNG batch work area (%zu bytes)", o_dyn + dyn);
+        PngLaneDev* d_lanes = nullptr;
+        infl::LaneResult* d_res = nullptr;
+        int64_t* d_obase = nullptr;
+        uint16_t* d_sub = nullptr;
+        int2* d_rows = nullptr;
+        int* d_pages = nullptr;
+        if (!rc) {
+            size_t o = o_dyn;
+            d_lanes = reinterpret_cast<PngLaneDev*>(dev + o);
+            o += up256(sizeof(PngLaneDev) * max_lanes);
+            d_res = reinterpret_cast<infl::LaneResult*>(dev + o);
+            o += up256(sizeof(infl::LaneResult) * max_lanes);
+            d_obase = reinterpret_cast<int64_t*>(dev + o);
+            o += up256(sizeof(int64_t) * max_lanes);
+            d_rows = reinterpret_cast<int2*>(dev + o);
+            o += up256(sizeof(int2) * nrows);
+            d_pages = reinterpret_cast<int*>(dev + o);
+            o += up256(sizeof(int) * npages);
+            d_sub = reinterpret_cast<uint16_t*>(dev + o);
+        }
+        // ---- upload streams (zero pad), image descriptors, chunk table ----
+        std::vector<PngImgDev> hd(m);
+        std::vector<int> ctab(2 * (size_t)nchunks);
+        for (int k = 0; k < m && !rc; ++k) {
+            PngJob& j = *J[k];
+            PngImgDev& d = hd[k];
+            d.words = reinterpret_cast<const uint32_t*>(dev + j.o_words);
+            d.bit0 = 16;
+            d.nbits = j.nbits;
+            d.u16 = reinterpret_cast<uint16_t*>(dev + j.o_u16);
+            d.raw_total = j.raw_total;
+            d.rowbytes = j.rowbytes;
+            d.H = (int)j.h;
+            d.bpp = j.bpp;
+            d.ft = dev + j.o_ft;
+            for (int c = 0; c < j.nchunks; ++c) {
+                ctab[2 * (size_t)(j.chunk0 + c)] = k;
+                ctab[2 * (size_t)(j.chunk0 + c) + 1] = c;
+            }
+            hipError_t e = hipMemsetAsync(dev + j.o_words + ((j.zlen + 3) & ~size_t(3)), 0, 64, s);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(dev + j.o_words, pin + j.z_off, (j.zlen + 3) & ~size_t(3), hipMemcpyHostToDevice, s);
+            if (e != hipSuccess) rc = hip_fail(e, "PNG stream upload");
+        }
+        std::vector<int> hchunk_img(nchunks), hchunk_idx(nchunks);
+        for (int c = 0; c < nchunks; ++c) { hchunk_img[c] = ctab[2 * (size_t)c]; hchunk_idx[c] = ctab[2 * (size_t)c + 1]; }
+        if (!rc) rc = copy_h2d_2d(dev + o_ctab, sizeof(int) * nchunks, reinterpret_cast<const uint8_t*>(hchunk_img.data()),
+                                  sizeof(int) * nchunks, sizeof(int) * nchunks, 1, s);
+        if (!rc) rc = copy_h2d_2d(dev + o_ctab + sizeof(int) * nchunks, sizeof(int) * nchunks,
+                                  reinterpret_cast<const uint8_t*>(hchunk_idx.data()), sizeof(int) * nchunks,
+                                  sizeof(int) * nchunks, 1, s);
+        if (!rc) rc = copy_h2d_2d(dev + o_imgs, sizeof(PngImgDev) * m, reinterpret_cast<const uint8_t*>(hd.data()),
+                                  sizeof(PngImgDev) * m, sizeof(PngImgDev) * m, 1, s);
+        const PngImgDev* d_imgs = reinterpret_cast<const PngImgDev*>(dev + o_imgs);
+        // ---- candidates ----
+        std::vector<int64_t> cand(nchunks);
+        if (!rc) {
+            rec(0, s);
+            hipError_t e = launch_png_find(d_imgs, reinterpret_cast<const int*>(dev + o_ctab),
+                                           reinterpret_cast<const int*>(dev + o_ctab) + nchunks, nchunks, cbits,
+                                           reinterpret_cast<int64_t*>(dev + o_cand), s);
+            rec(1, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(cand.data(), dev + o_cand, sizeof(int64_t) * nchunks,
+                                                    hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) rc = hip_fail(e, "PNG block search");
+        }
+        const double t2 = now_ms();
+        for (PngJob* j : J) {
+            std::vector<int64_t> c(cand.begin() + j->chunk0, cand.begin() + j->chunk0 + j->nchunks);
+            pngplan::build(c, j->lanes);
+        }
+        // ---- count rounds ----
+        int rounds = 0, dropped = 0;
+        std::vector<PngLaneDev> hl;
+        std::vector<std::pair<int, int>> who;  // (job, lane) of each launched lane
+        std::vector<infl::LaneResult> hres;
+        while (!rc) {
+            hl.clear();
+            who.clear();
+            for (int k = 0; k < m; ++k) {
+                PngJob& j = *J[k];
+                if (j.state) continue;
+                for (size_t i = 0; i < j.lanes.start.size(); ++i) {
+                    if (!j.lanes.dirty[i]) continue;
+                    PngLaneDev L{};
+                    L.start = j.lanes.start[i];
+                    L.stop = j.lanes.stop[i];
+                    L.obase = -1;
+                    L.img = (uint32_t)k;
+                    L.slot = (uint32_t)hl.size();
+                    L.first = i == 0;
+                    hl.push_back(L);
+                    who.emplace_back(k, (int)i);
+                }
+            }
+            if (hl.empty()) break;
+            if (hl.size() > max_lanes) { rc = fail(IK_ERR_DEVICE, "PNG lane table overflow"); break; }
+            const size_t lb = sizeof(PngLaneDev) * hl.size();
+            rc = copy_h2d_2d(reinterpret_cast<uint8_t*>(d_lanes), lb, reinterpret_cast<const uint8_t*>(hl.data()), lb, lb, 1, s);
+            if (rc) break;
+            hres.resize(hl.size());
+            rec(2, s);
+            hipError_t e = launch_png_inflate(false, d_imgs, d_lanes, (int)hl.size(), d_sub, d_res, s);
+            rec(3, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(hres.data(), d_res, sizeof(infl::LaneResult) * hl.size(),
+                                                    hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) { rc = hip_fail(e, "PNG inflate (count)"); break; }
+            count_dev += ev_ms(2, 3);
+            ++rounds;
+            for (size_t t = 0; t < hl.size(); ++t) {
+                PngJob& j = *J[who[t].first];
+                j.lanes.res[who[t].second] = hres[t];
+                j.lanes.dirty[who[t].second] = 0;
+            }
+            for (PngJob* j : J) {
+                if (j->state) continue;
+                const size_t before = j->lanes.start.size();
+                const int st = pngplan::check(j->lanes);
+                dropped += (int)(before - j->lanes.start.size());
+                if (st == 0) j->state = 1;
+                else if (st < 0) j->state = -1;
+            }
+        }
+        const double t3 = now_ms();
+        // ---- offsets, output images, emit ----
+        std::vector<int64_t> hob;
+        std::vector<int> hpages;
+        hl.clear();
+        for (int k = 0; k < m && !rc; ++k) {
+            PngJob& j = *J[k];
+            if (j.state != 1) continue;
+            std::vector<int64_t> ob;
+            uint64_t tot = 0;
+            pngplan::offsets(j.lanes, ob, &tot);
+            if (tot != j.raw_total) { j.state = -1; continue; }  // png: wrong amount of image data
+            if (alloc_image(j.w, j.h, (uint32_t)j.bpp, &j.img)) { j.state = -1; continue; }
+            hd[k].obase = d_obase + hob.size();
+            hd[k].page_lane = d_pages + hpages.size();
+            hd[k].nlanes = (int)ob.size();
+            // page -> decoder that holds the page's first byte (resolve's lane lookup)
+            for (uint64_t pg = 0, ln = 0; pg <= (j.raw_total >> kPngPageShift); ++pg) {
+                while (ln + 1 < ob.size() && (uint64_t)ob[ln + 1] <= (pg << kPngPageShift)) ++ln;
+                hpages.push_back((int)ln);
+            }
+            hd[k].dst = j.img->d;
+            hd[k].pitch = j.img->pitch;
+            for (size_t i = 0; i < ob.size(); ++i) {
+                PngLaneDev L{};
+                L.start = j.lanes.start[i];
+                L.stop = j.lanes.stop[i];
+                L.obase = ob[i];
+                L.img = (uint32_t)k;
+                L.slot = (uint32_t)hl.size();
+                L.first = i == 0;
+                hl.push_back(L);
+            }
+            hob.insert(hob.end(), ob.begin(), ob.end());
+        }
+        std::vector<int2> hrows;
+        std::vector<int> herr(m, 0);
+        if (!rc && !hl.empty()) {
+            for (int k = 0; k < m; ++k)
+                if (J[k]->state == 1)
+                    for (uint32_t y = 0; y < J[k]->h; ++y) hrows.push_back(make_int2(k, (int)y));
+            const size_t lb = sizeof(PngLaneDev) * hl.size();
+            rc = copy_h2d_2d(reinterpret_cast<uint8_t*>(d_lanes), lb, reinterpret_cast<const uint8_t*>(hl.data()), lb, lb, 1, s);
+            if (!rc) rc = copy_h2d_2d(reinterpret_cast<uint8_t*>(d_obase), sizeof(int64_t) * hob.size(),
+                                      reinterpret_cast<const uint8_t*>(hob.data()), sizeof(int64_t) * hob.size(),
+                                      sizeof(int64_t) * hob.size(), 1, s);
+            if (!rc) rc = copy_h2d_2d(reinterpret_cast<uint8_t*>(d_pages), sizeof(int) * hpages.size(),
+                                      reinterpret_cast<const uint8_t*>(hpages.data()), sizeof(int) * hpages.size(),
+                                      sizeof(int) * hpages.size(), 1, s);
+            if (!rc) rc = copy_h2d_2d(dev + o_imgs, sizeof(PngImgDev) * m, reinterpret_cast<const uint8_t*>(hd.data()),
+                                      sizeof(PngImgDev) * m, sizeof(PngImgDev) * m, 1, s);
+            if (!rc) rc = copy_h2d_2d(reinterpret_cast<uint8_t*>(d_rows), sizeof(int2) * hrows.size(),
+                                      reinterpret_cast<const uint8_t*>(hrows.data()), sizeof(int2) * hrows.size(),
+                                      sizeof(int2) * hrows.size(), 1, s);
+            hres.resize(hl.size());
+            if (!rc) {
+                hipError_t e = hipMemsetAsync(dev + o_err, 0, sizeof(int) * m, s);
+                rec(4, s);
+                if (e == hipSuccess) e = launch_png_inflate(true, d_imgs, d_lanes, (int)hl.size(), d_sub, d_res, s);
+                rec(5, s);
+                if (e == hipSuccess) e = launch_png_resolve(d_imgs, d_rows, (int)hrows.size(),
+                                                            reinterpret_cast<int*>(dev + o_err), s);
+                rec(6, s);
+                // unfilter: one launch per bytes-per-pixel class, over that class's images;
+                // the class descriptor arrays go where the emit pass's subtables were
+                // (that pass is done by then, in stream order), uploaded in one copy
+                if (e == hipSuccess) {
+                    std::vector<PngImgDev> cls;
+                    std::vector<std::pair<int, int>> ranges;  // (bpp, first) per class
+                    for (int bpp : {1, 2, 3, 4, 6, 8}) {
+                        const int first = (int)cls.size();
+                        for (int k = 0; k < m; ++k)
+                            if (J[k]->state == 1 && hd[k].bpp == bpp) cls.push_back(hd[k]);
+                        if ((int)cls.size() > first) ranges.emplace_back(bpp, first);
+                    }
+                    const size_t cb = sizeof(PngImgDev) * cls.size();
+                    uint8_t* stage = pinned_slot(2, cb);
+                    if (!stage) e = hipErrorOutOfMemory;
+                    if (e == hipSuccess) {
+                        std::memcpy(stage, cls.data(), cb);
+                        e = hipMemcpyAsync(d_sub, stage, cb, hipMemcpyHostToDevice, s);
+                    }
+                    for (size_t r = 0; r < ranges.size() && e == hipSuccess; ++r) {
+                        const int first = ranges[r].second;
+                        const int cnt = (r + 1 < ranges.size() ? ranges[r + 1].second : (int)cls.size()) - first;
+                        e = launch_png_unfilter(reinterpret_cast<const PngImgDev*>(d_sub) + first, cnt,
+                                                ranges[r].first, s);
+                    }
+                }
+                rec(7, s);
+                if (e == hipSuccess) e = hipMemcpyAsync(hres.data(), d_res, sizeof(infl::LaneResult) * hl.size(),
+                                                        hipMemcpyDeviceToHost, s);
+                if (e == hipSuccess) e = hipMemcpyAsync(herr.data(), dev + o_err, sizeof(int) * m, hipMemcpyDeviceToHost, s);
+                if (e == hipSuccess) e = hipStreamSynchronize(s);
+                if (e != hipSuccess) rc = hip_fail(e, "PNG inflate (emit) / unfilter");
+                if (!rc) {
+                    t_png_timing[3] = ev_ms(4, 5);
+                    t_png_timing[4] = ev_ms(5, 6);
+                    t_png_timing[5] = ev_ms(6, 7);
+                }
+            }
+            if (!rc) {
+                size_t t = 0;
+                for (int k = 0; k < m; ++k) {
+                    PngJob& j = *J[k];
+                    if (j.state != 1) continue;
+                    bool ok = herr[k] == 0;
+                    for (size_t i = 0; i < j.lanes.start.size(); ++i, ++t)
+                        ok = ok && hres[t].status == infl::kLaneOk && hres[t].out_len == j.lanes.res[i].out_len;
+                    if (!ok) j.state = -1;
+                }
+            }
+        }
+        t_png_timing[0] = t1 - t0;
+        t_png_timing[1] = ev_ms(0, 1);
+        t_png_timing[2] = count_dev;
+        t_png_timing[7] = rounds;
+        t_png_timing[8] = (double)hl.size();
+        t_png_timing[9] = m;
+        if (timing)
+            fprintf(stderr, "[png] %d streams (%d on the GPU): stage %.2f ms, find %.2f ms, count %.2f ms (%d rounds, %d "
+                    "dropped), emit+resolve+unfilter %.2f ms\n", n, m, t1 - t0, t2 - t1, t3 - t2, rounds, dropped,
+                    now_ms() - t3);
+        for (int k = 0; k < m; ++k) {
+            PngJob& j = *J[k];
+            if (!rc && j.state == 1) {
+                outs[j.idx] = j.img;
+                j.img = nullptr;
+            } else {
+                if (j.img) { ik_image_free(j.img); j.img = nullptr; }
+                gpu[j.idx] = 0;  // host decoder below
+            }
+        }
+        if (rc) {  // the device path failed as a whole: every stream on the host
+            for (int k = 0; k < m; ++k) gpu[J[k]->idx] = 0;
+        }
+    }
+    // ---- host decoder: streams outside the GPU path, and GPU rejects ----
+    std::vector<int> host;
+    for (int i = 0; i < n; ++i)
+        if (!gpu[i]) host.push_back(i);
+    parallel_for((int)host.size(), 0, [&](int k) {
+        const int i = host[k];
+        thread_local std::vector<uint8_t> px;
+        uint32_t w = 0, h = 0, c = 0;
+        int st = decode_png(bytes[i], lens[i], w, h, c, px);
+        if (!st) st = ik_image_from_host(px.data(), w, h, c, &outs[i]);
+        if (px.capacity() > (128u << 20)) std::vector<uint8_t>().swap(px);
+        status[i] = st;
+        if (st && msgs) {
+            char buf[512];
+            ik_last_error(buf, sizeof(buf));
+            msgs[i] = buf;
+        }
+    });
+    t_png_timing[6] = now_ms() - t0;
+    int first = IK_OK;
+    for (int i = 0; i < n; ++i)
+        if (status[i] && !first) first = status[i];
+    return first;
+}
+
+}  // namespace ik
+
+extern "C" int ik_png_last_timing(double* out, int n) {
+    for (int i = 0; i < n && i < 10; ++i) out[i] = ik::t_png_timing[i];
+    return IK_OK;
+}
+
+extern "C" int ik_set_png_gpu_min(long long min_raw_bytes) {
+    (void)ik::png_gpu_min();
+    ik::g_png_gpu_min.store(min_raw_bytes < 0 ? -1 : min_raw_bytes);
+    return IK_OK;
+}

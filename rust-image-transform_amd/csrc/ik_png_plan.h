@@ -1,0 +1,97 @@
+// ik_png_plan.h -- host-side bookkeeping of the parallel inflate (ik_inflate.h):
+// decoder lanes from chunk candidates, and the chain check that verifies them.
+// Shared by the GPU PNG decoder (ik_png_decode.cpp) and its CPU model
+// (ik_png_model.cpp, CPU tests only).
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "ik_inflate.h"
+
+namespace ik {
+namespace pngplan {
+
+// One image's decoder lanes: lane i decodes blocks from start[i] up to stop[i]
+// (the next lane's start, ~0 for the last lane).
+struct Lanes {
+    std::vector<uint64_t> start, stop;
+    std::vector<infl::LaneResult> res;
+    std::vector<char> dirty;  // needs (re)decoding in the next count round
+    int rounds = 0;
+};
+
+// candidates per chunk (chunk 0 = the first block, always valid; -1 = none found)
+inline void build(const std::vector<int64_t>& cand, Lanes& L) {
+    L.start.clear();
+    L.stop.clear();
+    for (int64_t c : cand)
+        if (c >= 0 && (L.start.empty() || (uint64_t)c > L.start.back())) L.start.push_back((uint64_t)c);
+    L.stop.resize(L.start.size());
+    for (size_t i = 0; i < L.start.size(); ++i) L.stop[i] = i + 1 < L.start.size() ? L.start[i + 1] : ~0ull;
+    L.res.assign(L.start.size(), infl::LaneResult{0, 0, infl::kLaneCorrupt, 0});
+    L.dirty.assign(L.start.size(), 1);
+    L.rounds = 0;
+}
+
+// After a count round: walk the chain from lane 0 (whose start is the stream's
+// first block, so verified).  A lane whose start is verified and that stopped
+// exactly on its successor's start verifies that start.  One that passed it
+// (mismatch) shows the successor's candidate was not a block boundary: the
+// successor is dropped and the lane decodes on to the next one next round.
+// Returns 0 when every lane is verified (the output offsets are then valid),
+// 1 when dirty lanes must be decoded again, -1 when a verified lane found the
+// stream corrupt (or the rounds ran out).
+inline int check(Lanes& L, int max_rounds = 24) {
+    ++L.rounds;
+    bool verified = true;  // lane i's start is verified by this round's results
+    bool any_dirty = false;
+    for (size_t i = 0; i < L.start.size();) {
+        if (L.dirty[i]) {  // not decoded yet in this state: its successors wait
+            verified = false;
+            any_dirty = true;
+            ++i;
+            continue;
+        }
+        const infl::LaneResult& r = L.res[i];
+        if (r.status == infl::kLaneOk) {
+            ++i;
+            continue;  // successor verified iff this one was
+        }
+        if (r.status == infl::kLaneCorrupt) {
+            if (verified) return -1;
+            ++i;  // its start may be false: the predecessor decides next round
+            continue;
+        }
+        // mismatch: drop the successor, decode on to the one after it
+        if (i + 1 >= L.start.size()) {  // cannot happen (the last lane has stop ~0); treat as corrupt
+            if (verified) return -1;
+            ++i;
+            continue;
+        }
+        L.start.erase(L.start.begin() + (long)(i + 1));
+        L.res.erase(L.res.begin() + (long)(i + 1));
+        L.dirty.erase(L.dirty.begin() + (long)(i + 1));
+        L.stop.erase(L.stop.begin() + (long)(i + 1));
+        L.stop[i] = i + 1 < L.start.size() ? L.start[i + 1] : ~0ull;
+        L.dirty[i] = 1;
+        any_dirty = true;
+        verified = false;
+        ++i;
+    }
+    if (!any_dirty) return 0;
+    return L.rounds >= max_rounds ? -1 : 1;
+}
+
+// output offsets of verified lanes (exclusive prefix sum); total in *total
+inline void offsets(const Lanes& L, std::vector<int64_t>& obase, uint64_t* total) {
+    obase.resize(L.start.size());
+    uint64_t t = 0;
+    for (size_t i = 0; i < L.start.size(); ++i) {
+        obase[i] = (int64_t)t;
+        t += L.res[i].out_len;
+    }
+    *total = t;
+}
+
+}  // namespace pngplan
+}  // namespace ik

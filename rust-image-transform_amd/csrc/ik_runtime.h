@@ -147,6 +147,14 @@ enum class Sniffed { Png, Jpeg, Gif, WebP, Tiff, Bmp, Ico, Hdr, Avif, OpenExr, Q
 Sniffed guess_format(const uint8_t* b, size_t n);
 const char* format_name(Sniffed f);
 int decode_png(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& c, std::vector<uint8_t>& px);
+uint32_t png_chunk_crc(const uint8_t* type, const uint8_t* data, size_t len);  // CRC-32 of type + data
+// PNG on the GPU (ik_png_decode.cpp + ik_png.hip): inflate + unfilter of n streams
+// in one set of launches, straight into new device images; streams the GPU path
+// does not cover (or that fail on it) go through decode_png.  Per-stream status
+// and message; returns the first failure.
+int decode_png_batch(const uint8_t* const* b, const size_t* lens, int n, ik_image** outs, int* status,
+                     std::string* msgs);
+bool png_gpu_enabled(size_t raw_bytes);  // IK_PNG_GPU / IK_PNG_GPU_MIN policy
 int decode_webp(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& c, std::vector<uint8_t>& px);
 
 // JPEG: host entropy decode + GPU reconstruction straight into a new device image

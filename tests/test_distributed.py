@@ -32,7 +32,7 @@ def _worker(rank, world, port, q):
     seeds = bench.shard_seeds(rank, 32)
     gathered = [None] * world
     dist.all_gather_object(gathered, seeds)
-    q.put((rank, m, gathered, bench.aggregate_mpix(world, 32, 10, 4096, m)))
+    q.put((rank, m, gathered, bench.aggregate_mpix(world, 32 * 10, 4096, m)))
     dist.barrier()
     dist.destroy_process_group()
 

@@ -35,12 +35,16 @@ def test_error_display_matches_thiserror():
 
 
 def test_bench_cli_formats_match_image_format(monkeypatch):
-    """bench.py's --format values are the ImageFormat discriminants the C ABI takes
-    (include/imagekit_hip.h ik_format), incl. the configs[4] AVIF runs."""
+    """tools/bench_pipeline.py's --format values are the ImageFormat discriminants the
+    C ABI takes (include/imagekit_hip.h ik_format), incl. the configs[4] AVIF runs;
+    bench.py (the headline) uses the same table."""
     import os
     import sys
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    import bench
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "tools")]
+    import bench as headline
+    import bench_pipeline as bench
+    assert headline.FORMATS == bench.FORMATS
     for f in ImageFormat:
         assert bench.FORMATS[str(f)] == f.value
     monkeypatch.setattr(sys, "argv", ["bench.py", "--size", "8192", "--out", "1024", "--filter", "lanczos3",
