@@ -243,6 +243,8 @@ def main():
     for _ in range(args.warmup):
         step()
     stage_ms.clear()
+    cnt0 = (ctypes.c_ulonglong * 2)()
+    lib.ik_png_counters(cnt0)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -252,11 +254,15 @@ def main():
     barrier()
     elapsed = reduce_max(elapsed, dist, dev)
     assert all(r is not None and r[:4] == b"RIFF" for r in res)
+    cnt1 = (ctypes.c_ulonglong * 2)()
+    lib.ik_png_counters(cnt1)
+    gpu_streams, host_streams = cnt1[0] - cnt0[0], cnt1[1] - cnt0[1]
     value = aggregate_mpix(world, B * args.steps, S, elapsed)
     st = np.mean(np.array(stage_ms), axis=0)
     png_stages = {k: round(float(v), 3) for k, v in zip(PNG_STAGES, st[:6])}
     png_stages.update({"decode_wall_ms": round(float(st[6]), 3), "count_rounds": float(st[7]),
-                       "decoder_lanes": int(st[8]), "streams_on_gpu": int(st[9])})
+                       "decoder_lanes": int(st[8]), "streams_on_gpu": int(st[9]),
+                       "timed_streams_gpu_decoded": int(gpu_streams), "timed_streams_host_decoded": int(host_streams)})
     out_bytes = sum(len(r) for r in res) // B
     in_bytes = sum(len(p) for p in reqs) // B
 

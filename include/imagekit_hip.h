@@ -109,8 +109,13 @@ int ik_decode_batch(const uint8_t *const *bytes, const size_t *lens, uint32_t n,
 int ik_set_png_gpu_min(long long min_raw_bytes);
 /* the calling thread's last GPU PNG batch: [0] host parse + staging ms, device ms
  * of [1] block search [2] count passes [3] emit pass [4] resolve [5] unfilter,
- * [6] wall ms, [7] count rounds, [8] decoder lanes, [9] streams on the GPU */
+ * [6] wall ms, [7] count rounds, [8] decoder lanes, [9] streams sent to the GPU,
+ * [10] PNG streams of the batch the GPU decoded, [11] streams the host decoder took
+ * (outside the GPU path, or rejected by it) */
 int ik_png_last_timing(double *out, int n);
+/* process-wide counts of PNG streams decoded since load: out[0] by the GPU path,
+ * out[1] by the host decoder (outside the GPU path, or rejected by it) */
+int ik_png_counters(unsigned long long *out);
 
 /* resize_image (src/transform.rs:62-90).  w/h < 0 mean None.  Both None returns
  * the input unchanged (*out == img); otherwise a new image (img is not freed:

@@ -32,9 +32,20 @@
 #include <hip/hip_runtime.h>
 #define IK_HD __host__ __device__ __forceinline__
 #define IK_HD_COLD __host__ __device__ __attribute__((noinline))
+#define IK_UNROLL _Pragma("unroll")
 #else
+#define IK_UNROLL
 #define IK_HD inline
 #define IK_HD_COLD inline
+#endif
+
+// device code: stream / output pointers in the global address space, so loads
+// and stores are global_* (vmcnt only) instead of flat_* (which also count in
+// lgkmcnt and would make every LDS wait wait for memory too)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define IK_GLOBAL __attribute__((address_space(1)))
+#else
+#define IK_GLOBAL
 #endif
 
 namespace ik {
@@ -542,6 +553,378 @@ IK_HD int resolve_at(U16 u16, Off lane_obase, int n, Pages page_lane, int page_s
         if (q < 0) return -1;
     }
     return -1;
+}
+
+
+// ---- canonical decoding, code-length limits in registers --------------------
+// The GPU decoder lanes keep per-code tables tiny so that many waves fit a CU:
+// for each code (literal/length, distance) the 15 left-justified limits live in
+// registers, and a few small per-length tables live in LDS.
+//   lim[L-1] (L = 1..15): exclusive upper bound of the codes of length <= L, as
+//   15-bit MSB-first values.  For the next 15 stream bits W (bit-reversed: the
+//   first bit read is the MSB), the code length is 1 + #{L < 15 : W >= lim[L-1]};
+//   W >= lim[14] is no code (an incomplete code's gap).
+// Canonical order within a length is by symbol value, so for the literal/length
+// code a length's codes are: its literals, then end-of-block, then length codes.
+// Table memory per lane (u32 words, CanonMem):
+//   [0..15]  linfo[L]: first code (15 bits) | #literals of length L (9) << 15
+//                      | EOB has length L (1) << 24 | rank of its first length code (5) << 25
+//   [16..31] lrank[L]: rank of its first literal (9 bits)
+//   [32..47] dinfo[L]: first code (15 bits) | rank of its first distance code (5) << 16
+//   bytes from word 48: lsyms[32] (length symbol - 257), dsyms[32], lits[256] (in canonical order)
+constexpr int kCanonWords = 48 + 8 + 8 + 64;  // 512 bytes
+constexpr int kCanonCountWords = 48 + 8 + 8;  // the count pass needs no literal values: 256 bytes
+struct CanonRegs {
+    uint32_t lpk[8], dpk[8];  // limits minus one, packed in signed 16-bit pairs (canon_len)
+};
+IK_HD void pack_limits(const uint32_t (&lim)[15], uint32_t (&pk)[8]) {
+    for (int k = 0; k < 7; ++k)
+        pk[k] = ((lim[2 * k] - 1u) & 0xFFFFu) | (((lim[2 * k + 1] - 1u) & 0xFFFFu) << 16);
+    pk[7] = (lim[14] - 1u) & 0xFFFFu;
+}
+
+IK_HD uint32_t rev32(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_bitreverse32(v);
+#else
+    v = ((v >> 1) & 0x55555555u) | ((v & 0x55555555u) << 1);
+    v = ((v >> 2) & 0x33333333u) | ((v & 0x33333333u) << 2);
+    v = ((v >> 4) & 0x0F0F0F0Fu) | ((v & 0x0F0F0F0Fu) << 4);
+    v = ((v >> 8) & 0x00FF00FFu) | ((v & 0x00FF00FFu) << 8);
+    return (v >> 16) | (v << 16);
+#endif
+}
+
+IK_HD uint8_t cm_byte(const uint32_t* m, int i) { return (uint8_t)(m[48 + (i >> 2)] >> (8 * (i & 3))); }
+
+// Build both codes' limits and tables (lens: literal/length lengths [0, nlen),
+// distance lengths at 288..).  lits: also the literal table (emit pass).
+template <class Mem>
+IK_HD_COLD void canon_build(const uint8_t* lens, int nlen, int ndist, bool lits, CanonRegs& R, Mem m) {
+    // literal/length code
+    uint32_t cnt[16], first[16], llim[15], dlim[15];
+    for (int l = 0; l < 16; ++l) cnt[l] = 0;
+    for (int s = 0; s < nlen; ++s) cnt[lens[s]]++;
+    uint32_t code = 0;
+    for (int l = 1; l <= 15; ++l) {
+        code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1;
+        first[l] = code;
+        llim[l - 1] = (first[l] + cnt[l]) << (15 - l);
+    }
+    for (int i = 0; i < 16; ++i) m[48 + i] = 0;  // lsyms, dsyms
+    uint32_t litr = 0, lenr = 0;
+    uint32_t lrank_of[16];
+    lrank_of[0] = 0;
+    for (int l = 1; l <= 15; ++l) {
+        uint32_t nl = 0, nlen_codes = 0, eob = 0;
+        for (int s = 0; s < nlen && s < 286; ++s) {
+            if (lens[s] != l) continue;
+            if (s < 256) {
+                if (lits) {
+                    const int w = 64 + (int)(litr + nl);
+                    m[48 + w / 4] = (m[48 + w / 4] & ~(255u << (8 * (w & 3)))) | ((uint32_t)s << (8 * (w & 3)));
+                }
+                ++nl;
+            } else if (s == 256) {
+                eob = 1;
+            } else {
+                const int w = (int)(lenr + nlen_codes);
+                if (w < 32)
+                    m[48 + w / 4] = (m[48 + w / 4] & ~(255u << (8 * (w & 3)))) | ((uint32_t)(s - 257) << (8 * (w & 3)));
+                ++nlen_codes;
+            }
+        }
+        m[l] = (first[l] & 0x7FFFu) | (nl << 15) | (eob << 24) | (lenr << 25);
+        m[16 + l] = litr;  // (kept for the layout; the decoder reads the copy in dinfo)
+        lrank_of[l] = litr;
+        litr += nl;
+        lenr += nlen_codes;
+    }
+    // distance code
+    for (int l = 0; l < 16; ++l) cnt[l] = 0;
+    for (int s = 0; s < ndist; ++s) cnt[lens[288 + s]]++;
+    code = 0;
+    uint32_t dr = 0;
+    for (int l = 1; l <= 15; ++l) {
+        code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1;
+        dlim[l - 1] = (code + cnt[l]) << (15 - l);
+        m[32 + l] = (code & 0x7FFFu) | (dr << 16) | (lrank_of[l] << 21);
+        for (int s = 0; s < ndist; ++s) {
+            if (lens[288 + s] != l) continue;
+            const int w = 32 + (int)dr;
+            if (dr < 32) m[48 + w / 4] = (m[48 + w / 4] & ~(255u << (8 * (w & 3)))) | ((uint32_t)s << (8 * (w & 3)));
+            ++dr;
+        }
+    }
+    pack_limits(llim, R.lpk);
+    pack_limits(dlim, R.dpk);
+}
+
+// code length for a 15-bit window; 16 = no code.  pk[k] holds lim[2k]-1 and
+// lim[2k+1]-1 as two signed 16-bit halves (pk[7]: lim[14]-1), so one packed
+// 16-bit subtract compares the window with two limits at once and the sign bits
+// count the limits at or below it (v_pk_sub_i16 + v_bcnt).
+IK_HD int canon_len(uint32_t c15, const uint32_t (&pk)[8]) {
+    uint32_t at_or_below = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef short s2 __attribute__((ext_vector_type(2)));
+    const s2 x = {(short)c15, (short)c15};
+    IK_UNROLL
+    for (int k = 0; k < 7; ++k) {
+        const s2 d = __builtin_bit_cast(s2, pk[k]) - x;  // lim - 1 - c15 < 0  <=>  lim <= c15
+        at_or_below += (uint32_t)__builtin_popcount(__builtin_bit_cast(uint32_t, d) & 0x80008000u);
+    }
+#else
+    for (int k = 0; k < 7; ++k) {
+        at_or_below += (int16_t)(pk[k] & 0xFFFFu) - (int)c15 < 0 ? 1u : 0u;
+        at_or_below += (int16_t)(pk[k] >> 16) - (int)c15 < 0 ? 1u : 0u;
+    }
+#endif
+    return (int)c15 > (int16_t)(pk[7] & 0xFFFFu) ? 16 : 1 + (int)at_or_below;
+}
+
+// Output of the emit pass: u16 symbols in global memory (or a host buffer).
+struct U16Out {
+    IK_GLOBAL uint16_t* p;
+    IK_HD uint16_t load(int64_t i) const { return p[i]; }
+    IK_HD void store1(int64_t i, uint16_t v) const { p[i] = v; }
+    IK_HD void store16(int64_t i, uint64_t lo, uint64_t hi) const {  // 8 symbols at i (a multiple of 8)
+        IK_GLOBAL uint64_t* q = reinterpret_cast<IK_GLOBAL uint64_t*>(p + i);
+        q[0] = lo;
+        q[1] = hi;
+    }
+};
+struct NoOut {
+    IK_HD uint16_t load(int64_t) const { return 0; }
+    IK_HD void store1(int64_t, uint16_t) const {}
+    IK_HD void store16(int64_t, uint64_t, uint64_t) const {}
+};
+
+// Input window of the hot loop: the three words holding the next 64+ bits
+// (a, b, c) and two prefetched ones (d, e).  After each symbol the window
+// slides by 0..2 words, choosing from registers, and the two words after it are
+// loaded for the NEXT symbol -- every load has a whole symbol of latency to
+// hide, and none sits behind a per-lane branch (a wave's vmcnt is shared by
+// its lanes).
+struct Win {
+    const IK_GLOBAL uint32_t* w;
+    uint32_t wend, wi, pos;  // streams under 2^32 bits (the host checks)
+    uint32_t a, b, c, d, e;
+    IK_HD uint32_t rd(uint32_t i) const { return i < wend ? w[i] : 0u; }
+    IK_HD void init(const IK_GLOBAL uint32_t* words, uint32_t nwords, uint32_t bit) {
+        w = words;
+        wend = nwords;
+        pos = bit;
+        wi = bit >> 5;
+        a = rd(wi); b = rd(wi + 1); c = rd(wi + 2); d = rd(wi + 3); e = rd(wi + 4);
+    }
+    IK_HD uint64_t bits64() const {  // the next 64 stream bits
+        const uint32_t sh = pos & 31u;
+        const uint64_t lo = (uint64_t)a | ((uint64_t)b << 32);
+        return sh ? (lo >> sh) | ((uint64_t)c << (64 - sh)) : lo;
+    }
+    // x0 / x1 / x2 for dd = 0 / 1 / 2, with masks (a ternary chain becomes an
+    // indexed private array, i.e. scratch memory)
+    IK_HD static uint32_t sel3(uint32_t m1, uint32_t m2, uint32_t x0, uint32_t x1, uint32_t x2) {
+        return (x0 & ~m1) | (x1 & m1 & ~m2) | (x2 & m2);
+    }
+    IK_HD void tick() {}  // (the LDS window refills its ring here)
+    IK_HD void advance(uint32_t k) {  // k <= 64
+        pos += k;
+        const uint32_t nwi = pos >> 5;
+        const uint32_t dd = nwi - wi;  // 0, 1 or 2
+        const uint32_t m1 = 0u - (uint32_t)(dd >= 1), m2 = 0u - (uint32_t)(dd >= 2);
+        const uint32_t d2 = rd(nwi + 3);  // needed only when dd == 2; a cached, independent load
+        const uint32_t na = sel3(m1, m2, a, b, c);
+        const uint32_t nb = sel3(m1, m2, b, c, d);
+        const uint32_t nc = sel3(m1, m2, c, d, e);
+        const uint32_t nd = sel3(m1, m2, d, e, d2);
+        wi = nwi;
+        a = na; b = nb; c = nc; d = nd;
+        e = rd(nwi + 4);
+    }
+};
+
+// Decoder lane with canonical decoding: the GPU kernels' decoder, same contract
+// as decode_lane.  m: this lane's table memory (kCanonWords u32; the count pass
+// kCanonCountWords).  EMIT: the last 8 output symbols live in two 64-bit
+// registers (h0: distances 8..5, h1: 4..1, newest in the top 16 bits), which
+// serve every copy with distance <= 8 and are written out as one aligned 16-byte
+// store each time the output position reaches a multiple of 8 -- so the loop
+// issues few stores, and copies from farther back only read flushed symbols.
+template <bool EMIT, class WinT, class Mem, class Out>
+IK_HD void decode_lane_canon(const uint32_t* words, uint64_t nbits, uint64_t start, uint64_t stop, Mem m, Out out,
+                             int64_t obase, uint64_t out_cap, LaneResult& r, WinT W) {
+    const uint64_t nwords = (nbits >> 5) + 4;
+    Bits b;
+    b.init(words, start, nwords);
+    const uint64_t plimit = nbits + 64;  // decoding past the stream's padding: corrupt
+    uint64_t cnt = 0;
+    uint64_t h0 = 0, h1 = 0;
+    r.status = kLaneCorrupt;
+    r.final_block = 0;
+    uint8_t lens[288 + 32];
+    CanonRegs R;
+    // append one symbol (EMIT): history push, aligned 16-byte store at each multiple of 8
+    auto put = [&](uint32_t v) {
+        h0 = (h0 >> 16) | (h1 << 48);
+        h1 = (h1 >> 16) | ((uint64_t)v << 48);
+        ++cnt;
+        const int64_t g = obase + (int64_t)cnt;
+        if ((g & 7) == 0) {
+            if ((int64_t)cnt >= 8) {
+                out.store16(g - 8, h0, h1);
+            } else {  // the group starts before this lane's first symbol: only ours
+                for (int64_t q = g - (int64_t)cnt; q < g; ++q) {
+                    const int dq = (int)(g - q);  // distance 1..7
+                    const uint32_t hv = (uint32_t)((dq <= 4 ? h1 >> (16 * (4 - dq)) : h0 >> (16 * (8 - dq)))) & 0xFFFFu;
+                    out.store1(q, (uint16_t)hv);
+                }
+            }
+        }
+    };
+    auto hist = [&](int d) -> uint32_t {  // the symbol d back (1..8)
+        return (uint32_t)((d <= 4 ? h1 >> (16 * (4 - d)) : h0 >> (16 * (8 - d)))) & 0xFFFFu;
+    };
+    for (;;) {
+        const uint64_t p = b.pos();
+        if (p >= stop) {
+            r.status = p == stop ? kLaneOk : kLaneMismatch;
+            break;
+        }
+        if (p + 3 > nbits) break;
+        b.refill();
+        const uint32_t hdr = b.peek(3);
+        b.drop(3);
+        const int bfinal = (int)(hdr & 1u), btype = (int)(hdr >> 1);
+        if (btype == 0) {  // stored
+            b.drop(b.n & 7);
+            const uint32_t len = b.get(16), nlen = b.get(16);
+            if ((len ^ 0xFFFFu) != nlen) break;
+            if (cnt + len > out_cap) break;
+            if (b.pos() + 8ull * len > nbits) break;
+            for (uint32_t i = 0; i < len; ++i) {
+                const uint32_t v = b.get(8);
+                if (EMIT) put(v);
+                else ++cnt;
+            }
+        } else if (btype == 3) {
+            break;
+        } else {
+            int nlen, ndist;
+            {
+                CodeInfo lci, dci;
+                if (btype == 2) {
+                    Bits hb = b;  // out-of-line parser on a copy: the hot state stays in registers
+                    const int prc = parse_dynamic(hb, lens, nlen, ndist, lci, dci);
+                    b = hb;
+                    if (prc) break;
+                    for (int i = ndist - 1; i >= 0; --i) lens[288 + i] = lens[nlen + i];
+                } else {
+                    fixed_lens(lens);
+                    nlen = 288;
+                    ndist = 30;
+                }
+                CanonRegs t;
+                canon_build(lens, nlen, ndist, EMIT, t, m);
+                R = t;
+            }
+            W.init((const IK_GLOBAL uint32_t*)words, (uint32_t)nwords, (uint32_t)b.pos());
+            bool bad = false;
+            for (;;) {
+                if ((uint64_t)W.pos > plimit) { bad = true; break; }
+                W.tick();
+                uint64_t v = W.bits64();
+                uint32_t k = 0;  // bits consumed by this symbol
+                const uint32_t c15 = rev32((uint32_t)v) >> 17;
+                const int len = canon_len(c15, R.lpk);
+                if (len > 15) { bad = true; break; }
+                const uint32_t info = m[len];
+                const uint32_t i = (c15 >> (15 - len)) - (info & 0x7FFFu);
+                const uint32_t nl = (info >> 15) & 0x1FFu;
+                v >>= len;
+                k += (uint32_t)len;
+                if (i < nl) {  // literal
+                    if (cnt >= out_cap) { bad = true; break; }
+                    if (EMIT) put(cm_byte(m, 64 + (int)((m[32 + len] >> 21) + i)));
+                    else ++cnt;
+                    W.advance(k);
+                    continue;
+                }
+                uint32_t j = i - nl;
+                if ((info >> 24) & 1u) {
+                    if (j == 0) { W.advance(k); break; }  // end of block
+                    --j;
+                }
+                const uint32_t lr = ((info >> 25) & 31u) + j;
+                if (lr > 28u) { bad = true; break; }  // 286/287
+                const int lsym = (int)cm_byte(m, (int)lr);
+                const int le = len_extra(257 + lsym);
+                const int ll = len_base(257 + lsym) + (int)((uint32_t)v & ((1u << le) - 1u));
+                v >>= le;
+                k += (uint32_t)le;
+                const uint32_t c15d = rev32((uint32_t)v) >> 17;
+                const int dl = canon_len(c15d, R.dpk);
+                if (dl > 15) { bad = true; break; }
+                const uint32_t dinfo = m[32 + dl];
+                const uint32_t di = ((c15d >> (15 - dl)) - (dinfo & 0x7FFFu)) + ((dinfo >> 16) & 31u);
+                if (di > 29u) { bad = true; break; }
+                v >>= dl;
+                k += (uint32_t)dl;
+                const int ds = (int)cm_byte(m, 32 + (int)di);
+                const int de = dist_extra(ds);
+                const int dist = dist_base(ds) + (int)((uint32_t)v & ((1u << de) - 1u));
+                k += (uint32_t)de;
+                if (cnt + (uint64_t)ll > out_cap) { bad = true; break; }
+                if (obase >= 0 && (int64_t)cnt + obase < dist) { bad = true; break; }
+                if (EMIT) {
+                    int q = 0;
+                    // sources before this lane's first symbol (window markers), or in the
+                    // history registers (distance <= 8: the registers roll as we copy)
+                    while (q < ll) {
+                        const int64_t sk = (int64_t)cnt - dist;
+                        if (sk < 0) put(0x8000u | (uint32_t)(kWindow + sk));
+                        else if (dist <= 8) put(hist(dist));
+                        else break;
+                        ++q;
+                    }
+                    // distance > 8: every source is at least 8 back, so already stored; in
+                    // groups of up to min(8, dist - 8) the loads go out together
+                    const int G = dist - 8 < 8 ? dist - 8 : 8;
+                    while (q < ll) {
+                        const int n = ll - q < G ? ll - q : G;
+                        const int64_t s0 = obase + (int64_t)cnt - dist;
+                        uint32_t vv[8];
+                        IK_UNROLL
+                        for (int t2 = 0; t2 < 8; ++t2) vv[t2] = t2 < n ? (uint32_t)out.load(s0 + t2) : 0u;
+                        IK_UNROLL
+                        for (int t2 = 0; t2 < 8; ++t2)
+                            if (t2 < n) put(vv[t2]);
+                        q += n;
+                    }
+                } else {
+                    cnt += (uint64_t)ll;
+                }
+                W.advance(k);
+            }
+            if (bad) break;
+            b.init(words, W.pos, nwords);
+        }
+        if (b.pos() > nbits + 64) break;
+        if (bfinal) {
+            r.final_block = 1;
+            r.status = stop == ~0ull ? kLaneOk : kLaneMismatch;
+            break;
+        }
+    }
+    // EMIT: the symbols after the last multiple of 8 are still only in the history
+    if (EMIT) {
+        const int64_t g = obase + (int64_t)cnt;
+        const int64_t q0 = g - (int64_t)(g & 7) > obase ? g - (int64_t)(g & 7) : obase;
+        for (int64_t q = q0; q < g; ++q) out.store1(q, (uint16_t)hist((int)(g - q)));
+    }
+    r.end_bit = b.pos();
+    r.out_len = cnt;
 }
 
 }  // namespace infl

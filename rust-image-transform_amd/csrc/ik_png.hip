@@ -4,7 +4,7 @@
 // DEFLATE core and the algorithm are in ik_inflate.h.
 //
 //   k_png_find      one wave per (chunk, image): the first plausible dynamic
-//                   block header in the chunk (64 bit offsets per wave step)
+//                   block header in the chunk (2,048 bit offsets per wave step)
 //   k_png_inflate   one thread per decoder lane: whole blocks from its start to
 //                   the next lane's start; count pass (lengths) or emit pass
 //                   (u16 symbols with window markers).  Root Huffman tables live
@@ -28,9 +28,45 @@
 namespace ik {
 
 // ---- find ------------------------------------------------------------------------
+// One wave per (chunk, image).  A lane owns one 32-bit stream word, i.e. 32
+// consecutive bit offsets, so a wave step covers 2,048 offsets from 64
+// coalesced word loads (prefetched one step ahead).  The cheap header tests run
+// bit-parallel over the lane's 32 offsets on shifted copies of its 128-bit
+// window -- BTYPE = 2 (bit 1 clear, bit 2 set), HLIT <= 29 and HDIST <= 29 (not
+// all of their top four bits set) -- and only the survivors (about a fifth)
+// take the scalar Kraft test of the code-length code (complete: sum 2^-len == 1).
+// Offsets passing it (~0.1 %: under two per wave step) go into a per-wave LDS
+// queue, and the streaming header check (ik_inflate.h dynamic_header_ok, LDS
+// code-length table per lane) runs on 64 queued offsets at a time, one per
+// lane -- run one by one as they turn up, it would take the whole wave for one
+// or two active lanes.  The result is the first offset of the chunk that passes
+// every test, as before: the queue is checked whenever it holds 64 offsets and at
+// the end of the chunk, and once some offset passed, the smallest passing one of
+// everything checked so far is the answer.
+__device__ __attribute__((noinline)) bool find_full_check(const uint32_t* words, uint64_t nbits, uint64_t p,
+                                                          uint32_t h, uint64_t bits, uint8_t* tab) {
+    return infl::dynamic_header_ok(words, nbits, p, h, bits, tab);
+}
+
+__device__ __forceinline__ uint32_t fsh(uint32_t lo, uint32_t hi, int k) {  // bits k .. k+31 of hi:lo, 0 < k < 32
+    return (lo >> k) | (hi << (32 - k));
+}
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t u = (uint32_t)__shfl_xor((int)v, o, 64);
+        v = u < v ? u : v;
+    }
+    return v;
+}
+
+constexpr uint32_t kFindQueue = 128;
+
 __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const int* chunk_img, const int* chunk_idx,
                                                  int nchunks_total, uint64_t chunk_bits, int64_t* cand) {
-    __shared__ uint8_t s_tab[64 * 128];  // per lane: code-length code lookup (symbol | length << 5)
+    __shared__ uint8_t s_tab[64 * 128];     // per lane: code-length code lookup (symbol | length << 5)
+    __shared__ uint32_t s_q[kFindQueue];    // Kraft-passing offsets (relative to the chunk) awaiting the full check
     const int g = blockIdx.x;
     if (g >= nchunks_total) return;
     const int im = chunk_img[g];
@@ -43,62 +79,199 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
         return;
     }
     const int lane = threadIdx.x;
-    int64_t found = -1;
-    for (uint64_t base = b0; base < b1; base += 64) {
-        const uint64_t p = base + lane;
-        bool ok = false;
-        if (p < b1) {
-            // quick filters on 17 header bits, then the precode's completeness,
-            // then the full header parse (rare)
-            const uint64_t wi = p >> 5;
-            const uint64_t v = ((uint64_t)I.words[wi] | ((uint64_t)I.words[wi + 1] << 32)) >> (p & 31);
-            const uint32_t h = (uint32_t)v;
-            if (((h >> 1) & 3u) == 2u && ((h >> 3) & 31u) <= 29u && ((h >> 8) & 31u) <= 29u) {
-                const int ncode = (int)((h >> 13) & 15u) + 4;
-                // precode lengths: up to 57 bits from bit 17
-                const uint64_t q = p + 17;
-                const uint64_t qi = q >> 5;
-                const uint32_t sh = (uint32_t)(q & 31);
-                const uint64_t lo = (uint64_t)I.words[qi] | ((uint64_t)I.words[qi + 1] << 32);
-                const uint64_t hi = (uint64_t)I.words[qi + 2];
-                const uint64_t bits = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
-                int kraft = 0, nz = 0;
-                for (int i = 0; i < ncode; ++i) {
-                    const int l = (int)((bits >> (3 * i)) & 7u);
-                    if (l) { kraft += 128 >> l; ++nz; }
-                }
-                if (kraft == 128 && nz)
-                    ok = infl::dynamic_header_ok(I.words, I.nbits, p, h, bits, s_tab + 128 * lane);
+    const IK_GLOBAL uint32_t* W = (const IK_GLOBAL uint32_t*)I.words;
+    uint32_t qlen = 0;           // wave-uniform
+    uint32_t best = 0xFFFFFFFFu; // smallest passing offset checked so far (relative to b0)
+    auto flush = [&]() {
+        for (uint32_t q0 = 0; q0 < qlen; q0 += 64) {
+            uint32_t v = 0xFFFFFFFFu;
+            if (q0 + (uint32_t)lane < qlen) {
+                const uint32_t off = s_q[q0 + lane];
+                const uint64_t p = b0 + off;
+                const uint64_t wi = p >> 5;
+                const uint32_t sh = (uint32_t)(p & 31);
+                const uint64_t lo = (uint64_t)W[wi] | ((uint64_t)W[wi + 1] << 32);
+                const uint64_t hi = (uint64_t)W[wi + 2] | ((uint64_t)W[wi + 3] << 32);
+                const uint64_t x = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;   // bits p .. p+63
+                const uint64_t x2 = sh ? (hi >> sh) : hi;                        // bits p+64 ..
+                const uint64_t cl = (x >> 17) | (x2 << 47);
+                if (find_full_check(I.words, I.nbits, p, (uint32_t)x, cl, s_tab + 128 * lane)) v = off;
             }
+            v = wave_min(v);
+            best = v < best ? v : best;
         }
-        const unsigned long long m = __ballot(ok);
-        if (m) {
-            found = (int64_t)(base + (uint64_t)__ffsll((long long)m) - 1);
-            break;
+        qlen = 0;
+    };
+    const uint64_t wlast = (b1 + 31) >> 5;  // words holding offsets < b1 (the stream is zero padded past them)
+    uint64_t wi = (b0 >> 5) + (uint64_t)lane;
+    uint32_t n0 = W[wi], n1 = W[wi + 1], n2 = W[wi + 2], n3 = W[wi + 3];
+    for (;;) {
+        const uint32_t w0 = n0, w1 = n1, w2 = n2, w3 = n3;
+        const uint64_t wn = wi + 64;
+        if (wn - (uint64_t)lane < wlast) {  // wave-uniform: prefetch the next step's words
+            n0 = W[wn]; n1 = W[wn + 1]; n2 = W[wn + 2]; n3 = W[wn + 3];
         }
+        // bit-parallel filters over offsets p = 32 wi + j, j = 0..31
+        uint32_t m = ~fsh(w0, w1, 1) & fsh(w0, w1, 2);                                          // BTYPE == 2
+        m &= ~(fsh(w0, w1, 4) & fsh(w0, w1, 5) & fsh(w0, w1, 6) & fsh(w0, w1, 7));             // HLIT <= 29
+        m &= ~(fsh(w0, w1, 9) & fsh(w0, w1, 10) & fsh(w0, w1, 11) & fsh(w0, w1, 12));           // HDIST <= 29
+        const uint64_t pw = wi << 5;
+        if (pw < b0) m &= b0 - pw >= 32 ? 0u : ~0u << (uint32_t)(b0 - pw);
+        if (pw + 32 > b1) m &= pw >= b1 ? 0u : (1u << (uint32_t)(b1 - pw)) - 1u;
+        const uint64_t lo = (uint64_t)w0 | ((uint64_t)w1 << 32), hi = (uint64_t)w2 | ((uint64_t)w3 << 32);
+        uint32_t km = 0;  // offsets passing the Kraft test
+        while (m) {
+            const uint32_t j = (uint32_t)__builtin_ctz(m);
+            m &= m - 1u;
+            const uint32_t h = (uint32_t)(lo >> j);
+            const uint32_t sh = j + 17;  // 17 .. 48
+            const uint64_t cl = (lo >> sh) | (hi << (64 - sh));  // code-length code lengths (57 bits)
+            const int ncode = (int)((h >> 13) & 15u) + 4;
+            const uint64_t used = cl & (ncode == 19 ? 0x1FFFFFFFFFFFFFFull : ((1ull << (3 * ncode)) - 1ull));
+            uint32_t kraft = 0;
+            IK_UNROLL
+            for (int i = 0; i < 19; ++i) {
+                const uint32_t l = (uint32_t)(used >> (3 * i)) & 7u;
+                kraft += l ? (128u >> l) : 0u;
+            }
+            if (kraft == 128u) km |= 1u << j;
+        }
+        // queue them: one per lane per round, compacted by lane rank
+        for (;;) {
+            const unsigned long long bal = __ballot(km != 0);
+            if (!bal) break;
+            if (qlen + 64 > kFindQueue) flush();
+            if (km) {
+                const uint32_t j = (uint32_t)__builtin_ctz(km);
+                km &= km - 1u;
+                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                s_q[qlen + r] = (uint32_t)(pw + j - b0);
+            }
+            qlen += (uint32_t)__popcll(bal);
+        }
+        if (qlen >= 64) flush();
+        if (best != 0xFFFFFFFFu) break;  // (flush below checks what this step queued after it)
+        wi = wn;
+        if (wi - (uint64_t)lane >= wlast) break;
     }
-    if (lane == 0) cand[g] = found;
+    flush();
+    if (lane == 0) cand[g] = best == 0xFFFFFFFFu ? -1 : (int64_t)(b0 + best);
 }
 
 // ---- inflate ------------------------------------------------------------------------
+// One thread per decoder lane, canonical decoding (ik_inflate.h decode_lane_canon):
+// the code-length limits sit in registers and the small per-length tables in
+// LDS.  The lane's compressed stream reaches the hot loop through a ring of
+// four 32-byte blocks per lane in LDS, filled by LDS-DMA (global_load_lds_dwordx4)
+// on a fixed schedule: every kRingTick symbols the lane waits for the DMAs it
+// issued last time (vmcnt(0): they are a full interval old) and issues the
+// block three ahead of the one it reads.  The loop itself then reads only LDS,
+// so no lane's memory latency stalls its wave (a wave's vmcnt is shared by its
+// 64 lanes).
+constexpr int kRingBW = 8;    // words per block (32 B, two 16-B DMA slots)
+constexpr int kRingTick = 4;  // symbols between refills (< 256 bits: at most one block per interval)
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+struct WinLds {
+    const IK_GLOBAL uint32_t* w;
+    uint32_t nwords, pos, nextb, it;
+    lds_u32* ring;   // this wave's ring: [block % 4][slot][lane][4 words]
+    uint32_t lane;
+    __device__ uint32_t word(uint32_t wi) const {
+        const uint32_t B = wi / kRingBW, sl = (wi % kRingBW) >> 2, q = wi & 3u;
+        return ring[(((B & 3u) * (kRingBW / 4) + sl) * 64u + lane) * 4u + q];
+    }
+    // One 16-byte LDS-DMA of each lane's source into ring slot `base` (byte address in
+    // LDS; lane L lands at base + 16 L).  M0 carries the base, written in the same
+    // statement (the compiler does not preserve it around asm), and each slot has
+    // its own asm text: identical statements in the four branches below would be
+    // merged into one with a per-lane base -- which M0 cannot hold.
+#define IK_GLDS16(TAG)                                                                                 \
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t" \
+                 "s_mov_b32 m0, %0 ; ring " TAG                                                        \
+                 : "=&s"(keep)                                                                         \
+                 : "v"(src), "s"(base)                                                                 \
+                 : "memory")
+    __device__ void dma(uint32_t B) {  // block B of the calling lanes into ring position B % 4
+        static_assert(kRingBW == 8, "two 16-byte slots per block");
+        const IK_GLOBAL uint32_t* g = w + (size_t)B * kRingBW;
+        const uint32_t r0 = (uint32_t)(size_t)ring;
+        uint32_t keep;
+        const IK_GLOBAL uint32_t* src;
+        uint32_t base;
+        switch (B & 3u) {
+        case 0:
+            src = g; base = r0 + 0 * 1024; IK_GLDS16("0a");
+            src = g + 4; base = r0 + 1 * 1024; IK_GLDS16("0b");
+            break;
+        case 1:
+            src = g; base = r0 + 2 * 1024; IK_GLDS16("1a");
+            src = g + 4; base = r0 + 3 * 1024; IK_GLDS16("1b");
+            break;
+        case 2:
+            src = g; base = r0 + 4 * 1024; IK_GLDS16("2a");
+            src = g + 4; base = r0 + 5 * 1024; IK_GLDS16("2b");
+            break;
+        default:
+            src = g; base = r0 + 6 * 1024; IK_GLDS16("3a");
+            src = g + 4; base = r0 + 7 * 1024; IK_GLDS16("3b");
+            break;
+        }
+    }
+#undef IK_GLDS16
+    __device__ void init(const IK_GLOBAL uint32_t* words, uint32_t nw, uint32_t bit) {
+        w = words;
+        nwords = nw;
+        pos = bit;
+        it = 0;
+        const uint32_t B0 = (bit >> 5) / kRingBW;
+        for (uint32_t k = 0; k < 4; ++k) dma(B0 + k);
+        nextb = B0 + 4;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __device__ void tick() {
+        if (++it % kRingTick) return;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // last interval's DMA has landed
+        if (nextb <= ((pos >> 5) / kRingBW) + 3u) {
+            dma(nextb);
+            ++nextb;
+        }
+    }
+    __device__ uint64_t bits64() const {
+        const uint32_t wi = pos >> 5, sh = pos & 31u;
+        const uint32_t a = word(wi), b = word(wi + 1), c = word(wi + 2);
+        const uint64_t lo = (uint64_t)a | ((uint64_t)b << 32);
+        return sh ? (lo >> sh) | ((uint64_t)c << (64 - sh)) : lo;
+    }
+    __device__ void advance(uint32_t k) { pos += k; }
+};
+
 template <bool EMIT>
 __global__ __launch_bounds__(kPngInflateThreads) void k_png_inflate(const PngImgDev* imgs, const PngLaneDev* lanes,
                                                                      int nlanes, uint16_t* sub_ws,
                                                                      infl::LaneResult* res) {
-    __shared__ uint16_t s_root[kPngInflateThreads * (infl::kLitRootN + infl::kDistRootN)];
+    constexpr int W = EMIT ? infl::kCanonWords : infl::kCanonCountWords;
+    __shared__ uint32_t s_tab[kPngInflateThreads * W];
+    __shared__ uint32_t s_ring[4 * (kRingBW / 4) * 64 * 4];  // 4 blocks x 32 B per lane (one wave)
     const int t = blockIdx.x * kPngInflateThreads + threadIdx.x;
     if (t >= nlanes) return;
     const PngLaneDev L = lanes[t];
     const PngImgDev I = imgs[L.img];
-    uint16_t* lroot = s_root + threadIdx.x * (infl::kLitRootN + infl::kDistRootN);
-    uint16_t* droot = lroot + infl::kLitRootN;
-    uint16_t* lsub = sub_ws + (size_t)L.slot * (infl::kLitSub + infl::kDistSub);
-    uint16_t* dsub = lsub + infl::kLitSub;
+    uint32_t* m = s_tab + threadIdx.x * W;
+    WinLds win;
+    win.ring = (lds_u32*)s_ring;
+    win.lane = threadIdx.x;
     infl::LaneResult r;
     const uint64_t cap = EMIT ? I.raw_total - (uint64_t)L.obase : I.raw_total;
-    infl::decode_lane<EMIT>(I.words, I.nbits, L.start, L.stop, lroot, lsub, droot, dsub, I.u16,
-                            EMIT ? L.obase : (L.first ? 0 : -1), cap, r);
+    if (EMIT)
+        infl::decode_lane_canon<true>(I.words, I.nbits, L.start, L.stop, m,
+                                      infl::U16Out{(IK_GLOBAL uint16_t*)I.u16}, L.obase, cap, r, win);
+    else
+        infl::decode_lane_canon<false>(I.words, I.nbits, L.start, L.stop, m, infl::NoOut{}, L.first ? 0 : -1, cap, r,
+                                       win);
     res[t] = r;
+    (void)sub_ws;
 }
 
 // ---- resolve ------------------------------------------------------------------------

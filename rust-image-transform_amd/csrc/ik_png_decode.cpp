@@ -122,8 +122,11 @@ double now_ms() {
 
 // the last batch's stage times on this thread (ik_png_last_timing): host parse +
 // staging, then device ms of find / count (all rounds) / emit / resolve / unfilter
-// from HIP events on the thread's stream, wall ms, rounds, lanes, GPU streams
-thread_local double t_png_timing[10];
+// from HIP events on the thread's stream, wall ms, rounds, lanes, streams sent to
+// the GPU, streams the GPU decoded (verified), streams the host decoder took
+thread_local double t_png_timing[12];
+// process-wide: PNG streams decoded by the GPU path / by the host decoder
+std::atomic<unsigned long long> g_png_gpu_streams{0}, g_png_host_streams{0};
 struct Events {
     hipEvent_t e[12] = {};
     bool ok = false;
@@ -200,7 +203,7 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             j->chunk0 = nchunks;
             nchunks += j->nchunks;
             j->o_words = total;
-            total += up256(((j->zlen + 3) & ~size_t(3)) + 64);  // 4 zero words past the end (Bits::wend)
+            total += up256(((j->zlen + 3) & ~size_t(3)) + 512);  // zero padding: Bits::wend, the LDS ring's DMAs
             j->o_u16 = total;
             total += up256(2 * (j->raw_total + 64));
             j->o_ft = total;
@@ -281,7 +284,7 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                 ctab[2 * (size_t)(j.chunk0 + c)] = k;
                 ctab[2 * (size_t)(j.chunk0 + c) + 1] = c;
             }
-            hipError_t e = hipMemsetAsync(dev + j.o_words + ((j.zlen + 3) & ~size_t(3)), 0, 64, s);
+            hipError_t e = hipMemsetAsync(dev + j.o_words + ((j.zlen + 3) & ~size_t(3)), 0, 512, s);
             if (e == hipSuccess)
                 e = hipMemcpyAsync(dev + j.o_words, pin + j.z_off, (j.zlen + 3) & ~size_t(3), hipMemcpyHostToDevice, s);
             if (e != hipSuccess) rc = hip_fail(e, "PNG stream upload");
@@ -508,6 +511,10 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
     std::vector<int> host;
     for (int i = 0; i < n; ++i)
         if (!gpu[i]) host.push_back(i);
+    t_png_timing[11] = (double)host.size();
+    t_png_timing[10] = (double)(n - (int)host.size());
+    g_png_gpu_streams += (unsigned long long)(n - (int)host.size());
+    g_png_host_streams += (unsigned long long)host.size();
     parallel_for((int)host.size(), 0, [&](int k) {
         const int i = host[k];
         thread_local std::vector<uint8_t> px;
@@ -531,8 +538,14 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
 
 }  // namespace ik
 
+extern "C" int ik_png_counters(unsigned long long* out) {
+    out[0] = ik::g_png_gpu_streams.load();
+    out[1] = ik::g_png_host_streams.load();
+    return IK_OK;
+}
+
 extern "C" int ik_png_last_timing(double* out, int n) {
-    for (int i = 0; i < n && i < 10; ++i) out[i] = ik::t_png_timing[i];
+    for (int i = 0; i < n && i < 12; ++i) out[i] = ik::t_png_timing[i];
     return IK_OK;
 }
 

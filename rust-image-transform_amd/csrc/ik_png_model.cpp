@@ -69,12 +69,17 @@ int ikm_inflate_chunked(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8
     pngplan::build(cand, L);
     const size_t nl0 = L.start.size();
     uint16_t lroot[infl::kLitRootN], lsub[infl::kLitSub], droot[infl::kDistRootN], dsub[infl::kDistSub];
+    uint32_t cm[infl::kCanonWords];
     int st;
     for (;;) {
         for (size_t i = 0; i < L.start.size(); ++i) {
             if (!L.dirty[i]) continue;
-            infl::decode_lane<false>(words.data(), nbits, L.start[i], L.stop[i], lroot, lsub, droot, dsub,
-                                     (uint16_t*)nullptr, i == 0 ? 0 : -1, out_cap, L.res[i]);
+            if (getenv("IKM_TABLES"))  // the two-level-table decoder (reference for the canonical one)
+                infl::decode_lane<false>(words.data(), nbits, L.start[i], L.stop[i], lroot, lsub, droot, dsub,
+                                         (uint16_t*)nullptr, i == 0 ? 0 : -1, out_cap, L.res[i]);
+            else
+                infl::decode_lane_canon<false>(words.data(), nbits, L.start[i], L.stop[i], cm, infl::NoOut{},
+                                               i == 0 ? 0 : -1, out_cap, L.res[i], infl::Win{});
             L.dirty[i] = 0;
         }
         if (getenv("IKM_DEBUG"))
@@ -95,11 +100,15 @@ int ikm_inflate_chunked(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8
     uint64_t total;
     pngplan::offsets(L, obase, &total);
     if (total > out_cap) return -3;
-    std::vector<uint16_t> u16(total + 1);
+    std::vector<uint16_t> u16(total + 16);
     for (size_t i = 0; i < L.start.size(); ++i) {
         infl::LaneResult r;
-        infl::decode_lane<true>(words.data(), nbits, L.start[i], L.stop[i], lroot, lsub, droot, dsub, u16.data(),
-                                obase[i], total - (uint64_t)obase[i], r);
+        if (getenv("IKM_TABLES"))
+            infl::decode_lane<true>(words.data(), nbits, L.start[i], L.stop[i], lroot, lsub, droot, dsub, u16.data(),
+                                    obase[i], total - (uint64_t)obase[i], r);
+        else
+            infl::decode_lane_canon<true>(words.data(), nbits, L.start[i], L.stop[i], cm, infl::U16Out{u16.data()},
+                                          obase[i], total - (uint64_t)obase[i], r, infl::Win{});
         if (r.status != infl::kLaneOk || r.out_len != L.res[i].out_len) return -4;
     }
     // page -> decoder table (as the host builds it for the GPU resolve pass)

@@ -53,6 +53,7 @@ SIGNATURES = [
     ("ik_set_resize_mode", ctypes.c_int, [ctypes.c_int]),
     ("ik_set_png_gpu_min", ctypes.c_int, [ctypes.c_longlong]),
     ("ik_png_last_timing", ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
+    ("ik_png_counters", ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
     ("ik_get_resize_mode", ctypes.c_int, []),
     ("ik_pipeline_submit", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint32]),
     ("ik_pipeline_collect", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_uint32)]),

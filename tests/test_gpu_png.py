@@ -24,11 +24,29 @@ MODES = {1: "L", 2: "LA", 3: "RGB", 4: "RGBA"}
 CTYPE = {1: 0, 2: 4, 3: 2, 4: 6}
 
 
+def png_counters(ik):
+    c = (ctypes.c_ulonglong * 2)()
+    assert ik.ik_png_counters(c) == 0
+    return c[0], c[1]
+
+
 @pytest.fixture(scope="module")
 def gpu_png(ik):
     assert ik.ik_set_png_gpu_min(0) == 0  # every PNG through the GPU path
     yield ik
     ik.ik_set_png_gpu_min(256 << 10)
+
+
+@pytest.fixture
+def on_gpu(gpu_png):
+    """The test's valid PNGs must all be decoded by the GPU path, none by the
+    host decoder's fallback (a GPU decoder that rejects a stream still gives
+    right pixels through the fallback, so pixel equality alone cannot tell)."""
+    g0, h0 = png_counters(gpu_png)
+    yield gpu_png
+    g1, h1 = png_counters(gpu_png)
+    assert g1 > g0, "no PNG stream went through the GPU path"
+    assert h1 == h0, f"{h1 - h0} PNG stream(s) fell back to the host decoder"
 
 
 def pil_png(img, **kw):
@@ -91,7 +109,7 @@ def pil_px(data):
 
 @pytest.mark.parametrize("c", [1, 2, 3, 4])
 @pytest.mark.parametrize("w,h", [(1, 1), (17, 9), (640, 480), (1001, 333)])
-def test_pillow_pngs(gpu_png, c, w, h):
+def test_pillow_pngs(on_gpu, c, w, h):
     img = ikutil.synth(w, h, c, seed=w * 7 + c)
     data = pil_png(img)
     np.testing.assert_array_equal(decode_px(data), img)
@@ -101,7 +119,7 @@ def test_pillow_pngs(gpu_png, c, w, h):
                                             (9, zlib.Z_DEFAULT_STRATEGY), (6, zlib.Z_FILTERED),
                                             (6, zlib.Z_HUFFMAN_ONLY), (6, zlib.Z_RLE), (6, zlib.Z_FIXED),
                                             (0, zlib.Z_DEFAULT_STRATEGY)])
-def test_all_filters_levels_strategies(gpu_png, level, strategy):
+def test_all_filters_levels_strategies(on_gpu, level, strategy):
     img = ikutil.synth(777, 401, 4, seed=level * 10 + strategy)
     data = own_png(img, level=level, strategy=strategy, idat_size=8192)
     np.testing.assert_array_equal(decode_px(data), img)
@@ -110,7 +128,7 @@ def test_all_filters_levels_strategies(gpu_png, level, strategy):
 
 @pytest.mark.parametrize("ft", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("c", [1, 3, 4])
-def test_each_filter_type(gpu_png, ft, c):
+def test_each_filter_type(on_gpu, ft, c):
     img = ikutil.synth(333, 130, c, seed=ft + 10 * c, pattern="N" if ft == 4 else "S")
     data = own_png(img, filters=ft)
     np.testing.assert_array_equal(decode_px(data), img)
@@ -129,14 +147,14 @@ def test_noise_and_host_decoder_agree(gpu_png):
     np.testing.assert_array_equal(host, img)
 
 
-def test_configs1_frame_4096(gpu_png):
+def test_configs1_frame_4096(on_gpu):
     """configs[1]: a 4096x4096 RGBA8 synthetic frame as PNG (35 MB, ~2,000 decoder lanes)."""
     img = ikutil.synth(4096, 4096, 4, seed=1)
     data = pil_png(img)
     np.testing.assert_array_equal(decode_px(data), img)
 
 
-def test_batch_mixed(gpu_png):
+def test_batch_mixed(on_gpu):
     imgs = [ikutil.synth(w, h, c, seed=k) for k, (w, h, c) in
             enumerate([(640, 480, 4), (1024, 768, 3), (333, 222, 1), (2048, 1024, 4), (100, 3000, 2)])]
     datas = [pil_png(im) for im in imgs] + [own_png(imgs[0], level=9, idat_size=1000)]
@@ -168,7 +186,7 @@ def test_corrupt_png_errors(gpu_png):
         np.testing.assert_array_equal(got, img)
 
 
-def test_transform_from_png_bytes(gpu_png, oracle):
+def test_transform_from_png_bytes(on_gpu, oracle):
     """decode (GPU PNG) -> resize_image -> encode_image: bytes equal the oracle's
     transform of the same pixels (configs[1] shape, reduced size)."""
     from imagekit import ImageFormat

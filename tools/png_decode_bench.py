@@ -1,0 +1,22 @@
+"""Dev tool: time the GPU PNG decode of a batch of 4096^2 RGBA8 PNG frames
+(decode_image_batch), printing the per-stage device times; used under rocprofv3."""
+import ctypes, io, os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "rust-image-transform_amd"), os.path.join(ROOT, "tests")]
+import numpy as np
+from PIL import Image
+import ikutil
+from imagekit import _lib, decode_image_batch
+lib = _lib.load(); assert lib.ik_init(0) == 0
+S = int(os.environ.get("S", 4096)); B = int(os.environ.get("B", 64)); R = int(os.environ.get("R", 3))
+pngs = []
+for k in range(min(4, B)):
+    b = io.BytesIO(); Image.fromarray(ikutil.synth(S, S, 4, seed=k), "RGBA").save(b, format="PNG"); pngs.append(b.getvalue())
+reqs = [pngs[i % len(pngs)] for i in range(B)]
+t = (ctypes.c_double * 10)()
+for r in range(R):
+    t0 = time.perf_counter(); out = decode_image_batch(reqs); el = time.perf_counter() - t0
+    lib.ik_png_last_timing(t, 10)
+    print(f"batch {B} x {S}^2: {el*1e3:.1f} ms wall; stage ms host {t[0]:.1f} find {t[1]:.1f} count {t[2]:.1f} "
+          f"emit {t[3]:.1f} resolve {t[4]:.1f} unfilter {t[5]:.1f} lanes {int(t[8])}", flush=True)
+    del out
