@@ -924,7 +924,7 @@ int ik_resize_batch_device(const uint8_t* dev_src, uint32_t W, uint32_t H, uint3
     ResizePlan* plan = get_resize_plan(current_device(), (int)W, (int)H, (int)C, (int)nw, (int)nh, filter, (int)n);
     if (!plan) return fail(IK_ERR_DEVICE, "cannot build resize plan");
     float* tmp = nullptr;
-    if (plan->slots == 0) {
+    if (plan->slots == 0 || !resize_fused_fits(src_pitch, H)) {
         tmp = (float*)scratch(sizeof(float) * (size_t)n * nh * W * C);
         if (!tmp) return fail(IK_ERR_DEVICE, "cannot allocate device scratch");
     }

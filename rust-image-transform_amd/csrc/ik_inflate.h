@@ -11,17 +11,21 @@
 //            HDIST ranges, a complete code-length code, code lengths that decode
 //            to exactly HLIT+HDIST entries, complete literal/distance codes with an
 //            end-of-block code).
-//  2. count: one decoder per candidate start decodes whole blocks until it
+//  2. decode: one decoder lane per candidate start decodes whole blocks until it
 //            reaches the next candidate; it must land exactly on it (else the
-//            candidate was not a real block start and is dropped).  Output
-//            lengths -> prefix sums -> each decoder's output offset.
-//  3. emit:  decode again, writing u16 symbols: a literal byte (< 256), or for a
-//            back-reference into bytes before the decoder's own output (written
-//            by its predecessor) a marker 0x8000 | index into the 32 KiB window
-//            that precedes the decoder's first output byte.  Markers copied
-//            within a decoder keep their value (they name an absolute position).
-//  4. resolve (in the PNG unfilter pass): a marker is replaced by the byte at its
-//            window position, following chains through earlier decoders.
+//            candidate was not a real block start: it is dropped and the lane
+//            decodes on next round).  The lane writes a token stream (literal
+//            ranks, matches, each block's literal table) into its own region and
+//            reports its output length -> prefix sums -> output offsets.
+//  3. expand: each lane's tokens -> u16 symbols at its output offset: a literal
+//            byte (< 256), or for a back-reference into bytes before the lane's
+//            own output (written by its predecessor) a marker 0x8000 | index into
+//            the 32 KiB window that precedes the lane's first output byte.
+//            Markers copied within a lane keep their value (they name an absolute
+//            position).  This pass holds no code tables, so it runs at full
+//            occupancy, which hides the latency of its copies' loads.
+//  4. resolve (before the PNG unfilter pass): a marker is replaced by the byte at
+//            its window position, following chains through earlier lanes.
 //
 // Everything here is written once for both compilers: IK_HD functions run in the
 // HIP kernels and in the CPU model that the CPU test suite checks against zlib.
@@ -51,17 +55,7 @@
 namespace ik {
 namespace infl {
 
-constexpr int kLitRoot = 9;    // root bits of the literal/length table
-constexpr int kDistRoot = 7;   // root bits of the distance table
-constexpr int kLitRootN = 1 << kLitRoot;
-constexpr int kDistRootN = 1 << kDistRoot;
-constexpr int kLitSub = 512;   // subtable entries for codes longer than the root (zlib's bound: 852 - 512)
-constexpr int kDistSub = 512;
 constexpr int kWindow = 32768;
-
-// table entry (u16): bit 15 = 0: symbol in bits 0..8, code length in bits 9..12
-//                    bit 15 = 1: subtable at index bits 0..10, index bits in 11..14
-IK_HD uint16_t ent(int sym, int len) { return (uint16_t)(sym | (len << 9)); }
 
 // 32-bit little-endian words of the stream; pos = absolute bit position of the
 // next bit.  The buffer must hold >= 4 zero words past the last stream word.
@@ -138,90 +132,6 @@ IK_HD uint32_t rev_bits(uint32_t v, int k) {
         v >>= 1;
     }
     return r;
-}
-
-// Build the two-level lookup of a canonical code (lengths[n]).  root: 2^rb
-// entries; sub: subtables (capacity sub_cap).  Returns 0, or -1 if the
-// subtables would not fit.  Entries for unused root slots (incomplete code) are
-// set to length 0, which the decoder treats as an invalid code.
-template <class RootT, class SubT>
-IK_HD_COLD int build_table(const uint8_t* lens, int n, const CodeInfo& ci, int rb, RootT root, SubT sub, int sub_cap) {
-    const int rootn = 1 << rb;
-    for (int i = 0; i < rootn; ++i) root[i] = 0;
-    if (ci.max == 0) return 0;
-    // first canonical code of each length (RFC 1951 3.2.2; bl_count[0] counts as 0)
-    uint32_t next[16];
-    uint32_t code = 0;
-    next[0] = 0;
-    for (int l = 1; l <= 15; ++l) {
-        code = (code + (l > 1 ? ci.count[l - 1] : 0)) << 1;
-        next[l] = code;
-    }
-    // remaining codes per length (for subtable sizing, zlib's rule)
-    int remain[16];
-    for (int l = 0; l < 16; ++l) remain[l] = ci.count[l];
-    int sub_used = 0;
-    int cur_prefix = -1, cur_base = 0, cur_bits = 0;
-    // walk codes in canonical order: by length, then symbol
-    for (int l = 1; l <= 15; ++l) {
-        if (!ci.count[l]) continue;
-        for (int s = 0; s < n; ++s) {
-            if (lens[s] != l) continue;
-            const uint32_t c = next[l]++;
-            const uint32_t r = rev_bits(c, l);
-            if (l <= rb) {
-                const uint16_t e = ent(s, l);
-                for (uint32_t i = r; i < (uint32_t)rootn; i += (1u << l)) root[i] = e;
-            } else {
-                const int prefix = (int)(r & (uint32_t)(rootn - 1));
-                if (prefix != cur_prefix) {
-                    // new subtable: smallest size covering the codes that share this
-                    // prefix (zlib inftrees' `curr` computation)
-                    int curr = l - rb;
-                    int left = 1 << curr;
-                    while (curr + rb < ci.max) {
-                        left -= remain[curr + rb];
-                        if (left <= 0) break;
-                        ++curr;
-                        left <<= 1;
-                    }
-                    if (sub_used + (1 << curr) > sub_cap) return -1;
-                    cur_prefix = prefix;
-                    cur_base = sub_used;
-                    cur_bits = curr;
-                    for (int i = 0; i < (1 << curr); ++i) sub[cur_base + i] = 0;
-                    sub_used += 1 << curr;
-                    root[prefix] = (uint16_t)(0x8000 | (cur_bits << 11) | cur_base);
-                }
-                const int sl = l - rb;
-                const uint32_t hi = r >> rb;
-                const uint16_t e = ent(s, sl);
-                for (uint32_t i = hi; i < (1u << cur_bits); i += (1u << sl)) sub[cur_base + i] = e;
-            }
-            remain[l]--;
-        }
-    }
-    return 0;
-}
-
-// decode one symbol with a two-level table; returns the symbol or -1 (invalid code)
-template <class RootT, class SubT>
-IK_HD int decode_sym(Bits& b, RootT root, SubT sub, int rb) {
-    b.refill();
-    uint32_t e = root[b.peek(rb)];
-    if (e & 0x8000u) {
-        const int bits = (int)((e >> 11) & 15u);
-        const uint32_t idx = (e & 0x7FFu) + ((uint32_t)(b.buf >> rb) & ((1u << bits) - 1u));
-        const uint32_t e2 = sub[idx];
-        const int len = (int)((e2 >> 9) & 15u);
-        if (!len) return -1;
-        b.drop(rb + len);
-        return (int)(e2 & 0x1FFu);
-    }
-    const int len = (int)((e >> 9) & 15u);
-    if (!len) return -1;
-    b.drop(len);
-    return (int)(e & 0x1FFu);
 }
 
 IK_HD int len_base(int s) {  // length symbols 257..285
@@ -420,8 +330,10 @@ enum LaneStatus { kLaneOk = 0, kLaneMismatch = 1, kLaneCorrupt = 2 };
 struct LaneResult {
     uint64_t end_bit;   // block boundary where the decoder stopped
     uint64_t out_len;   // bytes it decoded
-    int status;         // LaneStatus
+    uint32_t ntok;      // tokens it wrote (decode pass)
+    int status;         // LaneStatus (or kLaneOverflow)
     int final_block;    // it decoded the BFINAL block
+    int pad;
 };
 
 // Decode whole blocks from `start` (a block boundary) until a block boundary >=
@@ -430,106 +342,6 @@ struct LaneResult {
 // symbols at out[obase + k] (literal bytes, or window markers for bytes before
 // obase, see the file comment); obase < 0 = unknown (count pass).  out_cap
 // bounds the lane's output (corrupt past it).
-template <bool EMIT, class LRoot, class LSub, class DRoot, class DSub, class Out>
-IK_HD void decode_lane(const uint32_t* words, uint64_t nbits, uint64_t start, uint64_t stop, LRoot lroot, LSub lsub,
-                       DRoot droot, DSub dsub, Out out, int64_t obase, uint64_t out_cap, LaneResult& r) {
-    Bits b;
-    b.init(words, start, (nbits >> 5) + 4);
-    const uint64_t wlimit = (nbits >> 5) + 3;  // past the stream: corrupt
-    uint64_t cnt = 0;
-    r.status = kLaneCorrupt;
-    r.final_block = 0;
-    uint8_t lens[288 + 32];
-    for (;;) {
-        const uint64_t p = b.pos();
-        if (p >= stop) {
-            r.status = p == stop ? kLaneOk : kLaneMismatch;
-            break;
-        }
-        if (p + 3 > nbits) break;  // ran off the stream without a final block
-        b.refill();
-        const uint32_t hdr = b.peek(3);
-        b.drop(3);
-        const int bfinal = (int)(hdr & 1u), btype = (int)(hdr >> 1);
-        if (btype == 0) {  // stored
-            b.drop(b.n & 7);  // to the byte boundary
-            const uint32_t len = b.get(16), nlen = b.get(16);
-            if ((len ^ 0xFFFFu) != nlen) break;
-            if (cnt + len > out_cap) break;
-            if (b.pos() + 8ull * len > nbits) break;
-            for (uint32_t i = 0; i < len; ++i) {
-                const uint32_t v = b.get(8);
-                if (EMIT) out[obase + (int64_t)cnt] = (uint16_t)v;
-                ++cnt;
-            }
-        } else if (btype == 3) {
-            break;
-        } else {
-            int nlen, ndist;
-            CodeInfo lci, dci;
-            if (btype == 2) {
-                // the header parser is out of line: hand it a copy, so the hot loop's
-                // reader stays in registers (an escaping reference would put it in scratch)
-                Bits hb = b;
-                const int prc = parse_dynamic(hb, lens, nlen, ndist, lci, dci);
-                b = hb;
-                if (prc) break;
-                // the distance lengths follow the literal/length ones: move them to
-                // 288.. (backwards: the ranges overlap when nlen + ndist > 288)
-                for (int i = ndist - 1; i >= 0; --i) lens[288 + i] = lens[nlen + i];
-            } else {
-                fixed_lens(lens);
-                nlen = 288;
-                ndist = 30;
-                code_check(lens, 288, false, lci);
-                code_check(lens + 288, 30, false, dci);
-            }
-            if (build_table(lens, nlen, lci, kLitRoot, lroot, lsub, kLitSub)) break;
-            if (build_table(lens + 288, ndist, dci, kDistRoot, droot, dsub, kDistSub)) break;
-            bool bad = false;
-            for (;;) {
-                if (b.wi > wlimit) { bad = true; break; }
-                const int sym = decode_sym(b, lroot, lsub, kLitRoot);
-                if (sym < 256) {
-                    if (sym < 0 || cnt >= out_cap) { bad = true; break; }
-                    if (EMIT) out[obase + (int64_t)cnt] = (uint16_t)sym;
-                    ++cnt;
-                    continue;
-                }
-                if (sym == 256) break;
-                if (sym > 285) { bad = true; break; }
-                const int len = len_base(sym) + (int)b.get(len_extra(sym));
-                const int ds = decode_sym(b, droot, dsub, kDistRoot);
-                if (ds < 0 || ds > 29) { bad = true; break; }
-                const int de = dist_extra(ds);
-                const int dist = dist_base(ds) + (int)(de ? b.get(de) : 0u);
-                if (cnt + (uint64_t)len > out_cap) { bad = true; break; }
-                if (obase >= 0 && (int64_t)cnt + obase < dist) { bad = true; break; }  // before the stream start
-                if (EMIT) {
-                    int64_t src = (int64_t)cnt - dist;
-                    int64_t dst = (int64_t)cnt;
-                    for (int i = 0; i < len; ++i, ++src, ++dst) {
-                        // before this decoder's first byte: a window marker (the
-                        // predecessor's byte); else a copy, markers included
-                        out[obase + dst] = src < 0 ? (uint16_t)(0x8000 | (uint32_t)(kWindow + src))
-                                                   : (uint16_t)out[obase + src];
-                    }
-                }
-                cnt += (uint64_t)len;
-            }
-            if (bad) break;
-        }
-        if (b.pos() > nbits + 64) break;  // decoded zero padding
-        if (bfinal) {
-            r.final_block = 1;
-            r.status = stop == ~0ull ? kLaneOk : kLaneMismatch;
-            break;
-        }
-    }
-    r.end_bit = b.pos();
-    r.out_len = cnt;
-}
-
 // value of the u16 stream at absolute position q after following window markers.
 // lane_obase: output offsets of the image's decoders (ascending), n of them;
 // page_lane[q >> page_shift] = the decoder that holds the page's first byte.
@@ -566,14 +378,15 @@ IK_HD int resolve_at(U16 u16, Off lane_obase, int n, Pages page_lane, int page_s
 //   W >= lim[14] is no code (an incomplete code's gap).
 // Canonical order within a length is by symbol value, so for the literal/length
 // code a length's codes are: its literals, then end-of-block, then length codes.
-// Table memory per lane (u32 words, CanonMem):
+// Table memory per lane (u32 words):
 //   [0..15]  linfo[L]: first code (15 bits) | #literals of length L (9) << 15
 //                      | EOB has length L (1) << 24 | rank of its first length code (5) << 25
-//   [16..31] lrank[L]: rank of its first literal (9 bits)
-//   [32..47] dinfo[L]: first code (15 bits) | rank of its first distance code (5) << 16
-//   bytes from word 48: lsyms[32] (length symbol - 257), dsyms[32], lits[256] (in canonical order)
-constexpr int kCanonWords = 48 + 8 + 8 + 64;  // 512 bytes
-constexpr int kCanonCountWords = 48 + 8 + 8;  // the count pass needs no literal values: 256 bytes
+//   [16..31] dinfo[L]: first distance code (15 bits) | rank of its first distance code (5) << 16
+//                      | rank of the first LITERAL of length L (9) << 21
+//   bytes from word 32: lsyms[32] (length symbol - 257), dsyms[32]
+// A literal is identified by its rank (0..255) in canonical order; the rank ->
+// byte table of each block goes into the token stream (below), not into LDS.
+constexpr int kCanonWords = 48;  // 192 bytes
 struct CanonRegs {
     uint32_t lpk[8], dpk[8];  // limits minus one, packed in signed 16-bit pairs (canon_len)
 };
@@ -595,12 +408,72 @@ IK_HD uint32_t rev32(uint32_t v) {
 #endif
 }
 
-IK_HD uint8_t cm_byte(const uint32_t* m, int i) { return (uint8_t)(m[48 + (i >> 2)] >> (8 * (i & 3))); }
+IK_HD uint8_t cm_byte(const uint32_t* m, int i) { return (uint8_t)(m[32 + (i >> 2)] >> (8 * (i & 3))); }
+
+// ---- token stream ---------------------------------------------------------------
+// The decode pass writes each lane's output as u16 tokens into the lane's own
+// region (its output offset is not known yet); the expand pass turns them into
+// the u16 symbol stream (bytes, window markers) at the lane's output offset.
+//   0x0000..0x00FF      a literal of a Huffman block: its canonical rank
+//   0x4000 | byte       a literal of a stored block
+//   0x8000 | (len - 3)  a match, followed by one token: distance - 1
+//   0xFFFF              block start: 0xFFFE pads to a multiple of 8 tokens, then
+//                       128 tokens hold the block's literal table (256 bytes:
+//                       byte r = the literal of rank r)
+constexpr uint32_t kTokRaw = 0x4000u, kTokMatch = 0x8000u, kTokTable = 0xFFFFu, kTokPad = 0xFFFEu;
+constexpr uint32_t kTokTableLen = 128;
+constexpr uint32_t kTokSlack = 16;  // tokens a region holds past its capacity check (padding)
+
+// Token region capacity of a lane over `bits` compressed bits: a quarter token
+// per bit (image data runs ~8 bits per token), or with `exact` the true bound
+// (a token costs at least one bit: a literal >= 1, a match's two >= 2) -- for
+// the lanes that overflowed the first.  Multiple of 8, plus a block's table.
+IK_HD uint32_t tok_capacity(uint64_t bits, bool exact) {
+    uint64_t c = (exact ? bits : bits / 4) + 2 * kTokTableLen + 64;
+    if (c > 0x7FFFFFF0ull) c = 0x7FFFFFF0ull;
+    return (uint32_t)((c + 7) & ~7ull);
+}
+
+// Token output of one lane: `p` = its region (16-byte aligned).  Complete groups
+// of 8 tokens are held back (pending) and stored by flush(): the GPU decoder
+// flushes only at its input ring's refill points, so that the wait there covers
+// exactly the ring's DMA (see ik_png.hip WinLds::tick).
+struct TokOut {
+    IK_GLOBAL uint16_t* p;
+    uint64_t p0 = 0, p1 = 0;
+    uint32_t ppos = 0;
+    bool pend = false;
+    IK_HD void group(uint32_t pos, uint64_t lo, uint64_t hi) {
+        p0 = lo;
+        p1 = hi;
+        ppos = pos;
+        pend = true;
+    }
+    IK_HD bool flush() {
+        if (!pend) return false;
+#if defined(__HIP_DEVICE_COMPILE__)
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        const u4 v = {(uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32)};
+        *reinterpret_cast<IK_GLOBAL u4*>(p + ppos) = v;  // one 16-byte store
+#else
+        for (int k = 0; k < 4; ++k) {
+            p[ppos + k] = (uint16_t)(p0 >> (16 * k));
+            p[ppos + 4 + k] = (uint16_t)(p1 >> (16 * k));
+        }
+#endif
+        pend = false;
+        return true;
+    }
+    IK_HD void table_byte(uint32_t tpos, int rank, uint8_t v) const {
+        reinterpret_cast<IK_GLOBAL uint8_t*>(p + tpos)[rank] = v;
+    }
+};
 
 // Build both codes' limits and tables (lens: literal/length lengths [0, nlen),
-// distance lengths at 288..).  lits: also the literal table (emit pass).
+// distance lengths at 288..); the literal table goes to the token stream at tpos.
 template <class Mem>
-IK_HD_COLD void canon_build(const uint8_t* lens, int nlen, int ndist, bool lits, CanonRegs& R, Mem m) {
+IK_HD_COLD void canon_build(const uint8_t* lens, int nlen, int ndist, CanonRegs& R, Mem m, TokOut& out,
+                            uint32_t tpos) {
     // literal/length code
     uint32_t cnt[16], first[16], llim[15], dlim[15];
     for (int l = 0; l < 16; ++l) cnt[l] = 0;
@@ -611,7 +484,7 @@ IK_HD_COLD void canon_build(const uint8_t* lens, int nlen, int ndist, bool lits,
         first[l] = code;
         llim[l - 1] = (first[l] + cnt[l]) << (15 - l);
     }
-    for (int i = 0; i < 16; ++i) m[48 + i] = 0;  // lsyms, dsyms
+    for (int i = 0; i < 16; ++i) m[32 + i] = 0;  // lsyms, dsyms
     uint32_t litr = 0, lenr = 0;
     uint32_t lrank_of[16];
     lrank_of[0] = 0;
@@ -620,22 +493,18 @@ IK_HD_COLD void canon_build(const uint8_t* lens, int nlen, int ndist, bool lits,
         for (int s = 0; s < nlen && s < 286; ++s) {
             if (lens[s] != l) continue;
             if (s < 256) {
-                if (lits) {
-                    const int w = 64 + (int)(litr + nl);
-                    m[48 + w / 4] = (m[48 + w / 4] & ~(255u << (8 * (w & 3)))) | ((uint32_t)s << (8 * (w & 3)));
-                }
+                out.table_byte(tpos, (int)(litr + nl), (uint8_t)s);
                 ++nl;
             } else if (s == 256) {
                 eob = 1;
             } else {
                 const int w = (int)(lenr + nlen_codes);
                 if (w < 32)
-                    m[48 + w / 4] = (m[48 + w / 4] & ~(255u << (8 * (w & 3)))) | ((uint32_t)(s - 257) << (8 * (w & 3)));
+                    m[32 + w / 4] = (m[32 + w / 4] & ~(255u << (8 * (w & 3)))) | ((uint32_t)(s - 257) << (8 * (w & 3)));
                 ++nlen_codes;
             }
         }
         m[l] = (first[l] & 0x7FFFu) | (nl << 15) | (eob << 24) | (lenr << 25);
-        m[16 + l] = litr;  // (kept for the layout; the decoder reads the copy in dinfo)
         lrank_of[l] = litr;
         litr += nl;
         lenr += nlen_codes;
@@ -648,14 +517,16 @@ IK_HD_COLD void canon_build(const uint8_t* lens, int nlen, int ndist, bool lits,
     for (int l = 1; l <= 15; ++l) {
         code = (code + (l > 1 ? cnt[l - 1] : 0)) << 1;
         dlim[l - 1] = (code + cnt[l]) << (15 - l);
-        m[32 + l] = (code & 0x7FFFu) | (dr << 16) | (lrank_of[l] << 21);
+        m[16 + l] = (code & 0x7FFFu) | (dr << 16) | (lrank_of[l] << 21);
         for (int s = 0; s < ndist; ++s) {
             if (lens[288 + s] != l) continue;
             const int w = 32 + (int)dr;
-            if (dr < 32) m[48 + w / 4] = (m[48 + w / 4] & ~(255u << (8 * (w & 3)))) | ((uint32_t)s << (8 * (w & 3)));
+            if (dr < 32) m[32 + w / 4] = (m[32 + w / 4] & ~(255u << (8 * (w & 3)))) | ((uint32_t)s << (8 * (w & 3)));
             ++dr;
         }
     }
+    m[0] = 0;
+    m[16] = 0;
     pack_limits(llim, R.lpk);
     pack_limits(dlim, R.dpk);
 }
@@ -683,89 +554,197 @@ IK_HD int canon_len(uint32_t c15, const uint32_t (&pk)[8]) {
     return (int)c15 > (int16_t)(pk[7] & 0xFFFFu) ? 16 : 1 + (int)at_or_below;
 }
 
-// Output of the emit pass: u16 symbols in global memory (or a host buffer).
-struct U16Out {
-    IK_GLOBAL uint16_t* p;
-    IK_HD uint16_t load(int64_t i) const { return p[i]; }
-    IK_HD void store1(int64_t i, uint16_t v) const { p[i] = v; }
-    IK_HD void store16(int64_t i, uint64_t lo, uint64_t hi) const {  // 8 symbols at i (a multiple of 8)
-        IK_GLOBAL uint64_t* q = reinterpret_cast<IK_GLOBAL uint64_t*>(p + i);
-        q[0] = lo;
-        q[1] = hi;
-    }
-};
-struct NoOut {
-    IK_HD uint16_t load(int64_t) const { return 0; }
-    IK_HD void store1(int64_t, uint16_t) const {}
-    IK_HD void store16(int64_t, uint64_t, uint64_t) const {}
-};
-
-// Input window of the hot loop: the three words holding the next 64+ bits
-// (a, b, c) and two prefetched ones (d, e).  After each symbol the window
-// slides by 0..2 words, choosing from registers, and the two words after it are
-// loaded for the NEXT symbol -- every load has a whole symbol of latency to
-// hide, and none sits behind a per-lane branch (a wave's vmcnt is shared by
-// its lanes).
+// Input window of the hot loop on the host (the CPU model): the three words
+// holding the next 64+ bits.  The GPU decoder's window is ik_png.hip WinLds (an
+// LDS ring filled by DMA); both offer init / tick / bits64 / advance / pos.
 struct Win {
-    const IK_GLOBAL uint32_t* w;
-    uint32_t wend, wi, pos;  // streams under 2^32 bits (the host checks)
-    uint32_t a, b, c, d, e;
+    const uint32_t* w;
+    uint32_t wend, pos;  // streams under 2^32 bits (the host checks)
     IK_HD uint32_t rd(uint32_t i) const { return i < wend ? w[i] : 0u; }
-    IK_HD void init(const IK_GLOBAL uint32_t* words, uint32_t nwords, uint32_t bit) {
+    IK_HD void init(const uint32_t* words, uint32_t nwords, uint32_t bit) {
         w = words;
         wend = nwords;
         pos = bit;
-        wi = bit >> 5;
-        a = rd(wi); b = rd(wi + 1); c = rd(wi + 2); d = rd(wi + 3); e = rd(wi + 4);
     }
+    IK_HD void tick(TokOut& o) { o.flush(); }
     IK_HD uint64_t bits64() const {  // the next 64 stream bits
-        const uint32_t sh = pos & 31u;
-        const uint64_t lo = (uint64_t)a | ((uint64_t)b << 32);
-        return sh ? (lo >> sh) | ((uint64_t)c << (64 - sh)) : lo;
+        const uint32_t wi = pos >> 5, sh = pos & 31u;
+        const uint64_t lo = (uint64_t)rd(wi) | ((uint64_t)rd(wi + 1) << 32);
+        return sh ? (lo >> sh) | ((uint64_t)rd(wi + 2) << (64 - sh)) : lo;
     }
-    // x0 / x1 / x2 for dd = 0 / 1 / 2, with masks (a ternary chain becomes an
-    // indexed private array, i.e. scratch memory)
-    IK_HD static uint32_t sel3(uint32_t m1, uint32_t m2, uint32_t x0, uint32_t x1, uint32_t x2) {
-        return (x0 & ~m1) | (x1 & m1 & ~m2) | (x2 & m2);
-    }
-    IK_HD void tick() {}  // (the LDS window refills its ring here)
-    IK_HD void advance(uint32_t k) {  // k <= 64
-        pos += k;
-        const uint32_t nwi = pos >> 5;
-        const uint32_t dd = nwi - wi;  // 0, 1 or 2
-        const uint32_t m1 = 0u - (uint32_t)(dd >= 1), m2 = 0u - (uint32_t)(dd >= 2);
-        const uint32_t d2 = rd(nwi + 3);  // needed only when dd == 2; a cached, independent load
-        const uint32_t na = sel3(m1, m2, a, b, c);
-        const uint32_t nb = sel3(m1, m2, b, c, d);
-        const uint32_t nc = sel3(m1, m2, c, d, e);
-        const uint32_t nd = sel3(m1, m2, d, e, d2);
-        wi = nwi;
-        a = na; b = nb; c = nc; d = nd;
-        e = rd(nwi + 4);
-    }
+    IK_HD void advance(uint32_t k) { pos += k; }
 };
 
-// Decoder lane with canonical decoding: the GPU kernels' decoder, same contract
-// as decode_lane.  m: this lane's table memory (kCanonWords u32; the count pass
-// kCanonCountWords).  EMIT: the last 8 output symbols live in two 64-bit
-// registers (h0: distances 8..5, h1: 4..1, newest in the top 16 bits), which
-// serve every copy with distance <= 8 and are written out as one aligned 16-byte
-// store each time the output position reaches a multiple of 8 -- so the loop
-// issues few stores, and copies from farther back only read flushed symbols.
-template <bool EMIT, class WinT, class Mem, class Out>
-IK_HD void decode_lane_canon(const uint32_t* words, uint64_t nbits, uint64_t start, uint64_t stop, Mem m, Out out,
-                             int64_t obase, uint64_t out_cap, LaneResult& r, WinT W) {
+enum { kLaneOverflow = 3 };  // LaneStatus: the token region was too small
+
+// Decoder lane, decode pass: whole blocks from `start` (a block boundary) up to
+// `stop`, as decode_lane, writing the token stream (TokOut, capacity tcap tokens
+// + kTokSlack) and counting the output bytes.  m: this lane's table memory
+// (kCanonWords).  first: lane 0 (no distance may reach before its output).
+// The symbol loop computes the literal and the match decoding of every symbol
+// and selects -- a wave's 64 lanes hold both kinds in nearly every step, so
+// branching would run both paths anyway, plus the mask bookkeeping -- and keeps
+// the rare cases (end of block, invalid codes, full region) in one branch.
+template <class WinT, class Mem>
+IK_HD void decode_lane_tok(const uint32_t* words, uint64_t nbits, uint64_t start, uint64_t stop, Mem m, TokOut& out,
+                           uint32_t tcap, bool first, uint64_t out_cap, LaneResult& r, WinT W) {
     const uint64_t nwords = (nbits >> 5) + 4;
     Bits b;
     b.init(words, start, nwords);
     const uint64_t plimit = nbits + 64;  // decoding past the stream's padding: corrupt
     uint64_t cnt = 0;
-    uint64_t h0 = 0, h1 = 0;
+    uint32_t tc = 0;
+    uint64_t h0 = 0, h1 = 0;  // the last 8 tokens (newest in the top 16 bits of h1)
     r.status = kLaneCorrupt;
     r.final_block = 0;
     uint8_t lens[288 + 32];
     CanonRegs R;
-    // append one symbol (EMIT): history push, aligned 16-byte store at each multiple of 8
+    auto tput = [&](uint32_t v) {
+        h0 = (h0 >> 16) | (h1 << 48);
+        h1 = (h1 >> 16) | ((uint64_t)v << 48);
+        ++tc;
+        if ((tc & 7u) == 0) out.group(tc - 8, h0, h1);
+    };
+    for (;;) {
+        const uint64_t p = b.pos();
+        if (p >= stop) {
+            r.status = p == stop ? kLaneOk : kLaneMismatch;
+            break;
+        }
+        if (p + 3 > nbits) break;
+        b.refill();
+        const uint32_t hdr = b.peek(3);
+        b.drop(3);
+        const int bfinal = (int)(hdr & 1u), btype = (int)(hdr >> 1);
+        if (btype == 0) {  // stored
+            b.drop(b.n & 7);
+            const uint32_t len = b.get(16), nlen = b.get(16);
+            if ((len ^ 0xFFFFu) != nlen) break;
+            if (cnt + len > out_cap) break;
+            if (b.pos() + 8ull * len > nbits) break;
+            if ((uint64_t)tc + len > tcap) { r.status = kLaneOverflow; break; }
+            for (uint32_t i = 0; i < len; ++i) {
+                tput(kTokRaw | b.get(8));
+                out.flush();
+            }
+            cnt += len;
+        } else if (btype == 3) {
+            break;
+        } else {
+            int nlen, ndist;
+            if (btype == 2) {
+                CodeInfo lci, dci;
+                Bits hb = b;  // out-of-line parser on a copy: the hot state stays in registers
+                const int prc = parse_dynamic(hb, lens, nlen, ndist, lci, dci);
+                b = hb;
+                if (prc) break;
+                for (int i = ndist - 1; i >= 0; --i) lens[288 + i] = lens[nlen + i];
+            } else {
+                fixed_lens(lens);
+                nlen = 288;
+                ndist = 30;
+            }
+            if (tc + kTokTableLen + 8 > tcap) { r.status = kLaneOverflow; break; }
+            tput(kTokTable);
+            while (tc & 7u) tput(kTokPad);
+            out.flush();
+            {
+                CanonRegs t;
+                canon_build(lens, nlen, ndist, t, m, out, tc);
+                R = t;
+#if defined(__HIP_DEVICE_COMPILE__)
+                // R comes back through the stack (canon_build is out of line): take
+                // it into registers here, so the loop below holds no waits for those
+                // loads -- a wait on the memory counter inside the loop would also
+                // wait for the input ring's latest DMA, which the compiler cannot see
+                asm volatile("" ::"v"(R.lpk[0]), "v"(R.lpk[1]), "v"(R.lpk[2]), "v"(R.lpk[3]), "v"(R.lpk[4]),
+                             "v"(R.lpk[5]), "v"(R.lpk[6]), "v"(R.lpk[7]), "v"(R.dpk[0]), "v"(R.dpk[1]), "v"(R.dpk[2]),
+                             "v"(R.dpk[3]), "v"(R.dpk[4]), "v"(R.dpk[5]), "v"(R.dpk[6]), "v"(R.dpk[7]));
+#endif
+            }
+            tc += kTokTableLen;
+            W.init((const IK_GLOBAL uint32_t*)words, (uint32_t)nwords, (uint32_t)b.pos());
+            bool bad = false, full = false;
+            for (;;) {
+                if ((uint64_t)W.pos > plimit) { bad = true; break; }
+                W.tick(out);
+                const uint64_t v = W.bits64();
+                // literal/length code
+                const uint32_t c15 = rev32((uint32_t)v) >> 17;
+                const int L = canon_len(c15, R.lpk);
+                const int Lc = L > 15 ? 15 : L;
+                const uint32_t info = m[Lc];
+                const uint32_t i = (c15 >> (15 - Lc)) - (info & 0x7FFFu);
+                const uint32_t nl = (info >> 15) & 0x1FFu;
+                const bool lit = i < nl;
+                const uint32_t eob = (info >> 24) & 1u;
+                const uint32_t lr = ((info >> 25) & 31u) + (i - nl - eob);  // length code rank
+                const int lsym = (int)cm_byte(m, (int)(lr < 28u ? lr : 28u));
+                const int le = len_extra(257 + lsym);
+                const uint64_t v1 = v >> Lc;
+                const int ll = len_base(257 + lsym) + (int)((uint32_t)v1 & ((1u << le) - 1u));
+                // distance code (computed for literals too, and not used)
+                const uint64_t v2 = v1 >> le;
+                const uint32_t c15d = rev32((uint32_t)v2) >> 17;
+                const int D = canon_len(c15d, R.dpk);
+                const int Dc = D > 15 ? 15 : D;
+                const uint32_t dinfo = m[16 + Dc];
+                const uint32_t di = ((c15d >> (15 - Dc)) - (dinfo & 0x7FFFu)) + ((dinfo >> 16) & 31u);
+                const int ds = (int)cm_byte(m, 32 + (int)(di < 29u ? di : 29u));
+                const int de = dist_extra(ds);
+                const int dist = dist_base(ds) + (int)((uint32_t)(v2 >> Dc) & ((1u << de) - 1u));
+                // the rare cases, in one branch
+                const bool odd = !lit && ((eob && i == nl) || lr > 28u || D > 15 || di > 29u ||
+                                          (first && (int64_t)cnt < dist));
+                if (L > 15 || odd || tc + 2 > tcap || cnt + 258 > out_cap) {
+                    if (L > 15) { bad = true; break; }
+                    if (!lit && eob && i == nl) {  // end of block
+                        W.advance((uint32_t)Lc);
+                        break;
+                    }
+                    if (odd) { bad = true; break; }
+                    if (tc + 2 > tcap) { full = true; break; }
+                    if (cnt + (lit ? 1u : (uint64_t)ll) > out_cap) { bad = true; break; }
+                }
+                const uint32_t rank = ((m[16 + Lc] >> 21) & 0x1FFu) + i;
+                tput(lit ? rank : (kTokMatch | (uint32_t)(ll - 3)));
+                if (!lit) tput((uint32_t)(dist - 1));
+                cnt += lit ? 1u : (uint64_t)ll;
+                W.advance(lit ? (uint32_t)Lc : (uint32_t)(Lc + le + Dc + de));
+            }
+            out.flush();
+            if (full) { r.status = kLaneOverflow; break; }
+            if (bad) break;
+            b.init(words, W.pos, nwords);
+        }
+        if (b.pos() > nbits + 64) break;
+        if (bfinal) {
+            r.final_block = 1;
+            r.status = stop == ~0ull ? kLaneOk : kLaneMismatch;
+            break;
+        }
+    }
+    const uint32_t ntok = tc;
+    out.flush();
+    while (tc & 7u) tput(kTokPad);  // the last group, padded (capacity has kTokSlack)
+    out.flush();
+    r.end_bit = b.pos();
+    r.out_len = cnt;
+    r.ntok = ntok;
+}
+
+// Expand pass: a verified lane's tokens -> u16 symbols at out[obase ..): literal
+// bytes, and for copies from before the lane's first byte window markers (0x8000
+// | index into the 32 KiB before obase; copied markers keep their value).  The
+// last 8 symbols live in two 64-bit registers (h0: distances 8..5, h1: 4..1,
+// newest in the top 16 bits), which serve every copy with distance <= 8 and are
+// written out as one aligned 16-byte store each time the output position
+// reaches a multiple of 8 -- copies from farther back read stored symbols.
+// Returns 0, or -1 if the tokens do not make out_len bytes.
+template <class TokIn, class Out>
+IK_HD int expand_lane(TokIn& tin, uint32_t ntok, Out out, int64_t obase, uint64_t out_len) {
+    uint64_t cnt = 0;
+    uint64_t h0 = 0, h1 = 0;
     auto put = [&](uint32_t v) {
         h0 = (h0 >> 16) | (h1 << 48);
         h1 = (h1 >> 16) | ((uint64_t)v << 48);
@@ -786,146 +765,88 @@ IK_HD void decode_lane_canon(const uint32_t* words, uint64_t nbits, uint64_t sta
     auto hist = [&](int d) -> uint32_t {  // the symbol d back (1..8)
         return (uint32_t)((d <= 4 ? h1 >> (16 * (4 - d)) : h0 >> (16 * (8 - d)))) & 0xFFFFu;
     };
-    for (;;) {
-        const uint64_t p = b.pos();
-        if (p >= stop) {
-            r.status = p == stop ? kLaneOk : kLaneMismatch;
-            break;
+    bool have_tab = false;
+    int rc = 0;
+    for (uint32_t t = 0; t < ntok;) {
+        const uint32_t v = tin.next();
+        ++t;
+        if (v < 256u) {  // a Huffman literal (rank)
+            if (!have_tab || cnt >= out_len) { rc = -1; break; }
+            put(tin.table(v));
+            continue;
         }
-        if (p + 3 > nbits) break;
-        b.refill();
-        const uint32_t hdr = b.peek(3);
-        b.drop(3);
-        const int bfinal = (int)(hdr & 1u), btype = (int)(hdr >> 1);
-        if (btype == 0) {  // stored
-            b.drop(b.n & 7);
-            const uint32_t len = b.get(16), nlen = b.get(16);
-            if ((len ^ 0xFFFFu) != nlen) break;
-            if (cnt + len > out_cap) break;
-            if (b.pos() + 8ull * len > nbits) break;
-            for (uint32_t i = 0; i < len; ++i) {
-                const uint32_t v = b.get(8);
-                if (EMIT) put(v);
-                else ++cnt;
-            }
-        } else if (btype == 3) {
-            break;
-        } else {
-            int nlen, ndist;
-            {
-                CodeInfo lci, dci;
-                if (btype == 2) {
-                    Bits hb = b;  // out-of-line parser on a copy: the hot state stays in registers
-                    const int prc = parse_dynamic(hb, lens, nlen, ndist, lci, dci);
-                    b = hb;
-                    if (prc) break;
-                    for (int i = ndist - 1; i >= 0; --i) lens[288 + i] = lens[nlen + i];
-                } else {
-                    fixed_lens(lens);
-                    nlen = 288;
-                    ndist = 30;
-                }
-                CanonRegs t;
-                canon_build(lens, nlen, ndist, EMIT, t, m);
-                R = t;
-            }
-            W.init((const IK_GLOBAL uint32_t*)words, (uint32_t)nwords, (uint32_t)b.pos());
-            bool bad = false;
-            for (;;) {
-                if ((uint64_t)W.pos > plimit) { bad = true; break; }
-                W.tick();
-                uint64_t v = W.bits64();
-                uint32_t k = 0;  // bits consumed by this symbol
-                const uint32_t c15 = rev32((uint32_t)v) >> 17;
-                const int len = canon_len(c15, R.lpk);
-                if (len > 15) { bad = true; break; }
-                const uint32_t info = m[len];
-                const uint32_t i = (c15 >> (15 - len)) - (info & 0x7FFFu);
-                const uint32_t nl = (info >> 15) & 0x1FFu;
-                v >>= len;
-                k += (uint32_t)len;
-                if (i < nl) {  // literal
-                    if (cnt >= out_cap) { bad = true; break; }
-                    if (EMIT) put(cm_byte(m, 64 + (int)((m[32 + len] >> 21) + i)));
-                    else ++cnt;
-                    W.advance(k);
-                    continue;
-                }
-                uint32_t j = i - nl;
-                if ((info >> 24) & 1u) {
-                    if (j == 0) { W.advance(k); break; }  // end of block
-                    --j;
-                }
-                const uint32_t lr = ((info >> 25) & 31u) + j;
-                if (lr > 28u) { bad = true; break; }  // 286/287
-                const int lsym = (int)cm_byte(m, (int)lr);
-                const int le = len_extra(257 + lsym);
-                const int ll = len_base(257 + lsym) + (int)((uint32_t)v & ((1u << le) - 1u));
-                v >>= le;
-                k += (uint32_t)le;
-                const uint32_t c15d = rev32((uint32_t)v) >> 17;
-                const int dl = canon_len(c15d, R.dpk);
-                if (dl > 15) { bad = true; break; }
-                const uint32_t dinfo = m[32 + dl];
-                const uint32_t di = ((c15d >> (15 - dl)) - (dinfo & 0x7FFFu)) + ((dinfo >> 16) & 31u);
-                if (di > 29u) { bad = true; break; }
-                v >>= dl;
-                k += (uint32_t)dl;
-                const int ds = (int)cm_byte(m, 32 + (int)di);
-                const int de = dist_extra(ds);
-                const int dist = dist_base(ds) + (int)((uint32_t)v & ((1u << de) - 1u));
-                k += (uint32_t)de;
-                if (cnt + (uint64_t)ll > out_cap) { bad = true; break; }
-                if (obase >= 0 && (int64_t)cnt + obase < dist) { bad = true; break; }
-                if (EMIT) {
-                    int q = 0;
-                    // sources before this lane's first symbol (window markers), or in the
-                    // history registers (distance <= 8: the registers roll as we copy)
-                    while (q < ll) {
-                        const int64_t sk = (int64_t)cnt - dist;
-                        if (sk < 0) put(0x8000u | (uint32_t)(kWindow + sk));
-                        else if (dist <= 8) put(hist(dist));
-                        else break;
-                        ++q;
-                    }
-                    // distance > 8: every source is at least 8 back, so already stored; in
-                    // groups of up to min(8, dist - 8) the loads go out together
-                    const int G = dist - 8 < 8 ? dist - 8 : 8;
-                    while (q < ll) {
-                        const int n = ll - q < G ? ll - q : G;
-                        const int64_t s0 = obase + (int64_t)cnt - dist;
-                        uint32_t vv[8];
-                        IK_UNROLL
-                        for (int t2 = 0; t2 < 8; ++t2) vv[t2] = t2 < n ? (uint32_t)out.load(s0 + t2) : 0u;
-                        IK_UNROLL
-                        for (int t2 = 0; t2 < 8; ++t2)
-                            if (t2 < n) put(vv[t2]);
-                        q += n;
-                    }
-                } else {
-                    cnt += (uint64_t)ll;
-                }
-                W.advance(k);
-            }
-            if (bad) break;
-            b.init(words, W.pos, nwords);
+        if ((v & 0xFF00u) == kTokRaw) {
+            if (cnt >= out_len) { rc = -1; break; }
+            put(v & 0xFFu);
+            continue;
         }
-        if (b.pos() > nbits + 64) break;
-        if (bfinal) {
-            r.final_block = 1;
-            r.status = stop == ~0ull ? kLaneOk : kLaneMismatch;
-            break;
+        if (v == kTokTable) {
+            while (t & 7u) { (void)tin.next(); ++t; }
+            tin.set_table(t);
+            have_tab = true;
+            t += kTokTableLen;
+            tin.seek(t);
+            continue;
+        }
+        if ((v & 0xFF00u) != kTokMatch || t >= ntok) { rc = -1; break; }
+        const int ll = (int)(v & 0xFFu) + 3;
+        const int dist = (int)tin.next() + 1;
+        ++t;
+        if (cnt + (uint64_t)ll > out_len) { rc = -1; break; }
+        int q = 0;
+        // sources before this lane's first symbol (window markers), or in the
+        // history registers (distance <= 8: the registers roll as we copy)
+        while (q < ll) {
+            const int64_t sk = (int64_t)cnt - dist;
+            if (sk < 0) put(0x8000u | (uint32_t)(kWindow + sk));
+            else if (dist <= 8) put(hist(dist));
+            else break;
+            ++q;
+        }
+        // distance > 8: every source is at least 8 back, so already stored; in
+        // groups of up to min(8, dist - 8) the loads go out together
+        const int G = dist - 8 < 8 ? dist - 8 : 8;
+        while (q < ll) {
+            const int n = ll - q < G ? ll - q : G;
+            const int64_t s0 = obase + (int64_t)cnt - dist;
+            uint32_t vv[8];
+            IK_UNROLL
+            for (int t2 = 0; t2 < 8; ++t2) vv[t2] = t2 < n ? (uint32_t)out.load(s0 + t2) : 0u;
+            IK_UNROLL
+            for (int t2 = 0; t2 < 8; ++t2)
+                if (t2 < n) put(vv[t2]);
+            q += n;
         }
     }
-    // EMIT: the symbols after the last multiple of 8 are still only in the history
-    if (EMIT) {
-        const int64_t g = obase + (int64_t)cnt;
-        const int64_t q0 = g - (int64_t)(g & 7) > obase ? g - (int64_t)(g & 7) : obase;
-        for (int64_t q = q0; q < g; ++q) out.store1(q, (uint16_t)hist((int)(g - q)));
-    }
-    r.end_bit = b.pos();
-    r.out_len = cnt;
+    // the symbols after the last multiple of 8 are still only in the history
+    const int64_t g = obase + (int64_t)cnt;
+    const int64_t q0 = g - (int64_t)(g & 7) > obase ? g - (int64_t)(g & 7) : obase;
+    for (int64_t q = q0; q < g; ++q) out.store1(q, (uint16_t)hist((int)(g - q)));
+    return rc == 0 && cnt == out_len ? 0 : -1;
 }
+
+// Output of the expand pass: u16 symbols in global memory (or a host buffer).
+struct U16Out {
+    IK_GLOBAL uint16_t* p;
+    IK_HD uint16_t load(int64_t i) const { return p[i]; }
+    IK_HD void store1(int64_t i, uint16_t v) const { p[i] = v; }
+    IK_HD void store16(int64_t i, uint64_t lo, uint64_t hi) const {  // 8 symbols at i (a multiple of 8)
+        IK_GLOBAL uint64_t* q = reinterpret_cast<IK_GLOBAL uint64_t*>(p + i);
+        q[0] = lo;
+        q[1] = hi;
+    }
+};
+
+// Token input of the expand pass on the host (the GPU's reads 16-byte groups
+// ahead: ik_png.hip TokInDev).
+struct TokInHost {
+    const uint16_t* p;
+    uint32_t t = 0, tab = 0;
+    IK_HD uint32_t next() { return p[t++]; }
+    IK_HD void seek(uint32_t pos) { t = pos; }
+    IK_HD void set_table(uint32_t pos) { tab = pos; }  // the block's literal table is at token pos
+    IK_HD uint32_t table(uint32_t rank) const { return reinterpret_cast<const uint8_t*>(p + tab)[rank]; }
+};
 
 }  // namespace infl
 }  // namespace ik

@@ -70,6 +70,10 @@ struct ResizePlan {
 };
 
 // ---- launchers (ik_kernels.hip) ----
+// The fused kernel addresses one source image through a buffer descriptor with
+// 32-bit num_records and row offsets: images over INT32_MAX bytes take the naive
+// two-pass path (whose caller must then pass naive_tmp).
+inline bool resize_fused_fits(size_t src_pitch, size_t H) { return src_pitch * H <= 0x7FFFFFFFull; }
 hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_pitch,
                          size_t src_img_stride, uint8_t* dst, size_t dst_pitch,
                          size_t dst_img_stride, int n, float* naive_tmp, hipStream_t s);

@@ -348,7 +348,7 @@ hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_
     a.src = src; a.src_pitch = src_pitch; a.src_img_stride = src_img_stride;
     a.dst = dst; a.dst_pitch = dst_pitch; a.dst_img_stride = dst_img_stride;
     a.tmp = naive_tmp;
-    if (plan.slots > 0) {
+    if (plan.slots > 0 && resize_fused_fits(src_pitch, (size_t)a.H)) {
         dim3 grid(plan.NS * plan.NB * n);  // 1-D: the kernel maps it XCD-aware
         const bool wl = plan.weights_in_lds;
         const size_t lds = resize_lds_bytes(a, wl, plan.flush);

@@ -147,6 +147,8 @@ int check_batch(const ik_pipeline* p, const uint8_t* dev_src, size_t src_pitch, 
     if (src_pitch < (size_t)p->W * p->C || (src_pitch & 7) || ((uintptr_t)dev_src & 7))
         return fail(IK_ERR_INVALID, "source rows must be 8-byte aligned and >= W*C");
     if (n > 1 && src_image_stride < src_pitch * p->H) return fail(IK_ERR_INVALID, "image stride too small");
+    if (!resize_fused_fits(src_pitch, p->H) && !p->d_tmp)  // (created for tightly packed rows under 2 GiB)
+        return fail(IK_ERR_INVALID, "source image over 2 GiB at this pitch: use ik_resize_batch_device");
     return IK_OK;
 }
 
@@ -374,7 +376,8 @@ int pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t nh
     for (auto& sl : p->slot) IK_HIP(hipHostMalloc(&sl.h_stage, p->stage_bytes * max_batch, hipHostMallocDefault));
     ResizePlan* plan = get_resize_plan(p->device, (int)W, (int)H, (int)C, (int)nw, (int)nh, filter, (int)max_batch);
     if (!plan) return fail(IK_ERR_DEVICE, "cannot build resize plan");
-    if (plan->slots == 0) IK_HIP(hipMalloc(&p->d_tmp, sizeof(float) * (size_t)max_batch * nh * W * C));
+    if (plan->slots == 0 || !resize_fused_fits((size_t)W * C, H))  // naive path: its intermediate rows
+        IK_HIP(hipMalloc(&p->d_tmp, sizeof(float) * (size_t)max_batch * nh * W * C));
     if (threads <= 0) {
         threads = (int)std::thread::hardware_concurrency();
         if (threads > 16) threads = 16;

@@ -9,7 +9,8 @@
 
 namespace ik {
 
-constexpr int kPngInflateThreads = 64;     // decoder lanes per workgroup (LDS: 1280 B each)
+constexpr int kPngInflateThreads = 64;     // decoder lanes per workgroup (one wave: LDS 320 B per lane)
+constexpr int kPngExpandThreads = 64;      // expand lanes per workgroup (LDS: 256 B literal table each)
 constexpr int kPngUnfilterThreads = 1024;  // 16 waves: 16 bands in flight per image
 constexpr uint64_t kPngChunkBytes = 16384; // candidate-search chunk of the compressed stream
 constexpr int kPngPageShift = 12;          // resolve: output page -> decoder table
@@ -19,7 +20,7 @@ struct PngImgDev {
     const uint32_t* words;   // zlib stream (little-endian words, zero padded)
     uint64_t bit0;           // first DEFLATE bit (after the 2-byte zlib header)
     uint64_t nbits;          // stream length in bits
-    uint16_t* u16;           // emit pass output: raw_total symbols (+ padding)
+    uint16_t* u16;           // expand pass output: raw_total symbols (+ padding)
     uint64_t raw_total;      // bytes of the filtered image (H rows of 1 + rowbytes)
     const int64_t* obase;    // output offset of each decoder lane (ascending)
     const int* page_lane;    // decoder holding the first byte of each output page
@@ -31,18 +32,22 @@ struct PngImgDev {
 };
 
 struct PngLaneDev {
-    uint64_t start, stop;    // block boundary to start at; next lane's start (~0 = last)
-    int64_t obase;           // emit pass: output offset
+    uint64_t start, stop;    // decode: block boundary to start at; next lane's start (~0 = last)
+    uint64_t tbase;          // token region: index into the batch's token area (a multiple of 8)
+    int64_t obase;           // expand: output offset
+    uint64_t out_len;        // expand: output bytes
+    uint32_t ntok;           // decode: region capacity (tokens); expand: tokens to read
     uint32_t img;            // image of the batch
-    uint32_t slot;           // subtable work area index
-    uint32_t first;          // lane 0 of its image (output offset 0 is known)
+    uint32_t first;          // lane 0 of its image (no distance reaches before its output)
     uint32_t pad;
 };
 
 hipError_t launch_png_find(const PngImgDev* imgs, const int* chunk_img, const int* chunk_idx, int n,
                            uint64_t chunk_bits, int64_t* cand, hipStream_t s);
-hipError_t launch_png_inflate(bool emit, const PngImgDev* imgs, const PngLaneDev* lanes, int n, uint16_t* sub_ws,
-                              infl::LaneResult* res, hipStream_t s);
+hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, int n, uint16_t* tok,
+                             infl::LaneResult* res, hipStream_t s);
+hipError_t launch_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int n, const uint16_t* tok, int* status,
+                             hipStream_t s);
 hipError_t launch_png_resolve(const PngImgDev* imgs, const int2* rows, int nrows, int* err, hipStream_t s);
 hipError_t launch_png_unfilter(const PngImgDev* imgs, int n, int bpp, hipStream_t s);
 

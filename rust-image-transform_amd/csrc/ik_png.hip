@@ -5,10 +5,12 @@
 //
 //   k_png_find      one wave per (chunk, image): the first plausible dynamic
 //                   block header in the chunk (2,048 bit offsets per wave step)
-//   k_png_inflate   one thread per decoder lane: whole blocks from its start to
-//                   the next lane's start; count pass (lengths) or emit pass
-//                   (u16 symbols with window markers).  Root Huffman tables live
-//                   in LDS per thread, subtables in a per-lane global area.
+//   k_png_decode    one thread per decoder lane: whole blocks from its start to
+//                   the next lane's start -> the lane's token stream and output
+//                   length.  Code tables in LDS per thread (192 B), input through
+//                   an LDS ring filled by LDS-DMA (128 B per thread)
+//   k_png_expand    one thread per verified lane: tokens -> u16 symbols (bytes,
+//                   window markers) at the lane's output offset; no LDS
 //   k_png_resolve   u16 symbols -> the filtered bytes of every row, 16 per thread,
 //                   markers followed to their source; rows land 16-B aligned in
 //                   the destination image (pitched) and filter types in ft[]
@@ -230,9 +232,18 @@ struct WinLds {
         nextb = B0 + 4;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __device__ void tick() {
+    // Every kRingTick symbols: store the lane's pending token group (if any lane
+    // has one: one 16-byte store instruction for the wave), wait until all but
+    // that store are done -- the ring's DMA from the last tick among them -- and
+    // issue the block three ahead.  Between ticks the loop issues no memory
+    // instruction, so the count in the wait is exact.
+    __device__ void tick(infl::TokOut& o) {
         if (++it % kRingTick) return;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // last interval's DMA has landed
+        const bool st = o.flush();
+        if (__ballot(st))
+            asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (nextb <= ((pos >> 5) / kRingBW) + 3u) {
             dma(nextb);
             ++nextb;
@@ -247,31 +258,90 @@ struct WinLds {
     __device__ void advance(uint32_t k) { pos += k; }
 };
 
-template <bool EMIT>
-__global__ __launch_bounds__(kPngInflateThreads) void k_png_inflate(const PngImgDev* imgs, const PngLaneDev* lanes,
-                                                                     int nlanes, uint16_t* sub_ws,
-                                                                     infl::LaneResult* res) {
-    constexpr int W = EMIT ? infl::kCanonWords : infl::kCanonCountWords;
-    __shared__ uint32_t s_tab[kPngInflateThreads * W];
+__global__ __launch_bounds__(kPngInflateThreads) void k_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes,
+                                                                   int nlanes, uint16_t* tok, infl::LaneResult* res) {
+    __shared__ uint32_t s_tab[kPngInflateThreads * infl::kCanonWords];
     __shared__ uint32_t s_ring[4 * (kRingBW / 4) * 64 * 4];  // 4 blocks x 32 B per lane (one wave)
     const int t = blockIdx.x * kPngInflateThreads + threadIdx.x;
     if (t >= nlanes) return;
     const PngLaneDev L = lanes[t];
     const PngImgDev I = imgs[L.img];
-    uint32_t* m = s_tab + threadIdx.x * W;
+    uint32_t* m = s_tab + threadIdx.x * infl::kCanonWords;
     WinLds win;
     win.ring = (lds_u32*)s_ring;
     win.lane = threadIdx.x;
+    infl::TokOut out;
+    out.p = (IK_GLOBAL uint16_t*)(tok + L.tbase);
     infl::LaneResult r;
-    const uint64_t cap = EMIT ? I.raw_total - (uint64_t)L.obase : I.raw_total;
-    if (EMIT)
-        infl::decode_lane_canon<true>(I.words, I.nbits, L.start, L.stop, m,
-                                      infl::U16Out{(IK_GLOBAL uint16_t*)I.u16}, L.obase, cap, r, win);
-    else
-        infl::decode_lane_canon<false>(I.words, I.nbits, L.start, L.stop, m, infl::NoOut{}, L.first ? 0 : -1, cap, r,
-                                       win);
+    infl::decode_lane_tok(I.words, I.nbits, L.start, L.stop, m, out, L.ntok, L.first != 0, I.raw_total, r, win);
     res[t] = r;
-    (void)sub_ws;
+}
+
+// ---- expand -----------------------------------------------------------------------
+// One thread per verified lane: its tokens -> u16 symbols at its output offset
+// (ik_inflate.h expand_lane).  No LDS and few registers, so the CUs hold many
+// waves, and their copies' loads (distance > 8: symbols this lane stored
+// before) overlap across waves.  Tokens arrive in 16-byte groups, one group ahead.
+struct TokInDev {
+    const IK_GLOBAL uint64_t* g;  // the lane's region as pairs of u64 (16-byte groups)
+    uint64_t a0, a1, n0, n1;
+    uint32_t gi, k;
+    lds_u32* tab;                 // this thread's literal table in LDS: [16 B slot][thread][4 words]
+    uint32_t lane;
+    __device__ void init(const IK_GLOBAL uint16_t* p) {
+        g = (const IK_GLOBAL uint64_t*)p;
+        seek(0);
+    }
+    __device__ void seek(uint32_t t) {
+        gi = t >> 3;
+        k = t & 7u;
+        a0 = g[2 * gi]; a1 = g[2 * gi + 1];
+        n0 = g[2 * gi + 2]; n1 = g[2 * gi + 3];
+        gi += 2;
+    }
+    __device__ uint32_t next() {
+        const uint32_t v = (uint32_t)(((k < 4 ? a0 : a1) >> (16 * (k & 3u))) & 0xFFFFu);
+        if (++k == 8) {
+            a0 = n0; a1 = n1;
+            n0 = g[2 * gi]; n1 = g[2 * gi + 1];
+            ++gi;
+            k = 0;
+        }
+        return v;
+    }
+    // the block's literal table (256 bytes at token pos) -> LDS, 16 loads in flight
+    __device__ void set_table(uint32_t pos) {
+        const IK_GLOBAL uint64_t* q = g + (size_t)(pos >> 2);
+        uint64_t v[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) v[i] = q[i];
+#pragma unroll
+        for (int sl = 0; sl < 16; ++sl) {
+            lds_u32* d = tab + (sl * kPngExpandThreads + lane) * 4;
+            d[0] = (uint32_t)v[2 * sl];
+            d[1] = (uint32_t)(v[2 * sl] >> 32);
+            d[2] = (uint32_t)v[2 * sl + 1];
+            d[3] = (uint32_t)(v[2 * sl + 1] >> 32);
+        }
+    }
+    __device__ uint32_t table(uint32_t rank) const {
+        const uint32_t w = tab[((rank >> 4) * kPngExpandThreads + lane) * 4 + ((rank >> 2) & 3u)];
+        return (w >> (8 * (rank & 3u))) & 0xFFu;
+    }
+};
+
+__global__ __launch_bounds__(kPngExpandThreads) void k_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes,
+                                                                  int nlanes, const uint16_t* tok, int* status) {
+    __shared__ uint32_t s_lits[16 * kPngExpandThreads * 4];  // 256 B of literal table per thread
+    const int t = blockIdx.x * kPngExpandThreads + threadIdx.x;
+    if (t >= nlanes) return;
+    const PngLaneDev L = lanes[t];
+    const PngImgDev I = imgs[L.img];
+    TokInDev tin;
+    tin.tab = (lds_u32*)s_lits;
+    tin.lane = threadIdx.x;
+    tin.init((const IK_GLOBAL uint16_t*)(tok + L.tbase));
+    status[t] = infl::expand_lane(tin, L.ntok, infl::U16Out{(IK_GLOBAL uint16_t*)I.u16}, L.obase, L.out_len);
 }
 
 // ---- resolve ------------------------------------------------------------------------
@@ -423,14 +493,19 @@ hipError_t launch_png_find(const PngImgDev* imgs, const int* chunk_img, const in
     return hipGetLastError();
 }
 
-hipError_t launch_png_inflate(bool emit, const PngImgDev* imgs, const PngLaneDev* lanes, int n, uint16_t* sub_ws,
-                              infl::LaneResult* res, hipStream_t s) {
+hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, int n, uint16_t* tok,
+                             infl::LaneResult* res, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const dim3 grid((n + kPngInflateThreads - 1) / kPngInflateThreads);
-    if (emit)
-        hipLaunchKernelGGL(k_png_inflate<true>, grid, dim3(kPngInflateThreads), 0, s, imgs, lanes, n, sub_ws, res);
-    else
-        hipLaunchKernelGGL(k_png_inflate<false>, grid, dim3(kPngInflateThreads), 0, s, imgs, lanes, n, sub_ws, res);
+    hipLaunchKernelGGL(k_png_decode, grid, dim3(kPngInflateThreads), 0, s, imgs, lanes, n, tok, res);
+    return hipGetLastError();
+}
+
+hipError_t launch_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int n, const uint16_t* tok, int* status,
+                             hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((n + kPngExpandThreads - 1) / kPngExpandThreads);
+    hipLaunchKernelGGL(k_png_expand, grid, dim3(kPngExpandThreads), 0, s, imgs, lanes, n, tok, status);
     return hipGetLastError();
 }
 

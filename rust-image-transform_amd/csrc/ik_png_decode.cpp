@@ -6,9 +6,10 @@
 //   host   chunk walk + CRC check of every chunk (png verifies CRCs), IHDR;
 //          the IDAT payloads of all streams -> one pinned buffer -> one H2D copy
 //   GPU    k_png_find (block-start candidates per 16 KiB chunk)
-//   GPU    k_png_inflate count rounds; the host checks the lane chain after each
-//          (a false candidate is dropped and its predecessor decodes on)
-//   GPU    k_png_inflate emit (u16 symbols + window markers), k_png_resolve
+//   GPU    k_png_decode rounds (token streams + output lengths); the host checks
+//          the lane chain after each (a false candidate is dropped and its
+//          predecessor decodes on)
+//   GPU    k_png_expand (tokens -> u16 symbols + window markers), k_png_resolve
 //          (filtered rows into the image, markers followed), k_png_unfilter
 // The GPU path covers 8- and 16-bit, non-interlaced, non-palette streams
 // without tRNS (png's EXPAND leaves those samples as they are); everything else,
@@ -232,25 +233,37 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                 while ((size_t)(d - (pin + j.z_off)) & 3) *d++ = 0;
             });
         const double t1 = now_ms();
-        // the work area: grows with the largest round's lane tables (bounded below)
+        // the work area: lane tables (bounded by the chunk count), row / page
+        // tables, unfilter class descriptors, and the token area: a quarter token
+        // per compressed bit for every first-round lane, plus half again for lanes
+        // that decode again (a dropped successor, an overflow)
         size_t max_lanes = 0;
-        for (PngJob* j : J) max_lanes += (size_t)j->nchunks;
+        uint64_t tok_total = 0;
+        for (PngJob* j : J) {
+            max_lanes += (size_t)j->nchunks;
+            tok_total += infl::tok_capacity(j->nbits, false) + (uint64_t)j->nchunks * (infl::tok_capacity(0, false) +
+                                                                                       infl::kTokSlack);
+        }
+        tok_total += tok_total / 2 + 64;
         size_t dyn = up256(sizeof(PngLaneDev) * max_lanes) + up256(sizeof(infl::LaneResult) * max_lanes) +
-                     up256(sizeof(int64_t) * max_lanes) + (size_t)max_lanes * (infl::kLitSub + infl::kDistSub) * 2;
+                     up256(sizeof(int64_t) * max_lanes) + up256(sizeof(int) * max_lanes) +
+                     up256(sizeof(PngImgDev) * m);
         size_t nrows = 0, npages = 0;
         for (PngJob* j : J) {
             nrows += j->h;
             npages += (j->raw_total >> kPngPageShift) + 1;
         }
-        dyn += up256(sizeof(int2) * nrows) + up256(sizeof(int) * npages);
+        dyn += up256(sizeof(int2) * nrows) + up256(sizeof(int) * npages) + up256(2 * tok_total);
         uint8_t* dev = rc ? nullptr : scratch_slot(2, o_dyn + dyn);
         if (!rc && !dev) rc = fail(IK_ERR_DEVICE, "cannot allocate the PNG batch work area (%zu bytes)", o_dyn + dyn);
         PngLaneDev* d_lanes = nullptr;
         infl::LaneResult* d_res = nullptr;
         int64_t* d_obase = nullptr;
-        uint16_t* d_sub = nullptr;
+        int* d_xst = nullptr;
+        PngImgDev* d_cls = nullptr;
         int2* d_rows = nullptr;
         int* d_pages = nullptr;
+        uint16_t* d_tok = nullptr;
         if (!rc) {
             size_t o = o_dyn;
             d_lanes = reinterpret_cast<PngLaneDev*>(dev + o);
@@ -259,12 +272,17 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             o += up256(sizeof(infl::LaneResult) * max_lanes);
             d_obase = reinterpret_cast<int64_t*>(dev + o);
             o += up256(sizeof(int64_t) * max_lanes);
+            d_xst = reinterpret_cast<int*>(dev + o);
+            o += up256(sizeof(int) * max_lanes);
+            d_cls = reinterpret_cast<PngImgDev*>(dev + o);
+            o += up256(sizeof(PngImgDev) * m);
             d_rows = reinterpret_cast<int2*>(dev + o);
             o += up256(sizeof(int2) * nrows);
             d_pages = reinterpret_cast<int*>(dev + o);
             o += up256(sizeof(int) * npages);
-            d_sub = reinterpret_cast<uint16_t*>(dev + o);
+            d_tok = reinterpret_cast<uint16_t*>(dev + o);
         }
+        uint64_t tok_used = 0;
         // ---- upload streams (zero pad), image descriptors, chunk table ----
         std::vector<PngImgDev> hd(m);
         std::vector<int> ctab(2 * (size_t)nchunks);
@@ -317,8 +335,8 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             std::vector<int64_t> c(cand.begin() + j->chunk0, cand.begin() + j->chunk0 + j->nchunks);
             pngplan::build(c, j->lanes);
         }
-        // ---- count rounds ----
-        int rounds = 0, dropped = 0;
+        // ---- decode rounds: token streams; the host checks the lane chain ----
+        int rounds = 0, dropped = 0, overflows = 0;
         std::vector<PngLaneDev> hl;
         std::vector<std::pair<int, int>> who;  // (job, lane) of each launched lane
         std::vector<infl::LaneResult> hres;
@@ -328,18 +346,36 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             for (int k = 0; k < m; ++k) {
                 PngJob& j = *J[k];
                 if (j.state) continue;
-                for (size_t i = 0; i < j.lanes.start.size(); ++i) {
-                    if (!j.lanes.dirty[i]) continue;
+                pngplan::Lanes& LL = j.lanes;
+                for (size_t i = 0; i < LL.start.size(); ++i) {
+                    if (!LL.dirty[i]) continue;
+                    const uint64_t end = LL.stop[i] == ~0ull ? j.nbits : LL.stop[i];
+                    const uint32_t cap = infl::tok_capacity(end > LL.start[i] ? end - LL.start[i] : 0, LL.big[i] != 0);
+                    if (cap > LL.tcap[i]) {  // a (larger) region from the area
+                        const uint64_t need = cap + infl::kTokSlack;
+                        if (tok_used + need > tok_total) { j.state = -1; break; }  // out of room: host decoder
+                        LL.tbase[i] = tok_used;
+                        LL.tcap[i] = cap;
+                        tok_used += need;
+                    }
                     PngLaneDev L{};
-                    L.start = j.lanes.start[i];
-                    L.stop = j.lanes.stop[i];
-                    L.obase = -1;
+                    L.start = LL.start[i];
+                    L.stop = LL.stop[i];
+                    L.tbase = LL.tbase[i];
+                    L.ntok = LL.tcap[i];
                     L.img = (uint32_t)k;
-                    L.slot = (uint32_t)hl.size();
                     L.first = i == 0;
                     hl.push_back(L);
                     who.emplace_back(k, (int)i);
                 }
+            }
+            // lanes of a job that just fell back are dropped from the launch
+            if (!hl.empty()) {
+                size_t w = 0;
+                for (size_t t = 0; t < hl.size(); ++t)
+                    if (J[who[t].first]->state == 0) { hl[w] = hl[t]; who[w] = who[t]; ++w; }
+                hl.resize(w);
+                who.resize(w);
             }
             if (hl.empty()) break;
             if (hl.size() > max_lanes) { rc = fail(IK_ERR_DEVICE, "PNG lane table overflow"); break; }
@@ -348,30 +384,43 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             if (rc) break;
             hres.resize(hl.size());
             rec(2, s);
-            hipError_t e = launch_png_inflate(false, d_imgs, d_lanes, (int)hl.size(), d_sub, d_res, s);
+            hipError_t e = launch_png_decode(d_imgs, d_lanes, (int)hl.size(), d_tok, d_res, s);
             rec(3, s);
             if (e == hipSuccess) e = hipMemcpyAsync(hres.data(), d_res, sizeof(infl::LaneResult) * hl.size(),
                                                     hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
-            if (e != hipSuccess) { rc = hip_fail(e, "PNG inflate (count)"); break; }
+            if (e != hipSuccess) { rc = hip_fail(e, "PNG inflate (decode)"); break; }
             count_dev += ev_ms(2, 3);
             ++rounds;
+            std::vector<char> again(m, 0);  // a job with overflowed lanes: those first, then the check
             for (size_t t = 0; t < hl.size(); ++t) {
-                PngJob& j = *J[who[t].first];
-                j.lanes.res[who[t].second] = hres[t];
-                j.lanes.dirty[who[t].second] = 0;
+                pngplan::Lanes& LL = J[who[t].first]->lanes;
+                const int i = who[t].second;
+                LL.res[i] = hres[t];
+                LL.dirty[i] = 0;
+                if (hres[t].status == infl::kLaneOverflow) {
+                    ++overflows;
+                    if (LL.big[i]) {
+                        LL.res[i].status = infl::kLaneCorrupt;  // past the exact bound too (see tok_capacity)
+                    } else {
+                        LL.big[i] = 1;
+                        LL.dirty[i] = 1;
+                        again[who[t].first] = 1;
+                    }
+                }
             }
-            for (PngJob* j : J) {
-                if (j->state) continue;
-                const size_t before = j->lanes.start.size();
-                const int st = pngplan::check(j->lanes);
-                dropped += (int)(before - j->lanes.start.size());
-                if (st == 0) j->state = 1;
-                else if (st < 0) j->state = -1;
+            for (int k = 0; k < m; ++k) {
+                PngJob& j = *J[k];
+                if (j.state || again[k]) continue;
+                const size_t before = j.lanes.start.size();
+                const int st = pngplan::check(j.lanes);
+                dropped += (int)(before - j.lanes.start.size());
+                if (st == 0) j.state = 1;
+                else if (st < 0) j.state = -1;
             }
         }
         const double t3 = now_ms();
-        // ---- offsets, output images, emit ----
+        // ---- offsets, output images, expand, resolve, unfilter ----
         std::vector<int64_t> hob;
         std::vector<int> hpages;
         hl.clear();
@@ -395,18 +444,18 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             hd[k].pitch = j.img->pitch;
             for (size_t i = 0; i < ob.size(); ++i) {
                 PngLaneDev L{};
-                L.start = j.lanes.start[i];
-                L.stop = j.lanes.stop[i];
+                L.tbase = j.lanes.tbase[i];
                 L.obase = ob[i];
+                L.out_len = j.lanes.res[i].out_len;
+                L.ntok = j.lanes.res[i].ntok;
                 L.img = (uint32_t)k;
-                L.slot = (uint32_t)hl.size();
                 L.first = i == 0;
                 hl.push_back(L);
             }
             hob.insert(hob.end(), ob.begin(), ob.end());
         }
         std::vector<int2> hrows;
-        std::vector<int> herr(m, 0);
+        std::vector<int> herr(m, 0), hxst;
         if (!rc && !hl.empty()) {
             for (int k = 0; k < m; ++k)
                 if (J[k]->state == 1)
@@ -424,18 +473,16 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             if (!rc) rc = copy_h2d_2d(reinterpret_cast<uint8_t*>(d_rows), sizeof(int2) * hrows.size(),
                                       reinterpret_cast<const uint8_t*>(hrows.data()), sizeof(int2) * hrows.size(),
                                       sizeof(int2) * hrows.size(), 1, s);
-            hres.resize(hl.size());
+            hxst.resize(hl.size());
             if (!rc) {
                 hipError_t e = hipMemsetAsync(dev + o_err, 0, sizeof(int) * m, s);
                 rec(4, s);
-                if (e == hipSuccess) e = launch_png_inflate(true, d_imgs, d_lanes, (int)hl.size(), d_sub, d_res, s);
+                if (e == hipSuccess) e = launch_png_expand(d_imgs, d_lanes, (int)hl.size(), d_tok, d_xst, s);
                 rec(5, s);
                 if (e == hipSuccess) e = launch_png_resolve(d_imgs, d_rows, (int)hrows.size(),
                                                             reinterpret_cast<int*>(dev + o_err), s);
                 rec(6, s);
-                // unfilter: one launch per bytes-per-pixel class, over that class's images;
-                // the class descriptor arrays go where the emit pass's subtables were
-                // (that pass is done by then, in stream order), uploaded in one copy
+                // unfilter: one launch per bytes-per-pixel class, over that class's images
                 if (e == hipSuccess) {
                     std::vector<PngImgDev> cls;
                     std::vector<std::pair<int, int>> ranges;  // (bpp, first) per class
@@ -450,21 +497,20 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                     if (!stage) e = hipErrorOutOfMemory;
                     if (e == hipSuccess) {
                         std::memcpy(stage, cls.data(), cb);
-                        e = hipMemcpyAsync(d_sub, stage, cb, hipMemcpyHostToDevice, s);
+                        e = hipMemcpyAsync(d_cls, stage, cb, hipMemcpyHostToDevice, s);
                     }
                     for (size_t r = 0; r < ranges.size() && e == hipSuccess; ++r) {
                         const int first = ranges[r].second;
                         const int cnt = (r + 1 < ranges.size() ? ranges[r + 1].second : (int)cls.size()) - first;
-                        e = launch_png_unfilter(reinterpret_cast<const PngImgDev*>(d_sub) + first, cnt,
-                                                ranges[r].first, s);
+                        e = launch_png_unfilter(d_cls + first, cnt, ranges[r].first, s);
                     }
                 }
                 rec(7, s);
-                if (e == hipSuccess) e = hipMemcpyAsync(hres.data(), d_res, sizeof(infl::LaneResult) * hl.size(),
+                if (e == hipSuccess) e = hipMemcpyAsync(hxst.data(), d_xst, sizeof(int) * hl.size(),
                                                         hipMemcpyDeviceToHost, s);
                 if (e == hipSuccess) e = hipMemcpyAsync(herr.data(), dev + o_err, sizeof(int) * m, hipMemcpyDeviceToHost, s);
                 if (e == hipSuccess) e = hipStreamSynchronize(s);
-                if (e != hipSuccess) rc = hip_fail(e, "PNG inflate (emit) / unfilter");
+                if (e != hipSuccess) rc = hip_fail(e, "PNG inflate (expand) / unfilter");
                 if (!rc) {
                     t_png_timing[3] = ev_ms(4, 5);
                     t_png_timing[4] = ev_ms(5, 6);
@@ -477,8 +523,7 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                     PngJob& j = *J[k];
                     if (j.state != 1) continue;
                     bool ok = herr[k] == 0;
-                    for (size_t i = 0; i < j.lanes.start.size(); ++i, ++t)
-                        ok = ok && hres[t].status == infl::kLaneOk && hres[t].out_len == j.lanes.res[i].out_len;
+                    for (size_t i = 0; i < j.lanes.start.size(); ++i, ++t) ok = ok && hxst[t] == 0;
                     if (!ok) j.state = -1;
                 }
             }
@@ -490,9 +535,9 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
         t_png_timing[8] = (double)hl.size();
         t_png_timing[9] = m;
         if (timing)
-            fprintf(stderr, "[png] %d streams (%d on the GPU): stage %.2f ms, find %.2f ms, count %.2f ms (%d rounds, %d "
-                    "dropped), emit+resolve+unfilter %.2f ms\n", n, m, t1 - t0, t2 - t1, t3 - t2, rounds, dropped,
-                    now_ms() - t3);
+            fprintf(stderr, "[png] %d streams (%d on the GPU): stage %.2f ms, find %.2f ms, decode %.2f ms (%d rounds, "
+                    "%d dropped, %d overflows), expand+resolve+unfilter %.2f ms\n", n, m, t1 - t0, t2 - t1, t3 - t2,
+                    rounds, dropped, overflows, now_ms() - t3);
         for (int k = 0; k < m; ++k) {
             PngJob& j = *J[k];
             if (!rc && j.state == 1) {

@@ -2,8 +2,8 @@
 // into libik_pngmodel.so for the CPU test suite, never linked into the product).
 //
 // Runs the exact chunked algorithm of ik_png.hip / ik_png_decode.cpp -- candidate
-// search per chunk, count rounds with the chain check, emit with window markers,
-// marker resolution -- on the CPU with the same ik_inflate.h code, so that the
+// search per chunk, decode rounds (token streams) with the chain check, expand
+// with window markers, marker resolution -- on the CPU with the same ik_inflate.h code, so that the
 // tests can compare it with zlib on many streams without a GPU.
 #include <cstdio>
 #include <cstdlib>
@@ -19,7 +19,7 @@ extern "C" {
 
 // zlib stream -> inflated bytes through the chunked parallel algorithm.
 // stats (10 ints): chunks, candidates, lanes, rounds, markers, dropped
-// candidates, zlib header bits, status of the chain check
+// candidates, zlib header bits, status of the chain check, token region overflows
 int ikm_inflate_chunked(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8_t* out, size_t out_cap,
                         uint64_t* out_len, int* stats) {
     for (int i = 0; i < 10; ++i) stats[i] = 0;
@@ -68,29 +68,58 @@ int ikm_inflate_chunked(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8
     pngplan::Lanes L;
     pngplan::build(cand, L);
     const size_t nl0 = L.start.size();
-    uint16_t lroot[infl::kLitRootN], lsub[infl::kLitSub], droot[infl::kDistRootN], dsub[infl::kDistSub];
     uint32_t cm[infl::kCanonWords];
+    // token regions: capacity from the lane's compressed bits (as the GPU path),
+    // grown when a lane overflows
+    std::vector<std::vector<uint16_t>> tok(L.start.size());
     int st;
+    int overflows = 0;
     for (;;) {
         for (size_t i = 0; i < L.start.size(); ++i) {
             if (!L.dirty[i]) continue;
-            if (getenv("IKM_TABLES"))  // the two-level-table decoder (reference for the canonical one)
-                infl::decode_lane<false>(words.data(), nbits, L.start[i], L.stop[i], lroot, lsub, droot, dsub,
-                                         (uint16_t*)nullptr, i == 0 ? 0 : -1, out_cap, L.res[i]);
-            else
-                infl::decode_lane_canon<false>(words.data(), nbits, L.start[i], L.stop[i], cm, infl::NoOut{},
-                                               i == 0 ? 0 : -1, out_cap, L.res[i], infl::Win{});
+            const uint64_t bits = (L.stop[i] == ~0ull ? nbits : L.stop[i]) - L.start[i];
+            const uint32_t cap = infl::tok_capacity(bits, L.big[i] != 0);
+            tok[i].assign((size_t)cap + infl::kTokSlack, 0);
+            infl::TokOut to{tok[i].data()};
+            infl::decode_lane_tok(words.data(), nbits, L.start[i], L.stop[i], cm, to, cap, i == 0, out_cap, L.res[i],
+                                  infl::Win{});
+            if (L.res[i].status == infl::kLaneOverflow) {
+                ++overflows;
+                if (L.big[i]) {
+                    // past the large region too: garbage from a false start, or a
+                    // stream of tiny blocks (their tables); the chain check decides
+                    L.res[i].status = infl::kLaneCorrupt;
+                } else {
+                    L.big[i] = 1;
+                    continue;  // still dirty: again with the large region
+                }
+            }
             L.dirty[i] = 0;
         }
         if (getenv("IKM_DEBUG"))
             for (size_t i = 0; i < L.start.size(); ++i)
-                fprintf(stderr, "lane %zu start %llu stop %llu end %llu len %llu status %d final %d\n", i,
+                fprintf(stderr, "lane %zu start %llu stop %llu end %llu len %llu tok %u status %d final %d\n", i,
                         (unsigned long long)L.start[i], (unsigned long long)L.stop[i],
-                        (unsigned long long)L.res[i].end_bit, (unsigned long long)L.res[i].out_len, L.res[i].status,
-                        L.res[i].final_block);
+                        (unsigned long long)L.res[i].end_bit, (unsigned long long)L.res[i].out_len, L.res[i].ntok,
+                        L.res[i].status, L.res[i].final_block);
+        bool pending = false;
+        for (size_t i = 0; i < L.start.size(); ++i) pending = pending || L.dirty[i];
+        if (pending) continue;  // overflowed lanes first
+        // the chain check drops successors: keep the per-lane vectors in step
+        std::vector<uint64_t> before(L.start);
         st = pngplan::check(L);
+        if (L.start.size() != before.size()) {
+            std::vector<std::vector<uint16_t>> t2;
+            for (size_t i = 0, k = 0; i < before.size(); ++i)
+                if (k < L.start.size() && L.start[k] == before[i]) {
+                    t2.push_back(std::move(tok[i]));
+                    ++k;
+                }
+            tok.swap(t2);
+        }
         if (st != 1) break;
     }
+    stats[8] = overflows;
     stats[2] = (int)L.start.size();
     stats[3] = L.rounds;
     stats[5] = (int)(nl0 - L.start.size());
@@ -102,14 +131,8 @@ int ikm_inflate_chunked(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8
     if (total > out_cap) return -3;
     std::vector<uint16_t> u16(total + 16);
     for (size_t i = 0; i < L.start.size(); ++i) {
-        infl::LaneResult r;
-        if (getenv("IKM_TABLES"))
-            infl::decode_lane<true>(words.data(), nbits, L.start[i], L.stop[i], lroot, lsub, droot, dsub, u16.data(),
-                                    obase[i], total - (uint64_t)obase[i], r);
-        else
-            infl::decode_lane_canon<true>(words.data(), nbits, L.start[i], L.stop[i], cm, infl::U16Out{u16.data()},
-                                          obase[i], total - (uint64_t)obase[i], r, infl::Win{});
-        if (r.status != infl::kLaneOk || r.out_len != L.res[i].out_len) return -4;
+        infl::TokInHost tin{tok[i].data()};
+        if (infl::expand_lane(tin, L.res[i].ntok, infl::U16Out{u16.data()}, obase[i], L.res[i].out_len)) return -4;
     }
     // page -> decoder table (as the host builds it for the GPU resolve pass)
     const int shift = 12;

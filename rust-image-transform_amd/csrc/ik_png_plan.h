@@ -16,8 +16,20 @@ namespace pngplan {
 struct Lanes {
     std::vector<uint64_t> start, stop;
     std::vector<infl::LaneResult> res;
-    std::vector<char> dirty;  // needs (re)decoding in the next count round
+    std::vector<char> dirty;  // needs (re)decoding in the next decode round
+    std::vector<uint64_t> tbase;  // token region (the caller's allocation)
+    std::vector<uint32_t> tcap;   // its capacity (0: none yet)
+    std::vector<char> big;        // overflowed once: the region is sized by the exact bound
     int rounds = 0;
+    void erase(size_t i) {
+        start.erase(start.begin() + (long)i);
+        stop.erase(stop.begin() + (long)i);
+        res.erase(res.begin() + (long)i);
+        dirty.erase(dirty.begin() + (long)i);
+        tbase.erase(tbase.begin() + (long)i);
+        tcap.erase(tcap.begin() + (long)i);
+        big.erase(big.begin() + (long)i);
+    }
 };
 
 // candidates per chunk (chunk 0 = the first block, always valid; -1 = none found)
@@ -28,19 +40,23 @@ inline void build(const std::vector<int64_t>& cand, Lanes& L) {
         if (c >= 0 && (L.start.empty() || (uint64_t)c > L.start.back())) L.start.push_back((uint64_t)c);
     L.stop.resize(L.start.size());
     for (size_t i = 0; i < L.start.size(); ++i) L.stop[i] = i + 1 < L.start.size() ? L.start[i + 1] : ~0ull;
-    L.res.assign(L.start.size(), infl::LaneResult{0, 0, infl::kLaneCorrupt, 0});
+    L.res.assign(L.start.size(), infl::LaneResult{0, 0, 0, infl::kLaneCorrupt, 0, 0});
     L.dirty.assign(L.start.size(), 1);
+    L.tbase.assign(L.start.size(), 0);
+    L.tcap.assign(L.start.size(), 0);
+    L.big.assign(L.start.size(), 0);
     L.rounds = 0;
 }
 
-// After a count round: walk the chain from lane 0 (whose start is the stream's
+// After a decode round: walk the chain from lane 0 (whose start is the stream's
 // first block, so verified).  A lane whose start is verified and that stopped
 // exactly on its successor's start verifies that start.  One that passed it
 // (mismatch) shows the successor's candidate was not a block boundary: the
 // successor is dropped and the lane decodes on to the next one next round.
 // Returns 0 when every lane is verified (the output offsets are then valid),
 // 1 when dirty lanes must be decoded again, -1 when a verified lane found the
-// stream corrupt (or the rounds ran out).
+// stream corrupt (or the rounds ran out).  A lane that overflowed its token
+// region (kLaneOverflow) is decoded again; the caller gives it the large region.
 inline int check(Lanes& L, int max_rounds = 24) {
     ++L.rounds;
     bool verified = true;  // lane i's start is verified by this round's results
@@ -53,6 +69,13 @@ inline int check(Lanes& L, int max_rounds = 24) {
             continue;
         }
         const infl::LaneResult& r = L.res[i];
+        if (r.status == infl::kLaneOverflow) {  // token region too small: again, larger (the caller sizes it)
+            L.dirty[i] = 1;
+            verified = false;
+            any_dirty = true;
+            ++i;
+            continue;
+        }
         if (r.status == infl::kLaneOk) {
             ++i;
             continue;  // successor verified iff this one was
@@ -68,10 +91,7 @@ inline int check(Lanes& L, int max_rounds = 24) {
             ++i;
             continue;
         }
-        L.start.erase(L.start.begin() + (long)(i + 1));
-        L.res.erase(L.res.begin() + (long)(i + 1));
-        L.dirty.erase(L.dirty.begin() + (long)(i + 1));
-        L.stop.erase(L.stop.begin() + (long)(i + 1));
+        L.erase(i + 1);
         L.stop[i] = i + 1 < L.start.size() ? L.start[i + 1] : ~0ull;
         L.dirty[i] = 1;
         any_dirty = true;
