@@ -378,7 +378,8 @@ IK_HD int resolve_at(U16 u16, Off lane_obase, int n, Pages page_lane, int page_s
 //   W >= lim[14] is no code (an incomplete code's gap).
 // Canonical order within a length is by symbol value, so for the literal/length
 // code a length's codes are: its literals, then end-of-block, then length codes.
-// Table memory per lane (u32 words):
+// Table memory per lane (u32 words; the GPU keeps word w of lane l at LDS word
+// 64 w + l, so that lanes reading different words hit different banks):
 //   [0..15]  linfo[L]: first code (15 bits) | #literals of length L (9) << 15
 //                      | EOB has length L (1) << 24 | rank of its first length code (5) << 25
 //   [16..31] dinfo[L]: first distance code (15 bits) | rank of its first distance code (5) << 16
@@ -408,7 +409,8 @@ IK_HD uint32_t rev32(uint32_t v) {
 #endif
 }
 
-IK_HD uint8_t cm_byte(const uint32_t* m, int i) { return (uint8_t)(m[32 + (i >> 2)] >> (8 * (i & 3))); }
+template <class Mem>
+IK_HD uint8_t cm_byte(const Mem& m, int i) { return (uint8_t)(m[32 + (i >> 2)] >> (8 * (i & 3))); }
 
 // ---- token stream ---------------------------------------------------------------
 // The decode pass writes each lane's output as u16 tokens into the lane's own

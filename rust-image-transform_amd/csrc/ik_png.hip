@@ -170,58 +170,60 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
 // block three ahead of the one it reads.  The loop itself then reads only LDS,
 // so no lane's memory latency stalls its wave (a wave's vmcnt is shared by its
 // 64 lanes).
-constexpr int kRingBW = 8;    // words per block (32 B, two 16-B DMA slots)
+constexpr int kRingBW = 8;    // words per block (32 B)
 constexpr int kRingTick = 4;  // symbols between refills (< 256 bits: at most one block per interval)
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
+// a lane's u32 table in LDS, lane-minor (word w at 64 w + lane): conflict-free
+// whatever word each lane reads
+struct LaneLds {
+    lds_u32* p;  // s_tab + lane
+    __device__ lds_u32& operator[](int w) const { return p[w * 64]; }
+};
+
 struct WinLds {
     const IK_GLOBAL uint32_t* w;
     uint32_t nwords, pos, nextb, it;
-    lds_u32* ring;   // this wave's ring: [block % 4][slot][lane][4 words]
+    lds_u32* ring;   // this wave's ring, lane-minor: ring word r (0..31) of lane l at 64 r + l
     uint32_t lane;
-    __device__ uint32_t word(uint32_t wi) const {
-        const uint32_t B = wi / kRingBW, sl = (wi % kRingBW) >> 2, q = wi & 3u;
-        return ring[(((B & 3u) * (kRingBW / 4) + sl) * 64u + lane) * 4u + q];
-    }
-    // One 16-byte LDS-DMA of each lane's source into ring slot `base` (byte address in
-    // LDS; lane L lands at base + 16 L).  M0 carries the base, written in the same
-    // statement (the compiler does not preserve it around asm), and each slot has
-    // its own asm text: identical statements in the four branches below would be
-    // merged into one with a per-lane base -- which M0 cannot hold.
-#define IK_GLDS16(TAG)                                                                                 \
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t" \
+    __device__ uint32_t word(uint32_t wi) const { return ring[(wi & 31u) * 64u]; }
+    // Word k of block B of the calling lanes -> ring word 8 (B % 4) + k: one 4-byte
+    // LDS-DMA per word (the destination is M0 + 4 lane, i.e. lane-minor).  M0 is
+    // written in the same asm statement (the compiler does not preserve it), and
+    // each ring position has its own asm text: identical statements in the four
+    // branches would be merged into one with a per-lane base, which M0 cannot hold.
+#define IK_GLDS4(TAG)                                                                                  \
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"    \
                  "s_mov_b32 m0, %0 ; ring " TAG                                                        \
                  : "=&s"(keep)                                                                         \
                  : "v"(src), "s"(base)                                                                 \
                  : "memory")
-    __device__ void dma(uint32_t B) {  // block B of the calling lanes into ring position B % 4
-        static_assert(kRingBW == 8, "two 16-byte slots per block");
+#define IK_GLDS_BLOCK(P)                                                                               \
+    src = g + 0; base = r0 + ((P)*8 + 0) * 256; IK_GLDS4(#P "0");                                      \
+    src = g + 1; base = r0 + ((P)*8 + 1) * 256; IK_GLDS4(#P "1");                                      \
+    src = g + 2; base = r0 + ((P)*8 + 2) * 256; IK_GLDS4(#P "2");                                      \
+    src = g + 3; base = r0 + ((P)*8 + 3) * 256; IK_GLDS4(#P "3");                                      \
+    src = g + 4; base = r0 + ((P)*8 + 4) * 256; IK_GLDS4(#P "4");                                      \
+    src = g + 5; base = r0 + ((P)*8 + 5) * 256; IK_GLDS4(#P "5");                                      \
+    src = g + 6; base = r0 + ((P)*8 + 6) * 256; IK_GLDS4(#P "6");                                      \
+    src = g + 7; base = r0 + ((P)*8 + 7) * 256; IK_GLDS4(#P "7")
+    __device__ void dma(uint32_t B) {
+        static_assert(kRingBW == 8, "eight words per block");
         const IK_GLOBAL uint32_t* g = w + (size_t)B * kRingBW;
-        const uint32_t r0 = (uint32_t)(size_t)ring;
+        const uint32_t r0 = (uint32_t)(size_t)ring - 4u * lane;  // the wave's ring base (lane 0)
         uint32_t keep;
         const IK_GLOBAL uint32_t* src;
         uint32_t base;
         switch (B & 3u) {
-        case 0:
-            src = g; base = r0 + 0 * 1024; IK_GLDS16("0a");
-            src = g + 4; base = r0 + 1 * 1024; IK_GLDS16("0b");
-            break;
-        case 1:
-            src = g; base = r0 + 2 * 1024; IK_GLDS16("1a");
-            src = g + 4; base = r0 + 3 * 1024; IK_GLDS16("1b");
-            break;
-        case 2:
-            src = g; base = r0 + 4 * 1024; IK_GLDS16("2a");
-            src = g + 4; base = r0 + 5 * 1024; IK_GLDS16("2b");
-            break;
-        default:
-            src = g; base = r0 + 6 * 1024; IK_GLDS16("3a");
-            src = g + 4; base = r0 + 7 * 1024; IK_GLDS16("3b");
-            break;
+        case 0: IK_GLDS_BLOCK(0); break;
+        case 1: IK_GLDS_BLOCK(1); break;
+        case 2: IK_GLDS_BLOCK(2); break;
+        default: IK_GLDS_BLOCK(3); break;
         }
     }
-#undef IK_GLDS16
+#undef IK_GLDS_BLOCK
+#undef IK_GLDS4
     __device__ void init(const IK_GLOBAL uint32_t* words, uint32_t nw, uint32_t bit) {
         w = words;
         nwords = nw;
@@ -260,15 +262,15 @@ struct WinLds {
 
 __global__ __launch_bounds__(kPngInflateThreads) void k_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes,
                                                                    int nlanes, uint16_t* tok, infl::LaneResult* res) {
-    __shared__ uint32_t s_tab[kPngInflateThreads * infl::kCanonWords];
-    __shared__ uint32_t s_ring[4 * (kRingBW / 4) * 64 * 4];  // 4 blocks x 32 B per lane (one wave)
+    __shared__ uint32_t s_tab[kPngInflateThreads * infl::kCanonWords];  // lane-minor (LaneLds)
+    __shared__ uint32_t s_ring[4 * kRingBW * 64];                        // 4 blocks x 32 B per lane, lane-minor
     const int t = blockIdx.x * kPngInflateThreads + threadIdx.x;
     if (t >= nlanes) return;
     const PngLaneDev L = lanes[t];
     const PngImgDev I = imgs[L.img];
-    uint32_t* m = s_tab + threadIdx.x * infl::kCanonWords;
+    const LaneLds m{(lds_u32*)s_tab + threadIdx.x};
     WinLds win;
-    win.ring = (lds_u32*)s_ring;
+    win.ring = (lds_u32*)s_ring + threadIdx.x;
     win.lane = threadIdx.x;
     infl::TokOut out;
     out.p = (IK_GLOBAL uint16_t*)(tok + L.tbase);
@@ -286,7 +288,7 @@ struct TokInDev {
     const IK_GLOBAL uint64_t* g;  // the lane's region as pairs of u64 (16-byte groups)
     uint64_t a0, a1, n0, n1;
     uint32_t gi, k;
-    lds_u32* tab;                 // this thread's literal table in LDS: [16 B slot][thread][4 words]
+    lds_u32* tab;                 // this thread's literal table in LDS, lane-minor: word w at 64 w
     uint32_t lane;
     __device__ void init(const IK_GLOBAL uint16_t* p) {
         g = (const IK_GLOBAL uint64_t*)p;
@@ -309,36 +311,32 @@ struct TokInDev {
         }
         return v;
     }
-    // the block's literal table (256 bytes at token pos) -> LDS, 16 loads in flight
+    // the block's literal table (256 bytes at token pos) -> LDS, 32 loads in flight
     __device__ void set_table(uint32_t pos) {
         const IK_GLOBAL uint64_t* q = g + (size_t)(pos >> 2);
         uint64_t v[32];
 #pragma unroll
         for (int i = 0; i < 32; ++i) v[i] = q[i];
 #pragma unroll
-        for (int sl = 0; sl < 16; ++sl) {
-            lds_u32* d = tab + (sl * kPngExpandThreads + lane) * 4;
-            d[0] = (uint32_t)v[2 * sl];
-            d[1] = (uint32_t)(v[2 * sl] >> 32);
-            d[2] = (uint32_t)v[2 * sl + 1];
-            d[3] = (uint32_t)(v[2 * sl + 1] >> 32);
+        for (int i = 0; i < 32; ++i) {
+            tab[(2 * i) * kPngExpandThreads] = (uint32_t)v[i];
+            tab[(2 * i + 1) * kPngExpandThreads] = (uint32_t)(v[i] >> 32);
         }
     }
     __device__ uint32_t table(uint32_t rank) const {
-        const uint32_t w = tab[((rank >> 4) * kPngExpandThreads + lane) * 4 + ((rank >> 2) & 3u)];
-        return (w >> (8 * (rank & 3u))) & 0xFFu;
+        return (tab[(rank >> 2) * kPngExpandThreads] >> (8 * (rank & 3u))) & 0xFFu;
     }
 };
 
 __global__ __launch_bounds__(kPngExpandThreads) void k_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes,
                                                                   int nlanes, const uint16_t* tok, int* status) {
-    __shared__ uint32_t s_lits[16 * kPngExpandThreads * 4];  // 256 B of literal table per thread
+    __shared__ uint32_t s_lits[64 * kPngExpandThreads];  // 256 B of literal table per thread, lane-minor
     const int t = blockIdx.x * kPngExpandThreads + threadIdx.x;
     if (t >= nlanes) return;
     const PngLaneDev L = lanes[t];
     const PngImgDev I = imgs[L.img];
     TokInDev tin;
-    tin.tab = (lds_u32*)s_lits;
+    tin.tab = (lds_u32*)s_lits + threadIdx.x;
     tin.lane = threadIdx.x;
     tin.init((const IK_GLOBAL uint16_t*)(tok + L.tbase));
     status[t] = infl::expand_lane(tin, L.ntok, infl::U16Out{(IK_GLOBAL uint16_t*)I.u16}, L.obase, L.out_len);

@@ -1,0 +1,386 @@
+/* transform_test.c -- the reference's tests/transform.rs, ported to C over the
+ * C-ABI boundary (include/imagekit_hip.h) with host pixel buffers: every
+ * DynamicImage::new_rgb8 / new_rgba8 becomes ik_image_from_host of zeroed
+ * pixels, resize_image / encode_image / decode_image become ik_resize /
+ * ik_encode / ik_decode, and dimensions() is ik_image_info.  One function per
+ * #[test] of /root/reference/tests/transform.rs (same names, same assertions).
+ *
+ * Built by rust-image-transform_amd/Makefile (lib/transform_test, linked
+ * against lib/libimagekit_hip.so); run by tests/test_c_boundary.py on a GPU.
+ * Prints one line per test; the exit status is the number of failures. */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/imagekit_hip.h"
+
+static int failures = 0;
+static char msg[512];
+
+#define CHECK(cond, ...)                                  \
+    do {                                                  \
+        if (!(cond)) {                                    \
+            snprintf(msg, sizeof msg, __VA_ARGS__);       \
+            return 1;                                     \
+        }                                                 \
+    } while (0)
+
+static void run(const char *name, int (*fn)(void)) {
+    msg[0] = 0;
+    const int bad = fn();
+    printf("%s %s%s%s\n", bad ? "FAIL" : "PASS", name, bad ? ": " : "", bad ? msg : "");
+    failures += bad;
+}
+
+/* image::DynamicImage::new_rgb8 / new_rgba8: zeroed pixels */
+static ik_image *new_image(uint32_t w, uint32_t h, uint32_t c) {
+    uint8_t *px = calloc((size_t)w * h * c, 1);
+    ik_image *img = NULL;
+    if (px && ik_image_from_host(px, w, h, c, &img) != IK_OK) img = NULL;
+    free(px);
+    return img;
+}
+
+static void dims(const ik_image *img, uint32_t *w, uint32_t *h) {
+    uint32_t c = 0;
+    *w = *h = 0;
+    ik_image_info(img, w, h, &c);
+}
+
+/* resize_image(img, w, h): None = -1; the by-value argument is dropped */
+static ik_image *resize(ik_image *img, int64_t w, int64_t h) {
+    ik_image *out = NULL;
+    const int rc = ik_resize(img, w, h, IK_FILTER_LANCZOS3, &out);
+    if (rc != IK_OK) {
+        ik_image_free(img);
+        return NULL;
+    }
+    if (out != img) ik_image_free(img);
+    return out;
+}
+
+static int encode(const ik_image *img, int fmt, int q, uint8_t **out, size_t *len) {
+    *out = NULL;
+    *len = 0;
+    return ik_encode(img, fmt, q, out, len);
+}
+
+static int resize_case(uint32_t w0, uint32_t h0, int64_t w, int64_t h, uint32_t ew, uint32_t eh) {
+    ik_image *img = new_image(w0, h0, 3);
+    CHECK(img, "new_rgb8(%u, %u) failed", w0, h0);
+    ik_image *r = resize(img, w, h);
+    CHECK(r, "resize_image failed");
+    uint32_t rw, rh;
+    dims(r, &rw, &rh);
+    ik_image_free(r);
+    CHECK(rw == ew && rh == eh, "dimensions (%u, %u), expected (%u, %u)", rw, rh, ew, eh);
+    return 0;
+}
+
+/* ---- dimension verification ---- */
+static int test_resize_dimensions_width_only(void) { return resize_case(800, 600, 400, -1, 400, 300); }
+static int test_resize_dimensions_height_only(void) { return resize_case(800, 600, -1, 300, 400, 300); }
+static int test_resize_both_dimensions(void) { return resize_case(800, 600, 400, 300, 400, 300); }
+static int test_resize_preserves_aspect_ratio_non_standard(void) { return resize_case(1920, 1080, 960, -1, 960, 540); }
+
+/* ---- edge cases ---- */
+static int test_no_resize_when_no_dimensions(void) { return resize_case(800, 600, -1, -1, 800, 600); }
+static int test_resize_larger_than_original(void) { return resize_case(100, 100, 200, 200, 200, 200); }
+static int test_resize_minimum_dimensions(void) { return resize_case(800, 600, 1, 1, 1, 1); }
+static int test_resize_very_small_to_large(void) { return resize_case(2, 2, 200, 200, 200, 200); }
+
+/* ---- decode / encode ---- */
+static int test_decode_invalid_data(void) {
+    uint8_t data[100];
+    memset(data, 0, sizeof data);
+    ik_image *img = NULL;
+    int fmt = 0;
+    const int rc = ik_decode(data, sizeof data, &img, &fmt);
+    if (img) ik_image_free(img);
+    CHECK(rc != IK_OK, "Should fail on invalid image data");
+    return 0;
+}
+
+static int test_decode_empty_data(void) {
+    ik_image *img = NULL;
+    int fmt = 0;
+    static const uint8_t none[1] = {0};
+    const int rc = ik_decode(none, 0, &img, &fmt);
+    if (img) ik_image_free(img);
+    CHECK(rc != IK_OK, "Should fail on empty data");
+    return 0;
+}
+
+/* a PNG of w x h zero RGBA pixels (img.write_to(.., ImageFormat::Png) in the
+ * Rust test): zlib stored blocks, CRCs and Adler-32 computed here */
+static uint32_t crc_table[256];
+static uint32_t crc32_of(const uint8_t *p, size_t n, uint32_t c) {
+    if (!crc_table[1])
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t v = i;
+            for (int k = 0; k < 8; ++k) v = v & 1 ? 0xEDB88320u ^ (v >> 1) : v >> 1;
+            crc_table[i] = v;
+        }
+    c = ~c;
+    for (size_t i = 0; i < n; ++i) c = crc_table[(c ^ p[i]) & 255] ^ (c >> 8);
+    return ~c;
+}
+static void be32(uint8_t *p, uint32_t v) {
+    p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+}
+static size_t put_chunk(uint8_t *o, const char *type, const uint8_t *d, uint32_t n) {
+    be32(o, n);
+    memcpy(o + 4, type, 4);
+    if (n) memcpy(o + 8, d, n);
+    be32(o + 8 + n, crc32_of(o + 4, n + 4, 0));
+    return 12 + (size_t)n;
+}
+static uint8_t *zero_rgba_png(uint32_t w, uint32_t h, size_t *len) {
+    const size_t raw_n = (size_t)h * (1 + 4 * (size_t)w);
+    uint8_t *raw = calloc(raw_n, 1); /* filter byte 0 + zero pixels per row */
+    const size_t nblk = (raw_n + 65534) / 65535;
+    const size_t z_n = 2 + raw_n + 5 * nblk + 4;
+    uint8_t *z = malloc(z_n), *png = malloc(z_n + 128);
+    size_t o = 0, done = 0;
+    z[o++] = 0x78; z[o++] = 0x01;
+    while (done < raw_n) {
+        const size_t n = raw_n - done < 65535 ? raw_n - done : 65535;
+        z[o++] = done + n == raw_n ? 1 : 0;
+        z[o++] = (uint8_t)n; z[o++] = (uint8_t)(n >> 8);
+        z[o++] = (uint8_t)~n; z[o++] = (uint8_t)(~n >> 8);
+        memcpy(z + o, raw + done, n);
+        o += n;
+        done += n;
+    }
+    uint32_t a = 1, b = 0;
+    for (size_t i = 0; i < raw_n; ++i) { a = (a + raw[i]) % 65521; b = (b + a) % 65521; }
+    be32(z + o, (b << 16) | a);
+    o += 4;
+    size_t p = 0;
+    memcpy(png, "\x89PNG\r\n\x1a\n", 8);
+    p = 8;
+    uint8_t ihdr[13];
+    be32(ihdr, w); be32(ihdr + 4, h);
+    ihdr[8] = 8; ihdr[9] = 6; ihdr[10] = ihdr[11] = ihdr[12] = 0;
+    p += put_chunk(png + p, "IHDR", ihdr, 13);
+    p += put_chunk(png + p, "IDAT", z, (uint32_t)o);
+    p += put_chunk(png + p, "IEND", NULL, 0);
+    free(raw);
+    free(z);
+    *len = p;
+    return png;
+}
+
+static int decode_then_webp(void) {
+    size_t n;
+    uint8_t *png = zero_rgba_png(64, 64, &n);
+    ik_image *img = NULL;
+    int fmt = 0;
+    const int rc = ik_decode(png, n, &img, &fmt);
+    free(png);
+    CHECK(rc == IK_OK && img, "decode_image(png) failed");
+    uint8_t *out;
+    size_t len;
+    const int e = encode(img, IK_FORMAT_WEBP, 75, &out, &len);
+    ik_image_free(img);
+    CHECK(e == IK_OK && len > 0, "encode_image(webp) failed");
+    ik_buf_free(out);
+    return 0;
+}
+
+/* ---- format conversion ---- */
+static int test_all_format_encodings(void) {
+    ik_image *img = new_image(100, 100, 3);
+    CHECK(img, "new_rgb8 failed");
+    uint8_t *out;
+    size_t len;
+    int e = encode(img, IK_FORMAT_JPEG, 80, &out, &len);
+    const int jpeg_ok = e == IK_OK && len > 0, jpeg_hdr = jpeg_ok && out[0] == 0xFF && out[1] == 0xD8;
+    if (e == IK_OK) ik_buf_free(out);
+    e = encode(img, IK_FORMAT_WEBP, 80, &out, &len);
+    const int webp_ok = e == IK_OK && len > 0;
+    if (e == IK_OK) ik_buf_free(out);
+    e = encode(img, IK_FORMAT_AVIF, 80, &out, &len);
+    const int avif_ok = e == IK_OK && len > 0;
+    if (e == IK_OK) ik_buf_free(out);
+    ik_image_free(img);
+    CHECK(jpeg_ok, "JPEG encoding should produce output");
+    CHECK(jpeg_hdr, "Should have valid JPEG header");
+    CHECK(webp_ok, "WebP encoding should produce output");
+    CHECK(avif_ok, "AVIF encoding should produce output");
+    return 0;
+}
+
+static int test_format_conversion_round_trip(void) {
+    ik_image *img = new_image(50, 50, 3);
+    CHECK(img, "new_rgb8 failed");
+    uint8_t *out;
+    size_t len;
+    const int e = encode(img, IK_FORMAT_WEBP, 80, &out, &len);
+    ik_image_free(img);
+    CHECK(e == IK_OK, "encode_image(webp) failed");
+    ik_image *dec = NULL;
+    int fmt = -2;
+    const int d = ik_decode(out, len, &dec, &fmt);
+    ik_buf_free(out);
+    CHECK(d == IK_OK && dec, "decode_image(webp) failed");
+    uint32_t w, h;
+    dims(dec, &w, &h);
+    ik_image_free(dec);
+    CHECK(w == 50 && h == 50, "Dimensions should be preserved in round trip: (%u, %u)", w, h);
+    CHECK(fmt == IK_FORMAT_WEBP, "Format should be correctly detected (got %d)", fmt);
+    return 0;
+}
+
+/* ---- quality / compression ---- */
+static int test_quality_affects_jpeg_size(void) {
+    ik_image *img = new_image(500, 500, 3);
+    CHECK(img, "new_rgb8 failed");
+    uint8_t *lo, *hi;
+    size_t nlo, nhi;
+    const int a = encode(img, IK_FORMAT_JPEG, 10, &lo, &nlo), b = encode(img, IK_FORMAT_JPEG, 95, &hi, &nhi);
+    ik_image_free(img);
+    if (a == IK_OK) ik_buf_free(lo);
+    if (b == IK_OK) ik_buf_free(hi);
+    CHECK(a == IK_OK && b == IK_OK, "encode_image(jpeg) failed");
+    CHECK(nhi > nlo, "Higher quality JPEG should produce larger file. Low: %zu bytes, High: %zu bytes", nlo, nhi);
+    return 0;
+}
+
+static int test_quality_affects_webp_size(void) {
+    ik_image *img = new_image(500, 500, 3);
+    CHECK(img, "new_rgb8 failed");
+    uint8_t *lo, *hi;
+    size_t nlo, nhi;
+    const int a = encode(img, IK_FORMAT_WEBP, 10, &lo, &nlo), b = encode(img, IK_FORMAT_WEBP, 95, &hi, &nhi);
+    ik_image_free(img);
+    if (a == IK_OK) ik_buf_free(lo);
+    if (b == IK_OK) ik_buf_free(hi);
+    CHECK(a == IK_OK && nlo > 0, "Low quality WebP should produce output");
+    CHECK(b == IK_OK && nhi > 0, "High quality WebP should produce output");
+    return 0;
+}
+
+static int test_quality_clamping_jpeg(void) {
+    ik_image *img = new_image(100, 100, 3);
+    CHECK(img, "new_rgb8 failed");
+    uint8_t *o0, *o1;
+    size_t n0, n1;
+    const int a = encode(img, IK_FORMAT_JPEG, 0, &o0, &n0), b = encode(img, IK_FORMAT_JPEG, 101, &o1, &n1);
+    ik_image_free(img);
+    if (a == IK_OK) ik_buf_free(o0);
+    if (b == IK_OK) ik_buf_free(o1);
+    CHECK(a == IK_OK, "Should clamp quality 0 to valid range");
+    CHECK(b == IK_OK, "Should clamp quality 101 to valid range");
+    return 0;
+}
+
+/* ---- integration: resize + encode ---- */
+static int resize_and_encode_jpeg(void) {
+    ik_image *r = resize(new_image(800, 600, 3), 400, -1);
+    CHECK(r, "resize_image failed");
+    uint32_t w, h;
+    dims(r, &w, &h);
+    uint8_t *out;
+    size_t len;
+    const int e = encode(r, IK_FORMAT_JPEG, 80, &out, &len);
+    ik_image_free(r);
+    if (e == IK_OK) ik_buf_free(out);
+    CHECK(w == 400 && h == 300, "Resize should produce correct dimensions: (%u, %u)", w, h);
+    CHECK(e == IK_OK && len > 0, "Encoded JPEG should have non-zero size");
+    return 0;
+}
+
+static int test_full_pipeline_webp(void) {
+    ik_image *r = resize(new_image(1920, 1080, 3), 640, 480);
+    CHECK(r, "resize_image failed");
+    uint32_t w, h;
+    dims(r, &w, &h);
+    CHECK(w == 640 && h == 360, "Resize preserves aspect ratio: 1920x1080 -> 640x360, got (%u, %u)", w, h);
+    uint8_t *out;
+    size_t len;
+    const int e = encode(r, IK_FORMAT_WEBP, 85, &out, &len);
+    ik_image_free(r);
+    CHECK(e == IK_OK && len > 0, "encode_image(webp) failed");
+    ik_image *dec = NULL;
+    int fmt = -2;
+    const int d = ik_decode(out, len, &dec, &fmt);
+    ik_buf_free(out);
+    CHECK(d == IK_OK && dec, "decode_image(webp) failed");
+    dims(dec, &w, &h);
+    ik_image_free(dec);
+    CHECK(w == 640 && h == 360, "decoded (%u, %u)", w, h);
+    CHECK(fmt == IK_FORMAT_WEBP, "format %d", fmt);
+    return 0;
+}
+
+static int test_full_pipeline_avif(void) {
+    ik_image *r = resize(new_image(800, 600, 3), 400, -1);
+    CHECK(r, "resize_image failed");
+    uint32_t w, h;
+    dims(r, &w, &h);
+    CHECK(w == 400 && h == 300, "(%u, %u)", w, h);
+    uint8_t *out;
+    size_t len;
+    const int e = encode(r, IK_FORMAT_AVIF, 80, &out, &len);
+    ik_image_free(r);
+    if (e == IK_OK) ik_buf_free(out);
+    CHECK(e == IK_OK && len > 0, "encode_image(avif) failed");
+    return 0;
+}
+
+/* ---- performance / size ---- */
+static int test_resize_reduces_size(void) {
+    ik_image *img = new_image(1000, 1000, 3);
+    CHECK(img, "new_rgb8 failed");
+    uint8_t *o0, *o1;
+    size_t n0, n1;
+    const int a = encode(img, IK_FORMAT_JPEG, 80, &o0, &n0);
+    /* img.clone() into resize_image: the shim's by-value argument is a copy */
+    ik_image *copy = NULL;
+    uint8_t *px = malloc((size_t)1000 * 1000 * 3);
+    int c = px ? ik_image_to_host(img, px, (size_t)1000 * 1000 * 3) : IK_ERR_NOMEM;
+    if (c == IK_OK) c = ik_image_from_host(px, 1000, 1000, 3, &copy);
+    free(px);
+    ik_image_free(img);
+    ik_image *r = c == IK_OK ? resize(copy, 100, 100) : NULL;
+    const int b = r ? encode(r, IK_FORMAT_JPEG, 80, &o1, &n1) : IK_ERR_INVALID;
+    if (r) ik_image_free(r);
+    if (a == IK_OK) ik_buf_free(o0);
+    if (b == IK_OK) ik_buf_free(o1);
+    CHECK(a == IK_OK && b == IK_OK, "encode failed");
+    CHECK(n1 < n0, "Resized image should produce smaller file. Original: %zu bytes, Resized: %zu bytes", n0, n1);
+    return 0;
+}
+
+int main(void) {
+    if (ik_init(0) != IK_OK) {
+        char e[256];
+        ik_last_error(e, sizeof e);
+        printf("FAIL ik_init: %s\n", e);
+        return 99;
+    }
+    run("test_resize_dimensions_width_only", test_resize_dimensions_width_only);
+    run("test_resize_dimensions_height_only", test_resize_dimensions_height_only);
+    run("test_resize_both_dimensions", test_resize_both_dimensions);
+    run("test_resize_preserves_aspect_ratio_non_standard", test_resize_preserves_aspect_ratio_non_standard);
+    run("test_no_resize_when_no_dimensions", test_no_resize_when_no_dimensions);
+    run("test_resize_larger_than_original", test_resize_larger_than_original);
+    run("test_resize_minimum_dimensions", test_resize_minimum_dimensions);
+    run("test_resize_very_small_to_large", test_resize_very_small_to_large);
+    run("test_decode_invalid_data", test_decode_invalid_data);
+    run("test_decode_empty_data", test_decode_empty_data);
+    run("decode_then_webp", decode_then_webp);
+    run("test_all_format_encodings", test_all_format_encodings);
+    run("test_format_conversion_round_trip", test_format_conversion_round_trip);
+    run("test_quality_affects_jpeg_size", test_quality_affects_jpeg_size);
+    run("test_quality_affects_webp_size", test_quality_affects_webp_size);
+    run("test_quality_clamping_jpeg", test_quality_clamping_jpeg);
+    run("resize_and_encode_jpeg", resize_and_encode_jpeg);
+    run("test_full_pipeline_webp", test_full_pipeline_webp);
+    run("test_full_pipeline_avif", test_full_pipeline_avif);
+    run("test_resize_reduces_size", test_resize_reduces_size);
+    printf("%d failed\n", failures);
+    return failures;
+}
