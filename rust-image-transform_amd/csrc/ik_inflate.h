@@ -333,7 +333,10 @@ struct LaneResult {
     uint32_t ntok;      // tokens it wrote (decode pass)
     int status;         // LaneStatus (or kLaneOverflow)
     int final_block;    // it decoded the BFINAL block
-    int pad;
+    uint32_t iters;     // symbol-loop iterations (profile)
+    uint32_t kcycles;   // GPU: clock ticks / 1024 from start to end (profile)
+    uint32_t blocks;    // blocks decoded
+    uint32_t pad;
 };
 
 // Decode whole blocks from `start` (a block boundary) until a block boundary >=
@@ -599,6 +602,8 @@ IK_HD void decode_lane_tok(const uint32_t* words, uint64_t nbits, uint64_t start
     uint64_t h0 = 0, h1 = 0;  // the last 8 tokens (newest in the top 16 bits of h1)
     r.status = kLaneCorrupt;
     r.final_block = 0;
+    r.iters = 0;
+    r.blocks = 0;
     uint8_t lens[288 + 32];
     CanonRegs R;
     auto tput = [&](uint32_t v) {
@@ -666,8 +671,10 @@ IK_HD void decode_lane_tok(const uint32_t* words, uint64_t nbits, uint64_t start
             }
             tc += kTokTableLen;
             W.init((const IK_GLOBAL uint32_t*)words, (uint32_t)nwords, (uint32_t)b.pos());
+            ++r.blocks;
             bool bad = false, full = false;
             for (;;) {
+                ++r.iters;
                 if ((uint64_t)W.pos > plimit) { bad = true; break; }
                 W.tick(out);
                 const uint64_t v = W.bits64();

@@ -9,8 +9,10 @@
 //                   the next lane's start -> the lane's token stream and output
 //                   length.  Code tables in LDS per thread (192 B), input through
 //                   an LDS ring filled by LDS-DMA (128 B per thread)
-//   k_png_expand    one thread per verified lane: tokens -> u16 symbols (bytes,
-//                   window markers) at the lane's output offset; no LDS
+//   k_png_expand    one wave per verified lane: tokens -> u16 symbols (bytes,
+//                   window markers) at the lane's output offset, 64 tokens per
+//                   step with every output position resolved in parallel;
+//                   status and clock ticks / 1024 per lane (status[2 t], [2 t + 1])
 //   k_png_resolve   u16 symbols -> the filtered bytes of every row, 16 per thread,
 //                   markers followed to their source; rows land 16-B aligned in
 //                   the destination image (pitched) and filter types in ft[]
@@ -275,71 +277,198 @@ __global__ __launch_bounds__(kPngInflateThreads) void k_png_decode(const PngImgD
     infl::TokOut out;
     out.p = (IK_GLOBAL uint16_t*)(tok + L.tbase);
     infl::LaneResult r;
+    const uint64_t c0 = clock64();
     infl::decode_lane_tok(I.words, I.nbits, L.start, L.stop, m, out, L.ntok, L.first != 0, I.raw_total, r, win);
+    r.kcycles = (uint32_t)((clock64() - c0) >> 10);
     res[t] = r;
 }
 
 // ---- expand -----------------------------------------------------------------------
-// One thread per verified lane: its tokens -> u16 symbols at its output offset
-// (ik_inflate.h expand_lane).  No LDS and few registers, so the CUs hold many
-// waves, and their copies' loads (distance > 8: symbols this lane stored
-// before) overlap across waves.  Tokens arrive in 16-byte groups, one group ahead.
-struct TokInDev {
-    const IK_GLOBAL uint64_t* g;  // the lane's region as pairs of u64 (16-byte groups)
-    uint64_t a0, a1, n0, n1;
-    uint32_t gi, k;
-    lds_u32* tab;                 // this thread's literal table in LDS, lane-minor: word w at 64 w
-    uint32_t lane;
-    __device__ void init(const IK_GLOBAL uint16_t* p) {
-        g = (const IK_GLOBAL uint64_t*)p;
-        seek(0);
-    }
-    __device__ void seek(uint32_t t) {
-        gi = t >> 3;
-        k = t & 7u;
-        a0 = g[2 * gi]; a1 = g[2 * gi + 1];
-        n0 = g[2 * gi + 2]; n1 = g[2 * gi + 3];
-        gi += 2;
-    }
-    __device__ uint32_t next() {
-        const uint32_t v = (uint32_t)(((k < 4 ? a0 : a1) >> (16 * (k & 3u))) & 0xFFFFu);
-        if (++k == 8) {
-            a0 = n0; a1 = n1;
-            n0 = g[2 * gi]; n1 = g[2 * gi + 1];
-            ++gi;
-            k = 0;
-        }
-        return v;
-    }
-    // the block's literal table (256 bytes at token pos) -> LDS, 32 loads in flight
-    __device__ void set_table(uint32_t pos) {
-        const IK_GLOBAL uint64_t* q = g + (size_t)(pos >> 2);
-        uint64_t v[32];
-#pragma unroll
-        for (int i = 0; i < 32; ++i) v[i] = q[i];
-#pragma unroll
-        for (int i = 0; i < 32; ++i) {
-            tab[(2 * i) * kPngExpandThreads] = (uint32_t)v[i];
-            tab[(2 * i + 1) * kPngExpandThreads] = (uint32_t)(v[i] >> 32);
-        }
-    }
-    __device__ uint32_t table(uint32_t rank) const {
-        return (tab[(rank >> 2) * kPngExpandThreads] >> (8 * (rank & 3u))) & 0xFFu;
-    }
-};
+// One WAVE per verified lane (one DEFLATE block, ~32K symbols): the lane's tokens
+// -> u16 symbols at its output offset, in batches of up to 64 tokens:
+//   1. each thread takes one token; a token after a match's first token is its
+//      distance (distances are < 0x8000, so the test is local); a wave prefix
+//      sum of the symbols' output lengths gives every symbol's offset in the
+//      batch (batches end before a table record and hold <= kXCap symbols)
+//   2. every output position of the batch is resolved by its own thread: a
+//      literal; or, for a copy, the source position (period `dist` inside an
+//      overlapping copy) -- an earlier position of the same batch is followed
+//      back through its own symbol, a position before the batch is read from
+//      the wave's LDS ring of recent output (<= kXNear back) or from memory
+//      (farther; all of a thread's loads in flight together), and one before
+//      the lane's first symbol becomes a window marker (0x8000 | index into the
+//      32 KiB before the lane, as the resolve pass expects)
+//   3. the batch goes to the ring and, coalesced, to memory.
+// So a block costs a few memory round trips per 64 tokens instead of one per
+// copy, and 64 lanes share each one.
+constexpr int kXRing = 4096;            // recent output symbols per wave (LDS, power of two)
+constexpr int kXCap = 1024;             // output symbols per batch at most
+constexpr int kXNear = kXRing - kXCap;  // sources at most this far back come from the ring
+constexpr int kXGroup = 4;              // output positions per thread resolved together
+using infl::kTokMatch;
+using infl::kTokPad;
+using infl::kTokRaw;
+using infl::kTokTable;
+using infl::kTokTableLen;
 
-__global__ __launch_bounds__(kPngExpandThreads) void k_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes,
-                                                                  int nlanes, const uint16_t* tok, int* status) {
-    __shared__ uint32_t s_lits[64 * kPngExpandThreads];  // 256 B of literal table per thread, lane-minor
-    const int t = blockIdx.x * kPngExpandThreads + threadIdx.x;
-    if (t >= nlanes) return;
-    const PngLaneDev L = lanes[t];
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
+    const int x = threadIdx.x;
+    uint32_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = (uint32_t)__shfl_up((int)incl, o, 64);
+        if (x >= o) incl += u;
+    }
+    *total = (uint32_t)__shfl((int)incl, 63, 64);
+    return incl - v;
+}
+
+__global__ __launch_bounds__(64) void k_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int nlanes,
+                                                   const uint16_t* tok, int* status) {
+    __shared__ uint16_t s_ring[kXRing];
+    __shared__ uint32_t s_tab[64];   // the block's literal table (256 bytes)
+    __shared__ uint32_t s_end[64];   // per token slot: end offset of its symbol in the batch (inclusive scan)
+    __shared__ uint32_t s_info[64];  // per token slot: bit 31 set = literal (value in bits 0..7), else len | (dist - 1) << 16
+    const int li = blockIdx.x;
+    if (li >= nlanes) return;
+    const int x = threadIdx.x;
+    const uint64_t c0 = clock64();
+    const PngLaneDev L = lanes[li];
     const PngImgDev I = imgs[L.img];
-    TokInDev tin;
-    tin.tab = (lds_u32*)s_lits + threadIdx.x;
-    tin.lane = threadIdx.x;
-    tin.init((const IK_GLOBAL uint16_t*)(tok + L.tbase));
-    status[t] = infl::expand_lane(tin, L.ntok, infl::U16Out{(IK_GLOBAL uint16_t*)I.u16}, L.obase, L.out_len);
+    const IK_GLOBAL uint16_t* T = (const IK_GLOBAL uint16_t*)(tok + L.tbase);
+    IK_GLOBAL uint16_t* out = (IK_GLOBAL uint16_t*)I.u16 + L.obase;
+    const uint32_t ntok = L.ntok;
+    uint32_t t = 0, cnt = 0;
+    bool have_tab = false, bad = false;
+    // this batch's tokens (and the one after each), loaded one batch ahead
+    uint32_t u = x < (int)ntok ? (uint32_t)T[x] : kTokPad;
+    uint32_t un = x + 1 < (int)ntok ? (uint32_t)T[x + 1] : 0u;
+    while (t < ntok && !bad) {
+        // a table record at the batch start: the literal table -> LDS
+        const unsigned long long mk = __ballot(u == kTokTable);
+        if (mk & 1ull) {
+            const uint32_t tt = (t + 8) & ~7u;  // pads (0xFFFE) up to a multiple of 8 tokens
+            if (tt + kTokTableLen > ntok) { bad = true; break; }
+            s_tab[x] = ((const IK_GLOBAL uint32_t*)(T + tt))[x];
+            have_tab = true;
+            t = tt + kTokTableLen;
+            u = t + x < ntok ? (uint32_t)T[t + x] : kTokPad;
+            un = t + x + 1 < ntok ? (uint32_t)T[t + x + 1] : 0u;
+            __syncthreads();
+            continue;
+        }
+        uint32_t n = mk ? (uint32_t)__ffsll((long long)mk) - 1u : 64u;
+        if (t + n > ntok) n = ntok - t;
+        // a match's first token in the last slot: its distance is in the next batch
+        const unsigned long long mf = __ballot((u & 0xFF00u) == kTokMatch);
+        if ((mf >> (n - 1)) & 1ull) --n;
+        if (n == 0) { bad = true; break; }  // a match cut off by the end of the tokens
+        const uint32_t up = (uint32_t)__shfl_up((int)u, 1, 64);
+        const bool start = x < (int)n && !(x > 0 && (up & 0xFF00u) == kTokMatch);
+        uint32_t len = 0, info = 0;
+        if (start) {
+            if (u < 256u) {
+                if (!have_tab) bad = true;
+                len = 1;
+                info = 0x80000000u | ((s_tab[u >> 2] >> (8 * (u & 3u))) & 0xFFu);
+            } else if ((u & 0xFF00u) == kTokRaw) {
+                len = 1;
+                info = 0x80000000u | (u & 0xFFu);
+            } else if ((u & 0xFF00u) == kTokMatch) {
+                len = (u & 0xFFu) + 3u;
+                info = len | (un << 16);  // the distance token holds dist - 1 (< 0x8000)
+            } else {
+                bad = true;
+            }
+        }
+        if (__ballot(bad)) { bad = true; break; }
+        uint32_t tot;
+        uint32_t off = wave_excl_scan(len, &tot);
+        if (tot > (uint32_t)kXCap) {  // cut the batch before the first symbol that does not fit
+            const unsigned long long over = __ballot(start && off + len > (uint32_t)kXCap);
+            const uint32_t x0 = (uint32_t)__ffsll((long long)over) - 1u;  // > 0: one symbol always fits
+            n = x0;
+            if (x >= (int)x0) len = 0;
+            off = wave_excl_scan(len, &tot);
+        }
+        s_end[x] = off + len;
+        s_info[x] = info;
+        // the next batch's tokens, in flight while this one resolves
+        const uint32_t t2 = t + n;
+        u = t2 + x < ntok ? (uint32_t)T[t2 + x] : kTokPad;
+        un = t2 + x + 1 < ntok ? (uint32_t)T[t2 + x + 1] : 0u;
+        __syncthreads();
+        // resolve this thread's positions q = x + 64 k, kXGroup of them at a time
+        for (uint32_t g0 = 0; g0 < tot; g0 += 64 * kXGroup) {
+            int sl[kXGroup];
+            uint32_t qk[kXGroup];
+#pragma unroll
+            for (int k = 0; k < kXGroup; ++k) {
+                qk[k] = g0 + (uint32_t)x + 64u * k;
+                sl[k] = 0;
+            }
+            // the symbol holding q: the first slot whose end > q (all searches in lockstep)
+#pragma unroll
+            for (int st = 32; st >= 1; st >>= 1)
+#pragma unroll
+                for (int k = 0; k < kXGroup; ++k)
+                    if (s_end[sl[k] + st - 1] <= qk[k]) sl[k] += st;
+            uint16_t val[kXGroup];
+            int64_t gsrc[kXGroup];  // >= 0: read from memory at out[gsrc]
+#pragma unroll
+            for (int k = 0; k < kXGroup; ++k) {
+                val[k] = 0;
+                gsrc[k] = -1;
+                if (qk[k] >= tot) continue;
+                int32_t q = (int32_t)qk[k];
+                int lo = sl[k];
+                for (int guard = 0; guard < 1024; ++guard) {
+                    const uint32_t inf = s_info[lo];
+                    if (inf & 0x80000000u) { val[k] = (uint16_t)(inf & 0xFFu); break; }
+                    const int32_t o = (int32_t)(s_end[lo] - (inf & 0xFFFFu));
+                    const int32_t d = (int32_t)(inf >> 16) + 1;
+                    const int32_t j = q - o, ln = (int32_t)(inf & 0xFFFFu);
+                    const int32_t src = o - d + (d >= ln ? j : j % d);  // relative to the batch start
+                    if (src >= 0) {  // an earlier position of this batch: its own symbol
+                        q = src;
+                        lo = 0;
+#pragma unroll
+                        for (int st = 32; st >= 1; st >>= 1)
+                            if (s_end[lo + st - 1] <= (uint32_t)q) lo += st;
+                        continue;
+                    }
+                    const int64_t abs = (int64_t)cnt + src;  // relative to the lane's first symbol
+                    if (abs < 0) {
+                        if (abs < -(int64_t)infl::kWindow) bad = true;
+                        val[k] = (uint16_t)(0x8000u | (uint32_t)(infl::kWindow + abs));
+                    } else if (-src <= kXNear) {
+                        val[k] = s_ring[(uint32_t)abs & (kXRing - 1)];
+                    } else {
+                        gsrc[k] = abs;
+                    }
+                    break;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kXGroup; ++k)
+                if (gsrc[k] >= 0) val[k] = out[gsrc[k]];
+            // (ring slots written here held positions older than any this batch reads)
+#pragma unroll
+            for (int k = 0; k < kXGroup; ++k)
+                if (qk[k] < tot) {
+                    s_ring[(cnt + qk[k]) & (kXRing - 1)] = val[k];
+                    out[(int64_t)cnt + qk[k]] = val[k];
+                }
+        }
+        __syncthreads();
+        cnt += tot;
+        t = t2;
+        if (__ballot(bad)) bad = true;
+    }
+    if (x == 0) {
+        status[2 * li] = (!bad && cnt == L.out_len) ? 0 : -1;
+        status[2 * li + 1] = (int)((clock64() - c0) >> 10);  // profile: clock ticks / 1024
+    }
 }
 
 // ---- resolve ------------------------------------------------------------------------
@@ -502,8 +631,7 @@ hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, int
 hipError_t launch_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int n, const uint16_t* tok, int* status,
                              hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    const dim3 grid((n + kPngExpandThreads - 1) / kPngExpandThreads);
-    hipLaunchKernelGGL(k_png_expand, grid, dim3(kPngExpandThreads), 0, s, imgs, lanes, n, tok, status);
+    hipLaunchKernelGGL(k_png_expand, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status);
     return hipGetLastError();
 }
 

@@ -246,7 +246,7 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
         }
         tok_total += tok_total / 2 + 64;
         size_t dyn = up256(sizeof(PngLaneDev) * max_lanes) + up256(sizeof(infl::LaneResult) * max_lanes) +
-                     up256(sizeof(int64_t) * max_lanes) + up256(sizeof(int) * max_lanes) +
+                     up256(sizeof(int64_t) * max_lanes) + up256(2 * sizeof(int) * max_lanes) +
                      up256(sizeof(PngImgDev) * m);
         size_t nrows = 0, npages = 0;
         for (PngJob* j : J) {
@@ -273,7 +273,7 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             d_obase = reinterpret_cast<int64_t*>(dev + o);
             o += up256(sizeof(int64_t) * max_lanes);
             d_xst = reinterpret_cast<int*>(dev + o);
-            o += up256(sizeof(int) * max_lanes);
+            o += up256(2 * sizeof(int) * max_lanes);
             d_cls = reinterpret_cast<PngImgDev*>(dev + o);
             o += up256(sizeof(PngImgDev) * m);
             d_rows = reinterpret_cast<int2*>(dev + o);
@@ -473,7 +473,7 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             if (!rc) rc = copy_h2d_2d(reinterpret_cast<uint8_t*>(d_rows), sizeof(int2) * hrows.size(),
                                       reinterpret_cast<const uint8_t*>(hrows.data()), sizeof(int2) * hrows.size(),
                                       sizeof(int2) * hrows.size(), 1, s);
-            hxst.resize(hl.size());
+            hxst.resize(2 * hl.size());
             if (!rc) {
                 hipError_t e = hipMemsetAsync(dev + o_err, 0, sizeof(int) * m, s);
                 rec(4, s);
@@ -506,7 +506,7 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                     }
                 }
                 rec(7, s);
-                if (e == hipSuccess) e = hipMemcpyAsync(hxst.data(), d_xst, sizeof(int) * hl.size(),
+                if (e == hipSuccess) e = hipMemcpyAsync(hxst.data(), d_xst, 2 * sizeof(int) * hl.size(),
                                                         hipMemcpyDeviceToHost, s);
                 if (e == hipSuccess) e = hipMemcpyAsync(herr.data(), dev + o_err, sizeof(int) * m, hipMemcpyDeviceToHost, s);
                 if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -523,10 +523,26 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                     PngJob& j = *J[k];
                     if (j.state != 1) continue;
                     bool ok = herr[k] == 0;
-                    for (size_t i = 0; i < j.lanes.start.size(); ++i, ++t) ok = ok && hxst[t] == 0;
+                    for (size_t i = 0; i < j.lanes.start.size(); ++i, ++t) ok = ok && hxst[2 * t] == 0;
                     if (!ok) j.state = -1;
                 }
             }
+        }
+        if (timing && !hl.empty()) {  // per-lane profile of the last decode round and the expand pass
+            double si = 0, sc = 0, sx = 0, mi = 0, mc = 0, mx = 0, sb = 0, mb = 0;
+            for (size_t t = 0; t < hres.size(); ++t) {
+                si += hres[t].iters; sc += hres[t].kcycles; sb += hres[t].blocks;
+                mi = std::max(mi, (double)hres[t].iters); mc = std::max(mc, (double)hres[t].kcycles);
+                mb = std::max(mb, (double)hres[t].blocks);
+            }
+            for (size_t t = 0; 2 * t + 1 < hxst.size(); ++t) {
+                sx += hxst[2 * t + 1];
+                mx = std::max(mx, (double)hxst[2 * t + 1]);
+            }
+            const double n1 = (double)std::max<size_t>(1, hres.size()), n2 = (double)std::max<size_t>(1, hxst.size() / 2);
+            fprintf(stderr, "[png] decode lanes %zu: iters mean %.0f max %.0f, blocks mean %.2f max %.0f, kcycles mean %.0f "
+                    "max %.0f (%.0f cycles/iter); expand kcycles mean %.0f max %.0f\n", hres.size(), si / n1, mi, sb / n1,
+                    mb, sc / n1, mc, 1024.0 * sc / std::max(1.0, si), sx / n2, mx);
         }
         t_png_timing[0] = t1 - t0;
         t_png_timing[1] = ev_ms(0, 1);
