@@ -70,7 +70,8 @@ bool parse_png(const uint8_t* b, size_t n, PngJob& J) {
         if (len > n - pos - 12) return false;
         const uint8_t* type = b + pos + 4;
         const uint8_t* data = b + pos + 8;
-        if (png_chunk_crc(type, data, len) != be32(data + len)) return false;
+        // (IDAT CRCs are checked while the payload is staged: decode_png_batch)
+        if (std::memcmp(type, "IDAT", 4) && png_chunk_crc(type, data, len) != be32(data + len)) return false;
         if (!std::memcmp(type, "IHDR", 4)) {
             if (len != 13 || ihdr) return false;
             J.w = be32(data);
@@ -219,20 +220,6 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
         const size_t o_err = total;
         total += up256(sizeof(int) * m);
         const size_t o_dyn = total;  // lane tables, results, obase, rows, subtables: sized per round below
-        uint8_t* pin = pinned_slot(1, zbytes + 64);
-        if (!pin) rc = fail(IK_ERR_NOMEM, "cannot allocate pinned PNG staging");
-        // IDAT payloads -> pinned (host threads), word-padded
-        if (!rc)
-            parallel_for(m, 0, [&](int k) {
-                PngJob& j = *J[k];
-                uint8_t* d = pin + j.z_off;
-                for (auto& seg : j.idat) {
-                    std::memcpy(d, seg.first, seg.second);
-                    d += seg.second;
-                }
-                while ((size_t)(d - (pin + j.z_off)) & 3) *d++ = 0;
-            });
-        const double t1 = now_ms();
         // the work area: lane tables (bounded by the chunk count), row / page
         // tables, unfilter class descriptors, and the token area: a quarter token
         // per compressed bit for every first-round lane, plus half again for lanes
@@ -283,6 +270,32 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             d_tok = reinterpret_cast<uint16_t*>(dev + o);
         }
         uint64_t tok_used = 0;
+        uint8_t* pin = rc ? nullptr : pinned_slot(1, zbytes + 64);
+        if (!rc && !pin) rc = fail(IK_ERR_NOMEM, "cannot allocate pinned PNG staging");
+        // IDAT payloads -> pinned (host threads), CRC-checked on the way (png
+        // verifies every chunk's CRC), each stream's H2D copy issued as soon as it
+        // is staged, so the PCIe transfer overlaps the staging of the others
+        std::vector<char> crc_bad(m, 0);
+        std::atomic<int> up_err{0};
+        if (!rc)
+            parallel_for(m, 0, [&](int k) {
+                PngJob& j = *J[k];
+                uint8_t* d = pin + j.z_off;
+                for (auto& seg : j.idat) {
+                    if (png_chunk_crc(seg.first - 4, seg.first, seg.second) != be32(seg.first + seg.second)) crc_bad[k] = 1;
+                    std::memcpy(d, seg.first, seg.second);
+                    d += seg.second;
+                }
+                while ((size_t)(d - (pin + j.z_off)) & 3) *d++ = 0;
+                const size_t wb = (j.zlen + 3) & ~size_t(3);
+                hipError_t e = hipMemsetAsync(dev + j.o_words + wb, 0, 512, s);
+                if (e == hipSuccess) e = hipMemcpyAsync(dev + j.o_words, pin + j.z_off, wb, hipMemcpyHostToDevice, s);
+                if (e != hipSuccess) up_err = (int)e;
+            });
+        if (!rc && up_err) rc = hip_fail((hipError_t)up_err.load(), "PNG stream upload");
+        for (int k = 0; k < m; ++k)
+            if (crc_bad[k]) J[k]->state = -1;  // the host decoder reports png's CRC error
+        const double t1 = now_ms();
         // ---- upload streams (zero pad), image descriptors, chunk table ----
         std::vector<PngImgDev> hd(m);
         std::vector<int> ctab(2 * (size_t)nchunks);
@@ -302,10 +315,6 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                 ctab[2 * (size_t)(j.chunk0 + c)] = k;
                 ctab[2 * (size_t)(j.chunk0 + c) + 1] = c;
             }
-            hipError_t e = hipMemsetAsync(dev + j.o_words + ((j.zlen + 3) & ~size_t(3)), 0, 512, s);
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(dev + j.o_words, pin + j.z_off, (j.zlen + 3) & ~size_t(3), hipMemcpyHostToDevice, s);
-            if (e != hipSuccess) rc = hip_fail(e, "PNG stream upload");
         }
         std::vector<int> hchunk_img(nchunks), hchunk_idx(nchunks);
         for (int c = 0; c < nchunks; ++c) { hchunk_img[c] = ctab[2 * (size_t)c]; hchunk_idx[c] = ctab[2 * (size_t)c + 1]; }
