@@ -154,6 +154,21 @@ IK_HD int dist_base(int d) {  // distance symbols 0..29
 }
 IK_HD int dist_extra(int d) { return d < 4 ? 0 : (d - 2) >> 1; }
 
+// the same tables without branches (selects), for the GPU's symbol loop:
+// length code rank i = symbol - 257 (0..28), distance code d (0..29)
+IK_HD void len_code(int i, int& base, int& extra) {
+    const int e0 = (i - 4) >> 2, e = e0 < 0 ? 0 : e0;
+    const bool small = i < 8, last = i == 28;
+    extra = (small || last) ? 0 : e;
+    base = small ? 3 + i : (last ? 258 : ((4 + ((i - 4) & 3)) << e) + 3);
+}
+IK_HD void dist_code(int d, int& base, int& extra) {
+    const int e0 = (d - 2) >> 1, e = e0 < 0 ? 0 : e0;
+    const bool small = d < 4;
+    extra = small ? 0 : e;
+    base = small ? 1 + d : ((2 + (d & 1)) << e) + 1;
+}
+
 // Parse a dynamic block header at b (after BFINAL/BTYPE) into code lengths,
 // validating like zlib.  lens: 286 + 30 entries (literal/length then distance).
 // Returns 0 or -1.
@@ -572,6 +587,11 @@ struct Win {
         pos = bit;
     }
     IK_HD void tick(TokOut& o) { o.flush(); }
+    // x0 / x1 / x2 for a slide of 0 / 1 / 2 words, by masks: a ternary chain
+    // becomes an indexed private array on the GPU (scratch memory)
+    IK_HD static uint32_t sel3(uint32_t m1, uint32_t m2, uint32_t x0, uint32_t x1, uint32_t x2) {
+        return (x0 & ~m1) | (x1 & m1 & ~m2) | (x2 & m2);
+    }
     IK_HD uint64_t bits64() const {  // the next 64 stream bits
         const uint32_t wi = pos >> 5, sh = pos & 31u;
         const uint64_t lo = (uint64_t)rd(wi) | ((uint64_t)rd(wi + 1) << 32);
@@ -672,10 +692,9 @@ IK_HD void decode_lane_tok(const uint32_t* words, uint64_t nbits, uint64_t start
             tc += kTokTableLen;
             W.init((const IK_GLOBAL uint32_t*)words, (uint32_t)nwords, (uint32_t)b.pos());
             ++r.blocks;
-            bool bad = false, full = false;
+            int code = 0;  // why the symbol loop ended: 1 end of block, 2 corrupt, 3 token region full
             for (;;) {
                 ++r.iters;
-                if ((uint64_t)W.pos > plimit) { bad = true; break; }
                 W.tick(out);
                 const uint64_t v = W.bits64();
                 // literal/length code
@@ -688,10 +707,10 @@ IK_HD void decode_lane_tok(const uint32_t* words, uint64_t nbits, uint64_t start
                 const bool lit = i < nl;
                 const uint32_t eob = (info >> 24) & 1u;
                 const uint32_t lr = ((info >> 25) & 31u) + (i - nl - eob);  // length code rank
-                const int lsym = (int)cm_byte(m, (int)(lr < 28u ? lr : 28u));
-                const int le = len_extra(257 + lsym);
+                int lb, le;
+                len_code((int)cm_byte(m, (int)(lr < 28u ? lr : 28u)), lb, le);
                 const uint64_t v1 = v >> Lc;
-                const int ll = len_base(257 + lsym) + (int)((uint32_t)v1 & ((1u << le) - 1u));
+                const int ll = lb + (int)((uint32_t)v1 & ((1u << le) - 1u));
                 // distance code (computed for literals too, and not used)
                 const uint64_t v2 = v1 >> le;
                 const uint32_t c15d = rev32((uint32_t)v2) >> 17;
@@ -699,28 +718,34 @@ IK_HD void decode_lane_tok(const uint32_t* words, uint64_t nbits, uint64_t start
                 const int Dc = D > 15 ? 15 : D;
                 const uint32_t dinfo = m[16 + Dc];
                 const uint32_t di = ((c15d >> (15 - Dc)) - (dinfo & 0x7FFFu)) + ((dinfo >> 16) & 31u);
-                const int ds = (int)cm_byte(m, 32 + (int)(di < 29u ? di : 29u));
-                const int de = dist_extra(ds);
-                const int dist = dist_base(ds) + (int)((uint32_t)(v2 >> Dc) & ((1u << de) - 1u));
-                // the rare cases, in one branch
-                const bool odd = !lit && ((eob && i == nl) || lr > 28u || D > 15 || di > 29u ||
-                                          (first && (int64_t)cnt < dist));
-                if (L > 15 || odd || tc + 2 > tcap || cnt + 258 > out_cap) {
-                    if (L > 15) { bad = true; break; }
-                    if (!lit && eob && i == nl) {  // end of block
-                        W.advance((uint32_t)Lc);
+                int db, de;
+                dist_code((int)cm_byte(m, 32 + (int)(di < 29u ? di : 29u)), db, de);
+                const int dist = db + (int)((uint32_t)(v2 >> Dc) & ((1u << de) - 1u));
+                // the rare cases, one branch and one exit
+                const bool eobk = !lit && eob && i == nl;
+                const bool odd = L > 15 || (uint64_t)W.pos > plimit ||
+                                 (!lit && !eobk && (lr > 28u || D > 15 || di > 29u || (first && (int64_t)cnt < dist)));
+                if (odd || eobk || tc + 2 > tcap || cnt + 258 > out_cap) {
+                    code = odd ? 2 : eobk ? 1 : tc + 2 > tcap ? 3 : cnt + (lit ? 1u : (uint64_t)ll) > out_cap ? 2 : 0;
+                    if (code) {
+                        if (code == 1) W.advance((uint32_t)Lc);
                         break;
                     }
-                    if (odd) { bad = true; break; }
-                    if (tc + 2 > tcap) { full = true; break; }
-                    if (cnt + (lit ? 1u : (uint64_t)ll) > out_cap) { bad = true; break; }
                 }
-                const uint32_t rank = ((m[16 + Lc] >> 21) & 0x1FFu) + i;
-                tput(lit ? rank : (kTokMatch | (uint32_t)(ll - 3)));
-                if (!lit) tput((uint32_t)(dist - 1));
+                // one token (literal rank) or two (match length, distance), without branches
+                const uint32_t t1 = lit ? ((m[16 + Lc] >> 21) & 0x1FFu) + i : (kTokMatch | (uint32_t)(ll - 3));
+                const uint64_t a0 = (h0 >> 16) | (h1 << 48), a1 = (h1 >> 16) | ((uint64_t)t1 << 48);
+                const uint64_t b0 = (a0 >> 16) | (a1 << 48), b1 = (a1 >> 16) | ((uint64_t)(dist - 1) << 48);
+                const uint32_t tc1 = tc + 1;
+                const bool g1 = (tc1 & 7u) == 0, g2 = !lit && ((tc1 + 1) & 7u) == 0;  // a group of 8 completed
+                if (g1 || g2) out.group(g1 ? tc1 - 8 : tc1 - 7, g1 ? a0 : b0, g1 ? a1 : b1);
+                h0 = lit ? a0 : b0;
+                h1 = lit ? a1 : b1;
+                tc = lit ? tc1 : tc1 + 1;
                 cnt += lit ? 1u : (uint64_t)ll;
                 W.advance(lit ? (uint32_t)Lc : (uint32_t)(Lc + le + Dc + de));
             }
+            const bool bad = code == 2, full = code == 3;
             out.flush();
             if (full) { r.status = kLaneOverflow; break; }
             if (bad) break;

@@ -213,7 +213,7 @@ struct WinLds {
     __device__ void dma(uint32_t B) {
         static_assert(kRingBW == 8, "eight words per block");
         const IK_GLOBAL uint32_t* g = w + (size_t)B * kRingBW;
-        const uint32_t r0 = (uint32_t)(size_t)ring - 4u * lane;  // the wave's ring base (lane 0)
+        const uint32_t r0 = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)ring - 4u * lane);  // ring base (lane 0)
         uint32_t keep;
         const IK_GLOBAL uint32_t* src;
         uint32_t base;
@@ -253,6 +253,10 @@ struct WinLds {
             ++nextb;
         }
     }
+    // The next 64+ bits: three words read from the ring.  (A register window
+    // sliding by selects, with the next words read one symbol ahead, measured
+    // slower: 2,382 vs 2,187 cycles per symbol -- these reads are not what the
+    // symbol-to-symbol chain waits for.)
     __device__ uint64_t bits64() const {
         const uint32_t wi = pos >> 5, sh = pos & 31u;
         const uint32_t a = word(wi), b = word(wi + 1), c = word(wi + 2);

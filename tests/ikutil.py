@@ -140,8 +140,10 @@ def splitmix64(seed: int, n: int) -> np.ndarray:
     return z ^ (z >> np.uint64(31))
 
 
-def synth(w: int, h: int, c: int = 4, seed: int = 0, pattern: str = "S") -> np.ndarray:
-    """Pattern S: gradients + 16px checker + +-8 noise; pattern N: uniform noise.  alpha = 255."""
+def synth(w: int, h: int, c: int = 4, seed: int = 0, pattern: str = "S", alpha: str = "opaque") -> np.ndarray:
+    """Pattern S: gradients + 16px checker + +-8 noise; pattern N: uniform noise.
+    alpha (C = 2, 4): "opaque" = 255; "random" = uniform noise (independent of the
+    colour channels); "edge" = 0 on the left half (colour still set), 255 right."""
     with np.errstate(over="ignore"):
         r = splitmix64(0x1A6E0000 + seed, w * h).reshape(h, w)
     if pattern == "N":
@@ -158,6 +160,12 @@ def synth(w: int, h: int, c: int = 4, seed: int = 0, pattern: str = "S") -> np.n
         else:
             px = np.stack(chans + ([np.full_like(chans[0], 255)] if c == 4 else []), -1)
         px = px.astype(np.uint8)
-    if c in (2, 4) and pattern == "N":
-        px[..., -1] = 255
+    if c in (2, 4):
+        if alpha == "random":
+            px[..., -1] = ((r >> np.uint64(40)) & np.uint64(255)).astype(np.uint8)
+        elif alpha == "edge":
+            px[..., -1] = 255
+            px[:, : w // 2, -1] = 0
+        else:
+            px[..., -1] = 255
     return np.ascontiguousarray(px)
