@@ -15,8 +15,9 @@ threads the GPU path may use are stated (--threads, default 32 = an 8-GPU node's
 Beside it, in the same JSON line:
   cpu_baseline   the same PNG bytes through the reference CPU path restated
                  (oracle/: png decode + image 0.25.8 resize + libwebp), one image
-                 per thread, at 1 thread and at nproc threads (SURVEY D-6; the
-                 reference runs one synchronous transform per tokio worker).
+                 per worker at a time, on 1 core, on nproc worker processes and
+                 on the GPU's stated host budget (SURVEY D-6; the reference runs
+                 one synchronous transform per tokio worker).
   roofline       the dominant device kernel of the step by HIP-event time, its
                  algorithmic bytes per launch / its duration vs 8 TB/s; the
                  resize kernel's own roofline in roofline_resize.
@@ -49,7 +50,7 @@ METRIC = "transform MPix/s (decode+resize+encode) 4096²→512² WebP q80; 1/2/4
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FILTERS = {"nearest": 0, "triangle": 1, "catmullrom": 2, "gaussian": 3, "lanczos3": 4}
 FORMATS = {"jpeg": 0, "webp": 1, "avif": 2}
-PNG_STAGES = ["host_parse_stage", "find", "count", "emit", "resolve", "unfilter"]
+PNG_STAGES = ["host_parse_stage", "find", "decode", "expand", "resolve", "unfilter"]
 
 
 def parse():
@@ -117,10 +118,39 @@ def make_pngs(frames):
     return out
 
 
+_CPU = {}  # the oracle and the inputs, inherited by the forked cpu_baseline workers
+
+
+def _cpu_one(k):
+    """One reference-path transform on the CPU (oracle/): PNG bytes -> WebP bytes."""
+    import ikutil
+    L, pngs, O, f, fmt, q = (_CPU[x] for x in ("L", "pngs", "O", "f", "fmt", "q"))
+    data = pngs[k % len(pngs)]
+    px = ikutil.u8p()
+    w, h, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    n = L.iko_png_decode(data, len(data), ctypes.byref(px), ctypes.byref(w), ctypes.byref(h), ctypes.byref(c))
+    assert n > 0, n
+    out = ikutil.u8p()
+    ow, oh = ctypes.c_uint32(), ctypes.c_uint32()
+    m = L.iko_transform_u8(px, w.value, h.value, c.value, O, O, f, fmt, q, ctypes.byref(out),
+                           ctypes.byref(ow), ctypes.byref(oh))
+    L.iko_free(px)
+    assert m > 0 and (ow.value, oh.value) == (O, O)
+    L.iko_free(out)
+    return 1
+
+
 def cpu_baseline(args, pngs):
     """The reference CPU path restated (oracle/: PNG decode + image 0.25.8 resize +
-    libwebp WebPEncodeRGB) on the same PNG bytes, one image per thread, at 1 thread
-    and at nproc threads; each sample sized to about args.cpu_seconds of wall."""
+    libwebp WebPEncodeRGB) on the same PNG bytes, one image per worker at a time:
+    on 1 core, on nproc worker processes (all hardware threads), and on the GPU's
+    stated host budget (--threads processes).  Workers are forked processes, as
+    independent requests are: threads of one process serialise on the allocator
+    and on first-touch page faults of the ~100 MB per image (measured: 256 threads
+    reached only 9x one thread).  Runs before anything initialises the GPU (the
+    pools fork).  Each sample is sized to about args.cpu_seconds of wall."""
+    import multiprocessing as mp
+
     import ikutil
     orc = ikutil.Oracle()
     L = orc.lib
@@ -128,62 +158,43 @@ def cpu_baseline(args, pngs):
     L.iko_png_decode.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ikutil.u8p),
                                  ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                                  ctypes.POINTER(ctypes.c_uint32)]
-    f, fmt, O = FILTERS[args.filter], FORMATS["webp"], args.out
-
-    def one(k):
-        data = pngs[k % len(pngs)]
-        px = ikutil.u8p()
-        w, h, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
-        n = L.iko_png_decode(data, len(data), ctypes.byref(px), ctypes.byref(w), ctypes.byref(h), ctypes.byref(c))
-        assert n > 0, n
-        out = ikutil.u8p()
-        ow, oh = ctypes.c_uint32(), ctypes.c_uint32()
-        m = L.iko_transform_u8(px, w.value, h.value, c.value, O, O, f, fmt, args.quality, ctypes.byref(out),
-                               ctypes.byref(ow), ctypes.byref(oh))
-        L.iko_free(px)
-        assert m > 0 and (ow.value, oh.value) == (O, O)
-        L.iko_free(out)
-
-    one(0)
+    _CPU.update(L=L, pngs=pngs, O=args.out, f=FILTERS[args.filter], fmt=FORMATS["webp"], q=args.quality)
+    _cpu_one(0)
     t0 = time.perf_counter()
-    one(1)
+    _cpu_one(1)
     t1 = time.perf_counter() - t0
     n1 = max(2, int(args.cpu_seconds / max(t1, 1e-3)))
     t0 = time.perf_counter()
     for k in range(n1):
-        one(k)
+        _cpu_one(k)
     w1 = time.perf_counter() - t0
+
+    def pool_rate(nw):
+        per = max(2, min(8, int(args.cpu_seconds / 2 / max(t1, 1e-3))))
+        with mp.get_context("fork").Pool(nw) as pool:
+            pool.map(_cpu_one, range(nw), chunksize=1)  # every worker warm (library state, page tables)
+            t0 = time.perf_counter()
+            done = sum(pool.map(_cpu_one, range(nw * per), chunksize=per))
+            return done, time.perf_counter() - t0
+
     nproc = os.cpu_count() or 1
-    # nproc threads, each doing `per` images: ~cpu_seconds if the cores scaled perfectly
-    per = max(1, int(round(args.cpu_seconds / max(t1, 1e-3))))
-    per = min(per, 4)
-    done = [0]
-    lock = threading.Lock()
-
-    def worker(t):
-        for k in range(per):
-            one(t * per + k)
-            with lock:
-                done[0] += 1
-
-    ts = [threading.Thread(target=worker, args=(t,)) for t in range(nproc)]
-    t0 = time.perf_counter()
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join()
-    wn = time.perf_counter() - t0
-    S = args.size
+    done, wn = pool_rate(nproc)
+    nb = min(args.threads, nproc)
+    done_b, wb = pool_rate(nb)
+    S, O = args.size, args.out
     return {
-        "value": round(done[0] * S * S / wn / 1e6, 2),
+        "value": round(done * S * S / wn / 1e6, 2),
         "unit": "MPix/s",
         "cores": nproc,
         "kind": "port",
-        "sample": f"{done[0]} x {S}x{S} RGBA8 PNG (host memory) -> oracle PNG decode (CRC, libdeflate inflate, "
+        "sample": f"{done} x {S}x{S} RGBA8 PNG (host memory) -> oracle PNG decode (CRC, libdeflate inflate, "
                   f"unfilter) -> image 0.25.8 resize {O}x{O} {args.filter} -> libwebp q{args.quality}; one image per "
-                  f"thread, {nproc} threads, {wn:.1f}s wall",
+                  f"worker process at a time, {nproc} processes, {wn:.1f}s wall",
         "value_1core": round(n1 * S * S / w1 / 1e6, 2),
         "sample_1core": f"{n1} images on 1 thread, {w1:.1f}s wall",
+        "value_budget": round(done_b * S * S / wb / 1e6, 2),
+        "budget_processes": nb,
+        "sample_budget": f"{done_b} images on {nb} processes (the GPU's stated host budget), {wb:.1f}s wall",
         "host": host_info(),
     }
 
@@ -204,6 +215,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    S, O, B = args.size, args.out, args.batch
+    import ikutil
+    frames = [ikutil.synth(S, S, 4, seed=sd, pattern="S") for sd in shard_seeds(rank, args.distinct)]
+    pngs = make_pngs(frames)
+    reqs = [pngs[i % len(pngs)] for i in range(B)]
+    # the CPU leg first: its worker pools fork, and nothing may have touched the GPU yet
+    cpu = cpu_baseline(args, pngs) if rank == 0 and world == 1 and not args.no_cpu_baseline else None
     dist = None
     import torch
     if world > 1:
@@ -211,7 +229,6 @@ def main():
         dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
-    import ikutil
     from imagekit import _lib, transform_batch
     lib = _lib.load()
     if lib.ik_init(local) != 0:
@@ -223,20 +240,16 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    S, O, B = args.size, args.out, args.batch
     f = FILTERS[args.filter]
-    frames = [ikutil.synth(S, S, 4, seed=sd, pattern="S") for sd in shard_seeds(rank, args.distinct)]
-    pngs = make_pngs(frames)
-    reqs = [pngs[i % len(pngs)] for i in range(B)]
 
     # ---- headline: PNG bytes in host memory -> WebP bytes in host memory ----
-    timing = (ctypes.c_double * 10)()
+    timing = (ctypes.c_double * 13)()
     stage_ms = []
 
     def step():
         res = transform_batch(reqs, [(O, O)] * B, [FORMATS["webp"]] * B, [args.quality] * B, filter=f,
                               threads=args.threads)
-        lib.ik_png_last_timing(timing, 10)
+        lib.ik_png_last_timing(timing, 13)
         stage_ms.append(list(timing))
         return res
 
@@ -260,18 +273,20 @@ def main():
     value = aggregate_mpix(world, B * args.steps, S, elapsed)
     st = np.mean(np.array(stage_ms), axis=0)
     png_stages = {k: round(float(v), 3) for k, v in zip(PNG_STAGES, st[:6])}
-    png_stages.update({"decode_wall_ms": round(float(st[6]), 3), "count_rounds": float(st[7]),
+    png_stages.update({"decode_wall_ms": round(float(st[6]), 3), "decode_rounds": float(st[7]),
                        "decoder_lanes": int(st[8]), "streams_on_gpu": int(st[9]),
                        "timed_streams_gpu_decoded": int(gpu_streams), "timed_streams_host_decoded": int(host_streams)})
     out_bytes = sum(len(r) for r in res) // B
     in_bytes = sum(len(p) for p in reqs) // B
 
     # ---- device kernels of the step: algorithmic bytes per launch ----
-    raw = (S * 4 + 1) * S
+    raw = (S * 4 + 1) * S          # filtered image bytes per frame (filter byte + RGBA row)
+    tok = float(st[12])            # u16 tokens the decode pass wrote (whole batch)
     kern = {
-        # compressed stream read, u16 symbols written (count: read only)
-        "k_png_inflate<emit>": (png_stages["emit"], B * (in_bytes + 2 * raw)),
-        "k_png_inflate<count>": (png_stages["count"], B * in_bytes),
+        # compressed stream read, tokens written
+        "k_png_decode": (png_stages["decode"], B * in_bytes + 2 * tok),
+        # tokens read, u16 symbols written
+        "k_png_expand": (png_stages["expand"], 2 * tok + B * 2 * raw),
         "k_png_resolve": (png_stages["resolve"], B * (2 * raw + 4 * S * S)),
         "k_png_unfilter": (png_stages["unfilter"], B * (2 * 4 * S * S)),
         "k_png_find": (png_stages["find"], B * in_bytes),
@@ -280,9 +295,10 @@ def main():
     dms, dbytes = kern[dom]
     roof = {"bound": "hbm", "achieved": round(dbytes / (dms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(dbytes / (dms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None, "kernel": dom,
-            "kernel_ms": round(dms, 4), "bytes_per_launch": dbytes,
-            "note": "entropy decoding is bound by serial per-lane decode latency, not HBM; bytes = compressed in "
-                    "+ u16 symbols out"}
+            "kernel_ms": round(dms, 4), "bytes_per_launch": int(dbytes),
+            "note": "DEFLATE decoding: each lane's symbol-to-symbol chain bounds it (one lane per block, ~1,900 "
+                    "blocks per frame), not HBM; bytes = compressed bits in + u16 tokens out",
+            "tokens_per_batch": int(tok)}
     kernels = {k: {"ms": round(v[0], 4), "GBps": round(v[1] / max(v[0], 1e-6) / 1e6, 1)} for k, v in kern.items()}
 
     # ---- extras: HBM-resident pipeline (old headline) and JPEG-source leg ----
@@ -374,10 +390,6 @@ def main():
                    "bytes_per_source_image": sum(len(p) for p in jp) // 2,
                    "value": round(aggregate_mpix(world, n, S, te), 2), "unit": "MPix/s"}
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, pngs)
-
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -413,6 +425,7 @@ def main():
         }
         if cpu:
             line["ratio_vs_cpu_allcore"] = round(value / cpu["value"], 2)
+            line["ratio_vs_cpu_budget"] = round(value / cpu["value_budget"], 2)  # 1 GPU + N threads vs N cores
             line["ratio_vs_cpu_1core"] = round(value / cpu["value_1core"], 2)
         print(json.dumps(line))
     if dist is not None:

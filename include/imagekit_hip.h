@@ -111,7 +111,8 @@ int ik_set_png_gpu_min(long long min_raw_bytes);
  * of [1] block search [2] count passes [3] emit pass [4] resolve [5] unfilter,
  * [6] wall ms, [7] count rounds, [8] decoder lanes, [9] streams sent to the GPU,
  * [10] PNG streams of the batch the GPU decoded, [11] streams the host decoder took
- * (outside the GPU path, or rejected by it) */
+ * (outside the GPU path, or rejected by it), [12] tokens written by the verified
+ * decoder lanes (u16 each) */
 int ik_png_last_timing(double *out, int n);
 /* process-wide counts of PNG streams decoded since load: out[0] by the GPU path,
  * out[1] by the host decoder (outside the GPU path, or rejected by it) */

@@ -125,8 +125,9 @@ double now_ms() {
 // the last batch's stage times on this thread (ik_png_last_timing): host parse +
 // staging, then device ms of find / count (all rounds) / emit / resolve / unfilter
 // from HIP events on the thread's stream, wall ms, rounds, lanes, streams sent to
-// the GPU, streams the GPU decoded (verified), streams the host decoder took
-thread_local double t_png_timing[12];
+// the GPU, streams the GPU decoded (verified), streams the host decoder took,
+// tokens the verified lanes wrote (the decode pass's output, the expand pass's input)
+thread_local double t_png_timing[13];
 // process-wide: PNG streams decoded by the GPU path / by the host decoder
 std::atomic<unsigned long long> g_png_gpu_streams{0}, g_png_host_streams{0};
 struct Events {
@@ -451,6 +452,7 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             }
             hd[k].dst = j.img->d;
             hd[k].pitch = j.img->pitch;
+            for (size_t i = 0; i < ob.size(); ++i) t_png_timing[12] += (double)j.lanes.res[i].ntok;
             for (size_t i = 0; i < ob.size(); ++i) {
                 PngLaneDev L{};
                 L.tbase = j.lanes.tbase[i];
@@ -615,7 +617,7 @@ extern "C" int ik_png_counters(unsigned long long* out) {
 }
 
 extern "C" int ik_png_last_timing(double* out, int n) {
-    for (int i = 0; i < n && i < 12; ++i) out[i] = ik::t_png_timing[i];
+    for (int i = 0; i < n && i < 13; ++i) out[i] = ik::t_png_timing[i];
     return IK_OK;
 }
 

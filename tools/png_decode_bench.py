@@ -17,6 +17,6 @@ t = (ctypes.c_double * 10)()
 for r in range(R):
     t0 = time.perf_counter(); out = decode_image_batch(reqs); el = time.perf_counter() - t0
     lib.ik_png_last_timing(t, 10)
-    print(f"batch {B} x {S}^2: {el*1e3:.1f} ms wall; stage ms host {t[0]:.1f} find {t[1]:.1f} count {t[2]:.1f} "
-          f"emit {t[3]:.1f} resolve {t[4]:.1f} unfilter {t[5]:.1f} lanes {int(t[8])}", flush=True)
+    print(f"batch {B} x {S}^2: {el*1e3:.1f} ms wall; stage ms host {t[0]:.1f} find {t[1]:.1f} decode {t[2]:.1f} "
+          f"expand {t[3]:.1f} resolve {t[4]:.1f} unfilter {t[5]:.1f} lanes {int(t[8])}", flush=True)
     del out
