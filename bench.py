@@ -104,7 +104,18 @@ def host_info():
                 break
     except OSError:
         pass
-    return {"cpu_model": model, "nproc": os.cpu_count(),
+    quota = None  # the cgroup's CPU quota in cores (a GPU box shares its host: nproc shows the whole machine)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            quota = None if q <= 0 else round(q / per, 2)
+        except (OSError, ValueError):
+            pass
+    return {"cpu_model": model, "nproc": os.cpu_count(), "cgroup_cpu_quota_cores": quota,
             "affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
 
 
