@@ -83,6 +83,12 @@ int ik_image_from_host(const uint8_t *pixels, uint32_t width, uint32_t height, u
 int ik_image_wrap_device(uint8_t *dev_pixels, uint32_t width, uint32_t height, uint32_t channels,
                          size_t pitch, ik_image **out);
 int ik_image_info(const ik_image *img, uint32_t *width, uint32_t *height, uint32_t *channels);
+/* 16-bit images (Rgb16 / Rgba16 / L16 / La16 of DynamicImage; 16-bit PNG decodes to
+ * them): bytes per sample, 1 or 2; ik_image_to_host writes native-endian u16 for 2.
+ * resize_image keeps the depth; encode_image rescales to 8 bits first (to_rgb8). */
+int ik_image_depth(const ik_image *img);
+int ik_image_from_host16(const uint16_t *pixels, uint32_t width, uint32_t height, uint32_t channels,
+                         ik_image **out);
 int ik_image_to_host(const ik_image *img, uint8_t *dst, size_t cap); /* tightly packed */
 void ik_image_free(ik_image *img);
 void ik_buf_free(uint8_t *buf);

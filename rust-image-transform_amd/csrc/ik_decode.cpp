@@ -172,7 +172,8 @@ bool unfilter(uint8_t* data, size_t h, size_t rowbytes, size_t bpp, std::vector<
 
 }  // namespace
 
-int decode_png(const uint8_t* b, size_t n, uint32_t& W, uint32_t& H, uint32_t& C, std::vector<uint8_t>& px) {
+int decode_png(const uint8_t* b, size_t n, uint32_t& W, uint32_t& H, uint32_t& C, std::vector<uint8_t>& px,
+               uint32_t* depth_out) {
     size_t pos = 8;
     uint32_t w = 0, h = 0;
     int depth = 0, ctype = -1, interlace = 0;
@@ -218,11 +219,19 @@ int decode_png(const uint8_t* b, size_t n, uint32_t& W, uint32_t& H, uint32_t& C
     case 6: spp = 4; break;
     default: return fail(IK_ERR_TRANSFORM, "Format error decoding Png: bad color type %d", ctype);
     }
-    if (depth == 16) return fail(IK_ERR_UNSUPPORTED, "16-bit PNG decoding is not implemented in this build");
-    if (!(depth == 8 || ((ctype == 0 || ctype == 3) && (depth == 1 || depth == 2 || depth == 4))))
+    if (depth == 16 && ctype == 3) return fail(IK_ERR_TRANSFORM, "Format error decoding Png: bad bit depth 16");
+    if (depth == 16 && !depth_out) return fail(IK_ERR_UNSUPPORTED, "16-bit PNG decoding needs a 16-bit image");
+    if (!(depth == 8 || depth == 16 || ((ctype == 0 || ctype == 3) && (depth == 1 || depth == 2 || depth == 4))))
         return fail(IK_ERR_TRANSFORM, "Format error decoding Png: bad bit depth %d", depth);
     if (ctype == 3 && (plte.empty() || plte.size() % 3)) return fail(IK_ERR_TRANSFORM, "Format error decoding Png: bad palette");
-    if ((uint64_t)w * h > (512ull << 20)) return fail(IK_ERR_TRANSFORM, "Limits are exceeded");
+    {  // image's default Limits: max_alloc 512 MiB of DECODED bytes (after EXPAND: palette,
+       // tRNS alpha, low bit depths to 8; 16-bit samples take two bytes)
+        const uint64_t out_c = ctype == 3 ? (trns.empty() ? 3 : 4)
+                             : ctype == 0 ? (trns.size() >= 2 ? 2 : 1)
+                             : ctype == 2 ? (trns.size() >= 6 ? 4 : 3) : (uint64_t)spp;
+        if ((uint64_t)w * h * out_c * (depth == 16 ? 2 : 1) > (512ull << 20))
+            return fail(IK_ERR_TRANSFORM, "Limits are exceeded");
+    }
 
     const size_t bits_pp = (size_t)spp * depth;
     const size_t bpp = (bits_pp + 7) / 8;
@@ -256,6 +265,45 @@ int decode_png(const uint8_t* b, size_t n, uint32_t& W, uint32_t& H, uint32_t& C
             return fail(IK_ERR_TRANSFORM, "Format error decoding Png: corrupt deflate stream");
     }
 
+    if (depth == 16) {  // big-endian u16 samples -> native u16; tRNS -> alpha 0 / 65535
+        const bool ka = (ctype == 0 && trns.size() >= 2) || (ctype == 2 && trns.size() >= 6);
+        const uint32_t oc = (uint32_t)spp + (ka ? 1u : 0u);
+        std::vector<uint16_t> s16((size_t)w * h * oc);
+        std::vector<uint8_t> rows;
+        size_t off16 = 0;
+        for (int p = 0; p < npass; ++p) {
+            if (passes[p].x0 >= w || passes[p].y0 >= h) continue;
+            const size_t pw = (w - passes[p].x0 + passes[p].dx - 1) / passes[p].dx;
+            const size_t ph = (h - passes[p].y0 + passes[p].dy - 1) / passes[p].dy;
+            const size_t rb = rowbytes_of(pw);
+            if (!unfilter(raw.data() + off16, ph, rb, bpp, rows))
+                return fail(IK_ERR_TRANSFORM, "Format error decoding Png: unknown filter method");
+            off16 += ph * (rb + 1);
+            for (size_t y = 0; y < ph; ++y) {
+                const uint8_t* r = rows.data() + y * rb;
+                const size_t oy = passes[p].y0 + y * passes[p].dy;
+                for (size_t x = 0; x < pw; ++x) {
+                    const size_t ox = passes[p].x0 + x * passes[p].dx;
+                    uint16_t* o = s16.data() + (oy * w + ox) * oc;
+                    bool key = ka;
+                    for (int k = 0; k < spp; ++k) {
+                        const uint16_t v = (uint16_t)(r[2 * (x * spp + k)] << 8 | r[2 * (x * spp + k) + 1]);
+                        o[k] = v;
+                        if (ka) key = key && v == (uint16_t)(trns[2 * k] << 8 | trns[2 * k + 1]);
+                    }
+                    if (ka) o[spp] = key ? 0 : 65535;
+                }
+            }
+        }
+        W = w;
+        H = h;
+        C = oc;
+        px.resize(s16.size() * 2);
+        std::memcpy(px.data(), s16.data(), px.size());
+        *depth_out = 2;
+        return IK_OK;
+    }
+    if (depth_out) *depth_out = 1;
     // samples at 8 bits per sample (expanded), spp per pixel, full image
     std::vector<uint8_t>& samp = scratch.samp;  // every sample is written below
     size_t off = 0;

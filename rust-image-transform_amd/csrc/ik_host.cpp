@@ -207,10 +207,10 @@ size_t block_size(size_t bytes) {  // 64 KiB granules: images of similar sizes s
 }
 }  // namespace
 
-int alloc_image(uint32_t w, uint32_t h, uint32_t c, ik_image** out) {
+int alloc_image(uint32_t w, uint32_t h, uint32_t c, ik_image** out, uint32_t depth) {
     auto* img = new ik_image();
-    img->w = w; img->h = h; img->c = c;
-    img->pitch = pitch_for(w, c);
+    img->w = w; img->h = h; img->c = c; img->depth = depth;
+    img->pitch = pitch_for(w, c * depth);
     img->device = current_device();
     (void)hipSetDevice(img->device);
     // + 16 bytes: the fused kernel's 8-byte lane loads may touch the pitch tail
@@ -462,6 +462,25 @@ int ik_image_from_host(const uint8_t* pixels, uint32_t width, uint32_t height, u
     return IK_OK;
 }
 
+int ik_image_from_host16(const uint16_t* pixels, uint32_t width, uint32_t height, uint32_t channels,
+                         ik_image** out) {
+    if (!out || (!pixels && width && height)) return fail(IK_ERR_INVALID, "null pointer");
+    if (channels < 1 || channels > 4) return fail(IK_ERR_INVALID, "channels must be 1..4");
+    ik_image* img = nullptr;
+    int st = alloc_image(width, height, channels, &img, 2);
+    if (st) return st;
+    if (width && height) {
+        const size_t row = (size_t)width * channels * 2;
+        int rc = copy_h2d_2d(img->d, img->pitch, reinterpret_cast<const uint8_t*>(pixels), row, row, height,
+                             thread_stream());
+        if (rc) { ik_image_free(img); return rc; }
+    }
+    *out = img;
+    return IK_OK;
+}
+
+int ik_image_depth(const ik_image* img) { return img ? (int)img->depth : 0; }
+
 int ik_image_wrap_device(uint8_t* dev_pixels, uint32_t width, uint32_t height, uint32_t channels,
                          size_t pitch, ik_image** out) {
     if (!out || !dev_pixels) return fail(IK_ERR_INVALID, "null pointer");
@@ -484,7 +503,7 @@ int ik_image_info(const ik_image* img, uint32_t* w, uint32_t* h, uint32_t* c) {
 
 int ik_image_to_host(const ik_image* img, uint8_t* dst, size_t cap) {
     if (!img || !dst) return fail(IK_ERR_INVALID, "null pointer");
-    const size_t row = (size_t)img->w * img->c;
+    const size_t row = (size_t)img->w * img->c * img->depth;
     if (cap < row * img->h) return fail(IK_ERR_INVALID, "destination too small");
     if (!row || !img->h) return IK_OK;
     DeviceGuard g(img->device);
@@ -521,10 +540,10 @@ int ik_resize_exact(const ik_image* img, uint32_t nw, uint32_t nh, int filter, i
     if (nw == 0 || nh == 0) return fail(IK_ERR_INVALID, "zero output dimension");
     DeviceGuard g(img->device);
     ik_image* o = nullptr;
-    int st = alloc_image(nw, nh, img->c, &o);
+    int st = alloc_image(nw, nh, img->c, &o, img->depth);
     if (st) return st;
     hipStream_t s = thread_stream();
-    const size_t orow = (size_t)nw * img->c;
+    const size_t orow = (size_t)nw * img->c * img->depth;
     if (img->w == 0 || img->h == 0) {  // "nothing to sample from": blank image
         hipError_t e = hipMemset2DAsync(o->d, o->pitch, 0, orow, nh, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -539,8 +558,20 @@ int ik_resize_exact(const ik_image* img, uint32_t nw, uint32_t nh, int filter, i
         *out = o;
         return IK_OK;
     }
-    int rc = ik_resize_batch_device(img->d, img->w, img->h, img->c, img->pitch, 0, 1, nw, nh, filter,
+    int rc;
+    if (img->depth == 2) {  // 16-bit: the two-pass path over u16 samples
+        ResizePlan* plan = get_resize_plan(current_device(), (int)img->w, (int)img->h, (int)img->c, (int)nw, (int)nh,
+                                           filter, 1);
+        float* tmp = plan ? (float*)scratch(sizeof(float) * (size_t)nh * img->w * img->c) : nullptr;
+        if (!plan || !tmp) rc = fail(IK_ERR_DEVICE, "cannot set up the 16-bit resize");
+        else {
+            hipError_t e = launch_resize16(*plan, img->d, img->pitch, o->d, o->pitch, tmp, s);
+            rc = e == hipSuccess ? IK_OK : hip_fail(e, "resize (16-bit)");
+        }
+    } else {
+        rc = ik_resize_batch_device(img->d, img->w, img->h, img->c, img->pitch, 0, 1, nw, nh, filter,
                                     o->d, o->pitch, 0, s);
+    }
     if (rc == IK_OK) {
         hipError_t e = hipStreamSynchronize(s);
         if (e != hipSuccess) rc = hip_fail(e, "resize");
@@ -588,7 +619,19 @@ int ik_encode(const ik_image* img, int fmt, int quality, uint8_t** out, size_t* 
     if (img->w == 0 || img->h == 0) return fail(IK_ERR_TRANSFORM, "cannot encode an empty image");
     DeviceGuard g(img->device);
     std::vector<uint8_t> bytes;
-    int st = encode_device_image(img->d, img->w, img->h, img->c, img->pitch, fmt, quality, bytes);
+    int st;
+    if (img->depth == 2) {  // to_rgb8 / to_rgba8 rescale the u16 samples first
+        ik_image* u8 = nullptr;
+        st = alloc_image(img->w, img->h, img->c, &u8);
+        if (st) return st;
+        hipError_t e = launch_u16_to_u8(img->d, img->pitch, u8->d, u8->pitch, (int)(img->w * img->c), (int)img->h,
+                                        thread_stream());
+        st = e == hipSuccess ? encode_device_image(u8->d, u8->w, u8->h, u8->c, u8->pitch, fmt, quality, bytes)
+                             : hip_fail(e, "u16 -> u8");
+        ik_image_free(u8);
+    } else {
+        st = encode_device_image(img->d, img->w, img->h, img->c, img->pitch, fmt, quality, bytes);
+    }
     if (st) return st;
     *out = (uint8_t*)malloc(bytes.size() ? bytes.size() : 1);
     if (!*out) return fail(IK_ERR_NOMEM, "out of host memory");

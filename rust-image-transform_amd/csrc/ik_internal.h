@@ -74,6 +74,12 @@ struct ResizePlan {
 // 32-bit num_records and row offsets: images over INT32_MAX bytes take the naive
 // two-pass path (whose caller must then pass naive_tmp).
 inline bool resize_fused_fits(size_t src_pitch, size_t H) { return src_pitch * H <= 0x7FFFFFFFull; }
+// 16-bit images: the two-pass path over u16 samples (tmp: nh * W * C floats), and
+// the u16 -> u8 rescale of to_rgb8 / to_rgba8
+hipError_t launch_resize16(const ResizePlan& plan, const uint8_t* src, size_t src_pitch, uint8_t* dst,
+                           size_t dst_pitch, float* tmp, hipStream_t s);
+hipError_t launch_u16_to_u8(const uint8_t* src, size_t sp, uint8_t* dst, size_t dp, int row_samples, int rows,
+                            hipStream_t s);
 hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_pitch,
                          size_t src_img_stride, uint8_t* dst, size_t dst_pitch,
                          size_t dst_img_stride, int n, float* naive_tmp, hipStream_t s);

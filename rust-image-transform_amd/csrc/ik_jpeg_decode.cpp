@@ -178,7 +178,9 @@ struct Decoder {
         const int nc = s[5];
         if (!width || !height) return fail(IK_ERR_TRANSFORM, "%s: zero dimension", kFmtErr);
         if (nc != 1 && nc != 3) return fail(IK_ERR_UNSUPPORTED, "JPEG with %d components is not supported", nc);
-        if ((uint64_t)width * height > (512ull << 20) / 3) return fail(IK_ERR_TRANSFORM, "Limits are exceeded");
+        // image's default Limits: max_alloc 512 MiB of decoded bytes (L8: 1 per pixel, Rgb8: 3)
+        if ((uint64_t)width * height * (nc == 1 ? 1u : 3u) > (512ull << 20))
+            return fail(IK_ERR_TRANSFORM, "Limits are exceeded");
         comps.resize(nc);
         for (int i = 0; i < nc; ++i) {
             comps[i].id = s[6 + 3 * i];

@@ -328,6 +328,75 @@ __global__ __launch_bounds__(kThreads) void k_horz_naive(ResizeArgs a) {
     a.dst[(size_t)img * a.dst_img_stride + (size_t)r * a.dst_pitch + v] = float_nearest_u8(acc);
 }
 
+// ---- 16-bit images (Rgb16 / Rgba16 / L16 / La16 from 16-bit PNG) ----------------
+// image 0.25.8 resamples u16 samples with the same f32 sequence as u8 ones and
+// clamps to u16::MAX before FloatNearest; the two passes of the fallback path,
+// over samples instead of bytes (a.row_bytes counts samples here).
+__global__ __launch_bounds__(kThreads) void k_vert_naive16(ResizeArgs a) {
+    const int b = blockIdx.x * kThreads + threadIdx.x;
+    const int r = blockIdx.y;
+    if (b >= a.row_bytes) return;
+    const int l = a.ly[r], n = a.ny[r];
+    const float* __restrict__ w = a.wy + (size_t)r * a.Ty;
+    float t = 0.0f;
+    for (int k = 0; k < n; ++k) {
+        const uint16_t v = *reinterpret_cast<const uint16_t*>(a.src + (size_t)(l + k) * a.src_pitch + 2 * (size_t)b);
+        const float prod = (float)v * w[k];
+        t = t + prod;
+    }
+    a.tmp[(size_t)r * a.row_bytes + b] = t;
+}
+
+__global__ __launch_bounds__(kThreads) void k_horz_naive16(ResizeArgs a) {
+    const int v = blockIdx.x * kThreads + threadIdx.x;
+    const int r = blockIdx.y;
+    if (v >= a.nw * a.C) return;
+    const int ox = v / a.C, c = v - ox * a.C;
+    const float* __restrict__ t = a.tmp + (size_t)r * a.row_bytes;
+    const int n = a.nx[ox];
+    const float* __restrict__ w = a.wx + (size_t)ox * a.Tx;
+    int idx = a.lx[ox] * a.C + c;
+    float acc = 0.0f;
+    for (int k = 0; k < n; ++k, idx += a.C) {
+        const float prod = t[idx] * w[k];
+        acc = acc + prod;
+    }
+    acc = acc < 0.0f ? 0.0f : (acc > 65535.0f ? 65535.0f : acc);
+    *reinterpret_cast<uint16_t*>(a.dst + (size_t)r * a.dst_pitch + 2 * (size_t)v) = (uint16_t)roundf(acc);
+}
+
+hipError_t launch_resize16(const ResizePlan& plan, const uint8_t* src, size_t src_pitch, uint8_t* dst,
+                           size_t dst_pitch, float* tmp, hipStream_t s) {
+    ResizeArgs a = plan.args;
+    a.src = src; a.src_pitch = src_pitch; a.src_img_stride = 0;
+    a.dst = dst; a.dst_pitch = dst_pitch; a.dst_img_stride = 0;
+    a.tmp = tmp;
+    dim3 g1((a.row_bytes + kThreads - 1) / kThreads, a.nh);
+    hipLaunchKernelGGL(k_vert_naive16, g1, dim3(kThreads), 0, s, a);
+    dim3 g2((a.nw * a.C + kThreads - 1) / kThreads, a.nh);
+    hipLaunchKernelGGL(k_horz_naive16, g2, dim3(kThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+// to_rgb8 / to_rgba8 of a 16-bit image, per sample: u8 = (v + 128) / 257
+// (image's u16 -> u8 rescale, rounding; parity unpinned)
+__global__ __launch_bounds__(kThreads) void k_u16_to_u8(const uint8_t* src, size_t sp, uint8_t* dst, size_t dp,
+                                                        int row_samples) {
+    const int x = blockIdx.x * kThreads + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= row_samples) return;
+    const uint32_t v = *reinterpret_cast<const uint16_t*>(src + (size_t)y * sp + 2 * (size_t)x);
+    dst[(size_t)y * dp + x] = (uint8_t)((v + 128u) / 257u);
+}
+
+hipError_t launch_u16_to_u8(const uint8_t* src, size_t sp, uint8_t* dst, size_t dp, int row_samples, int rows,
+                            hipStream_t s) {
+    if (row_samples <= 0 || rows <= 0) return hipSuccess;
+    dim3 g((row_samples + kThreads - 1) / kThreads, rows);
+    hipLaunchKernelGGL(k_u16_to_u8, g, dim3(kThreads), 0, s, src, sp, dst, dp, row_samples);
+    return hipGetLastError();
+}
+
 size_t resize_lds_bytes(const ResizeArgs& a, bool wl, int flush) {
     return sizeof(float) * ((size_t)flush * kRowWords + (wl ? (size_t)a.max_strip_weights : 0) +
                             (size_t)a.max_strip_cols);

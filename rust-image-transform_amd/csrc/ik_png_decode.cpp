@@ -590,9 +590,10 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
     parallel_for((int)host.size(), 0, [&](int k) {
         const int i = host[k];
         thread_local std::vector<uint8_t> px;
-        uint32_t w = 0, h = 0, c = 0;
-        int st = decode_png(bytes[i], lens[i], w, h, c, px);
-        if (!st) st = ik_image_from_host(px.data(), w, h, c, &outs[i]);
+        uint32_t w = 0, h = 0, c = 0, dep = 1;
+        int st = decode_png(bytes[i], lens[i], w, h, c, px, &dep);
+        if (!st) st = dep == 2 ? ik_image_from_host16(reinterpret_cast<const uint16_t*>(px.data()), w, h, c, &outs[i])
+                               : ik_image_from_host(px.data(), w, h, c, &outs[i]);
         if (px.capacity() > (128u << 20)) std::vector<uint8_t>().swap(px);
         status[i] = st;
         if (st && msgs) {

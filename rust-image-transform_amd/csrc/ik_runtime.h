@@ -12,7 +12,8 @@
 #include "ik_internal.h"
 
 struct ik_image {
-    uint32_t w = 0, h = 0, c = 0;  // 8-bit, c interleaved channels
+    uint32_t w = 0, h = 0, c = 0;  // c interleaved channels
+    uint32_t depth = 1;            // bytes per sample: 1 (8-bit) or 2 (16-bit, native-endian u16)
     size_t pitch = 0;              // bytes between rows on the device (multiple of 256)
     uint8_t* d = nullptr;          // device pixels
     bool owned = true;
@@ -90,7 +91,7 @@ int copy_h2d_2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, 
                 size_t height, hipStream_t s);
 int copy_d2h_2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,
                 size_t height, hipStream_t s);
-int alloc_image(uint32_t w, uint32_t h, uint32_t c, ik_image** out);
+int alloc_image(uint32_t w, uint32_t h, uint32_t c, ik_image** out, uint32_t depth = 1);
 
 // per-device constant tables (WebP gamma tables)
 struct DeviceConsts {
@@ -146,7 +147,10 @@ int webp_encode_gpu(const uint8_t* d_yuv, int w, int h, int quality, std::vector
 enum class Sniffed { Png, Jpeg, Gif, WebP, Tiff, Bmp, Ico, Hdr, Avif, OpenExr, Qoi, Farbfeld, Pnm, Dds, Unknown };
 Sniffed guess_format(const uint8_t* b, size_t n);
 const char* format_name(Sniffed f);
-int decode_png(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& c, std::vector<uint8_t>& px);
+// depth (optional): 16-bit streams decode to native-endian u16 samples (*depth = 2);
+// without it they are unsupported
+int decode_png(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& c, std::vector<uint8_t>& px,
+               uint32_t* depth = nullptr);
 uint32_t png_chunk_crc(const uint8_t* type, const uint8_t* data, size_t len);  // CRC-32 of type + data
 // PNG on the GPU (ik_png_decode.cpp + ik_png.hip): inflate + unfilter of n streams
 // in one set of launches, straight into new device images; streams the GPU path

@@ -34,6 +34,8 @@ SIGNATURES = [
     ("ik_image_wrap_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_size_t, ctypes.POINTER(c_img_p)]),
     ("ik_image_info", ctypes.c_int, [c_img_p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     ("ik_image_to_host", ctypes.c_int, [c_img_p, ctypes.c_void_p, ctypes.c_size_t]),
+    ("ik_image_depth", ctypes.c_int, [c_img_p]),
+    ("ik_image_from_host16", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(c_img_p)]),
     ("ik_image_free", None, [c_img_p]),
     ("ik_buf_free", None, [ctypes.c_void_p]),
     ("ik_decode", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(c_img_p), ctypes.POINTER(ctypes.c_int)]),

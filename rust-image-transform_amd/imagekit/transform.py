@@ -55,16 +55,18 @@ class DynamicImage:
 
     @classmethod
     def from_array(cls, pixels: np.ndarray) -> "DynamicImage":
-        """ImageBuffer::from_raw on an (H, W) or (H, W, C) uint8 array."""
-        a = np.ascontiguousarray(pixels, dtype=np.uint8)
+        """ImageBuffer::from_raw on an (H, W) or (H, W, C) array: uint8 (L8 / La8 /
+        Rgb8 / Rgba8) or uint16 (L16 / La16 / Rgb16 / Rgba16)."""
+        wide = np.asarray(pixels).dtype == np.uint16
+        a = np.ascontiguousarray(pixels, dtype=np.uint16 if wide else np.uint8)
         if a.ndim == 2:
             a = a[:, :, None]
         if a.ndim != 3 or not 1 <= a.shape[2] <= 4:
-            raise InvalidArgument("expected (H, W, C) uint8 with C in 1..4")
+            raise InvalidArgument("expected (H, W, C) uint8 or uint16 with C in 1..4")
         h, w, c = a.shape
         lib = _lib.load()
         out = ctypes.c_void_p()
-        st = lib.ik_image_from_host(a.ctypes.data, w, h, c, ctypes.byref(out))
+        st = (lib.ik_image_from_host16 if wide else lib.ik_image_from_host)(a.ctypes.data, w, h, c, ctypes.byref(out))
         if st:
             _raise(st, "from_array")
         return cls(out.value)
@@ -93,7 +95,8 @@ class DynamicImage:
         return self._info()[2]
 
     def color(self) -> str:
-        return _COLOR[self._info()[2]]
+        name = _COLOR[self._info()[2]]
+        return name.replace("8", "16") if self.depth == 2 else name
 
     def _info(self):
         lib = _lib.load()
@@ -103,10 +106,16 @@ class DynamicImage:
             _raise(st, "image_info")
         return w.value, h.value, c.value
 
+    @property
+    def depth(self) -> int:
+        """Bytes per sample: 1 (8-bit) or 2 (16-bit)."""
+        return int(_lib.load().ik_image_depth(self._h))
+
     def to_array(self) -> np.ndarray:
-        """Copy the pixels back to the host as an (H, W, C) uint8 array."""
+        """Copy the pixels back to the host as an (H, W, C) array (uint8, or uint16
+        for a 16-bit image)."""
         w, h, c = self._info()
-        out = np.empty((h, w, c), np.uint8)
+        out = np.empty((h, w, c), np.uint16 if self.depth == 2 else np.uint8)
         st = _lib.load().ik_image_to_host(self._h, out.ctypes.data, out.nbytes)
         if st:
             _raise(st, "to_array")

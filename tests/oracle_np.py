@@ -91,14 +91,16 @@ def axis_weights(n_in: int, n_out: int, f: int):
     return out
 
 
-def _round_half_away(t: np.ndarray) -> np.ndarray:
-    t = np.clip(t.astype(np.float64), 0.0, 255.0)
-    return np.floor(t + 0.5).astype(np.uint8)  # t >= 0; exact in f64
+def _round_half_away(t: np.ndarray, maxv: float = 255.0, dtype=np.uint8) -> np.ndarray:
+    t = np.clip(t.astype(np.float64), 0.0, maxv)
+    return np.floor(t + 0.5).astype(dtype)  # t >= 0; exact in f64
 
 
 def resize(src: np.ndarray, nw: int, nh: int, f: int) -> np.ndarray:
-    """imageops::resize on an (H, W, C) uint8 array."""
+    """imageops::resize on an (H, W, C) uint8 or uint16 array (16-bit samples: the
+    same f32 sequence, clamped to u16::MAX)."""
     H, W, C = src.shape
+    wide = src.dtype == np.uint16
     if (nw, nh) == (W, H):
         return src.copy()
     tmp = np.zeros((nh, W, C), dtype=F)
@@ -107,12 +109,12 @@ def resize(src: np.ndarray, nw: int, nh: int, f: int) -> np.ndarray:
         for k, w in enumerate(ws):
             t = t + src[left + k].astype(F) * w
         tmp[oy] = t
-    out = np.zeros((nh, nw, C), dtype=np.uint8)
+    out = np.zeros((nh, nw, C), dtype=np.uint16 if wide else np.uint8)
     for ox, (left, ws) in enumerate(axis_weights(W, nw, f)):
         t = np.zeros((nh, C), dtype=F)
         for k, w in enumerate(ws):
             t = t + tmp[:, left + k, :] * w
-        out[:, ox, :] = _round_half_away(t)
+        out[:, ox, :] = _round_half_away(t, 65535.0, np.uint16) if wide else _round_half_away(t)
     return out
 
 

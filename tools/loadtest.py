@@ -13,7 +13,17 @@ decoded MPix/s.  --formats webp,jpeg,avif mixes output formats (the /sign mix,
 loadtest/src/main.rs:59-60); --restart adds RSTn markers per MCU row to the sources
 (GPU entropy decoding); without it the sources decode on the host entropy path.
 
-Usage: python tools/loadtest.py [--requests 1024 --batch 64 --sources 8 --threads 16]
+Dynamic queue (default when run as one process): the library serves every visible
+GPU itself (ik_init(-1); IK_DEVICES picks them), and --clients threads call
+ik_transform_batch concurrently, as request handlers would; each call's requests go
+to the devices with the least outstanding work.
+
+CPU leg (--cpu-seconds S): the same request mix through the reference CPU path
+restated -- Pillow's libjpeg-turbo decode (zune-jpeg is absent), the oracle's
+image 0.25.8 Lanczos3 resize and libwebp -- on nproc forked worker processes for
+about S seconds, before anything touches the GPU.
+
+Usage: python tools/loadtest.py [--requests 10000 --batch 64 --sources 8 --threads 16 --clients 4]
 """
 import argparse
 import io
@@ -41,6 +51,49 @@ def shard(reqs, rank, world):
     return reqs[rank::world]
 
 
+_CPU = {}
+
+
+def _cpu_one(k):
+    from PIL import Image
+    orc, srcs, reqs, q = _CPU["orc"], _CPU["srcs"], _CPU["reqs"], _CPU["q"]
+    s, w, h, f = reqs[k % len(reqs)]
+    img = np.asarray(Image.open(io.BytesIO(srcs[s])).convert("RGB"))
+    fmt = {"jpeg": 0, "webp": 1, "avif": 2}[f]
+    if fmt == 2:
+        return 0  # the oracle has no AVIF encoder: the leg covers the webp/jpeg requests
+    orc.transform(img, w, h, 4, fmt, q)
+    return 1
+
+
+def cpu_leg(args, srcs, reqs):
+    """Reference CPU path restated on the same requests: nproc forked processes, one
+    request each at a time, for about args.cpu_seconds (started before GPU use)."""
+    import multiprocessing as mp
+
+    import ikutil
+    _CPU.update(orc=ikutil.Oracle(), srcs=srcs, reqs=reqs, q=args.quality)
+    _cpu_one(0)
+    t0 = time.perf_counter()
+    for k in range(4):
+        _cpu_one(k)
+    t1 = (time.perf_counter() - t0) / 4
+    nproc = os.cpu_count() or 1
+    per = max(2, min(4, int(args.cpu_seconds / max(t1, 1e-3))))
+    print(f"[loadtest] cpu leg: {nproc} processes x {per} requests ({t1 * 1e3:.0f} ms each on one core)",
+          file=sys.stderr, flush=True)
+    with mp.get_context("fork").Pool(nproc) as pool:
+        pool.map(_cpu_one, range(nproc), chunksize=1)
+        t0 = time.perf_counter()
+        done = sum(pool.map(_cpu_one, range(nproc * per), chunksize=per))
+        wall = time.perf_counter() - t0
+    sys.path.insert(0, ROOT)
+    from bench import host_info  # host facts as bench.py records them (CPU model, nproc, cgroup quota)
+    return {"value": round(done / wall, 1), "unit": "requests/s", "processes": nproc, "requests": done,
+            "wall_s": round(wall, 2), "kind": "port (Pillow libjpeg-turbo decode + oracle Lanczos3 resize + libwebp)",
+            "single_thread_requests_per_s": round(1 / t1, 2), "host": host_info()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--requests", type=int, default=1024)
@@ -52,24 +105,16 @@ def main():
     ap.add_argument("--restart", action="store_true")
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--clients", type=int, default=0,
+                    help="client threads calling ik_transform_batch at once (0 = one per logical device)")
+    ap.add_argument("--cpu-seconds", type=float, default=0.0, help="CPU leg of about this long (0 = none)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
-    if torch.cuda.is_available():
-        torch.cuda.set_device(local)
     from PIL import Image
     import ikutil
-    from imagekit import ImageFormat, _lib, transform_batch
-    lib = _lib.load()
-    assert lib.ik_init(local) == 0, _lib.last_error()
-
     S = args.size
     srcs = []
     for k in range(args.sources):
@@ -77,8 +122,27 @@ def main():
         kw = {"restart_marker_rows": 1} if args.restart else {}
         Image.fromarray(ikutil.synth(S, S, 3, seed=100 + k, pattern="S")).save(buf, format="JPEG", quality=85, **kw)
         srcs.append(buf.getvalue())
-    fmts = [ImageFormat[f] for f in args.formats.split(",")]
-    mine = shard(make_requests(args.requests, args.sources, fmts, args.seed), rank, world)
+    fmt_names = args.formats.split(",")
+    reqs = make_requests(args.requests, args.sources, fmt_names, args.seed)
+    cpu = cpu_leg(args, srcs, reqs) if args.cpu_seconds > 0 and rank == 0 and world == 1 else None
+
+    import threading
+
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    from imagekit import ImageFormat, _lib, transform_batch
+    lib = _lib.load()
+    queue = world == 1
+    assert lib.ik_init(-1 if queue else local) == 0, _lib.last_error()
+    ndev = lib.ik_logical_device_count() if queue else 1
+    if args.clients <= 0:
+        args.clients = max(1, ndev)
+    mine = [(s, w, h, ImageFormat[f]) for s, w, h, f in shard(reqs, rank, world)]
 
     def run_batch(chunk):
         return transform_batch([srcs[s] for s, _, _, _ in chunk], [(w, h) for _, w, h, _ in chunk],
@@ -92,21 +156,41 @@ def main():
         if torch.cuda.is_available():
             torch.cuda.synchronize()
 
+    chunks = [mine[i:i + args.batch] for i in range(0, len(mine), args.batch)]
+    lat, out_bytes = [], [0]
+    lock = threading.Lock()
+    nxt = [0]
+
+    def client():  # a request handler: takes the next batch, waits for its bytes
+        while True:
+            with lock:
+                if nxt[0] >= len(chunks):
+                    return
+                chunk = chunks[nxt[0]]
+                nxt[0] += 1
+            tb = time.perf_counter()
+            res = run_batch(chunk)
+            dt = (time.perf_counter() - tb) * 1e3
+            with lock:
+                lat.append(dt)
+                out_bytes[0] += sum(len(r) for r in res)
+                if len(lat) % 20 == 0:
+                    print(f"[loadtest] {len(lat) * args.batch} requests", file=sys.stderr, flush=True)
+
     barrier()
     t0 = time.perf_counter()
-    lat, out_bytes = [], 0
-    for i in range(0, len(mine), args.batch):
-        chunk = mine[i:i + args.batch]
-        tb = time.perf_counter()
-        res = run_batch(chunk)
-        lat.append((time.perf_counter() - tb) * 1e3)
-        out_bytes += sum(len(r) for r in res)
+    ts = [threading.Thread(target=client) for _ in range(max(1, args.clients))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
     elapsed = time.perf_counter() - t0
     barrier()
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}" if torch.cuda.is_available() else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    out_bytes = out_bytes[0]
     if rank == 0:
         print(json.dumps({
             "metric": "loadtest /img requests/s (2000^2 JPEG sources, w,h in [200,800), q80)",
@@ -118,6 +202,10 @@ def main():
             "decoded_mpix_per_s": round(args.requests * S * S / elapsed / 1e6, 1),
             "output_bytes_per_request": out_bytes // max(1, len(mine)),
             "host_threads_per_gpu": args.threads,
+            "filter": "lanczos3 (the reference's)",
+            "dispatch": (f"in-library dynamic queue over {ndev} logical device(s), {args.clients} client threads"
+                         if queue else f"{world} processes, round-robin shards"),
+            "cpu_leg": cpu,
         }))
     if dist is not None:
         dist.destroy_process_group()
