@@ -118,7 +118,12 @@ uint8_t* pinned_slot(int slot, size_t bytes) {
     a.p = nullptr;
     a.cap = 0;
     size_t want = bytes < (1u << 20) ? (1u << 20) : bytes;
-    if (hipHostMalloc((void**)&a.p, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+    const hipError_t e = hipHostMalloc((void**)&a.p, want, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        a.p = nullptr;
+        fail(IK_ERR_NOMEM, "hipHostMalloc(%zu bytes): %s", want, hipGetErrorString(e));
+        return nullptr;
+    }
     a.cap = want;
     return a.p;
 }
@@ -135,7 +140,7 @@ int copy_h2d_2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, 
     for (size_t y0 = 0; y0 < height; y0 += chunk_rows) {
         const size_t rows = height - y0 < chunk_rows ? height - y0 : chunk_rows;
         uint8_t* st = staging(rows * width);
-        if (!st) return fail(IK_ERR_NOMEM, "cannot allocate pinned staging");
+        if (!st) return IK_ERR_NOMEM;  // pinned_slot recorded the error
         for (size_t y = 0; y < rows; ++y) std::memcpy(st + y * width, src + (y0 + y) * spitch, width);
         IK_HIP(hipMemcpy2DAsync(dst + y0 * dpitch, dpitch, st, width, width, rows, hipMemcpyHostToDevice, s));
         IK_HIP(hipStreamSynchronize(s));
@@ -149,7 +154,7 @@ int copy_d2h_2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, 
     for (size_t y0 = 0; y0 < height; y0 += chunk_rows) {
         const size_t rows = height - y0 < chunk_rows ? height - y0 : chunk_rows;
         uint8_t* st = staging(rows * width);
-        if (!st) return fail(IK_ERR_NOMEM, "cannot allocate pinned staging");
+        if (!st) return IK_ERR_NOMEM;  // pinned_slot recorded the error
         IK_HIP(hipMemcpy2DAsync(st, width, src + y0 * spitch, spitch, width, rows, hipMemcpyDeviceToHost, s));
         IK_HIP(hipStreamSynchronize(s));
         for (size_t y = 0; y < rows; ++y) std::memcpy(dst + (y0 + y) * dpitch, st + y * width, width);

@@ -363,11 +363,13 @@ struct LaneResult {
 // value of the u16 stream at absolute position q after following window markers.
 // lane_obase: output offsets of the image's decoders (ascending), n of them;
 // page_lane[q >> page_shift] = the decoder that holds the page's first byte.
-// Returns -1 on a malformed chain.
+// Returns -1 on a malformed chain.  Each hop lands in a strictly earlier decoder
+// (a marker points into the window before its decoder's first byte), so a chain
+// has at most n hops: repetitive data can carry a byte back through every lane.
 template <class U16, class Off, class Pages>
 IK_HD int resolve_at(U16 u16, Off lane_obase, int n, Pages page_lane, int page_shift, int64_t q) {
     int lane = -1;
-    for (int guard = 0; guard < 64; ++guard) {
+    for (int guard = 0; guard <= n; ++guard) {
         const uint32_t v = u16[q];
         if (v < 256u) return (int)v;
         if (!(v & 0x8000u)) return -1;

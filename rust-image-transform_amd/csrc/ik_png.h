@@ -11,7 +11,14 @@ namespace ik {
 
 constexpr int kPngInflateThreads = 64;     // decoder lanes per workgroup (one wave: LDS 320 B per lane)
 constexpr int kPngExpandThreads = 64;      // expand lanes per workgroup (LDS: 256 B literal table each)
-constexpr int kPngUnfilterThreads = 1024;  // 16 waves: 16 bands in flight per image
+constexpr int kPngUnfilterThreads = 1024;  // 16 waves, one 64-row band each
+constexpr int kPngUnfilterWaves = kPngUnfilterThreads / 64;
+// workgroups per image for the unfilter pass: one per 16 bands of 64 rows, at
+// most 32 (all of an image's workgroups must be resident together)
+IK_HD int png_unfilter_groups(int h) {
+    const int g = ((h + 63) / 64 + kPngUnfilterWaves - 1) / kPngUnfilterWaves;
+    return g < 32 ? g : 32;
+}
 constexpr uint64_t kPngChunkBytes = 16384; // candidate-search chunk of the compressed stream
 constexpr int kPngPageShift = 12;          // resolve: output page -> decoder table
 
@@ -49,6 +56,9 @@ hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, int
 hipError_t launch_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int n, const uint16_t* tok, int* status,
                              hipStream_t s);
 hipError_t launch_png_resolve(const PngImgDev* imgs, const int2* rows, int nrows, int* err, hipStream_t s);
-hipError_t launch_png_unfilter(const PngImgDev* imgs, int n, int bpp, hipStream_t s);
+// groups[t] = (image, band group) of the workgroup holding ticket t; prog: one
+// zeroed counter per band (the image's at prog_base[image]); ticket: zeroed
+hipError_t launch_png_unfilter(const PngImgDev* imgs, const int2* groups, int ngroups, const int* prog_base,
+                               unsigned* prog, unsigned* ticket, int bpp, hipStream_t s);
 
 }  // namespace ik

@@ -20,11 +20,11 @@
 //                   depends on the row above and on its own left bytes, so it is a
 //                   skewed wavefront: lane = row (64 rows per wave, one band),
 //                   16-byte chunks, lane l works on chunk s - l at step s and hands
-//                   its unfiltered chunk to lane l+1 by a DPP wave shift.  The
-//                   workgroup's waves take consecutive bands; a band's first row
-//                   reads the previous band's last row from memory once the
-//                   previous wave has published it (LDS progress counter,
-//                   workgroup-scope release/acquire).
+//                   its unfiltered chunk to lane l+1 by a DPP wave shift.  One wave
+//                   per band, an image's bands over several workgroups; a band's
+//                   first row reads the previous band's last row from memory once
+//                   it is published (global progress counters, agent-scope
+//                   release/acquire; workgroups ordered by a start ticket).
 #include "ik_inflate.h"
 #include "ik_internal.h"
 #include "ik_png.h"
@@ -532,87 +532,200 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t lane0) {
 
 __device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[4], int i) { return (w[i >> 2] >> (8 * (i & 3))) & 255u; }
 
+// One wave per 64-row band; an image's bands are spread over ceil(bands / 16)
+// workgroups (16 waves each), so a batch fills the chip instead of one CU per
+// image.  A band's first row needs the previous band's last row: that row's
+// lane stores its chunks sc1 (written through) and, once per group of kUnfG
+// steps, waits for them and sets the band's progress counter (sc1 store); the
+// next band's lane 0 polls it (sc1) and loads the group's kUnfG chunks of the
+// row above with sc1 loads -- MI355X_MICROARCH.md's measured cross-CU/XCD
+// hand-off, without an agent release (its L2 write-back costs microseconds).
+// Each lane's filtered bytes for the next group are prefetched a group ahead, so
+// a step waits on memory only at group boundaries.  Workgroups take a ticket from
+// a global counter when they start, and the ticket -- not blockIdx -- picks their
+// (image, workgroup k of the image's K); wave w takes band w K + k, so the bands
+// in flight spread over K CUs.  A band waits on the previous band, held by
+// another of the image's workgroups: tickets go out in start order, so at most
+// one image is partly started at any time, every other started image has all its
+// workgroups running and finishes, and the CUs it frees start the rest -- no
+// deadlock whatever the dispatch order (an image needs K <= the resident
+// workgroups of the chip, 256 at one per CU; K = bands / 16).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kUnfG = 8;
+
+typedef const __attribute__((address_space(1))) u32x4* gu32x4p;
+
+// a wave-uniform 64-bit value in SGPRs (readfirstlane returns int: zero-extend
+// each half, or a low word with bit 31 set sign-extends into the high word)
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// per-lane predictor masks (all-ones for the row's filter type): the byte loop
+// selects by AND/OR, not by per-lane branches
+struct FtMask {
+    uint32_t sub, up, avg, paeth;
+    __device__ explicit FtMask(uint32_t ft)
+        : sub(ft == 1 ? ~0u : 0u), up(ft == 2 ? ~0u : 0u), avg(ft == 3 ? ~0u : 0u), paeth(ft == 4 ? ~0u : 0u) {}
+};
+
 template <int BPP>
-__global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngImgDev* imgs) {
-    constexpr int NW = kPngUnfilterThreads / 64;
-    __shared__ unsigned s_prog[NW];
-    const PngImgDev I = imgs[blockIdx.x];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (threadIdx.x < NW) s_prog[threadIdx.x] = 0;
+__device__ __forceinline__ void unfilter_chunk(const u32x4& rawv, const uint32_t (&up)[4], const uint32_t (&prevup)[4],
+                                               const uint32_t (&prevcur)[4], const FtMask& fm, uint32_t (&o)[4]) {
+    const uint32_t raw[4] = {rawv.x, rawv.y, rawv.z, rawv.w};
+    o[0] = o[1] = o[2] = o[3] = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        // a = left, b = up, c = up-left (bytes BPP back; from the previous chunk at its start)
+        const uint32_t a = i >= BPP ? ((o[(i - BPP) >> 2] >> (8 * ((i - BPP) & 3))) & 255u)
+                                    : byte_of(prevcur, 16 + i - BPP);
+        const uint32_t b = byte_of(up, i);
+        const uint32_t c = i >= BPP ? byte_of(up, i - BPP) : byte_of(prevup, 16 + i - BPP);
+        const int d1 = (int)b - (int)c, d2 = (int)a - (int)c;
+        const int pa = d1 < 0 ? -d1 : d1, pb = d2 < 0 ? -d2 : d2, pc = (d1 + d2) < 0 ? -(d1 + d2) : (d1 + d2);
+        const uint32_t paeth = (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
+        const uint32_t pred = (a & fm.sub) | (b & fm.up) | (((a + b) >> 1) & fm.avg) | (paeth & fm.paeth);
+        const uint32_t v = (byte_of(raw, i) + pred) & 255u;
+        o[i >> 2] |= v << (8 * (i & 3));
+    }
+}
+
+template <int BPP>
+__global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngImgDev* imgs, const int2* groups,
+                                                                      const int* prog_base, unsigned* prog,
+                                                                      unsigned* ticket) {
+    constexpr int NW = kPngUnfilterThreads / 64, G = kUnfG;
+    __shared__ int s_t;
+    if (threadIdx.x == 0) s_t = (int)atomicAdd(ticket, 1u);
     __syncthreads();
+    const int2 gk = groups[s_t];  // (image, workgroup of the image)
+    const PngImgDev I = imgs[gk.x];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int nch = (I.rowbytes + 15) >> 4;
     const int nbands = (I.H + 63) >> 6;
-    const int pw = (wave + NW - 1) % NW;  // the wave that owns the previous band
-    int m = 0;                            // this wave's band sequence number
-    for (int band = wave; band < nbands; band += NW, ++m) {
+    // bands interleaved over the image's K workgroups: the ~(row chunks / 72)
+    // bands in flight at a time sit on K CUs, not all on one; past 16 K bands a
+    // wave takes its next band (in order: the lowest unfinished band always has
+    // a finished predecessor)
+    const int K = png_unfilter_groups(I.H);
+    unsigned* pg = prog + prog_base[gk.x];
+    for (int band = wave * K + gk.y; band < nbands; band += NW * K) {
         const int y = band * 64 + lane;
         const bool live = y < I.H;
         uint8_t* row = I.dst + (size_t)(live ? y : 0) * I.pitch;
-        const uint32_t ft = live ? I.ft[y] : 0u;
-        const uint8_t* above = band > 0 ? I.dst + (size_t)(band * 64 - 1) * I.pitch : nullptr;
-        // the previous band's sequence number in its wave
-        const int pm = band > 0 ? (band - 1) / NW : 0;
+        const FtMask fm(live ? I.ft[y] : 0u);
+        const uint64_t above = band > 0 ? (uint64_t)(size_t)(I.dst + (size_t)(band * 64 - 1) * I.pitch) : 0;
         uint32_t cur[4] = {0, 0, 0, 0}, up[4] = {0, 0, 0, 0};
         uint32_t prevcur[4] = {0, 0, 0, 0}, prevup[4] = {0, 0, 0, 0};  // last chunk (left context)
-        uint32_t raw[4] = {0, 0, 0, 0};
-        const int steps = nch + 63;
-        for (int s = 0; s < steps; ++s) {
-            const int j = s - lane;
-            // up chunk: lane l-1's result of the previous step; lane 0: previous band
-            uint32_t from_above[4] = {0, 0, 0, 0};
-            if (lane == 0 && above && j < nch) {
-                const unsigned need = (unsigned)(pm * nch + j + 1);
-                while (__hip_atomic_load(&s_prog[pw], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
-                    __builtin_amdgcn_s_sleep(1);
-                // the other wave's stores: read through to L2 (sc1), not a stale L1 line
-                const unsigned* ap = reinterpret_cast<const unsigned*>(above + 16 * j);
+        // this lane's filtered chunks for a group of steps (clamped: always a valid
+        // address), as asm loads off the image base: the compiler, which cannot count
+        // the other asm memory ops here, would otherwise wait for them at once
+        const uint64_t dbase = uniform_u64((uint64_t)(size_t)I.dst);
+        const uint32_t rowoff = (uint32_t)((size_t)(live ? y : 0) * I.pitch);
+        auto fetch = [&](int s0, u32x4 (&r)[G]) {
+            uint32_t off[G];
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    from_above[k] = __hip_atomic_load(ap + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            uint32_t nup[4];
+            for (int t = 0; t < G; ++t) off[t] = rowoff + 16u * (uint32_t)min(max(s0 + t - lane, 0), nch - 1);
+            // s_nop 4: VALU-written SGPR (readfirstlane) -> VMEM read needs 5 wait
+            // states, which the hazard recognizer does not insert for inline asm
+            asm volatile(
+                "s_nop 4\n\t"
+                "global_load_dwordx4 %0, %8, %16\n\t"
+                "global_load_dwordx4 %1, %9, %16\n\t"
+                "global_load_dwordx4 %2, %10, %16\n\t"
+                "global_load_dwordx4 %3, %11, %16\n\t"
+                "global_load_dwordx4 %4, %12, %16\n\t"
+                "global_load_dwordx4 %5, %13, %16\n\t"
+                "global_load_dwordx4 %6, %14, %16\n\t"
+                "global_load_dwordx4 %7, %15, %16"
+                : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7])
+                : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]), "v"(off[7]),
+                  "s"(dbase)
+                : "memory");
+        };
+        // every vector memory op of this wave has completed; r is read only after it
+        auto landed = [](u32x4 (&r)[G]) {
+            asm volatile("s_waitcnt vmcnt(0)"
+                         : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7])
+                         :
+                         : "memory");
+        };
+        u32x4 rcur[G], rnxt[G];
+        fetch(0, rcur);
+        landed(rcur);
+        unsigned seen = 0;  // lane 0: the previous band's progress last read
+        const int ngrp = (nch + 63 + G - 1) / G;
+        for (int g = 0; g < ngrp; ++g) {
+            const int s0 = g * G;
+            u32x4 ab[G];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) nup[k] = wave_shr1(cur[k], from_above[k]);
-            const bool act = live && j >= 0 && j < nch;
-            if (act) {
-                const uint4 u = *reinterpret_cast<const uint4*>(row + 16 * j);
-                raw[0] = u.x; raw[1] = u.y; raw[2] = u.z; raw[3] = u.w;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) { prevup[k] = up[k]; up[k] = nup[k]; prevcur[k] = cur[k]; }
-                if (j == 0) {
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) { prevup[k] = 0; prevcur[k] = 0; }
+            for (int t = 0; t < G; ++t) ab[t] = u32x4{0, 0, 0, 0};
+            if (lane == 0 && above && s0 < nch) {
+                const unsigned need = (unsigned)min(s0 + G, nch);
+                while (seen < need) {
+                    seen = __hip_atomic_load(pg + band - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (seen < need) __builtin_amdgcn_s_sleep(1);
                 }
-                uint32_t o[4] = {0, 0, 0, 0};
+                uint32_t off[G];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    // a = left, b = up, c = up-left (bytes BPP back; from the previous chunk at its start)
-                    const uint32_t a = i >= BPP ? ((o[(i - BPP) >> 2] >> (8 * ((i - BPP) & 3))) & 255u)
-                                                : byte_of(prevcur, 16 + i - BPP);
-                    const uint32_t b = byte_of(up, i);
-                    const uint32_t c = i >= BPP ? byte_of(up, i - BPP) : byte_of(prevup, 16 + i - BPP);
-                    const int d1 = (int)b - (int)c, d2 = (int)a - (int)c;
-                    const int pa = d1 < 0 ? -d1 : d1, pb = d2 < 0 ? -d2 : d2, pc = (d1 + d2) < 0 ? -(d1 + d2) : (d1 + d2);
-                    const uint32_t paeth = (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
-                    const uint32_t pred = ft == 1 ? a : ft == 2 ? b : ft == 3 ? ((a + b) >> 1) : ft == 4 ? paeth : 0u;
-                    const uint32_t v = (byte_of(raw, i) + pred) & 255u;
-                    o[i >> 2] |= v << (8 * (i & 3));
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) cur[k] = o[k];
-                *reinterpret_cast<uint4*>(row + 16 * j) = make_uint4(o[0], o[1], o[2], o[3]);
+                for (int t = 0; t < G; ++t) off[t] = 16u * (uint32_t)min(s0 + t, nch - 1);
+                const uint64_t base = uniform_u64(above);
+                asm volatile(
+                    "s_nop 4\n\t"
+                    "global_load_dwordx4 %0, %8, %16 sc1\n\t"
+                    "global_load_dwordx4 %1, %9, %16 sc1\n\t"
+                    "global_load_dwordx4 %2, %10, %16 sc1\n\t"
+                    "global_load_dwordx4 %3, %11, %16 sc1\n\t"
+                    "global_load_dwordx4 %4, %12, %16 sc1\n\t"
+                    "global_load_dwordx4 %5, %13, %16 sc1\n\t"
+                    "global_load_dwordx4 %6, %14, %16 sc1\n\t"
+                    "global_load_dwordx4 %7, %15, %16 sc1\n\t"
+                    "s_waitcnt vmcnt(0)"
+                    : "=&v"(ab[0]), "=&v"(ab[1]), "=&v"(ab[2]), "=&v"(ab[3]), "=&v"(ab[4]), "=&v"(ab[5]), "=&v"(ab[6]),
+                      "=&v"(ab[7])
+                    : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]),
+                      "v"(off[7]), "s"(base)
+                    : "memory");
             }
-            // the band's last row publishes its chunks for the next band's first row
-            if (lane == 63 && act) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the chunk's store has reached L2
-                __hip_atomic_store(&s_prog[wave], (unsigned)(m * nch + j + 1), __ATOMIC_RELEASE,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (g + 1 < ngrp) fetch(s0 + G, rnxt);
+#pragma unroll
+            for (int t = 0; t < G; ++t) {
+                const int j = s0 + t - lane;
+                // up chunk: lane l-1's result of the previous step; lane 0: the row above
+                uint32_t nup[4];
+                nup[0] = wave_shr1(cur[0], ab[t].x);
+                nup[1] = wave_shr1(cur[1], ab[t].y);
+                nup[2] = wave_shr1(cur[2], ab[t].z);
+                nup[3] = wave_shr1(cur[3], ab[t].w);
+                if (live && j >= 0 && j < nch) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) { prevup[k] = up[k]; up[k] = nup[k]; prevcur[k] = cur[k]; }
+                    if (j == 0) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) { prevup[k] = 0; prevcur[k] = 0; }
+                    }
+                    uint32_t o[4];
+                    unfilter_chunk<BPP>(rcur[t], up, prevup, prevcur, fm, o);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) cur[k] = o[k];
+                    const u32x4 ov = {o[0], o[1], o[2], o[3]};
+                    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(row + 16 * j), "v"(ov) : "memory");
+                }
+            }
+            // the band's last row publishes the chunks it finished in this group
+            const int jl = s0 + G - 1 - 63;
+            if (lane == 63 && live && jl >= 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its sc1 stores have completed
+                __hip_atomic_store(pg + band, (unsigned)min(jl + 1, nch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (g + 1 < ngrp) {
+                landed(rnxt);
+#pragma unroll
+                for (int t = 0; t < G; ++t) rcur[t] = rnxt[t];
             }
         }
-        // rows past the image (last band): publish completion so no waiter stalls
-        if (lane == 63 && !live)
-            __hip_atomic_store(&s_prog[wave], (unsigned)((m + 1) * nch), __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
@@ -646,18 +759,21 @@ hipError_t launch_png_resolve(const PngImgDev* imgs, const int2* rows, int nrows
     return hipGetLastError();
 }
 
-hipError_t launch_png_unfilter(const PngImgDev* imgs, int n, int bpp, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    const dim3 grid(n), block(kPngUnfilterThreads);
+hipError_t launch_png_unfilter(const PngImgDev* imgs, const int2* groups, int ngroups, const int* prog_base,
+                               unsigned* prog, unsigned* ticket, int bpp, hipStream_t s) {
+    if (ngroups <= 0) return hipSuccess;
+    const dim3 grid(ngroups), block(kPngUnfilterThreads);
+#define IK_UNF(B) hipLaunchKernelGGL(k_png_unfilter<B>, grid, block, 0, s, imgs, groups, prog_base, prog, ticket)
     switch (bpp) {
-    case 1: hipLaunchKernelGGL(k_png_unfilter<1>, grid, block, 0, s, imgs); break;
-    case 2: hipLaunchKernelGGL(k_png_unfilter<2>, grid, block, 0, s, imgs); break;
-    case 3: hipLaunchKernelGGL(k_png_unfilter<3>, grid, block, 0, s, imgs); break;
-    case 4: hipLaunchKernelGGL(k_png_unfilter<4>, grid, block, 0, s, imgs); break;
-    case 6: hipLaunchKernelGGL(k_png_unfilter<6>, grid, block, 0, s, imgs); break;
-    case 8: hipLaunchKernelGGL(k_png_unfilter<8>, grid, block, 0, s, imgs); break;
+    case 1: IK_UNF(1); break;
+    case 2: IK_UNF(2); break;
+    case 3: IK_UNF(3); break;
+    case 4: IK_UNF(4); break;
+    case 6: IK_UNF(6); break;
+    case 8: IK_UNF(8); break;
     default: return hipErrorInvalidValue;
     }
+#undef IK_UNF
     return hipGetLastError();
 }
 

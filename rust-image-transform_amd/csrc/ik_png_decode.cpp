@@ -178,6 +178,12 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
     for (double& v : t_png_timing) v = 0;
     Events& ev = events();
     auto rec = [&](int k, hipStream_t st) { if (ev.ok) (void)hipEventRecord(ev.e[k], st); };
+    // a stream the GPU path gives up on: the host decoder takes it (and gives png's
+    // error if the stream is malformed); IK_PNG_TIMING says why
+    auto reject = [&](PngJob& j, const char* why) {
+        j.state = -1;
+        if (timing) fprintf(stderr, "[png] stream %d (%ux%u) -> host decoder: %s\n", j.idx, j.w, j.h, why);
+    };
     double count_dev = 0;
     std::vector<PngJob> jobs(n);
     std::vector<char> gpu(n, 0);
@@ -236,12 +242,18 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
         size_t dyn = up256(sizeof(PngLaneDev) * max_lanes) + up256(sizeof(infl::LaneResult) * max_lanes) +
                      up256(sizeof(int64_t) * max_lanes) + up256(2 * sizeof(int) * max_lanes) +
                      up256(sizeof(PngImgDev) * m);
-        size_t nrows = 0, npages = 0;
+        size_t nrows = 0, npages = 0, nbands = 0, ngroups = 0;
         for (PngJob* j : J) {
             nrows += j->h;
             npages += (j->raw_total >> kPngPageShift) + 1;
+            nbands += ((size_t)j->h + 63) / 64;
+            ngroups += (size_t)png_unfilter_groups((int)j->h);
         }
-        dyn += up256(sizeof(int2) * nrows) + up256(sizeof(int) * npages) + up256(2 * tok_total);
+        // unfilter: band-group table + per-image band offsets (staged), then one
+        // progress counter per band and one ticket per class (zeroed)
+        const size_t unf_tab = up256(sizeof(int2) * ngroups) + up256(sizeof(int) * m);
+        const size_t unf_zero = up256(sizeof(unsigned) * (nbands + 8));
+        dyn += up256(sizeof(int2) * nrows) + up256(sizeof(int) * npages) + unf_tab + unf_zero + up256(2 * tok_total);
         uint8_t* dev = rc ? nullptr : scratch_slot(2, o_dyn + dyn);
         if (!rc && !dev) rc = fail(IK_ERR_DEVICE, "cannot allocate the PNG batch work area (%zu bytes)", o_dyn + dyn);
         PngLaneDev* d_lanes = nullptr;
@@ -251,6 +263,7 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
         PngImgDev* d_cls = nullptr;
         int2* d_rows = nullptr;
         int* d_pages = nullptr;
+        uint8_t* d_unf = nullptr;
         uint16_t* d_tok = nullptr;
         if (!rc) {
             size_t o = o_dyn;
@@ -268,6 +281,8 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             o += up256(sizeof(int2) * nrows);
             d_pages = reinterpret_cast<int*>(dev + o);
             o += up256(sizeof(int) * npages);
+            d_unf = dev + o;
+            o += unf_tab + unf_zero;
             d_tok = reinterpret_cast<uint16_t*>(dev + o);
         }
         uint64_t tok_used = 0;
@@ -363,7 +378,7 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                     const uint32_t cap = infl::tok_capacity(end > LL.start[i] ? end - LL.start[i] : 0, LL.big[i] != 0);
                     if (cap > LL.tcap[i]) {  // a (larger) region from the area
                         const uint64_t need = cap + infl::kTokSlack;
-                        if (tok_used + need > tok_total) { j.state = -1; break; }  // out of room: host decoder
+                        if (tok_used + need > tok_total) { reject(j, "token area full"); break; }  // host decoder
                         LL.tbase[i] = tok_used;
                         LL.tcap[i] = cap;
                         tok_used += need;
@@ -426,7 +441,7 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                 const int st = pngplan::check(j.lanes);
                 dropped += (int)(before - j.lanes.start.size());
                 if (st == 0) j.state = 1;
-                else if (st < 0) j.state = -1;
+                else if (st < 0) reject(j, "lane chain check");
             }
         }
         const double t3 = now_ms();
@@ -440,8 +455,8 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             std::vector<int64_t> ob;
             uint64_t tot = 0;
             pngplan::offsets(j.lanes, ob, &tot);
-            if (tot != j.raw_total) { j.state = -1; continue; }  // png: wrong amount of image data
-            if (alloc_image(j.w, j.h, (uint32_t)j.bpp, &j.img)) { j.state = -1; continue; }
+            if (tot != j.raw_total) { reject(j, "image data length"); continue; }  // png's error
+            if (alloc_image(j.w, j.h, (uint32_t)j.bpp, &j.img)) { reject(j, "image allocation"); continue; }
             hd[k].obase = d_obase + hob.size();
             hd[k].page_lane = d_pages + hpages.size();
             hd[k].nlanes = (int)ob.size();
@@ -493,27 +508,50 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                 if (e == hipSuccess) e = launch_png_resolve(d_imgs, d_rows, (int)hrows.size(),
                                                             reinterpret_cast<int*>(dev + o_err), s);
                 rec(6, s);
-                // unfilter: one launch per bytes-per-pixel class, over that class's images
+                // unfilter: one launch per bytes-per-pixel class, over that class's
+                // images; a workgroup per 16 bands, its (image, group) by ticket
                 if (e == hipSuccess) {
                     std::vector<PngImgDev> cls;
-                    std::vector<std::pair<int, int>> ranges;  // (bpp, first) per class
+                    std::vector<int2> groups;
+                    std::vector<int> pbase;
+                    struct Range { int bpp, img0, grp0; };
+                    std::vector<Range> ranges;
+                    int band0 = 0;
                     for (int bpp : {1, 2, 3, 4, 6, 8}) {
-                        const int first = (int)cls.size();
+                        const Range r{bpp, (int)cls.size(), (int)groups.size()};
                         for (int k = 0; k < m; ++k)
-                            if (J[k]->state == 1 && hd[k].bpp == bpp) cls.push_back(hd[k]);
-                        if ((int)cls.size() > first) ranges.emplace_back(bpp, first);
+                            if (J[k]->state == 1 && hd[k].bpp == bpp) {
+                                for (int g = 0; g < png_unfilter_groups(hd[k].H); ++g)
+                                    groups.push_back(make_int2((int)cls.size() - r.img0, g));
+                                pbase.push_back(band0);
+                                band0 += (hd[k].H + 63) / 64;
+                                cls.push_back(hd[k]);
+                            }
+                        if ((int)cls.size() > r.img0) ranges.push_back(r);
                     }
-                    const size_t cb = sizeof(PngImgDev) * cls.size();
-                    uint8_t* stage = pinned_slot(2, cb);
+                    const size_t gb = up256(sizeof(int2) * ngroups);
+                    uint8_t* stage = pinned_slot(2, gb + sizeof(int) * m + sizeof(PngImgDev) * m);
                     if (!stage) e = hipErrorOutOfMemory;
                     if (e == hipSuccess) {
-                        std::memcpy(stage, cls.data(), cb);
-                        e = hipMemcpyAsync(d_cls, stage, cb, hipMemcpyHostToDevice, s);
+                        std::memcpy(stage, groups.data(), sizeof(int2) * groups.size());
+                        std::memcpy(stage + gb, pbase.data(), sizeof(int) * pbase.size());
+                        e = hipMemcpyAsync(d_unf, stage, unf_tab, hipMemcpyHostToDevice, s);
                     }
+                    unsigned* d_prog = reinterpret_cast<unsigned*>(d_unf + unf_tab);
+                    unsigned* d_ticket = d_prog + nbands;
+                    if (e == hipSuccess) e = hipMemsetAsync(d_prog, 0, unf_zero, s);
+                    uint8_t* cstage = stage ? stage + gb + sizeof(int) * m : nullptr;
+                    if (e == hipSuccess) {
+                        std::memcpy(cstage, cls.data(), sizeof(PngImgDev) * cls.size());
+                        e = hipMemcpyAsync(d_cls, cstage, sizeof(PngImgDev) * cls.size(), hipMemcpyHostToDevice, s);
+                    }
+                    const int2* d_groups = reinterpret_cast<const int2*>(d_unf);
+                    const int* d_pbase = reinterpret_cast<const int*>(d_unf + gb);
                     for (size_t r = 0; r < ranges.size() && e == hipSuccess; ++r) {
-                        const int first = ranges[r].second;
-                        const int cnt = (r + 1 < ranges.size() ? ranges[r + 1].second : (int)cls.size()) - first;
-                        e = launch_png_unfilter(d_cls + first, cnt, ranges[r].first, s);
+                        const int g1 = r + 1 < ranges.size() ? ranges[r + 1].grp0 : (int)groups.size();
+                        const int g0 = ranges[r].grp0, i0 = ranges[r].img0;
+                        e = launch_png_unfilter(d_cls + i0, d_groups + g0, g1 - g0, d_pbase + i0, d_prog,
+                                                d_ticket + r, ranges[r].bpp, s);
                     }
                 }
                 rec(7, s);
@@ -533,9 +571,10 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                 for (int k = 0; k < m; ++k) {
                     PngJob& j = *J[k];
                     if (j.state != 1) continue;
-                    bool ok = herr[k] == 0;
-                    for (size_t i = 0; i < j.lanes.start.size(); ++i, ++t) ok = ok && hxst[2 * t] == 0;
-                    if (!ok) j.state = -1;
+                    const bool rows_ok = herr[k] == 0;
+                    bool lanes_ok = true;
+                    for (size_t i = 0; i < j.lanes.start.size(); ++i, ++t) lanes_ok = lanes_ok && hxst[2 * t] == 0;
+                    if (!rows_ok || !lanes_ok) reject(j, !lanes_ok ? "expand status" : "row filter bytes");
                 }
             }
         }

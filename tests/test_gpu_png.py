@@ -154,6 +154,19 @@ def test_configs1_frame_4096(on_gpu):
     np.testing.assert_array_equal(decode_px(data), img)
 
 
+def test_batch_tall_band_groups(on_gpu):
+    """Unfilter across workgroups: images taller than one 16-band group (1,024
+    rows), so band 16k waits on band 16k-1 of another workgroup; every filter
+    type (rows cycle through 0-4), several bytes-per-pixel classes in one batch,
+    heights off the 64-row band grid."""
+    shapes = [(300, 2500, 4), (517, 1100, 3), (64, 4100, 1), (1000, 1090, 4), (211, 3333, 2), (90, 2049, 4)]
+    imgs = [ikutil.synth(w, h, c, seed=50 + k, pattern="N" if k % 2 else "S") for k, (w, h, c) in enumerate(shapes)]
+    datas = [own_png(im, idat_size=65536) for im in imgs]
+    out = decode_image_batch(datas)
+    for (d, fmt), im in zip(out, imgs):
+        np.testing.assert_array_equal(d.to_array().reshape(im.shape), im)
+
+
 def test_batch_mixed(on_gpu):
     imgs = [ikutil.synth(w, h, c, seed=k) for k, (w, h, c) in
             enumerate([(640, 480, 4), (1024, 768, 3), (333, 222, 1), (2048, 1024, 4), (100, 3000, 2)])]

@@ -131,3 +131,17 @@ def test_corrupt_stream_is_rejected(model):
     if rc == 0:
         with pytest.raises(zlib.error):
             zlib.decompress(bytes(z))
+
+
+def test_deep_marker_chain(model):
+    """A smooth RGBA image with row filters cycling 0-4: long matches carry bytes
+    back through the window of every earlier decoder, so resolving a byte can
+    take more hops than any fixed bound (a byte hops at most once per decoder).
+    It once fell to the host decoder at 64 hops; the bound is now the lane count."""
+    from test_gpu_png import own_png
+    img = ikutil.synth(300, 2500, 4, seed=50, pattern="S")
+    z = _idat(own_png(img, idat_size=65536))
+    raw = zlib.decompress(z)
+    rc, out, st = inflate(model, z, len(raw), 16384)
+    assert rc == 0 and out == raw, st
+    assert st[2] > 64  # more decoders than the old hop bound
