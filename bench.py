@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--hbm-batch", type=int, default=64)
     ap.add_argument("--hbm-steps", type=int, default=6)
     ap.add_argument("--jpeg-images", type=int, default=64)
+    ap.add_argument("--split", type=int, default=1,
+                    help="parts a transform batch runs as at once (IK_BATCH_SPLIT: overlaps one part's host "
+                         "phases with another's kernels)")
     return ap.parse_args()
 
 
@@ -227,6 +230,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     S, O, B = args.size, args.out, args.batch
+    os.environ["IK_BATCH_SPLIT"] = str(args.split)  # read once, when the library first splits a batch
     import ikutil
     frames = [ikutil.synth(S, S, 4, seed=sd, pattern="S") for sd in shard_seeds(rank, args.distinct)]
     pngs = make_pngs(frames)
@@ -292,15 +296,19 @@ def main():
 
     # ---- device kernels of the step: algorithmic bytes per launch ----
     raw = (S * 4 + 1) * S          # filtered image bytes per frame (filter byte + RGBA row)
-    tok = float(st[12])            # u16 tokens the decode pass wrote (whole batch)
+    # the stage times are those of the calling thread's part of the batch (the
+    # library runs a batch as --split parts at once, ik_host.cpp batch_split):
+    # bytes per launch over that part's frames and tokens
+    nd = max(1, int(st[9]))        # frames in the timed decode launch
+    tok = float(st[12])            # u16 tokens its decode pass wrote
     kern = {
         # compressed stream read, tokens written
-        "k_png_decode": (png_stages["decode"], B * in_bytes + 2 * tok),
+        "k_png_decode": (png_stages["decode"], nd * in_bytes + 2 * tok),
         # tokens read, u16 symbols written
-        "k_png_expand": (png_stages["expand"], 2 * tok + B * 2 * raw),
-        "k_png_resolve": (png_stages["resolve"], B * (2 * raw + 4 * S * S)),
-        "k_png_unfilter": (png_stages["unfilter"], B * (2 * 4 * S * S)),
-        "k_png_find": (png_stages["find"], B * in_bytes),
+        "k_png_expand": (png_stages["expand"], 2 * tok + nd * 2 * raw),
+        "k_png_resolve": (png_stages["resolve"], nd * (2 * raw + 4 * S * S)),
+        "k_png_unfilter": (png_stages["unfilter"], nd * (2 * 4 * S * S)),
+        "k_png_find": (png_stages["find"], nd * in_bytes),
     }
     dom = max(kern, key=lambda k: kern[k][0])
     dms, dbytes = kern[dom]
@@ -419,7 +427,7 @@ def main():
                 "workload": f"{S}x{S} RGBA8 synthetic frames as PNG (zlib level 6) in host memory -> "
                             f"ik_transform_batch: decode_image (GPU inflate + unfilter) -> resize_image {O}x{O} "
                             f"({args.filter}) -> encode_image webp q{args.quality} (libwebp) -> WebP bytes in host memory",
-                "batch_per_gpu": B, "filter": args.filter, "format": "webp", "quality": args.quality,
+                "batch_per_gpu": B, "batch_split": args.split, "filter": args.filter, "format": "webp", "quality": args.quality,
                 "host_threads_per_gpu": args.threads, "png_bytes_per_image": in_bytes,
                 "webp_bytes_per_image": out_bytes,
                 "libwebp": "%d.%d.%d" % (lib.ik_libwebp_version() >> 16, (lib.ik_libwebp_version() >> 8) & 255,

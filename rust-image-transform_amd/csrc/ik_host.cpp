@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -817,9 +818,9 @@ namespace ik {
 // ik_transform_batch over the items idx[] of a batch, on the calling thread's
 // device: one batched decode (GPU entropy decoding where the stream allows), then
 // resize_image + encode_image per item on the device's persistent workers.
-static void transform_batch_dev(const uint8_t* const* bytes, const size_t* lens, const std::vector<uint32_t>& idx,
-                                const int64_t* w, const int64_t* h, const int* fmt, const int* quality, int filter,
-                                int threads, uint8_t** outs, size_t* out_lens, int* st, std::string* errs) {
+static void transform_part(const uint8_t* const* bytes, const size_t* lens, const std::vector<uint32_t>& idx,
+                           const int64_t* w, const int64_t* h, const int* fmt, const int* quality, int filter,
+                           int threads, uint8_t** outs, size_t* out_lens, int* st, std::string* errs) {
     const uint32_t m = (uint32_t)idx.size();
     if (!m) return;
     std::vector<const uint8_t*> b(m);
@@ -854,6 +855,49 @@ static void transform_batch_dev(const uint8_t* const* bytes, const size_t* lens,
     if (timing)
         fprintf(stderr, "[transform_batch] %u requests on device %d: resize %.1f ms, encode %.1f ms (summed)\n", m,
                 current_device(), t_resize, t_encode);
+}
+
+// IK_BATCH_SPLIT = P > 1 runs a batch as P parts of at least 8 requests at
+// once, each on its own worker (own stream, staging and device scratch), so that
+// one part's host phases (IDAT staging and CRC, lane planning, libwebp) could
+// overlap another's kernels.  Measured on MI355X (64 PNG frames of 4096^2 ->
+// WebP): 207 ms per batch at P = 1, 249 at 2, 343 at 4 -- the inflate decode
+// kernel takes ~35 ms per part whatever its size (each lane's symbol chain
+// bounds it), so smaller parts only add launches.  Default 1 (one batch).
+static int batch_split() {
+    static const int v = [] {
+        const char* e = getenv("IK_BATCH_SPLIT");
+        const int x = e && *e ? atoi(e) : 1;
+        return x < 1 ? 1 : x > 16 ? 16 : x;
+    }();
+    return v;
+}
+
+static void transform_batch_dev(const uint8_t* const* bytes, const size_t* lens, const std::vector<uint32_t>& idx,
+                                const int64_t* w, const int64_t* h, const int* fmt, const int* quality, int filter,
+                                int threads, uint8_t** outs, size_t* out_lens, int* st, std::string* errs) {
+    const uint32_t m = (uint32_t)idx.size();
+    const int P = (int)std::min<uint32_t>((uint32_t)batch_split(), m / 8);
+    if (P <= 1) {
+        transform_part(bytes, lens, idx, w, h, fmt, quality, filter, threads, outs, out_lens, st, errs);
+        return;
+    }
+    std::vector<std::vector<uint32_t>> parts(P);
+    for (uint32_t k = 0; k < m; ++k) parts[(size_t)k * P / m].push_back(idx[k]);
+    const int part_threads = threads > 0 ? std::max(1, threads / P) : 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int pending = P - 1;
+    Pool& pool = device_pool(current_device());
+    for (int p = 1; p < P; ++p)
+        pool.post([&, p] {
+            transform_part(bytes, lens, parts[p], w, h, fmt, quality, filter, part_threads, outs, out_lens, st, errs);
+            std::lock_guard<std::mutex> lk(mu);
+            if (--pending == 0) cv.notify_all();
+        });
+    transform_part(bytes, lens, parts[0], w, h, fmt, quality, filter, part_threads, outs, out_lens, st, errs);
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return pending == 0; });
 }
 
 }  // namespace ik
