@@ -139,6 +139,17 @@ typedef enum { IK_RESIZE_EXACT = 0, IK_RESIZE_FMA = 1 } ik_resize_mode;
 int ik_set_resize_mode(int mode);
 int ik_get_resize_mode(void);
 
+/* JPEG reconstruction behind decode_image (src/transform.rs:31 -> image 0.25.8
+ * -> zune-jpeg 0.4.21, Cargo.lock:3106).  IK_JPEG_RECON_ZUNE (default): zune-jpeg's
+ * integer IDCT (stb_image-derived, DC-only shortcut), upsampler and i16 YCbCr->RGB,
+ * restated (parity unpinned: no zune-jpeg in this environment).
+ * IK_JPEG_RECON_LIBJPEG: libjpeg-turbo's islow IDCT, fancy upsampling and
+ * jdcolor.c -- bit-exact with Pillow's decoder.  Entropy decoding is the same in
+ * both.  Process-wide; the default also comes from IK_JPEG_RECON=zune|libjpeg. */
+typedef enum { IK_JPEG_RECON_LIBJPEG = 0, IK_JPEG_RECON_ZUNE = 1 } ik_jpeg_recon;
+int ik_set_jpeg_reconstruction(int mode);
+int ik_get_jpeg_reconstruction(void);
+
 /* imageops::resize to exact dimensions (the resampler under resize_image) */
 int ik_resize_exact(const ik_image *img, uint32_t nw, uint32_t nh, int filter, ik_image **out);
 

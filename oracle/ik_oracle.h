@@ -78,6 +78,12 @@ long iko_jpeg_encode_rgb(const uint8_t *rgb, uint32_t w, uint32_t h, int quality
  * natural order), to check the GPU colour-convert+FDCT+quantise kernel. */
 int iko_jpeg_coeffs_rgb(const uint8_t *rgb, uint32_t w, uint32_t h, int quality, int16_t *coef);
 
+/* decode_image on a JPEG (jpeg_dec.c): baseline / progressive, 1, 3 or 4
+ * components -> L8 (c = 1) or RGB8 (c = 3) in *out (malloc'd; free with
+ * iko_free).  mode: the reconstruction restated (see jpeg_dec.c). */
+enum { IKO_JPEG_LIBJPEG = 0, IKO_JPEG_ZUNE = 1 };
+int iko_jpeg_decode(const uint8_t *bytes, size_t n, int mode, uint8_t **out, int *w, int *h, int *c);
+
 /* webp 0.3.1 Encoder::from_rgb(..).encode(q) == libwebp WebPEncodeRGB(rgb,w,h,3w,q)
  * through dlopen("libwebp.so.7").  Returns size, or -1 (library missing). */
 long iko_webp_encode_rgb(const uint8_t *rgb, int w, int h, int stride, float q, uint8_t **out);

@@ -102,7 +102,9 @@ hipError_t launch_jpeg_coeffs(const uint8_t* src, int w, int h, int C, size_t pi
 // colour-convert into the device image.
 struct JpegGeom {
     int ncomp, W, H, hmax, vmax;
-    int colorspace;                 // 0 gray, 1 YCbCr, 2 RGB
+    int colorspace;                 // 0 gray, 1 YCbCr, 2 RGB, 3 CMYK, 4 YCCK (4 components -> RGB8)
+    int adobe;                      // APP14 Adobe present: CMYK / YCCK samples are stored inverted
+    int recon;                      // IK_JPEG_RECON_LIBJPEG / IK_JPEG_RECON_ZUNE (ik_jpeg.hip)
     int h[4], v[4], bw[4], bh[4], dw[4], dh[4];
     long long blk0[4];              // first block of each component in coef
     long long plane0[4];            // byte offset of each component plane (bw*8 x bh*8)

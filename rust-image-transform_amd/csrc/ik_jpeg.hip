@@ -2,16 +2,25 @@
 // src/transform.rs:31 -> image 0.25.8 -> zune-jpeg 0.4.21), fed by the host
 // entropy decoder in ik_jpeg_decode.cpp:
 //
-//   k_jpeg_idct   one lane per 8x8 block: dequantise (coef * qt) and the libjpeg
-//                 jidctint.c "islow" 2-D IDCT with its descale/range-limit, into the
-//                 component's u8 sample plane.
-//   k_jpeg_color  one lane per output pixel: libjpeg(-turbo) "fancy" chroma
-//                 upsampling (h2v1 / h2v2 / h1v2 triangle filters with replicated
-//                 edge context, integer replication otherwise) and jdcolor.c's
-//                 fixed-point YCbCr->RGB, written into the device image.
+//   k_jpeg_idct   one lane per 8x8 block: dequantise (coef * qt) and a 2-D
+//                 integer IDCT into the component's u8 sample plane (MCU-padded).
+//   k_jpeg_color  one lane per output pixel: chroma upsampling and colour
+//                 conversion, written into the device image.
 //
-// All integer arithmetic; results equal libjpeg-turbo's decoder (Pillow) bit for
-// bit on the tests' streams (tests/test_gpu_decode.py).
+// Two reconstructions over the same coefficients (JpegGeom::recon):
+//   IK_JPEG_RECON_ZUNE (default; the reference's decoder) -- zune-jpeg 0.4.21
+//     restated: idct/scalar.rs (stb_image-derived fixed point; a block with 63
+//     zero AC coefficients takes clamp((dc >> 3) + 128)), upsampler/scalar.rs
+//     (separable (3 near + far + 2) >> 2, vertical first, over the MCU-padded
+//     rows), color_convert/scalar.rs (i16: 45/32, 11/32 + 23/32, 113/64).  Parity
+//     unpinned (no zune-jpeg here); equal to the oracle's restatement
+//     (oracle/jpeg_dec.c) bit for bit.
+//   IK_JPEG_RECON_LIBJPEG -- libjpeg-turbo: jidctint.c islow, jdsample.c fancy
+//     upsampling over the real component size, jdcolor.c (SCALEBITS 16); equal to
+//     Pillow's decoder bit for bit (tests/test_gpu_decode.py).
+// CMYK / YCCK (Adobe APP14 transform 0 / 2) convert to RGB8 as Pillow does
+// (inverted Adobe samples, Convert.c cmyk2rgb), in both modes.
+#include "../../include/imagekit_hip.h"
 #include "ik_internal.h"
 
 namespace ik {
@@ -48,6 +57,74 @@ __device__ __forceinline__ Idct8 idct8(int i0, int i1, int i2, int i3, int i4, i
     return {t10 + tmp3, t11 + tmp2, t12 + tmp1, t13 + tmp0, t13 - tmp0, t12 - tmp1, t11 - tmp2, t10 - tmp3};
 }
 
+// zune-jpeg idct_int's butterfly (stb_image stbi__idct_block constants, f2f =
+// (int)(x * 4096 + 0.5)): even part x[0..3] (+ bias), odd part t[0..3]
+__device__ __forceinline__ void zune8(int i0, int i1, int i2, int i3, int i4, int i5, int i6, int i7, int bias,
+                                      int (&x)[4], int (&t)[4]) {
+    int p2 = i2, p3 = i6;
+    int p1 = (p2 + p3) * 2217;
+    int t2 = p1 + p3 * -7567, t3 = p1 + p2 * 3135;
+    int t0 = (i0 + i4) * 4096, t1 = (i0 - i4) * 4096;
+    x[0] = t0 + t3 + bias; x[3] = t0 - t3 + bias; x[1] = t1 + t2 + bias; x[2] = t1 - t2 + bias;
+    t0 = i7; t1 = i5; t2 = i3; t3 = i1;
+    p3 = t0 + t2;
+    int p4 = t1 + t3;
+    p1 = t0 + t3;
+    p2 = t1 + t2;
+    const int p5 = (p3 + p4) * 4816;
+    t0 *= 1223; t1 *= 8410; t2 *= 12586; t3 *= 6149;
+    p1 = p5 + p1 * -3685; p2 = p5 + p2 * -10497; p3 *= -8034; p4 *= -1597;
+    t3 += p1 + p4; t2 += p2 + p3; t1 += p2 + p4; t0 += p1 + p3;
+    t[0] = t0; t[1] = t1; t[2] = t2; t[3] = t3;
+}
+
+__device__ __forceinline__ uint8_t clamp_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+// (x >> 17) clamped to 0..255, as a u32.  The empty asm keeps the shift and the
+// clamp apart: otherwise the compiler fuses pairs of them into gfx950's
+// v_ashr_pk_u8_i32 (16-bit result) and ORs the next two bytes into the same
+// register as if its upper half were zero -- measured on MI355X: bytes 2 and 3 of
+// every packed word came out corrupted.
+__device__ __forceinline__ uint32_t sat17(int x) {
+    int v = x >> 17;
+    asm volatile("" : "+v"(v));
+    return (uint32_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
+// zune-jpeg 0.4.21 idct/scalar.rs idct_int on dequantised coefficients
+__device__ __forceinline__ void idct_zune(const int (&in)[64], uint8_t* out, int pw) {
+    int ac = 0;
+#pragma unroll
+    for (int k = 1; k < 64; ++k) ac |= in[k];
+    if (!ac) {  // "the array has 63 zeroes": (dc >> 3) + 128 everywhere
+        const uint32_t v = clamp_u8((in[0] >> 3) + 128) * 0x01010101u;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) *reinterpret_cast<uint2*>(out + (size_t)r * pw) = make_uint2(v, v);
+        return;
+    }
+    int ws[64];
+    int x[4], t[4];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {  // vertical pass, 2 extra bits kept
+        zune8(in[c], in[8 + c], in[16 + c], in[24 + c], in[32 + c], in[40 + c], in[48 + c], in[56 + c], 512, x, t);
+        ws[c] = (x[0] + t[3]) >> 10; ws[8 + c] = (x[1] + t[2]) >> 10;
+        ws[16 + c] = (x[2] + t[1]) >> 10; ws[24 + c] = (x[3] + t[0]) >> 10;
+        ws[32 + c] = (x[3] - t[0]) >> 10; ws[40 + c] = (x[2] - t[1]) >> 10;
+        ws[48 + c] = (x[1] - t[2]) >> 10; ws[56 + c] = (x[0] - t[3]) >> 10;
+    }
+    constexpr int kScale = 512 + 65536 + (128 << 17);  // SCALE_BITS: rounding + the +128 level shift
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const int* w = ws + r * 8;
+        zune8(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], kScale, x, t);
+        const unsigned lo = sat17(x[0] + t[3]) | (sat17(x[1] + t[2]) << 8) | (sat17(x[2] + t[1]) << 16) |
+                            (sat17(x[3] + t[0]) << 24);
+        const unsigned hi = sat17(x[3] - t[0]) | (sat17(x[2] - t[1]) << 8) | (sat17(x[1] - t[2]) << 16) |
+                            (sat17(x[0] - t[3]) << 24);
+        *reinterpret_cast<uint2*>(out + (size_t)r * pw) = make_uint2(lo, hi);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_jpeg_idct(JpegGeom g) {
     const long long blk = (long long)blockIdx.x * 256 + threadIdx.x;
     if (blk >= g.nblocks) return;
@@ -75,6 +152,10 @@ __global__ __launch_bounds__(256) void k_jpeg_idct(JpegGeom g) {
             in[k] = (int)(int16_t)(w[j] & 0xffff) * (int)q[k];
             in[k + 1] = (int)(int16_t)((unsigned)w[j] >> 16) * (int)q[k + 1];
         }
+    }
+    if (g.recon == IK_JPEG_RECON_ZUNE) {
+        idct_zune(in, out, pw);
+        return;
     }
     // pass 1: columns -> ws (scaled by 2^PASS1_BITS)
     int ws[64];
@@ -159,31 +240,88 @@ __device__ __forceinline__ int upsampled(const JpegGeom& g, int ci, int x, int y
     return row(ys / fv)[xs / fh];  // int_upsample: replication
 }
 
+// zune-jpeg 0.4.21 upsampler/scalar.rs at output pixel (x, y): over the whole
+// MCU-padded plane (n = bw * 8 samples per row, bh * 8 rows), rows above / below
+// replicated at the padded edges; h2v2 = upsample_vertical into i16, then
+// upsample_horizontal on that row
+__device__ __forceinline__ int upsampled_zune(const JpegGeom& g, int ci, int x, int y) {
+    const int fh = g.hmax / g.h[ci], fv = g.vmax / g.v[ci];
+    const int n = g.bw[ci] * 8, ph = g.bh[ci] * 8;
+    const uint8_t* p = g.planes + g.plane0[ci];
+    auto row = [&](int r) { return p + (size_t)(r < 0 ? 0 : (r >= ph ? ph - 1 : r)) * n; };
+    if (fh == 1 && fv == 1) return row(y)[x];
+    if (fh == 1 && fv == 2) {
+        const int Y = y >> 1;
+        return (row(Y)[x] * 3 + row((y & 1) ? Y + 1 : Y - 1)[x] + 2) >> 2;
+    }
+    if (fh == 2 && (fv == 1 || fv == 2)) {
+        const uint8_t* i0 = row(fv == 2 ? y >> 1 : y);
+        const uint8_t* i1 = fv == 2 ? row((y & 1) ? (y >> 1) + 1 : (y >> 1) - 1) : i0;
+        // the (vertically upsampled) sample k of the row
+        auto at = [&](int k) { return fv == 2 ? (i0[k] * 3 + i1[k] + 2) >> 2 : (int)i0[k]; };
+        const int i = x >> 1;
+        if (x == 0) return at(0);
+        if (x == 1) return (at(0) * 3 + at(1) + 2) >> 2;
+        if (x == 2 * n - 2) return (at(n - 2) * 3 + at(n - 1) + 2) >> 2;
+        if (x == 2 * n - 1) return at(n - 1);
+        return (x & 1) ? (at(i) * 3 + at(i + 1) + 2) >> 2 : (at(i) * 3 + at(i - 1) + 2) >> 2;
+    }
+    return row(y / fv)[x / fh];  // upsample_generic: replication
+}
+
 __device__ __forceinline__ uint8_t clamp255(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+// Pillow Convert.c MULDIV255
+__device__ __forceinline__ int muldiv255(int a, int b) {
+    const int t = a * b + 128;
+    return ((t >> 8) + t) >> 8;
+}
 
 __global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restrict__ dst, size_t pitch) {
     const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
     if (x >= g.W) return;
+    const bool zune = g.recon == IK_JPEG_RECON_ZUNE;
+    auto sample = [&](int ci) { return zune ? upsampled_zune(g, ci, x, y) : upsampled(g, ci, x, y); };
     uint8_t* o = dst + (size_t)y * pitch;
     if (g.colorspace == 0) {
-        o[x] = (uint8_t)upsampled(g, 0, x, y);
+        o[x] = (uint8_t)sample(0);
         return;
     }
-    const int c0 = upsampled(g, 0, x, y), c1 = upsampled(g, 1, x, y), c2 = upsampled(g, 2, x, y);
-    uint8_t r, gg, b;
-    if (g.colorspace == 2) {
-        r = (uint8_t)c0; gg = (uint8_t)c1; b = (uint8_t)c2;
+    const int c0 = sample(0), c1 = sample(1), c2 = sample(2);
+    int r, gg, b;
+    if (g.colorspace == 2 || g.colorspace == 3) {
+        r = c0; gg = c1; b = c2;
+    } else if (zune) {
+        // color_convert/scalar.rs ycbcr_to_rgb_inner_16_scalar, i16 arithmetic
+        const int16_t cb = (int16_t)(c1 - 128), cr = (int16_t)(c2 - 128);
+        r = c0 + ((int16_t)(45 * cr) >> 5);
+        gg = c0 - ((int16_t)(11 * cb + 23 * cr) >> 5);
+        b = c0 + ((int16_t)(113 * cb) >> 6);
     } else {
         // jdcolor.c ycc_rgb_convert, SCALEBITS 16: FIX(1.402) 91881, FIX(1.772) 116130,
         // FIX(0.71414) 46802, FIX(0.34414) 22554
         const int cb = c1 - 128, cr = c2 - 128;
-        r = clamp255(c0 + ((91881 * cr + 32768) >> 16));
-        gg = clamp255(c0 + ((-22554 * cb + 32768 - 46802 * cr) >> 16));
-        b = clamp255(c0 + ((116130 * cb + 32768) >> 16));
+        r = c0 + ((91881 * cr + 32768) >> 16);
+        gg = c0 + ((-22554 * cb + 32768 - 46802 * cr) >> 16);
+        b = c0 + ((116130 * cb + 32768) >> 16);
     }
-    o[3 * x] = r;
-    o[3 * x + 1] = gg;
-    o[3 * x + 2] = b;
+    if (g.colorspace < 3) {
+        o[3 * x] = clamp255(r);
+        o[3 * x + 1] = clamp255(gg);
+        o[3 * x + 2] = clamp255(b);
+        return;
+    }
+    // CMYK / YCCK -> RGB8: YCCK's YCbCr part gives inverted C, M, Y (jdcolor.c
+    // ycck_cmyk_convert); Adobe samples are inverted (Pillow rawmode "CMYK;I");
+    // then Pillow Convert.c cmyk2rgb
+    int cc = r, mm = gg, yy = b;
+    if (g.colorspace == 4) { cc = 255 - clamp255(r); mm = 255 - clamp255(gg); yy = 255 - clamp255(b); }
+    int k = sample(3);
+    if (g.adobe) { cc = 255 - cc; mm = 255 - mm; yy = 255 - yy; k = 255 - k; }
+    const int nk = 255 - k;
+    o[3 * x] = clamp255(nk - muldiv255(cc, nk));
+    o[3 * x + 1] = clamp255(nk - muldiv255(mm, nk));
+    o[3 * x + 2] = clamp255(nk - muldiv255(yy, nk));
 }
 
 }  // namespace

@@ -5,14 +5,14 @@
 // block-coefficient image (quantised int16, natural order, one plane of 8x8
 // blocks per component): baseline sequential (SOF0/SOF1, interleaved or not) and
 // progressive (SOF2: DC first/refine, AC first/refine with EOB runs), restart
-// intervals, 8-bit, 1 (gray -> L8) or 3 components (YCbCr -> Rgb8, or RGB for
-// Adobe transform 0).  Reconstruction -- dequantise, islow IDCT, fancy chroma
-// upsampling, YCbCr->RGB -- runs on the GPU (ik_jpeg.hip) straight into the
-// device image.  zune-jpeg's output cannot be checked offline (no crate
-// sources), so reconstruction follows the libjpeg pipeline zune-jpeg aims to
-// match; parity is pinned against libjpeg-turbo (Pillow) in tests/test_gpu_decode.py.
-// Arithmetic-coded, lossless, hierarchical, 12-bit and CMYK JPEGs report
-// IK_ERR_UNSUPPORTED.
+// intervals, 8-bit, 1 (gray -> L8), 3 (YCbCr -> Rgb8, or RGB for Adobe
+// transform 0) or 4 components (CMYK / YCCK -> Rgb8).  Reconstruction --
+// dequantise, IDCT, chroma upsampling, colour conversion -- runs on the GPU
+// (ik_jpeg.hip) straight into the device image, by default as zune-jpeg 0.4.21
+// does it (restated, parity unpinned: no crate sources or outputs here; equal to
+// oracle/jpeg_dec.c), or as libjpeg-turbo does (bit-exact with Pillow) --
+// ik_set_jpeg_reconstruction.  Arithmetic-coded, lossless, hierarchical and
+// 12-bit JPEGs report IK_ERR_UNSUPPORTED.
 #include <algorithm>
 #include <thread>
 #include <memory>
@@ -177,7 +177,8 @@ struct Decoder {
         width = (int)s[3] << 8 | s[4];
         const int nc = s[5];
         if (!width || !height) return fail(IK_ERR_TRANSFORM, "%s: zero dimension", kFmtErr);
-        if (nc != 1 && nc != 3) return fail(IK_ERR_UNSUPPORTED, "JPEG with %d components is not supported", nc);
+        if (nc != 1 && nc != 3 && nc != 4)
+            return fail(IK_ERR_UNSUPPORTED, "JPEG with %d components is not supported", nc);
         // image's default Limits: max_alloc 512 MiB of decoded bytes (L8: 1 per pixel, Rgb8: 3)
         if ((uint64_t)width * height * (nc == 1 ? 1u : 3u) > (512ull << 20))
             return fail(IK_ERR_TRANSFORM, "Limits are exceeded");
@@ -576,7 +577,21 @@ struct Decoder {
 
 }  // namespace
 
+std::atomic<int> g_jpeg_recon{-1};  // -1: not yet read from IK_JPEG_RECON
+
 namespace {
+
+int jpeg_recon() {
+    int m = g_jpeg_recon.load();
+    if (m < 0) {
+        const char* e = getenv("IK_JPEG_RECON");
+        m = e && !strcmp(e, "libjpeg") ? IK_JPEG_RECON_LIBJPEG : IK_JPEG_RECON_ZUNE;
+        int expected = -1;
+        g_jpeg_recon.compare_exchange_strong(expected, m);
+        m = g_jpeg_recon.load();
+    }
+    return m;
+}
 
 // reconstruction geometry of a parsed stream; returns the plane bytes it needs
 size_t make_geom(const Decoder& d, JpegGeom& g) {
@@ -584,7 +599,10 @@ size_t make_geom(const Decoder& d, JpegGeom& g) {
     int colorspace = nc == 1 ? 0 : 1;  // gray / YCbCr
     if (nc == 3 && d.adobe && d.adobe_transform == 0) colorspace = 2;  // Adobe RGB-coded
     if (nc == 3 && !d.adobe && d.comps[0].id == 'R' && d.comps[1].id == 'G' && d.comps[2].id == 'B') colorspace = 2;
+    if (nc == 4) colorspace = d.adobe && d.adobe_transform == 2 ? 4 : 3;  // YCCK / CMYK
     g = JpegGeom{};
+    g.adobe = d.adobe ? 1 : 0;
+    g.recon = jpeg_recon();
     g.ncomp = nc;
     g.W = d.width;
     g.H = d.height;
@@ -1079,3 +1097,21 @@ int decode_jpeg_device(const uint8_t* bytes, size_t n, ik_image** out) {
 }
 
 }  // namespace ik
+
+namespace ik {
+int jpeg_recon_mode() { return jpeg_recon(); }
+}  // namespace ik
+
+extern "C" {
+
+int ik_set_jpeg_reconstruction(int mode) {
+    if (mode != IK_JPEG_RECON_LIBJPEG && mode != IK_JPEG_RECON_ZUNE)
+        return ik::fail(IK_ERR_INVALID, "bad JPEG reconstruction mode %d", mode);
+    (void)ik::jpeg_recon_mode();
+    ik::g_jpeg_recon.store(mode);
+    return IK_OK;
+}
+
+int ik_get_jpeg_reconstruction(void) { return ik::jpeg_recon_mode(); }
+
+}  // extern "C"

@@ -57,6 +57,8 @@ SIGNATURES = [
     ("ik_png_last_timing", ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     ("ik_png_counters", ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
     ("ik_get_resize_mode", ctypes.c_int, []),
+    ("ik_set_jpeg_reconstruction", ctypes.c_int, [ctypes.c_int]),
+    ("ik_get_jpeg_reconstruction", ctypes.c_int, []),
     ("ik_pipeline_submit", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint32]),
     ("ik_pipeline_collect", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_uint32)]),
     ("ik_pipeline_run_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint32]),

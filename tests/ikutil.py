@@ -117,6 +117,26 @@ class Oracle:
         self.lib.iko_jpeg_coeffs_rgb(_p(rgb), w, h, q, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)))
         return out
 
+    JPEG_LIBJPEG, JPEG_ZUNE = 0, 1
+
+    def jpeg_decode(self, data: bytes, mode: int = 1) -> np.ndarray:
+        """decode_image on a JPEG (oracle/jpeg_dec.c): mode 1 = zune-jpeg 0.4.21
+        restatement (the reference's decoder), 0 = libjpeg-turbo restatement.
+        Returns (h, w, 3) RGB8 or (h, w, 1) L8."""
+        out = u8p()
+        w, h, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self.lib.iko_jpeg_decode.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(u8p),
+                                             ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                             ctypes.POINTER(ctypes.c_int)]
+        rc = self.lib.iko_jpeg_decode(data, len(data), mode, ctypes.byref(out), ctypes.byref(w), ctypes.byref(h),
+                                      ctypes.byref(c))
+        if rc != 0:
+            raise ValueError("oracle: cannot decode this JPEG")
+        a = np.frombuffer(ctypes.string_at(out, w.value * h.value * c.value), np.uint8).reshape(h.value, w.value,
+                                                                                                   c.value).copy()
+        self.lib.iko_free(out)
+        return a
+
     def transform(self, img: np.ndarray, w, h, f: int, fmt: int, q: int):
         img = np.ascontiguousarray(img)
         H, W, C = img.shape

@@ -1,11 +1,12 @@
 """GPU: decode_image (reference src/transform.rs:27-43) through ik_decode.
 
-JPEG: the decoder follows libjpeg's reconstruction (islow IDCT, fancy
-upsampling, fixed-point YCbCr) and must equal libjpeg-turbo (Pillow) bit for bit.
-zune-jpeg itself (the reference's decoder) is not available: parity against it
-is unpinned.  PNG: decoding is specified exactly; checked against Pillow/libpng
-and against the source pixels, across colour types, bit depths, the five
-filter types and Adam7 (a small PNG writer below produces those).
+JPEG, in the libjpeg-turbo reconstruction mode (ik_set_jpeg_reconstruction(
+IK_JPEG_RECON_LIBJPEG): islow IDCT, fancy upsampling, fixed-point YCbCr) for the
+whole module: must equal libjpeg-turbo (Pillow) bit for bit, which pins the
+entropy decoding the default zune-jpeg mode shares (that mode:
+tests/test_gpu_jpeg_zune.py).  PNG: decoding is specified exactly; checked
+against Pillow/libpng and against the source pixels, across colour types, bit
+depths, the five filter types and Adam7 (a small PNG writer below produces those).
 """
 import io
 import struct
@@ -19,6 +20,15 @@ import ikutil
 from imagekit import ImageFormat, TransformError, decode_image
 
 pytestmark = pytest.mark.gpu
+
+IK_JPEG_RECON_LIBJPEG, IK_JPEG_RECON_ZUNE = 0, 1
+
+
+@pytest.fixture(autouse=True, scope="module")
+def libjpeg_reconstruction(ik):
+    assert ik.ik_set_jpeg_reconstruction(IK_JPEG_RECON_LIBJPEG) == 0
+    yield
+    assert ik.ik_set_jpeg_reconstruction(IK_JPEG_RECON_ZUNE) == 0
 
 
 def _jpeg(img, **kw):
@@ -366,7 +376,7 @@ def test_jpeg_seq_opt_in_is_correct():
         "    assert np.array_equal(img.to_array(), np.asarray(Image.open(io.BytesIO(b)))), k\n"
         "print('ok')\n")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, IK_JPEG_SEQ="1"),
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, IK_JPEG_SEQ="1", IK_JPEG_RECON="libjpeg"),
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
