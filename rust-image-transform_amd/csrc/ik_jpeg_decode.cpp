@@ -385,7 +385,11 @@ struct Decoder {
             break;  // a marker: the scan ends (the host feeds zeros from here)
         }
         if (clean.size() < kSeqMinBytes) return false;
-        const size_t nw = (clean.size() + 3) / 4 + 4;  // zero words past the end
+        // zero words past the end: a decoder (the GPU lanes, the host frontier walk)
+        // may start a block just before nbits and read one whole block of zero bits
+        // from there, at most 16 + 11 + 63 (16 + 10) bits, plus peek32's next word
+        constexpr size_t kSeqPadWords = (16 + 11 + 63 * (16 + 10) + 31) / 32 + 2;
+        const size_t nw = (clean.size() + 3) / 4 + kSeqPadWords;
         seq_words.assign(nw, 0u);
         for (size_t i = 0; i < clean.size(); ++i) seq_words[i >> 2] |= (uint32_t)clean[i] << (24 - 8 * (i & 3));
         a.nbits = (long long)clean.size() * 8;
