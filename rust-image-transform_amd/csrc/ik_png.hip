@@ -25,6 +25,8 @@
 //                   first row reads the previous band's last row from memory once
 //                   it is published (global progress counters, agent-scope
 //                   release/acquire; workgroups ordered by a start ticket).
+#include <type_traits>
+
 #include "ik_inflate.h"
 #include "ik_internal.h"
 #include "ik_png.h"
@@ -386,6 +388,21 @@ __global__ __launch_bounds__(64) void k_png_expand(const PngImgDev* imgs, const 
             }
         }
         if (__ballot(bad)) { bad = true; break; }
+        // every symbol of the batch one literal (the common case on poorly
+        // compressible data): lane x holds output position x, nothing to resolve
+        if (!__ballot(x < (int)n && !(info & 0x80000000u))) {
+            const uint16_t v = (uint16_t)(info & 0xFFu);
+            const uint32_t t2 = t + n;
+            u = t2 + x < ntok ? (uint32_t)T[t2 + x] : kTokPad;
+            un = t2 + x + 1 < ntok ? (uint32_t)T[t2 + x + 1] : 0u;
+            if (x < (int)n) {
+                s_ring[(cnt + (uint32_t)x) & (kXRing - 1)] = v;
+                out[(int64_t)cnt + x] = v;
+            }
+            cnt += n;
+            t = t2;
+            continue;
+        }
         uint32_t tot;
         uint32_t off = wave_excl_scan(len, &tot);
         if (tot > (uint32_t)kXCap) {  // cut the batch before the first symbol that does not fit
@@ -402,12 +419,14 @@ __global__ __launch_bounds__(64) void k_png_expand(const PngImgDev* imgs, const 
         u = t2 + x < ntok ? (uint32_t)T[t2 + x] : kTokPad;
         un = t2 + x + 1 < ntok ? (uint32_t)T[t2 + x + 1] : 0u;
         __syncthreads();
-        // resolve this thread's positions q = x + 64 k, kXGroup of them at a time
-        for (uint32_t g0 = 0; g0 < tot; g0 += 64 * kXGroup) {
-            int sl[kXGroup];
-            uint32_t qk[kXGroup];
+        // resolve this thread's positions q = x + 64 k, K of them at a time (one
+        // when the batch holds at most 64 symbols)
+        auto resolve = [&](auto kc, uint32_t g0) {
+            constexpr int K = decltype(kc)::value;
+            int sl[K];
+            uint32_t qk[K];
 #pragma unroll
-            for (int k = 0; k < kXGroup; ++k) {
+            for (int k = 0; k < K; ++k) {
                 qk[k] = g0 + (uint32_t)x + 64u * k;
                 sl[k] = 0;
             }
@@ -415,12 +434,12 @@ __global__ __launch_bounds__(64) void k_png_expand(const PngImgDev* imgs, const 
 #pragma unroll
             for (int st = 32; st >= 1; st >>= 1)
 #pragma unroll
-                for (int k = 0; k < kXGroup; ++k)
+                for (int k = 0; k < K; ++k)
                     if (s_end[sl[k] + st - 1] <= qk[k]) sl[k] += st;
-            uint16_t val[kXGroup];
-            int64_t gsrc[kXGroup];  // >= 0: read from memory at out[gsrc]
+            uint16_t val[K];
+            int64_t gsrc[K];  // >= 0: read from memory at out[gsrc]
 #pragma unroll
-            for (int k = 0; k < kXGroup; ++k) {
+            for (int k = 0; k < K; ++k) {
                 val[k] = 0;
                 gsrc[k] = -1;
                 if (qk[k] >= tot) continue;
@@ -454,15 +473,20 @@ __global__ __launch_bounds__(64) void k_png_expand(const PngImgDev* imgs, const 
                 }
             }
 #pragma unroll
-            for (int k = 0; k < kXGroup; ++k)
+            for (int k = 0; k < K; ++k)
                 if (gsrc[k] >= 0) val[k] = out[gsrc[k]];
             // (ring slots written here held positions older than any this batch reads)
 #pragma unroll
-            for (int k = 0; k < kXGroup; ++k)
+            for (int k = 0; k < K; ++k)
                 if (qk[k] < tot) {
                     s_ring[(cnt + qk[k]) & (kXRing - 1)] = val[k];
                     out[(int64_t)cnt + qk[k]] = val[k];
                 }
+        };
+        if (tot <= 64u) {
+            resolve(std::integral_constant<int, 1>{}, 0u);
+        } else {
+            for (uint32_t g0 = 0; g0 < tot; g0 += 64 * kXGroup) resolve(std::integral_constant<int, kXGroup>{}, g0);
         }
         __syncthreads();
         cnt += tot;
