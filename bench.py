@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--hbm-batch", type=int, default=64)
     ap.add_argument("--hbm-steps", type=int, default=6)
     ap.add_argument("--jpeg-images", type=int, default=64)
+    ap.add_argument("--clients", type=int, default=1,
+                    help="client threads calling ik_transform_batch at once, each on its own batch (a server's "
+                         "concurrent requests): one batch's host phases overlap another's kernels")
     ap.add_argument("--split", type=int, default=1,
                     help="parts a transform batch runs as at once (IK_BATCH_SPLIT: overlaps one part's host "
                          "phases with another's kernels)")
@@ -258,25 +261,58 @@ def main():
     f = FILTERS[args.filter]
 
     # ---- headline: PNG bytes in host memory -> WebP bytes in host memory ----
-    timing = (ctypes.c_double * 13)()
     stage_ms = []
 
     def step():
         res = transform_batch(reqs, [(O, O)] * B, [FORMATS["webp"]] * B, [args.quality] * B, filter=f,
-                              threads=args.threads)
+                              threads=max(1, args.threads // args.clients))
+        timing = (ctypes.c_double * 13)()  # this thread's last decode (thread-local in the library)
         lib.ik_png_last_timing(timing, 13)
         stage_ms.append(list(timing))
         return res
 
-    for _ in range(args.warmup):
-        step()
+    C = max(1, args.clients)
+    results = [None] * C
+    errors = []
+
+    def client(ci, nsteps, warm):
+        # one client: its own thread, so its own HIP stream, pinned staging and scratch
+        try:
+            if lib.ik_init(local) != 0:
+                raise RuntimeError(_lib.last_error())
+            for _ in range(warm):
+                step()
+            for _ in range(nsteps):
+                results[ci] = step()
+        except Exception as e:  # reported on the main thread
+            errors.append(e)
+
+    def run_clients(total, warm):
+        per = [total // C + (1 if c < total % C else 0) for c in range(C)]
+        th = [threading.Thread(target=client, args=(c, per[c], warm)) for c in range(C)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errors:
+            raise SystemExit(f"transform_batch failed: {errors[0]}")
+
+    if C == 1:
+        for _ in range(args.warmup):
+            step()
+    else:
+        run_clients(0, args.warmup)
     stage_ms.clear()
     cnt0 = (ctypes.c_ulonglong * 2)()
     lib.ik_png_counters(cnt0)
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res = step()
+    if C == 1:
+        for _ in range(args.steps):
+            res = step()
+    else:
+        run_clients(args.steps, 0)
+        res = next(r for r in results if r is not None)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     barrier()
@@ -427,7 +463,7 @@ def main():
                 "workload": f"{S}x{S} RGBA8 synthetic frames as PNG (zlib level 6) in host memory -> "
                             f"ik_transform_batch: decode_image (GPU inflate + unfilter) -> resize_image {O}x{O} "
                             f"({args.filter}) -> encode_image webp q{args.quality} (libwebp) -> WebP bytes in host memory",
-                "batch_per_gpu": B, "batch_split": args.split, "filter": args.filter, "format": "webp", "quality": args.quality,
+                "batch_per_gpu": B, "batch_split": args.split, "clients": C, "filter": args.filter, "format": "webp", "quality": args.quality,
                 "host_threads_per_gpu": args.threads, "png_bytes_per_image": in_bytes,
                 "webp_bytes_per_image": out_bytes,
                 "libwebp": "%d.%d.%d" % (lib.ik_libwebp_version() >> 16, (lib.ik_libwebp_version() >> 8) & 255,
