@@ -50,7 +50,7 @@ METRIC = "transform MPix/s (decode+resize+encode) 4096²→512² WebP q80; 1/2/4
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FILTERS = {"nearest": 0, "triangle": 1, "catmullrom": 2, "gaussian": 3, "lanczos3": 4}
 FORMATS = {"jpeg": 0, "webp": 1, "avif": 2}
-PNG_STAGES = ["host_parse_stage", "find", "decode", "expand", "resolve", "unfilter"]
+PNG_STAGES = ["host_parse_stage", "upload_find", "decode", "expand", "resolve", "unfilter"]
 
 
 def parse():
@@ -344,7 +344,6 @@ def main():
         "k_png_expand": (png_stages["expand"], 2 * tok + nd * 2 * raw),
         "k_png_resolve": (png_stages["resolve"], nd * (2 * raw + 4 * S * S)),
         "k_png_unfilter": (png_stages["unfilter"], nd * (2 * 4 * S * S)),
-        "k_png_find": (png_stages["find"], nd * in_bytes),
     }
     dom = max(kern, key=lambda k: kern[k][0])
     dms, dbytes = kern[dom]

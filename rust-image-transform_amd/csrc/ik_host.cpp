@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <tuple>
 #include <condition_variable>
 #include <mutex>
 #include <string>
@@ -75,7 +76,7 @@ struct Arena {
     int device = 0;
 };
 struct ThreadRes {
-    std::map<int, hipStream_t> streams;
+    std::map<int, hipStream_t> streams, copy_streams;
     std::map<std::pair<int, int>, Arena> dev;  // (device, slot)
     Arena pinned[4];
     ~ThreadRes() {
@@ -89,6 +90,7 @@ struct ThreadRes {
         for (Arena& a : pinned)
             if (a.p) (void)hipHostFree(a.p);
         for (auto& kv : streams) (void)hipStreamDestroy(kv.second);
+        for (auto& kv : copy_streams) (void)hipStreamDestroy(kv.second);
     }
 };
 ThreadRes& tres() {
@@ -109,11 +111,25 @@ hipStream_t thread_stream() {
     return s;
 }
 
+hipStream_t thread_copy_stream() {
+    ThreadRes& r = tres();
+    const int d = current_device();
+    auto it = r.copy_streams.find(d);
+    if (it != r.copy_streams.end()) return it->second;
+    (void)hipSetDevice(d);
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    r.copy_streams[d] = s;
+    return s;
+}
+
 uint8_t* pinned_slot(int slot, size_t bytes) {
     Arena& a = tres().pinned[slot];
     if (bytes <= a.cap) return a.p;
     if (a.p) {
         (void)hipStreamSynchronize(thread_stream());  // no copy may still read the old buffer
+        auto cs = tres().copy_streams.find(current_device());
+        if (cs != tres().copy_streams.end()) (void)hipStreamSynchronize(cs->second);
         (void)hipHostFree(a.p);
     }
     a.p = nullptr;
@@ -194,7 +210,10 @@ size_t pitch_for(uint32_t w, uint32_t c) { return ((size_t)w * c + 255) & ~size_
 // that fits in it; every API call has synchronised its own stream before it
 // returns, so a block is idle when it comes back.
 namespace {
-constexpr size_t kPoolBytes = size_t(4) << 30;
+// 32 GiB of the 288 GB: two 64-frame 4096^2 batches in flight hold 8 GiB of decoded
+// frames; at 4 GiB the pool overflowed every batch, and each hipFree of an
+// overflowing block stalled the whole device (and every concurrent batch)
+constexpr size_t kPoolBytes = size_t(32) << 30;
 struct ImagePool {
     std::mutex mu;
     std::multimap<size_t, uint8_t*> free_blocks;
@@ -297,9 +316,14 @@ const DeviceConsts* device_consts(int device) {
 // those planes on the host.  JPEG: to_rgb8 + YCbCr + FDCT + quantise on the GPU,
 // baseline Huffman coding on the host.  AVIF: to_rgba8 + YCbCr 4:4:4 on the GPU,
 // AV1 coding by libavif/aom on the host.
-int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, size_t pitch,
-                        int fmt, int quality, std::vector<uint8_t>& out) {
+int encode_device_front(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, size_t pitch, int fmt, int quality,
+                        EncodePrep& p, std::vector<uint8_t>& out) {
     const int q = quality < 1 ? 1 : (quality > 100 ? 100 : quality);
+    p.fmt = fmt;
+    p.q = q;
+    p.w = w;
+    p.h = h;
+    p.done = true;  // unless a host coder is left to run (encode_host_back)
     hipStream_t s = thread_stream();
     if (!s) return fail(IK_ERR_DEVICE, "cannot create HIP stream");
     if (fmt == IK_FORMAT_WEBP) {
@@ -310,16 +334,13 @@ int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, 
         const size_t bytes = (size_t)w * h + 2 * uvw * uvh;
         uint8_t* dyuv = scratch(bytes);
         if (!dyuv) return fail(IK_ERR_DEVICE, "cannot allocate device scratch");
-        std::vector<uint8_t> yuv(bytes);
         hipError_t e = launch_webp_yuv420(dev, (int)w, (int)h, (int)c, pitch, 0, dyuv, 0, 1,
                                           dc->gamma_to_lin, dc->lin_to_gamma, s);
         if (e != hipSuccess) return hip_fail(e, "webp yuv420");
         if (default_webp_encoder() == IK_WEBP_GPU) return webp_encode_gpu(dyuv, (int)w, (int)h, q, out);
-        int rc = copy_d2h_2d(yuv.data(), bytes, dyuv, bytes, bytes, 1, s);
-        if (rc) return rc;
-        const uint8_t* Y = yuv.data();
-        return webp_encode_yuv420(Y, Y + (size_t)w * h, Y + (size_t)w * h + uvw * uvh, (int)w, (int)h,
-                                  (float)q, out);
+        p.planes.resize(bytes);
+        p.done = false;  // libwebp's VP8 coding of the planes: encode_host_back
+        return copy_d2h_2d(p.planes.data(), bytes, dyuv, bytes, bytes, 1, s);
     }
     if (fmt == IK_FORMAT_JPEG) {
         if (w > 65535 || h > 65535) return fail(IK_ERR_TRANSFORM, "JPEG dimensions %ux%u exceed 65535", w, h);
@@ -381,14 +402,55 @@ int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, 
         int* dflag = reinterpret_cast<int*>(dp + 4 * n + 128 - ((4 * n) & 127));
         hipError_t e = launch_avif_yuv444(dev, (int)w, (int)h, (int)c, pitch, 0, dp, 0, dflag, 1, s);
         if (e != hipSuccess) return hip_fail(e, "avif yuv444");
-        std::vector<uint8_t> planes(4 * n);
+        p.planes.resize(4 * n);
         int transparent = 0;
-        int rc = copy_d2h_2d(planes.data(), 4 * n, dp, 4 * n, 4 * n, 1, s);
+        int rc = copy_d2h_2d(p.planes.data(), 4 * n, dp, 4 * n, 4 * n, 1, s);
         if (!rc) rc = copy_d2h_2d(reinterpret_cast<uint8_t*>(&transparent), 4, reinterpret_cast<const uint8_t*>(dflag), 4, 4, 1, s);
         if (rc) return rc;
-        return avif_encode_yuv444(planes.data(), transparent != 0, (int)w, (int)h, q, 4, out);
+        p.transparent = transparent != 0;
+        p.done = false;  // AV1 coding by libavif: encode_host_back
+        return IK_OK;
     }
     return fail(IK_ERR_INVALID, "unknown ImageFormat %d", fmt);
+}
+
+int encode_host_back(EncodePrep& p, std::vector<uint8_t>& out) {
+    if (p.done) return IK_OK;
+    p.done = true;
+    if (p.fmt == IK_FORMAT_WEBP) {
+        const size_t uvw = (p.w + 1) / 2, uvh = (p.h + 1) / 2;
+        const uint8_t* Y = p.planes.data();
+        return webp_encode_yuv420(Y, Y + (size_t)p.w * p.h, Y + (size_t)p.w * p.h + uvw * uvh, (int)p.w, (int)p.h,
+                                  (float)p.q, out);
+    }
+    if (p.fmt == IK_FORMAT_AVIF) return avif_encode_yuv444(p.planes.data(), p.transparent, (int)p.w, (int)p.h, p.q, 4, out);
+    return fail(IK_ERR_INVALID, "unknown ImageFormat %d", p.fmt);
+}
+
+int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, size_t pitch, int fmt, int quality,
+                        std::vector<uint8_t>& out) {
+    EncodePrep p;
+    const int rc = encode_device_front(dev, w, h, c, pitch, fmt, quality, p, out);
+    return rc ? rc : encode_host_back(p, out);
+}
+
+// the front half of ik_encode on a handle (u16 images are rescaled to u8 first,
+// as to_rgb8 / to_rgba8 do)
+int encode_image_front(const ik_image* img, int fmt, int quality, EncodePrep& p, std::vector<uint8_t>& out) {
+    if (!img) return fail(IK_ERR_INVALID, "null pointer");
+    if (img->w == 0 || img->h == 0) return fail(IK_ERR_TRANSFORM, "cannot encode an empty image");
+    DeviceGuard g(img->device);
+    if (img->depth != 2) return encode_device_front(img->d, img->w, img->h, img->c, img->pitch, fmt, quality, p, out);
+    ik_image* u8 = nullptr;
+    int st = alloc_image(img->w, img->h, img->c, &u8);
+    if (st) return st;
+    hipError_t e = launch_u16_to_u8(img->d, img->pitch, u8->d, u8->pitch, (int)(img->w * img->c), (int)img->h,
+                                    thread_stream());
+    st = e == hipSuccess ? encode_device_front(u8->d, u8->w, u8->h, u8->c, u8->pitch, fmt, quality, p, out)
+                         : hip_fail(e, "u16 -> u8");
+    if (e == hipSuccess && !st) (void)hipStreamSynchronize(thread_stream());  // u8 is read before it is freed
+    ik_image_free(u8);
+    return st;
 }
 
 }  // namespace ik
@@ -593,51 +655,99 @@ static uint32_t f32_as_u32(float v) {
     return (uint32_t)v;
 }
 
+}  // extern "C"
+
+namespace ik {
+
+// The output size of src/transform.rs:62-90 + DynamicImage::resize for a w x h
+// image and the request's (w, h) options (-1 = None; not both None)
+int resize_target(uint32_t W, uint32_t H, int64_t w, int64_t h, uint32_t* onw, uint32_t* onh) {
+    if (w > 0xFFFFFFFFll || h > 0xFFFFFFFFll) return fail(IK_ERR_INVALID, "dimension exceeds u32");
+    uint32_t tw, th;
+    if (w >= 0) tw = (uint32_t)w;
+    else tw = f32_as_u32(roundf((float)W * ((float)(uint32_t)h / (float)H)));
+    if (h >= 0) th = (uint32_t)h;
+    else th = f32_as_u32(roundf((float)H * ((float)(uint32_t)w / (float)W)));
+    if (tw < 1) tw = 1;
+    if (th < 1) th = 1;
+    uint32_t nw = tw, nh = th;
+    if (!(tw == W && th == H)) {
+        const double wr = (double)tw / (double)W, hr = (double)th / (double)H;
+        const double r = wr < hr ? wr : hr;
+        double fw = std::round((double)W * r), fh = std::round((double)H * r);
+        unsigned long long rw = fw < 1 ? 1 : (unsigned long long)fw;
+        unsigned long long rh = fh < 1 ? 1 : (unsigned long long)fh;
+        if (rw > 0xFFFFFFFFull || rh > 0xFFFFFFFFull) return fail(IK_ERR_INVALID, "dimension overflow");
+        nw = (uint32_t)rw; nh = (uint32_t)rh;
+    }
+    *onw = nw;
+    *onh = nh;
+    return IK_OK;
+}
+
+// imageops::resize over n 8-bit images of one geometry (same W, H, C, pitch) in
+// ONE fused launch: the kernel reads each image's base pointer from a table, so
+// the images may sit anywhere.  Same arithmetic as ik_resize_exact, per image.
+// Returns IK_ERR_UNSUPPORTED (nothing allocated) when the geometry needs the
+// two-kernel fallback; the caller then resizes image by image.
+int resize_group(const std::vector<ik_image*>& src, uint32_t nw, uint32_t nh, int filter, std::vector<ik_image*>& out) {
+    const size_t n = src.size();
+    out.assign(n, nullptr);
+    if (!n) return IK_OK;
+    const ik_image* s0 = src[0];
+    DeviceGuard g(s0->device);
+    ResizePlan* plan = get_resize_plan(current_device(), (int)s0->w, (int)s0->h, (int)s0->c, (int)nw, (int)nh, filter,
+                                       (int)n);
+    if (!plan) return fail(IK_ERR_DEVICE, "cannot build resize plan");
+    if (plan->slots == 0 || !resize_fused_fits(s0->pitch, s0->h) || (s0->pitch & 7)) return IK_ERR_UNSUPPORTED;
+    std::vector<uint64_t> tab(2 * n);
+    for (size_t i = 0; i < n; ++i) {
+        const int st = alloc_image(nw, nh, s0->c, &out[i]);
+        if (st) {
+            for (ik_image*& o : out) { ik_image_free(o); o = nullptr; }
+            return st;
+        }
+        tab[i] = (uint64_t)(uintptr_t)src[i]->d;
+        tab[n + i] = (uint64_t)(uintptr_t)out[i]->d;
+    }
+    hipStream_t s = thread_stream();
+    uint64_t* dtab = reinterpret_cast<uint64_t*>(scratch_slot(3, sizeof(uint64_t) * 2 * n));
+    int rc = dtab ? copy_h2d_2d(reinterpret_cast<uint8_t*>(dtab), 16 * n, reinterpret_cast<const uint8_t*>(tab.data()),
+                                16 * n, 16 * n, 1, s)
+                  : fail(IK_ERR_DEVICE, "cannot allocate device scratch");
+    if (!rc) {
+        hipError_t e = launch_resize(*plan, nullptr, s0->pitch, 0, nullptr, out[0]->pitch, 0, (int)n, nullptr, s, dtab,
+                                     dtab + n);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) rc = hip_fail(e, "resize (batched)");
+    }
+    if (rc)
+        for (ik_image*& o : out) { ik_image_free(o); o = nullptr; }
+    return rc;
+}
+
+}  // namespace ik
+
+extern "C" {
+
 // src/transform.rs:62-90 then DynamicImage::resize (image 0.25.8):
 // (nw,nh) == dims -> clone; else resize_dimensions(..., fill=false) (aspect FIT,
 // f64, round, max 1) -> imageops::resize.
 int ik_resize(ik_image* img, int64_t w, int64_t h, int filter, ik_image** out) {
     if (!img || !out) return fail(IK_ERR_INVALID, "null pointer");
     if (w < 0 && h < 0) { *out = img; return IK_OK; }
-    if (w > 0xFFFFFFFFll || h > 0xFFFFFFFFll) return fail(IK_ERR_INVALID, "dimension exceeds u32");
-    uint32_t tw, th;
-    if (w >= 0) tw = (uint32_t)w;
-    else tw = f32_as_u32(roundf((float)img->w * ((float)(uint32_t)h / (float)img->h)));
-    if (h >= 0) th = (uint32_t)h;
-    else th = f32_as_u32(roundf((float)img->h * ((float)(uint32_t)w / (float)img->w)));
-    if (tw < 1) tw = 1;
-    if (th < 1) th = 1;
-    uint32_t nw = tw, nh = th;
-    if (!(tw == img->w && th == img->h)) {
-        const double wr = (double)tw / (double)img->w, hr = (double)th / (double)img->h;
-        const double r = wr < hr ? wr : hr;
-        double fw = std::round((double)img->w * r), fh = std::round((double)img->h * r);
-        unsigned long long rw = fw < 1 ? 1 : (unsigned long long)fw;
-        unsigned long long rh = fh < 1 ? 1 : (unsigned long long)fh;
-        if (rw > 0xFFFFFFFFull || rh > 0xFFFFFFFFull) return fail(IK_ERR_INVALID, "dimension overflow");
-        nw = (uint32_t)rw; nh = (uint32_t)rh;
-    }
+    uint32_t nw, nh;
+    const int st = resize_target(img->w, img->h, w, h, &nw, &nh);
+    if (st) return st;
     return ik_resize_exact(img, nw, nh, filter, out);
 }
 
 int ik_encode(const ik_image* img, int fmt, int quality, uint8_t** out, size_t* out_len) {
     if (!img || !out || !out_len) return fail(IK_ERR_INVALID, "null pointer");
-    if (img->w == 0 || img->h == 0) return fail(IK_ERR_TRANSFORM, "cannot encode an empty image");
-    DeviceGuard g(img->device);
     std::vector<uint8_t> bytes;
-    int st;
-    if (img->depth == 2) {  // to_rgb8 / to_rgba8 rescale the u16 samples first
-        ik_image* u8 = nullptr;
-        st = alloc_image(img->w, img->h, img->c, &u8);
-        if (st) return st;
-        hipError_t e = launch_u16_to_u8(img->d, img->pitch, u8->d, u8->pitch, (int)(img->w * img->c), (int)img->h,
-                                        thread_stream());
-        st = e == hipSuccess ? encode_device_image(u8->d, u8->w, u8->h, u8->c, u8->pitch, fmt, quality, bytes)
-                             : hip_fail(e, "u16 -> u8");
-        ik_image_free(u8);
-    } else {
-        st = encode_device_image(img->d, img->w, img->h, img->c, img->pitch, fmt, quality, bytes);
-    }
+    EncodePrep prep;
+    int st = encode_image_front(img, fmt, quality, prep, bytes);
+    if (!st) st = encode_host_back(prep, bytes);
     if (st) return st;
     *out = (uint8_t*)malloc(bytes.size() ? bytes.size() : 1);
     if (!*out) return fail(IK_ERR_NOMEM, "out of host memory");
@@ -829,32 +939,89 @@ static void transform_part(const uint8_t* const* bytes, const size_t* lens, cons
     std::vector<ik_image*> imgs(m, nullptr);
     std::vector<int> ds(m, IK_OK);
     std::vector<std::string> dm(m);
-    decode_batch_dev(b.data(), l.data(), m, imgs.data(), nullptr, ds.data(), dm.data(), threads);
     static const bool timing = getenv("IK_TIMING") != nullptr;  // dev: per-stage sums to stderr
+    // GPU phases under the device's kernel gate (held from the decode kernels --
+    // decode_png_batch takes it after its upload phase -- through resize and the
+    // encoders' device front ends), then the host coders outside it, so that a
+    // concurrent batch's kernels run beside this one's libwebp / libavif coding
+    gate_pin(kGateKernels, true);
+    decode_batch_dev(b.data(), l.data(), m, imgs.data(), nullptr, ds.data(), dm.data(), threads);
+    gate_enter(kGateKernels);
     std::mutex tmu;
-    double t_resize = 0, t_encode = 0;
+    double t_resize = 0, t_front = 0, t_back = 0;
+    std::vector<EncodePrep> prep(m);
+    std::vector<std::vector<uint8_t>> bytes_out(m);
+    // requests whose decoded images share a geometry and an output size resize in
+    // one launch (resize_group); the rest, image by image below
+    std::vector<ik_image*> rsz(m, nullptr);
+    {
+        std::map<std::tuple<uint32_t, uint32_t, uint32_t, size_t, int, uint32_t, uint32_t>, std::vector<uint32_t>> groups;
+        for (uint32_t k = 0; k < m; ++k) {
+            const uint32_t i = idx[k];
+            if (ds[k] || !imgs[k] || imgs[k]->depth != 1 || (w[i] < 0 && h[i] < 0)) continue;
+            uint32_t nw, nh;
+            if (resize_target(imgs[k]->w, imgs[k]->h, w[i], h[i], &nw, &nh)) continue;
+            if (nw == imgs[k]->w && nh == imgs[k]->h) continue;
+            groups[std::make_tuple(imgs[k]->w, imgs[k]->h, imgs[k]->c, imgs[k]->pitch, imgs[k]->device, nw, nh)]
+                .push_back(k);
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        for (auto& kv : groups) {
+            if (kv.second.size() < 2) continue;
+            std::vector<ik_image*> src, out;
+            for (uint32_t k : kv.second) src.push_back(imgs[k]);
+            if (resize_group(src, std::get<5>(kv.first), std::get<6>(kv.first), filter, out) == IK_OK)
+                for (size_t j = 0; j < out.size(); ++j) rsz[kv.second[j]] = out[j];
+        }
+        t_resize += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
     parallel_for((int)m, threads, [&](int k) {
         const uint32_t i = idx[k];
         if (ds[k]) { st[i] = ds[k]; errs[i] = dm[k]; return; }
-        ik_image* rs = nullptr;
+        ik_image* rs = rsz[k];
         const auto t0 = std::chrono::steady_clock::now();
-        int r = ik_resize(imgs[k], w[i], h[i], filter, &rs);
+        int r = rs ? IK_OK : ik_resize(imgs[k], w[i], h[i], filter, &rs);
         const auto t1 = std::chrono::steady_clock::now();
-        if (!r) r = ik_encode(rs, fmt[i], quality[i], &outs[i], &out_lens[i]);
+        if (!r) r = encode_image_front(rs, fmt[i], quality[i], prep[k], bytes_out[k]);
         if (timing) {
             const auto t2 = std::chrono::steady_clock::now();
             std::lock_guard<std::mutex> lk(tmu);
             t_resize += std::chrono::duration<double, std::milli>(t1 - t0).count();
-            t_encode += std::chrono::duration<double, std::milli>(t2 - t1).count();
+            t_front += std::chrono::duration<double, std::milli>(t2 - t1).count();
         }
-        if (r) { errs[i] = last_error_str(); st[i] = r; }
+        if (r) { errs[i] = last_error_str(); st[i] = r; prep[k].done = true; }
         if (rs && rs != imgs[k]) ik_image_free(rs);
         ik_image_free(imgs[k]);
         imgs[k] = nullptr;
     });
+    const double tg = timing ? std::chrono::duration<double, std::milli>(
+                                   std::chrono::steady_clock::now().time_since_epoch()).count() : 0.0;
+    gate_pin(kGateKernels, false);
+    parallel_for((int)m, threads, [&](int k) {
+        const uint32_t i = idx[k];
+        if (st[i]) return;
+        const auto t0 = std::chrono::steady_clock::now();
+        int r = encode_host_back(prep[k], bytes_out[k]);
+        std::vector<uint8_t>().swap(prep[k].planes);
+        if (!r) {
+            outs[i] = (uint8_t*)malloc(bytes_out[k].size() ? bytes_out[k].size() : 1);
+            if (!outs[i]) r = fail(IK_ERR_NOMEM, "out of host memory");
+            else {
+                std::memcpy(outs[i], bytes_out[k].data(), bytes_out[k].size());
+                out_lens[i] = bytes_out[k].size();
+            }
+        }
+        if (timing) {
+            std::lock_guard<std::mutex> lk(tmu);
+            t_back += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        }
+        if (r) { errs[i] = last_error_str(); st[i] = r; }
+    });
     if (timing)
-        fprintf(stderr, "[transform_batch] %u requests on device %d: resize %.1f ms, encode %.1f ms (summed)\n", m,
-                current_device(), t_resize, t_encode);
+        fprintf(stderr, "[transform_batch] t=%.1f..%.1f %u requests on device %d: resize %.1f ms, encode front %.1f ms, "
+                "host coders %.1f ms (summed)\n", fmod(tg, 1e5), fmod(std::chrono::duration<double, std::milli>(
+                std::chrono::steady_clock::now().time_since_epoch()).count(), 1e5), m, current_device(), t_resize,
+                t_front, t_back);
 }
 
 // IK_BATCH_SPLIT = P > 1 runs a batch as P parts of at least 8 requests at

@@ -54,6 +54,10 @@ struct ResizeArgs {
     int max_strip_cols;      // max output columns of a strip (LDS table size)
     int max_strip_weights;   // max nox*Tx of a strip (LDS weights size when in LDS)
     float* tmp;        // naive path only: f32 vertical intermediate [n][nh][row_bytes]
+    // fused path, images anywhere in memory: per-image base pointers (device
+    // arrays, [n]); null = src + img * src_img_stride / dst + img * dst_img_stride
+    const uint64_t* src_tab;
+    const uint64_t* dst_tab;
 };
 
 // Host-side plan for one (W,H,C,nw,nh,filter,band height) geometry.
@@ -82,7 +86,8 @@ hipError_t launch_u16_to_u8(const uint8_t* src, size_t sp, uint8_t* dst, size_t 
                             hipStream_t s);
 hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_pitch,
                          size_t src_img_stride, uint8_t* dst, size_t dst_pitch,
-                         size_t dst_img_stride, int n, float* naive_tmp, hipStream_t s);
+                         size_t dst_img_stride, int n, float* naive_tmp, hipStream_t s,
+                         const uint64_t* src_tab = nullptr, const uint64_t* dst_tab = nullptr);
 // dynamic LDS bytes of the fused kernel
 size_t resize_lds_bytes(const ResizeArgs& a, bool wl, int flush);
 hipError_t launch_webp_yuv420(const uint8_t* src, int w, int h, int C, size_t pitch,

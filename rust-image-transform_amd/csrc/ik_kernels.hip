@@ -169,8 +169,9 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
     const int nox = ox1 - ox0;
     const int oy0 = bands[2 * band], oy1 = bands[2 * band + 1];
     const int kb = bstep[band], ke = bstep[band + 1];
-    const uint8_t* __restrict__ src = a.src + (size_t)img * a.src_img_stride;
-    uint8_t* __restrict__ dst = a.dst + (size_t)img * a.dst_img_stride;
+    const uint8_t* __restrict__ src =
+        a.src_tab ? reinterpret_cast<const uint8_t*>(a.src_tab[img]) : a.src + (size_t)img * a.src_img_stride;
+    uint8_t* __restrict__ dst = a.dst_tab ? reinterpret_cast<uint8_t*>(a.dst_tab[img]) : a.dst + (size_t)img * a.dst_img_stride;
 
     float* __restrict__ s_w = lds + F * kRowWords;
     int* __restrict__ s_off = reinterpret_cast<int*>(s_w + (WL ? a.max_strip_weights : 0));
@@ -370,6 +371,7 @@ hipError_t launch_resize16(const ResizePlan& plan, const uint8_t* src, size_t sr
     ResizeArgs a = plan.args;
     a.src = src; a.src_pitch = src_pitch; a.src_img_stride = 0;
     a.dst = dst; a.dst_pitch = dst_pitch; a.dst_img_stride = 0;
+    a.src_tab = nullptr; a.dst_tab = nullptr;
     a.tmp = tmp;
     dim3 g1((a.row_bytes + kThreads - 1) / kThreads, a.nh);
     hipLaunchKernelGGL(k_vert_naive16, g1, dim3(kThreads), 0, s, a);
@@ -412,11 +414,14 @@ size_t resize_lds_bytes(const ResizeArgs& a, bool wl, int flush) {
 
 hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_pitch,
                          size_t src_img_stride, uint8_t* dst, size_t dst_pitch,
-                         size_t dst_img_stride, int n, float* naive_tmp, hipStream_t s) {
+                         size_t dst_img_stride, int n, float* naive_tmp, hipStream_t s,
+                         const uint64_t* src_tab, const uint64_t* dst_tab) {
     ResizeArgs a = plan.args;
     a.src = src; a.src_pitch = src_pitch; a.src_img_stride = src_img_stride;
     a.dst = dst; a.dst_pitch = dst_pitch; a.dst_img_stride = dst_img_stride;
+    a.src_tab = src_tab; a.dst_tab = dst_tab;
     a.tmp = naive_tmp;
+    if (src_tab && !(plan.slots > 0 && resize_fused_fits(src_pitch, (size_t)a.H))) return hipErrorInvalidValue;
     if (plan.slots > 0 && resize_fused_fits(src_pitch, (size_t)a.H)) {
         dim3 grid(plan.NS * plan.NB * n);  // 1-D: the kernel maps it XCD-aware
         const bool wl = plan.weights_in_lds;

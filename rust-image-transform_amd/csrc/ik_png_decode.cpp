@@ -22,6 +22,8 @@
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <mutex>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -118,6 +120,15 @@ bool parse_png(const uint8_t* b, size_t n, PngJob& J) {
     return true;
 }
 
+struct HostTables {
+    std::vector<int> chunk_img, chunk_idx, pages, xst;
+    std::vector<int64_t> cand, obase;
+    std::vector<PngLaneDev> lanes;
+    std::vector<std::pair<int, int>> who;
+    std::vector<infl::LaneResult> res;
+    std::vector<int2> rows;
+};
+
 double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -202,17 +213,18 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
     const uint64_t cbits = kPngChunkBytes * 8;
     if (m) {
         // ---- device layout ----
+        constexpr size_t kPad = 512;  // zero bytes past each stream (Bits::wend, the LDS ring's DMAs)
         size_t total = 0, zbytes = 0;
         int nchunks = 0;
         for (PngJob* j : J) {
             j->z_off = zbytes;
-            zbytes += (j->zlen + 3) & ~size_t(3);
+            zbytes += ((j->zlen + 3) & ~size_t(3)) + kPad;  // the zero padding travels with the stream
             j->nbits = (uint64_t)j->zlen * 8;
             j->nchunks = (int)((j->nbits - 16 + cbits - 1) / cbits);
             j->chunk0 = nchunks;
             nchunks += j->nchunks;
             j->o_words = total;
-            total += up256(((j->zlen + 3) & ~size_t(3)) + 512);  // zero padding: Bits::wend, the LDS ring's DMAs
+            total += up256(((j->zlen + 3) & ~size_t(3)) + kPad);
             j->o_u16 = total;
             total += up256(2 * (j->raw_total + 64));
             j->o_ft = total;
@@ -286,35 +298,23 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             d_tok = reinterpret_cast<uint16_t*>(dev + o);
         }
         uint64_t tok_used = 0;
-        uint8_t* pin = rc ? nullptr : pinned_slot(1, zbytes + 64);
-        if (!rc && !pin) rc = fail(IK_ERR_NOMEM, "cannot allocate pinned PNG staging");
-        // IDAT payloads -> pinned (host threads), CRC-checked on the way (png
-        // verifies every chunk's CRC), each stream's H2D copy issued as soon as it
-        // is staged, so the PCIe transfer overlaps the staging of the others
-        std::vector<char> crc_bad(m, 0);
-        std::atomic<int> up_err{0};
-        if (!rc)
-            parallel_for(m, 0, [&](int k) {
-                PngJob& j = *J[k];
-                uint8_t* d = pin + j.z_off;
-                for (auto& seg : j.idat) {
-                    if (png_chunk_crc(seg.first - 4, seg.first, seg.second) != be32(seg.first + seg.second)) crc_bad[k] = 1;
-                    std::memcpy(d, seg.first, seg.second);
-                    d += seg.second;
-                }
-                while ((size_t)(d - (pin + j.z_off)) & 3) *d++ = 0;
-                const size_t wb = (j.zlen + 3) & ~size_t(3);
-                hipError_t e = hipMemsetAsync(dev + j.o_words + wb, 0, 512, s);
-                if (e == hipSuccess) e = hipMemcpyAsync(dev + j.o_words, pin + j.z_off, wb, hipMemcpyHostToDevice, s);
-                if (e != hipSuccess) up_err = (int)e;
-            });
-        if (!rc && up_err) rc = hip_fail((hipError_t)up_err.load(), "PNG stream upload");
-        for (int k = 0; k < m; ++k)
-            if (crc_bad[k]) J[k]->state = -1;  // the host decoder reports png's CRC error
-        const double t1 = now_ms();
-        // ---- upload streams (zero pad), image descriptors, chunk table ----
+        // phases: staging + upload + block search under the device's upload gate,
+        // the decode kernels on under its kernel gate (ik_runtime.h), so that
+        // concurrent batches take the GPU in turn
+        gate_enter(kGateUpload);
+        // with the device free, each stream's block search runs as soon as its copy
+        // lands; with another batch's kernels running, the searches wait for the
+        // kernel gate (sharing the CUs with those kernels slows both)
+        const bool early = gate_try_enter(kGateKernels);
+        // ---- image descriptors and the chunk table (before any stream lands) ----
         std::vector<PngImgDev> hd(m);
-        std::vector<int> ctab(2 * (size_t)nchunks);
+        // the large host tables are kept per thread between batches (clear() keeps
+        // the capacity): fresh multi-MB vectors cost page faults every batch
+        static thread_local HostTables ht;
+        std::vector<int>& hchunk_img = ht.chunk_img;
+        std::vector<int>& hchunk_idx = ht.chunk_idx;
+        hchunk_img.assign(nchunks, 0);
+        hchunk_idx.assign(nchunks, 0);
         for (int k = 0; k < m && !rc; ++k) {
             PngJob& j = *J[k];
             PngImgDev& d = hd[k];
@@ -328,12 +328,10 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             d.bpp = j.bpp;
             d.ft = dev + j.o_ft;
             for (int c = 0; c < j.nchunks; ++c) {
-                ctab[2 * (size_t)(j.chunk0 + c)] = k;
-                ctab[2 * (size_t)(j.chunk0 + c) + 1] = c;
+                hchunk_img[j.chunk0 + c] = k;
+                hchunk_idx[j.chunk0 + c] = c;
             }
         }
-        std::vector<int> hchunk_img(nchunks), hchunk_idx(nchunks);
-        for (int c = 0; c < nchunks; ++c) { hchunk_img[c] = ctab[2 * (size_t)c]; hchunk_idx[c] = ctab[2 * (size_t)c + 1]; }
         if (!rc) rc = copy_h2d_2d(dev + o_ctab, sizeof(int) * nchunks, reinterpret_cast<const uint8_t*>(hchunk_img.data()),
                                   sizeof(int) * nchunks, sizeof(int) * nchunks, 1, s);
         if (!rc) rc = copy_h2d_2d(dev + o_ctab + sizeof(int) * nchunks, sizeof(int) * nchunks,
@@ -342,29 +340,100 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
         if (!rc) rc = copy_h2d_2d(dev + o_imgs, sizeof(PngImgDev) * m, reinterpret_cast<const uint8_t*>(hd.data()),
                                   sizeof(PngImgDev) * m, sizeof(PngImgDev) * m, 1, s);
         const PngImgDev* d_imgs = reinterpret_cast<const PngImgDev*>(dev + o_imgs);
-        // ---- candidates ----
-        std::vector<int64_t> cand(nchunks);
+        const int* d_cimg = reinterpret_cast<const int*>(dev + o_ctab);
+        const int* d_cidx = d_cimg + nchunks;
+        int64_t* d_cand = reinterpret_cast<int64_t*>(dev + o_cand);
+        uint8_t* pin = rc ? nullptr : pinned_slot(1, zbytes + 64);
+        if (!rc && !pin) rc = fail(IK_ERR_NOMEM, "cannot allocate pinned PNG staging");
+        // IDAT payloads -> pinned (host threads), CRC-checked on the way (png
+        // verifies every chunk's CRC).  Each stream's H2D copy goes out on the copy
+        // stream as soon as it is staged, and its block search on the compute stream
+        // as soon as the copy has landed (an event), so the PCIe transfer overlaps
+        // the staging of the later streams and the search the transfer
+        hipStream_t sc = rc ? nullptr : thread_copy_stream();
+        if (!rc && !sc) rc = fail(IK_ERR_DEVICE, "cannot create the PNG copy stream");
+        static thread_local std::vector<hipEvent_t> landed;
+        while (!rc && (int)landed.size() < m) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+                rc = fail(IK_ERR_DEVICE, "cannot create PNG upload events");
+                break;
+            }
+            landed.push_back(e);
+        }
+        // (the workers below see their own thread_local vector: pass the caller's)
+        hipEvent_t* const ev_landed = landed.data();
+        std::vector<char> crc_bad(m, 0);
+        std::atomic<int> up_err{0};
+        std::atomic<long long> t_copy_calls{0};  // dev timing: us spent inside hipMemcpyAsync
+        const double t_stage0 = now_ms();
+        double t_stage1 = t_stage0;
         if (!rc) {
             rec(0, s);
-            hipError_t e = launch_png_find(d_imgs, reinterpret_cast<const int*>(dev + o_ctab),
-                                           reinterpret_cast<const int*>(dev + o_ctab) + nchunks, nchunks, cbits,
-                                           reinterpret_cast<int64_t*>(dev + o_cand), s);
+            parallel_for(m, 0, [&, s, sc](int k) {
+                PngJob& j = *J[k];
+                uint8_t* d = pin + j.z_off;
+                for (auto& seg : j.idat) {
+                    if (png_chunk_crc(seg.first - 4, seg.first, seg.second) != be32(seg.first + seg.second)) crc_bad[k] = 1;
+                    std::memcpy(d, seg.first, seg.second);
+                    d += seg.second;
+                }
+                const size_t wb = (j.zlen + 3) & ~size_t(3);
+                std::memset(d, 0, pin + j.z_off + wb + kPad - d);
+                // one plain copy per stream, with its zero padding (no memset kernel
+                // ahead of it, which would wait for a CU while other kernels run)
+                const double tc0 = timing ? now_ms() : 0.0;
+                hipError_t e = hipMemcpyAsync(dev + j.o_words, pin + j.z_off, wb + kPad, hipMemcpyHostToDevice, sc);
+                if (timing) t_copy_calls += (long long)(1000.0 * (now_ms() - tc0));
+                if (early) {
+                    if (e == hipSuccess) e = hipEventRecord(ev_landed[k], sc);
+                    if (e == hipSuccess) e = hipStreamWaitEvent(s, ev_landed[k], 0);
+                    if (e == hipSuccess)
+                        e = launch_png_find(d_imgs, d_cimg + j.chunk0, d_cidx + j.chunk0, j.nchunks, cbits,
+                                            d_cand + j.chunk0, s);
+                }
+                if (e != hipSuccess) up_err = (int)e;
+            });
+            t_stage1 = now_ms();
+            gate_leave(kGateUpload);
+            if (!early) {  // all copies are on sc: one event after the last, then one search launch
+                gate_enter(kGateKernels);
+                hipError_t e = hipEventRecord(ev_landed[0], sc);
+                if (e == hipSuccess) e = hipStreamWaitEvent(s, ev_landed[0], 0);
+                if (e == hipSuccess) e = launch_png_find(d_imgs, d_cimg, d_cidx, nchunks, cbits, d_cand, s);
+                if (e != hipSuccess) up_err = (int)e;
+            }
             rec(1, s);
-            if (e == hipSuccess) e = hipMemcpyAsync(cand.data(), dev + o_cand, sizeof(int64_t) * nchunks,
-                                                    hipMemcpyDeviceToHost, s);
+        }
+        if (!rc && up_err) rc = hip_fail((hipError_t)up_err.load(), "PNG stream upload / block search");
+        for (int k = 0; k < m; ++k)
+            if (crc_bad[k]) J[k]->state = -1;  // the host decoder reports png's CRC error
+        const double t1 = now_ms();
+        // ---- candidates ----
+        std::vector<int64_t>& cand = ht.cand;
+        cand.assign(nchunks, 0);
+        if (!rc) {
+            hipError_t e = hipMemcpyAsync(cand.data(), d_cand, sizeof(int64_t) * nchunks, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) rc = hip_fail(e, "PNG block search");
         }
+        gate_leave(kGateUpload);   // (error paths)
+        gate_enter(kGateKernels);
+        const double t_gate = now_ms();
         const double t2 = now_ms();
+        double mk[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // dev timing marks (IK_PNG_TIMING)
         for (PngJob* j : J) {
             std::vector<int64_t> c(cand.begin() + j->chunk0, cand.begin() + j->chunk0 + j->nchunks);
             pngplan::build(c, j->lanes);
         }
         // ---- decode rounds: token streams; the host checks the lane chain ----
         int rounds = 0, dropped = 0, overflows = 0;
-        std::vector<PngLaneDev> hl;
-        std::vector<std::pair<int, int>> who;  // (job, lane) of each launched lane
-        std::vector<infl::LaneResult> hres;
+        std::vector<PngLaneDev>& hl = ht.lanes;
+        std::vector<std::pair<int, int>>& who = ht.who;  // (job, lane) of each launched lane
+        std::vector<infl::LaneResult>& hres = ht.res;
+        hl.clear();
+        who.clear();
+        hres.clear();
         while (!rc) {
             hl.clear();
             who.clear();
@@ -408,6 +477,7 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             rc = copy_h2d_2d(reinterpret_cast<uint8_t*>(d_lanes), lb, reinterpret_cast<const uint8_t*>(hl.data()), lb, lb, 1, s);
             if (rc) break;
             hres.resize(hl.size());
+            if (!mk[0]) mk[0] = now_ms();  // plan built, lanes uploaded (first round)
             rec(2, s);
             hipError_t e = launch_png_decode(d_imgs, d_lanes, (int)hl.size(), d_tok, d_res, s);
             rec(3, s);
@@ -446,8 +516,10 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
         }
         const double t3 = now_ms();
         // ---- offsets, output images, expand, resolve, unfilter ----
-        std::vector<int64_t> hob;
-        std::vector<int> hpages;
+        std::vector<int64_t>& hob = ht.obase;
+        std::vector<int>& hpages = ht.pages;
+        hob.clear();
+        hpages.clear();
         hl.clear();
         for (int k = 0; k < m && !rc; ++k) {
             PngJob& j = *J[k];
@@ -480,8 +552,12 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             }
             hob.insert(hob.end(), ob.begin(), ob.end());
         }
-        std::vector<int2> hrows;
-        std::vector<int> herr(m, 0), hxst;
+        mk[1] = now_ms();  // offsets, images, page tables, lane table built
+        std::vector<int2>& hrows = ht.rows;
+        std::vector<int>& hxst = ht.xst;
+        hrows.clear();
+        hxst.clear();
+        std::vector<int> herr(m, 0);
         if (!rc && !hl.empty()) {
             for (int k = 0; k < m; ++k)
                 if (J[k]->state == 1)
@@ -500,6 +576,7 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                                       reinterpret_cast<const uint8_t*>(hrows.data()), sizeof(int2) * hrows.size(),
                                       sizeof(int2) * hrows.size(), 1, s);
             hxst.resize(2 * hl.size());
+            mk[2] = now_ms();  // row table built, tables uploaded
             if (!rc) {
                 hipError_t e = hipMemsetAsync(dev + o_err, 0, sizeof(int) * m, s);
                 rec(4, s);
@@ -559,6 +636,7 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                                                         hipMemcpyDeviceToHost, s);
                 if (e == hipSuccess) e = hipMemcpyAsync(herr.data(), dev + o_err, sizeof(int) * m, hipMemcpyDeviceToHost, s);
                 if (e == hipSuccess) e = hipStreamSynchronize(s);
+                mk[3] = now_ms();  // expand .. unfilter done
                 if (e != hipSuccess) rc = hip_fail(e, "PNG inflate (expand) / unfilter");
                 if (!rc) {
                     t_png_timing[3] = ev_ms(4, 5);
@@ -578,6 +656,8 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                 }
             }
         }
+        gate_leave(kGateUpload);   // (error paths)
+        gate_leave(kGateKernels);  // unless the caller pinned it (transform_part: resize + encode next)
         if (timing && !hl.empty()) {  // per-lane profile of the last decode round and the expand pass
             double si = 0, sc = 0, sx = 0, mi = 0, mc = 0, mx = 0, sb = 0, mb = 0;
             for (size_t t = 0; t < hres.size(); ++t) {
@@ -601,9 +681,15 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
         t_png_timing[8] = (double)hl.size();
         t_png_timing[9] = m;
         if (timing)
-            fprintf(stderr, "[png] %d streams (%d on the GPU): stage %.2f ms, find %.2f ms, decode %.2f ms (%d rounds, "
-                    "%d dropped, %d overflows), expand+resolve+unfilter %.2f ms\n", n, m, t1 - t0, t2 - t1, t3 - t2,
-                    rounds, dropped, overflows, now_ms() - t3);
+            fprintf(stderr, "[png] t=%.1f %d streams (%d on the GPU): stage %.2f ms, find %.2f ms (kernel gate at +%.2f), "
+                    "decode %.2f ms (%d rounds, %d dropped, %d overflows), expand+resolve+unfilter %.2f ms; staging "
+                    "loop %.2f ms (early %d), in hipMemcpyAsync %.2f ms summed\n",
+                    fmod(t0, 1e5), n, m, t1 - t0, t2 - t1, t_gate - t0, t3 - t2, rounds, dropped, overflows, now_ms() - t3,
+                    t_stage1 - t_stage0, (int)early, 1e-3 * (double)t_copy_calls.load());
+        if (timing)
+            fprintf(stderr, "[png] host: plan+lanes %.2f, (decode rounds) .. tables %.2f, rows+uploads %.2f, "
+                    "(expand..unfilter) %.2f, after %.2f ms\n", mk[0] - t2, mk[1] - t3, mk[2] - mk[1], mk[3] - mk[2],
+                    now_ms() - mk[3]);
         for (int k = 0; k < m; ++k) {
             PngJob& j = *J[k];
             if (!rc && j.state == 1) {
@@ -642,6 +728,7 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
         }
     });
     t_png_timing[6] = now_ms() - t0;
+    if (timing) fprintf(stderr, "[png] decode_png_batch returns at t=%.1f\n", fmod(now_ms(), 1e5));
     int first = IK_OK;
     for (int i = 0; i < n; ++i)
         if (status[i] && !first) first = status[i];

@@ -53,6 +53,54 @@ int default_threads() {
     return t;
 }
 
+// ---- phase gates -----------------------------------------------------------------
+namespace {
+bool gates_on() {
+    static const bool on = [] {
+        const char* e = getenv("IK_BATCH_GATE");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return on;
+}
+std::mutex& gate_mutex(int device, int which) {
+    static std::mutex m[64][2];
+    return m[(unsigned)device % 64u][which & 1];
+}
+struct GateState {
+    bool held[2] = {false, false}, pinned[2] = {false, false};
+    int dev[2] = {0, 0};
+};
+thread_local GateState t_gate;
+}  // namespace
+
+void gate_enter(int which) {
+    if (!gates_on() || t_gate.held[which]) return;
+    const int d = current_device();
+    gate_mutex(d, which).lock();
+    t_gate.held[which] = true;
+    t_gate.dev[which] = d;
+}
+
+bool gate_try_enter(int which) {
+    if (!gates_on() || t_gate.held[which]) return true;
+    const int d = current_device();
+    if (!gate_mutex(d, which).try_lock()) return false;
+    t_gate.held[which] = true;
+    t_gate.dev[which] = d;
+    return true;
+}
+
+void gate_leave(int which) {
+    if (!t_gate.held[which] || t_gate.pinned[which]) return;
+    gate_mutex(t_gate.dev[which], which).unlock();
+    t_gate.held[which] = false;
+}
+
+void gate_pin(int which, bool on) {
+    t_gate.pinned[which] = on;
+    if (!on) gate_leave(which);
+}
+
 // ---- Pool ----------------------------------------------------------------------
 Pool::Pool(int device, int max_threads) : device_(device), max_threads_(std::max(1, max_threads)) {}
 
@@ -72,7 +120,7 @@ void Pool::loop() {
         {
             std::unique_lock<std::mutex> lk(mu_);
             cv_.wait(lk, [&] { return !q_.empty(); });
-            task = std::move(q_.front());
+            task = std::move(q_.front().fn);
             q_.pop_front();
             ++busy_;
         }
@@ -82,13 +130,27 @@ void Pool::loop() {
     }
 }
 
-void Pool::post(std::function<void()> task) {
+void Pool::post(std::function<void()> task) { post_tagged(std::move(task), nullptr); }
+
+void Pool::post_tagged(std::function<void()> task, const void* tag) {
     {
         std::lock_guard<std::mutex> lk(mu_);
-        q_.push_back(std::move(task));
+        q_.push_back(Task{std::move(task), tag});
         ensure(busy_ + (int)q_.size());
     }
     cv_.notify_one();
+}
+
+// A finished parallel_for's helpers still queued would do nothing when run, but
+// they count as work in ensure(): left there, every later call would see them and
+// start more threads (each with its own stream and arenas) -- the pool crept
+// towards its cap under batch load.  Remove them.
+void Pool::withdraw(const void* tag) {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (auto it = q_.begin(); it != q_.end();) {
+        if (it->tag == tag) it = q_.erase(it);
+        else ++it;
+    }
 }
 
 namespace {
@@ -123,10 +185,13 @@ void Pool::parallel_for(int n, int threads, const std::function<void(int)>& fn) 
     // helpers: a helper dequeued after every index was claimed returns at once and
     // never touches fn; the caller always works too, so progress never depends on
     // a free worker (nested parallel_for from a worker is safe)
-    for (int t = 1; t < threads; ++t) post([st] { st->work(); });
+    for (int t = 1; t < threads; ++t) post_tagged([st] { st->work(); }, st.get());
     st->work();
-    std::unique_lock<std::mutex> lk(st->mu);
-    st->cv.wait(lk, [&] { return st->done == st->n; });
+    {
+        std::unique_lock<std::mutex> lk(st->mu);
+        st->cv.wait(lk, [&] { return st->done == st->n; });
+    }
+    withdraw(st.get());
 }
 
 Pool& device_pool(int device) {

@@ -53,13 +53,19 @@ public:
     int device() const { return device_; }
 
 private:
+    struct Task {
+        std::function<void()> fn;
+        const void* tag;  // parallel_for helpers: their ForState (withdrawn once it is done)
+    };
+    void post_tagged(std::function<void()> task, const void* tag);
+    void withdraw(const void* tag);
     void ensure(int nthreads);
     void loop();
     int device_, max_threads_;
     int nthreads_ = 0, busy_ = 0;
     std::mutex mu_;
     std::condition_variable cv_;
-    std::deque<std::function<void()>> q_;
+    std::deque<Task> q_;
 };
 Pool& device_pool(int device);  // the persistent workers of a physical device
 // fn(i) for i in [0, n) on the calling thread's device pool (and the caller)
@@ -81,6 +87,7 @@ bool sniff_dims(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& 
 uint64_t request_cost(const uint8_t* b, size_t n, int64_t w, int64_t h, int fmt);
 
 hipStream_t thread_stream();  // per-thread, per-device non-blocking stream
+hipStream_t thread_copy_stream();  // a second one, for uploads that overlap the first's kernels
 size_t pitch_for(uint32_t w, uint32_t c);
 uint8_t* scratch(size_t bytes);  // per-thread device scratch, valid until the next call
 // per-thread, per-device grow-only device arenas for batch work (slot 1: JPEG
@@ -172,5 +179,37 @@ int decode_jpeg_batch(const uint8_t* const* b, const size_t* lens, int n, ik_ima
 // device-side stage helpers used by ik_encode and the pipeline
 int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, size_t pitch,
                         int fmt, int quality, std::vector<uint8_t>& out);
+// encode_image in two halves: the device front end (colour conversion, FDCT and
+// Huffman coding for JPEG) leaves either the final bytes (done) or the planes the
+// host coder takes (WebP YUV420, AVIF YUV444 + alpha); the back end runs that
+// host coder (libwebp / libavif) and touches no device
+struct EncodePrep {
+    int fmt = -1, q = 0;
+    uint32_t w = 0, h = 0;
+    bool done = false, transparent = false;
+    std::vector<uint8_t> planes;
+};
+int encode_device_front(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, size_t pitch, int fmt, int quality,
+                        EncodePrep& p, std::vector<uint8_t>& out);
+int encode_image_front(const ik_image* img, int fmt, int quality, EncodePrep& p, std::vector<uint8_t>& out);
+int encode_host_back(EncodePrep& p, std::vector<uint8_t>& out);
+
+// resize_image's output size (src/transform.rs:62-90 + DynamicImage::resize) and
+// a one-launch resize of same-geometry 8-bit images (ik_host.cpp)
+int resize_target(uint32_t W, uint32_t H, int64_t w, int64_t h, uint32_t* nw, uint32_t* nh);
+int resize_group(const std::vector<ik_image*>& src, uint32_t nw, uint32_t nh, int filter, std::vector<ik_image*>& out);
+
+// Per-device phase gates (ik_pool.cpp).  Concurrent batch calls on one device
+// take its GPU phases in turn: kGateUpload covers a PNG batch's staging, H2D and
+// block search, kGateKernels the decode kernels through resize and the encoders'
+// device front ends.  A batch's host phases (libwebp / libavif coding) run
+// outside both, beside the next batch's kernels; its small kernels never queue
+// behind another batch's long ones.  gate_pin keeps a gate held across
+// gate_leave (a caller that spans several phases); IK_BATCH_GATE=0 disables them.
+enum { kGateUpload = 0, kGateKernels = 1 };
+void gate_enter(int which);
+bool gate_try_enter(int which);  // true if now held (or gates are off)
+void gate_leave(int which);
+void gate_pin(int which, bool on);
 
 }  // namespace ik
