@@ -73,8 +73,18 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
                                                  int nchunks_total, uint64_t chunk_bits, int64_t* cand) {
     __shared__ uint8_t s_tab[64 * 128];     // per lane: code-length code lookup (symbol | length << 5)
     __shared__ uint32_t s_q[kFindQueue];    // Kraft-passing offsets (relative to the chunk) awaiting the full check
+    __shared__ uint8_t s_kraft[512];        // 3 code-length-code lengths (9 bits) -> sum of 2^(7 - len), len > 0
     const int g = blockIdx.x;
     if (g >= nchunks_total) return;
+    for (int v = threadIdx.x; v < 512; v += 64) {
+        uint32_t k = 0;
+        for (int f = 0; f < 3; ++f) {
+            const uint32_t l = ((uint32_t)v >> (3 * f)) & 7u;
+            k += l ? (128u >> l) : 0u;
+        }
+        s_kraft[v] = (uint8_t)k;
+    }
+    __syncthreads();
     const int im = chunk_img[g];
     const int c = chunk_idx[g];
     const PngImgDev I = imgs[im];
@@ -134,12 +144,11 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
             const uint64_t cl = (lo >> sh) | (hi << (64 - sh));  // code-length code lengths (57 bits)
             const int ncode = (int)((h >> 13) & 15u) + 4;
             const uint64_t used = cl & (ncode == 19 ? 0x1FFFFFFFFFFFFFFull : ((1ull << (3 * ncode)) - 1ull));
-            uint32_t kraft = 0;
-            IK_UNROLL
-            for (int i = 0; i < 19; ++i) {
-                const uint32_t l = (uint32_t)(used >> (3 * i)) & 7u;
-                kraft += l ? (128u >> l) : 0u;
-            }
+            // Kraft sum over the 19 lengths, three at a time from the LDS table
+            const uint32_t ulo = (uint32_t)used, uhi = (uint32_t)(used >> 32);
+            uint32_t kraft = s_kraft[ulo & 511u] + s_kraft[(ulo >> 9) & 511u] + s_kraft[(ulo >> 18) & 511u] +
+                             s_kraft[((ulo >> 27) | (uhi << 5)) & 511u] + s_kraft[(uhi >> 4) & 511u] +
+                             s_kraft[(uhi >> 13) & 511u] + s_kraft[(uhi >> 22) & 7u];
             if (kraft == 128u) km |= 1u << j;
         }
         // queue them: one per lane per round, compacted by lane rank

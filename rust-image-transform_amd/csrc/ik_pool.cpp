@@ -32,6 +32,10 @@
 #include <numeric>
 #include <thread>
 
+#include <sys/resource.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include "../../include/imagekit_hip.h"
 #include "ik_runtime.h"
 
@@ -114,6 +118,11 @@ void Pool::ensure(int nthreads) {
 }
 
 void Pool::loop() {
+    // bulk host work (staging copies, libwebp / libavif coding) runs here: a lower
+    // priority than the callers' own threads, which launch the kernels and plan
+    // the next launch -- on a CPU-limited host those must not wait behind it
+    static const int nice_v = env_int("IK_WORKER_NICE", 5);
+    if (nice_v > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), nice_v);
     ik_init(device_);  // this worker's stream / staging / scratch live on device_
     for (;;) {
         std::function<void()> task;
