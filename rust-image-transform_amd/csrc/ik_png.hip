@@ -510,50 +510,83 @@ __global__ __launch_bounds__(64) void k_png_expand(const PngImgDev* imgs, const 
 
 // ---- resolve ------------------------------------------------------------------------
 // thread = (16-byte chunk of a row, row, image); grid.y over rows of all images via
-// a row table (image, row)
+// a row table (image, row).  Window markers (~4 % of the symbols, near each
+// decoder lane's start) are collected into an LDS list while the chunks are
+// stored, and then followed by all the workgroup's threads at once, one marker
+// per thread: a chunk's markers resolved by its own thread one after another
+// held the whole row for a chain of dependent loads per marker.
+constexpr int kResolveList = 4096;
+
 __global__ __launch_bounds__(256) void k_png_resolve(const PngImgDev* imgs, const int2* rows, int nrows,
                                                      int* err) {
+    __shared__ uint32_t s_pos[kResolveList];  // marker positions in the row (byte index after the filter byte)
+    __shared__ uint32_t s_cnt;
     const int rr = blockIdx.y * 65535 + blockIdx.x;  // row of the batch
     if (rr >= nrows) return;
     const int2 ir = rows[rr];
     const PngImgDev I = imgs[ir.x];
     const int y = ir.y;
     const int64_t rs = (int64_t)y * (I.rowbytes + 1);  // filter byte of row y
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
     if (threadIdx.x == 0) {
         const int v = infl::resolve_at(I.u16, I.obase, I.nlanes, I.page_lane, kPngPageShift, rs);
         I.ft[y] = (uint8_t)(v < 0 ? 255 : v);
         if (v < 0 || v > 4) atomicOr(err + ir.x, 1);
     }
+    uint8_t* const drow = I.dst + (size_t)y * I.pitch;
     for (int x0 = threadIdx.x * 16; x0 < I.rowbytes; x0 += 256 * 16) {
         const int64_t e0 = rs + 1 + x0;
-        // 16 u16 symbols from 9 aligned dwords (the u16 buffer is padded)
+        // 16 u16 symbols from 9 dwords in three loads (two dwordx4 at a dword-aligned
+        // address, the u16 buffer is padded), shifted by one symbol when e0 is odd
+        // (uniform over the row), then each output dword packs the low bytes of four
+        // symbols with one v_perm
         const uint32_t* w = reinterpret_cast<const uint32_t*>(I.u16) + (e0 >> 1);
-        uint32_t d[9];
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        const u4 va = *reinterpret_cast<const u4*>(w), vb = *reinterpret_cast<const u4*>(w + 4);
+        const uint32_t d[9] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w, w[8]};
+        uint32_t e[8];
+        if (e0 & 1) {
 #pragma unroll
-        for (int k = 0; k < 9; ++k) d[k] = w[k];
-        const int odd = (int)(e0 & 1);
-        uint32_t o[4] = {0, 0, 0, 0};
-        bool any_marker = false;
+            for (int i = 0; i < 8; ++i) e[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], 2u);
+        } else {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const uint32_t v = odd ? (d[(i + 1) >> 1] >> (16 * ((i + 1) & 1))) & 0xFFFFu
-                                   : (d[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-            any_marker |= v >= 256u;
-            o[i >> 2] |= (v & 255u) << (8 * (i & 3));
+            for (int i = 0; i < 8; ++i) e[i] = d[i];
         }
-        if (any_marker) {  // window markers: follow them to the byte they name
-            const int n = I.rowbytes - x0 < 16 ? I.rowbytes - x0 : 16;
-#pragma unroll 1
-            for (int i = 0; i < n; ++i) {
-                const uint32_t v = I.u16[e0 + i];
-                if (v < 256u) continue;
+        uint32_t mk = 0;  // bit i: symbol i is a window marker
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            mk |= ((e[i] & 0xFF00u) ? 1u : 0u) << (2 * i) | ((e[i] & 0xFF000000u) ? 1u : 0u) << (2 * i + 1);
+        const int n = I.rowbytes - x0 < 16 ? I.rowbytes - x0 : 16;
+        mk &= (1u << n) - 1u;
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = __builtin_amdgcn_perm(e[2 * k + 1], e[2 * k], 0x06040200u);
+        if (mk) {
+            // this thread's slots are [at, at + c): those inside the list are filled
+            // (so the list never has holes), the rest resolve here
+            uint32_t k = atomicAdd(&s_cnt, (uint32_t)__builtin_popcount(mk));
+            while (mk) {
+                const int i = __builtin_ctz(mk);
+                mk &= mk - 1u;
+                if (k < (uint32_t)kResolveList) {
+                    s_pos[k++] = (uint32_t)(x0 + i);
+                    continue;
+                }
                 const int rv = infl::resolve_at(I.u16, I.obase, I.nlanes, I.page_lane, kPngPageShift, e0 + i);
                 if (rv < 0) atomicOr(err + ir.x, 2);
                 o[i >> 2] = (o[i >> 2] & ~(255u << (8 * (i & 3)))) | (((uint32_t)rv & 255u) << (8 * (i & 3)));
             }
         }
-        uint8_t* dp = I.dst + (size_t)y * I.pitch + x0;
-        *reinterpret_cast<uint4*>(dp) = make_uint4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<uint4*>(drow + x0) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    __syncthreads();  // (also orders the chunk stores before the marker bytes below)
+    const uint32_t cnt = s_cnt < (uint32_t)kResolveList ? s_cnt : (uint32_t)kResolveList;
+    for (uint32_t m = threadIdx.x; m < cnt; m += 256) {
+        const uint32_t x = s_pos[m];
+        const int rv = infl::resolve_at(I.u16, I.obase, I.nlanes, I.page_lane, kPngPageShift, rs + 1 + (int64_t)x);
+        if (rv < 0) atomicOr(err + ir.x, 2);
+        drow[x] = (uint8_t)rv;
     }
 }
 
