@@ -74,6 +74,11 @@ def parse():
     ap.add_argument("--clients", type=int, default=1,
                     help="client threads calling ik_transform_batch at once, each on its own batch (a server's "
                          "concurrent requests): one batch's host phases overlap another's kernels")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="1: each step submits its batch (ik_transform_batch_submit: decode, resize and the "
+                         "encoders device half on this thread) and then waits for the previous step's host "
+                         "coders, so one batch's libwebp coding runs beside the next one's upload and kernels; "
+                         "0: one blocking ik_transform_batch per step")
     ap.add_argument("--split", type=int, default=1,
                     help="parts a transform batch runs as at once (IK_BATCH_SPLIT: overlaps one part's host "
                          "phases with another's kernels)")
@@ -247,7 +252,7 @@ def main():
         dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
-    from imagekit import _lib, transform_batch
+    from imagekit import _lib, transform_batch, transform_batch_submit
     lib = _lib.load()
     if lib.ik_init(local) != 0:
         raise SystemExit(f"ik_init({local}) failed: {_lib.last_error()}")
@@ -297,7 +302,27 @@ def main():
         if errors:
             raise SystemExit(f"transform_batch failed: {errors[0]}")
 
-    if C == 1:
+    def submit():
+        p = transform_batch_submit(reqs, [(O, O)] * B, [FORMATS["webp"]] * B, [args.quality] * B, filter=f,
+                                   threads=args.threads)
+        timing = (ctypes.c_double * 13)()
+        lib.ik_png_last_timing(timing, 13)
+        stage_ms.append(list(timing))
+        return p
+
+    def run_pipelined(nsteps):
+        pend, out = None, None
+        for _ in range(nsteps):
+            p = submit()
+            if pend is not None:
+                out = pend.wait()
+            pend = p
+        return pend.wait() if pend is not None else out
+
+    pipelined = bool(args.pipeline) and C == 1
+    if pipelined:
+        run_pipelined(args.warmup)
+    elif C == 1:
         for _ in range(args.warmup):
             step()
     else:
@@ -307,7 +332,9 @@ def main():
     lib.ik_png_counters(cnt0)
     barrier()
     t0 = time.perf_counter()
-    if C == 1:
+    if pipelined:
+        res = run_pipelined(args.steps)
+    elif C == 1:
         for _ in range(args.steps):
             res = step()
     else:
@@ -462,7 +489,7 @@ def main():
                 "workload": f"{S}x{S} RGBA8 synthetic frames as PNG (zlib level 6) in host memory -> "
                             f"ik_transform_batch: decode_image (GPU inflate + unfilter) -> resize_image {O}x{O} "
                             f"({args.filter}) -> encode_image webp q{args.quality} (libwebp) -> WebP bytes in host memory",
-                "batch_per_gpu": B, "batch_split": args.split, "clients": C, "filter": args.filter, "format": "webp", "quality": args.quality,
+                "batch_per_gpu": B, "batch_split": args.split, "clients": C, "pipelined": pipelined, "filter": args.filter, "format": "webp", "quality": args.quality,
                 "host_threads_per_gpu": args.threads, "png_bytes_per_image": in_bytes,
                 "webp_bytes_per_image": out_bytes,
                 "libwebp": "%d.%d.%d" % (lib.ik_libwebp_version() >> 16, (lib.ik_libwebp_version() >> 8) & 255,

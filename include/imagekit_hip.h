@@ -186,6 +186,21 @@ int ik_transform_batch(const uint8_t *const *bytes, const size_t *lens, uint32_t
                        const int64_t *h, const int *fmt, const int *quality, int filter, int threads,
                        uint8_t **outs, size_t *out_lens, int *status);
 
+/* ik_transform_batch as two calls, so that one batch's host coders (libwebp /
+ * libavif, CPU) run beside the next batch's decode (PCIe + GPU): submit runs the
+ * batch's device half -- decode, resize, the encoders' device front ends -- on the
+ * calling thread and queues its host coders on the device's workers; wait blocks
+ * until they are done, fills status[] (may be NULL) and returns the first
+ * failure, as ik_transform_batch does.  Every array passed to submit must stay
+ * valid until wait returns; each ticket is waited for exactly once.  With several
+ * devices (ik_init(-1)) or IK_BATCH_SPLIT the batch runs to completion inside
+ * submit.  (Same role as ik_transform_batch: the reference's handlers,
+ * src/lib.rs:175-191, serving many requests at once.) */
+int ik_transform_batch_submit(const uint8_t *const *bytes, const size_t *lens, uint32_t n, const int64_t *w,
+                              const int64_t *h, const int *fmt, const int *quality, int filter, int threads,
+                              uint8_t **outs, size_t *out_lens, int *status, uint64_t *ticket);
+int ik_transform_batch_wait(uint64_t ticket);
+
 /* A batch of n same-geometry 8-bit images already resident in device memory
  * (image i at dev_src + i*src_image_stride, rows src_pitch bytes apart) ->
  * resize to nw x nh -> encode.  Encoded bytes are written into the caller's

@@ -928,9 +928,23 @@ namespace ik {
 // ik_transform_batch over the items idx[] of a batch, on the calling thread's
 // device: one batched decode (GPU entropy decoding where the stream allows), then
 // resize_image + encode_image per item on the device's persistent workers.
-static void transform_part(const uint8_t* const* bytes, const size_t* lens, const std::vector<uint32_t>& idx,
-                           const int64_t* w, const int64_t* h, const int* fmt, const int* quality, int filter,
-                           int threads, uint8_t** outs, size_t* out_lens, int* st, std::string* errs) {
+// The host half of a batch: the encoders' host coders (libwebp / libavif) over the
+// planes the device half left, and the output buffers.
+struct HostPhase {
+    std::vector<uint32_t> idx;
+    std::vector<EncodePrep> prep;
+    std::vector<std::vector<uint8_t>> bytes_out;
+    int threads = 0;
+    double t_resize = 0, t_front = 0;
+};
+
+// Device half: decode (GPU where the stream allows), resize, the encoders' device
+// front ends; request i's status / message land in st[i] / errs[i]
+static void transform_device_phase(const uint8_t* const* bytes, const size_t* lens, const int64_t* w,
+                                   const int64_t* h, const int* fmt, const int* quality, int filter, int* st,
+                                   std::string* errs, HostPhase& hp) {
+    const std::vector<uint32_t>& idx = hp.idx;
+    const int threads = hp.threads;
     const uint32_t m = (uint32_t)idx.size();
     if (!m) return;
     std::vector<const uint8_t*> b(m);
@@ -948,9 +962,12 @@ static void transform_part(const uint8_t* const* bytes, const size_t* lens, cons
     decode_batch_dev(b.data(), l.data(), m, imgs.data(), nullptr, ds.data(), dm.data(), threads);
     gate_enter(kGateKernels);
     std::mutex tmu;
-    double t_resize = 0, t_front = 0, t_back = 0;
-    std::vector<EncodePrep> prep(m);
-    std::vector<std::vector<uint8_t>> bytes_out(m);
+    double& t_resize = hp.t_resize;
+    double& t_front = hp.t_front;
+    hp.prep.assign(m, EncodePrep());
+    hp.bytes_out.assign(m, std::vector<uint8_t>());
+    std::vector<EncodePrep>& prep = hp.prep;
+    std::vector<std::vector<uint8_t>>& bytes_out = hp.bytes_out;
     // requests whose decoded images share a geometry and an output size resize in
     // one launch (resize_group); the rest, image by image below
     std::vector<ik_image*> rsz(m, nullptr);
@@ -994,10 +1011,20 @@ static void transform_part(const uint8_t* const* bytes, const size_t* lens, cons
         ik_image_free(imgs[k]);
         imgs[k] = nullptr;
     });
+    gate_pin(kGateKernels, false);
+}
+
+static void transform_host_phase(uint8_t** outs, size_t* out_lens, int* st, std::string* errs, HostPhase& hp) {
+    static const bool timing = getenv("IK_TIMING") != nullptr;
+    const std::vector<uint32_t>& idx = hp.idx;
+    const uint32_t m = (uint32_t)idx.size();
+    std::vector<EncodePrep>& prep = hp.prep;
+    std::vector<std::vector<uint8_t>>& bytes_out = hp.bytes_out;
+    std::mutex tmu;
+    double t_back = 0;
     const double tg = timing ? std::chrono::duration<double, std::milli>(
                                    std::chrono::steady_clock::now().time_since_epoch()).count() : 0.0;
-    gate_pin(kGateKernels, false);
-    parallel_for((int)m, threads, [&](int k) {
+    parallel_for((int)m, hp.threads, [&](int k) {
         const uint32_t i = idx[k];
         if (st[i]) return;
         const auto t0 = std::chrono::steady_clock::now();
@@ -1020,8 +1047,19 @@ static void transform_part(const uint8_t* const* bytes, const size_t* lens, cons
     if (timing)
         fprintf(stderr, "[transform_batch] t=%.1f..%.1f %u requests on device %d: resize %.1f ms, encode front %.1f ms, "
                 "host coders %.1f ms (summed)\n", fmod(tg, 1e5), fmod(std::chrono::duration<double, std::milli>(
-                std::chrono::steady_clock::now().time_since_epoch()).count(), 1e5), m, current_device(), t_resize,
-                t_front, t_back);
+                std::chrono::steady_clock::now().time_since_epoch()).count(), 1e5), m, current_device(), hp.t_resize,
+                hp.t_front, t_back);
+}
+
+// ik_transform_batch over the items idx[] of a batch, on the calling thread's device
+static void transform_part(const uint8_t* const* bytes, const size_t* lens, const std::vector<uint32_t>& idx,
+                           const int64_t* w, const int64_t* h, const int* fmt, const int* quality, int filter,
+                           int threads, uint8_t** outs, size_t* out_lens, int* st, std::string* errs) {
+    HostPhase hp;
+    hp.idx = idx;
+    hp.threads = threads;
+    transform_device_phase(bytes, lens, w, h, fmt, quality, filter, st, errs, hp);
+    transform_host_phase(outs, out_lens, st, errs, hp);
 }
 
 // IK_BATCH_SPLIT = P > 1 runs a batch as P parts of at least 8 requests at
@@ -1120,6 +1158,90 @@ int ik_transform_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t
         if (st[i] && !first) { first = st[i]; first_i = i; }
     }
     if (first) return fail(first, "item %u: %s", first_i, errs[first_i].c_str());
+    return IK_OK;
+}
+
+// ---- pipelined batches: the device half on the caller, the host half queued ----
+namespace ik {
+namespace {
+struct AsyncBatch {
+    uint32_t n = 0;
+    uint8_t** outs = nullptr;
+    size_t* out_lens = nullptr;
+    int* status = nullptr;
+    std::vector<int> st;
+    std::vector<std::string> errs;
+    HostPhase hp;
+    int rc = IK_OK;  // set when the batch ran synchronously (several devices)
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+};
+std::mutex g_async_mu;
+std::map<uint64_t, std::shared_ptr<AsyncBatch>> g_async;
+uint64_t g_async_next = 1;
+}  // namespace
+}  // namespace ik
+
+int ik_transform_batch_submit(const uint8_t* const* bytes, const size_t* lens, uint32_t n, const int64_t* w,
+                              const int64_t* h, const int* fmt, const int* quality, int filter, int threads,
+                              uint8_t** outs, size_t* out_lens, int* status, uint64_t* ticket) {
+    if (!bytes || !lens || !w || !h || !fmt || !quality || !outs || !out_lens || !n || !ticket)
+        return fail(IK_ERR_INVALID, "bad batch");
+    auto job = std::make_shared<AsyncBatch>();
+    job->n = n;
+    job->outs = outs;
+    job->out_lens = out_lens;
+    job->status = status;
+    if (sched_multi() || batch_split() > 1) {  // already spread over workers: run it through
+        std::vector<int> stv(n, IK_OK);
+        job->rc = ik_transform_batch(bytes, lens, n, w, h, fmt, quality, filter, threads, outs, out_lens, stv.data());
+        if (status) std::copy(stv.begin(), stv.end(), status);
+        job->errs.assign(1, last_error_str());
+        job->done = true;
+    } else {
+        job->st.assign(n, IK_OK);
+        job->errs.assign(n, std::string());
+        for (uint32_t i = 0; i < n; ++i) { outs[i] = nullptr; out_lens[i] = 0; }
+        job->hp.idx.resize(n);
+        for (uint32_t i = 0; i < n; ++i) job->hp.idx[i] = i;
+        job->hp.threads = threads;
+        transform_device_phase(bytes, lens, w, h, fmt, quality, filter, job->st.data(), job->errs.data(), job->hp);
+        device_pool(current_device()).post([job] {
+            transform_host_phase(job->outs, job->out_lens, job->st.data(), job->errs.data(), job->hp);
+            job->hp = HostPhase();
+            std::lock_guard<std::mutex> lk(job->mu);
+            job->done = true;
+            job->cv.notify_all();
+        });
+    }
+    std::lock_guard<std::mutex> lk(g_async_mu);
+    *ticket = g_async_next++;
+    g_async[*ticket] = job;
+    return IK_OK;
+}
+
+int ik_transform_batch_wait(uint64_t ticket) {
+    std::shared_ptr<AsyncBatch> job;
+    {
+        std::lock_guard<std::mutex> lk(g_async_mu);
+        auto it = g_async.find(ticket);
+        if (it == g_async.end()) return fail(IK_ERR_INVALID, "unknown batch ticket %llu", (unsigned long long)ticket);
+        job = it->second;
+        g_async.erase(it);
+    }
+    {
+        std::unique_lock<std::mutex> lk(job->mu);
+        job->cv.wait(lk, [&] { return job->done; });
+    }
+    if (job->st.empty()) return job->rc ? fail(job->rc, "%s", job->errs[0].c_str()) : IK_OK;
+    int first = IK_OK;
+    uint32_t first_i = 0;
+    for (uint32_t i = 0; i < job->n; ++i) {
+        if (job->status) job->status[i] = job->st[i];
+        if (job->st[i] && !first) { first = job->st[i]; first_i = i; }
+    }
+    if (first) return fail(first, "item %u: %s", first_i, job->errs[first_i].c_str());
     return IK_OK;
 }
 

@@ -205,6 +205,59 @@ def transform_batch(datas, sizes, fmts, qualities, filter: "FilterType" = None, 
     return res
 
 
+class PendingBatch:
+    """A submitted ik_transform_batch_submit: its device half has run; wait() blocks
+    until its host coders are done and returns the encoded bytes per request (the
+    ctypes arrays the library writes into live here until then)."""
+
+    def __init__(self, keep, outs, olens, status, ticket, n):
+        self._keep, self._outs, self._olens, self._status = keep, outs, olens, status
+        self._ticket, self._n, self._done = ticket, n, False
+
+    def wait(self) -> List[bytes]:
+        if self._done:
+            raise InvalidArgument("batch already waited for")
+        lib = _lib.load()
+        st = lib.ik_transform_batch_wait(self._ticket)
+        self._done = True
+        res = []
+        for i in range(self._n):
+            o = self._outs[i]
+            res.append(ctypes.string_at(o, self._olens[i]) if o else None)
+            if o:
+                lib.ik_buf_free(o)
+        if st:
+            raise TransformError(_lib.last_error())
+        return res
+
+
+def transform_batch_submit(datas, sizes, fmts, qualities, filter: "FilterType" = None,
+                           threads: int = 0) -> PendingBatch:
+    """ik_transform_batch_submit: the device half of transform_batch now, the host
+    coders in the background; PendingBatch.wait() gives what transform_batch gives."""
+    lib = _lib.load()
+    bufs = [bytes(d) for d in datas]
+    n = len(bufs)
+    if n == 0:
+        raise InvalidArgument("empty batch")
+    filt = int(FilterType.Lanczos3 if filter is None else filter)
+    ptrs = (ctypes.c_void_p * n)(*[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p) for b in bufs])
+    lens = (ctypes.c_size_t * n)(*[len(b) for b in bufs])
+    ws = (ctypes.c_int64 * n)(*[-1 if s[0] is None else int(s[0]) for s in sizes])
+    hs = (ctypes.c_int64 * n)(*[-1 if s[1] is None else int(s[1]) for s in sizes])
+    fs = (ctypes.c_int * n)(*[int(f.value if isinstance(f, ImageFormat) else f) for f in fmts])
+    qs = (ctypes.c_int * n)(*[int(q) for q in qualities])
+    outs = (ctypes.c_void_p * n)()
+    olens = (ctypes.c_size_t * n)()
+    status = (ctypes.c_int * n)()
+    ticket = ctypes.c_uint64()
+    st = lib.ik_transform_batch_submit(ptrs, lens, n, ws, hs, fs, qs, filt, threads, outs, olens, status,
+                                       ctypes.byref(ticket))
+    if st:
+        raise TransformError(_lib.last_error())
+    return PendingBatch((bufs, ptrs, lens, ws, hs, fs, qs), outs, olens, status, ticket.value, n)
+
+
 def resize_image(img: DynamicImage, w: Optional[int], h: Optional[int],
                  filter: FilterType = FilterType.Lanczos3) -> DynamicImage:
     """src/transform.rs:62-90 (Lanczos3; `filter` is an extension)."""

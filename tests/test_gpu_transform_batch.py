@@ -12,7 +12,7 @@ import pytest
 from PIL import Image
 
 import ikutil
-from imagekit import ImageFormat, TransformError, _lib, transform_batch
+from imagekit import ImageFormat, TransformError, _lib, transform_batch, transform_batch_submit
 
 pytestmark = pytest.mark.gpu
 
@@ -70,6 +70,37 @@ def test_batch_error_message_is_the_decoders_own(ik):
     with pytest.raises(TransformError) as ei:
         transform_batch([blobs[0], bad_png, blobs[1]], [(10, None)] * 3, [ImageFormat.jpeg] * 3, [80] * 3)
     assert "item 1" in str(ei.value) and "Png" in str(ei.value)
+
+
+def test_submitted_batches_equal_blocking_batches(ik):
+    """ik_transform_batch_submit / _wait (pipelined batches: the next batch's device
+    half runs while the previous one's host coders finish): same bytes as the
+    blocking call, whatever the interleaving; errors and messages as the blocking
+    call reports them."""
+    blobs = _inputs()
+    sizes = [(320, None), (None, 240), (None, None), (400, 400), (150, 100), (512, None)] * 2
+    fmts = [ImageFormat.webp, ImageFormat.jpeg, ImageFormat.webp, ImageFormat.avif, ImageFormat.webp,
+            ImageFormat.jpeg] * 2
+    qs = [80, 85, 75, 60, 80, 80] * 2
+    datas = blobs * 2
+    ref = transform_batch(datas, sizes, fmts, qs, threads=4)
+    p1 = transform_batch_submit(datas, sizes, fmts, qs, threads=4)
+    p2 = transform_batch_submit(datas[::-1], sizes[::-1], fmts[::-1], qs[::-1], threads=4)
+    g2 = p2.wait()
+    g1 = p1.wait()
+    for got in (g1, g2[::-1]):
+        for r, g, f in zip(ref, got, fmts):
+            if f == ImageFormat.avif:  # libavif/aom threads: decodable, same size
+                assert Image.open(io.BytesIO(g)).size == Image.open(io.BytesIO(r)).size
+            else:
+                assert g == r
+    bad_png = blobs[4][:60]
+    p = transform_batch_submit([blobs[0], bad_png, blobs[1]], [(10, None)] * 3, [ImageFormat.jpeg] * 3, [80] * 3)
+    with pytest.raises(TransformError) as ei:
+        p.wait()
+    assert "item 1" in str(ei.value) and "Png" in str(ei.value)
+    lib = _lib.load()
+    assert lib.ik_transform_batch_wait(123456789) != 0  # unknown ticket
 
 
 def test_repeated_batches_do_not_grow_device_memory(ik):
