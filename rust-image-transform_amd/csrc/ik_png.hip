@@ -316,7 +316,7 @@ __global__ __launch_bounds__(kPngInflateThreads) void k_png_decode(const PngImgD
 //   3. the batch goes to the ring and, coalesced, to memory.
 // So a block costs a few memory round trips per 64 tokens instead of one per
 // copy, and 64 lanes share each one.
-constexpr int kXRing = 4096;            // recent output symbols per wave (LDS, power of two)
+constexpr int kXRing = 2048;            // recent output symbols per wave (LDS, power of two)
 constexpr int kXCap = 1024;             // output symbols per batch at most
 constexpr int kXNear = kXRing - kXCap;  // sources at most this far back come from the ring
 constexpr int kXGroup = 4;              // output positions per thread resolved together
