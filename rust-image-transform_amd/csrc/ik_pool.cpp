@@ -94,6 +94,8 @@ bool gate_try_enter(int which) {
     return true;
 }
 
+bool gate_held_any() { return t_gate.held[kGateKernels]; }
+
 void gate_leave(int which) {
     if (!t_gate.held[which] || t_gate.pinned[which]) return;
     gate_mutex(t_gate.dev[which], which).unlock();
@@ -142,9 +144,14 @@ void Pool::loop() {
 void Pool::post(std::function<void()> task) { post_tagged(std::move(task), nullptr); }
 
 void Pool::post_tagged(std::function<void()> task, const void* tag) {
+    // work for a caller inside a GPU phase (it holds a phase gate) goes to the front
+    // of the queue: behind another batch's bulk host work (staging copies, libwebp)
+    // it would keep the GPU phase -- and the gate, and the device -- waiting
+    const bool urgent = gate_held_any();
     {
         std::lock_guard<std::mutex> lk(mu_);
-        q_.push_back(Task{std::move(task), tag});
+        if (urgent) q_.push_front(Task{std::move(task), tag});
+        else q_.push_back(Task{std::move(task), tag});
         ensure(busy_ + (int)q_.size());
     }
     cv_.notify_one();

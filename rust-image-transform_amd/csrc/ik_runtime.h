@@ -209,6 +209,7 @@ int resize_group(const std::vector<ik_image*>& src, uint32_t nw, uint32_t nh, in
 enum { kGateUpload = 0, kGateKernels = 1 };
 void gate_enter(int which);
 bool gate_try_enter(int which);  // true if now held (or gates are off)
+bool gate_held_any();            // this thread holds its device's kernel gate
 void gate_leave(int which);
 void gate_pin(int which, bool on);
 
