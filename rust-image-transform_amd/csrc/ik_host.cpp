@@ -22,6 +22,7 @@
 #include <thread>
 
 #include "../../include/imagekit_hip.h"
+#include "ik_png.h"
 #include "ik_runtime.h"
 
 namespace ik {
@@ -78,7 +79,7 @@ struct Arena {
 struct ThreadRes {
     std::map<int, hipStream_t> streams, copy_streams;
     std::map<std::pair<int, int>, Arena> dev;  // (device, slot)
-    Arena pinned[4];
+    Arena pinned[6];
     ~ThreadRes() {
         for (auto& kv : dev) {
             if (!kv.second.p) continue;
@@ -332,15 +333,27 @@ int encode_device_front(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, 
         if (!dc) return fail(IK_ERR_DEVICE, "cannot upload WebP tables");
         const size_t uvw = (w + 1) / 2, uvh = (h + 1) / 2;
         const size_t bytes = (size_t)w * h + 2 * uvw * uvh;
-        uint8_t* dyuv = scratch(bytes);
-        if (!dyuv) return fail(IK_ERR_DEVICE, "cannot allocate device scratch");
-        hipError_t e = launch_webp_yuv420(dev, (int)w, (int)h, (int)c, pitch, 0, dyuv, 0, 1,
+        if (default_webp_encoder() == IK_WEBP_GPU) {
+            uint8_t* dyuv = scratch(bytes);
+            if (!dyuv) return fail(IK_ERR_DEVICE, "cannot allocate device scratch");
+            hipError_t e = launch_webp_yuv420(dev, (int)w, (int)h, (int)c, pitch, 0, dyuv, 0, 1,
+                                              dc->gamma_to_lin, dc->lin_to_gamma, s);
+            if (e != hipSuccess) return hip_fail(e, "webp yuv420");
+            return webp_encode_gpu(dyuv, (int)w, (int)h, q, out);
+        }
+        // the colour kernel writes the planes straight into pinned host memory: no
+        // copy-engine transfer, which would queue behind another batch's stream upload
+        uint8_t* hp = pinned_slot(4, bytes);
+        void* dhp = nullptr;
+        if (!hp || hipHostGetDevicePointer(&dhp, hp, 0) != hipSuccess || !dhp)
+            return fail(IK_ERR_NOMEM, "cannot map pinned WebP planes");
+        hipError_t e = launch_webp_yuv420(dev, (int)w, (int)h, (int)c, pitch, 0, reinterpret_cast<uint8_t*>(dhp), 0, 1,
                                           dc->gamma_to_lin, dc->lin_to_gamma, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_fail(e, "webp yuv420");
-        if (default_webp_encoder() == IK_WEBP_GPU) return webp_encode_gpu(dyuv, (int)w, (int)h, q, out);
-        p.planes.resize(bytes);
+        p.planes.assign(hp, hp + bytes);
         p.done = false;  // libwebp's VP8 coding of the planes: encode_host_back
-        return copy_d2h_2d(p.planes.data(), bytes, dyuv, bytes, bytes, 1, s);
+        return IK_OK;
     }
     if (fmt == IK_FORMAT_JPEG) {
         if (w > 65535 || h > 65535) return fail(IK_ERR_TRANSFORM, "JPEG dimensions %ux%u exceed 65535", w, h);
@@ -712,9 +725,21 @@ int resize_group(const std::vector<ik_image*>& src, uint32_t nw, uint32_t nh, in
     }
     hipStream_t s = thread_stream();
     uint64_t* dtab = reinterpret_cast<uint64_t*>(scratch_slot(3, sizeof(uint64_t) * 2 * n));
-    int rc = dtab ? copy_h2d_2d(reinterpret_cast<uint8_t*>(dtab), 16 * n, reinterpret_cast<const uint8_t*>(tab.data()),
-                                16 * n, 16 * n, 1, s)
-                  : fail(IK_ERR_DEVICE, "cannot allocate device scratch");
+    // the pointer table goes up through a copy kernel reading pinned memory (a
+    // copy-engine transfer would queue behind another batch's stream upload)
+    uint8_t* ht = pinned_slot(5, 16 * n);
+    void* dht = nullptr;
+    int rc = IK_OK;
+    if (!dtab) rc = fail(IK_ERR_DEVICE, "cannot allocate device scratch");
+    else if (!ht || hipHostGetDevicePointer(&dht, ht, 0) != hipSuccess || !dht)
+        rc = fail(IK_ERR_NOMEM, "cannot map pinned resize table");
+    if (!rc) {
+        (void)hipStreamSynchronize(s);  // the previous table is read
+        std::memcpy(ht, tab.data(), 16 * n);
+        const hipError_t e = launch_copy_words(reinterpret_cast<const uint32_t*>(dht), reinterpret_cast<uint32_t*>(dtab),
+                                               4 * n, s);
+        if (e != hipSuccess) rc = hip_fail(e, "resize table upload");
+    }
     if (!rc) {
         hipError_t e = launch_resize(*plan, nullptr, s0->pitch, 0, nullptr, out[0]->pitch, 0, (int)n, nullptr, s, dtab,
                                      dtab + n);

@@ -49,6 +49,9 @@ struct PngLaneDev {
     uint32_t pad;
 };
 
+// dst[i] = src[i] for n words, on the compute stream; one side may be pinned host
+// memory (the small transfers of the PNG kernel phase: ik_png_decode.cpp Xfer)
+hipError_t launch_copy_words(const uint32_t* src, uint32_t* dst, size_t n, hipStream_t s);
 hipError_t launch_png_find(const PngImgDev* imgs, const int* chunk_img, const int* chunk_idx, int n,
                            uint64_t chunk_bits, int64_t* cand, hipStream_t s);
 hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, int n, uint16_t* tok,

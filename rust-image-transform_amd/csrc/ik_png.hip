@@ -25,6 +25,7 @@
 //                   first row reads the previous band's last row from memory once
 //                   it is published (global progress counters, agent-scope
 //                   release/acquire; workgroups ordered by a start ticket).
+#include <algorithm>
 #include <type_traits>
 
 #include "ik_inflate.h"
@@ -793,6 +794,19 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngI
             }
         }
     }
+}
+
+// ---- small transfers through the compute queue ---------------------------------------
+__global__ __launch_bounds__(256) void k_copy_words(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                    size_t n) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+hipError_t launch_copy_words(const uint32_t* src, uint32_t* dst, size_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const size_t blocks = std::min<size_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_copy_words, dim3((unsigned)blocks), dim3(256), 0, s, src, dst, n);
+    return hipGetLastError();
 }
 
 // ---- launchers --------------------------------------------------------------------

@@ -129,6 +129,65 @@ struct HostTables {
     std::vector<int2> rows;
 };
 
+// Small host<->device transfers of the kernel phase (lane tables, offsets, row and
+// page tables, per-lane results) go through a copy kernel on the compute stream
+// that reads or writes pinned host memory directly, not through SDMA copies: those
+// queue behind any multi-GB stream upload on the same engine (another batch's, with
+// batches in flight), measured at 8-10 ms per table.  One pinned region per batch
+// (bump-allocated), so no transfer overwrites one a pending kernel still reads.
+struct Xfer {
+    uint8_t* pin = nullptr;   // host view
+    uint8_t* dpin = nullptr;  // the same memory as the device addresses it
+    size_t cap = 0, used = 0;
+    hipStream_t s = nullptr;
+    bool init(size_t bytes, hipStream_t st) {
+        s = st;
+        used = 0;
+        pin = pinned_slot(3, bytes);
+        void* dp = nullptr;
+        if (pin && hipHostGetDevicePointer(&dp, pin, 0) != hipSuccess) dp = nullptr;
+        dpin = reinterpret_cast<uint8_t*>(dp);
+        cap = dpin ? bytes : 0;
+        return dpin != nullptr;
+    }
+    size_t take(size_t n) {  // offset of a fresh region, or ~0 when the area is used up
+        n = (n + 255) & ~size_t(255);
+        if (used + n > cap) return ~size_t(0);
+        const size_t o = used;
+        used += n;
+        return o;
+    }
+    hipError_t h2d(void* dev, const void* host, size_t n) {
+        if (!n) return hipSuccess;
+        const size_t o = take(n + 4);
+        if (o == ~size_t(0))  // (more decode rounds than the area was sized for) the copy engine
+            return copy_h2d_2d(reinterpret_cast<uint8_t*>(dev), n, reinterpret_cast<const uint8_t*>(host), n, n, 1, s)
+                       ? hipErrorUnknown : hipSuccess;
+        std::memcpy(pin + o, host, n);
+        return launch_copy_words(reinterpret_cast<const uint32_t*>(dpin + o), reinterpret_cast<uint32_t*>(dev),
+                                 (n + 3) / 4, s);
+    }
+    // (synchronises the stream)
+    hipError_t d2h(void* host, const void* dev, size_t n) {
+        if (!n) return hipSuccess;
+        const size_t o = take(n + 4);
+        hipError_t e = hipSuccess;
+        size_t done = 0;
+        if (o != ~size_t(0)) {
+            e = launch_copy_words(reinterpret_cast<const uint32_t*>(dev), reinterpret_cast<uint32_t*>(dpin + o), n / 4, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e == hipSuccess) std::memcpy(host, pin + o, n & ~size_t(3));
+            done = n & ~size_t(3);
+        }
+        if (e == hipSuccess && done < n) {  // a tail under one word, or no room: the copy engine
+            e = hipMemcpyAsync(reinterpret_cast<uint8_t*>(host) + done, reinterpret_cast<const uint8_t*>(dev) + done,
+                               n - done, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+        }
+        return e;
+    }
+};
+
 double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -298,6 +357,12 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             d_tok = reinterpret_cast<uint16_t*>(dev + o);
         }
         uint64_t tok_used = 0;
+        Xfer X;
+        if (!rc && !X.init(2 * sizeof(PngLaneDev) * max_lanes + sizeof(infl::LaneResult) * max_lanes +
+                               sizeof(int64_t) * (max_lanes + nchunks) + 2 * sizeof(int) * max_lanes +
+                               sizeof(int2) * (nrows + ngroups) + sizeof(int) * (npages + 2 * m) +
+                               3 * sizeof(PngImgDev) * m + (64u << 10), s))
+            rc = fail(IK_ERR_NOMEM, "cannot allocate pinned PNG transfer area");
         // phases: staging + upload + block search under the device's upload gate,
         // the decode kernels on under its kernel gate (ik_runtime.h), so that
         // concurrent batches take the GPU in turn
@@ -413,8 +478,7 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
         std::vector<int64_t>& cand = ht.cand;
         cand.assign(nchunks, 0);
         if (!rc) {
-            hipError_t e = hipMemcpyAsync(cand.data(), d_cand, sizeof(int64_t) * nchunks, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            hipError_t e = X.d2h(cand.data(), d_cand, sizeof(int64_t) * nchunks);
             if (e != hipSuccess) rc = hip_fail(e, "PNG block search");
         }
         gate_leave(kGateUpload);   // (error paths)
@@ -474,16 +538,13 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             if (hl.empty()) break;
             if (hl.size() > max_lanes) { rc = fail(IK_ERR_DEVICE, "PNG lane table overflow"); break; }
             const size_t lb = sizeof(PngLaneDev) * hl.size();
-            rc = copy_h2d_2d(reinterpret_cast<uint8_t*>(d_lanes), lb, reinterpret_cast<const uint8_t*>(hl.data()), lb, lb, 1, s);
-            if (rc) break;
+            if (X.h2d(d_lanes, hl.data(), lb) != hipSuccess) { rc = fail(IK_ERR_DEVICE, "PNG lane table upload"); break; }
             hres.resize(hl.size());
             if (!mk[0]) mk[0] = now_ms();  // plan built, lanes uploaded (first round)
             rec(2, s);
             hipError_t e = launch_png_decode(d_imgs, d_lanes, (int)hl.size(), d_tok, d_res, s);
             rec(3, s);
-            if (e == hipSuccess) e = hipMemcpyAsync(hres.data(), d_res, sizeof(infl::LaneResult) * hl.size(),
-                                                    hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e == hipSuccess) e = X.d2h(hres.data(), d_res, sizeof(infl::LaneResult) * hl.size());
             if (e != hipSuccess) { rc = hip_fail(e, "PNG inflate (decode)"); break; }
             count_dev += ev_ms(2, 3);
             ++rounds;
@@ -563,18 +624,12 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                 if (J[k]->state == 1)
                     for (uint32_t y = 0; y < J[k]->h; ++y) hrows.push_back(make_int2(k, (int)y));
             const size_t lb = sizeof(PngLaneDev) * hl.size();
-            rc = copy_h2d_2d(reinterpret_cast<uint8_t*>(d_lanes), lb, reinterpret_cast<const uint8_t*>(hl.data()), lb, lb, 1, s);
-            if (!rc) rc = copy_h2d_2d(reinterpret_cast<uint8_t*>(d_obase), sizeof(int64_t) * hob.size(),
-                                      reinterpret_cast<const uint8_t*>(hob.data()), sizeof(int64_t) * hob.size(),
-                                      sizeof(int64_t) * hob.size(), 1, s);
-            if (!rc) rc = copy_h2d_2d(reinterpret_cast<uint8_t*>(d_pages), sizeof(int) * hpages.size(),
-                                      reinterpret_cast<const uint8_t*>(hpages.data()), sizeof(int) * hpages.size(),
-                                      sizeof(int) * hpages.size(), 1, s);
-            if (!rc) rc = copy_h2d_2d(dev + o_imgs, sizeof(PngImgDev) * m, reinterpret_cast<const uint8_t*>(hd.data()),
-                                      sizeof(PngImgDev) * m, sizeof(PngImgDev) * m, 1, s);
-            if (!rc) rc = copy_h2d_2d(reinterpret_cast<uint8_t*>(d_rows), sizeof(int2) * hrows.size(),
-                                      reinterpret_cast<const uint8_t*>(hrows.data()), sizeof(int2) * hrows.size(),
-                                      sizeof(int2) * hrows.size(), 1, s);
+            hipError_t ue = X.h2d(d_lanes, hl.data(), lb);
+            if (ue == hipSuccess) ue = X.h2d(d_obase, hob.data(), sizeof(int64_t) * hob.size());
+            if (ue == hipSuccess) ue = X.h2d(d_pages, hpages.data(), sizeof(int) * hpages.size());
+            if (ue == hipSuccess) ue = X.h2d(dev + o_imgs, hd.data(), sizeof(PngImgDev) * m);
+            if (ue == hipSuccess) ue = X.h2d(d_rows, hrows.data(), sizeof(int2) * hrows.size());
+            if (ue != hipSuccess) rc = hip_fail(ue, "PNG expand tables");
             hxst.resize(2 * hl.size());
             mk[2] = now_ms();  // row table built, tables uploaded
             if (!rc) {
@@ -607,21 +662,14 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                         if ((int)cls.size() > r.img0) ranges.push_back(r);
                     }
                     const size_t gb = up256(sizeof(int2) * ngroups);
-                    uint8_t* stage = pinned_slot(2, gb + sizeof(int) * m + sizeof(PngImgDev) * m);
-                    if (!stage) e = hipErrorOutOfMemory;
-                    if (e == hipSuccess) {
-                        std::memcpy(stage, groups.data(), sizeof(int2) * groups.size());
-                        std::memcpy(stage + gb, pbase.data(), sizeof(int) * pbase.size());
-                        e = hipMemcpyAsync(d_unf, stage, unf_tab, hipMemcpyHostToDevice, s);
-                    }
+                    std::vector<uint8_t> tabs(unf_tab, 0);
+                    std::memcpy(tabs.data(), groups.data(), sizeof(int2) * groups.size());
+                    std::memcpy(tabs.data() + gb, pbase.data(), sizeof(int) * pbase.size());
+                    e = X.h2d(d_unf, tabs.data(), unf_tab);
                     unsigned* d_prog = reinterpret_cast<unsigned*>(d_unf + unf_tab);
                     unsigned* d_ticket = d_prog + nbands;
                     if (e == hipSuccess) e = hipMemsetAsync(d_prog, 0, unf_zero, s);
-                    uint8_t* cstage = stage ? stage + gb + sizeof(int) * m : nullptr;
-                    if (e == hipSuccess) {
-                        std::memcpy(cstage, cls.data(), sizeof(PngImgDev) * cls.size());
-                        e = hipMemcpyAsync(d_cls, cstage, sizeof(PngImgDev) * cls.size(), hipMemcpyHostToDevice, s);
-                    }
+                    if (e == hipSuccess) e = X.h2d(d_cls, cls.data(), sizeof(PngImgDev) * cls.size());
                     const int2* d_groups = reinterpret_cast<const int2*>(d_unf);
                     const int* d_pbase = reinterpret_cast<const int*>(d_unf + gb);
                     for (size_t r = 0; r < ranges.size() && e == hipSuccess; ++r) {
@@ -632,10 +680,8 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                     }
                 }
                 rec(7, s);
-                if (e == hipSuccess) e = hipMemcpyAsync(hxst.data(), d_xst, 2 * sizeof(int) * hl.size(),
-                                                        hipMemcpyDeviceToHost, s);
-                if (e == hipSuccess) e = hipMemcpyAsync(herr.data(), dev + o_err, sizeof(int) * m, hipMemcpyDeviceToHost, s);
-                if (e == hipSuccess) e = hipStreamSynchronize(s);
+                if (e == hipSuccess) e = X.d2h(hxst.data(), d_xst, 2 * sizeof(int) * hl.size());
+                if (e == hipSuccess) e = X.d2h(herr.data(), dev + o_err, sizeof(int) * m);
                 mk[3] = now_ms();  // expand .. unfilter done
                 if (e != hipSuccess) rc = hip_fail(e, "PNG inflate (expand) / unfilter");
                 if (!rc) {
