@@ -59,13 +59,18 @@ int default_threads() {
 
 // ---- phase gates -----------------------------------------------------------------
 namespace {
-bool gates_on() {
-    static const bool on = [] {
+// IK_BATCH_GATE: unset = both gates, 0 = none, "upload" = the upload gate only
+int gates_mask() {
+    static const int m = [] {
         const char* e = getenv("IK_BATCH_GATE");
-        return !(e && !strcmp(e, "0"));
+        if (!e) return 3;
+        if (!strcmp(e, "0")) return 0;
+        if (!strcmp(e, "upload")) return 1;
+        return 3;
     }();
-    return on;
+    return m;
 }
+bool gates_on(int which) { return (gates_mask() >> which) & 1; }
 std::mutex& gate_mutex(int device, int which) {
     static std::mutex m[64][2];
     return m[(unsigned)device % 64u][which & 1];
@@ -78,7 +83,7 @@ thread_local GateState t_gate;
 }  // namespace
 
 void gate_enter(int which) {
-    if (!gates_on() || t_gate.held[which]) return;
+    if (!gates_on(which) || t_gate.held[which]) return;
     const int d = current_device();
     gate_mutex(d, which).lock();
     t_gate.held[which] = true;
@@ -86,7 +91,7 @@ void gate_enter(int which) {
 }
 
 bool gate_try_enter(int which) {
-    if (!gates_on() || t_gate.held[which]) return true;
+    if (!gates_on(which) || t_gate.held[which]) return true;
     const int d = current_device();
     if (!gate_mutex(d, which).try_lock()) return false;
     t_gate.held[which] = true;
@@ -123,7 +128,7 @@ void Pool::loop() {
     // bulk host work (staging copies, libwebp / libavif coding) runs here: a lower
     // priority than the callers' own threads, which launch the kernels and plan
     // the next launch -- on a CPU-limited host those must not wait behind it
-    static const int nice_v = env_int("IK_WORKER_NICE", 5);
+    static const int nice_v = env_int("IK_WORKER_NICE", 19);
     if (nice_v > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), nice_v);
     ik_init(device_);  // this worker's stream / staging / scratch live on device_
     for (;;) {
