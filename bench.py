@@ -285,6 +285,12 @@ def main():
         try:
             if lib.ik_init(local) != 0:
                 raise RuntimeError(_lib.last_error())
+            if args.pipeline:
+                run_pipelined(warm)
+                r = run_pipelined(nsteps)
+                if r is not None:
+                    results[ci] = r
+                return
             for _ in range(warm):
                 step()
             for _ in range(nsteps):
@@ -304,7 +310,7 @@ def main():
 
     def submit():
         p = transform_batch_submit(reqs, [(O, O)] * B, [FORMATS["webp"]] * B, [args.quality] * B, filter=f,
-                                   threads=args.threads)
+                                   threads=max(1, args.threads // C))
         timing = (ctypes.c_double * 13)()
         lib.ik_png_last_timing(timing, 13)
         stage_ms.append(list(timing))
