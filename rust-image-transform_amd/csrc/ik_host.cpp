@@ -1218,7 +1218,10 @@ int ik_transform_batch_submit(const uint8_t* const* bytes, const size_t* lens, u
     job->outs = outs;
     job->out_lens = out_lens;
     job->status = status;
-    if (sched_multi() || batch_split() > 1) {  // already spread over workers: run it through
+    // one logical device (ik_init(-1) on a one-GPU host): the device half right here
+    std::unique_ptr<DeviceGuard> one;
+    if (sched_multi() && sched_count() == 1) one.reset(new DeviceGuard(sched_phys(0)));
+    if ((sched_multi() && !one) || batch_split() > 1) {  // several devices: spread over their workers, run through
         std::vector<int> stv(n, IK_OK);
         job->rc = ik_transform_batch(bytes, lens, n, w, h, fmt, quality, filter, threads, outs, out_lens, stv.data());
         if (status) std::copy(stv.begin(), stv.end(), status);

@@ -108,6 +108,9 @@ def main():
     ap.add_argument("--clients", type=int, default=0,
                     help="client threads calling ik_transform_batch at once (0 = one per logical device)")
     ap.add_argument("--cpu-seconds", type=float, default=0.0, help="CPU leg of about this long (0 = none)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="1: each client submits its next batch (ik_transform_batch_submit) before waiting for "
+                         "the previous one's bytes, so one batch's libwebp coding runs beside the next one's GPU work")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -135,7 +138,7 @@ def main():
         dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
-    from imagekit import ImageFormat, _lib, transform_batch
+    from imagekit import ImageFormat, _lib, transform_batch, transform_batch_submit
     lib = _lib.load()
     queue = world == 1
     assert lib.ik_init(-1 if queue else local) == 0, _lib.last_error()
@@ -161,21 +164,33 @@ def main():
     lock = threading.Lock()
     nxt = [0]
 
+    def done(tb, res):
+        dt = (time.perf_counter() - tb) * 1e3
+        with lock:
+            lat.append(dt)
+            out_bytes[0] += sum(len(r) for r in res)
+            if len(lat) % 20 == 0:
+                print(f"[loadtest] {len(lat) * args.batch} requests", file=sys.stderr, flush=True)
+
     def client():  # a request handler: takes the next batch, waits for its bytes
+        pend = None  # (start time, PendingBatch) of the batch submitted last (--pipeline)
         while True:
             with lock:
-                if nxt[0] >= len(chunks):
-                    return
-                chunk = chunks[nxt[0]]
+                chunk = chunks[nxt[0]] if nxt[0] < len(chunks) else None
                 nxt[0] += 1
+            if chunk is None:
+                if pend is not None:
+                    done(pend[0], pend[1].wait())
+                return
             tb = time.perf_counter()
-            res = run_batch(chunk)
-            dt = (time.perf_counter() - tb) * 1e3
-            with lock:
-                lat.append(dt)
-                out_bytes[0] += sum(len(r) for r in res)
-                if len(lat) % 20 == 0:
-                    print(f"[loadtest] {len(lat) * args.batch} requests", file=sys.stderr, flush=True)
+            if not args.pipeline:
+                done(tb, run_batch(chunk))
+                continue
+            p = transform_batch_submit([srcs[s] for s, _, _, _ in chunk], [(w, h) for _, w, h, _ in chunk],
+                                       [f for _, _, _, f in chunk], [args.quality] * len(chunk), threads=args.threads)
+            if pend is not None:
+                done(pend[0], pend[1].wait())
+            pend = (tb, p)
 
     barrier()
     t0 = time.perf_counter()
@@ -203,6 +218,7 @@ def main():
             "output_bytes_per_request": out_bytes // max(1, len(mine)),
             "host_threads_per_gpu": args.threads,
             "filter": "lanczos3 (the reference's)",
+            "pipelined": bool(args.pipeline),
             "dispatch": (f"in-library dynamic queue over {ndev} logical device(s), {args.clients} client threads"
                          if queue else f"{world} processes, round-robin shards"),
             "cpu_leg": cpu,
