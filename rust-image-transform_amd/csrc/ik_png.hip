@@ -495,6 +495,8 @@ __global__ __launch_bounds__(64) void k_png_expand(const PngImgDev* imgs, const 
         };
         if (tot <= 64u) {
             resolve(std::integral_constant<int, 1>{}, 0u);
+        } else if (tot <= 128u) {  // the common case with a match or two in the step
+            resolve(std::integral_constant<int, 2>{}, 0u);
         } else {
             for (uint32_t g0 = 0; g0 < tot; g0 += 64 * kXGroup) resolve(std::integral_constant<int, kXGroup>{}, g0);
         }
