@@ -380,8 +380,15 @@ def main():
     }
     dom = max(kern, key=lambda k: kern[k][0])
     dms, dbytes = kern[dom]
+    traffic_png = None  # PMC HBM bytes of that kernel per 64-frame launch (tools/pmc_png_traffic.sh)
+    pmcp = os.path.join(ROOT, "profiles", "pmc_png.json")
+    if os.path.exists(pmcp) and B == 64 and S == 4096:
+        try:
+            traffic_png = json.load(open(pmcp)).get(dom, {}).get("hbm_bytes_per_batch")
+        except Exception:
+            traffic_png = None
     roof = {"bound": "hbm", "achieved": round(dbytes / (dms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(dbytes / (dms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None, "kernel": dom,
+            "frac": round(dbytes / (dms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": traffic_png, "kernel": dom,
             "kernel_ms": round(dms, 4), "bytes_per_launch": int(dbytes),
             "note": "DEFLATE decoding: each lane's symbol-to-symbol chain bounds it (one lane per block, ~1,900 "
                     "blocks per frame), not HBM; bytes = compressed bits in + u16 tokens out",
