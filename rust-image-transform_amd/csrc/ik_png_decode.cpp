@@ -582,6 +582,8 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
         hob.clear();
         hpages.clear();
         hl.clear();
+        size_t npg = 0;                        // page-table entries so far
+        std::vector<std::pair<int, size_t>> pj;  // (job, its first entry in hob) of every verified job
         for (int k = 0; k < m && !rc; ++k) {
             PngJob& j = *J[k];
             if (j.state != 1) continue;
@@ -591,13 +593,10 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             if (tot != j.raw_total) { reject(j, "image data length"); continue; }  // png's error
             if (alloc_image(j.w, j.h, (uint32_t)j.bpp, &j.img)) { reject(j, "image allocation"); continue; }
             hd[k].obase = d_obase + hob.size();
-            hd[k].page_lane = d_pages + hpages.size();
+            hd[k].page_lane = d_pages + npg;  // (the page table itself is built while expand runs)
             hd[k].nlanes = (int)ob.size();
-            // page -> decoder that holds the page's first byte (resolve's lane lookup)
-            for (uint64_t pg = 0, ln = 0; pg <= (j.raw_total >> kPngPageShift); ++pg) {
-                while (ln + 1 < ob.size() && (uint64_t)ob[ln + 1] <= (pg << kPngPageShift)) ++ln;
-                hpages.push_back((int)ln);
-            }
+            pj.emplace_back(k, hob.size());
+            npg += (j.raw_total >> kPngPageShift) + 1;
             hd[k].dst = j.img->d;
             hd[k].pitch = j.img->pitch;
             for (size_t i = 0; i < ob.size(); ++i) t_png_timing[12] += (double)j.lanes.res[i].ntok;
@@ -620,23 +619,34 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
         hxst.clear();
         std::vector<int> herr(m, 0);
         if (!rc && !hl.empty()) {
-            for (int k = 0; k < m; ++k)
-                if (J[k]->state == 1)
-                    for (uint32_t y = 0; y < J[k]->h; ++y) hrows.push_back(make_int2(k, (int)y));
+            // expand goes out first; the resolve pass's page and row tables are built
+            // on the host while it runs (stream order puts their uploads after it)
             const size_t lb = sizeof(PngLaneDev) * hl.size();
             hipError_t ue = X.h2d(d_lanes, hl.data(), lb);
             if (ue == hipSuccess) ue = X.h2d(d_obase, hob.data(), sizeof(int64_t) * hob.size());
-            if (ue == hipSuccess) ue = X.h2d(d_pages, hpages.data(), sizeof(int) * hpages.size());
             if (ue == hipSuccess) ue = X.h2d(dev + o_imgs, hd.data(), sizeof(PngImgDev) * m);
-            if (ue == hipSuccess) ue = X.h2d(d_rows, hrows.data(), sizeof(int2) * hrows.size());
+            if (ue == hipSuccess) ue = hipMemsetAsync(dev + o_err, 0, sizeof(int) * m, s);
             if (ue != hipSuccess) rc = hip_fail(ue, "PNG expand tables");
             hxst.resize(2 * hl.size());
-            mk[2] = now_ms();  // row table built, tables uploaded
+            mk[2] = now_ms();  // lane tables uploaded
             if (!rc) {
-                hipError_t e = hipMemsetAsync(dev + o_err, 0, sizeof(int) * m, s);
+                hipError_t e = hipSuccess;
                 rec(4, s);
                 if (e == hipSuccess) e = launch_png_expand(d_imgs, d_lanes, (int)hl.size(), d_tok, d_xst, s);
                 rec(5, s);
+                // page -> decoder that holds the page's first byte (resolve's lane lookup)
+                for (const auto& q : pj) {
+                    const PngJob& j = *J[q.first];
+                    const int64_t* ob = hob.data() + q.second;
+                    const size_t nl = (size_t)hd[q.first].nlanes;
+                    for (uint64_t pg = 0, ln = 0; pg <= (j.raw_total >> kPngPageShift); ++pg) {
+                        while (ln + 1 < nl && (uint64_t)ob[ln + 1] <= (pg << kPngPageShift)) ++ln;
+                        hpages.push_back((int)ln);
+                    }
+                    for (uint32_t y = 0; y < j.h; ++y) hrows.push_back(make_int2(q.first, (int)y));
+                }
+                if (e == hipSuccess) e = X.h2d(d_pages, hpages.data(), sizeof(int) * hpages.size());
+                if (e == hipSuccess) e = X.h2d(d_rows, hrows.data(), sizeof(int2) * hrows.size());
                 if (e == hipSuccess) e = launch_png_resolve(d_imgs, d_rows, (int)hrows.size(),
                                                             reinterpret_cast<int*>(dev + o_err), s);
                 rec(6, s);
