@@ -734,18 +734,31 @@ IK_HD void decode_lane_tok(const uint32_t* words, uint64_t nbits, uint64_t start
                         break;
                     }
                 }
-                // one token (literal rank) or two (match length, distance), without branches
+                // a second literal right behind a literal, decoded in the same step (about
+                // 92 % of the steps on image data): the bits after the first code, the same
+                // canonical decode; taken only when it is a literal (anything else -- a
+                // length, end of block, an invalid code -- is the next step's first symbol)
+                const uint32_t c15b = rev32((uint32_t)v1) >> 17;
+                const int L2 = canon_len(c15b, R.lpk);
+                const int Lc2 = L2 > 15 ? 15 : L2;
+                const uint32_t info2 = m[Lc2];
+                const uint32_t i2 = (c15b >> (15 - Lc2)) - (info2 & 0x7FFFu);
+                const bool dbl = lit && L2 <= 15 && i2 < ((info2 >> 15) & 0x1FFu);
+                // one token (literal rank), or two (two literal ranks; match length,
+                // distance), without branches
                 const uint32_t t1 = lit ? ((m[16 + Lc] >> 21) & 0x1FFu) + i : (kTokMatch | (uint32_t)(ll - 3));
+                const uint32_t t2 = lit ? ((m[16 + Lc2] >> 21) & 0x1FFu) + i2 : (uint32_t)(dist - 1);
+                const bool two = !lit || dbl;
                 const uint64_t a0 = (h0 >> 16) | (h1 << 48), a1 = (h1 >> 16) | ((uint64_t)t1 << 48);
-                const uint64_t b0 = (a0 >> 16) | (a1 << 48), b1 = (a1 >> 16) | ((uint64_t)(dist - 1) << 48);
+                const uint64_t b0 = (a0 >> 16) | (a1 << 48), b1 = (a1 >> 16) | ((uint64_t)t2 << 48);
                 const uint32_t tc1 = tc + 1;
-                const bool g1 = (tc1 & 7u) == 0, g2 = !lit && ((tc1 + 1) & 7u) == 0;  // a group of 8 completed
+                const bool g1 = (tc1 & 7u) == 0, g2 = two && ((tc1 + 1) & 7u) == 0;  // a group of 8 completed
                 if (g1 || g2) out.group(g1 ? tc1 - 8 : tc1 - 7, g1 ? a0 : b0, g1 ? a1 : b1);
-                h0 = lit ? a0 : b0;
-                h1 = lit ? a1 : b1;
-                tc = lit ? tc1 : tc1 + 1;
-                cnt += lit ? 1u : (uint64_t)ll;
-                W.advance(lit ? (uint32_t)Lc : (uint32_t)(Lc + le + Dc + de));
+                h0 = two ? b0 : a0;
+                h1 = two ? b1 : a1;
+                tc = two ? tc1 + 1 : tc1;
+                cnt += lit ? (dbl ? 2u : 1u) : (uint64_t)ll;
+                W.advance(lit ? (uint32_t)(dbl ? Lc + Lc2 : Lc) : (uint32_t)(Lc + le + Dc + de));
             }
             const bool bad = code == 2, full = code == 3;
             out.flush();
