@@ -457,34 +457,47 @@ IK_HD uint32_t tok_capacity(uint64_t bits, bool exact) {
 }
 
 // Token output of one lane: `p` = its region (16-byte aligned).  Complete groups
-// of 8 tokens are held back (pending) and stored by flush(): the GPU decoder
-// flushes only at its input ring's refill points, so that the wait there covers
-// exactly the ring's DMA (see ik_png.hip WinLds::tick).
+// of 8 tokens are held back (pending, at most two: a decode step adds up to three
+// tokens and the GPU flushes every four steps, so up to twelve tokens -- two groups
+// -- complete between flushes) and stored by flush(): the GPU decoder flushes only
+// at its input ring's refill points, so that the wait there covers exactly the
+// ring's DMA (see ik_png.hip WinLds::tick).
 struct TokOut {
     IK_GLOBAL uint16_t* p;
-    uint64_t p0 = 0, p1 = 0;
-    uint32_t ppos = 0;
-    bool pend = false;
+    uint64_t p0 = 0, p1 = 0, q0 = 0, q1 = 0;
+    uint32_t ppos = 0, qpos = 0;
+    int npend = 0;
     IK_HD void group(uint32_t pos, uint64_t lo, uint64_t hi) {
-        p0 = lo;
-        p1 = hi;
-        ppos = pos;
-        pend = true;
+        if (npend == 0) {
+            p0 = lo;
+            p1 = hi;
+            ppos = pos;
+        } else {
+            q0 = lo;
+            q1 = hi;
+            qpos = pos;
+        }
+        ++npend;
     }
-    IK_HD bool flush() {
-        if (!pend) return false;
+    IK_HD void store1(uint32_t pos, uint64_t lo, uint64_t hi) {
 #if defined(__HIP_DEVICE_COMPILE__)
         typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-        const u4 v = {(uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32)};
-        *reinterpret_cast<IK_GLOBAL u4*>(p + ppos) = v;  // one 16-byte store
+        const u4 v = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+        *reinterpret_cast<IK_GLOBAL u4*>(p + pos) = v;  // one 16-byte store
 #else
         for (int k = 0; k < 4; ++k) {
-            p[ppos + k] = (uint16_t)(p0 >> (16 * k));
-            p[ppos + 4 + k] = (uint16_t)(p1 >> (16 * k));
+            p[pos + k] = (uint16_t)(lo >> (16 * k));
+            p[pos + 4 + k] = (uint16_t)(hi >> (16 * k));
         }
 #endif
-        pend = false;
-        return true;
+    }
+    // stores the pending groups; returns how many (0, 1, 2)
+    IK_HD int flush() {
+        const int n = npend;
+        if (n >= 1) store1(ppos, p0, p1);
+        if (n >= 2) store1(qpos, q0, q1);
+        npend = 0;
+        return n;
     }
     IK_HD void table_byte(uint32_t tpos, int rank, uint8_t v) const {
         reinterpret_cast<IK_GLOBAL uint8_t*>(p + tpos)[rank] = v;
@@ -588,7 +601,11 @@ struct Win {
         wend = nwords;
         pos = bit;
     }
-    IK_HD void tick(TokOut& o) { o.flush(); }
+    uint32_t it = 0;
+    IK_HD void tick(TokOut& o) {  // every 4 steps, as the GPU's ring refill (ik_png.hip WinLds::tick)
+        if (++it % 4u) return;
+        o.flush();
+    }
     // x0 / x1 / x2 for a slide of 0 / 1 / 2 words, by masks: a ternary chain
     // becomes an indexed private array on the GPU (scratch memory)
     IK_HD static uint32_t sel3(uint32_t m1, uint32_t m2, uint32_t x0, uint32_t x1, uint32_t x2) {
@@ -723,17 +740,6 @@ IK_HD void decode_lane_tok(const uint32_t* words, uint64_t nbits, uint64_t start
                 int db, de;
                 dist_code((int)cm_byte(m, 32 + (int)(di < 29u ? di : 29u)), db, de);
                 const int dist = db + (int)((uint32_t)(v2 >> Dc) & ((1u << de) - 1u));
-                // the rare cases, one branch and one exit
-                const bool eobk = !lit && eob && i == nl;
-                const bool odd = L > 15 || (uint64_t)W.pos > plimit ||
-                                 (!lit && !eobk && (lr > 28u || D > 15 || di > 29u || (first && (int64_t)cnt < dist)));
-                if (odd || eobk || tc + 2 > tcap || cnt + 258 > out_cap) {
-                    code = odd ? 2 : eobk ? 1 : tc + 2 > tcap ? 3 : cnt + (lit ? 1u : (uint64_t)ll) > out_cap ? 2 : 0;
-                    if (code) {
-                        if (code == 1) W.advance((uint32_t)Lc);
-                        break;
-                    }
-                }
                 // a second literal right behind a literal, decoded in the same step (about
                 // 92 % of the steps on image data): the bits after the first code, the same
                 // canonical decode; taken only when it is a literal (anything else -- a
@@ -744,21 +750,44 @@ IK_HD void decode_lane_tok(const uint32_t* words, uint64_t nbits, uint64_t start
                 const uint32_t info2 = m[Lc2];
                 const uint32_t i2 = (c15b >> (15 - Lc2)) - (info2 & 0x7FFFu);
                 const bool dbl = lit && L2 <= 15 && i2 < ((info2 >> 15) & 0x1FFu);
-                // one token (literal rank), or two (two literal ranks; match length,
-                // distance), without branches
+                // and a third behind the second, the same way
+                const uint32_t c15c = rev32((uint32_t)(v1 >> Lc2)) >> 17;
+                const int L3 = canon_len(c15c, R.lpk);
+                const int Lc3 = L3 > 15 ? 15 : L3;
+                const uint32_t info3 = m[Lc3];
+                const uint32_t i3 = (c15c >> (15 - Lc3)) - (info3 & 0x7FFFu);
+                const bool tri = dbl && L3 <= 15 && i3 < ((info3 >> 15) & 0x1FFu);
+                // the rare cases, one branch and one exit
+                const bool eobk = !lit && eob && i == nl;
+                const bool odd = L > 15 || (uint64_t)W.pos > plimit ||
+                                 (!lit && !eobk && (lr > 28u || D > 15 || di > 29u || (first && (int64_t)cnt < dist)));
+                if (odd || eobk || tc + 3 > tcap || cnt + 258 > out_cap) {
+                    code = odd ? 2 : eobk ? 1 : tc + 3 > tcap ? 3
+                         : cnt + (lit ? (tri ? 3u : dbl ? 2u : 1u) : (uint64_t)ll) > out_cap ? 2 : 0;
+                    if (code) {
+                        if (code == 1) W.advance((uint32_t)Lc);
+                        break;
+                    }
+                }
+                // one token (literal rank), two (two literal ranks; match length,
+                // distance) or three (three literal ranks), without branches; three
+                // tokens complete at most one group of 8
                 const uint32_t t1 = lit ? ((m[16 + Lc] >> 21) & 0x1FFu) + i : (kTokMatch | (uint32_t)(ll - 3));
                 const uint32_t t2 = lit ? ((m[16 + Lc2] >> 21) & 0x1FFu) + i2 : (uint32_t)(dist - 1);
+                const uint32_t t3 = ((m[16 + Lc3] >> 21) & 0x1FFu) + i3;
                 const bool two = !lit || dbl;
                 const uint64_t a0 = (h0 >> 16) | (h1 << 48), a1 = (h1 >> 16) | ((uint64_t)t1 << 48);
                 const uint64_t b0 = (a0 >> 16) | (a1 << 48), b1 = (a1 >> 16) | ((uint64_t)t2 << 48);
+                const uint64_t e0 = (b0 >> 16) | (b1 << 48), e1 = (b1 >> 16) | ((uint64_t)t3 << 48);
                 const uint32_t tc1 = tc + 1;
-                const bool g1 = (tc1 & 7u) == 0, g2 = two && ((tc1 + 1) & 7u) == 0;  // a group of 8 completed
-                if (g1 || g2) out.group(g1 ? tc1 - 8 : tc1 - 7, g1 ? a0 : b0, g1 ? a1 : b1);
-                h0 = two ? b0 : a0;
-                h1 = two ? b1 : a1;
-                tc = two ? tc1 + 1 : tc1;
-                cnt += lit ? (dbl ? 2u : 1u) : (uint64_t)ll;
-                W.advance(lit ? (uint32_t)(dbl ? Lc + Lc2 : Lc) : (uint32_t)(Lc + le + Dc + de));
+                const bool g1 = (tc1 & 7u) == 0, g2 = two && ((tc1 + 1) & 7u) == 0, g3 = tri && ((tc1 + 2) & 7u) == 0;
+                if (g1 || g2 || g3)
+                    out.group(g1 ? tc1 - 8 : g2 ? tc1 - 7 : tc1 - 6, g1 ? a0 : g2 ? b0 : e0, g1 ? a1 : g2 ? b1 : e1);
+                h0 = tri ? e0 : two ? b0 : a0;
+                h1 = tri ? e1 : two ? b1 : a1;
+                tc = tri ? tc1 + 2 : two ? tc1 + 1 : tc1;
+                cnt += lit ? (tri ? 3u : dbl ? 2u : 1u) : (uint64_t)ll;
+                W.advance(lit ? (uint32_t)(Lc + (dbl ? Lc2 : 0) + (tri ? Lc3 : 0)) : (uint32_t)(Lc + le + Dc + de));
             }
             const bool bad = code == 2, full = code == 3;
             out.flush();

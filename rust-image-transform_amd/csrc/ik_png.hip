@@ -255,8 +255,10 @@ struct WinLds {
     // instruction, so the count in the wait is exact.
     __device__ void tick(infl::TokOut& o) {
         if (++it % kRingTick) return;
-        const bool st = o.flush();
-        if (__ballot(st))
+        const int st = o.flush();  // 0, 1 or 2 stores for this lane; the wave issued as many as its max
+        if (__ballot(st >= 2))
+            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else if (__ballot(st >= 1))
             asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
