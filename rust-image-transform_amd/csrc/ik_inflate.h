@@ -757,13 +757,20 @@ IK_HD void decode_lane_tok(const uint32_t* words, uint64_t nbits, uint64_t start
                 const uint32_t info3 = m[Lc3];
                 const uint32_t i3 = (c15c >> (15 - Lc3)) - (info3 & 0x7FFFu);
                 const bool tri = dbl && L3 <= 15 && i3 < ((info3 >> 15) & 0x1FFu);
+                // and a fourth (at most 60 bits for the four: within the 64-bit window)
+                const uint32_t c15q = rev32((uint32_t)((v1 >> Lc2) >> Lc3)) >> 17;
+                const int L4 = canon_len(c15q, R.lpk);
+                const int Lc4 = L4 > 15 ? 15 : L4;
+                const uint32_t info4 = m[Lc4];
+                const uint32_t i4 = (c15q >> (15 - Lc4)) - (info4 & 0x7FFFu);
+                const bool quad = tri && L4 <= 15 && i4 < ((info4 >> 15) & 0x1FFu);
                 // the rare cases, one branch and one exit
                 const bool eobk = !lit && eob && i == nl;
                 const bool odd = L > 15 || (uint64_t)W.pos > plimit ||
                                  (!lit && !eobk && (lr > 28u || D > 15 || di > 29u || (first && (int64_t)cnt < dist)));
-                if (odd || eobk || tc + 3 > tcap || cnt + 258 > out_cap) {
-                    code = odd ? 2 : eobk ? 1 : tc + 3 > tcap ? 3
-                         : cnt + (lit ? (tri ? 3u : dbl ? 2u : 1u) : (uint64_t)ll) > out_cap ? 2 : 0;
+                if (odd || eobk || tc + 4 > tcap || cnt + 258 > out_cap) {
+                    code = odd ? 2 : eobk ? 1 : tc + 4 > tcap ? 3
+                         : cnt + (lit ? (quad ? 4u : tri ? 3u : dbl ? 2u : 1u) : (uint64_t)ll) > out_cap ? 2 : 0;
                     if (code) {
                         if (code == 1) W.advance((uint32_t)Lc);
                         break;
@@ -775,19 +782,24 @@ IK_HD void decode_lane_tok(const uint32_t* words, uint64_t nbits, uint64_t start
                 const uint32_t t1 = lit ? ((m[16 + Lc] >> 21) & 0x1FFu) + i : (kTokMatch | (uint32_t)(ll - 3));
                 const uint32_t t2 = lit ? ((m[16 + Lc2] >> 21) & 0x1FFu) + i2 : (uint32_t)(dist - 1);
                 const uint32_t t3 = ((m[16 + Lc3] >> 21) & 0x1FFu) + i3;
+                const uint32_t t4 = ((m[16 + Lc4] >> 21) & 0x1FFu) + i4;
                 const bool two = !lit || dbl;
                 const uint64_t a0 = (h0 >> 16) | (h1 << 48), a1 = (h1 >> 16) | ((uint64_t)t1 << 48);
                 const uint64_t b0 = (a0 >> 16) | (a1 << 48), b1 = (a1 >> 16) | ((uint64_t)t2 << 48);
                 const uint64_t e0 = (b0 >> 16) | (b1 << 48), e1 = (b1 >> 16) | ((uint64_t)t3 << 48);
+                const uint64_t f0 = (e0 >> 16) | (e1 << 48), f1 = (e1 >> 16) | ((uint64_t)t4 << 48);
                 const uint32_t tc1 = tc + 1;
-                const bool g1 = (tc1 & 7u) == 0, g2 = two && ((tc1 + 1) & 7u) == 0, g3 = tri && ((tc1 + 2) & 7u) == 0;
-                if (g1 || g2 || g3)
-                    out.group(g1 ? tc1 - 8 : g2 ? tc1 - 7 : tc1 - 6, g1 ? a0 : g2 ? b0 : e0, g1 ? a1 : g2 ? b1 : e1);
-                h0 = tri ? e0 : two ? b0 : a0;
-                h1 = tri ? e1 : two ? b1 : a1;
-                tc = tri ? tc1 + 2 : two ? tc1 + 1 : tc1;
-                cnt += lit ? (tri ? 3u : dbl ? 2u : 1u) : (uint64_t)ll;
-                W.advance(lit ? (uint32_t)(Lc + (dbl ? Lc2 : 0) + (tri ? Lc3 : 0)) : (uint32_t)(Lc + le + Dc + de));
+                const bool g1 = (tc1 & 7u) == 0, g2 = two && ((tc1 + 1) & 7u) == 0, g3 = tri && ((tc1 + 2) & 7u) == 0,
+                           g4 = quad && ((tc1 + 3) & 7u) == 0;
+                if (g1 || g2 || g3 || g4)
+                    out.group(g1 ? tc1 - 8 : g2 ? tc1 - 7 : g3 ? tc1 - 6 : tc1 - 5, g1 ? a0 : g2 ? b0 : g3 ? e0 : f0,
+                              g1 ? a1 : g2 ? b1 : g3 ? e1 : f1);
+                h0 = quad ? f0 : tri ? e0 : two ? b0 : a0;
+                h1 = quad ? f1 : tri ? e1 : two ? b1 : a1;
+                tc = quad ? tc1 + 3 : tri ? tc1 + 2 : two ? tc1 + 1 : tc1;
+                cnt += lit ? (quad ? 4u : tri ? 3u : dbl ? 2u : 1u) : (uint64_t)ll;
+                W.advance(lit ? (uint32_t)(Lc + (dbl ? Lc2 : 0) + (tri ? Lc3 : 0) + (quad ? Lc4 : 0))
+                              : (uint32_t)(Lc + le + Dc + de));
             }
             const bool bad = code == 2, full = code == 3;
             out.flush();
