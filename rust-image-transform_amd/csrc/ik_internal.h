@@ -128,6 +128,9 @@ struct JpegHuffTables {
     int maxcode[8][18], valptr[8][17], mincode[8][17];
     int lj[8][17];  // left-justified 16-bit bound of the codes up to each length (carried over empty lengths)
     uint8_t vals[8][256];
+    // AC codes whose code + magnitude bits fit the 9-bit lookahead, decoded in one
+    // lookup (entry: value << 8 | run << 4 | bits; 0 = take the general path)
+    int16_t fast_ac[4][512];
 };
 struct JpegScanArgs {
     const uint8_t* data;          // the scan's entropy-coded bytes (stuffed, with RST markers)

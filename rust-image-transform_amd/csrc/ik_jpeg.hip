@@ -455,6 +455,15 @@ __device__ void huff_interval(const JpegScanArgs& a, const JpegHuffTables& T, co
                     pred[ci] += t ? extend_dev(br.get(t), t) : 0;
                     blk[0] = (int16_t)pred[ci];
                     for (int k = 1; k < 64;) {
+                        const int fa = T.fast_ac[a.ta[ci]][br.peek(9)];
+                        if (fa) {  // short code + magnitude in one lookup
+                            k += (fa >> 4) & 15;
+                            br.skip(fa & 15);
+                            if (k > 63) { atomicOr(a.err, 4); return; }
+                            blk[s_zz[k]] = (int16_t)(fa >> 8);
+                            ++k;
+                            continue;
+                        }
                         const int rs = decode_sym(br, T, 4 + a.ta[ci]);
                         if (rs < 0) { atomicOr(a.err, 2); return; }
                         const int r = rs >> 4, sz = rs & 15;
@@ -557,6 +566,15 @@ __device__ bool seq_block(SeqBits& br, const JpegHuffTables& T, const uint8_t* z
     if (t < 0 || t > 11) return false;
     *dcdiff = t ? extend_dev(seq_get(br, t), t) : 0;
     for (int k = 1; k < 64;) {
+        const int fa = T.fast_ac[ta][br.peek32() >> 23];
+        if (fa) {  // short code + magnitude in one lookup
+            k += (fa >> 4) & 15;
+            br.pos += fa & 15;
+            if (k > 63) return false;
+            if (blk) blk[zz[k]] = (int16_t)(fa >> 8);
+            ++k;
+            continue;
+        }
         const int rs = seq_sym(br, T, 4 + ta);
         if (rs < 0) return false;
         const int r = rs >> 4, sz = rs & 15;

@@ -421,6 +421,15 @@ struct Decoder {
                 if (h.maxcode[l] >= 0) carry = (h.maxcode[l] + 1) << (16 - l);
                 t.lj[k][l] = carry;
             }
+            if (k < 4) continue;
+            for (int i = 0; i < 512; ++i) {  // run/size code and its magnitude bits in one lookup
+                const int L = h.look_len[i], rs = h.look_val[i], r = rs >> 4, sz = rs & 15;
+                if (!L || !sz || L + sz > 9) continue;
+                const int v = (i >> (9 - L - sz)) & ((1 << sz) - 1);
+                const int val = v < (1 << (sz - 1)) ? v - (1 << sz) + 1 : v;
+                if (val < -128 || val > 127) continue;
+                t.fast_ac[k - 4][i] = (int16_t)(val * 256 + r * 16 + L + sz);
+            }
         }
     }
 
