@@ -698,6 +698,53 @@ int resize_target(uint32_t W, uint32_t H, int64_t w, int64_t h, uint32_t* onw, u
     return IK_OK;
 }
 
+// encode_image's device front end for n same-geometry 8-bit images going to WebP
+// through libwebp: ONE colour-conversion launch over per-image base pointers,
+// writing every image's YUV420 planes straight into pinned host memory; prep[i]
+// gets the planes for encode_host_back.  Returns IK_ERR_UNSUPPORTED (nothing
+// done) when the per-image path applies instead (the GPU VP8 encoder, > 16383).
+int webp_front_group(const std::vector<ik_image*>& imgs, int quality, std::vector<EncodePrep*>& prep) {
+    const size_t n = imgs.size();
+    if (!n) return IK_OK;
+    const ik_image* i0 = imgs[0];
+    if (default_webp_encoder() == IK_WEBP_GPU || i0->w > 16383 || i0->h > 16383 || i0->depth != 1)
+        return IK_ERR_UNSUPPORTED;
+    DeviceGuard g(i0->device);
+    const DeviceConsts* dc = device_consts(current_device());
+    if (!dc) return fail(IK_ERR_DEVICE, "cannot upload WebP tables");
+    const uint32_t w = i0->w, h = i0->h;
+    const size_t uvw = (w + 1) / 2, uvh = (h + 1) / 2, bytes = (size_t)w * h + 2 * uvw * uvh;
+    const size_t stride = (bytes + 255) & ~size_t(255);
+    uint8_t* hp = pinned_slot(4, stride * n + 16 * n + 256);
+    void* dhp = nullptr;
+    if (!hp || hipHostGetDevicePointer(&dhp, hp, 0) != hipSuccess || !dhp)
+        return fail(IK_ERR_NOMEM, "cannot map pinned WebP planes");
+    uint64_t* dtab = reinterpret_cast<uint64_t*>(scratch_slot(3, sizeof(uint64_t) * n));
+    if (!dtab) return fail(IK_ERR_DEVICE, "cannot allocate device scratch");
+    hipStream_t s = thread_stream();
+    (void)hipStreamSynchronize(s);  // nothing pending reads the pinned area
+    uint64_t* htab = reinterpret_cast<uint64_t*>(hp + stride * n);
+    for (size_t i = 0; i < n; ++i) htab[i] = (uint64_t)(uintptr_t)imgs[i]->d;
+    hipError_t e = launch_copy_words(reinterpret_cast<const uint32_t*>(reinterpret_cast<uint8_t*>(dhp) + stride * n),
+                                     reinterpret_cast<uint32_t*>(dtab), 2 * n, s);
+    if (e == hipSuccess)
+        e = launch_webp_yuv420(nullptr, (int)w, (int)h, (int)i0->c, i0->pitch, 0, reinterpret_cast<uint8_t*>(dhp), stride,
+                               (int)n, dc->gamma_to_lin, dc->lin_to_gamma, s, dtab);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "webp yuv420 (batched)");
+    const int q = quality < 1 ? 1 : (quality > 100 ? 100 : quality);
+    for (size_t i = 0; i < n; ++i) {
+        EncodePrep& p = *prep[i];
+        p.fmt = IK_FORMAT_WEBP;
+        p.q = q;
+        p.w = w;
+        p.h = h;
+        p.planes.assign(hp + stride * i, hp + stride * i + bytes);
+        p.done = false;
+    }
+    return IK_OK;
+}
+
 // imageops::resize over n 8-bit images of one geometry (same W, H, C, pitch) in
 // ONE fused launch: the kernel reads each image's base pointer from a table, so
 // the images may sit anywhere.  Same arithmetic as ik_resize_exact, per image.
@@ -996,6 +1043,7 @@ static void transform_device_phase(const uint8_t* const* bytes, const size_t* le
     // requests whose decoded images share a geometry and an output size resize in
     // one launch (resize_group); the rest, image by image below
     std::vector<ik_image*> rsz(m, nullptr);
+    std::vector<char> fronted(m, 0);  // encode front end already run (batched WebP colour conversion)
     {
         std::map<std::tuple<uint32_t, uint32_t, uint32_t, size_t, int, uint32_t, uint32_t>, std::vector<uint32_t>> groups;
         for (uint32_t k = 0; k < m; ++k) {
@@ -1012,8 +1060,20 @@ static void transform_device_phase(const uint8_t* const* bytes, const size_t* le
             if (kv.second.size() < 2) continue;
             std::vector<ik_image*> src, out;
             for (uint32_t k : kv.second) src.push_back(imgs[k]);
-            if (resize_group(src, std::get<5>(kv.first), std::get<6>(kv.first), filter, out) == IK_OK)
-                for (size_t j = 0; j < out.size(); ++j) rsz[kv.second[j]] = out[j];
+            if (resize_group(src, std::get<5>(kv.first), std::get<6>(kv.first), filter, out) != IK_OK) continue;
+            for (size_t j = 0; j < out.size(); ++j) rsz[kv.second[j]] = out[j];
+            // the group's WebP requests of one quality: one colour-conversion launch
+            std::map<int, std::vector<uint32_t>> byq;
+            for (uint32_t k : kv.second)
+                if (fmt[idx[k]] == IK_FORMAT_WEBP) byq[quality[idx[k]]].push_back(k);
+            for (auto& qv : byq) {
+                if (qv.second.size() < 2) continue;
+                std::vector<ik_image*> im;
+                std::vector<EncodePrep*> pp;
+                for (uint32_t k : qv.second) { im.push_back(rsz[k]); pp.push_back(&prep[k]); }
+                if (webp_front_group(im, qv.first, pp) == IK_OK)
+                    for (uint32_t k : qv.second) fronted[k] = 1;
+            }
         }
         t_resize += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
@@ -1024,7 +1084,7 @@ static void transform_device_phase(const uint8_t* const* bytes, const size_t* le
         const auto t0 = std::chrono::steady_clock::now();
         int r = rs ? IK_OK : ik_resize(imgs[k], w[i], h[i], filter, &rs);
         const auto t1 = std::chrono::steady_clock::now();
-        if (!r) r = encode_image_front(rs, fmt[i], quality[i], prep[k], bytes_out[k]);
+        if (!r && !fronted[k]) r = encode_image_front(rs, fmt[i], quality[i], prep[k], bytes_out[k]);
         if (timing) {
             const auto t2 = std::chrono::steady_clock::now();
             std::lock_guard<std::mutex> lk(tmu);

@@ -93,7 +93,8 @@ size_t resize_lds_bytes(const ResizeArgs& a, bool wl, int flush);
 hipError_t launch_webp_yuv420(const uint8_t* src, int w, int h, int C, size_t pitch,
                               size_t img_stride, uint8_t* yuv /* Y, U, V planes per image */,
                               size_t yuv_img_stride, int n, const uint16_t* gamma_to_lin,
-                              const int* lin_to_gamma, hipStream_t s);
+                              const int* lin_to_gamma, hipStream_t s,
+                              const uint64_t* src_tab = nullptr /* per-image bases instead of img_stride */);
 // n images; planes (Y, U, V, A: w*h each) plane_img_stride apart; transparent[n]
 // zeroed here, then set to 1 for every image with an alpha < 255
 hipError_t launch_avif_yuv444(const uint8_t* src, int w, int h, int C, size_t pitch, size_t img_stride,

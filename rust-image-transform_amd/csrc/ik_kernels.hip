@@ -485,7 +485,8 @@ __global__ __launch_bounds__(kThreads) void k_webp_yuv420(const uint8_t* __restr
                                                           size_t img_stride, uint8_t* __restrict__ Y,
                                                           size_t yuv_img_stride,
                                                           const uint16_t* __restrict__ g2l,
-                                                          const int* __restrict__ l2g) {
+                                                          const int* __restrict__ l2g,
+                                                          const uint64_t* __restrict__ src_tab) {
     __shared__ uint16_t s_g2l[256];
     __shared__ int s_l2g[33];
     for (int t = threadIdx.x; t < 256; t += kThreads) s_g2l[t] = g2l[t];
@@ -496,7 +497,8 @@ __global__ __launch_bounds__(kThreads) void k_webp_yuv420(const uint8_t* __restr
     const int cy = blockIdx.y * 4 + (threadIdx.x >> 6);
     const int img = blockIdx.z;
     if (cx >= uvw || cy >= uvh) return;
-    const uint8_t* __restrict__ base = src + (size_t)img * img_stride;
+    const uint8_t* __restrict__ base =
+        src_tab ? reinterpret_cast<const uint8_t*>(src_tab[img]) : src + (size_t)img * img_stride;
     uint8_t* __restrict__ y_img = Y + (size_t)img * yuv_img_stride;
     uint8_t* __restrict__ u_img = y_img + (size_t)w * h;
     uint8_t* __restrict__ v_img = u_img + (size_t)uvw * uvh;
@@ -539,11 +541,11 @@ __global__ __launch_bounds__(kThreads) void k_webp_yuv420(const uint8_t* __restr
 
 hipError_t launch_webp_yuv420(const uint8_t* src, int w, int h, int C, size_t pitch,
                               size_t img_stride, uint8_t* yuv, size_t yuv_img_stride, int n, const uint16_t* gamma_to_lin,
-                              const int* lin_to_gamma_tab, hipStream_t s) {
+                              const int* lin_to_gamma_tab, hipStream_t s, const uint64_t* src_tab) {
     const int uvw = (w + 1) >> 1, uvh = (h + 1) >> 1;
     dim3 grid((uvw + 63) / 64, (uvh + 3) / 4, n);
     hipLaunchKernelGGL(k_webp_yuv420, grid, dim3(kThreads), 0, s, src, w, h, C, pitch, img_stride,
-                       yuv, yuv_img_stride, gamma_to_lin, lin_to_gamma_tab);
+                       yuv, yuv_img_stride, gamma_to_lin, lin_to_gamma_tab, src_tab);
     return hipGetLastError();
 }
 

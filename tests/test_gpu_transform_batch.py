@@ -72,6 +72,25 @@ def test_batch_error_message_is_the_decoders_own(ik):
     assert "item 1" in str(ei.value) and "Png" in str(ei.value)
 
 
+def test_same_geometry_groups_equal_single_requests(ik):
+    """Requests sharing a decoded geometry and an output size resize in one launch
+    (resize_group) and, for WebP, convert colour in one launch (webp_front_group);
+    every request's bytes must equal its own ik_transform, across qualities, formats
+    and channel counts."""
+    blobs = []
+    for k, c in enumerate((4, 3, 4)):
+        buf = io.BytesIO()
+        Image.fromarray(ikutil.synth(333, 250, c, seed=40 + k, pattern="S")).save(buf, format="PNG")
+        blobs.append(buf.getvalue())
+    datas = [blobs[0], blobs[2], blobs[0], blobs[2], blobs[1], blobs[1], blobs[0], blobs[2]]
+    sizes = [(160, None)] * 4 + [(None, 100)] * 2 + [(160, None), (160, None)]
+    fmts = [ImageFormat.webp] * 6 + [ImageFormat.jpeg, ImageFormat.webp]
+    qs = [80, 80, 80, 75, 80, 80, 85, 80]
+    got = transform_batch(datas, sizes, fmts, qs, threads=4)
+    for b, (w, h), f, q, g in zip(datas, sizes, fmts, qs, got):
+        assert g == _single(ik, b, w, h, f, q)
+
+
 def test_submitted_batches_equal_blocking_batches(ik):
     """ik_transform_batch_submit / _wait (pipelined batches: the next batch's device
     half runs while the previous one's host coders finish): same bytes as the
