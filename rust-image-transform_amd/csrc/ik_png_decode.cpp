@@ -22,6 +22,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <memory>
 #include <mutex>
 #include <cmath>
 #include <cstdlib>
@@ -435,27 +436,71 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
         double t_stage1 = t_stage0;
         if (!rc) {
             rec(0, s);
-            parallel_for(m, 0, [&, s, sc](int k) {
-                PngJob& j = *J[k];
-                uint8_t* d = pin + j.z_off;
-                for (auto& seg : j.idat) {
-                    if (png_chunk_crc(seg.first - 4, seg.first, seg.second) != be32(seg.first + seg.second)) crc_bad[k] = 1;
-                    std::memcpy(d, seg.first, seg.second);
-                    d += seg.second;
+            // the first streams go up in pieces of <= kPiece bytes, so the PCIe transfer
+            // starts after one piece is staged instead of after whole 35-MB streams
+            // (measured: 5.5 ms from a batch's start to its first copy); the thread
+            // that finishes a stream's last piece records its event, launches its
+            // block search and then checks its CRCs; whole streams check their CRCs
+            // while staging, as before
+            constexpr size_t kPiece = size_t(4) << 20;
+            constexpr int kPieced = 2;
+            struct Piece { int k; size_t lo, n; };
+            std::vector<Piece> pieces;
+            std::vector<std::vector<size_t>> seg_off(m);  // logical start of each IDAT segment (pieced streams)
+            std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[m]);
+            for (int k = 0; k < m; ++k) {
+                const PngJob& j = *J[k];
+                const size_t tot = ((j.zlen + 3) & ~size_t(3)) + kPad;
+                const size_t piece = k < kPieced ? kPiece : tot;
+                int np = 0;
+                for (size_t lo = 0; lo < tot; lo += piece, ++np) pieces.push_back(Piece{k, lo, std::min(piece, tot - lo)});
+                left[k] = np;
+                if (np > 1) {
+                    size_t o = 0;
+                    for (auto& seg : j.idat) { seg_off[k].push_back(o); o += seg.second; }
                 }
-                const size_t wb = (j.zlen + 3) & ~size_t(3);
-                std::memset(d, 0, pin + j.z_off + wb + kPad - d);
-                // one plain copy per stream, with its zero padding (no memset kernel
-                // ahead of it, which would wait for a CU while other kernels run)
+            }
+            parallel_for((int)pieces.size(), 0, [&, s, sc](int pi) {
+                const Piece P = pieces[pi];
+                const int k = P.k;
+                const PngJob& j = *J[k];
+                const bool whole = P.lo == 0 && seg_off[k].empty();
+                uint8_t* d = pin + j.z_off + P.lo;
+                if (whole) {
+                    for (auto& seg : j.idat) {
+                        if (png_chunk_crc(seg.first - 4, seg.first, seg.second) != be32(seg.first + seg.second)) crc_bad[k] = 1;
+                        std::memcpy(d, seg.first, seg.second);
+                        d += seg.second;
+                    }
+                    std::memset(d, 0, pin + j.z_off + P.n - d);
+                } else {
+                    const std::vector<size_t>& so = seg_off[k];
+                    size_t lo = P.lo, n = P.n;
+                    size_t si = (size_t)(std::upper_bound(so.begin(), so.end(), lo) - so.begin()) - 1;
+                    while (n && lo < j.zlen) {
+                        const size_t in = lo - so[si], c = std::min(n, (size_t)j.idat[si].second - in);
+                        std::memcpy(d, j.idat[si].first + in, c);
+                        d += c; lo += c; n -= c; ++si;
+                    }
+                    if (n) std::memset(d, 0, n);
+                }
+                // one plain copy per piece (no memset kernel ahead of it, which would
+                // wait for a CU while other kernels run)
                 const double tc0 = timing ? now_ms() : 0.0;
-                hipError_t e = hipMemcpyAsync(dev + j.o_words, pin + j.z_off, wb + kPad, hipMemcpyHostToDevice, sc);
+                hipError_t e = hipMemcpyAsync(dev + j.o_words + P.lo, pin + j.z_off + P.lo, P.n, hipMemcpyHostToDevice, sc);
                 if (timing) t_copy_calls += (long long)(1000.0 * (now_ms() - tc0));
-                if (early) {
-                    if (e == hipSuccess) e = hipEventRecord(ev_landed[k], sc);
-                    if (e == hipSuccess) e = hipStreamWaitEvent(s, ev_landed[k], 0);
-                    if (e == hipSuccess)
-                        e = launch_png_find(d_imgs, d_cimg + j.chunk0, d_cidx + j.chunk0, j.nchunks, cbits,
-                                            d_cand + j.chunk0, s);
+                if (left[k].fetch_sub(1) == 1) {  // the stream is all queued
+                    if (early) {
+                        if (e == hipSuccess) e = hipEventRecord(ev_landed[k], sc);
+                        if (e == hipSuccess) e = hipStreamWaitEvent(s, ev_landed[k], 0);
+                        if (e == hipSuccess)
+                            e = launch_png_find(d_imgs, d_cimg + j.chunk0, d_cidx + j.chunk0, j.nchunks, cbits,
+                                                d_cand + j.chunk0, s);
+                    }
+                    if (!whole)
+                        for (auto& seg : j.idat)
+                            if (png_chunk_crc(seg.first - 4, seg.first, seg.second) != be32(seg.first + seg.second))
+                                crc_bad[k] = 1;
                 }
                 if (e != hipSuccess) up_err = (int)e;
             });
