@@ -123,6 +123,9 @@ int ik_png_last_timing(double *out, int n);
 /* process-wide counts of PNG streams decoded since load: out[0] by the GPU path,
  * out[1] by the host decoder (outside the GPU path, or rejected by it) */
 int ik_png_counters(unsigned long long *out);
+/* process-wide JPEG counters: out[0] = streams whose entropy decoding ran on the
+ * GPU (restart intervals or self-synchronising scans), out[1] = on the host */
+int ik_jpeg_counters(unsigned long long *out);
 
 /* resize_image (src/transform.rs:62-90).  w/h < 0 mean None.  Both None returns
  * the input unchanged (*out == img); otherwise a new image (img is not freed:
@@ -167,8 +170,13 @@ int ik_encode(const ik_image *img, int fmt, int quality, uint8_t **out, size_t *
 typedef enum { IK_WEBP_LIBWEBP = 0, IK_WEBP_GPU = 1 } ik_webp_encoder;
 int ik_set_webp_encoder(int encoder); /* process-wide, for ik_encode / ik_transform */
 /* version of the libwebp that codes WebP (WebPGetEncoderVersion, e.g. 0x010600),
- * -1 when none could be loaded; IK_LIBWEBP=<path> picks a specific copy */
+ * -1 when none could be loaded.  The codec libraries are explicit dependencies:
+ * IK_LIBWEBP=<path> / IK_LIBAVIF=<path> when set, else the system sonames
+ * libwebp.so.7 / libavif.so.16 through the dynamic loader (no other search). */
 int ik_libwebp_version(void);
+/* path of the library that codes fmt (IK_FORMAT_WEBP / IK_FORMAT_AVIF) into buf
+ * (NUL-terminated, truncated to cap); returns its length, 0 when none loaded */
+size_t ik_codec_library(int fmt, char *buf, size_t cap);
 int ik_get_webp_encoder(void);
 
 /* ---- fused / batched entry points (pixels stay in HBM) ----------------- */

@@ -46,31 +46,30 @@ struct WebPApi {
     void (*writer_init)(void*) = nullptr;
     void (*writer_clear)(void*) = nullptr;
     int version = 0;  // WebPGetEncoderVersion(): 0x010600 = 1.6.0
+    std::string path;  // the file the loader mapped
     bool ok = false;
     std::string err;
 };
 
-// libwebp candidates: $IK_LIBWEBP, then the libwebp bundled with Pillow (1.6.0 in
-// this image; its libsharpyuv sibling is loaded first, RTLD_GLOBAL), then the
-// system libwebp.so.7 (1.2.2).  The two give identical lossy bytes on every test
-// input (both are checked against the oracle, which loads the system copy) and
-// 1.6.0 codes a 512^2 frame ~8 % faster.
+// The codec libraries are explicit dependencies of the product library: the path
+// in $IK_LIBWEBP (resp. $IK_LIBAVIF) when set, else the system soname through the
+// dynamic loader.  Nothing is searched for in other packages' directories.  A
+// libwebp >= 1.3 built as separate objects needs its libsharpyuv: a
+// libsharpyuv*.so* next to $IK_LIBWEBP is loaded first (RTLD_GLOBAL).  libwebp
+// 1.2.2 (system) and 1.6.0 give identical lossy bytes on every test input (both
+// are checked against the oracle, which loads the system copy); 1.6.0 codes a
+// 512^2 frame ~8 % faster.  ik_libwebp_version() reports the one loaded.
 void* open_libwebp() {
     std::vector<std::string> cands;
-    if (const char* e = getenv("IK_LIBWEBP")) cands.push_back(e);
-    for (const char* dir : {"/usr/local/lib/python3*/dist-packages/pillow.libs", "/usr/lib/python3*/dist-packages/pillow.libs",
-                            "/usr/local/lib/python3*/site-packages/pillow.libs"}) {
-        glob_t g{};
-        if (glob((std::string(dir) + "/libwebp-*.so*").c_str(), 0, nullptr, &g) == 0)
-            for (size_t i = 0; i < g.gl_pathc; ++i) cands.push_back(g.gl_pathv[i]);
-        globfree(&g);
+    if (const char* e = getenv("IK_LIBWEBP")) {
+        if (*e) cands.push_back(e);
     }
     cands.push_back("libwebp.so.7");
     for (const auto& c : cands) {
         const size_t slash = c.rfind('/');
-        if (slash != std::string::npos && c.find("pillow.libs") != std::string::npos) {
+        if (slash != std::string::npos) {
             glob_t g{};
-            if (glob((c.substr(0, slash) + "/libsharpyuv-*.so*").c_str(), 0, nullptr, &g) == 0 && g.gl_pathc)
+            if (glob((c.substr(0, slash) + "/libsharpyuv*.so*").c_str(), 0, nullptr, &g) == 0 && g.gl_pathc)
                 dlopen(g.gl_pathv[0], RTLD_NOW | RTLD_GLOBAL);
             globfree(&g);
         }
@@ -92,7 +91,8 @@ const WebPApi& webp_api() {
     static std::once_flag once;
     std::call_once(once, [] {
         api.lib = open_libwebp();
-        if (!api.lib) { api.err = "libwebp.so.7 not found"; return; }
+        if (!api.lib) { api.err = "libwebp.so.7 not found (set IK_LIBWEBP to a libwebp path)"; return; }
+        if (Dl_info di{}; dladdr(dlsym(api.lib, "WebPEncode"), &di) && di.dli_fname) api.path = di.dli_fname;
         if (auto ver = (int (*)())dlsym(api.lib, "WebPGetEncoderVersion")) api.version = ver();
         api.config_init = (int (*)(void*, int, float, int))dlsym(api.lib, "WebPConfigInitInternal");
         api.picture_init = (int (*)(void*, int))dlsym(api.lib, "WebPPictureInitInternal");
@@ -132,6 +132,10 @@ extern "C" int ik_libwebp_version(void) {
     const WebPApi& api = webp_api();
     return api.ok ? api.version : -1;
 }
+
+namespace ik {
+const std::string& libwebp_path() { return webp_api().path; }
+}  // namespace ik
 
 int webp_encode_yuv420(const uint8_t* y, const uint8_t* u, const uint8_t* v, int w, int h,
                        float quality, std::vector<uint8_t>& out) {
@@ -370,6 +374,7 @@ struct AvifApi {
     void (*encoder_destroy)(void*) = nullptr;
     int (*encoder_write)(void*, const void*, void*) = nullptr;
     void (*rwdata_free)(void*) = nullptr;
+    std::string path;  // the file the loader mapped
     bool ok = false;
     std::string err;
 };
@@ -385,19 +390,18 @@ const AvifApi& avif_api() {
     static std::once_flag once;
     std::call_once(once, [] {
         std::vector<std::string> cands;
-        if (const char* e = getenv("IK_LIBAVIF")) cands.push_back(e);
-        cands.push_back("libavif.so.16");
-        for (const char* pat : {"/usr/local/lib/python3*/dist-packages/pillow.libs/libavif-*.so*",
-                                "/usr/lib/python3*/dist-packages/pillow.libs/libavif-*.so*",
-                                "/usr/local/lib/python3*/site-packages/pillow.libs/libavif-*.so*"}) {
-            glob_t g{};
-            if (glob(pat, 0, nullptr, &g) == 0)
-                for (size_t i = 0; i < g.gl_pathc; ++i) cands.push_back(g.gl_pathv[i]);
-            globfree(&g);
+        // explicit dependency, as libwebp above: $IK_LIBAVIF, else the system soname
+        if (const char* e = getenv("IK_LIBAVIF")) {
+            if (*e) cands.push_back(e);
         }
+        cands.push_back("libavif.so.16");
         for (const auto& c : cands)
             if ((api.lib = dlopen(c.c_str(), RTLD_NOW | RTLD_LOCAL))) break;
-        if (!api.lib) { api.err = "libavif (with an AV1 encoder) not found"; return; }
+        if (!api.lib) {
+            api.err = "libavif (with an AV1 encoder) not found: install libavif.so.16 or set IK_LIBAVIF to its path";
+            return;
+        }
+        if (Dl_info di{}; dladdr(dlsym(api.lib, "avifVersion"), &di) && di.dli_fname) api.path = di.dli_fname;
         api.image_create = (void* (*)(uint32_t, uint32_t, uint32_t, int))dlsym(api.lib, "avifImageCreate");
         api.image_alloc = (int (*)(void*, int))dlsym(api.lib, "avifImageAllocatePlanes");
         api.image_destroy = (void (*)(void*))dlsym(api.lib, "avifImageDestroy");
@@ -436,6 +440,19 @@ const AvifApi& avif_api() {
 }
 
 }  // namespace
+
+// the file behind an encoder, for reports: fmt IK_FORMAT_WEBP / IK_FORMAT_AVIF
+extern "C" size_t ik_codec_library(int fmt, char* buf, size_t cap) {
+    std::string p;
+    if (fmt == IK_FORMAT_WEBP) p = webp_api().ok ? webp_api().path : std::string();
+    else if (fmt == IK_FORMAT_AVIF) p = avif_api().ok ? avif_api().path : std::string();
+    if (buf && cap) {
+        const size_t n = p.size() < cap - 1 ? p.size() : cap - 1;
+        std::memcpy(buf, p.data(), n);
+        buf[n] = 0;
+    }
+    return p.size();
+}
 
 int avif_encode_yuv444(const uint8_t* planes, bool has_alpha, int w, int h, int quality, int speed,
                        std::vector<uint8_t>& out) {

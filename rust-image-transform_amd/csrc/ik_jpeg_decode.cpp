@@ -864,6 +864,9 @@ int run_seq(const Decoder& d, const uint8_t* dtabs, int16_t* dcoef, uint8_t* dev
 // try_gpu: baseline scans with restart intervals are entropy-decoded on the GPU
 // (k_jpeg_huff); anything else, and any stream the GPU finds a bad code in, goes
 // through the host decoder
+// process-wide: JPEG streams whose entropy decoding ran on the GPU / on the host
+std::atomic<unsigned long long> g_jpeg_gpu_streams{0}, g_jpeg_host_streams{0};
+
 int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gpu) {
     static const bool timing = getenv("IK_JPEG_TIMING") != nullptr;  // dev: phase times to stderr
     auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
@@ -956,6 +959,7 @@ int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gp
     if (timing)
         fprintf(stderr, "[jpeg] %s: parse %.2f alloc %.2f entropy/upload %.2f reconstruct %.2f ms\n",
                 gpu ? "gpu entropy" : "host entropy", t1 - t0, t2 - t1, t3 - t2, now() - t3);
+    (gpu ? g_jpeg_gpu_streams : g_jpeg_host_streams) += 1;
     *out = img;
     return IK_OK;
 }
@@ -1081,6 +1085,9 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
                 if (!errs[k]) host_idx.push_back(i);
                 st[i] = IK_OK;
             }
+        } else {
+            for (int k = 0; k < m; ++k)
+                if (outs[gpu_idx[k]]) g_jpeg_gpu_streams += 1;
         }
         (void)hdr;
     }
@@ -1126,5 +1133,12 @@ int ik_set_jpeg_reconstruction(int mode) {
 }
 
 int ik_get_jpeg_reconstruction(void) { return ik::jpeg_recon_mode(); }
+
+int ik_jpeg_counters(unsigned long long* out) {
+    if (!out) return ik::fail(IK_ERR_INVALID, "null pointer");
+    out[0] = ik::g_jpeg_gpu_streams.load();
+    out[1] = ik::g_jpeg_host_streams.load();
+    return IK_OK;
+}
 
 }  // extern "C"

@@ -45,6 +45,7 @@ SIGNATURES = [
     ("ik_transform", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]),
     ("ik_set_webp_encoder", ctypes.c_int, [ctypes.c_int]),
     ("ik_libwebp_version", ctypes.c_int, []),
+    ("ik_codec_library", ctypes.c_size_t, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
     ("ik_get_webp_encoder", ctypes.c_int, []),
     ("ik_pipeline_set_webp_encoder", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("ik_webp_encode_gpu_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]),
@@ -58,6 +59,7 @@ SIGNATURES = [
     ("ik_set_png_gpu_min", ctypes.c_int, [ctypes.c_longlong]),
     ("ik_png_last_timing", ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     ("ik_png_counters", ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
+    ("ik_jpeg_counters", ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
     ("ik_get_resize_mode", ctypes.c_int, []),
     ("ik_set_jpeg_reconstruction", ctypes.c_int, [ctypes.c_int]),
     ("ik_get_jpeg_reconstruction", ctypes.c_int, []),

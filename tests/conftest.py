@@ -12,6 +12,8 @@ for p in (ROOT, PKG, os.path.dirname(os.path.abspath(__file__))):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+    import ikutil
+    ikutil.use_pillow_codecs()  # the codec libraries are explicit: Pillow's copies, named
 
 
 @pytest.fixture(scope="session")

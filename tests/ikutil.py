@@ -17,6 +17,34 @@ u8p = ctypes.POINTER(ctypes.c_uint8)
 NEAREST, TRIANGLE, CATMULLROM, GAUSSIAN, LANCZOS3 = range(5)
 
 
+def pillow_codec_libs() -> dict:
+    """Paths of the libwebp / libavif copies bundled with Pillow in this image.
+
+    The product library loads its codecs only from IK_LIBWEBP / IK_LIBAVIF or the
+    system sonames (the image has libwebp.so.7 1.2.2 and no system libavif); the
+    harness (tests, bench, tools) names Pillow's copies explicitly, so AVIF can be
+    coded here and the WebP byte tests compare libwebp 1.6.0 with the oracle's
+    system 1.2.2."""
+    import glob
+    import PIL
+    d = os.path.join(os.path.dirname(os.path.dirname(PIL.__file__)), "pillow.libs")
+    out = {}
+    for key, pat in (("IK_LIBWEBP", "libwebp-*.so*"), ("IK_LIBAVIF", "libavif-*.so*")):
+        hits = sorted(glob.glob(os.path.join(d, pat)))
+        if hits:
+            out[key] = hits[0]
+    return out
+
+
+def use_pillow_codecs() -> dict:
+    """Point IK_LIBWEBP / IK_LIBAVIF at Pillow's copies unless already set (call
+    before the first encode: the library reads them once)."""
+    libs = pillow_codec_libs()
+    for k, v in libs.items():
+        os.environ.setdefault(k, v)
+    return {k: os.environ.get(k) for k in ("IK_LIBWEBP", "IK_LIBAVIF")}
+
+
 def build_oracle() -> str:
     if not os.path.exists(ORACLE_SO):
         subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True,

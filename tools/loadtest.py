@@ -36,6 +36,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "rust-image-transform_amd"), os.path.join(ROOT, "tests")]
+import ikutil  # noqa: E402
+
+ikutil.use_pillow_codecs()  # codec libraries named explicitly (IK_LIBWEBP / IK_LIBAVIF)
 
 
 def make_requests(n, sources, fmts, seed):
