@@ -3,14 +3,17 @@
 
 Headline `value` (BASELINE.json metric): synthetic 4096x4096
 RGBA8 frames as PNG files (Pillow, zlib level 6, adaptive filters; the configs[1]
-frame in the container SURVEY D-2 names) sit in HOST memory; one step is one
-ik_transform_batch call over a batch of them -- decode_image (GPU inflate +
-unfilter, ik_png.hip), resize_image to 512x512 (Triangle = configs[1]'s
-"bilinear"), encode_image WebP q80 (libwebp, byte-identical to the reference's
-webp 0.3.1 path) -- and ends with the WebP bytes in host memory.  value = input
-pixels of all ranks / max-over-ranks wall time of the K timed steps.  The host
-threads the GPU path may use are stated (--threads, default 32 = an 8-GPU node's
-256 cores / 8).
+frame in the container SURVEY D-2 names) sit in HOST memory (page-locked, as a
+server reads request bodies with ik_host_alloc; --pageable for ordinary memory);
+one step is one batch through ik_transform_batch_submit / _wait -- decode_image
+(upload + GPU gather/CRC, GPU inflate + unfilter, ik_png.hip), resize_image to
+512x512 (Triangle = configs[1]'s "bilinear"), encode_image WebP q80 (libwebp,
+byte-identical to the reference's webp 0.3.1 path) -- ending with the WebP bytes
+in host memory; --inflight batches are outstanding, so one batch's upload runs
+under another's kernels.  value = input pixels of all ranks / max-over-ranks wall
+time of the K timed steps (every timed batch waited for).  The host threads the
+GPU path may use are stated (--threads, default 32 = an 8-GPU node's 256 cores /
+8).
 
 Beside it, in the same JSON line:
   cpu_baseline   the same PNG bytes through the reference CPU path restated
@@ -22,6 +25,7 @@ Beside it, in the same JSON line:
   roofline       the dominant device kernel of the step by HIP-event time, its
                  algorithmic bytes per launch / its duration vs 8 TB/s; the
                  resize kernel's own roofline in roofline_resize.
+  pageable_input the same steps with the PNG files in ordinary host memory.
   hbm_resident   the old headline: the same frames already decoded in HBM ->
                  ik_pipeline (one resize launch per batch, WebP colour kernel,
                  libwebp on the host threads), two batches in flight.
@@ -39,7 +43,6 @@ import io
 import json
 import os
 import sys
-import threading
 import time
 
 import numpy as np
@@ -51,7 +54,9 @@ METRIC = "transform MPix/s (decode+resize+encode) 4096²→512² WebP q80; 1/2/4
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FILTERS = {"nearest": 0, "triangle": 1, "catmullrom": 2, "gaussian": 3, "lanczos3": 4}
 FORMATS = {"jpeg": 0, "webp": 1, "avif": 2}
-PNG_STAGES = ["host_parse_stage", "upload_find", "decode", "expand", "resolve", "unfilter"]
+# ik_png_last_timing fields reported (index -> name; include/imagekit_hip.h)
+PNG_STAGES = {0: "upload_host", 1: "upload_device", 14: "gather_crc", 15: "kernel_stage_wait_find", 13: "find",
+              2: "decode", 3: "expand", 4: "resolve", 5: "unfilter", 6: "kernel_stage_wall"}
 
 
 def parse():
@@ -72,17 +77,21 @@ def parse():
     ap.add_argument("--hbm-batch", type=int, default=64)
     ap.add_argument("--hbm-steps", type=int, default=6)
     ap.add_argument("--jpeg-images", type=int, default=64)
-    ap.add_argument("--clients", type=int, default=1,
-                    help="client threads calling ik_transform_batch at once, each on its own batch (a server's "
-                         "concurrent requests): one batch's host phases overlap another's kernels")
     ap.add_argument("--pipeline", type=int, default=1,
-                    help="1: each step submits its batch (ik_transform_batch_submit: decode, resize and the "
-                         "encoders device half on this thread) and then waits for the previous step's host "
-                         "coders, so one batch's libwebp coding runs beside the next one's upload and kernels; "
-                         "0: one blocking ik_transform_batch per step")
-    ap.add_argument("--split", type=int, default=1,
-                    help="parts a transform batch runs as at once (IK_BATCH_SPLIT: overlaps one part's host "
-                         "phases with another's kernels)")
+                    help="1: steps are ik_transform_batch_submit calls with --inflight batches outstanding, so "
+                         "one batch's upload, another's kernels and a third's libwebp coding overlap; 0: one "
+                         "blocking ik_transform_batch per step")
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="batches submitted before the oldest is waited for (upload / kernels / host coders "
+                         "of three batches overlap)")
+    ap.add_argument("--pageable", action="store_true",
+                    help="inputs in ordinary host memory (default: page-locked, ik_host_alloc)")
+    ap.add_argument("--pageable-steps", type=int, default=4,
+                    help="steps of the extra leg with pageable inputs (0 = skip)")
+    ap.add_argument("--inproc-devices", type=int, default=0,
+                    help="drive N logical devices from this one process (ik_init(-1), IK_DEVICES)")
+    ap.add_argument("--inproc-map", default="",
+                    help="physical device of each logical device, e.g. 0,0 (default 0..N-1)")
     return ap.parse_args()
 
 
@@ -272,14 +281,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     S, O, B = args.size, args.out, args.batch
-    os.environ["IK_BATCH_SPLIT"] = str(args.split)  # read once, when the library first splits a batch
+    if args.inproc_devices > 0:
+        # one process driving several logical devices through the library's own
+        # dispatch (ik_init(-1)); --inproc-map names their physical devices
+        devs = [int(x) for x in args.inproc_map.split(",")] if args.inproc_map else list(range(args.inproc_devices))
+        os.environ["IK_DEVICES"] = ",".join(str(d) for d in devs[:args.inproc_devices])
     import ikutil
     # the codec libraries are explicit dependencies of libimagekit_hip.so
     # (IK_LIBWEBP / IK_LIBAVIF, else the system sonames): name the copies used here
     ikutil.use_pillow_codecs()
     frames = [ikutil.synth(S, S, 4, seed=sd, pattern="S") for sd in shard_seeds(rank, args.distinct)]
     pngs = make_pngs(frames)
-    reqs = [pngs[i % len(pngs)] for i in range(B)]
     # the CPU leg first: its worker pools fork, and nothing may have touched the GPU yet
     cpu = cpu_baseline(args, pngs) if rank == 0 and world == 1 and not args.no_cpu_baseline else None
     dist = None
@@ -289,11 +301,15 @@ def main():
         dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
-    from imagekit import _lib, transform_batch, transform_batch_submit
+    from imagekit import PinnedBytes, _lib, transform_batch, transform_batch_submit
     lib = _lib.load()
-    if lib.ik_init(local) != 0:
-        raise SystemExit(f"ik_init({local}) failed: {_lib.last_error()}")
+    if lib.ik_init(-1 if args.inproc_devices > 0 else local) != 0:
+        raise SystemExit(f"ik_init failed: {_lib.last_error()}")
     dev = f"cuda:{local}"
+    # request bodies in page-locked host memory (ik_host_alloc), as a server reads
+    # them: the upload DMAs them in place (--pageable: ordinary Python bytes)
+    inputs = pngs if args.pageable else [PinnedBytes(p) for p in pngs]
+    reqs = [inputs[i % len(inputs)] for i in range(B)]
 
     def barrier():
         if dist is not None:
@@ -304,85 +320,49 @@ def main():
 
     # ---- headline: PNG bytes in host memory -> WebP bytes in host memory ----
     stage_ms = []
+    NT = 16  # ik_png_last_timing fields
 
-    def step():
-        res = transform_batch(reqs, [(O, O)] * B, [FORMATS["webp"]] * B, [args.quality] * B, filter=f,
-                              threads=max(1, args.threads // args.clients))
-        timing = (ctypes.c_double * 13)()  # this thread's last decode (thread-local in the library)
-        lib.ik_png_last_timing(timing, 13)
+    def note_timing():
+        timing = (ctypes.c_double * NT)()  # the last PNG batch the device finished
+        lib.ik_png_last_timing(timing, NT)
         stage_ms.append(list(timing))
-        return res
 
-    C = max(1, args.clients)
-    results = [None] * C
-    errors = []
+    def submit(rq):
+        return transform_batch_submit(rq, [(O, O)] * B, [FORMATS["webp"]] * B, [args.quality] * B, filter=f,
+                                      threads=args.threads)
 
-    def client(ci, nsteps, warm):
-        # one client: its own thread, so its own HIP stream, pinned staging and scratch
-        try:
-            if lib.ik_init(local) != 0:
-                raise RuntimeError(_lib.last_error())
-            if args.pipeline:
-                run_pipelined(warm)
-                r = run_pipelined(nsteps)
-                if r is not None:
-                    results[ci] = r
-                return
-            for _ in range(warm):
-                step()
-            for _ in range(nsteps):
-                results[ci] = step()
-        except Exception as e:  # reported on the main thread
-            errors.append(e)
-
-    def run_clients(total, warm):
-        per = [total // C + (1 if c < total % C else 0) for c in range(C)]
-        th = [threading.Thread(target=client, args=(c, per[c], warm)) for c in range(C)]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        if errors:
-            raise SystemExit(f"transform_batch failed: {errors[0]}")
-
-    def submit():
-        p = transform_batch_submit(reqs, [(O, O)] * B, [FORMATS["webp"]] * B, [args.quality] * B, filter=f,
-                                   threads=max(1, args.threads // C))
-        timing = (ctypes.c_double * 13)()
-        lib.ik_png_last_timing(timing, 13)
-        stage_ms.append(list(timing))
-        return p
-
-    def run_pipelined(nsteps):
-        pend, out = None, None
+    def run_pipelined(nsteps, rq=None, depth=None):
+        """nsteps batches with up to `depth` in flight (upload of one under the
+        kernels of another, host coders of a third); returns the last bytes"""
+        rq = reqs if rq is None else rq
+        depth = args.inflight if depth is None else depth
+        pend, out = [], None
         for _ in range(nsteps):
-            p = submit()
-            if pend is not None:
-                out = pend.wait()
-            pend = p
-        return pend.wait() if pend is not None else out
+            pend.append(submit(rq))
+            if len(pend) >= depth:
+                out = pend.pop(0).wait()
+                note_timing()
+        while pend:
+            out = pend.pop(0).wait()
+            note_timing()
+        return out
 
-    pipelined = bool(args.pipeline) and C == 1
-    if pipelined:
-        run_pipelined(args.warmup)
-    elif C == 1:
-        for _ in range(args.warmup):
-            step()
-    else:
-        run_clients(0, args.warmup)
+    def run_blocking(nsteps):
+        out = None
+        for _ in range(nsteps):
+            out = transform_batch(reqs, [(O, O)] * B, [FORMATS["webp"]] * B, [args.quality] * B, filter=f,
+                                  threads=args.threads)
+            note_timing()
+        return out
+
+    run = run_pipelined if args.pipeline else run_blocking
+    run(args.warmup)
     stage_ms.clear()
     cnt0 = (ctypes.c_ulonglong * 2)()
     lib.ik_png_counters(cnt0)
     barrier()
     t0 = time.perf_counter()
-    if pipelined:
-        res = run_pipelined(args.steps)
-    elif C == 1:
-        for _ in range(args.steps):
-            res = step()
-    else:
-        run_clients(args.steps, 0)
-        res = next(r for r in results if r is not None)
+    res = run(args.steps)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     barrier()
@@ -393,21 +373,21 @@ def main():
     gpu_streams, host_streams = cnt1[0] - cnt0[0], cnt1[1] - cnt0[1]
     value = aggregate_mpix(world, B * args.steps, S, elapsed)
     st = np.mean(np.array(stage_ms), axis=0)
-    png_stages = {k: round(float(v), 3) for k, v in zip(PNG_STAGES, st[:6])}
-    png_stages.update({"decode_wall_ms": round(float(st[6]), 3), "decode_rounds": float(st[7]),
-                       "decoder_lanes": int(st[8]), "streams_on_gpu": int(st[9]),
+    png_stages = {k: round(float(st[i]), 3) for i, k in PNG_STAGES.items()}
+    png_stages.update({"decode_rounds": float(st[7]), "decoder_lanes": int(st[8]), "streams_on_gpu": int(st[9]),
                        "timed_streams_gpu_decoded": int(gpu_streams), "timed_streams_host_decoded": int(host_streams)})
     out_bytes = sum(len(r) for r in res) // B
     in_bytes = sum(len(p) for p in reqs) // B
 
     # ---- device kernels of the step: algorithmic bytes per launch ----
     raw = (S * 4 + 1) * S          # filtered image bytes per frame (filter byte + RGBA row)
-    # the stage times are those of the calling thread's part of the batch (the
-    # library runs a batch as --split parts at once, ik_host.cpp batch_split):
-    # bytes per launch over that part's frames and tokens
     nd = max(1, int(st[9]))        # frames in the timed decode launch
     tok = float(st[12])            # u16 tokens its decode pass wrote
     kern = {
+        # the files read, the assembled streams (+ padding) written
+        "k_png_gather": (png_stages["gather_crc"], nd * 2 * in_bytes),
+        # the compressed streams read (every bit offset is examined)
+        "k_png_find": (png_stages["find"], nd * in_bytes),
         # compressed stream read, tokens written
         "k_png_decode": (png_stages["decode"], nd * in_bytes + 2 * tok),
         # tokens read, u16 symbols written
@@ -431,6 +411,18 @@ def main():
                     "blocks per frame), not HBM; bytes = compressed bits in + u16 tokens out",
             "tokens_per_batch": int(tok)}
     kernels = {k: {"ms": round(v[0], 4), "GBps": round(v[1] / max(v[0], 1e-6) / 1e6, 1)} for k, v in kern.items()}
+
+    # the same workload with the inputs in ordinary (pageable) memory: the upload
+    # stage copies them through pinned staging first
+    pageable = {}
+    if not args.pageable and not args.no_extras and args.pageable_steps > 0:
+        run_pipelined(1, rq=[pngs[i % len(pngs)] for i in range(B)])
+        barrier()
+        t1 = time.perf_counter()
+        run_pipelined(args.pageable_steps, rq=[pngs[i % len(pngs)] for i in range(B)])
+        te = reduce_max(time.perf_counter() - t1, dist, dev)
+        pageable = {"value": round(aggregate_mpix(world, B * args.pageable_steps, S, te), 2), "unit": "MPix/s",
+                    "steps": args.pageable_steps, "ms_per_step": round(te / args.pageable_steps * 1e3, 3)}
 
     # ---- extras: HBM-resident pipeline (old headline) and JPEG-source leg ----
     hbm = {}
@@ -539,7 +531,9 @@ def main():
                 "workload": f"{S}x{S} RGBA8 synthetic frames as PNG (zlib level 6) in host memory -> "
                             f"ik_transform_batch: decode_image (GPU inflate + unfilter) -> resize_image {O}x{O} "
                             f"({args.filter}) -> encode_image webp q{args.quality} (libwebp) -> WebP bytes in host memory",
-                "batch_per_gpu": B, "batch_split": args.split, "clients": C, "pipelined": pipelined, "filter": args.filter, "format": "webp", "quality": args.quality,
+                "batch_per_gpu": B, "inflight": args.inflight if args.pipeline else 1,
+                "inputs": "pageable host memory" if args.pageable else "page-locked host memory (ik_host_alloc)",
+                "inproc_devices": args.inproc_devices, "filter": args.filter, "format": "webp", "quality": args.quality,
                 "host_threads_per_gpu": args.threads, "png_bytes_per_image": in_bytes,
                 "webp_bytes_per_image": out_bytes,
                 "libwebp": "%d.%d.%d" % (lib.ik_libwebp_version() >> 16, (lib.ik_libwebp_version() >> 8) & 255,
@@ -551,6 +545,7 @@ def main():
             "roofline_resize": roof_resize,
             "png_decode_stages_ms": png_stages,
             "kernels": kernels,
+            "pageable_input": pageable,
             "hbm_resident": hbm,
             "decode_inclusive_jpeg": jpg,
             "cpu_baseline": cpu,

@@ -93,6 +93,16 @@ int ik_image_to_host(const ik_image *img, uint8_t *dst, size_t cap); /* tightly 
 void ik_image_free(ik_image *img);
 void ik_buf_free(uint8_t *buf);
 
+/* ---- caller-pinned input memory ------------------------------------------ */
+/* Encoded inputs in page-locked host memory are DMAed to the GPU in place (no
+ * staging copy): a server reads request bodies into buffers from ik_host_alloc
+ * (or registers its own buffer arena once with ik_host_register).  Inputs in
+ * ordinary memory work too; they are copied through pinned staging first. */
+int ik_host_alloc(size_t bytes, void **out);  /* page-locked, usable by every device */
+int ik_host_free(void *p);                     /* only for ik_host_alloc memory */
+int ik_host_register(void *p, size_t bytes);   /* page-lock an existing range */
+int ik_host_unregister(void *p);               /* the start of a registered range */
+
 /* ---- the three reference functions ------------------------------------ */
 /* decode_image (src/transform.rs:27-43): guess_format + load_from_memory_with_format.
  * *fmt_out = IK_FORMAT_* for webp/jpeg/avif, -1 (None) for other formats. */
@@ -113,12 +123,16 @@ int ik_decode_batch(const uint8_t *const *bytes, const size_t *lens, uint32_t n,
  * the GPU finds inconsistent use the host decoder.  -1 = host decoder only.
  * Default 256 KiB (IK_PNG_GPU_MIN; IK_PNG_GPU=0 = off). */
 int ik_set_png_gpu_min(long long min_raw_bytes);
-/* the calling thread's last GPU PNG batch: [0] host parse + staging ms, device ms
- * of [1] block search [2] count passes [3] emit pass [4] resolve [5] unfilter,
- * [6] wall ms, [7] count rounds, [8] decoder lanes, [9] streams sent to the GPU,
- * [10] PNG streams of the batch the GPU decoded, [11] streams the host decoder took
- * (outside the GPU path, or rejected by it), [12] tokens written by the verified
- * decoder lanes (u16 each) */
+/* the last GPU PNG batch finished on the calling thread's device (n <= 16 values):
+ * [0] upload stage host ms (parse, staging copies of unpinned inputs, DMA issue),
+ * device ms of [1] the upload (first DMA .. gather + CRC done) [2] decode rounds
+ * [3] expand [4] resolve [5] unfilter, [6] kernel stage wall ms, [7] decode rounds,
+ * [8] decoder lanes, [9] streams sent to the GPU, [10] PNG streams of the batch the
+ * GPU decoded, [11] streams the host decoder took (outside the GPU path, or
+ * rejected by it), [12] tokens written by the verified decoder lanes (u16 each),
+ * device ms of [13] the block search [14] the gather + CRC pass, [15] kernel stage
+ * ms until the block search's candidates were back (waiting for the upload
+ * included) */
 int ik_png_last_timing(double *out, int n);
 /* process-wide counts of PNG streams decoded since load: out[0] by the GPU path,
  * out[1] by the host decoder (outside the GPU path, or rejected by it) */
@@ -185,25 +199,31 @@ int ik_transform(const uint8_t *bytes, size_t len, int64_t w, int64_t h, int fmt
                  int filter, uint8_t **out, size_t *out_len);
 
 /* ik_transform over n requests at once (the /img handler under load, loadtest C4
- * mix): ik_decode_batch (one GPU entropy launch for the restart-interval JPEGs),
- * then resize_image + encode_image per request on `threads` host threads (0 =
- * default), each with its own HIP stream.  w/h (-1 = None), fmt and quality per
+ * mix): decode_image (one set of GPU launches for the batch's PNG streams, one GPU
+ * entropy launch for its restart-interval JPEGs), one resize launch per group of
+ * same-geometry requests, encode_image (device front ends; libwebp / libavif on
+ * `threads` host threads, 0 = default).  w/h (-1 = None), fmt and quality per
  * request; outs[i] (ik_buf_free) / out_lens[i] / status[i] per request (status
- * may be NULL); returns the first failure or IK_OK. */
+ * may be NULL); returns the first failure or IK_OK.  Equivalent to
+ * ik_transform_batch_submit + ik_transform_batch_wait. */
 int ik_transform_batch(const uint8_t *const *bytes, const size_t *lens, uint32_t n, const int64_t *w,
                        const int64_t *h, const int *fmt, const int *quality, int filter, int threads,
                        uint8_t **outs, size_t *out_lens, int *status);
 
-/* ik_transform_batch as two calls, so that one batch's host coders (libwebp /
- * libavif, CPU) run beside the next batch's decode (PCIe + GPU): submit runs the
- * batch's device half -- decode, resize, the encoders' device front ends -- on the
- * calling thread and queues its host coders on the device's workers; wait blocks
- * until they are done, fills status[] (may be NULL) and returns the first
- * failure, as ik_transform_batch does.  Every array passed to submit must stay
- * valid until wait returns; each ticket is waited for exactly once.  With several
- * devices (ik_init(-1)) or IK_BATCH_SPLIT the batch runs to completion inside
- * submit.  (Same role as ik_transform_batch: the reference's handlers,
- * src/lib.rs:175-191, serving many requests at once.) */
+/* ik_transform_batch as two calls.  Each device runs batches through three
+ * stages on their own threads -- upload (the PNG files' DMA, in place when the
+ * caller pinned them, then a GPU pass that assembles the zlib streams and checks
+ * the IDAT CRCs), kernels (decode, resize, the encoders' device front ends) and
+ * host coders (the device's worker pool) -- so consecutive batches overlap: batch
+ * k+1's upload runs under batch k's kernels, batch k's libwebp beside both.
+ * submit queues the batch and returns at once; wait blocks until its bytes are
+ * ready, fills status[] (may be NULL) and returns the first failure, as
+ * ik_transform_batch does.  Every array passed to submit -- the inputs included
+ * -- must stay valid until wait returns; each ticket is waited for exactly once.
+ * With several logical devices (ik_init(-1) / IK_DEVICES) a batch goes whole to
+ * the least-loaded device, or in parts of at least IK_MIN_DEVICE_BATCH (64)
+ * requests to several.  (The reference's handlers, src/lib.rs:175-191, serving
+ * many requests at once.) */
 int ik_transform_batch_submit(const uint8_t *const *bytes, const size_t *lens, uint32_t n, const int64_t *w,
                               const int64_t *h, const int *fmt, const int *quality, int filter, int threads,
                               uint8_t **outs, size_t *out_lens, int *status, uint64_t *ticket);

@@ -20,6 +20,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <deque>
 
 #include "../../include/imagekit_hip.h"
 #include "ik_png.h"
@@ -144,6 +145,26 @@ uint8_t* pinned_slot(int slot, size_t bytes) {
     }
     a.cap = want;
     return a.p;
+}
+
+// Caller-pinned ranges (ik_host_alloc / ik_host_register): inputs inside one are
+// DMAed in place.  Keyed by start address; the ranges never overlap.
+namespace {
+struct PinnedRange {
+    size_t n = 0;
+    bool owned = false;  // ik_host_alloc (hipHostFree) vs ik_host_register (hipHostUnregister)
+};
+std::mutex g_pin_mu;
+std::map<uintptr_t, PinnedRange> g_pins;
+}  // namespace
+
+bool host_pinned(const void* p, size_t n) {
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pins.upper_bound(a);
+    if (it == g_pins.begin()) return false;
+    --it;
+    return a >= it->first && a - it->first <= it->second.n && n <= it->second.n - (a - it->first);
 }
 
 // Host <-> device copies of pageable memory go through a per-thread pinned
@@ -473,6 +494,58 @@ using namespace ik;
 extern "C" {
 
 const char* ik_version(void) { return "imagekit-hip 0.1.0 (gfx950)"; }
+
+int ik_host_alloc(size_t bytes, void** out) {
+    if (!out) return fail(IK_ERR_INVALID, "null pointer");
+    *out = nullptr;
+    void* p = nullptr;
+    const hipError_t e = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable);
+    if (e != hipSuccess) return fail(IK_ERR_NOMEM, "hipHostMalloc(%zu bytes): %s", bytes, hipGetErrorString(e));
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    g_pins[(uintptr_t)p] = PinnedRange{bytes, true};
+    *out = p;
+    return IK_OK;
+}
+
+int ik_host_free(void* p) {
+    if (!p) return IK_OK;
+    {
+        std::lock_guard<std::mutex> lk(g_pin_mu);
+        auto it = g_pins.find((uintptr_t)p);
+        if (it == g_pins.end() || !it->second.owned) return fail(IK_ERR_INVALID, "not an ik_host_alloc pointer");
+        g_pins.erase(it);
+    }
+    IK_HIP(hipHostFree(p));
+    return IK_OK;
+}
+
+int ik_host_register(void* p, size_t bytes) {
+    if (!p || !bytes) return fail(IK_ERR_INVALID, "empty range");
+    {
+        std::lock_guard<std::mutex> lk(g_pin_mu);
+        auto it = g_pins.upper_bound((uintptr_t)p + bytes - 1);
+        if (it != g_pins.begin()) {
+            --it;
+            if (it->first + it->second.n > (uintptr_t)p) return fail(IK_ERR_INVALID, "range overlaps a pinned range");
+        }
+    }
+    const hipError_t e = hipHostRegister(p, bytes, hipHostRegisterPortable);
+    if (e != hipSuccess) return fail(IK_ERR_NOMEM, "hipHostRegister(%zu bytes): %s", bytes, hipGetErrorString(e));
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    g_pins[(uintptr_t)p] = PinnedRange{bytes, false};
+    return IK_OK;
+}
+
+int ik_host_unregister(void* p) {
+    {
+        std::lock_guard<std::mutex> lk(g_pin_mu);
+        auto it = g_pins.find((uintptr_t)p);
+        if (it == g_pins.end() || it->second.owned) return fail(IK_ERR_INVALID, "not an ik_host_register range");
+        g_pins.erase(it);
+    }
+    IK_HIP(hipHostUnregister(p));
+    return IK_OK;
+}
 
 size_t ik_last_error(char* buf, size_t cap) {
     const std::string& e = t_err;
@@ -879,9 +952,10 @@ static int decode_one(const uint8_t* bytes, size_t len, ik_image** out, int* fmt
 static std::string last_error_str() { return t_err; }
 
 // decode_image over a batch on the calling thread's device; per-item status and
-// message (the decoder's own, as TransformError(e.to_string()) carries it)
+// message (the decoder's own, as TransformError(e.to_string()) carries it).  up:
+// the batch's PNG streams' upload, already issued (png_upload_begin), or null
 int decode_batch_dev(const uint8_t* const* bytes, const size_t* lens, uint32_t n, ik_image** outs, int* fmts,
-                     int* st, std::string* msg, int threads) {
+                     int* st, std::string* msg, int threads, PngUpload* up = nullptr) {
     std::vector<const uint8_t*> jb, pb;
     std::vector<size_t> jl, pl;
     std::vector<uint32_t> ji, pi, other;
@@ -908,7 +982,8 @@ int decode_batch_dev(const uint8_t* const* bytes, const size_t* lens, uint32_t n
         std::vector<ik_image*> po(pi.size(), nullptr);
         std::vector<int> ps(pi.size(), IK_OK);
         std::vector<std::string> pm(pi.size());
-        decode_png_batch(pb.data(), pl.data(), (int)pi.size(), po.data(), ps.data(), pm.data());
+        if (up && up->n == (int)pi.size()) png_decode_finish(*up, po.data(), ps.data(), pm.data());
+        else decode_png_batch(pb.data(), pl.data(), (int)pi.size(), po.data(), ps.data(), pm.data());
         for (size_t k = 0; k < pi.size(); ++k) {
             outs[pi[k]] = po[k];
             st[pi[k]] = ps[k];
@@ -997,11 +1072,25 @@ int ik_get_resize_mode(void) { return resize_mode(); }
 
 namespace ik {
 
-// ik_transform_batch over the items idx[] of a batch, on the calling thread's
-// device: one batched decode (GPU entropy decoding where the stream allows), then
-// resize_image + encode_image per item on the device's persistent workers.
-// The host half of a batch: the encoders' host coders (libwebp / libavif) over the
-// planes the device half left, and the output buffers.
+// ---- batched transforms: a three-stage pipeline per device ------------------------
+// ik_transform_batch(_submit) -- the handlers of src/lib.rs:175-191 serving many
+// requests -- runs each batch through three stages, each on its own threads, so
+// that consecutive batches overlap on one device:
+//   upload   (one thread per device)  the PNG streams' upload: parse, DMA of the
+//            files (in place when the caller pinned them), the GPU gather + CRC
+//            pass, all on the upload thread's copy stream (png_upload_begin)
+//   kernels  (one thread per device)  decode (the PNG decode kernels once that
+//            upload has landed, JPEG entropy / reconstruction, host decoders for
+//            the rest), one resize launch per geometry group, the encoders'
+//            device front ends (png_decode_finish, transform_device_phase)
+//   host     (the device's worker pool)  the host coders (libwebp / libavif) and
+//            the output buffers (transform_host_phase)
+// so batch k+1's PCIe upload runs under batch k's kernels, and batch k's libwebp
+// beside both.  With several logical devices (ik_init(-1) / IK_DEVICES) each has
+// its own stages; a batch goes whole to the least-loaded device, or is split into
+// parts of at least IK_MIN_DEVICE_BATCH (64) requests over several devices -- the
+// inflate kernels' time hardly depends on how many frames a launch holds, so
+// small parts would only add launches.
 struct HostPhase {
     std::vector<uint32_t> idx;
     std::vector<EncodePrep> prep;
@@ -1010,11 +1099,24 @@ struct HostPhase {
     double t_resize = 0, t_front = 0;
 };
 
-// Device half: decode (GPU where the stream allows), resize, the encoders' device
-// front ends; request i's status / message land in st[i] / errs[i]
+// the PNG requests among idx (decode_batch_dev takes the same ones, in the same order)
+static void png_items(const uint8_t* const* bytes, const size_t* lens, const std::vector<uint32_t>& idx,
+                      std::vector<const uint8_t*>& pb, std::vector<size_t>& pl) {
+    pb.clear();
+    pl.clear();
+    for (uint32_t i : idx)
+        if ((bytes[i] || !lens[i]) && guess_format(bytes[i], lens[i]) == Sniffed::Png) {
+            pb.push_back(bytes[i]);
+            pl.push_back(lens[i]);
+        }
+}
+
+// Device half: decode (GPU where the stream allows; the PNG upload already issued
+// when up is given), resize, the encoders' device front ends; request i's status /
+// message land in st[i] / errs[i]
 static void transform_device_phase(const uint8_t* const* bytes, const size_t* lens, const int64_t* w,
                                    const int64_t* h, const int* fmt, const int* quality, int filter, int* st,
-                                   std::string* errs, HostPhase& hp) {
+                                   std::string* errs, HostPhase& hp, PngUpload* up) {
     const std::vector<uint32_t>& idx = hp.idx;
     const int threads = hp.threads;
     const uint32_t m = (uint32_t)idx.size();
@@ -1026,12 +1128,10 @@ static void transform_device_phase(const uint8_t* const* bytes, const size_t* le
     std::vector<int> ds(m, IK_OK);
     std::vector<std::string> dm(m);
     static const bool timing = getenv("IK_TIMING") != nullptr;  // dev: per-stage sums to stderr
-    // GPU phases under the device's kernel gate (held from the decode kernels --
-    // decode_png_batch takes it after its upload phase -- through resize and the
-    // encoders' device front ends), then the host coders outside it, so that a
-    // concurrent batch's kernels run beside this one's libwebp / libavif coding
+    // GPU phases under the device's kernel gate (held from the decode kernels
+    // through resize and the encoders' device front ends), the host coders after
     gate_pin(kGateKernels, true);
-    decode_batch_dev(b.data(), l.data(), m, imgs.data(), nullptr, ds.data(), dm.data(), threads);
+    decode_batch_dev(b.data(), l.data(), m, imgs.data(), nullptr, ds.data(), dm.data(), threads, up);
     gate_enter(kGateKernels);
     std::mutex tmu;
     double& t_resize = hp.t_resize;
@@ -1136,201 +1236,205 @@ static void transform_host_phase(uint8_t** outs, size_t* out_lens, int* st, std:
                 hp.t_front, t_back);
 }
 
-// ik_transform_batch over the items idx[] of a batch, on the calling thread's device
-static void transform_part(const uint8_t* const* bytes, const size_t* lens, const std::vector<uint32_t>& idx,
-                           const int64_t* w, const int64_t* h, const int* fmt, const int* quality, int filter,
-                           int threads, uint8_t** outs, size_t* out_lens, int* st, std::string* errs) {
-    HostPhase hp;
-    hp.idx = idx;
-    hp.threads = threads;
-    transform_device_phase(bytes, lens, w, h, fmt, quality, filter, st, errs, hp);
-    transform_host_phase(outs, out_lens, st, errs, hp);
-}
-
-// IK_BATCH_SPLIT = P > 1 runs a batch as P parts of at least 8 requests at
-// once, each on its own worker (own stream, staging and device scratch), so that
-// one part's host phases (IDAT staging and CRC, lane planning, libwebp) could
-// overlap another's kernels.  Measured on MI355X (64 PNG frames of 4096^2 ->
-// WebP): 207 ms per batch at P = 1, 249 at 2, 343 at 4 -- the inflate decode
-// kernel takes ~35 ms per part whatever its size (each lane's symbol chain
-// bounds it), so smaller parts only add launches.  Default 1 (one batch).
-static int batch_split() {
-    static const int v = [] {
-        const char* e = getenv("IK_BATCH_SPLIT");
-        const int x = e && *e ? atoi(e) : 1;
-        return x < 1 ? 1 : x > 16 ? 16 : x;
-    }();
-    return v;
-}
-
-static void transform_batch_dev(const uint8_t* const* bytes, const size_t* lens, const std::vector<uint32_t>& idx,
-                                const int64_t* w, const int64_t* h, const int* fmt, const int* quality, int filter,
-                                int threads, uint8_t** outs, size_t* out_lens, int* st, std::string* errs) {
-    const uint32_t m = (uint32_t)idx.size();
-    const int P = (int)std::min<uint32_t>((uint32_t)batch_split(), m / 8);
-    if (P <= 1) {
-        transform_part(bytes, lens, idx, w, h, fmt, quality, filter, threads, outs, out_lens, st, errs);
-        return;
-    }
-    std::vector<std::vector<uint32_t>> parts(P);
-    for (uint32_t k = 0; k < m; ++k) parts[(size_t)k * P / m].push_back(idx[k]);
-    const int part_threads = threads > 0 ? std::max(1, threads / P) : 0;
-    std::mutex mu;
-    std::condition_variable cv;
-    int pending = P - 1;
-    Pool& pool = device_pool(current_device());
-    for (int p = 1; p < P; ++p)
-        pool.post([&, p] {
-            transform_part(bytes, lens, parts[p], w, h, fmt, quality, filter, part_threads, outs, out_lens, st, errs);
-            std::lock_guard<std::mutex> lk(mu);
-            if (--pending == 0) cv.notify_all();
-        });
-    transform_part(bytes, lens, parts[0], w, h, fmt, quality, filter, part_threads, outs, out_lens, st, errs);
-    std::unique_lock<std::mutex> lk(mu);
-    cv.wait(lk, [&] { return pending == 0; });
-}
-
-}  // namespace ik
-
-extern "C" {
-
-int ik_transform_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t n, const int64_t* w,
-                       const int64_t* h, const int* fmt, const int* quality, int filter, int threads, uint8_t** outs,
-                       size_t* out_lens, int* status) {
-    if (!bytes || !lens || !w || !h || !fmt || !quality || !outs || !out_lens || !n)
-        return fail(IK_ERR_INVALID, "bad batch");
-    std::vector<int> st(n, IK_OK);
-    std::vector<std::string> errs(n);
-    for (uint32_t i = 0; i < n; ++i) { outs[i] = nullptr; out_lens[i] = 0; }
-    if (!sched_multi()) {
-        std::vector<uint32_t> all(n);
-        for (uint32_t i = 0; i < n; ++i) all[i] = i;
-        transform_batch_dev(bytes, lens, all, w, h, fmt, quality, filter, threads, outs, out_lens, st.data(),
-                            errs.data());
-    } else {
-        // several devices: the requests are split by least outstanding cost (largest
-        // first) and each device's share runs on that device's own workers
-        std::vector<uint64_t> cost(n);
-        for (uint32_t i = 0; i < n; ++i) cost[i] = request_cost(bytes[i], lens[i], w[i], h[i], fmt[i]);
-        std::vector<uint32_t> assign(n);
-        sched_acquire_batch(cost.data(), n, assign.data());
-        const int nd = sched_count();
-        std::vector<std::vector<uint32_t>> part(nd);
-        for (uint32_t i = 0; i < n; ++i) part[assign[i]].push_back(i);
-        std::mutex mu;
-        std::condition_variable cv;
-        int pending = 0;
-        for (int d = 0; d < nd; ++d) {
-            if (part[d].empty()) continue;
-            ++pending;
-            sched_pool(d).post([&, d] {
-                transform_batch_dev(bytes, lens, part[d], w, h, fmt, quality, filter, threads, outs, out_lens,
-                                    st.data(), errs.data());
-                uint64_t c = 0;
-                for (uint32_t i : part[d]) c += cost[i];
-                sched_release(d, c);
-                std::lock_guard<std::mutex> lk(mu);
-                if (--pending == 0) cv.notify_all();
-            });
-        }
-        std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return pending == 0; });
-    }
-    int first = IK_OK;
-    uint32_t first_i = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        if (status) status[i] = st[i];
-        if (st[i] && !first) { first = st[i]; first_i = i; }
-    }
-    if (first) return fail(first, "item %u: %s", first_i, errs[first_i].c_str());
-    return IK_OK;
-}
-
-// ---- pipelined batches: the device half on the caller, the host half queued ----
-namespace ik {
 namespace {
-struct AsyncBatch {
+
+// one submitted batch (a ticket): its parts run on one or more devices
+struct Ticket {
     uint32_t n = 0;
     uint8_t** outs = nullptr;
     size_t* out_lens = nullptr;
     int* status = nullptr;
     std::vector<int> st;
     std::vector<std::string> errs;
-    HostPhase hp;
-    int rc = IK_OK;  // set when the batch ran synchronously (several devices)
     std::mutex mu;
     std::condition_variable cv;
-    bool done = false;
+    int pending = 0;
 };
+
+// one device's share of a ticket
+struct BatchPart {
+    std::shared_ptr<Ticket> t;
+    const uint8_t* const* bytes = nullptr;
+    const size_t* lens = nullptr;
+    const int64_t* w = nullptr;
+    const int64_t* h = nullptr;
+    const int* fmt = nullptr;
+    const int* quality = nullptr;
+    int filter = 0;
+    HostPhase hp;
+    std::vector<const uint8_t*> pb;  // its PNG inputs (the upload stage's batch)
+    std::vector<size_t> pl;
+    PngUpload up;
+    int logical = -1;  // logical device (multi-device dispatch), -1 = none
+    uint64_t cost = 0;
+};
+
+class StageExec {
+public:
+    StageExec(int device, Pool* host_pool) : dev_(device), pool_(host_pool) {
+        std::thread([this] { loop(0); }).detach();  // live as long as the process
+        std::thread([this] { loop(1); }).detach();
+    }
+    void submit(std::shared_ptr<BatchPart> p) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            q_[0].push_back(std::move(p));
+        }
+        cv_.notify_all();
+    }
+
+private:
+    void loop(int stage) {
+        ik_init(dev_);  // this thread's streams, staging and scratch live on dev_
+        for (;;) {
+            std::shared_ptr<BatchPart> p;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return !q_[stage].empty(); });
+                p = std::move(q_[stage].front());
+                q_[stage].pop_front();
+            }
+            if (stage == 0) {
+                png_items(p->bytes, p->lens, p->hp.idx, p->pb, p->pl);
+                if (!p->pb.empty()) png_upload_begin(p->pb.data(), p->pl.data(), (int)p->pb.size(), p->up);
+                {
+                    std::lock_guard<std::mutex> lk(mu_);
+                    q_[1].push_back(std::move(p));
+                }
+                cv_.notify_all();
+                continue;
+            }
+            Ticket& t = *p->t;
+            transform_device_phase(p->bytes, p->lens, p->w, p->h, p->fmt, p->quality, p->filter, t.st.data(),
+                                   t.errs.data(), p->hp, p->pb.empty() ? nullptr : &p->up);
+            p->up = PngUpload();
+            pool_->post([p] {
+                Ticket& tk = *p->t;
+                transform_host_phase(tk.outs, tk.out_lens, tk.st.data(), tk.errs.data(), p->hp);
+                p->hp = HostPhase();
+                if (p->logical >= 0) sched_release(p->logical, p->cost);
+                std::lock_guard<std::mutex> lk(tk.mu);
+                if (--tk.pending == 0) tk.cv.notify_all();
+            });
+        }
+    }
+    int dev_;
+    Pool* pool_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::shared_ptr<BatchPart>> q_[2];
+};
+
+// the stages of a physical device (single-device mode) or of a logical device
+StageExec& stage_exec(int logical) {
+    static std::mutex mu;
+    static std::map<int, StageExec*> m;
+    const int key = logical >= 0 ? 1000 + logical : current_device();
+    std::lock_guard<std::mutex> lk(mu);
+    StageExec*& e = m[key];
+    if (!e) e = logical >= 0 ? new StageExec(sched_phys(logical), &sched_pool(logical))
+                             : new StageExec(current_device(), &device_pool(current_device()));
+    return *e;
+}
+
 std::mutex g_async_mu;
-std::map<uint64_t, std::shared_ptr<AsyncBatch>> g_async;
+std::map<uint64_t, std::shared_ptr<Ticket>> g_async;
 uint64_t g_async_next = 1;
+
+int min_device_batch() {
+    static const int v = [] {
+        const char* e = getenv("IK_MIN_DEVICE_BATCH");
+        const int x = e && *e ? atoi(e) : 64;
+        return x < 1 ? 1 : x;
+    }();
+    return v;
+}
+
 }  // namespace
 }  // namespace ik
+
+extern "C" {
 
 int ik_transform_batch_submit(const uint8_t* const* bytes, const size_t* lens, uint32_t n, const int64_t* w,
                               const int64_t* h, const int* fmt, const int* quality, int filter, int threads,
                               uint8_t** outs, size_t* out_lens, int* status, uint64_t* ticket) {
     if (!bytes || !lens || !w || !h || !fmt || !quality || !outs || !out_lens || !n || !ticket)
         return fail(IK_ERR_INVALID, "bad batch");
-    auto job = std::make_shared<AsyncBatch>();
-    job->n = n;
-    job->outs = outs;
-    job->out_lens = out_lens;
-    job->status = status;
-    // one logical device (ik_init(-1) on a one-GPU host): the device half right here
-    std::unique_ptr<DeviceGuard> one;
-    if (sched_multi() && sched_count() == 1) one.reset(new DeviceGuard(sched_phys(0)));
-    if ((sched_multi() && !one) || batch_split() > 1) {  // several devices: spread over their workers, run through
-        std::vector<int> stv(n, IK_OK);
-        job->rc = ik_transform_batch(bytes, lens, n, w, h, fmt, quality, filter, threads, outs, out_lens, stv.data());
-        if (status) std::copy(stv.begin(), stv.end(), status);
-        job->errs.assign(1, last_error_str());
-        job->done = true;
+    auto t = std::make_shared<Ticket>();
+    t->n = n;
+    t->outs = outs;
+    t->out_lens = out_lens;
+    t->status = status;
+    t->st.assign(n, IK_OK);
+    t->errs.assign(n, std::string());
+    for (uint32_t i = 0; i < n; ++i) { outs[i] = nullptr; out_lens[i] = 0; }
+    auto make_part = [&](uint32_t lo, uint32_t hi) {
+        auto p = std::make_shared<BatchPart>();
+        p->t = t;
+        p->bytes = bytes; p->lens = lens; p->w = w; p->h = h; p->fmt = fmt; p->quality = quality;
+        p->filter = filter;
+        p->hp.threads = threads;
+        for (uint32_t i = lo; i < hi; ++i) p->hp.idx.push_back(i);
+        return p;
+    };
+    std::vector<std::shared_ptr<BatchPart>> parts;
+    if (!sched_multi()) {
+        parts.push_back(make_part(0, n));
     } else {
-        job->st.assign(n, IK_OK);
-        job->errs.assign(n, std::string());
-        for (uint32_t i = 0; i < n; ++i) { outs[i] = nullptr; out_lens[i] = 0; }
-        job->hp.idx.resize(n);
-        for (uint32_t i = 0; i < n; ++i) job->hp.idx[i] = i;
-        job->hp.threads = threads;
-        transform_device_phase(bytes, lens, w, h, fmt, quality, filter, job->st.data(), job->errs.data(), job->hp);
-        device_pool(current_device()).post([job] {
-            transform_host_phase(job->outs, job->out_lens, job->st.data(), job->errs.data(), job->hp);
-            job->hp = HostPhase();
-            std::lock_guard<std::mutex> lk(job->mu);
-            job->done = true;
-            job->cv.notify_all();
-        });
+        // whole parts of >= IK_MIN_DEVICE_BATCH requests, each to the least-loaded device
+        const int nd = sched_count();
+        const uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)nd, n / (uint32_t)min_device_batch()));
+        for (uint32_t q = 0; q < P; ++q) {
+            auto p = make_part((uint32_t)((uint64_t)n * q / P), (uint32_t)((uint64_t)n * (q + 1) / P));
+            for (uint32_t i : p->hp.idx) p->cost += request_cost(bytes[i], lens[i], w[i], h[i], fmt[i]);
+            p->logical = sched_acquire(p->cost);
+            parts.push_back(p);
+        }
     }
-    std::lock_guard<std::mutex> lk(g_async_mu);
-    *ticket = g_async_next++;
-    g_async[*ticket] = job;
+    t->pending = (int)parts.size();
+    {
+        std::lock_guard<std::mutex> lk(g_async_mu);
+        *ticket = g_async_next++;
+        g_async[*ticket] = t;
+    }
+    for (auto& p : parts) {
+        const int ld = p->logical;
+        stage_exec(ld).submit(std::move(p));
+    }
     return IK_OK;
 }
 
 int ik_transform_batch_wait(uint64_t ticket) {
-    std::shared_ptr<AsyncBatch> job;
+    std::shared_ptr<Ticket> t;
     {
         std::lock_guard<std::mutex> lk(g_async_mu);
         auto it = g_async.find(ticket);
         if (it == g_async.end()) return fail(IK_ERR_INVALID, "unknown batch ticket %llu", (unsigned long long)ticket);
-        job = it->second;
+        t = it->second;
         g_async.erase(it);
     }
     {
-        std::unique_lock<std::mutex> lk(job->mu);
-        job->cv.wait(lk, [&] { return job->done; });
+        std::unique_lock<std::mutex> lk(t->mu);
+        t->cv.wait(lk, [&] { return t->pending == 0; });
     }
-    if (job->st.empty()) return job->rc ? fail(job->rc, "%s", job->errs[0].c_str()) : IK_OK;
     int first = IK_OK;
     uint32_t first_i = 0;
-    for (uint32_t i = 0; i < job->n; ++i) {
-        if (job->status) job->status[i] = job->st[i];
-        if (job->st[i] && !first) { first = job->st[i]; first_i = i; }
+    for (uint32_t i = 0; i < t->n; ++i) {
+        if (t->status) t->status[i] = t->st[i];
+        if (t->st[i] && !first) { first = t->st[i]; first_i = i; }
     }
-    if (first) return fail(first, "item %u: %s", first_i, job->errs[first_i].c_str());
+    if (first) return fail(first, "item %u: %s", first_i, t->errs[first_i].c_str());
     return IK_OK;
+}
+
+int ik_transform_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t n, const int64_t* w,
+                       const int64_t* h, const int* fmt, const int* quality, int filter, int threads, uint8_t** outs,
+                       size_t* out_lens, int* status) {
+    uint64_t ticket = 0;
+    if (int rc = ik_transform_batch_submit(bytes, lens, n, w, h, fmt, quality, filter, threads, outs, out_lens, status,
+                                           &ticket))
+        return rc;
+    return ik_transform_batch_wait(ticket);
 }
 
 static int transform_here(const uint8_t* bytes, size_t len, int64_t w, int64_t h, int fmt, int quality,

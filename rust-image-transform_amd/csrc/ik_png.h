@@ -6,6 +6,7 @@
 #include <cstdint>
 
 #include "ik_inflate.h"
+#include "ik_png_gather.h"
 
 namespace ik {
 
@@ -48,6 +49,32 @@ struct PngLaneDev {
     uint32_t first;          // lane 0 of its image (no distance reaches before its output)
     uint32_t pad;
 };
+
+// Upload of whole PNG files (ik_png_decode.cpp png_upload_begin): each file lands
+// byte for byte in a device "raw" area; k_png_gather then copies the IDAT payloads
+// into the contiguous zlib stream the decoder reads (plus its zero padding) and
+// computes every piece's CRC-32, and k_png_crc_check joins a chunk's pieces and
+// compares the result with the chunk's stored CRC (png verifies every chunk).
+// png's EXPAND of one image (k_png_px): its unfiltered rows (src, rowbytes wide)
+// -> 8-bit pixels of out_c channels: palette indices through pal (RGBA), gray
+// below 8 bits scaled to 8 bits, tRNS as alpha (key: gray level / RGB triple in
+// the image's bit depth, -1 = none)
+struct PngPxDev {
+    const uint8_t* src;
+    size_t sp;
+    uint8_t* dst;
+    size_t dp;
+    int w, h, depth, ctype, out_c, scale, key;
+    int key_rgb[3];
+    uint32_t pal[256];  // r | g << 8 | b << 16 | a << 24
+};
+hipError_t launch_png_px(const PngPxDev& px, hipStream_t s);
+
+// piece_crc[2 i] = finished CRC-32 of piece i's bytes, [2 i + 1] = its length
+hipError_t launch_png_gather(const uint8_t* raw, uint8_t* stream, const PngGatherPiece* pieces, int npieces,
+                             uint32_t* piece_crc, hipStream_t s);
+hipError_t launch_png_crc_check(const uint8_t* raw, const PngCrcChunk* chunks, int nchunks, const uint32_t* piece_crc,
+                                int* err, hipStream_t s);
 
 // dst[i] = src[i] for n words, on the compute stream; one side may be pinned host
 // memory (the small transfers of the PNG kernel phase: ik_png_decode.cpp Xfer)

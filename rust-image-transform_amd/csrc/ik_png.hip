@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <type_traits>
 
+#include "ik_crc.h"
 #include "ik_inflate.h"
 #include "ik_internal.h"
 #include "ik_png.h"
@@ -112,7 +113,12 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
                 const uint64_t x = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;   // bits p .. p+63
                 const uint64_t x2 = sh ? (hi >> sh) : hi;                        // bits p+64 ..
                 const uint64_t cl = (x >> 17) | (x2 << 47);
+#ifdef IK_FIND_NOCHECK  // dev experiment: the scan alone (every Kraft survivor taken)
+                (void)x; (void)cl;
+                v = off;
+#else
                 if (find_full_check(I.words, I.nbits, p, (uint32_t)x, cl, s_tab + 128 * lane)) v = off;
+#endif
             }
             v = wave_min(v);
             best = v < best ? v : best;
@@ -165,7 +171,11 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
             }
             qlen += (uint32_t)__popcll(bal);
         }
+#ifdef IK_FIND_FLUSH_AT  // dev experiment: check the queue as soon as it holds this many
+        if (qlen >= IK_FIND_FLUSH_AT) flush();
+#else
         if (qlen >= 64) flush();
+#endif
         if (best != 0xFFFFFFFFu) break;  // (flush below checks what this step queued after it)
         wi = wn;
         if (wi - (uint64_t)lane >= wlast) break;
@@ -810,6 +820,207 @@ hipError_t launch_copy_words(const uint32_t* src, uint32_t* dst, size_t n, hipSt
     if (!n) return hipSuccess;
     const size_t blocks = std::min<size_t>((n + 255) / 256, 1024);
     hipLaunchKernelGGL(k_copy_words, dim3((unsigned)blocks), dim3(256), 0, s, src, dst, n);
+    return hipGetLastError();
+}
+
+// ---- gather + CRC -----------------------------------------------------------------
+// The upload stage DMAs whole PNG files into the raw area; this pass assembles
+// each file's zlib stream from its IDAT payloads (and the zero padding after it)
+// and computes the CRC-32 png checks on every chunk, so the host neither copies
+// nor checksums the compressed bytes.  One 256-thread workgroup per piece of
+// <= 64 KiB; thread t copies and checksums bytes [256 t, 256 t + 256) of the
+// piece (dword stores once the destination is aligned, the source words
+// realigned with v_alignbyte), then the workgroup joins the 256 partial CRCs in
+// a tree (ik_crc.h: crc(A || B) = crc(A) x^(8 |B|) + crc(B)).
+struct CrcOps {
+    uint32_t x2n[32];    // x^(2^k) mod P
+    uint32_t level[8];   // x^(8 * 256 * 2^k): the join operator of full subtrees at tree level k
+    uint32_t piece;      // x^(8 * kPngGatherPiece): the join operator of a full piece
+    uint32_t crc_idat;   // finished CRC of the chunk type "IDAT" (the first 4 bytes a chunk CRC covers)
+};
+
+__global__ __launch_bounds__(256) void k_png_gather(const uint8_t* __restrict__ raw, uint8_t* __restrict__ stream,
+                                                    const PngGatherPiece* __restrict__ pieces,
+                                                    uint32_t* __restrict__ piece_crc, CrcOps ops) {
+    __shared__ uint32_t t[1024];
+    __shared__ uint32_t s_crc[256], s_len[256];
+    const int tid = (int)threadIdx.x;
+    t[tid] = crc::table_entry((uint32_t)tid);
+    __syncthreads();
+#pragma unroll
+    for (int sl = 1; sl < 4; ++sl) {
+        const uint32_t prev = t[256 * (sl - 1) + tid];
+        t[256 * sl + tid] = (prev >> 8) ^ t[prev & 255u];
+        __syncthreads();
+    }
+    const PngGatherPiece P = pieces[blockIdx.x];
+    const uint32_t b0 = 256u * (uint32_t)tid;
+    const uint32_t len = P.len > b0 ? (P.len - b0 < 256u ? P.len - b0 : 256u) : 0u;
+    uint32_t c = ~0u;
+    uint8_t* dp = stream + P.dst + b0;
+    if (len && P.src == kPngNoSrc) {
+        for (uint32_t i = 0; i < len; ++i) dp[i] = 0;
+    } else if (len) {
+        const uint8_t* sp = raw + P.src + b0;
+        uint32_t i = 0;
+        const uint32_t mis = (uint32_t)((uintptr_t)dp & 3u);
+        const uint32_t pre = mis ? (4u - mis < len ? 4u - mis : len) : 0u;
+        for (; i < pre; ++i) {
+            const uint32_t b = sp[i];
+            dp[i] = (uint8_t)b;
+            c = crc::step_byte(c, b, t);
+        }
+        const uint32_t nw = (len - i) >> 2;
+        if (nw) {
+            const uintptr_t sa = (uintptr_t)(sp + i);
+            const uint32_t sh = (uint32_t)(sa & 3u);
+            const uint32_t* ws = reinterpret_cast<const uint32_t*>(sa - sh);
+            uint32_t* wd = reinterpret_cast<uint32_t*>(dp + i);
+            uint32_t lo = ws[0];
+            uint32_t k = 0;
+            // eight words at a time: the loads are independent of the CRC chain
+            for (; k + 8 <= nw; k += 8) {
+                uint32_t in[9];
+                in[0] = lo;
+#pragma unroll
+                for (int u = 1; u <= 8; ++u) in[u] = sh ? ws[k + u] : (u < 8 ? ws[k + u] : 0u);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t v = sh ? __builtin_amdgcn_alignbyte(in[u + 1], in[u], sh) : in[u];
+                    wd[k + u] = v;
+                    c = crc::step_word(c, v, t);
+                }
+                lo = sh ? in[8] : (k + 8 < nw ? ws[k + 8] : 0u);
+            }
+            for (; k < nw; ++k) {
+                const uint32_t hi = sh ? ws[k + 1] : 0u;
+                const uint32_t v = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+                wd[k] = v;
+                c = crc::step_word(c, v, t);
+                lo = sh ? hi : (k + 1 < nw ? ws[k + 1] : 0u);
+            }
+            i += 4u * nw;
+        }
+        for (; i < len; ++i) {
+            const uint32_t b = sp[i];
+            dp[i] = (uint8_t)b;
+            c = crc::step_byte(c, b, t);
+        }
+    }
+    s_crc[tid] = ~c;  // finished CRC of this thread's bytes (0 for none)
+    s_len[tid] = len;
+    __syncthreads();
+#pragma unroll 1
+    for (int k = 0; k < 8; ++k) {
+        const int stride = 1 << k;
+        if ((tid & (2 * stride - 1)) == 0) {
+            const uint32_t rl = s_len[tid + stride];
+            if (rl) {
+                const uint32_t op = rl == (256u << k) ? ops.level[k] : crc::x8n(rl, ops.x2n);
+                s_crc[tid] = crc::combine_op(s_crc[tid], s_crc[tid + stride], op);
+                s_len[tid] += rl;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        piece_crc[2 * blockIdx.x] = s_crc[0];
+        piece_crc[2 * blockIdx.x + 1] = s_len[0];
+    }
+}
+
+// one thread per IDAT chunk: join "IDAT" and its pieces, compare with the stored CRC
+__global__ __launch_bounds__(256) void k_png_crc_check(const uint8_t* __restrict__ raw,
+                                                       const PngCrcChunk* __restrict__ chunks, int nchunks,
+                                                       const uint32_t* __restrict__ piece_crc, int* err, CrcOps ops) {
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= nchunks) return;
+    const PngCrcChunk C = chunks[i];
+    uint32_t c = ops.crc_idat;
+    for (uint32_t p = C.piece0; p < C.piece0 + C.npieces; ++p) {
+        const uint32_t len = piece_crc[2 * p + 1];
+        const uint32_t op = len == kPngGatherPiece ? ops.piece : crc::x8n(len, ops.x2n);
+        c = crc::combine_op(c, piece_crc[2 * p], op);
+    }
+    const uint8_t* q = raw + C.crc_at;
+    const uint32_t stored = (uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 | (uint32_t)q[2] << 8 | (uint32_t)q[3];
+    if (c != stored) err[C.stream] = 1;
+}
+
+static CrcOps crc_ops() {
+    static const CrcOps o = [] {
+        CrcOps r{};
+        crc::x2n_table(r.x2n);
+        for (int k = 0; k < 8; ++k) r.level[k] = crc::x8n((uint64_t)256 << k, r.x2n);
+        r.piece = crc::x8n(kPngGatherPiece, r.x2n);
+        uint32_t t[1024];
+        for (uint32_t i = 0; i < 256; ++i) t[i] = crc::table_entry(i);
+        for (int sl = 1; sl < 4; ++sl)
+            for (int i = 0; i < 256; ++i) t[256 * sl + i] = (t[256 * (sl - 1) + i] >> 8) ^ t[t[256 * (sl - 1) + i] & 255u];
+        uint32_t c = ~0u;
+        for (const char ch : {'I', 'D', 'A', 'T'}) c = crc::step_byte(c, (uint8_t)ch, t);
+        r.crc_idat = ~c;
+        return r;
+    }();
+    return o;
+}
+
+hipError_t launch_png_gather(const uint8_t* raw, uint8_t* stream, const PngGatherPiece* pieces, int npieces,
+                             uint32_t* piece_crc, hipStream_t s) {
+    if (npieces <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_png_gather, dim3((unsigned)npieces), dim3(256), 0, s, raw, stream, pieces, piece_crc,
+                       crc_ops());
+    return hipGetLastError();
+}
+
+hipError_t launch_png_crc_check(const uint8_t* raw, const PngCrcChunk* chunks, int nchunks, const uint32_t* piece_crc,
+                                int* err, hipStream_t s) {
+    if (nchunks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_png_crc_check, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0, s, raw, chunks,
+                       nchunks, piece_crc, err, crc_ops());
+    return hipGetLastError();
+}
+
+// ---- EXPAND -------------------------------------------------------------------------
+// png 0.18's EXPAND transformation (image 0.25.8 decodes with it: reference
+// src/transform.rs:31): one thread per pixel of the unfiltered rows.  Palette
+// index -> PLTE colour (an index past the palette: black) with tRNS alpha (255
+// past tRNS); gray of 1/2/4 bits -> v * 255 / (2^d - 1); a gray level or RGB
+// triple equal to the tRNS key -> alpha 0, else 255.
+__global__ __launch_bounds__(256) void k_png_px(PngPxDev P) {
+    __shared__ uint32_t pal[256];
+    if (P.ctype == 3) pal[threadIdx.x] = P.pal[threadIdx.x];
+    __syncthreads();
+    const int x = (int)(blockIdx.x * 256 + threadIdx.x), y = (int)blockIdx.y;
+    if (x >= P.w) return;
+    const uint8_t* r = P.src + (size_t)y * P.sp;
+    uint8_t* o = P.dst + (size_t)y * P.dp + (size_t)x * P.out_c;
+    if (P.ctype == 2) {  // RGB + tRNS key
+        const int R = r[3 * x], G = r[3 * x + 1], B = r[3 * x + 2];
+        o[0] = (uint8_t)R; o[1] = (uint8_t)G; o[2] = (uint8_t)B;
+        o[3] = (R == P.key_rgb[0] && G == P.key_rgb[1] && B == P.key_rgb[2]) ? 0 : 255;
+        return;
+    }
+    int v;
+    if (P.depth == 8) {
+        v = r[x];
+    } else {
+        const int bit = x * P.depth;
+        v = (r[bit >> 3] >> (8 - P.depth - (bit & 7))) & ((1 << P.depth) - 1);
+    }
+    if (P.ctype == 3) {
+        const uint32_t c = pal[v];
+        o[0] = (uint8_t)c; o[1] = (uint8_t)(c >> 8); o[2] = (uint8_t)(c >> 16);
+        if (P.out_c == 4) o[3] = (uint8_t)(c >> 24);
+    } else {
+        o[0] = (uint8_t)(v * P.scale);
+        if (P.out_c == 2) o[1] = v == P.key ? 0 : 255;
+    }
+}
+
+hipError_t launch_png_px(const PngPxDev& px, hipStream_t s) {
+    if (px.w <= 0 || px.h <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_png_px, dim3((unsigned)((px.w + 255) / 256), (unsigned)px.h), dim3(256), 0, s, px);
     return hipGetLastError();
 }
 

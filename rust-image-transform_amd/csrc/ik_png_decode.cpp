@@ -11,16 +11,18 @@
 //          predecessor decodes on)
 //   GPU    k_png_expand (tokens -> u16 symbols + window markers), k_png_resolve
 //          (filtered rows into the image, markers followed), k_png_unfilter
-// The GPU path covers 8- and 16-bit, non-interlaced, non-palette streams
-// without tRNS (png's EXPAND leaves those samples as they are); everything else,
-// and any stream the GPU finds inconsistent, goes through the host decoder, whose
-// error messages are png's.  The zlib Adler-32 is not verified, as png 0.18 does
+// The GPU path covers non-interlaced 8-bit streams of every colour type, palette
+// and gray streams of 1/2/4 bits, and tRNS (png's EXPAND: k_png_px); 16-bit and
+// interlaced streams, and any stream the GPU finds inconsistent, go through the
+// host decoder, whose error messages are png's.  The zlib Adler-32 is not verified, as png 0.18 does
 // not by default (CRCs cover the data).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <map>
 #include <cstdio>
 #include <memory>
 #include <mutex>
@@ -50,14 +52,23 @@ struct PngJob {
     size_t zlen = 0;                                 // IDAT payload bytes (zlib stream)
     uint64_t raw_total = 0;
     int rowbytes = 0;
-    // device layout (offsets into the batch work area)
-    size_t o_words = 0, o_u16 = 0, o_ft = 0;
-    size_t z_off = 0;                                // offset of the stream in the pinned buffer
+    // layout: the file in the upload area's raw part, its zlib stream in the
+    // stream part, its staging copy (inputs the caller did not pin); the kernel
+    // stage's u16 symbols and filter types
+    size_t raw_off = 0, z_off = 0, stage_off = 0;
+    size_t o_u16 = 0, o_ft = 0;
     uint64_t nbits = 0;
     int chunk0 = 0, nchunks = 0;                     // its chunks in the batch chunk table
     pngplan::Lanes lanes;
     int state = 0;                                   // 0 running, 1 verified, -1 host fallback
     ik_image* img = nullptr;
+    // png's EXPAND (palette -> RGB(A), gray below 8 bits -> 8 bits, tRNS -> alpha):
+    // the unfiltered rows land in `rows` (rowbytes wide) and k_png_px writes the
+    // expanded pixels (out_c channels) into img
+    bool expand = false;
+    int out_c = 0;
+    PngPxDev px{};
+    ik_image* rows = nullptr;
 };
 
 // png 0.18 + image's EXPAND: which streams the GPU path decodes.  Returns false
@@ -68,13 +79,17 @@ bool parse_png(const uint8_t* b, size_t n, PngJob& J) {
     size_t pos = 8;
     bool ihdr = false, trns = false;
     int interlace = 0;
+    std::vector<uint8_t> plte;
+    const uint8_t* trns_data = nullptr;
+    size_t trns_len = 0;
     while (pos + 12 <= n) {
         const uint32_t len = be32(b + pos);
         if (len > n - pos - 12) return false;
         const uint8_t* type = b + pos + 4;
         const uint8_t* data = b + pos + 8;
-        // (IDAT CRCs are checked while the payload is staged: decode_png_batch)
-        if (std::memcmp(type, "IDAT", 4) && png_chunk_crc(type, data, len) != be32(data + len)) return false;
+        // (IDAT payload CRCs are checked on the GPU by the upload's gather pass; an
+        // empty IDAT's here)
+        if ((std::memcmp(type, "IDAT", 4) || !len) && png_chunk_crc(type, data, len) != be32(data + len)) return false;
         if (!std::memcmp(type, "IHDR", 4)) {
             if (len != 13 || ihdr) return false;
             J.w = be32(data);
@@ -85,6 +100,10 @@ bool parse_png(const uint8_t* b, size_t n, PngJob& J) {
             ihdr = true;
         } else if (!std::memcmp(type, "tRNS", 4)) {
             trns = true;
+            trns_data = data;
+            trns_len = len;
+        } else if (!std::memcmp(type, "PLTE", 4)) {
+            plte.assign(data, data + len);
         } else if (!std::memcmp(type, "IDAT", 4)) {
             if (len) J.idat.emplace_back(data, len);
             J.zlen += len;
@@ -93,22 +112,61 @@ bool parse_png(const uint8_t* b, size_t n, PngJob& J) {
         }
         pos += 12 + len;
     }
-    if (!ihdr || J.idat.empty() || !J.w || !J.h || interlace || trns) return false;
-    if (J.depth != 8 && J.depth != 16) return false;
+    if (!ihdr || J.idat.empty() || !J.w || !J.h || interlace) return false;
+    // 8-bit L / LA / RGB / RGBA as they are; palette (1/2/4/8 bits), gray below 8
+    // bits and tRNS through png's EXPAND on the GPU (k_png_px); 16-bit: host
     int spp;
     switch (J.ctype) {
     case 0: spp = 1; break;
     case 2: spp = 3; break;
+    case 3: spp = 1; break;
     case 4: spp = 2; break;
     case 6: spp = 4; break;
-    default: return false;  // palette: host
+    default: return false;
     }
+    const bool low = J.depth == 1 || J.depth == 2 || J.depth == 4;
+    if (!(J.depth == 8 || (low && (J.ctype == 0 || J.ctype == 3)))) return false;
+    if (trns && J.ctype != 0 && J.ctype != 2 && J.ctype != 3) return false;  // (png rejects those)
     J.ch = spp;
-    J.bpp = spp * J.depth / 8;
-    if (J.depth == 16) return false;  // 16-bit samples: host (see decode_png)
-    const uint64_t rb = (uint64_t)J.w * J.bpp;
-    // image's default limit: 512 MiB of decoded pixels
-    if (rb * J.h > (512ull << 20) || rb > 0x7FFFFFF0ull) return false;
+    const uint64_t bits_pp = (uint64_t)spp * J.depth;
+    J.bpp = (int)((bits_pp + 7) / 8);
+    const uint64_t rb = ((uint64_t)J.w * bits_pp + 7) / 8;
+    J.expand = J.ctype == 3 || low || trns;
+    J.out_c = spp;
+    if (J.expand) {
+        PngPxDev& X = J.px;
+        X.w = (int)J.w;
+        X.h = (int)J.h;
+        X.depth = J.depth;
+        X.ctype = J.ctype;
+        X.key = -1;
+        if (J.ctype == 3) {
+            if (plte.empty() || plte.size() % 3 || plte.size() > 768) return false;
+            J.out_c = trns_len ? 4 : 3;
+            const size_t np = plte.size() / 3;
+            for (size_t i = 0; i < 256; ++i) {
+                const uint32_t r = i < np ? plte[3 * i] : 0, g = i < np ? plte[3 * i + 1] : 0, bl = i < np ? plte[3 * i + 2] : 0;
+                const uint32_t a = i < trns_len ? trns_data[i] : 255u;
+                X.pal[i] = r | g << 8 | bl << 16 | a << 24;
+            }
+        } else if (J.ctype == 0) {
+            J.out_c = trns_len >= 2 ? 2 : 1;
+            if (trns_len >= 2) X.key = (int)((trns_data[0] << 8) | trns_data[1]);
+            X.scale = J.depth == 1 ? 255 : J.depth == 2 ? 85 : J.depth == 4 ? 17 : 1;
+        } else {  // RGB + tRNS
+            if (trns_len < 6) { J.expand = false; }
+            else {
+                J.out_c = 4;
+                X.key_rgb[0] = (trns_data[0] << 8) | trns_data[1];
+                X.key_rgb[1] = (trns_data[2] << 8) | trns_data[3];
+                X.key_rgb[2] = (trns_data[4] << 8) | trns_data[5];
+                X.key = 0;
+            }
+        }
+        X.out_c = J.out_c;
+    }
+    // image's default limit: 512 MiB of decoded (expanded) pixels
+    if ((uint64_t)J.w * J.h * J.out_c > (512ull << 20) || rb > 0x7FFFFFF0ull) return false;
     J.rowbytes = (int)rb;
     J.raw_total = (rb + 1) * J.h;
     // zlib header: CM 8, window <= 32 KiB, FCHECK, no preset dictionary
@@ -193,12 +251,7 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// the last batch's stage times on this thread (ik_png_last_timing): host parse +
-// staging, then device ms of find / count (all rounds) / emit / resolve / unfilter
-// from HIP events on the thread's stream, wall ms, rounds, lanes, streams sent to
-// the GPU, streams the GPU decoded (verified), streams the host decoder took,
-// tokens the verified lanes wrote (the decode pass's output, the expand pass's input)
-thread_local double t_png_timing[13];
+// the last batch's stage times (ik_png_last_timing, per device): see the header
 // process-wide: PNG streams decoded by the GPU path / by the host decoder
 std::atomic<unsigned long long> g_png_gpu_streams{0}, g_png_host_streams{0};
 struct Events {
@@ -242,49 +295,251 @@ bool png_gpu_enabled(size_t raw_bytes) {
     return v >= 0 && (long long)raw_bytes >= v;
 }
 
-int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_image** outs, int* status,
-                     std::string* msgs) {
+// ---- upload areas ----------------------------------------------------------------
+// A batch's upload stage fills an area of device memory -- the PNG files exactly
+// as the caller holds them (raw), the zlib streams assembled from their IDAT
+// payloads (+ zero padding), the gather plan, per-piece CRCs and per-stream CRC
+// flags -- that its kernel stage reads until its decode rounds end.  Two areas
+// per device: the next batch's upload (PCIe + the gather pass) runs while the
+// current batch's kernels read the other one.
+namespace {
+struct UploadArea {
+    int device = 0;
+    uint8_t* dev = nullptr;
+    size_t cap = 0;
+    uint8_t* pin = nullptr;  // pinned: the plan tables, and staging for inputs the caller did not pin
+    size_t pin_cap = 0;
+    hipEvent_t ev[3] = {};   // upload issued, file DMAs done, gather + CRC done (the kernel stage waits on [2])
+    bool busy = false;
+};
+constexpr int kUploadAreas = 2;
+struct AreaPool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<UploadArea*> areas;
+};
+AreaPool& area_pool(int device) {
+    static std::mutex mu;
+    static std::map<int, AreaPool*> pools;
+    std::lock_guard<std::mutex> lk(mu);
+    AreaPool*& p = pools[device];
+    if (!p) p = new AreaPool();
+    return *p;
+}
+UploadArea* acquire_area(int device) {
+    AreaPool& P = area_pool(device);
+    std::unique_lock<std::mutex> lk(P.mu);
+    for (;;) {
+        for (UploadArea* a : P.areas)
+            if (!a->busy) { a->busy = true; return a; }
+        if ((int)P.areas.size() < kUploadAreas) {
+            auto* a = new UploadArea();
+            a->device = device;
+            for (hipEvent_t& e : a->ev)
+                if (hipEventCreate(&e) != hipSuccess) e = nullptr;
+            a->busy = true;
+            P.areas.push_back(a);
+            return a;
+        }
+        P.cv.wait(lk);
+    }
+}
+void release_area(UploadArea*& a) {
+    if (!a) return;
+    AreaPool& P = area_pool(a->device);
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        a->busy = false;
+    }
+    P.cv.notify_all();
+    a = nullptr;
+}
+// grow an idle area (nothing pending reads it: it was released after its batch's
+// decode rounds synchronised)
+bool area_reserve(UploadArea* a, size_t dev_bytes, size_t pin_bytes) {
+    if (dev_bytes > a->cap) {
+        if (a->dev) (void)hipFree(a->dev);
+        a->dev = nullptr;
+        a->cap = 0;
+        const size_t want = dev_bytes + dev_bytes / 8;
+        if (hipMalloc((void**)&a->dev, want) != hipSuccess) { a->dev = nullptr; return false; }
+        a->cap = want;
+    }
+    if (pin_bytes > a->pin_cap) {
+        if (a->pin) (void)hipHostFree(a->pin);
+        a->pin = nullptr;
+        a->pin_cap = 0;
+        const size_t want = std::max<size_t>(pin_bytes + pin_bytes / 8, 1u << 20);
+        if (hipHostMalloc((void**)&a->pin, want, hipHostMallocDefault) != hipSuccess) { a->pin = nullptr; return false; }
+        a->pin_cap = want;
+    }
+    return true;
+}
+
+// the last batch's stage times per device (ik_png_last_timing)
+std::mutex g_timing_mu;
+std::map<int, std::vector<double>> g_timing;
+}  // namespace
+
+// the upload stage's hand-off to the kernel stage
+struct PngBatchState {
+    int device = 0;
+    int n = 0;
+    std::vector<PngJob> jobs;
+    std::vector<char> gpu;
+    std::vector<PngJob*> J;
+    UploadArea* area = nullptr;
+    int rc = IK_OK;
+    size_t o_zs = 0, o_err = 0;  // area offsets: assembled streams, per-stream CRC flags
+    int pinned_streams = 0;
+    double t0 = 0, t_host = 0;
+    ~PngBatchState() { release_area(area); }
+};
+
+int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, PngUpload& up) {
+    static const bool timing = getenv("IK_PNG_TIMING") != nullptr;
+    auto st = std::make_shared<PngBatchState>();
+    up.st = st;
+    up.bytes = bytes;
+    up.lens = lens;
+    up.n = n;
+    PngBatchState& S = *st;
+    S.device = current_device();
+    S.n = n;
+    S.t0 = now_ms();
+    S.jobs.assign(n, PngJob());
+    S.gpu.assign(n, 0);
+    parallel_for(n, 0, [&](int i) {
+        S.jobs[i].idx = i;
+        S.gpu[i] = parse_png(bytes[i], lens[i], S.jobs[i]) && png_gpu_enabled(S.jobs[i].raw_total);
+    });
+    for (int i = 0; i < n; ++i)
+        if (S.gpu[i]) S.J.push_back(&S.jobs[i]);
+    const int m = (int)S.J.size();
+    if (!m) return IK_OK;
+    constexpr size_t kPad = 512;  // zero bytes past each stream (Bits::wend, the LDS ring's DMAs)
+    // ---- layout of the area: [raw files][streams][pieces][chunks][piece CRCs][flags] ----
+    size_t raw = 0, zs = 0, stage = 0;
+    std::vector<PngGatherPiece> pieces;
+    std::vector<PngCrcChunk> chunks;
+    std::vector<char> pinned(m, 0);
+    for (int k = 0; k < m; ++k) {
+        PngJob& j = *S.J[k];
+        j.raw_off = raw;
+        raw += up256(lens[j.idx] + 4);  // (+4: the gather pass reads whole words)
+        j.z_off = zs;
+        zs += up256(((j.zlen + 3) & ~size_t(3)) + kPad);
+        pinned[k] = host_pinned(bytes[j.idx], lens[j.idx]);
+        if (!pinned[k]) {
+            j.stage_off = stage;
+            stage += up256(lens[j.idx]);
+        }
+        S.pinned_streams += pinned[k];
+    }
+    for (int k = 0; k < m; ++k) {
+        const PngJob& j = *S.J[k];
+        const uint32_t tail = (uint32_t)((((j.zlen + 3) & ~size_t(3)) + kPad) - j.zlen);
+        png_gather_plan(bytes[j.idx], j.raw_off, j.idat, raw + j.z_off, tail, (uint32_t)k, pieces, chunks);
+    }
+    // (the pieces' dst offsets are area offsets: the stream area follows the raw one)
+    S.o_zs = raw;
+    const size_t o_pieces = raw + up256(zs);
+    const size_t o_chunks = o_pieces + up256(sizeof(PngGatherPiece) * pieces.size());
+    const size_t o_pcrc = o_chunks + up256(sizeof(PngCrcChunk) * chunks.size());
+    S.o_err = o_pcrc + up256(2 * sizeof(uint32_t) * pieces.size());
+    const size_t dev_bytes = S.o_err + up256(sizeof(int) * m);
+    const size_t tab_bytes = up256(sizeof(PngGatherPiece) * pieces.size()) + up256(sizeof(PngCrcChunk) * chunks.size());
+    S.area = acquire_area(S.device);  // waits while two earlier batches' kernel stages hold both areas
+    UploadArea* A = S.area;
+    if (!area_reserve(A, dev_bytes, tab_bytes + stage)) {
+        S.rc = fail(IK_ERR_DEVICE, "cannot allocate the PNG upload area (%zu device bytes)", dev_bytes);
+        return IK_OK;  // the kernel stage sends every stream to the host decoder
+    }
+    hipStream_t sc = thread_copy_stream();
+    if (!sc) { S.rc = fail(IK_ERR_DEVICE, "cannot create the PNG copy stream"); return IK_OK; }
+    // the upload goes out under the device's upload gate: concurrent batches take
+    // PCIe in turn (ik_runtime.h)
+    gate_enter(kGateUpload);
+    std::atomic<int> err{0};
+    if (A->ev[0]) (void)hipEventRecord(A->ev[0], sc);
+    // files the caller pinned (ik_host_alloc / ik_host_register) go straight from
+    // its memory; the others through the area's pinned staging (host memcpy only:
+    // the CRCs are the GPU's)
+    for (int k = 0; k < m; ++k) {
+        if (!pinned[k]) continue;
+        const PngJob& j = *S.J[k];
+        if (hipMemcpyAsync(A->dev + j.raw_off, bytes[j.idx], lens[j.idx], hipMemcpyHostToDevice, sc) != hipSuccess)
+            err = 1;
+    }
+    std::vector<int> staged;
+    for (int k = 0; k < m; ++k)
+        if (!pinned[k]) staged.push_back(k);
+    uint8_t* stg = A->pin + tab_bytes;
+    parallel_for((int)staged.size(), 0, [&, sc](int q) {
+        const PngJob& j = *S.J[staged[q]];
+        std::memcpy(stg + j.stage_off, bytes[j.idx], lens[j.idx]);
+        if (hipMemcpyAsync(A->dev + j.raw_off, stg + j.stage_off, lens[j.idx], hipMemcpyHostToDevice, sc) != hipSuccess)
+            err = 1;
+    });
+    if (A->ev[1]) (void)hipEventRecord(A->ev[1], sc);
+    std::memcpy(A->pin, pieces.data(), sizeof(PngGatherPiece) * pieces.size());
+    std::memcpy(A->pin + up256(sizeof(PngGatherPiece) * pieces.size()), chunks.data(),
+                sizeof(PngCrcChunk) * chunks.size());
+    hipError_t e = hipMemcpyAsync(A->dev + o_pieces, A->pin, tab_bytes, hipMemcpyHostToDevice, sc);
+    if (e == hipSuccess) e = hipMemsetAsync(A->dev + S.o_err, 0, sizeof(int) * m, sc);
+    if (e == hipSuccess)
+        e = launch_png_gather(A->dev, A->dev, reinterpret_cast<const PngGatherPiece*>(A->dev + o_pieces),
+                              (int)pieces.size(), reinterpret_cast<uint32_t*>(A->dev + o_pcrc), sc);
+    if (e == hipSuccess)
+        e = launch_png_crc_check(A->dev, reinterpret_cast<const PngCrcChunk*>(A->dev + o_chunks), (int)chunks.size(),
+                                 reinterpret_cast<const uint32_t*>(A->dev + o_pcrc),
+                                 reinterpret_cast<int*>(A->dev + S.o_err), sc);
+    if (e == hipSuccess && A->ev[2]) e = hipEventRecord(A->ev[2], sc);
+    if (e == hipSuccess && !A->ev[2]) e = hipStreamSynchronize(sc);  // (no event: the stage waits here)
+    gate_leave(kGateUpload);
+    if (e != hipSuccess || err) S.rc = hip_fail(e != hipSuccess ? e : hipErrorUnknown, "PNG upload / gather");
+    S.t_host = now_ms() - S.t0;
+    if (timing)
+        fprintf(stderr, "[png] upload t=%.1f: %d streams (%d pinned), %zu pieces, %zu IDAT chunks, host %.2f ms\n",
+                fmod(S.t0, 1e5), m, S.pinned_streams, pieces.size(), chunks.size(), S.t_host);
+    return IK_OK;
+}
+
+int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* msgs) {
     static const bool timing = getenv("IK_PNG_TIMING") != nullptr;
     const double t0 = now_ms();
-    for (double& v : t_png_timing) v = 0;
+    double tim[kPngTimingFields] = {};
     Events& ev = events();
     auto rec = [&](int k, hipStream_t st) { if (ev.ok) (void)hipEventRecord(ev.e[k], st); };
-    // a stream the GPU path gives up on: the host decoder takes it (and gives png's
-    // error if the stream is malformed); IK_PNG_TIMING says why
     auto reject = [&](PngJob& j, const char* why) {
         j.state = -1;
         if (timing) fprintf(stderr, "[png] stream %d (%ux%u) -> host decoder: %s\n", j.idx, j.w, j.h, why);
     };
-    double count_dev = 0;
-    std::vector<PngJob> jobs(n);
-    std::vector<char> gpu(n, 0);
-    parallel_for(n, 0, [&](int i) {
+    PngBatchState& S = *up.st;
+    const uint8_t* const* bytes = up.bytes;
+    const size_t* lens = up.lens;
+    const int n = up.n;
+    for (int i = 0; i < n; ++i) {
         outs[i] = nullptr;
         status[i] = IK_OK;
-        jobs[i].idx = i;
-        gpu[i] = parse_png(bytes[i], lens[i], jobs[i]) && png_gpu_enabled(jobs[i].raw_total);
-    });
-    std::vector<PngJob*> J;
-    for (int i = 0; i < n; ++i)
-        if (gpu[i]) J.push_back(&jobs[i]);
+    }
+    double count_dev = 0;
+    std::vector<PngJob*>& J = S.J;
+    std::vector<char>& gpu = S.gpu;
     const int m = (int)J.size();
     hipStream_t s = thread_stream();
-    int rc = IK_OK;
+    int rc = S.rc;
     const uint64_t cbits = kPngChunkBytes * 8;
-    if (m) {
-        // ---- device layout ----
-        constexpr size_t kPad = 512;  // zero bytes past each stream (Bits::wend, the LDS ring's DMAs)
-        size_t total = 0, zbytes = 0;
+    UploadArea* A = S.area;
+    if (m && !rc) {
+        // ---- the kernel stage's work area (this thread's) ----
+        size_t total = 0;
         int nchunks = 0;
         for (PngJob* j : J) {
-            j->z_off = zbytes;
-            zbytes += ((j->zlen + 3) & ~size_t(3)) + kPad;  // the zero padding travels with the stream
             j->nbits = (uint64_t)j->zlen * 8;
             j->nchunks = (int)((j->nbits - 16 + cbits - 1) / cbits);
             j->chunk0 = nchunks;
             nchunks += j->nchunks;
-            j->o_words = total;
-            total += up256(((j->zlen + 3) & ~size_t(3)) + kPad);
             j->o_u16 = total;
             total += up256(2 * (j->raw_total + 64));
             j->o_ft = total;
@@ -326,8 +581,8 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
         const size_t unf_tab = up256(sizeof(int2) * ngroups) + up256(sizeof(int) * m);
         const size_t unf_zero = up256(sizeof(unsigned) * (nbands + 8));
         dyn += up256(sizeof(int2) * nrows) + up256(sizeof(int) * npages) + unf_tab + unf_zero + up256(2 * tok_total);
-        uint8_t* dev = rc ? nullptr : scratch_slot(2, o_dyn + dyn);
-        if (!rc && !dev) rc = fail(IK_ERR_DEVICE, "cannot allocate the PNG batch work area (%zu bytes)", o_dyn + dyn);
+        uint8_t* dev = scratch_slot(2, o_dyn + dyn);
+        if (!dev) rc = fail(IK_ERR_DEVICE, "cannot allocate the PNG batch work area (%zu bytes)", o_dyn + dyn);
         PngLaneDev* d_lanes = nullptr;
         infl::LaneResult* d_res = nullptr;
         int64_t* d_obase = nullptr;
@@ -361,30 +616,22 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
         Xfer X;
         if (!rc && !X.init(2 * sizeof(PngLaneDev) * max_lanes + sizeof(infl::LaneResult) * max_lanes +
                                sizeof(int64_t) * (max_lanes + nchunks) + 2 * sizeof(int) * max_lanes +
-                               sizeof(int2) * (nrows + ngroups) + sizeof(int) * (npages + 2 * m) +
-                               3 * sizeof(PngImgDev) * m + (64u << 10), s))
+                               sizeof(int2) * (nrows + ngroups) + sizeof(int) * (npages + 4 * m) +
+                               3 * sizeof(PngImgDev) * m + 2 * sizeof(int) * nchunks + (64u << 10), s))
             rc = fail(IK_ERR_NOMEM, "cannot allocate pinned PNG transfer area");
-        // phases: staging + upload + block search under the device's upload gate,
-        // the decode kernels on under its kernel gate (ik_runtime.h), so that
-        // concurrent batches take the GPU in turn
-        gate_enter(kGateUpload);
-        // with the device free, each stream's block search runs as soon as its copy
-        // lands; with another batch's kernels running, the searches wait for the
-        // kernel gate (sharing the CUs with those kernels slows both)
-        const bool early = gate_try_enter(kGateKernels);
-        // ---- image descriptors and the chunk table (before any stream lands) ----
+        // the kernels run under the device's kernel gate (ik_runtime.h)
+        gate_enter(kGateKernels);
+        // ---- image descriptors and the chunk table ----
         std::vector<PngImgDev> hd(m);
         // the large host tables are kept per thread between batches (clear() keeps
         // the capacity): fresh multi-MB vectors cost page faults every batch
         static thread_local HostTables ht;
-        std::vector<int>& hchunk_img = ht.chunk_img;
-        std::vector<int>& hchunk_idx = ht.chunk_idx;
-        hchunk_img.assign(nchunks, 0);
-        hchunk_idx.assign(nchunks, 0);
+        std::vector<int>& hchunk = ht.chunk_img;
+        hchunk.assign(2 * (size_t)nchunks, 0);
         for (int k = 0; k < m && !rc; ++k) {
             PngJob& j = *J[k];
             PngImgDev& d = hd[k];
-            d.words = reinterpret_cast<const uint32_t*>(dev + j.o_words);
+            d.words = reinterpret_cast<const uint32_t*>(A->dev + S.o_zs + j.z_off);
             d.bit0 = 16;
             d.nbits = j.nbits;
             d.u16 = reinterpret_cast<uint16_t*>(dev + j.o_u16);
@@ -394,141 +641,35 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             d.bpp = j.bpp;
             d.ft = dev + j.o_ft;
             for (int c = 0; c < j.nchunks; ++c) {
-                hchunk_img[j.chunk0 + c] = k;
-                hchunk_idx[j.chunk0 + c] = c;
+                hchunk[j.chunk0 + c] = k;
+                hchunk[nchunks + j.chunk0 + c] = c;
             }
         }
-        if (!rc) rc = copy_h2d_2d(dev + o_ctab, sizeof(int) * nchunks, reinterpret_cast<const uint8_t*>(hchunk_img.data()),
-                                  sizeof(int) * nchunks, sizeof(int) * nchunks, 1, s);
-        if (!rc) rc = copy_h2d_2d(dev + o_ctab + sizeof(int) * nchunks, sizeof(int) * nchunks,
-                                  reinterpret_cast<const uint8_t*>(hchunk_idx.data()), sizeof(int) * nchunks,
-                                  sizeof(int) * nchunks, 1, s);
-        if (!rc) rc = copy_h2d_2d(dev + o_imgs, sizeof(PngImgDev) * m, reinterpret_cast<const uint8_t*>(hd.data()),
-                                  sizeof(PngImgDev) * m, sizeof(PngImgDev) * m, 1, s);
         const PngImgDev* d_imgs = reinterpret_cast<const PngImgDev*>(dev + o_imgs);
         const int* d_cimg = reinterpret_cast<const int*>(dev + o_ctab);
         const int* d_cidx = d_cimg + nchunks;
         int64_t* d_cand = reinterpret_cast<int64_t*>(dev + o_cand);
-        uint8_t* pin = rc ? nullptr : pinned_slot(1, zbytes + 64);
-        if (!rc && !pin) rc = fail(IK_ERR_NOMEM, "cannot allocate pinned PNG staging");
-        // IDAT payloads -> pinned (host threads), CRC-checked on the way (png
-        // verifies every chunk's CRC).  Each stream's H2D copy goes out on the copy
-        // stream as soon as it is staged, and its block search on the compute stream
-        // as soon as the copy has landed (an event), so the PCIe transfer overlaps
-        // the staging of the later streams and the search the transfer
-        hipStream_t sc = rc ? nullptr : thread_copy_stream();
-        if (!rc && !sc) rc = fail(IK_ERR_DEVICE, "cannot create the PNG copy stream");
-        static thread_local std::vector<hipEvent_t> landed;
-        while (!rc && (int)landed.size() < m) {
-            hipEvent_t e = nullptr;
-            if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-                rc = fail(IK_ERR_DEVICE, "cannot create PNG upload events");
-                break;
-            }
-            landed.push_back(e);
-        }
-        // (the workers below see their own thread_local vector: pass the caller's)
-        hipEvent_t* const ev_landed = landed.data();
-        std::vector<char> crc_bad(m, 0);
-        std::atomic<int> up_err{0};
-        std::atomic<long long> t_copy_calls{0};  // dev timing: us spent inside hipMemcpyAsync
-        const double t_stage0 = now_ms();
-        double t_stage1 = t_stage0;
-        if (!rc) {
-            rec(0, s);
-            // the first streams go up in pieces of <= kPiece bytes, so the PCIe transfer
-            // starts after one piece is staged instead of after whole 35-MB streams
-            // (measured: 5.5 ms from a batch's start to its first copy); the thread
-            // that finishes a stream's last piece records its event, launches its
-            // block search and then checks its CRCs; whole streams check their CRCs
-            // while staging, as before
-            constexpr size_t kPiece = size_t(4) << 20;
-            constexpr int kPieced = 2;
-            struct Piece { int k; size_t lo, n; };
-            std::vector<Piece> pieces;
-            std::vector<std::vector<size_t>> seg_off(m);  // logical start of each IDAT segment (pieced streams)
-            std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[m]);
-            for (int k = 0; k < m; ++k) {
-                const PngJob& j = *J[k];
-                const size_t tot = ((j.zlen + 3) & ~size_t(3)) + kPad;
-                const size_t piece = k < kPieced ? kPiece : tot;
-                int np = 0;
-                for (size_t lo = 0; lo < tot; lo += piece, ++np) pieces.push_back(Piece{k, lo, std::min(piece, tot - lo)});
-                left[k] = np;
-                if (np > 1) {
-                    size_t o = 0;
-                    for (auto& seg : j.idat) { seg_off[k].push_back(o); o += seg.second; }
-                }
-            }
-            parallel_for((int)pieces.size(), 0, [&, s, sc](int pi) {
-                const Piece P = pieces[pi];
-                const int k = P.k;
-                const PngJob& j = *J[k];
-                const bool whole = P.lo == 0 && seg_off[k].empty();
-                uint8_t* d = pin + j.z_off + P.lo;
-                if (whole) {
-                    for (auto& seg : j.idat) {
-                        if (png_chunk_crc(seg.first - 4, seg.first, seg.second) != be32(seg.first + seg.second)) crc_bad[k] = 1;
-                        std::memcpy(d, seg.first, seg.second);
-                        d += seg.second;
-                    }
-                    std::memset(d, 0, pin + j.z_off + P.n - d);
-                } else {
-                    const std::vector<size_t>& so = seg_off[k];
-                    size_t lo = P.lo, n = P.n;
-                    size_t si = (size_t)(std::upper_bound(so.begin(), so.end(), lo) - so.begin()) - 1;
-                    while (n && lo < j.zlen) {
-                        const size_t in = lo - so[si], c = std::min(n, (size_t)j.idat[si].second - in);
-                        std::memcpy(d, j.idat[si].first + in, c);
-                        d += c; lo += c; n -= c; ++si;
-                    }
-                    if (n) std::memset(d, 0, n);
-                }
-                // one plain copy per piece (no memset kernel ahead of it, which would
-                // wait for a CU while other kernels run)
-                const double tc0 = timing ? now_ms() : 0.0;
-                hipError_t e = hipMemcpyAsync(dev + j.o_words + P.lo, pin + j.z_off + P.lo, P.n, hipMemcpyHostToDevice, sc);
-                if (timing) t_copy_calls += (long long)(1000.0 * (now_ms() - tc0));
-                if (left[k].fetch_sub(1) == 1) {  // the stream is all queued
-                    if (early) {
-                        if (e == hipSuccess) e = hipEventRecord(ev_landed[k], sc);
-                        if (e == hipSuccess) e = hipStreamWaitEvent(s, ev_landed[k], 0);
-                        if (e == hipSuccess)
-                            e = launch_png_find(d_imgs, d_cimg + j.chunk0, d_cidx + j.chunk0, j.nchunks, cbits,
-                                                d_cand + j.chunk0, s);
-                    }
-                    if (!whole)
-                        for (auto& seg : j.idat)
-                            if (png_chunk_crc(seg.first - 4, seg.first, seg.second) != be32(seg.first + seg.second))
-                                crc_bad[k] = 1;
-                }
-                if (e != hipSuccess) up_err = (int)e;
-            });
-            t_stage1 = now_ms();
-            gate_leave(kGateUpload);
-            if (!early) {  // all copies are on sc: one event after the last, then one search launch
-                gate_enter(kGateKernels);
-                hipError_t e = hipEventRecord(ev_landed[0], sc);
-                if (e == hipSuccess) e = hipStreamWaitEvent(s, ev_landed[0], 0);
-                if (e == hipSuccess) e = launch_png_find(d_imgs, d_cimg, d_cidx, nchunks, cbits, d_cand, s);
-                if (e != hipSuccess) up_err = (int)e;
-            }
-            rec(1, s);
-        }
-        if (!rc && up_err) rc = hip_fail((hipError_t)up_err.load(), "PNG stream upload / block search");
-        for (int k = 0; k < m; ++k)
-            if (crc_bad[k]) J[k]->state = -1;  // the host decoder reports png's CRC error
-        const double t1 = now_ms();
-        // ---- candidates ----
+        // ---- the block search over every stream once its upload has landed ----
+        hipError_t e = rc ? hipSuccess : X.h2d(dev + o_ctab, hchunk.data(), sizeof(int) * 2 * nchunks);
+        if (!rc && e == hipSuccess) e = X.h2d(dev + o_imgs, hd.data(), sizeof(PngImgDev) * m);
+        if (!rc && e == hipSuccess && A->ev[2]) e = hipStreamWaitEvent(s, A->ev[2], 0);
+        rec(8, s);
+        if (!rc && e == hipSuccess) e = launch_png_find(d_imgs, d_cimg, d_cidx, nchunks, cbits, d_cand, s);
+        rec(9, s);
         std::vector<int64_t>& cand = ht.cand;
         cand.assign(nchunks, 0);
-        if (!rc) {
-            hipError_t e = X.d2h(cand.data(), d_cand, sizeof(int64_t) * nchunks);
-            if (e != hipSuccess) rc = hip_fail(e, "PNG block search");
+        std::vector<int> crc_err(m, 0);
+        if (!rc && e == hipSuccess) e = X.d2h(cand.data(), d_cand, sizeof(int64_t) * nchunks);
+        if (!rc && e == hipSuccess) {
+            e = launch_copy_words(reinterpret_cast<const uint32_t*>(A->dev + S.o_err),
+                                  reinterpret_cast<uint32_t*>(dev + o_err), (size_t)m, s);
+            if (e == hipSuccess) e = X.d2h(crc_err.data(), dev + o_err, sizeof(int) * m);
         }
-        gate_leave(kGateUpload);   // (error paths)
-        gate_enter(kGateKernels);
-        const double t_gate = now_ms();
+        if (!rc && e != hipSuccess) rc = hip_fail(e, "PNG block search");
+        for (int k = 0; k < m; ++k)
+            if (crc_err[k]) reject(*J[k], "IDAT CRC");  // the host decoder reports png's CRC error
+        const double t1 = now_ms();
+        tim[15] = t1 - t0;  // from the stage's start until the candidates are back (upload wait + search)
         const double t2 = now_ms();
         double mk[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // dev timing marks (IK_PNG_TIMING)
         for (PngJob* j : J) {
@@ -587,10 +728,10 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             hres.resize(hl.size());
             if (!mk[0]) mk[0] = now_ms();  // plan built, lanes uploaded (first round)
             rec(2, s);
-            hipError_t e = launch_png_decode(d_imgs, d_lanes, (int)hl.size(), d_tok, d_res, s);
+            hipError_t e2 = launch_png_decode(d_imgs, d_lanes, (int)hl.size(), d_tok, d_res, s);
             rec(3, s);
-            if (e == hipSuccess) e = X.d2h(hres.data(), d_res, sizeof(infl::LaneResult) * hl.size());
-            if (e != hipSuccess) { rc = hip_fail(e, "PNG inflate (decode)"); break; }
+            if (e2 == hipSuccess) e2 = X.d2h(hres.data(), d_res, sizeof(infl::LaneResult) * hl.size());
+            if (e2 != hipSuccess) { rc = hip_fail(e2, "PNG inflate (decode)"); break; }
             count_dev += ev_ms(2, 3);
             ++rounds;
             std::vector<char> again(m, 0);  // a job with overflowed lanes: those first, then the check
@@ -620,6 +761,10 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                 else if (st < 0) reject(j, "lane chain check");
             }
         }
+        // the compressed streams are read for the last time (every decode round's
+        // results were synchronised): the next batch may upload into the area
+        (void)hipStreamSynchronize(s);
+        release_area(S.area);
         const double t3 = now_ms();
         // ---- offsets, output images, expand, resolve, unfilter ----
         std::vector<int64_t>& hob = ht.obase;
@@ -636,15 +781,23 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             uint64_t tot = 0;
             pngplan::offsets(j.lanes, ob, &tot);
             if (tot != j.raw_total) { reject(j, "image data length"); continue; }  // png's error
-            if (alloc_image(j.w, j.h, (uint32_t)j.bpp, &j.img)) { reject(j, "image allocation"); continue; }
+            if (j.expand) {  // unfiltered rows in a row image, then k_png_px into the output image
+                if (alloc_image((uint32_t)j.rowbytes, j.h, 1, &j.rows) || alloc_image(j.w, j.h, (uint32_t)j.out_c, &j.img)) {
+                    reject(j, "image allocation");
+                    continue;
+                }
+            } else if (alloc_image(j.w, j.h, (uint32_t)j.bpp, &j.img)) {
+                reject(j, "image allocation");
+                continue;
+            }
             hd[k].obase = d_obase + hob.size();
             hd[k].page_lane = d_pages + npg;  // (the page table itself is built while expand runs)
             hd[k].nlanes = (int)ob.size();
             pj.emplace_back(k, hob.size());
             npg += (j.raw_total >> kPngPageShift) + 1;
-            hd[k].dst = j.img->d;
-            hd[k].pitch = j.img->pitch;
-            for (size_t i = 0; i < ob.size(); ++i) t_png_timing[12] += (double)j.lanes.res[i].ntok;
+            hd[k].dst = j.expand ? j.rows->d : j.img->d;
+            hd[k].pitch = j.expand ? j.rows->pitch : j.img->pitch;
+            for (size_t i = 0; i < ob.size(); ++i) tim[12] += (double)j.lanes.res[i].ntok;
             for (size_t i = 0; i < ob.size(); ++i) {
                 PngLaneDev L{};
                 L.tbase = j.lanes.tbase[i];
@@ -675,9 +828,9 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             hxst.resize(2 * hl.size());
             mk[2] = now_ms();  // lane tables uploaded
             if (!rc) {
-                hipError_t e = hipSuccess;
+                hipError_t e3 = hipSuccess;
                 rec(4, s);
-                if (e == hipSuccess) e = launch_png_expand(d_imgs, d_lanes, (int)hl.size(), d_tok, d_xst, s);
+                if (e3 == hipSuccess) e3 = launch_png_expand(d_imgs, d_lanes, (int)hl.size(), d_tok, d_xst, s);
                 rec(5, s);
                 // page -> decoder that holds the page's first byte (resolve's lane lookup)
                 for (const auto& q : pj) {
@@ -690,14 +843,14 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                     }
                     for (uint32_t y = 0; y < j.h; ++y) hrows.push_back(make_int2(q.first, (int)y));
                 }
-                if (e == hipSuccess) e = X.h2d(d_pages, hpages.data(), sizeof(int) * hpages.size());
-                if (e == hipSuccess) e = X.h2d(d_rows, hrows.data(), sizeof(int2) * hrows.size());
-                if (e == hipSuccess) e = launch_png_resolve(d_imgs, d_rows, (int)hrows.size(),
-                                                            reinterpret_cast<int*>(dev + o_err), s);
+                if (e3 == hipSuccess) e3 = X.h2d(d_pages, hpages.data(), sizeof(int) * hpages.size());
+                if (e3 == hipSuccess) e3 = X.h2d(d_rows, hrows.data(), sizeof(int2) * hrows.size());
+                if (e3 == hipSuccess) e3 = launch_png_resolve(d_imgs, d_rows, (int)hrows.size(),
+                                                              reinterpret_cast<int*>(dev + o_err), s);
                 rec(6, s);
                 // unfilter: one launch per bytes-per-pixel class, over that class's
                 // images; a workgroup per 16 bands, its (image, group) by ticket
-                if (e == hipSuccess) {
+                if (e3 == hipSuccess) {
                     std::vector<PngImgDev> cls;
                     std::vector<int2> groups;
                     std::vector<int> pbase;
@@ -720,29 +873,39 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                     std::vector<uint8_t> tabs(unf_tab, 0);
                     std::memcpy(tabs.data(), groups.data(), sizeof(int2) * groups.size());
                     std::memcpy(tabs.data() + gb, pbase.data(), sizeof(int) * pbase.size());
-                    e = X.h2d(d_unf, tabs.data(), unf_tab);
+                    e3 = X.h2d(d_unf, tabs.data(), unf_tab);
                     unsigned* d_prog = reinterpret_cast<unsigned*>(d_unf + unf_tab);
                     unsigned* d_ticket = d_prog + nbands;
-                    if (e == hipSuccess) e = hipMemsetAsync(d_prog, 0, unf_zero, s);
-                    if (e == hipSuccess) e = X.h2d(d_cls, cls.data(), sizeof(PngImgDev) * cls.size());
+                    if (e3 == hipSuccess) e3 = hipMemsetAsync(d_prog, 0, unf_zero, s);
+                    if (e3 == hipSuccess) e3 = X.h2d(d_cls, cls.data(), sizeof(PngImgDev) * cls.size());
                     const int2* d_groups = reinterpret_cast<const int2*>(d_unf);
                     const int* d_pbase = reinterpret_cast<const int*>(d_unf + gb);
-                    for (size_t r = 0; r < ranges.size() && e == hipSuccess; ++r) {
+                    for (size_t r = 0; r < ranges.size() && e3 == hipSuccess; ++r) {
                         const int g1 = r + 1 < ranges.size() ? ranges[r + 1].grp0 : (int)groups.size();
                         const int g0 = ranges[r].grp0, i0 = ranges[r].img0;
-                        e = launch_png_unfilter(d_cls + i0, d_groups + g0, g1 - g0, d_pbase + i0, d_prog,
-                                                d_ticket + r, ranges[r].bpp, s);
+                        e3 = launch_png_unfilter(d_cls + i0, d_groups + g0, g1 - g0, d_pbase + i0, d_prog,
+                                                 d_ticket + r, ranges[r].bpp, s);
                     }
                 }
+                // png's EXPAND for the palette / low-bit / tRNS images
+                for (int k = 0; k < m && e3 == hipSuccess; ++k) {
+                    PngJob& j = *J[k];
+                    if (j.state != 1 || !j.expand || !j.rows) continue;
+                    j.px.src = j.rows->d;
+                    j.px.sp = j.rows->pitch;
+                    j.px.dst = j.img->d;
+                    j.px.dp = j.img->pitch;
+                    e3 = launch_png_px(j.px, s);
+                }
                 rec(7, s);
-                if (e == hipSuccess) e = X.d2h(hxst.data(), d_xst, 2 * sizeof(int) * hl.size());
-                if (e == hipSuccess) e = X.d2h(herr.data(), dev + o_err, sizeof(int) * m);
+                if (e3 == hipSuccess) e3 = X.d2h(hxst.data(), d_xst, 2 * sizeof(int) * hl.size());
+                if (e3 == hipSuccess) e3 = X.d2h(herr.data(), dev + o_err, sizeof(int) * m);
                 mk[3] = now_ms();  // expand .. unfilter done
-                if (e != hipSuccess) rc = hip_fail(e, "PNG inflate (expand) / unfilter");
+                if (e3 != hipSuccess) rc = hip_fail(e3, "PNG inflate (expand) / unfilter");
                 if (!rc) {
-                    t_png_timing[3] = ev_ms(4, 5);
-                    t_png_timing[4] = ev_ms(5, 6);
-                    t_png_timing[5] = ev_ms(6, 7);
+                    tim[3] = ev_ms(4, 5);
+                    tim[4] = ev_ms(5, 6);
+                    tim[5] = ev_ms(6, 7);
                 }
             }
             if (!rc) {
@@ -757,7 +920,6 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                 }
             }
         }
-        gate_leave(kGateUpload);   // (error paths)
         gate_leave(kGateKernels);  // unless the caller pinned it (transform_part: resize + encode next)
         if (timing && !hl.empty()) {  // per-lane profile of the last decode round and the expand pass
             double si = 0, sc = 0, sx = 0, mi = 0, mc = 0, mx = 0, sb = 0, mb = 0;
@@ -775,24 +937,34 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
                     "max %.0f (%.0f cycles/iter); expand kcycles mean %.0f max %.0f\n", hres.size(), si / n1, mi, sb / n1,
                     mb, sc / n1, mc, 1024.0 * sc / std::max(1.0, si), sx / n2, mx);
         }
-        t_png_timing[0] = t1 - t0;
-        t_png_timing[1] = ev_ms(0, 1);
-        t_png_timing[2] = count_dev;
-        t_png_timing[7] = rounds;
-        t_png_timing[8] = (double)hl.size();
-        t_png_timing[9] = m;
+        tim[0] = S.t_host;
+        if (A && A->ev[0] && A->ev[2]) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, A->ev[0], A->ev[2]) == hipSuccess) tim[1] = ms;
+            if (hipEventElapsedTime(&ms, A->ev[1], A->ev[2]) == hipSuccess) tim[14] = ms;
+        }
+        tim[2] = count_dev;
+        tim[7] = rounds;
+        tim[8] = (double)hl.size();
+        tim[9] = m;
+        tim[13] = ev_ms(8, 9);
         if (timing)
-            fprintf(stderr, "[png] t=%.1f %d streams (%d on the GPU): stage %.2f ms, find %.2f ms (kernel gate at +%.2f), "
-                    "decode %.2f ms (%d rounds, %d dropped, %d overflows), expand+resolve+unfilter %.2f ms; staging "
-                    "loop %.2f ms (early %d), in hipMemcpyAsync %.2f ms summed\n",
-                    fmod(t0, 1e5), n, m, t1 - t0, t2 - t1, t_gate - t0, t3 - t2, rounds, dropped, overflows, now_ms() - t3,
-                    t_stage1 - t_stage0, (int)early, 1e-3 * (double)t_copy_calls.load());
+            fprintf(stderr, "[png] t=%.1f %d streams (%d on the GPU): upload host %.2f ms, upload device %.2f ms (gather "
+                    "%.2f), waited+find %.2f ms (find %.2f), decode %.2f ms (%d rounds, %d dropped, %d overflows), "
+                    "expand+resolve+unfilter %.2f ms\n",
+                    fmod(t0, 1e5), n, m, tim[0], tim[1], tim[14], t1 - t0, tim[13], t3 - t2, rounds, dropped, overflows,
+                    now_ms() - t3);
         if (timing)
             fprintf(stderr, "[png] host: plan+lanes %.2f, (decode rounds) .. tables %.2f, rows+uploads %.2f, "
                     "(expand..unfilter) %.2f, after %.2f ms\n", mk[0] - t2, mk[1] - t3, mk[2] - mk[1], mk[3] - mk[2],
                     now_ms() - mk[3]);
+    }
+    release_area(S.area);  // (error paths)
+    if (m) {
+        (void)hipStreamSynchronize(s);  // the row images are read
         for (int k = 0; k < m; ++k) {
             PngJob& j = *J[k];
+            if (j.rows) { ik_image_free(j.rows); j.rows = nullptr; }
             if (!rc && j.state == 1) {
                 outs[j.idx] = j.img;
                 j.img = nullptr;
@@ -809,8 +981,8 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
     std::vector<int> host;
     for (int i = 0; i < n; ++i)
         if (!gpu[i]) host.push_back(i);
-    t_png_timing[11] = (double)host.size();
-    t_png_timing[10] = (double)(n - (int)host.size());
+    tim[11] = (double)host.size();
+    tim[10] = (double)(n - (int)host.size());
     g_png_gpu_streams += (unsigned long long)(n - (int)host.size());
     g_png_host_streams += (unsigned long long)host.size();
     parallel_for((int)host.size(), 0, [&](int k) {
@@ -828,12 +1000,24 @@ int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_
             msgs[i] = buf;
         }
     });
-    t_png_timing[6] = now_ms() - t0;
+    tim[6] = now_ms() - t0;
+    if (m) {
+        std::lock_guard<std::mutex> lk(g_timing_mu);
+        g_timing[S.device].assign(tim, tim + kPngTimingFields);
+    }
     if (timing) fprintf(stderr, "[png] decode_png_batch returns at t=%.1f\n", fmod(now_ms(), 1e5));
+    up.st.reset();
     int first = IK_OK;
     for (int i = 0; i < n; ++i)
         if (status[i] && !first) first = status[i];
     return first;
+}
+
+int decode_png_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_image** outs, int* status,
+                     std::string* msgs) {
+    PngUpload up;
+    png_upload_begin(bytes, lens, n, up);
+    return png_decode_finish(up, outs, status, msgs);
 }
 
 }  // namespace ik
@@ -845,7 +1029,14 @@ extern "C" int ik_png_counters(unsigned long long* out) {
 }
 
 extern "C" int ik_png_last_timing(double* out, int n) {
-    for (int i = 0; i < n && i < 13; ++i) out[i] = ik::t_png_timing[i];
+    if (!out) return ik::fail(IK_ERR_INVALID, "null pointer");
+    std::vector<double> t;
+    {
+        std::lock_guard<std::mutex> lk(ik::g_timing_mu);
+        auto it = ik::g_timing.find(ik::current_device());
+        if (it != ik::g_timing.end()) t = it->second;
+    }
+    for (int i = 0; i < n; ++i) out[i] = i < (int)t.size() ? t[i] : 0.0;
     return IK_OK;
 }
 

@@ -10,7 +10,9 @@
 #include <cstring>
 #include <vector>
 
+#include "ik_crc.h"
 #include "ik_inflate.h"
+#include "ik_png_gather.h"
 #include "ik_png_plan.h"
 
 using namespace ik;
@@ -151,6 +153,113 @@ int ikm_inflate_chunked(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8
     stats[4] = markers;
     *out_len = total;
     return 0;
+}
+
+// The upload gather pass (ik_png.hip k_png_gather + k_png_crc_check) on the host:
+// the same plan (ik_png_gather.h), the same per-thread split (256 B per thread,
+// bytes until the destination is word aligned, then words), the same tree join of
+// the 256 partial CRCs and the same chunk check.  file: a whole PNG file as
+// uploaded at raw offset `raw_off` (the destination alignment follows z_off).
+// Writes the assembled zlib stream + `tail` zero bytes to stream[z_off ..];
+// bad[k] = 1 for each IDAT chunk whose CRC does not match; returns the number of
+// IDAT chunks (-1 on a malformed chunk walk).
+int ikm_gather_check(const uint8_t* file, size_t len, uint64_t z_off, uint32_t tail, uint8_t* stream, size_t cap,
+                     int* bad, int bad_cap) {
+    auto be32 = [](const uint8_t* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; };
+    std::vector<std::pair<const uint8_t*, uint32_t>> idat;
+    size_t pos = 8;
+    while (pos + 12 <= len) {
+        const uint32_t n = be32(file + pos);
+        if (n > len - pos - 12) return -1;
+        if (!std::memcmp(file + pos + 4, "IDAT", 4) && n) idat.emplace_back(file + pos + 8, n);
+        if (!std::memcmp(file + pos + 4, "IEND", 4)) break;
+        pos += 12 + n;
+    }
+    std::vector<PngGatherPiece> pieces;
+    std::vector<PngCrcChunk> chunks;
+    png_gather_plan(file, 0, idat, z_off, tail, 0, pieces, chunks);
+    uint32_t t[1024], x2n[32], level[8];
+    for (uint32_t i = 0; i < 256; ++i) t[i] = crc::table_entry(i);
+    for (int sl = 1; sl < 4; ++sl)
+        for (int i = 0; i < 256; ++i) t[256 * sl + i] = (t[256 * (sl - 1) + i] >> 8) ^ t[t[256 * (sl - 1) + i] & 255u];
+    crc::x2n_table(x2n);
+    for (int k = 0; k < 8; ++k) level[k] = crc::x8n((uint64_t)256 << k, x2n);
+    std::vector<uint32_t> piece_crc(2 * pieces.size());
+    for (size_t b = 0; b < pieces.size(); ++b) {
+        const PngGatherPiece& P = pieces[b];
+        if (P.dst + P.len > cap) return -1;
+        uint32_t sc[256], sl[256];
+        for (uint32_t tid = 0; tid < 256; ++tid) {
+            const uint32_t b0 = 256u * tid;
+            const uint32_t n = P.len > b0 ? (P.len - b0 < 256u ? P.len - b0 : 256u) : 0u;
+            uint32_t c = ~0u;
+            uint8_t* dp = stream + P.dst + b0;
+            if (n && P.src == kPngNoSrc) {
+                std::memset(dp, 0, n);
+            } else if (n) {
+                const uint8_t* sp = file + P.src + b0;
+                uint32_t i = 0;
+                const uint32_t mis = (uint32_t)((P.dst + b0) & 3u);
+                const uint32_t pre = mis ? (4u - mis < n ? 4u - mis : n) : 0u;
+                for (; i < pre; ++i) { dp[i] = sp[i]; c = crc::step_byte(c, sp[i], t); }
+                for (; i + 4 <= n; i += 4) {
+                    uint32_t v;
+                    std::memcpy(&v, sp + i, 4);
+                    std::memcpy(dp + i, &v, 4);
+                    c = crc::step_word(c, v, t);
+                }
+                for (; i < n; ++i) { dp[i] = sp[i]; c = crc::step_byte(c, sp[i], t); }
+            }
+            sc[tid] = ~c;
+            sl[tid] = n;
+        }
+        for (int k = 0; k < 8; ++k) {
+            const int stride = 1 << k;
+            for (int tid = 0; tid < 256; tid += 2 * stride) {
+                const uint32_t rl = sl[tid + stride];
+                if (!rl) continue;
+                const uint32_t op = rl == (256u << k) ? level[k] : crc::x8n(rl, x2n);
+                sc[tid] = crc::combine_op(sc[tid], sc[tid + stride], op);
+                sl[tid] += rl;
+            }
+        }
+        piece_crc[2 * b] = sc[0];
+        piece_crc[2 * b + 1] = sl[0];
+    }
+    uint32_t cidat = ~0u;
+    for (const char ch : {'I', 'D', 'A', 'T'}) cidat = crc::step_byte(cidat, (uint8_t)ch, t);
+    cidat = ~cidat;
+    for (size_t k = 0; k < chunks.size(); ++k) {
+        uint32_t c = cidat;
+        for (uint32_t p = chunks[k].piece0; p < chunks[k].piece0 + chunks[k].npieces; ++p)
+            c = crc::combine_op(c, piece_crc[2 * p], crc::x8n(piece_crc[2 * p + 1], x2n));
+        if ((int)k < bad_cap) bad[k] = c != be32(file + chunks[k].crc_at);
+    }
+    return (int)chunks.size();
+}
+
+// finished CRC-32 of data split into pieces / 256-B runs and joined (ik_crc.h), for
+// direct comparison with zlib.crc32
+uint32_t ikm_crc32_joined(const uint8_t* data, size_t len, size_t run) {
+    uint32_t t[1024], x2n[32];
+    for (uint32_t i = 0; i < 256; ++i) t[i] = crc::table_entry(i);
+    for (int sl = 1; sl < 4; ++sl)
+        for (int i = 0; i < 256; ++i) t[256 * sl + i] = (t[256 * (sl - 1) + i] >> 8) ^ t[t[256 * (sl - 1) + i] & 255u];
+    crc::x2n_table(x2n);
+    uint32_t acc = 0;
+    for (size_t o = 0; o < len; o += run) {
+        const size_t n = len - o < run ? len - o : run;
+        uint32_t c = ~0u;
+        size_t i = 0;
+        for (; i + 4 <= n; i += 4) {
+            uint32_t v;
+            std::memcpy(&v, data + o + i, 4);
+            c = crc::step_word(c, v, t);
+        }
+        for (; i < n; ++i) c = crc::step_byte(c, data[o + i], t);
+        acc = crc::combine_op(acc, ~c, crc::x8n(n, x2n));
+    }
+    return acc;
 }
 
 // the candidate test alone at one bit position (for the filter-strength test)

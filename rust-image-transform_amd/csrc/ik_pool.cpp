@@ -99,7 +99,7 @@ bool gate_try_enter(int which) {
     return true;
 }
 
-bool gate_held_any() { return t_gate.held[kGateKernels]; }
+bool gate_held_any() { return t_gate.held[kGateKernels] || t_gate.held[kGateUpload]; }
 
 void gate_leave(int which) {
     if (!t_gate.held[which] || t_gate.pinned[which]) return;
@@ -149,9 +149,9 @@ void Pool::loop() {
 void Pool::post(std::function<void()> task) { post_tagged(std::move(task), nullptr); }
 
 void Pool::post_tagged(std::function<void()> task, const void* tag) {
-    // work for a caller inside a GPU phase (it holds a phase gate) goes to the front
-    // of the queue: behind another batch's bulk host work (staging copies, libwebp)
-    // it would keep the GPU phase -- and the gate, and the device -- waiting
+    // work for a caller inside a GPU phase (it holds a phase gate: an upload or a
+    // kernel stage) goes to the front of the queue: behind another batch's bulk
+    // host work (libwebp) it would keep the GPU phase -- and the device -- waiting
     const bool urgent = gate_held_any();
     {
         std::lock_guard<std::mutex> lk(mu_);

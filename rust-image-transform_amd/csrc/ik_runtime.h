@@ -5,6 +5,7 @@
 #include <cstdint>
 #include <deque>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -165,6 +166,25 @@ uint32_t png_chunk_crc(const uint8_t* type, const uint8_t* data, size_t len);  /
 // and message; returns the first failure.
 int decode_png_batch(const uint8_t* const* b, const size_t* lens, int n, ik_image** outs, int* status,
                      std::string* msgs);
+// decode_png_batch as two stages, so that one batch's upload (PCIe + the GPU
+// gather / CRC pass, on the calling thread's copy stream) runs under the previous
+// batch's kernels: png_upload_begin parses the streams and issues the upload
+// (returns once issued); png_decode_finish, on the kernel stage's thread, runs the
+// decode kernels once the upload has landed.  The input arrays stay valid until
+// finish returns; every begin is finished exactly once.
+struct PngBatchState;
+struct PngUpload {
+    const uint8_t* const* bytes = nullptr;
+    const size_t* lens = nullptr;
+    int n = 0;
+    std::shared_ptr<PngBatchState> st;
+};
+int png_upload_begin(const uint8_t* const* b, const size_t* lens, int n, PngUpload& up);
+int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* msgs);
+constexpr int kPngTimingFields = 16;  // ik_png_last_timing
+// caller-pinned host memory (ik_host_alloc / ik_host_register): [p, p + n) lies
+// inside one such range, so DMAs may read it in place
+bool host_pinned(const void* p, size_t n);
 bool png_gpu_enabled(size_t raw_bytes);  // IK_PNG_GPU / IK_PNG_GPU_MIN policy
 int decode_webp(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& c, std::vector<uint8_t>& px);
 
@@ -209,7 +229,7 @@ int resize_group(const std::vector<ik_image*>& src, uint32_t nw, uint32_t nh, in
 enum { kGateUpload = 0, kGateKernels = 1 };
 void gate_enter(int which);
 bool gate_try_enter(int which);  // true if now held (or gates are off)
-bool gate_held_any();            // this thread holds its device's kernel gate
+bool gate_held_any();            // this thread holds one of its device's gates
 void gate_leave(int which);
 void gate_pin(int which, bool on);
 

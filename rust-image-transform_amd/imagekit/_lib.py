@@ -30,6 +30,10 @@ SIGNATURES = [
     ("ik_schedule_plan", None, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
     ("ik_last_error", ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_size_t]),
     ("ik_version", ctypes.c_char_p, []),
+    ("ik_host_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+    ("ik_host_free", ctypes.c_int, [ctypes.c_void_p]),
+    ("ik_host_register", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
+    ("ik_host_unregister", ctypes.c_int, [ctypes.c_void_p]),
     ("ik_image_from_host", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(c_img_p)]),
     ("ik_image_wrap_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_size_t, ctypes.POINTER(c_img_p)]),
     ("ik_image_info", ctypes.c_int, [c_img_p, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),

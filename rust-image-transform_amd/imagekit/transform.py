@@ -176,17 +176,56 @@ def decode_image_batch(datas) -> List[Tuple[DynamicImage, Optional[ImageFormat]]
     return [(imgs[i], None if fmts[i] < 0 else ImageFormat(fmts[i])) for i in range(n)]
 
 
+class PinnedBytes:
+    """Encoded input bytes in page-locked host memory (ik_host_alloc): the batch
+    calls DMA them to the GPU in place, with no staging copy -- what a server does
+    by reading request bodies into such buffers.  Accepted wherever the batch
+    calls take `bytes`."""
+
+    __slots__ = ("ptr", "len", "__weakref__")
+
+    def __init__(self, data: bytes):
+        lib = _lib.load()
+        p = ctypes.c_void_p()
+        if lib.ik_host_alloc(max(1, len(data)), ctypes.byref(p)) != 0:
+            raise TransformError(_lib.last_error())
+        ctypes.memmove(p, data, len(data))
+        self.ptr, self.len = p.value, len(data)
+
+    def __len__(self) -> int:
+        return self.len
+
+    def tobytes(self) -> bytes:
+        return ctypes.string_at(self.ptr, self.len)
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            try:
+                _lib.load().ik_host_free(ctypes.c_void_p(self.ptr))
+            except Exception:
+                pass
+            self.ptr = None
+
+
+def _inputs(datas):
+    """(keep-alive list, pointer array, length array) for a batch call."""
+    keep = [d if isinstance(d, PinnedBytes) else bytes(d) for d in datas]
+    n = len(keep)
+    ptrs = (ctypes.c_void_p * n)(*[d.ptr if isinstance(d, PinnedBytes) else
+                                   ctypes.cast(ctypes.c_char_p(d), ctypes.c_void_p).value for d in keep])
+    lens = (ctypes.c_size_t * n)(*[len(d) for d in keep])
+    return keep, ptrs, lens
+
+
 def transform_batch(datas, sizes, fmts, qualities, filter: "FilterType" = None, threads: int = 0) -> List[bytes]:
     """ik_transform_batch: decode -> resize_image -> encode_image for many requests
     (sizes: (w, h) per request, None = unset; fmts: ImageFormat per request)."""
     lib = _lib.load()
-    bufs = [bytes(d) for d in datas]
+    bufs, ptrs, lens = _inputs(datas)
     n = len(bufs)
     if n == 0:
         return []
     filt = int(FilterType.Lanczos3 if filter is None else filter)
-    ptrs = (ctypes.c_void_p * n)(*[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p) for b in bufs])
-    lens = (ctypes.c_size_t * n)(*[len(b) for b in bufs])
     ws = (ctypes.c_int64 * n)(*[-1 if s[0] is None else int(s[0]) for s in sizes])
     hs = (ctypes.c_int64 * n)(*[-1 if s[1] is None else int(s[1]) for s in sizes])
     fs = (ctypes.c_int * n)(*[int(f.value if isinstance(f, ImageFormat) else f) for f in fmts])
@@ -236,13 +275,11 @@ def transform_batch_submit(datas, sizes, fmts, qualities, filter: "FilterType" =
     """ik_transform_batch_submit: the device half of transform_batch now, the host
     coders in the background; PendingBatch.wait() gives what transform_batch gives."""
     lib = _lib.load()
-    bufs = [bytes(d) for d in datas]
+    bufs, ptrs, lens = _inputs(datas)
     n = len(bufs)
     if n == 0:
         raise InvalidArgument("empty batch")
     filt = int(FilterType.Lanczos3 if filter is None else filter)
-    ptrs = (ctypes.c_void_p * n)(*[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p) for b in bufs])
-    lens = (ctypes.c_size_t * n)(*[len(b) for b in bufs])
     ws = (ctypes.c_int64 * n)(*[-1 if s[0] is None else int(s[0]) for s in sizes])
     hs = (ctypes.c_int64 * n)(*[-1 if s[1] is None else int(s[1]) for s in sizes])
     fs = (ctypes.c_int * n)(*[int(f.value if isinstance(f, ImageFormat) else f) for f in fmts])

@@ -209,3 +209,176 @@ def test_transform_from_png_bytes(on_gpu, oracle):
     got = transform(data, 128, 128, ImageFormat.webp, 80, filter=1)
     want, dims = oracle.transform(img, 128, 128, 1, 1, 80)
     assert dims == (128, 128) and got == want
+
+
+def test_gpu_crc_check_in_batch(gpu_png):
+    """The upload's GPU gather pass checks every IDAT CRC (png 0.18 verifies them):
+    in one batch, a payload byte flipped in the second IDAT chunk and a stored CRC
+    flipped in the last one each give png's CRC error for that stream only (the
+    host decoder reports it); the intact streams decode on the GPU."""
+    imgs = [ikutil.synth(700, 300 + 50 * k, 4, seed=70 + k, pattern="N" if k % 2 else "S") for k in range(4)]
+    datas = [own_png(im, idat_size=20000) for im in imgs]
+    bad_payload = bytearray(datas[1])
+    p = bad_payload.index(b"IDAT")
+    p = bad_payload.index(b"IDAT", p + 4)  # the second IDAT chunk
+    bad_payload[p + 4 + 777] ^= 0x01
+    bad_crc = bytearray(datas[3])
+    q = bad_crc.rindex(b"IDAT")
+    ln = struct.unpack(">I", bad_crc[q - 4:q])[0]
+    bad_crc[q + 4 + ln + 1] ^= 0x80
+    batch = [datas[0], bytes(bad_payload), datas[2], bytes(bad_crc)]
+    lib = _lib.load()
+    n = len(batch)
+    ptrs = (ctypes.c_void_p * n)(*[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p) for b in batch])
+    lens = (ctypes.c_size_t * n)(*[len(b) for b in batch])
+    outs = (ctypes.c_void_p * n)()
+    fmts = (ctypes.c_int * n)()
+    status = (ctypes.c_int * n)()
+    g0, h0 = png_counters(gpu_png)
+    rc = lib.ik_decode_batch(ptrs, lens, n, outs, fmts, status)
+    g1, h1 = png_counters(gpu_png)
+    assert rc != 0 and "crc" in _lib.last_error().lower()
+    assert [status[i] != 0 for i in range(n)] == [False, True, False, True]
+    assert (g1 - g0, h1 - h0) == (2, 2)
+    from imagekit.transform import DynamicImage
+    for i in (0, 2):
+        np.testing.assert_array_equal(DynamicImage(outs[i]).to_array(), imgs[i])
+
+
+def test_pinned_inputs_equal_pageable(on_gpu):
+    """Inputs in page-locked memory (ik_host_alloc, DMAed in place) and in
+    ordinary memory (staged) give the same bytes through transform_batch."""
+    from imagekit import ImageFormat, PinnedBytes, transform_batch
+    imgs = [ikutil.synth(1200, 900, c, seed=90 + c) for c in (3, 4)]
+    datas = [pil_png(im) for im in imgs]
+    pinned = [PinnedBytes(d) for d in datas]
+    assert [p.tobytes() for p in pinned] == datas
+    sizes, fmts, qs = [(300, None)] * 2, [ImageFormat.webp, ImageFormat.jpeg], [80, 85]
+    a = transform_batch(datas, sizes, fmts, qs, filter=1)
+    b = transform_batch(pinned, sizes, fmts, qs, filter=1)
+    c = transform_batch([pinned[0], datas[1]], sizes, fmts, qs, filter=1)
+    assert a == b == c
+
+
+def _pack_rows(samples, depth):
+    """(h, w) samples < 2^depth -> packed PNG rows (MSB first), filter byte 0 or 1..4 cycling."""
+    h, w = samples.shape
+    per = 8 // depth
+    rows = []
+    for y in range(h):
+        v = samples[y].astype(np.int64)
+        if depth < 8:
+            pad = (-w) % per
+            v = np.concatenate([v, np.zeros(pad, np.int64)]).reshape(-1, per)
+            shifts = np.array([8 - depth * (k + 1) for k in range(per)])
+            row = (v << shifts).sum(1).astype(np.uint8)
+        else:
+            row = v.astype(np.uint8)
+        rows.append(row)
+    return rows
+
+
+def expand_png(samples, depth, ctype, plte=None, trns=None, level=6):
+    """A PNG of gray / palette / RGB samples at `depth` bits with optional PLTE / tRNS;
+    rows cycle through the five filter types (bpp = 1 byte below 8 bits)."""
+    if ctype == 2:
+        h, w, _ = samples.shape
+        raw_rows = [samples[y].reshape(-1).astype(np.uint8) for y in range(h)]
+        bpp = 3
+    else:
+        h, w = samples.shape
+        raw_rows = _pack_rows(samples, depth)
+        bpp = 1
+    out_rows, prev = [], np.zeros(len(raw_rows[0]), np.int32)
+    for y, r in enumerate(raw_rows):
+        cur = r.astype(np.int32)
+        a = np.concatenate([np.zeros(bpp, np.int32), cur[:-bpp]])
+        c = np.concatenate([np.zeros(bpp, np.int32), prev[:-bpp]])
+        ft = y % 5
+        if ft == 0:
+            f = cur
+        elif ft == 1:
+            f = cur - a
+        elif ft == 2:
+            f = cur - prev
+        elif ft == 3:
+            f = cur - ((a + prev) >> 1)
+        else:
+            p = a + prev - c
+            pa, pb, pc = np.abs(p - a), np.abs(p - prev), np.abs(p - c)
+            f = cur - np.where((pa <= pb) & (pa <= pc), a, np.where(pb <= pc, prev, c))
+        out_rows.append(bytes([ft]) + (f & 255).astype(np.uint8).tobytes())
+        prev = cur
+    z = zlib.compress(b"".join(out_rows), level)
+    out = b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, depth, ctype, 0, 0, 0))
+    if plte is not None:
+        out += chunk(b"PLTE", plte)
+    if trns is not None:
+        out += chunk(b"tRNS", trns)
+    for i in range(0, len(z), 30000):
+        out += chunk(b"IDAT", z[i:i + 30000])
+    return out + chunk(b"IEND", b"")
+
+
+EXPAND_CASES = [("P", 8, False), ("P", 8, True), ("P", 4, False), ("P", 4, True), ("P", 2, True), ("P", 1, False),
+                ("L", 1, False), ("L", 2, False), ("L", 4, False), ("L", 8, True), ("L", 4, True), ("L", 1, True),
+                ("RGB", 8, True)]
+
+
+@pytest.mark.parametrize("kind,depth,with_trns", EXPAND_CASES)
+@pytest.mark.parametrize("w,h", [(333, 77), (1001, 300)])
+def test_expand_on_gpu(gpu_png, kind, depth, with_trns, w, h):
+    """png's EXPAND on the GPU path (k_png_px): palette -> RGB / RGBA, gray below 8
+    bits -> 8 bits, tRNS -> alpha; pixels equal the EXPAND rule and the host decoder."""
+    rng = np.random.default_rng(w * 131 + depth * 7 + with_trns)
+    if kind == "P":
+        npal = min(1 << depth, 200 if depth == 8 else 1 << depth)
+        pal = rng.integers(0, 256, (npal, 3), dtype=np.uint8)
+        idx = rng.integers(0, min(1 << depth, npal + 3), (h, w)).astype(np.uint8)  # a few indices past the palette
+        trns = rng.integers(0, 256, max(1, npal // 2), dtype=np.uint8) if with_trns else None
+        data = expand_png(idx, depth, 3, plte=pal.tobytes(), trns=None if trns is None else trns.tobytes())
+        big = np.zeros((256, 3), np.uint8)
+        big[:npal] = pal
+        want = big[idx]
+        if trns is not None:
+            alpha = np.full(256, 255, np.uint8)
+            alpha[:len(trns)] = trns
+            want = np.concatenate([want, alpha[idx][..., None]], -1)
+    elif kind == "L":
+        v = rng.integers(0, 1 << depth, (h, w)).astype(np.uint8)
+        key = int(v[3, 5])
+        data = expand_png(v, depth, 0, trns=struct.pack(">H", key) if with_trns else None)
+        g = (v.astype(np.int32) * {1: 255, 2: 85, 4: 17, 8: 1}[depth]).astype(np.uint8)
+        want = g[..., None]
+        if with_trns:
+            want = np.concatenate([want, np.where(v == key, 0, 255).astype(np.uint8)[..., None]], -1)
+    else:
+        px = rng.integers(0, 4, (h, w, 3)).astype(np.uint8) * 60  # few colours: the key hits often
+        key = px[2, 2]
+        data = expand_png(px, 8, 2, trns=struct.pack(">HHH", *[int(k) for k in key]))
+        want = np.concatenate([px, np.where((px == key).all(-1), 0, 255).astype(np.uint8)[..., None]], -1)
+    g0, h0 = png_counters(gpu_png)
+    got = decode_px(data)
+    g1, h1 = png_counters(gpu_png)
+    assert (g1 - g0, h1 - h0) == (1, 0), "the stream must decode on the GPU path"
+    np.testing.assert_array_equal(got, want)
+    gpu_png.ik_set_png_gpu_min(-1)
+    try:
+        host = decode_px(data)
+    finally:
+        gpu_png.ik_set_png_gpu_min(0)
+    np.testing.assert_array_equal(host, want)
+
+
+def test_pillow_palette_pngs(on_gpu):
+    """Pillow's own palette PNGs (P mode, with and without transparency) through the GPU path."""
+    rng = np.random.default_rng(5)
+    idx = rng.integers(0, 60, (480, 640)).astype(np.uint8)
+    im = Image.fromarray(idx, "P")
+    im.putpalette(rng.integers(0, 256, 768, dtype=np.uint8).tobytes())
+    for kw in ({}, {"transparency": 7}, {"transparency": bytes(range(0, 240, 4))}):
+        b = io.BytesIO()
+        im.save(b, format="PNG", **kw)
+        data = b.getvalue()
+        want = np.asarray(Image.open(io.BytesIO(data)).convert("RGBA" if kw else "RGB"))
+        np.testing.assert_array_equal(decode_px(data), want)

@@ -33,8 +33,16 @@ S, O, B = 4096, 512, 64
 TRI = 1
 
 
+STREAM = None
+
+
 def timed(lib, src, dst, reps=5):
-    st = torch.cuda.current_stream()
+    # a stream of our own: torch's default stream is the null stream (handle 0),
+    # which the library would read as "use the thread's stream"
+    global STREAM
+    if STREAM is None:
+        STREAM = torch.cuda.Stream()
+    st = STREAM
     ms = []
     for r in range(reps + 1):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -55,6 +63,7 @@ def main():
     assert lib.ik_init(0) == 0
     out = {}
     frames = [ikutil.synth(S, S, 4, seed=s, pattern="S") for s in range(4)]
+    torch.cuda.synchronize()
     src = torch.empty((B, S, S * 4), dtype=torch.uint8, device="cuda")
     for i in range(B):
         src[i].copy_(torch.from_numpy(frames[i % 4].reshape(S, S * 4)))
