@@ -56,7 +56,8 @@ FILTERS = {"nearest": 0, "triangle": 1, "catmullrom": 2, "gaussian": 3, "lanczos
 FORMATS = {"jpeg": 0, "webp": 1, "avif": 2}
 # ik_png_last_timing fields reported (index -> name; include/imagekit_hip.h)
 PNG_STAGES = {0: "upload_host", 1: "upload_device", 14: "gather_crc", 15: "kernel_stage_wait_find", 13: "find",
-              2: "decode", 3: "expand", 4: "resolve", 5: "unfilter", 6: "kernel_stage_wall"}
+              2: "decode", 3: "expand", 4: "resolve", 5: "unfilter", 6: "kernel_stage_wall",
+              16: "find_beside_previous_batch"}
 
 
 def parse():
@@ -320,7 +321,7 @@ def main():
 
     # ---- headline: PNG bytes in host memory -> WebP bytes in host memory ----
     stage_ms = []
-    NT = 16  # ik_png_last_timing fields
+    NT = 17  # ik_png_last_timing fields
 
     def note_timing():
         timing = (ctypes.c_double * NT)()  # the last PNG batch the device finished

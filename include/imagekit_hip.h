@@ -123,7 +123,7 @@ int ik_decode_batch(const uint8_t *const *bytes, const size_t *lens, uint32_t n,
  * the GPU finds inconsistent use the host decoder.  -1 = host decoder only.
  * Default 256 KiB (IK_PNG_GPU_MIN; IK_PNG_GPU=0 = off). */
 int ik_set_png_gpu_min(long long min_raw_bytes);
-/* the last GPU PNG batch finished on the calling thread's device (n <= 16 values):
+/* the last GPU PNG batch finished on the calling thread's device (n <= 17 values):
  * [0] upload stage host ms (parse, staging copies of unpinned inputs, DMA issue),
  * device ms of [1] the upload (first DMA .. gather + CRC done) [2] decode rounds
  * [3] expand [4] resolve [5] unfilter, [6] kernel stage wall ms, [7] decode rounds,
@@ -132,7 +132,7 @@ int ik_set_png_gpu_min(long long min_raw_bytes);
  * rejected by it), [12] tokens written by the verified decoder lanes (u16 each),
  * device ms of [13] the block search [14] the gather + CRC pass, [15] kernel stage
  * ms until the block search's candidates were back (waiting for the upload
- * included) */
+ * included), [16] 1 if the block search ran beside the previous batch's kernels */
 int ik_png_last_timing(double *out, int n);
 /* process-wide counts of PNG streams decoded since load: out[0] by the GPU path,
  * out[1] by the host decoder (outside the GPU path, or rejected by it) */

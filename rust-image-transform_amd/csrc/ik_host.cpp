@@ -1305,6 +1305,16 @@ private:
                 continue;
             }
             Ticket& t = *p->t;
+            // once this batch's decode rounds are done, the next queued batch's
+            // block search goes out beside this batch's expand / resolve / unfilter
+            p->up.on_decoded = [this] {
+                std::shared_ptr<BatchPart> nx;
+                {
+                    std::lock_guard<std::mutex> lk(mu_);
+                    if (!q_[1].empty()) nx = q_[1].front();
+                }
+                if (nx && !nx->pb.empty()) png_find_prelaunch(nx->up, thread_copy_stream());
+            };
             transform_device_phase(p->bytes, p->lens, p->w, p->h, p->fmt, p->quality, p->filter, t.st.data(),
                                    t.errs.data(), p->hp, p->pb.empty() ? nullptr : &p->up);
             p->up = PngUpload();

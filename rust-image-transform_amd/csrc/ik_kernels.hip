@@ -27,6 +27,12 @@ __device__ __forceinline__ int lds_idx(int i) { return i + ((i >> 5) << 2); }
 // v_readfirstlane (the tables are never written by a kernel).
 template <typename T>
 using cptr = const __attribute__((address_space(4))) T*;
+// output rows in the global address space: global_store (vmcnt only).  A generic
+// pointer makes them flat_store, which count in vmcnt and lgkmcnt; with one
+// pending, LLVM's wait-count pass cannot order vmcnt and falls back to vmcnt(0)
+// at every row of the fused kernel's prefetch ring (measured 1.44 vs 1.03 ms per
+// 64 x 4096^2 -> 512^2 Triangle launch when dst became a loaded generic pointer)
+typedef __attribute__((address_space(1))) uint8_t g_u8;
 template <typename T>
 __device__ __forceinline__ cptr<T> as_const(const T* p) { return (cptr<T>)p; }
 
@@ -50,7 +56,7 @@ template <int C, bool FMA, int kHTaps = 2>
 __device__ __forceinline__ void horizontal_rows_c(const ResizeArgs& a, const float* __restrict__ lds,
                                                   const float* __restrict__ sw, const int* __restrict__ soff,
                                                   int r0, int nrows, int ox0, int nox, int hq, int hox,
-                                                  uint8_t* __restrict__ dst) {
+                                                  g_u8* __restrict__ dst) {
     const int total = nox * nrows;
     const int Tx = a.Tx;
     for (int v = threadIdx.x; v < total; v += kThreads) {
@@ -100,11 +106,11 @@ __device__ __forceinline__ void horizontal_rows_c(const ResizeArgs& a, const flo
                     }
                 }
         }
-        uint8_t* o = dst + (size_t)(r0 + q) * a.dst_pitch + (size_t)(ox0 + oxl) * C;
+        g_u8* o = dst + (size_t)(r0 + q) * a.dst_pitch + (size_t)(ox0 + oxl) * C;
         if constexpr (C == 4) {
             const unsigned u = (unsigned)float_nearest_u8(acc[0]) | ((unsigned)float_nearest_u8(acc[1]) << 8) |
                                ((unsigned)float_nearest_u8(acc[2]) << 16) | ((unsigned)float_nearest_u8(acc[3]) << 24);
-            *reinterpret_cast<unsigned*>(o) = u;  // dst rows are 256-B pitched, columns 4-B aligned
+            *reinterpret_cast<__attribute__((address_space(1))) unsigned*>(o) = u;  // dst rows are 256-B pitched, columns 4-B aligned
         } else {
 #pragma unroll
             for (int c = 0; c < C; ++c) o[c] = float_nearest_u8(acc[c]);
@@ -116,7 +122,7 @@ template <bool FMA>
 __device__ __forceinline__ void horizontal_rows(const ResizeArgs& a, const float* __restrict__ lds,
                                                 const float* __restrict__ sw, const int* __restrict__ soff,
                                                 int r0, int nrows, int ox0, int nox, int hq, int hox,
-                                                uint8_t* __restrict__ dst) {
+                                                g_u8* __restrict__ dst) {
     switch (a.C) {
     case 4: horizontal_rows_c<4, FMA>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
     case 3: horizontal_rows_c<3, FMA>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
@@ -169,9 +175,12 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
     const int nox = ox1 - ox0;
     const int oy0 = bands[2 * band], oy1 = bands[2 * band + 1];
     const int kb = bstep[band], ke = bstep[band + 1];
+    // per-image bases through the constant address space (img is wave-uniform:
+    // scalar loads); dst in the global address space (g_u8, see above)
     const uint8_t* __restrict__ src =
-        a.src_tab ? reinterpret_cast<const uint8_t*>(a.src_tab[img]) : a.src + (size_t)img * a.src_img_stride;
-    uint8_t* __restrict__ dst = a.dst_tab ? reinterpret_cast<uint8_t*>(a.dst_tab[img]) : a.dst + (size_t)img * a.dst_img_stride;
+        a.src_tab ? reinterpret_cast<const uint8_t*>(as_const(a.src_tab)[img]) : a.src + (size_t)img * a.src_img_stride;
+    g_u8* __restrict__ dst = (g_u8*)(a.dst_tab ? reinterpret_cast<uint8_t*>(as_const(a.dst_tab)[img])
+                                               : a.dst + (size_t)img * a.dst_img_stride);
 
     float* __restrict__ s_w = lds + F * kRowWords;
     int* __restrict__ s_off = reinterpret_cast<int*>(s_w + (WL ? a.max_strip_weights : 0));

@@ -79,6 +79,9 @@ hipError_t launch_png_crc_check(const uint8_t* raw, const PngCrcChunk* chunks, i
 // dst[i] = src[i] for n words, on the compute stream; one side may be pinned host
 // memory (the small transfers of the PNG kernel phase: ik_png_decode.cpp Xfer)
 hipError_t launch_copy_words(const uint32_t* src, uint32_t* dst, size_t n, hipStream_t s);
+#ifdef IK_FIND_PROF
+hipError_t png_find_prof_read(unsigned long long* out);  // dev build: k_png_find's phase clock sums (reset)
+#endif
 hipError_t launch_png_find(const PngImgDev* imgs, const int* chunk_img, const int* chunk_idx, int n,
                            uint64_t chunk_bits, int64_t* cand, hipStream_t s);
 hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, int n, uint16_t* tok,

@@ -26,6 +26,8 @@
 //                   it is published (global progress counters, agent-scope
 //                   release/acquire; workgroups ordered by a start ticket).
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "ik_crc.h"
@@ -44,16 +46,171 @@ namespace ik {
 // all of their top four bits set) -- and only the survivors (about a fifth)
 // take the scalar Kraft test of the code-length code (complete: sum 2^-len == 1).
 // Offsets passing it (~0.1 %: under two per wave step) go into a per-wave LDS
-// queue, and the streaming header check (ik_inflate.h dynamic_header_ok, LDS
-// code-length table per lane) runs on 64 queued offsets at a time, one per
-// lane -- run one by one as they turn up, it would take the whole wave for one
-// or two active lanes.  The result is the first offset of the chunk that passes
+// queue, and the streaming header check (find_check_win: infl::dynamic_header_ok's
+// test over an LDS window of the stream) runs on 64 queued offsets at a time,
+// one per lane -- run one by one as they turn up, it would take the whole wave
+// for one or two active lanes.  The result is the first offset of the chunk that passes
 // every test, as before: the queue is checked whenever it holds 64 offsets and at
 // the end of the chunk, and once some offset passed, the smallest passing one of
 // everything checked so far is the answer.
-__device__ __attribute__((noinline)) bool find_full_check(const uint32_t* words, uint64_t nbits, uint64_t p,
-                                                          uint32_t h, uint64_t bits, uint8_t* tab) {
-    return infl::dynamic_header_ok(words, nbits, p, h, bits, tab);
+// The same test as infl::dynamic_header_ok (the same accept set: the CPU model's
+// search uses that one), shaped for the GPU's flush, where 64 lanes check 64
+// candidates at once and the wave waits for its slowest lane (a true header's
+// ~300 code lengths, a false one's median ~32):
+//  - the lane's next 32 stream words are fetched into its LDS window with all 32
+//    loads in flight (refetched when the decode runs past them), so the symbol
+//    loop waits on LDS, not on one dependent global load per word;
+//  - the code-length code is decoded canonically (its left-justified limits,
+//    first codes and rank offsets packed bytewise in registers; the symbols in
+//    canonical order, 19 bytes per lane in LDS), so no 128-entry table is built
+//    per candidate.
+// win: this lane's window, word k at win[64 k]; syms: its 19 symbol bytes, entry
+// i at syms[64 i].
+typedef __attribute__((address_space(3))) uint32_t lds_word;
+typedef __attribute__((address_space(3))) uint8_t lds_byte;
+__device__ __attribute__((noinline)) bool find_check_win(const IK_GLOBAL uint32_t* W, uint64_t nbits, uint64_t p,
+                                                         uint32_t h, uint64_t bits, lds_word* win, lds_byte* syms) {
+    const int nlen = (int)((h >> 3) & 31u) + 257, ndist = (int)((h >> 8) & 31u) + 1;
+    const int ncode = (int)((h >> 13) & 15u) + 4;
+    // code-length code: count per length, then ranks in canonical (length, symbol) order
+    constexpr uint8_t inv_order[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};
+    uint64_t cnt = 0;  // byte L: codes of length L (L = 1..7)
+#pragma unroll
+    for (int s = 0; s < 19; ++s) {
+        const int i = inv_order[s];
+        const uint32_t len = i < ncode ? (uint32_t)(bits >> (3 * i)) & 7u : 0u;
+        if (len) cnt += 1ull << (8 * len);
+    }
+    uint64_t first = 0, offs = 0, lim = 0;  // bytes L: first code, rank of the first code, left-justified limit
+    {
+        uint32_t code = 0, rank = 0;
+#pragma unroll
+        for (int L = 1; L <= 7; ++L) {
+            const uint32_t cprev = L > 1 ? (uint32_t)(cnt >> (8 * (L - 1))) & 255u : 0u;
+            const uint32_t cl = (uint32_t)(cnt >> (8 * L)) & 255u;
+            code = (code + cprev) << 1;
+            first |= (uint64_t)code << (8 * L);
+            offs |= (uint64_t)rank << (8 * L);
+            lim |= (uint64_t)((code + cl) << (7 - L)) << (8 * L);
+            rank += cl;
+        }
+    }
+    {
+        uint64_t ctr = 0;  // byte L: symbols of length L placed so far
+#pragma unroll
+        for (int s = 0; s < 19; ++s) {
+            const int i = inv_order[s];
+            const uint32_t len = i < ncode ? (uint32_t)(bits >> (3 * i)) & 7u : 0u;
+            if (len) {
+                const uint32_t r = ((uint32_t)(offs >> (8 * len)) & 255u) + ((uint32_t)(ctr >> (8 * len)) & 255u);
+                syms[64 * r] = (uint8_t)s;
+                ctr += 1ull << (8 * len);
+            }
+        }
+    }
+    // bit reader over the LDS window
+    const uint64_t wend = (nbits >> 5) + 4;  // words past it read as zero (as infl::Bits)
+    const uint64_t bit = p + 17 + 3 * (uint64_t)ncode;
+    uint64_t wb = bit >> 5;  // window base (word index)
+    // 32 words by LDS-DMA (global_load_lds_dword: lane l's word lands at M0 + 4 l, so
+    // row k of the lane-minor window takes one instruction for the whole wave), all
+    // in flight at once, no VGPRs; near the end of the stream (past the zero padding
+    // the window could reach) word by word with the bounds check
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const uint32_t r0 = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)win - 4u * lane);  // row 0, lane 0
+    auto fetch = [&](uint64_t base) {
+        if (base + 32 > wend + 64) {
+            for (int k = 0; k < 32; ++k) win[64 * k] = base + k < wend ? W[base + k] : 0u;
+            return;
+        }
+        const IK_GLOBAL uint32_t* src = W + base;
+        uint32_t keep;
+#define IK_FWIN(K)                                                                                     \
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t" \
+                 "s_mov_b32 m0, %0 ; fwin " #K                                                         \
+                 : "=&s"(keep)                                                                         \
+                 : "v"(src + K), "s"(__builtin_amdgcn_readfirstlane(r0 + 256u * K))                   \
+                 : "memory")
+        IK_FWIN(0); IK_FWIN(1); IK_FWIN(2); IK_FWIN(3); IK_FWIN(4); IK_FWIN(5); IK_FWIN(6); IK_FWIN(7);
+        IK_FWIN(8); IK_FWIN(9); IK_FWIN(10); IK_FWIN(11); IK_FWIN(12); IK_FWIN(13); IK_FWIN(14); IK_FWIN(15);
+        IK_FWIN(16); IK_FWIN(17); IK_FWIN(18); IK_FWIN(19); IK_FWIN(20); IK_FWIN(21); IK_FWIN(22); IK_FWIN(23);
+        IK_FWIN(24); IK_FWIN(25); IK_FWIN(26); IK_FWIN(27); IK_FWIN(28); IK_FWIN(29); IK_FWIN(30); IK_FWIN(31);
+#undef IK_FWIN
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    fetch(wb);
+    uint64_t buf = (uint64_t)(win[0] >> (bit & 31));
+    int n = 32 - (int)(bit & 31);
+    uint32_t k = 1;  // next window word
+    auto refill = [&]() {
+        if (n < 32) {
+            if (k == 32) {
+                wb += 32;
+                fetch(wb);
+                k = 0;
+            }
+            buf |= (uint64_t)win[64 * k] << n;
+            n += 32;
+            ++k;
+        }
+    };
+    auto get = [&](int bitsn) {
+        refill();
+        const uint32_t v = (uint32_t)buf & ((1u << bitsn) - 1u);
+        buf >>= bitsn;
+        n -= bitsn;
+        return v;
+    };
+    const int total = nlen + ndist;
+    int i = 0, prev = -1;
+    uint32_t kl = 0, kd = 0;
+    int maxl = 0, maxd = 0;
+    bool eob = false;
+    while (i < total) {
+        refill();
+        const uint32_t c = __builtin_bitreverse32((uint32_t)buf) >> 25;  // the next 7 bits, first bit as MSB
+        int L = 1;
+#pragma unroll
+        for (int l = 1; l < 7; ++l) L += c >= ((uint32_t)(lim >> (8 * l)) & 255u) ? 1 : 0;
+        const uint32_t r = (c >> (7 - L)) - ((uint32_t)(first >> (8 * L)) & 255u) + ((uint32_t)(offs >> (8 * L)) & 255u);
+        const int sym = syms[64 * r];
+        buf >>= L;
+        n -= L;
+        int rep = 1, val = sym;
+        if (sym == 16) {
+            if (prev < 0) return false;
+            val = prev;
+            rep = 3 + (int)get(2);
+        } else if (sym == 17) {
+            val = 0;
+            rep = 3 + (int)get(3);
+        } else if (sym == 18) {
+            val = 0;
+            rep = 11 + (int)get(7);
+        }
+        if (i + rep > total) return false;
+        if (val) {
+            const int nl = i < nlen ? (i + rep <= nlen ? rep : nlen - i) : 0;
+            const int nd = rep - nl;
+            if (nl) {
+                kl += (uint32_t)nl << (15 - val);
+                if (kl > 32768u) return false;
+                if (val > maxl) maxl = val;
+                if (i <= 256 && 256 < i + nl) eob = true;
+            }
+            if (nd) {
+                kd += (uint32_t)nd << (15 - val);
+                if (kd > 32768u) return false;
+                if (val > maxd) maxd = val;
+            }
+        }
+        i += rep;
+        prev = val;
+    }
+    if (!eob) return false;
+    if (kl != 32768u && !(maxl == 1 && kl == 16384u)) return false;
+    if (kd != 0u && kd != 32768u && !(maxd == 1 && kd == 16384u)) return false;
+    return true;
 }
 
 __device__ __forceinline__ uint32_t fsh(uint32_t lo, uint32_t hi, int k) {  // bits k .. k+31 of hi:lo, 0 < k < 32
@@ -71,9 +228,20 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 
 constexpr uint32_t kFindQueue = 128;
 
+#ifdef IK_FIND_PROF  // dev build: per-phase clock sums of k_png_find (tools/gpu_*.sh experiments)
+__device__ unsigned long long g_find_prof[8];
+hipError_t png_find_prof_read(unsigned long long* out) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_find_prof), sizeof(g_find_prof));
+    unsigned long long z[8] = {};
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_find_prof), z, sizeof(z));
+    return e;
+}
+#endif
+
 __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const int* chunk_img, const int* chunk_idx,
                                                  int nchunks_total, uint64_t chunk_bits, int64_t* cand) {
-    __shared__ uint8_t s_tab[64 * 128];     // per lane: code-length code lookup (symbol | length << 5)
+    __shared__ uint32_t s_win[64 * 32];     // per lane: 32 stream words of the candidate being checked (lane-minor)
+    __shared__ uint8_t s_sym[64 * 20];      // per lane: code-length-code symbols in canonical order (lane-minor)
     __shared__ uint32_t s_q[kFindQueue];    // Kraft-passing offsets (relative to the chunk) awaiting the full check
     __shared__ uint8_t s_kraft[512];        // 3 code-length-code lengths (9 bits) -> sum of 2^(7 - len), len > 0
     const int g = blockIdx.x;
@@ -100,7 +268,16 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
     const IK_GLOBAL uint32_t* W = (const IK_GLOBAL uint32_t*)I.words;
     uint32_t qlen = 0;           // wave-uniform
     uint32_t best = 0xFFFFFFFFu; // smallest passing offset checked so far (relative to b0)
+#ifdef IK_FIND_PROF
+    const unsigned long long t_begin = __builtin_readcyclecounter();
+    unsigned long long t_flush = 0, n_flush = 0, n_steps = 0, n_cand = 0;
+#endif
     auto flush = [&]() {
+#ifdef IK_FIND_PROF
+        const unsigned long long tf0 = __builtin_readcyclecounter();
+        n_flush += qlen ? 1 : 0;
+        n_cand += qlen;
+#endif
         for (uint32_t q0 = 0; q0 < qlen; q0 += 64) {
             uint32_t v = 0xFFFFFFFFu;
             if (q0 + (uint32_t)lane < qlen) {
@@ -117,18 +294,25 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
                 (void)x; (void)cl;
                 v = off;
 #else
-                if (find_full_check(I.words, I.nbits, p, (uint32_t)x, cl, s_tab + 128 * lane)) v = off;
+                if (find_check_win(W, I.nbits, p, (uint32_t)x, cl, (lds_word*)(s_win + lane), (lds_byte*)(s_sym + lane)))
+                    v = off;
 #endif
             }
             v = wave_min(v);
             best = v < best ? v : best;
         }
         qlen = 0;
+#ifdef IK_FIND_PROF
+        t_flush += __builtin_readcyclecounter() - tf0;
+#endif
     };
     const uint64_t wlast = (b1 + 31) >> 5;  // words holding offsets < b1 (the stream is zero padded past them)
     uint64_t wi = (b0 >> 5) + (uint64_t)lane;
     uint32_t n0 = W[wi], n1 = W[wi + 1], n2 = W[wi + 2], n3 = W[wi + 3];
     for (;;) {
+#ifdef IK_FIND_PROF
+        ++n_steps;
+#endif
         const uint32_t w0 = n0, w1 = n1, w2 = n2, w3 = n3;
         const uint64_t wn = wi + 64;
         if (wn - (uint64_t)lane < wlast) {  // wave-uniform: prefetch the next step's words
@@ -182,6 +366,16 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
     }
     flush();
     if (lane == 0) cand[g] = best == 0xFFFFFFFFu ? -1 : (int64_t)(b0 + best);
+#ifdef IK_FIND_PROF
+    if (lane == 0) {
+        atomicAdd(&g_find_prof[0], __builtin_readcyclecounter() - t_begin);
+        atomicAdd(&g_find_prof[1], t_flush);
+        atomicAdd(&g_find_prof[2], n_flush);
+        atomicAdd(&g_find_prof[3], n_steps);
+        atomicAdd(&g_find_prof[4], n_cand);
+        atomicAdd(&g_find_prof[5], 1ull);
+    }
+#endif
 }
 
 // ---- inflate ------------------------------------------------------------------------
@@ -549,16 +743,17 @@ __global__ __launch_bounds__(256) void k_png_resolve(const PngImgDev* imgs, cons
         I.ft[y] = (uint8_t)(v < 0 ? 255 : v);
         if (v < 0 || v > 4) atomicOr(err + ir.x, 1);
     }
-    uint8_t* const drow = I.dst + (size_t)y * I.pitch;
+    // (global address space: global_* ops, counted in vmcnt only, not flat_*)
+    IK_GLOBAL uint8_t* const drow = (IK_GLOBAL uint8_t*)(I.dst + (size_t)y * I.pitch);
     for (int x0 = threadIdx.x * 16; x0 < I.rowbytes; x0 += 256 * 16) {
         const int64_t e0 = rs + 1 + x0;
         // 16 u16 symbols from 9 dwords in three loads (two dwordx4 at a dword-aligned
         // address, the u16 buffer is padded), shifted by one symbol when e0 is odd
         // (uniform over the row), then each output dword packs the low bytes of four
         // symbols with one v_perm
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(I.u16) + (e0 >> 1);
+        const IK_GLOBAL uint32_t* w = (const IK_GLOBAL uint32_t*)(reinterpret_cast<const uint32_t*>(I.u16) + (e0 >> 1));
         typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-        const u4 va = *reinterpret_cast<const u4*>(w), vb = *reinterpret_cast<const u4*>(w + 4);
+        const u4 va = *reinterpret_cast<const IK_GLOBAL u4*>(w), vb = *reinterpret_cast<const IK_GLOBAL u4*>(w + 4);
         const uint32_t d[9] = {va.x, va.y, va.z, va.w, vb.x, vb.y, vb.z, vb.w, w[8]};
         uint32_t e[8];
         if (e0 & 1) {
@@ -593,7 +788,7 @@ __global__ __launch_bounds__(256) void k_png_resolve(const PngImgDev* imgs, cons
                 o[i >> 2] = (o[i >> 2] & ~(255u << (8 * (i & 3)))) | (((uint32_t)rv & 255u) << (8 * (i & 3)));
             }
         }
-        *reinterpret_cast<uint4*>(drow + x0) = make_uint4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<IK_GLOBAL uint4*>(drow + x0) = make_uint4(o[0], o[1], o[2], o[3]);
     }
     __syncthreads();  // (also orders the chunk stores before the marker bytes below)
     const uint32_t cnt = s_cnt < (uint32_t)kResolveList ? s_cnt : (uint32_t)kResolveList;
@@ -810,6 +1005,158 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngI
     }
 }
 
+// The same wavefront over 8-byte chunks (BPP <= 4).  The chain of a frame is
+// (row chunks + rows) steps -- every band starts 64 steps after the one above it,
+// so with 16-byte chunks 4,096 of a 4096^2 RGBA frame's 5,120 steps are that lag --
+// and a step's cost is the chunk's bytes: halving the chunk takes the chain to
+// 2,048 + 4,096 steps of half the work.
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t byte2(const uint32_t (&w)[2], int i) { return (w[i >> 2] >> (8 * (i & 3))) & 255u; }
+
+template <int BPP>
+__device__ __forceinline__ void unfilter_chunk8(const u32x2& rawv, const uint32_t (&up)[2], const uint32_t (&prevup)[2],
+                                                const uint32_t (&prevcur)[2], const FtMask& fm, uint32_t (&o)[2]) {
+    const uint32_t raw[2] = {rawv.x, rawv.y};
+    o[0] = o[1] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t a = i >= BPP ? ((o[(i - BPP) >> 2] >> (8 * ((i - BPP) & 3))) & 255u) : byte2(prevcur, 8 + i - BPP);
+        const uint32_t b = byte2(up, i);
+        const uint32_t c = i >= BPP ? byte2(up, i - BPP) : byte2(prevup, 8 + i - BPP);
+        const int d1 = (int)b - (int)c, d2 = (int)a - (int)c;
+        const int pa = d1 < 0 ? -d1 : d1, pb = d2 < 0 ? -d2 : d2, pc = (d1 + d2) < 0 ? -(d1 + d2) : (d1 + d2);
+        const uint32_t paeth = (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
+        const uint32_t pred = (a & fm.sub) | (b & fm.up) | (((a + b) >> 1) & fm.avg) | (paeth & fm.paeth);
+        const uint32_t v = (byte2(raw, i) + pred) & 255u;
+        o[i >> 2] |= v << (8 * (i & 3));
+    }
+}
+
+template <int BPP>
+__global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter8(const PngImgDev* imgs, const int2* groups,
+                                                                       const int* prog_base, unsigned* prog,
+                                                                       unsigned* ticket) {
+    static_assert(BPP <= 4, "8-byte chunks carry at most 4 bytes of left context");
+    constexpr int NW = kPngUnfilterThreads / 64, G = kUnfG;
+    __shared__ int s_t;
+    if (threadIdx.x == 0) s_t = (int)atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int2 gk = groups[s_t];  // (image, workgroup of the image)
+    const PngImgDev I = imgs[gk.x];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int nch = (I.rowbytes + 7) >> 3;
+    const int nbands = (I.H + 63) >> 6;
+    const int K = png_unfilter_groups(I.H);
+    unsigned* pg = prog + prog_base[gk.x];
+    for (int band = wave * K + gk.y; band < nbands; band += NW * K) {
+        const int y = band * 64 + lane;
+        const bool live = y < I.H;
+        IK_GLOBAL uint8_t* row = (IK_GLOBAL uint8_t*)(I.dst + (size_t)(live ? y : 0) * I.pitch);
+        const FtMask fm(live ? ((const IK_GLOBAL uint8_t*)I.ft)[y] : 0u);
+        const uint64_t above = band > 0 ? (uint64_t)(size_t)(I.dst + (size_t)(band * 64 - 1) * I.pitch) : 0;
+        uint32_t cur[2] = {0, 0}, up[2] = {0, 0};
+        uint32_t prevcur[2] = {0, 0}, prevup[2] = {0, 0};  // last chunk (left context)
+        const uint64_t dbase = uniform_u64((uint64_t)(size_t)I.dst);
+        const uint32_t rowoff = (uint32_t)((size_t)(live ? y : 0) * I.pitch);
+        auto fetch = [&](int s0, u32x2 (&r)[G]) {
+            uint32_t off[G];
+#pragma unroll
+            for (int t = 0; t < G; ++t) off[t] = rowoff + 8u * (uint32_t)min(max(s0 + t - lane, 0), nch - 1);
+            asm volatile(
+                "s_nop 4\n\t"
+                "global_load_dwordx2 %0, %8, %16\n\t"
+                "global_load_dwordx2 %1, %9, %16\n\t"
+                "global_load_dwordx2 %2, %10, %16\n\t"
+                "global_load_dwordx2 %3, %11, %16\n\t"
+                "global_load_dwordx2 %4, %12, %16\n\t"
+                "global_load_dwordx2 %5, %13, %16\n\t"
+                "global_load_dwordx2 %6, %14, %16\n\t"
+                "global_load_dwordx2 %7, %15, %16"
+                : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7])
+                : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]), "v"(off[7]),
+                  "s"(dbase)
+                : "memory");
+        };
+        auto landed = [](u32x2 (&r)[G]) {
+            asm volatile("s_waitcnt vmcnt(0)"
+                         : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7])
+                         :
+                         : "memory");
+        };
+        u32x2 rcur[G], rnxt[G];
+        fetch(0, rcur);
+        landed(rcur);
+        unsigned seen = 0;  // lane 0: the previous band's progress last read
+        const int ngrp = (nch + 63 + G - 1) / G;
+        for (int g = 0; g < ngrp; ++g) {
+            const int s0 = g * G;
+            u32x2 ab[G];
+#pragma unroll
+            for (int t = 0; t < G; ++t) ab[t] = u32x2{0, 0};
+            if (lane == 0 && above && s0 < nch) {
+                const unsigned need = (unsigned)min(s0 + G, nch);
+                while (seen < need) {
+                    seen = __hip_atomic_load(pg + band - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (seen < need) __builtin_amdgcn_s_sleep(1);
+                }
+                uint32_t off[G];
+#pragma unroll
+                for (int t = 0; t < G; ++t) off[t] = 8u * (uint32_t)min(s0 + t, nch - 1);
+                const uint64_t base = uniform_u64(above);
+                asm volatile(
+                    "s_nop 4\n\t"
+                    "global_load_dwordx2 %0, %8, %16 sc1\n\t"
+                    "global_load_dwordx2 %1, %9, %16 sc1\n\t"
+                    "global_load_dwordx2 %2, %10, %16 sc1\n\t"
+                    "global_load_dwordx2 %3, %11, %16 sc1\n\t"
+                    "global_load_dwordx2 %4, %12, %16 sc1\n\t"
+                    "global_load_dwordx2 %5, %13, %16 sc1\n\t"
+                    "global_load_dwordx2 %6, %14, %16 sc1\n\t"
+                    "global_load_dwordx2 %7, %15, %16 sc1\n\t"
+                    "s_waitcnt vmcnt(0)"
+                    : "=&v"(ab[0]), "=&v"(ab[1]), "=&v"(ab[2]), "=&v"(ab[3]), "=&v"(ab[4]), "=&v"(ab[5]), "=&v"(ab[6]),
+                      "=&v"(ab[7])
+                    : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]),
+                      "v"(off[7]), "s"(base)
+                    : "memory");
+            }
+            if (g + 1 < ngrp) fetch(s0 + G, rnxt);
+#pragma unroll
+            for (int t = 0; t < G; ++t) {
+                const int j = s0 + t - lane;
+                uint32_t nup[2];
+                nup[0] = wave_shr1(cur[0], ab[t].x);
+                nup[1] = wave_shr1(cur[1], ab[t].y);
+                if (live && j >= 0 && j < nch) {
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) { prevup[k] = up[k]; up[k] = nup[k]; prevcur[k] = cur[k]; }
+                    if (j == 0) {
+#pragma unroll
+                        for (int k = 0; k < 2; ++k) { prevup[k] = 0; prevcur[k] = 0; }
+                    }
+                    uint32_t o[2];
+                    unfilter_chunk8<BPP>(rcur[t], up, prevup, prevcur, fm, o);
+                    cur[0] = o[0];
+                    cur[1] = o[1];
+                    const u32x2 ov = {o[0], o[1]};
+                    asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(row + 8 * j), "v"(ov) : "memory");
+                }
+            }
+            const int jl = s0 + G - 1 - 63;
+            if (lane == 63 && live && jl >= 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its sc1 stores have completed
+                __hip_atomic_store(pg + band, (unsigned)min(jl + 1, nch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (g + 1 < ngrp) {
+                landed(rnxt);
+#pragma unroll
+                for (int t = 0; t < G; ++t) rcur[t] = rnxt[t];
+            }
+        }
+    }
+}
+
 // ---- small transfers through the compute queue ---------------------------------------
 __global__ __launch_bounds__(256) void k_copy_words(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                                     size_t n) {
@@ -857,11 +1204,11 @@ __global__ __launch_bounds__(256) void k_png_gather(const uint8_t* __restrict__ 
     const uint32_t b0 = 256u * (uint32_t)tid;
     const uint32_t len = P.len > b0 ? (P.len - b0 < 256u ? P.len - b0 : 256u) : 0u;
     uint32_t c = ~0u;
-    uint8_t* dp = stream + P.dst + b0;
+    IK_GLOBAL uint8_t* dp = (IK_GLOBAL uint8_t*)(stream + P.dst + b0);
     if (len && P.src == kPngNoSrc) {
         for (uint32_t i = 0; i < len; ++i) dp[i] = 0;
     } else if (len) {
-        const uint8_t* sp = raw + P.src + b0;
+        const IK_GLOBAL uint8_t* sp = (const IK_GLOBAL uint8_t*)(raw + P.src + b0);
         uint32_t i = 0;
         const uint32_t mis = (uint32_t)((uintptr_t)dp & 3u);
         const uint32_t pre = mis ? (4u - mis < len ? 4u - mis : len) : 0u;
@@ -874,8 +1221,8 @@ __global__ __launch_bounds__(256) void k_png_gather(const uint8_t* __restrict__ 
         if (nw) {
             const uintptr_t sa = (uintptr_t)(sp + i);
             const uint32_t sh = (uint32_t)(sa & 3u);
-            const uint32_t* ws = reinterpret_cast<const uint32_t*>(sa - sh);
-            uint32_t* wd = reinterpret_cast<uint32_t*>(dp + i);
+            const IK_GLOBAL uint32_t* ws = reinterpret_cast<const IK_GLOBAL uint32_t*>(sa - sh);
+            IK_GLOBAL uint32_t* wd = reinterpret_cast<IK_GLOBAL uint32_t*>(dp + i);
             uint32_t lo = ws[0];
             uint32_t k = 0;
             // eight words at a time: the loads are independent of the CRC chain
@@ -1058,6 +1405,22 @@ hipError_t launch_png_unfilter(const PngImgDev* imgs, const int2* groups, int ng
                                unsigned* prog, unsigned* ticket, int bpp, hipStream_t s) {
     if (ngroups <= 0) return hipSuccess;
     const dim3 grid(ngroups), block(kPngUnfilterThreads);
+    // 8-byte chunks for up to 4 bytes per pixel (IK_PNG_UNF16=1: the 16-byte kernel)
+    static const bool wide = [] {
+        const char* e = getenv("IK_PNG_UNF16");
+        return e && !strcmp(e, "1");
+    }();
+    if (!wide && bpp <= 4) {
+#define IK_UNF8(B) hipLaunchKernelGGL(k_png_unfilter8<B>, grid, block, 0, s, imgs, groups, prog_base, prog, ticket)
+        switch (bpp) {
+        case 1: IK_UNF8(1); break;
+        case 2: IK_UNF8(2); break;
+        case 3: IK_UNF8(3); break;
+        default: IK_UNF8(4); break;
+        }
+#undef IK_UNF8
+        return hipGetLastError();
+    }
 #define IK_UNF(B) hipLaunchKernelGGL(k_png_unfilter<B>, grid, block, 0, s, imgs, groups, prog_base, prog, ticket)
     switch (bpp) {
     case 1: IK_UNF(1); break;

@@ -309,7 +309,9 @@ struct UploadArea {
     size_t cap = 0;
     uint8_t* pin = nullptr;  // pinned: the plan tables, and staging for inputs the caller did not pin
     size_t pin_cap = 0;
-    hipEvent_t ev[3] = {};   // upload issued, file DMAs done, gather + CRC done (the kernel stage waits on [2])
+    // upload issued, file DMAs done, gather + CRC done, block search done, block
+    // search started (the block search waits on [2], the kernel stage on [3])
+    hipEvent_t ev[5] = {};
     bool busy = false;
 };
 constexpr int kUploadAreas = 2;
@@ -391,6 +393,9 @@ struct PngBatchState {
     UploadArea* area = nullptr;
     int rc = IK_OK;
     size_t o_zs = 0, o_err = 0;  // area offsets: assembled streams, per-stream CRC flags
+    size_t o_ftab = 0, o_fimg = 0, o_cand = 0;  // the block search's chunk table, stream descriptors, candidates
+    int nchunks = 0;
+    bool find_launched = false;
     int pinned_streams = 0;
     double t0 = 0, t_host = 0;
     ~PngBatchState() { release_area(area); }
@@ -441,14 +446,27 @@ int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Png
         const uint32_t tail = (uint32_t)((((j.zlen + 3) & ~size_t(3)) + kPad) - j.zlen);
         png_gather_plan(bytes[j.idx], j.raw_off, j.idat, raw + j.z_off, tail, (uint32_t)k, pieces, chunks);
     }
+    // the block search's chunks: 16 KiB of stream each (chunk 0 starts at the first block)
+    const uint64_t cbits = kPngChunkBytes * 8;
+    int nchunks = 0;
+    for (PngJob* j : S.J) {
+        j->nbits = (uint64_t)j->zlen * 8;
+        j->nchunks = (int)((j->nbits - 16 + cbits - 1) / cbits);
+        j->chunk0 = nchunks;
+        nchunks += j->nchunks;
+    }
+    S.nchunks = nchunks;
     // (the pieces' dst offsets are area offsets: the stream area follows the raw one)
     S.o_zs = raw;
     const size_t o_pieces = raw + up256(zs);
     const size_t o_chunks = o_pieces + up256(sizeof(PngGatherPiece) * pieces.size());
-    const size_t o_pcrc = o_chunks + up256(sizeof(PngCrcChunk) * chunks.size());
+    S.o_ftab = o_chunks + up256(sizeof(PngCrcChunk) * chunks.size());
+    S.o_fimg = S.o_ftab + up256(2 * sizeof(int) * nchunks);
+    const size_t o_pcrc = S.o_fimg + up256(sizeof(PngImgDev) * m);
     S.o_err = o_pcrc + up256(2 * sizeof(uint32_t) * pieces.size());
-    const size_t dev_bytes = S.o_err + up256(sizeof(int) * m);
-    const size_t tab_bytes = up256(sizeof(PngGatherPiece) * pieces.size()) + up256(sizeof(PngCrcChunk) * chunks.size());
+    S.o_cand = S.o_err + up256(sizeof(int) * m);
+    const size_t dev_bytes = S.o_cand + up256(sizeof(int64_t) * nchunks);
+    const size_t tab_bytes = o_pcrc - o_pieces;  // pieces, chunks, search chunk table, search descriptors
     S.area = acquire_area(S.device);  // waits while two earlier batches' kernel stages hold both areas
     UploadArea* A = S.area;
     if (!area_reserve(A, dev_bytes, tab_bytes + stage)) {
@@ -483,8 +501,23 @@ int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Png
     });
     if (A->ev[1]) (void)hipEventRecord(A->ev[1], sc);
     std::memcpy(A->pin, pieces.data(), sizeof(PngGatherPiece) * pieces.size());
-    std::memcpy(A->pin + up256(sizeof(PngGatherPiece) * pieces.size()), chunks.data(),
-                sizeof(PngCrcChunk) * chunks.size());
+    std::memcpy(A->pin + (o_chunks - o_pieces), chunks.data(), sizeof(PngCrcChunk) * chunks.size());
+    {
+        int* ft = reinterpret_cast<int*>(A->pin + (S.o_ftab - o_pieces));
+        PngImgDev* fi = reinterpret_cast<PngImgDev*>(A->pin + (S.o_fimg - o_pieces));
+        for (int k = 0; k < m; ++k) {
+            const PngJob& j = *S.J[k];
+            PngImgDev d{};
+            d.words = reinterpret_cast<const uint32_t*>(A->dev + S.o_zs + j.z_off);
+            d.bit0 = 16;
+            d.nbits = j.nbits;
+            fi[k] = d;
+            for (int c = 0; c < j.nchunks; ++c) {
+                ft[j.chunk0 + c] = k;
+                ft[nchunks + j.chunk0 + c] = c;
+            }
+        }
+    }
     hipError_t e = hipMemcpyAsync(A->dev + o_pieces, A->pin, tab_bytes, hipMemcpyHostToDevice, sc);
     if (e == hipSuccess) e = hipMemsetAsync(A->dev + S.o_err, 0, sizeof(int) * m, sc);
     if (e == hipSuccess)
@@ -503,6 +536,28 @@ int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Png
         fprintf(stderr, "[png] upload t=%.1f: %d streams (%d pinned), %zu pieces, %zu IDAT chunks, host %.2f ms\n",
                 fmod(S.t0, 1e5), m, S.pinned_streams, pieces.size(), chunks.size(), S.t_host);
     return IK_OK;
+}
+
+// the block search of a batch whose upload was issued: on stream s, once the
+// upload (with its gather + CRC pass) has landed; once per batch
+static void png_find_launch(PngBatchState& S, hipStream_t s) {
+    if (S.find_launched || S.rc || !S.area || S.J.empty()) return;
+    UploadArea* A = S.area;
+    const uint64_t cbits = kPngChunkBytes * 8;
+    hipError_t e = A->ev[2] ? hipStreamWaitEvent(s, A->ev[2], 0) : hipSuccess;
+    if (e == hipSuccess && A->ev[4]) e = hipEventRecord(A->ev[4], s);
+    const int* ft = reinterpret_cast<const int*>(A->dev + S.o_ftab);
+    if (e == hipSuccess)
+        e = launch_png_find(reinterpret_cast<const PngImgDev*>(A->dev + S.o_fimg), ft, ft + S.nchunks, S.nchunks, cbits,
+                            reinterpret_cast<int64_t*>(A->dev + S.o_cand), s);
+    if (e == hipSuccess && A->ev[3]) e = hipEventRecord(A->ev[3], s);
+    if (e == hipSuccess && !A->ev[3]) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) S.rc = hip_fail(e, "PNG block search");
+    S.find_launched = true;
+}
+
+void png_find_prelaunch(PngUpload& up, hipStream_t s) {
+    if (up.st) png_find_launch(*up.st, s);
 }
 
 int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* msgs) {
@@ -529,17 +584,12 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
     const int m = (int)J.size();
     hipStream_t s = thread_stream();
     int rc = S.rc;
-    const uint64_t cbits = kPngChunkBytes * 8;
     UploadArea* A = S.area;
     if (m && !rc) {
         // ---- the kernel stage's work area (this thread's) ----
         size_t total = 0;
-        int nchunks = 0;
+        const int nchunks = S.nchunks;
         for (PngJob* j : J) {
-            j->nbits = (uint64_t)j->zlen * 8;
-            j->nchunks = (int)((j->nbits - 16 + cbits - 1) / cbits);
-            j->chunk0 = nchunks;
-            nchunks += j->nchunks;
             j->o_u16 = total;
             total += up256(2 * (j->raw_total + 64));
             j->o_ft = total;
@@ -547,10 +597,6 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         }
         const size_t o_imgs = total;
         total += up256(sizeof(PngImgDev) * m);
-        const size_t o_ctab = total;
-        total += up256(sizeof(int) * 2 * nchunks);
-        const size_t o_cand = total;
-        total += up256(sizeof(int64_t) * nchunks);
         const size_t o_err = total;
         total += up256(sizeof(int) * m);
         const size_t o_dyn = total;  // lane tables, results, obase, rows, subtables: sized per round below
@@ -621,13 +667,11 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             rc = fail(IK_ERR_NOMEM, "cannot allocate pinned PNG transfer area");
         // the kernels run under the device's kernel gate (ik_runtime.h)
         gate_enter(kGateKernels);
-        // ---- image descriptors and the chunk table ----
+        // ---- image descriptors ----
         std::vector<PngImgDev> hd(m);
         // the large host tables are kept per thread between batches (clear() keeps
         // the capacity): fresh multi-MB vectors cost page faults every batch
         static thread_local HostTables ht;
-        std::vector<int>& hchunk = ht.chunk_img;
-        hchunk.assign(2 * (size_t)nchunks, 0);
         for (int k = 0; k < m && !rc; ++k) {
             PngJob& j = *J[k];
             PngImgDev& d = hd[k];
@@ -640,26 +684,33 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             d.H = (int)j.h;
             d.bpp = j.bpp;
             d.ft = dev + j.o_ft;
-            for (int c = 0; c < j.nchunks; ++c) {
-                hchunk[j.chunk0 + c] = k;
-                hchunk[nchunks + j.chunk0 + c] = c;
-            }
         }
         const PngImgDev* d_imgs = reinterpret_cast<const PngImgDev*>(dev + o_imgs);
-        const int* d_cimg = reinterpret_cast<const int*>(dev + o_ctab);
-        const int* d_cidx = d_cimg + nchunks;
-        int64_t* d_cand = reinterpret_cast<int64_t*>(dev + o_cand);
-        // ---- the block search over every stream once its upload has landed ----
-        hipError_t e = rc ? hipSuccess : X.h2d(dev + o_ctab, hchunk.data(), sizeof(int) * 2 * nchunks);
-        if (!rc && e == hipSuccess) e = X.h2d(dev + o_imgs, hd.data(), sizeof(PngImgDev) * m);
-        if (!rc && e == hipSuccess && A->ev[2]) e = hipStreamWaitEvent(s, A->ev[2], 0);
-        rec(8, s);
-        if (!rc && e == hipSuccess) e = launch_png_find(d_imgs, d_cimg, d_cidx, nchunks, cbits, d_cand, s);
-        rec(9, s);
+        // ---- the block search: launched here unless the kernel stage launched it
+        // while the previous batch's expand / resolve / unfilter ran (PngUpload::
+        // on_decoded); its candidates come from the upload area ----
+        hipError_t e = rc ? hipSuccess : X.h2d(dev + o_imgs, hd.data(), sizeof(PngImgDev) * m);
+        const bool pre = S.find_launched;
+        if (!rc && e == hipSuccess) {
+            png_find_launch(S, s);
+            rc = S.rc;
+        }
+        if (!rc && e == hipSuccess && A->ev[3]) e = hipStreamWaitEvent(s, A->ev[3], 0);
+#ifdef IK_FIND_PROF
+        {
+            (void)hipStreamSynchronize(s);
+            unsigned long long pf[8] = {};
+            if (png_find_prof_read(pf) == hipSuccess && pf[5])
+                fprintf(stderr, "[find-prof] waves %llu: cycles/wave %.0f, flush cycles/wave %.0f (%.1f%%), flushes/wave %.2f, "
+                        "steps/wave %.1f, candidates/wave %.1f, kernel %.2f ms\n", pf[5], (double)pf[0] / pf[5],
+                        (double)pf[1] / pf[5], 100.0 * pf[1] / std::max(1.0, (double)pf[0]), (double)pf[2] / pf[5],
+                        (double)pf[3] / pf[5], (double)pf[4] / pf[5], ev_ms(8, 9));
+        }
+#endif
         std::vector<int64_t>& cand = ht.cand;
         cand.assign(nchunks, 0);
         std::vector<int> crc_err(m, 0);
-        if (!rc && e == hipSuccess) e = X.d2h(cand.data(), d_cand, sizeof(int64_t) * nchunks);
+        if (!rc && e == hipSuccess) e = X.d2h(cand.data(), A->dev + S.o_cand, sizeof(int64_t) * nchunks);
         if (!rc && e == hipSuccess) {
             e = launch_copy_words(reinterpret_cast<const uint32_t*>(A->dev + S.o_err),
                                   reinterpret_cast<uint32_t*>(dev + o_err), (size_t)m, s);
@@ -764,7 +815,17 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         // the compressed streams are read for the last time (every decode round's
         // results were synchronised): the next batch may upload into the area
         (void)hipStreamSynchronize(s);
+        {
+            float ms = 0;
+            if (A->ev[3] && A->ev[4] && hipEventElapsedTime(&ms, A->ev[4], A->ev[3]) == hipSuccess) tim[13] = ms;
+            if (A->ev[0] && A->ev[2] && hipEventElapsedTime(&ms, A->ev[0], A->ev[2]) == hipSuccess) tim[1] = ms;
+            if (A->ev[1] && A->ev[2] && hipEventElapsedTime(&ms, A->ev[1], A->ev[2]) == hipSuccess) tim[14] = ms;
+        }
+        tim[16] = pre ? 1.0 : 0.0;
         release_area(S.area);
+        // the next batch's block search may start now, beside this batch's expand,
+        // resolve and unfilter (the stage executor's hook)
+        if (up.on_decoded) up.on_decoded();
         const double t3 = now_ms();
         // ---- offsets, output images, expand, resolve, unfilter ----
         std::vector<int64_t>& hob = ht.obase;
@@ -938,16 +999,10 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                     mb, sc / n1, mc, 1024.0 * sc / std::max(1.0, si), sx / n2, mx);
         }
         tim[0] = S.t_host;
-        if (A && A->ev[0] && A->ev[2]) {
-            float ms = 0;
-            if (hipEventElapsedTime(&ms, A->ev[0], A->ev[2]) == hipSuccess) tim[1] = ms;
-            if (hipEventElapsedTime(&ms, A->ev[1], A->ev[2]) == hipSuccess) tim[14] = ms;
-        }
         tim[2] = count_dev;
         tim[7] = rounds;
         tim[8] = (double)hl.size();
         tim[9] = m;
-        tim[13] = ev_ms(8, 9);
         if (timing)
             fprintf(stderr, "[png] t=%.1f %d streams (%d on the GPU): upload host %.2f ms, upload device %.2f ms (gather "
                     "%.2f), waited+find %.2f ms (find %.2f), decode %.2f ms (%d rounds, %d dropped, %d overflows), "

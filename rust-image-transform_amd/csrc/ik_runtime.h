@@ -178,10 +178,17 @@ struct PngUpload {
     const size_t* lens = nullptr;
     int n = 0;
     std::shared_ptr<PngBatchState> st;
+    // called by png_decode_finish once the batch's decode rounds are done (its
+    // compressed streams are no longer read): the stage executor launches the
+    // next batch's block search there, beside this batch's remaining kernels
+    std::function<void()> on_decoded;
 };
 int png_upload_begin(const uint8_t* const* b, const size_t* lens, int n, PngUpload& up);
 int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* msgs);
-constexpr int kPngTimingFields = 16;  // ik_png_last_timing
+// the block search of an issued upload, on stream s (after the upload lands);
+// png_decode_finish then only waits for it.  Kernel-stage thread only.
+void png_find_prelaunch(PngUpload& up, hipStream_t s);
+constexpr int kPngTimingFields = 17;  // ik_png_last_timing
 // caller-pinned host memory (ik_host_alloc / ik_host_register): [p, p + n) lies
 // inside one such range, so DMAs may read it in place
 bool host_pinned(const void* p, size_t n);

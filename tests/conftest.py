@@ -25,6 +25,14 @@ def oracle():
 @pytest.fixture(scope="session")
 def ik():
     """The product library on a GPU; GPU tests fail loudly (no fallback) without one."""
+    # torch's HIP runtime first (some tests use torch tensors as device buffers):
+    # initialised after the library's worker threads exist, it has reported no devices
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
     from imagekit import _lib
     lib = _lib.load()
     n = lib.ik_device_count()
