@@ -1305,15 +1305,18 @@ private:
                 continue;
             }
             Ticket& t = *p->t;
-            // once this batch's decode rounds are done, the next queued batch's
-            // block search goes out beside this batch's expand / resolve / unfilter
-            p->up.on_decoded = [this] {
+            // once this batch's resolve pass is done, the next queued batch's block
+            // search goes out beside this batch's unfilter and resize
+            p->up.on_next_search = [this](hipEvent_t after) {
                 std::shared_ptr<BatchPart> nx;
                 {
                     std::lock_guard<std::mutex> lk(mu_);
                     if (!q_[1].empty()) nx = q_[1].front();
                 }
-                if (nx && !nx->pb.empty()) png_find_prelaunch(nx->up, thread_copy_stream());
+                if (!nx || nx->pb.empty()) return;
+                hipStream_t fs = thread_copy_stream();
+                if (after && hipStreamWaitEvent(fs, after, 0) != hipSuccess) return;
+                png_find_prelaunch(nx->up, fs);
             };
             transform_device_phase(p->bytes, p->lens, p->w, p->h, p->fmt, p->quality, p->filter, t.st.data(),
                                    t.errs.data(), p->hp, p->pb.empty() ? nullptr : &p->up);

@@ -37,6 +37,12 @@
 
 namespace ik {
 
+// The next batch's block search runs beside this batch's later kernels (ik_host.cpp
+// StageExec): those raise their waves' issue priority so that the search's
+// VALU-heavy waves take the SIMD cycles they leave idle, not the ones their
+// latency-bound chains wait for.
+__device__ __forceinline__ void raise_priority() { __builtin_amdgcn_s_setprio(3); }
+
 // ---- find ------------------------------------------------------------------------
 // One wave per (chunk, image).  A lane owns one 32-bit stream word, i.e. 32
 // consecutive bit offsets, so a wave step covers 2,048 offsets from 64
@@ -547,6 +553,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) 
 
 __global__ __launch_bounds__(64) void k_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int nlanes,
                                                    const uint16_t* tok, int* status) {
+    raise_priority();
     __shared__ uint16_t s_ring[kXRing];
     __shared__ uint32_t s_tab[64];   // the block's literal table (256 bytes)
     __shared__ uint32_t s_end[64];   // per token slot: end offset of its symbol in the batch (inclusive scan)
@@ -717,6 +724,238 @@ __global__ __launch_bounds__(64) void k_png_expand(const PngImgDev* imgs, const 
     }
 }
 
+// k_png_expand with four tokens per thread (256 per batch) and the copies done in
+// token order instead of every output position searching for its symbol: on
+// image data ~96 % of the tokens are literals and a match is ~1 in 25 tokens,
+// so the batch costs a load, a prefix sum (DPP) and one LDS write per literal,
+// ~20 instructions per match, and a coalesced ring -> memory copy.
+//   1. the literals of the batch go to the LDS ring (indexed by absolute symbol
+//      position) at their offsets;
+//   2. the matches, in token order, each by the whole wave: a position of the
+//      copy reads its source from the ring (this batch's earlier positions --
+//      literals and earlier copies are in place -- or <= kXNear back), from
+//      memory (farther back, written by an earlier batch), or becomes a window
+//      marker (before the lane's first symbol);
+//   3. the batch's positions go from the ring to memory in aligned groups of 4
+//      (8-byte stores; a group's 1-3 positions before the batch are rewritten
+//      with the same values, its positions after the batch -- stale ring data --
+//      are rewritten by the next batch; groups are clipped to the lane's output).
+// IK_PNG_EXPAND=1: k_png_expand.  Same output.
+constexpr uint32_t kX4Tok = 256;
+
+// inclusive wave prefix sum: row_shr steps within rows of 16, then row totals
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
+    const int row = threadIdx.x >> 4;
+    return v + (row >= 1 ? r0 : 0u) + (row >= 2 ? r1 : 0u) + (row >= 3 ? r2 : 0u);
+}
+
+__global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const PngLaneDev* lanes, int nlanes,
+                                                    const uint16_t* tok, int* status) {
+    raise_priority();
+    __shared__ __attribute__((aligned(16))) uint16_t s_ring[kXRing];  // recent output, by absolute position
+    __shared__ uint32_t s_tab[64];                                      // the block's literal table
+    constexpr uint32_t M = kXRing - 1;
+    const int li = blockIdx.x;
+    if (li >= nlanes) return;
+    const int x = threadIdx.x;
+    const uint64_t c0 = clock64();
+    const PngLaneDev L = lanes[li];
+    const PngImgDev I = imgs[L.img];
+    const IK_GLOBAL uint16_t* T = (const IK_GLOBAL uint16_t*)(tok + L.tbase);
+    IK_GLOBAL uint16_t* const U = (IK_GLOBAL uint16_t*)I.u16;
+    const int64_t ob = L.obase, oe = L.obase + (int64_t)L.out_len;
+    const uint32_t ntok = L.ntok;
+    uint32_t t = 0;
+    int64_t cnt = 0;
+    bool have_tab = false, bad = false;
+    // this thread's 4 tokens of the batch window at a (a multiple of 4; the region
+    // is 16-byte aligned and padded past ntok to a multiple of 8 tokens)
+    auto load4 = [&](uint32_t a) -> uint64_t {
+        const uint32_t i = a + 4u * (uint32_t)x;
+        return i < ntok ? *(const IK_GLOBAL uint64_t*)(T + i) : 0xFFFEFFFEFFFEFFFEull;
+    };
+    uint64_t w = load4(0);
+    while (t < ntok) {
+        const uint32_t a = t & ~3u, i0 = a + 4u * (uint32_t)x;
+        uint32_t u[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) u[k] = (uint32_t)(w >> (16 * k)) & 0xFFFFu;
+        // the first table record at or after t in the window
+        int ft = 4;
+#pragma unroll
+        for (int k = 3; k >= 0; --k)
+            if (i0 + k >= t && i0 + k < ntok && u[k] == kTokTable) ft = k;
+        const unsigned long long tl = __ballot(ft < 4);
+        uint32_t end = a + kX4Tok < ntok ? a + kX4Tok : ntok;
+        if (tl) {
+            const int l = __builtin_ctzll(tl);
+            const uint32_t e = a + 4u * (uint32_t)l + (uint32_t)__builtin_amdgcn_readlane(ft, l);
+            if (e == t) {  // the table: the literal table -> LDS
+                const uint32_t tt = (t + 8) & ~7u;
+                if (tt + kTokTableLen > ntok) { bad = true; break; }
+                s_tab[x] = ((const IK_GLOBAL uint32_t*)(T + tt))[x];
+                have_tab = true;
+                t = tt + kTokTableLen;
+                w = load4(t & ~3u);
+                __syncthreads();
+                continue;
+            }
+            end = e;
+        }
+        // a match's first token last: its distance is in the next window
+        {
+            const uint32_t q = end - 1u;
+            const bool mine = q >= t && (q >> 2) == (i0 >> 2);
+            const uint32_t uq = (uint32_t)(w >> (16 * (q & 3u))) & 0xFFFFu;
+            if (__ballot(mine && (uq & 0xFF00u) == kTokMatch)) --end;
+        }
+        if (end <= t) { bad = true; break; }
+        // the token after each slot (a match's distance) and before slot 0
+        const uint32_t nx = (uint32_t)__shfl_down((int)u[0], 1, 64);
+        const uint32_t pv = (uint32_t)__shfl_up((int)u[3], 1, 64);
+        uint32_t len[4], val[4];
+        bool lit[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t idx = i0 + k;
+            const uint32_t prev = k ? u[k - 1] : pv;
+            const bool valid = idx >= t && idx < end;
+            const bool dist_tok = idx > t && (prev & 0xFF00u) == kTokMatch;
+            const bool start = valid && !dist_tok;
+            const uint32_t v = u[k];
+            len[k] = 0;
+            val[k] = 0;
+            lit[k] = false;
+            if (start) {
+                if (v < 256u) {
+                    if (!have_tab) bad = true;
+                    len[k] = 1;
+                    lit[k] = true;
+                    val[k] = (s_tab[v >> 2] >> (8 * (v & 3u))) & 0xFFu;
+                } else if ((v & 0xFF00u) == kTokRaw) {
+                    len[k] = 1;
+                    lit[k] = true;
+                    val[k] = v & 0xFFu;
+                } else if ((v & 0xFF00u) == kTokMatch) {
+                    len[k] = (v & 0xFFu) + 3u;
+                    val[k] = (k < 3 ? u[k + 1] : nx) + 1u;  // the distance
+                } else {
+                    bad = true;
+                }
+            }
+        }
+        if (__ballot(bad)) { bad = true; break; }
+        uint32_t off[4], tot;
+        for (;;) {
+            const uint32_t sum = len[0] + len[1] + len[2] + len[3];
+            const uint32_t incl = wave_incl_scan_dpp(sum);
+            tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            off[0] = incl - sum;
+            off[1] = off[0] + len[0];
+            off[2] = off[1] + len[1];
+            off[3] = off[2] + len[2];
+            if (tot <= (uint32_t)kXCap) break;
+            // cut the batch before the first symbol that does not fit (one always does)
+            int fk = 4;
+#pragma unroll
+            for (int k = 3; k >= 0; --k)
+                if (len[k] && off[k] + len[k] > (uint32_t)kXCap) fk = k;
+            const unsigned long long ov = __ballot(fk < 4);
+            const int l = __builtin_ctzll(ov);
+            end = a + 4u * (uint32_t)l + (uint32_t)__builtin_amdgcn_readlane(fk, l);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (i0 + k >= end) len[k] = 0;
+        }
+        // the next window's tokens, in flight while this batch is written
+        const uint32_t t2 = end;
+        const uint64_t wn = t2 < ntok ? load4(t2 & ~3u) : 0ull;
+        const uint32_t gb = (uint32_t)(ob + cnt);  // ring index base (absolute position, low bits)
+        // 1. literals
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (len[k] && lit[k]) s_ring[(gb + off[k]) & M] = (uint16_t)val[k];
+        // 2. matches in token order (a thread holds at most two)
+        uint32_t ma0 = 0, ma1 = 0, md0 = 0, md1 = 0;
+        int nm = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (len[k] && !lit[k]) {
+                if (nm == 0) { ma0 = off[k] | (len[k] << 16); md0 = val[k]; }
+                else { ma1 = off[k] | (len[k] << 16); md1 = val[k]; }
+                ++nm;
+            }
+        unsigned long long m1 = __ballot(nm >= 1);
+        const unsigned long long m2 = __ballot(nm >= 2);
+        auto copy = [&](uint32_t A, uint32_t d) {
+            const uint32_t o = A & 0xFFFFu, ln = A >> 16;
+            const bool wrap = d < ln;  // overlapping: the source repeats with period d
+            const float rd = __builtin_amdgcn_rcpf((float)d);
+            for (uint32_t j = (uint32_t)x; j < ln; j += 64) {
+                uint32_t jj = j;
+                if (wrap) {
+                    const uint32_t qq = (uint32_t)((float)j * rd);
+                    int32_t r = (int32_t)(j - qq * d);
+                    if (r < 0) r += (int32_t)d;
+                    else if (r >= (int32_t)d) r -= (int32_t)d;
+                    jj = (uint32_t)r;
+                }
+                const int32_t sr = (int32_t)o - (int32_t)d + (int32_t)jj;  // relative to the batch start
+                const int64_t ab = cnt + sr;                                // relative to the lane's first symbol
+                uint16_t v;
+                if (ab < 0) {
+                    if (ab < -(int64_t)infl::kWindow) bad = true;
+                    v = (uint16_t)(0x8000u | (uint32_t)(infl::kWindow + ab));
+                } else if (sr >= -kXNear) {
+                    v = s_ring[(gb + (uint32_t)sr) & M];
+                } else {
+                    v = U[ob + ab];
+                }
+                s_ring[(gb + o + j) & M] = v;
+            }
+        };
+        while (m1) {
+            const int l = __builtin_ctzll(m1);
+            m1 &= m1 - 1ull;
+            copy((uint32_t)__builtin_amdgcn_readlane((int)ma0, l), (uint32_t)__builtin_amdgcn_readlane((int)md0, l));
+            if ((m2 >> l) & 1ull)
+                copy((uint32_t)__builtin_amdgcn_readlane((int)ma1, l), (uint32_t)__builtin_amdgcn_readlane((int)md1, l));
+        }
+        // 3. ring -> memory, aligned groups of 4 positions
+        {
+            const int64_t s0 = ob + cnt, s1 = s0 + tot, cb = s0 & ~3ll;
+            const int64_t ng = (s1 - cb + 3) >> 2;
+            for (int64_t g = x; g < ng; g += 64) {
+                const int64_t ca = cb + 4 * g;
+                const uint64_t v4 = *(const uint64_t*)&s_ring[(uint32_t)ca & M];
+                if (ca >= ob && ca + 4 <= oe) {
+                    *(IK_GLOBAL uint64_t*)(U + ca) = v4;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (ca + k >= ob && ca + k < oe) U[ca + k] = (uint16_t)(v4 >> (16 * k));
+                }
+            }
+        }
+        __syncthreads();
+        cnt += tot;
+        t = t2;
+        w = wn;
+        if (__ballot(bad)) { bad = true; break; }
+    }
+    if (x == 0) {
+        status[2 * li] = (!bad && cnt == (int64_t)L.out_len) ? 0 : -1;
+        status[2 * li + 1] = (int)((clock64() - c0) >> 10);  // profile: clock ticks / 1024
+    }
+}
+
 // ---- resolve ------------------------------------------------------------------------
 // thread = (16-byte chunk of a row, row, image); grid.y over rows of all images via
 // a row table (image, row).  Window markers (~4 % of the symbols, near each
@@ -728,6 +967,7 @@ constexpr int kResolveList = 4096;
 
 __global__ __launch_bounds__(256) void k_png_resolve(const PngImgDev* imgs, const int2* rows, int nrows,
                                                      int* err) {
+    raise_priority();
     __shared__ uint32_t s_pos[kResolveList];  // marker positions in the row (byte index after the filter byte)
     __shared__ uint32_t s_cnt;
     const int rr = blockIdx.y * 65535 + blockIdx.x;  // row of the batch
@@ -872,6 +1112,7 @@ template <int BPP>
 __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngImgDev* imgs, const int2* groups,
                                                                       const int* prog_base, unsigned* prog,
                                                                       unsigned* ticket) {
+    raise_priority();
     constexpr int NW = kPngUnfilterThreads / 64, G = kUnfG;
     __shared__ int s_t;
     if (threadIdx.x == 0) s_t = (int)atomicAdd(ticket, 1u);
@@ -1037,6 +1278,7 @@ template <int BPP>
 __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter8(const PngImgDev* imgs, const int2* groups,
                                                                        const int* prog_base, unsigned* prog,
                                                                        unsigned* ticket) {
+    raise_priority();
     static_assert(BPP <= 4, "8-byte chunks carry at most 4 bytes of left context");
     constexpr int NW = kPngUnfilterThreads / 64, G = kUnfG;
     __shared__ int s_t;
@@ -1390,7 +1632,12 @@ hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, int
 hipError_t launch_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int n, const uint16_t* tok, int* status,
                              hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_png_expand, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status);
+    static const int which = [] {  // IK_PNG_EXPAND=1: the per-position search kernel
+        const char* e = getenv("IK_PNG_EXPAND");
+        return e && !strcmp(e, "1") ? 1 : 2;
+    }();
+    if (which == 1) hipLaunchKernelGGL(k_png_expand, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status);
+    else hipLaunchKernelGGL(k_png_expand4, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status);
     return hipGetLastError();
 }
 
@@ -1405,12 +1652,13 @@ hipError_t launch_png_unfilter(const PngImgDev* imgs, const int2* groups, int ng
                                unsigned* prog, unsigned* ticket, int bpp, hipStream_t s) {
     if (ngroups <= 0) return hipSuccess;
     const dim3 grid(ngroups), block(kPngUnfilterThreads);
-    // 8-byte chunks for up to 4 bytes per pixel (IK_PNG_UNF16=1: the 16-byte kernel)
-    static const bool wide = [] {
-        const char* e = getenv("IK_PNG_UNF16");
+    // IK_PNG_UNF8=1: 8-byte chunks (measured slower on MI355X: 15.3 vs 8.7 ms per
+    // 64 4096^2 RGBA frames, beside the next batch's block search)
+    static const bool narrow = [] {
+        const char* e = getenv("IK_PNG_UNF8");
         return e && !strcmp(e, "1");
     }();
-    if (!wide && bpp <= 4) {
+    if (narrow && bpp <= 4) {
 #define IK_UNF8(B) hipLaunchKernelGGL(k_png_unfilter8<B>, grid, block, 0, s, imgs, groups, prog_base, prog, ticket)
         switch (bpp) {
         case 1: IK_UNF8(1); break;

@@ -538,6 +538,14 @@ int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Png
     return IK_OK;
 }
 
+static bool search_after_resolve() {
+    static const bool v = [] {
+        const char* e = getenv("IK_FIND_AFTER");
+        return e && !strcmp(e, "resolve");
+    }();
+    return v;
+}
+
 // the block search of a batch whose upload was issued: on stream s, once the
 // upload (with its gather + CRC pass) has landed; once per batch
 static void png_find_launch(PngBatchState& S, hipStream_t s) {
@@ -687,8 +695,8 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         }
         const PngImgDev* d_imgs = reinterpret_cast<const PngImgDev*>(dev + o_imgs);
         // ---- the block search: launched here unless the kernel stage launched it
-        // while the previous batch's expand / resolve / unfilter ran (PngUpload::
-        // on_decoded); its candidates come from the upload area ----
+        // beside the previous batch's unfilter (PngUpload::on_next_search); its
+        // candidates come from the upload area ----
         hipError_t e = rc ? hipSuccess : X.h2d(dev + o_imgs, hd.data(), sizeof(PngImgDev) * m);
         const bool pre = S.find_launched;
         if (!rc && e == hipSuccess) {
@@ -823,9 +831,6 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         }
         tim[16] = pre ? 1.0 : 0.0;
         release_area(S.area);
-        // the next batch's block search may start now, beside this batch's expand,
-        // resolve and unfilter (the stage executor's hook)
-        if (up.on_decoded) up.on_decoded();
         const double t3 = now_ms();
         // ---- offsets, output images, expand, resolve, unfilter ----
         std::vector<int64_t>& hob = ht.obase;
@@ -888,6 +893,11 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             if (ue != hipSuccess) rc = hip_fail(ue, "PNG expand tables");
             hxst.resize(2 * hl.size());
             mk[2] = now_ms();  // lane tables uploaded
+            // the next batch's block search (VALU-bound) beside this batch's expand,
+            // resolve and unfilter, which run at a raised wave priority (ik_png.hip
+            // raise_priority): the stage executor's hook.  IK_FIND_AFTER=resolve
+            // holds it until this batch's resolve pass is done.
+            if (!rc && up.on_next_search && !search_after_resolve()) up.on_next_search(nullptr);
             if (!rc) {
                 hipError_t e3 = hipSuccess;
                 rec(4, s);
@@ -909,6 +919,8 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                 if (e3 == hipSuccess) e3 = launch_png_resolve(d_imgs, d_rows, (int)hrows.size(),
                                                               reinterpret_cast<int*>(dev + o_err), s);
                 rec(6, s);
+                if (e3 == hipSuccess && up.on_next_search && search_after_resolve())
+                    up.on_next_search(ev.ok ? ev.e[6] : nullptr);
                 // unfilter: one launch per bytes-per-pixel class, over that class's
                 // images; a workgroup per 16 bands, its (image, group) by ticket
                 if (e3 == hipSuccess) {

@@ -178,10 +178,11 @@ struct PngUpload {
     const size_t* lens = nullptr;
     int n = 0;
     std::shared_ptr<PngBatchState> st;
-    // called by png_decode_finish once the batch's decode rounds are done (its
-    // compressed streams are no longer read): the stage executor launches the
-    // next batch's block search there, beside this batch's remaining kernels
-    std::function<void()> on_decoded;
+    // called by png_decode_finish once the batch's decode rounds are done (or, with
+    // IK_FIND_AFTER=resolve, once its resolve pass is queued, with an event
+    // recorded after it; null = none): the stage executor launches the next
+    // batch's block search there, beside this batch's remaining kernels
+    std::function<void(hipEvent_t)> on_next_search;
 };
 int png_upload_begin(const uint8_t* const* b, const size_t* lens, int n, PngUpload& up);
 int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* msgs);

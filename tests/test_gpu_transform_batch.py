@@ -205,8 +205,11 @@ def test_two_logical_devices_match_single_device(ik):
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, IK_DEVICES="0,0", IK_PKG=os.path.join(root, "rust-image-transform_amd"),
-               IK_TESTS=os.path.join(root, "tests"))
+    # IK_MIN_DEVICE_BATCH=8: the 20-request batch splits over both devices (with the
+    # default 64 it would go whole to one, and the balance check below would weigh
+    # one batch against the single-request traffic)
+    env = dict(os.environ, IK_DEVICES="0,0", IK_MIN_DEVICE_BATCH="8",
+               IK_PKG=os.path.join(root, "rust-image-transform_amd"), IK_TESTS=os.path.join(root, "tests"))
     r = subprocess.run([sys.executable, "-c", MULTI_SCRIPT], env=env, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stderr[-2000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])

@@ -16,7 +16,7 @@ import zlib
 
 import numpy as np
 import pytest
-from PIL import Image
+from PIL import Image, ImageFile
 
 import ikutil
 
@@ -99,7 +99,12 @@ def test_gather_assembles_stream_and_passes_crcs(model, chunk, z_off):
 def test_pillow_stream_crcs(model):
     px = ikutil.synth(1024, 700, 3, seed=5, pattern="S")
     b = io.BytesIO()
-    Image.fromarray(px).save(b, format="PNG")
+    # Pillow writes one IDAT per MAXBLOCK bytes; other test modules enlarge it
+    keep, ImageFile.MAXBLOCK = ImageFile.MAXBLOCK, 65536
+    try:
+        Image.fromarray(px).save(b, format="PNG")
+    finally:
+        ImageFile.MAXBLOCK = keep
     png = b.getvalue()
     n, got, _, bad = _run(model, png)
     assert n >= 2 and not any(bad)
