@@ -3,17 +3,21 @@
 
 Headline `value` (BASELINE.json metric): synthetic 4096x4096
 RGBA8 frames as PNG files (Pillow, zlib level 6, adaptive filters; the configs[1]
-frame in the container SURVEY D-2 names) sit in HOST memory (page-locked, as a
-server reads request bodies with ik_host_alloc; --pageable for ordinary memory);
-one step is one batch through ik_transform_batch_submit / _wait -- decode_image
-(upload + GPU gather/CRC, GPU inflate + unfilter, ik_png.hip), resize_image to
-512x512 (Triangle = configs[1]'s "bilinear"), encode_image WebP q80 (libwebp,
-byte-identical to the reference's webp 0.3.1 path) -- ending with the WebP bytes
-in host memory; --inflight batches are outstanding, so one batch's upload runs
-under another's kernels.  value = input pixels of all ranks / max-over-ranks wall
-time of the K timed steps (every timed batch waited for).  The host threads the
-GPU path may use are stated (--threads, default 32 = an 8-GPU node's 256 cores /
-8).
+frame in the container SURVEY D-2 names), one device allocation per request,
+already resident in HBM when the timed region starts (the measurement contract);
+one step is one batch through ik_transform_batch_submit_device / _wait --
+decode_image (GPU chunk walk, gather + IDAT CRCs, inflate + unfilter, ik_png.hip),
+resize_image to 512x512 (Triangle = configs[1]'s "bilinear"), encode_image WebP
+q80 (libwebp, byte-identical to the reference's webp 0.3.1 path) -- ending with
+the WebP bytes in host memory; --inflight batches are outstanding.  value = input
+pixels of all ranks / max-over-ranks wall time of the K timed steps (every timed
+batch waited for).  The host threads the GPU path may use are stated (--threads,
+default 32 = an 8-GPU node's 256 cores / 8).
+
+pcie_inclusive: the same steps with the PNG files in HOST memory (page-locked, as a
+server reads request bodies with ik_host_alloc) through ik_transform_batch_submit,
+so the compressed bytes cross PCIe inside the timed region (upload of one batch
+under another's kernels).
 
 Beside it, in the same JSON line:
   cpu_baseline   the same PNG bytes through the reference CPU path restated
@@ -85,6 +89,7 @@ def parse():
     ap.add_argument("--inflight", type=int, default=3,
                     help="batches submitted before the oldest is waited for (upload / kernels / host coders "
                          "of three batches overlap)")
+    ap.add_argument("--no-pcie-leg", action="store_true", help="skip the pcie_inclusive leg (host-memory inputs)")
     ap.add_argument("--pageable", action="store_true",
                     help="inputs in ordinary host memory (default: page-locked, ik_host_alloc)")
     ap.add_argument("--pageable-steps", type=int, default=4,
@@ -302,7 +307,8 @@ def main():
         dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
-    from imagekit import PinnedBytes, _lib, transform_batch, transform_batch_submit
+    from imagekit import (DeviceBytes, PinnedBytes, _lib, transform_batch, transform_batch_submit,
+                          transform_batch_submit_device)
     lib = _lib.load()
     if lib.ik_init(-1 if args.inproc_devices > 0 else local) != 0:
         raise SystemExit(f"ik_init failed: {_lib.last_error()}")
@@ -311,6 +317,8 @@ def main():
     # them: the upload DMAs them in place (--pageable: ordinary Python bytes)
     inputs = pngs if args.pageable else [PinnedBytes(p) for p in pngs]
     reqs = [inputs[i % len(inputs)] for i in range(B)]
+    # the headline's inputs: every request its own device allocation in HBM
+    dreqs = [DeviceBytes(pngs[i % len(pngs)]) for i in range(B)]
 
     def barrier():
         if dist is not None:
@@ -329,8 +337,8 @@ def main():
         stage_ms.append(list(timing))
 
     def submit(rq):
-        return transform_batch_submit(rq, [(O, O)] * B, [FORMATS["webp"]] * B, [args.quality] * B, filter=f,
-                                      threads=args.threads)
+        fn = transform_batch_submit_device if isinstance(rq[0], DeviceBytes) else transform_batch_submit
+        return fn(rq, [(O, O)] * B, [FORMATS["webp"]] * B, [args.quality] * B, filter=f, threads=args.threads)
 
     def run_pipelined(nsteps, rq=None, depth=None):
         """nsteps batches with up to `depth` in flight (upload of one under the
@@ -356,7 +364,27 @@ def main():
             note_timing()
         return out
 
-    run = run_pipelined if args.pipeline else run_blocking
+    # PCIe-inclusive leg: the same steps from host memory (reported beside value)
+    pcie = {}
+    if not args.no_pcie_leg:
+        run_pipelined(args.warmup, rq=reqs) if args.pipeline else run_blocking(args.warmup)
+        barrier()
+        t1 = time.perf_counter()
+        r1 = run_pipelined(args.steps, rq=reqs) if args.pipeline else run_blocking(args.steps)
+        torch.cuda.synchronize()
+        te = reduce_max(time.perf_counter() - t1, dist, dev)
+        barrier()
+        assert all(r is not None and r[:4] == b"RIFF" for r in r1)
+        pst = np.mean(np.array(stage_ms), axis=0)
+        stage_ms.clear()
+        pcie = {"value": round(aggregate_mpix(world, B * args.steps, S, te), 2), "unit": "MPix/s",
+                "ms_per_step": round(te / args.steps * 1e3, 3),
+                "inputs": "pageable host memory" if args.pageable else "page-locked host memory (ik_host_alloc)",
+                "entry": "ik_transform_batch_submit", "png_bytes_per_step": int(sum(len(p) for p in reqs)),
+                "upload_device_ms": round(float(pst[1]), 3)}
+
+    # headline: inputs resident in HBM
+    run = (lambda k: run_pipelined(k, rq=dreqs)) if args.pipeline else run_blocking
     run(args.warmup)
     stage_ms.clear()
     cnt0 = (ctypes.c_ulonglong * 2)()
@@ -529,11 +557,13 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": f"{S}x{S} RGBA8 synthetic frames as PNG (zlib level 6) in host memory -> "
-                            f"ik_transform_batch: decode_image (GPU inflate + unfilter) -> resize_image {O}x{O} "
-                            f"({args.filter}) -> encode_image webp q{args.quality} (libwebp) -> WebP bytes in host memory",
+                "workload": f"{S}x{S} RGBA8 synthetic frames as PNG (zlib level 6), resident in HBM (one device "
+                            f"allocation per request) -> ik_transform_batch_submit_device: decode_image (GPU chunk "
+                            f"walk, gather + CRC, inflate + unfilter) -> resize_image {O}x{O} ({args.filter}) -> "
+                            f"encode_image webp q{args.quality} (libwebp) -> WebP bytes in host memory",
                 "batch_per_gpu": B, "inflight": args.inflight if args.pipeline else 1,
-                "inputs": "pageable host memory" if args.pageable else "page-locked host memory (ik_host_alloc)",
+                "inputs": "device memory (HBM), resident before the timed region" if args.pipeline else
+                          ("pageable host memory" if args.pageable else "page-locked host memory (ik_host_alloc)"),
                 "inproc_devices": args.inproc_devices, "filter": args.filter, "format": "webp", "quality": args.quality,
                 "host_threads_per_gpu": args.threads, "png_bytes_per_image": in_bytes,
                 "webp_bytes_per_image": out_bytes,
@@ -546,6 +576,7 @@ def main():
             "roofline_resize": roof_resize,
             "png_decode_stages_ms": png_stages,
             "kernels": kernels,
+            "pcie_inclusive": pcie,
             "pageable_input": pageable,
             "hbm_resident": hbm,
             "decode_inclusive_jpeg": jpg,

@@ -229,6 +229,20 @@ int ik_transform_batch_submit(const uint8_t *const *bytes, const size_t *lens, u
                               uint8_t **outs, size_t *out_lens, int *status, uint64_t *ticket);
 int ik_transform_batch_wait(uint64_t ticket);
 
+/* ik_transform_batch_submit over request bodies already in device memory (HBM)
+ * of one device: dev_bytes[i] are device addresses (hipMalloc / ik_dev_alloc),
+ * valid until the wait returns.  The batch runs on the device that holds them.
+ * PNG files are walked, gathered, CRC-checked and decoded on the GPU where they
+ * lie (no PCIe transfer of the compressed bytes); any other item, and a PNG the
+ * GPU path does not take, is copied back to host memory first.  Outputs, status
+ * and errors as ik_transform_batch_submit; wait with ik_transform_batch_wait.
+ * (The reference's handlers receive bodies in host memory, src/lib.rs:175-191;
+ * this entry serves callers that already hold them on the device.) */
+int ik_transform_batch_submit_device(const uint8_t *const *dev_bytes, const size_t *lens, uint32_t n,
+                                     const int64_t *w, const int64_t *h, const int *fmt, const int *quality,
+                                     int filter, int threads, uint8_t **outs, size_t *out_lens, int *status,
+                                     uint64_t *ticket);
+
 /* A batch of n same-geometry 8-bit images already resident in device memory
  * (image i at dev_src + i*src_image_stride, rows src_pitch bytes apart) ->
  * resize to nw x nh -> encode.  Encoded bytes are written into the caller's

@@ -954,9 +954,17 @@ static std::string last_error_str() { return t_err; }
 // decode_image over a batch on the calling thread's device; per-item status and
 // message (the decoder's own, as TransformError(e.to_string()) carries it).  up:
 // the batch's PNG streams' upload, already issued (png_upload_begin), or null
+// sniff: null, or a host copy of each item's first bytes (sniff_len(i) of them) when
+// bytes holds device addresses for the PNG items (device-resident inputs: every
+// other item is a host copy already)
+static size_t sniff_len(const uint8_t* const* sniff, const uint8_t* const* bytes, const size_t* lens, uint32_t i) {
+    return sniff && sniff[i] != bytes[i] ? std::min<size_t>(lens[i], 64) : lens[i];
+}
+
 int decode_batch_dev(const uint8_t* const* bytes, const size_t* lens, uint32_t n, ik_image** outs, int* fmts,
-                     int* st, std::string* msg, int threads, PngUpload* up = nullptr) {
-    std::vector<const uint8_t*> jb, pb;
+                     int* st, std::string* msg, int threads, PngUpload* up = nullptr,
+                     const uint8_t* const* sniff = nullptr) {
+    std::vector<const uint8_t*> jb, pb, ph;
     std::vector<size_t> jl, pl;
     std::vector<uint32_t> ji, pi, other;
     for (uint32_t i = 0; i < n; ++i) {
@@ -964,7 +972,7 @@ int decode_batch_dev(const uint8_t* const* bytes, const size_t* lens, uint32_t n
         st[i] = IK_OK;
         if (fmts) fmts[i] = -1;
         if (!bytes[i] && lens[i]) { st[i] = fail(IK_ERR_INVALID, "null bytes"); msg[i] = t_err; continue; }
-        const Sniffed f = guess_format(bytes[i], lens[i]);
+        const Sniffed f = guess_format(sniff ? sniff[i] : bytes[i], sniff_len(sniff, bytes, lens, i));
         if (f == Sniffed::Jpeg) {
             jb.push_back(bytes[i]);
             jl.push_back(lens[i]);
@@ -973,6 +981,7 @@ int decode_batch_dev(const uint8_t* const* bytes, const size_t* lens, uint32_t n
         } else if (f == Sniffed::Png) {
             pb.push_back(bytes[i]);
             pl.push_back(lens[i]);
+            ph.push_back(sniff ? sniff[i] : bytes[i]);
             pi.push_back(i);
         } else {
             other.push_back(i);
@@ -982,8 +991,15 @@ int decode_batch_dev(const uint8_t* const* bytes, const size_t* lens, uint32_t n
         std::vector<ik_image*> po(pi.size(), nullptr);
         std::vector<int> ps(pi.size(), IK_OK);
         std::vector<std::string> pm(pi.size());
-        if (up && up->n == (int)pi.size()) png_decode_finish(*up, po.data(), ps.data(), pm.data());
-        else decode_png_batch(pb.data(), pl.data(), (int)pi.size(), po.data(), ps.data(), pm.data());
+        if (up && up->n == (int)pi.size()) {
+            png_decode_finish(*up, po.data(), ps.data(), pm.data());
+        } else {
+            PngUpload u;
+            u.dev = sniff != nullptr;  // (device-resident inputs: the PNG items are device addresses)
+            u.heads = ph.data();
+            png_upload_begin(pb.data(), pl.data(), (int)pi.size(), u);
+            png_decode_finish(u, po.data(), ps.data(), pm.data());
+        }
         for (size_t k = 0; k < pi.size(); ++k) {
             outs[pi[k]] = po[k];
             st[pi[k]] = ps[k];
@@ -1100,14 +1116,18 @@ struct HostPhase {
 };
 
 // the PNG requests among idx (decode_batch_dev takes the same ones, in the same order)
-static void png_items(const uint8_t* const* bytes, const size_t* lens, const std::vector<uint32_t>& idx,
-                      std::vector<const uint8_t*>& pb, std::vector<size_t>& pl) {
+static void png_items(const uint8_t* const* bytes, const size_t* lens, const uint8_t* const* sniff,
+                      const std::vector<uint32_t>& idx, std::vector<const uint8_t*>& pb, std::vector<size_t>& pl,
+                      std::vector<const uint8_t*>& ph) {
     pb.clear();
     pl.clear();
+    ph.clear();
     for (uint32_t i : idx)
-        if ((bytes[i] || !lens[i]) && guess_format(bytes[i], lens[i]) == Sniffed::Png) {
+        if ((bytes[i] || !lens[i]) &&
+            guess_format(sniff ? sniff[i] : bytes[i], sniff_len(sniff, bytes, lens, i)) == Sniffed::Png) {
             pb.push_back(bytes[i]);
             pl.push_back(lens[i]);
+            ph.push_back(sniff ? sniff[i] : bytes[i]);
         }
 }
 
@@ -1116,14 +1136,19 @@ static void png_items(const uint8_t* const* bytes, const size_t* lens, const std
 // message land in st[i] / errs[i]
 static void transform_device_phase(const uint8_t* const* bytes, const size_t* lens, const int64_t* w,
                                    const int64_t* h, const int* fmt, const int* quality, int filter, int* st,
-                                   std::string* errs, HostPhase& hp, PngUpload* up) {
+                                   std::string* errs, HostPhase& hp, PngUpload* up,
+                                   const uint8_t* const* sniff = nullptr) {
     const std::vector<uint32_t>& idx = hp.idx;
     const int threads = hp.threads;
     const uint32_t m = (uint32_t)idx.size();
     if (!m) return;
-    std::vector<const uint8_t*> b(m);
+    std::vector<const uint8_t*> b(m), sn(sniff ? m : 0);
     std::vector<size_t> l(m);
-    for (uint32_t k = 0; k < m; ++k) { b[k] = bytes[idx[k]]; l[k] = lens[idx[k]]; }
+    for (uint32_t k = 0; k < m; ++k) {
+        b[k] = bytes[idx[k]];
+        l[k] = lens[idx[k]];
+        if (sniff) sn[k] = sniff[idx[k]];
+    }
     std::vector<ik_image*> imgs(m, nullptr);
     std::vector<int> ds(m, IK_OK);
     std::vector<std::string> dm(m);
@@ -1131,7 +1156,8 @@ static void transform_device_phase(const uint8_t* const* bytes, const size_t* le
     // GPU phases under the device's kernel gate (held from the decode kernels
     // through resize and the encoders' device front ends), the host coders after
     gate_pin(kGateKernels, true);
-    decode_batch_dev(b.data(), l.data(), m, imgs.data(), nullptr, ds.data(), dm.data(), threads, up);
+    decode_batch_dev(b.data(), l.data(), m, imgs.data(), nullptr, ds.data(), dm.data(), threads, up,
+                     sniff ? sn.data() : nullptr);
     gate_enter(kGateKernels);
     std::mutex tmu;
     double& t_resize = hp.t_resize;
@@ -1249,6 +1275,12 @@ struct Ticket {
     std::mutex mu;
     std::condition_variable cv;
     int pending = 0;
+    // device-resident inputs (ik_transform_batch_submit_device): the request array
+    // the stages read (PNG items: the caller's device addresses; others: host
+    // copies), the host copies, and each item's sniff bytes
+    std::vector<const uint8_t*> eff, sniff;
+    std::vector<std::vector<uint8_t>> hcopy;
+    std::vector<uint8_t> heads;
 };
 
 // one device's share of a ticket
@@ -1264,6 +1296,8 @@ struct BatchPart {
     HostPhase hp;
     std::vector<const uint8_t*> pb;  // its PNG inputs (the upload stage's batch)
     std::vector<size_t> pl;
+    std::vector<const uint8_t*> ph;  // their first bytes in host memory
+    const uint8_t* const* sniff = nullptr;  // device-resident inputs (Ticket::sniff), else null
     PngUpload up;
     int logical = -1;  // logical device (multi-device dispatch), -1 = none
     uint64_t cost = 0;
@@ -1295,7 +1329,9 @@ private:
                 q_[stage].pop_front();
             }
             if (stage == 0) {
-                png_items(p->bytes, p->lens, p->hp.idx, p->pb, p->pl);
+                png_items(p->bytes, p->lens, p->sniff, p->hp.idx, p->pb, p->pl, p->ph);
+                p->up.dev = p->sniff != nullptr;
+                p->up.heads = p->ph.data();
                 if (!p->pb.empty()) png_upload_begin(p->pb.data(), p->pl.data(), (int)p->pb.size(), p->up);
                 {
                     std::lock_guard<std::mutex> lk(mu_);
@@ -1319,7 +1355,7 @@ private:
                 png_find_prelaunch(nx->up, fs);
             };
             transform_device_phase(p->bytes, p->lens, p->w, p->h, p->fmt, p->quality, p->filter, t.st.data(),
-                                   t.errs.data(), p->hp, p->pb.empty() ? nullptr : &p->up);
+                                   t.errs.data(), p->hp, p->pb.empty() ? nullptr : &p->up, p->sniff);
             p->up = PngUpload();
             pool_->post([p] {
                 Ticket& tk = *p->t;
@@ -1368,38 +1404,46 @@ int min_device_batch() {
 
 extern "C" {
 
-int ik_transform_batch_submit(const uint8_t* const* bytes, const size_t* lens, uint32_t n, const int64_t* w,
-                              const int64_t* h, const int* fmt, const int* quality, int filter, int threads,
-                              uint8_t** outs, size_t* out_lens, int* status, uint64_t* ticket) {
-    if (!bytes || !lens || !w || !h || !fmt || !quality || !outs || !out_lens || !n || !ticket)
-        return fail(IK_ERR_INVALID, "bad batch");
-    auto t = std::make_shared<Ticket>();
-    t->n = n;
-    t->outs = outs;
-    t->out_lens = out_lens;
-    t->status = status;
-    t->st.assign(n, IK_OK);
-    t->errs.assign(n, std::string());
-    for (uint32_t i = 0; i < n; ++i) { outs[i] = nullptr; out_lens[i] = 0; }
+}  // extern "C"
+
+namespace ik {
+namespace {
+
+// the parts of a ticket to the stage executors.  bytes / sniff: the request array
+// the stages read (Ticket::eff / sniff for device-resident inputs); phys >= 0:
+// the inputs live on that physical device, so the batch goes whole to it
+int submit_parts(const std::shared_ptr<Ticket>& t, const uint8_t* const* bytes, const uint8_t* const* sniff,
+                 int phys, const size_t* lens, uint32_t n, const int64_t* w, const int64_t* h, const int* fmt,
+                 const int* quality, int filter, int threads, uint64_t* ticket) {
     auto make_part = [&](uint32_t lo, uint32_t hi) {
         auto p = std::make_shared<BatchPart>();
         p->t = t;
         p->bytes = bytes; p->lens = lens; p->w = w; p->h = h; p->fmt = fmt; p->quality = quality;
+        p->sniff = sniff;
         p->filter = filter;
         p->hp.threads = threads;
         for (uint32_t i = lo; i < hi; ++i) p->hp.idx.push_back(i);
         return p;
     };
+    auto cost_of = [&](uint32_t i) {
+        return request_cost(sniff ? sniff[i] : bytes[i], sniff_len(sniff, bytes, lens, i), w[i], h[i], fmt[i]);
+    };
     std::vector<std::shared_ptr<BatchPart>> parts;
     if (!sched_multi()) {
         parts.push_back(make_part(0, n));
+    } else if (phys >= 0) {
+        auto p = make_part(0, n);
+        for (uint32_t i = 0; i < n; ++i) p->cost += cost_of(i);
+        p->logical = sched_acquire_on(phys, p->cost);
+        if (p->logical < 0) return fail(IK_ERR_INVALID, "the inputs are on device %d, which serves no logical device", phys);
+        parts.push_back(p);
     } else {
         // whole parts of >= IK_MIN_DEVICE_BATCH requests, each to the least-loaded device
         const int nd = sched_count();
         const uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)nd, n / (uint32_t)min_device_batch()));
         for (uint32_t q = 0; q < P; ++q) {
             auto p = make_part((uint32_t)((uint64_t)n * q / P), (uint32_t)((uint64_t)n * (q + 1) / P));
-            for (uint32_t i : p->hp.idx) p->cost += request_cost(bytes[i], lens[i], w[i], h[i], fmt[i]);
+            for (uint32_t i : p->hp.idx) p->cost += cost_of(i);
             p->logical = sched_acquire(p->cost);
             parts.push_back(p);
         }
@@ -1415,6 +1459,92 @@ int ik_transform_batch_submit(const uint8_t* const* bytes, const size_t* lens, u
         stage_exec(ld).submit(std::move(p));
     }
     return IK_OK;
+}
+
+std::shared_ptr<Ticket> new_ticket(uint32_t n, uint8_t** outs, size_t* out_lens, int* status) {
+    auto t = std::make_shared<Ticket>();
+    t->n = n;
+    t->outs = outs;
+    t->out_lens = out_lens;
+    t->status = status;
+    t->st.assign(n, IK_OK);
+    t->errs.assign(n, std::string());
+    for (uint32_t i = 0; i < n; ++i) { outs[i] = nullptr; out_lens[i] = 0; }
+    return t;
+}
+
+}  // namespace
+}  // namespace ik
+
+extern "C" {
+
+int ik_transform_batch_submit(const uint8_t* const* bytes, const size_t* lens, uint32_t n, const int64_t* w,
+                              const int64_t* h, const int* fmt, const int* quality, int filter, int threads,
+                              uint8_t** outs, size_t* out_lens, int* status, uint64_t* ticket) {
+    if (!bytes || !lens || !w || !h || !fmt || !quality || !outs || !out_lens || !n || !ticket)
+        return fail(IK_ERR_INVALID, "bad batch");
+    auto t = new_ticket(n, outs, out_lens, status);
+    return submit_parts(t, bytes, nullptr, -1, lens, n, w, h, fmt, quality, filter, threads, ticket);
+}
+
+int ik_transform_batch_submit_device(const uint8_t* const* dev_bytes, const size_t* lens, uint32_t n,
+                                     const int64_t* w, const int64_t* h, const int* fmt, const int* quality,
+                                     int filter, int threads, uint8_t** outs, size_t* out_lens, int* status,
+                                     uint64_t* ticket) {
+    if (!dev_bytes || !lens || !w || !h || !fmt || !quality || !outs || !out_lens || !n || !ticket)
+        return fail(IK_ERR_INVALID, "bad batch");
+    // every input must be device memory of one device (the batch runs there)
+    int phys = -1;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (!lens[i]) continue;
+        if (!dev_bytes[i]) return fail(IK_ERR_INVALID, "input %u: null bytes", i);
+        hipPointerAttribute_t at{};
+        if (hipPointerGetAttributes(&at, dev_bytes[i]) != hipSuccess || at.type != hipMemoryTypeDevice) {
+            (void)hipGetLastError();
+            return fail(IK_ERR_INVALID, "input %u is not device memory", i);
+        }
+        if (phys < 0) phys = at.device;
+        else if (phys != at.device) return fail(IK_ERR_INVALID, "inputs on devices %d and %d", phys, at.device);
+    }
+    if (phys < 0) phys = current_device();
+    auto t = new_ticket(n, outs, out_lens, status);
+    t->eff.assign(dev_bytes, dev_bytes + n);
+    t->sniff.assign(n, nullptr);
+    t->hcopy.resize(n);
+    t->heads.assign(64 * (size_t)n, 0);
+    {
+        DeviceGuard g(phys);
+        // the first 64 bytes of every file, through pinned memory
+        const size_t o_files = (64 * (size_t)n + 255) & ~size_t(255);
+        uint8_t* pin = pinned_slot(5, o_files + 2 * sizeof(uint64_t) * n);
+        void* dp = nullptr;
+        if (!pin || hipHostGetDevicePointer(&dp, pin, 0) != hipSuccess || !dp)
+            return fail(IK_ERR_NOMEM, "cannot allocate pinned memory for the input headers");
+        uint64_t* files = reinterpret_cast<uint64_t*>(pin + o_files);
+        for (uint32_t i = 0; i < n; ++i) {
+            files[i] = (uint64_t)(uintptr_t)dev_bytes[i];
+            files[n + i] = dev_bytes[i] ? lens[i] : 0;
+        }
+        hipStream_t s = thread_stream();
+        const uint64_t* df = reinterpret_cast<const uint64_t*>(reinterpret_cast<uint8_t*>(dp) + o_files);
+        IK_HIP(launch_copy_heads(df, df + n, (int)n, reinterpret_cast<uint8_t*>(dp), s));
+        IK_HIP(hipStreamSynchronize(s));
+        std::memcpy(t->heads.data(), pin, 64 * (size_t)n);
+        // PNG files stay where they are (the upload stage walks and gathers them on
+        // the GPU); any other item comes back to host memory for its host-side parse
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint8_t* hd = t->heads.data() + 64 * (size_t)i;
+            if (!dev_bytes[i] || guess_format(hd, std::min<size_t>(lens[i], 64)) == Sniffed::Png) {
+                t->sniff[i] = dev_bytes[i] ? hd : nullptr;
+                continue;
+            }
+            t->hcopy[i].resize(lens[i]);
+            IK_HIP(hipMemcpy(t->hcopy[i].data(), dev_bytes[i], lens[i], hipMemcpyDeviceToHost));
+            t->eff[i] = t->sniff[i] = t->hcopy[i].data();
+        }
+    }
+    return submit_parts(t, t->eff.data(), t->sniff.data(), sched_multi() ? phys : -1, lens, n, w, h, fmt, quality,
+                        filter, threads, ticket);
 }
 
 int ik_transform_batch_wait(uint64_t ticket) {

@@ -70,11 +70,34 @@ struct PngPxDev {
 };
 hipError_t launch_png_px(const PngPxDev& px, hipStream_t s);
 
-// piece_crc[2 i] = finished CRC-32 of piece i's bytes, [2 i + 1] = its length
-hipError_t launch_png_gather(const uint8_t* raw, uint8_t* stream, const PngGatherPiece* pieces, int npieces,
+// piece_crc[2 i] = finished CRC-32 of piece i's bytes, [2 i + 1] = its length.
+// raw: the base address the pieces' src / the chunks' crc_at offsets are relative
+// to (the upload area, or 0 when they are the caller's device addresses)
+hipError_t launch_png_gather(uintptr_t raw, uint8_t* stream, const PngGatherPiece* pieces, int npieces,
                              uint32_t* piece_crc, hipStream_t s);
-hipError_t launch_png_crc_check(const uint8_t* raw, const PngCrcChunk* chunks, int nchunks, const uint32_t* piece_crc,
+hipError_t launch_png_crc_check(uintptr_t raw, const PngCrcChunk* chunks, int nchunks, const uint32_t* piece_crc,
                                 int* err, hipStream_t s);
+
+// Chunk walk of PNG files already in device memory (the caller's request bodies
+// in HBM): one wave per file follows the chunk lengths from byte 8, as png does,
+// and records every chunk; the contents of the non-IDAT chunks (IHDR, PLTE, tRNS,
+// ancillary: type + data + CRC) and the first bytes of each IDAT payload go to the
+// file's side area, so the host can plan the stream from host memory alone.
+struct PngWalkRec {
+    uint64_t off;      // file offset of the chunk's length field
+    uint32_t len;      // data length
+    uint32_t side;     // offset of type + data + CRC in the file's side area (non-IDAT), ~0 if none
+    uint8_t type[4];
+    uint8_t head[4];   // first data bytes (IDAT: the zlib header lives in the first)
+};
+// out_n[f]: chunks recorded (>= 0), or -1 (record table full) / -2 (side area
+// full): the host then copies the file back and decodes it there
+constexpr int kPngWalkRecs = 4096;         // chunks recorded per file
+constexpr uint32_t kPngWalkSide = 65536;   // side-area bytes per file
+// out[64 f + t] = byte t of file f (0 past its end)
+hipError_t launch_copy_heads(const uint64_t* files, const uint64_t* lens, int n, uint8_t* out, hipStream_t s);
+hipError_t launch_png_walk(const uint64_t* files, const uint64_t* lens, int n, PngWalkRec* recs, uint8_t* side,
+                           int* out_n, hipStream_t s);
 
 // dst[i] = src[i] for n words, on the compute stream; one side may be pinned host
 // memory (the small transfers of the PNG kernel phase: ik_png_decode.cpp Xfer)

@@ -1428,7 +1428,7 @@ struct CrcOps {
     uint32_t crc_idat;   // finished CRC of the chunk type "IDAT" (the first 4 bytes a chunk CRC covers)
 };
 
-__global__ __launch_bounds__(256) void k_png_gather(const uint8_t* __restrict__ raw, uint8_t* __restrict__ stream,
+__global__ __launch_bounds__(256) void k_png_gather(uintptr_t raw, uint8_t* __restrict__ stream,
                                                     const PngGatherPiece* __restrict__ pieces,
                                                     uint32_t* __restrict__ piece_crc, CrcOps ops) {
     __shared__ uint32_t t[1024];
@@ -1450,7 +1450,7 @@ __global__ __launch_bounds__(256) void k_png_gather(const uint8_t* __restrict__ 
     if (len && P.src == kPngNoSrc) {
         for (uint32_t i = 0; i < len; ++i) dp[i] = 0;
     } else if (len) {
-        const IK_GLOBAL uint8_t* sp = (const IK_GLOBAL uint8_t*)(raw + P.src + b0);
+        const IK_GLOBAL uint8_t* sp = (const IK_GLOBAL uint8_t*)(raw + (uintptr_t)(P.src + b0));
         uint32_t i = 0;
         const uint32_t mis = (uint32_t)((uintptr_t)dp & 3u);
         const uint32_t pre = mis ? (4u - mis < len ? 4u - mis : len) : 0u;
@@ -1519,7 +1519,7 @@ __global__ __launch_bounds__(256) void k_png_gather(const uint8_t* __restrict__ 
 }
 
 // one thread per IDAT chunk: join "IDAT" and its pieces, compare with the stored CRC
-__global__ __launch_bounds__(256) void k_png_crc_check(const uint8_t* __restrict__ raw,
+__global__ __launch_bounds__(256) void k_png_crc_check(uintptr_t raw,
                                                        const PngCrcChunk* __restrict__ chunks, int nchunks,
                                                        const uint32_t* __restrict__ piece_crc, int* err, CrcOps ops) {
     const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -1531,7 +1531,7 @@ __global__ __launch_bounds__(256) void k_png_crc_check(const uint8_t* __restrict
         const uint32_t op = len == kPngGatherPiece ? ops.piece : crc::x8n(len, ops.x2n);
         c = crc::combine_op(c, piece_crc[2 * p], op);
     }
-    const uint8_t* q = raw + C.crc_at;
+    const IK_GLOBAL uint8_t* q = (const IK_GLOBAL uint8_t*)(raw + (uintptr_t)C.crc_at);
     const uint32_t stored = (uint32_t)q[0] << 24 | (uint32_t)q[1] << 16 | (uint32_t)q[2] << 8 | (uint32_t)q[3];
     if (c != stored) err[C.stream] = 1;
 }
@@ -1554,7 +1554,7 @@ static CrcOps crc_ops() {
     return o;
 }
 
-hipError_t launch_png_gather(const uint8_t* raw, uint8_t* stream, const PngGatherPiece* pieces, int npieces,
+hipError_t launch_png_gather(uintptr_t raw, uint8_t* stream, const PngGatherPiece* pieces, int npieces,
                              uint32_t* piece_crc, hipStream_t s) {
     if (npieces <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_png_gather, dim3((unsigned)npieces), dim3(256), 0, s, raw, stream, pieces, piece_crc,
@@ -1562,11 +1562,82 @@ hipError_t launch_png_gather(const uint8_t* raw, uint8_t* stream, const PngGathe
     return hipGetLastError();
 }
 
-hipError_t launch_png_crc_check(const uint8_t* raw, const PngCrcChunk* chunks, int nchunks, const uint32_t* piece_crc,
+hipError_t launch_png_crc_check(uintptr_t raw, const PngCrcChunk* chunks, int nchunks, const uint32_t* piece_crc,
                                 int* err, hipStream_t s) {
     if (nchunks <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_png_crc_check, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0, s, raw, chunks,
                        nchunks, piece_crc, err, crc_ops());
+    return hipGetLastError();
+}
+
+// ---- chunk walk of device-resident files ------------------------------------------
+// One wave per file (PngWalkRec, ik_png.h).  The chunk chain is serial -- each
+// length gives the next chunk's position -- so every lane follows it with the
+// same (wave-uniform) loads; the lanes then copy a non-IDAT chunk's type, data and
+// CRC into the side area together.  Mirrors parse_png's loop (ik_png_decode.cpp):
+// chunks while 12 bytes remain, stop after IEND; a length past the file's end, a
+// full record table or side area sends the file to the host decoder.
+__global__ __launch_bounds__(64) void k_png_walk(const uint64_t* __restrict__ files, const uint64_t* __restrict__ lens,
+                                                 PngWalkRec* __restrict__ recs, uint8_t* __restrict__ side,
+                                                 int* __restrict__ out_n) {
+    const int f = (int)blockIdx.x, lane = (int)threadIdx.x;
+    const IK_GLOBAL uint8_t* b = (const IK_GLOBAL uint8_t*)(uintptr_t)files[f];
+    const uint64_t n = lens[f];
+    PngWalkRec* R = recs + (size_t)f * kPngWalkRecs;
+    uint8_t* S = side + (size_t)f * kPngWalkSide;
+    uint64_t pos = 8;
+    uint32_t used = 0;
+    int cnt = 0, st = 0;
+    while (pos + 12 <= n) {
+        uint8_t h[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) h[k] = b[pos + k];  // length, type, first 4 data (or CRC) bytes
+        const uint32_t len = (uint32_t)h[0] << 24 | (uint32_t)h[1] << 16 | (uint32_t)h[2] << 8 | h[3];
+        if ((uint64_t)len > n - pos - 12) { st = -3; break; }
+        if (cnt == kPngWalkRecs) { st = -1; break; }
+        const bool idat = h[4] == 'I' && h[5] == 'D' && h[6] == 'A' && h[7] == 'T';
+        uint32_t so = ~0u;
+        if (!idat || !len) {
+            if (used + len + 8 > kPngWalkSide) { st = -2; break; }
+            so = used;
+            for (uint32_t i = (uint32_t)lane; i < len + 8; i += 64) S[so + i] = b[pos + 4 + i];
+            used += (len + 8 + 3) & ~3u;
+        }
+        if (lane == 0) {
+            PngWalkRec r;
+            r.off = pos;
+            r.len = len;
+            r.side = so;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { r.type[k] = h[4 + k]; r.head[k] = h[8 + k]; }
+            R[cnt] = r;
+        }
+        ++cnt;
+        pos += 12 + (uint64_t)len;
+        if (h[4] == 'I' && h[5] == 'E' && h[6] == 'N' && h[7] == 'D') break;
+    }
+    if (lane == 0) out_n[f] = st ? st : cnt;
+}
+
+// the first 64 bytes of each device-resident file (the host sniffs the format
+// and the dimensions from them): one wave per file, a byte per lane
+__global__ __launch_bounds__(64) void k_copy_heads(const uint64_t* __restrict__ files, const uint64_t* __restrict__ lens,
+                                                   uint8_t* __restrict__ out) {
+    const int f = (int)blockIdx.x, t = (int)threadIdx.x;
+    const IK_GLOBAL uint8_t* b = (const IK_GLOBAL uint8_t*)(uintptr_t)files[f];
+    out[64 * (size_t)f + t] = (uint64_t)t < lens[f] ? b[t] : 0;
+}
+
+hipError_t launch_copy_heads(const uint64_t* files, const uint64_t* lens, int n, uint8_t* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_copy_heads, dim3((unsigned)n), dim3(64), 0, s, files, lens, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_png_walk(const uint64_t* files, const uint64_t* lens, int n, PngWalkRec* recs, uint8_t* side,
+                           int* out_n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_png_walk, dim3((unsigned)n), dim3(64), 0, s, files, lens, recs, side, out_n);
     return hipGetLastError();
 }
 

@@ -48,7 +48,7 @@ struct PngJob {
     int idx = -1;                                   // stream index in the batch
     uint32_t w = 0, h = 0;
     int depth = 0, ctype = 0, bpp = 0, ch = 0;       // bytes per pixel, image channels
-    std::vector<std::pair<const uint8_t*, uint32_t>> idat;
+    std::vector<std::pair<uint64_t, uint32_t>> idat;  // non-empty IDAT payloads: (file offset, length)
     size_t zlen = 0;                                 // IDAT payload bytes (zlib stream)
     uint64_t raw_total = 0;
     int rowbytes = 0;
@@ -71,27 +71,73 @@ struct PngJob {
     ik_image* rows = nullptr;
 };
 
-// png 0.18 + image's EXPAND: which streams the GPU path decodes.  Returns false
-// for streams that must go to the host decoder (which also produces png's
-// errors for malformed ones).
-bool parse_png(const uint8_t* b, size_t n, PngJob& J) {
+// One chunk as parse_chunks sees it: its type, its data where the host can read
+// it (null for an IDAT payload of a device-resident file), the file offset of its
+// length field, whether its stored CRC matches (IDAT payload CRCs are checked on
+// the GPU by the gather pass instead), and its first data bytes.
+struct ChunkRef {
+    const uint8_t* type;
+    const uint8_t* data;
+    uint32_t len;
+    uint64_t off;
+    bool crc_ok;
+    const uint8_t* head;
+};
+
+// the chunks of a PNG file in host memory, as png walks them: while 12 bytes
+// remain, stop after IEND; false on a length past the end of the file
+bool host_chunks(const uint8_t* b, size_t n, std::vector<ChunkRef>& out) {
+    out.clear();
     if (n < 8 || std::memcmp(b, "\x89PNG\r\n\x1a\n", 8)) return false;
     size_t pos = 8;
-    bool ihdr = false, trns = false;
-    int interlace = 0;
-    std::vector<uint8_t> plte;
-    const uint8_t* trns_data = nullptr;
-    size_t trns_len = 0;
     while (pos + 12 <= n) {
         const uint32_t len = be32(b + pos);
         if (len > n - pos - 12) return false;
         const uint8_t* type = b + pos + 4;
         const uint8_t* data = b + pos + 8;
-        // (IDAT payload CRCs are checked on the GPU by the upload's gather pass; an
-        // empty IDAT's here)
-        if ((std::memcmp(type, "IDAT", 4) || !len) && png_chunk_crc(type, data, len) != be32(data + len)) return false;
+        const bool idat = !std::memcmp(type, "IDAT", 4) && len;
+        out.push_back(ChunkRef{type, data, len, pos, idat || png_chunk_crc(type, data, len) == be32(data + len), data});
+        pos += 12 + len;
+        if (!std::memcmp(type, "IEND", 4)) break;
+    }
+    return true;
+}
+
+// the chunks of a device-resident file from its walk (k_png_walk): non-IDAT chunk
+// contents from the side area (type + data + CRC)
+bool walk_chunks(const PngWalkRec* R, int nrec, const uint8_t* side, std::vector<ChunkRef>& out) {
+    out.clear();
+    if (nrec < 0) return false;
+    for (int k = 0; k < nrec; ++k) {
+        const PngWalkRec& r = R[k];
+        if (r.side != ~0u) {
+            const uint8_t* t = side + r.side;
+            out.push_back(ChunkRef{t, t + 4, r.len, r.off, png_chunk_crc(t, t + 4, r.len) == be32(t + 4 + r.len), t + 4});
+        } else {
+            out.push_back(ChunkRef{r.type, nullptr, r.len, r.off, true, r.head});
+        }
+    }
+    return true;
+}
+
+// png 0.18 + image's EXPAND: which streams the GPU path decodes.  Returns false
+// for streams that must go to the host decoder (which also produces png's
+// errors for malformed ones).
+bool parse_chunks(const std::vector<ChunkRef>& C, PngJob& J) {
+    bool ihdr = false, trns = false;
+    int interlace = 0;
+    std::vector<uint8_t> plte;
+    const uint8_t* trns_data = nullptr;
+    size_t trns_len = 0;
+    const uint8_t* zh[2] = {nullptr, nullptr};  // first payload bytes of the first two IDATs
+    uint32_t zl0 = 0;
+    for (const ChunkRef& c : C) {
+        const uint8_t* type = c.type;
+        const uint8_t* data = c.data;
+        const uint32_t len = c.len;
+        if (!c.crc_ok) return false;
         if (!std::memcmp(type, "IHDR", 4)) {
-            if (len != 13 || ihdr) return false;
+            if (len != 13 || ihdr || !data) return false;
             J.w = be32(data);
             J.h = be32(data + 4);
             J.depth = data[8];
@@ -99,18 +145,23 @@ bool parse_png(const uint8_t* b, size_t n, PngJob& J) {
             interlace = data[12];
             ihdr = true;
         } else if (!std::memcmp(type, "tRNS", 4)) {
+            if (!data && len) return false;
             trns = true;
             trns_data = data;
             trns_len = len;
         } else if (!std::memcmp(type, "PLTE", 4)) {
+            if (!data && len) return false;
             plte.assign(data, data + len);
         } else if (!std::memcmp(type, "IDAT", 4)) {
-            if (len) J.idat.emplace_back(data, len);
+            if (len) {
+                if (J.idat.empty()) { zh[0] = c.head; zl0 = len; }
+                else if (J.idat.size() == 1) zh[1] = c.head;
+                J.idat.emplace_back(c.off + 8, len);
+            }
             J.zlen += len;
         } else if (!std::memcmp(type, "IEND", 4)) {
             break;
         }
-        pos += 12 + len;
     }
     if (!ihdr || J.idat.empty() || !J.w || !J.h || interlace) return false;
     // 8-bit L / LA / RGB / RGBA as they are; palette (1/2/4/8 bits), gray below 8
@@ -170,10 +221,9 @@ bool parse_png(const uint8_t* b, size_t n, PngJob& J) {
     J.rowbytes = (int)rb;
     J.raw_total = (rb + 1) * J.h;
     // zlib header: CM 8, window <= 32 KiB, FCHECK, no preset dictionary
-    const uint8_t* z0 = J.idat[0].first;
     uint8_t cmf, flg;
-    if (J.idat[0].second >= 2) { cmf = z0[0]; flg = z0[1]; }
-    else if (J.idat.size() > 1) { cmf = z0[0]; flg = J.idat[1].first[0]; }
+    if (zl0 >= 2) { cmf = zh[0][0]; flg = zh[0][1]; }
+    else if (J.idat.size() > 1) { cmf = zh[0][0]; flg = zh[1][0]; }
     else return false;
     if ((cmf & 15) != 8 || (cmf >> 4) > 7 || ((cmf << 8) | flg) % 31 || (flg & 0x20)) return false;
     return true;
@@ -397,6 +447,7 @@ struct PngBatchState {
     int nchunks = 0;
     bool find_launched = false;
     int pinned_streams = 0;
+    bool dev = false;  // the files are the caller's device copies (PngUpload::dev)
     double t0 = 0, t_host = 0;
     ~PngBatchState() { release_area(area); }
 };
@@ -414,10 +465,53 @@ int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Png
     S.t0 = now_ms();
     S.jobs.assign(n, PngJob());
     S.gpu.assign(n, 0);
-    parallel_for(n, 0, [&](int i) {
-        S.jobs[i].idx = i;
-        S.gpu[i] = parse_png(bytes[i], lens[i], S.jobs[i]) && png_gpu_enabled(S.jobs[i].raw_total);
-    });
+    S.dev = up.dev;
+    hipStream_t sc = thread_copy_stream();
+    if (!sc) { S.rc = fail(IK_ERR_DEVICE, "cannot create the PNG copy stream"); return IK_OK; }
+    if (up.dev) {
+        // the files are in device memory: the GPU walks their chunks into pinned
+        // memory (records + the small chunks' contents), the host plans from that
+        const size_t o_rec = 0, o_side = up256(sizeof(PngWalkRec) * kPngWalkRecs * (size_t)n);
+        const size_t o_n = o_side + up256((size_t)kPngWalkSide * n);
+        const size_t o_files = o_n + up256(sizeof(int) * n);
+        const size_t wbytes = o_files + 2 * sizeof(uint64_t) * n;
+        uint8_t* wp = pinned_slot(4, wbytes);
+        void* wd = nullptr;
+        if (!wp || hipHostGetDevicePointer(&wd, wp, 0) != hipSuccess || !wd) {
+            S.rc = fail(IK_ERR_NOMEM, "cannot allocate the PNG chunk-walk area");
+            return IK_OK;
+        }
+        uint8_t* wdev = reinterpret_cast<uint8_t*>(wd);
+        uint64_t* files = reinterpret_cast<uint64_t*>(wp + o_files);
+        for (int i = 0; i < n; ++i) {
+            files[i] = (uint64_t)(uintptr_t)bytes[i];
+            files[n + i] = lens[i];
+        }
+        int* cnt = reinterpret_cast<int*>(wp + o_n);
+        hipError_t e = launch_png_walk(reinterpret_cast<const uint64_t*>(wdev + o_files),
+                                       reinterpret_cast<const uint64_t*>(wdev + o_files) + n, n,
+                                       reinterpret_cast<PngWalkRec*>(wdev + o_rec), wdev + o_side,
+                                       reinterpret_cast<int*>(wdev + o_n), sc);
+        if (e == hipSuccess) e = hipStreamSynchronize(sc);
+        if (e != hipSuccess) { S.rc = hip_fail(e, "PNG chunk walk"); return IK_OK; }
+        const PngWalkRec* recs = reinterpret_cast<const PngWalkRec*>(wp + o_rec);
+        const uint8_t* side = wp + o_side;
+        parallel_for(n, 0, [&](int i) {
+            S.jobs[i].idx = i;
+            thread_local std::vector<ChunkRef> cr;
+            // (a file shorter than the signature, or without it, goes to the host decoder)
+            S.gpu[i] = lens[i] >= 8 && up.heads && !std::memcmp(up.heads[i], "\x89PNG\r\n\x1a\n", 8) &&
+                       walk_chunks(recs + (size_t)i * kPngWalkRecs, cnt[i], side + (size_t)i * kPngWalkSide, cr) &&
+                       parse_chunks(cr, S.jobs[i]) && png_gpu_enabled(S.jobs[i].raw_total);
+        });
+    } else {
+        parallel_for(n, 0, [&](int i) {
+            S.jobs[i].idx = i;
+            thread_local std::vector<ChunkRef> cr;
+            S.gpu[i] = host_chunks(bytes[i], lens[i], cr) && parse_chunks(cr, S.jobs[i]) &&
+                       png_gpu_enabled(S.jobs[i].raw_total);
+        });
+    }
     for (int i = 0; i < n; ++i)
         if (S.gpu[i]) S.J.push_back(&S.jobs[i]);
     const int m = (int)S.J.size();
@@ -430,10 +524,14 @@ int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Png
     std::vector<char> pinned(m, 0);
     for (int k = 0; k < m; ++k) {
         PngJob& j = *S.J[k];
-        j.raw_off = raw;
-        raw += up256(lens[j.idx] + 4);  // (+4: the gather pass reads whole words)
         j.z_off = zs;
         zs += up256(((j.zlen + 3) & ~size_t(3)) + kPad);
+        if (S.dev) {  // the gather pass reads the caller's device copy (raw base 0)
+            j.raw_off = (uint64_t)(uintptr_t)bytes[j.idx];
+            continue;
+        }
+        j.raw_off = raw;
+        raw += up256(lens[j.idx] + 4);  // (+4: the gather pass reads whole words)
         pinned[k] = host_pinned(bytes[j.idx], lens[j.idx]);
         if (!pinned[k]) {
             j.stage_off = stage;
@@ -444,7 +542,7 @@ int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Png
     for (int k = 0; k < m; ++k) {
         const PngJob& j = *S.J[k];
         const uint32_t tail = (uint32_t)((((j.zlen + 3) & ~size_t(3)) + kPad) - j.zlen);
-        png_gather_plan(bytes[j.idx], j.raw_off, j.idat, raw + j.z_off, tail, (uint32_t)k, pieces, chunks);
+        png_gather_plan(j.raw_off, j.idat, raw + j.z_off, tail, (uint32_t)k, pieces, chunks);
     }
     // the block search's chunks: 16 KiB of stream each (chunk 0 starts at the first block)
     const uint64_t cbits = kPngChunkBytes * 8;
@@ -473,8 +571,6 @@ int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Png
         S.rc = fail(IK_ERR_DEVICE, "cannot allocate the PNG upload area (%zu device bytes)", dev_bytes);
         return IK_OK;  // the kernel stage sends every stream to the host decoder
     }
-    hipStream_t sc = thread_copy_stream();
-    if (!sc) { S.rc = fail(IK_ERR_DEVICE, "cannot create the PNG copy stream"); return IK_OK; }
     // the upload goes out under the device's upload gate: concurrent batches take
     // PCIe in turn (ik_runtime.h)
     gate_enter(kGateUpload);
@@ -484,14 +580,14 @@ int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Png
     // its memory; the others through the area's pinned staging (host memcpy only:
     // the CRCs are the GPU's)
     for (int k = 0; k < m; ++k) {
-        if (!pinned[k]) continue;
+        if (S.dev || !pinned[k]) continue;
         const PngJob& j = *S.J[k];
         if (hipMemcpyAsync(A->dev + j.raw_off, bytes[j.idx], lens[j.idx], hipMemcpyHostToDevice, sc) != hipSuccess)
             err = 1;
     }
     std::vector<int> staged;
     for (int k = 0; k < m; ++k)
-        if (!pinned[k]) staged.push_back(k);
+        if (!S.dev && !pinned[k]) staged.push_back(k);
     uint8_t* stg = A->pin + tab_bytes;
     parallel_for((int)staged.size(), 0, [&, sc](int q) {
         const PngJob& j = *S.J[staged[q]];
@@ -521,10 +617,10 @@ int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Png
     hipError_t e = hipMemcpyAsync(A->dev + o_pieces, A->pin, tab_bytes, hipMemcpyHostToDevice, sc);
     if (e == hipSuccess) e = hipMemsetAsync(A->dev + S.o_err, 0, sizeof(int) * m, sc);
     if (e == hipSuccess)
-        e = launch_png_gather(A->dev, A->dev, reinterpret_cast<const PngGatherPiece*>(A->dev + o_pieces),
+        e = launch_png_gather(S.dev ? 0 : (uintptr_t)A->dev, A->dev, reinterpret_cast<const PngGatherPiece*>(A->dev + o_pieces),
                               (int)pieces.size(), reinterpret_cast<uint32_t*>(A->dev + o_pcrc), sc);
     if (e == hipSuccess)
-        e = launch_png_crc_check(A->dev, reinterpret_cast<const PngCrcChunk*>(A->dev + o_chunks), (int)chunks.size(),
+        e = launch_png_crc_check(S.dev ? 0 : (uintptr_t)A->dev, reinterpret_cast<const PngCrcChunk*>(A->dev + o_chunks), (int)chunks.size(),
                                  reinterpret_cast<const uint32_t*>(A->dev + o_pcrc),
                                  reinterpret_cast<int*>(A->dev + S.o_err), sc);
     if (e == hipSuccess && A->ev[2]) e = hipEventRecord(A->ev[2], sc);
@@ -1056,7 +1152,19 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         const int i = host[k];
         thread_local std::vector<uint8_t> px;
         uint32_t w = 0, h = 0, c = 0, dep = 1;
-        int st = decode_png(bytes[i], lens[i], w, h, c, px, &dep);
+        // a device-resident file comes back to host memory for the host decoder
+        std::vector<uint8_t> hb;
+        const uint8_t* src = bytes[i];
+        if (up.dev) {
+            hb.resize(lens[i]);
+            if (lens[i] && hipMemcpy(hb.data(), bytes[i], lens[i], hipMemcpyDeviceToHost) != hipSuccess) {
+                status[i] = hip_fail(hipErrorUnknown, "PNG device input copy");
+                if (msgs) msgs[i] = "PNG device input copy failed";
+                return;
+            }
+            src = hb.data();
+        }
+        int st = decode_png(src, lens[i], w, h, c, px, &dep);
         if (!st) st = dep == 2 ? ik_image_from_host16(reinterpret_cast<const uint16_t*>(px.data()), w, h, c, &outs[i])
                                : ik_image_from_host(px.data(), w, h, c, &outs[i]);
         if (px.capacity() > (128u << 20)) std::vector<uint8_t>().swap(px);

@@ -33,17 +33,18 @@ struct PngCrcChunk {
     uint32_t pad;
 };
 
-// One stream's share of the plan.  file: the PNG file as uploaded (raw_off: where
-// its first byte lands in the raw area); idat: its non-empty IDAT payloads in
-// order (pointers into file); z_off: where its zlib stream starts in the stream
-// area; tail: zero bytes to write after the stream's zlen payload bytes.
-inline void png_gather_plan(const uint8_t* file, uint64_t raw_off,
-                            const std::vector<std::pair<const uint8_t*, uint32_t>>& idat, uint64_t z_off,
+// One stream's share of the plan.  raw_off: where the file's first byte is in the
+// raw address space the gather pass reads (an offset into the upload area, or the
+// file's own device address when the caller's files are already in device
+// memory); idat: its non-empty IDAT payloads in order (file offset, length);
+// z_off: where its zlib stream starts in the stream area; tail: zero bytes to
+// write after the stream's zlen payload bytes.
+inline void png_gather_plan(uint64_t raw_off, const std::vector<std::pair<uint64_t, uint32_t>>& idat, uint64_t z_off,
                             uint32_t tail, uint32_t stream, std::vector<PngGatherPiece>& pieces,
                             std::vector<PngCrcChunk>& chunks) {
     uint64_t dst = z_off;
     for (const auto& seg : idat) {
-        const uint64_t fo = (uint64_t)(seg.first - file);
+        const uint64_t fo = seg.first;
         PngCrcChunk c{};
         c.crc_at = raw_off + fo + seg.second;
         c.piece0 = (uint32_t)pieces.size();

@@ -166,18 +166,18 @@ int ikm_inflate_chunked(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8
 int ikm_gather_check(const uint8_t* file, size_t len, uint64_t z_off, uint32_t tail, uint8_t* stream, size_t cap,
                      int* bad, int bad_cap) {
     auto be32 = [](const uint8_t* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; };
-    std::vector<std::pair<const uint8_t*, uint32_t>> idat;
+    std::vector<std::pair<uint64_t, uint32_t>> idat;
     size_t pos = 8;
     while (pos + 12 <= len) {
         const uint32_t n = be32(file + pos);
         if (n > len - pos - 12) return -1;
-        if (!std::memcmp(file + pos + 4, "IDAT", 4) && n) idat.emplace_back(file + pos + 8, n);
+        if (!std::memcmp(file + pos + 4, "IDAT", 4) && n) idat.emplace_back((uint64_t)(pos + 8), n);
         if (!std::memcmp(file + pos + 4, "IEND", 4)) break;
         pos += 12 + n;
     }
     std::vector<PngGatherPiece> pieces;
     std::vector<PngCrcChunk> chunks;
-    png_gather_plan(file, 0, idat, z_off, tail, 0, pieces, chunks);
+    png_gather_plan(0, idat, z_off, tail, 0, pieces, chunks);
     uint32_t t[1024], x2n[32], level[8];
     for (uint32_t i = 0; i < 256; ++i) t[i] = crc::table_entry(i);
     for (int sl = 1; sl < 4; ++sl)

@@ -305,6 +305,23 @@ int sched_acquire(uint64_t cost) {
     return best;
 }
 
+int sched_acquire_on(int phys, uint64_t cost) {
+    Sched& s = sched();
+    std::lock_guard<std::mutex> lk(s.mu);
+    int best = -1;
+    uint64_t bv = UINT64_MAX;
+    for (size_t i = 0; i < s.devs.size(); ++i) {
+        if (s.devs[i]->phys != phys) continue;
+        const uint64_t v = s.devs[i]->outstanding.load();
+        if (v < bv) { bv = v; best = (int)i; }
+    }
+    if (best >= 0) {
+        s.devs[best]->outstanding += cost;
+        s.devs[best]->jobs += 1;
+    }
+    return best;
+}
+
 void sched_release(int ld, uint64_t cost) {
     Logical& L = *sched().devs[ld];
     L.outstanding -= cost;

@@ -79,6 +79,8 @@ int sched_count();
 int sched_phys(int logical);
 Pool& sched_pool(int logical);
 int sched_acquire(uint64_t cost);
+// the least-loaded logical device on physical device `phys` (-1: none)
+int sched_acquire_on(int phys, uint64_t cost);
 void sched_release(int logical, uint64_t cost);
 void sched_acquire_batch(const uint64_t* costs, uint32_t n, uint32_t* assign);
 void sched_plan(const uint64_t* costs, uint32_t n, uint32_t ndev, const uint64_t* outstanding, uint32_t* assign);
@@ -178,6 +180,11 @@ struct PngUpload {
     const size_t* lens = nullptr;
     int n = 0;
     std::shared_ptr<PngBatchState> st;
+    // dev: bytes[i] are device addresses on the calling thread's device (the
+    // caller's files already in HBM), heads[i] a host copy of each file's first 8
+    // bytes; the upload then walks the chunks on the GPU and gathers from there
+    bool dev = false;
+    const uint8_t* const* heads = nullptr;
     // called by png_decode_finish once the batch's decode rounds are done (or, with
     // IK_FIND_AFTER=resolve, once its resolve pass is queued, with an event
     // recorded after it; null = none): the stage executor launches the next

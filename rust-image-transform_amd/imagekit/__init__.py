@@ -6,11 +6,11 @@ Layout mirrors the crate: `imagekit.transform` (src/transform.rs),
 from . import config, transform
 from .config import DEFAULT_QUALITY, MAX_QUALITY, MIN_QUALITY, ImageFormat, ImageKitConfig
 from .errors import ImageKitError, InvalidArgument, TransformError
-from .transform import DynamicImage, FilterType, PinnedBytes, decode_image, decode_image_batch, encode_image, resize_image, transform_batch, transform_batch_submit
+from .transform import DeviceBytes, DynamicImage, FilterType, PinnedBytes, decode_image, decode_image_batch, encode_image, resize_image, transform_batch, transform_batch_submit, transform_batch_submit_device
 
 __all__ = [
     "config", "transform", "ImageFormat", "ImageKitConfig", "DEFAULT_QUALITY", "MIN_QUALITY",
     "MAX_QUALITY", "ImageKitError", "TransformError", "InvalidArgument", "DynamicImage",
     "FilterType", "decode_image", "decode_image_batch", "encode_image", "resize_image", "transform_batch",
-    "transform_batch_submit", "PinnedBytes",
+    "transform_batch_submit", "transform_batch_submit_device", "PinnedBytes", "DeviceBytes",
 ]

@@ -207,6 +207,34 @@ class PinnedBytes:
             self.ptr = None
 
 
+class DeviceBytes:
+    """Encoded input bytes in device memory (ik_dev_alloc on the current device):
+    request bodies a caller already holds in HBM, for transform_batch_submit_device."""
+
+    __slots__ = ("ptr", "len", "__weakref__")
+
+    def __init__(self, data: bytes):
+        lib = _lib.load()
+        p = ctypes.c_void_p()
+        if lib.ik_dev_alloc(max(1, len(data)), ctypes.byref(p)) != 0:
+            raise TransformError(_lib.last_error())
+        if len(data) and lib.ik_memcpy_h2d(p, bytes(data), len(data)) != 0:
+            lib.ik_dev_free(p)
+            raise TransformError(_lib.last_error())
+        self.ptr, self.len = p.value, len(data)
+
+    def __len__(self) -> int:
+        return self.len
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            try:
+                _lib.load().ik_dev_free(ctypes.c_void_p(self.ptr))
+            except Exception:
+                pass
+            self.ptr = None
+
+
 def _inputs(datas):
     """(keep-alive list, pointer array, length array) for a batch call."""
     keep = [d if isinstance(d, PinnedBytes) else bytes(d) for d in datas]
@@ -293,6 +321,35 @@ def transform_batch_submit(datas, sizes, fmts, qualities, filter: "FilterType" =
     if st:
         raise TransformError(_lib.last_error())
     return PendingBatch((bufs, ptrs, lens, ws, hs, fs, qs), outs, olens, status, ticket.value, n)
+
+
+def transform_batch_submit_device(datas, sizes, fmts, qualities, filter: "FilterType" = None,
+                                  threads: int = 0) -> PendingBatch:
+    """ik_transform_batch_submit_device: as transform_batch_submit, over request
+    bodies already in device memory (DeviceBytes)."""
+    lib = _lib.load()
+    keep = list(datas)
+    n = len(keep)
+    if n == 0:
+        raise InvalidArgument("empty batch")
+    if not all(isinstance(d, DeviceBytes) for d in keep):
+        raise InvalidArgument("transform_batch_submit_device takes DeviceBytes")
+    ptrs = (ctypes.c_void_p * n)(*[d.ptr for d in keep])
+    lens = (ctypes.c_size_t * n)(*[len(d) for d in keep])
+    filt = int(FilterType.Lanczos3 if filter is None else filter)
+    ws = (ctypes.c_int64 * n)(*[-1 if s[0] is None else int(s[0]) for s in sizes])
+    hs = (ctypes.c_int64 * n)(*[-1 if s[1] is None else int(s[1]) for s in sizes])
+    fs = (ctypes.c_int * n)(*[int(f.value if isinstance(f, ImageFormat) else f) for f in fmts])
+    qs = (ctypes.c_int * n)(*[int(q) for q in qualities])
+    outs = (ctypes.c_void_p * n)()
+    olens = (ctypes.c_size_t * n)()
+    status = (ctypes.c_int * n)()
+    ticket = ctypes.c_uint64()
+    st = lib.ik_transform_batch_submit_device(ptrs, lens, n, ws, hs, fs, qs, filt, threads, outs, olens, status,
+                                              ctypes.byref(ticket))
+    if st:
+        raise TransformError(_lib.last_error())
+    return PendingBatch((keep, ptrs, lens, ws, hs, fs, qs), outs, olens, status, ticket.value, n)
 
 
 def resize_image(img: DynamicImage, w: Optional[int], h: Optional[int],

@@ -15,6 +15,11 @@ real sizes (VERDICT r2 "Next" 1).
   src/transform.rs:88), WebP q80, through the same batch path.  Oracle: the
   zune-jpeg 0.4.21 restatement's decode -> resize -> WebPEncodeRGB.
 
+* `value` since round 3: the same PNG files already in device memory (HBM)
+  through ik_transform_batch_submit_device (GPU chunk walk, gather + CRC from the
+  caller's buffers, then the same kernels): bytes == the oracle's, and a mixed
+  batch (palette / tRNS / 16-bit / JPEG / WebP / corrupt) == the host-input path.
+
 Both assert that no stream went to a host decoder (ik_png_counters /
 ik_jpeg_counters), so the HIP path is what was compared."""
 import ctypes
@@ -25,7 +30,7 @@ import pytest
 from PIL import Image
 
 import ikutil
-from imagekit import ImageFormat, _lib, transform_batch_submit
+from imagekit import DeviceBytes, ImageFormat, _lib, transform_batch, transform_batch_submit, transform_batch_submit_device
 
 pytestmark = pytest.mark.gpu
 
@@ -112,3 +117,99 @@ def test_loadtest_mix_batch_path_equals_oracle(ik, oracle, loadtest_sources):
         px = oracle.jpeg_decode(src, mode=1)  # zune-jpeg 0.4.21 restatement (the reference's decoder)
         want, _ = oracle.transform(px, w, h, LANCZOS3, WEBP, 80)
         assert got[i] == want, f"request {i} ({w}x{h}, {'RSTn' if i % 2 == 0 else 'no RSTn'}): bytes differ"
+
+
+def test_headline_device_inputs_equal_oracle(ik, oracle, headline_frames):
+    """bench.py's `value`: the PNG files already in HBM (DeviceBytes), two batches
+    in flight through ik_transform_batch_submit_device."""
+    frames, pngs = headline_frames
+    n = len(pngs)
+    dev = [DeviceBytes(p) for p in pngs]
+    g0, h0 = _png_counts(ik)
+    pa = transform_batch_submit_device(dev, [(512, 512)] * n, [WEBP] * n, [80] * n, filter=TRIANGLE, threads=16)
+    pb = transform_batch_submit_device(dev[::-1], [(512, 512)] * n, [WEBP] * n, [80] * n, filter=TRIANGLE,
+                                       threads=16)
+    ga, gb = pa.wait(), pb.wait()
+    g1, h1 = _png_counts(ik)
+    assert (g1 - g0, h1 - h0) == (2 * n, 0), "every device-resident 4096^2 stream must decode on the GPU"
+    for i in range(n):
+        want, _ = oracle.transform(frames[i], 512, 512, TRIANGLE, WEBP, 80)
+        assert ga[i] == want, f"frame {i}: device-input batch bytes differ from the oracle's transform"
+        assert gb[n - 1 - i] == want, f"frame {i} (second batch): bytes differ"
+
+
+def _mixed_inputs():
+    """Small inputs of every kind the device entry must route: RGBA / RGB / gray PNG
+    (GPU), palette + tRNS and 4-bit gray PNG (GPU EXPAND), 16-bit and interlaced
+    PNG (host decoder after a copy back), JPEG and WebP (host parse), a PNG with a
+    corrupt IDAT CRC and one truncated (png's errors), garbage (unknown format)."""
+    out = []
+    rgba = ikutil.synth(700, 500, 4, seed=11, pattern="S")
+    for mode, arr in (("RGBA", rgba), ("RGB", rgba[..., :3]), ("L", rgba[..., 0])):
+        b = io.BytesIO()
+        Image.fromarray(np.ascontiguousarray(arr), mode).save(b, format="PNG")
+        out.append(b.getvalue())
+    pal = Image.fromarray(rgba[..., :3]).convert("P", palette=Image.Palette.ADAPTIVE, colors=200)
+    b = io.BytesIO()
+    pal.save(b, format="PNG", transparency=3)
+    out.append(b.getvalue())
+    b = io.BytesIO()
+    Image.fromarray(rgba[..., 1]).convert("L").quantize(16).save(b, format="PNG", bits=4)
+    out.append(b.getvalue())
+    b = io.BytesIO()
+    Image.fromarray((rgba[..., 0].astype(np.uint16) * 257)).save(b, format="PNG")
+    out.append(b.getvalue())
+    b = io.BytesIO()
+    Image.fromarray(rgba[..., :3]).save(b, format="PNG", interlace=1)
+    out.append(b.getvalue())
+    b = io.BytesIO()
+    Image.fromarray(rgba[..., :3]).save(b, format="JPEG", quality=85)
+    out.append(b.getvalue())
+    b = io.BytesIO()
+    Image.fromarray(rgba[..., :3]).save(b, format="WEBP", quality=80)
+    out.append(b.getvalue())
+    bad = bytearray(out[0])
+    k = bytes(bad).find(b"IDAT")
+    bad[k + 4 + 100] ^= 0x55  # a payload byte: the IDAT CRC no longer matches
+    out.append(bytes(bad))
+    out.append(out[1][: len(out[1]) // 2])
+    out.append(b"\x00" * 64)
+    return out
+
+
+def test_device_inputs_mixed_batch_equals_host_inputs(ik):
+    datas = _mixed_inputs()
+    n = len(datas)
+    sizes = [(320, None)] * n
+    fmts = [WEBP] * n
+    qs = [80] * n
+    # the host-input batch path, item by item (its errors are the reference's)
+    want, werr = [], []
+    for d in datas:
+        try:
+            want.append(transform_batch([d], [(320, None)], [WEBP], [80], filter=LANCZOS3)[0])
+            werr.append(None)
+        except Exception as e:  # noqa: BLE001
+            want.append(None)
+            werr.append(str(e))
+    dev = [DeviceBytes(d) for d in datas]
+    p = transform_batch_submit_device(dev, sizes, fmts, qs, filter=LANCZOS3)
+    try:
+        got = p.wait()
+        err = None
+    except Exception as e:  # noqa: BLE001
+        got, err = None, str(e)
+    st = p._status
+    assert err is not None, "the batch holds failing items"
+    for i in range(n):
+        if werr[i] is None:
+            assert st[i] == 0, f"item {i}: failed on the device path, not on the host path"
+        else:
+            assert st[i] != 0, f"item {i}: succeeded on the device path but not on the host path ({werr[i]})"
+    # successful items: identical bytes (rerun without the failing items to read them)
+    ok = [i for i in range(n) if werr[i] is None]
+    p2 = transform_batch_submit_device([dev[i] for i in ok], [sizes[i] for i in ok], [fmts[i] for i in ok],
+                                       [qs[i] for i in ok], filter=LANCZOS3)
+    got2 = p2.wait()
+    for j, i in enumerate(ok):
+        assert got2[j] == want[i], f"item {i}: device-input bytes differ from the host-input path"
