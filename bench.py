@@ -74,6 +74,10 @@ def parse():
     ap.add_argument("--out", type=int, default=512)
     ap.add_argument("--filter", default="triangle", choices=sorted(FILTERS))
     ap.add_argument("--quality", type=int, default=80)
+    ap.add_argument("--format", default="webp", choices=sorted(FORMATS), help="output format (encode_image)")
+    ap.add_argument("--source", default="png", choices=["png", "jpeg-rst", "jpeg"],
+                    help="input container: PNG (configs[1]), or JPEG q90 4:2:0 with a restart marker per MCU "
+                         "row / without (configs[2]'s sources)")
     ap.add_argument("--distinct", type=int, default=4, help="distinct PNG frames per rank (tiled over the batch)")
     ap.add_argument("--threads", type=int, default=32, help="host threads per GPU (stated budget)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of each cpu_baseline sample")
@@ -163,6 +167,18 @@ def make_pngs(frames):
     return out
 
 
+def make_jpegs(frames, rst):
+    from PIL import Image
+    out = []
+    for im in frames:
+        b = io.BytesIO()
+        kw = {"restart_marker_rows": 1} if rst else {}
+        Image.fromarray(np.ascontiguousarray(im[..., :3]), "RGB").save(b, format="JPEG", quality=90, subsampling=2,
+                                                                     **kw)
+        out.append(b.getvalue())
+    return out
+
+
 _CPU = {}  # the oracle and the inputs, inherited by the forked cpu_baseline workers
 
 
@@ -172,8 +188,13 @@ def _cpu_one(k):
     L, pngs, O, f, fmt, q = (_CPU[x] for x in ("L", "pngs", "O", "f", "fmt", "q"))
     data = pngs[k % len(pngs)]
     px = ikutil.u8p()
-    w, h, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
-    n = L.iko_png_decode(data, len(data), ctypes.byref(px), ctypes.byref(w), ctypes.byref(h), ctypes.byref(c))
+    if data[:4] == b"\x89PNG":
+        w, h, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        n = L.iko_png_decode(data, len(data), ctypes.byref(px), ctypes.byref(w), ctypes.byref(h), ctypes.byref(c))
+    else:  # JPEG: the zune-jpeg 0.4.21 restatement (the reference's decoder)
+        w, h, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        n = L.iko_jpeg_decode(data, len(data), 1, ctypes.byref(px), ctypes.byref(w), ctypes.byref(h), ctypes.byref(c))
+        n = 1 if n == 0 else -abs(n) - 1
     assert n > 0, n
     out = ikutil.u8p()
     ow, oh = ctypes.c_uint32(), ctypes.c_uint32()
@@ -202,7 +223,11 @@ def cpu_baseline(args, pngs):
     L.iko_png_decode.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ikutil.u8p),
                                  ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                                  ctypes.POINTER(ctypes.c_uint32)]
-    _CPU.update(L=L, pngs=pngs, O=args.out, f=FILTERS[args.filter], fmt=FORMATS["webp"], q=args.quality)
+    L.iko_jpeg_decode.restype = ctypes.c_int
+    L.iko_jpeg_decode.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ikutil.u8p),
+                                  ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                  ctypes.POINTER(ctypes.c_int)]
+    _CPU.update(L=L, pngs=pngs, O=args.out, f=FILTERS[args.filter], fmt=FORMATS[args.format], q=args.quality)
     _cpu_one(0)
     t0 = time.perf_counter()
     _cpu_one(1)
@@ -235,9 +260,12 @@ def cpu_baseline(args, pngs):
         "cores_basis": "effective cores = min(nproc, cgroup CPU quota, affinity); the job cannot use more",
         "nproc": nproc,
         "kind": "port",
-        "sample": f"{done} x {S}x{S} RGBA8 PNG (host memory) -> oracle PNG decode (CRC, libdeflate inflate, "
-                  f"unfilter) -> image 0.25.8 resize {O}x{O} {args.filter} -> libwebp q{args.quality}; one image per "
-                  f"worker process at a time, {eff} processes on {eff} effective cores, {wn:.1f}s wall",
+        "sample": (f"{done} x {S}x{S} RGBA8 PNG (host memory) -> oracle PNG decode (CRC, libdeflate inflate, "
+                   f"unfilter)" if args.source == "png" else
+                   f"{done} x {S}x{S} JPEG q90 4:2:0 ({args.source}, host memory) -> oracle zune-jpeg restatement "
+                   f"decode") + f" -> image 0.25.8 resize {O}x{O} {args.filter} -> {args.format} q{args.quality} "
+                  f"({'libwebp' if args.format == 'webp' else 'restated image JpegEncoder' if args.format == 'jpeg' else 'libavif/aom'}); "
+                  f"one image per worker process at a time, {eff} processes on {eff} effective cores, {wn:.1f}s wall",
         "value_1core": v1,
         "sample_1core": f"{n1} images on 1 thread, {w1:.1f}s wall",
         # not a measurement: the 1-core rate times the host's physical cores, what
@@ -297,7 +325,7 @@ def main():
     # (IK_LIBWEBP / IK_LIBAVIF, else the system sonames): name the copies used here
     ikutil.use_pillow_codecs()
     frames = [ikutil.synth(S, S, 4, seed=sd, pattern="S") for sd in shard_seeds(rank, args.distinct)]
-    pngs = make_pngs(frames)
+    pngs = make_pngs(frames) if args.source == "png" else make_jpegs(frames, args.source == "jpeg-rst")
     # the CPU leg first: its worker pools fork, and nothing may have touched the GPU yet
     cpu = cpu_baseline(args, pngs) if rank == 0 and world == 1 and not args.no_cpu_baseline else None
     dist = None
@@ -317,8 +345,12 @@ def main():
     # them: the upload DMAs them in place (--pageable: ordinary Python bytes)
     inputs = pngs if args.pageable else [PinnedBytes(p) for p in pngs]
     reqs = [inputs[i % len(inputs)] for i in range(B)]
-    # the headline's inputs: every request its own device allocation in HBM
-    dreqs = [DeviceBytes(pngs[i % len(pngs)]) for i in range(B)]
+    # the headline's inputs: every request its own device allocation in HBM (PNG:
+    # the GPU walks and gathers them in place).  JPEG sources are parsed on the host
+    # (markers, restart scan), so they stay in page-locked host memory.
+    dreqs = [DeviceBytes(pngs[i % len(pngs)]) for i in range(B)] if args.source == "png" else reqs
+    magic = {"webp": lambda r: r[:4] == b"RIFF", "jpeg": lambda r: r[:2] == b"\xff\xd8",
+             "avif": lambda r: r[4:8] == b"ftyp"}[args.format]
 
     def barrier():
         if dist is not None:
@@ -338,7 +370,7 @@ def main():
 
     def submit(rq):
         fn = transform_batch_submit_device if isinstance(rq[0], DeviceBytes) else transform_batch_submit
-        return fn(rq, [(O, O)] * B, [FORMATS["webp"]] * B, [args.quality] * B, filter=f, threads=args.threads)
+        return fn(rq, [(O, O)] * B, [FORMATS[args.format]] * B, [args.quality] * B, filter=f, threads=args.threads)
 
     def run_pipelined(nsteps, rq=None, depth=None):
         """nsteps batches with up to `depth` in flight (upload of one under the
@@ -359,14 +391,14 @@ def main():
     def run_blocking(nsteps):
         out = None
         for _ in range(nsteps):
-            out = transform_batch(reqs, [(O, O)] * B, [FORMATS["webp"]] * B, [args.quality] * B, filter=f,
+            out = transform_batch(reqs, [(O, O)] * B, [FORMATS[args.format]] * B, [args.quality] * B, filter=f,
                                   threads=args.threads)
             note_timing()
         return out
 
     # PCIe-inclusive leg: the same steps from host memory (reported beside value)
     pcie = {}
-    if not args.no_pcie_leg:
+    if not args.no_pcie_leg and args.source == "png":
         run_pipelined(args.warmup, rq=reqs) if args.pipeline else run_blocking(args.warmup)
         barrier()
         t1 = time.perf_counter()
@@ -374,7 +406,7 @@ def main():
         torch.cuda.synchronize()
         te = reduce_max(time.perf_counter() - t1, dist, dev)
         barrier()
-        assert all(r is not None and r[:4] == b"RIFF" for r in r1)
+        assert all(r is not None and magic(r) for r in r1)
         pst = np.mean(np.array(stage_ms), axis=0)
         stage_ms.clear()
         pcie = {"value": round(aggregate_mpix(world, B * args.steps, S, te), 2), "unit": "MPix/s",
@@ -396,7 +428,7 @@ def main():
     elapsed = time.perf_counter() - t0
     barrier()
     elapsed = reduce_max(elapsed, dist, dev)
-    assert all(r is not None and r[:4] == b"RIFF" for r in res)
+    assert all(r is not None and magic(r) for r in res)
     cnt1 = (ctypes.c_ulonglong * 2)()
     lib.ik_png_counters(cnt1)
     gpu_streams, host_streams = cnt1[0] - cnt0[0], cnt1[1] - cnt0[1]
@@ -424,8 +456,10 @@ def main():
         "k_png_resolve": (png_stages["resolve"], nd * (2 * raw + 4 * S * S)),
         "k_png_unfilter": (png_stages["unfilter"], nd * (2 * 4 * S * S)),
     }
-    dom = max(kern, key=lambda k: kern[k][0])
-    dms, dbytes = kern[dom]
+    if args.source != "png":
+        kern = {}  # (the PNG stage times do not apply; the resize kernel's line is roofline_resize)
+    dom = max(kern, key=lambda k: kern[k][0]) if kern else None
+    dms, dbytes = kern[dom] if dom else (1.0, 0)
     traffic_png = None  # PMC HBM bytes of that kernel per 64-frame launch (tools/pmc_png_traffic.sh)
     pmcp = os.path.join(ROOT, "profiles", "pmc_png.json")
     if os.path.exists(pmcp) and B == 64 and S == 4096:
@@ -468,7 +502,7 @@ def main():
                 src[i].copy_(src[i % len(frames)])
         torch.cuda.synchronize()
         pipe = ctypes.c_void_p()
-        if lib.ik_pipeline_create(S, S, 4, O, O, f, FORMATS["webp"], args.quality, HB, args.threads,
+        if lib.ik_pipeline_create(S, S, 4, O, O, f, FORMATS[args.format], args.quality, HB, args.threads,
                                   ctypes.byref(pipe)):
             raise SystemExit(f"pipeline: {_lib.last_error()}")
         cap = HB * O * O * 4 + (1 << 20)
@@ -500,8 +534,8 @@ def main():
         lib.ik_pipeline_destroy(pipe)
         kmm = np.mean(np.array(km), axis=0)
         rb = HB * (4 * S * S + 4 * O * O)
-        hbm = {"workload": f"{S}x{S} RGBA8 frames already in HBM -> resize {O}x{O} {args.filter} -> WebP q{args.quality} "
-                           "(libwebp), bytes to host; two batches in flight",
+        hbm = {"workload": f"{S}x{S} RGBA8 frames already in HBM -> resize {O}x{O} {args.filter} -> {args.format} "
+                           f"q{args.quality}, bytes to host; two batches in flight",
                "value": round(aggregate_mpix(world, HB * args.hbm_steps, S, te), 2), "unit": "MPix/s",
                "ms_per_step": round(te / args.hbm_steps * 1e3, 3), "batch_per_gpu": HB,
                "resize_ms": round(float(kmm[0]), 4), "colour_ms": round(float(kmm[1]), 4),
@@ -542,6 +576,19 @@ def main():
                    "bytes_per_source_image": sum(len(p) for p in jp) // 2,
                    "value": round(aggregate_mpix(world, n, S, te), 2), "unit": "MPix/s"}
 
+    if args.source != "png" and roof_resize:
+        roof = dict(roof_resize, note="JPEG sources: the resize kernel's line (its HIP-event time in the "
+                                      "hbm_resident leg); the JPEG decode kernels are in the rocprof stats")
+    src_desc = ({"png": "PNG (zlib level 6), resident in HBM (one device allocation per request) -> "
+                        "ik_transform_batch_submit_device: decode_image (GPU chunk walk, gather + CRC, inflate + "
+                        "unfilter)",
+                 "jpeg-rst": "JPEG q90 4:2:0 with a restart marker per MCU row, in page-locked host memory -> "
+                             "ik_transform_batch_submit: decode_image (GPU entropy decoding per restart interval, "
+                             "IDCT, upsampling, colour)",
+                 "jpeg": "JPEG q90 4:2:0 without restart markers, in page-locked host memory -> "
+                         "ik_transform_batch_submit: decode_image (GPU self-synchronising entropy decoding, IDCT, "
+                         "upsampling, colour)"}[args.source] if args.pipeline else "host memory -> ik_transform_batch")
+    coder = {"webp": "libwebp", "jpeg": "GPU FDCT + Huffman", "avif": "libavif/aom"}[args.format]
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -557,14 +604,14 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": f"{S}x{S} RGBA8 synthetic frames as PNG (zlib level 6), resident in HBM (one device "
-                            f"allocation per request) -> ik_transform_batch_submit_device: decode_image (GPU chunk "
-                            f"walk, gather + CRC, inflate + unfilter) -> resize_image {O}x{O} ({args.filter}) -> "
-                            f"encode_image webp q{args.quality} (libwebp) -> WebP bytes in host memory",
+                "workload": f"{S}x{S} RGBA8 synthetic frames as {src_desc} -> resize_image {O}x{O} "
+                            f"({args.filter}) -> encode_image {args.format} q{args.quality} ({coder}) -> encoded bytes "
+                            f"in host memory",
+                "source": args.source,
                 "batch_per_gpu": B, "inflight": args.inflight if args.pipeline else 1,
-                "inputs": "device memory (HBM), resident before the timed region" if args.pipeline else
+                "inputs": "device memory (HBM), resident before the timed region" if args.pipeline and args.source == "png" else
                           ("pageable host memory" if args.pageable else "page-locked host memory (ik_host_alloc)"),
-                "inproc_devices": args.inproc_devices, "filter": args.filter, "format": "webp", "quality": args.quality,
+                "inproc_devices": args.inproc_devices, "filter": args.filter, "format": args.format, "quality": args.quality,
                 "host_threads_per_gpu": args.threads, "png_bytes_per_image": in_bytes,
                 "webp_bytes_per_image": out_bytes,
                 "libwebp": "%d.%d.%d" % (lib.ik_libwebp_version() >> 16, (lib.ik_libwebp_version() >> 8) & 255,

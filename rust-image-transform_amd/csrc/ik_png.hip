@@ -1646,7 +1646,8 @@ hipError_t launch_png_walk(const uint64_t* files, const uint64_t* lens, int n, P
 // src/transform.rs:31): one thread per pixel of the unfiltered rows.  Palette
 // index -> PLTE colour (an index past the palette: black) with tRNS alpha (255
 // past tRNS); gray of 1/2/4 bits -> v * 255 / (2^d - 1); a gray level or RGB
-// triple equal to the tRNS key -> alpha 0, else 255.
+// triple equal to the tRNS key -> alpha 0, else 255.  16-bit samples (L16 / La16
+// / Rgb16 / Rgba16) -> native-endian u16, tRNS alpha 0 / 65535.
 __global__ __launch_bounds__(256) void k_png_px(PngPxDev P) {
     __shared__ uint32_t pal[256];
     if (P.ctype == 3) pal[threadIdx.x] = P.pal[threadIdx.x];
@@ -1654,6 +1655,20 @@ __global__ __launch_bounds__(256) void k_png_px(PngPxDev P) {
     const int x = (int)(blockIdx.x * 256 + threadIdx.x), y = (int)blockIdx.y;
     if (x >= P.w) return;
     const uint8_t* r = P.src + (size_t)y * P.sp;
+    if (P.depth == 16) {  // big-endian samples -> native u16; a tRNS key match -> alpha 0, else 65535
+        const int spp = P.ctype == 0 ? 1 : P.ctype == 2 ? 3 : P.ctype == 4 ? 2 : 4;
+        const uint8_t* s = r + (size_t)2 * spp * x;
+        uint16_t* o16 = reinterpret_cast<uint16_t*>(P.dst + (size_t)y * P.dp) + (size_t)x * P.out_c;
+        bool key = P.out_c > spp;
+#pragma unroll 4
+        for (int k = 0; k < spp; ++k) {
+            const int v = (int)s[2 * k] << 8 | s[2 * k + 1];
+            o16[k] = (uint16_t)v;
+            key = key && v == (P.ctype == 0 ? P.key : P.key_rgb[k]);
+        }
+        if (P.out_c > spp) o16[spp] = key ? 0 : 65535;
+        return;
+    }
     uint8_t* o = P.dst + (size_t)y * P.dp + (size_t)x * P.out_c;
     if (P.ctype == 2) {  // RGB + tRNS key
         const int R = r[3 * x], G = r[3 * x + 1], B = r[3 * x + 2];

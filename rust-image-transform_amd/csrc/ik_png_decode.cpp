@@ -176,13 +176,15 @@ bool parse_chunks(const std::vector<ChunkRef>& C, PngJob& J) {
     default: return false;
     }
     const bool low = J.depth == 1 || J.depth == 2 || J.depth == 4;
-    if (!(J.depth == 8 || (low && (J.ctype == 0 || J.ctype == 3)))) return false;
+    const bool d16 = J.depth == 16;
+    if (!(J.depth == 8 || (d16 && J.ctype != 3) || (low && (J.ctype == 0 || J.ctype == 3)))) return false;
     if (trns && J.ctype != 0 && J.ctype != 2 && J.ctype != 3) return false;  // (png rejects those)
     J.ch = spp;
     const uint64_t bits_pp = (uint64_t)spp * J.depth;
     J.bpp = (int)((bits_pp + 7) / 8);
     const uint64_t rb = ((uint64_t)J.w * bits_pp + 7) / 8;
-    J.expand = J.ctype == 3 || low || trns;
+    // (16-bit: the big-endian samples become native u16 in k_png_px, with tRNS alpha 0 / 65535)
+    J.expand = J.ctype == 3 || low || trns || d16;
     J.out_c = spp;
     if (J.expand) {
         PngPxDev& X = J.px;
@@ -204,8 +206,8 @@ bool parse_chunks(const std::vector<ChunkRef>& C, PngJob& J) {
             J.out_c = trns_len >= 2 ? 2 : 1;
             if (trns_len >= 2) X.key = (int)((trns_data[0] << 8) | trns_data[1]);
             X.scale = J.depth == 1 ? 255 : J.depth == 2 ? 85 : J.depth == 4 ? 17 : 1;
-        } else {  // RGB + tRNS
-            if (trns_len < 6) { J.expand = false; }
+        } else if (J.ctype == 2) {  // RGB + tRNS
+            if (trns_len < 6) { J.expand = d16; }
             else {
                 J.out_c = 4;
                 X.key_rgb[0] = (trns_data[0] << 8) | trns_data[1];
@@ -216,8 +218,8 @@ bool parse_chunks(const std::vector<ChunkRef>& C, PngJob& J) {
         }
         X.out_c = J.out_c;
     }
-    // image's default limit: 512 MiB of decoded (expanded) pixels
-    if ((uint64_t)J.w * J.h * J.out_c > (512ull << 20) || rb > 0x7FFFFFF0ull) return false;
+    // image's default limit: 512 MiB of decoded (expanded) pixel bytes
+    if ((uint64_t)J.w * J.h * J.out_c * (d16 ? 2 : 1) > (512ull << 20) || rb > 0x7FFFFFF0ull) return false;
     J.rowbytes = (int)rb;
     J.raw_total = (rb + 1) * J.h;
     // zlib header: CM 8, window <= 32 KiB, FCHECK, no preset dictionary
@@ -944,7 +946,8 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             pngplan::offsets(j.lanes, ob, &tot);
             if (tot != j.raw_total) { reject(j, "image data length"); continue; }  // png's error
             if (j.expand) {  // unfiltered rows in a row image, then k_png_px into the output image
-                if (alloc_image((uint32_t)j.rowbytes, j.h, 1, &j.rows) || alloc_image(j.w, j.h, (uint32_t)j.out_c, &j.img)) {
+                if (alloc_image((uint32_t)j.rowbytes, j.h, 1, &j.rows) ||
+                alloc_image(j.w, j.h, (uint32_t)j.out_c, &j.img, j.depth == 16 ? 2 : 1)) {
                     reject(j, "image allocation");
                     continue;
                 }

@@ -134,3 +134,27 @@ def test_limits_count_decoded_bytes(ik):
     bad = hdr16 + chunk(b"IDAT", zlib.compress(b"\x00" * 64)) + chunk(b"IEND", b"")
     with pytest.raises(TransformError, match="Limits"):
         decode_image(bad)
+
+
+@pytest.mark.parametrize("c,trns", [(1, None), (2, None), (3, None), (4, None), (1, "key"), (3, "key")])
+def test_16bit_decodes_on_the_gpu(ik, c, trns):
+    """16-bit streams above the GPU threshold go through the GPU inflate + unfilter
+    and k_png_px (byte order, tRNS alpha), not the host decoder."""
+    import ctypes
+    img = synth16(640, 480, c, seed=40 + c)
+    key = None
+    if trns:
+        key = tuple(int(v) for v in img[7, 9])
+        img[100:140, :] = key
+    c0 = (ctypes.c_ulonglong * 2)()
+    ik.ik_png_counters(c0)
+    d, _ = decode_image(png16(img, trns=key))
+    c1 = (ctypes.c_ulonglong * 2)()
+    ik.ik_png_counters(c1)
+    assert (c1[0] - c0[0], c1[1] - c0[1]) == (1, 0), "the 16-bit stream must decode on the GPU"
+    got = d.to_array()
+    assert d.depth == 2
+    np.testing.assert_array_equal(got[..., :c], img)
+    if key is not None:
+        want_a = np.where((img == np.array(key, np.uint16)).all(-1), 0, 65535)
+        np.testing.assert_array_equal(got[..., c], want_a)
