@@ -34,6 +34,7 @@
 #include "ik_inflate.h"
 #include "ik_internal.h"
 #include "ik_png.h"
+#include "ik_unfilter.h"
 
 namespace ik {
 
@@ -1087,10 +1088,22 @@ struct FtMask {
         : sub(ft == 1 ? ~0u : 0u), up(ft == 2 ? ~0u : 0u), avg(ft == 3 ? ~0u : 0u), paeth(ft == 4 ? ~0u : 0u) {}
 };
 
-template <int BPP>
+template <int BPP, bool SWAR = false>
 __device__ __forceinline__ void unfilter_chunk(const u32x4& rawv, const uint32_t (&up)[4], const uint32_t (&prevup)[4],
                                                const uint32_t (&prevcur)[4], const FtMask& fm, uint32_t (&o)[4]) {
     const uint32_t raw[4] = {rawv.x, rawv.y, rawv.z, rawv.w};
+    if constexpr (SWAR && (BPP == 4 || BPP == 8)) {
+        // a word at a time (ik_unfilter.h): the word BPP bytes back is one word earlier
+        // (RGBA8) or two (8-byte pixels), so the chunk's chain is 4 or 2 words long
+        constexpr int K = BPP / 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t a = k >= K ? o[k - K] : prevcur[4 + k - K];
+            const uint32_t c = k >= K ? up[k - K] : prevup[4 + k - K];
+            o[k] = unfilter_word(raw[k], a, up[k], c, fm.sub, fm.up, fm.avg, fm.paeth);
+        }
+        return;
+    }
     o[0] = o[1] = o[2] = o[3] = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -1108,7 +1121,7 @@ __device__ __forceinline__ void unfilter_chunk(const u32x4& rawv, const uint32_t
     }
 }
 
-template <int BPP>
+template <int BPP, bool SWAR>
 __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngImgDev* imgs, const int2* groups,
                                                                       const int* prog_base, unsigned* prog,
                                                                       unsigned* ticket) {
@@ -1224,7 +1237,7 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngI
                         for (int k = 0; k < 4; ++k) { prevup[k] = 0; prevcur[k] = 0; }
                     }
                     uint32_t o[4];
-                    unfilter_chunk<BPP>(rcur[t], up, prevup, prevcur, fm, o);
+                    unfilter_chunk<BPP, SWAR>(rcur[t], up, prevup, prevcur, fm, o);
 #pragma unroll
                     for (int k = 0; k < 4; ++k) cur[k] = o[k];
                     const u32x4 ov = {o[0], o[1], o[2], o[3]};
@@ -1755,14 +1768,19 @@ hipError_t launch_png_unfilter(const PngImgDev* imgs, const int2* groups, int ng
 #undef IK_UNF8
         return hipGetLastError();
     }
-#define IK_UNF(B) hipLaunchKernelGGL(k_png_unfilter<B>, grid, block, 0, s, imgs, groups, prog_base, prog, ticket)
+    // IK_PNG_UNF_SWAR=0: the byte-at-a-time chunk for 4- and 8-byte pixels too (A/B)
+    static const bool swar = [] {
+        const char* e = getenv("IK_PNG_UNF_SWAR");
+        return !(e && !strcmp(e, "0"));
+    }();
+#define IK_UNF(B, W) hipLaunchKernelGGL((k_png_unfilter<B, W>), grid, block, 0, s, imgs, groups, prog_base, prog, ticket)
     switch (bpp) {
-    case 1: IK_UNF(1); break;
-    case 2: IK_UNF(2); break;
-    case 3: IK_UNF(3); break;
-    case 4: IK_UNF(4); break;
-    case 6: IK_UNF(6); break;
-    case 8: IK_UNF(8); break;
+    case 1: IK_UNF(1, false); break;
+    case 2: IK_UNF(2, false); break;
+    case 3: IK_UNF(3, false); break;
+    case 4: if (swar) IK_UNF(4, true); else IK_UNF(4, false); break;
+    case 6: IK_UNF(6, false); break;
+    case 8: if (swar) IK_UNF(8, true); else IK_UNF(8, false); break;
     default: return hipErrorInvalidValue;
     }
 #undef IK_UNF

@@ -14,6 +14,7 @@
 #include "ik_inflate.h"
 #include "ik_png_gather.h"
 #include "ik_png_plan.h"
+#include "ik_unfilter.h"
 
 using namespace ik;
 
@@ -270,3 +271,47 @@ int ikm_plausible_dynamic(const uint8_t* z, size_t zlen, uint64_t bit) {
 }
 
 }  // extern "C"
+
+// unfilter_word (ik_unfilter.h, the GPU's word-at-a-time row filters for 4- and
+// 8-byte pixels) against png's byte-wise definition, exhaustively: every (a, b, c)
+// byte triple under every filter type, four different triples per word (so a
+// carry or borrow between bytes shows up), raw bytes from a fixed sequence.
+// Returns the number of mismatching bytes.
+extern "C" long ikm_unfilter_word_check(void) {
+    auto ref = [](int ft, int x, int a, int b, int c) {
+        int p = 0;
+        if (ft == 1) p = a;
+        else if (ft == 2) p = b;
+        else if (ft == 3) p = (a + b) >> 1;
+        else if (ft == 4) {
+            const int pa = std::abs(b - c), pb = std::abs(a - c), pc = std::abs(a + b - 2 * c);
+            p = (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
+        }
+        return (x + p) & 255;
+    };
+    long bad = 0;
+    uint32_t seq = 12345u;
+    for (int ft = 0; ft <= 4; ++ft) {
+        const uint32_t ms = ft == 1 ? ~0u : 0u, mu = ft == 2 ? ~0u : 0u, mv = ft == 3 ? ~0u : 0u, mp = ft == 4 ? ~0u : 0u;
+        for (uint32_t t = 0; t < (1u << 24); t += 4) {
+            uint32_t A = 0, B = 0, C = 0, X = 0;
+            int av[4], bv[4], cv[4], xv[4];
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t q = (t + (uint32_t)k * 0x40404u + (uint32_t)k) & 0xFFFFFFu;  // a different triple per byte
+                av[k] = (int)(q & 255u);
+                bv[k] = (int)((q >> 8) & 255u);
+                cv[k] = (int)((q >> 16) & 255u);
+                seq = seq * 1103515245u + 12345u;
+                xv[k] = (int)((seq >> 16) & 255u);
+                A |= (uint32_t)av[k] << (8 * k);
+                B |= (uint32_t)bv[k] << (8 * k);
+                C |= (uint32_t)cv[k] << (8 * k);
+                X |= (uint32_t)xv[k] << (8 * k);
+            }
+            const uint32_t got = ik::unfilter_word(X, A, B, C, ms, mu, mv, mp);
+            for (int k = 0; k < 4; ++k)
+                bad += (int)((got >> (8 * k)) & 255u) != ref(ft, xv[k], av[k], bv[k], cv[k]);
+        }
+    }
+    return bad;
+}

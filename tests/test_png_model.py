@@ -145,3 +145,12 @@ def test_deep_marker_chain(model):
     rc, out, st = inflate(model, z, len(raw), 16384)
     assert rc == 0 and out == raw, st
     assert st[2] > 64  # more decoders than the old hop bound
+
+
+def test_unfilter_word_equals_bytewise_definition():
+    """ik_unfilter.h's word-at-a-time row filters (the GPU unfilter for 4- and
+    8-byte pixels) against png's byte-wise Sub / Up / Average / Paeth, over every
+    (a, b, c) byte triple and every filter type."""
+    L = ctypes.CDLL(MODEL)
+    L.ikm_unfilter_word_check.restype = ctypes.c_long
+    assert L.ikm_unfilter_word_check() == 0
