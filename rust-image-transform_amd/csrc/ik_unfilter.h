@@ -30,11 +30,14 @@ IK_HD uint32_t unfilter_half(uint32_t r, uint32_t a, uint32_t b, uint32_t c, uin
     const s2 t = __builtin_elementwise_min(pb, pc);
     // ~0 in a lane where pa > min(pb, pc) / where pb > pc: the sign of a packed
     // difference spread over its lane (one v_pk_ashrrev_i16; written out, as the
-    // compiler otherwise turns the shift into per-lane compares and selects)
+    // compiler otherwise turns the shift into per-lane compares and selects).  The
+    // shift count comes from a register holding 15 in both halves: an inline
+    // constant would give the high half a count of 0 (it reads the constant's high bits).
     uint32_t m1, m2;
     const uint32_t e1 = __builtin_bit_cast(uint32_t, (s2)(t - pa)), e2 = __builtin_bit_cast(uint32_t, (s2)(pc - pb));
-    asm("v_pk_ashrrev_i16 %0, 15, %1" : "=v"(m1) : "v"(e1));
-    asm("v_pk_ashrrev_i16 %0, 15, %1" : "=v"(m2) : "v"(e2));
+    const uint32_t k15 = 0x000F000Fu;
+    asm("v_pk_ashrrev_i16 %0, %2, %1" : "=v"(m1) : "v"(e1), "v"(k15));
+    asm("v_pk_ashrrev_i16 %0, %2, %1" : "=v"(m2) : "v"(e2), "v"(k15));
     const uint32_t avg = __builtin_bit_cast(uint32_t, (s2)((A + B) >> 1));
 #else
     typedef short s2 __attribute__((vector_size(4)));
