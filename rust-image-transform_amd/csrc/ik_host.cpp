@@ -78,9 +78,9 @@ struct Arena {
     int device = 0;
 };
 struct ThreadRes {
-    std::map<int, hipStream_t> streams, copy_streams;
+    std::map<int, hipStream_t> streams, copy_streams, search_streams;
     std::map<std::pair<int, int>, Arena> dev;  // (device, slot)
-    Arena pinned[6];
+    Arena pinned[8];
     ~ThreadRes() {
         for (auto& kv : dev) {
             if (!kv.second.p) continue;
@@ -93,6 +93,7 @@ struct ThreadRes {
             if (a.p) (void)hipHostFree(a.p);
         for (auto& kv : streams) (void)hipStreamDestroy(kv.second);
         for (auto& kv : copy_streams) (void)hipStreamDestroy(kv.second);
+        for (auto& kv : search_streams) (void)hipStreamDestroy(kv.second);
     }
 };
 ThreadRes& tres() {
@@ -122,6 +123,33 @@ hipStream_t thread_copy_stream() {
     hipStream_t s = nullptr;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
     r.copy_streams[d] = s;
+    return s;
+}
+
+// A stream on a hardware queue of its own, for the next batch's block search
+// beside the current batch's kernels.  Ordinary streams share the device's
+// GPU_MAX_HW_QUEUES (4) queues round-robin, and two streams on one queue run in
+// order: the rocprof trace showed the search serialised behind / before expand on
+// the kernel stage's queue.  A CU-masked stream gets a dedicated queue; the mask
+// is every CU, or the first IK_FIND_CUS of them.
+hipStream_t search_stream() {
+    ThreadRes& r = tres();
+    const int d = current_device();
+    auto it = r.search_streams.find(d);
+    if (it != r.search_streams.end()) return it->second;
+    (void)hipSetDevice(d);
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || ncu <= 0) ncu = 256;
+    int use = ncu;
+    if (const char* e = getenv("IK_FIND_CUS")) use = std::max(1, std::min(ncu, atoi(e)));
+    std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+    for (int c = 0; c < use; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
+    hipStream_t s = nullptr;
+    if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+        (void)hipGetLastError();
+        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    }
+    r.search_streams[d] = s;
     return s;
 }
 
@@ -1350,7 +1378,13 @@ private:
                     if (!q_[1].empty()) nx = q_[1].front();
                 }
                 if (!nx || nx->pb.empty()) return;
-                hipStream_t fs = thread_copy_stream();
+                // (IK_FIND_STREAM=copy: the stage thread's copy stream, which shares a
+                // hardware queue with the kernel stream -- the A/B baseline)
+                static const bool on_copy = [] {
+                    const char* e = getenv("IK_FIND_STREAM");
+                    return e && !strcmp(e, "copy");
+                }();
+                hipStream_t fs = on_copy ? thread_copy_stream() : search_stream();
                 if (after && hipStreamWaitEvent(fs, after, 0) != hipSuccess) return;
                 png_find_prelaunch(nx->up, fs);
             };
@@ -1516,7 +1550,7 @@ int ik_transform_batch_submit_device(const uint8_t* const* dev_bytes, const size
         DeviceGuard g(phys);
         // the first 64 bytes of every file, through pinned memory
         const size_t o_files = (64 * (size_t)n + 255) & ~size_t(255);
-        uint8_t* pin = pinned_slot(5, o_files + 2 * sizeof(uint64_t) * n);
+        uint8_t* pin = pinned_slot(7, o_files + 2 * sizeof(uint64_t) * n);
         void* dp = nullptr;
         if (!pin || hipHostGetDevicePointer(&dp, pin, 0) != hipSuccess || !dp)
             return fail(IK_ERR_NOMEM, "cannot allocate pinned memory for the input headers");

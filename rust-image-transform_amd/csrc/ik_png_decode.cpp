@@ -477,7 +477,7 @@ int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Png
         const size_t o_n = o_side + up256((size_t)kPngWalkSide * n);
         const size_t o_files = o_n + up256(sizeof(int) * n);
         const size_t wbytes = o_files + 2 * sizeof(uint64_t) * n;
-        uint8_t* wp = pinned_slot(4, wbytes);
+        uint8_t* wp = pinned_slot(6, wbytes);
         void* wd = nullptr;
         if (!wp || hipHostGetDevicePointer(&wd, wp, 0) != hipSuccess || !wd) {
             S.rc = fail(IK_ERR_NOMEM, "cannot allocate the PNG chunk-walk area");

@@ -91,6 +91,7 @@ uint64_t request_cost(const uint8_t* b, size_t n, int64_t w, int64_t h, int fmt)
 
 hipStream_t thread_stream();  // per-thread, per-device non-blocking stream
 hipStream_t thread_copy_stream();  // a second one, for uploads that overlap the first's kernels
+hipStream_t search_stream();       // a third, on a hardware queue of its own (the next batch's block search)
 size_t pitch_for(uint32_t w, uint32_t c);
 uint8_t* scratch(size_t bytes);  // per-thread device scratch, valid until the next call
 // per-thread, per-device grow-only device arenas for batch work (slot 1: JPEG
