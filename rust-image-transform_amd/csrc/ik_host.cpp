@@ -93,7 +93,8 @@ struct ThreadRes {
             if (a.p) (void)hipHostFree(a.p);
         for (auto& kv : streams) (void)hipStreamDestroy(kv.second);
         for (auto& kv : copy_streams) (void)hipStreamDestroy(kv.second);
-        for (auto& kv : search_streams) (void)hipStreamDestroy(kv.second);
+        // (search streams are left to the runtime's teardown: destroying a CU-masked
+        // stream from a thread-exit destructor crashed at process exit under rocprofv3)
     }
 };
 ThreadRes& tres() {
@@ -1378,13 +1379,15 @@ private:
                     if (!q_[1].empty()) nx = q_[1].front();
                 }
                 if (!nx || nx->pb.empty()) return;
-                // (IK_FIND_STREAM=copy: the stage thread's copy stream, which shares a
-                // hardware queue with the kernel stream -- the A/B baseline)
-                static const bool on_copy = [] {
+                // the stage thread's copy stream.  IK_FIND_STREAM=search: a stream with
+                // a hardware queue of its own (search_stream), so the search really runs
+                // beside expand / resolve / unfilter -- measured no faster over 12 steps
+                // (63.3 vs 63.9 ms: the search slowed resolve 3.6 -> 13.4 ms), so off
+                static const bool own_queue = [] {
                     const char* e = getenv("IK_FIND_STREAM");
-                    return e && !strcmp(e, "copy");
+                    return e && !strcmp(e, "search");
                 }();
-                hipStream_t fs = on_copy ? thread_copy_stream() : search_stream();
+                hipStream_t fs = own_queue ? search_stream() : thread_copy_stream();
                 if (after && hipStreamWaitEvent(fs, after, 0) != hipSuccess) return;
                 png_find_prelaunch(nx->up, fs);
             };

@@ -102,6 +102,9 @@ hipError_t launch_png_walk(const uint64_t* files, const uint64_t* lens, int n, P
 // dst[i] = src[i] for n words, on the compute stream; one side may be pinned host
 // memory (the small transfers of the PNG kernel phase: ik_png_decode.cpp Xfer)
 hipError_t launch_copy_words(const uint32_t* src, uint32_t* dst, size_t n, hipStream_t s);
+#ifdef IK_UNF_PROF
+hipError_t png_unf_prof_read(unsigned long long* out);  // dev build: k_png_unfilter's segment clock sums (reset)
+#endif
 #ifdef IK_FIND_PROF
 hipError_t png_find_prof_read(unsigned long long* out);  // dev build: k_png_find's phase clock sums (reset)
 #endif

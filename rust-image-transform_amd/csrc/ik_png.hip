@@ -1121,6 +1121,19 @@ __device__ __forceinline__ void unfilter_chunk(const u32x4& rawv, const uint32_t
     }
 }
 
+#ifdef IK_UNF_PROF  // dev build: per-segment clock sums of k_png_unfilter (s_memtime; costs ~10 %)
+__device__ unsigned long long g_unf_prof[8];
+hipError_t png_unf_prof_read(unsigned long long* out) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_unf_prof), sizeof(g_unf_prof));
+    unsigned long long z[8] = {};
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_unf_prof), z, sizeof(z));
+    return e;
+}
+#define IK_UNF_T(k) do { const unsigned long long _t = clock64(); up_[k] += _t - t_; t_ = _t; } while (0)
+#else
+#define IK_UNF_T(k) do { } while (0)
+#endif
+
 template <int BPP, bool SWAR>
 __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngImgDev* imgs, const int2* groups,
                                                                       const int* prog_base, unsigned* prog,
@@ -1141,6 +1154,9 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngI
     // a finished predecessor)
     const int K = png_unfilter_groups(I.H);
     unsigned* pg = prog + prog_base[gk.x];
+#ifdef IK_UNF_PROF
+    unsigned long long up_[6] = {0, 0, 0, 0, 0, 0}, t_ = clock64();
+#endif
     for (int band = wave * K + gk.y; band < nbands; band += NW * K) {
         const int y = band * 64 + lane;
         const bool live = y < I.H;
@@ -1192,6 +1208,7 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngI
             u32x4 ab[G];
 #pragma unroll
             for (int t = 0; t < G; ++t) ab[t] = u32x4{0, 0, 0, 0};
+            IK_UNF_T(0);
             if (lane == 0 && above && s0 < nch) {
                 const unsigned need = (unsigned)min(s0 + G, nch);
                 while (seen < need) {
@@ -1219,6 +1236,7 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngI
                       "v"(off[7]), "s"(base)
                     : "memory");
             }
+            IK_UNF_T(1);
             if (g + 1 < ngrp) fetch(s0 + G, rnxt);
 #pragma unroll
             for (int t = 0; t < G; ++t) {
@@ -1244,19 +1262,28 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngI
                     asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(row + 16 * j), "v"(ov) : "memory");
                 }
             }
+            IK_UNF_T(2);
             // the band's last row publishes the chunks it finished in this group
             const int jl = s0 + G - 1 - 63;
             if (lane == 63 && live && jl >= 0) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its sc1 stores have completed
                 __hip_atomic_store(pg + band, (unsigned)min(jl + 1, nch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            IK_UNF_T(3);
             if (g + 1 < ngrp) {
                 landed(rnxt);
 #pragma unroll
                 for (int t = 0; t < G; ++t) rcur[t] = rnxt[t];
             }
+            IK_UNF_T(4);
         }
     }
+#ifdef IK_UNF_PROF
+    if (lane == 0) {
+        for (int k = 0; k < 5; ++k) atomicAdd(&g_unf_prof[k], up_[k]);
+        atomicAdd(&g_unf_prof[7], 1ull);
+    }
+#endif
 }
 
 // The same wavefront over 8-byte chunks (BPP <= 4).  The chain of a frame is

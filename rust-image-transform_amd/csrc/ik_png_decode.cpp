@@ -1070,6 +1070,16 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                     e3 = launch_png_px(j.px, s);
                 }
                 rec(7, s);
+#ifdef IK_UNF_PROF
+                {
+                    (void)hipStreamSynchronize(s);
+                    unsigned long long pf[8] = {};
+                    if (png_unf_prof_read(pf) == hipSuccess && pf[7])
+                        fprintf(stderr, "[unf-prof] waves %llu: cycles/wave above %.0f, fetch-issue %.0f, steps %.0f, publish "
+                                "%.0f, landed %.0f; unfilter %.2f ms\n", pf[7], (double)pf[0] / pf[7], (double)pf[1] / pf[7],
+                                (double)pf[2] / pf[7], (double)pf[3] / pf[7], (double)pf[4] / pf[7], ev_ms(6, 7));
+                }
+#endif
                 if (e3 == hipSuccess) e3 = X.d2h(hxst.data(), d_xst, 2 * sizeof(int) * hl.size());
                 if (e3 == hipSuccess) e3 = X.d2h(herr.data(), dev + o_err, sizeof(int) * m);
                 mk[3] = now_ms();  // expand .. unfilter done

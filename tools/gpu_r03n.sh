@@ -16,3 +16,6 @@ for v in "search:" "copy:" "search:128" "search:64"; do
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_prof -o run -f csv -- python bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-extras --no-pcie-leg > gpurun_out/${T}_prof.json 2> gpurun_out/${T}_prof.err || { echo "PROFILE FAILED"; exit 1; }
 show gpurun_out/${T}_prof.json
+# the unfilter's per-segment clock (dev build with IK_UNF_PROF)
+IK_LIB_PATH=$PWD/rust-image-transform_amd/lib_exp/libimagekit_hip_unfprof.so timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras --no-pcie-leg > gpurun_out/${T}_unfprof.json 2> gpurun_out/${T}_unfprof.err || { tail -5 gpurun_out/${T}_unfprof.err; exit 1; }
+grep "unf-prof" gpurun_out/${T}_unfprof.err | tail -3
