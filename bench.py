@@ -67,8 +67,8 @@ PNG_STAGES = {0: "upload_host", 1: "upload_device", 14: "gather_crc", 15: "kerne
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=4)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=64, help="PNG requests per GPU per step")
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--out", type=int, default=512)
