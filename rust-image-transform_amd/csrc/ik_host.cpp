@@ -852,6 +852,93 @@ int webp_front_group(const std::vector<ik_image*>& imgs, int quality, std::vecto
 // the images may sit anywhere.  Same arithmetic as ik_resize_exact, per image.
 // Returns IK_ERR_UNSUPPORTED (nothing allocated) when the geometry needs the
 // two-kernel fallback; the caller then resizes image by image.
+// encode_image's JPEG branch for a group of same-size 8-bit images (one quality),
+// batched: one coefficient launch (to_rgb8 + YCbCr + FDCT + quantise) and one
+// Huffman launch over all of them, writing the stuffed streams and their lengths
+// straight into pinned host memory -- instead of a launch pair and two blocking
+// copies per image, which serialised 256 small launches per configs[2] batch.
+// Images whose stream does not fit the GPU coder's buffer are coded by the
+// single-image path (its host fallback).  out[i] gets the finished JPEG bytes.
+int jpeg_front_group(const std::vector<ik_image*>& imgs, int quality, std::vector<std::vector<uint8_t>*>& out) {
+    const size_t n = imgs.size();
+    if (!n) return IK_OK;
+    const ik_image* i0 = imgs[0];
+    if (i0->w > 65535 || i0->h > 65535 || i0->depth != 1) return IK_ERR_UNSUPPORTED;
+    DeviceGuard g(i0->device);
+    const DeviceConsts* dc = device_consts(current_device());
+    if (!dc) return fail(IK_ERR_DEVICE, "cannot upload JPEG tables");
+    const int q = quality < 1 ? 1 : (quality > 100 ? 100 : quality);
+    const uint32_t w = i0->w, h = i0->h;
+    uint8_t qt[128];
+    jpeg_quant_tables(q, qt);
+    std::vector<uint8_t> hdr;
+    jpeg_header((int)w, (int)h, qt, hdr);
+    const size_t nmcu = (size_t)((w + 7) / 8) * ((h + 7) / 8);
+    const size_t cimg = ((nmcu * 3 * 64 * sizeof(int16_t)) + 255) & ~size_t(255);  // coefficients per image
+    const size_t cap = jpeg_enc_cap((int)w, (int)h);
+    hipStream_t s = thread_stream();
+    // sub-batches bound the device and pinned memory (2 cap + coefficients per image)
+    constexpr size_t kSub = 64;
+    for (size_t b0 = 0; b0 < n; b0 += kSub) {
+        const size_t m = std::min(kSub, n - b0);
+        // device: [qt 256][src table][coefficients][Huffman work]; pinned: [streams][lengths][qt + table staging]
+        const size_t o_tab = 256, o_coef = o_tab + ((sizeof(uint64_t) * m + 255) & ~size_t(255));
+        const size_t o_work = o_coef + cimg * m;
+        uint8_t* dv = scratch_slot(4, o_work + 2 * cap * m);
+        const size_t p_len = cap * m, p_stage = p_len + ((sizeof(uint32_t) * m + 255) & ~size_t(255));
+        uint8_t* hp = pinned_slot(5, p_stage + 256 + sizeof(uint64_t) * m);
+        void* dhp = nullptr;
+        if (!dv || !hp || hipHostGetDevicePointer(&dhp, hp, 0) != hipSuccess || !dhp)
+            return fail(IK_ERR_NOMEM, "cannot allocate the batched JPEG encoder's buffers");
+        uint8_t* dh = reinterpret_cast<uint8_t*>(dhp);
+        (void)hipStreamSynchronize(s);  // nothing pending reads the pinned area
+        std::memcpy(hp + p_stage, qt, 128);
+        uint64_t* htab = reinterpret_cast<uint64_t*>(hp + p_stage + 256);
+        for (size_t i = 0; i < m; ++i) htab[i] = (uint64_t)(uintptr_t)imgs[b0 + i]->d;
+        hipError_t e = launch_copy_words(reinterpret_cast<const uint32_t*>(dh + p_stage), reinterpret_cast<uint32_t*>(dv),
+                                         32, s);
+        if (e == hipSuccess)
+            e = launch_copy_words(reinterpret_cast<const uint32_t*>(dh + p_stage + 256),
+                                  reinterpret_cast<uint32_t*>(dv + o_tab), 2 * m, s);
+        if (e == hipSuccess)
+            e = launch_jpeg_coeffs(nullptr, (int)w, (int)h, (int)i0->c, i0->pitch, 0, dv,
+                                   reinterpret_cast<int16_t*>(dv + o_coef), cimg / sizeof(int16_t), (int)m, s,
+                                   reinterpret_cast<const uint64_t*>(dv + o_tab));
+        if (e == hipSuccess) {
+            JpegEncArgs a{};
+            a.coef = reinterpret_cast<const int16_t*>(dv + o_coef);
+            a.coef_img_stride = cimg / sizeof(int16_t);
+            a.nmcu = (int)nmcu;
+            a.huff = dc->jpeg_huff;
+            a.work = dv + o_work;
+            a.work_img_bytes = 2 * cap;
+            a.words_bytes = cap;
+            a.out = dh;
+            a.out_img_stride = cap;
+            a.out_cap = cap;
+            a.out_len = reinterpret_cast<uint32_t*>(dh + p_len);
+            e = launch_jpeg_huff_enc(a, (int)m, s);
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return hip_fail(e, "jpeg encode (batched)");
+        const uint32_t* lens = reinterpret_cast<const uint32_t*>(hp + p_len);
+        for (size_t i = 0; i < m; ++i) {
+            std::vector<uint8_t>& o = *out[b0 + i];
+            if (lens[i] == 0xffffffffu) {  // past the GPU coder's buffer: the single-image path (host coder)
+                EncodePrep pp;
+                if (int rc = encode_device_front(imgs[b0 + i]->d, w, h, i0->c, i0->pitch, IK_FORMAT_JPEG, q, pp, o))
+                    return rc;
+                continue;
+            }
+            o.assign(hdr.begin(), hdr.end());
+            o.insert(o.end(), hp + cap * i, hp + cap * i + lens[i]);
+            o.push_back(0xFF);
+            o.push_back(0xD9);
+        }
+    }
+    return IK_OK;
+}
+
 int resize_group(const std::vector<ik_image*>& src, uint32_t nw, uint32_t nh, int filter, std::vector<ik_image*>& out) {
     const size_t n = src.size();
     out.assign(n, nullptr);
@@ -1217,10 +1304,13 @@ static void transform_device_phase(const uint8_t* const* bytes, const size_t* le
             for (uint32_t k : kv.second) src.push_back(imgs[k]);
             if (resize_group(src, std::get<5>(kv.first), std::get<6>(kv.first), filter, out) != IK_OK) continue;
             for (size_t j = 0; j < out.size(); ++j) rsz[kv.second[j]] = out[j];
-            // the group's WebP requests of one quality: one colour-conversion launch
-            std::map<int, std::vector<uint32_t>> byq;
-            for (uint32_t k : kv.second)
+            // the group's WebP requests of one quality: one colour-conversion launch;
+            // its JPEG requests of one quality: one coefficient + one Huffman launch
+            std::map<int, std::vector<uint32_t>> byq, jbyq;
+            for (uint32_t k : kv.second) {
                 if (fmt[idx[k]] == IK_FORMAT_WEBP) byq[quality[idx[k]]].push_back(k);
+                if (fmt[idx[k]] == IK_FORMAT_JPEG) jbyq[quality[idx[k]]].push_back(k);
+            }
             for (auto& qv : byq) {
                 if (qv.second.size() < 2) continue;
                 std::vector<ik_image*> im;
@@ -1228,6 +1318,18 @@ static void transform_device_phase(const uint8_t* const* bytes, const size_t* le
                 for (uint32_t k : qv.second) { im.push_back(rsz[k]); pp.push_back(&prep[k]); }
                 if (webp_front_group(im, qv.first, pp) == IK_OK)
                     for (uint32_t k : qv.second) fronted[k] = 1;
+            }
+            for (auto& qv : jbyq) {
+                if (qv.second.size() < 2) continue;
+                std::vector<ik_image*> im;
+                std::vector<std::vector<uint8_t>*> oo;
+                for (uint32_t k : qv.second) { im.push_back(rsz[k]); oo.push_back(&bytes_out[k]); }
+                if (jpeg_front_group(im, qv.first, oo) == IK_OK)
+                    for (uint32_t k : qv.second) {
+                        fronted[k] = 1;
+                        prep[k].fmt = IK_FORMAT_JPEG;
+                        prep[k].done = true;  // the bytes are final: no host coder
+                    }
             }
         }
         t_resize += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1379,15 +1481,21 @@ private:
                     if (!q_[1].empty()) nx = q_[1].front();
                 }
                 if (!nx || nx->pb.empty()) return;
-                // the stage thread's copy stream.  IK_FIND_STREAM=search: a stream with
-                // a hardware queue of its own (search_stream), so the search really runs
-                // beside expand / resolve / unfilter -- measured no faster over 12 steps
-                // (63.3 vs 63.9 ms: the search slowed resolve 3.6 -> 13.4 ms), so off
-                static const bool own_queue = [] {
+                // On the kernel stream itself, between this batch's decode rounds and its
+                // expand (it covers the host planning there), once the next batch's
+                // upload has landed (else its own kernel stage launches it).  Beside
+                // expand / resolve / unfilter it only slows them: a stream on another
+                // hardware queue measured 63-69 vs 61-62 ms per step (the search took
+                // resolve from 3.6 to 13-19 ms), and which queue the copy stream gets is
+                // the runtime's round-robin, so it differed from run to run.
+                // IK_FIND_STREAM=copy / search: the copy stream / a CU-masked stream
+                // with a queue of its own (A/B).
+                static const int where = [] {
                     const char* e = getenv("IK_FIND_STREAM");
-                    return e && !strcmp(e, "search");
+                    return e && !strcmp(e, "search") ? 2 : (e && !strcmp(e, "copy") ? 1 : 0);
                 }();
-                hipStream_t fs = own_queue ? search_stream() : thread_copy_stream();
+                if (where == 0 && !png_upload_landed(nx->up)) return;
+                hipStream_t fs = where == 2 ? search_stream() : where == 1 ? thread_copy_stream() : thread_stream();
                 if (after && hipStreamWaitEvent(fs, after, 0) != hipSuccess) return;
                 png_find_prelaunch(nx->up, fs);
             };

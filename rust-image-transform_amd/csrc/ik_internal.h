@@ -102,7 +102,8 @@ hipError_t launch_avif_yuv444(const uint8_t* src, int w, int h, int C, size_t pi
                               uint8_t* planes, size_t plane_img_stride, int* transparent, int n, hipStream_t s);
 hipError_t launch_jpeg_coeffs(const uint8_t* src, int w, int h, int C, size_t pitch,
                               size_t img_stride, const uint8_t* qtables /*dev, 128 B*/,
-                              int16_t* coef, size_t coef_img_stride, int n, hipStream_t s);
+                              int16_t* coef, size_t coef_img_stride, int n, hipStream_t s,
+                              const uint64_t* src_tab = nullptr /* per-image bases (device), or src + i * img_stride */);
 
 // JPEG reconstruction (ik_jpeg.hip): dequantise + islow IDCT every 8x8 block of
 // the coefficient image into per-component sample planes, then fancy-upsample +

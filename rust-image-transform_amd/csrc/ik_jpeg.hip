@@ -277,14 +277,12 @@ __device__ __forceinline__ int muldiv255(int a, int b) {
     return ((t >> 8) + t) >> 8;
 }
 
-__global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restrict__ dst, size_t pitch) {
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
-    if (x >= g.W) return;
+// one output pixel (x, y): gray -> o[0]; otherwise RGB -> o[0..2]
+__device__ __forceinline__ void color_pixel(const JpegGeom& g, int x, int y, uint8_t* o) {
     const bool zune = g.recon == IK_JPEG_RECON_ZUNE;
     auto sample = [&](int ci) { return zune ? upsampled_zune(g, ci, x, y) : upsampled(g, ci, x, y); };
-    uint8_t* o = dst + (size_t)y * pitch;
     if (g.colorspace == 0) {
-        o[x] = (uint8_t)sample(0);
+        o[0] = (uint8_t)sample(0);
         return;
     }
     const int c0 = sample(0), c1 = sample(1), c2 = sample(2);
@@ -306,9 +304,9 @@ __global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restr
         b = c0 + ((116130 * cb + 32768) >> 16);
     }
     if (g.colorspace < 3) {
-        o[3 * x] = clamp255(r);
-        o[3 * x + 1] = clamp255(gg);
-        o[3 * x + 2] = clamp255(b);
+        o[0] = clamp255(r);
+        o[1] = clamp255(gg);
+        o[2] = clamp255(b);
         return;
     }
     // CMYK / YCCK -> RGB8: YCCK's YCbCr part gives inverted C, M, Y (jdcolor.c
@@ -319,9 +317,36 @@ __global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restr
     int k = sample(3);
     if (g.adobe) { cc = 255 - cc; mm = 255 - mm; yy = 255 - yy; k = 255 - k; }
     const int nk = 255 - k;
-    o[3 * x] = clamp255(nk - muldiv255(cc, nk));
-    o[3 * x + 1] = clamp255(nk - muldiv255(mm, nk));
-    o[3 * x + 2] = clamp255(nk - muldiv255(yy, nk));
+    o[0] = clamp255(nk - muldiv255(cc, nk));
+    o[1] = clamp255(nk - muldiv255(mm, nk));
+    o[2] = clamp255(nk - muldiv255(yy, nk));
+}
+
+// Four consecutive pixels per thread: the row's output goes out as whole dwords (3
+// per thread for RGB, 1 for gray; rows are 256-B pitched, so 4 pixels start on a
+// 4-byte boundary) instead of three byte stores per pixel; a partial group at the
+// row's end is stored byte by byte.
+__global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restrict__ dst, size_t pitch) {
+    const int x0 = 4 * (blockIdx.x * 256 + threadIdx.x), y = blockIdx.y;
+    if (x0 >= g.W) return;
+    const int C = g.colorspace == 0 ? 1 : 3;
+    uint8_t px[12];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (x0 + k < g.W) color_pixel(g, x0 + k, y, px + C * k);
+    uint8_t* o = dst + (size_t)y * pitch + (size_t)C * x0;
+    if (x0 + 4 <= g.W) {
+        uint32_t w[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            w[i] = (uint32_t)px[4 * i] | (uint32_t)px[4 * i + 1] << 8 | (uint32_t)px[4 * i + 2] << 16 |
+                   (uint32_t)px[4 * i + 3] << 24;
+        uint32_t* o32 = reinterpret_cast<uint32_t*>(o);
+        o32[0] = w[0];
+        if (C == 3) { o32[1] = w[1]; o32[2] = w[2]; }
+        return;
+    }
+    for (int i = 0; i < C * (g.W - x0); ++i) o[i] = px[i];
 }
 
 }  // namespace
@@ -721,7 +746,7 @@ hipError_t launch_jpeg_reconstruct(const JpegGeom& g, uint8_t* dst, size_t dst_p
     if (g.nblocks <= 0 || g.W <= 0 || g.H <= 0) return hipErrorInvalidValue;
     const unsigned nb = (unsigned)((g.nblocks + 255) / 256);
     hipLaunchKernelGGL(k_jpeg_idct, dim3(nb), dim3(256), 0, s, g);
-    hipLaunchKernelGGL(k_jpeg_color, dim3((g.W + 255) / 256, g.H), dim3(256), 0, s, g, dst, dst_pitch);
+    hipLaunchKernelGGL(k_jpeg_color, dim3((g.W + 1023) / 1024, g.H), dim3(256), 0, s, g, dst, dst_pitch);
     return hipGetLastError();
 }
 

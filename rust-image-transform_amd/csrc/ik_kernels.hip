@@ -653,7 +653,8 @@ __global__ __launch_bounds__(192) void k_jpeg_coeffs(const uint8_t* __restrict__
                                                      int C, size_t pitch, size_t img_stride,
                                                      const uint8_t* __restrict__ qt,
                                                      int16_t* __restrict__ coef,
-                                                     size_t coef_img_stride, int nmcu) {
+                                                     size_t coef_img_stride, int nmcu,
+                                                     const uint64_t* __restrict__ src_tab) {
     __shared__ int rows[24][8][9];
     const int t = threadIdx.x;
     const int blk = t >> 3, line = t & 7;
@@ -665,7 +666,8 @@ __global__ __launch_bounds__(192) void k_jpeg_coeffs(const uint8_t* __restrict__
         const int bx = m % nbx, by = m / nbx;
         int py = by * 8 + line;
         if (py >= h) py = h - 1;
-        const uint8_t* row = src + (size_t)img * img_stride + (size_t)py * pitch;
+        const uint8_t* base = src_tab ? reinterpret_cast<const uint8_t*>(src_tab[img]) : src + (size_t)img * img_stride;
+        const uint8_t* row = base + (size_t)py * pitch;
         int smp[8];
         const float mx = 255.0f;
 #pragma unroll
@@ -703,11 +705,11 @@ __global__ __launch_bounds__(192) void k_jpeg_coeffs(const uint8_t* __restrict__
 
 hipError_t launch_jpeg_coeffs(const uint8_t* src, int w, int h, int C, size_t pitch,
                               size_t img_stride, const uint8_t* qtables, int16_t* coef,
-                              size_t coef_img_stride, int n, hipStream_t s) {
+                              size_t coef_img_stride, int n, hipStream_t s, const uint64_t* src_tab) {
     const int nmcu = ((w + 7) >> 3) * ((h + 7) >> 3);
     dim3 grid((nmcu + 7) / 8, n);
     hipLaunchKernelGGL(k_jpeg_coeffs, grid, dim3(192), 0, s, src, w, h, C, pitch, img_stride,
-                       qtables, coef, coef_img_stride, nmcu);
+                       qtables, coef, coef_img_stride, nmcu, src_tab);
     return hipGetLastError();
 }
 

@@ -662,6 +662,12 @@ static void png_find_launch(PngBatchState& S, hipStream_t s) {
     S.find_launched = true;
 }
 
+bool png_upload_landed(const PngUpload& up) {
+    if (!up.st || !up.st->area) return false;
+    hipEvent_t e = up.st->area->ev[2];
+    return e && hipEventQuery(e) == hipSuccess;
+}
+
 void png_find_prelaunch(PngUpload& up, hipStream_t s) {
     if (up.st) png_find_launch(*up.st, s);
 }
