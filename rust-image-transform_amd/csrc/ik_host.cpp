@@ -482,11 +482,11 @@ int encode_host_back(EncodePrep& p, std::vector<uint8_t>& out) {
     p.done = true;
     if (p.fmt == IK_FORMAT_WEBP) {
         const size_t uvw = (p.w + 1) / 2, uvh = (p.h + 1) / 2;
-        const uint8_t* Y = p.planes.data();
+        const uint8_t* Y = p.plane_data();
         return webp_encode_yuv420(Y, Y + (size_t)p.w * p.h, Y + (size_t)p.w * p.h + uvw * uvh, (int)p.w, (int)p.h,
                                   (float)p.q, out);
     }
-    if (p.fmt == IK_FORMAT_AVIF) return avif_encode_yuv444(p.planes.data(), p.transparent, (int)p.w, (int)p.h, p.q, 4, out);
+    if (p.fmt == IK_FORMAT_AVIF) return avif_encode_yuv444(p.plane_data(), p.transparent, (int)p.w, (int)p.h, p.q, 4, out);
     return fail(IK_ERR_INVALID, "unknown ImageFormat %d", p.fmt);
 }
 
@@ -805,6 +805,35 @@ int resize_target(uint32_t W, uint32_t H, int64_t w, int64_t h, uint32_t* onw, u
 // writing every image's YUV420 planes straight into pinned host memory; prep[i]
 // gets the planes for encode_host_back.  Returns IK_ERR_UNSUPPORTED (nothing
 // done) when the per-image path applies instead (the GPU VP8 encoder, > 16383).
+// Page-locked blocks shared by the requests of a batched colour launch: a pool of
+// free blocks (process-wide); a block goes back when its last holder drops it.
+namespace {
+std::mutex g_pblk_mu;
+std::vector<std::pair<uint8_t*, size_t>> g_pblk_free;
+}  // namespace
+static std::shared_ptr<uint8_t> pinned_block(size_t bytes) {
+    uint8_t* p = nullptr;
+    size_t cap = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_pblk_mu);
+        for (size_t i = 0; i < g_pblk_free.size(); ++i)
+            if (g_pblk_free[i].second >= bytes) {
+                p = g_pblk_free[i].first;
+                cap = g_pblk_free[i].second;
+                g_pblk_free.erase(g_pblk_free.begin() + (long)i);
+                break;
+            }
+    }
+    if (!p) {
+        cap = bytes;
+        if (hipHostMalloc((void**)&p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+    }
+    return std::shared_ptr<uint8_t>(p, [cap](uint8_t* q) {
+        std::lock_guard<std::mutex> lk(g_pblk_mu);
+        g_pblk_free.emplace_back(q, cap);
+    });
+}
+
 int webp_front_group(const std::vector<ik_image*>& imgs, int quality, std::vector<EncodePrep*>& prep) {
     const size_t n = imgs.size();
     if (!n) return IK_OK;
@@ -817,7 +846,8 @@ int webp_front_group(const std::vector<ik_image*>& imgs, int quality, std::vecto
     const uint32_t w = i0->w, h = i0->h;
     const size_t uvw = (w + 1) / 2, uvh = (h + 1) / 2, bytes = (size_t)w * h + 2 * uvw * uvh;
     const size_t stride = (bytes + 255) & ~size_t(255);
-    uint8_t* hp = pinned_slot(4, stride * n + 16 * n + 256);
+    std::shared_ptr<uint8_t> blk = pinned_block(stride * n + 16 * n + 256);
+    uint8_t* hp = blk.get();
     void* dhp = nullptr;
     if (!hp || hipHostGetDevicePointer(&dhp, hp, 0) != hipSuccess || !dhp)
         return fail(IK_ERR_NOMEM, "cannot map pinned WebP planes");
@@ -841,7 +871,8 @@ int webp_front_group(const std::vector<ik_image*>& imgs, int quality, std::vecto
         p.q = q;
         p.w = w;
         p.h = h;
-        p.planes.assign(hp + stride * i, hp + stride * i + bytes);
+        p.pin_block = blk;
+        p.pin_planes = hp + stride * i;
         p.done = false;
     }
     return IK_OK;
@@ -1372,6 +1403,8 @@ static void transform_host_phase(uint8_t** outs, size_t* out_lens, int* st, std:
         const auto t0 = std::chrono::steady_clock::now();
         int r = encode_host_back(prep[k], bytes_out[k]);
         std::vector<uint8_t>().swap(prep[k].planes);
+        prep[k].pin_block.reset();  // (the batch's pinned plane block goes back to its pool with the last)
+        prep[k].pin_planes = nullptr;
         if (!r) {
             outs[i] = (uint8_t*)malloc(bytes_out[k].size() ? bytes_out[k].size() : 1);
             if (!outs[i]) r = fail(IK_ERR_NOMEM, "out of host memory");

@@ -4,8 +4,8 @@
 //
 //   k_jpeg_idct   one lane per 8x8 block: dequantise (coef * qt) and a 2-D
 //                 integer IDCT into the component's u8 sample plane (MCU-padded).
-//   k_jpeg_color  one lane per output pixel: chroma upsampling and colour
-//                 conversion, written into the device image.
+//   k_jpeg_color  one lane per four output pixels: chroma upsampling and colour
+//                 conversion, written into the device image as whole dwords.
 //
 // Two reconstructions over the same coefficients (JpegGeom::recon):
 //   IK_JPEG_RECON_ZUNE (default; the reference's decoder) -- zune-jpeg 0.4.21

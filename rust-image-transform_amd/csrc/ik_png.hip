@@ -247,7 +247,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
 }
 
 constexpr uint32_t kFindQueue = 128;
-constexpr uint32_t kFindDense = 1024;  // bit-filter survivors of one wave step checked in dense rounds (LDS list)
 
 #ifdef IK_FIND_PROF  // dev build: per-phase clock sums of k_png_find (tools/gpu_*.sh experiments)
 __device__ unsigned long long g_find_prof[8];
@@ -260,13 +259,11 @@ hipError_t png_find_prof_read(unsigned long long* out) {
 #endif
 
 __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const int* chunk_img, const int* chunk_idx,
-                                                 int nchunks_total, uint64_t chunk_bits, int64_t* cand, int dense) {
+                                                 int nchunks_total, uint64_t chunk_bits, int64_t* cand) {
     __shared__ uint32_t s_win[64 * 32];     // per lane: 32 stream words of the candidate being checked (lane-minor)
     __shared__ uint8_t s_sym[64 * 20];      // per lane: code-length-code symbols in canonical order (lane-minor)
     __shared__ uint32_t s_q[kFindQueue];    // Kraft-passing offsets (relative to the chunk) awaiting the full check
     __shared__ uint8_t s_kraft[512];        // 3 code-length-code lengths (9 bits) -> sum of 2^(7 - len), len > 0
-    __shared__ uint16_t s_cand[kFindDense]; // this step's bit-filter survivors: lane << 5 | bit
-    __shared__ uint32_t s_w4[4 * 64];       // this step's four words per lane (lane-minor)
     const int g = blockIdx.x;
     if (g >= nchunks_total) return;
     for (int v = threadIdx.x; v < 512; v += 64) {
@@ -349,61 +346,7 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
         if (pw < b0) m &= b0 - pw >= 32 ? 0u : ~0u << (uint32_t)(b0 - pw);
         if (pw + 32 > b1) m &= pw >= b1 ? 0u : (1u << (uint32_t)(b1 - pw)) - 1u;
         const uint64_t lo = (uint64_t)w0 | ((uint64_t)w1 << 32), hi = (uint64_t)w2 | ((uint64_t)w3 << 32);
-        // Dense rounds: the wave's survivors (~22 % of its 2,048 offsets) are compacted
-        // into an LDS list, and every lane takes one per round, so the Kraft test runs
-        // on 64 live lanes instead of a divergent per-lane loop as long as the lane
-        // with the most survivors (IK_FIND_DENSE=0: that loop, the A/B baseline)
-        const uint32_t incl = wave_incl_scan_dpp((uint32_t)__builtin_popcount(m));
-        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        if (dense && tot && tot <= kFindDense) {
-            s_w4[lane] = w0;
-            s_w4[64 + lane] = w1;
-            s_w4[128 + lane] = w2;
-            s_w4[192 + lane] = w3;
-            uint32_t mm = m, o = incl - (uint32_t)__builtin_popcount(m);
-            while (mm) {
-                const uint32_t j = (uint32_t)__builtin_ctz(mm);
-                mm &= mm - 1u;
-                s_cand[o++] = (uint16_t)(((uint32_t)lane << 5) | j);
-            }
-            __syncthreads();
-            const uint64_t pw0 = (wi - (uint64_t)lane) << 5;  // lane 0's first offset
-            for (uint32_t r0 = 0; r0 < tot; r0 += 64) {
-                const uint32_t idx = r0 + (uint32_t)lane;
-                bool pass = false;
-                uint32_t off = 0;
-                if (idx < tot) {
-                    const uint32_t e = s_cand[idx];
-                    const uint32_t l = e >> 5, j = e & 31u;
-                    const uint64_t clo = (uint64_t)s_w4[l] | ((uint64_t)s_w4[64 + l] << 32);
-                    const uint64_t chi = (uint64_t)s_w4[128 + l] | ((uint64_t)s_w4[192 + l] << 32);
-                    const uint32_t h = (uint32_t)(clo >> j);
-                    const uint32_t sh = j + 17;
-                    const uint64_t cl = (clo >> sh) | (chi << (64 - sh));
-                    const int ncode = (int)((h >> 13) & 15u) + 4;
-                    const uint64_t used = cl & (ncode == 19 ? 0x1FFFFFFFFFFFFFFull : ((1ull << (3 * ncode)) - 1ull));
-                    const uint32_t ulo = (uint32_t)used, uhi = (uint32_t)(used >> 32);
-                    const uint32_t kraft = s_kraft[ulo & 511u] + s_kraft[(ulo >> 9) & 511u] + s_kraft[(ulo >> 18) & 511u] +
-                                           s_kraft[((ulo >> 27) | (uhi << 5)) & 511u] + s_kraft[(uhi >> 4) & 511u] +
-                                           s_kraft[(uhi >> 13) & 511u] + s_kraft[(uhi >> 22) & 7u];
-                    pass = kraft == 128u;
-                    off = (uint32_t)(pw0 + 32u * l + j - b0);
-                }
-                const unsigned long long bal = __ballot(pass);
-                if (bal) {
-                    if (qlen + 64 > kFindQueue) flush();
-                    if (pass) {
-                        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                        s_q[qlen + r] = off;
-                    }
-                    qlen += (uint32_t)__popcll(bal);
-                }
-            }
-            __syncthreads();  // (the list is rewritten next step)
-            m = 0;
-        }
-        uint32_t km = 0;  // offsets passing the Kraft test (per-lane loop)
+        uint32_t km = 0;  // offsets passing the Kraft test
         while (m) {
             const uint32_t j = (uint32_t)__builtin_ctz(m);
             m &= m - 1u;
@@ -1800,11 +1743,7 @@ hipError_t launch_png_px(const PngPxDev& px, hipStream_t s) {
 hipError_t launch_png_find(const PngImgDev* imgs, const int* chunk_img, const int* chunk_idx, int n,
                            uint64_t chunk_bits, int64_t* cand, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    static const int dense = [] {  // IK_FIND_DENSE=0: the per-lane Kraft loop (A/B)
-        const char* e = getenv("IK_FIND_DENSE");
-        return e && !strcmp(e, "0") ? 0 : 1;
-    }();
-    hipLaunchKernelGGL(k_png_find, dim3(n), dim3(64), 0, s, imgs, chunk_img, chunk_idx, n, chunk_bits, cand, dense);
+    hipLaunchKernelGGL(k_png_find, dim3(n), dim3(64), 0, s, imgs, chunk_img, chunk_idx, n, chunk_bits, cand);
     return hipGetLastError();
 }
 

@@ -278,6 +278,25 @@ struct Xfer {
         return launch_copy_words(reinterpret_cast<const uint32_t*>(dpin + o), reinterpret_cast<uint32_t*>(dev),
                                  (n + 3) / 4, s);
     }
+    // d2h in two halves: start queues the copy kernel (its data lands in the pinned
+    // region returned in *off), finish waits for the event recorded after it and
+    // copies out -- so work queued between the two (the next batch's block search)
+    // runs while the host waits for nothing but the copy
+    hipError_t d2h_start(const void* dev, size_t n, size_t* off, hipEvent_t ev) {
+        const size_t o = take(n + 4);
+        if (o == ~size_t(0) || (n & 3) || !ev) { *off = ~size_t(0); return hipSuccess; }
+        hipError_t e = launch_copy_words(reinterpret_cast<const uint32_t*>(dev), reinterpret_cast<uint32_t*>(dpin + o),
+                                         n / 4, s);
+        if (e == hipSuccess) e = hipEventRecord(ev, s);
+        *off = o;
+        return e;
+    }
+    hipError_t d2h_finish(void* host, const void* dev, size_t n, size_t off, hipEvent_t ev) {
+        if (off == ~size_t(0)) return d2h(host, dev, n);  // (no room / odd size: the synchronous path)
+        hipError_t e = hipEventSynchronize(ev);
+        if (e == hipSuccess) std::memcpy(host, pin + off, n);
+        return e;
+    }
     // (synchronises the stream)
     hipError_t d2h(void* host, const void* dev, size_t n) {
         if (!n) return hipSuccess;
@@ -841,6 +860,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         }
         // ---- decode rounds: token streams; the host checks the lane chain ----
         int rounds = 0, dropped = 0, overflows = 0;
+        bool search_done = false;  // the next batch's block search was handed to the hook
         std::vector<PngLaneDev>& hl = ht.lanes;
         std::vector<std::pair<int, int>>& who = ht.who;  // (job, lane) of each launched lane
         std::vector<infl::LaneResult>& hres = ht.res;
@@ -893,7 +913,17 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             rec(2, s);
             hipError_t e2 = launch_png_decode(d_imgs, d_lanes, (int)hl.size(), d_tok, d_res, s);
             rec(3, s);
-            if (e2 == hipSuccess) e2 = X.d2h(hres.data(), d_res, sizeof(infl::LaneResult) * hl.size());
+            // the lane results come back behind the decode; the next batch's block
+            // search (the stage executor's hook) queues behind that copy, so it runs
+            // while this thread checks the lane chain and plans expand / resolve
+            size_t roff = ~size_t(0);
+            const size_t rbytes = sizeof(infl::LaneResult) * hl.size();
+            if (e2 == hipSuccess) e2 = X.d2h_start(d_res, rbytes, &roff, ev.ok ? ev.e[10] : nullptr);
+            if (e2 == hipSuccess && !search_done && up.on_next_search && !search_after_resolve()) {
+                up.on_next_search(nullptr);
+                search_done = true;
+            }
+            if (e2 == hipSuccess) e2 = X.d2h_finish(hres.data(), d_res, rbytes, roff, ev.ok ? ev.e[10] : nullptr);
             if (e2 != hipSuccess) { rc = hip_fail(e2, "PNG inflate (decode)"); break; }
             count_dev += ev_ms(2, 3);
             ++rounds;
@@ -1002,7 +1032,10 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             // resolve and unfilter, which run at a raised wave priority (ik_png.hip
             // raise_priority): the stage executor's hook.  IK_FIND_AFTER=resolve
             // holds it until this batch's resolve pass is done.
-            if (!rc && up.on_next_search && !search_after_resolve()) up.on_next_search(nullptr);
+            if (!rc && !search_done && up.on_next_search && !search_after_resolve()) {
+                up.on_next_search(nullptr);
+                search_done = true;
+            }
             if (!rc) {
                 hipError_t e3 = hipSuccess;
                 rec(4, s);

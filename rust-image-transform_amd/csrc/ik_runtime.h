@@ -225,6 +225,12 @@ struct EncodePrep {
     uint32_t w = 0, h = 0;
     bool done = false, transparent = false;
     std::vector<uint8_t> planes;
+    // or the planes in a shared page-locked block written by a batched colour
+    // launch (webp_front_group): no copy into `planes`; the block returns to its
+    // pool when the last request holding it is coded
+    std::shared_ptr<uint8_t> pin_block;
+    const uint8_t* pin_planes = nullptr;
+    const uint8_t* plane_data() const { return pin_planes ? pin_planes : planes.data(); }
 };
 int encode_device_front(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, size_t pitch, int fmt, int quality,
                         EncodePrep& p, std::vector<uint8_t>& out);
