@@ -1286,6 +1286,188 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngI
 #endif
 }
 
+// The same wavefront with the bands of a workgroup in blocks: workgroups of
+// kPngUnfBlkWaves (4) waves, workgroup k of an image holding bands 4 k .. 4 k + 3
+// (wave w: band 4 k + w), so 3 of every 4 band-to-band hand-offs stay inside the
+// CU, while the ~14 bands of an image in flight still spread over as many CUs as
+// with the interleaved layout (16-wave blocks put them on one or two CUs, 4 waves
+// a SIMD: 9.4 vs 7.6 ms).  A band's last row goes to the next
+// wave through an LDS ring (kUnfRing chunks per wave) and an LDS progress word,
+// written after `s_waitcnt lgkmcnt(0)` -- no store has to reach memory first --
+// and its rows are stored plain; only the workgroup's last band keeps the sc1
+// hand-off to the next workgroup (stores sc1 + vmcnt(0) + a global progress word,
+// as k_png_unfilter) and only its first band polls one.  The segment clock of
+// k_png_unfilter showed its bands waiting 75 % of the time, one per group on a
+// write-through drain and a cross-CU poll.  The consumer acknowledges what it has
+// read (s_cons), and a producer that would overwrite unread ring chunks waits for
+// it (never in practice: a band runs ~9 groups behind the one above; the ring
+// holds 32).  Bands past 4 K take further passes in the same layout.  Tickets as
+// k_png_unfilter.
+constexpr int kUnfRing = 256;
+
+template <int BPP, bool SWAR>
+__global__ __launch_bounds__(kPngUnfBlkWaves * 64) void k_png_unfilter_blk(const PngImgDev* imgs, const int2* groups,
+                                                                          const int* prog_base, unsigned* prog,
+                                                                          unsigned* ticket) {
+    raise_priority();
+    constexpr int NW = kPngUnfBlkWaves, G = kUnfG, R = kUnfRing;
+    __shared__ int s_t;
+    __shared__ u32x4 s_ring[NW][R];
+    __shared__ unsigned s_prog[NW], s_cons[NW];
+    if (threadIdx.x == 0) s_t = (int)atomicAdd(ticket, 1u);
+    if (threadIdx.x < NW) { s_prog[threadIdx.x] = 0u; s_cons[threadIdx.x] = 0u; }
+    __syncthreads();
+    const int2 gk = groups[s_t];  // (image, workgroup of the image)
+    const PngImgDev I = imgs[gk.x];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int nch = (I.rowbytes + 15) >> 4;
+    const int nbands = (I.H + 63) >> 6;
+    const int K = png_unfilter_blk_groups(I.H);
+    unsigned* pg = prog + prog_base[gk.x];
+    volatile unsigned* vprog = s_prog;
+    volatile unsigned* vcons = s_cons;
+    for (int pass = 0;; ++pass) {
+        const int band = pass * NW * K + gk.y * NW + wave;
+        if (band >= nbands) break;
+        const unsigned seq = (unsigned)(pass * nch);  // this pass's chunks in the LDS ring / progress
+        const bool lds_in = wave > 0, glob_in = wave == 0 && band > 0;
+        const bool lds_out = wave < NW - 1 && band + 1 < nbands, glob_out = wave == NW - 1 && band + 1 < nbands;
+        const int y = band * 64 + lane;
+        const bool live = y < I.H;
+        uint8_t* row = I.dst + (size_t)(live ? y : 0) * I.pitch;
+        const FtMask fm(live ? I.ft[y] : 0u);
+        const uint64_t above = glob_in ? (uint64_t)(size_t)(I.dst + (size_t)(band * 64 - 1) * I.pitch) : 0;
+        uint32_t cur[4] = {0, 0, 0, 0}, up[4] = {0, 0, 0, 0};
+        uint32_t prevcur[4] = {0, 0, 0, 0}, prevup[4] = {0, 0, 0, 0};
+        const uint64_t dbase = uniform_u64((uint64_t)(size_t)I.dst);
+        const uint32_t rowoff = (uint32_t)((size_t)(live ? y : 0) * I.pitch);
+        auto fetch = [&](int s0, u32x4 (&r)[G]) {
+            uint32_t off[G];
+#pragma unroll
+            for (int t = 0; t < G; ++t) off[t] = rowoff + 16u * (uint32_t)min(max(s0 + t - lane, 0), nch - 1);
+            asm volatile(
+                "s_nop 4\n\t"
+                "global_load_dwordx4 %0, %8, %16\n\t"
+                "global_load_dwordx4 %1, %9, %16\n\t"
+                "global_load_dwordx4 %2, %10, %16\n\t"
+                "global_load_dwordx4 %3, %11, %16\n\t"
+                "global_load_dwordx4 %4, %12, %16\n\t"
+                "global_load_dwordx4 %5, %13, %16\n\t"
+                "global_load_dwordx4 %6, %14, %16\n\t"
+                "global_load_dwordx4 %7, %15, %16"
+                : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7])
+                : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]), "v"(off[7]),
+                  "s"(dbase)
+                : "memory");
+        };
+        auto landed = [](u32x4 (&r)[G]) {
+            asm volatile("s_waitcnt vmcnt(0)"
+                         : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7])
+                         :
+                         : "memory");
+        };
+        u32x4 rcur[G], rnxt[G];
+        fetch(0, rcur);
+        landed(rcur);
+        unsigned seen = 0;  // lane 0: the band above's progress last read
+        const int ngrp = (nch + 63 + G - 1) / G;
+        for (int g = 0; g < ngrp; ++g) {
+            const int s0 = g * G;
+            u32x4 ab[G];
+#pragma unroll
+            for (int t = 0; t < G; ++t) ab[t] = u32x4{0, 0, 0, 0};
+            if (lane == 0 && s0 < nch && (glob_in || lds_in)) {
+                const unsigned need = (unsigned)min(s0 + G, nch);
+                if (glob_in) {
+                    while (seen < need) {
+                        seen = __hip_atomic_load(pg + band - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (seen < need) __builtin_amdgcn_s_sleep(1);
+                    }
+                    uint32_t off[G];
+#pragma unroll
+                    for (int t = 0; t < G; ++t) off[t] = 16u * (uint32_t)min(s0 + t, nch - 1);
+                    const uint64_t base = uniform_u64(above);
+                    asm volatile(
+                        "s_nop 4\n\t"
+                        "global_load_dwordx4 %0, %8, %16 sc1\n\t"
+                        "global_load_dwordx4 %1, %9, %16 sc1\n\t"
+                        "global_load_dwordx4 %2, %10, %16 sc1\n\t"
+                        "global_load_dwordx4 %3, %11, %16 sc1\n\t"
+                        "global_load_dwordx4 %4, %12, %16 sc1\n\t"
+                        "global_load_dwordx4 %5, %13, %16 sc1\n\t"
+                        "global_load_dwordx4 %6, %14, %16 sc1\n\t"
+                        "global_load_dwordx4 %7, %15, %16 sc1\n\t"
+                        "s_waitcnt vmcnt(0)"
+                        : "=&v"(ab[0]), "=&v"(ab[1]), "=&v"(ab[2]), "=&v"(ab[3]), "=&v"(ab[4]), "=&v"(ab[5]), "=&v"(ab[6]),
+                          "=&v"(ab[7])
+                        : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]),
+                          "v"(off[7]), "s"(base)
+                        : "memory");
+                } else {
+                    while (seen < seq + need) {
+                        seen = vprog[wave - 1];
+                        if (seen < seq + need) __builtin_amdgcn_s_sleep(1);
+                    }
+                    asm volatile("" ::: "memory");
+#pragma unroll
+                    for (int t = 0; t < G; ++t) ab[t] = s_ring[wave - 1][(seq + (unsigned)min(s0 + t, nch - 1)) % R];
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    vcons[wave] = seq + need;  // read: the producer may reuse those slots
+                }
+            }
+            if (g + 1 < ngrp) fetch(s0 + G, rnxt);
+            // this group writes ring chunks up to jmax: their slots must have been read
+            const int jmax = min(s0 + G - 1 - 63, nch - 1);
+            if (lds_out && lane == 63 && jmax >= R) {
+                const unsigned want = seq + (unsigned)(jmax - R + 1);
+                while (vcons[wave + 1] < want) __builtin_amdgcn_s_sleep(1);
+                asm volatile("" ::: "memory");
+            }
+#pragma unroll
+            for (int t = 0; t < G; ++t) {
+                const int j = s0 + t - lane;
+                uint32_t nup[4];
+                nup[0] = wave_shr1(cur[0], ab[t].x);
+                nup[1] = wave_shr1(cur[1], ab[t].y);
+                nup[2] = wave_shr1(cur[2], ab[t].z);
+                nup[3] = wave_shr1(cur[3], ab[t].w);
+                if (live && j >= 0 && j < nch) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) { prevup[k] = up[k]; up[k] = nup[k]; prevcur[k] = cur[k]; }
+                    if (j == 0) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) { prevup[k] = 0; prevcur[k] = 0; }
+                    }
+                    uint32_t o[4];
+                    unfilter_chunk<BPP, SWAR>(rcur[t], up, prevup, prevcur, fm, o);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) cur[k] = o[k];
+                    const u32x4 ov = {o[0], o[1], o[2], o[3]};
+                    if (glob_out) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(row + 16 * j), "v"(ov) : "memory");
+                    else asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(row + 16 * j), "v"(ov) : "memory");
+                    if (lds_out && lane == 63) s_ring[wave][(seq + (unsigned)j) % R] = ov;
+                }
+            }
+            // the band's last row publishes the chunks it finished in this group
+            const int jl = s0 + G - 1 - 63;
+            if (lane == 63 && live && jl >= 0) {
+                if (lds_out) {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the ring chunks are in LDS
+                    vprog[wave] = seq + (unsigned)min(jl + 1, nch);
+                } else if (glob_out) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its sc1 stores have completed
+                    __hip_atomic_store(pg + band, (unsigned)min(jl + 1, nch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            if (g + 1 < ngrp) {
+                landed(rnxt);
+#pragma unroll
+                for (int t = 0; t < G; ++t) rcur[t] = rnxt[t];
+            }
+        }
+    }
+}
+
 // The same wavefront over 8-byte chunks (BPP <= 4).  The chain of a frame is
 // (row chunks + rows) steps -- every band starts 64 steps after the one above it,
 // so with 16-byte chunks 4,096 of a 4096^2 RGBA frame's 5,120 steps are that lag --
@@ -1774,10 +1956,20 @@ hipError_t launch_png_resolve(const PngImgDev* imgs, const int2* rows, int nrows
     return hipGetLastError();
 }
 
+// IK_PNG_UNF_BLK=0: the interleaved band layout (every hand-off across CUs; A/B)
+bool png_unfilter_blocked() {
+    static const bool blk = [] {
+        const char* e = getenv("IK_PNG_UNF_BLK");
+        const char* n = getenv("IK_PNG_UNF8");  // (the 8-byte-chunk variant keeps the interleaved layout)
+        return !(e && !strcmp(e, "0")) && !(n && !strcmp(n, "1"));
+    }();
+    return blk;
+}
+
 hipError_t launch_png_unfilter(const PngImgDev* imgs, const int2* groups, int ngroups, const int* prog_base,
                                unsigned* prog, unsigned* ticket, int bpp, hipStream_t s) {
     if (ngroups <= 0) return hipSuccess;
-    const dim3 grid(ngroups), block(kPngUnfilterThreads);
+    const dim3 grid(ngroups), block(png_unfilter_blocked() ? kPngUnfBlkWaves * 64 : kPngUnfilterThreads);
     // IK_PNG_UNF8=1: 8-byte chunks (measured slower on MI355X: 15.3 vs 8.7 ms per
     // 64 4096^2 RGBA frames, beside the next batch's block search)
     static const bool narrow = [] {
@@ -1800,7 +1992,12 @@ hipError_t launch_png_unfilter(const PngImgDev* imgs, const int2* groups, int ng
         const char* e = getenv("IK_PNG_UNF_SWAR");
         return !(e && !strcmp(e, "0"));
     }();
-#define IK_UNF(B, W) hipLaunchKernelGGL((k_png_unfilter<B, W>), grid, block, 0, s, imgs, groups, prog_base, prog, ticket)
+    const bool blk = png_unfilter_blocked();
+#define IK_UNF(B, W)                                                                                            \
+    do {                                                                                                        \
+        if (blk) hipLaunchKernelGGL((k_png_unfilter_blk<B, W>), grid, block, 0, s, imgs, groups, prog_base, prog, ticket); \
+        else hipLaunchKernelGGL((k_png_unfilter<B, W>), grid, block, 0, s, imgs, groups, prog_base, prog, ticket);    \
+    } while (0)
     switch (bpp) {
     case 1: IK_UNF(1, false); break;
     case 2: IK_UNF(2, false); break;

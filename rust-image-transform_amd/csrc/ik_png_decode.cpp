@@ -751,7 +751,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             nrows += j->h;
             npages += (j->raw_total >> kPngPageShift) + 1;
             nbands += ((size_t)j->h + 63) / 64;
-            ngroups += (size_t)png_unfilter_groups((int)j->h);
+            ngroups += (size_t)(png_unfilter_blocked() ? png_unfilter_blk_groups((int)j->h) : png_unfilter_groups((int)j->h));
         }
         // unfilter: band-group table + per-image band offsets (staged), then one
         // progress counter per band and one ticket per class (zeroed)
@@ -1072,7 +1072,8 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                         const Range r{bpp, (int)cls.size(), (int)groups.size()};
                         for (int k = 0; k < m; ++k)
                             if (J[k]->state == 1 && hd[k].bpp == bpp) {
-                                for (int g = 0; g < png_unfilter_groups(hd[k].H); ++g)
+                                for (int g = 0; g < (png_unfilter_blocked() ? png_unfilter_blk_groups(hd[k].H)
+                                                                            : png_unfilter_groups(hd[k].H)); ++g)
                                     groups.push_back(make_int2((int)cls.size() - r.img0, g));
                                 pbase.push_back(band0);
                                 band0 += (hd[k].H + 63) / 64;
