@@ -1956,12 +1956,16 @@ hipError_t launch_png_resolve(const PngImgDev* imgs, const int2* rows, int nrows
     return hipGetLastError();
 }
 
-// IK_PNG_UNF_BLK=0: the interleaved band layout (every hand-off across CUs; A/B)
+// IK_PNG_UNF_BLK=1: blocked bands (LDS hand-off inside a 4-wave workgroup).  Off by
+// default: measured 10.8 vs 7.8 ms per step against the interleaved layout
+// (profiles/r03s_unfilter_blk.txt) -- the four waves of a block sit on one CU and
+// wait on each other in a chain, where interleaved bands of different images fill
+// the CU's other slots.
 bool png_unfilter_blocked() {
     static const bool blk = [] {
         const char* e = getenv("IK_PNG_UNF_BLK");
         const char* n = getenv("IK_PNG_UNF8");  // (the 8-byte-chunk variant keeps the interleaved layout)
-        return !(e && !strcmp(e, "0")) && !(n && !strcmp(n, "1"));
+        return e && !strcmp(e, "1") && !(n && !strcmp(n, "1"));
     }();
     return blk;
 }
