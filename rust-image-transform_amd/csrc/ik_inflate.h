@@ -243,6 +243,21 @@ IK_HD_COLD void fixed_lens(uint8_t* lens) {
     for (int i = 0; i < 30; ++i) lens[288 + i] = 5;
 }
 
+// Kraft sum of a dynamic header's code-length code, in units of 2^-7 (complete =
+// 128).  `cl` holds the 3-bit code-length-code lengths from bit 0 (57 bits; bits
+// past the ncode fields may be anything); `T` maps 9 bits (three lengths) to the
+// sum of 2^(7 - len) over its nonzero lengths.  Shifting the ncode fields to the
+// top of the word drops the absent ones and leaves zeros below, and as 64 = 1 mod
+// 3, every field then starts at a bit = 1 (mod 3): seven aligned 9-bit groups from
+// bit 1 cover them, absent lengths reading as 0 -- no mask by ncode.
+template <class Tab>
+IK_HD uint32_t cl_kraft_top(uint64_t cl, int ncode, Tab T) {
+    const uint64_t x = cl << (64 - 3 * ncode);  // ncode 4..19: shift 52..7
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    return (uint32_t)T[(xl >> 1) & 511u] + T[(xl >> 10) & 511u] + T[(xl >> 19) & 511u] +
+           T[((xl >> 28) | (xh << 4)) & 511u] + T[(xh >> 5) & 511u] + T[(xh >> 14) & 511u] + T[xh >> 23];
+}
+
 // The finder's full header check, streaming: decodes the code lengths with the
 // caller's 128-entry code-length-code table (LDS; entry = symbol | length << 5)
 // and keeps only running sums -- no length arrays -- rejecting as soon as the
@@ -315,6 +330,117 @@ IK_HD bool dynamic_header_ok(const uint32_t* words, uint64_t nbits, uint64_t bit
                 if (val > maxd) maxd = val;
             }
         }
+        i += rep;
+        prev = val;
+    }
+    if (!eob) return false;
+    if (kl != 32768u && !(maxl == 1 && kl == 16384u)) return false;
+    if (kd != 0u && kd != 32768u && !(maxd == 1 && kd == 16384u)) return false;
+    return true;
+}
+
+// dynamic_header_ok's test shaped for the GPU block search's flush (k_png_find),
+// where 64 lanes check 64 candidates at once and the wave waits for its slowest
+// lane: the code-length code is decoded canonically -- left-justified limits,
+// first codes and rank offsets packed bytewise in registers, the symbols by rank 5
+// bits each in two more -- so no 128-entry table is built per candidate and the
+// loop's dependent chain touches memory once per 32 bits (the window word); one
+// refill per code length (32 bits cover a code of <= 7 bits and its <= 7 repeat
+// bits), the repeat codes decoded without branches.  Same accept set as
+// dynamic_header_ok (the CPU model holds the two equal on every candidate of its
+// streams).  Win: fetch(w) loads stream words w .. w + 31, word(k) reads the k-th.
+IK_HD uint32_t rev32(uint32_t v);
+template <class Win>
+IK_HD bool dynamic_header_win(uint64_t p, uint32_t h, uint64_t bits, Win& win) {
+    const int nlen = (int)((h >> 3) & 31u) + 257, ndist = (int)((h >> 8) & 31u) + 1;
+    const int ncode = (int)((h >> 13) & 15u) + 4;
+    // code-length code: count per length, then ranks in canonical (length, symbol) order
+    constexpr uint8_t inv_order[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};
+    uint64_t cnt = 0;  // byte L: codes of length L (L = 1..7)
+IK_UNROLL
+    for (int s = 0; s < 19; ++s) {
+        const int i = inv_order[s];
+        const uint32_t len = i < ncode ? (uint32_t)(bits >> (3 * i)) & 7u : 0u;
+        if (len) cnt += 1ull << (8 * len);
+    }
+    uint64_t first = 0, offs = 0, lim = 0;  // bytes L: first code, rank of the first code, left-justified limit
+    {
+        uint32_t code = 0, rank = 0;
+IK_UNROLL
+        for (int L = 1; L <= 7; ++L) {
+            const uint32_t cprev = L > 1 ? (uint32_t)(cnt >> (8 * (L - 1))) & 255u : 0u;
+            const uint32_t cl = (uint32_t)(cnt >> (8 * L)) & 255u;
+            code = (code + cprev) << 1;
+            first |= (uint64_t)code << (8 * L);
+            offs |= (uint64_t)rank << (8 * L);
+            lim |= (uint64_t)((code + cl) << (7 - L)) << (8 * L);
+            rank += cl;
+        }
+    }
+    // the symbols by canonical rank, 5 bits each in two registers (ranks 0..11, 12..18):
+    // a register select per code length, not an LDS round trip on the loop's chain
+    uint64_t sy_lo = 0, sy_hi = 0;
+    {
+        uint64_t ctr = 0;  // byte L: symbols of length L placed so far
+IK_UNROLL
+        for (int s = 0; s < 19; ++s) {
+            const int i = inv_order[s];
+            const uint32_t len = i < ncode ? (uint32_t)(bits >> (3 * i)) & 7u : 0u;
+            if (len) {
+                const uint32_t r = ((uint32_t)(offs >> (8 * len)) & 255u) + ((uint32_t)(ctr >> (8 * len)) & 255u);
+                if (r < 12) sy_lo |= (uint64_t)s << (5 * r);
+                else sy_hi |= (uint64_t)s << (5 * (r - 12));
+                ctr += 1ull << (8 * len);
+            }
+        }
+    }
+    const uint64_t bit = p + 17 + 3 * (uint64_t)ncode;
+    uint64_t wb = bit >> 5;  // window base (word index)
+    win.fetch(wb);
+    uint64_t buf = (uint64_t)(win.word(0) >> (bit & 31));
+    int n = 32 - (int)(bit & 31);
+    uint32_t k = 1;  // next window word
+    const int total = nlen + ndist;
+    int i = 0, prev = -1;
+    uint32_t kl = 0, kd = 0;
+    int maxl = 0, maxd = 0;
+    bool eob = false;
+    // one refill per code length: 32 bits in the buffer cover a code (<= 7 bits) and
+    // its repeat bits (<= 7); the repeat symbols are decoded without branches (the
+    // lanes of a flush hold different symbols, so branches ran every path anyway)
+    while (i < total) {
+        if (n < 32) {
+            if (k == 32) {
+                wb += 32;
+                win.fetch(wb);
+                k = 0;
+            }
+            buf |= (uint64_t)win.word(k) << n;
+            n += 32;
+            ++k;
+        }
+        const uint32_t c = rev32((uint32_t)buf) >> 25;  // the next 7 bits, first bit as MSB
+        int L = 1;
+IK_UNROLL
+        for (int l = 1; l < 7; ++l) L += c >= ((uint32_t)(lim >> (8 * l)) & 255u) ? 1 : 0;
+        const uint32_t r = (c >> (7 - L)) - ((uint32_t)(first >> (8 * L)) & 255u) + ((uint32_t)(offs >> (8 * L)) & 255u);
+        const int sym = (int)((r < 12 ? sy_lo >> (5 * r) : sy_hi >> (5 * (r - 12))) & 31u);
+        const int xb = sym < 16 ? 0 : sym == 16 ? 2 : sym == 17 ? 3 : 7;  // repeat bits
+        const int rep = sym < 16 ? 1 : (sym == 18 ? 11 : 3) + (int)((uint32_t)(buf >> L) & ((1u << xb) - 1u));
+        buf >>= L + xb;
+        n -= L + xb;
+        const int val = sym < 16 ? sym : sym == 16 ? prev : 0;
+        if ((sym == 16 && prev < 0) || i + rep > total) return false;
+        // the run's lengths split between the literal/length and distance codes
+        const int nl = i < nlen ? (i + rep <= nlen ? rep : nlen - i) : 0;
+        const int nd = rep - nl;
+        const uint32_t w = val ? 1u << (15 - val) : 0u;
+        kl += (uint32_t)nl * w;
+        kd += (uint32_t)nd * w;
+        if (kl > 32768u || kd > 32768u) return false;
+        maxl = nl && val > maxl ? val : maxl;
+        maxd = nd && val > maxd ? val : maxd;
+        eob = eob || (val && i <= 256 && 256 < i + nl);
         i += rep;
         prev = val;
     }

@@ -119,8 +119,9 @@ hipError_t png_find_prof_read(unsigned long long* out);  // dev build: k_png_fin
 #endif
 hipError_t launch_png_find(const PngImgDev* imgs, const int* chunk_img, const int* chunk_idx, int n,
                            uint64_t chunk_bits, int64_t* cand, hipStream_t s);
-hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, int n, uint16_t* tok,
-                             infl::LaneResult* res, hipStream_t s);
+// order (nullable): launch slot -> lane index; lane t's result goes to res[t]
+hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, const uint32_t* order, int n,
+                             uint16_t* tok, infl::LaneResult* res, hipStream_t s);
 hipError_t launch_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int n, const uint16_t* tok, int* status,
                              hipStream_t s);
 hipError_t launch_png_resolve(const PngImgDev* imgs, const int2* rows, int nrows, int* err, hipStream_t s);

@@ -68,64 +68,23 @@ __device__ __forceinline__ void raise_priority() { __builtin_amdgcn_s_setprio(3)
 //    loads in flight (refetched when the decode runs past them), so the symbol
 //    loop waits on LDS, not on one dependent global load per word;
 //  - the code-length code is decoded canonically (its left-justified limits,
-//    first codes and rank offsets packed bytewise in registers; the symbols in
-//    canonical order, 19 bytes per lane in LDS), so no 128-entry table is built
-//    per candidate.
-// win: this lane's window, word k at win[64 k]; syms: its 19 symbol bytes, entry
-// i at syms[64 i].
+//    first codes and rank offsets packed bytewise in registers, the symbols by
+//    rank 5 bits each in two more), so no 128-entry table is built per candidate
+//    and the loop's chain has one LDS access (the window word) per 32 bits;
+//  - one refill per code length and the repeat codes decoded without branches.
+// win: this lane's window, word k at win[64 k].
 typedef __attribute__((address_space(3))) uint32_t lds_word;
-typedef __attribute__((address_space(3))) uint8_t lds_byte;
-__device__ __attribute__((noinline)) bool find_check_win(const IK_GLOBAL uint32_t* W, uint64_t nbits, uint64_t p,
-                                                         uint32_t h, uint64_t bits, lds_word* win, lds_byte* syms) {
-    const int nlen = (int)((h >> 3) & 31u) + 257, ndist = (int)((h >> 8) & 31u) + 1;
-    const int ncode = (int)((h >> 13) & 15u) + 4;
-    // code-length code: count per length, then ranks in canonical (length, symbol) order
-    constexpr uint8_t inv_order[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};
-    uint64_t cnt = 0;  // byte L: codes of length L (L = 1..7)
-#pragma unroll
-    for (int s = 0; s < 19; ++s) {
-        const int i = inv_order[s];
-        const uint32_t len = i < ncode ? (uint32_t)(bits >> (3 * i)) & 7u : 0u;
-        if (len) cnt += 1ull << (8 * len);
-    }
-    uint64_t first = 0, offs = 0, lim = 0;  // bytes L: first code, rank of the first code, left-justified limit
-    {
-        uint32_t code = 0, rank = 0;
-#pragma unroll
-        for (int L = 1; L <= 7; ++L) {
-            const uint32_t cprev = L > 1 ? (uint32_t)(cnt >> (8 * (L - 1))) & 255u : 0u;
-            const uint32_t cl = (uint32_t)(cnt >> (8 * L)) & 255u;
-            code = (code + cprev) << 1;
-            first |= (uint64_t)code << (8 * L);
-            offs |= (uint64_t)rank << (8 * L);
-            lim |= (uint64_t)((code + cl) << (7 - L)) << (8 * L);
-            rank += cl;
-        }
-    }
-    {
-        uint64_t ctr = 0;  // byte L: symbols of length L placed so far
-#pragma unroll
-        for (int s = 0; s < 19; ++s) {
-            const int i = inv_order[s];
-            const uint32_t len = i < ncode ? (uint32_t)(bits >> (3 * i)) & 7u : 0u;
-            if (len) {
-                const uint32_t r = ((uint32_t)(offs >> (8 * len)) & 255u) + ((uint32_t)(ctr >> (8 * len)) & 255u);
-                syms[64 * r] = (uint8_t)s;
-                ctr += 1ull << (8 * len);
-            }
-        }
-    }
-    // bit reader over the LDS window
-    const uint64_t wend = (nbits >> 5) + 4;  // words past it read as zero (as infl::Bits)
-    const uint64_t bit = p + 17 + 3 * (uint64_t)ncode;
-    uint64_t wb = bit >> 5;  // window base (word index)
-    // 32 words by LDS-DMA (global_load_lds_dword: lane l's word lands at M0 + 4 l, so
-    // row k of the lane-minor window takes one instruction for the whole wave), all
-    // in flight at once, no VGPRs; near the end of the stream (past the zero padding
-    // the window could reach) word by word with the bounds check
-    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    const uint32_t r0 = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)win - 4u * lane);  // row 0, lane 0
-    auto fetch = [&](uint64_t base) {
+// The lane's stream window for infl::dynamic_header_win: 32 words by LDS-DMA
+// (global_load_lds_dword: lane l's word lands at M0 + 4 l, so row k of the
+// lane-minor window takes one instruction for the whole wave), all in flight at
+// once, no VGPRs; near the end of the stream (past the zero padding the window
+// could reach) word by word with the bounds check.
+struct FindWin {
+    const IK_GLOBAL uint32_t* W;
+    uint64_t wend;  // words past it read as zero (as infl::Bits)
+    lds_word* win;  // this lane's word 0; word k at win[64 k]
+    uint32_t r0;    // LDS address of row 0, lane 0 (wave-uniform)
+    __device__ void fetch(uint64_t base) {
         if (base + 32 > wend + 64) {
             for (int k = 0; k < 32; ++k) win[64 * k] = base + k < wend ? W[base + k] : 0u;
             return;
@@ -144,80 +103,15 @@ __device__ __attribute__((noinline)) bool find_check_win(const IK_GLOBAL uint32_
         IK_FWIN(24); IK_FWIN(25); IK_FWIN(26); IK_FWIN(27); IK_FWIN(28); IK_FWIN(29); IK_FWIN(30); IK_FWIN(31);
 #undef IK_FWIN
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    };
-    fetch(wb);
-    uint64_t buf = (uint64_t)(win[0] >> (bit & 31));
-    int n = 32 - (int)(bit & 31);
-    uint32_t k = 1;  // next window word
-    auto refill = [&]() {
-        if (n < 32) {
-            if (k == 32) {
-                wb += 32;
-                fetch(wb);
-                k = 0;
-            }
-            buf |= (uint64_t)win[64 * k] << n;
-            n += 32;
-            ++k;
-        }
-    };
-    auto get = [&](int bitsn) {
-        refill();
-        const uint32_t v = (uint32_t)buf & ((1u << bitsn) - 1u);
-        buf >>= bitsn;
-        n -= bitsn;
-        return v;
-    };
-    const int total = nlen + ndist;
-    int i = 0, prev = -1;
-    uint32_t kl = 0, kd = 0;
-    int maxl = 0, maxd = 0;
-    bool eob = false;
-    while (i < total) {
-        refill();
-        const uint32_t c = __builtin_bitreverse32((uint32_t)buf) >> 25;  // the next 7 bits, first bit as MSB
-        int L = 1;
-#pragma unroll
-        for (int l = 1; l < 7; ++l) L += c >= ((uint32_t)(lim >> (8 * l)) & 255u) ? 1 : 0;
-        const uint32_t r = (c >> (7 - L)) - ((uint32_t)(first >> (8 * L)) & 255u) + ((uint32_t)(offs >> (8 * L)) & 255u);
-        const int sym = syms[64 * r];
-        buf >>= L;
-        n -= L;
-        int rep = 1, val = sym;
-        if (sym == 16) {
-            if (prev < 0) return false;
-            val = prev;
-            rep = 3 + (int)get(2);
-        } else if (sym == 17) {
-            val = 0;
-            rep = 3 + (int)get(3);
-        } else if (sym == 18) {
-            val = 0;
-            rep = 11 + (int)get(7);
-        }
-        if (i + rep > total) return false;
-        if (val) {
-            const int nl = i < nlen ? (i + rep <= nlen ? rep : nlen - i) : 0;
-            const int nd = rep - nl;
-            if (nl) {
-                kl += (uint32_t)nl << (15 - val);
-                if (kl > 32768u) return false;
-                if (val > maxl) maxl = val;
-                if (i <= 256 && 256 < i + nl) eob = true;
-            }
-            if (nd) {
-                kd += (uint32_t)nd << (15 - val);
-                if (kd > 32768u) return false;
-                if (val > maxd) maxd = val;
-            }
-        }
-        i += rep;
-        prev = val;
     }
-    if (!eob) return false;
-    if (kl != 32768u && !(maxl == 1 && kl == 16384u)) return false;
-    if (kd != 0u && kd != 32768u && !(maxd == 1 && kd == 16384u)) return false;
-    return true;
+    __device__ uint32_t word(uint32_t k) const { return win[64 * k]; }
+};
+
+__device__ __attribute__((noinline)) bool find_check_win(const IK_GLOBAL uint32_t* W, uint64_t nbits, uint64_t p,
+                                                         uint32_t h, uint64_t bits, lds_word* win) {
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    FindWin fw{W, (nbits >> 5) + 4, win, (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(size_t)win - 4u * lane)};
+    return infl::dynamic_header_win(p, h, bits, fw);
 }
 
 __device__ __forceinline__ uint32_t fsh(uint32_t lo, uint32_t hi, int k) {  // bits k .. k+31 of hi:lo, 0 < k < 32
@@ -261,7 +155,6 @@ hipError_t png_find_prof_read(unsigned long long* out) {
 __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const int* chunk_img, const int* chunk_idx,
                                                  int nchunks_total, uint64_t chunk_bits, int64_t* cand) {
     __shared__ uint32_t s_win[64 * 32];     // per lane: 32 stream words of the candidate being checked (lane-minor)
-    __shared__ uint8_t s_sym[64 * 20];      // per lane: code-length-code symbols in canonical order (lane-minor)
     __shared__ uint32_t s_q[kFindQueue];    // Kraft-passing offsets (relative to the chunk) awaiting the full check
     __shared__ uint8_t s_kraft[512];        // 3 code-length-code lengths (9 bits) -> sum of 2^(7 - len), len > 0
     const int g = blockIdx.x;
@@ -314,7 +207,7 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
                 (void)x; (void)cl;
                 v = off;
 #else
-                if (find_check_win(W, I.nbits, p, (uint32_t)x, cl, (lds_word*)(s_win + lane), (lds_byte*)(s_sym + lane)))
+                if (find_check_win(W, I.nbits, p, (uint32_t)x, cl, (lds_word*)(s_win + lane)))
                     v = off;
 #endif
             }
@@ -350,17 +243,11 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
         while (m) {
             const uint32_t j = (uint32_t)__builtin_ctz(m);
             m &= m - 1u;
-            const uint32_t h = (uint32_t)(lo >> j);
             const uint32_t sh = j + 17;  // 17 .. 48
             const uint64_t cl = (lo >> sh) | (hi << (64 - sh));  // code-length code lengths (57 bits)
-            const int ncode = (int)((h >> 13) & 15u) + 4;
-            const uint64_t used = cl & (ncode == 19 ? 0x1FFFFFFFFFFFFFFull : ((1ull << (3 * ncode)) - 1ull));
-            // Kraft sum over the 19 lengths, three at a time from the LDS table
-            const uint32_t ulo = (uint32_t)used, uhi = (uint32_t)(used >> 32);
-            uint32_t kraft = s_kraft[ulo & 511u] + s_kraft[(ulo >> 9) & 511u] + s_kraft[(ulo >> 18) & 511u] +
-                             s_kraft[((ulo >> 27) | (uhi << 5)) & 511u] + s_kraft[(uhi >> 4) & 511u] +
-                             s_kraft[(uhi >> 13) & 511u] + s_kraft[(uhi >> 22) & 7u];
-            if (kraft == 128u) km |= 1u << j;
+            const int ncode = (int)((uint32_t)(lo >> (j + 13)) & 15u) + 4;
+            // Kraft sum over the ncode lengths, three at a time from the LDS table
+            if (infl::cl_kraft_top(cl, ncode, s_kraft) == 128u) km |= 1u << j;
         }
         // queue them: one per lane per round, compacted by lane rank
         for (;;) {
@@ -505,11 +392,13 @@ struct WinLds {
 };
 
 __global__ __launch_bounds__(kPngInflateThreads) void k_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes,
-                                                                   int nlanes, uint16_t* tok, infl::LaneResult* res) {
+                                                                   const uint32_t* order, int nlanes, uint16_t* tok,
+                                                                   infl::LaneResult* res) {
     __shared__ uint32_t s_tab[kPngInflateThreads * infl::kCanonWords];  // lane-minor (LaneLds)
     __shared__ uint32_t s_ring[4 * kRingBW * 64];                        // 4 blocks x 32 B per lane, lane-minor
-    const int t = blockIdx.x * kPngInflateThreads + threadIdx.x;
-    if (t >= nlanes) return;
+    const int slot = blockIdx.x * kPngInflateThreads + threadIdx.x;
+    if (slot >= nlanes) return;
+    const int t = order ? (int)order[slot] : slot;  // launch order (ik_png_decode.cpp order_lanes)
     const PngLaneDev L = lanes[t];
     const PngImgDev I = imgs[L.img];
     const LaneLds m{(lds_u32*)s_tab + threadIdx.x};
@@ -1929,11 +1818,11 @@ hipError_t launch_png_find(const PngImgDev* imgs, const int* chunk_img, const in
     return hipGetLastError();
 }
 
-hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, int n, uint16_t* tok,
-                             infl::LaneResult* res, hipStream_t s) {
+hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, const uint32_t* order, int n,
+                             uint16_t* tok, infl::LaneResult* res, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const dim3 grid((n + kPngInflateThreads - 1) / kPngInflateThreads);
-    hipLaunchKernelGGL(k_png_decode, grid, dim3(kPngInflateThreads), 0, s, imgs, lanes, n, tok, res);
+    hipLaunchKernelGGL(k_png_decode, grid, dim3(kPngInflateThreads), 0, s, imgs, lanes, order, n, tok, res);
     return hipGetLastError();
 }
 

@@ -236,6 +236,7 @@ struct HostTables {
     std::vector<int64_t> cand, obase;
     std::vector<PngLaneDev> lanes;
     std::vector<std::pair<int, int>> who;
+    std::vector<uint32_t> order;
     std::vector<infl::LaneResult> res;
     std::vector<int2> rows;
 };
@@ -698,38 +699,42 @@ void png_find_prelaunch(PngUpload& up, hipStream_t s) {
 // length, longest first, fill the first half of the waves; the second half takes
 // the shortest first, so wave i and wave W/2 + i -- which the dispatcher puts on
 // the same SIMD, one round of waves apart -- pair a long group with a short one
-// and the long wave runs alone once its partner is done.  Results go back through
-// `who`, which is permuted with the lanes.  IK_PNG_LANE_ORDER=0: job order (A/B).
-static void order_lanes(std::vector<PngLaneDev>& hl, std::vector<std::pair<int, int>>& who,
-                        const std::vector<PngJob*>& J) {
+// and the long wave runs alone once its partner is done.  The kernel reads lane
+// order[slot] at launch slot `slot` and writes that lane's result in place, so the
+// lane table and its results keep job order.  Returns false (no order table) for
+// small launches and under IK_PNG_LANE_ORDER=0 (A/B).
+static bool order_lanes(const std::vector<PngLaneDev>& hl, const std::vector<PngJob*>& J,
+                        std::vector<uint32_t>& order) {
     static const bool on = [] {
         const char* e = getenv("IK_PNG_LANE_ORDER");
         return !(e && !strcmp(e, "0"));
     }();
     const size_t n = hl.size();
-    if (!on || n < 2 * 64) return;
-    std::vector<uint64_t> len(n);
+    if (!on || n < 2 * 64) return false;
+    // counting sort on the length in 512-bit buckets, longest first: O(n), as this
+    // sits on the host between the decode rounds
+    constexpr uint32_t kBuckets = 1024;
+    thread_local std::vector<uint16_t> key;
+    thread_local std::vector<uint32_t> cnt;
+    key.resize(n);
+    cnt.assign(kBuckets + 1, 0);
     for (size_t t = 0; t < n; ++t) {
-        const uint64_t end = hl[t].stop == ~0ull ? J[hl[t].img]->nbits : hl[t].stop;
-        len[t] = end > hl[t].start ? end - hl[t].start : 0;
+        const PngLaneDev& L = hl[t];
+        const uint64_t end = L.stop == ~0ull ? J[L.img]->nbits : L.stop;
+        const uint64_t len = end > L.start ? end - L.start : 0;
+        const uint32_t b = kBuckets - 1 - (uint32_t)std::min<uint64_t>(len >> 9, kBuckets - 1);  // longest -> 0
+        key[t] = (uint16_t)b;
+        ++cnt[b + 1];
     }
-    std::vector<uint32_t> idx(n);
-    for (size_t t = 0; t < n; ++t) idx[t] = (uint32_t)t;
-    std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return len[a] > len[b]; });
-    const size_t waves = (n + 63) / 64, half = (waves + 1) / 2;
-    std::vector<uint32_t> pos;  // launch position -> sorted index
-    pos.reserve(n);
-    const size_t nlong = std::min(n, half * 64);
-    for (size_t t = 0; t < nlong; ++t) pos.push_back(idx[t]);
-    for (size_t t = n; t > nlong; --t) pos.push_back(idx[t - 1]);  // shortest first
-    std::vector<PngLaneDev> h2(n);
-    std::vector<std::pair<int, int>> w2(n);
+    for (uint32_t b = 0; b < kBuckets; ++b) cnt[b + 1] += cnt[b];
+    // sorted rank r -> launch slot: ranks [0, nlong) in order, then the rest reversed
+    const size_t waves = (n + 63) / 64, nlong = std::min(n, (waves + 1) / 2 * 64);
+    order.resize(n);
     for (size_t t = 0; t < n; ++t) {
-        h2[t] = hl[pos[t]];
-        w2[t] = who[pos[t]];
+        const size_t r = cnt[key[t]]++;
+        order[r < nlong ? r : n - 1 - (r - nlong)] = (uint32_t)t;
     }
-    hl.swap(h2);
-    who.swap(w2);
+    return true;
 }
 
 int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* msgs) {
@@ -786,7 +791,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         tok_total += tok_total / 2 + 64;
         size_t dyn = up256(sizeof(PngLaneDev) * max_lanes) + up256(sizeof(infl::LaneResult) * max_lanes) +
                      up256(sizeof(int64_t) * max_lanes) + up256(2 * sizeof(int) * max_lanes) +
-                     up256(sizeof(PngImgDev) * m);
+                     up256(sizeof(uint32_t) * max_lanes) + up256(sizeof(PngImgDev) * m);
         size_t nrows = 0, npages = 0, nbands = 0, ngroups = 0;
         for (PngJob* j : J) {
             nrows += j->h;
@@ -805,6 +810,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         infl::LaneResult* d_res = nullptr;
         int64_t* d_obase = nullptr;
         int* d_xst = nullptr;
+        uint32_t* d_order = nullptr;
         PngImgDev* d_cls = nullptr;
         int2* d_rows = nullptr;
         int* d_pages = nullptr;
@@ -820,6 +826,8 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             o += up256(sizeof(int64_t) * max_lanes);
             d_xst = reinterpret_cast<int*>(dev + o);
             o += up256(2 * sizeof(int) * max_lanes);
+            d_order = reinterpret_cast<uint32_t*>(dev + o);
+            o += up256(sizeof(uint32_t) * max_lanes);
             d_cls = reinterpret_cast<PngImgDev*>(dev + o);
             o += up256(sizeof(PngImgDev) * m);
             d_rows = reinterpret_cast<int2*>(dev + o);
@@ -833,7 +841,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         uint64_t tok_used = 0;
         Xfer X;
         if (!rc && !X.init(2 * sizeof(PngLaneDev) * max_lanes + sizeof(infl::LaneResult) * max_lanes +
-                               sizeof(int64_t) * (max_lanes + nchunks) + 2 * sizeof(int) * max_lanes +
+                               sizeof(int64_t) * (max_lanes + nchunks) + 3 * sizeof(int) * max_lanes +
                                sizeof(int2) * (nrows + ngroups) + sizeof(int) * (npages + 4 * m) +
                                3 * sizeof(PngImgDev) * m + 2 * sizeof(int) * nchunks + (64u << 10), s))
             rc = fail(IK_ERR_NOMEM, "cannot allocate pinned PNG transfer area");
@@ -905,6 +913,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         std::vector<PngLaneDev>& hl = ht.lanes;
         std::vector<std::pair<int, int>>& who = ht.who;  // (job, lane) of each launched lane
         std::vector<infl::LaneResult>& hres = ht.res;
+        std::vector<uint32_t>& lane_order = ht.order;  // launch slot -> lane (order_lanes)
         hl.clear();
         who.clear();
         hres.clear();
@@ -947,13 +956,17 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             }
             if (hl.empty()) break;
             if (hl.size() > max_lanes) { rc = fail(IK_ERR_DEVICE, "PNG lane table overflow"); break; }
-            order_lanes(hl, who, J);
+            const bool ordered = order_lanes(hl, J, lane_order);
             const size_t lb = sizeof(PngLaneDev) * hl.size();
-            if (X.h2d(d_lanes, hl.data(), lb) != hipSuccess) { rc = fail(IK_ERR_DEVICE, "PNG lane table upload"); break; }
+            if (X.h2d(d_lanes, hl.data(), lb) != hipSuccess ||
+                (ordered && X.h2d(d_order, lane_order.data(), sizeof(uint32_t) * hl.size()) != hipSuccess)) {
+                rc = fail(IK_ERR_DEVICE, "PNG lane table upload");
+                break;
+            }
             hres.resize(hl.size());
             if (!mk[0]) mk[0] = now_ms();  // plan built, lanes uploaded (first round)
             rec(2, s);
-            hipError_t e2 = launch_png_decode(d_imgs, d_lanes, (int)hl.size(), d_tok, d_res, s);
+            hipError_t e2 = launch_png_decode(d_imgs, d_lanes, ordered ? d_order : nullptr, (int)hl.size(), d_tok, d_res, s);
             rec(3, s);
             // the lane results come back behind the decode; the next batch's block
             // search (the stage executor's hook) queues behind that copy, so it runs

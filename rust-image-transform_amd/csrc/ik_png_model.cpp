@@ -18,6 +18,35 @@
 
 using namespace ik;
 
+namespace {
+// the window of infl::dynamic_header_win over host words (the GPU's is LDS, k_png_find)
+struct HostWin {
+    const uint32_t* W;
+    uint64_t wend;
+    uint32_t w[32];
+    void fetch(uint64_t base) {
+        for (int k = 0; k < 32; ++k) w[k] = base + k < wend ? W[base + k] : 0u;
+    }
+    uint32_t word(uint32_t k) const { return w[k]; }
+};
+// 9 bits (three code-length-code lengths) -> sum of 2^(7 - len) (k_png_find's s_kraft)
+struct KraftTab {
+    uint8_t t[512];
+    KraftTab() {
+        for (int v = 0; v < 512; ++v) {
+            uint32_t k = 0;
+            for (int f = 0; f < 3; ++f) {
+                const uint32_t l = ((uint32_t)v >> (3 * f)) & 7u;
+                k += l ? (128u >> l) : 0u;
+            }
+            t[v] = (uint8_t)k;
+        }
+    }
+};
+const KraftTab g_kraft;
+const uint8_t* const kraft_tab = g_kraft.t;
+}  // namespace
+
 extern "C" {
 
 // zlib stream -> inflated bytes through the chunked parallel algorithm.
@@ -54,10 +83,13 @@ int ikm_inflate_chunked(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8
                 const int l = (int)((bits >> (3 * i)) & 7u);
                 if (l) { kraft += 128 >> l; ++nz; }
             }
+            if ((infl::cl_kraft_top(bits, ncode, kraft_tab) == 128u) != (kraft == 128 && nz)) return -10;
             if (kraft != 128 || !nz) continue;
             uint8_t tab[128];
             const bool fast = infl::dynamic_header_ok(words.data(), nbits, p, h, bits, tab);
-            if (fast != infl::plausible_dynamic(words.data(), nbits, p)) return -9;  // the two checks must agree
+            if (fast != infl::plausible_dynamic(words.data(), nbits, p)) return -9;  // the checks must agree
+            HostWin hw{words.data(), (nbits >> 5) + 4, {}};
+            if (fast != infl::dynamic_header_win(p, h, bits, hw)) return -11;  // (the GPU search's check)
             if (fast) {
                 cand[c] = (int64_t)p;
                 ++found;
@@ -311,6 +343,37 @@ extern "C" long ikm_unfilter_word_check(void) {
             const uint32_t got = ik::unfilter_word(X, A, B, C, ms, mu, mv, mp);
             for (int k = 0; k < 4; ++k)
                 bad += (int)((got >> (8 * k)) & 255u) != ref(ft, xv[k], av[k], bv[k], cv[k]);
+        }
+    }
+    return bad;
+}
+
+// infl::cl_kraft_top (the block search's Kraft sum with the absent code-length
+// lengths shifted out) against the plain sum over the ncode lengths, on pseudo-
+// random 57-bit fields with random garbage above them.  Returns the mismatches.
+extern "C" long ikm_cl_kraft_check(long n) {
+    uint8_t T[512];
+    for (int v = 0; v < 512; ++v) {
+        uint32_t k = 0;
+        for (int f = 0; f < 3; ++f) {
+            const uint32_t l = ((uint32_t)v >> (3 * f)) & 7u;
+            k += l ? (128u >> l) : 0u;
+        }
+        T[v] = (uint8_t)k;
+    }
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    long bad = 0;
+    for (long t = 0; t < n; ++t) {
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        uint64_t cl = x;
+        if (t & 1) cl &= 0x1249249249249249ull * 3;  // many short lengths: sums near 128 more often
+        for (int ncode = 4; ncode <= 19; ++ncode) {
+            uint32_t ref = 0;
+            for (int i = 0; i < ncode; ++i) {
+                const uint32_t l = (uint32_t)(cl >> (3 * i)) & 7u;
+                ref += l ? (128u >> l) : 0u;
+            }
+            if (infl::cl_kraft_top(cl, ncode, (const uint8_t*)T) != ref) ++bad;
         }
     }
     return bad;

@@ -154,3 +154,12 @@ def test_unfilter_word_equals_bytewise_definition():
     L = ctypes.CDLL(MODEL)
     L.ikm_unfilter_word_check.restype = ctypes.c_long
     assert L.ikm_unfilter_word_check() == 0
+
+
+def test_block_search_kraft_sum_equals_definition():
+    """cl_kraft_top (k_png_find's Kraft test, absent lengths shifted out) equals the
+    plain sum of 2^(7 - len) over a header's ncode code-length-code lengths."""
+    L = ctypes.CDLL(MODEL)
+    L.ikm_cl_kraft_check.restype = ctypes.c_long
+    L.ikm_cl_kraft_check.argtypes = [ctypes.c_long]
+    assert L.ikm_cl_kraft_check(200000) == 0
