@@ -53,25 +53,15 @@ __device__ __forceinline__ void raise_priority() { __builtin_amdgcn_s_setprio(3)
 // all of their top four bits set) -- and only the survivors (about a fifth)
 // take the scalar Kraft test of the code-length code (complete: sum 2^-len == 1).
 // Offsets passing it (~0.1 %: under two per wave step) go into a per-wave LDS
-// queue, and the streaming header check (find_check_win: infl::dynamic_header_ok's
-// test over an LDS window of the stream) runs on 64 queued offsets at a time,
-// one per lane -- run one by one as they turn up, it would take the whole wave
-// for one or two active lanes.  The result is the first offset of the chunk that passes
-// every test, as before: the queue is checked whenever it holds 64 offsets and at
-// the end of the chunk, and once some offset passed, the smallest passing one of
-// everything checked so far is the answer.
-// The same test as infl::dynamic_header_ok (the same accept set: the CPU model's
-// search uses that one), shaped for the GPU's flush, where 64 lanes check 64
-// candidates at once and the wave waits for its slowest lane (a true header's
-// ~300 code lengths, a false one's median ~32):
-//  - the lane's next 32 stream words are fetched into its LDS window with all 32
-//    loads in flight (refetched when the decode runs past them), so the symbol
-//    loop waits on LDS, not on one dependent global load per word;
-//  - the code-length code is decoded canonically (its left-justified limits,
-//    first codes and rank offsets packed bytewise in registers, the symbols by
-//    rank 5 bits each in two more), so no 128-entry table is built per candidate
-//    and the loop's chain has one LDS access (the window word) per 32 bits;
-//  - one refill per code length and the repeat codes decoded without branches.
+// queue, and the streaming header check (find_check_win: infl::dynamic_header_win,
+// dynamic_header_ok's test over an LDS window of the stream) runs on 64 queued
+// offsets at a time, one per lane -- run one by one as they turn up, it would
+// take the whole wave for one or two active lanes.  The queue is checked whenever
+// it holds 64 offsets (its first 64; the rest wait for the next check) and at the
+// end of the chunk; the search stops at the first check that passes an offset,
+// with the smallest passing one of that check.  It need not be the chunk's first
+// header: any block start serves as a lane start, and an offset that passes the
+// check but starts no block is dropped by the decode's chain check.
 // win: this lane's window, word k at win[64 k].
 typedef __attribute__((address_space(3))) uint32_t lds_word;
 // The lane's stream window for infl::dynamic_header_win: 32 words by LDS-DMA
@@ -185,15 +175,20 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
     const unsigned long long t_begin = __builtin_readcyclecounter();
     unsigned long long t_flush = 0, n_flush = 0, n_steps = 0, n_cand = 0;
 #endif
-    auto flush = [&]() {
+    // check the queue: all of it at the end of the chunk (all), else its first 64
+    // entries, the rest moving to the front for the next check -- one candidate
+    // past 64 would otherwise take a check round of its own, the wave waiting on
+    // its one lane for up to a true header's ~300 code lengths
+    auto flush = [&](bool all) {
+        const uint32_t take = all || qlen < 64 ? qlen : 64u;
 #ifdef IK_FIND_PROF
         const unsigned long long tf0 = __builtin_readcyclecounter();
-        n_flush += qlen ? 1 : 0;
-        n_cand += qlen;
+        n_flush += take ? 1 : 0;
+        n_cand += take;
 #endif
-        for (uint32_t q0 = 0; q0 < qlen; q0 += 64) {
+        for (uint32_t q0 = 0; q0 < take; q0 += 64) {
             uint32_t v = 0xFFFFFFFFu;
-            if (q0 + (uint32_t)lane < qlen) {
+            if (q0 + (uint32_t)lane < take) {
                 const uint32_t off = s_q[q0 + lane];
                 const uint64_t p = b0 + off;
                 const uint64_t wi = p >> 5;
@@ -214,7 +209,10 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
             v = wave_min(v);
             best = v < best ? v : best;
         }
-        qlen = 0;
+        const uint32_t rest = qlen - take;  // < 64 (the queue holds < 128)
+        const uint32_t moved = (uint32_t)lane < rest ? s_q[take + lane] : 0u;
+        if ((uint32_t)lane < rest) s_q[lane] = moved;
+        qlen = rest;
 #ifdef IK_FIND_PROF
         t_flush += __builtin_readcyclecounter() - tf0;
 #endif
@@ -253,7 +251,7 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
         for (;;) {
             const unsigned long long bal = __ballot(km != 0);
             if (!bal) break;
-            if (qlen + 64 > kFindQueue) flush();
+            if (qlen + 64 > kFindQueue) flush(false);
             if (km) {
                 const uint32_t j = (uint32_t)__builtin_ctz(km);
                 km &= km - 1u;
@@ -263,15 +261,15 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
             qlen += (uint32_t)__popcll(bal);
         }
 #ifdef IK_FIND_FLUSH_AT  // dev experiment: check the queue as soon as it holds this many
-        if (qlen >= IK_FIND_FLUSH_AT) flush();
+        if (qlen >= IK_FIND_FLUSH_AT) flush(false);
 #else
-        if (qlen >= 64) flush();
+        if (qlen >= 64) flush(false);
 #endif
-        if (best != 0xFFFFFFFFu) break;  // (flush below checks what this step queued after it)
+        if (best != 0xFFFFFFFFu) break;  // any header that passes will do (the decode chain checks it)
         wi = wn;
         if (wi - (uint64_t)lane >= wlast) break;
     }
-    flush();
+    if (best == 0xFFFFFFFFu) flush(true);
     if (lane == 0) cand[g] = best == 0xFFFFFFFFu ? -1 : (int64_t)(b0 + best);
 #ifdef IK_FIND_PROF
     if (lane == 0) {
