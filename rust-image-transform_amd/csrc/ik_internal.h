@@ -150,8 +150,14 @@ struct JpegScanArgs {
     int16_t* coef;                // [block][64] natural order, pre-zeroed
     int* err;                     // set non-zero on a bad code (the host then redoes the scan)
     int lanes;                    // intervals per 64-lane workgroup (64, or fewer to cut divergence)
+    // progressive scans (k_jpeg_prog): 1 DC first, 2 DC refine, 3 AC first, 4 AC refine
+    int kind, Ss, Se, Al;
 };
 hipError_t launch_jpeg_huff(const JpegScanArgs& a, hipStream_t s);
+// One progressive scan with restart intervals (ik_jpeg.hip k_jpeg_prog): a lane per
+// interval, the EOB run and DC predictions reset at each RSTn; the scans of an
+// image run in stream order, each refining the coefficients of the ones before.
+hipError_t launch_jpeg_prog(const JpegScanArgs& a, hipStream_t s);
 // Baseline scans WITHOUT restart markers (ik_jpeg.hip k_jpeg_seq_sync / k_jpeg_seq_decode):
 // the unstuffed scan is cut into subsequences of L bits; a lane owns the blocks
 // whose first bit lies in its subsequence.  Sync rounds find each subsequence's

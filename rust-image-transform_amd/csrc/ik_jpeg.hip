@@ -394,7 +394,20 @@ struct GpuBits {
             if ((int)(fetched - pos) < 128) chunk();
     }
     __device__ uint32_t byte_at(uint32_t o) const { return (ring[(o >> 2) & (kRingDw - 1)] >> ((o & 3) * 8)) & 0xffu; }
-    __device__ void fill() {
+    __device__ void fill() {  // called with n < 16
+        // four bytes at once when none of them is 0xFF (no stuffing, no marker):
+        // entropy-coded data holds an 0xFF in about 1 of 256 bytes
+        if (!marker && pos + 4 <= size && (int)(fetched - pos) >= 4) {
+            const uint32_t w0 = ring[(pos >> 2) & (kRingDw - 1)], w1 = ring[((pos >> 2) + 1) & (kRingDw - 1)];
+            const uint32_t x = __builtin_amdgcn_alignbyte(w1, w0, pos & 3u);  // bytes pos .. pos+3, little-endian
+            const uint32_t nx = ~x;
+            if (!((nx - 0x01010101u) & ~nx & 0x80808080u)) {
+                acc |= (unsigned long long)__builtin_bswap32(x) << (32 - n);
+                n += 32;
+                pos += 4;
+                return;
+            }
+        }
         while (n <= 56) {
             uint32_t v = 0;
             if (!marker && pos < size) {
@@ -526,16 +539,132 @@ __global__ __launch_bounds__(kHuffThreads) void k_jpeg_huff(JpegScanArgs a) {
 }
 
 // a batch of scans: grid.y = scan, each with its own tables; `lanes` intervals per workgroup
+// The rings are dynamic LDS, one per decoding lane (`lanes` x (kRingDw + 1) dwords):
+// sized for all 64 threads they cost 16.6 KB per workgroup, which with 16 lanes
+// held a CU to four workgroups.
 __global__ __launch_bounds__(kHuffThreads) void k_jpeg_huff_batch(const JpegScanArgs* __restrict__ scans, int lanes) {
     __shared__ JpegHuffTables T;
     __shared__ uint8_t s_zz[64];
-    __shared__ uint32_t s_ring[kHuffThreads][kRingDw + 1];  // +1: lanes' rings start in different banks
+    extern __shared__ uint32_t s_rings[];  // +1 dword per ring: lanes' rings start in different banks
     const JpegScanArgs a = scans[blockIdx.y];
     if ((int)blockIdx.x * lanes >= a.n_seg) return;  // whole workgroup past this scan's intervals
     load_tables(a.tabs, T, s_zz);
     __syncthreads();
     const int seg = blockIdx.x * lanes + threadIdx.x;
-    if ((int)threadIdx.x < lanes && seg < a.n_seg) huff_interval(a, T, s_zz, s_ring[threadIdx.x], seg);
+    if ((int)threadIdx.x < lanes && seg < a.n_seg) huff_interval(a, T, s_zz, s_rings + threadIdx.x * (kRingDw + 1), seg);
+}
+
+// ---- progressive scans with restart intervals ----------------------------------
+// One lane per restart interval of one scan (ITU T.81 G.1.2; the host decoder's
+// block_dc_first / block_dc_refine / block_ac_first / block_ac_refine, libjpeg
+// jdphuff.c): the interval's DC predictions and EOB run start at zero, so the
+// intervals are independent; a refinement scan reads the coefficients the scans
+// before it wrote, which the stream order of the launches guarantees.
+__device__ void prog_interval(const JpegScanArgs& a, const JpegHuffTables& T, const uint8_t* s_zz, uint32_t* ring,
+                              int seg) {
+    GpuBits br;
+    br.g = reinterpret_cast<const uint32_t*>(a.data);
+    br.ring = ring;
+    br.pos = a.seg[seg];
+    br.fetched = br.pos & ~3u;
+    br.size = (uint32_t)a.size;
+    br.acc = 0;
+    br.n = 0;
+    br.marker = false;
+    int pred[4] = {0, 0, 0, 0};
+    int eobrun = 0;
+    const int kind = a.kind, Ss = a.Ss, Se = a.Se, Al = a.Al;
+    const int p1 = 1 << Al, m1 = -p1;
+    const long long m0 = (long long)seg * a.restart;
+    const int nm = (int)min((long long)a.restart, a.total_mcu - m0);
+    const int row_len = a.single ? a.single_bw : a.mcux;
+    int mx = (int)(m0 % row_len), my = (int)(m0 / row_len);
+    for (int i = 0; i < nm; ++i) {
+        for (int ci = 0; ci < a.ns; ++ci) {
+            const int nby = a.single ? 1 : a.v[ci], nbx = a.single ? 1 : a.h[ci];
+            for (int by = 0; by < nby; ++by)
+                for (int bx = 0; bx < nbx; ++bx) {
+                    const long long bi = a.single ? a.blk0[ci] + (long long)my * a.bw[ci] + mx
+                                                  : a.blk0[ci] + (long long)(my * a.v[ci] + by) * a.bw[ci] + mx * a.h[ci] + bx;
+                    int16_t* blk = a.coef + bi * 64;
+                    br.top_up();
+                    if (kind == 1) {  // DC first
+                        const int t = decode_sym(br, T, a.td[ci]);
+                        if (t < 0 || t > 11) { atomicOr(a.err, 1); return; }
+                        pred[ci] += t ? extend_dev(br.get(t), t) : 0;
+                        blk[0] = (int16_t)(pred[ci] * p1);
+                    } else if (kind == 2) {  // DC refine
+                        if (br.get(1)) blk[0] = (int16_t)(blk[0] | p1);
+                    } else if (kind == 3) {  // AC first
+                        if (eobrun > 0) { --eobrun; continue; }
+                        for (int k = Ss; k <= Se; ++k) {
+                            const int rs = decode_sym(br, T, 4 + a.ta[ci]);
+                            if (rs < 0) { atomicOr(a.err, 2); return; }
+                            const int r = rs >> 4, sz = rs & 15;
+                            if (sz) {
+                                k += r;
+                                if (k > Se) { atomicOr(a.err, 4); return; }
+                                blk[s_zz[k]] = (int16_t)(extend_dev(br.get(sz), sz) * p1);
+                            } else if (r == 15) {
+                                k += 15;
+                            } else {
+                                eobrun = (1 << r) + (r ? br.get(r) : 0) - 1;
+                                break;
+                            }
+                        }
+                    } else {  // AC refine
+                        int k = Ss;
+                        if (eobrun == 0) {
+                            for (; k <= Se; ++k) {
+                                const int rs = decode_sym(br, T, 4 + a.ta[ci]);
+                                if (rs < 0) { atomicOr(a.err, 2); return; }
+                                int r = rs >> 4, val = 0;
+                                const int sz = rs & 15;
+                                if (sz) {
+                                    if (sz != 1) { atomicOr(a.err, 8); return; }
+                                    val = br.get(1) ? p1 : m1;
+                                } else if (r != 15) {
+                                    eobrun = (1 << r) + (r ? br.get(r) : 0);
+                                    break;  // the rest of the band: the EOB-run pass below
+                                }
+                                // skip r zero-history coefficients, refining the nonzero ones passed
+                                do {
+                                    int16_t* co = blk + s_zz[k];
+                                    if (*co != 0) {
+                                        if (br.get(1) && (*co & p1) == 0) *co = (int16_t)(*co >= 0 ? *co + p1 : *co + m1);
+                                    } else if (--r < 0) {
+                                        break;
+                                    }
+                                    ++k;
+                                } while (k <= Se);
+                                if (val) {
+                                    if (k > Se) { atomicOr(a.err, 4); return; }
+                                    blk[s_zz[k]] = (int16_t)val;
+                                }
+                            }
+                        }
+                        if (eobrun > 0) {
+                            for (; k <= Se; ++k) {
+                                int16_t* co = blk + s_zz[k];
+                                if (*co != 0 && br.get(1) && (*co & p1) == 0) *co = (int16_t)(*co >= 0 ? *co + p1 : *co + m1);
+                            }
+                            --eobrun;
+                        }
+                    }
+                }
+        }
+        if (++mx == row_len) { mx = 0; ++my; }
+    }
+}
+
+__global__ __launch_bounds__(kHuffThreads) void k_jpeg_prog(JpegScanArgs a) {
+    __shared__ JpegHuffTables T;
+    __shared__ uint8_t s_zz[64];
+    extern __shared__ uint32_t s_rings[];  // a.lanes rings of kRingDw + 1 dwords
+    load_tables(a.tabs, T, s_zz);
+    __syncthreads();
+    const int seg = blockIdx.x * a.lanes + threadIdx.x;
+    if ((int)threadIdx.x < a.lanes && seg < a.n_seg) prog_interval(a, T, s_zz, s_rings + threadIdx.x * (kRingDw + 1), seg);
 }
 
 // ---- baseline scans without restart markers: self-synchronising decoding ------
@@ -713,7 +842,7 @@ int huff_lanes(int dflt) {
 
 int jpeg_lanes_for(long long total) {
     int want = 1;
-    while (want < 16 && (long long)want * 2 * 1024 <= total) want *= 2;
+    while (want < 32 && (long long)want * 2 * 1024 <= total) want *= 2;
     return huff_lanes(want);
 }
 
@@ -729,16 +858,29 @@ hipError_t launch_jpeg_huff(const JpegScanArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+hipError_t launch_jpeg_prog(const JpegScanArgs& a, hipStream_t s) {
+    if (a.n_seg <= 0 || a.restart <= 0 || a.ns < 1 || a.ns > 4 || a.kind < 1 || a.kind > 4 || a.Ss < 0 || a.Se > 63 ||
+        a.Al > 13)
+        return hipErrorInvalidValue;
+    JpegScanArgs b = a;
+    b.lanes = jpeg_lanes_for(a.n_seg);
+    hipLaunchKernelGGL(k_jpeg_prog, dim3((a.n_seg + b.lanes - 1) / b.lanes), dim3(kHuffThreads),
+                       sizeof(uint32_t) * (kRingDw + 1) * b.lanes, s, b);
+    return hipGetLastError();
+}
+
 hipError_t launch_jpeg_huff_batch(const JpegScanArgs* dev_scans, int n, int max_seg, hipStream_t s) {
     if (n <= 0 || max_seg <= 0 || n > 65535) return hipErrorInvalidValue;
     // many intervals: pack total/1024 per wave (about a thousand waves in flight;
-    // measured on 32 x 256 intervals: 1 -> 97 ms, 2 -> 72, 4 -> 59, 8 -> 51 ms)
+    // measured on 32 x 256 intervals: 1 -> 97 ms, 2 -> 72, 4 -> 59, 8 -> 51 ms; with
+    // the rings sized per lane, configs[2]'s 256 x 256 intervals: 16 -> 162, 32 ->
+    // 148, 64 -> 148 ms per step, profiles/r03x_jpeg_lanes.txt)
     const long long total = (long long)n * max_seg;
     int want = 1;
-    while (want < 16 && (long long)want * 2 * 1024 <= total) want *= 2;
+    while (want < 32 && (long long)want * 2 * 1024 <= total) want *= 2;
     const int lanes = huff_lanes(want);
-    hipLaunchKernelGGL(k_jpeg_huff_batch, dim3((max_seg + lanes - 1) / lanes, n), dim3(kHuffThreads), 0,
-                       s, dev_scans, lanes);
+    hipLaunchKernelGGL(k_jpeg_huff_batch, dim3((max_seg + lanes - 1) / lanes, n), dim3(kHuffThreads),
+                       sizeof(uint32_t) * (kRingDw + 1) * lanes, s, dev_scans, lanes);
     return hipGetLastError();
 }
 

@@ -140,6 +140,16 @@ bool seq_enabled() {
 }
 constexpr size_t kSeqMinBytes = 32 << 10;  // smaller scans: the host decoder is faster
 
+// Progressive scans with restart intervals on the GPU (k_jpeg_prog);
+// IK_JPEG_PROG=0 keeps them on the host entropy decoder.
+bool prog_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("IK_JPEG_PROG");
+        return !(e && !strcmp(e, "0"));
+    }();
+    return on;
+}
+
 struct Decoder {
     const uint8_t* b;
     const uint8_t* end;
@@ -158,6 +168,16 @@ struct Decoder {
     const uint8_t* gpu_data = nullptr;
     std::vector<unsigned> gpu_segs;
     JpegScanArgs gpu_scan{};
+    // progressive scans with restart intervals, recorded for k_jpeg_prog (all of
+    // the image's scans, in order: one the GPU cannot take sends the image to the
+    // host decoder, or keeps it there from the first scan on)
+    struct ProgScan {
+        JpegScanArgs a;
+        std::vector<unsigned> segs;
+        JpegHuffTables tabs;
+    };
+    std::vector<ProgScan> prog;
+    bool prog_host = false;
     // baseline scan without restart markers (self-synchronising GPU decoding)
     bool seq = false;
     std::vector<uint32_t> seq_words;  // unstuffed scan, big-endian words
@@ -353,6 +373,31 @@ struct Decoder {
         return true;
     }
 
+    // Record a progressive scan with restart intervals for k_jpeg_prog, as
+    // defer_scan records a baseline one; a.data holds the scan's offset in the file.
+    bool defer_prog(const std::vector<int>& order, int kind, int Ss, int Se, int Al, const uint8_t* data,
+                    const uint8_t*& next) {
+        const uint8_t* nx = next;
+        std::vector<unsigned> keep;
+        keep.swap(gpu_segs);
+        const bool ok = defer_scan(order, data, nx);
+        deferred = false;  // (defer_scan's single-scan record is not used)
+        ProgScan ps;
+        ps.segs.swap(gpu_segs);
+        gpu_segs.swap(keep);
+        if (!ok) return false;
+        ps.a = gpu_scan;
+        ps.a.data = reinterpret_cast<const uint8_t*>((uintptr_t)(data - b));
+        ps.a.kind = kind;
+        ps.a.Ss = Ss;
+        ps.a.Se = Se;
+        ps.a.Al = Al;
+        tables(ps.tabs);
+        prog.push_back(std::move(ps));
+        next = nx;
+        return true;
+    }
+
     // Record a baseline scan without restart markers for k_jpeg_seq_*: unstuff it
     // (0xFF 0x00 -> 0xFF) up to the first marker into big-endian words.
     bool defer_seq(const std::vector<int>& order, const uint8_t* data, const uint8_t*& next) {
@@ -471,6 +516,15 @@ struct Decoder {
         if (deferred) {  // a second scan: the whole image goes through the host decoder
             need_host = true;
             return IK_OK;
+        }
+        if (try_gpu && progressive && !prog_host && prog_enabled()) {
+            scanned = true;
+            if (restart > 0 && defer_prog(order, kind, Ss, Se, Al, se, next)) return IK_OK;
+            if (!prog.empty()) {  // a later scan the GPU cannot take: all scans on the host
+                need_host = true;
+                return IK_OK;
+            }
+            prog_host = true;  // the first scan: this and every later one on the host
         }
         const bool first_scan = !scanned;
         scanned = true;
@@ -862,7 +916,9 @@ int run_seq(const Decoder& d, const uint8_t* dtabs, int16_t* dcoef, uint8_t* dev
 }
 
 // try_gpu: baseline scans with restart intervals are entropy-decoded on the GPU
-// (k_jpeg_huff); anything else, and any stream the GPU finds a bad code in, goes
+// (k_jpeg_huff), restart-free baseline scans by self-synchronising decoding
+// (k_jpeg_seq_*), progressive scans with restart intervals scan by scan
+// (k_jpeg_prog); anything else, and any stream the GPU finds a bad code in, goes
 // through the host decoder
 // process-wide: JPEG streams whose entropy decoding ran on the GPU / on the host
 std::atomic<unsigned long long> g_jpeg_gpu_streams{0}, g_jpeg_host_streams{0};
@@ -902,7 +958,30 @@ int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gp
     const size_t t_off = pl_off + (plane_bytes + 255) / 256 * 256;
     const size_t e_off = t_off + tbytes, s_off = e_off + 256, d_off = s_off + sbytes;
     const size_t q_off = up256(d_off + dbytes + 1024);  // the restart bit reader fetches 64-B chunks past the end
-    uint8_t* dev = scratch(q_off + (gpu && seq ? seq_bytes(d) : 0));
+    // progressive scans on the GPU: [the file (+ reader slack)][error flag][per scan:
+    // tables, interval starts], staged in one host buffer and copied at once
+    const bool prog = !d.prog.empty();
+    std::vector<uint8_t> pstage;
+    std::vector<size_t> ptab_off, pseg_off;
+    size_t p_err = 0;
+    if (prog) {
+        size_t o = up256(n + 1024);
+        p_err = o;
+        o += 256;
+        for (const auto& ps : d.prog) {
+            ptab_off.push_back(o);
+            o += up256(sizeof(JpegHuffTables));
+            pseg_off.push_back(o);
+            o += up256(ps.segs.size() * sizeof(unsigned));
+        }
+        pstage.assign(o, 0);
+        std::memcpy(pstage.data(), bytes, n);
+        for (size_t k = 0; k < d.prog.size(); ++k) {
+            std::memcpy(pstage.data() + ptab_off[k], &d.prog[k].tabs, sizeof(JpegHuffTables));
+            std::memcpy(pstage.data() + pseg_off[k], d.prog[k].segs.data(), d.prog[k].segs.size() * sizeof(unsigned));
+        }
+    }
+    uint8_t* dev = scratch(q_off + (gpu && seq ? seq_bytes(d) : 0) + pstage.size());
     if (!dev) { ik_image_free(img); return fail(IK_ERR_DEVICE, "cannot allocate device scratch"); }
     hipStream_t s = thread_stream();
     st = copy_h2d_2d(dev, qbytes, reinterpret_cast<const uint8_t*>(q.data()), qbytes, qbytes, 1, s);
@@ -945,6 +1024,30 @@ int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gp
                 return decode_jpeg_impl(bytes, n, out, false);
             }
         }
+    } else if (!st && prog) {
+        uint8_t* pb = dev + q_off;
+        st = copy_h2d_2d(pb, pstage.size(), pstage.data(), pstage.size(), pstage.size(), 1, s);
+        if (!st) {
+            hipError_t e = hipMemsetAsync(dev + qbytes, 0, cbytes, s);
+            int* d_err = reinterpret_cast<int*>(pb + p_err);
+            for (size_t k = 0; k < d.prog.size() && e == hipSuccess; ++k) {
+                JpegScanArgs a = d.prog[k].a;
+                a.data = pb + (size_t)(uintptr_t)a.data;  // the scan's offset in the file
+                a.seg = reinterpret_cast<const unsigned*>(pb + pseg_off[k]);
+                a.tabs = reinterpret_cast<const JpegHuffTables*>(pb + ptab_off[k]);
+                a.coef = reinterpret_cast<int16_t*>(dev + qbytes);
+                a.err = d_err;
+                e = launch_jpeg_prog(a, s);
+            }
+            int err = 0;
+            if (e == hipSuccess) e = hipMemcpyAsync(&err, d_err, sizeof(int), hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) { ik_image_free(img); return hip_fail(e, "jpeg progressive entropy decode"); }
+            if (err) {  // a bad code somewhere: the host decoder reports it
+                ik_image_free(img);
+                return decode_jpeg_impl(bytes, n, out, false);
+            }
+        }
     } else if (!st && cbytes) {
         st = copy_h2d_2d(dev + qbytes, cbytes, reinterpret_cast<const uint8_t*>(d.coef.data()), cbytes, cbytes, 1, s);
     }
@@ -958,8 +1061,8 @@ int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gp
     if (e != hipSuccess) { ik_image_free(img); return hip_fail(e, "jpeg reconstruct"); }
     if (timing)
         fprintf(stderr, "[jpeg] %s: parse %.2f alloc %.2f entropy/upload %.2f reconstruct %.2f ms\n",
-                gpu ? "gpu entropy" : "host entropy", t1 - t0, t2 - t1, t3 - t2, now() - t3);
-    (gpu ? g_jpeg_gpu_streams : g_jpeg_host_streams) += 1;
+                gpu || prog ? "gpu entropy" : "host entropy", t1 - t0, t2 - t1, t3 - t2, now() - t3);
+    (gpu || prog ? g_jpeg_gpu_streams : g_jpeg_host_streams) += 1;
     *out = img;
     return IK_OK;
 }
@@ -991,7 +1094,7 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
         outs[i] = nullptr;
         if (st[i]) continue;
         if (ds[i]->deferred && !ds[i]->need_host && !ds[i]->seq) gpu_idx.push_back(i);
-        else if (ds[i]->seq && !ds[i]->need_host) seq_idx.push_back(i);
+        else if ((ds[i]->seq || !ds[i]->prog.empty()) && !ds[i]->need_host) seq_idx.push_back(i);  // one by one, GPU
         else host_idx.push_back(i);
     }
     // 2. the deferred scans: one device allocation, one Huffman launch over all of them

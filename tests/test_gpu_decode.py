@@ -87,6 +87,79 @@ def test_jpeg_progressive_gray_and_restarts(ik):
     np.testing.assert_array_equal(img.to_array(), np.asarray(Image.open(io.BytesIO(b))))
 
 
+def _jpeg_counts(ik):
+    import ctypes
+    c = (ctypes.c_ulonglong * 2)()
+    assert ik.ik_jpeg_counters(c) == 0
+    return c[0], c[1]
+
+
+@pytest.mark.parametrize("wh,sub,q,rst", [
+    ((640, 480), 2, 90, {"restart_marker_rows": 1}),
+    ((333, 211), 0, 75, {"restart_marker_blocks": 5}),
+    ((1000, 700), 1, 95, {"restart_marker_rows": 2}),
+    ((64, 64), 2, 30, {"restart_marker_blocks": 1}),
+    ((17, 9), 0, 50, {"restart_marker_blocks": 2}),
+    ((2048, 1536), 2, 85, {"restart_marker_rows": 1}),
+])
+def test_jpeg_progressive_restarts_entropy_decoded_on_the_gpu(ik, wh, sub, q, rst):
+    """Progressive scans with restart intervals (DC first/refine, AC first with EOB
+    runs, AC refine) go through k_jpeg_prog, one lane per interval, scan after scan:
+    equal to libjpeg-turbo, and the stream counted as GPU-decoded, not host."""
+    w, h = wh
+    b = _jpeg(ikutil.synth(w, h, 3, seed=w + h + q, pattern="N" if q == 95 else "S"), quality=q, subsampling=sub,
+              progressive=True, **rst)
+    assert b"\xff\xc2" in b and b"\xff\xdd" in b
+    g0, h0 = _jpeg_counts(ik)
+    img, fmt = decode_image(b)
+    g1, h1 = _jpeg_counts(ik)
+    assert fmt is ImageFormat.jpeg
+    assert (g1 - g0, h1 - h0) == (1, 0)
+    np.testing.assert_array_equal(img.to_array(), np.asarray(Image.open(io.BytesIO(b))))
+
+
+def test_jpeg_progressive_restarts_gray_on_the_gpu(ik):
+    g = ikutil.synth(257, 131, 1, seed=9)[..., 0]
+    b = _jpeg(g, quality=88, progressive=True, restart_marker_blocks=4)
+    g0, h0 = _jpeg_counts(ik)
+    img, _ = decode_image(b)
+    g1, h1 = _jpeg_counts(ik)
+    assert (g1 - g0, h1 - h0) == (1, 0)
+    np.testing.assert_array_equal(img.to_array()[..., 0], np.asarray(Image.open(io.BytesIO(b))))
+
+
+def test_jpeg_progressive_without_restarts_stays_on_the_host(ik):
+    # a restart-free progressive scan is one serial bitstream: the host decoder
+    b = _jpeg(ikutil.synth(120, 80, 3, seed=11), quality=80, progressive=True)
+    g0, h0 = _jpeg_counts(ik)
+    img, _ = decode_image(b)
+    g1, h1 = _jpeg_counts(ik)
+    assert (g1 - g0, h1 - h0) == (0, 1)
+    np.testing.assert_array_equal(img.to_array(), np.asarray(Image.open(io.BytesIO(b))))
+
+
+def test_jpeg_progressive_restarts_corrupt_interval_gives_the_host_answer(ik):
+    # a bad code in one interval: the GPU flags it and the host decoder decides
+    b = bytearray(_jpeg(ikutil.synth(320, 240, 3, seed=12), quality=85, progressive=True,
+                        restart_marker_rows=1))
+    sos = [i for i in range(len(b) - 1) if b[i] == 0xFF and b[i + 1] == 0xDA]
+    k = sos[len(sos) // 2] + 40  # inside a middle scan's data
+    for j in range(k, k + 8):
+        if b[j] != 0xFF and b[j - 1] != 0xFF:
+            b[j] ^= 0x5A
+    b = bytes(b)
+    try:
+        ref = np.asarray(Image.open(io.BytesIO(b)))
+    except OSError:
+        ref = None
+    try:
+        img, _ = decode_image(b)
+        if ref is not None:
+            assert img.to_array().shape == ref.shape
+    except TransformError as e:
+        assert "Jpeg" in str(e) or "jpeg" in str(e)
+
+
 def test_jpeg_truncated_progressive_is_an_error_or_partial(ik):
     # a stream cut inside its entropy data decodes like libjpeg (missing bits read as
     # zeros) or fails with the reference's error string, never crashes
