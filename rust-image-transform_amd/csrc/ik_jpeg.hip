@@ -326,11 +326,78 @@ __device__ __forceinline__ void color_pixel(const JpegGeom& g, int x, int y, uin
 // per thread for RGB, 1 for gray; rows are 256-B pitched, so 4 pixels start on a
 // 4-byte boundary) instead of three byte stores per pixel; a partial group at the
 // row's end is stored byte by byte.
+// zune YCbCr with chroma at half width (4:2:0 / 4:2:2) and full-resolution luma,
+// four pixels x0 .. x0+3 away from the row's ends (x0 >= 4, x0 + 3 < 2n - 2; n =
+// the chroma plane's padded width): upsampled_zune's interior formulas and
+// color_pixel's arithmetic on whole dwords -- one luma dword, four chroma bytes
+// per row and plane -- instead of per-sample byte loads and the generic branches.
+__device__ __forceinline__ bool zune_fast(const JpegGeom& g) {
+    return g.recon == IK_JPEG_RECON_ZUNE && g.colorspace == 1 && g.ncomp == 3 && g.h[0] == g.hmax &&
+           g.v[0] == g.vmax && g.hmax == 2 * g.h[1] && g.hmax == 2 * g.h[2] && g.v[1] == g.v[2] &&
+           (g.vmax == g.v[1] || g.vmax == 2 * g.v[1]) && g.bw[1] == g.bw[2] && g.bh[1] == g.bh[2];
+}
+
+// bytes i .. i+3 of a 4-B-aligned row (i odd here, so both dwords hold bytes used:
+// no read past the row)
+__device__ __forceinline__ uint32_t bytes4(const uint8_t* p, uint32_t i) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(p) + (i >> 2);
+    return __builtin_amdgcn_alignbyte(w[1], w[0], i & 3u);
+}
+
+__device__ __forceinline__ void color4_zune(const JpegGeom& g, int x0, int y, uint8_t* px) {
+    const int fv = g.vmax / g.v[1];
+    const int nY = g.bw[0] * 8, n = g.bw[1] * 8, ph = g.bh[1] * 8;
+    const uint32_t yv = *reinterpret_cast<const uint32_t*>(g.planes + g.plane0[0] + (size_t)y * nY + x0);
+    const int Y = fv == 2 ? y >> 1 : y;
+    int r1 = fv == 2 ? ((y & 1) ? Y + 1 : Y - 1) : Y;
+    r1 = r1 < 0 ? 0 : (r1 >= ph ? ph - 1 : r1);
+    const uint32_t i = (uint32_t)x0 >> 1;  // samples i-1 .. i+2 of the chroma row
+    int at[2][4];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const uint8_t* p = g.planes + g.plane0[1 + c];
+        const uint32_t a = bytes4(p + (size_t)Y * n, i - 1), b = bytes4(p + (size_t)r1 * n, i - 1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int s0 = (int)((a >> (8 * k)) & 255u), s1 = (int)((b >> (8 * k)) & 255u);
+            at[c][k] = fv == 2 ? (s0 * 3 + s1 + 2) >> 2 : s0;
+        }
+    }
+    // pixel x0 + j: even -> (at(i') * 3 + at(i' - 1) + 2) >> 2, odd -> (at(i') * 3 + at(i' + 1) + 2) >> 2,
+    // i' = (x0 + j) >> 1; at index k <-> sample i - 1 + k
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int ip = 1 + (j >> 1), nb = (j & 1) ? ip + 1 : ip - 1;
+        const int c0 = (int)((yv >> (8 * j)) & 255u);
+        const int c1 = (at[0][ip] * 3 + at[0][nb] + 2) >> 2, c2 = (at[1][ip] * 3 + at[1][nb] + 2) >> 2;
+        const int16_t cb = (int16_t)(c1 - 128), cr = (int16_t)(c2 - 128);
+        const int r = c0 + ((int16_t)(45 * cr) >> 5);
+        const int gg = c0 - ((int16_t)(11 * cb + 23 * cr) >> 5);
+        const int b = c0 + ((int16_t)(113 * cb) >> 6);
+        px[3 * j] = clamp255(r);
+        px[3 * j + 1] = clamp255(gg);
+        px[3 * j + 2] = clamp255(b);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restrict__ dst, size_t pitch) {
     const int x0 = 4 * (blockIdx.x * 256 + threadIdx.x), y = blockIdx.y;
     if (x0 >= g.W) return;
     const int C = g.colorspace == 0 ? 1 : 3;
     uint8_t px[12];
+    if (zune_fast(g) && x0 >= 4 && x0 + 4 <= g.W && x0 + 3 < 2 * g.bw[1] * 8 - 2) {
+        color4_zune(g, x0, y, px);
+        uint32_t w[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            w[i] = (uint32_t)px[4 * i] | (uint32_t)px[4 * i + 1] << 8 | (uint32_t)px[4 * i + 2] << 16 |
+                   (uint32_t)px[4 * i + 3] << 24;
+        uint32_t* o32 = reinterpret_cast<uint32_t*>(dst + (size_t)y * pitch + (size_t)3 * x0);
+        o32[0] = w[0];
+        o32[1] = w[1];
+        o32[2] = w[2];
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         if (x0 + k < g.W) color_pixel(g, x0 + k, y, px + C * k);

@@ -804,7 +804,11 @@ __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const
                 } else if (sr >= -kXNear) {
                     v = s_ring[(gb + (uint32_t)sr) & M];
                 } else {
+#ifdef IK_X4_NOFAR  // dev experiment (wrong output): far sources from the ring, to bound their cost
+                    v = s_ring[(gb + (uint32_t)sr) & M];
+#else
                     v = U[ob + ab];
+#endif
                 }
                 s_ring[(gb + o + j) & M] = v;
             }

@@ -903,10 +903,12 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         tim[15] = t1 - t0;  // from the stage's start until the candidates are back (upload wait + search)
         const double t2 = now_ms();
         double mk[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // dev timing marks (IK_PNG_TIMING)
-        for (PngJob* j : J) {
+        // the lane plans, one job per pool task (the decode waits on this host work)
+        parallel_for(m, 0, [&](int k) {
+            PngJob* j = J[k];
             std::vector<int64_t> c(cand.begin() + j->chunk0, cand.begin() + j->chunk0 + j->nchunks);
             pngplan::build(c, j->lanes);
-        }
+        });
         // ---- decode rounds: token streams; the host checks the lane chain ----
         int rounds = 0, dropped = 0, overflows = 0;
         bool search_done = false;  // the next batch's block search was handed to the hook
@@ -917,35 +919,95 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         hl.clear();
         who.clear();
         hres.clear();
-        while (!rc) {
-            hl.clear();
-            who.clear();
+        // first round, in parallel: every lane of every live job is new, and the token
+        // area was sized for all of them, so each job's lanes and token regions go to
+        // fixed offsets (prefix sums over the jobs) and the jobs fill their parts at once
+        bool first_built = false;
+        {
+            std::vector<size_t> l0(m + 1, 0);
+            std::vector<uint64_t> t0(m + 1, 0);
             for (int k = 0; k < m; ++k) {
-                PngJob& j = *J[k];
-                if (j.state) continue;
-                pngplan::Lanes& LL = j.lanes;
-                for (size_t i = 0; i < LL.start.size(); ++i) {
-                    if (!LL.dirty[i]) continue;
-                    const uint64_t end = LL.stop[i] == ~0ull ? j.nbits : LL.stop[i];
-                    const uint32_t cap = infl::tok_capacity(end > LL.start[i] ? end - LL.start[i] : 0, LL.big[i] != 0);
-                    if (cap > LL.tcap[i]) {  // a (larger) region from the area
-                        const uint64_t need = cap + infl::kTokSlack;
-                        if (tok_used + need > tok_total) { reject(j, "token area full"); break; }  // host decoder
-                        LL.tbase[i] = tok_used;
-                        LL.tcap[i] = cap;
-                        tok_used += need;
+                const PngJob& j = *J[k];
+                const pngplan::Lanes& LL = j.lanes;
+                size_t nl = 0;
+                uint64_t need = 0;
+                if (!j.state)
+                    for (size_t i = 0; i < LL.start.size(); ++i) {
+                        if (!LL.dirty[i]) continue;
+                        const uint64_t end = LL.stop[i] == ~0ull ? j.nbits : LL.stop[i];
+                        const uint32_t cap = infl::tok_capacity(end > LL.start[i] ? end - LL.start[i] : 0, LL.big[i] != 0);
+                        ++nl;
+                        if (cap > LL.tcap[i]) need += cap + infl::kTokSlack;
                     }
-                    PngLaneDev L{};
-                    L.start = LL.start[i];
-                    L.stop = LL.stop[i];
-                    L.tbase = LL.tbase[i];
-                    L.ntok = LL.tcap[i];
-                    L.img = (uint32_t)k;
-                    L.first = i == 0;
-                    hl.push_back(L);
-                    who.emplace_back(k, (int)i);
+                l0[k + 1] = l0[k] + nl;
+                t0[k + 1] = t0[k] + need;
+            }
+            if (tok_used + t0[m] <= tok_total && l0[m] <= max_lanes) {
+                hl.resize(l0[m]);
+                who.resize(l0[m]);
+                parallel_for(m, 0, [&](int k) {
+                    PngJob& j = *J[k];
+                    if (j.state) return;
+                    pngplan::Lanes& LL = j.lanes;
+                    size_t t = l0[k];
+                    uint64_t tu = tok_used + t0[k];
+                    for (size_t i = 0; i < LL.start.size(); ++i) {
+                        if (!LL.dirty[i]) continue;
+                        const uint64_t end = LL.stop[i] == ~0ull ? j.nbits : LL.stop[i];
+                        const uint32_t cap = infl::tok_capacity(end > LL.start[i] ? end - LL.start[i] : 0, LL.big[i] != 0);
+                        if (cap > LL.tcap[i]) {
+                            LL.tbase[i] = tu;
+                            LL.tcap[i] = cap;
+                            tu += cap + infl::kTokSlack;
+                        }
+                        PngLaneDev L{};
+                        L.start = LL.start[i];
+                        L.stop = LL.stop[i];
+                        L.tbase = LL.tbase[i];
+                        L.ntok = LL.tcap[i];
+                        L.img = (uint32_t)k;
+                        L.first = i == 0;
+                        hl[t] = L;
+                        who[t] = {k, (int)i};
+                        ++t;
+                    }
+                });
+                tok_used += t0[m];
+                first_built = true;
+            }
+        }
+        while (!rc) {
+            if (!first_built) {
+                hl.clear();
+                who.clear();
+                for (int k = 0; k < m; ++k) {
+                    PngJob& j = *J[k];
+                    if (j.state) continue;
+                    pngplan::Lanes& LL = j.lanes;
+                    for (size_t i = 0; i < LL.start.size(); ++i) {
+                        if (!LL.dirty[i]) continue;
+                        const uint64_t end = LL.stop[i] == ~0ull ? j.nbits : LL.stop[i];
+                        const uint32_t cap = infl::tok_capacity(end > LL.start[i] ? end - LL.start[i] : 0, LL.big[i] != 0);
+                        if (cap > LL.tcap[i]) {  // a (larger) region from the area
+                            const uint64_t need = cap + infl::kTokSlack;
+                            if (tok_used + need > tok_total) { reject(j, "token area full"); break; }  // host decoder
+                            LL.tbase[i] = tok_used;
+                            LL.tcap[i] = cap;
+                            tok_used += need;
+                        }
+                        PngLaneDev L{};
+                        L.start = LL.start[i];
+                        L.stop = LL.stop[i];
+                        L.tbase = LL.tbase[i];
+                        L.ntok = LL.tcap[i];
+                        L.img = (uint32_t)k;
+                        L.first = i == 0;
+                        hl.push_back(L);
+                        who.emplace_back(k, (int)i);
+                    }
                 }
             }
+            first_built = false;
             // lanes of a job that just fell back are dropped from the launch
             if (!hl.empty()) {
                 size_t w = 0;
