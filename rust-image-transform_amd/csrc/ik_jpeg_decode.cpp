@@ -831,13 +831,21 @@ int run_seq(const Decoder& d, const uint8_t* dtabs, int16_t* dcoef, uint8_t* dev
     };
     // round 1 from the naive guesses; round 2 from its results (most already exact),
     // so that the walk below meets a chain whose starts are mostly right
+    // (IK_JPEG_SEQ_ROUNDS: GPU rounds before the walk, default 2; each round fixes
+    // at least one more lane of every unsynchronised stretch)
+    static const int max_rounds = [] {
+        const char* e = getenv("IK_JPEG_SEQ_ROUNDS");
+        const int v = e ? atoi(e) : 2;
+        return v < 1 ? 1 : (v > 64 ? 64 : v);
+    }();
     int changed = round();
-    int walked = 0;
+    int walked = 0, rounds_run = 1;
     if (changed < 0) return 1;
-    if (changed > 0) {
+    while (changed > 0 && rounds_run < max_rounds) {
         S = G;
         Sj = Gj;
         changed = round();
+        ++rounds_run;
         if (changed < 0) return 1;
     }
     if (changed > 0) {
