@@ -528,13 +528,7 @@ __device__ int decode_sym(GpuBits& br, const JpegHuffTables& T, int t) {
 
 }  // namespace
 
-// the whole interval `seg` of scan `a` (tables and `a` itself in LDS: a component
-// index picks h / v / bw / td / ta / blk0 there, where a copy in registers would
-// have to be private memory).  One loop iteration decodes one symbol of every
-// lane -- a block's DC, or one AC code -- with the block position advanced in
-// place at each block's end: lanes decoding different intervals no longer wait at
-// every block for the wave's longest block.  DC predictions in four registers
-// (selects, not an indexed array).
+// the whole interval `seg` of scan `a` (tables already in LDS)
 __device__ void huff_interval(const JpegScanArgs& a, const JpegHuffTables& T, const uint8_t* s_zz, uint32_t* ring,
                               int seg) {
     GpuBits br;
@@ -546,74 +540,51 @@ __device__ void huff_interval(const JpegScanArgs& a, const JpegHuffTables& T, co
     br.acc = 0;
     br.n = 0;
     br.marker = false;
-    int p0 = 0, p1 = 0, p2 = 0, p3 = 0;
+    int pred[4] = {0, 0, 0, 0};
     const long long m0 = (long long)seg * a.restart;
     const int nm = (int)min((long long)a.restart, a.total_mcu - m0);
     // MCU position, advanced incrementally (no 64-bit divisions per block)
-    const bool single = a.single != 0;
-    const int row_len = single ? a.single_bw : a.mcux;
-    const int ns = a.ns;
+    const int row_len = a.single ? a.single_bw : a.mcux;
     int mx = (int)(m0 % row_len), my = (int)(m0 / row_len);
-    int i = 0, ci = 0, by = 0, bx = 0, k = 0;
-    int16_t* blk = nullptr;
-    int ta = 0;
-    while (i < nm) {
-        br.top_up();
-        if (k == 0) {  // a block's DC: locate the block, then its difference
-            const int h = single ? 1 : a.h[ci], v = single ? 1 : a.v[ci];
-            const long long bi = single ? a.blk0[ci] + (long long)my * a.bw[ci] + mx
-                                        : a.blk0[ci] + (long long)(my * v + by) * a.bw[ci] + mx * h + bx;
-            blk = a.coef + bi * 64;
-            ta = a.ta[ci];
-            const int t = decode_sym(br, T, a.td[ci]);
-            if (t < 0 || t > 11) { atomicOr(a.err, 1); return; }
-            const int d = t ? extend_dev(br.get(t), t) : 0;
-            const int pr = (ci == 0 ? p0 : ci == 1 ? p1 : ci == 2 ? p2 : p3) + d;
-            p0 = ci == 0 ? pr : p0;
-            p1 = ci == 1 ? pr : p1;
-            p2 = ci == 2 ? pr : p2;
-            p3 = ci == 3 ? pr : p3;
-            blk[0] = (int16_t)pr;
-            k = 1;
-        } else {  // one AC code
-            bool end = false;
-            const int fa = T.fast_ac[ta][br.peek(9)];
-            if (fa) {  // short code + magnitude in one lookup
-                k += (fa >> 4) & 15;
-                br.skip(fa & 15);
-                if (k > 63) { atomicOr(a.err, 4); return; }
-                blk[s_zz[k]] = (int16_t)(fa >> 8);
-                end = ++k > 63;
-            } else {
-                const int rs = decode_sym(br, T, 4 + ta);
-                if (rs < 0) { atomicOr(a.err, 2); return; }
-                const int r = rs >> 4, sz = rs & 15;
-                if (!sz) {
-                    if (r != 15) end = true;  // EOB
-                    else end = (k += 16) > 63;
-                } else {
-                    k += r;
-                    if (k > 63) { atomicOr(a.err, 4); return; }
-                    blk[s_zz[k]] = (int16_t)extend_dev(br.get(sz), sz);
-                    end = ++k > 63;
-                }
-            }
-            if (end) {  // the next block: (bx, by) within the component, then the component, then the MCU
-                k = 0;
-                const int h = single ? 1 : a.h[ci], v = single ? 1 : a.v[ci];
-                if (++bx == h) {
-                    bx = 0;
-                    if (++by == v) {
-                        by = 0;
-                        if (++ci == ns) {
-                            ci = 0;
-                            ++i;
-                            if (++mx == row_len) { mx = 0; ++my; }
+    for (int i = 0; i < nm; ++i) {
+        for (int ci = 0; ci < a.ns; ++ci) {
+            const int nby = a.single ? 1 : a.v[ci], nbx = a.single ? 1 : a.h[ci];
+            for (int by = 0; by < nby; ++by)
+                for (int bx = 0; bx < nbx; ++bx) {
+                    const long long bi = a.single ? a.blk0[ci] + (long long)my * a.bw[ci] + mx
+                                                  : a.blk0[ci] + (long long)(my * a.v[ci] + by) * a.bw[ci] + mx * a.h[ci] + bx;
+                    int16_t* blk = a.coef + bi * 64;
+                    br.top_up();
+                    const int t = decode_sym(br, T, a.td[ci]);
+                    if (t < 0 || t > 11) { atomicOr(a.err, 1); return; }
+                    pred[ci] += t ? extend_dev(br.get(t), t) : 0;
+                    blk[0] = (int16_t)pred[ci];
+                    for (int k = 1; k < 64;) {
+                        const int fa = T.fast_ac[a.ta[ci]][br.peek(9)];
+                        if (fa) {  // short code + magnitude in one lookup
+                            k += (fa >> 4) & 15;
+                            br.skip(fa & 15);
+                            if (k > 63) { atomicOr(a.err, 4); return; }
+                            blk[s_zz[k]] = (int16_t)(fa >> 8);
+                            ++k;
+                            continue;
                         }
+                        const int rs = decode_sym(br, T, 4 + a.ta[ci]);
+                        if (rs < 0) { atomicOr(a.err, 2); return; }
+                        const int r = rs >> 4, sz = rs & 15;
+                        if (!sz) {
+                            if (r != 15) break;  // EOB
+                            k += 16;
+                            continue;
+                        }
+                        k += r;
+                        if (k > 63) { atomicOr(a.err, 4); return; }
+                        blk[s_zz[k]] = (int16_t)extend_dev(br.get(sz), sz);
+                        ++k;
                     }
                 }
-            }
         }
+        if (++mx == row_len) { mx = 0; ++my; }
     }
 }
 
@@ -624,13 +595,11 @@ __device__ __forceinline__ void load_tables(const JpegHuffTables* g, JpegHuffTab
     if (threadIdx.x < 64) s_zz[threadIdx.x] = kZz[threadIdx.x];
 }
 
-__global__ __launch_bounds__(kHuffThreads) void k_jpeg_huff(JpegScanArgs arg) {
+__global__ __launch_bounds__(kHuffThreads) void k_jpeg_huff(JpegScanArgs a) {
     __shared__ JpegHuffTables T;
     __shared__ uint8_t s_zz[64];
     __shared__ uint32_t s_ring[kHuffThreads][kRingDw + 1];  // +1: lanes' rings start in different banks
-    __shared__ JpegScanArgs a;                               // (indexed by component: see huff_interval)
-    if (threadIdx.x == 0) a = arg;
-    load_tables(arg.tabs, T, s_zz);
+    load_tables(a.tabs, T, s_zz);
     __syncthreads();
     const int seg = blockIdx.x * a.lanes + threadIdx.x;
     if ((int)threadIdx.x < a.lanes && seg < a.n_seg) huff_interval(a, T, s_zz, s_ring[threadIdx.x], seg);
@@ -644,10 +613,8 @@ __global__ __launch_bounds__(kHuffThreads) void k_jpeg_huff_batch(const JpegScan
     __shared__ JpegHuffTables T;
     __shared__ uint8_t s_zz[64];
     extern __shared__ uint32_t s_rings[];  // +1 dword per ring: lanes' rings start in different banks
-    __shared__ JpegScanArgs a;             // (indexed by component: LDS, not private memory)
-    if ((int)blockIdx.x * lanes >= scans[blockIdx.y].n_seg) return;  // whole workgroup past this scan's intervals
-    if (threadIdx.x == 0) a = scans[blockIdx.y];
-    __syncthreads();
+    const JpegScanArgs a = scans[blockIdx.y];
+    if ((int)blockIdx.x * lanes >= a.n_seg) return;  // whole workgroup past this scan's intervals
     load_tables(a.tabs, T, s_zz);
     __syncthreads();
     const int seg = blockIdx.x * lanes + threadIdx.x;
