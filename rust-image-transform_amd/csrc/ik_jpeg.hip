@@ -441,7 +441,7 @@ __device__ const uint8_t kZz[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 
 constexpr int kRingDw = 64;  // 256 bytes per lane
 
 struct GpuBits {
-    const uint32_t* g;  // the scan bytes as dwords (256-B aligned base, padded past the end)
+    const __attribute__((address_space(1))) uint32_t* g;  // the scan bytes as dwords (256-B aligned base, padded past the end)
     uint32_t* ring;     // this lane's ring
     uint32_t pos, fetched, size;  // next byte, ring filled up to (multiple of 4), scan end
     unsigned long long acc;
@@ -528,11 +528,31 @@ __device__ int decode_sym(GpuBits& br, const JpegHuffTables& T, int t) {
 
 }  // namespace
 
-// the whole interval `seg` of scan `a` (tables already in LDS)
+// the whole interval `seg` of scan `a` (tables already in LDS).  lb: the lane's
+// 64-coefficient block buffer in LDS (zeroed).  A block's coefficients go there as
+// they are decoded and the whole block (zeros included) to memory in eight 16-byte
+// stores, issued right after the next block's ring top-up -- so the top-up's wait
+// for its loads does not also wait for the stores (before: one 2-byte store per
+// coefficient, all of them ahead of the top-up's loads in the memory counter).
+typedef __attribute__((address_space(3))) int16_t lds_i16;
+typedef __attribute__((address_space(1))) int16_t glb_i16;
 __device__ void huff_interval(const JpegScanArgs& a, const JpegHuffTables& T, const uint8_t* s_zz, uint32_t* ring,
-                              int seg) {
+                              int seg, lds_i16* lb) {
+    typedef int16_t s8 __attribute__((ext_vector_type(8)));
+    typedef __attribute__((address_space(3))) s8 lds_s8;
+    typedef __attribute__((address_space(1))) s8 glb_s8;
+    glb_i16* pend = nullptr;  // the block in lb not yet written to memory
+    auto flush = [&]() {
+        if (!pend) return;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            reinterpret_cast<glb_s8*>(pend)[q] = reinterpret_cast<const lds_s8*>(lb)[q];
+            reinterpret_cast<lds_s8*>(lb)[q] = s8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+        pend = nullptr;
+    };
     GpuBits br;
-    br.g = reinterpret_cast<const uint32_t*>(a.data);
+    br.g = (const __attribute__((address_space(1))) uint32_t*)a.data;
     br.ring = ring;
     br.pos = a.seg[seg];
     br.fetched = br.pos & ~3u;
@@ -553,8 +573,11 @@ __device__ void huff_interval(const JpegScanArgs& a, const JpegHuffTables& T, co
                 for (int bx = 0; bx < nbx; ++bx) {
                     const long long bi = a.single ? a.blk0[ci] + (long long)my * a.bw[ci] + mx
                                                   : a.blk0[ci] + (long long)(my * a.v[ci] + by) * a.bw[ci] + mx * a.h[ci] + bx;
-                    int16_t* blk = a.coef + bi * 64;
+                    glb_i16* const gblk = (glb_i16*)(a.coef + bi * 64);
                     br.top_up();
+                    flush();
+                    lds_i16* const blk = lb;
+                    pend = gblk;
                     const int t = decode_sym(br, T, a.td[ci]);
                     if (t < 0 || t > 11) { atomicOr(a.err, 1); return; }
                     pred[ci] += t ? extend_dev(br.get(t), t) : 0;
@@ -586,6 +609,7 @@ __device__ void huff_interval(const JpegScanArgs& a, const JpegHuffTables& T, co
         }
         if (++mx == row_len) { mx = 0; ++my; }
     }
+    flush();
 }
 
 __device__ __forceinline__ void load_tables(const JpegHuffTables* g, JpegHuffTables& T, uint8_t* s_zz) {
@@ -599,10 +623,14 @@ __global__ __launch_bounds__(kHuffThreads) void k_jpeg_huff(JpegScanArgs a) {
     __shared__ JpegHuffTables T;
     __shared__ uint8_t s_zz[64];
     __shared__ uint32_t s_ring[kHuffThreads][kRingDw + 1];  // +1: lanes' rings start in different banks
+    __shared__ __attribute__((aligned(16))) int16_t s_blk[kHuffThreads * 64];
+    for (int i = threadIdx.x; i < kHuffThreads * 16; i += kHuffThreads)
+        reinterpret_cast<uint4*>(s_blk)[i] = make_uint4(0, 0, 0, 0);
     load_tables(a.tabs, T, s_zz);
     __syncthreads();
     const int seg = blockIdx.x * a.lanes + threadIdx.x;
-    if ((int)threadIdx.x < a.lanes && seg < a.n_seg) huff_interval(a, T, s_zz, s_ring[threadIdx.x], seg);
+    if ((int)threadIdx.x < a.lanes && seg < a.n_seg)
+        huff_interval(a, T, s_zz, s_ring[threadIdx.x], seg, (lds_i16*)(s_blk + threadIdx.x * 64));
 }
 
 // a batch of scans: grid.y = scan, each with its own tables; `lanes` intervals per workgroup
@@ -613,12 +641,20 @@ __global__ __launch_bounds__(kHuffThreads) void k_jpeg_huff_batch(const JpegScan
     __shared__ JpegHuffTables T;
     __shared__ uint8_t s_zz[64];
     extern __shared__ uint32_t s_rings[];  // +1 dword per ring: lanes' rings start in different banks
-    const JpegScanArgs a = scans[blockIdx.y];
-    if ((int)blockIdx.x * lanes >= a.n_seg) return;  // whole workgroup past this scan's intervals
+    // the scan's arguments in LDS: huff_interval indexes their per-component arrays,
+    // which in a register copy became private memory (224 bytes of scratch per lane)
+    __shared__ JpegScanArgs a;
+    if ((int)blockIdx.x * lanes >= scans[blockIdx.y].n_seg) return;  // whole workgroup past this scan's intervals
+    if (threadIdx.x == 0) a = scans[blockIdx.y];
+    __syncthreads();
+    // then a 128-byte block buffer per lane (zeroed), 16-byte aligned
+    int16_t* const s_blk = reinterpret_cast<int16_t*>(s_rings + ((lanes * (kRingDw + 1) + 3) & ~3));
+    for (int i = threadIdx.x; i < lanes * 16; i += kHuffThreads) reinterpret_cast<uint4*>(s_blk)[i] = make_uint4(0, 0, 0, 0);
     load_tables(a.tabs, T, s_zz);
     __syncthreads();
     const int seg = blockIdx.x * lanes + threadIdx.x;
-    if ((int)threadIdx.x < lanes && seg < a.n_seg) huff_interval(a, T, s_zz, s_rings + threadIdx.x * (kRingDw + 1), seg);
+    if ((int)threadIdx.x < lanes && seg < a.n_seg)
+        huff_interval(a, T, s_zz, s_rings + threadIdx.x * (kRingDw + 1), seg, (lds_i16*)(s_blk + threadIdx.x * 64));
 }
 
 // ---- progressive scans with restart intervals ----------------------------------
@@ -630,7 +666,7 @@ __global__ __launch_bounds__(kHuffThreads) void k_jpeg_huff_batch(const JpegScan
 __device__ void prog_interval(const JpegScanArgs& a, const JpegHuffTables& T, const uint8_t* s_zz, uint32_t* ring,
                               int seg) {
     GpuBits br;
-    br.g = reinterpret_cast<const uint32_t*>(a.data);
+    br.g = (const __attribute__((address_space(1))) uint32_t*)a.data;
     br.ring = ring;
     br.pos = a.seg[seg];
     br.fetched = br.pos & ~3u;
@@ -946,8 +982,9 @@ hipError_t launch_jpeg_huff_batch(const JpegScanArgs* dev_scans, int n, int max_
     int want = 1;
     while (want < 32 && (long long)want * 2 * 1024 <= total) want *= 2;
     const int lanes = huff_lanes(want);
+    const size_t ring_bytes = sizeof(uint32_t) * (((size_t)lanes * (kRingDw + 1) + 3) & ~size_t(3));
     hipLaunchKernelGGL(k_jpeg_huff_batch, dim3((max_seg + lanes - 1) / lanes, n), dim3(kHuffThreads),
-                       sizeof(uint32_t) * (kRingDw + 1) * lanes, s, dev_scans, lanes);
+                       ring_bytes + 128 * (size_t)lanes, s, dev_scans, lanes);
     return hipGetLastError();
 }
 
