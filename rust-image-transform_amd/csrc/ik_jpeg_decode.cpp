@@ -1161,9 +1161,10 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
                              sizeof(JpegScanArgs) * m, sizeof(JpegScanArgs) * m, 1, s);
         }
         if (!rc) {
+            // (no zeroing of the coefficient images: the decoder stores every block
+            // whole, and a deferred scan covers every block of its image -- all
+            // components interleaved, or the one component of a gray image)
             hipError_t e = hipMemsetAsync(dev + 256 + up256(sizeof(JpegScanArgs) * m), 0, sizeof(int) * m, s);
-            for (int k = 0; k < m && e == hipSuccess; ++k)
-                e = hipMemsetAsync(dev + lay[k].coef, 0, lay[k].pl - lay[k].coef, s);
             if (e == hipSuccess)
                 e = launch_jpeg_huff_batch(reinterpret_cast<const JpegScanArgs*>(dev + 256), m, max_seg, s);
             if (e == hipSuccess)
