@@ -31,16 +31,19 @@ def main():
     c, nc = per_kernel(cdir, "FETCH_SIZE")
     known = 32 * 4096 * 4096 * 4  # tools/bw_probe.py pattern 0: each byte of 32 x 4096^2 RGBA8 read once
     calib = known / (c["k_strip"] / nc["k_strip"] * 1024.0) if c.get("k_strip") else None
-    res = {"note": "per 64-frame batch (bench.py headline); fetch doubled per MI355X_MICROARCH.md (gfx950 "
-                   "FETCH_SIZE = half of a streaming read); bw_probe calibration factor recorded",
+    res = {"note": "per 64-frame batch (bench.py headline; counter sums over the run's dispatches / dispatch "
+                   "count); fetch doubled per MI355X_MICROARCH.md (gfx950 FETCH_SIZE = half of a streaming "
+                   "read), confirmed by the bw_probe calibration factor (known bytes / FETCH_SIZE bytes)",
            "bw_probe_fetch_factor": calib}
     for k in KERNELS:
         if k not in f or k not in w:
             continue
-        fetch = f[k] * 1024.0 * 2.0   # all dispatches of the batch (k_png_find: one per stream)
-        write = w[k] * 1024.0
+        # one dispatch per kernel per batch (round 3: k_png_find too); the run may hold
+        # more than one batch, so the sums are divided by the dispatch count
+        fetch = f[k] * 1024.0 * 2.0 / nf[k]
+        write = w[k] * 1024.0 / nw[k]
         res[k] = {"hbm_bytes_per_batch": int(fetch + write), "fetch_bytes_corrected": int(fetch),
-                  "write_bytes": int(write), "fetch_size_kb_raw": f[k], "write_size_kb_raw": w[k],
+                  "write_bytes": int(write), "fetch_size_kb_raw_total": f[k], "write_size_kb_raw_total": w[k],
                   "dispatches": nf[k]}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
