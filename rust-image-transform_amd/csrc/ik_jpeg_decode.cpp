@@ -339,7 +339,11 @@ struct Decoder {
         gpu_segs.assign(1, 0u);
         const uint8_t* q = data;
         while (q + 1 < end) {
-            if (q[0] != 0xFF) { ++q; continue; }
+            if (q[0] != 0xFF) {  // to the next 0xFF (memchr: entropy-coded data holds ~1 in 256 bytes)
+                const void* f = std::memchr(q, 0xFF, (size_t)(end - 1 - q));
+                if (!f) { q = end - 1; break; }
+                q = static_cast<const uint8_t*>(f);
+            }
             const uint8_t m = q[1];
             if (m == 0x00) { q += 2; continue; }
             if (m == 0xFF) { ++q; continue; }
@@ -424,7 +428,13 @@ struct Decoder {
         clean.reserve((size_t)(end - data));
         const uint8_t* q = data;
         while (q < end) {
-            if (q[0] != 0xFF) { clean.push_back(*q++); continue; }
+            if (q[0] != 0xFF) {  // the run up to the next 0xFF in one copy
+                const void* f = std::memchr(q, 0xFF, (size_t)(end - q));
+                const uint8_t* r = f ? static_cast<const uint8_t*>(f) : end;
+                clean.insert(clean.end(), q, r);
+                q = r;
+                continue;
+            }
             if (q + 1 < end && q[1] == 0x00) { clean.push_back(0xFF); q += 2; continue; }
             if (q + 1 >= end) { clean.push_back(0xFF); ++q; continue; }  // a lone 0xFF at the end: stuffed, as on the host
             break;  // a marker: the scan ends (the host feeds zeros from here)
@@ -436,7 +446,13 @@ struct Decoder {
         constexpr size_t kSeqPadWords = (16 + 11 + 63 * (16 + 10) + 31) / 32 + 2;
         const size_t nw = (clean.size() + 3) / 4 + kSeqPadWords;
         seq_words.assign(nw, 0u);
-        for (size_t i = 0; i < clean.size(); ++i) seq_words[i >> 2] |= (uint32_t)clean[i] << (24 - 8 * (i & 3));
+        const size_t nfull = clean.size() / 4;
+        for (size_t i = 0; i < nfull; ++i) {  // big-endian words, four bytes at a time
+            uint32_t v;
+            std::memcpy(&v, clean.data() + 4 * i, 4);
+            seq_words[i] = __builtin_bswap32(v);
+        }
+        for (size_t i = 4 * nfull; i < clean.size(); ++i) seq_words[i >> 2] |= (uint32_t)clean[i] << (24 - 8 * (i & 3));
         a.nbits = (long long)clean.size() * 8;
         a.L = 8192;
         a.nsub = (int)std::max<long long>(1, (a.nbits + a.L - 1) / a.L);
