@@ -1121,22 +1121,38 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
         else if ((ds[i]->seq || !ds[i]->prog.empty()) && !ds[i]->need_host) seq_idx.push_back(i);  // one by one, GPU
         else host_idx.push_back(i);
     }
-    // 2. the deferred scans: one device allocation, one Huffman launch over all of them
+    // 2. the deferred scans: one device allocation, one Huffman launch over all of them.
+    // Layout: [args][error flags][every image's quantisation + Huffman tables and
+    // interval starts][every image's scan bytes][every image's coefficients and
+    // planes].  The tables go up in one copy from a pinned block filled by the pool;
+    // scan bytes already in page-locked memory (ik_host_alloc) are DMAed in place, the
+    // rest through a pinned block the pool fills -- all asynchronous on the stream,
+    // ordered before the launch (before: four synchronous staged copies per image).
     const int m = (int)gpu_idx.size();
     if (m) {
         struct Lay { size_t q, t, sg, dt, coef, pl, end; JpegGeom g; };
         std::vector<Lay> lay(m);
-        size_t total = 256 + up256(sizeof(JpegScanArgs) * m) + up256(sizeof(int) * m);
-        const size_t hdr = total;
-        for (int k = 0; k < m; ++k) {
+        const size_t o_args = 256, o_err = o_args + up256(sizeof(JpegScanArgs) * m);
+        size_t total = o_err + up256(sizeof(int) * m);
+        const size_t o_small = total;
+        for (int k = 0; k < m; ++k) {  // tables and interval starts
             const Decoder& d = *ds[gpu_idx[k]];
             Lay& L = lay[k];
-            const size_t pb = make_geom(d, L.g);
             L.q = total;
             L.t = L.q + 512;
             L.sg = L.t + up256(sizeof(JpegHuffTables));
-            L.dt = L.sg + up256(d.gpu_segs.size() * sizeof(unsigned));
-            L.coef = L.dt + up256((size_t)d.gpu_scan.size + 1024);  // 64-B chunk fetches past the end
+            total = L.sg + up256(d.gpu_segs.size() * sizeof(unsigned));
+        }
+        const size_t small_bytes = total - o_small;
+        for (int k = 0; k < m; ++k) {  // scan bytes
+            lay[k].dt = total;
+            total += up256((size_t)ds[gpu_idx[k]]->gpu_scan.size + 1024);  // 64-B chunk fetches past the end
+        }
+        for (int k = 0; k < m; ++k) {  // coefficients and planes
+            const Decoder& d = *ds[gpu_idx[k]];
+            Lay& L = lay[k];
+            const size_t pb = make_geom(d, L.g);
+            L.coef = total;
             L.pl = L.coef + up256(d.nblocks * 64 * sizeof(int16_t));
             L.end = L.pl + up256(pb);
             total = L.end;
@@ -1146,46 +1162,68 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
         hipStream_t s = thread_stream();
         uint8_t* dev = scratch_slot(1, total);
         int rc = dev ? IK_OK : fail(IK_ERR_DEVICE, "cannot allocate the JPEG batch work area");
+        uint8_t* hsmall = rc ? nullptr : pinned_slot(1, small_bytes);
+        if (!rc && !hsmall) rc = IK_ERR_NOMEM;
+        std::vector<char> in_place(m, 0);
+        std::vector<size_t> st_off(m, 0);
+        size_t st_total = 0;
+        for (int k = 0; k < m && !rc; ++k) {
+            const Decoder& d = *ds[gpu_idx[k]];
+            in_place[k] = host_pinned(d.gpu_data, (size_t)d.gpu_scan.size) ? 1 : 0;
+            if (!in_place[k]) {
+                st_off[k] = st_total;
+                st_total += up256((size_t)d.gpu_scan.size);
+            }
+        }
+        uint8_t* hdata = !rc && st_total ? pinned_slot(2, st_total) : nullptr;
+        if (!rc && st_total && !hdata) rc = IK_ERR_NOMEM;
         std::vector<JpegScanArgs> args(m);
         int max_seg = 0;
+        if (!rc) {
+            parallel_for(m, 0, [&](int k) {
+                const Decoder& d = *ds[gpu_idx[k]];
+                const Lay& L = lay[k];
+                qtables(d, reinterpret_cast<uint16_t*>(hsmall + (L.q - o_small)));
+                d.tables(*reinterpret_cast<JpegHuffTables*>(hsmall + (L.t - o_small)));
+                std::memcpy(hsmall + (L.sg - o_small), d.gpu_segs.data(), d.gpu_segs.size() * sizeof(unsigned));
+                if (!in_place[k]) std::memcpy(hdata + st_off[k], d.gpu_data, (size_t)d.gpu_scan.size);
+            });
+            hipError_t e = hipMemcpyAsync(dev + o_small, hsmall, small_bytes, hipMemcpyHostToDevice, s);
+            for (int k = 0; k < m && e == hipSuccess; ++k) {
+                const Decoder& d = *ds[gpu_idx[k]];
+                const size_t db = (size_t)d.gpu_scan.size;
+                if (db)
+                    e = hipMemcpyAsync(dev + lay[k].dt, in_place[k] ? d.gpu_data : hdata + st_off[k], db,
+                                       hipMemcpyHostToDevice, s);
+            }
+            if (e != hipSuccess) rc = hip_fail(e, "jpeg batch upload");
+        }
         for (int k = 0; k < m && !rc; ++k) {
             const Decoder& d = *ds[gpu_idx[k]];
             const Lay& L = lay[k];
-            uint16_t q[256];
-            qtables(d, q);
-            JpegHuffTables tabs;
-            d.tables(tabs);
-            rc = copy_h2d_2d(dev + L.q, 512, reinterpret_cast<const uint8_t*>(q), 512, 512, 1, s);
-            if (!rc) rc = copy_h2d_2d(dev + L.t, sizeof(tabs), reinterpret_cast<const uint8_t*>(&tabs), sizeof(tabs),
-                                      sizeof(tabs), 1, s);
-            const size_t sb = d.gpu_segs.size() * sizeof(unsigned);
-            if (!rc) rc = copy_h2d_2d(dev + L.sg, sb, reinterpret_cast<const uint8_t*>(d.gpu_segs.data()), sb, sb, 1, s);
-            const size_t db = (size_t)d.gpu_scan.size;
-            if (!rc && db) rc = copy_h2d_2d(dev + L.dt, db, d.gpu_data, db, db, 1, s);
             JpegScanArgs& a = args[k];
             a = d.gpu_scan;
             a.data = dev + L.dt;
             a.seg = reinterpret_cast<const unsigned*>(dev + L.sg);
             a.tabs = reinterpret_cast<const JpegHuffTables*>(dev + L.t);
             a.coef = reinterpret_cast<int16_t*>(dev + L.coef);
-            a.err = reinterpret_cast<int*>(dev + 256 + up256(sizeof(JpegScanArgs) * m)) + k;
+            a.err = reinterpret_cast<int*>(dev + o_err) + k;
             max_seg = std::max(max_seg, a.n_seg);
         }
+        const size_t hdr = o_small;
         std::vector<int> errs(m, 0);
-        if (!rc) {
-            rc = copy_h2d_2d(dev + 256, sizeof(JpegScanArgs) * m, reinterpret_cast<const uint8_t*>(args.data()),
+        if (!rc) {  // (synchronous: also the point where the async uploads above are ordered before the launch)
+            rc = copy_h2d_2d(dev + o_args, sizeof(JpegScanArgs) * m, reinterpret_cast<const uint8_t*>(args.data()),
                              sizeof(JpegScanArgs) * m, sizeof(JpegScanArgs) * m, 1, s);
         }
         if (!rc) {
             // (no zeroing of the coefficient images: the decoder stores every block
             // whole, and a deferred scan covers every block of its image -- all
             // components interleaved, or the one component of a gray image)
-            hipError_t e = hipMemsetAsync(dev + 256 + up256(sizeof(JpegScanArgs) * m), 0, sizeof(int) * m, s);
+            hipError_t e = hipMemsetAsync(dev + o_err, 0, sizeof(int) * m, s);
             if (e == hipSuccess)
-                e = launch_jpeg_huff_batch(reinterpret_cast<const JpegScanArgs*>(dev + 256), m, max_seg, s);
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(errs.data(), dev + 256 + up256(sizeof(JpegScanArgs) * m), sizeof(int) * m,
-                                   hipMemcpyDeviceToHost, s);
+                e = launch_jpeg_huff_batch(reinterpret_cast<const JpegScanArgs*>(dev + o_args), m, max_seg, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(errs.data(), dev + o_err, sizeof(int) * m, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) rc = hip_fail(e, "jpeg batch entropy decode");
         }
