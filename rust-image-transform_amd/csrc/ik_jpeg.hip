@@ -398,6 +398,9 @@ __global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restr
         o32[2] = w[2];
         return;
     }
+#ifdef IK_COLOR_NOEDGE  // dev experiment (wrong pixels at the row ends): the cost of the generic edge path
+    if (zune_fast(g)) return;
+#endif
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         if (x0 + k < g.W) color_pixel(g, x0 + k, y, px + C * k);
