@@ -331,7 +331,7 @@ __device__ __forceinline__ void color_pixel(const JpegGeom& g, int x, int y, uin
 // the chroma plane's padded width): upsampled_zune's interior formulas and
 // color_pixel's arithmetic on whole dwords -- one luma dword, four chroma bytes
 // per row and plane -- instead of per-sample byte loads and the generic branches.
-__device__ __forceinline__ bool zune_fast(const JpegGeom& g) {
+__host__ __device__ __forceinline__ bool zune_fast(const JpegGeom& g) {
     return g.recon == IK_JPEG_RECON_ZUNE && g.colorspace == 1 && g.ncomp == 3 && g.h[0] == g.hmax &&
            g.v[0] == g.vmax && g.hmax == 2 * g.h[1] && g.hmax == 2 * g.h[2] && g.v[1] == g.v[2] &&
            (g.vmax == g.v[1] || g.vmax == 2 * g.v[1]) && g.bw[1] == g.bw[2] && g.bh[1] == g.bh[2];
@@ -380,6 +380,20 @@ __device__ __forceinline__ void color4_zune(const JpegGeom& g, int x0, int y, ui
     }
 }
 
+// one pixel of a zune_fast image anywhere in the row (color_pixel's zune YCbCr path
+// without its other modes): the row ends, where color4_zune does not apply.  A
+// wave holding a row-end thread otherwise ran all of color_pixel's branches.
+__device__ __forceinline__ void color1_zune(const JpegGeom& g, int x, int y, uint8_t* o) {
+    const int c0 = upsampled_zune(g, 0, x, y), c1 = upsampled_zune(g, 1, x, y), c2 = upsampled_zune(g, 2, x, y);
+    const int16_t cb = (int16_t)(c1 - 128), cr = (int16_t)(c2 - 128);
+    const int r = c0 + ((int16_t)(45 * cr) >> 5);
+    const int gg = c0 - ((int16_t)(11 * cb + 23 * cr) >> 5);
+    const int b = c0 + ((int16_t)(113 * cb) >> 6);
+    o[0] = clamp255(r);
+    o[1] = clamp255(gg);
+    o[2] = clamp255(b);
+}
+
 __global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restrict__ dst, size_t pitch) {
     const int x0 = 4 * (blockIdx.x * 256 + threadIdx.x), y = blockIdx.y;
     if (x0 >= g.W) return;
@@ -398,9 +412,7 @@ __global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restr
         o32[2] = w[2];
         return;
     }
-#ifdef IK_COLOR_NOEDGE  // dev experiment (wrong pixels at the row ends): the cost of the generic edge path
-    if (zune_fast(g)) return;
-#endif
+    if (zune_fast(g)) return;  // a row end: k_jpeg_color_ends
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         if (x0 + k < g.W) color_pixel(g, x0 + k, y, px + C * k);
@@ -417,6 +429,27 @@ __global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restr
         return;
     }
     for (int i = 0; i < C * (g.W - x0); ++i) o[i] = px[i];
+}
+
+// The row ends of a zune_fast image (the groups of four k_jpeg_color leaves:
+// x0 = 0, and from the first group that reaches the plane's last two chroma
+// samples or the image's right edge), one thread per (row, end): kept out of
+// k_jpeg_color, where a wave holding a row-end thread ran these branches for all
+// of its lanes (50 vs 27 us per 4096^2 frame with them outside).
+__global__ __launch_bounds__(256) void k_jpeg_color_ends(JpegGeom g, uint8_t* __restrict__ dst, size_t pitch) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= 2 * g.H) return;
+    const int y = t >> 1;
+    const int lim = 2 * g.bw[1] * 8 - 2;  // a group is interior iff x0 >= 4, x0 + 4 <= W and x0 + 3 < lim
+    // the first group past the interior ones: the last interior x0 is the largest
+    // multiple of 4 <= min(W - 4, lim - 4)
+    const int xm = (g.W - 4 < lim - 4 ? g.W - 4 : lim - 4);
+    const int xc = xm < 4 ? 4 : (xm & ~3) + 4;
+    int xa, xb;
+    if (t & 1) { xa = xc; xb = g.W; }
+    else { xa = 0; xb = g.W < 4 ? g.W : 4; }
+    uint8_t* o = dst + (size_t)y * pitch;
+    for (int x = xa; x < xb; ++x) color1_zune(g, x, y, o + 3 * x);
 }
 
 }  // namespace
@@ -996,6 +1029,8 @@ hipError_t launch_jpeg_reconstruct(const JpegGeom& g, uint8_t* dst, size_t dst_p
     const unsigned nb = (unsigned)((g.nblocks + 255) / 256);
     hipLaunchKernelGGL(k_jpeg_idct, dim3(nb), dim3(256), 0, s, g);
     hipLaunchKernelGGL(k_jpeg_color, dim3((g.W + 1023) / 1024, g.H), dim3(256), 0, s, g, dst, dst_pitch);
+    if (zune_fast(g))
+        hipLaunchKernelGGL(k_jpeg_color_ends, dim3((2 * g.H + 255) / 256), dim3(256), 0, s, g, dst, dst_pitch);
     return hipGetLastError();
 }
 
