@@ -454,7 +454,12 @@ struct Decoder {
         }
         for (size_t i = 4 * nfull; i < clean.size(); ++i) seq_words[i >> 2] |= (uint32_t)clean[i] << (24 - 8 * (i & 3));
         a.nbits = (long long)clean.size() * 8;
-        a.L = 8192;
+        static const int kL = [] {  // bits per lane (IK_JPEG_SEQ_L: A/B; a multiple of 32)
+            const char* e = getenv("IK_JPEG_SEQ_L");
+            const int v = e ? atoi(e) : 8192;
+            return v < 1024 ? 1024 : (v > 65536 ? 65536 : v & ~31);
+        }();
+        a.L = kL;
         a.nsub = (int)std::max<long long>(1, (a.nbits + a.L - 1) / a.L);
         a.bpm = bpm;
         a.mcux = mcux;
