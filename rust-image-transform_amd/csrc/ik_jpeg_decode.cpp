@@ -454,9 +454,13 @@ struct Decoder {
         }
         for (size_t i = 4 * nfull; i < clean.size(); ++i) seq_words[i >> 2] |= (uint32_t)clean[i] << (24 - 8 * (i & 3));
         a.nbits = (long long)clean.size() * 8;
-        static const int kL = [] {  // bits per lane (IK_JPEG_SEQ_L: A/B; a multiple of 32)
+        // bits per lane (IK_JPEG_SEQ_L, a multiple of 32): 2048, not 8192 -- four times
+        // the lanes, each round a quarter as long; the host walk stays small
+        // (loadtest restart-free 645 -> 1,061 requests/s, configs[2] restart-free
+        // 7,757 -> 14,901 MPix/s, profiles/r03am_jpeg_seq_lane_bits.txt)
+        static const int kL = [] {
             const char* e = getenv("IK_JPEG_SEQ_L");
-            const int v = e ? atoi(e) : 8192;
+            const int v = e ? atoi(e) : 2048;
             return v < 1024 ? 1024 : (v > 65536 ? 65536 : v & ~31);
         }();
         a.L = kL;
