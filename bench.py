@@ -363,10 +363,16 @@ def main():
     stage_ms = []
     NT = 17  # ik_png_last_timing fields
 
+    batch_ms = []
+    NB = 10  # ik_batch_last_timing fields
+
     def note_timing():
         timing = (ctypes.c_double * NT)()  # the last PNG batch the device finished
         lib.ik_png_last_timing(timing, NT)
         stage_ms.append(list(timing))
+        bt = (ctypes.c_double * NB)()  # the last batch's JPEG decode / resize / JPEG encode launches
+        lib.ik_batch_last_timing(bt, NB)
+        batch_ms.append(list(bt))
 
     def submit(rq):
         fn = transform_batch_submit_device if isinstance(rq[0], DeviceBytes) else transform_batch_submit
@@ -419,6 +425,7 @@ def main():
     run = (lambda k: run_pipelined(k, rq=dreqs)) if args.pipeline else run_blocking
     run(args.warmup)
     stage_ms.clear()
+    batch_ms.clear()
     cnt0 = (ctypes.c_ulonglong * 2)()
     lib.ik_png_counters(cnt0)
     barrier()
@@ -456,8 +463,27 @@ def main():
         "k_png_resolve": (png_stages["resolve"], nd * (2 * raw + 4 * S * S)),
         "k_png_unfilter": (png_stages["unfilter"], nd * (2 * 4 * S * S)),
     }
+    # the batch path's own launches (ik_batch_last_timing, HIP events on the kernel
+    # stream): JPEG entropy decoding, the grouped resize, the batched JPEG encoder
+    bt = np.mean(np.array(batch_ms), axis=0) if batch_ms else np.zeros(10)
+    jpeg_huff = None
     if args.source != "png":
-        kern = {}  # (the PNG stage times do not apply; the resize kernel's line is roofline_resize)
+        # JPEG sources: the PNG stage times do not apply.  The entropy decoding launch
+        # reads the scans and writes every block's int16 coefficients (the bytes a
+        # decode of these frames must move, SURVEY 8(d) D-5's decode-stage share)
+        kern = {"k_jpeg_huff_batch" if args.source == "jpeg-rst" else "k_jpeg_seq_decode":
+                (float(bt[0]), float(bt[1] + bt[2]))}
+        jpeg_huff = {"ms": round(float(bt[0]), 4), "scan_bytes": int(bt[1]), "coef_bytes": int(bt[2]),
+                     "images": int(bt[3]), "lanes": int(bt[4])}
+    resize_batch = None
+    if bt[5] > 0:
+        resize_batch = {"bound": "hbm", "achieved": round(bt[6] / (bt[5] * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                        "unit": "GB/s", "frac": round(bt[6] / (bt[5] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                        "traffic": None, "kernel": "k_resize_fused", "kernel_ms": round(float(bt[5]), 4),
+                        "bytes_per_launch": int(bt[6]), "batch": int(bt[7]),
+                        "note": "the grouped resize launch of the measured batches themselves (HIP events on the "
+                                "kernel stream); bytes = C*W*H in + C*w*h out per image"}
+    jpeg_enc = {"ms": round(float(bt[8]), 4), "images": int(bt[9])} if bt[9] > 0 else None
     dom = max(kern, key=lambda k: kern[k][0]) if kern else None
     dms, dbytes = kern[dom] if dom else (1.0, 0)
     traffic_png = None  # PMC HBM bytes of that kernel per 64-frame launch (tools/pmc_png_traffic.sh)
@@ -467,12 +493,18 @@ def main():
             traffic_png = json.load(open(pmcp)).get(dom, {}).get("hbm_bytes_per_batch")
         except Exception:
             traffic_png = None
+    if args.source == "png":
+        note = ("DEFLATE decoding: each lane's symbol-to-symbol chain bounds it (one lane per block, ~1,900 "
+                "blocks per frame), not HBM; bytes = compressed bits in + u16 tokens out")
+    else:
+        note = ("JPEG entropy decoding: each lane's Huffman symbol chain bounds it, not HBM; bytes = the "
+                "entropy-coded scans read + every block's int16 coefficients written (HIP events on the kernel "
+                "stream around the launch)")
     roof = {"bound": "hbm", "achieved": round(dbytes / (dms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(dbytes / (dms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": traffic_png, "kernel": dom,
-            "kernel_ms": round(dms, 4), "bytes_per_launch": int(dbytes),
-            "note": "DEFLATE decoding: each lane's symbol-to-symbol chain bounds it (one lane per block, ~1,900 "
-                    "blocks per frame), not HBM; bytes = compressed bits in + u16 tokens out",
-            "tokens_per_batch": int(tok)}
+            "kernel_ms": round(dms, 4), "bytes_per_launch": int(dbytes), "note": note}
+    if args.source == "png":
+        roof["tokens_per_batch"] = int(tok)
     kernels = {k: {"ms": round(v[0], 4), "GBps": round(v[1] / max(v[0], 1e-6) / 1e6, 1)} for k, v in kern.items()}
 
     # the same workload with the inputs in ordinary (pageable) memory: the upload
@@ -576,9 +608,8 @@ def main():
                    "bytes_per_source_image": sum(len(p) for p in jp) // 2,
                    "value": round(aggregate_mpix(world, n, S, te), 2), "unit": "MPix/s"}
 
-    if args.source != "png" and roof_resize:
-        roof = dict(roof_resize, note="JPEG sources: the resize kernel's line (its HIP-event time in the "
-                                      "hbm_resident leg); the JPEG decode kernels are in the rocprof stats")
+    if roof_resize is None:
+        roof_resize = resize_batch  # (no hbm_resident leg: the measured batches' own resize launch)
     src_desc = ({"png": "PNG (zlib level 6), resident in HBM (one device allocation per request) -> "
                         "ik_transform_batch_submit_device: decode_image (GPU chunk walk, gather + CRC, inflate + "
                         "unfilter)",
@@ -611,6 +642,9 @@ def main():
                 "batch_per_gpu": B, "inflight": args.inflight if args.pipeline else 1,
                 "inputs": "device memory (HBM), resident before the timed region" if args.pipeline and args.source == "png" else
                           ("pageable host memory" if args.pageable else "page-locked host memory (ik_host_alloc)"),
+                "value_basis": ("HBM-resident inputs (the measurement contract); SURVEY D-1's host-memory-to-host-"
+                                "memory figure is pcie_inclusive.value" if args.pipeline and args.source == "png"
+                                else "encoded inputs in host memory -> encoded outputs in host memory (SURVEY D-1)"),
                 "inproc_devices": args.inproc_devices, "filter": args.filter, "format": args.format, "quality": args.quality,
                 "host_threads_per_gpu": args.threads, "png_bytes_per_image": in_bytes,
                 "webp_bytes_per_image": out_bytes,
@@ -621,6 +655,9 @@ def main():
             },
             "roofline": roof,
             "roofline_resize": roof_resize,
+            "roofline_resize_batch_path": resize_batch,
+            "jpeg_entropy_decode": jpeg_huff,
+            "jpeg_encode_batched": jpeg_enc,
             "png_decode_stages_ms": png_stages,
             "kernels": kernels,
             "pcie_inclusive": pcie,

@@ -72,6 +72,15 @@ uint64_t ik_request_cost(const uint8_t *bytes, size_t len, int64_t w, int64_t h,
  * assign[i]; largest request first to the least-loaded device */
 void ik_schedule_plan(const uint64_t *costs, uint32_t n, uint32_t ndev, const uint64_t *outstanding,
                       uint32_t *assign);
+/* Orderly teardown: waits for every submitted batch, ends
+ * the library's stage threads and worker pools (each releases its HIP streams
+ * and arenas), then frees the pooled images, upload areas, resize plans and
+ * pinned blocks -- while the HIP runtime is still alive, so that nothing is left
+ * to destructors running at process exit.  Call it once before exit (the Python
+ * package registers it with atexit; the Rust shim calls it from Drop of its
+ * runtime guard).  Images, pipelines and buffers the caller still holds must be
+ * freed first; the library may be used again afterwards (ik_init). */
+int ik_shutdown(void);
 size_t ik_last_error(char *buf, size_t cap); /* thread-local message of the last failure */
 const char *ik_version(void);
 
@@ -134,6 +143,14 @@ int ik_set_png_gpu_min(long long min_raw_bytes);
  * ms until the block search's candidates were back (waiting for the upload
  * included), [16] 1 if the block search ran beside the previous batch's kernels */
 int ik_png_last_timing(double *out, int n);
+/* the last batch the calling thread's device ran through its kernel stage
+ * (ik_transform_batch*): device ms from HIP events on the kernel stream and the
+ * algorithmic bytes of the same launches (n <= 10 values): [0] JPEG entropy
+ * decoding ms, [1] entropy-coded bytes read, [2] int16 coefficient bytes written,
+ * [3] images, [4] decoder lanes; [5] grouped resize ms, [6] resize bytes (C*W*H
+ * in + C*w*h out per image), [7] images resized in groups; [8] batched JPEG
+ * encoder ms (coefficients + Huffman), [9] images it coded */
+int ik_batch_last_timing(double *out, int n);
 /* process-wide counts of PNG streams decoded since load: out[0] by the GPU path,
  * out[1] by the host decoder (outside the GPU path, or rejected by it) */
 int ik_png_counters(unsigned long long *out);

@@ -93,7 +93,7 @@ const Deflate& deflate_api() {
         d.zlib_decompress = (int (*)(void*, const void*, size_t, void*, size_t, size_t*))dlsym(lib, "libdeflate_zlib_decompress");
         d.release = (void (*)(void*))dlsym(lib, "libdeflate_free_decompressor");
         d.crc32 = (uint32_t (*)(uint32_t, const void*, size_t))dlsym(lib, "libdeflate_crc32");
-        d.ok = d.alloc && d.zlib_decompress && d.release && !getenv("IK_PNG_ZLIB");
+        d.ok = d.alloc && d.zlib_decompress && d.release;
     });
     return d;
 }

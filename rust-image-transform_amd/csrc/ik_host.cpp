@@ -78,30 +78,75 @@ struct Arena {
     int device = 0;
 };
 struct ThreadRes {
-    std::map<int, hipStream_t> streams, copy_streams, search_streams;
+    std::map<int, hipStream_t> streams, copy_streams;
     std::map<std::pair<int, int>, Arena> dev;  // (device, slot)
     Arena pinned[8];
-    ~ThreadRes() {
+    void release() {
+        for (auto& kv : streams) (void)hipStreamSynchronize(kv.second);
+        for (auto& kv : copy_streams) (void)hipStreamSynchronize(kv.second);
         for (auto& kv : dev) {
             if (!kv.second.p) continue;
             (void)hipSetDevice(kv.second.device);
-            auto s = streams.find(kv.second.device);
-            if (s != streams.end()) (void)hipStreamSynchronize(s->second);
             (void)hipFree(kv.second.p);
         }
         for (Arena& a : pinned)
             if (a.p) (void)hipHostFree(a.p);
         for (auto& kv : streams) (void)hipStreamDestroy(kv.second);
         for (auto& kv : copy_streams) (void)hipStreamDestroy(kv.second);
-        // (search streams are left to the runtime's teardown: destroying a CU-masked
-        // stream from a thread-exit destructor crashed at process exit under rocprofv3)
+        streams.clear();
+        copy_streams.clear();
+        dev.clear();
+        for (Arena& a : pinned) a = Arena();
     }
+    // a caller's own thread that exits releases its set here; workers and stage
+    // threads release theirs before they end (ik_shutdown), and after ik_shutdown
+    // the process's main thread holds none, so nothing is left to a destructor that
+    // runs during process exit
+    ~ThreadRes() { release(); }
 };
 ThreadRes& tres() {
     static thread_local ThreadRes r;
     return r;
 }
 }  // namespace
+
+void release_thread_resources() { tres().release(); }
+
+namespace {
+std::mutex g_bt_mu;
+std::map<int, std::vector<double>> g_bt, g_bt_last;  // the batch in the kernel stage, the last one finished
+struct ThreadEvents {
+    EvPair p[4];
+    ~ThreadEvents() {}  // (events are left to the runtime: a thread-exit destructor may run at process exit)
+};
+}  // namespace
+
+void batch_timing_reset(int device) {
+    std::lock_guard<std::mutex> lk(g_bt_mu);
+    g_bt[device].assign(kBtFields, 0.0);
+}
+void batch_timing_commit(int device) {
+    std::lock_guard<std::mutex> lk(g_bt_mu);
+    g_bt_last[device] = g_bt[device];
+}
+void batch_timing_add(int device, int field, double v) {
+    std::lock_guard<std::mutex> lk(g_bt_mu);
+    std::vector<double>& t = g_bt[device];
+    if (t.size() < (size_t)kBtFields) t.resize(kBtFields, 0.0);
+    t[(size_t)field] += v;
+}
+EvPair& thread_events(int which) {
+    static thread_local ThreadEvents te;
+    EvPair& e = te.p[which & 3];
+    if (!e.a && hipEventCreate(&e.a) != hipSuccess) e.a = nullptr;
+    if (!e.b && hipEventCreate(&e.b) != hipSuccess) e.b = nullptr;
+    return e;
+}
+float ev_pair_ms(const EvPair& e) {
+    float ms = 0;
+    if (!e.a || !e.b || hipEventElapsedTime(&ms, e.a, e.b) != hipSuccess) return 0.f;
+    return ms;
+}
 
 hipStream_t thread_stream() {
     ThreadRes& r = tres();
@@ -124,33 +169,6 @@ hipStream_t thread_copy_stream() {
     hipStream_t s = nullptr;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
     r.copy_streams[d] = s;
-    return s;
-}
-
-// A stream on a hardware queue of its own, for the next batch's block search
-// beside the current batch's kernels.  Ordinary streams share the device's
-// GPU_MAX_HW_QUEUES (4) queues round-robin, and two streams on one queue run in
-// order: the rocprof trace showed the search serialised behind / before expand on
-// the kernel stage's queue.  A CU-masked stream gets a dedicated queue; the mask
-// is every CU, or the first IK_FIND_CUS of them.
-hipStream_t search_stream() {
-    ThreadRes& r = tres();
-    const int d = current_device();
-    auto it = r.search_streams.find(d);
-    if (it != r.search_streams.end()) return it->second;
-    (void)hipSetDevice(d);
-    int ncu = 0;
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || ncu <= 0) ncu = 256;
-    int use = ncu;
-    if (const char* e = getenv("IK_FIND_CUS")) use = std::max(1, std::min(ncu, atoi(e)));
-    std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-    for (int c = 0; c < use; ++c) mask[(size_t)c / 32] |= 1u << (c % 32);
-    hipStream_t s = nullptr;
-    if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
-        (void)hipGetLastError();
-        if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    }
-    r.search_streams[d] = s;
     return s;
 }
 
@@ -270,11 +288,11 @@ struct ImagePool {
     std::multimap<size_t, uint8_t*> free_blocks;
     size_t held = 0;
 };
+std::mutex g_ipool_mu;
+std::map<int, ImagePool*> g_ipools;
 ImagePool& image_pool(int device) {
-    static std::mutex mu;
-    static std::map<int, ImagePool*> pools;
-    std::lock_guard<std::mutex> lk(mu);
-    ImagePool*& p = pools[device];
+    std::lock_guard<std::mutex> lk(g_ipool_mu);
+    ImagePool*& p = g_ipools[device];
     if (!p) p = new ImagePool();
     return *p;
 }
@@ -335,9 +353,14 @@ int resize_mode() {
     return m;
 }
 
+namespace {
+std::mutex g_consts_mu;
+std::map<int, DeviceConsts*> g_consts;
+}  // namespace
+
 const DeviceConsts* device_consts(int device) {
-    static std::mutex mu;
-    static std::map<int, DeviceConsts*> m;
+    std::mutex& mu = g_consts_mu;
+    std::map<int, DeviceConsts*>& m = g_consts;
     std::lock_guard<std::mutex> lk(mu);
     auto it = m.find(device);
     if (it != m.end()) return it->second;
@@ -807,30 +830,42 @@ int resize_target(uint32_t W, uint32_t H, int64_t w, int64_t h, uint32_t* onw, u
 // done) when the per-image path applies instead (the GPU VP8 encoder, > 16383).
 // Page-locked blocks shared by the requests of a batched colour launch: a pool of
 // free blocks (process-wide); a block goes back when its last holder drops it.
+// Best fit (the smallest free block that holds the request, at most twice its
+// size, so a small group does not take the block a large one needs), and at most
+// kPinnedPoolBytes kept: a block returned past that goes back to the runtime.
 namespace {
+constexpr size_t kPinnedPoolBytes = size_t(2) << 30;
 std::mutex g_pblk_mu;
-std::vector<std::pair<uint8_t*, size_t>> g_pblk_free;
+std::multimap<size_t, uint8_t*> g_pblk_free;  // capacity -> block
+size_t g_pblk_held = 0;
 }  // namespace
 static std::shared_ptr<uint8_t> pinned_block(size_t bytes) {
     uint8_t* p = nullptr;
     size_t cap = 0;
     {
         std::lock_guard<std::mutex> lk(g_pblk_mu);
-        for (size_t i = 0; i < g_pblk_free.size(); ++i)
-            if (g_pblk_free[i].second >= bytes) {
-                p = g_pblk_free[i].first;
-                cap = g_pblk_free[i].second;
-                g_pblk_free.erase(g_pblk_free.begin() + (long)i);
-                break;
-            }
+        auto it = g_pblk_free.lower_bound(bytes);
+        if (it != g_pblk_free.end() && it->first <= 2 * bytes) {
+            cap = it->first;
+            p = it->second;
+            g_pblk_held -= cap;
+            g_pblk_free.erase(it);
+        }
     }
     if (!p) {
         cap = bytes;
         if (hipHostMalloc((void**)&p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
     }
     return std::shared_ptr<uint8_t>(p, [cap](uint8_t* q) {
-        std::lock_guard<std::mutex> lk(g_pblk_mu);
-        g_pblk_free.emplace_back(q, cap);
+        {
+            std::lock_guard<std::mutex> lk(g_pblk_mu);
+            if (g_pblk_held + cap <= kPinnedPoolBytes) {
+                g_pblk_free.emplace(cap, q);
+                g_pblk_held += cap;
+                return;
+            }
+        }
+        (void)hipHostFree(q);
     });
 }
 
@@ -926,8 +961,10 @@ int jpeg_front_group(const std::vector<ik_image*>& imgs, int quality, std::vecto
         std::memcpy(hp + p_stage, qt, 128);
         uint64_t* htab = reinterpret_cast<uint64_t*>(hp + p_stage + 256);
         for (size_t i = 0; i < m; ++i) htab[i] = (uint64_t)(uintptr_t)imgs[b0 + i]->d;
+        EvPair& ev = thread_events(1);
         hipError_t e = launch_copy_words(reinterpret_cast<const uint32_t*>(dh + p_stage), reinterpret_cast<uint32_t*>(dv),
                                          32, s);
+        if (e == hipSuccess && ev.a) e = hipEventRecord(ev.a, s);
         if (e == hipSuccess)
             e = launch_copy_words(reinterpret_cast<const uint32_t*>(dh + p_stage + 256),
                                   reinterpret_cast<uint32_t*>(dv + o_tab), 2 * m, s);
@@ -950,8 +987,11 @@ int jpeg_front_group(const std::vector<ik_image*>& imgs, int quality, std::vecto
             a.out_len = reinterpret_cast<uint32_t*>(dh + p_len);
             e = launch_jpeg_huff_enc(a, (int)m, s);
         }
+        if (e == hipSuccess && ev.b) e = hipEventRecord(ev.b, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_fail(e, "jpeg encode (batched)");
+        batch_timing_add(current_device(), kBtJpegEncMs, ev_pair_ms(ev));
+        batch_timing_add(current_device(), kBtJpegEncImages, (double)m);
         const uint32_t* lens = reinterpret_cast<const uint32_t*>(hp + p_len);
         for (size_t i = 0; i < m; ++i) {
             std::vector<uint8_t>& o = *out[b0 + i];
@@ -1008,10 +1048,19 @@ int resize_group(const std::vector<ik_image*>& src, uint32_t nw, uint32_t nh, in
         if (e != hipSuccess) rc = hip_fail(e, "resize table upload");
     }
     if (!rc) {
-        hipError_t e = launch_resize(*plan, nullptr, s0->pitch, 0, nullptr, out[0]->pitch, 0, (int)n, nullptr, s, dtab,
-                                     dtab + n);
+        EvPair& ev = thread_events(0);
+        hipError_t e = ev.a ? hipEventRecord(ev.a, s) : hipSuccess;
+        if (e == hipSuccess)
+            e = launch_resize(*plan, nullptr, s0->pitch, 0, nullptr, out[0]->pitch, 0, (int)n, nullptr, s, dtab, dtab + n);
+        if (e == hipSuccess && ev.b) e = hipEventRecord(ev.b, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) rc = hip_fail(e, "resize (batched)");
+        if (!rc) {
+            const int d = current_device();
+            batch_timing_add(d, kBtResizeMs, ev_pair_ms(ev));
+            batch_timing_add(d, kBtResizeBytes, (double)n * s0->c * ((double)s0->w * s0->h + (double)nw * nh));
+            batch_timing_add(d, kBtResizeImages, (double)n);
+        }
     }
     if (rc)
         for (ik_image*& o : out) { ik_image_free(o); o = nullptr; }
@@ -1303,6 +1352,7 @@ static void transform_device_phase(const uint8_t* const* bytes, const size_t* le
     // GPU phases under the device's kernel gate (held from the decode kernels
     // through resize and the encoders' device front ends), the host coders after
     gate_pin(kGateKernels, true);
+    batch_timing_reset(current_device());
     decode_batch_dev(b.data(), l.data(), m, imgs.data(), nullptr, ds.data(), dm.data(), threads, up,
                      sniff ? sn.data() : nullptr);
     gate_enter(kGateKernels);
@@ -1385,6 +1435,7 @@ static void transform_device_phase(const uint8_t* const* bytes, const size_t* le
         imgs[k] = nullptr;
     });
     gate_pin(kGateKernels, false);
+    batch_timing_commit(current_device());
 }
 
 static void transform_host_phase(uint8_t** outs, size_t* out_lens, int* st, std::string* errs, HostPhase& hp) {
@@ -1470,8 +1521,23 @@ struct BatchPart {
 class StageExec {
 public:
     StageExec(int device, Pool* host_pool) : dev_(device), pool_(host_pool) {
-        std::thread([this] { loop(0); }).detach();  // live as long as the process
-        std::thread([this] { loop(1); }).detach();
+        th_[0] = std::thread([this] { loop(0); });  // live until stop() (ik_shutdown)
+        th_[1] = std::thread([this] { loop(1); });
+    }
+    // ik_shutdown: the stages finish what is queued (upload before kernels), then end
+    void stop() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            done_[0] = true;
+        }
+        cv_.notify_all();
+        th_[0].join();
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            done_[1] = true;
+        }
+        cv_.notify_all();
+        th_[1].join();
     }
     void submit(std::shared_ptr<BatchPart> p) {
         {
@@ -1488,7 +1554,8 @@ private:
             std::shared_ptr<BatchPart> p;
             {
                 std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return !q_[stage].empty(); });
+                cv_.wait(lk, [&] { return done_[stage] || !q_[stage].empty(); });
+                if (q_[stage].empty()) break;  // stopped, nothing left
                 p = std::move(q_[stage].front());
                 q_[stage].pop_front();
             }
@@ -1519,16 +1586,9 @@ private:
                 // upload has landed (else its own kernel stage launches it).  Beside
                 // expand / resolve / unfilter it only slows them: a stream on another
                 // hardware queue measured 63-69 vs 61-62 ms per step (the search took
-                // resolve from 3.6 to 13-19 ms), and which queue the copy stream gets is
-                // the runtime's round-robin, so it differed from run to run.
-                // IK_FIND_STREAM=copy / search: the copy stream / a CU-masked stream
-                // with a queue of its own (A/B).
-                static const int where = [] {
-                    const char* e = getenv("IK_FIND_STREAM");
-                    return e && !strcmp(e, "search") ? 2 : (e && !strcmp(e, "copy") ? 1 : 0);
-                }();
-                if (where == 0 && !png_upload_landed(nx->up)) return;
-                hipStream_t fs = where == 2 ? search_stream() : where == 1 ? thread_copy_stream() : thread_stream();
+                // resolve from 3.6 to 13-19 ms; profiles/r03n_find_*.json).
+                if (!png_upload_landed(nx->up)) return;
+                hipStream_t fs = thread_stream();
                 if (after && hipStreamWaitEvent(fs, after, 0) != hipSuccess) return;
                 png_find_prelaunch(nx->up, fs);
             };
@@ -1544,29 +1604,102 @@ private:
                 if (--tk.pending == 0) tk.cv.notify_all();
             });
         }
+        release_thread_resources();
     }
     int dev_;
     Pool* pool_;
     std::mutex mu_;
     std::condition_variable cv_;
     std::deque<std::shared_ptr<BatchPart>> q_[2];
+    bool done_[2] = {false, false};
+    std::thread th_[2];
 };
 
-// the stages of a physical device (single-device mode) or of a logical device
-StageExec& stage_exec(int logical) {
-    static std::mutex mu;
-    static std::map<int, StageExec*> m;
-    const int key = logical >= 0 ? 1000 + logical : current_device();
-    std::lock_guard<std::mutex> lk(mu);
-    StageExec*& e = m[key];
+std::mutex g_stage_mu;
+std::map<int, StageExec*> g_stages;
+
+// the stages of a logical device, or (single-device mode) of physical device
+// `phys` (-1: the calling thread's device)
+StageExec& stage_exec(int logical, int phys) {
+    const int dev = phys >= 0 ? phys : current_device();
+    const int key = logical >= 0 ? 1000 + logical : dev;
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    StageExec*& e = g_stages[key];
     if (!e) e = logical >= 0 ? new StageExec(sched_phys(logical), &sched_pool(logical))
-                             : new StageExec(current_device(), &device_pool(current_device()));
+                             : new StageExec(dev, &device_pool(dev));
     return *e;
 }
 
 std::mutex g_async_mu;
 std::map<uint64_t, std::shared_ptr<Ticket>> g_async;
 uint64_t g_async_next = 1;
+
+}  // namespace
+
+// ik_shutdown's device-memory part: pooled image blocks, the batched colour
+// launches' pinned blocks, the per-device constant tables
+static void memory_shutdown() {
+    {
+        std::lock_guard<std::mutex> lk(g_ipool_mu);
+        for (auto& kv : g_ipools) {
+            std::lock_guard<std::mutex> lk2(kv.second->mu);
+            (void)hipSetDevice(kv.first);
+            for (auto& b : kv.second->free_blocks) (void)hipFree(b.second);
+            kv.second->free_blocks.clear();
+            kv.second->held = 0;
+        }
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_pblk_mu);
+        for (auto& b : g_pblk_free) (void)hipHostFree(b.second);
+        g_pblk_free.clear();
+        g_pblk_held = 0;
+    }
+    std::lock_guard<std::mutex> lk(g_consts_mu);
+    for (auto& kv : g_consts) {
+        (void)hipSetDevice(kv.first);
+        (void)hipFree(kv.second->gamma_to_lin);
+        (void)hipFree(kv.second->lin_to_gamma);
+        (void)hipFree(kv.second->jpeg_huff);
+        delete kv.second;
+    }
+    g_consts.clear();
+}
+
+// ik_shutdown: wait for every submitted batch, end the stage threads and the
+// worker pools (each releases its streams and arenas), then free what the
+// library holds, all while the HIP runtime is alive
+int shutdown_all() {
+    std::vector<std::shared_ptr<Ticket>> ts;
+    {
+        std::lock_guard<std::mutex> lk(g_async_mu);
+        for (auto& kv : g_async) ts.push_back(kv.second);
+    }
+    for (auto& t : ts) {
+        std::unique_lock<std::mutex> lk(t->mu);
+        t->cv.wait(lk, [&] { return t->pending == 0; });
+    }
+    std::vector<StageExec*> st;
+    {
+        std::lock_guard<std::mutex> lk(g_stage_mu);
+        for (auto& kv : g_stages) st.push_back(kv.second);
+        g_stages.clear();
+    }
+    for (StageExec* e : st) {
+        e->stop();
+        delete e;
+    }
+    pools_shutdown();
+    const int dev = t_device;
+    png_shutdown();
+    plans_shutdown();
+    memory_shutdown();
+    release_thread_resources();
+    if (dev >= 0) (void)hipSetDevice(dev);
+    return IK_OK;
+}
+
+namespace {
 
 int min_device_batch() {
     static const int v = [] {
@@ -1608,7 +1741,7 @@ int submit_parts(const std::shared_ptr<Ticket>& t, const uint8_t* const* bytes, 
     };
     std::vector<std::shared_ptr<BatchPart>> parts;
     if (!sched_multi()) {
-        parts.push_back(make_part(0, n));
+        parts.push_back(make_part(0, n));  // to the stages of `phys` (the inputs' device) or the caller's device
     } else if (phys >= 0) {
         auto p = make_part(0, n);
         for (uint32_t i = 0; i < n; ++i) p->cost += cost_of(i);
@@ -1634,7 +1767,7 @@ int submit_parts(const std::shared_ptr<Ticket>& t, const uint8_t* const* bytes, 
     }
     for (auto& p : parts) {
         const int ld = p->logical;
-        stage_exec(ld).submit(std::move(p));
+        stage_exec(ld, ld >= 0 ? -1 : phys).submit(std::move(p));
     }
     return IK_OK;
 }
@@ -1721,8 +1854,20 @@ int ik_transform_batch_submit_device(const uint8_t* const* dev_bytes, const size
             t->eff[i] = t->sniff[i] = t->hcopy[i].data();
         }
     }
-    return submit_parts(t, t->eff.data(), t->sniff.data(), sched_multi() ? phys : -1, lens, n, w, h, fmt, quality,
-                        filter, threads, ticket);
+    // the batch runs where its inputs are: on a logical device of `phys`, or (single-
+    // device mode) on the stages of `phys` whatever the calling thread's device is
+    return submit_parts(t, t->eff.data(), t->sniff.data(), phys, lens, n, w, h, fmt, quality, filter, threads, ticket);
+}
+
+int ik_shutdown(void) { return shutdown_all(); }
+
+int ik_batch_last_timing(double* out, int n) {
+    if (!out || n <= 0) return fail(IK_ERR_INVALID, "bad timing buffer");
+    const int d = current_device();
+    std::lock_guard<std::mutex> lk(g_bt_mu);
+    auto it = g_bt_last.find(d);
+    for (int i = 0; i < n; ++i) out[i] = it != g_bt_last.end() && i < (int)it->second.size() ? it->second[(size_t)i] : 0.0;
+    return IK_OK;
 }
 
 int ik_transform_batch_wait(uint64_t ticket) {

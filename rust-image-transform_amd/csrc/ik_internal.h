@@ -58,7 +58,6 @@ struct ResizeArgs {
     // arrays, [n]); null = src + img * src_img_stride / dst + img * dst_img_stride
     const uint64_t* src_tab;
     const uint64_t* dst_tab;
-    int htaps;         // fused path: horizontal taps whose LDS reads go out together (2 or 4)
 };
 
 // Host-side plan for one (W,H,C,nw,nh,filter,band height) geometry.

@@ -969,14 +969,7 @@ hipError_t launch_jpeg_seq_decode(const JpegSeqArgs& a, hipStream_t s) {
 }
 
 namespace {
-int huff_lanes(int dflt) {
-    static const int forced = [] {
-        const char* e = getenv("IK_HUFF_LANES");
-        return e ? atoi(e) : 0;
-    }();
-    const int v = forced > 0 ? forced : dflt;
-    return v < 1 ? 1 : (v > kHuffThreads ? kHuffThreads : v);
-}
+int huff_lanes(int v) { return v < 1 ? 1 : (v > kHuffThreads ? kHuffThreads : v); }
 }  // namespace
 
 int jpeg_lanes_for(long long total) {

@@ -1226,15 +1226,38 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
                              sizeof(JpegScanArgs) * m, sizeof(JpegScanArgs) * m, 1, s);
         }
         if (!rc) {
-            // (no zeroing of the coefficient images: the decoder stores every block
-            // whole, and a deferred scan covers every block of its image -- all
-            // components interleaved, or the one component of a gray image)
+            // No zeroing of the coefficient images where the decoder stores every
+            // block whole: an interleaved scan covers every block of its image.  A
+            // one-component scan covers only the blocks of the component's own size;
+            // when its sampling factors pad the component to more (a gray image with
+            // H = V = 2), the padding blocks are zeroed so that no stale scratch
+            // reaches the reconstruction, even where the crop drops it.
             hipError_t e = hipMemsetAsync(dev + o_err, 0, sizeof(int) * m, s);
+            for (int k = 0; k < m && e == hipSuccess; ++k)
+                if (args[k].single && (size_t)args[k].total_mcu < ds[gpu_idx[k]]->nblocks)
+                    e = hipMemsetAsync(dev + lay[k].coef, 0, ds[gpu_idx[k]]->nblocks * 64 * sizeof(int16_t), s);
+            EvPair& ev = thread_events(2);
+            if (e == hipSuccess && ev.a) e = hipEventRecord(ev.a, s);
             if (e == hipSuccess)
                 e = launch_jpeg_huff_batch(reinterpret_cast<const JpegScanArgs*>(dev + o_args), m, max_seg, s);
+            if (e == hipSuccess && ev.b) e = hipEventRecord(ev.b, s);
             if (e == hipSuccess) e = hipMemcpyAsync(errs.data(), dev + o_err, sizeof(int) * m, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) rc = hip_fail(e, "jpeg batch entropy decode");
+            if (!rc) {  // ik_batch_last_timing: the launch's time and algorithmic bytes
+                double scan = 0, coef = 0, lanes = 0;
+                for (int k = 0; k < m; ++k) {
+                    scan += (double)args[k].size;
+                    coef += (double)ds[gpu_idx[k]]->nblocks * 64 * sizeof(int16_t);
+                    lanes += args[k].n_seg;
+                }
+                const int d = current_device();
+                batch_timing_add(d, kBtJpegHuffMs, ev_pair_ms(ev));
+                batch_timing_add(d, kBtJpegScanBytes, scan);
+                batch_timing_add(d, kBtJpegCoefBytes, coef);
+                batch_timing_add(d, kBtJpegImages, m);
+                batch_timing_add(d, kBtJpegLanes, lanes);
+            }
         }
         // 3. reconstruction of every image the GPU decoded cleanly
         for (int k = 0; k < m && !rc; ++k) {

@@ -125,8 +125,7 @@ __device__ __forceinline__ void horizontal_rows(const ResizeArgs& a, const float
                                                 g_u8* __restrict__ dst) {
     switch (a.C) {
     case 4:
-        if (a.htaps == 4) horizontal_rows_c<4, FMA, 4>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst);
-        else horizontal_rows_c<4, FMA>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst);
+        horizontal_rows_c<4, FMA>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst);
         break;
     case 3: horizontal_rows_c<3, FMA>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
     case 2: horizontal_rows_c<2, FMA>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
@@ -433,11 +432,6 @@ hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_
     a.dst = dst; a.dst_pitch = dst_pitch; a.dst_img_stride = dst_img_stride;
     a.src_tab = src_tab; a.dst_tab = dst_tab;
     a.tmp = naive_tmp;
-    static const int htaps = [] {  // IK_HTAPS=4: four horizontal taps' LDS reads in flight (tuning)
-        const char* e = getenv("IK_HTAPS");
-        return e && atoi(e) == 4 ? 4 : 2;
-    }();
-    a.htaps = htaps;
     if (src_tab && !(plan.slots > 0 && resize_fused_fits(src_pitch, (size_t)a.H))) return hipErrorInvalidValue;
     if (plan.slots > 0 && resize_fused_fits(src_pitch, (size_t)a.H)) {
         dim3 grid(plan.NS * plan.NB * n);  // 1-D: the kernel maps it XCD-aware

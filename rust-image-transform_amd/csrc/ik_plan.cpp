@@ -124,7 +124,7 @@ namespace {
 std::mutex g_plan_mu;
 std::map<std::tuple<int, int, int, int, int, int, int, int, int>, ResizePlan*> g_plans;
 // request -> plan (several requests can share one plan in g_plans)
-std::map<std::tuple<int, int, int, int, int, int, int, int, int, int, int>, ResizePlan*> g_front;
+std::map<std::tuple<int, int, int, int, int, int, int, int>, ResizePlan*> g_front;
 
 template <typename T>
 size_t put(std::vector<char>& blob, const std::vector<T>& v) {
@@ -139,11 +139,9 @@ size_t put(std::vector<char>& blob, const std::vector<T>& v) {
 ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, int filter, int n);
 
 ResizePlan* get_resize_plan(int device, int W, int H, int C, int nw, int nh, int filter, int n) {
-    // front cache on the request itself (plus the dev overrides), so a repeated
-    // geometry costs a map lookup, not a recomputation of the weights
-    auto env_i = [](const char* k) { const char* e = getenv(k); return e ? atoi(e) : -1; };
-    const auto fkey = std::make_tuple(device, W, H, C, nw, nh, filter, n, env_i("IK_TARGET_WG"),
-                                      env_i("IK_BAND_ROWS"), env_i("IK_FLUSH_ROWS"));
+    // front cache on the request itself, so a repeated geometry costs a map
+    // lookup, not a recomputation of the weights
+    const auto fkey = std::make_tuple(device, W, H, C, nw, nh, filter, n);
     {
         std::lock_guard<std::mutex> lk(g_plan_mu);
         auto it = g_front.find(fkey);
@@ -181,7 +179,6 @@ ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, i
     // column strips: as many output columns as fit kStripBytes source bytes (and,
     // when possible, kMaxStripWeights horizontal weights in LDS)
     bool wl = (long)Tx <= kMaxStripWeights;
-    if (const char* e = getenv("IK_WEIGHTS_LDS")) wl = wl && atoi(e) != 0;  // tuning experiments
     std::vector<int> strips;
     for (int pass = 0; pass < 2 && slots; ++pass) {
         strips.clear();
@@ -219,8 +216,7 @@ ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, i
     const int NS = slots ? (int)strips.size() / 3 : 0;
     int band_h = nh;
     if (slots) {
-        long target = 8192;  // measured best on MI355X for 4096^2->512^2 batches (tools/sweep_resize.py)
-        if (const char* e = getenv("IK_TARGET_WG")) target = atol(e);
+        const long target = 8192;  // measured best on MI355X for 4096^2->512^2 batches (tools/sweep_resize.py)
         long per_img = (target + n - 1) / n;
         long nb = (per_img + NS - 1) / NS;
         if (nb < 1) nb = 1;
@@ -231,16 +227,11 @@ ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, i
         band_h = ((band_h + slots - 1) / slots) * slots;
         if (band_h > nh) band_h = nh;
     }
-    if (const char* e = getenv("IK_BAND_ROWS")) band_h = std::max(1, std::min(nh, atoi(e)));
     // flush depth F (vertical rows staged in LDS per horizontal pass): 3 measured
     // best on MI355X for both triangle and lanczos3 8x downscales (deeper costs
     // resident workgroups, shallower runs the barrier-bound horizontal pass more
     // often; tools/sweep_resize.py FLUSH=2,3,4)
-    int flush = 3;
-    if (const char* e = getenv("IK_FLUSH_ROWS")) flush = std::max(2, std::min(kMaxFlushRows, atoi(e)));
-    if (getenv("IK_DEBUG_PLAN"))
-        fprintf(stderr, "[ik plan] %dx%dx%d -> %dx%d f%d: A=%d R=%d NS=%d band_h=%d wl=%d flush=%d Tx=%d\n",
-                W, H, C, nw, nh, filter, slots, rows, NS, band_h, (int)wl, flush, Tx);
+    const int flush = 3;
     const auto key = std::make_tuple(device, W, H, C, nw, nh, filter, band_h, flush);
     std::lock_guard<std::mutex> lk(g_plan_mu);
     auto it = g_plans.find(key);
@@ -337,6 +328,17 @@ ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, i
     a.band_step = (const int*)(d + o_bst);
     g_plans[key] = p;
     return p;
+}
+
+// ik_shutdown: every cached plan's device tables
+void plans_shutdown() {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    for (auto& kv : g_plans) {
+        if (kv.second->dev_tables) (void)hipFree(kv.second->dev_tables);
+        delete kv.second;
+    }
+    g_plans.clear();
+    g_front.clear();
 }
 
 }  // namespace ik

@@ -20,15 +20,6 @@ IK_HD int png_unfilter_groups(int h) {
     const int g = ((h + 63) / 64 + kPngUnfilterWaves - 1) / kPngUnfilterWaves;
     return g < 32 ? g : 32;
 }
-// the blocked-band unfilter (k_png_unfilter_blk): workgroups of kPngUnfBlkWaves
-// consecutive bands, at most 256 per image (all of an image's workgroups must be
-// resident together: 4 per CU)
-constexpr int kPngUnfBlkWaves = 4;
-IK_HD int png_unfilter_blk_groups(int h) {
-    const int g = ((h + 63) / 64 + kPngUnfBlkWaves - 1) / kPngUnfBlkWaves;
-    return g < 256 ? g : 256;
-}
-bool png_unfilter_blocked();  // IK_PNG_UNF_BLK (default on): the launcher's choice, for the host's group tables
 constexpr uint64_t kPngChunkBytes = 16384; // candidate-search chunk of the compressed stream
 constexpr int kPngPageShift = 12;          // resolve: output page -> decoder table
 

@@ -9,9 +9,9 @@
 //                   the next lane's start -> the lane's token stream and output
 //                   length.  Code tables in LDS per thread (192 B), input through
 //                   an LDS ring filled by LDS-DMA (128 B per thread)
-//   k_png_expand    one wave per verified lane: tokens -> u16 symbols (bytes,
-//                   window markers) at the lane's output offset, 64 tokens per
-//                   step with every output position resolved in parallel;
+//   k_png_expand4   one wave per verified lane: tokens -> u16 symbols (bytes,
+//                   window markers) at the lane's output offset, 256 tokens per
+//                   step, literals by a wave prefix sum, copies in token order;
 //                   status and clock ticks / 1024 per lane (status[2 t], [2 t + 1])
 //   k_png_resolve   u16 symbols -> the filtered bytes of every row, 16 per thread,
 //                   markers followed to their source; rows land 16-B aligned in
@@ -414,219 +414,19 @@ __global__ __launch_bounds__(kPngInflateThreads) void k_png_decode(const PngImgD
 
 // ---- expand -----------------------------------------------------------------------
 // One WAVE per verified lane (one DEFLATE block, ~32K symbols): the lane's tokens
-// -> u16 symbols at its output offset, in batches of up to 64 tokens:
-//   1. each thread takes one token; a token after a match's first token is its
-//      distance (distances are < 0x8000, so the test is local); a wave prefix
-//      sum of the symbols' output lengths gives every symbol's offset in the
-//      batch (batches end before a table record and hold <= kXCap symbols)
-//   2. every output position of the batch is resolved by its own thread: a
-//      literal; or, for a copy, the source position (period `dist` inside an
-//      overlapping copy) -- an earlier position of the same batch is followed
-//      back through its own symbol, a position before the batch is read from
-//      the wave's LDS ring of recent output (<= kXNear back) or from memory
-//      (farther; all of a thread's loads in flight together), and one before
-//      the lane's first symbol becomes a window marker (0x8000 | index into the
-//      32 KiB before the lane, as the resolve pass expects)
-//   3. the batch goes to the ring and, coalesced, to memory.
-// So a block costs a few memory round trips per 64 tokens instead of one per
-// copy, and 64 lanes share each one.
+// -> u16 symbols at its output offset: literal bytes, or window markers (0x8000 |
+// index into the 32 KiB before the lane, as the resolve pass expects) for copies
+// that reach before the lane's first symbol.
 constexpr int kXRing = 2048;            // recent output symbols per wave (LDS, power of two)
 constexpr int kXCap = 1024;             // output symbols per batch at most
 constexpr int kXNear = kXRing - kXCap;  // sources at most this far back come from the ring
-constexpr int kXGroup = 4;              // output positions per thread resolved together
 using infl::kTokMatch;
 using infl::kTokPad;
 using infl::kTokRaw;
 using infl::kTokTable;
 using infl::kTokTableLen;
 
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
-    const int x = threadIdx.x;
-    uint32_t incl = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = (uint32_t)__shfl_up((int)incl, o, 64);
-        if (x >= o) incl += u;
-    }
-    *total = (uint32_t)__shfl((int)incl, 63, 64);
-    return incl - v;
-}
-
-__global__ __launch_bounds__(64) void k_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int nlanes,
-                                                   const uint16_t* tok, int* status) {
-    raise_priority();
-    __shared__ uint16_t s_ring[kXRing];
-    __shared__ uint32_t s_tab[64];   // the block's literal table (256 bytes)
-    __shared__ uint32_t s_end[64];   // per token slot: end offset of its symbol in the batch (inclusive scan)
-    __shared__ uint32_t s_info[64];  // per token slot: bit 31 set = literal (value in bits 0..7), else len | (dist - 1) << 16
-    const int li = blockIdx.x;
-    if (li >= nlanes) return;
-    const int x = threadIdx.x;
-    const uint64_t c0 = clock64();
-    const PngLaneDev L = lanes[li];
-    const PngImgDev I = imgs[L.img];
-    const IK_GLOBAL uint16_t* T = (const IK_GLOBAL uint16_t*)(tok + L.tbase);
-    IK_GLOBAL uint16_t* out = (IK_GLOBAL uint16_t*)I.u16 + L.obase;
-    const uint32_t ntok = L.ntok;
-    uint32_t t = 0, cnt = 0;
-    bool have_tab = false, bad = false;
-    // this batch's tokens (and the one after each), loaded one batch ahead
-    uint32_t u = x < (int)ntok ? (uint32_t)T[x] : kTokPad;
-    uint32_t un = x + 1 < (int)ntok ? (uint32_t)T[x + 1] : 0u;
-    while (t < ntok && !bad) {
-        // a table record at the batch start: the literal table -> LDS
-        const unsigned long long mk = __ballot(u == kTokTable);
-        if (mk & 1ull) {
-            const uint32_t tt = (t + 8) & ~7u;  // pads (0xFFFE) up to a multiple of 8 tokens
-            if (tt + kTokTableLen > ntok) { bad = true; break; }
-            s_tab[x] = ((const IK_GLOBAL uint32_t*)(T + tt))[x];
-            have_tab = true;
-            t = tt + kTokTableLen;
-            u = t + x < ntok ? (uint32_t)T[t + x] : kTokPad;
-            un = t + x + 1 < ntok ? (uint32_t)T[t + x + 1] : 0u;
-            __syncthreads();
-            continue;
-        }
-        uint32_t n = mk ? (uint32_t)__ffsll((long long)mk) - 1u : 64u;
-        if (t + n > ntok) n = ntok - t;
-        // a match's first token in the last slot: its distance is in the next batch
-        const unsigned long long mf = __ballot((u & 0xFF00u) == kTokMatch);
-        if ((mf >> (n - 1)) & 1ull) --n;
-        if (n == 0) { bad = true; break; }  // a match cut off by the end of the tokens
-        const uint32_t up = (uint32_t)__shfl_up((int)u, 1, 64);
-        const bool start = x < (int)n && !(x > 0 && (up & 0xFF00u) == kTokMatch);
-        uint32_t len = 0, info = 0;
-        if (start) {
-            if (u < 256u) {
-                if (!have_tab) bad = true;
-                len = 1;
-                info = 0x80000000u | ((s_tab[u >> 2] >> (8 * (u & 3u))) & 0xFFu);
-            } else if ((u & 0xFF00u) == kTokRaw) {
-                len = 1;
-                info = 0x80000000u | (u & 0xFFu);
-            } else if ((u & 0xFF00u) == kTokMatch) {
-                len = (u & 0xFFu) + 3u;
-                info = len | (un << 16);  // the distance token holds dist - 1 (< 0x8000)
-            } else {
-                bad = true;
-            }
-        }
-        if (__ballot(bad)) { bad = true; break; }
-        // every symbol of the batch one literal (the common case on poorly
-        // compressible data): lane x holds output position x, nothing to resolve
-        if (!__ballot(x < (int)n && !(info & 0x80000000u))) {
-            const uint16_t v = (uint16_t)(info & 0xFFu);
-            const uint32_t t2 = t + n;
-            u = t2 + x < ntok ? (uint32_t)T[t2 + x] : kTokPad;
-            un = t2 + x + 1 < ntok ? (uint32_t)T[t2 + x + 1] : 0u;
-            if (x < (int)n) {
-                s_ring[(cnt + (uint32_t)x) & (kXRing - 1)] = v;
-                out[(int64_t)cnt + x] = v;
-            }
-            cnt += n;
-            t = t2;
-            continue;
-        }
-        uint32_t tot;
-        uint32_t off = wave_excl_scan(len, &tot);
-        if (tot > (uint32_t)kXCap) {  // cut the batch before the first symbol that does not fit
-            const unsigned long long over = __ballot(start && off + len > (uint32_t)kXCap);
-            const uint32_t x0 = (uint32_t)__ffsll((long long)over) - 1u;  // > 0: one symbol always fits
-            n = x0;
-            if (x >= (int)x0) len = 0;
-            off = wave_excl_scan(len, &tot);
-        }
-        s_end[x] = off + len;
-        s_info[x] = info;
-        // the next batch's tokens, in flight while this one resolves
-        const uint32_t t2 = t + n;
-        u = t2 + x < ntok ? (uint32_t)T[t2 + x] : kTokPad;
-        un = t2 + x + 1 < ntok ? (uint32_t)T[t2 + x + 1] : 0u;
-        __syncthreads();
-        // resolve this thread's positions q = x + 64 k, K of them at a time (one
-        // when the batch holds at most 64 symbols)
-        auto resolve = [&](auto kc, uint32_t g0) {
-            constexpr int K = decltype(kc)::value;
-            int sl[K];
-            uint32_t qk[K];
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                qk[k] = g0 + (uint32_t)x + 64u * k;
-                sl[k] = 0;
-            }
-            // the symbol holding q: the first slot whose end > q (all searches in lockstep)
-#pragma unroll
-            for (int st = 32; st >= 1; st >>= 1)
-#pragma unroll
-                for (int k = 0; k < K; ++k)
-                    if (s_end[sl[k] + st - 1] <= qk[k]) sl[k] += st;
-            uint16_t val[K];
-            int64_t gsrc[K];  // >= 0: read from memory at out[gsrc]
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                val[k] = 0;
-                gsrc[k] = -1;
-                if (qk[k] >= tot) continue;
-                int32_t q = (int32_t)qk[k];
-                int lo = sl[k];
-                for (int guard = 0; guard < 1024; ++guard) {
-                    const uint32_t inf = s_info[lo];
-                    if (inf & 0x80000000u) { val[k] = (uint16_t)(inf & 0xFFu); break; }
-                    const int32_t o = (int32_t)(s_end[lo] - (inf & 0xFFFFu));
-                    const int32_t d = (int32_t)(inf >> 16) + 1;
-                    const int32_t j = q - o, ln = (int32_t)(inf & 0xFFFFu);
-                    const int32_t src = o - d + (d >= ln ? j : j % d);  // relative to the batch start
-                    if (src >= 0) {  // an earlier position of this batch: its own symbol
-                        q = src;
-                        lo = 0;
-#pragma unroll
-                        for (int st = 32; st >= 1; st >>= 1)
-                            if (s_end[lo + st - 1] <= (uint32_t)q) lo += st;
-                        continue;
-                    }
-                    const int64_t abs = (int64_t)cnt + src;  // relative to the lane's first symbol
-                    if (abs < 0) {
-                        if (abs < -(int64_t)infl::kWindow) bad = true;
-                        val[k] = (uint16_t)(0x8000u | (uint32_t)(infl::kWindow + abs));
-                    } else if (-src <= kXNear) {
-                        val[k] = s_ring[(uint32_t)abs & (kXRing - 1)];
-                    } else {
-                        gsrc[k] = abs;
-                    }
-                    break;
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (gsrc[k] >= 0) val[k] = out[gsrc[k]];
-            // (ring slots written here held positions older than any this batch reads)
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (qk[k] < tot) {
-                    s_ring[(cnt + qk[k]) & (kXRing - 1)] = val[k];
-                    out[(int64_t)cnt + qk[k]] = val[k];
-                }
-        };
-        if (tot <= 64u) {
-            resolve(std::integral_constant<int, 1>{}, 0u);
-        } else if (tot <= 128u) {  // the common case with a match or two in the step
-            resolve(std::integral_constant<int, 2>{}, 0u);
-        } else {
-            for (uint32_t g0 = 0; g0 < tot; g0 += 64 * kXGroup) resolve(std::integral_constant<int, kXGroup>{}, g0);
-        }
-        __syncthreads();
-        cnt += tot;
-        t = t2;
-        if (__ballot(bad)) bad = true;
-    }
-    if (x == 0) {
-        status[2 * li] = (!bad && cnt == L.out_len) ? 0 : -1;
-        status[2 * li + 1] = (int)((clock64() - c0) >> 10);  // profile: clock ticks / 1024
-    }
-}
-
-// k_png_expand with four tokens per thread (256 per batch) and the copies done in
-// token order instead of every output position searching for its symbol: on
+// Four tokens per thread (256 per batch) and the copies done in token order: on
 // image data ~96 % of the tokens are literals and a match is ~1 in 25 tokens,
 // so the batch costs a load, a prefix sum (DPP) and one LDS write per literal,
 // ~20 instructions per match, and a coalesced ring -> memory copy.
@@ -641,7 +441,6 @@ __global__ __launch_bounds__(64) void k_png_expand(const PngImgDev* imgs, const 
 //      (8-byte stores; a group's 1-3 positions before the batch are rewritten
 //      with the same values, its positions after the batch -- stale ring data --
 //      are rewritten by the next batch; groups are clipped to the lane's output).
-// IK_PNG_EXPAND=1: k_png_expand.  Same output.
 constexpr uint32_t kX4Tok = 256;
 
 __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const PngLaneDev* lanes, int nlanes,
@@ -1177,341 +976,6 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngI
 #endif
 }
 
-// The same wavefront with the bands of a workgroup in blocks: workgroups of
-// kPngUnfBlkWaves (4) waves, workgroup k of an image holding bands 4 k .. 4 k + 3
-// (wave w: band 4 k + w), so 3 of every 4 band-to-band hand-offs stay inside the
-// CU, while the ~14 bands of an image in flight still spread over as many CUs as
-// with the interleaved layout (16-wave blocks put them on one or two CUs, 4 waves
-// a SIMD: 9.4 vs 7.6 ms).  A band's last row goes to the next
-// wave through an LDS ring (kUnfRing chunks per wave) and an LDS progress word,
-// written after `s_waitcnt lgkmcnt(0)` -- no store has to reach memory first --
-// and its rows are stored plain; only the workgroup's last band keeps the sc1
-// hand-off to the next workgroup (stores sc1 + vmcnt(0) + a global progress word,
-// as k_png_unfilter) and only its first band polls one.  The segment clock of
-// k_png_unfilter showed its bands waiting 75 % of the time, one per group on a
-// write-through drain and a cross-CU poll.  The consumer acknowledges what it has
-// read (s_cons), and a producer that would overwrite unread ring chunks waits for
-// it (never in practice: a band runs ~9 groups behind the one above; the ring
-// holds 32).  Bands past 4 K take further passes in the same layout.  Tickets as
-// k_png_unfilter.
-constexpr int kUnfRing = 256;
-
-template <int BPP, bool SWAR>
-__global__ __launch_bounds__(kPngUnfBlkWaves * 64) void k_png_unfilter_blk(const PngImgDev* imgs, const int2* groups,
-                                                                          const int* prog_base, unsigned* prog,
-                                                                          unsigned* ticket) {
-    raise_priority();
-    constexpr int NW = kPngUnfBlkWaves, G = kUnfG, R = kUnfRing;
-    __shared__ int s_t;
-    __shared__ u32x4 s_ring[NW][R];
-    __shared__ unsigned s_prog[NW], s_cons[NW];
-    if (threadIdx.x == 0) s_t = (int)atomicAdd(ticket, 1u);
-    if (threadIdx.x < NW) { s_prog[threadIdx.x] = 0u; s_cons[threadIdx.x] = 0u; }
-    __syncthreads();
-    const int2 gk = groups[s_t];  // (image, workgroup of the image)
-    const PngImgDev I = imgs[gk.x];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int nch = (I.rowbytes + 15) >> 4;
-    const int nbands = (I.H + 63) >> 6;
-    const int K = png_unfilter_blk_groups(I.H);
-    unsigned* pg = prog + prog_base[gk.x];
-    volatile unsigned* vprog = s_prog;
-    volatile unsigned* vcons = s_cons;
-    for (int pass = 0;; ++pass) {
-        const int band = pass * NW * K + gk.y * NW + wave;
-        if (band >= nbands) break;
-        const unsigned seq = (unsigned)(pass * nch);  // this pass's chunks in the LDS ring / progress
-        const bool lds_in = wave > 0, glob_in = wave == 0 && band > 0;
-        const bool lds_out = wave < NW - 1 && band + 1 < nbands, glob_out = wave == NW - 1 && band + 1 < nbands;
-        const int y = band * 64 + lane;
-        const bool live = y < I.H;
-        uint8_t* row = I.dst + (size_t)(live ? y : 0) * I.pitch;
-        const FtMask fm(live ? I.ft[y] : 0u);
-        const uint64_t above = glob_in ? (uint64_t)(size_t)(I.dst + (size_t)(band * 64 - 1) * I.pitch) : 0;
-        uint32_t cur[4] = {0, 0, 0, 0}, up[4] = {0, 0, 0, 0};
-        uint32_t prevcur[4] = {0, 0, 0, 0}, prevup[4] = {0, 0, 0, 0};
-        const uint64_t dbase = uniform_u64((uint64_t)(size_t)I.dst);
-        const uint32_t rowoff = (uint32_t)((size_t)(live ? y : 0) * I.pitch);
-        auto fetch = [&](int s0, u32x4 (&r)[G]) {
-            uint32_t off[G];
-#pragma unroll
-            for (int t = 0; t < G; ++t) off[t] = rowoff + 16u * (uint32_t)min(max(s0 + t - lane, 0), nch - 1);
-            asm volatile(
-                "s_nop 4\n\t"
-                "global_load_dwordx4 %0, %8, %16\n\t"
-                "global_load_dwordx4 %1, %9, %16\n\t"
-                "global_load_dwordx4 %2, %10, %16\n\t"
-                "global_load_dwordx4 %3, %11, %16\n\t"
-                "global_load_dwordx4 %4, %12, %16\n\t"
-                "global_load_dwordx4 %5, %13, %16\n\t"
-                "global_load_dwordx4 %6, %14, %16\n\t"
-                "global_load_dwordx4 %7, %15, %16"
-                : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7])
-                : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]), "v"(off[7]),
-                  "s"(dbase)
-                : "memory");
-        };
-        auto landed = [](u32x4 (&r)[G]) {
-            asm volatile("s_waitcnt vmcnt(0)"
-                         : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7])
-                         :
-                         : "memory");
-        };
-        u32x4 rcur[G], rnxt[G];
-        fetch(0, rcur);
-        landed(rcur);
-        unsigned seen = 0;  // lane 0: the band above's progress last read
-        const int ngrp = (nch + 63 + G - 1) / G;
-        for (int g = 0; g < ngrp; ++g) {
-            const int s0 = g * G;
-            u32x4 ab[G];
-#pragma unroll
-            for (int t = 0; t < G; ++t) ab[t] = u32x4{0, 0, 0, 0};
-            if (lane == 0 && s0 < nch && (glob_in || lds_in)) {
-                const unsigned need = (unsigned)min(s0 + G, nch);
-                if (glob_in) {
-                    while (seen < need) {
-                        seen = __hip_atomic_load(pg + band - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (seen < need) __builtin_amdgcn_s_sleep(1);
-                    }
-                    uint32_t off[G];
-#pragma unroll
-                    for (int t = 0; t < G; ++t) off[t] = 16u * (uint32_t)min(s0 + t, nch - 1);
-                    const uint64_t base = uniform_u64(above);
-                    asm volatile(
-                        "s_nop 4\n\t"
-                        "global_load_dwordx4 %0, %8, %16 sc1\n\t"
-                        "global_load_dwordx4 %1, %9, %16 sc1\n\t"
-                        "global_load_dwordx4 %2, %10, %16 sc1\n\t"
-                        "global_load_dwordx4 %3, %11, %16 sc1\n\t"
-                        "global_load_dwordx4 %4, %12, %16 sc1\n\t"
-                        "global_load_dwordx4 %5, %13, %16 sc1\n\t"
-                        "global_load_dwordx4 %6, %14, %16 sc1\n\t"
-                        "global_load_dwordx4 %7, %15, %16 sc1\n\t"
-                        "s_waitcnt vmcnt(0)"
-                        : "=&v"(ab[0]), "=&v"(ab[1]), "=&v"(ab[2]), "=&v"(ab[3]), "=&v"(ab[4]), "=&v"(ab[5]), "=&v"(ab[6]),
-                          "=&v"(ab[7])
-                        : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]),
-                          "v"(off[7]), "s"(base)
-                        : "memory");
-                } else {
-                    while (seen < seq + need) {
-                        seen = vprog[wave - 1];
-                        if (seen < seq + need) __builtin_amdgcn_s_sleep(1);
-                    }
-                    asm volatile("" ::: "memory");
-#pragma unroll
-                    for (int t = 0; t < G; ++t) ab[t] = s_ring[wave - 1][(seq + (unsigned)min(s0 + t, nch - 1)) % R];
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    vcons[wave] = seq + need;  // read: the producer may reuse those slots
-                }
-            }
-            if (g + 1 < ngrp) fetch(s0 + G, rnxt);
-            // this group writes ring chunks up to jmax: their slots must have been read
-            const int jmax = min(s0 + G - 1 - 63, nch - 1);
-            if (lds_out && lane == 63 && jmax >= R) {
-                const unsigned want = seq + (unsigned)(jmax - R + 1);
-                while (vcons[wave + 1] < want) __builtin_amdgcn_s_sleep(1);
-                asm volatile("" ::: "memory");
-            }
-#pragma unroll
-            for (int t = 0; t < G; ++t) {
-                const int j = s0 + t - lane;
-                uint32_t nup[4];
-                nup[0] = wave_shr1(cur[0], ab[t].x);
-                nup[1] = wave_shr1(cur[1], ab[t].y);
-                nup[2] = wave_shr1(cur[2], ab[t].z);
-                nup[3] = wave_shr1(cur[3], ab[t].w);
-                if (live && j >= 0 && j < nch) {
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) { prevup[k] = up[k]; up[k] = nup[k]; prevcur[k] = cur[k]; }
-                    if (j == 0) {
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) { prevup[k] = 0; prevcur[k] = 0; }
-                    }
-                    uint32_t o[4];
-                    unfilter_chunk<BPP, SWAR>(rcur[t], up, prevup, prevcur, fm, o);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) cur[k] = o[k];
-                    const u32x4 ov = {o[0], o[1], o[2], o[3]};
-                    if (glob_out) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(row + 16 * j), "v"(ov) : "memory");
-                    else asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(row + 16 * j), "v"(ov) : "memory");
-                    if (lds_out && lane == 63) s_ring[wave][(seq + (unsigned)j) % R] = ov;
-                }
-            }
-            // the band's last row publishes the chunks it finished in this group
-            const int jl = s0 + G - 1 - 63;
-            if (lane == 63 && live && jl >= 0) {
-                if (lds_out) {
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the ring chunks are in LDS
-                    vprog[wave] = seq + (unsigned)min(jl + 1, nch);
-                } else if (glob_out) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its sc1 stores have completed
-                    __hip_atomic_store(pg + band, (unsigned)min(jl + 1, nch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            if (g + 1 < ngrp) {
-                landed(rnxt);
-#pragma unroll
-                for (int t = 0; t < G; ++t) rcur[t] = rnxt[t];
-            }
-        }
-    }
-}
-
-// The same wavefront over 8-byte chunks (BPP <= 4).  The chain of a frame is
-// (row chunks + rows) steps -- every band starts 64 steps after the one above it,
-// so with 16-byte chunks 4,096 of a 4096^2 RGBA frame's 5,120 steps are that lag --
-// and a step's cost is the chunk's bytes: halving the chunk takes the chain to
-// 2,048 + 4,096 steps of half the work.
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t byte2(const uint32_t (&w)[2], int i) { return (w[i >> 2] >> (8 * (i & 3))) & 255u; }
-
-template <int BPP>
-__device__ __forceinline__ void unfilter_chunk8(const u32x2& rawv, const uint32_t (&up)[2], const uint32_t (&prevup)[2],
-                                                const uint32_t (&prevcur)[2], const FtMask& fm, uint32_t (&o)[2]) {
-    const uint32_t raw[2] = {rawv.x, rawv.y};
-    o[0] = o[1] = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t a = i >= BPP ? ((o[(i - BPP) >> 2] >> (8 * ((i - BPP) & 3))) & 255u) : byte2(prevcur, 8 + i - BPP);
-        const uint32_t b = byte2(up, i);
-        const uint32_t c = i >= BPP ? byte2(up, i - BPP) : byte2(prevup, 8 + i - BPP);
-        const int d1 = (int)b - (int)c, d2 = (int)a - (int)c;
-        const int pa = d1 < 0 ? -d1 : d1, pb = d2 < 0 ? -d2 : d2, pc = (d1 + d2) < 0 ? -(d1 + d2) : (d1 + d2);
-        const uint32_t paeth = (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
-        const uint32_t pred = (a & fm.sub) | (b & fm.up) | (((a + b) >> 1) & fm.avg) | (paeth & fm.paeth);
-        const uint32_t v = (byte2(raw, i) + pred) & 255u;
-        o[i >> 2] |= v << (8 * (i & 3));
-    }
-}
-
-template <int BPP>
-__global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter8(const PngImgDev* imgs, const int2* groups,
-                                                                       const int* prog_base, unsigned* prog,
-                                                                       unsigned* ticket) {
-    raise_priority();
-    static_assert(BPP <= 4, "8-byte chunks carry at most 4 bytes of left context");
-    constexpr int NW = kPngUnfilterThreads / 64, G = kUnfG;
-    __shared__ int s_t;
-    if (threadIdx.x == 0) s_t = (int)atomicAdd(ticket, 1u);
-    __syncthreads();
-    const int2 gk = groups[s_t];  // (image, workgroup of the image)
-    const PngImgDev I = imgs[gk.x];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int nch = (I.rowbytes + 7) >> 3;
-    const int nbands = (I.H + 63) >> 6;
-    const int K = png_unfilter_groups(I.H);
-    unsigned* pg = prog + prog_base[gk.x];
-    for (int band = wave * K + gk.y; band < nbands; band += NW * K) {
-        const int y = band * 64 + lane;
-        const bool live = y < I.H;
-        IK_GLOBAL uint8_t* row = (IK_GLOBAL uint8_t*)(I.dst + (size_t)(live ? y : 0) * I.pitch);
-        const FtMask fm(live ? ((const IK_GLOBAL uint8_t*)I.ft)[y] : 0u);
-        const uint64_t above = band > 0 ? (uint64_t)(size_t)(I.dst + (size_t)(band * 64 - 1) * I.pitch) : 0;
-        uint32_t cur[2] = {0, 0}, up[2] = {0, 0};
-        uint32_t prevcur[2] = {0, 0}, prevup[2] = {0, 0};  // last chunk (left context)
-        const uint64_t dbase = uniform_u64((uint64_t)(size_t)I.dst);
-        const uint32_t rowoff = (uint32_t)((size_t)(live ? y : 0) * I.pitch);
-        auto fetch = [&](int s0, u32x2 (&r)[G]) {
-            uint32_t off[G];
-#pragma unroll
-            for (int t = 0; t < G; ++t) off[t] = rowoff + 8u * (uint32_t)min(max(s0 + t - lane, 0), nch - 1);
-            asm volatile(
-                "s_nop 4\n\t"
-                "global_load_dwordx2 %0, %8, %16\n\t"
-                "global_load_dwordx2 %1, %9, %16\n\t"
-                "global_load_dwordx2 %2, %10, %16\n\t"
-                "global_load_dwordx2 %3, %11, %16\n\t"
-                "global_load_dwordx2 %4, %12, %16\n\t"
-                "global_load_dwordx2 %5, %13, %16\n\t"
-                "global_load_dwordx2 %6, %14, %16\n\t"
-                "global_load_dwordx2 %7, %15, %16"
-                : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7])
-                : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]), "v"(off[7]),
-                  "s"(dbase)
-                : "memory");
-        };
-        auto landed = [](u32x2 (&r)[G]) {
-            asm volatile("s_waitcnt vmcnt(0)"
-                         : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7])
-                         :
-                         : "memory");
-        };
-        u32x2 rcur[G], rnxt[G];
-        fetch(0, rcur);
-        landed(rcur);
-        unsigned seen = 0;  // lane 0: the previous band's progress last read
-        const int ngrp = (nch + 63 + G - 1) / G;
-        for (int g = 0; g < ngrp; ++g) {
-            const int s0 = g * G;
-            u32x2 ab[G];
-#pragma unroll
-            for (int t = 0; t < G; ++t) ab[t] = u32x2{0, 0};
-            if (lane == 0 && above && s0 < nch) {
-                const unsigned need = (unsigned)min(s0 + G, nch);
-                while (seen < need) {
-                    seen = __hip_atomic_load(pg + band - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (seen < need) __builtin_amdgcn_s_sleep(1);
-                }
-                uint32_t off[G];
-#pragma unroll
-                for (int t = 0; t < G; ++t) off[t] = 8u * (uint32_t)min(s0 + t, nch - 1);
-                const uint64_t base = uniform_u64(above);
-                asm volatile(
-                    "s_nop 4\n\t"
-                    "global_load_dwordx2 %0, %8, %16 sc1\n\t"
-                    "global_load_dwordx2 %1, %9, %16 sc1\n\t"
-                    "global_load_dwordx2 %2, %10, %16 sc1\n\t"
-                    "global_load_dwordx2 %3, %11, %16 sc1\n\t"
-                    "global_load_dwordx2 %4, %12, %16 sc1\n\t"
-                    "global_load_dwordx2 %5, %13, %16 sc1\n\t"
-                    "global_load_dwordx2 %6, %14, %16 sc1\n\t"
-                    "global_load_dwordx2 %7, %15, %16 sc1\n\t"
-                    "s_waitcnt vmcnt(0)"
-                    : "=&v"(ab[0]), "=&v"(ab[1]), "=&v"(ab[2]), "=&v"(ab[3]), "=&v"(ab[4]), "=&v"(ab[5]), "=&v"(ab[6]),
-                      "=&v"(ab[7])
-                    : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]),
-                      "v"(off[7]), "s"(base)
-                    : "memory");
-            }
-            if (g + 1 < ngrp) fetch(s0 + G, rnxt);
-#pragma unroll
-            for (int t = 0; t < G; ++t) {
-                const int j = s0 + t - lane;
-                uint32_t nup[2];
-                nup[0] = wave_shr1(cur[0], ab[t].x);
-                nup[1] = wave_shr1(cur[1], ab[t].y);
-                if (live && j >= 0 && j < nch) {
-#pragma unroll
-                    for (int k = 0; k < 2; ++k) { prevup[k] = up[k]; up[k] = nup[k]; prevcur[k] = cur[k]; }
-                    if (j == 0) {
-#pragma unroll
-                        for (int k = 0; k < 2; ++k) { prevup[k] = 0; prevcur[k] = 0; }
-                    }
-                    uint32_t o[2];
-                    unfilter_chunk8<BPP>(rcur[t], up, prevup, prevcur, fm, o);
-                    cur[0] = o[0];
-                    cur[1] = o[1];
-                    const u32x2 ov = {o[0], o[1]};
-                    asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(row + 8 * j), "v"(ov) : "memory");
-                }
-            }
-            const int jl = s0 + G - 1 - 63;
-            if (lane == 63 && live && jl >= 0) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its sc1 stores have completed
-                __hip_atomic_store(pg + band, (unsigned)min(jl + 1, nch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (g + 1 < ngrp) {
-                landed(rnxt);
-#pragma unroll
-                for (int t = 0; t < G; ++t) rcur[t] = rnxt[t];
-            }
-        }
-    }
-}
-
 // ---- small transfers through the compute queue ---------------------------------------
 __global__ __launch_bounds__(256) void k_copy_words(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                                     size_t n) {
@@ -1831,12 +1295,7 @@ hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, con
 hipError_t launch_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int n, const uint16_t* tok, int* status,
                              hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    static const int which = [] {  // IK_PNG_EXPAND=1: the per-position search kernel
-        const char* e = getenv("IK_PNG_EXPAND");
-        return e && !strcmp(e, "1") ? 1 : 2;
-    }();
-    if (which == 1) hipLaunchKernelGGL(k_png_expand, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status);
-    else hipLaunchKernelGGL(k_png_expand4, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status);
+    hipLaunchKernelGGL(k_png_expand4, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status);
     return hipGetLastError();
 }
 
@@ -1847,59 +1306,19 @@ hipError_t launch_png_resolve(const PngImgDev* imgs, const int2* rows, int nrows
     return hipGetLastError();
 }
 
-// IK_PNG_UNF_BLK=1: blocked bands (LDS hand-off inside a 4-wave workgroup).  Off by
-// default: measured 10.8 vs 7.8 ms per step against the interleaved layout
-// (profiles/r03s_unfilter_blk.txt) -- the four waves of a block sit on one CU and
-// wait on each other in a chain, where interleaved bands of different images fill
-// the CU's other slots.
-bool png_unfilter_blocked() {
-    static const bool blk = [] {
-        const char* e = getenv("IK_PNG_UNF_BLK");
-        const char* n = getenv("IK_PNG_UNF8");  // (the 8-byte-chunk variant keeps the interleaved layout)
-        return e && !strcmp(e, "1") && !(n && !strcmp(n, "1"));
-    }();
-    return blk;
-}
-
+// 4- and 8-byte pixels (RGBA8, La16, Rgba16) take the word-at-a-time chunk (ik_unfilter.h)
 hipError_t launch_png_unfilter(const PngImgDev* imgs, const int2* groups, int ngroups, const int* prog_base,
                                unsigned* prog, unsigned* ticket, int bpp, hipStream_t s) {
     if (ngroups <= 0) return hipSuccess;
-    const dim3 grid(ngroups), block(png_unfilter_blocked() ? kPngUnfBlkWaves * 64 : kPngUnfilterThreads);
-    // IK_PNG_UNF8=1: 8-byte chunks (measured slower on MI355X: 15.3 vs 8.7 ms per
-    // 64 4096^2 RGBA frames, beside the next batch's block search)
-    static const bool narrow = [] {
-        const char* e = getenv("IK_PNG_UNF8");
-        return e && !strcmp(e, "1");
-    }();
-    if (narrow && bpp <= 4) {
-#define IK_UNF8(B) hipLaunchKernelGGL(k_png_unfilter8<B>, grid, block, 0, s, imgs, groups, prog_base, prog, ticket)
-        switch (bpp) {
-        case 1: IK_UNF8(1); break;
-        case 2: IK_UNF8(2); break;
-        case 3: IK_UNF8(3); break;
-        default: IK_UNF8(4); break;
-        }
-#undef IK_UNF8
-        return hipGetLastError();
-    }
-    // IK_PNG_UNF_SWAR=0: the byte-at-a-time chunk for 4- and 8-byte pixels too (A/B)
-    static const bool swar = [] {
-        const char* e = getenv("IK_PNG_UNF_SWAR");
-        return !(e && !strcmp(e, "0"));
-    }();
-    const bool blk = png_unfilter_blocked();
-#define IK_UNF(B, W)                                                                                            \
-    do {                                                                                                        \
-        if (blk) hipLaunchKernelGGL((k_png_unfilter_blk<B, W>), grid, block, 0, s, imgs, groups, prog_base, prog, ticket); \
-        else hipLaunchKernelGGL((k_png_unfilter<B, W>), grid, block, 0, s, imgs, groups, prog_base, prog, ticket);    \
-    } while (0)
+    const dim3 grid(ngroups), block(kPngUnfilterThreads);
+#define IK_UNF(B, W) hipLaunchKernelGGL((k_png_unfilter<B, W>), grid, block, 0, s, imgs, groups, prog_base, prog, ticket)
     switch (bpp) {
     case 1: IK_UNF(1, false); break;
     case 2: IK_UNF(2, false); break;
     case 3: IK_UNF(3, false); break;
-    case 4: if (swar) IK_UNF(4, true); else IK_UNF(4, false); break;
+    case 4: IK_UNF(4, true); break;
     case 6: IK_UNF(6, false); break;
-    case 8: if (swar) IK_UNF(8, true); else IK_UNF(8, false); break;
+    case 8: IK_UNF(8, true); break;
     default: return hipErrorInvalidValue;
     }
 #undef IK_UNF

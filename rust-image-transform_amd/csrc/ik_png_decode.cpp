@@ -392,11 +392,11 @@ struct AreaPool {
     std::condition_variable cv;
     std::vector<UploadArea*> areas;
 };
+std::mutex g_area_mu;
+std::map<int, AreaPool*> g_area_pools;
 AreaPool& area_pool(int device) {
-    static std::mutex mu;
-    static std::map<int, AreaPool*> pools;
-    std::lock_guard<std::mutex> lk(mu);
-    AreaPool*& p = pools[device];
+    std::lock_guard<std::mutex> lk(g_area_mu);
+    AreaPool*& p = g_area_pools[device];
     if (!p) p = new AreaPool();
     return *p;
 }
@@ -450,6 +450,31 @@ bool area_reserve(UploadArea* a, size_t dev_bytes, size_t pin_bytes) {
     return true;
 }
 
+}  // namespace
+
+// ik_shutdown: the upload areas' device and pinned buffers and events (no batch is
+// in flight: the stage threads have ended)
+void png_shutdown() {
+    std::vector<AreaPool*> ps;
+    {
+        std::lock_guard<std::mutex> lk(g_area_mu);
+        for (auto& kv : g_area_pools) ps.push_back(kv.second);
+    }
+    for (AreaPool* P : ps) {
+        std::lock_guard<std::mutex> lk(P->mu);
+        for (UploadArea* a : P->areas) {
+            (void)hipSetDevice(a->device);
+            if (a->dev) (void)hipFree(a->dev);
+            if (a->pin) (void)hipHostFree(a->pin);
+            for (hipEvent_t e : a->ev)
+                if (e) (void)hipEventDestroy(e);
+            delete a;
+        }
+        P->areas.clear();
+    }
+}
+
+namespace {
 // the last batch's stage times per device (ik_png_last_timing)
 std::mutex g_timing_mu;
 std::map<int, std::vector<double>> g_timing;
@@ -475,7 +500,7 @@ struct PngBatchState {
 };
 
 int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, PngUpload& up) {
-    static const bool timing = getenv("IK_PNG_TIMING") != nullptr;
+    static const bool timing = getenv("IK_TIMING") != nullptr;
     auto st = std::make_shared<PngBatchState>();
     up.st = st;
     up.bytes = bytes;
@@ -656,14 +681,6 @@ int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Png
     return IK_OK;
 }
 
-static bool search_after_resolve() {
-    static const bool v = [] {
-        const char* e = getenv("IK_FIND_AFTER");
-        return e && !strcmp(e, "resolve");
-    }();
-    return v;
-}
-
 // the block search of a batch whose upload was issued: on stream s, once the
 // upload (with its gather + CRC pass) has landed; once per batch
 static void png_find_launch(PngBatchState& S, hipStream_t s) {
@@ -695,22 +712,18 @@ void png_find_prelaunch(PngUpload& up, hipStream_t s) {
 // Decode lanes in launch order.  All lanes of a batch run in one round (two waves
 // per SIMD), and a wave lasts as long as its longest lane, so the kernel ends with
 // the slowest waves -- the longest blocks, ~20 % past the mean lane
-// (IK_PNG_TIMING: 8,729 mean / 10,171 max steps).  Lanes sorted by compressed
+// (IK_TIMING: 8,729 mean / 10,171 max steps).  Lanes sorted by compressed
 // length, longest first, fill the first half of the waves; the second half takes
 // the shortest first, so wave i and wave W/2 + i -- which the dispatcher puts on
 // the same SIMD, one round of waves apart -- pair a long group with a short one
 // and the long wave runs alone once its partner is done.  The kernel reads lane
 // order[slot] at launch slot `slot` and writes that lane's result in place, so the
 // lane table and its results keep job order.  Returns false (no order table) for
-// small launches and under IK_PNG_LANE_ORDER=0 (A/B).
+// small launches.
 static bool order_lanes(const std::vector<PngLaneDev>& hl, const std::vector<PngJob*>& J,
                         std::vector<uint32_t>& order) {
-    static const bool on = [] {
-        const char* e = getenv("IK_PNG_LANE_ORDER");
-        return !(e && !strcmp(e, "0"));
-    }();
     const size_t n = hl.size();
-    if (!on || n < 2 * 64) return false;
+    if (n < 2 * 64) return false;
     // counting sort on the length in 512-bit buckets, longest first: O(n), as this
     // sits on the host between the decode rounds
     constexpr uint32_t kBuckets = 1024;
@@ -738,7 +751,7 @@ static bool order_lanes(const std::vector<PngLaneDev>& hl, const std::vector<Png
 }
 
 int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* msgs) {
-    static const bool timing = getenv("IK_PNG_TIMING") != nullptr;
+    static const bool timing = getenv("IK_TIMING") != nullptr;
     const double t0 = now_ms();
     double tim[kPngTimingFields] = {};
     Events& ev = events();
@@ -797,7 +810,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             nrows += j->h;
             npages += (j->raw_total >> kPngPageShift) + 1;
             nbands += ((size_t)j->h + 63) / 64;
-            ngroups += (size_t)(png_unfilter_blocked() ? png_unfilter_blk_groups((int)j->h) : png_unfilter_groups((int)j->h));
+            ngroups += (size_t)png_unfilter_groups((int)j->h);
         }
         // unfilter: band-group table + per-image band offsets (staged), then one
         // progress counter per band and one ticket per class (zeroed)
@@ -902,7 +915,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         const double t1 = now_ms();
         tim[15] = t1 - t0;  // from the stage's start until the candidates are back (upload wait + search)
         const double t2 = now_ms();
-        double mk[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // dev timing marks (IK_PNG_TIMING)
+        double mk[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // dev timing marks (IK_TIMING)
         // the lane plans, one job per pool task (the decode waits on this host work)
         parallel_for(m, 0, [&](int k) {
             PngJob* j = J[k];
@@ -1036,7 +1049,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             size_t roff = ~size_t(0);
             const size_t rbytes = sizeof(infl::LaneResult) * hl.size();
             if (e2 == hipSuccess) e2 = X.d2h_start(d_res, rbytes, &roff, ev.ok ? ev.e[10] : nullptr);
-            if (e2 == hipSuccess && !search_done && up.on_next_search && !search_after_resolve()) {
+            if (e2 == hipSuccess && !search_done && up.on_next_search) {
                 up.on_next_search(nullptr);
                 search_done = true;
             }
@@ -1147,9 +1160,8 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             mk[2] = now_ms();  // lane tables uploaded
             // the next batch's block search (VALU-bound) beside this batch's expand,
             // resolve and unfilter, which run at a raised wave priority (ik_png.hip
-            // raise_priority): the stage executor's hook.  IK_FIND_AFTER=resolve
-            // holds it until this batch's resolve pass is done.
-            if (!rc && !search_done && up.on_next_search && !search_after_resolve()) {
+            // raise_priority): the stage executor's hook
+            if (!rc && !search_done && up.on_next_search) {
                 up.on_next_search(nullptr);
                 search_done = true;
             }
@@ -1174,8 +1186,6 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                 if (e3 == hipSuccess) e3 = launch_png_resolve(d_imgs, d_rows, (int)hrows.size(),
                                                               reinterpret_cast<int*>(dev + o_err), s);
                 rec(6, s);
-                if (e3 == hipSuccess && up.on_next_search && search_after_resolve())
-                    up.on_next_search(ev.ok ? ev.e[6] : nullptr);
                 // unfilter: one launch per bytes-per-pixel class, over that class's
                 // images; a workgroup per 16 bands, its (image, group) by ticket
                 if (e3 == hipSuccess) {
@@ -1189,8 +1199,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                         const Range r{bpp, (int)cls.size(), (int)groups.size()};
                         for (int k = 0; k < m; ++k)
                             if (J[k]->state == 1 && hd[k].bpp == bpp) {
-                                for (int g = 0; g < (png_unfilter_blocked() ? png_unfilter_blk_groups(hd[k].H)
-                                                                            : png_unfilter_groups(hd[k].H)); ++g)
+                                for (int g = 0; g < png_unfilter_groups(hd[k].H); ++g)
                                     groups.push_back(make_int2((int)cls.size() - r.img0, g));
                                 pbase.push_back(band0);
                                 band0 += (hd[k].H + 63) / 64;

@@ -59,18 +59,6 @@ int default_threads() {
 
 // ---- phase gates -----------------------------------------------------------------
 namespace {
-// IK_BATCH_GATE: unset = both gates, 0 = none, "upload" = the upload gate only
-int gates_mask() {
-    static const int m = [] {
-        const char* e = getenv("IK_BATCH_GATE");
-        if (!e) return 3;
-        if (!strcmp(e, "0")) return 0;
-        if (!strcmp(e, "upload")) return 1;
-        return 3;
-    }();
-    return m;
-}
-bool gates_on(int which) { return (gates_mask() >> which) & 1; }
 std::mutex& gate_mutex(int device, int which) {
     static std::mutex m[64][2];
     return m[(unsigned)device % 64u][which & 1];
@@ -83,7 +71,7 @@ thread_local GateState t_gate;
 }  // namespace
 
 void gate_enter(int which) {
-    if (!gates_on(which) || t_gate.held[which]) return;
+    if (t_gate.held[which]) return;
     const int d = current_device();
     gate_mutex(d, which).lock();
     t_gate.held[which] = true;
@@ -91,7 +79,7 @@ void gate_enter(int which) {
 }
 
 bool gate_try_enter(int which) {
-    if (!gates_on(which) || t_gate.held[which]) return true;
+    if (t_gate.held[which]) return true;
     const int d = current_device();
     if (!gate_mutex(d, which).try_lock()) return false;
     t_gate.held[which] = true;
@@ -116,12 +104,26 @@ void gate_pin(int which, bool on) {
 Pool::Pool(int device, int max_threads) : device_(device), max_threads_(std::max(1, max_threads)) {}
 
 void Pool::ensure(int nthreads) {
-    // called with mu_ held
+    // called with mu_ held; workers live until stop() (ik_shutdown)
     nthreads = std::min(nthreads, max_threads_);
     while (nthreads_ < nthreads) {
-        std::thread([this] { loop(); }).detach();  // lives as long as the process
+        threads_.emplace_back([this] { loop(); });
         ++nthreads_;
     }
+}
+
+void Pool::stop() {
+    std::vector<std::thread> ts;
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        stop_ = true;
+        ts.swap(threads_);
+    }
+    cv_.notify_all();
+    for (std::thread& t : ts) t.join();
+    std::lock_guard<std::mutex> lk(mu_);
+    nthreads_ = 0;
+    stop_ = false;
 }
 
 void Pool::loop() {
@@ -135,7 +137,8 @@ void Pool::loop() {
         std::function<void()> task;
         {
             std::unique_lock<std::mutex> lk(mu_);
-            cv_.wait(lk, [&] { return !q_.empty(); });
+            cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+            if (q_.empty()) break;  // stopped, nothing left to run
             task = std::move(q_.front().fn);
             q_.pop_front();
             ++busy_;
@@ -144,6 +147,7 @@ void Pool::loop() {
         std::lock_guard<std::mutex> lk(mu_);
         --busy_;
     }
+    release_thread_resources();  // while the runtime is alive (not a thread-exit destructor)
 }
 
 void Pool::post(std::function<void()> task) { post_tagged(std::move(task), nullptr); }
@@ -215,11 +219,14 @@ void Pool::parallel_for(int n, int threads, const std::function<void(int)>& fn) 
     withdraw(st.get());
 }
 
+namespace {
+std::mutex g_dpool_mu;
+std::map<int, Pool*> g_dpools;  // never freed: a Pool& handed out stays valid
+}  // namespace
+
 Pool& device_pool(int device) {
-    static std::mutex mu;
-    static std::map<int, Pool*> pools;
-    std::lock_guard<std::mutex> lk(mu);
-    Pool*& p = pools[device];
+    std::lock_guard<std::mutex> lk(g_dpool_mu);
+    Pool*& p = g_dpools[device];
     if (!p) p = new Pool(device, env_int("IK_MAX_WORKERS", 256));
     return *p;
 }
@@ -283,6 +290,25 @@ int sched_configure(const int* devices, int n) {
     }
     s.multi = true;
     return IK_OK;
+}
+
+void pools_shutdown() {
+    Sched& s = sched();
+    {
+        std::lock_guard<std::mutex> lk(s.mu);
+        for (auto& L : s.devs) L->pool->stop();
+        // (the Logical records stay allocated: a caller may still hold a pool
+        // reference; a later ik_init(-1) configures afresh)
+        for (auto& L : s.devs) (void)L.release();
+        s.devs.clear();
+        s.multi = false;
+    }
+    std::vector<Pool*> ps;
+    {
+        std::lock_guard<std::mutex> lk(g_dpool_mu);
+        for (auto& kv : g_dpools) ps.push_back(kv.second);
+    }
+    for (Pool* p : ps) p->stop();
 }
 
 bool sched_multi() { return sched().multi; }

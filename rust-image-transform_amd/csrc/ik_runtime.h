@@ -8,6 +8,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ik_internal.h"
@@ -52,6 +53,9 @@ public:
     void parallel_for(int n, int threads, const std::function<void(int)>& fn);
     void post(std::function<void()> task);  // run on a worker (device already selected)
     int device() const { return device_; }
+    // ik_shutdown: run what is queued, then end and join every worker (each
+    // releases its streams and arenas first); the pool takes work again after
+    void stop();
 
 private:
     struct Task {
@@ -64,13 +68,50 @@ private:
     void loop();
     int device_, max_threads_;
     int nthreads_ = 0, busy_ = 0;
+    bool stop_ = false;
     std::mutex mu_;
     std::condition_variable cv_;
     std::deque<Task> q_;
+    std::vector<std::thread> threads_;
 };
 Pool& device_pool(int device);  // the persistent workers of a physical device
 // fn(i) for i in [0, n) on the calling thread's device pool (and the caller)
 void parallel_for(int n, int threads, const std::function<void(int)>& fn);
+
+// Figures of the last batch each device's kernel stage ran (ik_batch_last_timing):
+// device ms from HIP events on the kernel stream and the algorithmic bytes of the
+// same launches.  Reset when a batch's kernel stage starts; summed over its launches.
+enum BatchTimingField {
+    kBtJpegHuffMs = 0,   // JPEG entropy decoding launches (restart intervals / self-sync)
+    kBtJpegScanBytes,    // entropy-coded bytes they read
+    kBtJpegCoefBytes,    // int16 coefficients they wrote
+    kBtJpegImages,
+    kBtJpegLanes,        // decoder lanes (restart intervals or self-sync subsequences)
+    kBtResizeMs,         // grouped resize launches
+    kBtResizeBytes,      // C*W*H in + C*w*h out per image
+    kBtResizeImages,
+    kBtJpegEncMs,        // batched JPEG encoder (coefficients + Huffman) launches
+    kBtJpegEncImages,
+    kBtFields
+};
+void batch_timing_reset(int device);
+void batch_timing_commit(int device);  // the kernel stage is done: its figures become the last batch's
+void batch_timing_add(int device, int field, double v);
+// a pair of events on the calling thread (timing one launch sequence); ms between them
+struct EvPair {
+    hipEvent_t a = nullptr, b = nullptr;
+};
+EvPair& thread_events(int which);  // which < 4
+float ev_pair_ms(const EvPair& e);
+
+// ik_shutdown: stop and join every pool's workers (device and logical pools);
+// multi-device dispatch is unconfigured
+void pools_shutdown();
+// release the calling thread's streams and arenas (synchronised first); a later
+// call on this thread creates them again
+void release_thread_resources();
+void png_shutdown();    // the PNG upload areas (ik_png_decode.cpp)
+void plans_shutdown();  // the cached resize plans (ik_plan.cpp)
 
 // multi-device dispatch (ik_init(-1) / IK_DEVICES): logical devices, least outstanding cost
 int sched_configure(const int* devices, int n);
@@ -91,7 +132,6 @@ uint64_t request_cost(const uint8_t* b, size_t n, int64_t w, int64_t h, int fmt)
 
 hipStream_t thread_stream();  // per-thread, per-device non-blocking stream
 hipStream_t thread_copy_stream();  // a second one, for uploads that overlap the first's kernels
-hipStream_t search_stream();       // a third, on a hardware queue of its own (the next batch's block search)
 size_t pitch_for(uint32_t w, uint32_t c);
 uint8_t* scratch(size_t bytes);  // per-thread device scratch, valid until the next call
 // per-thread, per-device grow-only device arenas for batch work (slot 1: JPEG

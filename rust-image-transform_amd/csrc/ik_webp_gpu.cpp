@@ -82,20 +82,7 @@ int Vp8Work::launch(const uint8_t* d_yuv, size_t yuv_stride, int n, int quality,
     a.nz = d_nz;
     a.q = vp8::qparams_for_quality((float)quality);
     a.stamps = nullptr;
-    const int T = (a.mb_w - 1) + 2 * (a.mb_h - 1) + 1;
-    if (getenv("IK_VP8_STAMPS")) IK_HIP(hipMalloc(&a.stamps, sizeof(unsigned long long) * 8 * T));
     IK_HIP(vp8::launch_vp8_encode(a, n, s));
-    if (a.stamps) {  // dev tool: mean clocks per phase of one MB per diagonal
-        std::vector<unsigned long long> st((size_t)8 * T);
-        IK_HIP(hipStreamSynchronize(s));
-        IK_HIP(hipMemcpy(st.data(), a.stamps, st.size() * 8, hipMemcpyDeviceToHost));
-        double ph[4] = {0, 0, 0, 0};
-        for (int t = 0; t < T; ++t)
-            for (int k = 0; k < 4; ++k) ph[k] += (double)(st[8 * t + k + 1] - st[8 * t + k]) / T;
-        fprintf(stderr, "[vp8 stamps] per MB (memtime ticks): load %.0f search %.0f decide %.0f out %.0f; diag span %.0f\n",
-                ph[0], ph[1], ph[2], ph[3], (double)(st[8 * (T - 1)] - st[0]) / (T - 1));
-        (void)hipFree(a.stamps);
-    }
     return IK_OK;
 }
 

@@ -6,6 +6,7 @@ rust-image-transform_amd` (or `__graft_entry__.build()`) first.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 import threading
@@ -22,6 +23,7 @@ c_img_p = ctypes.c_void_p
 # (name, restype, argtypes) for every entry point declared in include/imagekit_hip.h
 SIGNATURES = [
     ("ik_init", ctypes.c_int, [ctypes.c_int]),
+    ("ik_shutdown", ctypes.c_int, []),
     ("ik_device_count", ctypes.c_int, []),
     ("ik_init_devices", ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ("ik_logical_device_count", ctypes.c_int, []),
@@ -63,6 +65,7 @@ SIGNATURES = [
     ("ik_set_resize_mode", ctypes.c_int, [ctypes.c_int]),
     ("ik_set_png_gpu_min", ctypes.c_int, [ctypes.c_longlong]),
     ("ik_png_last_timing", ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
+    ("ik_batch_last_timing", ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     ("ik_png_counters", ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
     ("ik_jpeg_counters", ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
     ("ik_get_resize_mode", ctypes.c_int, []),
@@ -105,6 +108,10 @@ def load() -> ctypes.CDLL:
             fn.restype = res
             fn.argtypes = args
         _lib = lib
+        # orderly teardown while the HIP runtime is alive (ik_shutdown: the worker
+        # and stage threads end, streams and arenas are released), not in
+        # destructors during process exit
+        atexit.register(lib.ik_shutdown)
         return lib
 
 

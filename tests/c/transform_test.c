@@ -354,6 +354,32 @@ static int test_resize_reduces_size(void) {
     return 0;
 }
 
+/* Not a reference test: a batch through the stage threads and worker pools, then
+ * ik_shutdown (orderly teardown: the threads end, streams and arenas are freed)
+ * and a second ik_shutdown (idempotent).  The process then exits through the
+ * HIP runtime's own teardown with nothing of the library's left to destroy. */
+static int batch_then_shutdown(void) {
+    enum { N = 3 };
+    size_t n;
+    uint8_t *png = zero_rgba_png(300, 200, &n);
+    const uint8_t *bytes[N] = {png, png, png};
+    size_t lens[N] = {n, n, n};
+    int64_t w[N] = {64, 64, 64}, h[N] = {-1, -1, -1};
+    int fmt[N] = {IK_FORMAT_WEBP, IK_FORMAT_JPEG, IK_FORMAT_WEBP}, q[N] = {80, 85, 80}, st[N];
+    uint8_t *outs[N];
+    size_t out_lens[N];
+    const int rc = ik_transform_batch(bytes, lens, N, w, h, fmt, q, IK_FILTER_LANCZOS3, 2, outs, out_lens, st);
+    free(png);
+    CHECK(rc == IK_OK, "ik_transform_batch failed");
+    for (int i = 0; i < N; ++i) {
+        CHECK(out_lens[i] > 0, "empty output");
+        ik_buf_free(outs[i]);
+    }
+    CHECK(ik_shutdown() == IK_OK, "ik_shutdown failed");
+    CHECK(ik_shutdown() == IK_OK, "second ik_shutdown failed");
+    return 0;
+}
+
 int main(void) {
     if (ik_init(0) != IK_OK) {
         char e[256];
@@ -381,6 +407,7 @@ int main(void) {
     run("test_full_pipeline_webp", test_full_pipeline_webp);
     run("test_full_pipeline_avif", test_full_pipeline_avif);
     run("test_resize_reduces_size", test_resize_reduces_size);
+    run("batch_then_shutdown", batch_then_shutdown);
     printf("%d failed\n", failures);
-    return failures;
+    return failures;  /* the process must then exit cleanly (rc == failures) */
 }
