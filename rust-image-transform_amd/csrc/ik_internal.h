@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/imagekit_hip.h"
+#include "ik_jpeg_sync.h"
 
 namespace ik {
 
@@ -122,18 +123,36 @@ struct JpegGeom {
 };
 hipError_t launch_jpeg_reconstruct(const JpegGeom& g, uint8_t* dst, size_t dst_pitch, hipStream_t s);
 
-// Baseline Huffman decoding on the GPU, one thread per restart interval
-// (ik_jpeg.hip k_jpeg_huff).  Tables: 4 DC then 4 AC, canonical form plus a 9-bit
-// lookahead (look = length << 8 | value, length 0 = longer code).
-struct JpegHuffTables {
-    uint16_t look[8][512];
-    int maxcode[8][18], valptr[8][17], mincode[8][17];
-    int lj[8][17];  // left-justified 16-bit bound of the codes up to each length (carried over empty lengths)
-    uint8_t vals[8][256];
-    // AC codes whose code + magnitude bits fit the 9-bit lookahead, decoded in one
-    // lookup (entry: value << 8 | run << 4 | bits; 0 = take the general path)
-    int16_t fast_ac[4][512];
+// Baseline Huffman tables (JpegHuffTables) and the self-synchronising decoder's
+// per-lane code are in ik_jpeg_sync.h (shared with its CPU model).
+//
+// The self-synchronising baseline decoder (ik_jsync.hip), one batch of scans:
+// one image's scan as the unstuffing kernels see it
+struct JsImageDev {
+    const uint8_t* scan;   // the entropy-coded bytes (stuffed, with RSTn markers), device
+    long long scan_len;
+    uint8_t* out;          // unstuffed bytes as big-endian words (scan_len + 4 kPadWords + 8 bytes)
+    long long* ivl;        // interval start bits: ivl_cap entries (intervals + 1)
+    int ivl_cap;
+    int chunk0, nchunks;   // the image's 4 KiB chunks in the batch's chunk table
+    int pad;
+    uint32_t* totals;      // [0] bytes kept, [1] restart markers
+    int* status;           // bit 0 a stray marker, 1 too many restart markers, 4 inconsistent / missing
+                           // blocks, 8 a bad code in the decode pass: the host decoder decides
 };
+hipError_t launch_jsync_unstuff(JsImageDev* imgs, int nimg, const int2* chunks, int nchunks, uint2* counts,
+                                hipStream_t s);
+// wgs: (image, first lane of the image) per 256-lane workgroup; every image's lanes
+// start on a multiple of 256 (jsync::Scan::lane0)
+hipError_t launch_jsync_sync(const jsync::Scan* scans, const int2* wgs, int nwg, jsync::LaneRec* recs, hipStream_t s);
+hipError_t launch_jsync_fix(const jsync::Scan* scans, const int2* wgs, int nwg, jsync::LaneRec* recs, int* changed,
+                            hipStream_t s);
+// bases (segmented prefix sums over each interval's lanes) then the decode pass;
+// chunk_scratch: jsync_chunk_scratch_bytes(lanes); status[image]
+hipError_t launch_jsync_bases_decode(const jsync::Scan* scans, int nimg, const int2* wgs, int nwg,
+                                     const jsync::LaneRec* recs, jsync::LaneBase* bases, void* chunk_scratch,
+                                     int* status, hipStream_t s);
+size_t jsync_chunk_scratch_bytes(long long lanes);
 struct JpegScanArgs {
     const uint8_t* data;          // the scan's entropy-coded bytes (stuffed, with RST markers)
     long long size;

@@ -761,6 +761,9 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kUnfG = 8;
 
 typedef const __attribute__((address_space(1))) u32x4* gu32x4p;
+// buffer intrinsics' cache-policy operand: sc1 (gfx940+ CPol::SC1) -- write-through
+// stores, loads served by L2 past the CU's L1
+constexpr int kCpolSc1 = 16;
 
 // a wave-uniform 64-bit value in SGPRs (readfirstlane returns int: zero-extend
 // each half, or a low word with bit 31 set sign-extends into the high word)
@@ -850,84 +853,60 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngI
     for (int band = wave * K + gk.y; band < nbands; band += NW * K) {
         const int y = band * 64 + lane;
         const bool live = y < I.H;
-        uint8_t* row = I.dst + (size_t)(live ? y : 0) * I.pitch;
         const FtMask fm(live ? I.ft[y] : 0u);
-        const uint64_t above = band > 0 ? (uint64_t)(size_t)(I.dst + (size_t)(band * 64 - 1) * I.pitch) : 0;
+        const bool above = band > 0;
         uint32_t cur[4] = {0, 0, 0, 0}, up[4] = {0, 0, 0, 0};
         uint32_t prevcur[4] = {0, 0, 0, 0}, prevup[4] = {0, 0, 0, 0};  // last chunk (left context)
-        // this lane's filtered chunks for a group of steps (clamped: always a valid
-        // address), as asm loads off the image base: the compiler, which cannot count
-        // the other asm memory ops here, would otherwise wait for them at once
+        // The image through a buffer descriptor: the lane's row offset and chunk in
+        // voffset.  Every load and store here is an intrinsic the compiler sees, so
+        // its own wait counts hold: the prefetch of the next group's chunks is waited
+        // for only where those registers are first read.  (Round 3 issued the loads
+        // as inline asm and "landed" them with an asm s_waitcnt; the register
+        // allocator copied the destination registers before that wait -- v_mov of
+        // registers still being loaded -- so a group could read the previous
+        // group's bytes when its loads were slow: wrong bands in ~1 of 6 frames at
+        // 64-frame batches, none at 8.)
         const uint64_t dbase = uniform_u64((uint64_t)(size_t)I.dst);
+        const size_t ibytes = I.pitch * (size_t)I.H;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)dbase, (short)0, (int)(ibytes < 0x7fffffffu ? ibytes : 0x7fffffffu), 0x00020000);
         const uint32_t rowoff = (uint32_t)((size_t)(live ? y : 0) * I.pitch);
         auto fetch = [&](int s0, u32x4 (&r)[G]) {
-            uint32_t off[G];
 #pragma unroll
-            for (int t = 0; t < G; ++t) off[t] = rowoff + 16u * (uint32_t)min(max(s0 + t - lane, 0), nch - 1);
-            // s_nop 4: VALU-written SGPR (readfirstlane) -> VMEM read needs 5 wait
-            // states, which the hazard recognizer does not insert for inline asm
-            asm volatile(
-                "s_nop 4\n\t"
-                "global_load_dwordx4 %0, %8, %16\n\t"
-                "global_load_dwordx4 %1, %9, %16\n\t"
-                "global_load_dwordx4 %2, %10, %16\n\t"
-                "global_load_dwordx4 %3, %11, %16\n\t"
-                "global_load_dwordx4 %4, %12, %16\n\t"
-                "global_load_dwordx4 %5, %13, %16\n\t"
-                "global_load_dwordx4 %6, %14, %16\n\t"
-                "global_load_dwordx4 %7, %15, %16"
-                : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7])
-                : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]), "v"(off[7]),
-                  "s"(dbase)
-                : "memory");
+            for (int t = 0; t < G; ++t) {
+                const uint32_t off = rowoff + 16u * (uint32_t)min(max(s0 + t - lane, 0), nch - 1);
+                r[t] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
+            }
         };
-        // every vector memory op of this wave has completed; r is read only after it
-        auto landed = [](u32x4 (&r)[G]) {
-            asm volatile("s_waitcnt vmcnt(0)"
-                         : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]), "+v"(r[6]), "+v"(r[7])
-                         :
-                         : "memory");
-        };
-        u32x4 rcur[G], rnxt[G];
-        fetch(0, rcur);
-        landed(rcur);
         unsigned seen = 0;  // lane 0: the previous band's progress last read
         const int ngrp = (nch + 63 + G - 1) / G;
-        for (int g = 0; g < ngrp; ++g) {
+        // one group of G steps on the chunks in `rc`, the next group's prefetched into `rn`
+        auto group = [&](int g, u32x4 (&rc)[G], u32x4 (&rn)[G]) {
             const int s0 = g * G;
             u32x4 ab[G];
 #pragma unroll
             for (int t = 0; t < G; ++t) ab[t] = u32x4{0, 0, 0, 0};
             IK_UNF_T(0);
-            if (lane == 0 && above && s0 < nch) {
+            // Wave-uniform control flow around every load and store (out-of-range
+            // buffer offsets are dropped by the hardware instead of branching per lane),
+            // so that the compiler's wait counts stay exact across the group loop.
+            if (above && s0 < nch) {
                 const unsigned need = (unsigned)min(s0 + G, nch);
-                while (seen < need) {
-                    seen = __hip_atomic_load(pg + band - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                while (seen < need) {  // the whole wave polls lane 0's read of the flag
+                    const unsigned v = __hip_atomic_load(pg + band - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    seen = (unsigned)__builtin_amdgcn_readfirstlane((int)v);
                     if (seen < need) __builtin_amdgcn_s_sleep(1);
                 }
-                uint32_t off[G];
+                // the row above, sc1 (L2-served, past this CU's L1): the hand-off's loads,
+                // lane 0 only (the other lanes' offsets are out of range: zeros)
+                const uint32_t aoff = lane == 0 ? (uint32_t)((size_t)(band * 64 - 1) * I.pitch) : 0x80000000u;
 #pragma unroll
-                for (int t = 0; t < G; ++t) off[t] = 16u * (uint32_t)min(s0 + t, nch - 1);
-                const uint64_t base = uniform_u64(above);
-                asm volatile(
-                    "s_nop 4\n\t"
-                    "global_load_dwordx4 %0, %8, %16 sc1\n\t"
-                    "global_load_dwordx4 %1, %9, %16 sc1\n\t"
-                    "global_load_dwordx4 %2, %10, %16 sc1\n\t"
-                    "global_load_dwordx4 %3, %11, %16 sc1\n\t"
-                    "global_load_dwordx4 %4, %12, %16 sc1\n\t"
-                    "global_load_dwordx4 %5, %13, %16 sc1\n\t"
-                    "global_load_dwordx4 %6, %14, %16 sc1\n\t"
-                    "global_load_dwordx4 %7, %15, %16 sc1\n\t"
-                    "s_waitcnt vmcnt(0)"
-                    : "=&v"(ab[0]), "=&v"(ab[1]), "=&v"(ab[2]), "=&v"(ab[3]), "=&v"(ab[4]), "=&v"(ab[5]), "=&v"(ab[6]),
-                      "=&v"(ab[7])
-                    : "v"(off[0]), "v"(off[1]), "v"(off[2]), "v"(off[3]), "v"(off[4]), "v"(off[5]), "v"(off[6]),
-                      "v"(off[7]), "s"(base)
-                    : "memory");
+                for (int t = 0; t < G; ++t)
+                    ab[t] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                          rs, (int)(aoff + 16u * (uint32_t)min(s0 + t, nch - 1)), 0, kCpolSc1));
             }
             IK_UNF_T(1);
-            if (g + 1 < ngrp) fetch(s0 + G, rnxt);
+            if (g + 1 < ngrp) fetch(s0 + G, rn);
 #pragma unroll
             for (int t = 0; t < G; ++t) {
                 const int j = s0 + t - lane;
@@ -937,7 +916,8 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngI
                 nup[1] = wave_shr1(cur[1], ab[t].y);
                 nup[2] = wave_shr1(cur[2], ab[t].z);
                 nup[3] = wave_shr1(cur[3], ab[t].w);
-                if (live && j >= 0 && j < nch) {
+                const bool act = live && j >= 0 && j < nch;
+                if (act) {
 #pragma unroll
                     for (int k = 0; k < 4; ++k) { prevup[k] = up[k]; up[k] = nup[k]; prevcur[k] = cur[k]; }
                     if (j == 0) {
@@ -945,27 +925,33 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngI
                         for (int k = 0; k < 4; ++k) { prevup[k] = 0; prevcur[k] = 0; }
                     }
                     uint32_t o[4];
-                    unfilter_chunk<BPP, SWAR>(rcur[t], up, prevup, prevcur, fm, o);
+                    unfilter_chunk<BPP, SWAR>(rc[t], up, prevup, prevcur, fm, o);
 #pragma unroll
                     for (int k = 0; k < 4; ++k) cur[k] = o[k];
-                    const u32x4 ov = {o[0], o[1], o[2], o[3]};
-                    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(row + 16 * j), "v"(ov) : "memory");
                 }
+                // every lane issues the store; an inactive lane's offset is out of range (dropped)
+                const u32x4 ov = {cur[0], cur[1], cur[2], cur[3]};
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, ov),
+                                                       rs, (int)(act ? rowoff + 16u * (uint32_t)j : 0x80000000u), 0,
+                                                       kCpolSc1);
             }
             IK_UNF_T(2);
             // the band's last row publishes the chunks it finished in this group
             const int jl = s0 + G - 1 - 63;
-            if (lane == 63 && live && jl >= 0) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its sc1 stores have completed
-                __hip_atomic_store(pg + band, (unsigned)min(jl + 1, nch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (jl >= 0 && band * 64 + 63 < I.H) {  // (wave-uniform)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // lane 63's sc1 stores have completed
+                if (lane == 63)
+                    __hip_atomic_store(pg + band, (unsigned)min(jl + 1, nch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             IK_UNF_T(3);
-            if (g + 1 < ngrp) {
-                landed(rnxt);
-#pragma unroll
-                for (int t = 0; t < G; ++t) rcur[t] = rnxt[t];
-            }
-            IK_UNF_T(4);
+        };
+        // ping-pong between two register sets, no copies: the compiler's wait for a
+        // group's chunks sits at their first read, a group after their loads went out
+        u32x4 ra[G], rb[G];
+        fetch(0, ra);
+        for (int g = 0; g < ngrp; g += 2) {
+            group(g, ra, rb);
+            if (g + 1 < ngrp) group(g + 1, rb, ra);
         }
     }
 #ifdef IK_UNF_PROF

@@ -362,6 +362,26 @@ long long png_gpu_min() {
 }
 }  // namespace
 
+#ifdef IK_PNG_DUMP
+namespace {
+std::mutex g_dump_mu;
+std::vector<std::vector<uint8_t>> g_dump;  // per image of the last batch: H rows of rowbytes, then H filter types
+}  // namespace
+template <typename JV, typename HV>
+static void png_dump_store(const JV& J, const HV& hd, int m) {
+    std::lock_guard<std::mutex> lk(g_dump_mu);
+    g_dump.assign(m, std::vector<uint8_t>());
+    for (int k = 0; k < m; ++k) {
+        if (J[k]->state != 1 || J[k]->idx < 0 || J[k]->idx >= m) continue;
+        const auto& I = hd[k];
+        std::vector<uint8_t>& o = g_dump[J[k]->idx];
+        o.resize((size_t)I.H * I.rowbytes + I.H);
+        (void)hipMemcpy2D(o.data(), I.rowbytes, I.dst, I.pitch, I.rowbytes, I.H, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(o.data() + (size_t)I.H * I.rowbytes, I.ft, I.H, hipMemcpyDeviceToHost);
+    }
+}
+#endif
+
 bool png_gpu_enabled(size_t raw_bytes) {
     const long long v = png_gpu_min();
     return v >= 0 && (long long)raw_bytes >= v;
@@ -1186,6 +1206,12 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                 if (e3 == hipSuccess) e3 = launch_png_resolve(d_imgs, d_rows, (int)hrows.size(),
                                                               reinterpret_cast<int*>(dev + o_err), s);
                 rec(6, s);
+#ifdef IK_PNG_DUMP  // dev experiment: every image's filtered rows and filter types before the unfilter
+                if (e3 == hipSuccess) {
+                    (void)hipStreamSynchronize(s);
+                    png_dump_store(J, hd, m);
+                }
+#endif
                 // unfilter: one launch per bytes-per-pixel class, over that class's
                 // images; a workgroup per 16 bands, its (image, group) by ticket
                 if (e3 == hipSuccess) {
@@ -1399,3 +1425,14 @@ extern "C" int ik_set_png_gpu_min(long long min_raw_bytes) {
     ik::g_png_gpu_min.store(min_raw_bytes < 0 ? -1 : min_raw_bytes);
     return IK_OK;
 }
+
+#ifdef IK_PNG_DUMP
+// dev experiment: image i of the last GPU PNG batch before its unfilter (rows, then filter types)
+extern "C" long long ik_dev_png_dump(int i, uint8_t* out, size_t cap) {
+    std::lock_guard<std::mutex> lk(ik::g_dump_mu);
+    if (i < 0 || i >= (int)ik::g_dump.size()) return -1;
+    const auto& v = ik::g_dump[i];
+    if (out) std::memcpy(out, v.data(), std::min(cap, v.size()));
+    return (long long)v.size();
+}
+#endif
