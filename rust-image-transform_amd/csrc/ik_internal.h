@@ -171,50 +171,11 @@ struct JpegScanArgs {
     // progressive scans (k_jpeg_prog): 1 DC first, 2 DC refine, 3 AC first, 4 AC refine
     int kind, Ss, Se, Al;
 };
-hipError_t launch_jpeg_huff(const JpegScanArgs& a, hipStream_t s);
 // One progressive scan with restart intervals (ik_jpeg.hip k_jpeg_prog): a lane per
 // interval, the EOB run and DC predictions reset at each RSTn; the scans of an
 // image run in stream order, each refining the coefficients of the ones before.
 hipError_t launch_jpeg_prog(const JpegScanArgs& a, hipStream_t s);
-// Baseline scans WITHOUT restart markers (ik_jpeg.hip k_jpeg_seq_sync / k_jpeg_seq_decode):
-// the unstuffed scan is cut into subsequences of L bits; a lane owns the blocks
-// whose first bit lies in its subsequence.  Sync rounds find each subsequence's
-// first block start (bit, block-in-MCU index j) by decoding on from the previous
-// lane's guess until no guess changes (Huffman codes resynchronise within a few
-// blocks); the decode pass then writes coefficients with block and DC bases
-// from prefix sums of the per-lane block counts and DC-difference sums.
-constexpr int kSeqMaxBPM = 10;
-struct JpegSeqArgs {
-    const uint32_t* words;        // unstuffed scan, big-endian 32-bit words, >= 2 zero words past nbits
-    long long nbits;
-    int nsub, L;                  // subsequences, bits per subsequence
-    int bpm;                      // blocks per MCU (1 for a one-component scan)
-    int comp_of[kSeqMaxBPM], bx_of[kSeqMaxBPM], by_of[kSeqMaxBPM];  // per block of an MCU: scan component, offset
-    int mcux, single, single_bw;
-    int h[4], v[4], bw[4], td[4], ta[4];
-    long long blk0[4];
-    long long total_blocks;
-    const JpegHuffTables* tabs;
-    const unsigned long long* start_bit;  // [nsub] this round's guesses (lane 0: 0)
-    const int* start_j;
-    unsigned long long* next_bit;         // [nsub] next round's (lane t writes t+1)
-    int* next_j;
-    int* nblocks;                         // [nsub]
-    int* dcsum;                           // [nsub][4]
-    int* changed;
-    int* flags;                           // [nsub] lane t+1's guess changed this round (lane 0: 0)
-    const long long* block_base;          // decode pass: [nsub]
-    const int* dc_base;                   // [nsub][4]
-    int16_t* coef;
-    int* err;
-    int lanes;
-};
-hipError_t launch_jpeg_seq_sync(const JpegSeqArgs& a, hipStream_t s);
 int jpeg_lanes_for(long long total_lanes);  // lanes per wave for that many independent decoders
-hipError_t launch_jpeg_seq_decode(const JpegSeqArgs& a, hipStream_t s);
-
-// n scans in one launch (dev_scans: device array of n JpegScanArgs; max_seg = most intervals)
-hipError_t launch_jpeg_huff_batch(const JpegScanArgs* dev_scans, int n, int max_seg, hipStream_t s);
 
 // Baseline Huffman coding of k_jpeg_coeffs' output on the GPU (ik_jpeg_enc.hip),
 // the same bytes as ik_codec.cpp's host coder.  Per image: entropy-coded segment

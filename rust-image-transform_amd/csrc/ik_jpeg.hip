@@ -564,133 +564,11 @@ __device__ int decode_sym(GpuBits& br, const JpegHuffTables& T, int t) {
 
 }  // namespace
 
-// the whole interval `seg` of scan `a` (tables already in LDS).  lb: the lane's
-// 64-coefficient block buffer in LDS (zeroed).  A block's coefficients go there as
-// they are decoded and the whole block (zeros included) to memory in eight 16-byte
-// stores, issued right after the next block's ring top-up -- so the top-up's wait
-// for its loads does not also wait for the stores (before: one 2-byte store per
-// coefficient, all of them ahead of the top-up's loads in the memory counter).
-typedef __attribute__((address_space(3))) int16_t lds_i16;
-typedef __attribute__((address_space(1))) int16_t glb_i16;
-__device__ void huff_interval(const JpegScanArgs& a, const JpegHuffTables& T, const uint8_t* s_zz, uint32_t* ring,
-                              int seg, lds_i16* lb) {
-    typedef int16_t s8 __attribute__((ext_vector_type(8)));
-    typedef __attribute__((address_space(3))) s8 lds_s8;
-    typedef __attribute__((address_space(1))) s8 glb_s8;
-    glb_i16* pend = nullptr;  // the block in lb not yet written to memory
-    auto flush = [&]() {
-        if (!pend) return;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            reinterpret_cast<glb_s8*>(pend)[q] = reinterpret_cast<const lds_s8*>(lb)[q];
-            reinterpret_cast<lds_s8*>(lb)[q] = s8{0, 0, 0, 0, 0, 0, 0, 0};
-        }
-        pend = nullptr;
-    };
-    GpuBits br;
-    br.g = (const __attribute__((address_space(1))) uint32_t*)a.data;
-    br.ring = ring;
-    br.pos = a.seg[seg];
-    br.fetched = br.pos & ~3u;
-    br.size = (uint32_t)a.size;
-    br.acc = 0;
-    br.n = 0;
-    br.marker = false;
-    int pred[4] = {0, 0, 0, 0};
-    const long long m0 = (long long)seg * a.restart;
-    const int nm = (int)min((long long)a.restart, a.total_mcu - m0);
-    // MCU position, advanced incrementally (no 64-bit divisions per block)
-    const int row_len = a.single ? a.single_bw : a.mcux;
-    int mx = (int)(m0 % row_len), my = (int)(m0 / row_len);
-    for (int i = 0; i < nm; ++i) {
-        for (int ci = 0; ci < a.ns; ++ci) {
-            const int nby = a.single ? 1 : a.v[ci], nbx = a.single ? 1 : a.h[ci];
-            for (int by = 0; by < nby; ++by)
-                for (int bx = 0; bx < nbx; ++bx) {
-                    const long long bi = a.single ? a.blk0[ci] + (long long)my * a.bw[ci] + mx
-                                                  : a.blk0[ci] + (long long)(my * a.v[ci] + by) * a.bw[ci] + mx * a.h[ci] + bx;
-                    glb_i16* const gblk = (glb_i16*)(a.coef + bi * 64);
-                    br.top_up();
-                    flush();
-                    lds_i16* const blk = lb;
-                    pend = gblk;
-                    const int t = decode_sym(br, T, a.td[ci]);
-                    if (t < 0 || t > 11) { atomicOr(a.err, 1); return; }
-                    pred[ci] += t ? extend_dev(br.get(t), t) : 0;
-                    blk[0] = (int16_t)pred[ci];
-                    for (int k = 1; k < 64;) {
-                        const int fa = T.fast_ac[a.ta[ci]][br.peek(9)];
-                        if (fa) {  // short code + magnitude in one lookup
-                            k += (fa >> 4) & 15;
-                            br.skip(fa & 15);
-                            if (k > 63) { atomicOr(a.err, 4); return; }
-                            blk[s_zz[k]] = (int16_t)(fa >> 8);
-                            ++k;
-                            continue;
-                        }
-                        const int rs = decode_sym(br, T, 4 + a.ta[ci]);
-                        if (rs < 0) { atomicOr(a.err, 2); return; }
-                        const int r = rs >> 4, sz = rs & 15;
-                        if (!sz) {
-                            if (r != 15) break;  // EOB
-                            k += 16;
-                            continue;
-                        }
-                        k += r;
-                        if (k > 63) { atomicOr(a.err, 4); return; }
-                        blk[s_zz[k]] = (int16_t)extend_dev(br.get(sz), sz);
-                        ++k;
-                    }
-                }
-        }
-        if (++mx == row_len) { mx = 0; ++my; }
-    }
-    flush();
-}
-
 __device__ __forceinline__ void load_tables(const JpegHuffTables* g, JpegHuffTables& T, uint8_t* s_zz) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(g);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&T);
     for (int i = threadIdx.x; i < (int)(sizeof(JpegHuffTables) / 4); i += kHuffThreads) dst[i] = src[i];
     if (threadIdx.x < 64) s_zz[threadIdx.x] = kZz[threadIdx.x];
-}
-
-__global__ __launch_bounds__(kHuffThreads) void k_jpeg_huff(JpegScanArgs a) {
-    __shared__ JpegHuffTables T;
-    __shared__ uint8_t s_zz[64];
-    __shared__ uint32_t s_ring[kHuffThreads][kRingDw + 1];  // +1: lanes' rings start in different banks
-    __shared__ __attribute__((aligned(16))) int16_t s_blk[kHuffThreads * 64];
-    for (int i = threadIdx.x; i < kHuffThreads * 16; i += kHuffThreads)
-        reinterpret_cast<uint4*>(s_blk)[i] = make_uint4(0, 0, 0, 0);
-    load_tables(a.tabs, T, s_zz);
-    __syncthreads();
-    const int seg = blockIdx.x * a.lanes + threadIdx.x;
-    if ((int)threadIdx.x < a.lanes && seg < a.n_seg)
-        huff_interval(a, T, s_zz, s_ring[threadIdx.x], seg, (lds_i16*)(s_blk + threadIdx.x * 64));
-}
-
-// a batch of scans: grid.y = scan, each with its own tables; `lanes` intervals per workgroup
-// The rings are dynamic LDS, one per decoding lane (`lanes` x (kRingDw + 1) dwords):
-// sized for all 64 threads they cost 16.6 KB per workgroup, which with 16 lanes
-// held a CU to four workgroups.
-__global__ __launch_bounds__(kHuffThreads) void k_jpeg_huff_batch(const JpegScanArgs* __restrict__ scans, int lanes) {
-    __shared__ JpegHuffTables T;
-    __shared__ uint8_t s_zz[64];
-    extern __shared__ uint32_t s_rings[];  // +1 dword per ring: lanes' rings start in different banks
-    // the scan's arguments in LDS: huff_interval indexes their per-component arrays,
-    // which in a register copy became private memory (224 bytes of scratch per lane)
-    __shared__ JpegScanArgs a;
-    if ((int)blockIdx.x * lanes >= scans[blockIdx.y].n_seg) return;  // whole workgroup past this scan's intervals
-    if (threadIdx.x == 0) a = scans[blockIdx.y];
-    __syncthreads();
-    // then a 128-byte block buffer per lane (zeroed), 16-byte aligned
-    int16_t* const s_blk = reinterpret_cast<int16_t*>(s_rings + ((lanes * (kRingDw + 1) + 3) & ~3));
-    for (int i = threadIdx.x; i < lanes * 16; i += kHuffThreads) reinterpret_cast<uint4*>(s_blk)[i] = make_uint4(0, 0, 0, 0);
-    load_tables(a.tabs, T, s_zz);
-    __syncthreads();
-    const int seg = blockIdx.x * lanes + threadIdx.x;
-    if ((int)threadIdx.x < lanes && seg < a.n_seg)
-        huff_interval(a, T, s_zz, s_rings + threadIdx.x * (kRingDw + 1), seg, (lds_i16*)(s_blk + threadIdx.x * 64));
 }
 
 // ---- progressive scans with restart intervals ----------------------------------
@@ -806,168 +684,6 @@ __global__ __launch_bounds__(kHuffThreads) void k_jpeg_prog(JpegScanArgs a) {
     if ((int)threadIdx.x < a.lanes && seg < a.n_seg) prog_interval(a, T, s_zz, s_rings + threadIdx.x * (kRingDw + 1), seg);
 }
 
-// ---- baseline scans without restart markers: self-synchronising decoding ------
-namespace {
-
-// MSB-first reader over the unstuffed scan (no markers, no stuffing), keeping
-// two words in registers: a load only when the position crosses a word
-struct SeqBits {
-    const uint32_t* w;
-    unsigned long long pos;
-    unsigned long long buf;  // words [idx, idx+1]
-    long long idx;
-    __device__ uint32_t peek32() {
-        const long long i = (long long)(pos >> 5);
-        if (i != idx) {
-            const uint32_t hi = (i == idx + 1) ? (uint32_t)buf : w[i];
-            buf = ((unsigned long long)hi << 32) | w[i + 1];
-            idx = i;
-        }
-        return (uint32_t)((buf << (pos & 31)) >> 32);
-    }
-};
-
-__device__ __forceinline__ int seq_sym(SeqBits& br, const JpegHuffTables& T, int t) {
-    const uint32_t win = br.peek32();
-    const int lv = T.look[t][win >> 23];
-    if (lv >> 8) {
-        br.pos += lv >> 8;
-        return lv & 0xff;
-    }
-    const int code = (int)(win >> 16);
-    int len = 10;
-#pragma unroll
-    for (int l = 10; l <= 16; ++l) len += code >= T.lj[t][l];
-    if (len > 16) return -1;
-    br.pos += len;
-    const int c = code >> (16 - len);
-    return T.vals[t][T.valptr[t][len] + c - T.mincode[t][len]];
-}
-
-__device__ __forceinline__ int seq_get(SeqBits& br, int n) {
-    if (!n) return 0;
-    const uint32_t v = br.peek32() >> (32 - n);
-    br.pos += n;
-    return (int)v;
-}
-
-// one block: DC difference into *dcdiff, AC levels into blk (natural order) when
-// blk != null; false on a bad code
-__device__ bool seq_block(SeqBits& br, const JpegHuffTables& T, const uint8_t* zz, int td, int ta, int* dcdiff,
-                          int16_t* blk) {
-    const int t = seq_sym(br, T, td);
-    if (t < 0 || t > 11) return false;
-    *dcdiff = t ? extend_dev(seq_get(br, t), t) : 0;
-    for (int k = 1; k < 64;) {
-        const int fa = T.fast_ac[ta][br.peek32() >> 23];
-        if (fa) {  // short code + magnitude in one lookup
-            k += (fa >> 4) & 15;
-            br.pos += fa & 15;
-            if (k > 63) return false;
-            if (blk) blk[zz[k]] = (int16_t)(fa >> 8);
-            ++k;
-            continue;
-        }
-        const int rs = seq_sym(br, T, 4 + ta);
-        if (rs < 0) return false;
-        const int r = rs >> 4, sz = rs & 15;
-        if (!sz) {
-            if (r != 15) break;
-            k += 16;
-            continue;
-        }
-        k += r;
-        if (k > 63) return false;
-        const int val = extend_dev(seq_get(br, sz), sz);
-        if (blk) blk[zz[k]] = (int16_t)val;
-        ++k;
-    }
-    return true;
-}
-
-}  // namespace
-
-// one sync round: lane t decodes from its guessed first block start to the
-// first block start at or past its subsequence end, which becomes lane t+1's guess
-__global__ __launch_bounds__(kHuffThreads) void k_jpeg_seq_sync(JpegSeqArgs a) {
-    __shared__ JpegHuffTables T;
-    __shared__ uint8_t s_zz[64];
-    load_tables(a.tabs, T, s_zz);
-    __syncthreads();
-    const int t = blockIdx.x * a.lanes + threadIdx.x;
-    if ((int)threadIdx.x >= a.lanes || t >= a.nsub) return;
-    SeqBits br{a.words, a.start_bit[t], 0, -2};
-    int j = a.start_j[t];
-    const unsigned long long end = (unsigned long long)(t + 1) * (unsigned long long)a.L;
-    int n = 0, dc[4] = {0, 0, 0, 0};
-    bool ok = true;
-    while (br.pos < end && br.pos < (unsigned long long)a.nbits) {
-        const int c = a.comp_of[j];
-        int diff;
-        if (!seq_block(br, T, s_zz, a.td[c], a.ta[c], &diff, nullptr)) { ok = false; break; }
-        dc[c] += diff;
-        ++n;
-        j = j + 1 == a.bpm ? 0 : j + 1;
-        if (n > (1 << 24)) { ok = false; break; }  // runaway guard
-    }
-    a.nblocks[t] = n;
-    for (int c = 0; c < 4; ++c) a.dcsum[t * 4 + c] = dc[c];
-    if (t + 1 < a.nsub) {
-        const unsigned long long nb = ok ? br.pos : ~0ull;  // a bad code: this guess is wrong, keep iterating
-        const int ch = nb != a.start_bit[t + 1] || (ok ? j : 0) != a.start_j[t + 1];
-        a.flags[t + 1] = ch;
-        if (ch) atomicAdd(a.changed, 1);
-        a.next_bit[t + 1] = nb;
-        a.next_j[t + 1] = ok ? j : 0;
-    }
-    // the last lane runs into the scan's padding bits past the final block: what
-    // it decodes (or fails on) there is cut off by the host at the known block count
-}
-
-// the decode pass: converged starts, block and DC bases from prefix sums
-__global__ __launch_bounds__(kHuffThreads) void k_jpeg_seq_decode(JpegSeqArgs a) {
-    __shared__ JpegHuffTables T;
-    __shared__ uint8_t s_zz[64];
-    load_tables(a.tabs, T, s_zz);
-    __syncthreads();
-    const int t = blockIdx.x * a.lanes + threadIdx.x;
-    if ((int)threadIdx.x >= a.lanes || t >= a.nsub) return;
-    SeqBits br{a.words, a.start_bit[t], 0, -2};
-    const unsigned long long end = (unsigned long long)(t + 1) * (unsigned long long)a.L;
-    long long b = a.block_base[t];
-    int pred[4];
-    for (int c = 0; c < 4; ++c) pred[c] = a.dc_base[t * 4 + c];
-    const int nb = a.nblocks[t];
-    long long mcu = b / a.bpm;
-    int j = (int)(b - mcu * a.bpm);
-    int mx = (int)(mcu % a.mcux), my = (int)(mcu / a.mcux);
-    for (int i = 0; i < nb && br.pos < end; ++i, ++b) {
-        const int c = a.comp_of[j];
-        long long bi;
-        if (a.single) bi = a.blk0[c] + (b / a.single_bw) * a.bw[c] + (b % a.single_bw);
-        else bi = a.blk0[c] + (long long)(my * a.v[c] + a.by_of[j]) * a.bw[c] + mx * a.h[c] + a.bx_of[j];
-        int16_t* blk = a.coef + bi * 64;
-        int diff;
-        if (!seq_block(br, T, s_zz, a.td[c], a.ta[c], &diff, blk)) { atomicOr(a.err, 1); return; }
-        pred[c] += diff;
-        blk[0] = (int16_t)pred[c];
-        if (++j == a.bpm) {
-            j = 0;
-            if (++mx == a.mcux) { mx = 0; ++my; }
-        }
-    }
-}
-
-hipError_t launch_jpeg_seq_sync(const JpegSeqArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_jpeg_seq_sync, dim3((a.nsub + a.lanes - 1) / a.lanes), dim3(kHuffThreads), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_jpeg_seq_decode(const JpegSeqArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_jpeg_seq_decode, dim3((a.nsub + a.lanes - 1) / a.lanes), dim3(kHuffThreads), 0, s, a);
-    return hipGetLastError();
-}
-
 namespace {
 int huff_lanes(int v) { return v < 1 ? 1 : (v > kHuffThreads ? kHuffThreads : v); }
 }  // namespace
@@ -978,18 +694,6 @@ int jpeg_lanes_for(long long total) {
     return huff_lanes(want);
 }
 
-hipError_t launch_jpeg_huff(const JpegScanArgs& a, hipStream_t s) {
-    if (a.n_seg <= 0 || a.restart <= 0 || a.ns < 1 || a.ns > 4) return hipErrorInvalidValue;
-    // Lanes of a wave decode different intervals and diverge on every symbol, so a
-    // lone image runs one interval per wave (its waves spread over the CUs);
-    // IK_HUFF_LANES overrides (dev)
-    JpegScanArgs b = a;
-    const int lanes = huff_lanes(1);
-    b.lanes = lanes;
-    hipLaunchKernelGGL(k_jpeg_huff, dim3((a.n_seg + lanes - 1) / lanes), dim3(kHuffThreads), 0, s, b);
-    return hipGetLastError();
-}
-
 hipError_t launch_jpeg_prog(const JpegScanArgs& a, hipStream_t s) {
     if (a.n_seg <= 0 || a.restart <= 0 || a.ns < 1 || a.ns > 4 || a.kind < 1 || a.kind > 4 || a.Ss < 0 || a.Se > 63 ||
         a.Al > 13)
@@ -998,22 +702,6 @@ hipError_t launch_jpeg_prog(const JpegScanArgs& a, hipStream_t s) {
     b.lanes = jpeg_lanes_for(a.n_seg);
     hipLaunchKernelGGL(k_jpeg_prog, dim3((a.n_seg + b.lanes - 1) / b.lanes), dim3(kHuffThreads),
                        sizeof(uint32_t) * (kRingDw + 1) * b.lanes, s, b);
-    return hipGetLastError();
-}
-
-hipError_t launch_jpeg_huff_batch(const JpegScanArgs* dev_scans, int n, int max_seg, hipStream_t s) {
-    if (n <= 0 || max_seg <= 0 || n > 65535) return hipErrorInvalidValue;
-    // many intervals: pack total/1024 per wave (about a thousand waves in flight;
-    // measured on 32 x 256 intervals: 1 -> 97 ms, 2 -> 72, 4 -> 59, 8 -> 51 ms; with
-    // the rings sized per lane, configs[2]'s 256 x 256 intervals: 16 -> 162, 32 ->
-    // 148, 64 -> 148 ms per step, profiles/r03x_jpeg_lanes.txt)
-    const long long total = (long long)n * max_seg;
-    int want = 1;
-    while (want < 32 && (long long)want * 2 * 1024 <= total) want *= 2;
-    const int lanes = huff_lanes(want);
-    const size_t ring_bytes = sizeof(uint32_t) * (((size_t)lanes * (kRingDw + 1) + 3) & ~size_t(3));
-    hipLaunchKernelGGL(k_jpeg_huff_batch, dim3((max_seg + lanes - 1) / lanes, n), dim3(kHuffThreads),
-                       ring_bytes + 128 * (size_t)lanes, s, dev_scans, lanes);
     return hipGetLastError();
 }
 

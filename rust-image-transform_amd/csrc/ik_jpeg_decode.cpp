@@ -129,16 +129,9 @@ struct Component {
 
 const char* const kFmtErr = "Format error decoding Jpeg";
 
-// Restart-free baseline scans on the GPU (self-synchronising decoding, run_seq);
-// IK_JPEG_SEQ=0 keeps them on the host entropy decoder.
-bool seq_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("IK_JPEG_SEQ");
-        return !(e && !strcmp(e, "0"));
-    }();
-    return on;
-}
-constexpr size_t kSeqMinBytes = 32 << 10;  // smaller scans: the host decoder is faster
+// Baseline scans go to the self-synchronising GPU decoder (ik_jsync.hip) from this
+// size up; smaller ones are faster on the host entropy decoder.
+constexpr size_t kJsyncMinBytes = 4 << 10;
 
 // Progressive scans with restart intervals on the GPU (k_jpeg_prog);
 // IK_JPEG_PROG=0 keeps them on the host entropy decoder.
@@ -178,10 +171,13 @@ struct Decoder {
     };
     std::vector<ProgScan> prog;
     bool prog_host = false;
-    // baseline scan without restart markers (self-synchronising GPU decoding)
-    bool seq = false;
-    std::vector<uint32_t> seq_words;  // unstuffed scan, big-endian words
-    JpegSeqArgs seq_args{};
+    // a baseline scan for the self-synchronising GPU decoder (ik_jsync.hip): its
+    // entropy-coded bytes (stuffed, with any RSTn markers) and geometry
+    bool js = false;
+    const uint8_t* js_data = nullptr;
+    size_t js_len = 0;
+    long long js_nivl = 0;  // restart intervals the frame must have
+    jsync::Scan js_scan{};  // geometry (device pointers filled at launch)
 
     void ensure_coef() {
         if (coef.empty()) coef.assign(nblocks * 64, 0);
@@ -402,17 +398,20 @@ struct Decoder {
         return true;
     }
 
-    // Record a baseline scan without restart markers for k_jpeg_seq_*: unstuff it
-    // (0xFF 0x00 -> 0xFF) up to the first marker into big-endian words.
-    bool defer_seq(const std::vector<int>& order, const uint8_t* data, const uint8_t*& next) {
+    // Record a baseline scan for the self-synchronising GPU decoder: its bytes run
+    // to the file's final EOI marker (the GPU's unstuffing flags any other marker
+    // inside them, and counts the restart markers against the frame's intervals;
+    // either mismatch sends the image to the host decoder, which reports png's --
+    // zune-jpeg's -- error).
+    bool defer_jsync(const std::vector<int>& order, const uint8_t* data, const uint8_t*& next) {
         const bool single = order.size() == 1;
+        jsync::Scan a{};
         int bpm = 0;
-        JpegSeqArgs a{};
         for (size_t i = 0; i < order.size(); ++i) {
             const Component& c = comps[order[i]];
             const int nb = single ? 1 : c.h * c.v;
             for (int k = 0; k < nb; ++k) {
-                if (bpm >= kSeqMaxBPM) return false;
+                if (bpm >= jsync::kMaxBPM) return false;
                 a.comp_of[bpm] = (int)i;
                 a.bx_of[bpm] = single ? 0 : k % c.h;
                 a.by_of[bpm] = single ? 0 : k / c.h;
@@ -424,56 +423,27 @@ struct Decoder {
         const Component& c0 = comps[order[0]];
         const int single_bw = (c0.dw + 7) / 8, single_bh = (c0.dh + 7) / 8;
         const long long total_mcu = single ? (long long)single_bw * single_bh : (long long)mcux * mcuy;
-        std::vector<uint8_t> clean;
-        clean.reserve((size_t)(end - data));
-        const uint8_t* q = data;
-        while (q < end) {
-            if (q[0] != 0xFF) {  // the run up to the next 0xFF in one copy
-                const void* f = std::memchr(q, 0xFF, (size_t)(end - q));
-                const uint8_t* r = f ? static_cast<const uint8_t*>(f) : end;
-                clean.insert(clean.end(), q, r);
-                q = r;
-                continue;
-            }
-            if (q + 1 < end && q[1] == 0x00) { clean.push_back(0xFF); q += 2; continue; }
-            if (q + 1 >= end) { clean.push_back(0xFF); ++q; continue; }  // a lone 0xFF at the end: stuffed, as on the host
-            break;  // a marker: the scan ends (the host feeds zeros from here)
-        }
-        if (clean.size() < kSeqMinBytes) return false;
-        // zero words past the end: a decoder (the GPU lanes, the host frontier walk)
-        // may start a block just before nbits and read one whole block of zero bits
-        // from there, at most 16 + 11 + 63 (16 + 10) bits, plus peek32's next word
-        constexpr size_t kSeqPadWords = (16 + 11 + 63 * (16 + 10) + 31) / 32 + 2;
-        const size_t nw = (clean.size() + 3) / 4 + kSeqPadWords;
-        seq_words.assign(nw, 0u);
-        const size_t nfull = clean.size() / 4;
-        for (size_t i = 0; i < nfull; ++i) {  // big-endian words, four bytes at a time
-            uint32_t v;
-            std::memcpy(&v, clean.data() + 4 * i, 4);
-            seq_words[i] = __builtin_bswap32(v);
-        }
-        for (size_t i = 4 * nfull; i < clean.size(); ++i) seq_words[i >> 2] |= (uint32_t)clean[i] << (24 - 8 * (i & 3));
-        a.nbits = (long long)clean.size() * 8;
-        // bits per lane (IK_JPEG_SEQ_L, a multiple of 32): 2048, not 8192 -- four times
-        // the lanes, each round a quarter as long; the host walk stays small
-        // (loadtest restart-free 645 -> 1,061 requests/s, configs[2] restart-free
-        // 7,757 -> 14,901 MPix/s, profiles/r03am_jpeg_seq_lane_bits.txt)
-        static const int kL = [] {
-            const char* e = getenv("IK_JPEG_SEQ_L");
-            const int v = e ? atoi(e) : 2048;
-            return v < 1024 ? 1024 : (v > 65536 ? 65536 : v & ~31);
-        }();
-        a.L = kL;
-        a.nsub = (int)std::max<long long>(1, (a.nbits + a.L - 1) / a.L);
+        // the scan's end: the last FF D9 of the file (trailing bytes after EOI are
+        // ignored, as the parser ignores them), else the file's end
+        const uint8_t* e = end;
+        for (const uint8_t* q = end - 2; q >= data && q >= end - 4096; --q)
+            if (q[0] == 0xFF && q[1] == 0xD9) { e = q; break; }
+        if ((size_t)(e - data) < kJsyncMinBytes) return false;
         a.bpm = bpm;
         a.mcux = mcux;
         a.single = single ? 1 : 0;
         a.single_bw = single_bw;
         a.total_blocks = total_mcu * bpm;
-        seq_args = a;
-        seq = true;
+        a.ivl_blocks = restart ? (long long)restart * bpm : a.total_blocks;
+        a.L = jsync::kLaneBits;
+        a.W = jsync::kWarmBits;
+        js_scan = a;
+        js_nivl = restart ? (total_mcu + restart - 1) / restart : 1;
+        js_data = data;
+        js_len = (size_t)(e - data);
+        js = true;
         deferred = true;
-        next = q;
+        next = e;
         return true;
     }
 
@@ -553,10 +523,7 @@ struct Decoder {
         }
         const bool first_scan = !scanned;
         scanned = true;
-        if (try_gpu && first_scan && kind == 0 && restart > 0 && ns == (int)comps.size() && defer_scan(order, se, next))
-            return IK_OK;
-        if (try_gpu && first_scan && kind == 0 && restart == 0 && ns == (int)comps.size() && seq_enabled() &&
-            defer_seq(order, se, next))
+        if (try_gpu && first_scan && kind == 0 && ns == (int)comps.size() && defer_jsync(order, se, next))
             return IK_OK;
         ensure_coef();
         for (auto& c : comps) c.pred = 0;
@@ -720,244 +687,284 @@ void qtables(const Decoder& d, uint16_t q[256]) {
 
 inline size_t up256(size_t x) { return (x + 255) / 256 * 256; }
 
-// Host decoder over the unstuffed words from an arbitrary (bit, MCU phase) state:
-// the frontier walk below uses it on the few lanes the GPU rounds leave unsynced.
-struct HostSeq {
-    const Decoder& d;
-    const JpegSeqArgs& a;
-    const uint32_t* w;
-    uint32_t peek32(unsigned long long pos) const {
-        const size_t i = (size_t)(pos >> 5);
-        const uint64_t buf = ((uint64_t)w[i] << 32) | w[i + 1];
-        return (uint32_t)((buf << (pos & 31)) >> 32);
-    }
-    int sym(unsigned long long& pos, const HuffTable& t) const {
-        const uint32_t win = peek32(pos);
-        const int look = (int)(win >> 23);
-        if (t.look_len[look]) { pos += t.look_len[look]; return t.look_val[look]; }
-        const int code = (int)(win >> 16);
-        for (int len = 10; len <= 16; ++len) {
-            const int c = code >> (16 - len);
-            if (t.maxcode[len] >= 0 && c <= t.maxcode[len] && c >= t.mincode[len]) {
-                pos += len;
-                return t.vals[t.valptr[len] + c - t.mincode[len]];
-            }
-        }
-        return -1;
-    }
-    int get(unsigned long long& pos, int n) const {
-        if (!n) return 0;
-        const int v = (int)(peek32(pos) >> (32 - n));
-        pos += n;
-        return v;
-    }
-    bool block(unsigned long long& pos, int c) const {
-        const int t = sym(pos, d.dc[a.td[c]]);
-        if (t < 0 || t > 11) return false;
-        (void)get(pos, t);
-        for (int k = 1; k < 64;) {
-            const int rs = sym(pos, d.ac[a.ta[c]]);
-            if (rs < 0) return false;
-            const int r = rs >> 4, sz = rs & 15;
-            if (!sz) {
-                if (r != 15) break;
-                k += 16;
-                continue;
-            }
-            k += r;
-            if (k > 63) return false;
-            (void)get(pos, sz);
-            ++k;
-        }
-        return true;
-    }
-    // lane u from (bit, j): the first block start at or past its end; false on a bad code
-    bool lane(int u, unsigned long long& bit, int& j) const {
-        const unsigned long long end = (unsigned long long)(u + 1) * (unsigned long long)a.L;
-        while (bit < end && bit < (unsigned long long)a.nbits) {
-            if (!block(bit, a.comp_of[j])) return false;
-            j = j + 1 == a.bpm ? 0 : j + 1;
-        }
-        return true;
-    }
-};
-
-// Self-synchronising GPU decoding of a scan recorded by defer_seq into the
-// coefficient image dcoef (pre-zeroed).
-//  1. GPU rounds: every lane decodes from its guessed first block start (bit, MCU
-//     phase) to its end; the state there is the next lane's new guess.  Most lanes
-//     synchronise in the first round.
-//  2. Frontier walk on the host: from the first lane whose guess changed (its new
-//     guess is exact), decode lane by lane until the walk meets the GPU's chain
-//     again, then jump to the next changed lane -- only the unsynchronised stretches
-//     are decoded serially.
-//  3. A GPU round on the corrected starts must change nothing; its block counts and
-//     DC sums give the bases (host prefix sums) for the decode pass.
-// IK_OK, or 1: inconsistent (bad data) -> host decoder.
-// device bytes run_seq needs (part of the caller's scratch: no hipMalloc/hipFree,
-// which would synchronise the device under concurrent decodes)
-size_t seq_bytes(const Decoder& d) {
-    const size_t ns = (size_t)d.seq_args.nsub;
-    return up256(d.seq_words.size() * 4) + 2 * up256(8 * ns) + 3 * up256(4 * ns) + up256(16 * ns) + up256(8 * ns) +
-           up256(16 * ns) + up256(4 * ns) + 256;
-}
-
-int run_seq(const Decoder& d, const uint8_t* dtabs, int16_t* dcoef, uint8_t* dev, hipStream_t s) {
-    const JpegSeqArgs& base = d.seq_args;
-    const int ns = base.nsub;
-    const size_t wbytes = d.seq_words.size() * 4;
-    const size_t o_sb = up256(wbytes), o_nbit = o_sb + up256(8ull * ns), o_sj = o_nbit + up256(8ull * ns);
-    const size_t o_nj = o_sj + up256(4ull * ns), o_nb = o_nj + up256(4ull * ns), o_dc = o_nb + up256(4ull * ns);
-    const size_t o_bb = o_dc + up256(16ull * ns), o_db = o_bb + up256(8ull * ns), o_fg = o_db + up256(16ull * ns);
-    const size_t o_fl = o_fg + up256(4ull * ns);
-    static const bool timing = getenv("IK_JPEG_TIMING") != nullptr;
-    const auto t0 = std::chrono::steady_clock::now();
-    std::vector<unsigned long long> S(ns), G(ns);
-    std::vector<int> Sj(ns, 0), Gj(ns, 0), flags(ns, 0);
-    for (int t = 0; t < ns; ++t) S[t] = (unsigned long long)t * base.L;  // guess: a block starts at each cut
-    int rc = copy_h2d_2d(dev, wbytes, reinterpret_cast<const uint8_t*>(d.seq_words.data()), wbytes, wbytes, 1, s);
-    if (rc) return rc;
-    JpegSeqArgs a = base;
-    a.words = reinterpret_cast<const uint32_t*>(dev);
-    a.tabs = reinterpret_cast<const JpegHuffTables*>(dtabs);
-    a.start_bit = reinterpret_cast<const unsigned long long*>(dev + o_sb);
-    a.start_j = reinterpret_cast<const int*>(dev + o_sj);
-    a.next_bit = reinterpret_cast<unsigned long long*>(dev + o_nbit);
-    a.next_j = reinterpret_cast<int*>(dev + o_nj);
-    a.nblocks = reinterpret_cast<int*>(dev + o_nb);
-    a.dcsum = reinterpret_cast<int*>(dev + o_dc);
-    a.flags = reinterpret_cast<int*>(dev + o_fg);
-    a.changed = reinterpret_cast<int*>(dev + o_fl);
-    a.err = reinterpret_cast<int*>(dev + o_fl + 4);
-    a.coef = dcoef;
-    a.lanes = jpeg_lanes_for(ns);
-    // one GPU round on the starts S: new guesses into G, flags; returns the changed count or < 0
-    auto round = [&]() -> int {
-        int changed = 0;
-        int r = copy_h2d_2d(dev + o_sb, 8ull * ns, reinterpret_cast<const uint8_t*>(S.data()), 8ull * ns, 8ull * ns, 1, s);
-        if (!r) r = copy_h2d_2d(dev + o_sj, 4ull * ns, reinterpret_cast<const uint8_t*>(Sj.data()), 4ull * ns, 4ull * ns, 1, s);
-        if (r) return -1;
-        hipError_t e = hipMemsetAsync(a.changed, 0, 4, s);
-        if (e == hipSuccess) e = hipMemsetAsync(a.flags, 0, 4ull * ns, s);
-        if (e == hipSuccess) e = launch_jpeg_seq_sync(a, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(&changed, a.changed, 4, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) { hip_fail(e, "jpeg seq sync"); return -1; }
-        if (changed) {
-            r = copy_d2h_2d(reinterpret_cast<uint8_t*>(G.data()), 8ull * ns, dev + o_nbit, 8ull * ns, 8ull * ns, 1, s);
-            if (!r) r = copy_d2h_2d(reinterpret_cast<uint8_t*>(Gj.data()), 4ull * ns, dev + o_nj, 4ull * ns, 4ull * ns, 1, s);
-            if (!r) r = copy_d2h_2d(reinterpret_cast<uint8_t*>(flags.data()), 4ull * ns, dev + o_fg, 4ull * ns, 4ull * ns, 1, s);
-            if (r) return -1;
-            G[0] = 0;
-            Gj[0] = 0;
-            flags[0] = 0;
-        }
-        return changed;
-    };
-    // round 1 from the naive guesses; round 2 from its results (most already exact),
-    // so that the walk below meets a chain whose starts are mostly right
-    // (IK_JPEG_SEQ_ROUNDS: GPU rounds before the walk, default 2; each round fixes
-    // at least one more lane of every unsynchronised stretch)
-    static const int max_rounds = [] {
-        const char* e = getenv("IK_JPEG_SEQ_ROUNDS");
-        const int v = e ? atoi(e) : 2;
-        return v < 1 ? 1 : (v > 64 ? 64 : v);
-    }();
-    int changed = round();
-    int walked = 0, rounds_run = 1;
-    if (changed < 0) return 1;
-    while (changed > 0 && rounds_run < max_rounds) {
-        S = G;
-        Sj = Gj;
-        changed = round();
-        ++rounds_run;
-        if (changed < 0) return 1;
-    }
-    if (changed > 0) {
-        // lanes before the first changed one are consistent from lane 0, so that
-        // lane's new guess is exact; walk from there
-        const HostSeq hs{d, base, d.seq_words.data()};
-        std::vector<unsigned long long> T = S;
-        std::vector<int> Tj = Sj;
-        int u = 1;
-        while (u < ns && !flags[u]) ++u;
-        while (u < ns) {
-            unsigned long long bit = G[u];
-            int j = Gj[u];
-            T[u] = bit;
-            Tj[u] = j;
-            // walk until the walked state equals the GPU's guess for a lane whose own
-            // guess did not change (from there the GPU chain is consistent)
-            for (;;) {
-                if (!hs.lane(u, bit, j)) return 1;
-                ++walked;
-                ++u;
-                if (u >= ns) break;
-                T[u] = bit;
-                Tj[u] = j;
-                if (!flags[u] && bit == S[u] && j == Sj[u]) break;
-            }
-            while (u < ns && !flags[u]) ++u;  // consistent stretch: keep the GPU's starts
-        }
-        S = T;
-        Sj = Tj;
-        changed = round();  // verification: nothing may change now
-        if (changed != 0) return 1;
-    }
-    if (timing)
-        fprintf(stderr, "[jpeg seq] %d lanes, %d per wave, %d lanes walked on the host, %.2f ms\n", ns, a.lanes, walked,
-                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-    // prefix sums on the host (a few thousand lanes)
-    std::vector<int> nb(ns), dc(4ull * ns);
-    rc = copy_d2h_2d(reinterpret_cast<uint8_t*>(nb.data()), 4ull * ns, dev + o_nb, 4ull * ns, 4ull * ns, 1, s);
-    if (!rc) rc = copy_d2h_2d(reinterpret_cast<uint8_t*>(dc.data()), 16ull * ns, dev + o_dc, 16ull * ns, 16ull * ns, 1, s);
-    if (rc) return rc;
-    long long acc = 0;
-    for (int t = 0; t < ns; ++t) acc += nb[t];
-    if (acc < base.total_blocks) return 1;  // a real block failed to decode: the host decoder decides
-    if (acc > base.total_blocks) {  // blocks decoded from the padding past the final block: drop them
-        long long excess = acc - base.total_blocks;
-        for (int t = ns - 1; t >= 0 && excess > 0; --t) {
-            const long long take = std::min<long long>(nb[t], excess);
-            nb[t] -= (int)take;
-            excess -= take;
-        }
-        rc = copy_h2d_2d(dev + o_nb, 4ull * ns, reinterpret_cast<const uint8_t*>(nb.data()), 4ull * ns, 4ull * ns, 1, s);
-        if (rc) return rc;
-    }
-    std::vector<long long> bb(ns);
-    std::vector<int> db(4ull * ns);
-    acc = 0;
-    int dacc[4] = {0, 0, 0, 0};
-    for (int t = 0; t < ns; ++t) {
-        bb[t] = acc;
-        acc += nb[t];
-        for (int c = 0; c < 4; ++c) { db[4 * t + c] = dacc[c]; dacc[c] += dc[4 * t + c]; }
-    }
-    rc = copy_h2d_2d(dev + o_bb, 8ull * ns, reinterpret_cast<const uint8_t*>(bb.data()), 8ull * ns, 8ull * ns, 1, s);
-    if (!rc) rc = copy_h2d_2d(dev + o_db, 16ull * ns, reinterpret_cast<const uint8_t*>(db.data()), 16ull * ns, 16ull * ns, 1, s);
-    if (rc) return rc;
-    a.block_base = reinterpret_cast<const long long*>(dev + o_bb);
-    a.dc_base = reinterpret_cast<const int*>(dev + o_db);
-    int err = 0;
-    hipError_t e = hipMemsetAsync(a.err, 0, 4, s);
-    if (e == hipSuccess) e = launch_jpeg_seq_decode(a, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(&err, a.err, 4, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return hip_fail(e, "jpeg seq decode");
-    return err ? 1 : IK_OK;
-}
-
-// try_gpu: baseline scans with restart intervals are entropy-decoded on the GPU
-// (k_jpeg_huff), restart-free baseline scans by self-synchronising decoding
-// (k_jpeg_seq_*), progressive scans with restart intervals scan by scan
-// (k_jpeg_prog); anything else, and any stream the GPU finds a bad code in, goes
-// through the host decoder
 // process-wide: JPEG streams whose entropy decoding ran on the GPU / on the host
 std::atomic<unsigned long long> g_jpeg_gpu_streams{0}, g_jpeg_host_streams{0};
 
+// The baseline scans of a batch (ds[idx[k]]->js), all through the self-synchronising
+// GPU decoder at once (ik_jsync.hip; algorithm ik_jpeg_sync.h):
+//   1. upload: every scan's bytes (DMAed in place when page-locked, else staged),
+//      Huffman and quantisation tables, the unstuffing chunk table -- one small copy
+//   2. unstuffing on the GPU, then the interval tables come back (a few KB)
+//   3. lanes: per image, each interval cut into jsync::kLaneBits pieces (host)
+//   4. the sync pass, fix rounds until no lane changes, bases, the decode pass
+//   5. reconstruction of every image (IDCT, upsampling, colour)
+// An image the GPU finds inconsistent (a stray marker, a restart count that does
+// not match the frame, lanes that never synchronise, a bad code) goes to host_idx:
+// the host decoder decides and reports the reference's errors.
+static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::vector<int>& idx, ik_image** outs,
+                        std::vector<int>& st, std::vector<int>& host_idx) {
+    using namespace jsync;
+    const int m = (int)idx.size();
+    if (!m) return;
+    static const bool timing = getenv("IK_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    constexpr int kChunkBytes = 4096;
+    // ---- layout ----
+    struct Lay {
+        size_t scan, out, ivl, qt, tab, coef, pl;
+        long long lanes_max, lane0;
+        int chunk0, nchunks, ivl0;
+        JpegGeom g;
+    };
+    std::vector<Lay> lay(m);
+    size_t o = 0;
+    auto take = [&](size_t bytes) { const size_t r = o; o += up256(bytes); return r; };
+    const size_t o_img = take(sizeof(JsImageDev) * m);
+    int nchunks = 0, nivl_total = 0;
+    long long lanes_max = 0;
+    for (int k = 0; k < m; ++k) {
+        const Decoder& d = *ds[idx[k]];
+        Lay& L = lay[k];
+        L.chunk0 = nchunks;
+        L.nchunks = (int)((d.js_len + kChunkBytes - 1) / kChunkBytes);
+        nchunks += L.nchunks;
+        L.ivl0 = nivl_total;
+        nivl_total += (int)d.js_nivl + 1;
+        L.lane0 = lanes_max;
+        L.lanes_max = ((long long)(8 * d.js_len) / kLaneBits + d.js_nivl + 1 + 255) & ~255ll;
+        lanes_max += L.lanes_max;
+    }
+    const size_t o_chunks = take(sizeof(int2) * nchunks);
+    for (int k = 0; k < m; ++k) lay[k].tab = take(sizeof(JpegHuffTables));
+    for (int k = 0; k < m; ++k) lay[k].qt = take(512);
+    const size_t small_end = o;  // [images | chunks | tables | qt]: one upload
+    const size_t o_status = take(sizeof(int) * m), o_totals = take(sizeof(uint32_t) * 2 * m);
+    const size_t o_ivl = take(sizeof(long long) * nivl_total);  // contiguous: one read-back
+    const size_t small2_end = o;  // [status | totals | ivl]: one read-back
+    const size_t o_counts = take(sizeof(uint2) * nchunks);
+    const size_t o_scans = take(sizeof(Scan) * m);
+    const size_t o_ivlane = take(sizeof(int) * nivl_total);
+    const size_t o_wgs = take(sizeof(int2) * (size_t)(lanes_max / 256));
+    const size_t tab2_bytes = o - o_scans;  // [scans | ivl_lane | wgs]: the second upload
+    const size_t o_changed = take(256);
+    const size_t o_recs = take(sizeof(LaneRec) * (size_t)lanes_max);
+    const size_t o_bases = take(sizeof(LaneBase) * (size_t)lanes_max);
+    const size_t o_cs = take(jsync_chunk_scratch_bytes(lanes_max));
+    for (int k = 0; k < m; ++k) {
+        const Decoder& d = *ds[idx[k]];
+        Lay& L = lay[k];
+        L.scan = take(d.js_len + 64);
+        L.out = take(d.js_len + 4 * kPadWords + 8);
+        const size_t pb = make_geom(d, L.g);
+        L.coef = take(d.nblocks * 64 * sizeof(int16_t));
+        L.pl = take(pb);
+    }
+    hipStream_t s = thread_stream();
+    uint8_t* dev = scratch_slot(1, o);
+    const size_t pin_bytes = std::max(small_end, std::max(small2_end - o_status, tab2_bytes)) + 256;
+    uint8_t* hp = dev ? pinned_slot(1, pin_bytes) : nullptr;
+    auto fail_all = [&](const char* why) {
+        (void)why;
+        for (int k = 0; k < m; ++k) host_idx.push_back(idx[k]);
+    };
+    if (!dev || !hp) { fail_all("memory"); return; }
+    (void)hipStreamSynchronize(s);  // the pinned block is free
+    // ---- 1. upload ----
+    {
+        JsImageDev* I = reinterpret_cast<JsImageDev*>(hp + o_img);
+        int2* ch = reinterpret_cast<int2*>(hp + o_chunks);
+        for (int k = 0; k < m; ++k) {
+            const Decoder& d = *ds[idx[k]];
+            const Lay& L = lay[k];
+            JsImageDev& J = I[k];
+            J = JsImageDev{};
+            J.scan = dev + L.scan;
+            J.scan_len = (long long)d.js_len;
+            J.out = dev + L.out;
+            J.ivl = reinterpret_cast<long long*>(dev + o_ivl) + L.ivl0;
+            J.ivl_cap = (int)d.js_nivl + 1;
+            J.chunk0 = L.chunk0;
+            J.nchunks = L.nchunks;
+            J.totals = reinterpret_cast<uint32_t*>(dev + o_totals) + 2 * k;
+            J.status = reinterpret_cast<int*>(dev + o_status) + k;
+            for (int c = 0; c < L.nchunks; ++c) ch[L.chunk0 + c] = make_int2(k, c);
+        }
+        parallel_for(m, 0, [&](int k) {
+            const Decoder& d = *ds[idx[k]];
+            d.tables(*reinterpret_cast<JpegHuffTables*>(hp + lay[k].tab));
+            qtables(d, reinterpret_cast<uint16_t*>(hp + lay[k].qt));
+        });
+    }
+    // the scan bytes: in place from page-locked memory, else through pinned staging
+    std::vector<char> in_place(m, 0);
+    std::vector<size_t> st_off(m, 0);
+    size_t st_total = 0;
+    for (int k = 0; k < m; ++k) {
+        const Decoder& d = *ds[idx[k]];
+        in_place[k] = host_pinned(d.js_data, d.js_len) ? 1 : 0;
+        if (!in_place[k]) { st_off[k] = st_total; st_total += up256(d.js_len); }
+    }
+    uint8_t* hdata = st_total ? pinned_slot(2, st_total) : nullptr;
+    if (st_total && !hdata) { fail_all("memory"); return; }
+    if (st_total)
+        parallel_for(m, 0, [&](int k) {
+            if (!in_place[k]) std::memcpy(hdata + st_off[k], ds[idx[k]]->js_data, ds[idx[k]]->js_len);
+        });
+    hipError_t e = hipMemcpyAsync(dev, hp, small_end, hipMemcpyHostToDevice, s);
+    for (int k = 0; k < m && e == hipSuccess; ++k) {
+        const Decoder& d = *ds[idx[k]];
+        e = hipMemcpyAsync(dev + lay[k].scan, in_place[k] ? d.js_data : hdata + st_off[k], d.js_len,
+                           hipMemcpyHostToDevice, s);
+    }
+    if (e == hipSuccess) e = hipMemsetAsync(dev + o_status, 0, small2_end - o_status, s);
+    // ---- 2. unstuffing; the interval tables back ----
+    if (e == hipSuccess)
+        e = launch_jsync_unstuff(reinterpret_cast<JsImageDev*>(dev + o_img), m,
+                                 reinterpret_cast<const int2*>(dev + o_chunks), nchunks,
+                                 reinterpret_cast<uint2*>(dev + o_counts), s);
+    if (e == hipSuccess) e = hipMemcpyAsync(hp, dev + o_status, small2_end - o_status, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) { (void)hip_fail(e, "jpeg unstuff"); fail_all("device"); return; }
+    const double t_unstuff = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    // ---- 3. lanes ----
+    std::vector<int> ok(m, 0), hstatus(m);
+    std::vector<int> ivl_lane((size_t)nivl_total, 0);
+    std::vector<int2> wgs;
+    std::vector<Scan> scans(m);
+    long long lanes_used = 0;
+    {
+        const int* hst = reinterpret_cast<const int*>(hp);
+        const uint32_t* tot = reinterpret_cast<const uint32_t*>(hp + (o_totals - o_status));
+        const long long* hivl = reinterpret_cast<const long long*>(hp + (o_ivl - o_status));
+        for (int k = 0; k < m; ++k) {
+            const Decoder& d = *ds[idx[k]];
+            Lay& L = lay[k];
+            if (hst[k] || (long long)tot[2 * k + 1] + 1 != d.js_nivl) continue;  // stray marker / wrong restart count
+            const long long* iv = hivl + L.ivl0;
+            int* il = ivl_lane.data() + L.ivl0;
+            bool good = true;
+            il[0] = 0;
+            for (long long q = 0; q < d.js_nivl; ++q) {
+                const long long bits = iv[q + 1] - iv[q];
+                if (bits < 0) { good = false; break; }
+                il[q + 1] = il[q] + (int)std::max<long long>(1, (bits + kLaneBits - 1) / kLaneBits);
+            }
+            if (!good || il[d.js_nivl] > L.lanes_max) continue;
+            ok[k] = 1;
+            const int nl = il[d.js_nivl];
+            lanes_used += nl;
+            for (int w = 0; w < nl; w += 256) wgs.push_back(make_int2(k, w));
+            Scan& S = scans[k];
+            S = d.js_scan;
+            S.words = reinterpret_cast<const uint32_t*>(dev + L.out);
+            S.ivl = reinterpret_cast<const long long*>(dev + o_ivl) + L.ivl0;
+            S.nivl = (int)d.js_nivl;
+            S.lane0 = L.lane0;
+            S.ivl_lane = reinterpret_cast<const int*>(dev + o_ivlane) + L.ivl0;
+            S.tabs = reinterpret_cast<const JpegHuffTables*>(dev + L.tab);
+            S.coef = reinterpret_cast<int16_t*>(dev + L.coef);
+        }
+    }
+    for (int k = 0; k < m; ++k)
+        if (!ok[k]) host_idx.push_back(idx[k]);
+    const int nwg = (int)wgs.size();
+    if (!nwg) return;
+    std::memcpy(hp, scans.data(), sizeof(Scan) * m);
+    std::memcpy(hp + (o_ivlane - o_scans), ivl_lane.data(), sizeof(int) * nivl_total);
+    std::memcpy(hp + (o_wgs - o_scans), wgs.data(), sizeof(int2) * nwg);
+    const Scan* d_scans = reinterpret_cast<const Scan*>(dev + o_scans);
+    const int2* d_wgs = reinterpret_cast<const int2*>(dev + o_wgs);
+    LaneRec* d_recs = reinterpret_cast<LaneRec*>(dev + o_recs);
+    int* d_status = reinterpret_cast<int*>(dev + o_status);
+    int* d_changed = reinterpret_cast<int*>(dev + o_changed);
+    // ---- 4. sync, fix rounds, bases, decode ----
+    EvPair& ev = thread_events(2);
+    e = hipMemcpyAsync(dev + o_scans, hp, tab2_bytes, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && ev.a) e = hipEventRecord(ev.a, s);
+    if (e == hipSuccess) e = launch_jsync_sync(d_scans, d_wgs, nwg, d_recs, s);
+    int rounds = 0;
+    int* hchanged = reinterpret_cast<int*>(hp + tab2_bytes);  // (pinned, past what the upload reads)
+    while (e == hipSuccess) {
+        e = hipMemsetAsync(d_changed, 0, sizeof(int), s);
+        if (e == hipSuccess) e = launch_jsync_fix(d_scans, d_wgs, nwg, d_recs, d_changed, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(hchanged, d_changed, sizeof(int), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        ++rounds;
+        if (e != hipSuccess || *hchanged == 0 || rounds > 4096) break;
+    }
+    if (e == hipSuccess)
+        e = launch_jsync_bases_decode(d_scans, m, d_wgs, nwg, d_recs, reinterpret_cast<LaneBase*>(dev + o_bases),
+                                      dev + o_cs, d_status, s);
+    if (e == hipSuccess && ev.b) e = hipEventRecord(ev.b, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(hstatus.data(), d_status, sizeof(int) * m, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess || rounds > 4096) {
+        if (e != hipSuccess) (void)hip_fail(e, "jpeg entropy decode");
+        for (int k = 0; k < m; ++k)
+            if (ok[k]) host_idx.push_back(idx[k]);
+        return;
+    }
+    {  // ik_batch_last_timing: the decoding launches' time and algorithmic bytes
+        double scan = 0, coef = 0;
+        for (int k = 0; k < m; ++k)
+            if (ok[k]) {
+                scan += (double)ds[idx[k]]->js_len;
+                coef += (double)ds[idx[k]]->nblocks * 64 * sizeof(int16_t);
+            }
+        const int d = current_device();
+        batch_timing_add(d, kBtJpegHuffMs, ev_pair_ms(ev));
+        batch_timing_add(d, kBtJpegScanBytes, scan);
+        batch_timing_add(d, kBtJpegCoefBytes, coef);
+        batch_timing_add(d, kBtJpegImages, (double)(lanes_used ? std::count(ok.begin(), ok.end(), 1) : 0));
+        batch_timing_add(d, kBtJpegLanes, (double)lanes_used);
+    }
+    // ---- 5. reconstruction ----
+    for (int k = 0; k < m; ++k) {
+        if (!ok[k]) continue;
+        const int i = idx[k];
+        if (hstatus[k]) { host_idx.push_back(i); continue; }
+        const Decoder& d = *ds[i];
+        JpegGeom g = lay[k].g;
+        g.qt = reinterpret_cast<const uint16_t*>(dev + lay[k].qt);
+        g.coef = reinterpret_cast<const int16_t*>(dev + lay[k].coef);
+        g.planes = dev + lay[k].pl;
+        ik_image* img = nullptr;
+        st[i] = alloc_image((uint32_t)d.width, (uint32_t)d.height, d.comps.size() == 1 ? 1u : 3u, &img);
+        if (st[i]) continue;
+        e = launch_jpeg_reconstruct(g, img->d, img->pitch, s);
+        if (e != hipSuccess) { ik_image_free(img); st[i] = hip_fail(e, "jpeg reconstruct"); continue; }
+        outs[i] = img;
+    }
+    e = hipStreamSynchronize(s);
+    for (int k = 0; k < m; ++k) {
+        const int i = idx[k];
+        if (!ok[k] || hstatus[k] || !outs[i]) continue;
+        if (e != hipSuccess) {  // the device failed: the host decoder takes them
+            ik_image_free(outs[i]);
+            outs[i] = nullptr;
+            st[i] = IK_OK;
+            host_idx.push_back(i);
+            continue;
+        }
+        g_jpeg_gpu_streams += 1;
+    }
+    if (timing)
+        fprintf(stderr, "[jsync] %d images, %lld lanes, %d fix rounds: unstuff %.2f ms, total %.2f ms\n", m, lanes_used,
+                rounds, t_unstuff,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+}
+
+}  // namespace
+int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_image** outs, int* status,
+                      std::string* msgs);
+namespace {
+
+// try_gpu: baseline scans go through the self-synchronising GPU decoder (the batch
+// path with one image), progressive scans with restart intervals scan by scan
+// (k_jpeg_prog); anything else, and any stream the GPU finds inconsistent, goes
+// through the host decoder
 int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gpu) {
-    static const bool timing = getenv("IK_JPEG_TIMING") != nullptr;  // dev: phase times to stderr
+    static const bool timing = getenv("IK_TIMING") != nullptr;  // dev: phase times to stderr
     auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double t0 = timing ? now() : 0;
     Decoder d;
@@ -967,19 +974,20 @@ int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gp
     int st = d.parse();
     if (st) return st;
     if (d.need_host) return decode_jpeg_impl(bytes, n, out, false);  // several scans: all on the host
+    if (d.js) {
+        int status = IK_OK;
+        std::string msg;
+        st = decode_jpeg_batch(&bytes, &n, 1, out, &status, &msg);
+        if (st && !msg.empty()) return fail(st, "%s", msg.c_str());
+        return st;
+    }
     const int nc = (int)d.comps.size();
     JpegGeom g;
     const size_t plane_bytes = make_geom(d, g);
 
-    // device scratch: [qtables 4x64 u16][coefficients][planes][GPU entropy decoding:
-    // tables, error flag, segment starts, scan bytes]
+    // device scratch: [qtables 4x64 u16][coefficients][planes][progressive scans]
     const size_t qbytes = 256 * sizeof(uint16_t);
     const size_t cbytes = d.nblocks * 64 * sizeof(int16_t);
-    const bool gpu = d.deferred;
-    const bool seq = d.seq;
-    const size_t tbytes = gpu ? (sizeof(JpegHuffTables) + 255) / 256 * 256 : 0;
-    const size_t sbytes = gpu && !seq ? (d.gpu_segs.size() * sizeof(unsigned) + 255) / 256 * 256 : 0;
-    const size_t dbytes = gpu && !seq ? (size_t)d.gpu_scan.size : 0;
     std::vector<uint16_t> q(256, 0);
     qtables(d, q.data());
     const double t1 = timing ? now() : 0;
@@ -988,9 +996,7 @@ int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gp
     if (st) return st;
     const double t2 = timing ? now() : 0;
     const size_t pl_off = qbytes + (cbytes + 255) / 256 * 256;
-    const size_t t_off = pl_off + (plane_bytes + 255) / 256 * 256;
-    const size_t e_off = t_off + tbytes, s_off = e_off + 256, d_off = s_off + sbytes;
-    const size_t q_off = up256(d_off + dbytes + 1024);  // the restart bit reader fetches 64-B chunks past the end
+    const size_t q_off = pl_off + (plane_bytes + 255) / 256 * 256;
     // progressive scans on the GPU: [the file (+ reader slack)][error flag][per scan:
     // tables, interval starts], staged in one host buffer and copied at once
     const bool prog = !d.prog.empty();
@@ -1014,50 +1020,11 @@ int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gp
             std::memcpy(pstage.data() + pseg_off[k], d.prog[k].segs.data(), d.prog[k].segs.size() * sizeof(unsigned));
         }
     }
-    uint8_t* dev = scratch(q_off + (gpu && seq ? seq_bytes(d) : 0) + pstage.size());
+    uint8_t* dev = scratch(q_off + pstage.size());
     if (!dev) { ik_image_free(img); return fail(IK_ERR_DEVICE, "cannot allocate device scratch"); }
     hipStream_t s = thread_stream();
     st = copy_h2d_2d(dev, qbytes, reinterpret_cast<const uint8_t*>(q.data()), qbytes, qbytes, 1, s);
-    if (!st && gpu && seq) {
-        JpegHuffTables tabs;
-        d.tables(tabs);
-        st = copy_h2d_2d(dev + t_off, sizeof(tabs), reinterpret_cast<const uint8_t*>(&tabs), sizeof(tabs),
-                         sizeof(tabs), 1, s);
-        if (!st && hipMemsetAsync(dev + qbytes, 0, cbytes, s) != hipSuccess) st = fail(IK_ERR_DEVICE, "memset");
-        if (!st) st = run_seq(d, dev + t_off, reinterpret_cast<int16_t*>(dev + qbytes), dev + q_off, s);
-        if (st == 1) {  // not resolved on the GPU: the host decoder decides
-            ik_image_free(img);
-            return decode_jpeg_impl(bytes, n, out, false);
-        }
-    } else if (!st && gpu) {
-        JpegHuffTables tabs;
-        d.tables(tabs);
-        st = copy_h2d_2d(dev + t_off, sizeof(tabs), reinterpret_cast<const uint8_t*>(&tabs), sizeof(tabs),
-                         sizeof(tabs), 1, s);
-        if (!st)
-            st = copy_h2d_2d(dev + s_off, sbytes, reinterpret_cast<const uint8_t*>(d.gpu_segs.data()),
-                             d.gpu_segs.size() * sizeof(unsigned), d.gpu_segs.size() * sizeof(unsigned), 1, s);
-        if (!st && dbytes) st = copy_h2d_2d(dev + d_off, dbytes, d.gpu_data, dbytes, dbytes, 1, s);
-        if (!st) {
-            hipError_t e = hipMemsetAsync(dev + qbytes, 0, cbytes, s);
-            if (e == hipSuccess) e = hipMemsetAsync(dev + e_off, 0, sizeof(int), s);
-            JpegScanArgs a = d.gpu_scan;
-            a.data = dev + d_off;
-            a.seg = reinterpret_cast<const unsigned*>(dev + s_off);
-            a.tabs = reinterpret_cast<const JpegHuffTables*>(dev + t_off);
-            a.coef = reinterpret_cast<int16_t*>(dev + qbytes);
-            a.err = reinterpret_cast<int*>(dev + e_off);
-            if (e == hipSuccess) e = launch_jpeg_huff(a, s);
-            int err = 0;
-            if (e == hipSuccess) e = hipMemcpyAsync(&err, dev + e_off, sizeof(int), hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
-            if (e != hipSuccess) { ik_image_free(img); return hip_fail(e, "jpeg entropy decode"); }
-            if (err) {  // a bad code somewhere: the host decoder reports it
-                ik_image_free(img);
-                return decode_jpeg_impl(bytes, n, out, false);
-            }
-        }
-    } else if (!st && prog) {
+    if (!st && prog) {
         uint8_t* pb = dev + q_off;
         st = copy_h2d_2d(pb, pstage.size(), pstage.data(), pstage.size(), pstage.size(), 1, s);
         if (!st) {
@@ -1094,8 +1061,8 @@ int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gp
     if (e != hipSuccess) { ik_image_free(img); return hip_fail(e, "jpeg reconstruct"); }
     if (timing)
         fprintf(stderr, "[jpeg] %s: parse %.2f alloc %.2f entropy/upload %.2f reconstruct %.2f ms\n",
-                gpu || prog ? "gpu entropy" : "host entropy", t1 - t0, t2 - t1, t3 - t2, now() - t3);
-    (gpu || prog ? g_jpeg_gpu_streams : g_jpeg_host_streams) += 1;
+                prog ? "gpu entropy" : "host entropy", t1 - t0, t2 - t1, t3 - t2, now() - t3);
+    (prog ? g_jpeg_gpu_streams : g_jpeg_host_streams) += 1;
     *out = img;
     return IK_OK;
 }
@@ -1104,7 +1071,7 @@ int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gp
 
 int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_image** outs, int* status,
                       std::string* msgs) {
-    // 1. parse every stream (host threads); restart-interval baseline scans are deferred
+    // 1. parse every stream (host threads); baseline scans are deferred to the GPU
     std::vector<std::unique_ptr<Decoder>> ds(n);
     std::vector<int> st(n, IK_OK);
     auto note = [&](int i) {
@@ -1122,177 +1089,20 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
         st[i] = ds[i]->parse();
         note(i);
     });
-    std::vector<int> gpu_idx, host_idx, seq_idx;
+    std::vector<int> js_idx, host_idx, prog_idx;
     for (int i = 0; i < n; ++i) {
         outs[i] = nullptr;
         if (st[i]) continue;
-        if (ds[i]->deferred && !ds[i]->need_host && !ds[i]->seq) gpu_idx.push_back(i);
-        else if ((ds[i]->seq || !ds[i]->prog.empty()) && !ds[i]->need_host) seq_idx.push_back(i);  // one by one, GPU
+        if (ds[i]->js && !ds[i]->need_host) js_idx.push_back(i);
+        else if (!ds[i]->prog.empty() && !ds[i]->need_host) prog_idx.push_back(i);  // one by one, GPU
         else host_idx.push_back(i);
     }
-    // 2. the deferred scans: one device allocation, one Huffman launch over all of them.
-    // Layout: [args][error flags][every image's quantisation + Huffman tables and
-    // interval starts][every image's scan bytes][every image's coefficients and
-    // planes].  The tables go up in one copy from a pinned block filled by the pool;
-    // scan bytes already in page-locked memory (ik_host_alloc) are DMAed in place, the
-    // rest through a pinned block the pool fills -- all asynchronous on the stream,
-    // ordered before the launch (before: four synchronous staged copies per image).
-    const int m = (int)gpu_idx.size();
-    if (m) {
-        struct Lay { size_t q, t, sg, dt, coef, pl, end; JpegGeom g; };
-        std::vector<Lay> lay(m);
-        const size_t o_args = 256, o_err = o_args + up256(sizeof(JpegScanArgs) * m);
-        size_t total = o_err + up256(sizeof(int) * m);
-        const size_t o_small = total;
-        for (int k = 0; k < m; ++k) {  // tables and interval starts
-            const Decoder& d = *ds[gpu_idx[k]];
-            Lay& L = lay[k];
-            L.q = total;
-            L.t = L.q + 512;
-            L.sg = L.t + up256(sizeof(JpegHuffTables));
-            total = L.sg + up256(d.gpu_segs.size() * sizeof(unsigned));
-        }
-        const size_t small_bytes = total - o_small;
-        for (int k = 0; k < m; ++k) {  // scan bytes
-            lay[k].dt = total;
-            total += up256((size_t)ds[gpu_idx[k]]->gpu_scan.size + 1024);  // 64-B chunk fetches past the end
-        }
-        for (int k = 0; k < m; ++k) {  // coefficients and planes
-            const Decoder& d = *ds[gpu_idx[k]];
-            Lay& L = lay[k];
-            const size_t pb = make_geom(d, L.g);
-            L.coef = total;
-            L.pl = L.coef + up256(d.nblocks * 64 * sizeof(int16_t));
-            L.end = L.pl + up256(pb);
-            total = L.end;
-        }
-        // the batch's device work area: a grow-only per-thread arena (hipFree would
-        // synchronise the whole device under concurrent batches)
-        hipStream_t s = thread_stream();
-        uint8_t* dev = scratch_slot(1, total);
-        int rc = dev ? IK_OK : fail(IK_ERR_DEVICE, "cannot allocate the JPEG batch work area");
-        uint8_t* hsmall = rc ? nullptr : pinned_slot(1, small_bytes);
-        if (!rc && !hsmall) rc = IK_ERR_NOMEM;
-        std::vector<char> in_place(m, 0);
-        std::vector<size_t> st_off(m, 0);
-        size_t st_total = 0;
-        for (int k = 0; k < m && !rc; ++k) {
-            const Decoder& d = *ds[gpu_idx[k]];
-            in_place[k] = host_pinned(d.gpu_data, (size_t)d.gpu_scan.size) ? 1 : 0;
-            if (!in_place[k]) {
-                st_off[k] = st_total;
-                st_total += up256((size_t)d.gpu_scan.size);
-            }
-        }
-        uint8_t* hdata = !rc && st_total ? pinned_slot(2, st_total) : nullptr;
-        if (!rc && st_total && !hdata) rc = IK_ERR_NOMEM;
-        std::vector<JpegScanArgs> args(m);
-        int max_seg = 0;
-        if (!rc) {
-            parallel_for(m, 0, [&](int k) {
-                const Decoder& d = *ds[gpu_idx[k]];
-                const Lay& L = lay[k];
-                qtables(d, reinterpret_cast<uint16_t*>(hsmall + (L.q - o_small)));
-                d.tables(*reinterpret_cast<JpegHuffTables*>(hsmall + (L.t - o_small)));
-                std::memcpy(hsmall + (L.sg - o_small), d.gpu_segs.data(), d.gpu_segs.size() * sizeof(unsigned));
-                if (!in_place[k]) std::memcpy(hdata + st_off[k], d.gpu_data, (size_t)d.gpu_scan.size);
-            });
-            hipError_t e = hipMemcpyAsync(dev + o_small, hsmall, small_bytes, hipMemcpyHostToDevice, s);
-            for (int k = 0; k < m && e == hipSuccess; ++k) {
-                const Decoder& d = *ds[gpu_idx[k]];
-                const size_t db = (size_t)d.gpu_scan.size;
-                if (db)
-                    e = hipMemcpyAsync(dev + lay[k].dt, in_place[k] ? d.gpu_data : hdata + st_off[k], db,
-                                       hipMemcpyHostToDevice, s);
-            }
-            if (e != hipSuccess) rc = hip_fail(e, "jpeg batch upload");
-        }
-        for (int k = 0; k < m && !rc; ++k) {
-            const Decoder& d = *ds[gpu_idx[k]];
-            const Lay& L = lay[k];
-            JpegScanArgs& a = args[k];
-            a = d.gpu_scan;
-            a.data = dev + L.dt;
-            a.seg = reinterpret_cast<const unsigned*>(dev + L.sg);
-            a.tabs = reinterpret_cast<const JpegHuffTables*>(dev + L.t);
-            a.coef = reinterpret_cast<int16_t*>(dev + L.coef);
-            a.err = reinterpret_cast<int*>(dev + o_err) + k;
-            max_seg = std::max(max_seg, a.n_seg);
-        }
-        const size_t hdr = o_small;
-        std::vector<int> errs(m, 0);
-        if (!rc) {  // (synchronous: also the point where the async uploads above are ordered before the launch)
-            rc = copy_h2d_2d(dev + o_args, sizeof(JpegScanArgs) * m, reinterpret_cast<const uint8_t*>(args.data()),
-                             sizeof(JpegScanArgs) * m, sizeof(JpegScanArgs) * m, 1, s);
-        }
-        if (!rc) {
-            // No zeroing of the coefficient images where the decoder stores every
-            // block whole: an interleaved scan covers every block of its image.  A
-            // one-component scan covers only the blocks of the component's own size;
-            // when its sampling factors pad the component to more (a gray image with
-            // H = V = 2), the padding blocks are zeroed so that no stale scratch
-            // reaches the reconstruction, even where the crop drops it.
-            hipError_t e = hipMemsetAsync(dev + o_err, 0, sizeof(int) * m, s);
-            for (int k = 0; k < m && e == hipSuccess; ++k)
-                if (args[k].single && (size_t)args[k].total_mcu < ds[gpu_idx[k]]->nblocks)
-                    e = hipMemsetAsync(dev + lay[k].coef, 0, ds[gpu_idx[k]]->nblocks * 64 * sizeof(int16_t), s);
-            EvPair& ev = thread_events(2);
-            if (e == hipSuccess && ev.a) e = hipEventRecord(ev.a, s);
-            if (e == hipSuccess)
-                e = launch_jpeg_huff_batch(reinterpret_cast<const JpegScanArgs*>(dev + o_args), m, max_seg, s);
-            if (e == hipSuccess && ev.b) e = hipEventRecord(ev.b, s);
-            if (e == hipSuccess) e = hipMemcpyAsync(errs.data(), dev + o_err, sizeof(int) * m, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
-            if (e != hipSuccess) rc = hip_fail(e, "jpeg batch entropy decode");
-            if (!rc) {  // ik_batch_last_timing: the launch's time and algorithmic bytes
-                double scan = 0, coef = 0, lanes = 0;
-                for (int k = 0; k < m; ++k) {
-                    scan += (double)args[k].size;
-                    coef += (double)ds[gpu_idx[k]]->nblocks * 64 * sizeof(int16_t);
-                    lanes += args[k].n_seg;
-                }
-                const int d = current_device();
-                batch_timing_add(d, kBtJpegHuffMs, ev_pair_ms(ev));
-                batch_timing_add(d, kBtJpegScanBytes, scan);
-                batch_timing_add(d, kBtJpegCoefBytes, coef);
-                batch_timing_add(d, kBtJpegImages, m);
-                batch_timing_add(d, kBtJpegLanes, lanes);
-            }
-        }
-        // 3. reconstruction of every image the GPU decoded cleanly
-        for (int k = 0; k < m && !rc; ++k) {
-            const int i = gpu_idx[k];
-            if (errs[k]) { host_idx.push_back(i); continue; }
-            const Decoder& d = *ds[i];
-            JpegGeom g = lay[k].g;
-            g.qt = reinterpret_cast<const uint16_t*>(dev + lay[k].q);
-            g.coef = reinterpret_cast<const int16_t*>(dev + lay[k].coef);
-            g.planes = dev + lay[k].pl;
-            ik_image* img = nullptr;
-            st[i] = alloc_image((uint32_t)d.width, (uint32_t)d.height, d.comps.size() == 1 ? 1u : 3u, &img);
-            if (st[i]) continue;
-            hipError_t e = launch_jpeg_reconstruct(g, img->d, img->pitch, s);
-            if (e != hipSuccess) { ik_image_free(img); st[i] = hip_fail(e, "jpeg reconstruct"); continue; }
-            outs[i] = img;
-        }
-        hipError_t e = rc ? hipSuccess : hipStreamSynchronize(s);
-        if (rc || e != hipSuccess) {  // the batch as a whole failed on the device: each image on its own path
-            for (int k = 0; k < m; ++k) {
-                const int i = gpu_idx[k];
-                if (outs[i]) { ik_image_free(outs[i]); outs[i] = nullptr; }
-                if (!errs[k]) host_idx.push_back(i);
-                st[i] = IK_OK;
-            }
-        } else {
-            for (int k = 0; k < m; ++k)
-                if (outs[gpu_idx[k]]) g_jpeg_gpu_streams += 1;
-        }
-        (void)hdr;
-    }
-    // 4. everything else: the single-image path with host entropy decoding
-    // restart-free baseline scans: self-synchronising GPU decoding, one stream per host thread
+    // 2. the baseline scans: the self-synchronising GPU decoder over all of them at once
+    jsync_batch(ds, js_idx, outs, st, host_idx);
+    // 3. everything else: progressive scans with restart intervals on the GPU image by
+    // image, the rest (and anything the GPU found inconsistent) with host entropy decoding
     const int nh = (int)host_idx.size();
-    host_idx.insert(host_idx.end(), seq_idx.begin(), seq_idx.end());
+    host_idx.insert(host_idx.end(), prog_idx.begin(), prog_idx.end());
     parallel_for((int)host_idx.size(), 0, [&](int k) {
         const int i = host_idx[k];
         st[i] = decode_jpeg_impl(bytes[i], lens[i], &outs[i], k >= nh);
@@ -1306,13 +1116,7 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
     return first;
 }
 
-int decode_jpeg_device(const uint8_t* bytes, size_t n, ik_image** out) {
-    static const bool gpu = [] {
-        const char* e = getenv("IK_JPEG_GPU_ENTROPY");
-        return !(e && !strcmp(e, "0"));
-    }();
-    return decode_jpeg_impl(bytes, n, out, gpu);
-}
+int decode_jpeg_device(const uint8_t* bytes, size_t n, ik_image** out) { return decode_jpeg_impl(bytes, n, out, true); }
 
 }  // namespace ik
 

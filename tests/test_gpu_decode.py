@@ -8,6 +8,7 @@ tests/test_gpu_jpeg_zune.py).  PNG: decoding is specified exactly; checked
 against Pillow/libpng and against the source pixels, across colour types, bit
 depths, the five filter types and Adam7 (a small PNG writer below produces those).
 """
+import ctypes
 import io
 import struct
 import zlib
@@ -434,33 +435,30 @@ def test_decode_batch_reports_failures(ik):
         decode_image_batch([good, b"\x00" * 10, good])
 
 
-def test_jpeg_seq_opt_in_is_correct():
-    """IK_JPEG_SEQ=1 (self-synchronising GPU decoding of restart-free scans, opt-in):
-    pixels still equal libjpeg-turbo's, through the GPU or through the fallback."""
-    import os
-    import subprocess
-    import sys
-    code = (
-        "import io,sys,numpy as np; sys.path[:0]=['rust-image-transform_amd','tests']\n"
-        "from PIL import Image; import ikutil; from imagekit import decode_image\n"
-        "for k,(w,h,sub) in enumerate([(640,480,2),(300,200,0),(97,61,1)]):\n"
-        "    buf=io.BytesIO(); Image.fromarray(ikutil.synth(w,h,3,seed=k,pattern='S')).save(buf,format='JPEG',quality=85,subsampling=sub)\n"
-        "    b=buf.getvalue(); img,_=decode_image(b)\n"
-        "    assert np.array_equal(img.to_array(), np.asarray(Image.open(io.BytesIO(b)))), k\n"
-        "print('ok')\n")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=dict(os.environ, IK_JPEG_SEQ="1", IK_JPEG_RECON="libjpeg"),
-                       capture_output=True, text=True, timeout=110)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+def test_jpeg_small_scans_counted_where_decoded(ik):
+    """Baseline scans of 4 KiB and up go to the self-synchronising GPU decoder
+    (counted GPU), smaller ones to the host entropy decoder (counted host): pixels
+    equal libjpeg-turbo's either way."""
+    c0 = (ctypes.c_ulonglong * 2)()
+    ik.ik_jpeg_counters(c0)
+    small = _jpeg(ikutil.synth(40, 30, 3, seed=3, pattern="S"), quality=85)
+    big = _jpeg(ikutil.synth(700, 500, 3, seed=4, pattern="S"), quality=85)
+    assert len(small) < 4096 < len(big)
+    for b in (small, big):
+        img, _ = decode_image(b)
+        np.testing.assert_array_equal(img.to_array(), np.asarray(Image.open(io.BytesIO(b))))
+    c1 = (ctypes.c_ulonglong * 2)()
+    ik.ik_jpeg_counters(c1)
+    assert (c1[0] - c0[0], c1[1] - c0[1]) == (1, 1)
 
 
 @pytest.mark.parametrize("wh", [(1500, 1100), (2048, 1536), (1001, 999)])
 @pytest.mark.parametrize("sub", [0, 1, 2])
 @pytest.mark.parametrize("pat", ["S", "N"])
 def test_jpeg_no_restart_self_sync_gpu(ik, wh, sub, pat):
-    """Restart-free baseline scans >= 32 KB go through self-synchronising GPU
-    decoding (GPU rounds + host frontier walk + GPU decode pass): pixels equal
-    libjpeg-turbo's."""
+    """Restart-free baseline scans go through the self-synchronising GPU decoder
+    (sync pass with warm-up, fix rounds, bases, decode pass -- all on the GPU):
+    pixels equal libjpeg-turbo's."""
     w, h = wh
     b = _jpeg(ikutil.synth(w, h, 3, seed=w + sub, pattern=pat), quality=92 if pat == "S" else 60, subsampling=sub)
     img, _ = decode_image(b)
