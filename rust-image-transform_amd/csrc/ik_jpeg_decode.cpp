@@ -22,6 +22,8 @@
 #include <cstdio>
 #include <cstring>
 #include <vector>
+#include <array>
+#include <mutex>
 
 #include "../../include/imagekit_hip.h"
 #include "ik_runtime.h"
@@ -690,6 +692,11 @@ inline size_t up256(size_t x) { return (x + 255) / 256 * 256; }
 // process-wide: JPEG streams whose entropy decoding ran on the GPU / on the host
 std::atomic<unsigned long long> g_jpeg_gpu_streams{0}, g_jpeg_host_streams{0};
 
+#ifdef IK_JPEG_DUMP
+std::mutex g_jdump_mu;
+std::vector<std::array<std::vector<uint8_t>, 7>> g_jdump;  // per image of the last batch
+#endif
+
 // The baseline scans of a batch (ds[idx[k]]->js), all through the self-synchronising
 // GPU decoder at once (ik_jsync.hip; algorithm ik_jpeg_sync.h):
 //   1. upload: every scan's bytes (DMAed in place when page-locked, else staged),
@@ -904,6 +911,32 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
             if (ok[k]) host_idx.push_back(idx[k]);
         return;
     }
+#ifdef IK_JPEG_DUMP  // dev experiment: every image's unstuffed words, lane tables and coefficients
+    if (e == hipSuccess) {
+        std::lock_guard<std::mutex> lk(g_jdump_mu);
+        g_jdump.assign(m, {});
+        for (int k = 0; k < m; ++k) {
+            if (!ok[k]) continue;
+            const Decoder& d = *ds[idx[k]];
+            const Lay& L = lay[k];
+            const int nl = ivl_lane[L.ivl0 + d.js_nivl];
+            auto get = [&](int what, const void* src, size_t bytes) {
+                g_jdump[k][what].resize(bytes);
+                (void)hipMemcpy(g_jdump[k][what].data(), src, bytes, hipMemcpyDeviceToHost);
+            };
+            get(0, dev + L.out, d.js_len);
+            get(1, dev + o_ivl + sizeof(long long) * L.ivl0, sizeof(long long) * (d.js_nivl + 1));
+            get(2, dev + o_recs + sizeof(LaneRec) * L.lane0, sizeof(LaneRec) * nl);
+            get(3, dev + o_bases + sizeof(LaneBase) * L.lane0, sizeof(LaneBase) * nl);
+            get(4, dev + L.coef, d.nblocks * 64 * sizeof(int16_t));
+            g_jdump[k][5].resize(sizeof(int) * (d.js_nivl + 1));
+            std::memcpy(g_jdump[k][5].data(), ivl_lane.data() + L.ivl0, sizeof(int) * (d.js_nivl + 1));
+            g_jdump[k][6].resize(sizeof(int) * 2);
+            std::memcpy(g_jdump[k][6].data(), &hstatus[k], sizeof(int));
+            std::memcpy(g_jdump[k][6].data() + sizeof(int), &rounds, sizeof(int));
+        }
+    }
+#endif
     {  // ik_batch_last_timing: the decoding launches' time and algorithmic bytes
         double scan = 0, coef = 0;
         for (int k = 0; k < m; ++k)
@@ -1144,3 +1177,16 @@ int ik_jpeg_counters(unsigned long long* out) {
 }
 
 }  // extern "C"
+
+#ifdef IK_JPEG_DUMP
+// dev experiment: part `what` of image i of the last self-synchronising batch
+// (0 unstuffed bytes, 1 interval bits, 2 lane records, 3 lane bases, 4 coefficients,
+// 5 interval lanes, 6 status and fix rounds); returns its size
+extern "C" long long ik_dev_jpeg_dump(int i, int what, uint8_t* out, size_t cap) {
+    std::lock_guard<std::mutex> lk(ik::g_jdump_mu);
+    if (i < 0 || i >= (int)ik::g_jdump.size() || what < 0 || what > 6) return -1;
+    const auto& v = ik::g_jdump[i][what];
+    if (out) std::memcpy(out, v.data(), std::min(cap, v.size()));
+    return (long long)v.size();
+}
+#endif

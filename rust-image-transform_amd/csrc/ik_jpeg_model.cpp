@@ -334,7 +334,7 @@ int ikm_jsync_decode(const uint8_t* jpeg, size_t n, int lane_bits, int warm_bits
             int16_t* blk = &par[(size_t)bi * 64];
             const int c = S.comp_of[j];
             int diff;
-            if (!block(br, T, kZz, S.td[c], S.ta[c], &diff, blk)) { ok = false; break; }
+            if (!block<true>(br, T, kZz, S.td[c], S.ta[c], &diff, blk)) { ok = false; break; }
             pred[c] += diff;
             blk[0] = (int16_t)pred[c];
             j = j + 1 == S.bpm ? 0 : j + 1;
@@ -354,7 +354,7 @@ int ikm_jsync_decode(const uint8_t* jpeg, size_t n, int lane_bits, int warm_bits
             const int c = S.comp_of[j];
             int16_t* blk = &ser[(size_t)block_index(S, b) * 64];
             int diff;
-            if (!block(br, T, kZz, S.td[c], S.ta[c], &diff, blk)) { sok = false; break; }
+            if (!block<true>(br, T, kZz, S.td[c], S.ta[c], &diff, blk)) { sok = false; break; }
             pred[c] += diff;
             blk[0] = (int16_t)pred[c];
         }

@@ -188,9 +188,10 @@ IK_HD int getbits(Bits& br, int n) {
 }
 
 // One block (T.81 F.2.2.1-2): the DC difference into *dcdiff; the AC levels into
-// blk (natural order, zz maps zigzag -> natural) when blk != null, else skipped.
-// false on a bad code.
-template <typename Blk>
+// blk (natural order, zz maps zigzag -> natural) when kStore, else skipped.
+// false on a bad code.  (A template flag, not a null test: an LDS block at
+// address 0 is a valid pointer the compiler may still treat as null.)
+template <bool kStore, typename Blk>
 IK_HD bool block(Bits& br, const JpegHuffTables& T, const uint8_t* zz, int td, int ta, int* dcdiff, Blk blk) {
     const int t = sym(br, T, td);
     if (t < 0 || t > 11) return false;
@@ -201,7 +202,7 @@ IK_HD bool block(Bits& br, const JpegHuffTables& T, const uint8_t* zz, int td, i
             k += (fa >> 4) & 15;
             br.pos += (uint32_t)(fa & 15);
             if (k > 63) return false;
-            if (blk) blk[zz[k]] = (int16_t)(fa >> 8);
+            if (kStore) blk[zz[k]] = (int16_t)(fa >> 8);
             ++k;
             continue;
         }
@@ -216,7 +217,7 @@ IK_HD bool block(Bits& br, const JpegHuffTables& T, const uint8_t* zz, int td, i
         k += r;
         if (k > 63) return false;
         const int val = extend(getbits(br, sz), sz);
-        if (blk) blk[zz[k]] = (int16_t)val;
+        if (kStore) blk[zz[k]] = (int16_t)val;
         ++k;
     }
     return true;
@@ -285,7 +286,7 @@ IK_HD void run_lane(const Scan& S, const JpegHuffTables& T, const uint8_t* zz, c
         }
         const int c = S.comp_of[j];
         int diff;
-        if (!block(br, T, zz, S.td[c], S.ta[c], &diff, (int16_t*)nullptr)) {
+        if (!block<false>(br, T, zz, S.td[c], S.ta[c], &diff, (int16_t*)nullptr)) {
             r.err = 1 + r.nblk;
             if (counting) ++r.nblk;  // the block started in the range (a padding block at an interval end)
             return;

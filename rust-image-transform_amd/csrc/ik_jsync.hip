@@ -385,12 +385,14 @@ __global__ __launch_bounds__(kLanesPerWG) void k_jsync_decode(const Scan* scans,
     int pred[4];
     for (int c = 0; c < 4; ++c) pred[c] = B.dc[c];
     typedef __attribute__((address_space(3))) int16_t lds_i16;
-    typedef int16_t s8 __attribute__((ext_vector_type(8)));
+    // may_alias: the block's 16-byte reads must see block()'s 2-byte stores (without
+    // it type-based alias analysis lets the compiler move the reads above them)
+    typedef int16_t s8 __attribute__((ext_vector_type(8), __may_alias__));
     lds_i16* blk = (lds_i16*)(s_blk + threadIdx.x * 64);
     for (int i = 0; i < B.count; ++i) {
         const int c = S.comp_of[j];
         int diff;
-        if (!block(br, L.T, L.zz, S.td[c], S.ta[c], &diff, blk)) {
+        if (!block<true>(br, L.T, L.zz, S.td[c], S.ta[c], &diff, blk)) {
             atomicOr(status + w.x, 8);
             return;
         }
