@@ -471,8 +471,7 @@ def main():
         # JPEG sources: the PNG stage times do not apply.  The entropy decoding launch
         # reads the scans and writes every block's int16 coefficients (the bytes a
         # decode of these frames must move, SURVEY 8(d) D-5's decode-stage share)
-        kern = {"k_jpeg_huff_batch" if args.source == "jpeg-rst" else "k_jpeg_seq_decode":
-                (float(bt[0]), float(bt[1] + bt[2]))}
+        kern = {"k_jsync_*": (float(bt[0]), float(bt[1] + bt[2]))}
         jpeg_huff = {"ms": round(float(bt[0]), 4), "scan_bytes": int(bt[1]), "coef_bytes": int(bt[2]),
                      "images": int(bt[3]), "lanes": int(bt[4])}
     resize_batch = None
@@ -497,9 +496,10 @@ def main():
         note = ("DEFLATE decoding: each lane's symbol-to-symbol chain bounds it (one lane per block, ~1,900 "
                 "blocks per frame), not HBM; bytes = compressed bits in + u16 tokens out")
     else:
-        note = ("JPEG entropy decoding: each lane's Huffman symbol chain bounds it, not HBM; bytes = the "
-                "entropy-coded scans read + every block's int16 coefficients written (HIP events on the kernel "
-                "stream around the launch)")
+        note = ("JPEG entropy decoding, self-synchronising (k_jsync_sync, the k_jsync_fix rounds, "
+                "k_jsync_seg1-3, k_jsync_decode: HIP events on the kernel stream around them, the fix "
+                "rounds' host round trips included): each lane's Huffman symbol chain bounds it, not HBM; "
+                "bytes = the unstuffed scans read + every block's int16 coefficients written")
     roof = {"bound": "hbm", "achieved": round(dbytes / (dms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(dbytes / (dms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": traffic_png, "kernel": dom,
             "kernel_ms": round(dms, 4), "bytes_per_launch": int(dbytes), "note": note}
@@ -614,7 +614,7 @@ def main():
                         "ik_transform_batch_submit_device: decode_image (GPU chunk walk, gather + CRC, inflate + "
                         "unfilter)",
                  "jpeg-rst": "JPEG q90 4:2:0 with a restart marker per MCU row, in page-locked host memory -> "
-                             "ik_transform_batch_submit: decode_image (GPU entropy decoding per restart interval, "
+                             "ik_transform_batch_submit: decode_image (self-synchronising GPU entropy decoding, "
                              "IDCT, upsampling, colour)",
                  "jpeg": "JPEG q90 4:2:0 without restart markers, in page-locked host memory -> "
                          "ik_transform_batch_submit: decode_image (GPU self-synchronising entropy decoding, IDCT, "
