@@ -145,8 +145,8 @@ hipError_t launch_jsync_unstuff(JsImageDev* imgs, int nimg, const int2* chunks, 
 // wgs: (image, first lane of the image) per 256-lane workgroup; every image's lanes
 // start on a multiple of 256 (jsync::Scan::lane0)
 hipError_t launch_jsync_sync(const jsync::Scan* scans, const int2* wgs, int nwg, jsync::LaneRec* recs, hipStream_t s);
-hipError_t launch_jsync_fix(const jsync::Scan* scans, const int2* wgs, int nwg, jsync::LaneRec* recs, int* changed,
-                            hipStream_t s);
+hipError_t launch_jsync_fix(const jsync::Scan* scans, int nimg, const int2* wgs, int nwg, jsync::LaneRec* recs,
+                            int* rounds, hipStream_t s);
 // bases (segmented prefix sums over each interval's lanes) then the decode pass;
 // chunk_scratch: jsync_chunk_scratch_bytes(lanes); status[image]
 hipError_t launch_jsync_bases_decode(const jsync::Scan* scans, int nimg, const int2* wgs, int nwg,

@@ -134,6 +134,8 @@ const char* const kFmtErr = "Format error decoding Jpeg";
 // Baseline scans go to the self-synchronising GPU decoder (ik_jsync.hip) from this
 // size up; smaller ones are faster on the host entropy decoder.
 constexpr size_t kJsyncMinBytes = 4 << 10;
+// lanes a batch's self-synchronising decoding aims for (about what the chip holds at once)
+constexpr long long kJsyncLanes = 512 << 10;
 
 // Progressive scans with restart intervals on the GPU (k_jpeg_prog);
 // IK_JPEG_PROG=0 keeps them on the host entropy decoder.
@@ -702,8 +704,9 @@ std::vector<std::array<std::vector<uint8_t>, 7>> g_jdump;  // per image of the l
 //   1. upload: every scan's bytes (DMAed in place when page-locked, else staged),
 //      Huffman and quantisation tables, the unstuffing chunk table -- one small copy
 //   2. unstuffing on the GPU, then the interval tables come back (a few KB)
-//   3. lanes: per image, each interval cut into jsync::kLaneBits pieces (host)
-//   4. the sync pass, fix rounds until no lane changes, bases, the decode pass
+//   3. lanes: per image, each interval cut into pieces of lane_bits (host)
+//   4. the sync pass, the fix rounds (one over all lanes, then the settle kernel's
+//      per image until no lane changes), bases, the decode pass -- no host round trip
 //   5. reconstruction of every image (IDCT, upsampling, colour)
 // An image the GPU finds inconsistent (a stray marker, a restart count that does
 // not match the frame, lanes that never synchronise, a bad code) goes to host_idx:
@@ -729,6 +732,14 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
     const size_t o_img = take(sizeof(JsImageDev) * m);
     int nchunks = 0, nivl_total = 0;
     long long lanes_max = 0;
+    // lane length: 1,024 bits, longer for large batches (up to 4,096) while the batch
+    // still has ~kJsyncLanes lanes -- a longer lane costs the sync pass less warm-up
+    // per bit and the fix rounds about as many rounds (ik_jpeg_model.cpp on the
+    // bench's 4096^2 frames: sync + fix work 2.8x the scan at 1,024, 1.7x at 4,096)
+    long long batch_bits = 0;
+    for (int k = 0; k < m; ++k) batch_bits += 8ll * (long long)ds[idx[k]]->js_len;
+    const int lane_bits = (int)std::min<long long>(4 * kLaneBits,
+                                                   std::max<long long>(1, batch_bits / kJsyncLanes / kLaneBits) * kLaneBits);
     for (int k = 0; k < m; ++k) {
         const Decoder& d = *ds[idx[k]];
         Lay& L = lay[k];
@@ -738,7 +749,7 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
         L.ivl0 = nivl_total;
         nivl_total += (int)d.js_nivl + 1;
         L.lane0 = lanes_max;
-        L.lanes_max = ((long long)(8 * d.js_len) / kLaneBits + d.js_nivl + 1 + 255) & ~255ll;
+        L.lanes_max = ((long long)(8 * d.js_len) / lane_bits + d.js_nivl + 1 + 255) & ~255ll;
         lanes_max += L.lanes_max;
     }
     const size_t o_chunks = take(sizeof(int2) * nchunks);
@@ -854,7 +865,7 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
             for (long long q = 0; q < d.js_nivl; ++q) {
                 const long long bits = iv[q + 1] - iv[q];
                 if (bits < 0) { good = false; break; }
-                il[q + 1] = il[q] + (int)std::max<long long>(1, (bits + kLaneBits - 1) / kLaneBits);
+                il[q + 1] = il[q] + (int)std::max<long long>(1, (bits + lane_bits - 1) / lane_bits);
             }
             if (!good || il[d.js_nivl] > L.lanes_max) continue;
             ok[k] = 1;
@@ -863,6 +874,7 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
             for (int w = 0; w < nl; w += 256) wgs.push_back(make_int2(k, w));
             Scan& S = scans[k];
             S = d.js_scan;
+            S.L = lane_bits;
             S.words = reinterpret_cast<const uint32_t*>(dev + L.out);
             S.ivl = reinterpret_cast<const long long*>(dev + o_ivl) + L.ivl0;
             S.nivl = (int)d.js_nivl;
@@ -889,23 +901,17 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
     e = hipMemcpyAsync(dev + o_scans, hp, tab2_bytes, hipMemcpyHostToDevice, s);
     if (e == hipSuccess && ev.a) e = hipEventRecord(ev.a, s);
     if (e == hipSuccess) e = launch_jsync_sync(d_scans, d_wgs, nwg, d_recs, s);
-    int rounds = 0;
-    int* hchanged = reinterpret_cast<int*>(hp + tab2_bytes);  // (pinned, past what the upload reads)
-    while (e == hipSuccess) {
-        e = hipMemsetAsync(d_changed, 0, sizeof(int), s);
-        if (e == hipSuccess) e = launch_jsync_fix(d_scans, d_wgs, nwg, d_recs, d_changed, s);
-        if (e == hipSuccess) e = hipMemcpyAsync(hchanged, d_changed, sizeof(int), hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        ++rounds;
-        if (e != hipSuccess || *hchanged == 0 || rounds > 4096) break;
-    }
+    if (e == hipSuccess) e = hipMemsetAsync(d_changed, 0, sizeof(int), s);
+    if (e == hipSuccess) e = launch_jsync_fix(d_scans, m, d_wgs, nwg, d_recs, d_changed, s);
     if (e == hipSuccess)
         e = launch_jsync_bases_decode(d_scans, m, d_wgs, nwg, d_recs, reinterpret_cast<LaneBase*>(dev + o_bases),
                                       dev + o_cs, d_status, s);
     if (e == hipSuccess && ev.b) e = hipEventRecord(ev.b, s);
+    int rounds = 0;  // the settle kernel's most rounds over the batch's images
     if (e == hipSuccess) e = hipMemcpyAsync(hstatus.data(), d_status, sizeof(int) * m, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(&rounds, d_changed, sizeof(int), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess || rounds > 4096) {
+    if (e != hipSuccess) {
         if (e != hipSuccess) (void)hip_fail(e, "jpeg entropy decode");
         for (int k = 0; k < m; ++k)
             if (ok[k]) host_idx.push_back(idx[k]);

@@ -275,6 +275,9 @@ IK_HD void run_lane(const Scan& S, const JpegHuffTables& T, const uint8_t* zz, c
     br.init(S.words, st_bit(from), g.e);
     int j = st_j(from);
     bool counting = false;
+    // the DC sums in four registers (an array indexed by the component would live
+    // in scratch memory on the GPU)
+    int dc0 = 0, dc1 = 0, dc2 = 0, dc3 = 0;
     for (;;) {
         if (!counting && br.pos >= g.lo) {
             counting = true;
@@ -282,22 +285,30 @@ IK_HD void run_lane(const Scan& S, const JpegHuffTables& T, const uint8_t* zz, c
         }
         if (br.pos >= g.hi) {
             r.exit = st_pack(br.pos, j);
-            return;
+            break;
         }
         const int c = S.comp_of[j];
         int diff;
         if (!block<false>(br, T, zz, S.td[c], S.ta[c], &diff, (int16_t*)nullptr)) {
             r.err = 1 + r.nblk;
             if (counting) ++r.nblk;  // the block started in the range (a padding block at an interval end)
-            return;
+            break;
         }
         ++r.work;
         if (counting) {
             ++r.nblk;
-            r.dc[c] += diff;
+            const int d = diff;
+            dc0 += c == 0 ? d : 0;
+            dc1 += c == 1 ? d : 0;
+            dc2 += c == 2 ? d : 0;
+            dc3 += c == 3 ? d : 0;
         }
         j = j + 1 == S.bpm ? 0 : j + 1;
     }
+    r.dc[0] = dc0;
+    r.dc[1] = dc1;
+    r.dc[2] = dc2;
+    r.dc[3] = dc3;
 }
 
 // the sync pass's starting state for lane q: the interval start for q = 0, else a

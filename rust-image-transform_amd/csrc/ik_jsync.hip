@@ -12,7 +12,9 @@
 //                    position (big-endian words), interval starts
 //   k_jsync_sync     a thread per lane: warm-up, START, EXIT, block count, DC sums
 //   k_jsync_fix      a thread per lane: re-decode an inconsistent lane from its
-//                    predecessor's EXIT (one round; the host repeats until none)
+//                    predecessor's EXIT (the first fix round, at full occupancy)
+//   k_jsync_settle   a workgroup per image: the remaining fix rounds, over a list
+//                    of the lanes whose predecessor changed, until none is left
 //   k_jsync_seg1..3  per-lane block bases and DC predictions: a segmented prefix
 //                    sum over each interval's lanes (a wave per 64 lanes, the carries
 //                    between chunks per image, then per lane), the padding's blocks
@@ -172,20 +174,29 @@ struct JsLds {
     JpegHuffTables T;
     uint8_t zz[64];
 };
+// the workgroup's Scan in LDS: the per-block reads of its component tables
+// (comp_of, td, ta by a lane's own MCU phase) are LDS reads, not memory loads
+__device__ __forceinline__ void load_scan(const Scan* g, Scan& s) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(g);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&s);
+    for (int i = threadIdx.x; i < (int)(sizeof(Scan) / 4); i += blockDim.x) dst[i] = src[i];
+}
 __device__ __forceinline__ void load_tables(const JpegHuffTables* g, JsLds& L) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(g);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&L.T);
     for (int i = threadIdx.x; i < (int)(sizeof(JpegHuffTables) / 4); i += blockDim.x) dst[i] = src[i];
     if (threadIdx.x < 64) L.zz[threadIdx.x] = kZzNat[threadIdx.x];
 }
+
 }  // namespace
 
 // wg: (image, first lane of the image's lanes this workgroup takes)
 __global__ __launch_bounds__(kLanesPerWG) void k_jsync_sync(const Scan* scans, const int2* wgs, LaneRec* recs) {
     __shared__ JsLds L;
+    __shared__ Scan S;
     const int2 w = wgs[blockIdx.x];
-    const Scan& S = scans[w.x];
-    load_tables(S.tabs, L);
+    load_scan(scans + w.x, S);
+    load_tables(scans[w.x].tabs, L);
     __syncthreads();
     const int r = w.y + (int)threadIdx.x;
     if (r >= S.ivl_lane[S.nivl]) return;
@@ -196,15 +207,19 @@ __global__ __launch_bounds__(kLanesPerWG) void k_jsync_sync(const Scan* scans, c
     recs[S.lane0 + r] = rec;
 }
 
-// one fix round: an inconsistent lane re-decodes from its predecessor's EXIT
-// (a predecessor re-decoded in the same round may be read before or after its
-// update -- either is a valid state of the chain; its EXIT is one 8-byte word)
-__global__ __launch_bounds__(kLanesPerWG) void k_jsync_fix(const Scan* scans, const int2* wgs, LaneRec* recs,
-                                                           int* changed) {
+// the first fix round, over every lane of the batch at full occupancy: an
+// inconsistent lane re-decodes from its predecessor's EXIT (a predecessor
+// re-decoded in the same round may be read before or after its update -- either
+// is a valid state of the chain, its EXIT one 8-byte word; k_jsync_settle checks
+// every lane again)
+__global__ __launch_bounds__(kLanesPerWG) void k_jsync_fix(const Scan* scans, const int2* wgs, LaneRec* recs) {
     __shared__ JsLds L;
+    __shared__ Scan S;
     __shared__ int s_any;
     const int2 w = wgs[blockIdx.x];
-    const Scan& S = scans[w.x];
+    load_scan(scans + w.x, S);
+    if (threadIdx.x == 0) s_any = 0;
+    __syncthreads();
     const int r = w.y + (int)threadIdx.x;
     const long long l = S.lane0 + r;
     int k = 0, q = 0;
@@ -218,8 +233,6 @@ __global__ __launch_bounds__(kLanesPerWG) void k_jsync_fix(const Scan* scans, co
             todo = from != 0 && recs[l].start != from;
         }
     }
-    if (threadIdx.x == 0) s_any = 0;
-    __syncthreads();
     if (todo) s_any = 1;
     __syncthreads();
     if (!s_any) return;  // (the whole workgroup: nothing to redo, no tables to load)
@@ -236,7 +249,96 @@ __global__ __launch_bounds__(kLanesPerWG) void k_jsync_fix(const Scan* scans, co
     recs[l].work = rec.work;
     for (int c = 0; c < 4; ++c) recs[l].dc[c] = rec.dc[c];
     __hip_atomic_store(&recs[l].exit, rec.exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    atomicAdd(changed, 1);
+}
+
+// The remaining fix rounds, one workgroup per image, until its lanes are
+// consistent -- no launch and no host round trip per round.  A round works a list
+// of lanes in passes of kSettleThreads: a listed lane whose START differs from its
+// predecessor's EXIT re-decodes from that EXIT, the results are committed, and
+// then each re-decoded lane whose successor's START differs from its new EXIT
+// appends the successor to the next round's list.  The barriers between the three
+// steps keep a pass free of races: every EXIT a pass reads was committed before
+// it, a lane is committed by one thread, and successors are checked against
+// committed STARTs.  The first list is a scan of all the image's lanes, and so is
+// the list after one that overflowed.  After kSettleMaxRounds rounds the rest is
+// left inconsistent (the bases pass flags it; the host decoder takes the image).
+namespace {
+constexpr int kSettleThreads = 1024;
+constexpr int kSettleList = 4096;
+constexpr int kSettleMaxRounds = 8192;
+struct SettleLds {
+    int lane[2][kSettleList];
+    int n[2];
+    int full[2];
+};
+}  // namespace
+
+__global__ __launch_bounds__(kSettleThreads) void k_jsync_settle(const Scan* scans, LaneRec* recs, int* rounds_out) {
+    __shared__ JsLds L;
+    __shared__ Scan S;
+    __shared__ SettleLds Q;
+    const int t = threadIdx.x;
+    load_scan(scans + blockIdx.x, S);
+    load_tables(scans[blockIdx.x].tabs, L);
+    if (t == 0) { Q.n[0] = Q.n[1] = 0; Q.full[0] = 1; Q.full[1] = 0; }
+    __syncthreads();
+    const int nl = S.ivl_lane[S.nivl];
+    if (nl <= 1) return;
+    LaneRec* const R = recs + S.lane0;
+    // lane r (not an interval's first) against its predecessor's committed EXIT
+    auto behind = [&](int r, uint64_t& f) -> bool {
+        f = R[r - 1].exit;
+        return f != 0 && R[r].start != f;
+    };
+    int round = 0;
+    for (; round < kSettleMaxRounds; ++round) {
+        const int c = round & 1, nx = c ^ 1;
+        if (Q.full[c]) {  // the list from a scan of every lane
+            if (t == 0) Q.n[c] = 0;
+            __syncthreads();
+            for (int r = t; r < nl; r += kSettleThreads) {
+                uint64_t f;
+                if (r == S.ivl_lane[lane_interval(S, r)] || !behind(r, f)) continue;
+                const int i = atomicAdd(&Q.n[c], 1);
+                if (i < kSettleList) Q.lane[c][i] = r;
+            }
+            __syncthreads();
+        }
+        const int nc = Q.n[c];
+        const int n = nc < kSettleList ? nc : kSettleList;
+        if (n == 0) break;
+        __syncthreads();  // (every thread has read n[c] and full[c] before the resets below)
+        if (t == 0) { Q.n[nx] = 0; Q.full[nx] = nc > kSettleList ? 1 : 0; }
+        __syncthreads();
+        for (int p0 = 0; p0 < n; p0 += kSettleThreads) {
+            const int i = p0 + t;
+            bool did = false;
+            int r = 0, k = 0;
+            LaneRec rec;
+            if (i < n) {
+                r = Q.lane[c][i];
+                uint64_t f;
+                if (behind(r, f)) {
+                    k = lane_interval(S, r);
+                    const LaneGeom g = lane_geom(S, k, r - S.ivl_lane[k]);
+                    const int wk = R[r].work;
+                    run_lane(S, L.T, L.zz, g, f, rec);
+                    rec.work += wk;
+                    did = true;
+                }
+            }
+            __syncthreads();  // every read of the pass done
+            if (did) R[r] = rec;
+            __syncthreads();  // every commit of the pass done
+            if (did && r + 1 < S.ivl_lane[k + 1] && rec.exit && R[r + 1].start != rec.exit) {
+                const int j = atomicAdd(&Q.n[nx], 1);
+                if (j < kSettleList) Q.lane[nx][j] = r + 1;
+                else Q.full[nx] = 1;
+            }
+            __syncthreads();
+        }
+    }
+    if (t == 0) atomicMax(rounds_out, round);
 }
 
 // ---- bases: segmented prefix sums of (blocks, DC sums) over each interval's lanes --
@@ -365,9 +467,10 @@ __global__ __launch_bounds__(kLanesPerWG) void k_jsync_decode(const Scan* scans,
                                                               const LaneBase* bases, int* status) {
     __shared__ JsLds L;
     __shared__ __attribute__((aligned(16))) int16_t s_blk[kLanesPerWG * 64];
+    __shared__ Scan S;
     const int2 w = wgs[blockIdx.x];
-    const Scan& S = scans[w.x];
-    load_tables(S.tabs, L);
+    load_scan(scans + w.x, S);
+    load_tables(scans[w.x].tabs, L);
     for (int i = threadIdx.x; i < kLanesPerWG * 8; i += kLanesPerWG)
         reinterpret_cast<uint4*>(s_blk)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
@@ -424,9 +527,11 @@ hipError_t launch_jsync_sync(const Scan* scans, const int2* wgs, int nwg, LaneRe
     return hipGetLastError();
 }
 
-hipError_t launch_jsync_fix(const Scan* scans, const int2* wgs, int nwg, LaneRec* recs, int* changed, hipStream_t s) {
+hipError_t launch_jsync_fix(const Scan* scans, int nimg, const int2* wgs, int nwg, LaneRec* recs, int* rounds,
+                            hipStream_t s) {
     if (nwg <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_jsync_fix, dim3(nwg), dim3(kLanesPerWG), 0, s, scans, wgs, recs, changed);
+    hipLaunchKernelGGL(k_jsync_fix, dim3(nwg), dim3(kLanesPerWG), 0, s, scans, wgs, recs);
+    hipLaunchKernelGGL(k_jsync_settle, dim3(nimg), dim3(kSettleThreads), 0, s, scans, recs, rounds);
     return hipGetLastError();
 }
 
