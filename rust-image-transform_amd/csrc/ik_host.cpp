@@ -1159,7 +1159,7 @@ static size_t sniff_len(const uint8_t* const* sniff, const uint8_t* const* bytes
 
 int decode_batch_dev(const uint8_t* const* bytes, const size_t* lens, uint32_t n, ik_image** outs, int* fmts,
                      int* st, std::string* msg, int threads, PngUpload* up = nullptr,
-                     const uint8_t* const* sniff = nullptr) {
+                     const uint8_t* const* sniff = nullptr, const JpegUpload* jup = nullptr) {
     std::vector<const uint8_t*> jb, pb, ph;
     std::vector<size_t> jl, pl;
     std::vector<uint32_t> ji, pi, other;
@@ -1211,7 +1211,7 @@ int decode_batch_dev(const uint8_t* const* bytes, const size_t* lens, uint32_t n
         std::vector<ik_image*> jo(ji.size(), nullptr);
         std::vector<int> js(ji.size(), IK_OK);
         std::vector<std::string> jm(ji.size());
-        decode_jpeg_batch(jb.data(), jl.data(), (int)ji.size(), jo.data(), js.data(), jm.data());
+        decode_jpeg_batch(jb.data(), jl.data(), (int)ji.size(), jo.data(), js.data(), jm.data(), jup);
         for (size_t k = 0; k < ji.size(); ++k) {
             outs[ji[k]] = jo[k];
             st[ji[k]] = js[k];
@@ -1327,13 +1327,26 @@ static void png_items(const uint8_t* const* bytes, const size_t* lens, const uin
         }
 }
 
+// the JPEG requests among idx, host inputs only (device-resident batches copy
+// their non-PNG items to the host first)
+static void jpeg_items(const uint8_t* const* bytes, const size_t* lens, const std::vector<uint32_t>& idx,
+                       std::vector<const uint8_t*>& jb, std::vector<size_t>& jl) {
+    jb.clear();
+    jl.clear();
+    for (uint32_t i : idx)
+        if (bytes[i] && guess_format(bytes[i], lens[i]) == Sniffed::Jpeg) {
+            jb.push_back(bytes[i]);
+            jl.push_back(lens[i]);
+        }
+}
+
 // Device half: decode (GPU where the stream allows; the PNG upload already issued
 // when up is given), resize, the encoders' device front ends; request i's status /
 // message land in st[i] / errs[i]
 static void transform_device_phase(const uint8_t* const* bytes, const size_t* lens, const int64_t* w,
                                    const int64_t* h, const int* fmt, const int* quality, int filter, int* st,
                                    std::string* errs, HostPhase& hp, PngUpload* up,
-                                   const uint8_t* const* sniff = nullptr) {
+                                   const uint8_t* const* sniff = nullptr, const JpegUpload* jup = nullptr) {
     const std::vector<uint32_t>& idx = hp.idx;
     const int threads = hp.threads;
     const uint32_t m = (uint32_t)idx.size();
@@ -1354,7 +1367,7 @@ static void transform_device_phase(const uint8_t* const* bytes, const size_t* le
     gate_pin(kGateKernels, true);
     batch_timing_reset(current_device());
     decode_batch_dev(b.data(), l.data(), m, imgs.data(), nullptr, ds.data(), dm.data(), threads, up,
-                     sniff ? sn.data() : nullptr);
+                     sniff ? sn.data() : nullptr, jup);
     gate_enter(kGateKernels);
     std::mutex tmu;
     double& t_resize = hp.t_resize;
@@ -1514,6 +1527,9 @@ struct BatchPart {
     std::vector<const uint8_t*> ph;  // their first bytes in host memory
     const uint8_t* const* sniff = nullptr;  // device-resident inputs (Ticket::sniff), else null
     PngUpload up;
+    std::vector<const uint8_t*> jb;  // its JPEG inputs in host memory
+    std::vector<size_t> jl;
+    JpegUpload jup;  // their device copies (the upload stage's JPEG DMA)
     int logical = -1;  // logical device (multi-device dispatch), -1 = none
     uint64_t cost = 0;
 };
@@ -1564,6 +1580,10 @@ private:
                 p->up.dev = p->sniff != nullptr;
                 p->up.heads = p->ph.data();
                 if (!p->pb.empty()) png_upload_begin(p->pb.data(), p->pl.data(), (int)p->pb.size(), p->up);
+                if (!p->sniff) {
+                    jpeg_items(p->bytes, p->lens, p->hp.idx, p->jb, p->jl);
+                    if (!p->jb.empty()) jpeg_upload_begin(p->jb.data(), p->jl.data(), (int)p->jb.size(), p->jup);
+                }
                 {
                     std::lock_guard<std::mutex> lk(mu_);
                     q_[1].push_back(std::move(p));
@@ -1593,8 +1613,9 @@ private:
                 png_find_prelaunch(nx->up, fs);
             };
             transform_device_phase(p->bytes, p->lens, p->w, p->h, p->fmt, p->quality, p->filter, t.st.data(),
-                                   t.errs.data(), p->hp, p->pb.empty() ? nullptr : &p->up, p->sniff);
+                                   t.errs.data(), p->hp, p->pb.empty() ? nullptr : &p->up, p->sniff, &p->jup);
             p->up = PngUpload();
+            p->jup = JpegUpload();  // (the decode has returned: its area is free again)
             pool_->post([p] {
                 Ticket& tk = *p->t;
                 transform_host_phase(tk.outs, tk.out_lens, tk.st.data(), tk.errs.data(), p->hp);
@@ -1692,6 +1713,7 @@ int shutdown_all() {
     pools_shutdown();
     const int dev = t_device;
     png_shutdown();
+    jpeg_shutdown();
     plans_shutdown();
     memory_shutdown();
     release_thread_resources();

@@ -122,6 +122,15 @@ struct JpegGeom {
     uint8_t* planes;
 };
 hipError_t launch_jpeg_reconstruct(const JpegGeom& g, uint8_t* dst, size_t dst_pitch, hipStream_t s);
+// a batch's reconstructions in three launches (items in device memory)
+struct JpegReconItem {
+    JpegGeom g;
+    uint8_t* dst;
+    size_t pitch;
+};
+hipError_t launch_jpeg_reconstruct_batch(const JpegReconItem* items, int m, long long max_blocks, int max_w, int max_h,
+                                         bool any_fast, hipStream_t s);
+bool jpeg_zune_fast(const JpegGeom& g);
 
 // Baseline Huffman tables (JpegHuffTables) and the self-synchronising decoder's
 // per-lane code are in ik_jpeg_sync.h (shared with its CPU model).

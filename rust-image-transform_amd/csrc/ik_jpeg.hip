@@ -125,8 +125,7 @@ __device__ __forceinline__ void idct_zune(const int (&in)[64], uint8_t* out, int
     }
 }
 
-__global__ __launch_bounds__(256) void k_jpeg_idct(JpegGeom g) {
-    const long long blk = (long long)blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void idct_block(const JpegGeom& g, long long blk) {
     if (blk >= g.nblocks) return;
     int ci = 0;
 #pragma unroll
@@ -197,6 +196,12 @@ __global__ __launch_bounds__(256) void k_jpeg_idct(JpegGeom g) {
         const unsigned hi = o[4] | (o[5] << 8) | (o[6] << 16) | ((unsigned)o[7] << 24);
         *reinterpret_cast<uint2*>(out + (size_t)r * pw) = make_uint2(lo, hi);  // 8-B aligned
     }
+}
+
+__global__ __launch_bounds__(256) void k_jpeg_idct(JpegGeom g) { idct_block(g, (long long)blockIdx.x * 256 + threadIdx.x); }
+// the batch's images in one launch: blockIdx.y = image
+__global__ __launch_bounds__(256) void k_jpeg_idct_b(const JpegReconItem* items) {
+    idct_block(items[blockIdx.y].g, (long long)blockIdx.x * 256 + threadIdx.x);
 }
 
 // upsampled sample of component ci at output pixel (x, y)
@@ -394,9 +399,8 @@ __device__ __forceinline__ void color1_zune(const JpegGeom& g, int x, int y, uin
     o[2] = clamp255(b);
 }
 
-__global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restrict__ dst, size_t pitch) {
-    const int x0 = 4 * (blockIdx.x * 256 + threadIdx.x), y = blockIdx.y;
-    if (x0 >= g.W) return;
+__device__ __forceinline__ void color_group(const JpegGeom& g, uint8_t* __restrict__ dst, size_t pitch, int x0, int y) {
+    if (x0 >= g.W || y >= g.H) return;
     const int C = g.colorspace == 0 ? 1 : 3;
     uint8_t px[12];
     if (zune_fast(g) && x0 >= 4 && x0 + 4 <= g.W && x0 + 3 < 2 * g.bw[1] * 8 - 2) {
@@ -431,13 +435,21 @@ __global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restr
     for (int i = 0; i < C * (g.W - x0); ++i) o[i] = px[i];
 }
 
+__global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restrict__ dst, size_t pitch) {
+    color_group(g, dst, pitch, 4 * (blockIdx.x * 256 + threadIdx.x), blockIdx.y);
+}
+// the batch's images in one launch: blockIdx.z = image
+__global__ __launch_bounds__(256) void k_jpeg_color_b(const JpegReconItem* items) {
+    const JpegReconItem& it = items[blockIdx.z];
+    color_group(it.g, it.dst, it.pitch, 4 * (blockIdx.x * 256 + threadIdx.x), blockIdx.y);
+}
+
 // The row ends of a zune_fast image (the groups of four k_jpeg_color leaves:
 // x0 = 0, and from the first group that reaches the plane's last two chroma
 // samples or the image's right edge), one thread per (row, end): kept out of
 // k_jpeg_color, where a wave holding a row-end thread ran these branches for all
 // of its lanes (50 vs 27 us per 4096^2 frame with them outside).
-__global__ __launch_bounds__(256) void k_jpeg_color_ends(JpegGeom g, uint8_t* __restrict__ dst, size_t pitch) {
-    const int t = blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void color_ends(const JpegGeom& g, uint8_t* __restrict__ dst, size_t pitch, int t) {
     if (t >= 2 * g.H) return;
     const int y = t >> 1;
     const int lim = 2 * g.bw[1] * 8 - 2;  // a group is interior iff x0 >= 4, x0 + 4 <= W and x0 + 3 < lim
@@ -450,6 +462,15 @@ __global__ __launch_bounds__(256) void k_jpeg_color_ends(JpegGeom g, uint8_t* __
     else { xa = 0; xb = g.W < 4 ? g.W : 4; }
     uint8_t* o = dst + (size_t)y * pitch;
     for (int x = xa; x < xb; ++x) color1_zune(g, x, y, o + 3 * x);
+}
+
+__global__ __launch_bounds__(256) void k_jpeg_color_ends(JpegGeom g, uint8_t* __restrict__ dst, size_t pitch) {
+    color_ends(g, dst, pitch, blockIdx.x * 256 + threadIdx.x);
+}
+// the batch's zune_fast images in one launch: blockIdx.y = image (the others return)
+__global__ __launch_bounds__(256) void k_jpeg_color_ends_b(const JpegReconItem* items) {
+    const JpegReconItem& it = items[blockIdx.y];
+    if (zune_fast(it.g)) color_ends(it.g, it.dst, it.pitch, blockIdx.x * 256 + threadIdx.x);
 }
 
 }  // namespace
@@ -704,6 +725,19 @@ hipError_t launch_jpeg_prog(const JpegScanArgs& a, hipStream_t s) {
                        sizeof(uint32_t) * (kRingDw + 1) * b.lanes, s, b);
     return hipGetLastError();
 }
+
+// the reconstruction of a batch's images, three launches for all of them (items:
+// device array of m; maxima over the images: blocks, width, height)
+hipError_t launch_jpeg_reconstruct_batch(const JpegReconItem* items, int m, long long max_blocks, int max_w, int max_h,
+                                         bool any_fast, hipStream_t s) {
+    if (m <= 0) return hipSuccess;
+    if (max_blocks <= 0 || max_w <= 0 || max_h <= 0 || m > 65535 || max_h > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_jpeg_idct_b, dim3((unsigned)((max_blocks + 255) / 256), m), dim3(256), 0, s, items);
+    hipLaunchKernelGGL(k_jpeg_color_b, dim3((max_w + 1023) / 1024, max_h, m), dim3(256), 0, s, items);
+    if (any_fast) hipLaunchKernelGGL(k_jpeg_color_ends_b, dim3((2 * max_h + 255) / 256, m), dim3(256), 0, s, items);
+    return hipGetLastError();
+}
+bool jpeg_zune_fast(const JpegGeom& g) { return zune_fast(g); }
 
 hipError_t launch_jpeg_reconstruct(const JpegGeom& g, uint8_t* dst, size_t dst_pitch, hipStream_t s) {
     if (g.nblocks <= 0 || g.W <= 0 || g.H <= 0) return hipErrorInvalidValue;

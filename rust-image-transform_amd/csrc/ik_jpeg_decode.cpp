@@ -24,6 +24,8 @@
 #include <vector>
 #include <array>
 #include <mutex>
+#include <condition_variable>
+#include <map>
 
 #include "../../include/imagekit_hip.h"
 #include "ik_runtime.h"
@@ -694,6 +696,136 @@ inline size_t up256(size_t x) { return (x + 255) / 256 * 256; }
 // process-wide: JPEG streams whose entropy decoding ran on the GPU / on the host
 std::atomic<unsigned long long> g_jpeg_gpu_streams{0}, g_jpeg_host_streams{0};
 
+}  // namespace
+
+// ---- the upload stage's JPEG areas (JpegUpload) ------------------------------------
+struct JpegArea {
+    int device = 0;
+    uint8_t* dev = nullptr;
+    size_t cap = 0;
+    uint8_t* pin = nullptr;  // staging for files the caller did not pin
+    size_t pin_cap = 0;
+    hipEvent_t ev = nullptr;
+    bool busy = false;
+};
+
+namespace {
+constexpr int kJpegAreas = 2;
+struct JpegAreaPool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<JpegArea*> areas;
+};
+std::mutex g_jarea_mu;
+std::map<int, JpegAreaPool*> g_jarea_pools;
+JpegAreaPool& jarea_pool(int device) {
+    std::lock_guard<std::mutex> lk(g_jarea_mu);
+    JpegAreaPool*& p = g_jarea_pools[device];
+    if (!p) p = new JpegAreaPool();
+    return *p;
+}
+// an idle area of the device (waits while the batches ahead hold both), as a
+// shared_ptr whose deleter hands it back
+std::shared_ptr<JpegArea> jarea_acquire(int device) {
+    JpegAreaPool& P = jarea_pool(device);
+    std::unique_lock<std::mutex> lk(P.mu);
+    JpegArea* got = nullptr;
+    while (!got) {
+        for (JpegArea* a : P.areas)
+            if (!a->busy) { got = a; break; }
+        if (!got && (int)P.areas.size() < kJpegAreas) {
+            got = new JpegArea();
+            got->device = device;
+            if (hipEventCreateWithFlags(&got->ev, hipEventDisableTiming) != hipSuccess) got->ev = nullptr;
+            P.areas.push_back(got);
+        }
+        if (!got) P.cv.wait(lk);
+    }
+    got->busy = true;
+    return std::shared_ptr<JpegArea>(got, [](JpegArea* a) {
+        JpegAreaPool& Q = jarea_pool(a->device);
+        {
+            std::lock_guard<std::mutex> l2(Q.mu);
+            a->busy = false;
+        }
+        Q.cv.notify_all();
+    });
+}
+}  // namespace
+
+int jpeg_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, JpegUpload& up) {
+    up = JpegUpload();
+    if (n <= 0) return IK_OK;
+    std::vector<size_t> off(n), soff(n, (size_t)-1);
+    size_t total = 0, stotal = 0;
+    for (int i = 0; i < n; ++i) {
+        off[i] = total;
+        total += up256(lens[i] + 64);
+        if (!host_pinned(bytes[i], lens[i])) { soff[i] = stotal; stotal += up256(lens[i]); }
+    }
+    std::shared_ptr<JpegArea> A = jarea_acquire(current_device());
+    if (!A->ev) return IK_OK;  // (no event: the kernel stage copies the scans itself)
+    // grow an idle area (nothing pending reads it: it was handed back after its batch's decode)
+    if (total > A->cap) {
+        if (A->dev) (void)hipFree(A->dev);
+        A->dev = nullptr;
+        A->cap = 0;
+        if (hipMalloc((void**)&A->dev, total + total / 8) != hipSuccess) { A->dev = nullptr; return IK_OK; }
+        A->cap = total + total / 8;
+    }
+    if (stotal > A->pin_cap) {
+        if (A->pin) (void)hipHostFree(A->pin);
+        A->pin = nullptr;
+        A->pin_cap = 0;
+        if (hipHostMalloc((void**)&A->pin, stotal + stotal / 8, hipHostMallocDefault) != hipSuccess) {
+            A->pin = nullptr;
+            return IK_OK;
+        }
+        A->pin_cap = stotal + stotal / 8;
+    }
+    if (stotal)
+        parallel_for(n, 0, [&](int i) {
+            if (soff[i] != (size_t)-1) std::memcpy(A->pin + soff[i], bytes[i], lens[i]);
+        });
+    hipStream_t s = thread_stream();
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < n && e == hipSuccess; ++i)
+        e = hipMemcpyAsync(A->dev + off[i], soff[i] == (size_t)-1 ? bytes[i] : A->pin + soff[i], lens[i],
+                           hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipEventRecord(A->ev, s);
+    if (e != hipSuccess) {  // the kernel stage copies the scans itself
+        (void)hipStreamSynchronize(s);
+        return IK_OK;
+    }
+    for (int i = 0; i < n; ++i) up.dev[bytes[i]] = A->dev + off[i];
+    up.n = n;
+    up.ev = A->ev;
+    up.area = std::move(A);
+    return IK_OK;
+}
+
+// ik_shutdown: the JPEG upload areas (no batch is in flight)
+void jpeg_shutdown() {
+    std::vector<JpegAreaPool*> ps;
+    {
+        std::lock_guard<std::mutex> lk(g_jarea_mu);
+        for (auto& kv : g_jarea_pools) ps.push_back(kv.second);
+    }
+    for (JpegAreaPool* P : ps) {
+        std::lock_guard<std::mutex> lk(P->mu);
+        for (JpegArea* a : P->areas) {
+            (void)hipSetDevice(a->device);
+            if (a->dev) (void)hipFree(a->dev);
+            if (a->pin) (void)hipHostFree(a->pin);
+            if (a->ev) (void)hipEventDestroy(a->ev);
+            delete a;
+        }
+        P->areas.clear();
+    }
+}
+
+namespace {
+
 #ifdef IK_JPEG_DUMP
 std::mutex g_jdump_mu;
 std::vector<std::array<std::vector<uint8_t>, 7>> g_jdump;  // per image of the last batch
@@ -712,7 +844,8 @@ std::vector<std::array<std::vector<uint8_t>, 7>> g_jdump;  // per image of the l
 // not match the frame, lanes that never synchronise, a bad code) goes to host_idx:
 // the host decoder decides and reports the reference's errors.
 static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::vector<int>& idx, ik_image** outs,
-                        std::vector<int>& st, std::vector<int>& host_idx) {
+                        std::vector<int>& st, std::vector<int>& host_idx, const uint8_t* const* files,
+                        const JpegUpload* up) {
     using namespace jsync;
     const int m = (int)idx.size();
     if (!m) return;
@@ -768,6 +901,7 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
     const size_t o_recs = take(sizeof(LaneRec) * (size_t)lanes_max);
     const size_t o_bases = take(sizeof(LaneBase) * (size_t)lanes_max);
     const size_t o_cs = take(jsync_chunk_scratch_bytes(lanes_max));
+    const size_t o_items = take(sizeof(JpegReconItem) * m);  // the reconstruction launches' image table
     for (int k = 0; k < m; ++k) {
         const Decoder& d = *ds[idx[k]];
         Lay& L = lay[k];
@@ -779,7 +913,8 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
     }
     hipStream_t s = thread_stream();
     uint8_t* dev = scratch_slot(1, o);
-    const size_t pin_bytes = std::max(small_end, std::max(small2_end - o_status, tab2_bytes)) + 256;
+    const size_t pin_bytes =
+        std::max(std::max(small_end, sizeof(JpegReconItem) * m), std::max(small2_end - o_status, tab2_bytes)) + 256;
     uint8_t* hp = dev ? pinned_slot(1, pin_bytes) : nullptr;
     auto fail_all = [&](const char* why) {
         (void)why;
@@ -813,15 +948,26 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
             qtables(d, reinterpret_cast<uint16_t*>(hp + lay[k].qt));
         });
     }
-    // the scan bytes: in place from page-locked memory, else through pinned staging
+    // the scan bytes: where the upload stage put them (JpegUpload), else DMAed in
+    // place from page-locked memory, else through pinned staging
     std::vector<char> in_place(m, 0);
     std::vector<size_t> st_off(m, 0);
+    std::vector<const uint8_t*> on_dev(m, nullptr);
     size_t st_total = 0;
     for (int k = 0; k < m; ++k) {
         const Decoder& d = *ds[idx[k]];
+        if (up && up->n) {
+            auto it = up->dev.find(files[idx[k]]);
+            if (it != up->dev.end()) {
+                on_dev[k] = it->second + (d.js_data - files[idx[k]]);
+                continue;
+            }
+        }
         in_place[k] = host_pinned(d.js_data, d.js_len) ? 1 : 0;
         if (!in_place[k]) { st_off[k] = st_total; st_total += up256(d.js_len); }
     }
+    for (int k = 0; k < m; ++k)
+        if (on_dev[k]) reinterpret_cast<JsImageDev*>(hp + o_img)[k].scan = on_dev[k];
     uint8_t* hdata = st_total ? pinned_slot(2, st_total) : nullptr;
     if (st_total && !hdata) { fail_all("memory"); return; }
     if (st_total)
@@ -831,9 +977,11 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
     hipError_t e = hipMemcpyAsync(dev, hp, small_end, hipMemcpyHostToDevice, s);
     for (int k = 0; k < m && e == hipSuccess; ++k) {
         const Decoder& d = *ds[idx[k]];
+        if (on_dev[k]) continue;
         e = hipMemcpyAsync(dev + lay[k].scan, in_place[k] ? d.js_data : hdata + st_off[k], d.js_len,
                            hipMemcpyHostToDevice, s);
     }
+    if (e == hipSuccess && up && up->n && up->ev) e = hipStreamWaitEvent(s, up->ev, 0);
     if (e == hipSuccess) e = hipMemsetAsync(dev + o_status, 0, small2_end - o_status, s);
     // ---- 2. unstuffing; the interval tables back ----
     if (e == hipSuccess)
@@ -957,24 +1105,37 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
         batch_timing_add(d, kBtJpegImages, (double)(lanes_used ? std::count(ok.begin(), ok.end(), 1) : 0));
         batch_timing_add(d, kBtJpegLanes, (double)lanes_used);
     }
-    // ---- 5. reconstruction ----
-    for (int k = 0; k < m; ++k) {
-        if (!ok[k]) continue;
-        const int i = idx[k];
-        if (hstatus[k]) { host_idx.push_back(i); continue; }
-        const Decoder& d = *ds[i];
-        JpegGeom g = lay[k].g;
-        g.qt = reinterpret_cast<const uint16_t*>(dev + lay[k].qt);
-        g.coef = reinterpret_cast<const int16_t*>(dev + lay[k].coef);
-        g.planes = dev + lay[k].pl;
-        ik_image* img = nullptr;
-        st[i] = alloc_image((uint32_t)d.width, (uint32_t)d.height, d.comps.size() == 1 ? 1u : 3u, &img);
-        if (st[i]) continue;
-        e = launch_jpeg_reconstruct(g, img->d, img->pitch, s);
-        if (e != hipSuccess) { ik_image_free(img); st[i] = hip_fail(e, "jpeg reconstruct"); continue; }
-        outs[i] = img;
+    // ---- 5. reconstruction: every image in three launches ----
+    {
+        JpegReconItem* items = reinterpret_cast<JpegReconItem*>(hp);
+        int mi = 0, max_w = 0, max_h = 0;
+        long long max_blocks = 0;
+        bool any_fast = false;
+        for (int k = 0; k < m; ++k) {
+            if (!ok[k]) continue;
+            const int i = idx[k];
+            if (hstatus[k]) { host_idx.push_back(i); continue; }
+            const Decoder& d = *ds[i];
+            JpegGeom g = lay[k].g;
+            g.qt = reinterpret_cast<const uint16_t*>(dev + lay[k].qt);
+            g.coef = reinterpret_cast<const int16_t*>(dev + lay[k].coef);
+            g.planes = dev + lay[k].pl;
+            ik_image* img = nullptr;
+            st[i] = alloc_image((uint32_t)d.width, (uint32_t)d.height, d.comps.size() == 1 ? 1u : 3u, &img);
+            if (st[i]) continue;
+            outs[i] = img;
+            items[mi++] = JpegReconItem{g, img->d, img->pitch};
+            max_blocks = std::max(max_blocks, g.nblocks);
+            max_w = std::max(max_w, g.W);
+            max_h = std::max(max_h, g.H);
+            any_fast = any_fast || jpeg_zune_fast(g);
+        }
+        const JpegReconItem* d_items = reinterpret_cast<const JpegReconItem*>(dev + o_items);
+        e = mi ? hipMemcpyAsync(dev + o_items, hp, sizeof(JpegReconItem) * mi, hipMemcpyHostToDevice, s) : hipSuccess;
+        if (e == hipSuccess) e = launch_jpeg_reconstruct_batch(d_items, mi, max_blocks, max_w, max_h, any_fast, s);
+        if (e != hipSuccess) (void)hip_fail(e, "jpeg reconstruct");
     }
-    e = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
     for (int k = 0; k < m; ++k) {
         const int i = idx[k];
         if (!ok[k] || hstatus[k] || !outs[i]) continue;
@@ -995,7 +1156,7 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
 
 }  // namespace
 int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_image** outs, int* status,
-                      std::string* msgs);
+                      std::string* msgs, const JpegUpload* up);
 namespace {
 
 // try_gpu: baseline scans go through the self-synchronising GPU decoder (the batch
@@ -1016,7 +1177,7 @@ int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gp
     if (d.js) {
         int status = IK_OK;
         std::string msg;
-        st = decode_jpeg_batch(&bytes, &n, 1, out, &status, &msg);
+        st = decode_jpeg_batch(&bytes, &n, 1, out, &status, &msg, nullptr);
         if (st && !msg.empty()) return fail(st, "%s", msg.c_str());
         return st;
     }
@@ -1109,7 +1270,7 @@ int decode_jpeg_impl(const uint8_t* bytes, size_t n, ik_image** out, bool try_gp
 }  // namespace
 
 int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik_image** outs, int* status,
-                      std::string* msgs) {
+                      std::string* msgs, const JpegUpload* up) {
     // 1. parse every stream (host threads); baseline scans are deferred to the GPU
     std::vector<std::unique_ptr<Decoder>> ds(n);
     std::vector<int> st(n, IK_OK);
@@ -1137,7 +1298,7 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
         else host_idx.push_back(i);
     }
     // 2. the baseline scans: the self-synchronising GPU decoder over all of them at once
-    jsync_batch(ds, js_idx, outs, st, host_idx);
+    jsync_batch(ds, js_idx, outs, st, host_idx, bytes, up);
     // 3. everything else: progressive scans with restart intervals on the GPU image by
     // image, the rest (and anything the GPU found inconsistent) with host entropy decoding
     const int nh = (int)host_idx.size();

@@ -10,6 +10,7 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include <unordered_map>
 
 #include "ik_internal.h"
 
@@ -248,10 +249,28 @@ int decode_webp(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& 
 // JPEG: host entropy decode + GPU reconstruction straight into a new device image
 // (ik_jpeg_decode.cpp + ik_jpeg.hip)
 int decode_jpeg_device(const uint8_t* b, size_t n, ik_image** out);
-// n streams at once: restart-interval baseline scans entropy-decoded in one GPU
-// launch; per-stream status (outs[i] null on failure); returns the first failure
+// A batch's JPEG files DMAed to the device by the upload stage (ik_host.cpp
+// StageExec), so that the kernel stage's self-synchronising decoder reads their
+// scans where they lie instead of copying them in its own time.  The files of the
+// batch in one device area (two per device, as the PNG upload areas), DMAed in
+// place when the caller pinned them, else through pinned staging; `ev` marks the
+// DMAs' end on the upload thread's stream.  Dropping the JpegUpload (after the
+// batch's decode returned) frees the area for the next batch.
+struct JpegArea;
+struct JpegUpload {
+    int n = 0;
+    std::unordered_map<const uint8_t*, const uint8_t*> dev;  // host file -> its device copy
+    hipEvent_t ev = nullptr;
+    std::shared_ptr<JpegArea> area;
+};
+int jpeg_upload_begin(const uint8_t* const* b, const size_t* lens, int n, JpegUpload& up);
+void jpeg_shutdown();  // ik_shutdown: the JPEG upload areas
+// n streams at once: baseline scans entropy-decoded together by the self-
+// synchronising GPU decoder; per-stream status (outs[i] null on failure); returns
+// the first failure.  up: the files' device copies (jpeg_upload_begin), or null
 int decode_jpeg_batch(const uint8_t* const* b, const size_t* lens, int n, ik_image** outs, int* status,
-                      std::string* msgs /* [n] or null: per-stream error message */);
+                      std::string* msgs /* [n] or null: per-stream error message */,
+                      const JpegUpload* up = nullptr);
 
 // device-side stage helpers used by ik_encode and the pipeline
 int encode_device_image(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, size_t pitch,
