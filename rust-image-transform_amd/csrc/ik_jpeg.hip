@@ -438,9 +438,11 @@ __device__ __forceinline__ void color_group(const JpegGeom& g, uint8_t* __restri
 __global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restrict__ dst, size_t pitch) {
     color_group(g, dst, pitch, 4 * (blockIdx.x * 256 + threadIdx.x), blockIdx.y);
 }
-// the batch's images in one launch: blockIdx.z = image
+// the batch's images in one launch: blockIdx.z = image.  (The kernel takes its
+// image's table entry by value: its fields load together, up front, instead of one
+// dependent scalar load per test of zune_fast.)
 __global__ __launch_bounds__(256) void k_jpeg_color_b(const JpegReconItem* items) {
-    const JpegReconItem& it = items[blockIdx.z];
+    const JpegReconItem it = items[blockIdx.z];
     color_group(it.g, it.dst, it.pitch, 4 * (blockIdx.x * 256 + threadIdx.x), blockIdx.y);
 }
 
@@ -469,7 +471,7 @@ __global__ __launch_bounds__(256) void k_jpeg_color_ends(JpegGeom g, uint8_t* __
 }
 // the batch's zune_fast images in one launch: blockIdx.y = image (the others return)
 __global__ __launch_bounds__(256) void k_jpeg_color_ends_b(const JpegReconItem* items) {
-    const JpegReconItem& it = items[blockIdx.y];
+    const JpegReconItem it = items[blockIdx.y];
     if (zune_fast(it.g)) color_ends(it.g, it.dst, it.pitch, blockIdx.x * 256 + threadIdx.x);
 }
 

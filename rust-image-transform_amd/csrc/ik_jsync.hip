@@ -501,7 +501,10 @@ __global__ __launch_bounds__(kLanesPerWG) void k_jsync_decode(const Scan* scans,
         }
         pred[c] += diff;
         blk[0] = (int16_t)pred[c];
-        s8* gb = reinterpret_cast<s8*>(S.coef + block_index(S, B.block + i) * 64);
+        // (a global-address-space store: a flat store would also count in lgkmcnt, and
+        // every LDS table read of the next block would wait for it)
+        typedef __attribute__((address_space(1))) s8 gs8;
+        gs8* gb = (gs8*)(S.coef + block_index(S, B.block + i) * 64);
 #pragma unroll
         for (int p = 0; p < 8; ++p) {
             gb[p] = reinterpret_cast<const __attribute__((address_space(3))) s8*>(blk)[p];

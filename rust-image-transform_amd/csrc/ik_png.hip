@@ -973,11 +973,13 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngI
 // are one dword per lane and step (each lane walks its own row; out-of-range
 // offsets are dropped by the buffer descriptor, so every instruction is issued by
 // the whole wave and the compiler's wait counts hold); a group's G pixels are
-// prefetched a group ahead.  Hand-off: the band's last row stores sc1, and at the
-// end of each group the band publishes the previous group's pixels -- by then at
-// least G newer memory operations have been issued, so vmcnt(G) covers that
-// group's stores without draining this one's; the next band's lane 0 polls the
-// counter a group ahead of its need and loads the row above's pixels sc1.
+// prefetched a group ahead.  Hand-off: the band's last row stores sc1 (the other
+// rows plain: sc1 stores of 4 bytes each, written through one by one, made the
+// kernel 4x slower than the chunked one), and at the end of each group the band
+// publishes the previous group's pixels -- by then at least G newer memory
+// operations have been issued, so vmcnt(G) covers that group's stores without
+// draining this one's; the next band's lane 0 reads the counter a group ahead of
+// its need and loads the row above's pixels sc1.
 template <int G>
 __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter_px4(const PngImgDev* imgs, const int2* groups,
                                                                           const int* prog_base, unsigned* prog,
@@ -1064,8 +1066,12 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter_px4(const 
                 const bool act = live && x >= 0 && x < W;
                 up = nup;
                 if (act) cur = v;
-                __builtin_amdgcn_raw_buffer_store_b32(cur, rs, (int)(act ? rowoff + 4u * (uint32_t)x : kOut), 0,
-                                                      kCpolSc1);
+                // rows 0..62 of the band plain (a line fills in L2 over 32 steps); the
+                // band's last row, which the band below reads, sc1 (written through) --
+                // two instructions, each lane's offset out of range in the other
+                const uint32_t off = act ? rowoff + 4u * (uint32_t)x : kOut;
+                __builtin_amdgcn_raw_buffer_store_b32(cur, rs, (int)(lane == 63 ? kOut : off), 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(cur, rs, (int)(lane == 63 ? off : kOut), 0, kCpolSc1);
             }
             // publish the previous group's pixels of the band's last row: this group's
             // G stores were issued after them
