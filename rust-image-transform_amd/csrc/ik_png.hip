@@ -962,144 +962,6 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngI
 #endif
 }
 
-// Pixel-granular wavefront for 4-byte pixels (RGBA8, LA16; the headline's frames):
-// lane = row as above, but lane l unfilters PIXEL s - l at step s, so a band of 64
-// rows trails the band above by 64 steps of one pixel instead of 64 steps of a
-// 16-byte chunk.  The frame's chain is H + W pixel steps (+ the hand-off's lag per
-// band) instead of H + W/4 chunk steps of four pixels each: 5,700 chunk steps =
-// ~23,000 pixel-equivalents per 4096^2 frame before, ~10,000 now.  The row
-// above's pixel comes from lane l-1's previous step (DPP shift), the up-left from
-// this lane's previous step, the left from its own last result.  Loads and stores
-// are one dword per lane and step (each lane walks its own row; out-of-range
-// offsets are dropped by the buffer descriptor, so every instruction is issued by
-// the whole wave and the compiler's wait counts hold); a group's G pixels are
-// prefetched a group ahead.  Hand-off: the band's last row stores sc1 (the other
-// rows plain: sc1 stores of 4 bytes each, written through one by one, made the
-// kernel 4x slower than the chunked one), and at the end of each group the band
-// publishes the previous group's pixels -- by then at least G newer memory
-// operations have been issued, so vmcnt(G) covers that group's stores without
-// draining this one's; the next band's lane 0 reads the counter a group ahead of
-// its need and loads the row above's pixels sc1.
-template <int G>
-__global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter_px4(const PngImgDev* imgs, const int2* groups,
-                                                                          const int* prog_base, unsigned* prog,
-                                                                          unsigned* ticket) {
-    raise_priority();
-    constexpr int NW = kPngUnfilterThreads / 64;
-    __shared__ int s_t;
-    if (threadIdx.x == 0) s_t = (int)atomicAdd(ticket, 1u);
-    __syncthreads();
-    const int2 gk = groups[s_t];  // (image, workgroup of the image)
-    const PngImgDev I = imgs[gk.x];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int W = I.rowbytes >> 2;  // pixels per row
-    const int nbands = (I.H + 63) >> 6;
-    const int K = png_unfilter_groups(I.H);
-    unsigned* pg = prog + prog_base[gk.x];
-    const uint64_t dbase = uniform_u64((uint64_t)(size_t)I.dst);
-    const size_t ibytes = I.pitch * (size_t)I.H;
-    // (every field wave-uniform in SGPRs: a descriptor in VGPRs makes each buffer
-    // access a readfirstlane loop)
-    const int nrec = __builtin_amdgcn_readfirstlane((int)(ibytes < 0x7fffffffu ? ibytes : 0x7fffffffu));
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)dbase, (short)0, nrec, 0x00020000);
-    const int ngrp = (W + 63 + G - 1) / G;
-    constexpr uint32_t kOut = 0x80000000u;  // an out-of-range offset: loads read 0, stores are dropped
-    for (int band = wave * K + gk.y; band < nbands; band += NW * K) {
-        const int y = band * 64 + lane;
-        const bool live = y < I.H;
-        const FtMask fm(live ? I.ft[y] : 0u);
-        const bool above = band > 0;                       // (wave-uniform)
-        const bool publish = band * 64 + 63 < I.H;         // a band below waits on this one (wave-uniform)
-        const uint32_t rowoff = (uint32_t)((size_t)(live ? y : 0) * I.pitch);
-        const uint32_t aoff = lane == 0 ? (uint32_t)((size_t)(above ? band * 64 - 1 : 0) * I.pitch) : kOut;
-        unsigned seen = 0;  // the band above's progress last read
-        // the band above's counter, read a group ahead: its value is used a group
-        // after the load went out, so the wait for it does not wait for the group's
-        // stores behind it; only when that value is short does the band poll (and
-        // then it waits for the band above anyway)
-        unsigned flag = above ? __hip_atomic_load(pg + band - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-        uint32_t cur = 0, up = 0;
-        auto fetch = [&](int s0, uint32_t (&r)[G]) {
-#pragma unroll
-            for (int t = 0; t < G; ++t) {
-                const int x = s0 + t - lane;
-                const uint32_t off = live && x >= 0 && x < W ? rowoff + 4u * (uint32_t)x : kOut;
-                r[t] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0);
-            }
-        };
-        // lane 0's row above for the steps from s0 (pixel x = s0 + t), once the band
-        // above has published them (wave-uniform: band > 0 only)
-        auto fetch_above = [&](int s0, uint32_t (&a)[G]) {
-            const unsigned need = (unsigned)min(s0 + G, W);
-            if (seen < need) seen = (unsigned)__builtin_amdgcn_readfirstlane((int)flag);
-            while (seen < need) {
-                __builtin_amdgcn_s_sleep(1);
-                const unsigned v = __hip_atomic_load(pg + band - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                seen = (unsigned)__builtin_amdgcn_readfirstlane((int)v);
-            }
-#pragma unroll
-            for (int t = 0; t < G; ++t) {
-                const int x = s0 + t;
-                a[t] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(x < W ? aoff + 4u * (uint32_t)x : kOut), 0,
-                                                            kCpolSc1);
-            }
-            flag = __hip_atomic_load(pg + band - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        };
-        auto group = [&](int g, const uint32_t (&rc)[G], const uint32_t (&ac)[G], uint32_t (&rn)[G],
-                         uint32_t (&an)[G]) {
-            const int s0 = g * G;
-            if (g + 1 < ngrp) {
-                fetch(s0 + G, rn);
-                if (above && s0 + G < W) fetch_above(s0 + G, an);
-                else {
-#pragma unroll
-                    for (int t = 0; t < G; ++t) an[t] = 0;
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < G; ++t) {
-                const int x = s0 + t - lane;
-                const uint32_t nup = wave_shr1(cur, ac[t]);  // the row above's pixel x (lane 0: from memory)
-                const bool first = x == 0;
-                const uint32_t v = unfilter_word(rc[t], first ? 0u : cur, nup, first ? 0u : up, fm.sub, fm.up, fm.avg,
-                                                 fm.paeth);
-                const bool act = live && x >= 0 && x < W;
-                up = nup;
-                if (act) cur = v;
-                // rows 0..62 of the band plain (a line fills in L2 over 32 steps); the
-                // band's last row, which the band below reads, sc1 (written through) --
-                // two instructions, each lane's offset out of range in the other
-                const uint32_t off = act ? rowoff + 4u * (uint32_t)x : kOut;
-                __builtin_amdgcn_raw_buffer_store_b32(cur, rs, (int)(lane == 63 ? kOut : off), 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(cur, rs, (int)(lane == 63 ? off : kOut), 0, kCpolSc1);
-            }
-            // publish the previous group's pixels of the band's last row: this group's
-            // G stores were issued after them
-            if (publish && g >= 1) {
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-                const int done = s0 - 63;  // pixels 0 .. s0 - 64 of lane 63's row
-                if (lane == 63 && done > 0)
-                    __hip_atomic_store(pg + band, (unsigned)min(done, W), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        };
-        uint32_t ra[G], rb[G], aa[G], ab[G];
-        fetch(0, ra);
-        if (above) fetch_above(0, aa);
-        else {
-#pragma unroll
-            for (int t = 0; t < G; ++t) aa[t] = 0;
-        }
-        for (int g = 0; g < ngrp; g += 2) {
-            group(g, ra, aa, rb, ab);
-            if (g + 1 < ngrp) group(g + 1, rb, ab, ra, aa);
-        }
-        if (publish) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 63) __hip_atomic_store(pg + band, (unsigned)W, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
 // ---- small transfers through the compute queue ---------------------------------------
 __global__ __launch_bounds__(256) void k_copy_words(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                                     size_t n) {
@@ -1440,7 +1302,7 @@ hipError_t launch_png_unfilter(const PngImgDev* imgs, const int2* groups, int ng
     case 1: IK_UNF(1, false); break;
     case 2: IK_UNF(2, false); break;
     case 3: IK_UNF(3, false); break;
-    case 4: hipLaunchKernelGGL((k_png_unfilter_px4<8>), grid, block, 0, s, imgs, groups, prog_base, prog, ticket); break;
+    case 4: IK_UNF(4, true); break;
     case 6: IK_UNF(6, false); break;
     case 8: IK_UNF(8, true); break;
     default: return hipErrorInvalidValue;

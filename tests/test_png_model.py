@@ -164,55 +164,3 @@ def test_block_search_kraft_sum_equals_definition():
     L.ikm_cl_kraft_check.argtypes = [ctypes.c_long]
     assert L.ikm_cl_kraft_check(200000) == 0
 
-
-def _paeth(a, b, c):
-    p = a + b - c
-    pa, pb, pc = abs(p - a), abs(p - b), abs(p - c)
-    return a if pa <= pb and pa <= pc else (b if pb <= pc else c)
-
-
-def test_unfilter_pixel_wavefront_schedule():
-    """k_png_unfilter_px4's schedule, restated step by step: lane l of a 64-row band
-    unfilters pixel s - l at step s; the row above comes from lane l-1's result of the
-    previous step (the DPP shift; lane 0: the previous band's last row), the up-left
-    from this lane's previous step, the left from its own last result, both zero at
-    x = 0.  The result equals png's row-by-row definition for every filter type."""
-    rng = np.random.default_rng(7)
-    H, W = 70, 9  # rows, 4-byte pixels (two bands, the second partial)
-    raw = rng.integers(0, 256, (H, 4 * W))
-    ft = rng.integers(0, 5, H)
-
-    def unf(r, a, b, c, f):
-        out = []
-        for k in range(len(r)):
-            pred = [0, a[k], b[k], (a[k] + b[k]) >> 1, _paeth(a[k], b[k], c[k])][f]
-            out.append((int(r[k]) + pred) & 255)
-        return out
-
-    ref = np.zeros((H, 4 * W), np.int64)
-    for y in range(H):
-        for i in range(4 * W):
-            a = ref[y, i - 4] if i >= 4 else 0
-            b = ref[y - 1, i] if y else 0
-            c = ref[y - 1, i - 4] if y and i >= 4 else 0
-            ref[y, i] = unf([raw[y, i]], [a], [b], [c], ft[y])[0]
-    dst = np.zeros_like(ref)
-    z = [0, 0, 0, 0]
-    for band in range((H + 63) // 64):
-        cur, up = [z] * 64, [z] * 64
-        for s in range(W + 63):
-            prev = list(cur)
-            for lane in range(64):
-                y, x = band * 64 + lane, s - lane
-                if lane == 0:
-                    nup = list(dst[band * 64 - 1, 4 * s:4 * s + 4]) if band and s < W else z
-                else:
-                    nup = prev[lane - 1]
-                act = y < H and 0 <= x < W
-                if act:
-                    v = unf(raw[y, 4 * x:4 * x + 4], z if x == 0 else cur[lane], nup, z if x == 0 else up[lane], ft[y])
-                up[lane] = nup
-                if act:
-                    cur[lane] = v
-                    dst[y, 4 * x:4 * x + 4] = v
-    assert np.array_equal(dst, ref)
