@@ -227,10 +227,10 @@ struct PngUpload {
     // bytes; the upload then walks the chunks on the GPU and gathers from there
     bool dev = false;
     const uint8_t* const* heads = nullptr;
-    // called by png_decode_finish once the batch's decode rounds are done (or, with
-    // IK_FIND_AFTER=resolve, once its resolve pass is queued, with an event
-    // recorded after it; null = none): the stage executor launches the next
-    // batch's block search there, beside this batch's remaining kernels
+    // called by png_decode_finish once the batch's decode rounds are done (argument:
+    // an event to wait for first, or null): the stage executor launches the next
+    // batch's block search there, on the kernel stream before this batch's expand
+    // (beside the unfilter instead it doubled the unfilter: profiles/r04k_*)
     std::function<void(hipEvent_t)> on_next_search;
 };
 int png_upload_begin(const uint8_t* const* b, const size_t* lens, int n, PngUpload& up);
