@@ -1364,10 +1364,16 @@ static void transform_device_phase(const uint8_t* const* bytes, const size_t* le
     static const bool timing = getenv("IK_TIMING") != nullptr;  // dev: per-stage sums to stderr
     // GPU phases under the device's kernel gate (held from the decode kernels
     // through resize and the encoders' device front ends), the host coders after
+    const auto tg0 = std::chrono::steady_clock::now();
     gate_pin(kGateKernels, true);
+    const auto tg1 = std::chrono::steady_clock::now();
     batch_timing_reset(current_device());
     decode_batch_dev(b.data(), l.data(), m, imgs.data(), nullptr, ds.data(), dm.data(), threads, up,
                      sniff ? sn.data() : nullptr, jup);
+    if (timing)
+        fprintf(stderr, "[device_phase] gate wait %.2f ms, decode %.2f ms\n",
+                std::chrono::duration<double, std::milli>(tg1 - tg0).count(),
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tg1).count());
     gate_enter(kGateKernels);
     std::mutex tmu;
     double& t_resize = hp.t_resize;

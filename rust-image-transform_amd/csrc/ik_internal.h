@@ -127,6 +127,8 @@ struct JpegReconItem {
     JpegGeom g;
     uint8_t* dst;
     size_t pitch;
+    int fast;  // jpeg_zune_fast(g)
+    int pad;
 };
 hipError_t launch_jpeg_reconstruct_batch(const JpegReconItem* items, int m, long long max_blocks, int max_w, int max_h,
                                          bool any_fast, hipStream_t s);

@@ -200,7 +200,7 @@ __device__ __forceinline__ void idct_block(const JpegGeom& g, long long blk) {
 
 __global__ __launch_bounds__(256) void k_jpeg_idct(JpegGeom g) { idct_block(g, (long long)blockIdx.x * 256 + threadIdx.x); }
 // the batch's images in one launch: blockIdx.y = image
-__global__ __launch_bounds__(256) void k_jpeg_idct_b(const JpegReconItem* items) {
+__global__ __launch_bounds__(256) void k_jpeg_idct_b(const JpegReconItem* __restrict__ items) {
     idct_block(items[blockIdx.y].g, (long long)blockIdx.x * 256 + threadIdx.x);
 }
 
@@ -399,11 +399,12 @@ __device__ __forceinline__ void color1_zune(const JpegGeom& g, int x, int y, uin
     o[2] = clamp255(b);
 }
 
-__device__ __forceinline__ void color_group(const JpegGeom& g, uint8_t* __restrict__ dst, size_t pitch, int x0, int y) {
+__device__ __forceinline__ void color_group(const JpegGeom& g, uint8_t* __restrict__ dst, size_t pitch, int x0, int y,
+                                            bool fast) {
     if (x0 >= g.W || y >= g.H) return;
     const int C = g.colorspace == 0 ? 1 : 3;
     uint8_t px[12];
-    if (zune_fast(g) && x0 >= 4 && x0 + 4 <= g.W && x0 + 3 < 2 * g.bw[1] * 8 - 2) {
+    if (fast && x0 >= 4 && x0 + 4 <= g.W && x0 + 3 < 2 * g.bw[1] * 8 - 2) {
         color4_zune(g, x0, y, px);
         uint32_t w[3];
 #pragma unroll
@@ -416,7 +417,7 @@ __device__ __forceinline__ void color_group(const JpegGeom& g, uint8_t* __restri
         o32[2] = w[2];
         return;
     }
-    if (zune_fast(g)) return;  // a row end: k_jpeg_color_ends
+    if (fast) return;  // a row end: k_jpeg_color_ends
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         if (x0 + k < g.W) color_pixel(g, x0 + k, y, px + C * k);
@@ -436,14 +437,20 @@ __device__ __forceinline__ void color_group(const JpegGeom& g, uint8_t* __restri
 }
 
 __global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restrict__ dst, size_t pitch) {
-    color_group(g, dst, pitch, 4 * (blockIdx.x * 256 + threadIdx.x), blockIdx.y);
+    color_group(g, dst, pitch, 4 * (blockIdx.x * 256 + threadIdx.x), blockIdx.y, zune_fast(g));
 }
-// the batch's images in one launch: blockIdx.z = image.  (The kernel takes its
-// image's table entry by value: its fields load together, up front, instead of one
-// dependent scalar load per test of zune_fast.)
-__global__ __launch_bounds__(256) void k_jpeg_color_b(const JpegReconItem* items) {
-    const JpegReconItem it = items[blockIdx.z];
-    color_group(it.g, it.dst, it.pitch, 4 * (blockIdx.x * 256 + threadIdx.x), blockIdx.y);
+// the batch's images in one launch: blockIdx.z = image.  (zune_fast comes from the
+// host with the entry: tested here field by field it is a chain of dependent
+// scalar loads per workgroup; the whole entry copied to registers instead costs
+// ~100 SGPRs and half the waves)
+// A workgroup takes kColorRows rows, so that each entry's fields are loaded once per
+// eight rows of work, not once per row.
+constexpr int kColorRows = 8;
+__global__ __launch_bounds__(256) void k_jpeg_color_b(const JpegReconItem* __restrict__ items) {
+    const JpegReconItem& it = items[blockIdx.z];  // (restrict: its loads hoist past the row stores)
+    const bool fast = it.fast != 0;
+    const int x0 = 4 * (blockIdx.x * 256 + threadIdx.x);
+    for (int r = 0; r < kColorRows; ++r) color_group(it.g, it.dst, it.pitch, x0, blockIdx.y * kColorRows + r, fast);
 }
 
 // The row ends of a zune_fast image (the groups of four k_jpeg_color leaves:
@@ -470,9 +477,9 @@ __global__ __launch_bounds__(256) void k_jpeg_color_ends(JpegGeom g, uint8_t* __
     color_ends(g, dst, pitch, blockIdx.x * 256 + threadIdx.x);
 }
 // the batch's zune_fast images in one launch: blockIdx.y = image (the others return)
-__global__ __launch_bounds__(256) void k_jpeg_color_ends_b(const JpegReconItem* items) {
-    const JpegReconItem it = items[blockIdx.y];
-    if (zune_fast(it.g)) color_ends(it.g, it.dst, it.pitch, blockIdx.x * 256 + threadIdx.x);
+__global__ __launch_bounds__(256) void k_jpeg_color_ends_b(const JpegReconItem* __restrict__ items) {
+    const JpegReconItem& it = items[blockIdx.y];
+    if (it.fast) color_ends(it.g, it.dst, it.pitch, blockIdx.x * 256 + threadIdx.x);
 }
 
 }  // namespace
@@ -735,7 +742,8 @@ hipError_t launch_jpeg_reconstruct_batch(const JpegReconItem* items, int m, long
     if (m <= 0) return hipSuccess;
     if (max_blocks <= 0 || max_w <= 0 || max_h <= 0 || m > 65535 || max_h > 65535) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_jpeg_idct_b, dim3((unsigned)((max_blocks + 255) / 256), m), dim3(256), 0, s, items);
-    hipLaunchKernelGGL(k_jpeg_color_b, dim3((max_w + 1023) / 1024, max_h, m), dim3(256), 0, s, items);
+    hipLaunchKernelGGL(k_jpeg_color_b, dim3((max_w + 1023) / 1024, (max_h + kColorRows - 1) / kColorRows, m), dim3(256),
+                       0, s, items);
     if (any_fast) hipLaunchKernelGGL(k_jpeg_color_ends_b, dim3((2 * max_h + 255) / 256, m), dim3(256), 0, s, items);
     return hipGetLastError();
 }

@@ -28,6 +28,7 @@
 #include <map>
 
 #include "../../include/imagekit_hip.h"
+#include "ik_png.h"
 #include "ik_runtime.h"
 
 namespace ik {
@@ -793,6 +794,11 @@ int jpeg_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Jp
         e = hipMemcpyAsync(A->dev + off[i], soff[i] == (size_t)-1 ? bytes[i] : A->pin + soff[i], lens[i],
                            hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipEventRecord(A->ev, s);
+    static const bool timing = getenv("IK_TIMING") != nullptr;
+    if (timing)
+        fprintf(stderr, "[jpeg-upload] %d files, %.1f MB (%.1f MB staged) queued at t=%.1f ms\n", n, total / 1e6, stotal / 1e6,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count() -
+                    1e3 * (double)(long long)(std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() / 1000) * 1000);
     if (e != hipSuccess) {  // the kernel stage copies the scans itself
         (void)hipStreamSynchronize(s);
         return IK_OK;
@@ -913,15 +919,35 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
     }
     hipStream_t s = thread_stream();
     uint8_t* dev = scratch_slot(1, o);
-    const size_t pin_bytes =
-        std::max(std::max(small_end, sizeof(JpegReconItem) * m), std::max(small2_end - o_status, tab2_bytes)) + 256;
+    const size_t pin_bytes = std::max(std::max(small_end, sizeof(JpegReconItem) * m + 256),
+                                      std::max(small2_end - o_status, tab2_bytes)) + up256(sizeof(int) * m) + 256;
     uint8_t* hp = dev ? pinned_slot(1, pin_bytes) : nullptr;
     auto fail_all = [&](const char* why) {
         (void)why;
         for (int k = 0; k < m; ++k) host_idx.push_back(idx[k]);
     };
     if (!dev || !hp) { fail_all("memory"); return; }
+    const double tm_layout = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     (void)hipStreamSynchronize(s);  // the pinned block is free
+    // Small transfers between hp and the device go through a copy kernel on this
+    // stream that reads or writes the pinned block directly (ik_png_decode.cpp Xfer):
+    // SDMA copies queue behind the next batch's scan upload on the same engine --
+    // ~12 ms per transfer with configs[2]'s 683 MB batches in flight.
+    uint8_t* hp_dev = nullptr;
+    if (hipHostGetDevicePointer((void**)&hp_dev, hp, 0) != hipSuccess) hp_dev = nullptr;
+    auto h2d = [&](uint8_t* d, size_t off, size_t n) -> hipError_t {  // hp[off, off + n) -> d
+        if (!n) return hipSuccess;
+        if (!hp_dev) return hipMemcpyAsync(d, hp + off, n, hipMemcpyHostToDevice, s);
+        return launch_copy_words(reinterpret_cast<const uint32_t*>(hp_dev + off), reinterpret_cast<uint32_t*>(d),
+                                 (n + 3) / 4, s);
+    };
+    auto d2h = [&](size_t off, const uint8_t* d, size_t n) -> hipError_t {  // d -> hp[off, off + n)
+        if (!n) return hipSuccess;
+        if (!hp_dev) return hipMemcpyAsync(hp + off, d, n, hipMemcpyDeviceToHost, s);
+        return launch_copy_words(reinterpret_cast<const uint32_t*>(d), reinterpret_cast<uint32_t*>(hp_dev + off),
+                                 (n + 3) / 4, s);
+    };
+    const double tm_sync = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     // ---- 1. upload ----
     {
         JsImageDev* I = reinterpret_cast<JsImageDev*>(hp + o_img);
@@ -974,7 +1000,14 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
         parallel_for(m, 0, [&](int k) {
             if (!in_place[k]) std::memcpy(hdata + st_off[k], ds[idx[k]]->js_data, ds[idx[k]]->js_len);
         });
-    hipError_t e = hipMemcpyAsync(dev, hp, small_end, hipMemcpyHostToDevice, s);
+    const double tm_tables = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    double tm_upwait = -1;  // (IK_TIMING: how long the upload stage's DMA still had to run)
+    if (timing && up && up->n && up->ev) {
+        const auto tw = std::chrono::steady_clock::now();
+        if (hipEventQuery(up->ev) != hipSuccess) (void)hipEventSynchronize(up->ev);
+        tm_upwait = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count();
+    }
+    hipError_t e = h2d(dev, 0, small_end);
     for (int k = 0; k < m && e == hipSuccess; ++k) {
         const Decoder& d = *ds[idx[k]];
         if (on_dev[k]) continue;
@@ -988,7 +1021,7 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
         e = launch_jsync_unstuff(reinterpret_cast<JsImageDev*>(dev + o_img), m,
                                  reinterpret_cast<const int2*>(dev + o_chunks), nchunks,
                                  reinterpret_cast<uint2*>(dev + o_counts), s);
-    if (e == hipSuccess) e = hipMemcpyAsync(hp, dev + o_status, small2_end - o_status, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = d2h(0, dev + o_status, small2_end - o_status);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) { (void)hip_fail(e, "jpeg unstuff"); fail_all("device"); return; }
     const double t_unstuff = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1046,7 +1079,7 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
     int* d_changed = reinterpret_cast<int*>(dev + o_changed);
     // ---- 4. sync, fix rounds, bases, decode ----
     EvPair& ev = thread_events(2);
-    e = hipMemcpyAsync(dev + o_scans, hp, tab2_bytes, hipMemcpyHostToDevice, s);
+    e = h2d(dev + o_scans, 0, tab2_bytes);
     if (e == hipSuccess && ev.a) e = hipEventRecord(ev.a, s);
     if (e == hipSuccess) e = launch_jsync_sync(d_scans, d_wgs, nwg, d_recs, s);
     if (e == hipSuccess) e = hipMemsetAsync(d_changed, 0, sizeof(int), s);
@@ -1056,9 +1089,13 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
                                       dev + o_cs, d_status, s);
     if (e == hipSuccess && ev.b) e = hipEventRecord(ev.b, s);
     int rounds = 0;  // the settle kernel's most rounds over the batch's images
-    if (e == hipSuccess) e = hipMemcpyAsync(hstatus.data(), d_status, sizeof(int) * m, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(&rounds, d_changed, sizeof(int), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = d2h(0, reinterpret_cast<const uint8_t*>(d_status), sizeof(int) * m);
+    if (e == hipSuccess) e = d2h(up256(sizeof(int) * m), reinterpret_cast<const uint8_t*>(d_changed), sizeof(int));
     if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess) {
+        std::memcpy(hstatus.data(), hp, sizeof(int) * m);
+        std::memcpy(&rounds, hp + up256(sizeof(int) * m), sizeof(int));
+    }
     if (e != hipSuccess) {
         if (e != hipSuccess) (void)hip_fail(e, "jpeg entropy decode");
         for (int k = 0; k < m; ++k)
@@ -1124,14 +1161,15 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
             st[i] = alloc_image((uint32_t)d.width, (uint32_t)d.height, d.comps.size() == 1 ? 1u : 3u, &img);
             if (st[i]) continue;
             outs[i] = img;
-            items[mi++] = JpegReconItem{g, img->d, img->pitch};
+            const bool fast = jpeg_zune_fast(g);
+            items[mi++] = JpegReconItem{g, img->d, img->pitch, fast ? 1 : 0, 0};
             max_blocks = std::max(max_blocks, g.nblocks);
             max_w = std::max(max_w, g.W);
             max_h = std::max(max_h, g.H);
-            any_fast = any_fast || jpeg_zune_fast(g);
+            any_fast = any_fast || fast;
         }
         const JpegReconItem* d_items = reinterpret_cast<const JpegReconItem*>(dev + o_items);
-        e = mi ? hipMemcpyAsync(dev + o_items, hp, sizeof(JpegReconItem) * mi, hipMemcpyHostToDevice, s) : hipSuccess;
+        e = h2d(dev + o_items, 0, sizeof(JpegReconItem) * mi);
         if (e == hipSuccess) e = launch_jpeg_reconstruct_batch(d_items, mi, max_blocks, max_w, max_h, any_fast, s);
         if (e != hipSuccess) (void)hip_fail(e, "jpeg reconstruct");
     }
@@ -1149,8 +1187,8 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
         g_jpeg_gpu_streams += 1;
     }
     if (timing)
-        fprintf(stderr, "[jsync] %d images, %lld lanes, %d fix rounds: unstuff %.2f ms, total %.2f ms\n", m, lanes_used,
-                rounds, t_unstuff,
+        fprintf(stderr, "[jsync] %d images, %lld lanes, %d fix rounds: layout %.2f, sync %.2f, tables %.2f, upload wait %.2f, "
+                "unstuff %.2f ms, total %.2f ms\n", m, lanes_used, rounds, tm_layout, tm_sync, tm_tables, tm_upwait, t_unstuff,
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
 }
 
@@ -1281,6 +1319,8 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
             msgs[i] = buf;
         }
     };
+    static const bool timing = getenv("IK_TIMING") != nullptr;
+    const auto tp0 = std::chrono::steady_clock::now();
     parallel_for(n, 0, [&](int i) {
         ds[i].reset(new Decoder());
         ds[i]->b = bytes[i];
@@ -1289,6 +1329,9 @@ int decode_jpeg_batch(const uint8_t* const* bytes, const size_t* lens, int n, ik
         st[i] = ds[i]->parse();
         note(i);
     });
+    if (timing)
+        fprintf(stderr, "[jpeg-batch] %d streams parsed in %.2f ms\n", n,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp0).count());
     std::vector<int> js_idx, host_idx, prog_idx;
     for (int i = 0; i < n; ++i) {
         outs[i] = nullptr;
