@@ -1170,7 +1170,7 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
         }
         const JpegReconItem* d_items = reinterpret_cast<const JpegReconItem*>(dev + o_items);
         e = h2d(dev + o_items, 0, sizeof(JpegReconItem) * mi);
-        if (e == hipSuccess) e = launch_jpeg_reconstruct_batch(d_items, mi, max_blocks, max_w, max_h, any_fast, s);
+        if (e == hipSuccess) e = launch_jpeg_reconstruct_batch(d_items, mi, max_blocks, max_w, max_h, any_fast, true, s);
         if (e != hipSuccess) (void)hip_fail(e, "jpeg reconstruct");
     }
     if (e == hipSuccess) e = hipStreamSynchronize(s);
