@@ -114,24 +114,31 @@ void release_thread_resources() { tres().release(); }
 
 namespace {
 std::mutex g_bt_mu;
-std::map<int, std::vector<double>> g_bt, g_bt_last;  // the batch in the kernel stage, the last one finished
+// per device: the batches in the decode and post stages, the last one finished
+std::map<int, std::vector<double>> g_bt_dec, g_bt_post, g_bt_last;
+bool bt_post_field(int f) { return f >= kBtResizeMs; }
 struct ThreadEvents {
     EvPair p[4];
     ~ThreadEvents() {}  // (events are left to the runtime: a thread-exit destructor may run at process exit)
 };
 }  // namespace
 
-void batch_timing_reset(int device) {
+void batch_timing_reset(int device, bool post) {
     std::lock_guard<std::mutex> lk(g_bt_mu);
-    g_bt[device].assign(kBtFields, 0.0);
+    (post ? g_bt_post : g_bt_dec)[device].assign(kBtFields, 0.0);
 }
-void batch_timing_commit(int device) {
+void batch_timing_commit(int device, bool post) {
     std::lock_guard<std::mutex> lk(g_bt_mu);
-    g_bt_last[device] = g_bt[device];
+    std::vector<double>& src = (post ? g_bt_post : g_bt_dec)[device];
+    std::vector<double>& dst = g_bt_last[device];
+    src.resize(kBtFields, 0.0);
+    dst.resize(kBtFields, 0.0);
+    for (int f = 0; f < kBtFields; ++f)
+        if (bt_post_field(f) == post) dst[(size_t)f] = src[(size_t)f];
 }
 void batch_timing_add(int device, int field, double v) {
     std::lock_guard<std::mutex> lk(g_bt_mu);
-    std::vector<double>& t = g_bt[device];
+    std::vector<double>& t = (bt_post_field(field) ? g_bt_post : g_bt_dec)[device];
     if (t.size() < (size_t)kBtFields) t.resize(kBtFields, 0.0);
     t[(size_t)field] += v;
 }
@@ -1284,17 +1291,20 @@ int ik_get_resize_mode(void) { return resize_mode(); }
 
 namespace ik {
 
-// ---- batched transforms: a three-stage pipeline per device ------------------------
+// ---- batched transforms: a four-stage pipeline per device -------------------------
 // ik_transform_batch(_submit) -- the handlers of src/lib.rs:175-191 serving many
-// requests -- runs each batch through three stages, each on its own threads, so
+// requests -- runs each batch through four stages, each on its own threads, so
 // that consecutive batches overlap on one device:
 //   upload   (one thread per device)  the PNG streams' upload: parse, DMA of the
 //            files (in place when the caller pinned them), the GPU gather + CRC
-//            pass, all on the upload thread's copy stream (png_upload_begin)
-//   kernels  (one thread per device)  decode (the PNG decode kernels once that
-//            upload has landed, JPEG entropy / reconstruction, host decoders for
-//            the rest), one resize launch per geometry group, the encoders'
-//            device front ends (png_decode_finish, transform_device_phase)
+//            pass, and the JPEG files' DMA, on the upload thread's copy stream
+//            (png_upload_begin, jpeg_upload_begin)
+//   decode   (one thread per device)  the PNG decode kernels once that upload has
+//            landed, JPEG entropy decoding and reconstruction, host decoders for
+//            the rest (transform_decode_phase)
+//   post     (one thread per device)  one resize launch per geometry group, the
+//            encoders' device front ends (transform_post_phase), on its own stream:
+//            batch k's resize runs beside batch k+1's decode kernels
 //   host     (the device's worker pool)  the host coders (libwebp / libavif) and
 //            the output buffers (transform_host_phase)
 // so batch k+1's PCIe upload runs under batch k's kernels, and batch k's libwebp
@@ -1309,6 +1319,10 @@ struct HostPhase {
     std::vector<std::vector<uint8_t>> bytes_out;
     int threads = 0;
     double t_resize = 0, t_front = 0;
+    // the decode stage's results, for the post stage: decoded images, status, message
+    std::vector<ik_image*> imgs;
+    std::vector<int> ds;
+    std::vector<std::string> dm;
 };
 
 // the PNG requests among idx (decode_batch_dev takes the same ones, in the same order)
@@ -1340,16 +1354,16 @@ static void jpeg_items(const uint8_t* const* bytes, const size_t* lens, const st
         }
 }
 
-// Device half: decode (GPU where the stream allows; the PNG upload already issued
-// when up is given), resize, the encoders' device front ends; request i's status /
-// message land in st[i] / errs[i]
-static void transform_device_phase(const uint8_t* const* bytes, const size_t* lens, const int64_t* w,
-                                   const int64_t* h, const int* fmt, const int* quality, int filter, int* st,
-                                   std::string* errs, HostPhase& hp, PngUpload* up,
+// Device half, decode stage: decode (GPU where the stream allows; the PNG upload
+// already issued when up is given) under the device's kernel gate; the images,
+// statuses and messages go to hp.imgs / ds / dm for the post stage
+static void transform_decode_phase(const uint8_t* const* bytes, const size_t* lens, HostPhase& hp, PngUpload* up,
                                    const uint8_t* const* sniff = nullptr, const JpegUpload* jup = nullptr) {
     const std::vector<uint32_t>& idx = hp.idx;
-    const int threads = hp.threads;
     const uint32_t m = (uint32_t)idx.size();
+    hp.imgs.assign(m, nullptr);
+    hp.ds.assign(m, IK_OK);
+    hp.dm.assign(m, std::string());
     if (!m) return;
     std::vector<const uint8_t*> b(m), sn(sniff ? m : 0);
     std::vector<size_t> l(m);
@@ -1358,23 +1372,37 @@ static void transform_device_phase(const uint8_t* const* bytes, const size_t* le
         l[k] = lens[idx[k]];
         if (sniff) sn[k] = sniff[idx[k]];
     }
-    std::vector<ik_image*> imgs(m, nullptr);
-    std::vector<int> ds(m, IK_OK);
-    std::vector<std::string> dm(m);
     static const bool timing = getenv("IK_TIMING") != nullptr;  // dev: per-stage sums to stderr
-    // GPU phases under the device's kernel gate (held from the decode kernels
-    // through resize and the encoders' device front ends), the host coders after
     const auto tg0 = std::chrono::steady_clock::now();
     gate_pin(kGateKernels, true);
     const auto tg1 = std::chrono::steady_clock::now();
-    batch_timing_reset(current_device());
-    decode_batch_dev(b.data(), l.data(), m, imgs.data(), nullptr, ds.data(), dm.data(), threads, up,
+    batch_timing_reset(current_device(), false);
+    decode_batch_dev(b.data(), l.data(), m, hp.imgs.data(), nullptr, hp.ds.data(), hp.dm.data(), hp.threads, up,
                      sniff ? sn.data() : nullptr, jup);
+    batch_timing_commit(current_device(), false);
+    gate_pin(kGateKernels, false);
     if (timing)
         fprintf(stderr, "[device_phase] gate wait %.2f ms, decode %.2f ms\n",
                 std::chrono::duration<double, std::milli>(tg1 - tg0).count(),
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tg1).count());
-    gate_enter(kGateKernels);
+}
+
+// Device half, post stage: resize, the encoders' device front ends (under the
+// post gate, so a batch's resize runs beside the next batch's decode kernels);
+// request i's status / message land in st[i] / errs[i]
+static void transform_post_phase(const int64_t* w, const int64_t* h, const int* fmt, const int* quality, int filter,
+                                 int* st, std::string* errs, HostPhase& hp) {
+    const std::vector<uint32_t>& idx = hp.idx;
+    const int threads = hp.threads;
+    const uint32_t m = (uint32_t)idx.size();
+    if (!m) return;
+    std::vector<ik_image*>& imgs = hp.imgs;
+    std::vector<int>& ds = hp.ds;
+    std::vector<std::string>& dm = hp.dm;
+    static const bool timing = getenv("IK_TIMING") != nullptr;
+    gate_pin(kGatePost, true);
+    gate_enter(kGatePost);
+    batch_timing_reset(current_device(), true);
     std::mutex tmu;
     double& t_resize = hp.t_resize;
     double& t_front = hp.t_front;
@@ -1453,8 +1481,11 @@ static void transform_device_phase(const uint8_t* const* bytes, const size_t* le
         ik_image_free(imgs[k]);
         imgs[k] = nullptr;
     });
-    gate_pin(kGateKernels, false);
-    batch_timing_commit(current_device());
+    batch_timing_commit(current_device(), true);
+    gate_pin(kGatePost, false);
+    std::vector<ik_image*>().swap(hp.imgs);
+    std::vector<int>().swap(hp.ds);
+    std::vector<std::string>().swap(hp.dm);
 }
 
 static void transform_host_phase(uint8_t** outs, size_t* out_lens, int* st, std::string* errs, HostPhase& hp) {
@@ -1543,23 +1574,18 @@ struct BatchPart {
 class StageExec {
 public:
     StageExec(int device, Pool* host_pool) : dev_(device), pool_(host_pool) {
-        th_[0] = std::thread([this] { loop(0); });  // live until stop() (ik_shutdown)
-        th_[1] = std::thread([this] { loop(1); });
+        for (int k = 0; k < kStages; ++k) th_[k] = std::thread([this, k] { loop(k); });  // live until stop()
     }
-    // ik_shutdown: the stages finish what is queued (upload before kernels), then end
+    // ik_shutdown: the stages finish what is queued (upload, then decode, then post), then end
     void stop() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            done_[0] = true;
+        for (int k = 0; k < kStages; ++k) {
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                done_[k] = true;
+            }
+            cv_.notify_all();
+            th_[k].join();
         }
-        cv_.notify_all();
-        th_[0].join();
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            done_[1] = true;
-        }
-        cv_.notify_all();
-        th_[1].join();
     }
     void submit(std::shared_ptr<BatchPart> p) {
         {
@@ -1597,9 +1623,22 @@ private:
                 cv_.notify_all();
                 continue;
             }
-            Ticket& t = *p->t;
-            // once this batch's resolve pass is done, the next queued batch's block
-            // search goes out beside this batch's unfilter and resize
+            if (stage == 2) {
+                // resize + the encoders' device front ends, beside the next batch's decode
+                Ticket& t = *p->t;
+                transform_post_phase(p->w, p->h, p->fmt, p->quality, p->filter, t.st.data(), t.errs.data(), p->hp);
+                pool_->post([p] {
+                    Ticket& tk = *p->t;
+                    transform_host_phase(tk.outs, tk.out_lens, tk.st.data(), tk.errs.data(), p->hp);
+                    p->hp = HostPhase();
+                    if (p->logical >= 0) sched_release(p->logical, p->cost);
+                    std::lock_guard<std::mutex> lk(tk.mu);
+                    if (--tk.pending == 0) tk.cv.notify_all();
+                });
+                continue;
+            }
+            // the next queued batch's block search goes out on this stream between
+            // this batch's decode rounds and its expand
             p->up.on_next_search = [this](hipEvent_t after) {
                 std::shared_ptr<BatchPart> nx;
                 {
@@ -1618,18 +1657,14 @@ private:
                 if (after && hipStreamWaitEvent(fs, after, 0) != hipSuccess) return;
                 png_find_prelaunch(nx->up, fs);
             };
-            transform_device_phase(p->bytes, p->lens, p->w, p->h, p->fmt, p->quality, p->filter, t.st.data(),
-                                   t.errs.data(), p->hp, p->pb.empty() ? nullptr : &p->up, p->sniff, &p->jup);
+            transform_decode_phase(p->bytes, p->lens, p->hp, p->pb.empty() ? nullptr : &p->up, p->sniff, &p->jup);
             p->up = PngUpload();
             p->jup = JpegUpload();  // (the decode has returned: its area is free again)
-            pool_->post([p] {
-                Ticket& tk = *p->t;
-                transform_host_phase(tk.outs, tk.out_lens, tk.st.data(), tk.errs.data(), p->hp);
-                p->hp = HostPhase();
-                if (p->logical >= 0) sched_release(p->logical, p->cost);
-                std::lock_guard<std::mutex> lk(tk.mu);
-                if (--tk.pending == 0) tk.cv.notify_all();
-            });
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                q_[2].push_back(std::move(p));
+            }
+            cv_.notify_all();
         }
         release_thread_resources();
     }
@@ -1637,9 +1672,10 @@ private:
     Pool* pool_;
     std::mutex mu_;
     std::condition_variable cv_;
-    std::deque<std::shared_ptr<BatchPart>> q_[2];
-    bool done_[2] = {false, false};
-    std::thread th_[2];
+    static constexpr int kStages = 3;  // upload, decode, post (resize + device front ends)
+    std::deque<std::shared_ptr<BatchPart>> q_[kStages];
+    bool done_[kStages] = {false, false, false};
+    std::thread th_[kStages];
 };
 
 std::mutex g_stage_mu;

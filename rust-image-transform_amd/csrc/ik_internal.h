@@ -131,7 +131,7 @@ struct JpegReconItem {
     int pad;
 };
 hipError_t launch_jpeg_reconstruct_batch(const JpegReconItem* items, int m, long long max_blocks, int max_w, int max_h,
-                                         bool any_fast, bool idct, hipStream_t s);
+                                         bool any_fast, bool any_slow, bool idct, hipStream_t s);
 bool jpeg_zune_fast(const JpegGeom& g);
 
 // Baseline Huffman tables (JpegHuffTables) and the self-synchronising decoder's

@@ -305,8 +305,8 @@ __device__ __forceinline__ void color_group(const JpegGeom& g, uint8_t* __restri
 __global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restrict__ dst, size_t pitch) {
     color_group(g, dst, pitch, 4 * (blockIdx.x * 256 + threadIdx.x), blockIdx.y, zune_fast(g));
 }
-// the batch's images in one launch: blockIdx.z = image.  (zune_fast comes from the
-// host with the entry: tested here field by field it is a chain of dependent
+// the batch's images that are not zune_fast in one launch: blockIdx.z = image.
+// (zune_fast comes from the host with the entry: tested here field by field it is a chain of dependent
 // scalar loads per workgroup; the whole entry copied to registers instead costs
 // ~100 SGPRs and half the waves)
 // A workgroup takes kColorRows rows, so that each entry's fields are loaded once per
@@ -314,9 +314,9 @@ __global__ __launch_bounds__(256) void k_jpeg_color(JpegGeom g, uint8_t* __restr
 constexpr int kColorRows = 8;
 __global__ __launch_bounds__(256) void k_jpeg_color_b(const JpegReconItem* __restrict__ items) {
     const JpegReconItem& it = items[blockIdx.z];  // (restrict: its loads hoist past the row stores)
-    const bool fast = it.fast != 0;
+    if (it.fast) return;  // k_jpeg_color_fast_b + k_jpeg_color_ends_b
     const int x0 = 4 * (blockIdx.x * 256 + threadIdx.x);
-    for (int r = 0; r < kColorRows; ++r) color_group(it.g, it.dst, it.pitch, x0, blockIdx.y * kColorRows + r, fast);
+    for (int r = 0; r < kColorRows; ++r) color_group(it.g, it.dst, it.pitch, x0, blockIdx.y * kColorRows + r, false);
 }
 
 // The row ends of a zune_fast image (the groups of four k_jpeg_color leaves:
@@ -324,28 +324,168 @@ __global__ __launch_bounds__(256) void k_jpeg_color_b(const JpegReconItem* __res
 // samples or the image's right edge), one thread per (row, end): kept out of
 // k_jpeg_color, where a wave holding a row-end thread ran these branches for all
 // of its lanes (50 vs 27 us per 4096^2 frame with them outside).
+// G: the interior kernel's group width (4: k_jpeg_color, 8: k_jpeg_color_fast_b)
+template <int G>
 __device__ __forceinline__ void color_ends(const JpegGeom& g, uint8_t* __restrict__ dst, size_t pitch, int t) {
     if (t >= 2 * g.H) return;
     const int y = t >> 1;
-    const int lim = 2 * g.bw[1] * 8 - 2;  // a group is interior iff x0 >= 4, x0 + 4 <= W and x0 + 3 < lim
+    const int lim = 2 * g.bw[1] * 8 - 2;  // a group is interior iff x0 >= G, x0 + G <= W and x0 + G - 1 < lim
     // the first group past the interior ones: the last interior x0 is the largest
-    // multiple of 4 <= min(W - 4, lim - 4)
-    const int xm = (g.W - 4 < lim - 4 ? g.W - 4 : lim - 4);
-    const int xc = xm < 4 ? 4 : (xm & ~3) + 4;
+    // multiple of G <= min(W - G, lim - G)
+    const int xm = (g.W - G < lim - G ? g.W - G : lim - G);
+    const int xc = xm < G ? G : (xm & ~(G - 1)) + G;
     int xa, xb;
     if (t & 1) { xa = xc; xb = g.W; }
-    else { xa = 0; xb = g.W < 4 ? g.W : 4; }
+    else { xa = 0; xb = g.W < G ? g.W : G; }
     uint8_t* o = dst + (size_t)y * pitch;
     for (int x = xa; x < xb; ++x) color1_zune(g, x, y, o + 3 * x);
 }
 
 __global__ __launch_bounds__(256) void k_jpeg_color_ends(JpegGeom g, uint8_t* __restrict__ dst, size_t pitch) {
-    color_ends(g, dst, pitch, blockIdx.x * 256 + threadIdx.x);
+    color_ends<4>(g, dst, pitch, blockIdx.x * 256 + threadIdx.x);
 }
-// the batch's zune_fast images in one launch: blockIdx.y = image (the others return)
+constexpr int kFastPx = 8;  // k_jpeg_color_fast_b's pixels per thread
+// the batch's zune_fast images in one launch: blockIdx.y = image (the others
+// return).  One thread per end pixel: slots 0 .. 15 of a row are its left end
+// [0, min(W, 8)), slots 16 .. 31 its right end [xc, W) (at most 9 pixels unless
+// W < 16; slot 31 takes any past xc + 16)
 __global__ __launch_bounds__(256) void k_jpeg_color_ends_b(const JpegReconItem* __restrict__ items) {
     const JpegReconItem& it = items[blockIdx.y];
-    if (it.fast) color_ends(it.g, it.dst, it.pitch, blockIdx.x * 256 + threadIdx.x);
+    if (!it.fast) return;
+    const JpegGeom& g = it.g;
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    const int y = t >> 5, k = t & 31;
+    if (y >= g.H) return;
+    uint8_t* o = it.dst + (size_t)y * it.pitch;
+    if (k < 16) {
+        if (k < kFastPx && k < g.W) color1_zune(g, k, y, o + 3 * k);
+        return;
+    }
+    const int lim = 2 * g.bw[1] * 8 - 2;  // as color_ends<kFastPx>
+    const int xm = (g.W - kFastPx < lim - kFastPx ? g.W - kFastPx : lim - kFastPx);
+    const int xc = xm < kFastPx ? kFastPx : (xm & ~(kFastPx - 1)) + kFastPx;
+    const int x = xc + (k - 16);
+    if (k < 31) {
+        if (x < g.W) color1_zune(g, x, y, o + 3 * x);
+        return;
+    }
+    for (int xx = x; xx < g.W; ++xx) color1_zune(g, xx, y, o + 3 * xx);
+}
+
+// ---- the batch's zune_fast images: eight pixels by kFastRows rows per thread ----
+// k_jpeg_color_b's per-pixel path re-derived the geometry per row (a scalar
+// division for the vertical factor), loaded through generic pointers and waited
+// on every load in turn: 7.9 ms per 256 4096^2 frames, about a third of HBM
+// speed.  Here a thread keeps its column's three chroma rows (above, this,
+// below) of both planes in registers and walks down its rows: per output row one
+// 8-byte luma load, per chroma row one 12-byte load per plane (bytes i-4 .. i+7,
+// i = x0 / 2: the samples i-1 .. i+4 the eight pixels use), and two 12-byte
+// stores.  The arithmetic is color4_zune's (upsampler/scalar.rs vertical then
+// horizontal (3 near + far + 2) >> 2, color_convert/scalar.rs i16 YCbCr).
+typedef __attribute__((address_space(1))) uint8_t g8;
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+
+__device__ __forceinline__ uint32_t pack_px(int v) { return (uint32_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+// one output row's eight pixels: yv = luma bytes x0 .. x0+7; s[c] / t[c]: plane
+// c's chroma row (near) and its vertical neighbour (far), bytes i-4 .. i+7
+template <int FV>
+__device__ __forceinline__ void color8_row(u32x2 yv, const u32x3 (&s)[2], const u32x3 (&t)[2], g8* __restrict__ o) {
+    int at[2][6];  // the vertically upsampled samples i-1 .. i+4
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const int b = 3 + k;  // byte of the 12 (i-4 .. i+7)
+            const uint32_t ws = b < 4 ? s[c].x : b < 8 ? s[c].y : s[c].z;
+            const int s0 = (int)((ws >> (8 * (b & 3))) & 255u);
+            if (FV == 2) {
+                const uint32_t wt = b < 4 ? t[c].x : b < 8 ? t[c].y : t[c].z;
+                const int s1 = (int)((wt >> (8 * (b & 3))) & 255u);
+                at[c][k] = (s0 * 3 + s1 + 2) >> 2;
+            } else {
+                at[c][k] = s0;
+            }
+        }
+    }
+    uint32_t px[8];  // 0x00BBGGRR per pixel
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int ip = 1 + (j >> 1), nb = (j & 1) ? ip + 1 : ip - 1;
+        const int c0 = (int)(((j < 4 ? yv.x : yv.y) >> (8 * (j & 3))) & 255u);
+        const int c1 = (at[0][ip] * 3 + at[0][nb] + 2) >> 2, c2 = (at[1][ip] * 3 + at[1][nb] + 2) >> 2;
+        const int16_t cb = (int16_t)(c1 - 128), cr = (int16_t)(c2 - 128);
+        const int r = c0 + ((int16_t)(45 * cr) >> 5);
+        const int gg = c0 - ((int16_t)(11 * cb + 23 * cr) >> 5);
+        const int b = c0 + ((int16_t)(113 * cb) >> 6);
+        px[j] = pack_px(r) | pack_px(gg) << 8 | pack_px(b) << 16;
+    }
+    // 24 bytes R0 G0 B0 R1 G1 B1 ... as six dwords
+    u32x3 lo, hi;
+    lo.x = px[0] | px[1] << 24;
+    lo.y = px[1] >> 8 | px[2] << 16;
+    lo.z = px[2] >> 16 | px[3] << 8;
+    hi.x = px[4] | px[5] << 24;
+    hi.y = px[5] >> 8 | px[6] << 16;
+    hi.z = px[6] >> 16 | px[7] << 8;
+    *reinterpret_cast<u32x3 __attribute__((address_space(1)))*>(o) = lo;
+    *reinterpret_cast<u32x3 __attribute__((address_space(1)))*>(o + 12) = hi;
+}
+
+template <int FV>
+__device__ __forceinline__ void color_fast_rows(const JpegGeom& g, g8* __restrict__ dst, size_t pitch, int x0, int y0,
+                                                int y1) {
+    const int nY = g.bw[0] * 8, n = g.bw[1] * 8, ph = g.bh[1] * 8;
+    const g8* yp = (const g8*)g.planes + g.plane0[0] + x0;
+    const g8* cp[2] = {(const g8*)g.planes + g.plane0[1] + (x0 >> 1) - 4,
+                       (const g8*)g.planes + g.plane0[2] + (x0 >> 1) - 4};
+    auto ldc = [&](int c, int r) -> u32x3 {
+        r = r < 0 ? 0 : (r >= ph ? ph - 1 : r);
+        return *reinterpret_cast<const u32x3 __attribute__((address_space(1)))*>(cp[c] + (size_t)r * n);
+    };
+    auto ldy = [&](int y) -> u32x2 {
+        return *reinterpret_cast<const u32x2 __attribute__((address_space(1)))*>(yp + (size_t)y * nY);
+    };
+    g8* o = dst + (size_t)y0 * pitch + (size_t)3 * x0;
+    if (FV == 2) {
+        // y0 even: rows 2Y and 2Y+1 share chroma row Y (far rows Y-1 and Y+1)
+        int Y = y0 >> 1;
+        u32x3 up[2] = {ldc(0, Y - 1), ldc(1, Y - 1)}, mid[2] = {ldc(0, Y), ldc(1, Y)};
+        for (int y = y0; y < y1; y += 2, ++Y) {
+            const u32x3 dn[2] = {ldc(0, Y + 1), ldc(1, Y + 1)};
+            const u32x2 ya = ldy(y);
+            const u32x2 yb = ldy(y + 1 < y1 ? y + 1 : y);
+            color8_row<2>(ya, mid, up, o);
+            o += pitch;
+            if (y + 1 < y1) color8_row<2>(yb, mid, dn, o);
+            o += pitch;
+            up[0] = mid[0]; up[1] = mid[1];
+            mid[0] = dn[0]; mid[1] = dn[1];
+        }
+    } else {
+        for (int y = y0; y < y1; ++y) {
+            const u32x3 c[2] = {ldc(0, y), ldc(1, y)};
+            color8_row<1>(ldy(y), c, c, o);
+            o += pitch;
+        }
+    }
+}
+
+// grid: (column groups of 8 x 256, row bands of kFastRows, image); the interior
+// groups only (x0 >= 8, x0 + 8 <= W, x0 + 7 < 2n - 2), k_jpeg_color_ends_b the rest
+constexpr int kFastRows = 16;
+__global__ __launch_bounds__(256) void k_jpeg_color_fast_b(const JpegReconItem* __restrict__ items) {
+    const JpegReconItem& it = items[blockIdx.z];
+    if (!it.fast) return;
+    const JpegGeom& g = it.g;
+    const int x0 = kFastPx * (blockIdx.x * 256 + threadIdx.x);
+    const int y0 = blockIdx.y * kFastRows;
+    if (y0 >= g.H || x0 < kFastPx || x0 + kFastPx > g.W || x0 + kFastPx - 1 >= 2 * g.bw[1] * 8 - 2) return;
+    const int y1 = y0 + kFastRows < g.H ? y0 + kFastRows : g.H;
+    g8* dst = (g8*)it.dst;
+    if (g.vmax == 2 * g.v[1]) color_fast_rows<2>(g, dst, it.pitch, x0, y0, y1);
+    else color_fast_rows<1>(g, dst, it.pitch, x0, y0, y1);
 }
 
 }  // namespace
@@ -605,13 +745,19 @@ hipError_t launch_jpeg_prog(const JpegScanArgs& a, hipStream_t s) {
 // device array of m; maxima over the images: blocks, width, height; idct: false
 // when the sample planes are already there)
 hipError_t launch_jpeg_reconstruct_batch(const JpegReconItem* items, int m, long long max_blocks, int max_w, int max_h,
-                                         bool any_fast, bool idct, hipStream_t s) {
+                                         bool any_fast, bool any_slow, bool idct, hipStream_t s) {
     if (m <= 0) return hipSuccess;
     if (max_blocks <= 0 || max_w <= 0 || max_h <= 0 || m > 65535 || max_h > 65535) return hipErrorInvalidValue;
     if (idct) hipLaunchKernelGGL(k_jpeg_idct_b, dim3((unsigned)((max_blocks + 255) / 256), m), dim3(256), 0, s, items);
-    hipLaunchKernelGGL(k_jpeg_color_b, dim3((max_w + 1023) / 1024, (max_h + kColorRows - 1) / kColorRows, m), dim3(256),
-                       0, s, items);
-    if (any_fast) hipLaunchKernelGGL(k_jpeg_color_ends_b, dim3((2 * max_h + 255) / 256, m), dim3(256), 0, s, items);
+    if (any_slow)
+        hipLaunchKernelGGL(k_jpeg_color_b, dim3((max_w + 1023) / 1024, (max_h + kColorRows - 1) / kColorRows, m),
+                           dim3(256), 0, s, items);
+    if (any_fast) {
+        hipLaunchKernelGGL(k_jpeg_color_fast_b,
+                           dim3((max_w + 256 * kFastPx - 1) / (256 * kFastPx), (max_h + kFastRows - 1) / kFastRows, m),
+                           dim3(256), 0, s, items);
+        hipLaunchKernelGGL(k_jpeg_color_ends_b, dim3((32 * max_h + 255) / 256, m), dim3(256), 0, s, items);
+    }
     return hipGetLastError();
 }
 bool jpeg_zune_fast(const JpegGeom& g) { return zune_fast(g); }

@@ -1147,7 +1147,7 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
         JpegReconItem* items = reinterpret_cast<JpegReconItem*>(hp);
         int mi = 0, max_w = 0, max_h = 0;
         long long max_blocks = 0;
-        bool any_fast = false;
+        bool any_fast = false, any_slow = false;
         for (int k = 0; k < m; ++k) {
             if (!ok[k]) continue;
             const int i = idx[k];
@@ -1167,10 +1167,11 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
             max_w = std::max(max_w, g.W);
             max_h = std::max(max_h, g.H);
             any_fast = any_fast || fast;
+            any_slow = any_slow || !fast;
         }
         const JpegReconItem* d_items = reinterpret_cast<const JpegReconItem*>(dev + o_items);
         e = h2d(dev + o_items, 0, sizeof(JpegReconItem) * mi);
-        if (e == hipSuccess) e = launch_jpeg_reconstruct_batch(d_items, mi, max_blocks, max_w, max_h, any_fast, true, s);
+        if (e == hipSuccess) e = launch_jpeg_reconstruct_batch(d_items, mi, max_blocks, max_w, max_h, any_fast, any_slow, true, s);
         if (e != hipSuccess) (void)hip_fail(e, "jpeg reconstruct");
     }
     if (e == hipSuccess) e = hipStreamSynchronize(s);

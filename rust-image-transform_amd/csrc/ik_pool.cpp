@@ -60,12 +60,12 @@ int default_threads() {
 // ---- phase gates -----------------------------------------------------------------
 namespace {
 std::mutex& gate_mutex(int device, int which) {
-    static std::mutex m[64][2];
-    return m[(unsigned)device % 64u][which & 1];
+    static std::mutex m[64][3];
+    return m[(unsigned)device % 64u][(unsigned)which % 3u];
 }
 struct GateState {
-    bool held[2] = {false, false}, pinned[2] = {false, false};
-    int dev[2] = {0, 0};
+    bool held[3] = {false, false, false}, pinned[3] = {false, false, false};
+    int dev[3] = {0, 0, 0};
 };
 thread_local GateState t_gate;
 }  // namespace
@@ -87,7 +87,7 @@ bool gate_try_enter(int which) {
     return true;
 }
 
-bool gate_held_any() { return t_gate.held[kGateKernels] || t_gate.held[kGateUpload]; }
+bool gate_held_any() { return t_gate.held[kGateKernels] || t_gate.held[kGateUpload] || t_gate.held[kGatePost]; }
 
 void gate_leave(int which) {
     if (!t_gate.held[which] || t_gate.pinned[which]) return;

@@ -79,9 +79,11 @@ Pool& device_pool(int device);  // the persistent workers of a physical device
 // fn(i) for i in [0, n) on the calling thread's device pool (and the caller)
 void parallel_for(int n, int threads, const std::function<void(int)>& fn);
 
-// Figures of the last batch each device's kernel stage ran (ik_batch_last_timing):
-// device ms from HIP events on the kernel stream and the algorithmic bytes of the
-// same launches.  Reset when a batch's kernel stage starts; summed over its launches.
+// Figures of the last batch each device's kernel stages ran (ik_batch_last_timing):
+// device ms from HIP events on the stage's stream and the algorithmic bytes of the
+// same launches.  Two records per device, one per stage: the decode stage's fields
+// (kBtJpeg* up to kBtJpegLanes) and the post stage's (resize, JPEG encoder); each is
+// reset when its stage starts a batch and summed over that batch's launches.
 enum BatchTimingField {
     kBtJpegHuffMs = 0,   // JPEG entropy decoding launches (restart intervals / self-sync)
     kBtJpegScanBytes,    // entropy-coded bytes they read
@@ -95,8 +97,8 @@ enum BatchTimingField {
     kBtJpegEncImages,
     kBtFields
 };
-void batch_timing_reset(int device);
-void batch_timing_commit(int device);  // the kernel stage is done: its figures become the last batch's
+void batch_timing_reset(int device, bool post);
+void batch_timing_commit(int device, bool post);  // the stage is done: its fields become the last batch's
 void batch_timing_add(int device, int field, double v);
 // a pair of events on the calling thread (timing one launch sequence); ms between them
 struct EvPair {
@@ -303,12 +305,13 @@ int resize_group(const std::vector<ik_image*>& src, uint32_t nw, uint32_t nh, in
 
 // Per-device phase gates (ik_pool.cpp).  Concurrent batch calls on one device
 // take its GPU phases in turn: kGateUpload covers a PNG batch's staging, H2D and
-// block search, kGateKernels the decode kernels through resize and the encoders'
-// device front ends.  A batch's host phases (libwebp / libavif coding) run
-// outside both, beside the next batch's kernels; its small kernels never queue
+// block search, kGateKernels the decode kernels, kGatePost the resize and the
+// encoders' device front ends (so one batch's resize runs beside the next batch's
+// decode kernels).  A batch's host phases (libwebp / libavif coding) run outside
+// all three, beside the next batch's kernels; its small kernels never queue
 // behind another batch's long ones.  gate_pin keeps a gate held across
-// gate_leave (a caller that spans several phases); IK_BATCH_GATE=0 disables them.
-enum { kGateUpload = 0, kGateKernels = 1 };
+// gate_leave (a caller that spans several phases).
+enum { kGateUpload = 0, kGateKernels = 1, kGatePost = 2 };
 void gate_enter(int which);
 bool gate_try_enter(int which);  // true if now held (or gates are off)
 bool gate_held_any();            // this thread holds one of its device's gates

@@ -126,3 +126,20 @@ def test_config1_jpeg_to_webp_equals_oracle(oracle):
     want, dims = oracle.transform(oracle.jpeg_decode(b, ZUNE), 320, None, 4, 1, 80)
     assert dims == (320, 240)
     assert encode_image(out, ImageFormat.webp, 80) == want
+
+
+@pytest.mark.parametrize("sub", [1, 2])
+def test_batch_colour_edges_equal_restatement(oracle, sub):
+    """The batched colour kernels (ik_jpeg.hip k_jpeg_color_fast_b: eight pixels by
+    16 rows per thread, interior groups only; k_jpeg_color_ends_b: the row ends)
+    over images whose widths and heights fall on and off the group, MCU and band
+    boundaries, mixed in one batch so that the grid is sized by the widest."""
+    sizes = [(48, 48), (49, 50), (57, 41), (63, 64), (65, 33), (100, 61), (257, 129), (1023, 77), (4001, 24),
+             (520, 9), (16, 300), (24, 17)]
+    blobs = [_jpeg(ikutil.synth(w, h, 3, seed=40 + k, pattern="N"), quality=95, subsampling=sub,
+                   **({"restart_marker_rows": 1} if k % 3 == 0 else {}))
+             for k, (w, h) in enumerate(sizes)]
+    out = decode_image_batch(blobs)
+    for (img, fmt), b, wh in zip(out, blobs, sizes):
+        assert fmt is ImageFormat.jpeg
+        np.testing.assert_array_equal(img.to_array(), oracle.jpeg_decode(b, ZUNE), err_msg=str(wh))

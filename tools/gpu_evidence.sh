@@ -10,6 +10,8 @@
 #   c2norst   configs[2] with restart-free sources
 #   lt        the loadtest mix (configs[3]), restart-free sources, 10,000 requests, CPU leg included
 #   ltrst     the same with a restart marker per MCU row
+#   jtests    the JPEG GPU parity tests only (decode, zune reconstruction, the configs[2] parity case)
+#   ptime     the headline bench with IK_TIMING (host stage marks on stderr)
 # Outputs go to gpurun_out/${TAG}_*; copy what is judged into profiles/.
 set -o pipefail
 export TMPDIR=/tmp
@@ -58,6 +60,14 @@ for s in $STEPS; do
       timeout -k 10 900 python -u tools/loadtest.py --requests 10000 --batch 64 --threads 16 --restart > ${O}_ltrst.json 2> ${O}_ltrst.err \
         || { echo "LOADTEST FAILED"; tail -20 ${O}_ltrst.err; exit 1; }
       tail -c 600 ${O}_ltrst.json ;;
+    jtests)
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_jpeg_zune.py tests/test_gpu_decode.py tests/test_gpu_headline_parity.py -x -q -m gpu --timeout 300 --timeout-method thread > ${O}_jtests.log 2>&1 \
+        || { echo "JPEG TESTS FAILED"; tail -40 ${O}_jtests.log; exit 1; }
+      tail -2 ${O}_jtests.log ;;
+    ptime)
+      IK_TIMING=1 timeout -k 10 600 python -u bench.py --no-cpu-baseline --no-extras --steps 6 > ${O}_ptime.json 2> ${O}_ptime.err \
+        || { echo "PTIME FAILED"; tail -20 ${O}_ptime.err; exit 1; }
+      python tools/bench_summary.py ${O}_ptime.json ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
