@@ -481,7 +481,8 @@ def main():
                         "traffic": None, "kernel": "k_resize_fused", "kernel_ms": round(float(bt[5]), 4),
                         "bytes_per_launch": int(bt[6]), "batch": int(bt[7]),
                         "note": "the grouped resize launch of the measured batches themselves (HIP events on the "
-                                "kernel stream); bytes = C*W*H in + C*w*h out per image"}
+                                "post stage's stream, beside the next batch's decode kernels); bytes = C*W*H in + "
+                                "C*w*h out per image"}
     jpeg_enc = {"ms": round(float(bt[8]), 4), "images": int(bt[9])} if bt[9] > 0 else None
     dom = max(kern, key=lambda k: kern[k][0]) if kern else None
     dms, dbytes = kern[dom] if dom else (1.0, 0)
@@ -609,7 +610,37 @@ def main():
                    "value": round(aggregate_mpix(world, n, S, te), 2), "unit": "MPix/s"}
 
     if roof_resize is None:
-        roof_resize = resize_batch  # (no hbm_resident leg: the measured batches' own resize launch)
+        # the resize kernel alone on the measured batch's geometry (C channels as the
+        # decoded frames: 3 for JPEG sources): in the four-stage pipeline the batch's
+        # own resize runs beside the next batch's decode kernels, so its event time
+        # (roofline_resize_batch_path) includes their contention
+        C = 3 if args.source != "png" else 4
+        src = torch.empty((B, S, S * C), dtype=torch.uint8, device=dev)
+        for i in range(B):
+            src[i].random_(0, 256)
+        dstt = torch.empty((B, O, O * C), dtype=torch.uint8, device=dev)
+        st = torch.cuda.Stream()
+        torch.cuda.synchronize()
+        rms = []
+        for r in range(4):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            if lib.ik_resize_batch_device(src.data_ptr(), S, S, C, S * C, S * S * C, B, O, O, f, dstt.data_ptr(),
+                                          O * C, O * O * C, ctypes.c_void_p(st.cuda_stream)):
+                raise SystemExit(f"resize: {_lib.last_error()}")
+            e1.record(st)
+            e1.synchronize()
+            if r:
+                rms.append(e0.elapsed_time(e1))
+        rms_med = float(np.median(rms))
+        rb = B * C * (S * S + O * O)
+        roof_resize = {"bound": "hbm", "achieved": round(rb / (rms_med * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                       "unit": "GB/s", "frac": round(rb / (rms_med * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                       "kernel": "k_resize_fused", "kernel_ms": round(rms_med, 4), "bytes_per_launch": rb, "batch": B,
+                       "note": f"the resize kernel alone (ik_resize_batch_device, {C} channels, the batch's "
+                               f"geometry and filter), HIP events on its stream, median of 3 launches"}
+        del src, dstt
+        torch.cuda.empty_cache()
     src_desc = ({"png": "PNG (zlib level 6), resident in HBM (one device allocation per request) -> "
                         "ik_transform_batch_submit_device: decode_image (GPU chunk walk, gather + CRC, inflate + "
                         "unfilter)",

@@ -23,7 +23,7 @@ constexpr int kStripBytes = kBytesPerLane * kThreads;  // 2048 source bytes per 
 constexpr int kRowWords = kStripBytes + kStripBytes / 8;  // LDS f32 row, +4 words per 32
 constexpr int kMaxFlushRows = 4;         // vertical rows staged in LDS per horizontal pass (plan: 2..4)
 constexpr int kMaxStripCols = 512;       // output columns per strip (LDS offset/count tables)
-constexpr int kMaxStripWeights = 3072;   // horizontal weights per strip kept in LDS (12 KB)
+constexpr int kMaxStripWeights = 4096;   // horizontal weights per strip kept in LDS (16 KB: an RGB Lanczos3 8x strip's 85 x 48)
 
 // Everything the resize kernels read.  Weight tables follow image 0.25.8
 // sample.rs (see ik_plan.cpp); tables live in one device allocation per plan.

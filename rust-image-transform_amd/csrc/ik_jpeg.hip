@@ -345,6 +345,36 @@ __global__ __launch_bounds__(256) void k_jpeg_color_ends(JpegGeom g, uint8_t* __
     color_ends<4>(g, dst, pitch, blockIdx.x * 256 + threadIdx.x);
 }
 constexpr int kFastPx = 8;  // k_jpeg_color_fast_b's pixels per thread
+// one pixel of a zune_fast image with its vertical factor fv known: color1_zune
+// (upsampled_zune's horizontal cases x = 0, 1, 2n-2, 2n-1 and the interior one)
+// without the per-component factor divisions and the other modes' branches
+__device__ __forceinline__ void color1_fast(const JpegGeom& g, int fv, int x, int y, uint8_t* o) {
+    const int n = g.bw[1] * 8, ph = g.bh[1] * 8;
+    const int c0 = g.planes[g.plane0[0] + (size_t)y * (g.bw[0] * 8) + x];
+    const int Y = fv == 2 ? y >> 1 : y;
+    int r1 = fv == 2 ? ((y & 1) ? Y + 1 : Y - 1) : Y;
+    r1 = r1 < 0 ? 0 : (r1 >= ph ? ph - 1 : r1);
+    int cc[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const uint8_t* p0 = g.planes + g.plane0[1 + c] + (size_t)Y * n;
+        const uint8_t* p1 = g.planes + g.plane0[1 + c] + (size_t)r1 * n;
+        auto at = [&](int k) { return fv == 2 ? (p0[k] * 3 + p1[k] + 2) >> 2 : (int)p0[k]; };
+        const int i = x >> 1;
+        int v;
+        if (x == 0) v = at(0);
+        else if (x == 1) v = (at(0) * 3 + at(1) + 2) >> 2;
+        else if (x == 2 * n - 2) v = (at(n - 2) * 3 + at(n - 1) + 2) >> 2;
+        else if (x == 2 * n - 1) v = at(n - 1);
+        else v = (x & 1) ? (at(i) * 3 + at(i + 1) + 2) >> 2 : (at(i) * 3 + at(i - 1) + 2) >> 2;
+        cc[c] = v;
+    }
+    const int16_t cb = (int16_t)(cc[0] - 128), cr = (int16_t)(cc[1] - 128);
+    o[0] = clamp255(c0 + ((int16_t)(45 * cr) >> 5));
+    o[1] = clamp255(c0 - ((int16_t)(11 * cb + 23 * cr) >> 5));
+    o[2] = clamp255(c0 + ((int16_t)(113 * cb) >> 6));
+}
+
 // the batch's zune_fast images in one launch: blockIdx.y = image (the others
 // return).  One thread per end pixel: slots 0 .. 15 of a row are its left end
 // [0, min(W, 8)), slots 16 .. 31 its right end [xc, W) (at most 9 pixels unless
@@ -357,8 +387,9 @@ __global__ __launch_bounds__(256) void k_jpeg_color_ends_b(const JpegReconItem* 
     const int y = t >> 5, k = t & 31;
     if (y >= g.H) return;
     uint8_t* o = it.dst + (size_t)y * it.pitch;
+    const int fv = g.vmax == 2 * g.v[1] ? 2 : 1;
     if (k < 16) {
-        if (k < kFastPx && k < g.W) color1_zune(g, k, y, o + 3 * k);
+        if (k < kFastPx && k < g.W) color1_fast(g, fv, k, y, o + 3 * k);
         return;
     }
     const int lim = 2 * g.bw[1] * 8 - 2;  // as color_ends<kFastPx>
@@ -366,10 +397,10 @@ __global__ __launch_bounds__(256) void k_jpeg_color_ends_b(const JpegReconItem* 
     const int xc = xm < kFastPx ? kFastPx : (xm & ~(kFastPx - 1)) + kFastPx;
     const int x = xc + (k - 16);
     if (k < 31) {
-        if (x < g.W) color1_zune(g, x, y, o + 3 * x);
+        if (x < g.W) color1_fast(g, fv, x, y, o + 3 * x);
         return;
     }
-    for (int xx = x; xx < g.W; ++xx) color1_zune(g, xx, y, o + 3 * xx);
+    for (int xx = x; xx < g.W; ++xx) color1_fast(g, fv, xx, y, o + 3 * xx);
 }
 
 // ---- the batch's zune_fast images: eight pixels by kFastRows rows per thread ----

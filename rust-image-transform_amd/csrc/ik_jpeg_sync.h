@@ -130,16 +130,12 @@ IK_HD int lane_interval(const Scan& S, int r) {
 // MSB-first reader over the unstuffed words; bits at or past `end` read as zero
 // (the interval's end: the host decoder feeds zeros at a marker)
 // (a block never advances more than 27 bits between two peeks, so the window
-// moves one word at a time.  The three words after the window are held in
-// registers and the next one is loaded three advances before it is needed: a
-// memory wait also waits for every earlier store (the decode pass's block
-// stores), so a load one word ahead stalled the lane behind the stores of the
-// block before.  The scans' kPadWords zero words cover the reads past the end.)
+// moves one word at a time, and the word after it is loaded a step ahead)
 struct Bits {
     const IK_GLOBAL uint32_t* w;
     uint64_t pos, end;
-    uint64_t buf;            // words [idx, idx + 1]
-    uint32_t n0, n1, n2;     // words idx + 2 .. idx + 4
+    uint64_t buf;  // words [idx, idx + 1]
+    uint32_t nxt;  // word idx + 2
     long long idx;
     IK_HD void init(const IK_GLOBAL uint32_t* words, uint64_t p, uint64_t e) {
         w = words;
@@ -147,24 +143,17 @@ struct Bits {
         end = e;
         idx = (long long)(p >> 5);
         buf = (uint64_t)w[idx] << 32 | w[idx + 1];
-        n0 = w[idx + 2];
-        n1 = w[idx + 3];
-        n2 = w[idx + 4];
+        nxt = w[idx + 2];
     }
     IK_HD uint32_t peek32() {
         const long long i = (long long)(pos >> 5);
         if (i != idx) {
             if (i == idx + 1) {
-                buf = buf << 32 | n0;
-                n0 = n1;
-                n1 = n2;
-                n2 = w[i + 4];
+                buf = buf << 32 | nxt;
             } else {
                 buf = (uint64_t)w[i] << 32 | w[i + 1];
-                n0 = w[i + 2];
-                n1 = w[i + 3];
-                n2 = w[i + 4];
             }
+            nxt = w[i + 2];
             idx = i;
         }
         uint32_t v = (uint32_t)((buf << (pos & 31)) >> 32);

@@ -127,7 +127,10 @@ __device__ __forceinline__ void horizontal_rows(const ResizeArgs& a, const float
     case 4:
         horizontal_rows_c<4, FMA>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst);
         break;
-    case 3: horizontal_rows_c<3, FMA>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
+    case 3:  // four taps per iteration: twelve LDS reads in flight (6.48 -> 6.14 ms per 256 RGB 4096^2 -> 512^2
+             // Lanczos3 launches, profiles/r04u_resize_horizontal_variants.txt; RGBA measured better at two)
+        horizontal_rows_c<3, FMA, 4>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst);
+        break;
     case 2: horizontal_rows_c<2, FMA>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
     default: horizontal_rows_c<1, FMA>(a, lds, sw, soff, r0, nrows, ox0, nox, hq, hox, dst); break;
     }

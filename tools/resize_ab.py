@@ -40,4 +40,6 @@ for filt, name in ((1, "triangle"), (4, "lanczos3")):
         if r:
             ms.append(e0.elapsed_time(e1))
     res[name] = round(float(np.median(ms)), 4)
+    flat = dst.view(-1).to(torch.int64)
+    res[name + "_sum"] = int((flat * (torch.arange(flat.numel(), device="cuda") % 251 + 1)).sum().item())
 print(json.dumps({"lib": sys.argv[1], "C": C, "B": B, **res}))
