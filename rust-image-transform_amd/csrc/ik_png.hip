@@ -198,13 +198,8 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
                 const uint64_t x = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;   // bits p .. p+63
                 const uint64_t x2 = sh ? (hi >> sh) : hi;                        // bits p+64 ..
                 const uint64_t cl = (x >> 17) | (x2 << 47);
-#ifdef IK_FIND_NOCHECK  // dev experiment: the scan alone (every Kraft survivor taken)
-                (void)x; (void)cl;
-                v = off;
-#else
                 if (find_check_win(W, I.nbits, p, (uint32_t)x, cl, (lds_word*)(s_win + lane)))
                     v = off;
-#endif
             }
             v = wave_min(v);
             best = v < best ? v : best;
@@ -260,11 +255,7 @@ __global__ __launch_bounds__(64) void k_png_find(const PngImgDev* imgs, const in
             }
             qlen += (uint32_t)__popcll(bal);
         }
-#ifdef IK_FIND_FLUSH_AT  // dev experiment: check the queue as soon as it holds this many
-        if (qlen >= IK_FIND_FLUSH_AT) flush(false);
-#else
         if (qlen >= 64) flush(false);
-#endif
         if (best != 0xFFFFFFFFu) break;  // any header that passes will do (the decode chain checks it)
         wi = wn;
         if (wi - (uint64_t)lane >= wlast) break;
@@ -603,11 +594,7 @@ __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const
                 } else if (sr >= -kXNear) {
                     v = s_ring[(gb + (uint32_t)sr) & M];
                 } else {
-#ifdef IK_X4_NOFAR  // dev experiment (wrong output): far sources from the ring, to bound their cost
-                    v = s_ring[(gb + (uint32_t)sr) & M];
-#else
                     v = U[ob + ab];
-#endif
                 }
                 s_ring[(gb + o + j) & M] = v;
             }
