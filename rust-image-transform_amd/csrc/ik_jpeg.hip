@@ -64,10 +64,28 @@ __device__ __forceinline__ void idct_block(const JpegGeom& g, long long blk) {
     idct_islow(in, out, pw);
 }
 
+// the first pixel column past a zune_fast image's interior groups of eight
+// (k_jpeg_color_fast_b takes x0 in [8, xc), k_jpeg_color_ends_b the rest)
+__device__ __forceinline__ int fast_xc(const JpegGeom& g) {
+    const int lim = 2 * g.bw[1] * 8 - 2;
+    const int xm = (g.W - 8 < lim - 8 ? g.W - 8 : lim - 8);
+    return xm < 8 ? 8 : (xm & ~7) + 8;
+}
+
 __global__ __launch_bounds__(256) void k_jpeg_idct(JpegGeom g) { idct_block(g, (long long)blockIdx.x * 256 + threadIdx.x); }
 // the batch's images in one launch: blockIdx.y = image
 __global__ __launch_bounds__(256) void k_jpeg_idct_b(const JpegReconItem* __restrict__ items) {
-    idct_block(items[blockIdx.y].g, (long long)blockIdx.x * 256 + threadIdx.x);
+    const JpegReconItem& it = items[blockIdx.y];
+    const long long blk = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (it.fast && blk < it.g.blk0[1]) {
+        // a zune_fast image's luma blocks in the interior columns are k_jpeg_color_fast_b's own
+        // (its groups x0 in [8, xc) step 8 are block columns 1 .. xc/8 - 1; the row ends'
+        // columns stay here, for k_jpeg_color_ends_b)
+        const JpegGeom& g = it.g;
+        const int bx = (int)(blk % g.bw[0]);
+        if (bx >= 1 && bx < fast_xc(g) / 8) return;
+    }
+    idct_block(it.g, blk);
 }
 
 // upsampled sample of component ci at output pixel (x, y)
@@ -392,9 +410,7 @@ __global__ __launch_bounds__(256) void k_jpeg_color_ends_b(const JpegReconItem* 
         if (k < kFastPx && k < g.W) color1_fast(g, fv, k, y, o + 3 * k);
         return;
     }
-    const int lim = 2 * g.bw[1] * 8 - 2;  // as color_ends<kFastPx>
-    const int xm = (g.W - kFastPx < lim - kFastPx ? g.W - kFastPx : lim - kFastPx);
-    const int xc = xm < kFastPx ? kFastPx : (xm & ~(kFastPx - 1)) + kFastPx;
+    const int xc = fast_xc(g);
     const int x = xc + (k - 16);
     if (k < 31) {
         if (x < g.W) color1_fast(g, fv, x, y, o + 3 * x);
@@ -413,6 +429,7 @@ __global__ __launch_bounds__(256) void k_jpeg_color_ends_b(const JpegReconItem* 
 // i = x0 / 2: the samples i-1 .. i+4 the eight pixels use), and two 12-byte
 // stores.  The arithmetic is color4_zune's (upsampler/scalar.rs vertical then
 // horizontal (3 near + far + 2) >> 2, color_convert/scalar.rs i16 YCbCr).
+constexpr int kFastRowsT = 16;  // rows per thread (two luma blocks)
 typedef __attribute__((address_space(1))) uint8_t g8;
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
@@ -464,7 +481,46 @@ __device__ __forceinline__ void color8_row(u32x2 yv, const u32x3 (&s)[2], const 
     *reinterpret_cast<u32x3 __attribute__((address_space(1)))*>(o + 12) = hi;
 }
 
-template <int FV>
+// the luma IDCT's rows into registers (k_jpeg_color_fast_b with LI): idct_zune's
+// row stores through this sink land in v[2 r], v[2 r + 1] (constant indices once
+// unrolled, so the block stays in VGPRs)
+struct RegRow {
+    uint32_t* v;
+};
+struct RegSink {
+    uint32_t* v;
+    __device__ RegRow operator+(size_t off) const { return RegRow{v + 2 * (off >> 3)}; }
+};
+__device__ __forceinline__ void store8(RegRow p, uint32_t lo, uint32_t hi) {
+    p.v[0] = lo;
+    p.v[1] = hi;
+}
+
+// luma block (bx, by) of g: dequantised and through zune's IDCT into yr[0..15]
+__device__ __forceinline__ void luma_idct(const JpegGeom& g, int bx, int by, uint32_t (&yr)[16]) {
+    const long long blk = g.blk0[0] + (long long)by * g.bw[0] + bx;
+    const int4* cp = reinterpret_cast<const int4*>(g.coef + blk * 64);
+    const __attribute__((address_space(4))) uint16_t* q = (const __attribute__((address_space(4))) uint16_t*)g.qt;
+    int in[64];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int4 v = cp[i];
+        const int w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = i * 8 + 2 * j;
+            in[k] = (int)(int16_t)(w[j] & 0xffff) * (int)q[k];
+            in[k + 1] = (int)(int16_t)((unsigned)w[j] >> 16) * (int)q[k + 1];
+        }
+    }
+    idct_zune(in, RegSink{yr}, 8);
+}
+
+// LI: the luma rows come from the thread's own IDCT of its two luma blocks (8 x 16
+// pixels = blocks (x0/8, y0/8) and (x0/8, y0/8 + 1)) instead of the luma plane:
+// k_jpeg_idct_b leaves those blocks to this kernel, and the plane's write and read
+// (a third of the reconstruction's bytes) are not made
+template <int FV, bool LI>
 __device__ __forceinline__ void color_fast_rows(const JpegGeom& g, g8* __restrict__ dst, size_t pitch, int x0, int y0,
                                                 int y1) {
     const int nY = g.bw[0] * 8, n = g.bw[1] * 8, ph = g.bh[1] * 8;
@@ -475,29 +531,38 @@ __device__ __forceinline__ void color_fast_rows(const JpegGeom& g, g8* __restric
         r = r < 0 ? 0 : (r >= ph ? ph - 1 : r);
         return *reinterpret_cast<const u32x3 __attribute__((address_space(1)))*>(cp[c] + (size_t)r * n);
     };
-    auto ldy = [&](int y) -> u32x2 {
-        return *reinterpret_cast<const u32x2 __attribute__((address_space(1)))*>(yp + (size_t)y * nY);
+    uint32_t yr[2][16];
+    if (LI) {
+        luma_idct(g, x0 >> 3, y0 >> 3, yr[0]);
+        if (y0 + 8 < y1) luma_idct(g, x0 >> 3, (y0 >> 3) + 1, yr[1]);
+    }
+    // row rr (0 .. 15) of the thread's band: registers (LI, rr constant once unrolled) or the plane
+    auto ldy = [&](int rr) -> u32x2 {
+        if (LI) return u32x2{yr[rr >> 3][2 * (rr & 7)], yr[rr >> 3][2 * (rr & 7) + 1]};
+        return *reinterpret_cast<const u32x2 __attribute__((address_space(1)))*>(yp + (size_t)(y0 + rr) * nY);
     };
     g8* o = dst + (size_t)y0 * pitch + (size_t)3 * x0;
     if (FV == 2) {
         // y0 even: rows 2Y and 2Y+1 share chroma row Y (far rows Y-1 and Y+1)
         int Y = y0 >> 1;
         u32x3 up[2] = {ldc(0, Y - 1), ldc(1, Y - 1)}, mid[2] = {ldc(0, Y), ldc(1, Y)};
-        for (int y = y0; y < y1; y += 2, ++Y) {
+#pragma unroll
+        for (int rr = 0; rr < kFastRowsT; rr += 2, ++Y) {
+            if (y0 + rr >= y1) break;
             const u32x3 dn[2] = {ldc(0, Y + 1), ldc(1, Y + 1)};
-            const u32x2 ya = ldy(y);
-            const u32x2 yb = ldy(y + 1 < y1 ? y + 1 : y);
-            color8_row<2>(ya, mid, up, o);
+            color8_row<2>(ldy(rr), mid, up, o);
             o += pitch;
-            if (y + 1 < y1) color8_row<2>(yb, mid, dn, o);
+            if (y0 + rr + 1 < y1) color8_row<2>(ldy(rr + 1), mid, dn, o);
             o += pitch;
             up[0] = mid[0]; up[1] = mid[1];
             mid[0] = dn[0]; mid[1] = dn[1];
         }
     } else {
-        for (int y = y0; y < y1; ++y) {
-            const u32x3 c[2] = {ldc(0, y), ldc(1, y)};
-            color8_row<1>(ldy(y), c, c, o);
+#pragma unroll
+        for (int rr = 0; rr < kFastRowsT; ++rr) {
+            if (y0 + rr >= y1) break;
+            const u32x3 c[2] = {ldc(0, y0 + rr), ldc(1, y0 + rr)};
+            color8_row<1>(ldy(rr), c, c, o);
             o += pitch;
         }
     }
@@ -505,7 +570,8 @@ __device__ __forceinline__ void color_fast_rows(const JpegGeom& g, g8* __restric
 
 // grid: (column groups of 8 x 256, row bands of kFastRows, image); the interior
 // groups only (x0 >= 8, x0 + 8 <= W, x0 + 7 < 2n - 2), k_jpeg_color_ends_b the rest
-constexpr int kFastRows = 16;
+constexpr int kFastRows = kFastRowsT;
+template <bool LI>
 __global__ __launch_bounds__(256) void k_jpeg_color_fast_b(const JpegReconItem* __restrict__ items) {
     const JpegReconItem& it = items[blockIdx.z];
     if (!it.fast) return;
@@ -515,8 +581,8 @@ __global__ __launch_bounds__(256) void k_jpeg_color_fast_b(const JpegReconItem* 
     if (y0 >= g.H || x0 < kFastPx || x0 + kFastPx > g.W || x0 + kFastPx - 1 >= 2 * g.bw[1] * 8 - 2) return;
     const int y1 = y0 + kFastRows < g.H ? y0 + kFastRows : g.H;
     g8* dst = (g8*)it.dst;
-    if (g.vmax == 2 * g.v[1]) color_fast_rows<2>(g, dst, it.pitch, x0, y0, y1);
-    else color_fast_rows<1>(g, dst, it.pitch, x0, y0, y1);
+    if (g.vmax == 2 * g.v[1]) color_fast_rows<2, LI>(g, dst, it.pitch, x0, y0, y1);
+    else color_fast_rows<1, LI>(g, dst, it.pitch, x0, y0, y1);
 }
 
 }  // namespace
@@ -784,9 +850,9 @@ hipError_t launch_jpeg_reconstruct_batch(const JpegReconItem* items, int m, long
         hipLaunchKernelGGL(k_jpeg_color_b, dim3((max_w + 1023) / 1024, (max_h + kColorRows - 1) / kColorRows, m),
                            dim3(256), 0, s, items);
     if (any_fast) {
-        hipLaunchKernelGGL(k_jpeg_color_fast_b,
-                           dim3((max_w + 256 * kFastPx - 1) / (256 * kFastPx), (max_h + kFastRows - 1) / kFastRows, m),
-                           dim3(256), 0, s, items);
+        const dim3 gf((max_w + 256 * kFastPx - 1) / (256 * kFastPx), (max_h + kFastRows - 1) / kFastRows, m);
+        if (idct) hipLaunchKernelGGL(k_jpeg_color_fast_b<true>, gf, dim3(256), 0, s, items);
+        else hipLaunchKernelGGL(k_jpeg_color_fast_b<false>, gf, dim3(256), 0, s, items);
         hipLaunchKernelGGL(k_jpeg_color_ends_b, dim3((32 * max_h + 255) / 256, m), dim3(256), 0, s, items);
     }
     return hipGetLastError();
