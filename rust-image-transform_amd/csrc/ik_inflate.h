@@ -701,11 +701,16 @@ IK_HD int canon_len(uint32_t c15, const uint32_t (&pk)[8]) {
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef short s2 __attribute__((ext_vector_type(2)));
     const s2 x = {(short)c15, (short)c15};
+    uint32_t d[7];
     IK_UNROLL
-    for (int k = 0; k < 7; ++k) {
-        const s2 d = __builtin_bit_cast(s2, pk[k]) - x;  // lim - 1 - c15 < 0  <=>  lim <= c15
-        at_or_below += (uint32_t)__builtin_popcount(__builtin_bit_cast(uint32_t, d) & 0x80008000u);
-    }
+    for (int k = 0; k < 7; ++k)
+        d[k] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(s2, pk[k]) - x);  // lim - 1 - c15 < 0  <=>  lim <= c15
+    // the sign bits sit in bytes 1 and 3: v_perm_b32 gathers those bytes of two
+    // differences into one word, so one AND and one popcount count four limits
+    IK_UNROLL
+    for (int k = 0; k < 6; k += 2)
+        at_or_below += (uint32_t)__builtin_popcount(__builtin_amdgcn_perm(d[k], d[k + 1], 0x07050301u) & 0x80808080u);
+    at_or_below += (uint32_t)__builtin_popcount(d[6] & 0x80008000u);
 #else
     for (int k = 0; k < 7; ++k) {
         at_or_below += (int16_t)(pk[k] & 0xFFFFu) - (int)c15 < 0 ? 1u : 0u;
