@@ -79,8 +79,20 @@ void ik_schedule_plan(const uint64_t *costs, uint32_t n, uint32_t ndev, const ui
  * to destructors running at process exit.  Call it once before exit (the Python
  * package registers it with atexit; the Rust shim calls it from Drop of its
  * runtime guard).  Images, pipelines and buffers the caller still holds must be
- * freed first; the library may be used again afterwards (ik_init). */
+ * freed first; the library may be used again afterwards (ik_init).  Callers
+ * still inside the library on other threads return first: every entry point
+ * holds the library's lifetime lock shared, teardown takes it exclusively. */
 int ik_shutdown(void);
+/* ik_shutdown for process exit, when threads of the caller (a server's daemon
+ * request threads) may still call in: afterwards every entry point that does
+ * device work returns IK_ERR_INVALID ("closed") instead of bringing the library
+ * back up.  The Python package registers this one with atexit. */
+int ik_close(void);
+/* bytes the library holds, by pool (n <= 7 values): [0] device image blocks in
+ * use, [1] image blocks kept free for reuse, [2] per-thread device arenas, [3]
+ * per-thread pinned arenas, [4] upload areas (device), [5] upload areas (pinned),
+ * [6] cached resize plans' device tables */
+int ik_memory_stats(uint64_t *out, int n);
 size_t ik_last_error(char *buf, size_t cap); /* thread-local message of the last failure */
 const char *ik_version(void);
 
@@ -117,20 +129,23 @@ int ik_host_unregister(void *p);               /* the start of a registered rang
  * *fmt_out = IK_FORMAT_* for webp/jpeg/avif, -1 (None) for other formats. */
 int ik_decode(const uint8_t *bytes, size_t len, ik_image **out, int *fmt_out);
 
-/* decode_image over n inputs at once (the /img handler under load).  JPEGs whose
- * scan has restart intervals are entropy-decoded by ONE GPU launch (one lane per
- * interval, all images together) and reconstructed on the GPU; other inputs go
- * through ik_decode.  outs[i] / fmts[i] / status[i] per input (outs[i] NULL on
- * failure; fmts and status may be NULL); returns the first failure or IK_OK. */
+/* decode_image over n inputs at once (the /img handler under load).  Baseline
+ * JPEG scans (with or without restart markers) are entropy-decoded together by
+ * the self-synchronising GPU decoder (a few launches for the whole batch) and
+ * reconstructed on the GPU; PNG streams go through the batched GPU inflate; other
+ * inputs through ik_decode.  outs[i] / fmts[i] / status[i] per input (outs[i]
+ * NULL on failure; fmts and status may be NULL); returns the first failure or
+ * IK_OK. */
 int ik_decode_batch(const uint8_t *const *bytes, const size_t *lens, uint32_t n, ik_image **outs,
                     int *fmts, int *status);
 
 /* PNG decoding on the GPU (ik_decode / ik_decode_batch / ik_transform*): streams
  * whose filtered image data is at least min_raw_bytes are inflated and unfiltered
  * on the GPU (parallel DEFLATE over block-start candidates, row-wavefront
- * unfilter); smaller ones, palette / tRNS / interlaced / 16-bit streams and any
- * the GPU finds inconsistent use the host decoder.  -1 = host decoder only.
- * Default 256 KiB (IK_PNG_GPU_MIN; IK_PNG_GPU=0 = off). */
+ * unfilter), every non-interlaced colour type included (palette, low bit depths,
+ * tRNS, 16-bit); smaller ones, interlaced (Adam7) streams and any the GPU finds
+ * inconsistent use the host decoder.  -1 = host decoder only.  Default 256 KiB
+ * (IK_PNG_GPU_MIN; IK_PNG_GPU=0 = off). */
 int ik_set_png_gpu_min(long long min_raw_bytes);
 /* the last GPU PNG batch finished on the calling thread's device (n <= 17 values):
  * [0] upload stage host ms (parse, staging copies of unpinned inputs, DMA issue),
@@ -145,11 +160,13 @@ int ik_set_png_gpu_min(long long min_raw_bytes);
 int ik_png_last_timing(double *out, int n);
 /* the last batch the calling thread's device ran through its kernel stage
  * (ik_transform_batch*): device ms from HIP events on the kernel stream and the
- * algorithmic bytes of the same launches (n <= 10 values): [0] JPEG entropy
+ * algorithmic bytes of the same launches (n <= 13 values): [0] JPEG entropy
  * decoding ms, [1] entropy-coded bytes read, [2] int16 coefficient bytes written,
  * [3] images, [4] decoder lanes; [5] grouped resize ms, [6] resize bytes (C*W*H
  * in + C*w*h out per image), [7] images resized in groups; [8] batched JPEG
- * encoder ms (coefficients + Huffman), [9] images it coded */
+ * encoder ms (coefficients + Huffman), [9] images it coded; the host coder stage
+ * (libwebp / libavif on the worker pool): [10] wall ms of the batch, [11] thread
+ * CPU ms summed over its requests (core-ms), [12] requests it coded */
 int ik_batch_last_timing(double *out, int n);
 /* process-wide counts of PNG streams decoded since load: out[0] by the GPU path,
  * out[1] by the host decoder (outside the GPU path, or rejected by it) */
@@ -216,8 +233,9 @@ int ik_transform(const uint8_t *bytes, size_t len, int64_t w, int64_t h, int fmt
                  int filter, uint8_t **out, size_t *out_len);
 
 /* ik_transform over n requests at once (the /img handler under load, loadtest C4
- * mix): decode_image (one set of GPU launches for the batch's PNG streams, one GPU
- * entropy launch for its restart-interval JPEGs), one resize launch per group of
+ * mix): decode_image (one set of GPU launches for the batch's PNG streams, one set
+ * of self-synchronising entropy launches for its baseline JPEGs), one resize launch
+ * per group of
  * same-geometry requests, encode_image (device front ends; libwebp / libavif on
  * `threads` host threads, 0 = default).  w/h (-1 = None), fmt and quality per
  * request; outs[i] (ik_buf_free) / out_lens[i] / status[i] per request (status
@@ -227,12 +245,13 @@ int ik_transform_batch(const uint8_t *const *bytes, const size_t *lens, uint32_t
                        const int64_t *h, const int *fmt, const int *quality, int filter, int threads,
                        uint8_t **outs, size_t *out_lens, int *status);
 
-/* ik_transform_batch as two calls.  Each device runs batches through three
- * stages on their own threads -- upload (the PNG files' DMA, in place when the
- * caller pinned them, then a GPU pass that assembles the zlib streams and checks
- * the IDAT CRCs), kernels (decode, resize, the encoders' device front ends) and
- * host coders (the device's worker pool) -- so consecutive batches overlap: batch
- * k+1's upload runs under batch k's kernels, batch k's libwebp beside both.
+/* ik_transform_batch as two calls.  Each device runs batches through four
+ * stages on their own threads -- upload (the PNG / JPEG files' DMA, in place when
+ * the caller pinned them, then a GPU pass that assembles the zlib streams and
+ * checks the IDAT CRCs), decode kernels, post (resize and the encoders' device
+ * front ends) and host coders (the device's worker pool) -- so consecutive
+ * batches overlap: batch k+1's upload runs under batch k's kernels, batch k's
+ * resize beside batch k+1's decode, batch k's libwebp beside both.
  * submit queues the batch and returns at once; wait blocks until its bytes are
  * ready, fills status[] (may be NULL) and returns the first failure, as
  * ik_transform_batch does.  Every array passed to submit -- the inputs included

@@ -8,12 +8,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <map>
 #include <tuple>
 #include <condition_variable>
@@ -88,9 +90,13 @@ struct ThreadRes {
             if (!kv.second.p) continue;
             (void)hipSetDevice(kv.second.device);
             (void)hipFree(kv.second.p);
+            mem_stat(kMemArenaDev, -(int64_t)kv.second.cap);
         }
         for (Arena& a : pinned)
-            if (a.p) (void)hipHostFree(a.p);
+            if (a.p) {
+                (void)hipHostFree(a.p);
+                mem_stat(kMemArenaPinned, -(int64_t)a.cap);
+            }
         for (auto& kv : streams) (void)hipStreamDestroy(kv.second);
         for (auto& kv : copy_streams) (void)hipStreamDestroy(kv.second);
         streams.clear();
@@ -116,12 +122,76 @@ namespace {
 std::mutex g_bt_mu;
 // per device: the batches in the decode and post stages, the last one finished
 std::map<int, std::vector<double>> g_bt_dec, g_bt_post, g_bt_last;
-bool bt_post_field(int f) { return f >= kBtResizeMs; }
+bool bt_post_field(int f) { return f >= kBtResizeMs && f < kBtHostWallMs; }
+bool bt_host_field(int f) { return f >= kBtHostWallMs; }
+thread_local bool t_bt_active = false;  // inside a stage's batch (BatchTimingScope)
+// per device (an event records only on its own device's streams); the events are
+// left to the runtime: a thread-exit destructor may run at process exit
 struct ThreadEvents {
-    EvPair p[4];
-    ~ThreadEvents() {}  // (events are left to the runtime: a thread-exit destructor may run at process exit)
+    std::map<int, std::array<EvPair, 4>> p;
 };
+
+// the lifetime lock (ApiGuard): shared by callers, exclusive for teardown, and
+// writer-preferring -- a waiting teardown holds back new callers, so callers that
+// keep calling (a server's request threads) cannot starve it
+struct LifeLock {
+    std::mutex mu;
+    std::condition_variable cv;
+    int readers = 0, writers_waiting = 0;
+    bool writer = false;
+    void lock_shared() {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return !writer && writers_waiting == 0; });
+        ++readers;
+    }
+    void unlock_shared() {
+        std::lock_guard<std::mutex> lk(mu);
+        if (--readers == 0) cv.notify_all();
+    }
+    void lock() {
+        std::unique_lock<std::mutex> lk(mu);
+        ++writers_waiting;
+        cv.wait(lk, [&] { return !writer && readers == 0; });
+        --writers_waiting;
+        writer = true;
+    }
+    void unlock() {
+        std::lock_guard<std::mutex> lk(mu);
+        writer = false;
+        cv.notify_all();
+    }
+};
+LifeLock g_life;
+std::atomic<bool> g_closed{false};
+thread_local int t_api_depth = 0;
+thread_local bool t_internal = false;
 }  // namespace
+
+ApiGuard::ApiGuard() {
+    if (t_internal) return;
+    if (t_api_depth++ == 0) {
+        g_life.lock_shared();
+        held = true;
+    }
+    closed = g_closed.load(std::memory_order_acquire);
+}
+ApiGuard::~ApiGuard() {
+    if (t_internal) return;
+    if (--t_api_depth == 0 && held) g_life.unlock_shared();
+}
+void mark_internal_thread() { t_internal = true; }
+
+namespace {
+std::atomic<int64_t> g_mem[kMemStats];
+}  // namespace
+void mem_stat(int which, int64_t delta) { g_mem[which].fetch_add(delta, std::memory_order_relaxed); }
+
+BatchTimingScope::BatchTimingScope() : prev(t_bt_active) { t_bt_active = true; }
+BatchTimingScope::~BatchTimingScope() { t_bt_active = prev; }
+
+void ev_record(hipEvent_t e, hipStream_t s) {
+    if (e && hipEventRecord(e, s) != hipSuccess) (void)hipGetLastError();
+}
 
 void batch_timing_reset(int device, bool post) {
     std::lock_guard<std::mutex> lk(g_bt_mu);
@@ -134,9 +204,18 @@ void batch_timing_commit(int device, bool post) {
     src.resize(kBtFields, 0.0);
     dst.resize(kBtFields, 0.0);
     for (int f = 0; f < kBtFields; ++f)
-        if (bt_post_field(f) == post) dst[(size_t)f] = src[(size_t)f];
+        if (!bt_host_field(f) && bt_post_field(f) == post) dst[(size_t)f] = src[(size_t)f];
+}
+void batch_timing_host(int device, double wall_ms, double core_ms, double images) {
+    std::lock_guard<std::mutex> lk(g_bt_mu);
+    std::vector<double>& dst = g_bt_last[device];
+    dst.resize(kBtFields, 0.0);
+    dst[kBtHostWallMs] = wall_ms;
+    dst[kBtHostCoreMs] = core_ms;
+    dst[kBtHostImages] = images;
 }
 void batch_timing_add(int device, int field, double v) {
+    if (!t_bt_active) return;
     std::lock_guard<std::mutex> lk(g_bt_mu);
     std::vector<double>& t = (bt_post_field(field) ? g_bt_post : g_bt_dec)[device];
     if (t.size() < (size_t)kBtFields) t.resize(kBtFields, 0.0);
@@ -144,7 +223,7 @@ void batch_timing_add(int device, int field, double v) {
 }
 EvPair& thread_events(int which) {
     static thread_local ThreadEvents te;
-    EvPair& e = te.p[which & 3];
+    EvPair& e = te.p[current_device()][which & 3];
     if (!e.a && hipEventCreate(&e.a) != hipSuccess) e.a = nullptr;
     if (!e.b && hipEventCreate(&e.b) != hipSuccess) e.b = nullptr;
     return e;
@@ -187,6 +266,7 @@ uint8_t* pinned_slot(int slot, size_t bytes) {
         auto cs = tres().copy_streams.find(current_device());
         if (cs != tres().copy_streams.end()) (void)hipStreamSynchronize(cs->second);
         (void)hipHostFree(a.p);
+        mem_stat(kMemArenaPinned, -(int64_t)a.cap);
     }
     a.p = nullptr;
     a.cap = 0;
@@ -198,6 +278,7 @@ uint8_t* pinned_slot(int slot, size_t bytes) {
         return nullptr;
     }
     a.cap = want;
+    mem_stat(kMemArenaPinned, (int64_t)want);
     return a.p;
 }
 
@@ -265,6 +346,7 @@ uint8_t* scratch_slot(int slot, size_t bytes) {
     if (a.p) {
         (void)hipStreamSynchronize(thread_stream());
         (void)hipFree(a.p);
+        mem_stat(kMemArenaDev, -(int64_t)a.cap);
     }
     a.p = nullptr;
     a.cap = 0;
@@ -273,6 +355,7 @@ uint8_t* scratch_slot(int slot, size_t bytes) {
     (void)hipSetDevice(d);
     if (hipMalloc((void**)&a.p, want) != hipSuccess) return nullptr;
     a.cap = want;
+    mem_stat(kMemArenaDev, (int64_t)want);
     return a.p;
 }
 
@@ -325,6 +408,7 @@ int alloc_image(uint32_t w, uint32_t h, uint32_t c, ik_image** out, uint32_t dep
             img->block = it->first;
             pool.held -= it->first;
             pool.free_blocks.erase(it);
+            mem_stat(kMemImageFree, -(int64_t)img->block);
         }
     }
     if (!img->d) {
@@ -332,6 +416,7 @@ int alloc_image(uint32_t w, uint32_t h, uint32_t c, ik_image** out, uint32_t dep
         if (e != hipSuccess) { delete img; return hip_fail(e, "hipMalloc(image)"); }
         img->block = need;
     }
+    mem_stat(kMemImageLive, (int64_t)img->block);
     *out = img;
     return IK_OK;
 }
@@ -623,6 +708,7 @@ int ik_device_count(void) {
 }
 
 int ik_init(int device) {
+    IK_API_ENTER();
     int n = 0;
     IK_HIP(hipGetDeviceCount(&n));
     if (device >= n) return fail(IK_ERR_INVALID, "device %d out of range (%d devices)", device, n);
@@ -637,6 +723,7 @@ int ik_init(int device) {
 }
 
 int ik_init_devices(const int* devices, int n) {
+    IK_API_ENTER();
     if (!devices || n <= 0) return fail(IK_ERR_INVALID, "empty device list");
     if (int rc = sched_configure(devices, n)) return rc;
     return ik_init(sched_phys(0));
@@ -645,6 +732,7 @@ int ik_init_devices(const int* devices, int n) {
 int ik_logical_device_count(void) { return sched_multi() ? sched_count() : 0; }
 
 int ik_logical_device_stats(uint32_t logical, uint64_t* jobs, uint64_t* cost_done, uint64_t* outstanding) {
+    IK_API_ENTER();
     if (!sched_multi()) return fail(IK_ERR_INVALID, "multi-device dispatch is not enabled");
     return sched_stats(logical, jobs, cost_done, outstanding);
 }
@@ -661,6 +749,7 @@ void ik_schedule_plan(const uint64_t* costs, uint32_t n, uint32_t ndev, const ui
 
 int ik_image_from_host(const uint8_t* pixels, uint32_t width, uint32_t height, uint32_t channels,
                        ik_image** out) {
+    IK_API_ENTER();
     if (!out || (!pixels && width && height)) return fail(IK_ERR_INVALID, "null pointer");
     if (channels < 1 || channels > 4) return fail(IK_ERR_INVALID, "channels must be 1..4");
     ik_image* img = nullptr;
@@ -677,6 +766,7 @@ int ik_image_from_host(const uint8_t* pixels, uint32_t width, uint32_t height, u
 
 int ik_image_from_host16(const uint16_t* pixels, uint32_t width, uint32_t height, uint32_t channels,
                          ik_image** out) {
+    IK_API_ENTER();
     if (!out || (!pixels && width && height)) return fail(IK_ERR_INVALID, "null pointer");
     if (channels < 1 || channels > 4) return fail(IK_ERR_INVALID, "channels must be 1..4");
     ik_image* img = nullptr;
@@ -696,6 +786,7 @@ int ik_image_depth(const ik_image* img) { return img ? (int)img->depth : 0; }
 
 int ik_image_wrap_device(uint8_t* dev_pixels, uint32_t width, uint32_t height, uint32_t channels,
                          size_t pitch, ik_image** out) {
+    IK_API_ENTER();
     if (!out || !dev_pixels) return fail(IK_ERR_INVALID, "null pointer");
     if (channels < 1 || channels > 4) return fail(IK_ERR_INVALID, "channels must be 1..4");
     if (pitch < (size_t)width * channels) return fail(IK_ERR_INVALID, "pitch smaller than a row");
@@ -715,6 +806,7 @@ int ik_image_info(const ik_image* img, uint32_t* w, uint32_t* h, uint32_t* c) {
 }
 
 int ik_image_to_host(const ik_image* img, uint8_t* dst, size_t cap) {
+    IK_API_ENTER();
     if (!img || !dst) return fail(IK_ERR_INVALID, "null pointer");
     const size_t row = (size_t)img->w * img->c * img->depth;
     if (cap < row * img->h) return fail(IK_ERR_INVALID, "destination too small");
@@ -724,16 +816,19 @@ int ik_image_to_host(const ik_image* img, uint8_t* dst, size_t cap) {
 }
 
 void ik_image_free(ik_image* img) {
+    IK_API_ENTER_VOID();
     if (!img) return;
     if (img->owned && img->d) {
         ImagePool& pool = image_pool(img->device);
         bool kept = false;
         if (img->block) {
+            mem_stat(kMemImageLive, -(int64_t)img->block);
             std::lock_guard<std::mutex> lk(pool.mu);
             if (pool.held + img->block <= kPoolBytes) {
                 pool.free_blocks.emplace(img->block, img->d);
                 pool.held += img->block;
                 kept = true;
+                mem_stat(kMemImageFree, (int64_t)img->block);
             }
         }
         if (!kept) {
@@ -748,6 +843,7 @@ void ik_buf_free(uint8_t* buf) { free(buf); }
 
 // imageops::resize(image, nw, nh, filter)
 int ik_resize_exact(const ik_image* img, uint32_t nw, uint32_t nh, int filter, ik_image** out) {
+    IK_API_ENTER();
     if (!img || !out) return fail(IK_ERR_INVALID, "null pointer");
     if (filter < 0 || filter > 4) return fail(IK_ERR_INVALID, "unknown filter %d", filter);
     if (nw == 0 || nh == 0) return fail(IK_ERR_INVALID, "zero output dimension");
@@ -971,7 +1067,7 @@ int jpeg_front_group(const std::vector<ik_image*>& imgs, int quality, std::vecto
         EvPair& ev = thread_events(1);
         hipError_t e = launch_copy_words(reinterpret_cast<const uint32_t*>(dh + p_stage), reinterpret_cast<uint32_t*>(dv),
                                          32, s);
-        if (e == hipSuccess && ev.a) e = hipEventRecord(ev.a, s);
+        if (e == hipSuccess) ev_record(ev.a, s);
         if (e == hipSuccess)
             e = launch_copy_words(reinterpret_cast<const uint32_t*>(dh + p_stage + 256),
                                   reinterpret_cast<uint32_t*>(dv + o_tab), 2 * m, s);
@@ -994,7 +1090,7 @@ int jpeg_front_group(const std::vector<ik_image*>& imgs, int quality, std::vecto
             a.out_len = reinterpret_cast<uint32_t*>(dh + p_len);
             e = launch_jpeg_huff_enc(a, (int)m, s);
         }
-        if (e == hipSuccess && ev.b) e = hipEventRecord(ev.b, s);
+        if (e == hipSuccess) ev_record(ev.b, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_fail(e, "jpeg encode (batched)");
         batch_timing_add(current_device(), kBtJpegEncMs, ev_pair_ms(ev));
@@ -1056,10 +1152,10 @@ int resize_group(const std::vector<ik_image*>& src, uint32_t nw, uint32_t nh, in
     }
     if (!rc) {
         EvPair& ev = thread_events(0);
-        hipError_t e = ev.a ? hipEventRecord(ev.a, s) : hipSuccess;
-        if (e == hipSuccess)
-            e = launch_resize(*plan, nullptr, s0->pitch, 0, nullptr, out[0]->pitch, 0, (int)n, nullptr, s, dtab, dtab + n);
-        if (e == hipSuccess && ev.b) e = hipEventRecord(ev.b, s);
+        ev_record(ev.a, s);
+        hipError_t e = launch_resize(*plan, nullptr, s0->pitch, 0, nullptr, out[0]->pitch, 0, (int)n, nullptr, s, dtab,
+                                     dtab + n);
+        if (e == hipSuccess) ev_record(ev.b, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) rc = hip_fail(e, "resize (batched)");
         if (!rc) {
@@ -1082,6 +1178,7 @@ extern "C" {
 // (nw,nh) == dims -> clone; else resize_dimensions(..., fill=false) (aspect FIT,
 // f64, round, max 1) -> imageops::resize.
 int ik_resize(ik_image* img, int64_t w, int64_t h, int filter, ik_image** out) {
+    IK_API_ENTER();
     if (!img || !out) return fail(IK_ERR_INVALID, "null pointer");
     if (w < 0 && h < 0) { *out = img; return IK_OK; }
     uint32_t nw, nh;
@@ -1091,6 +1188,7 @@ int ik_resize(ik_image* img, int64_t w, int64_t h, int filter, ik_image** out) {
 }
 
 int ik_encode(const ik_image* img, int fmt, int quality, uint8_t** out, size_t* out_len) {
+    IK_API_ENTER();
     if (!img || !out || !out_len) return fail(IK_ERR_INVALID, "null pointer");
     std::vector<uint8_t> bytes;
     EncodePrep prep;
@@ -1235,6 +1333,7 @@ int decode_batch_dev(const uint8_t* const* bytes, const size_t* lens, uint32_t n
 extern "C" {
 
 int ik_decode(const uint8_t* bytes, size_t len, ik_image** out, int* fmt_out) {
+    IK_API_ENTER();
     if (!sched_multi()) return decode_one(bytes, len, out, fmt_out);
     // several devices: the least-loaded one decodes (the image stays there)
     const uint64_t cost = request_cost(bytes, len, -1, -1, IK_FORMAT_JPEG);
@@ -1250,6 +1349,7 @@ int ik_decode(const uint8_t* bytes, size_t len, ik_image** out, int* fmt_out) {
 
 int ik_decode_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t n, ik_image** outs, int* fmts,
                     int* status) {
+    IK_API_ENTER();
     if (!bytes || !lens || !outs || !n) return fail(IK_ERR_INVALID, "bad batch");
     std::vector<int> st(n, IK_OK);
     std::vector<std::string> msg(n);
@@ -1377,6 +1477,7 @@ static void transform_decode_phase(const uint8_t* const* bytes, const size_t* le
     gate_pin(kGateKernels, true);
     const auto tg1 = std::chrono::steady_clock::now();
     batch_timing_reset(current_device(), false);
+    BatchTimingScope bts;
     decode_batch_dev(b.data(), l.data(), m, hp.imgs.data(), nullptr, hp.ds.data(), hp.dm.data(), hp.threads, up,
                      sniff ? sn.data() : nullptr, jup);
     batch_timing_commit(current_device(), false);
@@ -1403,6 +1504,7 @@ static void transform_post_phase(const int64_t* w, const int64_t* h, const int* 
     gate_pin(kGatePost, true);
     gate_enter(kGatePost);
     batch_timing_reset(current_device(), true);
+    BatchTimingScope bts;
     std::mutex tmu;
     double& t_resize = hp.t_resize;
     double& t_front = hp.t_front;
@@ -1496,13 +1598,24 @@ static void transform_host_phase(uint8_t** outs, size_t* out_lens, int* st, std:
     std::vector<std::vector<uint8_t>>& bytes_out = hp.bytes_out;
     std::mutex tmu;
     double t_back = 0;
+    std::atomic<int64_t> cpu_ns{0};  // thread CPU time of the coders (core budget)
+    std::atomic<int> coded{0};
+    const auto tw0 = std::chrono::steady_clock::now();
     const double tg = timing ? std::chrono::duration<double, std::milli>(
                                    std::chrono::steady_clock::now().time_since_epoch()).count() : 0.0;
+    auto thread_cpu_ns = [] {
+        timespec ts{};
+        clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+        return (int64_t)ts.tv_sec * 1000000000ll + ts.tv_nsec;
+    };
     parallel_for((int)m, hp.threads, [&](int k) {
         const uint32_t i = idx[k];
         if (st[i]) return;
         const auto t0 = std::chrono::steady_clock::now();
+        const int64_t c0 = thread_cpu_ns();
+        if (!prep[k].done) coded.fetch_add(1);  // a host coder runs (libwebp / libavif)
         int r = encode_host_back(prep[k], bytes_out[k]);
+        cpu_ns.fetch_add(thread_cpu_ns() - c0);
         std::vector<uint8_t>().swap(prep[k].planes);
         prep[k].pin_block.reset();  // (the batch's pinned plane block goes back to its pool with the last)
         prep[k].pin_planes = nullptr;
@@ -1520,6 +1633,9 @@ static void transform_host_phase(uint8_t** outs, size_t* out_lens, int* st, std:
         }
         if (r) { errs[i] = last_error_str(); st[i] = r; }
     });
+    batch_timing_host(current_device(),
+                      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw0).count(),
+                      (double)cpu_ns.load() * 1e-6, (double)coded.load());
     if (timing)
         fprintf(stderr, "[transform_batch] t=%.1f..%.1f %u requests on device %d: resize %.1f ms, encode front %.1f ms, "
                 "host coders %.1f ms (summed)\n", fmod(tg, 1e5), fmod(std::chrono::duration<double, std::milli>(
@@ -1597,6 +1713,7 @@ public:
 
 private:
     void loop(int stage) {
+        mark_internal_thread();  // the library's own thread: no lifetime lock (ApiGuard)
         ik_init(dev_);  // this thread's streams, staging and scratch live on dev_
         for (;;) {
             std::shared_ptr<BatchPart> p;
@@ -1707,7 +1824,10 @@ static void memory_shutdown() {
         for (auto& kv : g_ipools) {
             std::lock_guard<std::mutex> lk2(kv.second->mu);
             (void)hipSetDevice(kv.first);
-            for (auto& b : kv.second->free_blocks) (void)hipFree(b.second);
+            for (auto& b : kv.second->free_blocks) {
+                (void)hipFree(b.second);
+                mem_stat(kMemImageFree, -(int64_t)b.first);
+            }
             kv.second->free_blocks.clear();
             kv.second->held = 0;
         }
@@ -1732,7 +1852,12 @@ static void memory_shutdown() {
 // ik_shutdown: wait for every submitted batch, end the stage threads and the
 // worker pools (each releases its streams and arenas), then free what the
 // library holds, all while the HIP runtime is alive
-int shutdown_all() {
+int shutdown_all(bool close) {
+    // exclusive: every caller still inside the library returns first (ApiGuard);
+    // nested entry points called from here see depth > 0 and take nothing
+    std::unique_lock<LifeLock> life(g_life);
+    ++t_api_depth;
+    if (close) g_closed.store(true, std::memory_order_release);
     std::vector<std::shared_ptr<Ticket>> ts;
     {
         std::lock_guard<std::mutex> lk(g_async_mu);
@@ -1760,6 +1885,7 @@ int shutdown_all() {
     memory_shutdown();
     release_thread_resources();
     if (dev >= 0) (void)hipSetDevice(dev);
+    --t_api_depth;
     return IK_OK;
 }
 
@@ -1856,6 +1982,7 @@ extern "C" {
 int ik_transform_batch_submit(const uint8_t* const* bytes, const size_t* lens, uint32_t n, const int64_t* w,
                               const int64_t* h, const int* fmt, const int* quality, int filter, int threads,
                               uint8_t** outs, size_t* out_lens, int* status, uint64_t* ticket) {
+    IK_API_ENTER();
     if (!bytes || !lens || !w || !h || !fmt || !quality || !outs || !out_lens || !n || !ticket)
         return fail(IK_ERR_INVALID, "bad batch");
     auto t = new_ticket(n, outs, out_lens, status);
@@ -1866,6 +1993,7 @@ int ik_transform_batch_submit_device(const uint8_t* const* dev_bytes, const size
                                      const int64_t* w, const int64_t* h, const int* fmt, const int* quality,
                                      int filter, int threads, uint8_t** outs, size_t* out_lens, int* status,
                                      uint64_t* ticket) {
+    IK_API_ENTER();
     if (!dev_bytes || !lens || !w || !h || !fmt || !quality || !outs || !out_lens || !n || !ticket)
         return fail(IK_ERR_INVALID, "bad batch");
     // every input must be device memory of one device (the batch runs there)
@@ -1923,7 +2051,14 @@ int ik_transform_batch_submit_device(const uint8_t* const* dev_bytes, const size
     return submit_parts(t, t->eff.data(), t->sniff.data(), phys, lens, n, w, h, fmt, quality, filter, threads, ticket);
 }
 
-int ik_shutdown(void) { return shutdown_all(); }
+int ik_memory_stats(uint64_t* out, int n) {
+    if (!out || n <= 0) return fail(IK_ERR_INVALID, "bad stats buffer");
+    for (int i = 0; i < n; ++i) out[i] = i < kMemStats ? (uint64_t)std::max<int64_t>(0, g_mem[i].load()) : 0;
+    return IK_OK;
+}
+
+int ik_shutdown(void) { return shutdown_all(false); }
+int ik_close(void) { return shutdown_all(true); }
 
 int ik_batch_last_timing(double* out, int n) {
     if (!out || n <= 0) return fail(IK_ERR_INVALID, "bad timing buffer");
@@ -1935,6 +2070,7 @@ int ik_batch_last_timing(double* out, int n) {
 }
 
 int ik_transform_batch_wait(uint64_t ticket) {
+    IK_API_ENTER();
     std::shared_ptr<Ticket> t;
     {
         std::lock_guard<std::mutex> lk(g_async_mu);
@@ -1960,6 +2096,7 @@ int ik_transform_batch_wait(uint64_t ticket) {
 int ik_transform_batch(const uint8_t* const* bytes, const size_t* lens, uint32_t n, const int64_t* w,
                        const int64_t* h, const int* fmt, const int* quality, int filter, int threads, uint8_t** outs,
                        size_t* out_lens, int* status) {
+    IK_API_ENTER();
     uint64_t ticket = 0;
     if (int rc = ik_transform_batch_submit(bytes, lens, n, w, h, fmt, quality, filter, threads, outs, out_lens, status,
                                            &ticket))
@@ -1983,6 +2120,7 @@ static int transform_here(const uint8_t* bytes, size_t len, int64_t w, int64_t h
 
 int ik_transform(const uint8_t* bytes, size_t len, int64_t w, int64_t h, int fmt, int quality,
                  int filter, uint8_t** out, size_t* out_len) {
+    IK_API_ENTER();
     if (!sched_multi()) return transform_here(bytes, len, w, h, fmt, quality, filter, out, out_len);
     // several devices: queue the request to the least-loaded device's workers
     const uint64_t cost = request_cost(bytes, len, w, h, fmt);
@@ -2014,6 +2152,7 @@ int ik_resize_batch_device(const uint8_t* dev_src, uint32_t W, uint32_t H, uint3
                            size_t src_pitch, size_t src_image_stride, uint32_t n, uint32_t nw,
                            uint32_t nh, int filter, uint8_t* dev_dst, size_t dst_pitch,
                            size_t dst_image_stride, void* hip_stream) {
+    IK_API_ENTER();
     if (!dev_src || !dev_dst) return fail(IK_ERR_INVALID, "null device pointer");
     if (C < 1 || C > 4 || !W || !H || !nw || !nh || !n) return fail(IK_ERR_INVALID, "bad geometry");
     if (filter < 0 || filter > 4) return fail(IK_ERR_INVALID, "unknown filter %d", filter);
@@ -2039,6 +2178,7 @@ int ik_resize_batch_device(const uint8_t* dev_src, uint32_t W, uint32_t H, uint3
 
 int ik_webp_yuv420_device(const uint8_t* dev_src, uint32_t w, uint32_t h, uint32_t C, size_t pitch,
                           uint8_t* dev_yuv, void* hip_stream) {
+    IK_API_ENTER();
     if (!dev_src || !dev_yuv || !w || !h || C < 1 || C > 4) return fail(IK_ERR_INVALID, "bad arguments");
     const DeviceConsts* dc = device_consts(current_device());
     if (!dc) return fail(IK_ERR_DEVICE, "cannot upload WebP tables");
@@ -2050,6 +2190,7 @@ int ik_webp_yuv420_device(const uint8_t* dev_src, uint32_t w, uint32_t h, uint32
 
 int ik_jpeg_coeffs_device(const uint8_t* dev_src, uint32_t w, uint32_t h, uint32_t C, size_t pitch,
                           int quality, int16_t* dev_coef, void* hip_stream) {
+    IK_API_ENTER();
     if (!dev_src || !dev_coef || !w || !h || C < 1 || C > 4) return fail(IK_ERR_INVALID, "bad arguments");
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : thread_stream();
     uint8_t qt[128];
@@ -2070,10 +2211,12 @@ int ik_dev_alloc(size_t bytes, void** dev_ptr) {
 }
 int ik_dev_free(void* p) { IK_HIP(hipFree(p)); return IK_OK; }
 int ik_memcpy_h2d(void* d, const void* h, size_t n) {
+    IK_API_ENTER();
     IK_HIP(hipDeviceSynchronize());
     return copy_h2d_2d((uint8_t*)d, n, (const uint8_t*)h, n, n, n ? 1 : 0, thread_stream());
 }
 int ik_memcpy_d2h(void* h, const void* d, size_t n) {
+    IK_API_ENTER();
     IK_HIP(hipDeviceSynchronize());
     return copy_d2h_2d((uint8_t*)h, n, (const uint8_t*)d, n, n, n ? 1 : 0, thread_stream());
 }

@@ -768,14 +768,15 @@ int jpeg_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Jp
     if (!A->ev) return IK_OK;  // (no event: the kernel stage copies the scans itself)
     // grow an idle area (nothing pending reads it: it was handed back after its batch's decode)
     if (total > A->cap) {
-        if (A->dev) (void)hipFree(A->dev);
+        if (A->dev) { (void)hipFree(A->dev); mem_stat(kMemUploadDev, -(int64_t)A->cap); }
         A->dev = nullptr;
         A->cap = 0;
         if (hipMalloc((void**)&A->dev, total + total / 8) != hipSuccess) { A->dev = nullptr; return IK_OK; }
         A->cap = total + total / 8;
+        mem_stat(kMemUploadDev, (int64_t)A->cap);
     }
     if (stotal > A->pin_cap) {
-        if (A->pin) (void)hipHostFree(A->pin);
+        if (A->pin) { (void)hipHostFree(A->pin); mem_stat(kMemUploadPinned, -(int64_t)A->pin_cap); }
         A->pin = nullptr;
         A->pin_cap = 0;
         if (hipHostMalloc((void**)&A->pin, stotal + stotal / 8, hipHostMallocDefault) != hipSuccess) {
@@ -783,6 +784,7 @@ int jpeg_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Jp
             return IK_OK;
         }
         A->pin_cap = stotal + stotal / 8;
+        mem_stat(kMemUploadPinned, (int64_t)A->pin_cap);
     }
     if (stotal)
         parallel_for(n, 0, [&](int i) {
@@ -821,8 +823,8 @@ void jpeg_shutdown() {
         std::lock_guard<std::mutex> lk(P->mu);
         for (JpegArea* a : P->areas) {
             (void)hipSetDevice(a->device);
-            if (a->dev) (void)hipFree(a->dev);
-            if (a->pin) (void)hipHostFree(a->pin);
+            if (a->dev) { (void)hipFree(a->dev); mem_stat(kMemUploadDev, -(int64_t)a->cap); }
+            if (a->pin) { (void)hipHostFree(a->pin); mem_stat(kMemUploadPinned, -(int64_t)a->pin_cap); }
             if (a->ev) (void)hipEventDestroy(a->ev);
             delete a;
         }
@@ -866,6 +868,14 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
         JpegGeom g;
     };
     std::vector<Lay> lay(m);
+    // scans the upload stage already put on the device (JpegUpload) are read where
+    // they lie: no scratch copy is laid out for them
+    std::vector<const uint8_t*> on_dev(m, nullptr);
+    if (up && up->n)
+        for (int k = 0; k < m; ++k) {
+            auto it = up->dev.find(files[idx[k]]);
+            if (it != up->dev.end()) on_dev[k] = it->second + (ds[idx[k]]->js_data - files[idx[k]]);
+        }
     size_t o = 0;
     auto take = [&](size_t bytes) { const size_t r = o; o += up256(bytes); return r; };
     const size_t o_img = take(sizeof(JsImageDev) * m);
@@ -911,7 +921,7 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
     for (int k = 0; k < m; ++k) {
         const Decoder& d = *ds[idx[k]];
         Lay& L = lay[k];
-        L.scan = take(d.js_len + 64);
+        L.scan = on_dev[k] ? 0 : take(d.js_len + 64);
         L.out = take(d.js_len + 4 * kPadWords + 8);
         const size_t pb = make_geom(d, L.g);
         L.coef = take(d.nblocks * 64 * sizeof(int16_t));
@@ -978,17 +988,10 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
     // place from page-locked memory, else through pinned staging
     std::vector<char> in_place(m, 0);
     std::vector<size_t> st_off(m, 0);
-    std::vector<const uint8_t*> on_dev(m, nullptr);
     size_t st_total = 0;
     for (int k = 0; k < m; ++k) {
         const Decoder& d = *ds[idx[k]];
-        if (up && up->n) {
-            auto it = up->dev.find(files[idx[k]]);
-            if (it != up->dev.end()) {
-                on_dev[k] = it->second + (d.js_data - files[idx[k]]);
-                continue;
-            }
-        }
+        if (on_dev[k]) continue;
         in_place[k] = host_pinned(d.js_data, d.js_len) ? 1 : 0;
         if (!in_place[k]) { st_off[k] = st_total; st_total += up256(d.js_len); }
     }
@@ -1080,14 +1083,14 @@ static void jsync_batch(std::vector<std::unique_ptr<Decoder>>& ds, const std::ve
     // ---- 4. sync, fix rounds, bases, decode ----
     EvPair& ev = thread_events(2);
     e = h2d(dev + o_scans, 0, tab2_bytes);
-    if (e == hipSuccess && ev.a) e = hipEventRecord(ev.a, s);
+    if (e == hipSuccess) ev_record(ev.a, s);
     if (e == hipSuccess) e = launch_jsync_sync(d_scans, d_wgs, nwg, d_recs, s);
     if (e == hipSuccess) e = hipMemsetAsync(d_changed, 0, sizeof(int), s);
     if (e == hipSuccess) e = launch_jsync_fix(d_scans, m, d_wgs, nwg, d_recs, d_changed, s);
     if (e == hipSuccess)
         e = launch_jsync_bases_decode(d_scans, m, d_wgs, nwg, d_recs, reinterpret_cast<LaneBase*>(dev + o_bases),
                                       dev + o_cs, d_status, s);
-    if (e == hipSuccess && ev.b) e = hipEventRecord(ev.b, s);
+    if (e == hipSuccess) ev_record(ev.b, s);
     int rounds = 0;  // the settle kernel's most rounds over the batch's images
     if (e == hipSuccess) e = d2h(0, reinterpret_cast<const uint8_t*>(d_status), sizeof(int) * m);
     if (e == hipSuccess) e = d2h(up256(sizeof(int) * m), reinterpret_cast<const uint8_t*>(d_changed), sizeof(int));

@@ -69,6 +69,7 @@ private:
         }
     }
     void loop() {
+        mark_internal_thread();  // the library's own thread: no lifetime lock (ApiGuard)
         uint64_t seen = 0;
         for (;;) {
             {
@@ -316,6 +317,7 @@ int pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t nh
 
 int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t nh, int filter,
                        int fmt, int quality, uint32_t max_batch, int threads, ik_pipeline** out) {
+    IK_API_ENTER();
     if (!out || !W || !H || !nw || !nh || !max_batch || C < 1 || C > 4) return fail(IK_ERR_INVALID, "bad geometry");
     if (fmt != IK_FORMAT_WEBP && fmt != IK_FORMAT_JPEG && fmt != IK_FORMAT_AVIF)
         return fail(IK_ERR_INVALID, "unknown ImageFormat %d", fmt);
@@ -392,6 +394,7 @@ int pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t nh
 extern "C" {
 
 int ik_pipeline_set_webp_encoder(ik_pipeline* p, int encoder) {
+    IK_API_ENTER();
     if (!p) return fail(IK_ERR_INVALID, "null pipeline");
     if (encoder != IK_WEBP_LIBWEBP && encoder != IK_WEBP_GPU) return fail(IK_ERR_INVALID, "bad WebP encoder %d", encoder);
     if (p->fmt != IK_FORMAT_WEBP) return fail(IK_ERR_INVALID, "not a WebP pipeline");
@@ -414,6 +417,7 @@ int ik_pipeline_set_webp_encoder(ik_pipeline* p, int encoder) {
 
 int ik_pipeline_run_device(ik_pipeline* p, const uint8_t* dev_src, size_t src_pitch,
                            size_t src_image_stride, uint32_t n) {
+    IK_API_ENTER();
     if (int rc = check_batch(p, dev_src, src_pitch, src_image_stride, n)) return rc;
     if (p->inflight) return fail(IK_ERR_INVALID, "batches in flight: collect them first");
     if (int rc = enqueue(p, p->slot[0], dev_src, src_pitch, src_image_stride, n, false)) return rc;
@@ -422,6 +426,7 @@ int ik_pipeline_run_device(ik_pipeline* p, const uint8_t* dev_src, size_t src_pi
 
 int ik_pipeline_submit(ik_pipeline* p, const uint8_t* dev_src, size_t src_pitch, size_t src_image_stride,
                        uint32_t n) {
+    IK_API_ENTER();
     if (int rc = check_batch(p, dev_src, src_pitch, src_image_stride, n)) return rc;
     if (p->inflight >= 2) return fail(IK_ERR_INVALID, "two batches already in flight: collect one first");
     ik_pipeline::Slot& s = p->slot[p->head & 1];
@@ -432,6 +437,7 @@ int ik_pipeline_submit(ik_pipeline* p, const uint8_t* dev_src, size_t src_pitch,
 }
 
 int ik_pipeline_collect(ik_pipeline* p, uint8_t* out, size_t out_cap, size_t* out_sizes, uint32_t* n_out) {
+    IK_API_ENTER();
     if (!p) return fail(IK_ERR_INVALID, "null pipeline");
     if (!p->inflight) return fail(IK_ERR_INVALID, "no batch in flight");
     ik_pipeline::Slot& s = p->slot[(p->head - p->inflight) & 1];
@@ -443,6 +449,7 @@ int ik_pipeline_collect(ik_pipeline* p, uint8_t* out, size_t out_cap, size_t* ou
 
 int ik_pipeline_run(ik_pipeline* p, const uint8_t* dev_src, size_t src_pitch, size_t src_image_stride,
                     uint32_t n, uint8_t* out, size_t out_cap, size_t* out_sizes) {
+    IK_API_ENTER();
     if (p && p->inflight) return fail(IK_ERR_INVALID, "batches in flight: collect them first");
     if (int rc = ik_pipeline_submit(p, dev_src, src_pitch, src_image_stride, n)) return rc;
     return ik_pipeline_collect(p, out, out_cap, out_sizes, nullptr);
@@ -454,6 +461,7 @@ double ik_pipeline_kernel_ms(const ik_pipeline* p, int which) {
 }
 
 int ik_pipeline_fetch_resized(ik_pipeline* p, uint32_t i, uint8_t* dst, size_t cap) {
+    IK_API_ENTER();
     if (!p || !dst || i >= p->last_n) return fail(IK_ERR_INVALID, "bad image index");
     const size_t row = (size_t)p->nw * p->C;
     if (cap < row * p->nh) return fail(IK_ERR_INVALID, "destination too small");
@@ -461,6 +469,7 @@ int ik_pipeline_fetch_resized(ik_pipeline* p, uint32_t i, uint8_t* dst, size_t c
 }
 
 void ik_pipeline_destroy(ik_pipeline* p) {
+    IK_API_ENTER_VOID();
     if (!p) return;
     (void)hipSetDevice(p->device);
     if (p->stream) (void)hipStreamSynchronize(p->stream);

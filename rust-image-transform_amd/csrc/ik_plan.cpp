@@ -304,13 +304,16 @@ ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, i
     p->table_bytes = blob.size();
     // upload on this thread's stream, synchronised there (copy_h2d_2d): done
     // before any stream launches with the plan, without a device-wide sync
-    if (hipMalloc(&p->dev_tables, blob.size()) != hipSuccess ||
+    if (hipMalloc(&p->dev_tables, blob.size()) != hipSuccess) p->dev_tables = nullptr;
+    if (!p->dev_tables ||
         copy_h2d_2d(static_cast<uint8_t*>(p->dev_tables), blob.size(), reinterpret_cast<const uint8_t*>(blob.data()),
                     blob.size(), blob.size(), 1,
                     thread_stream()) != IK_OK) {
+        if (p->dev_tables) (void)hipFree(p->dev_tables);
         delete p;
         return nullptr;
     }
+    mem_stat(kMemPlans, (int64_t)p->table_bytes);
     char* d = static_cast<char*>(p->dev_tables);
     ResizeArgs& a = p->args;
     a.W = W; a.H = H; a.C = C; a.nw = nw; a.nh = nh; a.row_bytes = W * C;
@@ -334,7 +337,10 @@ ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, i
 void plans_shutdown() {
     std::lock_guard<std::mutex> lk(g_plan_mu);
     for (auto& kv : g_plans) {
-        if (kv.second->dev_tables) (void)hipFree(kv.second->dev_tables);
+        if (kv.second->dev_tables) {
+            (void)hipFree(kv.second->dev_tables);
+            mem_stat(kMemPlans, -(int64_t)kv.second->table_bytes);
+        }
         delete kv.second;
     }
     g_plans.clear();

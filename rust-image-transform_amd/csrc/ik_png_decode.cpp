@@ -452,20 +452,22 @@ void release_area(UploadArea*& a) {
 // decode rounds synchronised)
 bool area_reserve(UploadArea* a, size_t dev_bytes, size_t pin_bytes) {
     if (dev_bytes > a->cap) {
-        if (a->dev) (void)hipFree(a->dev);
+        if (a->dev) { (void)hipFree(a->dev); mem_stat(kMemUploadDev, -(int64_t)a->cap); }
         a->dev = nullptr;
         a->cap = 0;
         const size_t want = dev_bytes + dev_bytes / 8;
         if (hipMalloc((void**)&a->dev, want) != hipSuccess) { a->dev = nullptr; return false; }
         a->cap = want;
+        mem_stat(kMemUploadDev, (int64_t)want);
     }
     if (pin_bytes > a->pin_cap) {
-        if (a->pin) (void)hipHostFree(a->pin);
+        if (a->pin) { (void)hipHostFree(a->pin); mem_stat(kMemUploadPinned, -(int64_t)a->pin_cap); }
         a->pin = nullptr;
         a->pin_cap = 0;
         const size_t want = std::max<size_t>(pin_bytes + pin_bytes / 8, 1u << 20);
         if (hipHostMalloc((void**)&a->pin, want, hipHostMallocDefault) != hipSuccess) { a->pin = nullptr; return false; }
         a->pin_cap = want;
+        mem_stat(kMemUploadPinned, (int64_t)want);
     }
     return true;
 }
@@ -484,8 +486,8 @@ void png_shutdown() {
         std::lock_guard<std::mutex> lk(P->mu);
         for (UploadArea* a : P->areas) {
             (void)hipSetDevice(a->device);
-            if (a->dev) (void)hipFree(a->dev);
-            if (a->pin) (void)hipHostFree(a->pin);
+            if (a->dev) { (void)hipFree(a->dev); mem_stat(kMemUploadDev, -(int64_t)a->cap); }
+            if (a->pin) { (void)hipHostFree(a->pin); mem_stat(kMemUploadPinned, -(int64_t)a->pin_cap); }
             for (hipEvent_t e : a->ev)
                 if (e) (void)hipEventDestroy(e);
             delete a;

@@ -132,6 +132,7 @@ void Pool::loop() {
     // the next launch -- on a CPU-limited host those must not wait behind it
     static const int nice_v = env_int("IK_WORKER_NICE", 19);
     if (nice_v > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), nice_v);
+    mark_internal_thread();  // the library's own thread: no lifetime lock (ApiGuard)
     ik_init(device_);  // this worker's stream / staging / scratch live on device_
     for (;;) {
         std::function<void()> task;

@@ -95,8 +95,14 @@ enum BatchTimingField {
     kBtResizeImages,
     kBtJpegEncMs,        // batched JPEG encoder (coefficients + Huffman) launches
     kBtJpegEncImages,
+    kBtHostWallMs,       // the host coder stage (libwebp / libavif): wall ms of the batch
+    kBtHostCoreMs,       // its thread CPU ms summed over the requests (core-ms)
+    kBtHostImages,       // requests it coded
     kBtFields
 };
+// the host coder stage's record of the batch it just finished (set directly: that
+// stage runs on the device's worker pool after the post stage committed)
+void batch_timing_host(int device, double wall_ms, double core_ms, double images);
 void batch_timing_reset(int device, bool post);
 void batch_timing_commit(int device, bool post);  // the stage is done: its fields become the last batch's
 void batch_timing_add(int device, int field, double v);
@@ -106,6 +112,48 @@ struct EvPair {
 };
 EvPair& thread_events(int which);  // which < 4
 float ev_pair_ms(const EvPair& e);
+
+// A scope in which batch_timing_add records (the decode and post stages of a
+// batch set it on their thread); work outside one -- a single-image ik_decode, a
+// pool worker's own resize -- adds nothing to ik_batch_last_timing
+struct BatchTimingScope {
+    bool prev;
+    BatchTimingScope();
+    ~BatchTimingScope();
+};
+// record a timing-only event: a failure is ignored (the pair then reads 0 ms) and
+// never changes the caller's path
+void ev_record(hipEvent_t e, hipStream_t s);
+
+// The library's lifetime against ik_shutdown / ik_close: every public
+// entry point holds the lifetime lock shared for its call (ApiGuard; nested calls
+// on one thread take it once), shutdown takes it exclusively, so teardown never
+// runs under a caller that is still inside the library (e.g. a daemon thread of
+// a server during interpreter exit).  Threads the library owns (pool workers,
+// stage threads, pipeline workers) are marked internal and never take it:
+// shutdown waits for them while it holds the lock.  After ik_close, entry points
+// that take it return IK_ERR_INVALID.
+struct ApiGuard {
+    bool held = false, closed = false;
+    ApiGuard();
+    ~ApiGuard();
+};
+void mark_internal_thread();
+#define IK_API_ENTER()                                                                        \
+    ::ik::ApiGuard ik_api_guard_;                                                             \
+    if (ik_api_guard_.closed) return ::ik::fail(IK_ERR_INVALID, "the library is closed (ik_close)")
+#define IK_API_ENTER_VOID()          \
+    ::ik::ApiGuard ik_api_guard_;    \
+    if (ik_api_guard_.closed) return
+
+// Bytes the library holds, by pool (ik_memory_stats): device image blocks in use
+// and kept free for reuse, the per-thread device and pinned arenas, the PNG / JPEG
+// upload areas (device, pinned), the cached resize plans' device tables
+enum MemStat {
+    kMemImageLive = 0, kMemImageFree, kMemArenaDev, kMemArenaPinned, kMemUploadDev, kMemUploadPinned,
+    kMemPlans, kMemStats
+};
+void mem_stat(int which, int64_t delta);
 
 // ik_shutdown: stop and join every pool's workers (device and logical pools);
 // multi-device dispatch is unconfigured

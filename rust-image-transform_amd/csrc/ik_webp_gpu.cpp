@@ -152,6 +152,7 @@ int ik_get_webp_encoder(void) { return default_webp_encoder(); }
 
 int ik_webp_encode_gpu_device(const uint8_t* dev_yuv, uint32_t w, uint32_t h, int quality, uint8_t** out,
                               size_t* out_len) {
+    IK_API_ENTER();
     if (!dev_yuv || !out || !out_len) return fail(IK_ERR_INVALID, "null pointer");
     const int q = quality < 1 ? 1 : (quality > 100 ? 100 : quality);
     std::vector<uint8_t> bytes;

@@ -24,6 +24,8 @@ c_img_p = ctypes.c_void_p
 SIGNATURES = [
     ("ik_init", ctypes.c_int, [ctypes.c_int]),
     ("ik_shutdown", ctypes.c_int, []),
+    ("ik_close", ctypes.c_int, []),
+    ("ik_memory_stats", ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     ("ik_device_count", ctypes.c_int, []),
     ("ik_init_devices", ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ("ik_logical_device_count", ctypes.c_int, []),
@@ -108,10 +110,12 @@ def load() -> ctypes.CDLL:
             fn.restype = res
             fn.argtypes = args
         _lib = lib
-        # orderly teardown while the HIP runtime is alive (ik_shutdown: the worker
-        # and stage threads end, streams and arenas are released), not in
-        # destructors during process exit
-        atexit.register(lib.ik_shutdown)
+        # orderly teardown while the HIP runtime is alive (ik_close: callers still
+        # inside the library return first, the worker and stage threads end,
+        # streams and arenas are released, later calls fail instead of bringing
+        # the library back up under daemon threads), not in destructors during
+        # process exit
+        atexit.register(lib.ik_close)
         return lib
 
 

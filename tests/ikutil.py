@@ -217,3 +217,22 @@ def synth(w: int, h: int, c: int = 4, seed: int = 0, pattern: str = "S", alpha: 
         else:
             px[..., -1] = 255
     return np.ascontiguousarray(px)
+
+
+# The sources of the GPU PNG decode path: PMC traffic files (profiles/pmc_png.json,
+# tools/pmc_png_traffic.py) record their hash, and bench.py quotes a traffic figure
+# only when it was collected on the code it is measuring.
+PNG_PATH_SOURCES = ["ik_png.hip", "ik_inflate.h", "ik_png_decode.cpp", "ik_png_plan.h", "ik_png.h", "ik_unfilter.h",
+                    "ik_png_wave.h"]
+
+
+def png_code_sha16() -> str:
+    import hashlib
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "rust-image-transform_amd", "csrc")
+    h = hashlib.sha256()
+    for n in PNG_PATH_SOURCES:
+        p = os.path.join(csrc, n)
+        if os.path.exists(p):
+            h.update(n.encode())
+            h.update(open(p, "rb").read())
+    return h.hexdigest()[:16]

@@ -13,9 +13,11 @@
   4:2:0 with a restart marker per MCU row, page-locked inputs) -- 256 requests,
   512^2 Lanczos3, JPEG q85 -- next to a second 256-request batch mixing
   restart-marked and restart-free sources (the self-synchronising path), both in
-  flight together through ik_transform_batch_submit.  256 requests take one
-  k_jpeg_huff_batch launch over all restart intervals and four 64-image
-  sub-batches of the batched JPEG encoder (ik_host.cpp jpeg_front_group).  Oracle:
+  flight together through ik_transform_batch_submit.  All 256 scans go through
+  the self-synchronising GPU entropy decoder together (k_jsync_sync, k_jsync_fix
+  + k_jsync_settle, k_jsync_seg1-3, k_jsync_decode: one launch each per batch),
+  then four 64-image sub-batches of the batched JPEG encoder (ik_host.cpp
+  jpeg_front_group).  Oracle:
   oracle.jpeg_encode_rgb(to_rgb8(resize(jpeg_decode(src, zune), 512, 512,
   LANCZOS3)), 85) -- /root/reference/src/transform.rs:27-43,85-89,121-128.
 

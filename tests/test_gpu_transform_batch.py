@@ -132,6 +132,16 @@ def test_repeated_batches_do_not_grow_device_memory(ik):
     fmts = [ImageFormat.webp, ImageFormat.jpeg] * 9
     datas = blobs * 3
 
+    import ctypes
+    lib = _lib.load()
+    names = ["image blocks in use", "image blocks kept free", "device arenas", "pinned arenas",
+             "upload areas (device)", "upload areas (pinned)", "resize plans"]
+
+    def stats():
+        v = (ctypes.c_uint64 * len(names))()
+        assert lib.ik_memory_stats(v, len(names)) == 0
+        return list(v)
+
     def run():
         transform_batch(datas, sizes, fmts, [80] * len(datas), threads=8)
         torch.cuda.synchronize()
@@ -139,10 +149,18 @@ def test_repeated_batches_do_not_grow_device_memory(ik):
 
     run()
     run()
-    f0 = run()
+    f0, s0 = run(), stats()
+    hist = []
     for _ in range(6):
         f1 = run()
-    assert f0 - f1 < (32 << 20), f"device memory fell by {(f0 - f1) >> 20} MiB over 6 batches"
+        hist.append(stats())
+    # which of the library's pools grew (a 40 MiB fall seen once)
+    grew = {n: (hist[-1][i] - s0[i]) >> 10 for i, n in enumerate(names) if hist[-1][i] != s0[i]}
+    steps = [{n: (b[i] - a[i]) >> 10 for i, n in enumerate(names) if b[i] != a[i]} for a, b in zip([s0] + hist, hist)]
+    print(f"device memory {(f0 - f1) >> 20} MiB fallen; library pools changed by (KiB) {grew}; per batch {steps}")
+    assert f0 - f1 < (32 << 20), (f"device memory fell by {(f0 - f1) >> 20} MiB over 6 batches; library pools "
+                                  f"changed by (KiB) {grew}; per batch {steps}")
+    assert s0[0] == hist[-1][0], f"image blocks still in use after the batches: {hist[-1][0] - s0[0]} bytes more"
 
 
 MULTI_SCRIPT = r'''

@@ -6,9 +6,12 @@ as is (exact for 16-B-per-lane streaming stores, the token / symbol / row stores
 
 usage: python tools/pmc_png_traffic.py FETCH_DIR WRITE_DIR CALIB_DIR OUT_JSON
 """
-import csv, json, os, sys
+import csv, json, os, subprocess, sys
 
-KERNELS = ["k_png_decode", "k_png_expand", "k_png_resolve", "k_png_unfilter", "k_png_find"]
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+import ikutil  # noqa: E402  (png_code_sha16: the code the counters were measured on)
+
+KERNELS = ["k_png_decode", "k_png_expand", "k_png_resolve", "k_png_unfilter", "k_png_find", "k_png_wave"]
 
 
 def per_kernel(d, counter):
@@ -34,7 +37,13 @@ def main():
     res = {"note": "per 64-frame batch (bench.py headline; counter sums over the run's dispatches / dispatch "
                    "count); fetch doubled per MI355X_MICROARCH.md (gfx950 FETCH_SIZE = half of a streaming "
                    "read), confirmed by the bw_probe calibration factor (known bytes / FETCH_SIZE bytes)",
-           "bw_probe_fetch_factor": calib}
+           "bw_probe_fetch_factor": calib,
+           "code_sha16": ikutil.png_code_sha16()}
+    try:
+        res["git_head"] = subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                                         text=True).stdout.strip() or None
+    except OSError:
+        res["git_head"] = None
     for k in KERNELS:
         if k not in f or k not in w:
             continue
