@@ -12,6 +12,8 @@
 #   ltrst     the same with a restart marker per MCU row
 #   jtests    the JPEG GPU parity tests only (decode, zune reconstruction, the configs[2] parity case)
 #   ptime     the headline bench with IK_TIMING (host stage marks on stderr)
+#   pmc       PMC HBM traffic of the PNG kernels (tools/pmc_png_traffic.sh) -> ${TAG}_pmc_png.json
+#   gtest     the GPU tests named in $GTESTS
 # Outputs go to gpurun_out/${TAG}_*; copy what is judged into profiles/.
 set -o pipefail
 export TMPDIR=/tmp
@@ -68,6 +70,16 @@ for s in $STEPS; do
       IK_TIMING=1 timeout -k 10 600 python -u bench.py --no-cpu-baseline --no-extras --steps 6 > ${O}_ptime.json 2> ${O}_ptime.err \
         || { echo "PTIME FAILED"; tail -20 ${O}_ptime.err; exit 1; }
       python tools/bench_summary.py ${O}_ptime.json ;;
+    pmc)
+      # PMC HBM traffic of the PNG kernels on this code (FETCH_SIZE / WRITE_SIZE passes, each its own run)
+      bash tools/pmc_png_traffic.sh > ${O}_pmc.log 2>&1 || { echo "PMC FAILED"; tail -20 ${O}_pmc.log; exit 1; }
+      cp gpurun_out/pmc_png.json ${O}_pmc_png.json
+      python -c "import json;d=json.load(open('${O}_pmc_png.json'));print({k:v['hbm_bytes_per_batch'] for k,v in d.items() if isinstance(v,dict)}, d.get('code_sha16'))" ;;
+    gtest)
+      # the GPU tests named in GTESTS only
+      timeout -k 10 600 python -u -m pytest ${GTESTS} -x -q -m gpu --timeout 300 --timeout-method thread > ${O}_gtest.log 2>&1 \
+        || { echo "GPU TESTS FAILED"; tail -40 ${O}_gtest.log; exit 1; }
+      tail -2 ${O}_gtest.log ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
