@@ -477,7 +477,7 @@ struct LaneResult {
     uint32_t iters;     // symbol-loop iterations (profile)
     uint32_t kcycles;   // GPU: clock ticks / 1024 from start to end (profile)
     uint32_t blocks;    // blocks decoded
-    uint32_t pad;
+    uint32_t pieces;    // wave decoder (ik_png_wave.h): token pieces written
 };
 
 // Decode whole blocks from `start` (a block boundary) until a block boundary >=
@@ -751,6 +751,10 @@ struct Win {
 };
 
 enum { kLaneOverflow = 3 };  // LaneStatus: the token region was too small
+// LaneStatus of the wave decoder (ik_png_wave.h): the lane decoded whole blocks up to
+// end_bit (a block boundary before its stop) and has no room for more pieces; the
+// chain check starts a new lane there (ik_png_plan.h)
+enum { kLaneSplit = 4 };
 
 // Decoder lane, decode pass: whole blocks from `start` (a block boundary) up to
 // `stop`, as decode_lane, writing the token stream (TokOut, capacity tcap tokens
@@ -1001,6 +1005,7 @@ IK_HD int expand_lane(TokIn& tin, uint32_t ntok, Out out, int64_t obase, uint64_
             put(v & 0xFFu);
             continue;
         }
+        if (v == kTokPad) continue;  // the padding of a wave decoder's piece (ik_png_wave.h)
         if (v == kTokTable) {
             while (t & 7u) { (void)tin.next(); ++t; }
             tin.set_table(t);

@@ -47,6 +47,9 @@ struct PngLaneDev {
     uint32_t ntok;           // decode: region capacity (tokens); expand: tokens to read
     uint32_t img;            // image of the batch
     uint32_t first;          // lane 0 of its image (no distance reaches before its output)
+    uint32_t big;            // wave decoder: the region is sized by the exact bound (an overflow before)
+    uint64_t pbase;          // wave decoder: its piece table, from entry pbase of the batch's
+    uint32_t npieces;        // wave decoder: the table's entries; expand: pieces to read (0: one contiguous run)
     uint32_t pad;
 };
 
@@ -114,7 +117,12 @@ hipError_t launch_png_find(const PngImgDev* imgs, const int* chunk_img, const in
 hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, const uint32_t* order, int n,
                              uint16_t* tok, infl::LaneResult* res, hipStream_t s);
 hipError_t launch_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int n, const uint16_t* tok, int* status,
-                             hipStream_t s);
+                             hipStream_t s, const uint2* pieces = nullptr);
+// the wave decoder (ik_png_wave.h): one wave per lane; pieces: (token base in the
+// lane's region, first index in its virtual token stream) per piece, a table of
+// lanes[t].npieces entries at lanes[t].pbase
+hipError_t launch_png_wave(const PngImgDev* imgs, const PngLaneDev* lanes, const uint32_t* order, int n,
+                           uint16_t* tok, uint2* pieces, infl::LaneResult* res, hipStream_t s);
 hipError_t launch_png_resolve(const PngImgDev* imgs, const int2* rows, int nrows, int* err, hipStream_t s);
 // groups[t] = (image, band group) of the workgroup holding ticket t; prog: one
 // zeroed counter per band (the image's at prog_base[image]); ticket: zeroed

@@ -34,6 +34,7 @@
 #include "ik_inflate.h"
 #include "ik_internal.h"
 #include "ik_png.h"
+#include "ik_png_wave.h"
 #include "ik_unfilter.h"
 
 namespace ik {
@@ -403,6 +404,285 @@ __global__ __launch_bounds__(kPngInflateThreads) void k_png_decode(const PngImgD
     res[t] = r;
 }
 
+// ---- the wave decoder (ik_png_wave.h) ------------------------------------------------
+// One wave per decoder lane: the lane's blocks one after another; per block the
+// header (lane 0), the shared lookup tables (all lanes), then the body window by
+// window: the window's stream words staged in LDS with coalesced 16-byte loads,
+// 64 sub-lanes decoding sub-ranges at once (wave::sub_decode), fix rounds until
+// the sub-lanes' starts and exits chain, the chained sub-lanes' token pieces
+// recorded.  Every branch around the sub-lane passes is wave-uniform.
+constexpr uint32_t kWaveWinWords = (uint32_t)(wave::kWindowBits / 32) + 16;  // + the last sub-lane's overshoot
+
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+
+// the 64 stream bits from pos, out of the staged window (w[0] = stream bit `base`)
+struct WaveLdsWin {
+    const lds_u32* w;
+    uint64_t base;
+    __device__ uint64_t operator()(uint64_t pos) const {
+        const uint32_t o = (uint32_t)(pos - base);
+        const uint32_t wi = o >> 5, sh = o & 31u;
+        const uint32_t a = w[wi], b = w[wi + 1], c = w[wi + 2];
+        const uint32_t lo = __builtin_amdgcn_alignbit(b, a, sh), hi = __builtin_amdgcn_alignbit(c, b, sh);
+        return ((uint64_t)hi << 32) | lo;
+    }
+};
+// the same straight from the stream in memory (block headers, stored blocks)
+struct WaveGlobalWin {
+    const IK_GLOBAL uint32_t* w;
+    __device__ uint64_t operator()(uint64_t pos) const {
+        const uint64_t wi = pos >> 5;
+        const uint32_t sh = (uint32_t)(pos & 31u);
+        const uint32_t a = w[wi], b = w[wi + 1], c = w[wi + 2];
+        const uint32_t lo = __builtin_amdgcn_alignbit(b, a, sh), hi = __builtin_amdgcn_alignbit(c, b, sh);
+        return ((uint64_t)hi << 32) | lo;
+    }
+};
+
+__device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v, int d) {
+    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d, 64), hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o, 64), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o, 64);
+        v += ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const PngLaneDev* lanes, const uint32_t* order,
+                                                 int nlanes, uint16_t* tok, uint2* pieces, infl::LaneResult* res) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_win[kWaveWinWords];
+    __shared__ uint32_t s_lit[1u << wave::kLB];
+    __shared__ uint32_t s_dist[1u << wave::kDB];
+    __shared__ uint16_t s_lsym[288];
+    __shared__ uint16_t s_dsym[32];
+    __shared__ uint8_t s_lens[288 + 32];
+    __shared__ wave::Code s_code[2];
+    __shared__ int s_hdr[4];  // lane 0's header parse: status, body position (lo, hi)
+    const int slot = blockIdx.x;
+    if (slot >= nlanes) return;
+    const int t = order ? (int)order[slot] : slot;
+    const int lane = threadIdx.x;
+    const PngLaneDev L = lanes[t];
+    const PngImgDev I = imgs[L.img];
+    const uint64_t nbits = I.nbits, start = L.start, stop = L.stop;
+    const uint64_t stop_eff = stop == ~0ull ? nbits : (stop < nbits ? stop : nbits);
+    const IK_GLOBAL uint32_t* W = (const IK_GLOBAL uint32_t*)I.words;
+    const WaveGlobalWin gwin{W};
+    IK_GLOBAL uint16_t* const region = (IK_GLOBAL uint16_t*)(tok + L.tbase);
+    IK_GLOBAL uint2* const ptab = (IK_GLOBAL uint2*)(pieces + L.pbase);
+    const uint64_t cap = L.ntok;
+    const uint32_t pcap = L.npieces;  // piece-table entries of this lane (wave::pieces_capacity)
+    const bool big = L.big != 0;
+    const uint64_t c0 = clock64();
+    uint64_t p = start, used = 0, total = 0;
+    uint32_t npieces = 0, nblocks = 0, steps = 0;
+    uint64_t written = 0;  // tokens in the pieces (padding included)
+    uint64_t prev_bits = 0;  // the last block's body length (wave::window_end)
+    int status = infl::kLaneCorrupt, final_block = 0;
+    const lds_u32* lit = (const lds_u32*)s_lit;
+    const lds_u32* dist = (const lds_u32*)s_dist;
+    const lds_u16* lsym = (const lds_u16*)s_lsym;
+    const lds_u16* dsym = (const lds_u16*)s_dsym;
+    for (;;) {
+        if (p >= stop) {
+            status = p == stop ? infl::kLaneOk : infl::kLaneMismatch;
+            break;
+        }
+        if (p + 3 > nbits) break;
+        const uint64_t blk_start = p, blk_total = total, blk_used = used, blk_written = written;
+        const uint32_t blk_pieces = npieces;
+        const uint64_t h = gwin(p);
+        const int bfinal = (int)(h & 1u), btype = (int)((h >> 1) & 3u);
+        ++nblocks;
+        if (btype == 3) break;
+        if (btype == 0) {  // stored: one piece of raw tokens, all lanes
+            uint64_t q = (p + 3 + 7) & ~7ull;
+            const uint64_t lh = gwin(q);
+            const uint32_t len = (uint32_t)lh & 0xFFFFu, nlen = (uint32_t)(lh >> 16) & 0xFFFFu;
+            if ((len ^ 0xFFFFu) != nlen) break;
+            q += 32;
+            if (q + 8ull * len > nbits) break;
+            if (stop != ~0ull && q + 8ull * len > stop) {  // the block passes the lane's stop: no tokens needed
+                p = q + 8ull * len;
+                status = infl::kLaneMismatch;
+                break;
+            }
+            const uint32_t n8 = (len + 7u) & ~7u;
+            if (used + n8 > cap) { status = infl::kLaneOverflow; break; }
+            if (npieces >= pcap) {
+                status = p > start ? (int)infl::kLaneSplit : (int)infl::kLaneOverflow;
+                break;
+            }
+            const IK_GLOBAL uint8_t* B = (const IK_GLOBAL uint8_t*)W + (q >> 3);
+            for (uint32_t i = (uint32_t)lane; i < n8; i += 64)
+                region[used + i] = i < len ? (uint16_t)(infl::kTokRaw | B[i]) : (uint16_t)infl::kTokPad;
+            if (lane == 0) ptab[npieces] = make_uint2((uint32_t)used, (uint32_t)written);
+            ++npieces;
+            used += n8;
+            written += n8;
+            total += len;
+            p = q + 8ull * len;
+        } else {
+            // ---- the block's codes: lane 0 parses the header and builds both codes ----
+            if (lane == 0) {
+                int ok = 0;
+                uint64_t body = p + 3;
+                if (btype == 2) {
+                    infl::Bits b;
+                    b.init((const uint32_t*)I.words, p + 3, (nbits >> 5) + 4);
+                    infl::CodeInfo lci, dci;
+                    int nlen = 0, ndist = 0;
+                    uint8_t* lens = (uint8_t*)s_lens;
+                    if (infl::parse_dynamic(b, lens, nlen, ndist, lci, dci) == 0) {
+                        for (int i = ndist - 1; i >= 0; --i) lens[288 + i] = lens[nlen + i];
+                        body = b.pos();
+                        ok = wave::code_build(lens, nlen, false, s_code[0], (uint16_t*)s_lsym) == 0 &&
+                             wave::code_build(lens + 288, ndist, true, s_code[1], (uint16_t*)s_dsym) == 0;
+                    }
+                } else {
+                    uint8_t* lens = (uint8_t*)s_lens;
+                    infl::fixed_lens(lens);
+                    ok = wave::code_build(lens, 288, false, s_code[0], (uint16_t*)s_lsym, true) == 0 &&
+                         wave::code_build(lens + 288, 30, true, s_code[1], (uint16_t*)s_dsym, true) == 0;
+                }
+                s_hdr[0] = ok;
+                s_hdr[1] = (int)(uint32_t)body;
+                s_hdr[2] = (int)(uint32_t)(body >> 32);
+            }
+            __syncthreads();
+            if (!s_hdr[0]) break;
+            const uint64_t body = (uint64_t)(uint32_t)s_hdr[1] | ((uint64_t)(uint32_t)s_hdr[2] << 32);
+            // ---- the lookup tables, all lanes ----
+            for (uint32_t e = (uint32_t)lane; e < (1u << wave::kLB); e += 64) s_lit[e] = wave::lit_table_entry(e, s_code[0], lsym);
+            for (uint32_t e = (uint32_t)lane; e < (1u << wave::kDB); e += 64) s_dist[e] = wave::dist_table_entry(e, s_code[1], dsym);
+            __syncthreads();
+            // ---- the body, window by window ----
+            uint64_t bp = body;
+            bool first_window = true;
+            int done = 0;  // 1 block ended, 2 lane ends (status set), 3 corrupt / overflow, 4 split
+            while (!done) {
+                if (bp >= stop_eff) {
+                    status = stop == ~0ull ? infl::kLaneCorrupt : infl::kLaneMismatch;
+                    done = 2;
+                    break;
+                }
+                const uint64_t re = wave::window_end(bp, stop_eff, first_window ? prev_bits : 0);
+                first_window = false;
+                const wave::Split sp = wave::split_range(bp, re, big);
+                if (used + (uint64_t)sp.nsub * sp.cap > cap) { status = infl::kLaneOverflow; done = 3; break; }
+                // stage the window: words from bp's 16-byte group to past the last sub-lane's overshoot
+                const uint64_t w0 = (bp >> 5) & ~3ull;
+                // (the last sub-lane reads up to 48 + 64 bits past re)
+                uint32_t nq = (uint32_t)((((re + 160) >> 5) + 1 - w0 + 3) >> 2);  // 16-byte groups
+                nq = nq < kWaveWinWords / 4 ? nq : kWaveWinWords / 4;
+                {
+                    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+                    const IK_GLOBAL u4* src = (const IK_GLOBAL u4*)(W + w0);
+                    __syncthreads();  // the previous window's readers are done
+                    for (uint32_t k = (uint32_t)lane; k < nq; k += 64) *(u4*)(s_win + 4 * k) = src[k];
+                    __syncthreads();
+                }
+                const WaveLdsWin win{(const lds_u32*)s_win, w0 << 5};
+                const int j = lane;
+                const bool act = j < sp.nsub;
+                const uint64_t lo = bp + 32ull * sp.lw * (uint64_t)j;
+                const uint64_t hi = j + 1 < sp.nsub ? lo + 32ull * sp.lw : re;
+                wave::SubOut o{region + used + (uint64_t)j * sp.cap, sp.cap};
+                wave::SubRes r{};
+                r.start = r.exit = ~0ull;
+                if (act) {
+                    const uint64_t p0 = j == 0 ? bp : (lo >= bp + wave::kWarmBits ? lo - wave::kWarmBits : bp);
+                    wave::sub_decode(win, p0, lo, hi, lit, dist, s_code[0], lsym, s_code[1], dsym, o, r);
+                    o.finish();
+                    steps += r.steps;
+                }
+                // fix rounds (all lanes in the shuffles; the redone sub-lanes diverge)
+                int v = 0;
+                for (;;) {
+                    const uint64_t exp = shfl_up_u64(r.exit, 1);
+                    const int eobp = __shfl_up(r.eob, 1, 64), badp = __shfl_up(r.bad, 1, 64);
+                    const bool chain = j == 0 || (r.start == exp && !eobp && !badp);
+                    const unsigned long long broken = __ballot(act && j >= 1 && !chain);
+                    v = broken ? __builtin_ctzll(broken) - 1 : sp.nsub - 1;
+                    if (!broken) break;
+                    if (__builtin_amdgcn_readlane(r.eob, v) || __builtin_amdgcn_readlane(r.bad, v)) break;
+                    if (act && j > v && !chain && !eobp && !badp) {
+                        wave::sub_decode(win, exp, lo, hi, lit, dist, s_code[0], lsym, s_code[1], dsym, o, r);
+                        o.finish();
+                        steps += r.steps;
+                    }
+                }
+                const bool in = j <= v;
+                if (__ballot(in && r.over)) { status = infl::kLaneOverflow; done = 3; break; }
+                if (npieces + (uint32_t)(v + 1) > pcap) {
+                    status = blk_start > start ? (int)infl::kLaneSplit : (int)infl::kLaneOverflow;
+                    done = 4;
+                    break;
+                }
+                {
+                    // (base, virtual start) of each chained sub-lane's piece: the exclusive scan of the padded counts
+                    const uint32_t n8 = in ? (r.ntok + 7u) & ~7u : 0u;
+                    const uint32_t incl = wave_incl_scan_dpp(n8);
+                    if (in)
+                        ptab[npieces + (uint32_t)j] =
+                            make_uint2((uint32_t)(used + (uint64_t)j * sp.cap), (uint32_t)written + incl - n8);
+                    written += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                }
+                npieces += (uint32_t)(v + 1);
+                total += wave_sum_u64(in ? r.out : 0ull);
+                // the next window's sub-lanes start past the last piece (its region's rest is free)
+                used += (uint64_t)v * sp.cap + (uint64_t)((__builtin_amdgcn_readlane((int)r.ntok, v) + 7u) & ~7u);
+                const uint64_t exv = readlane_u64(r.exit, v);
+                if (__builtin_amdgcn_readlane(r.bad, v)) { done = 3; break; }
+                if (__builtin_amdgcn_readlane(r.eob, v)) {
+                    p = exv;
+                    prev_bits = p - body;
+                    done = 1;
+                    break;
+                }
+                bp = exv;
+            }
+            if (done == 4) {
+                npieces = blk_pieces;
+                total = blk_total;
+                used = blk_used;
+                written = blk_written;
+                p = blk_start;
+                break;
+            }
+            if (done != 1) break;
+        }
+        if (bfinal) {
+            final_block = 1;
+            status = stop == ~0ull ? infl::kLaneOk : infl::kLaneMismatch;
+            break;
+        }
+    }
+    const uint32_t tsteps = (uint32_t)wave_sum_u64(steps);
+    if (lane == 0) {
+        infl::LaneResult r{};
+        r.end_bit = p;
+        r.out_len = total;
+        r.ntok = (uint32_t)written;
+        r.status = status;
+        r.final_block = final_block;
+        r.iters = tsteps;
+        r.kcycles = (uint32_t)((clock64() - c0) >> 10);
+        r.blocks = nblocks;
+        r.pieces = npieces;
+        res[t] = r;
+    }
+}
+
 // ---- expand -----------------------------------------------------------------------
 // One WAVE per verified lane (one DEFLATE block, ~32K symbols): the lane's tokens
 // -> u16 symbols at its output offset: literal bytes, or window markers (0x8000 |
@@ -435,7 +715,7 @@ using infl::kTokTableLen;
 constexpr uint32_t kX4Tok = 256;
 
 __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const PngLaneDev* lanes, int nlanes,
-                                                    const uint16_t* tok, int* status) {
+                                                    const uint16_t* tok, int* status, const uint2* pieces) {
     raise_priority();
     __shared__ __attribute__((aligned(16))) uint16_t s_ring[kXRing];  // recent output, by absolute position
     __shared__ uint32_t s_tab[64];                                      // the block's literal table
@@ -449,7 +729,17 @@ __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const
     const IK_GLOBAL uint16_t* T = (const IK_GLOBAL uint16_t*)(tok + L.tbase);
     IK_GLOBAL uint16_t* const U = (IK_GLOBAL uint16_t*)I.u16;
     const int64_t ob = L.obase, oe = L.obase + (int64_t)L.out_len;
-    const uint32_t ntok = L.ntok;
+    uint32_t ntok = L.ntok;
+    // the wave decoder's lanes: their tokens are pieces of the region (ik_png_wave.h),
+    // read in order as one virtual stream of ntok tokens (each piece a multiple of 8);
+    // a thread keeps its current piece (base, virtual start) and the next one's start
+    const uint32_t np = pieces ? L.npieces : 0u;
+    const IK_GLOBAL uint2* P = (const IK_GLOBAL uint2*)(pieces + (pieces ? L.pbase : 0));
+    uint32_t kc = 0, pc_base = 0, pc_start = 0, pn_start = 0xFFFFFFFFu;
+    if (np) {
+        pc_base = P[0].x;
+        pn_start = np > 1 ? P[1].y : 0xFFFFFFFFu;
+    }
     uint32_t t = 0;
     int64_t cnt = 0;
     bool have_tab = false, bad = false;
@@ -457,7 +747,15 @@ __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const
     // is 16-byte aligned and padded past ntok to a multiple of 8 tokens)
     auto load4 = [&](uint32_t a) -> uint64_t {
         const uint32_t i = a + 4u * (uint32_t)x;
-        return i < ntok ? *(const IK_GLOBAL uint64_t*)(T + i) : 0xFFFEFFFEFFFEFFFEull;
+        if (i >= ntok) return 0xFFFEFFFEFFFEFFFEull;
+        if (!np) return *(const IK_GLOBAL uint64_t*)(T + i);
+        while (i >= pn_start) {  // (the index only grows: a piece or two per window)
+            ++kc;
+            pc_base = P[kc].x;
+            pc_start = pn_start;
+            pn_start = kc + 1 < np ? P[kc + 1].y : 0xFFFFFFFFu;
+        }
+        return *(const IK_GLOBAL uint64_t*)(T + pc_base + (i - pc_start));
     };
     uint64_t w = load4(0);
     while (t < ntok) {
@@ -524,7 +822,7 @@ __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const
                 } else if ((v & 0xFF00u) == kTokMatch) {
                     len[k] = (v & 0xFFu) + 3u;
                     val[k] = (k < 3 ? u[k + 1] : nx) + 1u;  // the distance
-                } else {
+                } else if (v != kTokPad) {  // (padding of a wave decoder's piece: no symbol)
                     bad = true;
                 }
             }
@@ -1266,9 +1564,16 @@ hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, con
 }
 
 hipError_t launch_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int n, const uint16_t* tok, int* status,
-                             hipStream_t s) {
+                             hipStream_t s, const uint2* pieces) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_png_expand4, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status);
+    hipLaunchKernelGGL(k_png_expand4, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status, pieces);
+    return hipGetLastError();
+}
+
+hipError_t launch_png_wave(const PngImgDev* imgs, const PngLaneDev* lanes, const uint32_t* order, int n,
+                           uint16_t* tok, uint2* pieces, infl::LaneResult* res, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_png_wave, dim3(n), dim3(64), 0, s, imgs, lanes, order, n, tok, pieces, res);
     return hipGetLastError();
 }
 

@@ -35,6 +35,7 @@
 #include "../../include/imagekit_hip.h"
 #include "ik_png.h"
 #include "ik_png_plan.h"
+#include "ik_png_wave.h"
 #include "ik_runtime.h"
 
 namespace ik {
@@ -772,8 +773,26 @@ static bool order_lanes(const std::vector<PngLaneDev>& hl, const std::vector<Png
     return true;
 }
 
+// The decode pass: the wave decoder (ik_png_wave.h, k_png_wave: a wave per lane,
+// 64 self-synchronising sub-lanes over shared lookup tables) by default;
+// IK_PNG_DECODE=lane selects round 4's one-thread-per-lane canonical decoder
+// (k_png_decode, token streams with literal tables) for A/B runs.
+static bool png_wave_decoder() {
+    static const bool v = [] {
+        const char* e = getenv("IK_PNG_DECODE");
+        return !(e && !strcmp(e, "lane"));
+    }();
+    return v;
+}
+
+// token region of a lane of `bits` compressed bits (its capacity in tokens)
+static uint64_t lane_tok_capacity(uint64_t bits, bool big) {
+    return png_wave_decoder() ? wave::region_capacity(bits, big) : infl::tok_capacity(bits, big);
+}
+
 int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* msgs) {
     static const bool timing = getenv("IK_TIMING") != nullptr;
+    const bool wavedec = png_wave_decoder();
     const double t0 = now_ms();
     double tim[kPngTimingFields] = {};
     Events& ev = events();
@@ -819,11 +838,20 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         size_t max_lanes = 0;
         uint64_t tok_total = 0;
         for (PngJob* j : J) {
-            max_lanes += (size_t)j->nchunks;
-            tok_total += infl::tok_capacity(j->nbits, false) + (uint64_t)j->nchunks * (infl::tok_capacity(0, false) +
-                                                                                       infl::kTokSlack);
+            // (the wave decoder may split lanes at block boundaries: room for more)
+            max_lanes += (size_t)j->nchunks + (wavedec ? (size_t)j->nchunks / 4 + 16 : 0);
+            tok_total += lane_tok_capacity(j->nbits, false) + (uint64_t)j->nchunks * (lane_tok_capacity(0, false) +
+                                                                                      infl::kTokSlack);
         }
         tok_total += tok_total / 2 + 64;
+        // the wave decoder's piece tables: per lane wave::pieces_capacity(its bits) entries, handed out as
+        // the token regions are (a lane decoded again over a longer range gets a larger one)
+        uint64_t pieces_total = 0;
+        if (wavedec) {
+            for (PngJob* j : J) pieces_total += wave::pieces_capacity(j->nbits) + 64ull * (uint64_t)j->nchunks;
+            pieces_total += pieces_total / 2 + 4096;
+        }
+        const size_t pieces_bytes = up256(sizeof(uint2) * pieces_total);
         size_t dyn = up256(sizeof(PngLaneDev) * max_lanes) + up256(sizeof(infl::LaneResult) * max_lanes) +
                      up256(sizeof(int64_t) * max_lanes) + up256(2 * sizeof(int) * max_lanes) +
                      up256(sizeof(uint32_t) * max_lanes) + up256(sizeof(PngImgDev) * m);
@@ -838,7 +866,8 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         // progress counter per band and one ticket per class (zeroed)
         const size_t unf_tab = up256(sizeof(int2) * ngroups) + up256(sizeof(int) * m);
         const size_t unf_zero = up256(sizeof(unsigned) * (nbands + 8));
-        dyn += up256(sizeof(int2) * nrows) + up256(sizeof(int) * npages) + unf_tab + unf_zero + up256(2 * tok_total);
+        dyn += up256(sizeof(int2) * nrows) + up256(sizeof(int) * npages) + unf_tab + unf_zero + pieces_bytes +
+               up256(2 * tok_total);
         uint8_t* dev = scratch_slot(2, o_dyn + dyn);
         if (!dev) rc = fail(IK_ERR_DEVICE, "cannot allocate the PNG batch work area (%zu bytes)", o_dyn + dyn);
         PngLaneDev* d_lanes = nullptr;
@@ -850,6 +879,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         int2* d_rows = nullptr;
         int* d_pages = nullptr;
         uint8_t* d_unf = nullptr;
+        uint2* d_pieces = nullptr;
         uint16_t* d_tok = nullptr;
         if (!rc) {
             size_t o = o_dyn;
@@ -871,6 +901,8 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             o += up256(sizeof(int) * npages);
             d_unf = dev + o;
             o += unf_tab + unf_zero;
+            d_pieces = pieces_bytes ? reinterpret_cast<uint2*>(dev + o) : nullptr;
+            o += pieces_bytes;
             d_tok = reinterpret_cast<uint16_t*>(dev + o);
         }
         uint64_t tok_used = 0;
@@ -958,26 +990,30 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         // area was sized for all of them, so each job's lanes and token regions go to
         // fixed offsets (prefix sums over the jobs) and the jobs fill their parts at once
         bool first_built = false;
+        uint64_t p_used = 0;  // piece-table entries handed out (the wave decoder)
         {
             std::vector<size_t> l0(m + 1, 0);
-            std::vector<uint64_t> t0(m + 1, 0);
+            std::vector<uint64_t> t0(m + 1, 0), q0(m + 1, 0);
             for (int k = 0; k < m; ++k) {
                 const PngJob& j = *J[k];
                 const pngplan::Lanes& LL = j.lanes;
                 size_t nl = 0;
-                uint64_t need = 0;
+                uint64_t need = 0, pneed = 0;
                 if (!j.state)
                     for (size_t i = 0; i < LL.start.size(); ++i) {
                         if (!LL.dirty[i]) continue;
                         const uint64_t end = LL.stop[i] == ~0ull ? j.nbits : LL.stop[i];
-                        const uint32_t cap = infl::tok_capacity(end > LL.start[i] ? end - LL.start[i] : 0, LL.big[i] != 0);
+                        const uint64_t bits = end > LL.start[i] ? end - LL.start[i] : 0;
+                        const uint32_t cap = (uint32_t)lane_tok_capacity(bits, LL.big[i] != 0);
                         ++nl;
                         if (cap > LL.tcap[i]) need += cap + infl::kTokSlack;
+                        if (wavedec && wave::pieces_capacity(bits) > LL.pcap[i]) pneed += wave::pieces_capacity(bits);
                     }
                 l0[k + 1] = l0[k] + nl;
                 t0[k + 1] = t0[k] + need;
+                q0[k + 1] = q0[k] + pneed;
             }
-            if (tok_used + t0[m] <= tok_total && l0[m] <= max_lanes) {
+            if (tok_used + t0[m] <= tok_total && l0[m] <= max_lanes && p_used + q0[m] <= pieces_total) {
                 hl.resize(l0[m]);
                 who.resize(l0[m]);
                 parallel_for(m, 0, [&](int k) {
@@ -985,15 +1021,21 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                     if (j.state) return;
                     pngplan::Lanes& LL = j.lanes;
                     size_t t = l0[k];
-                    uint64_t tu = tok_used + t0[k];
+                    uint64_t tu = tok_used + t0[k], pu = p_used + q0[k];
                     for (size_t i = 0; i < LL.start.size(); ++i) {
                         if (!LL.dirty[i]) continue;
                         const uint64_t end = LL.stop[i] == ~0ull ? j.nbits : LL.stop[i];
-                        const uint32_t cap = infl::tok_capacity(end > LL.start[i] ? end - LL.start[i] : 0, LL.big[i] != 0);
+                        const uint64_t bits = end > LL.start[i] ? end - LL.start[i] : 0;
+                        const uint32_t cap = (uint32_t)lane_tok_capacity(bits, LL.big[i] != 0);
                         if (cap > LL.tcap[i]) {
                             LL.tbase[i] = tu;
                             LL.tcap[i] = cap;
                             tu += cap + infl::kTokSlack;
+                        }
+                        if (wavedec && wave::pieces_capacity(bits) > LL.pcap[i]) {
+                            LL.pslot[i] = (int64_t)pu;
+                            LL.pcap[i] = wave::pieces_capacity(bits);
+                            pu += LL.pcap[i];
                         }
                         PngLaneDev L{};
                         L.start = LL.start[i];
@@ -1002,12 +1044,16 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                         L.ntok = LL.tcap[i];
                         L.img = (uint32_t)k;
                         L.first = i == 0;
+                        L.big = LL.big[i] ? 1u : 0u;
+                        L.pbase = LL.pslot[i] < 0 ? 0 : (uint64_t)LL.pslot[i];
+                        L.npieces = LL.pcap[i];
                         hl[t] = L;
                         who[t] = {k, (int)i};
                         ++t;
                     }
                 });
                 tok_used += t0[m];
+                p_used += q0[m];
                 first_built = true;
             }
         }
@@ -1022,13 +1068,21 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                     for (size_t i = 0; i < LL.start.size(); ++i) {
                         if (!LL.dirty[i]) continue;
                         const uint64_t end = LL.stop[i] == ~0ull ? j.nbits : LL.stop[i];
-                        const uint32_t cap = infl::tok_capacity(end > LL.start[i] ? end - LL.start[i] : 0, LL.big[i] != 0);
+                        const uint32_t cap = (uint32_t)lane_tok_capacity(end > LL.start[i] ? end - LL.start[i] : 0,
+                                                                         LL.big[i] != 0);
                         if (cap > LL.tcap[i]) {  // a (larger) region from the area
                             const uint64_t need = cap + infl::kTokSlack;
                             if (tok_used + need > tok_total) { reject(j, "token area full"); break; }  // host decoder
                             LL.tbase[i] = tok_used;
                             LL.tcap[i] = cap;
                             tok_used += need;
+                        }
+                        const uint32_t pneed = wavedec ? wave::pieces_capacity(end > LL.start[i] ? end - LL.start[i] : 0) : 0;
+                        if (pneed > LL.pcap[i]) {
+                            if (p_used + pneed > pieces_total) { reject(j, "piece tables full"); break; }  // host decoder
+                            LL.pslot[i] = (int64_t)p_used;
+                            LL.pcap[i] = pneed;
+                            p_used += pneed;
                         }
                         PngLaneDev L{};
                         L.start = LL.start[i];
@@ -1037,6 +1091,9 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                         L.ntok = LL.tcap[i];
                         L.img = (uint32_t)k;
                         L.first = i == 0;
+                        L.big = LL.big[i] ? 1u : 0u;
+                        L.pbase = LL.pslot[i] < 0 ? 0 : (uint64_t)LL.pslot[i];
+                        L.npieces = LL.pcap[i];
                         hl.push_back(L);
                         who.emplace_back(k, (int)i);
                     }
@@ -1063,7 +1120,10 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             hres.resize(hl.size());
             if (!mk[0]) mk[0] = now_ms();  // plan built, lanes uploaded (first round)
             rec(2, s);
-            hipError_t e2 = launch_png_decode(d_imgs, d_lanes, ordered ? d_order : nullptr, (int)hl.size(), d_tok, d_res, s);
+            hipError_t e2 = wavedec ? launch_png_wave(d_imgs, d_lanes, ordered ? d_order : nullptr, (int)hl.size(), d_tok,
+                                                      d_pieces, d_res, s)
+                                    : launch_png_decode(d_imgs, d_lanes, ordered ? d_order : nullptr, (int)hl.size(), d_tok,
+                                                        d_res, s);
             rec(3, s);
             // the lane results come back behind the decode; the next batch's block
             // search (the stage executor's hook) queues behind that copy, so it runs
@@ -1159,6 +1219,10 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                 L.ntok = j.lanes.res[i].ntok;
                 L.img = (uint32_t)k;
                 L.first = i == 0;
+                if (wavedec) {  // the tokens are the lane's pieces (piece table at its slot)
+                    L.pbase = (uint64_t)j.lanes.pslot[i];
+                    L.npieces = j.lanes.res[i].pieces;
+                }
                 hl.push_back(L);
             }
             hob.insert(hob.end(), ob.begin(), ob.end());
@@ -1190,7 +1254,8 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             if (!rc) {
                 hipError_t e3 = hipSuccess;
                 rec(4, s);
-                if (e3 == hipSuccess) e3 = launch_png_expand(d_imgs, d_lanes, (int)hl.size(), d_tok, d_xst, s);
+                if (e3 == hipSuccess)
+                    e3 = launch_png_expand(d_imgs, d_lanes, (int)hl.size(), d_tok, d_xst, s, wavedec ? d_pieces : nullptr);
                 rec(5, s);
                 // page -> decoder that holds the page's first byte (resolve's lane lookup)
                 for (const auto& q : pj) {

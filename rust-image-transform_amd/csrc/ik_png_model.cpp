@@ -8,12 +8,14 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <vector>
 
 #include "ik_crc.h"
 #include "ik_inflate.h"
 #include "ik_png_gather.h"
 #include "ik_png_plan.h"
+#include "ik_png_wave.h"
 #include "ik_unfilter.h"
 
 using namespace ik;
@@ -45,24 +47,14 @@ struct KraftTab {
 };
 const KraftTab g_kraft;
 const uint8_t* const kraft_tab = g_kraft.t;
-}  // namespace
 
-extern "C" {
-
-// zlib stream -> inflated bytes through the chunked parallel algorithm.
-// stats (10 ints): chunks, candidates, lanes, rounds, markers, dropped
-// candidates, zlib header bits, status of the chain check, token region overflows
-int ikm_inflate_chunked(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8_t* out, size_t out_cap,
-                        uint64_t* out_len, int* stats) {
-    for (int i = 0; i < 10; ++i) stats[i] = 0;
-    if (zlen < 2) return -1;
-    if ((z[0] & 15) != 8 || ((z[0] << 8) | z[1]) % 31 || (z[1] & 0x20)) return -1;  // CM=8, FCHECK, no FDICT
-    const uint64_t nbits = (uint64_t)zlen * 8;
-    std::vector<uint32_t> words((zlen + 3) / 4 + 8, 0);
-    std::memcpy(words.data(), z, zlen);
+// the GPU block search (k_png_find) restated: per chunk, the first bit offset whose
+// dynamic header passes every check; cand[0] = the first block.  Returns the
+// candidates found, or < 0 if two of the checks disagree.
+int find_candidates(const std::vector<uint32_t>& words, uint64_t nbits, size_t chunk_bytes, std::vector<int64_t>& cand) {
     const uint64_t cbits = (uint64_t)chunk_bytes * 8;
     const uint64_t nchunks = (nbits + cbits - 1) / cbits;
-    std::vector<int64_t> cand(nchunks, -1);
+    cand.assign(nchunks, -1);
     cand[0] = 16;
     int found = 0;
     for (uint64_t c = 1; c < nchunks; ++c) {
@@ -97,6 +89,29 @@ int ikm_inflate_chunked(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8
             }
         }
     }
+    return found;
+}
+
+}  // namespace
+
+extern "C" {
+
+// zlib stream -> inflated bytes through the chunked parallel algorithm.
+// stats (10 ints): chunks, candidates, lanes, rounds, markers, dropped
+// candidates, zlib header bits, status of the chain check, token region overflows
+int ikm_inflate_chunked(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8_t* out, size_t out_cap,
+                        uint64_t* out_len, int* stats) {
+    for (int i = 0; i < 10; ++i) stats[i] = 0;
+    if (zlen < 2) return -1;
+    if ((z[0] & 15) != 8 || ((z[0] << 8) | z[1]) % 31 || (z[1] & 0x20)) return -1;  // CM=8, FCHECK, no FDICT
+    const uint64_t nbits = (uint64_t)zlen * 8;
+    std::vector<uint32_t> words((zlen + 3) / 4 + 8, 0);
+    std::memcpy(words.data(), z, zlen);
+    const uint64_t cbits = (uint64_t)chunk_bytes * 8;
+    const uint64_t nchunks = (nbits + cbits - 1) / cbits;
+    std::vector<int64_t> cand;
+    int found = find_candidates(words, nbits, chunk_bytes, cand);
+    if (found < 0) return found;
     stats[0] = (int)nchunks;
     stats[1] = found;
     stats[6] = 16;
@@ -184,6 +199,129 @@ int ikm_inflate_chunked(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8
         out[q] = (uint8_t)v;
     }
     stats[4] = markers;
+    *out_len = total;
+    return 0;
+}
+
+// The same stream through the wave decoder's algorithm (ik_png_wave.h: one lane
+// = whole blocks decoded by up to 64 self-synchronising sub-lanes with shared
+// lookup tables, its tokens in pieces), then the unchanged expand / resolve.
+// warm_bits: overrides kWarmBits when > 0 (the model's sweep).  stats (16 x u64):
+// chunks, candidates, lanes, rounds, overflows, windows, sub-lane passes, redo
+// passes, fix rounds, most fix rounds of one window, blocks, decoded symbol bits,
+// chain-check status, token-region tokens used, markers
+int ikm_inflate_wave(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8_t* out, size_t out_cap,
+                     uint64_t* out_len, uint64_t* stats) {
+    for (int i = 0; i < 16; ++i) stats[i] = 0;
+    if (zlen < 2) return -1;
+    if ((z[0] & 15) != 8 || ((z[0] << 8) | z[1]) % 31 || (z[1] & 0x20)) return -1;
+    const uint64_t nbits = (uint64_t)zlen * 8;
+    std::vector<uint32_t> words((zlen + 3) / 4 + 8, 0);
+    std::memcpy(words.data(), z, zlen);
+    std::vector<int64_t> cand;
+    const int found = find_candidates(words, nbits, chunk_bytes, cand);
+    if (found < 0) return found;
+    stats[0] = cand.size();
+    stats[1] = (uint64_t)found;
+    struct W {
+        const uint32_t* words;
+        uint64_t nw;
+        uint64_t operator()(uint64_t pos) const {
+            const uint64_t wi = pos >> 5;
+            const uint32_t sh = (uint32_t)(pos & 31);
+            auto rd = [&](uint64_t i) -> uint64_t { return i < nw ? words[i] : 0u; };
+            const uint64_t lo = rd(wi) | (rd(wi + 1) << 32);
+            return sh ? (lo >> sh) | (rd(wi + 2) << (64 - sh)) : lo;
+        }
+    } win{words.data(), (nbits >> 5) + 1};
+    pngplan::Lanes L;
+    pngplan::build(cand, L);
+    // tokens and pieces by lane start (the chain check drops and splits lanes)
+    std::map<uint64_t, std::vector<uint16_t>> tok;
+    std::map<uint64_t, std::vector<std::pair<uint32_t, uint32_t>>> pieces;  // (base, vstart)
+    wave::Stats ws;
+    int st, overflows = 0;
+    for (;;) {
+        for (size_t i = 0; i < L.start.size(); ++i) {
+            if (!L.dirty[i]) continue;
+            const uint64_t end = L.stop[i] == ~0ull ? nbits : L.stop[i];
+            const uint64_t cap = wave::region_capacity(end > L.start[i] ? end - L.start[i] : 0, L.big[i] != 0);
+            std::vector<uint16_t>& t = tok[L.start[i]];
+            t.assign(cap, 0);
+            static const uint64_t warm = getenv("IKM_WARM") ? strtoull(getenv("IKM_WARM"), nullptr, 10) : wave::kWarmBits;
+            wave::lane_host(win, nbits, L.start[i], L.stop[i], L.big[i] != 0, t.data(), cap, L.res[i],
+                            pieces[L.start[i]], &ws, warm);
+            if (L.res[i].status == infl::kLaneOverflow) {
+                ++overflows;
+                if (L.big[i]) {
+                    L.res[i].status = infl::kLaneCorrupt;
+                } else {
+                    L.big[i] = 1;
+                    continue;
+                }
+            }
+            L.dirty[i] = 0;
+        }
+        if (getenv("IKM_DEBUG"))
+            for (size_t i = 0; i < L.start.size(); ++i)
+                fprintf(stderr, "lane %zu start %llu stop %llu end %llu len %llu pieces %u status %d final %d\n", i,
+                        (unsigned long long)L.start[i], (unsigned long long)L.stop[i],
+                        (unsigned long long)L.res[i].end_bit, (unsigned long long)L.res[i].out_len,
+                        (unsigned)pieces[L.start[i]].size(),
+                        L.res[i].status, L.res[i].final_block);
+        bool pending = false;
+        for (size_t i = 0; i < L.start.size(); ++i) pending = pending || L.dirty[i];
+        if (pending) continue;
+        st = pngplan::check(L);
+        if (st != 1) break;
+    }
+    stats[2] = L.start.size();
+    stats[3] = (uint64_t)L.rounds;
+    stats[4] = (uint64_t)overflows;
+    stats[5] = ws.windows;
+    stats[6] = ws.sub_passes;
+    stats[7] = ws.redo_passes;
+    stats[8] = ws.fix_rounds;
+    stats[9] = ws.max_rounds;
+    stats[10] = ws.blocks;
+    stats[11] = ws.symbols_bits;
+    stats[12] = (uint64_t)(int64_t)st;
+    stats[15] = ws.steps;
+    if (st) return -2;
+    std::vector<int64_t> obase;
+    uint64_t total;
+    pngplan::offsets(L, obase, &total);
+    if (total > out_cap) return -3;
+    std::vector<uint16_t> u16(total + 16);
+    for (size_t i = 0; i < L.start.size(); ++i) {
+        // the pieces in order, as the GPU expand pass reads them
+        std::vector<uint16_t> cat;
+        const std::vector<std::pair<uint32_t, uint32_t>>& pt = pieces[L.start[i]];
+        const std::vector<uint16_t>& t = tok[L.start[i]];
+        for (size_t k = 0; k < pt.size(); ++k) {
+            const uint32_t n = (k + 1 < pt.size() ? pt[k + 1].second : L.res[i].ntok) - pt[k].second;
+            cat.insert(cat.end(), t.begin() + pt[k].first, t.begin() + pt[k].first + n);
+        }
+        stats[13] += cat.size();
+        cat.resize(cat.size() + 16, (uint16_t)infl::kTokPad);
+        infl::TokInHost tin{cat.data()};
+        if (infl::expand_lane(tin, (uint32_t)(cat.size() - 16), infl::U16Out{u16.data()}, obase[i], L.res[i].out_len))
+            return -4;
+    }
+    const int shift = 12;
+    std::vector<int> pages((total >> shift) + 1);
+    for (size_t pg = 0, ln = 0; pg < pages.size(); ++pg) {
+        while (ln + 1 < obase.size() && (uint64_t)obase[ln + 1] <= (pg << shift)) ++ln;
+        pages[pg] = (int)ln;
+    }
+    uint64_t markers = 0;
+    for (uint64_t q = 0; q < total; ++q) {
+        if (u16[q] >= 256) ++markers;
+        const int v = infl::resolve_at(u16.data(), obase.data(), (int)obase.size(), pages.data(), shift, (int64_t)q);
+        if (v < 0) return -5;
+        out[q] = (uint8_t)v;
+    }
+    stats[14] = markers;
     *out_len = total;
     return 0;
 }

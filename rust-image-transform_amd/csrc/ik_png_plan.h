@@ -20,7 +20,23 @@ struct Lanes {
     std::vector<uint64_t> tbase;  // token region (the caller's allocation)
     std::vector<uint32_t> tcap;   // its capacity (0: none yet)
     std::vector<char> big;        // overflowed once: the region is sized by the exact bound
+    std::vector<int64_t> pslot;   // wave decoder: the lane's piece table (first entry; -1: none yet)
+    std::vector<uint32_t> pcap;   // and its entries
     int rounds = 0;
+    // a new dirty lane [b, stop[i]) after lane i, which now stops at b
+    void split(size_t i, uint64_t b) {
+        const size_t k = i + 1;
+        start.insert(start.begin() + (long)k, b);
+        stop.insert(stop.begin() + (long)k, stop[i]);
+        stop[i] = b;
+        res.insert(res.begin() + (long)k, infl::LaneResult{0, 0, 0, infl::kLaneCorrupt, 0, 0, 0, 0, 0});
+        dirty.insert(dirty.begin() + (long)k, 1);
+        tbase.insert(tbase.begin() + (long)k, 0);
+        tcap.insert(tcap.begin() + (long)k, 0);
+        big.insert(big.begin() + (long)k, 0);
+        pslot.insert(pslot.begin() + (long)k, -1);
+        pcap.insert(pcap.begin() + (long)k, 0);
+    }
     void erase(size_t i) {
         start.erase(start.begin() + (long)i);
         stop.erase(stop.begin() + (long)i);
@@ -29,6 +45,8 @@ struct Lanes {
         tbase.erase(tbase.begin() + (long)i);
         tcap.erase(tcap.begin() + (long)i);
         big.erase(big.begin() + (long)i);
+        pslot.erase(pslot.begin() + (long)i);
+        pcap.erase(pcap.begin() + (long)i);
     }
 };
 
@@ -45,6 +63,8 @@ inline void build(const std::vector<int64_t>& cand, Lanes& L) {
     L.tbase.assign(L.start.size(), 0);
     L.tcap.assign(L.start.size(), 0);
     L.big.assign(L.start.size(), 0);
+    L.pslot.assign(L.start.size(), -1);
+    L.pcap.assign(L.start.size(), 0);
     L.rounds = 0;
 }
 
@@ -52,7 +72,9 @@ inline void build(const std::vector<int64_t>& cand, Lanes& L) {
 // first block, so verified).  A lane whose start is verified and that stopped
 // exactly on its successor's start verifies that start.  One that passed it
 // (mismatch) shows the successor's candidate was not a block boundary: the
-// successor is dropped and the lane decodes on to the next one next round.
+// successor is dropped and the lane decodes on to the next one next round.  A
+// lane that split (kLaneSplit: whole blocks up to end_bit) gets a new lane from
+// end_bit to its old stop.
 // Returns 0 when every lane is verified (the output offsets are then valid),
 // 1 when dirty lanes must be decoded again, -1 when a verified lane found the
 // stream corrupt (or the rounds ran out).  A lane that overflowed its token
@@ -74,6 +96,19 @@ inline int check(Lanes& L, int max_rounds = 24) {
             verified = false;
             any_dirty = true;
             ++i;
+            continue;
+        }
+        if (r.status == infl::kLaneSplit) {  // (wave decoder) whole blocks up to end_bit: a new lane from there
+            if (r.end_bit <= L.start[i] || r.end_bit >= L.stop[i]) {
+                if (verified) return -1;
+                ++i;
+                continue;
+            }
+            L.split(i, r.end_bit);
+            L.res[i].status = infl::kLaneOk;
+            any_dirty = true;
+            verified = false;  // the new lane is not decoded yet: its successors wait
+            i += 2;
             continue;
         }
         if (r.status == infl::kLaneOk) {
