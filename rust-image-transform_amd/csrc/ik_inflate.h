@@ -478,6 +478,8 @@ struct LaneResult {
     uint32_t kcycles;   // GPU: clock ticks / 1024 from start to end (profile)
     uint32_t blocks;    // blocks decoded
     uint32_t pieces;    // wave decoder (ik_png_wave.h): token pieces written
+    uint32_t kc_setup;  // wave decoder, profile: clock ticks / 1024 in block codes, tables and window staging
+    uint32_t pad2;
 };
 
 // Decode whole blocks from `start` (a block boundary) until a block boundary >=

@@ -439,6 +439,46 @@ struct WaveGlobalWin {
     }
 };
 
+// A sub-lane's token output on the GPU: the open group of 8 tokens sits in LDS
+// (a 16-token ring per lane, lane-minor: token slot q of lane l at 16-bit half q & 1
+// of dword 64 (q >> 1) + l, so no two lanes share a bank), each completed group
+// goes to the sub-lane's piece with one 16-byte store.  (may_alias: the slots are
+// written as u16 and read back as dwords.)
+typedef __attribute__((address_space(3), may_alias)) uint16_t lds_u16a;
+typedef __attribute__((address_space(3), may_alias)) uint32_t lds_u32a;
+struct WaveOut {
+    IK_GLOBAL uint16_t* p;
+    uint32_t cap;        // tokens (a multiple of 8)
+    uint32_t n;          // tokens put
+    lds_u32a* ring;      // this lane's dword 0 (s_ring + lane)
+    __device__ void reset() { n = 0; }
+    __device__ void slot(uint32_t q, uint32_t t) const {
+        ((lds_u16a*)(ring + 64u * ((q & 15u) >> 1)))[q & 1u] = (uint16_t)t;
+    }
+    __device__ void flush(uint32_t g) const {  // the group of tokens [g, g + 8) (g a multiple of 8)
+        if (g + 8u > cap) return;
+        const uint32_t r0 = (g & 15u) >> 1;
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        const u4 q = {ring[64u * r0], ring[64u * (r0 + 1u)], ring[64u * (r0 + 2u)], ring[64u * (r0 + 3u)]};
+        *reinterpret_cast<IK_GLOBAL u4*>(p + g) = q;
+    }
+    __device__ void put4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+        if (k > 0u) slot(n, a);
+        if (k > 1u) slot(n + 1u, b);
+        if (k > 2u) slot(n + 2u, c);
+        if (k > 3u) slot(n + 3u, d);
+        const uint32_t n2 = n + k;
+        if ((n2 ^ n) & ~7u) flush((n2 & ~7u) - 8u);  // a group completed
+        n = n2;
+    }
+    __device__ void finish() {  // pad the open group and store it
+        if (n & 7u) {
+            for (uint32_t q = n; q & 7u; ++q) slot(q, infl::kTokPad);
+            flush(n & ~7u);
+        }
+    }
+};
+
 __device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v, int d) {
     const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d, 64), hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, 64);
     return ((uint64_t)hi << 32) | lo;
@@ -457,6 +497,185 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
     return v;
 }
 
+// rank of this lane among the lanes of mask m below it
+__device__ __forceinline__ uint32_t lane_rank(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// One canonical code built by the wave (wave::code_build's result, without its
+// serial loops): lens[0..n) in LDS; per-length counts by ballots, the validity
+// rule of zlib, the left-justified limits and per-length info (C, lane 0 writes
+// it) and the symbols in canonical order (syms), each lane placing its symbols.
+__device__ bool wave_code_build(const uint8_t* lens, int n, bool is_dist, bool fixed, wave::Code& C, uint16_t* syms) {
+    const int lane = threadIdx.x;
+    uint32_t cnt[16];
+#pragma unroll
+    for (int l = 0; l < 16; ++l) cnt[l] = 0;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        const int sy = c0 + lane;
+        const uint32_t l = sy < n ? lens[sy] & 15u : 0u;
+#pragma unroll
+        for (int L = 1; L <= 15; ++L) cnt[L] += (uint32_t)__popcll(__ballot(l == (uint32_t)L));
+    }
+    int maxl = 0, left = 1;
+#pragma unroll
+    for (int L = 1; L <= 15; ++L) {
+        if (cnt[L]) maxl = L;
+        left = (left << 1) - (int)cnt[L];
+    }
+    bool ok = left >= 0;
+    if (!fixed) {
+        if (maxl == 0) ok = ok && is_dist;
+        else if (left > 0 && maxl != 1) ok = false;
+    }
+    if (!ok) return false;
+    uint32_t lim[15], off[16], code = 0, rank = 0;
+    off[0] = 0;
+#pragma unroll
+    for (int L = 1; L <= 15; ++L) {
+        code = (code + (L > 1 ? cnt[L - 1] : 0u)) << 1;
+        if (lane == 0) C.info[L] = (code & 0x7FFFu) | (rank << 16);
+        lim[L - 1] = (code + cnt[L]) << (15 - L);
+        off[L] = rank;
+        rank += cnt[L];
+    }
+    if (lane == 0) {
+        C.info[0] = 0;
+        uint32_t pk[8];
+        infl::pack_limits(lim, pk);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) C.pk[k] = pk[k];
+    }
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        const int sy = c0 + lane;
+        const uint32_t l = sy < n ? lens[sy] & 15u : 0u;
+#pragma unroll
+        for (int L = 1; L <= 15; ++L) {
+            const unsigned long long m = __ballot(l == (uint32_t)L);
+            if (l == (uint32_t)L) syms[off[L] + lane_rank(m)] = (uint16_t)sy;
+            off[L] += (uint32_t)__popcll(m);
+        }
+    }
+    return true;
+}
+
+// The block's codes by the wave: a dynamic header's code-length code (lanes 0..18
+// take one length each) and its 7-bit decode table (cl, LDS), the literal/length
+// and distance code lengths (lane 0, serial: the repeat codes chain them) from the
+// header's bits staged in hw (LDS words from stream bit hb0), then both codes
+// (wave_code_build).  Checks as infl::parse_dynamic (zlib).  *body = the first
+// bit of the block's data.
+__device__ bool wave_block_codes(const IK_GLOBAL uint32_t* W, uint64_t nbits, uint64_t p, int btype, uint32_t* hw,
+                                 uint8_t* cl, uint8_t* lens, wave::Code* code, uint16_t* lsym, uint16_t* dsym,
+                                 int* shared_ok, uint64_t* body) {
+    const int lane = threadIdx.x;
+    __syncthreads();  // the previous block's readers of hw (the staged window) and of the tables are done
+    if (btype == 1) {
+        for (int i = lane; i < 288 + 32; i += 64) lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < 288 ? 8 : 5;
+        __syncthreads();
+        *body = p + 3;
+        const bool a = wave_code_build(lens, 288, false, true, code[0], lsym);
+        const bool b = wave_code_build(lens + 288, 30, true, true, code[1], dsym);
+        __syncthreads();
+        return a && b;
+    }
+    // stage the header: 17 + 57 + 316 * 14 bits at most -- 160 words from p's word
+    const uint64_t hb0 = (p >> 5) << 5;
+    const uint64_t wmax = (nbits >> 5) + 64;  // (the stream's zero padding: 128 words)
+    for (int k = lane; k < 160; k += 64) hw[k] = (p >> 5) + (uint64_t)k < wmax ? W[(p >> 5) + (uint64_t)k] : 0u;
+    __syncthreads();
+    auto bits = [&](uint32_t o) -> uint64_t {  // 64 bits from relative bit o
+        const uint32_t wi = o >> 5, sh = o & 31u;
+        const uint32_t a = hw[wi], b = hw[wi + 1], c = hw[wi + 2];
+        return ((uint64_t)__builtin_amdgcn_alignbit(c, b, sh) << 32) | __builtin_amdgcn_alignbit(b, a, sh);
+    };
+    const uint32_t o0 = (uint32_t)(p - hb0) + 3;
+    const uint64_t h = bits(o0);
+    const int nlen = (int)(h & 31u) + 257, ndist = (int)((h >> 5) & 31u) + 1, ncode = (int)((h >> 10) & 15u) + 4;
+    if (nlen > 286 || ndist > 30) return false;
+    // the code-length code: lane s holds symbol s's length
+    constexpr uint8_t inv_order[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};
+    const uint64_t clb = bits(o0 + 14);
+    uint32_t myl = 0;
+    if (lane < 19) {
+        const int i = inv_order[lane];
+        myl = i < ncode ? (uint32_t)(clb >> (3 * i)) & 7u : 0u;
+    }
+    uint32_t cnt[8];
+#pragma unroll
+    for (int L = 1; L <= 7; ++L) cnt[L] = (uint32_t)__popcll(__ballot(myl == (uint32_t)L));
+    uint32_t kraft = 0;
+#pragma unroll
+    for (int L = 1; L <= 7; ++L) kraft += cnt[L] << (7 - L);
+    if (kraft != 128u) return false;  // the code-length code must be complete
+    {
+        uint32_t code_l = 0, first[8];
+#pragma unroll
+        for (int L = 1; L <= 7; ++L) {
+            code_l = (code_l + (L > 1 ? cnt[L - 1] : 0u)) << 1;
+            first[L] = code_l;
+        }
+        uint32_t mycode = 0;
+#pragma unroll
+        for (int L = 1; L <= 7; ++L) {
+            const unsigned long long m = __ballot(myl == (uint32_t)L);
+            if (myl == (uint32_t)L) mycode = first[L] + lane_rank(m);
+        }
+        if (myl) {
+            const uint32_t r = __builtin_bitreverse32(mycode) >> (32 - myl);
+            for (uint32_t e = r; e < 128u; e += 1u << myl) cl[e] = (uint8_t)(lane | (myl << 5));
+        }
+    }
+    __syncthreads();
+    if (lane == 0) {
+        uint32_t o = o0 + 14 + 3 * (uint32_t)ncode;
+        const int total = nlen + ndist;
+        int i = 0, ok = 1, prev = -1;
+        while (i < total) {
+            const uint64_t v = bits(o);
+            const uint32_t e = cl[(uint32_t)v & 127u];
+            const uint32_t L = e >> 5, sym = e & 31u;
+            int rep = 1, val = (int)sym;
+            uint32_t xb = 0;
+            if (sym == 16) {
+                if (prev < 0) { ok = 0; break; }
+                val = prev;  // (the previous length: the literal/length code's last one for the first distance)
+                xb = 2;
+                rep = 3 + (int)((uint32_t)(v >> L) & 3u);
+            } else if (sym == 17) {
+                val = 0;
+                xb = 3;
+                rep = 3 + (int)((uint32_t)(v >> L) & 7u);
+            } else if (sym == 18) {
+                val = 0;
+                xb = 7;
+                rep = 11 + (int)((uint32_t)(v >> L) & 127u);
+            }
+            if (i + rep > total) { ok = 0; break; }
+            for (int k = 0; k < rep; ++k) {
+                // the distance lengths go to lens[288 ..] directly
+                const int d = i + k;
+                lens[d < nlen ? d : 288 + (d - nlen)] = (uint8_t)val;
+            }
+            i += rep;
+            prev = val;
+            o += L + xb;
+            if (o > 160 * 32 - 96) { ok = 0; break; }  // past any valid header
+        }
+        if (ok && lens[256] == 0) ok = 0;  // no end-of-block code
+        shared_ok[0] = ok;
+        shared_ok[1] = (int)o;
+    }
+    __syncthreads();
+    if (!shared_ok[0]) return false;
+    *body = hb0 + (uint32_t)shared_ok[1];
+    if (*body > nbits) return false;
+    const bool a = wave_code_build(lens, nlen, false, false, code[0], lsym);
+    const bool b = wave_code_build(lens + 288, ndist, true, false, code[1], dsym);
+    __syncthreads();
+    return a && b;
+}
+
 __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const PngLaneDev* lanes, const uint32_t* order,
                                                  int nlanes, uint16_t* tok, uint2* pieces, infl::LaneResult* res) {
     __shared__ __attribute__((aligned(16))) uint32_t s_win[kWaveWinWords];
@@ -465,6 +684,8 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
     __shared__ uint16_t s_lsym[288];
     __shared__ uint16_t s_dsym[32];
     __shared__ uint8_t s_lens[288 + 32];
+    __shared__ uint8_t s_cl[128];  // the code-length code's decode table (symbol | length << 5)
+    __shared__ uint32_t s_ring[8 * 64];  // the sub-lanes' open token groups (WaveOut)
     __shared__ wave::Code s_code[2];
     __shared__ int s_hdr[4];  // lane 0's header parse: status, body position (lo, hi)
     const int slot = blockIdx.x;
@@ -487,6 +708,7 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
     uint32_t npieces = 0, nblocks = 0, steps = 0;
     uint64_t written = 0;  // tokens in the pieces (padding included)
     uint64_t prev_bits = 0;  // the last block's body length (wave::window_end)
+    uint64_t ck_setup = 0;   // profile: clock in codes, tables, staging
     int status = infl::kLaneCorrupt, final_block = 0;
     const lds_u32* lit = (const lds_u32*)s_lit;
     const lds_u32* dist = (const lds_u32*)s_dist;
@@ -532,39 +754,15 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
             total += len;
             p = q + 8ull * len;
         } else {
-            // ---- the block's codes: lane 0 parses the header and builds both codes ----
-            if (lane == 0) {
-                int ok = 0;
-                uint64_t body = p + 3;
-                if (btype == 2) {
-                    infl::Bits b;
-                    b.init((const uint32_t*)I.words, p + 3, (nbits >> 5) + 4);
-                    infl::CodeInfo lci, dci;
-                    int nlen = 0, ndist = 0;
-                    uint8_t* lens = (uint8_t*)s_lens;
-                    if (infl::parse_dynamic(b, lens, nlen, ndist, lci, dci) == 0) {
-                        for (int i = ndist - 1; i >= 0; --i) lens[288 + i] = lens[nlen + i];
-                        body = b.pos();
-                        ok = wave::code_build(lens, nlen, false, s_code[0], (uint16_t*)s_lsym) == 0 &&
-                             wave::code_build(lens + 288, ndist, true, s_code[1], (uint16_t*)s_dsym) == 0;
-                    }
-                } else {
-                    uint8_t* lens = (uint8_t*)s_lens;
-                    infl::fixed_lens(lens);
-                    ok = wave::code_build(lens, 288, false, s_code[0], (uint16_t*)s_lsym, true) == 0 &&
-                         wave::code_build(lens + 288, 30, true, s_code[1], (uint16_t*)s_dsym, true) == 0;
-                }
-                s_hdr[0] = ok;
-                s_hdr[1] = (int)(uint32_t)body;
-                s_hdr[2] = (int)(uint32_t)(body >> 32);
-            }
-            __syncthreads();
-            if (!s_hdr[0]) break;
-            const uint64_t body = (uint64_t)(uint32_t)s_hdr[1] | ((uint64_t)(uint32_t)s_hdr[2] << 32);
+            // ---- the block's codes, by the wave ----
+            uint64_t body = 0;
+            const uint64_t ck0 = clock64();
+            if (!wave_block_codes(W, nbits, p, btype, s_win, s_cl, s_lens, s_code, s_lsym, s_dsym, s_hdr, &body)) break;
             // ---- the lookup tables, all lanes ----
             for (uint32_t e = (uint32_t)lane; e < (1u << wave::kLB); e += 64) s_lit[e] = wave::lit_table_entry(e, s_code[0], lsym);
             for (uint32_t e = (uint32_t)lane; e < (1u << wave::kDB); e += 64) s_dist[e] = wave::dist_table_entry(e, s_code[1], dsym);
             __syncthreads();
+            ck_setup += clock64() - ck0;
             // ---- the body, window by window ----
             uint64_t bp = body;
             bool first_window = true;
@@ -585,18 +783,20 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
                 uint32_t nq = (uint32_t)((((re + 160) >> 5) + 1 - w0 + 3) >> 2);  // 16-byte groups
                 nq = nq < kWaveWinWords / 4 ? nq : kWaveWinWords / 4;
                 {
+                    const uint64_t ck1 = clock64();
                     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
                     const IK_GLOBAL u4* src = (const IK_GLOBAL u4*)(W + w0);
                     __syncthreads();  // the previous window's readers are done
                     for (uint32_t k = (uint32_t)lane; k < nq; k += 64) *(u4*)(s_win + 4 * k) = src[k];
                     __syncthreads();
+                    ck_setup += clock64() - ck1;
                 }
                 const WaveLdsWin win{(const lds_u32*)s_win, w0 << 5};
                 const int j = lane;
                 const bool act = j < sp.nsub;
                 const uint64_t lo = bp + 32ull * sp.lw * (uint64_t)j;
                 const uint64_t hi = j + 1 < sp.nsub ? lo + 32ull * sp.lw : re;
-                wave::SubOut o{region + used + (uint64_t)j * sp.cap, sp.cap};
+                WaveOut o{region + used + (uint64_t)j * sp.cap, sp.cap, 0u, (lds_u32a*)s_ring + lane};
                 wave::SubRes r{};
                 r.start = r.exit = ~0ull;
                 if (act) {
@@ -679,6 +879,7 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
         r.kcycles = (uint32_t)((clock64() - c0) >> 10);
         r.blocks = nblocks;
         r.pieces = npieces;
+        r.kc_setup = (uint32_t)(ck_setup >> 10);
         res[t] = r;
     }
 }

@@ -1356,16 +1356,26 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                     if (j.state != 1) continue;
                     const bool rows_ok = herr[k] == 0;
                     bool lanes_ok = true;
-                    for (size_t i = 0; i < j.lanes.start.size(); ++i, ++t) lanes_ok = lanes_ok && hxst[2 * t] == 0;
+                    for (size_t i = 0; i < j.lanes.start.size(); ++i, ++t) {
+                        lanes_ok = lanes_ok && hxst[2 * t] == 0;
+                        if (timing && hxst[2 * t] != 0) {
+                            const infl::LaneResult& q = j.lanes.res[i];
+                            fprintf(stderr, "[png] stream %d lane %zu/%zu: expand failed (start %llu stop %llu end %llu out %llu "
+                                    "tokens %u pieces %u blocks %u status %d)\n", j.idx, i, j.lanes.start.size(),
+                                    (unsigned long long)j.lanes.start[i], (unsigned long long)j.lanes.stop[i],
+                                    (unsigned long long)q.end_bit, (unsigned long long)q.out_len, q.ntok, q.pieces, q.blocks,
+                                    q.status);
+                        }
+                    }
                     if (!rows_ok || !lanes_ok) reject(j, !lanes_ok ? "expand status" : "row filter bytes");
                 }
             }
         }
         gate_leave(kGateKernels);  // unless the caller pinned it (transform_part: resize + encode next)
         if (timing && !hl.empty()) {  // per-lane profile of the last decode round and the expand pass
-            double si = 0, sc = 0, sx = 0, mi = 0, mc = 0, mx = 0, sb = 0, mb = 0;
+            double si = 0, sc = 0, sx = 0, mi = 0, mc = 0, mx = 0, sb = 0, mb = 0, ss = 0;
             for (size_t t = 0; t < hres.size(); ++t) {
-                si += hres[t].iters; sc += hres[t].kcycles; sb += hres[t].blocks;
+                si += hres[t].iters; sc += hres[t].kcycles; sb += hres[t].blocks; ss += hres[t].kc_setup;
                 mi = std::max(mi, (double)hres[t].iters); mc = std::max(mc, (double)hres[t].kcycles);
                 mb = std::max(mb, (double)hres[t].blocks);
             }
@@ -1375,8 +1385,9 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             }
             const double n1 = (double)std::max<size_t>(1, hres.size()), n2 = (double)std::max<size_t>(1, hxst.size() / 2);
             fprintf(stderr, "[png] decode lanes %zu: iters mean %.0f max %.0f, blocks mean %.2f max %.0f, kcycles mean %.0f "
-                    "max %.0f (%.0f cycles/iter); expand kcycles mean %.0f max %.0f\n", hres.size(), si / n1, mi, sb / n1,
-                    mb, sc / n1, mc, 1024.0 * sc / std::max(1.0, si), sx / n2, mx);
+                    "max %.0f (%.0f cycles/iter; setup kcycles mean %.0f); expand kcycles mean %.0f max %.0f\n",
+                    hres.size(), si / n1, mi, sb / n1, mb, sc / n1, mc, 1024.0 * sc / std::max(1.0, si), ss / n1, sx / n2,
+                    mx);
         }
         tim[0] = S.t_host;
         tim[2] = count_dev;

@@ -305,8 +305,25 @@ int ikm_inflate_wave(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8_t*
         stats[13] += cat.size();
         cat.resize(cat.size() + 16, (uint16_t)infl::kTokPad);
         infl::TokInHost tin{cat.data()};
-        if (infl::expand_lane(tin, (uint32_t)(cat.size() - 16), infl::U16Out{u16.data()}, obase[i], L.res[i].out_len))
+        if (infl::expand_lane(tin, (uint32_t)(cat.size() - 16), infl::U16Out{u16.data()}, obase[i], L.res[i].out_len)) {
+            if (getenv("IKM_DEBUG")) {
+                // where the tokens stop making sense: count the output they describe
+                uint64_t n = 0, bad = 0;
+                for (size_t q = 0; q + 16 < cat.size(); ++q) {
+                    const uint32_t v = cat[q];
+                    if (v == infl::kTokPad) continue;
+                    if ((v & 0xFF00u) == infl::kTokRaw) { ++n; continue; }
+                    if ((v & 0xFF00u) == infl::kTokMatch) { n += (v & 255u) + 3; ++q; continue; }
+                    if (!bad) fprintf(stderr, "lane %zu: bad token 0x%04x at %zu (out so far %llu)\n", i, v, q,
+                                      (unsigned long long)n);
+                    ++bad;
+                }
+                fprintf(stderr, "lane %zu expand failed: tokens %zu describe %llu bytes (out_len %llu), %llu bad\n", i,
+                        cat.size() - 16, (unsigned long long)n, (unsigned long long)L.res[i].out_len,
+                        (unsigned long long)bad);
+            }
             return -4;
+        }
     }
     const int shift = 12;
     std::vector<int> pages((total >> shift) + 1);

@@ -29,7 +29,7 @@ struct Lanes {
         start.insert(start.begin() + (long)k, b);
         stop.insert(stop.begin() + (long)k, stop[i]);
         stop[i] = b;
-        res.insert(res.begin() + (long)k, infl::LaneResult{0, 0, 0, infl::kLaneCorrupt, 0, 0, 0, 0, 0});
+        res.insert(res.begin() + (long)k, infl::LaneResult{0, 0, 0, infl::kLaneCorrupt, 0, 0, 0, 0, 0, 0, 0});
         dirty.insert(dirty.begin() + (long)k, 1);
         tbase.insert(tbase.begin() + (long)k, 0);
         tcap.insert(tcap.begin() + (long)k, 0);
@@ -58,7 +58,7 @@ inline void build(const std::vector<int64_t>& cand, Lanes& L) {
         if (c >= 0 && (L.start.empty() || (uint64_t)c > L.start.back())) L.start.push_back((uint64_t)c);
     L.stop.resize(L.start.size());
     for (size_t i = 0; i < L.start.size(); ++i) L.stop[i] = i + 1 < L.start.size() ? L.start[i + 1] : ~0ull;
-    L.res.assign(L.start.size(), infl::LaneResult{0, 0, 0, infl::kLaneCorrupt, 0, 0, 0, 0, 0});
+    L.res.assign(L.start.size(), infl::LaneResult{0, 0, 0, infl::kLaneCorrupt, 0, 0, 0, 0, 0, 0, 0});
     L.dirty.assign(L.start.size(), 1);
     L.tbase.assign(L.start.size(), 0);
     L.tcap.assign(L.start.size(), 0);

@@ -201,43 +201,26 @@ IK_HD uint32_t dist_slow(uint64_t v, const Code& C, const Syms& syms) {
     return dist_symbol_entry(s, (uint32_t)D);
 }
 
-// Token output of one sub-lane: tokens go to p[0 .. cap), 8 at a time (a full
-// group is stored as one 16-byte store), the last group padded with kTokPad.
-struct SubOut {
-    IK_GLOBAL uint16_t* p;
+// Token output of one sub-lane: tokens go to p[0 .. cap) in groups of 8 (one
+// 16-byte store each); the last group is padded with kTokPad.  put4 takes up to
+// four tokens at once (a step's output).  The host form writes straight to p; the
+// GPU's (ik_png.hip WaveOut) stages the open group in LDS.
+struct SubOutHost {
+    uint16_t* p;
     uint32_t cap;        // tokens (a multiple of 8)
-    uint32_t n = 0;      // tokens written
-    uint64_t h0 = 0, h1 = 0;
-    bool over = false;   // the region was too small
-    IK_HD void put(uint32_t t) {
-        h0 = (h0 >> 16) | (h1 << 48);
-        h1 = (h1 >> 16) | ((uint64_t)t << 48);
-        ++n;
-        if ((n & 7u) == 0) {
-            if (n > cap) {
-                over = true;
-            } else {
-#if defined(__HIP_DEVICE_COMPILE__)
-                typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-                const u4 q = {(uint32_t)h0, (uint32_t)(h0 >> 32), (uint32_t)h1, (uint32_t)(h1 >> 32)};
-                *reinterpret_cast<IK_GLOBAL u4*>(p + (n - 8)) = q;
-#else
-                for (int k = 0; k < 4; ++k) {
-                    p[n - 8 + k] = (uint16_t)(h0 >> (16 * k));
-                    p[n - 4 + k] = (uint16_t)(h1 >> (16 * k));
-                }
-#endif
-            }
+    uint32_t n = 0;      // tokens put
+    IK_HD void reset() { n = 0; }
+    IK_HD void put4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+        const uint32_t t[4] = {a, b, c, d};
+        for (uint32_t i = 0; i < k; ++i) {
+            if (n < cap) p[n] = (uint16_t)t[i];
+            ++n;
         }
     }
-    // pad the last group; returns the padded count
-    IK_HD uint32_t finish() {
-        const uint32_t real = n;
-        while (n & 7u) put(infl::kTokPad);
-        n = real;
-        return (real + 7u) & ~7u;
+    IK_HD void finish() {
+        for (uint32_t i = n; i < ((n + 7u) & ~7u); ++i)
+            if (i < cap) p[i] = (uint16_t)infl::kTokPad;
     }
-    IK_HD void reset() { n = 0; over = false; }
 };
 
 // Result of one sub-lane pass.
@@ -253,101 +236,82 @@ struct SubRes {
 };
 
 // Decode one sub-lane.  From bit p0 (a guessed boundary, or the exact one when
-// p0 >= lo), symbols before `lo` are the warm-up (no output; invalid codes and
-// end-of-block skipped); from the first boundary >= lo (START) tokens go out until
-// the first boundary >= hi (EXIT) or an end-of-block code.  win(pos) = the 64
-// stream bits from pos; lit / dist = the shared tables; C / syms = the codes.
-template <class Win, class LitTab, class DistTab, class LSyms, class DSyms>
+// p0 >= lo), symbols before `lo` are the warm-up (no output; invalid codes skip a
+// bit, end-of-block codes are stepped over); from the first boundary >= lo (START)
+// tokens go out until the first boundary >= hi (EXIT) or an end-of-block code.
+// win(pos) = the 64 stream bits from pos; lit / dist = the shared tables; C / syms
+// = the codes (the slow path).  One step decodes up to four literals (two table
+// entries of one or two each) or one match; both are computed and selected, so
+// the lanes of a wave stay together except on the rare slow codes.
+template <class Win, class LitTab, class DistTab, class LSyms, class DSyms, class Out>
 IK_HD void sub_decode(Win& win, uint64_t p0, uint64_t lo, uint64_t hi, const LitTab& lit, const DistTab& dist,
-                      const Code& LC, const LSyms& lsyms, const Code& DC, const DSyms& dsyms, SubOut& out,
+                      const Code& LC, const LSyms& lsyms, const Code& DC, const DSyms& dsyms, Out& out,
                       SubRes& r) {
     uint64_t pos = p0;
     bool started = p0 >= lo;
     r.start = started ? p0 : 0;
-    r.exit = 0;
-    r.out = 0;
     r.eob = 0;
     r.bad = 0;
     out.reset();
     uint64_t cnt = 0;
-    r.steps = 0;
+    uint32_t steps = 0;
     for (;;) {
-        ++r.steps;
-        const uint64_t limit = started ? hi : lo;
+        ++steps;
+        uint64_t limit = started ? hi : lo;
         if (pos >= limit) {
             if (started) break;
-            started = true;
+            started = true;  // START: the first boundary at or past lo
             r.start = pos;
-            continue;
+            limit = hi;
+            if (pos >= limit) break;
         }
         const uint64_t v = win(pos);
         uint32_t e1 = lit[(uint32_t)v & kLM];
         if (e_kind(e1) == kKSlow) e1 = lit_slow(v, LC, lsyms);
-        const uint32_t k1 = e_kind(e1);
-        if (k1 == kKLit) {
-            // up to four literals: this entry's one or two, then the next entry's
-            const uint32_t L1 = e_len1(e1);
-            const bool two1 = e_two(e1) && pos + L1 < limit;
-            const uint32_t c1 = two1 ? e_bits(e1) : L1;  // bits taken from this entry
-            uint64_t q = pos + c1;
-            if (started) {
-                out.put(infl::kTokRaw | e_lit1(e1));
-                if (two1) out.put(infl::kTokRaw | e_lit2(e1));
-                cnt += two1 ? 2 : 1;
-            }
-            if ((two1 || !e_two(e1)) && q < limit) {  // all of this entry's literals taken: the next entry
-                const uint32_t e2 = lit[(uint32_t)(v >> c1) & kLM];
-                if (e_kind(e2) == kKLit) {
-                    const uint32_t L2 = e_len1(e2);
-                    const bool two2 = e_two(e2) && q + L2 < limit;
-                    if (started) {
-                        out.put(infl::kTokRaw | e_lit1(e2));
-                        if (two2) out.put(infl::kTokRaw | e_lit2(e2));
-                        cnt += two2 ? 2 : 1;
-                    }
-                    q += two2 ? e_bits(e2) : L2;
-                }
-            }
-            pos = q;
-            continue;
+        const uint32_t k1 = e_kind(e1), n1 = e_bits(e1), L1 = e_len1(e1);
+        // literals: e1's one or two, then the next entry's (each taken only while
+        // it starts before the limit)
+        const bool isl = k1 == kKLit;
+        const bool two1 = e_two(e1) && pos + L1 < limit;
+        const uint32_t c1 = two1 ? n1 : L1;
+        const uint32_t e2 = lit[(uint32_t)(v >> c1) & kLM];
+        const bool lit2 = isl && (two1 || !e_two(e1)) && pos + c1 < limit && e_kind(e2) == kKLit;
+        const uint32_t L2 = e_len1(e2);
+        const bool two2 = lit2 && e_two(e2) && pos + c1 + L2 < limit;
+        const uint32_t c2 = lit2 ? (two2 ? e_bits(e2) : L2) : 0u;
+        // a match (computed for every symbol, used for a length code)
+        const uint32_t le = e_lextra(e1);
+        const uint32_t ll = e_lbase(e1) + ((uint32_t)(v >> n1) & ((1u << le) - 1u));
+        const uint64_t vd = v >> (n1 + le);
+        uint32_t d = dist[(uint32_t)vd & kDM];
+        const bool isn = k1 == kKLen;
+        if (isn && d_slow(d)) d = dist_slow(vd, DC, dsyms);
+        const bool bad = k1 == kKSlow || (isn && d_slow(d));
+        const uint32_t D = d_len(d), de = d_extra(d);
+        const uint32_t dd = d_base(d) + ((uint32_t)(vd >> D) & ((1u << de) - 1u));
+        const bool eob = k1 == kKEob;
+        if (started && (bad || eob)) {
+            if (eob) pos += n1;
+            r.eob = eob;
+            r.bad = bad;
+            break;
         }
-        if (k1 == kKLen) {
-            const uint32_t L = e_bits(e1), le = e_lextra(e1);
-            const uint32_t ll = e_lbase(e1) + ((uint32_t)(v >> L) & ((1u << le) - 1u));
-            const uint64_t vd = v >> (L + le);
-            uint32_t d = dist[(uint32_t)vd & kDM];
-            if (d_slow(d)) d = dist_slow(vd, DC, dsyms);
-            if (d_slow(d)) {  // no distance code here
-                if (started) { r.bad = 1; break; }
-                pos += 1;
-                continue;
-            }
-            const uint32_t D = d_len(d), de = d_extra(d);
-            const uint32_t dd = d_base(d) + ((uint32_t)(vd >> D) & ((1u << de) - 1u));
-            if (started) {
-                out.put(infl::kTokMatch | (ll - 3u));
-                out.put(dd - 1u);
-                cnt += ll;
-            }
-            pos += L + le + D + de;
-            continue;
-        }
-        if (k1 == kKEob) {
-            pos += e_bits(e1);
-            if (started) {
-                r.eob = 1;
-                break;
-            }
-            continue;
-        }
-        // no literal/length code at pos
-        if (started) { r.bad = 1; break; }
-        pos += 1;
+        // tokens: literals a b c d (two1 / lit2 / two2 say which), or the match's two
+        const uint32_t t1 = isl ? infl::kTokRaw | e_lit1(e1) : infl::kTokMatch | (ll - 3u);
+        const uint32_t t2 = isl ? infl::kTokRaw | (two1 ? e_lit2(e1) : e_lit1(e2)) : dd - 1u;
+        const uint32_t t3 = infl::kTokRaw | (two1 ? e_lit1(e2) : e_lit2(e2));
+        const uint32_t t4 = infl::kTokRaw | e_lit2(e2);
+        const uint32_t nl = 1u + (two1 ? 1u : 0u) + (lit2 ? 1u : 0u) + (two2 ? 1u : 0u);
+        const uint32_t k = !started ? 0u : isl ? nl : isn ? 2u : 0u;
+        out.put4(t1, t2, t3, t4, k);
+        cnt += !started ? 0u : isl ? nl : isn ? ll : 0u;
+        pos += isl ? c1 + c2 : isn ? n1 + le + D + de : eob ? n1 : 1u;  // (warm-up: an invalid code skips a bit)
     }
     r.exit = pos;
     r.out = cnt;
     r.ntok = out.n;
-    r.over = out.over;
+    r.over = ((out.n + 7u) & ~7u) > out.cap;  // (the padded last group must fit too)
+    r.steps = steps;
 }
 
 // One lane's pieces for the expand pass, entry k = (base, vstart): piece k is the
@@ -378,7 +342,9 @@ IK_HD Split split_range(uint64_t bp, uint64_t re, bool big) {
     Split s;
     s.nsub = (int)(ns < 1 ? 1 : ns);
     s.lw = (uint32_t)lw;
-    const uint64_t c = (big ? 32 * lw : 8 * lw) + 24;  // a token costs >= 1 bit; image data ~8 bits
+    // a token costs >= 1 bit (big); image data ~0.23 tokens per bit, more in a sub-range's
+    // compressible stretches: 0.375 leaves room for those without a second round
+    const uint64_t c = (big ? 32 * lw : 12 * lw) + 32;
     s.cap = (uint32_t)((c + 7) & ~7ull);
     return s;
 }
@@ -400,8 +366,9 @@ IK_HD uint64_t window_end(uint64_t bp, uint64_t stop_eff, uint64_t prev_bits) {
 // (a quarter token per bit, plus each window's rounding; `big`: a token per bit,
 // the bound, for a lane whose region overflowed)
 IK_HD uint64_t region_capacity(uint64_t bits, bool big) {
-    const uint64_t slack = (bits / kWindowBits + 2) * 2560 + 64;
-    return big ? bits + 32ull * pieces_capacity(bits) + slack : bits / 4 + slack;
+    const uint64_t slack = (bits / kWindowBits + 2) * 3072 + 64;
+    const uint64_t c = big ? bits + 32ull * pieces_capacity(bits) + slack : bits / 8 * 3 + slack;
+    return (c + 7) & ~7ull;  // (regions start 16-byte aligned: whole groups of 8 tokens)
 }
 
 // statistics of the CPU model (ikm_inflate_wave)
@@ -510,7 +477,7 @@ inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, 
                 for (int j = 0; j < sp.nsub; ++j) lo[j] = bp + 32ull * sp.lw * (uint64_t)j;
                 lo[sp.nsub] = re;
                 for (int j = 0; j < sp.nsub; ++j) {
-                    SubOut o{reinterpret_cast<IK_GLOBAL uint16_t*>(region + used + (uint64_t)j * sp.cap), sp.cap};
+                    SubOutHost o{region + used + (uint64_t)j * sp.cap, sp.cap};
                     const uint64_t p0 = j == 0 ? bp : (lo[j] >= bp + warm ? lo[j] - warm : bp);
                     sub_decode(win, p0, lo[j], lo[j + 1], lit, dist, LC, lsyms, DC, dsyms, o, sr[j]);
                     o.finish();
@@ -532,7 +499,7 @@ inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, 
                     }
                     for (int j = v + 1; j < sp.nsub; ++j) {
                         if (!redo[j]) continue;
-                        SubOut o{reinterpret_cast<IK_GLOBAL uint16_t*>(region + used + (uint64_t)j * sp.cap), sp.cap};
+                        SubOutHost o{region + used + (uint64_t)j * sp.cap, sp.cap};
                         sub_decode(win, ex[j - 1], lo[j], lo[j + 1], lit, dist, LC, lsyms, DC, dsyms, o, sr[j]);
                         o.finish();
                         if (stats) ++stats->redo_passes;
@@ -556,6 +523,22 @@ inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, 
                     done = 4;
                     break;
                 }
+#ifdef IKM_WAVE_DEBUG
+                for (int j = 0; j <= v; ++j) {
+                    const uint16_t* q = region + used + (uint64_t)j * sp.cap;
+                    uint64_t nb = 0;
+                    for (uint32_t k = 0; k < ((sr[j].ntok + 7u) & ~7u); ++k) {
+                        const uint32_t t = q[k];
+                        if ((t & 0xFF00u) == infl::kTokRaw) ++nb;
+                        else if ((t & 0xFF00u) == infl::kTokMatch) { nb += (t & 255u) + 3; ++k; }
+                    }
+                    if (nb != sr[j].out)
+                        fprintf(stderr, "sub-lane %d of %d: tokens %u describe %llu bytes, counted %llu (start %llu exit %llu lo %llu hi %llu eob %d)\n",
+                                j, sp.nsub, sr[j].ntok, (unsigned long long)nb, (unsigned long long)sr[j].out,
+                                (unsigned long long)sr[j].start, (unsigned long long)sr[j].exit, (unsigned long long)lo[j],
+                                (unsigned long long)lo[j + 1], sr[j].eob);
+                }
+#endif
                 for (int j = 0; j <= v; ++j) {
                     pt.push_back({(uint32_t)(used + (uint64_t)j * sp.cap), (uint32_t)written});
                     written += (sr[j].ntok + 7u) & ~7u;

@@ -108,6 +108,21 @@ def test_pillow_png_streams(model, mode, c):
     assert st["lanes"] >= 8 and st["rounds"] == 1
 
 
+@pytest.mark.parametrize("size,seed", [(1024, 8), (640, 480), (1500, 3)])
+def test_pillow_rgba_frames(model, size, seed):
+    """Pillow's own encoder on bench-pattern RGBA frames: sub-lane pieces that fill
+    their token capacity exactly (the padded last group must fit too -- a GPU
+    test caught a piece whose last group was not stored)."""
+    from PIL import Image
+    img = ikutil.synth(size, size, 4, seed=seed, pattern="S")
+    b = io.BytesIO()
+    Image.fromarray(img, "RGBA").save(b, format="PNG")
+    z = _idat(b.getvalue())
+    raw = zlib.decompress(z)
+    rc, out, st = inflate(model, z, len(raw), 16384)
+    assert rc == 0 and out == raw, st
+
+
 def test_bench_frame_synchronises(model):
     """A bench-pattern 2048^2 RGBA8 frame as Pillow writes it: every lane's
     sub-lanes synchronise within the warm-up (no fix round), and the sub-lanes
