@@ -415,12 +415,10 @@ constexpr uint32_t kWaveWinWords = (uint32_t)(wave::kWindowBits / 32) + 16;  // 
 
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 
-// the 64 stream bits from pos, out of the staged window (w[0] = stream bit `base`)
+// the 64 stream bits from bit o of the staged window (relative positions: w[0]'s bit 0 = 0)
 struct WaveLdsWin {
     const lds_u32* w;
-    uint64_t base;
-    __device__ uint64_t operator()(uint64_t pos) const {
-        const uint32_t o = (uint32_t)(pos - base);
+    __device__ uint64_t operator()(uint32_t o) const {
         const uint32_t wi = o >> 5, sh = o & 31u;
         const uint32_t a = w[wi], b = w[wi + 1], c = w[wi + 2];
         const uint32_t lo = __builtin_amdgcn_alignbit(b, a, sh), hi = __builtin_amdgcn_alignbit(c, b, sh);
@@ -791,16 +789,18 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
                     __syncthreads();
                     ck_setup += clock64() - ck1;
                 }
-                const WaveLdsWin win{(const lds_u32*)s_win, w0 << 5};
+                const WaveLdsWin win{(const lds_u32*)s_win};
                 const int j = lane;
                 const bool act = j < sp.nsub;
-                const uint64_t lo = bp + 32ull * sp.lw * (uint64_t)j;
-                const uint64_t hi = j + 1 < sp.nsub ? lo + 32ull * sp.lw : re;
+                // positions relative to the staged window's first bit (w0 << 5)
+                const uint32_t rb = (uint32_t)(bp - (w0 << 5));
+                const uint32_t lo = rb + 32u * sp.lw * (uint32_t)j;
+                const uint32_t hi = j + 1 < sp.nsub ? lo + 32u * sp.lw : (uint32_t)(re - (w0 << 5));
                 WaveOut o{region + used + (uint64_t)j * sp.cap, sp.cap, 0u, (lds_u32a*)s_ring + lane};
                 wave::SubRes r{};
-                r.start = r.exit = ~0ull;
+                r.start = r.exit = ~0u;
                 if (act) {
-                    const uint64_t p0 = j == 0 ? bp : (lo >= bp + wave::kWarmBits ? lo - wave::kWarmBits : bp);
+                    const uint32_t p0 = j == 0 ? rb : (lo >= rb + wave::kWarmBits ? lo - (uint32_t)wave::kWarmBits : rb);
                     wave::sub_decode(win, p0, lo, hi, lit, dist, s_code[0], lsym, s_code[1], dsym, o, r);
                     o.finish();
                     steps += r.steps;
@@ -808,7 +808,7 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
                 // fix rounds (all lanes in the shuffles; the redone sub-lanes diverge)
                 int v = 0;
                 for (;;) {
-                    const uint64_t exp = shfl_up_u64(r.exit, 1);
+                    const uint32_t exp = (uint32_t)__shfl_up((int)r.exit, 1, 64);
                     const int eobp = __shfl_up(r.eob, 1, 64), badp = __shfl_up(r.bad, 1, 64);
                     const bool chain = j == 0 || (r.start == exp && !eobp && !badp);
                     const unsigned long long broken = __ballot(act && j >= 1 && !chain);
@@ -841,7 +841,7 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
                 total += wave_sum_u64(in ? r.out : 0ull);
                 // the next window's sub-lanes start past the last piece (its region's rest is free)
                 used += (uint64_t)v * sp.cap + (uint64_t)((__builtin_amdgcn_readlane((int)r.ntok, v) + 7u) & ~7u);
-                const uint64_t exv = readlane_u64(r.exit, v);
+                const uint64_t exv = (w0 << 5) + (uint32_t)__builtin_amdgcn_readlane((int)r.exit, v);
                 if (__builtin_amdgcn_readlane(r.bad, v)) { done = 3; break; }
                 if (__builtin_amdgcn_readlane(r.eob, v)) {
                     p = exv;

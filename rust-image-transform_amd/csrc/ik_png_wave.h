@@ -44,7 +44,10 @@ constexpr uint32_t kLM = (1u << kLB) - 1u, kDM = (1u << kDB) - 1u;
 constexpr int kSub = 64;                // sub-lanes (one wave)
 constexpr int kWarmBits = 256;          // warm-up before a guessed sub-range start
 constexpr int kMinSubBits = 512;        // fewer sub-lanes for shorter ranges
-constexpr uint64_t kWindowBits = 8ull * 20480;  // stream bits of one window of a block's body (LDS staging)
+// stream bits of one window of a block's body (LDS staging): 12 KiB keeps the
+// wave's LDS at ~20 KB (8 waves per CU) at ~8 % more sub-lane steps than a
+// window holding a whole ~18 KB block
+constexpr uint64_t kWindowBits = 8ull * 12288;
 
 // literal/length entry (u32):
 //   bits 0..4   bits consumed by the entry's symbols (0: slow / invalid)
@@ -223,10 +226,10 @@ struct SubOutHost {
     }
 };
 
-// Result of one sub-lane pass.
+// Result of one sub-lane pass (positions relative to the window's base bit).
 struct SubRes {
-    uint64_t start;   // first symbol boundary >= the range start (or where an exact start began)
-    uint64_t exit;    // first symbol boundary >= the range end, or just past a verified end of block
+    uint32_t start;   // first symbol boundary >= the range start (or where an exact start began)
+    uint32_t exit;    // first symbol boundary >= the range end, or just past a verified end of block
     uint64_t out;     // output bytes from start to exit
     uint32_t ntok;    // tokens written
     int eob;          // an end-of-block code ended the pass (exit = just past it)
@@ -235,8 +238,9 @@ struct SubRes {
     uint32_t steps;   // loop iterations (profile)
 };
 
-// Decode one sub-lane.  From bit p0 (a guessed boundary, or the exact one when
-// p0 >= lo), symbols before `lo` are the warm-up (no output; invalid codes skip a
+// Decode one sub-lane.  Positions are bits relative to the window's base (32-bit
+// arithmetic on the step's chain).  From bit p0 (a guessed boundary, or the exact
+// one when p0 >= lo), symbols before `lo` are the warm-up (no output; invalid codes skip a
 // bit, end-of-block codes are stepped over); from the first boundary >= lo (START)
 // tokens go out until the first boundary >= hi (EXIT) or an end-of-block code.
 // win(pos) = the 64 stream bits from pos; lit / dist = the shared tables; C / syms
@@ -244,10 +248,10 @@ struct SubRes {
 // entries of one or two each) or one match; both are computed and selected, so
 // the lanes of a wave stay together except on the rare slow codes.
 template <class Win, class LitTab, class DistTab, class LSyms, class DSyms, class Out>
-IK_HD void sub_decode(Win& win, uint64_t p0, uint64_t lo, uint64_t hi, const LitTab& lit, const DistTab& dist,
+IK_HD void sub_decode(Win& win, uint32_t p0, uint32_t lo, uint32_t hi, const LitTab& lit, const DistTab& dist,
                       const Code& LC, const LSyms& lsyms, const Code& DC, const DSyms& dsyms, Out& out,
                       SubRes& r) {
-    uint64_t pos = p0;
+    uint32_t pos = p0;
     bool started = p0 >= lo;
     r.start = started ? p0 : 0;
     r.eob = 0;
@@ -257,7 +261,7 @@ IK_HD void sub_decode(Win& win, uint64_t p0, uint64_t lo, uint64_t hi, const Lit
     uint32_t steps = 0;
     for (;;) {
         ++steps;
-        uint64_t limit = started ? hi : lo;
+        uint32_t limit = started ? hi : lo;
         if (pos >= limit) {
             if (started) break;
             started = true;  // START: the first boundary at or past lo
@@ -473,13 +477,19 @@ inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, 
                 if (used + (uint64_t)sp.nsub * sp.cap > cap) { r.status = infl::kLaneOverflow; done = 3; break; }
                 if (stats) ++stats->windows;
                 SubRes sr[kSub];
-                uint64_t lo[kSub + 1];
-                for (int j = 0; j < sp.nsub; ++j) lo[j] = bp + 32ull * sp.lw * (uint64_t)j;
-                lo[sp.nsub] = re;
+                // positions relative to the window's first bit bp
+                struct RelWin {
+                    WinFn& w;
+                    uint64_t base;
+                    uint64_t operator()(uint32_t rel) const { return w(base + rel); }
+                } rwin{win, bp};
+                uint32_t lo[kSub + 1];
+                for (int j = 0; j < sp.nsub; ++j) lo[j] = 32u * sp.lw * (uint32_t)j;
+                lo[sp.nsub] = (uint32_t)(re - bp);
                 for (int j = 0; j < sp.nsub; ++j) {
                     SubOutHost o{region + used + (uint64_t)j * sp.cap, sp.cap};
-                    const uint64_t p0 = j == 0 ? bp : (lo[j] >= bp + warm ? lo[j] - warm : bp);
-                    sub_decode(win, p0, lo[j], lo[j + 1], lit, dist, LC, lsyms, DC, dsyms, o, sr[j]);
+                    const uint32_t p0 = j == 0 ? 0u : (lo[j] >= warm ? lo[j] - (uint32_t)warm : 0u);
+                    sub_decode(rwin, p0, lo[j], lo[j + 1], lit, dist, LC, lsyms, DC, dsyms, o, sr[j]);
                     o.finish();
                     if (stats) { ++stats->sub_passes; stats->steps += sr[j].steps; }
                 }
@@ -491,7 +501,7 @@ inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, 
                     while (v + 1 < sp.nsub && !sr[v].eob && !sr[v].bad && sr[v + 1].start == sr[v].exit) ++v;
                     if (sr[v].eob || sr[v].bad || v + 1 == sp.nsub) break;
                     ++rounds;
-                    uint64_t ex[kSub];
+                    uint32_t ex[kSub];
                     bool redo[kSub];
                     for (int j = 0; j < sp.nsub; ++j) {
                         ex[j] = sr[j].exit;
@@ -500,7 +510,7 @@ inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, 
                     for (int j = v + 1; j < sp.nsub; ++j) {
                         if (!redo[j]) continue;
                         SubOutHost o{region + used + (uint64_t)j * sp.cap, sp.cap};
-                        sub_decode(win, ex[j - 1], lo[j], lo[j + 1], lit, dist, LC, lsyms, DC, dsyms, o, sr[j]);
+                        sub_decode(rwin, ex[j - 1], lo[j], lo[j + 1], lit, dist, LC, lsyms, DC, dsyms, o, sr[j]);
                         o.finish();
                         if (stats) ++stats->redo_passes;
                     }
@@ -549,12 +559,12 @@ inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, 
                 used += (uint64_t)v * sp.cap + ((sr[v].ntok + 7u) & ~7u);
                 if (sr[v].bad) { done = 3; break; }  // an invalid code on the verified chain: corrupt
                 if (sr[v].eob) {
-                    p = sr[v].exit;
+                    p = bp + sr[v].exit;
                     prev_bits = p - body;
                     done = 1;
                     break;
                 }
-                bp = sr[v].exit;  // the window ended inside the block: the next window
+                bp += sr[v].exit;  // the window ended inside the block: the next window
             }
             if (done == 4) {  // split: undo this block (its earlier windows' pieces and output)
                 pt.resize(blk_pieces);
