@@ -460,11 +460,14 @@ struct WaveOut {
         const u4 q = {ring[64u * r0], ring[64u * (r0 + 1u)], ring[64u * (r0 + 2u)], ring[64u * (r0 + 3u)]};
         *reinterpret_cast<IK_GLOBAL u4*>(p + g) = q;
     }
+    // all four slots are written whatever k is: a slot past the k tokens is a free
+    // slot of the open group or the next, which a later token overwrites before the
+    // group is stored (and it is never in the group this call completes)
     __device__ void put4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
-        if (k > 0u) slot(n, a);
-        if (k > 1u) slot(n + 1u, b);
-        if (k > 2u) slot(n + 2u, c);
-        if (k > 3u) slot(n + 3u, d);
+        slot(n, a);
+        slot(n + 1u, b);
+        slot(n + 2u, c);
+        slot(n + 3u, d);
         const uint32_t n2 = n + k;
         if ((n2 ^ n) & ~7u) flush((n2 & ~7u) - 8u);  // a group completed
         n = n2;
@@ -936,27 +939,52 @@ __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const
     // a thread keeps its current piece (base, virtual start) and the next one's start
     const uint32_t np = pieces ? L.npieces : 0u;
     const IK_GLOBAL uint2* P = (const IK_GLOBAL uint2*)(pieces + (pieces ? L.pbase : 0));
-    uint32_t kc = 0, pc_base = 0, pc_start = 0, pn_start = 0xFFFFFFFFu;
+    // the first 128 entries in registers (lane x: entries x and 64 + x), read as
+    // wave-uniform values (readlane) when a window is loaded; past 128, memory
+    uint32_t pr_b0 = 0, pr_s0 = 0, pr_b1 = 0, pr_s1 = 0;
     if (np) {
-        pc_base = P[0].x;
-        pn_start = np > 1 ? P[1].y : 0xFFFFFFFFu;
+        if ((uint32_t)x < np) { pr_b0 = P[x].x; pr_s0 = P[x].y; }
+        if ((uint32_t)x + 64u < np) { pr_b1 = P[x + 64].x; pr_s1 = P[x + 64].y; }
     }
+    auto piece_base = [&](uint32_t k) -> uint32_t {  // k wave-uniform
+        if (k < 64u) return (uint32_t)__builtin_amdgcn_readlane((int)pr_b0, (int)k);
+        if (k < 128u) return (uint32_t)__builtin_amdgcn_readlane((int)pr_b1, (int)(k - 64u));
+        return P[k].x;
+    };
+    auto piece_start = [&](uint32_t k) -> uint32_t {  // k wave-uniform
+        if (k < 64u) return (uint32_t)__builtin_amdgcn_readlane((int)pr_s0, (int)k);
+        if (k < 128u) return (uint32_t)__builtin_amdgcn_readlane((int)pr_s1, (int)(k - 64u));
+        return P[k].y;
+    };
+    uint32_t kb = 0;  // the piece holding the current window's first token (only grows)
     uint32_t t = 0;
     int64_t cnt = 0;
     bool have_tab = false, bad = false;
     // this thread's 4 tokens of the batch window at a (a multiple of 4; the region
     // is 16-byte aligned and padded past ntok to a multiple of 8 tokens)
+    // (called by the whole wave with a wave-uniform a)
     auto load4 = [&](uint32_t a) -> uint64_t {
         const uint32_t i = a + 4u * (uint32_t)x;
-        if (i >= ntok) return 0xFFFEFFFEFFFEFFFEull;
-        if (!np) return *(const IK_GLOBAL uint64_t*)(T + i);
-        while (i >= pn_start) {  // (the index only grows: a piece or two per window)
-            ++kc;
-            pc_base = P[kc].x;
-            pc_start = pn_start;
-            pn_start = kc + 1 < np ? P[kc + 1].y : 0xFFFFFFFFu;
+        if (!np) return i < ntok ? *(const IK_GLOBAL uint64_t*)(T + i) : 0xFFFEFFFEFFFEFFFEull;
+        while (kb + 1 < np && piece_start(kb + 1) <= a) ++kb;
+        // the window's 256 tokens lie in pieces kb .. kb + 7 (a piece of a sub-lane
+        // holds tens of tokens or more); each thread picks its own
+        uint32_t base = piece_base(kb), st = piece_start(kb);
+#pragma unroll
+        for (uint32_t m = 1; m < 8; ++m) {
+            if (kb + m < np) {
+                const uint32_t sm = piece_start(kb + m);
+                if (i >= sm) { base = piece_base(kb + m); st = sm; }
+            }
         }
-        return *(const IK_GLOBAL uint64_t*)(T + pc_base + (i - pc_start));
+        if (i >= ntok) return 0xFFFEFFFEFFFEFFFEull;
+        if (kb + 8 < np && i >= piece_start(kb + 8)) {  // more, shorter pieces: walk them
+            uint32_t k = kb + 8;
+            while (k + 1 < np && P[k + 1].y <= i) ++k;
+            base = P[k].x;
+            st = P[k].y;
+        }
+        return *(const IK_GLOBAL uint64_t*)(T + base + (i - st));
     };
     uint64_t w = load4(0);
     while (t < ntok) {

@@ -230,7 +230,7 @@ struct SubOutHost {
 struct SubRes {
     uint32_t start;   // first symbol boundary >= the range start (or where an exact start began)
     uint32_t exit;    // first symbol boundary >= the range end, or just past a verified end of block
-    uint64_t out;     // output bytes from start to exit
+    uint32_t out;     // output bytes from start to exit
     uint32_t ntok;    // tokens written
     int eob;          // an end-of-block code ended the pass (exit = just past it)
     int bad;          // an invalid code inside the range (corrupt, or an unsynchronised start)
@@ -257,7 +257,7 @@ IK_HD void sub_decode(Win& win, uint32_t p0, uint32_t lo, uint32_t hi, const Lit
     r.eob = 0;
     r.bad = 0;
     out.reset();
-    uint64_t cnt = 0;
+    uint32_t cnt = 0;
     uint32_t steps = 0;
     for (;;) {
         ++steps;
