@@ -917,12 +917,14 @@ using infl::kTokTableLen;
 //      with the same values, its positions after the batch -- stale ring data --
 //      are rewritten by the next batch; groups are clipped to the lane's output).
 constexpr uint32_t kX4Tok = 256;
+constexpr int kXPieces = 160;  // piece-table entries staged in LDS (a lane of two windows has ~100)
 
 __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const PngLaneDev* lanes, int nlanes,
                                                     const uint16_t* tok, int* status, const uint2* pieces) {
     raise_priority();
     __shared__ __attribute__((aligned(16))) uint16_t s_ring[kXRing];  // recent output, by absolute position
     __shared__ uint32_t s_tab[64];                                      // the block's literal table
+    __shared__ uint32_t s_pb[kXPieces], s_ps[kXPieces];                 // wave decoder lanes: piece table
     constexpr uint32_t M = kXRing - 1;
     const int li = blockIdx.x;
     if (li >= nlanes) return;
@@ -939,52 +941,39 @@ __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const
     // a thread keeps its current piece (base, virtual start) and the next one's start
     const uint32_t np = pieces ? L.npieces : 0u;
     const IK_GLOBAL uint2* P = (const IK_GLOBAL uint2*)(pieces + (pieces ? L.pbase : 0));
-    // the first 128 entries in registers (lane x: entries x and 64 + x), read as
-    // wave-uniform values (readlane) when a window is loaded; past 128, memory
-    uint32_t pr_b0 = 0, pr_s0 = 0, pr_b1 = 0, pr_s1 = 0;
+    // the first kXPieces entries staged in LDS; past them, memory.  Each thread
+    // keeps the piece of its last token (its index only grows: a window is 256
+    // tokens, a piece tens to hundreds), so a load walks a step or two at most
     if (np) {
-        if ((uint32_t)x < np) { pr_b0 = P[x].x; pr_s0 = P[x].y; }
-        if ((uint32_t)x + 64u < np) { pr_b1 = P[x + 64].x; pr_s1 = P[x + 64].y; }
+        for (uint32_t k = (uint32_t)x; k < np && k < (uint32_t)kXPieces; k += 64) {
+            s_pb[k] = P[k].x;
+            s_ps[k] = P[k].y;
+        }
+        __syncthreads();
     }
-    auto piece_base = [&](uint32_t k) -> uint32_t {  // k wave-uniform
-        if (k < 64u) return (uint32_t)__builtin_amdgcn_readlane((int)pr_b0, (int)k);
-        if (k < 128u) return (uint32_t)__builtin_amdgcn_readlane((int)pr_b1, (int)(k - 64u));
-        return P[k].x;
-    };
-    auto piece_start = [&](uint32_t k) -> uint32_t {  // k wave-uniform
-        if (k < 64u) return (uint32_t)__builtin_amdgcn_readlane((int)pr_s0, (int)k);
-        if (k < 128u) return (uint32_t)__builtin_amdgcn_readlane((int)pr_s1, (int)(k - 64u));
-        return P[k].y;
-    };
-    uint32_t kb = 0;  // the piece holding the current window's first token (only grows)
+    auto piece_base = [&](uint32_t k) -> uint32_t { return k < (uint32_t)kXPieces ? s_pb[k] : P[k].x; };
+    auto piece_start = [&](uint32_t k) -> uint32_t { return k < (uint32_t)kXPieces ? s_ps[k] : P[k].y; };
+    uint32_t kc = 0, pc_base = 0, pc_start = 0, pn_start = 0xFFFFFFFFu;
+    if (np) {
+        pc_base = piece_base(0);
+        pn_start = np > 1 ? piece_start(1) : 0xFFFFFFFFu;
+    }
     uint32_t t = 0;
     int64_t cnt = 0;
     bool have_tab = false, bad = false;
     // this thread's 4 tokens of the batch window at a (a multiple of 4; the region
     // is 16-byte aligned and padded past ntok to a multiple of 8 tokens)
-    // (called by the whole wave with a wave-uniform a)
     auto load4 = [&](uint32_t a) -> uint64_t {
         const uint32_t i = a + 4u * (uint32_t)x;
-        if (!np) return i < ntok ? *(const IK_GLOBAL uint64_t*)(T + i) : 0xFFFEFFFEFFFEFFFEull;
-        while (kb + 1 < np && piece_start(kb + 1) <= a) ++kb;
-        // the window's 256 tokens lie in pieces kb .. kb + 7 (a piece of a sub-lane
-        // holds tens of tokens or more); each thread picks its own
-        uint32_t base = piece_base(kb), st = piece_start(kb);
-#pragma unroll
-        for (uint32_t m = 1; m < 8; ++m) {
-            if (kb + m < np) {
-                const uint32_t sm = piece_start(kb + m);
-                if (i >= sm) { base = piece_base(kb + m); st = sm; }
-            }
-        }
         if (i >= ntok) return 0xFFFEFFFEFFFEFFFEull;
-        if (kb + 8 < np && i >= piece_start(kb + 8)) {  // more, shorter pieces: walk them
-            uint32_t k = kb + 8;
-            while (k + 1 < np && P[k + 1].y <= i) ++k;
-            base = P[k].x;
-            st = P[k].y;
+        if (!np) return *(const IK_GLOBAL uint64_t*)(T + i);
+        while (i >= pn_start) {
+            ++kc;
+            pc_base = piece_base(kc);
+            pc_start = pn_start;
+            pn_start = kc + 1 < np ? piece_start(kc + 1) : 0xFFFFFFFFu;
         }
-        return *(const IK_GLOBAL uint64_t*)(T + base + (i - st));
+        return *(const IK_GLOBAL uint64_t*)(T + pc_base + (i - pc_start));
     };
     uint64_t w = load4(0);
     while (t < ntok) {
