@@ -479,7 +479,7 @@ struct LaneResult {
     uint32_t blocks;    // blocks decoded
     uint32_t pieces;    // wave decoder (ik_png_wave.h): token pieces written
     uint32_t kc_setup;  // wave decoder, profile: clock ticks / 1024 in block codes, tables and window staging
-    uint32_t pad2;
+    uint32_t units;     // wave decoder: expand units recorded (ik_png_wave.h kUnitMinTok)
 };
 
 // Decode whole blocks from `start` (a block boundary) until a block boundary >=

@@ -21,6 +21,7 @@ IK_HD int png_unfilter_groups(int h) {
     return g < 32 ? g : 32;
 }
 constexpr uint64_t kPngChunkBytes = 16384; // candidate-search chunk of the compressed stream
+constexpr uint64_t kPngWaveChunkBytes = 65536; // the same, for the wave decoder (ik_png_decode.cpp png_chunk_bytes)
 constexpr int kPngPageShift = 12;          // resolve: output page -> decoder table
 
 // one image of a batch, as the kernels see it
@@ -50,6 +51,9 @@ struct PngLaneDev {
     uint32_t big;            // wave decoder: the region is sized by the exact bound (an overflow before)
     uint64_t pbase;          // wave decoder: its piece table, from entry pbase of the batch's
     uint32_t npieces;        // wave decoder: the table's entries; expand: pieces to read (0: one contiguous run)
+    uint32_t ubase;          // expand (wave decoder): the lane's first unit in the batch
+    uint32_t uimg;           // expand: its image's first unit in the batch
+    uint32_t nunits;         // expand: the lane's units (LaneResult::units)
     uint32_t pad;
 };
 
@@ -116,13 +120,24 @@ hipError_t launch_png_find(const PngImgDev* imgs, const int* chunk_img, const in
 // order (nullable): launch slot -> lane index; lane t's result goes to res[t]
 hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, const uint32_t* order, int n,
                              uint16_t* tok, infl::LaneResult* res, hipStream_t s);
+// expand: one wave per lane (units == nullptr; n lanes), or -- the wave decoder's
+// lanes -- one wave per expand unit (n units; unit u of lane ulane[u], its record at
+// units[lanes[l].pbase + u - lanes[l].ubase]); status: 2 ints per lane / unit
 hipError_t launch_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int n, const uint16_t* tok, int* status,
-                             hipStream_t s, const uint2* pieces = nullptr);
+                             hipStream_t s, const uint2* pieces = nullptr, const uint2* units = nullptr,
+                             const uint32_t* ulane = nullptr);
 // the wave decoder (ik_png_wave.h): one wave per lane; pieces: (token base in the
 // lane's region, first index in its virtual token stream) per piece, a table of
-// lanes[t].npieces entries at lanes[t].pbase
+// lanes[t].npieces entries at lanes[t].pbase; units: the lane's expand-unit
+// records (first piece, output bytes before it) at the same slots
 hipError_t launch_png_wave(const PngImgDev* imgs, const PngLaneDev* lanes, const uint32_t* order, int n,
-                           uint16_t* tok, uint2* pieces, infl::LaneResult* res, hipStream_t s);
+                           uint16_t* tok, uint2* pieces, uint2* units, infl::LaneResult* res, hipStream_t s);
+// the expand units' tables from the verified lanes (n lanes, each with obase,
+// out_len, pbase, ubase, uimg, nunits set): every unit's output offset into its
+// image's obase table (imgs[].obase, as resolve reads it), its lane into ulane, and
+// the image's page table (imgs[].page_lane: page -> the unit holding its first byte)
+hipError_t launch_png_units(const PngImgDev* imgs, const PngLaneDev* lanes, int n, const uint2* units,
+                            uint32_t* ulane, hipStream_t s);
 hipError_t launch_png_resolve(const PngImgDev* imgs, const int2* rows, int nrows, int* err, hipStream_t s);
 // groups[t] = (image, band group) of the workgroup holding ticket t; prog: one
 // zeroed counter per band (the image's at prog_base[image]); ticket: zeroed

@@ -678,7 +678,8 @@ __device__ bool wave_block_codes(const IK_GLOBAL uint32_t* W, uint64_t nbits, ui
 }
 
 __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const PngLaneDev* lanes, const uint32_t* order,
-                                                 int nlanes, uint16_t* tok, uint2* pieces, infl::LaneResult* res) {
+                                                 int nlanes, uint16_t* tok, uint2* pieces, uint2* units,
+                                                 infl::LaneResult* res) {
     __shared__ __attribute__((aligned(16))) uint32_t s_win[kWaveWinWords];
     __shared__ uint32_t s_lit[1u << wave::kLB];
     __shared__ uint32_t s_dist[1u << wave::kDB];
@@ -701,13 +702,15 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
     const WaveGlobalWin gwin{W};
     IK_GLOBAL uint16_t* const region = (IK_GLOBAL uint16_t*)(tok + L.tbase);
     IK_GLOBAL uint2* const ptab = (IK_GLOBAL uint2*)(pieces + L.pbase);
+    IK_GLOBAL uint2* const utab = (IK_GLOBAL uint2*)(units + L.pbase);  // expand-unit records (wave::unit_starts)
     const uint64_t cap = L.ntok;
     const uint32_t pcap = L.npieces;  // piece-table entries of this lane (wave::pieces_capacity)
     const bool big = L.big != 0;
     const uint64_t c0 = clock64();
     uint64_t p = start, used = 0, total = 0;
-    uint32_t npieces = 0, nblocks = 0, steps = 0;
+    uint32_t npieces = 0, nblocks = 0, steps = 0, nunits = 0;
     uint64_t written = 0;  // tokens in the pieces (padding included)
+    uint64_t unit_v0 = 0;  // the current expand unit's first token
     uint64_t prev_bits = 0;  // the last block's body length (wave::window_end)
     uint64_t ck_setup = 0;   // profile: clock in codes, tables, staging
     int status = infl::kLaneCorrupt, final_block = 0;
@@ -722,7 +725,14 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
         }
         if (p + 3 > nbits) break;
         const uint64_t blk_start = p, blk_total = total, blk_used = used, blk_written = written;
-        const uint32_t blk_pieces = npieces;
+        const uint32_t blk_pieces = npieces, blk_units = nunits;
+        const uint64_t blk_v0 = unit_v0;
+        if (wave::unit_starts(nunits, written, unit_v0)) {  // (undone with the block on a split)
+            // (nunits <= npieces <= pcap; at pcap the block splits and the record is dropped)
+            if (lane == 0 && nunits < pcap) utab[nunits] = make_uint2(npieces, (uint32_t)total);
+            ++nunits;
+            unit_v0 = written;
+        }
         const uint64_t h = gwin(p);
         const int bfinal = (int)(h & 1u), btype = (int)((h >> 1) & 3u);
         ++nblocks;
@@ -742,6 +752,7 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
             const uint32_t n8 = (len + 7u) & ~7u;
             if (used + n8 > cap) { status = infl::kLaneOverflow; break; }
             if (npieces >= pcap) {
+                nunits = blk_units;  // (the split lane ends before this block)
                 status = p > start ? (int)infl::kLaneSplit : (int)infl::kLaneOverflow;
                 break;
             }
@@ -766,7 +777,7 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
             ck_setup += clock64() - ck0;
             // ---- the body, window by window ----
             uint64_t bp = body;
-            bool first_window = true;
+            const uint64_t est_end = wave::block_end_estimate(body, prev_bits);
             int done = 0;  // 1 block ended, 2 lane ends (status set), 3 corrupt / overflow, 4 split
             while (!done) {
                 if (bp >= stop_eff) {
@@ -774,8 +785,7 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
                     done = 2;
                     break;
                 }
-                const uint64_t re = wave::window_end(bp, stop_eff, first_window ? prev_bits : 0);
-                first_window = false;
+                const uint64_t re = wave::window_end(bp, stop_eff, est_end);
                 const wave::Split sp = wave::split_range(bp, re, big);
                 if (used + (uint64_t)sp.nsub * sp.cap > cap) { status = infl::kLaneOverflow; done = 3; break; }
                 // stage the window: words from bp's 16-byte group to past the last sub-lane's overshoot
@@ -855,6 +865,8 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
                 bp = exv;
             }
             if (done == 4) {
+                nunits = blk_units;
+                unit_v0 = blk_v0;
                 npieces = blk_pieces;
                 total = blk_total;
                 used = blk_used;
@@ -883,6 +895,7 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
         r.blocks = nblocks;
         r.pieces = npieces;
         r.kc_setup = (uint32_t)(ck_setup >> 10);
+        r.units = nunits;
         res[t] = r;
     }
 }
@@ -917,48 +930,65 @@ using infl::kTokTableLen;
 //      with the same values, its positions after the batch -- stale ring data --
 //      are rewritten by the next batch; groups are clipped to the lane's output).
 constexpr uint32_t kX4Tok = 256;
-constexpr int kXPieces = 160;  // piece-table entries staged in LDS (a lane of two windows has ~100)
+constexpr int kXPieces = 192;  // piece-table entries staged in LDS (a unit of one 18 KiB block has ~130)
 
 __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const PngLaneDev* lanes, int nlanes,
-                                                    const uint16_t* tok, int* status, const uint2* pieces) {
+                                                    const uint16_t* tok, int* status, const uint2* pieces,
+                                                    const uint2* units, const uint32_t* ulane) {
     raise_priority();
     __shared__ __attribute__((aligned(16))) uint16_t s_ring[kXRing];  // recent output, by absolute position
     __shared__ uint32_t s_tab[64];                                      // the block's literal table
     __shared__ uint32_t s_pb[kXPieces], s_ps[kXPieces];                 // wave decoder lanes: piece table
     constexpr uint32_t M = kXRing - 1;
-    const int li = blockIdx.x;
+    const int li = blockIdx.x;  // lane, or expand unit
     if (li >= nlanes) return;
     const int x = threadIdx.x;
     const uint64_t c0 = clock64();
-    const PngLaneDev L = lanes[li];
+    const PngLaneDev L = lanes[units ? (int)ulane[li] : li];
     const PngImgDev I = imgs[L.img];
     const IK_GLOBAL uint16_t* T = (const IK_GLOBAL uint16_t*)(tok + L.tbase);
     IK_GLOBAL uint16_t* const U = (IK_GLOBAL uint16_t*)I.u16;
-    const int64_t ob = L.obase, oe = L.obase + (int64_t)L.out_len;
+    int64_t ob = L.obase, oe = L.obase + (int64_t)L.out_len;
     uint32_t ntok = L.ntok;
     // the wave decoder's lanes: their tokens are pieces of the region (ik_png_wave.h),
     // read in order as one virtual stream of ntok tokens (each piece a multiple of 8);
     // a thread keeps its current piece (base, virtual start) and the next one's start
     const uint32_t np = pieces ? L.npieces : 0u;
     const IK_GLOBAL uint2* P = (const IK_GLOBAL uint2*)(pieces + (pieces ? L.pbase : 0));
-    // the first kXPieces entries staged in LDS; past them, memory.  Each thread
+    // an expand unit (ik_png_wave.h unit_starts): pieces [pf, pe) of its lane, virtual
+    // tokens [t0, ntok), output [ob, oe) -- markers for copies before ob, as for a lane
+    uint32_t pf = 0, t0 = 0;
+    if (units) {
+        const IK_GLOBAL uint2* R = (const IK_GLOBAL uint2*)(units + L.pbase);
+        const uint32_t b = (uint32_t)li - L.ubase;
+        const uint2 r0 = make_uint2(R[b].x, R[b].y);
+        const bool last = b + 1 >= L.nunits;
+        uint2 r1 = make_uint2(np, (uint32_t)L.out_len);
+        if (!last) r1 = make_uint2(R[b + 1].x, R[b + 1].y);
+        pf = r0.x;
+        t0 = P[pf].y;
+        ntok = r1.x < np ? P[r1.x].y : L.ntok;
+        ob = L.obase + (int64_t)r0.y;
+        oe = L.obase + (int64_t)r1.y;
+    }
+    // the unit's first kXPieces entries staged in LDS; past them, memory.  Each thread
     // keeps the piece of its last token (its index only grows: a window is 256
     // tokens, a piece tens to hundreds), so a load walks a step or two at most
     if (np) {
-        for (uint32_t k = (uint32_t)x; k < np && k < (uint32_t)kXPieces; k += 64) {
-            s_pb[k] = P[k].x;
-            s_ps[k] = P[k].y;
+        for (uint32_t k = (uint32_t)x; pf + k < np && k < (uint32_t)kXPieces; k += 64) {
+            s_pb[k] = P[pf + k].x;
+            s_ps[k] = P[pf + k].y;
         }
         __syncthreads();
     }
-    auto piece_base = [&](uint32_t k) -> uint32_t { return k < (uint32_t)kXPieces ? s_pb[k] : P[k].x; };
-    auto piece_start = [&](uint32_t k) -> uint32_t { return k < (uint32_t)kXPieces ? s_ps[k] : P[k].y; };
-    uint32_t kc = 0, pc_base = 0, pc_start = 0, pn_start = 0xFFFFFFFFu;
+    auto piece_base = [&](uint32_t k) -> uint32_t { return k - pf < (uint32_t)kXPieces ? s_pb[k - pf] : P[k].x; };
+    auto piece_start = [&](uint32_t k) -> uint32_t { return k - pf < (uint32_t)kXPieces ? s_ps[k - pf] : P[k].y; };
+    uint32_t kc = pf, pc_base = 0, pc_start = t0, pn_start = 0xFFFFFFFFu;
     if (np) {
-        pc_base = piece_base(0);
-        pn_start = np > 1 ? piece_start(1) : 0xFFFFFFFFu;
+        pc_base = piece_base(pf);
+        pn_start = pf + 1 < np ? piece_start(pf + 1) : 0xFFFFFFFFu;
     }
-    uint32_t t = 0;
+    uint32_t t = t0;
     int64_t cnt = 0;
     bool have_tab = false, bad = false;
     // this thread's 4 tokens of the batch window at a (a multiple of 4; the region
@@ -975,7 +1005,7 @@ __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const
         }
         return *(const IK_GLOBAL uint64_t*)(T + pc_base + (i - pc_start));
     };
-    uint64_t w = load4(0);
+    uint64_t w = load4(t0);
     while (t < ntok) {
         const uint32_t a = t & ~3u, i0 = a + 4u * (uint32_t)x;
         uint32_t u[4];
@@ -1145,8 +1175,33 @@ __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const
         if (__ballot(bad)) { bad = true; break; }
     }
     if (x == 0) {
-        status[2 * li] = (!bad && cnt == (int64_t)L.out_len) ? 0 : -1;
+        status[2 * li] = (!bad && cnt == oe - ob) ? 0 : -1;
         status[2 * li + 1] = (int)((clock64() - c0) >> 10);  // profile: clock ticks / 1024
+    }
+}
+
+// ---- expand units ---------------------------------------------------------------
+// One thread per verified lane of the wave decoder: its units' output offsets into
+// the image's unit offset table (ascending, resolve's lane_obase), unit -> lane,
+// and the page table entries of the pages whose first byte lies in each unit.
+__global__ __launch_bounds__(256) void k_png_units(const PngImgDev* imgs, const PngLaneDev* lanes, int n,
+                                                   const uint2* units, uint32_t* ulane) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const PngLaneDev L = lanes[i];
+    const PngImgDev I = imgs[L.img];
+    IK_GLOBAL int64_t* const uob = (IK_GLOBAL int64_t*)I.obase;
+    IK_GLOBAL int* const pages = (IK_GLOBAL int*)I.page_lane;
+    const IK_GLOBAL uint2* R = (const IK_GLOBAL uint2*)(units + L.pbase);
+    const uint32_t base = L.ubase - L.uimg;  // the lane's first unit within its image
+    constexpr int64_t P = 1ll << kPngPageShift;
+    int64_t o = L.obase + (int64_t)R[0].y;
+    for (uint32_t b = 0; b < L.nunits; ++b) {
+        const int64_t oe = b + 1 < L.nunits ? L.obase + (int64_t)R[b + 1].y : L.obase + (int64_t)L.out_len;
+        uob[base + b] = o;
+        ulane[L.ubase + b] = (uint32_t)i;
+        for (int64_t pg = (o + P - 1) >> kPngPageShift; (pg << kPngPageShift) < oe; ++pg) pages[pg] = (int)(base + b);
+        o = oe;
     }
 }
 
@@ -1782,16 +1837,24 @@ hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, con
 }
 
 hipError_t launch_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int n, const uint16_t* tok, int* status,
-                             hipStream_t s, const uint2* pieces) {
+                             hipStream_t s, const uint2* pieces, const uint2* units, const uint32_t* ulane) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_png_expand4, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status, pieces);
+    if ((units != nullptr) != (ulane != nullptr) || (units && !pieces)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_png_expand4, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status, pieces, units, ulane);
     return hipGetLastError();
 }
 
 hipError_t launch_png_wave(const PngImgDev* imgs, const PngLaneDev* lanes, const uint32_t* order, int n,
-                           uint16_t* tok, uint2* pieces, infl::LaneResult* res, hipStream_t s) {
+                           uint16_t* tok, uint2* pieces, uint2* units, infl::LaneResult* res, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_png_wave, dim3(n), dim3(64), 0, s, imgs, lanes, order, n, tok, pieces, res);
+    hipLaunchKernelGGL(k_png_wave, dim3(n), dim3(64), 0, s, imgs, lanes, order, n, tok, pieces, units, res);
+    return hipGetLastError();
+}
+
+hipError_t launch_png_units(const PngImgDev* imgs, const PngLaneDev* lanes, int n, const uint2* units,
+                            uint32_t* ulane, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_png_units, dim3((n + 255) / 256), dim3(256), 0, s, imgs, lanes, n, units, ulane);
     return hipGetLastError();
 }
 

@@ -522,6 +522,34 @@ struct PngBatchState {
     ~PngBatchState() { release_area(area); }
 };
 
+// The decode pass: the wave decoder (ik_png_wave.h, k_png_wave: a wave per lane,
+// 64 self-synchronising sub-lanes over shared lookup tables) by default;
+// IK_PNG_DECODE=lane selects round 4's one-thread-per-lane canonical decoder
+// (k_png_decode, token streams with literal tables) for A/B runs.
+static bool png_wave_decoder() {
+    static const bool v = [] {
+        const char* e = getenv("IK_PNG_DECODE");
+        return !(e && !strcmp(e, "lane"));
+    }();
+    return v;
+}
+
+// The search chunk: one decoder lane starts at (about) each chunk's first block.
+// The wave decoder's lanes run 64 sub-lanes over each block, so a lane can span
+// several blocks: 64 KiB chunks (~7 blocks of image data) take a quarter of the
+// block searches of 16 KiB and a quarter of the lane starts (window markers, chain
+// links) at the same decode parallelism; the one-thread lane decoder keeps 16 KiB.
+// IK_PNG_CHUNK_KB overrides (A/B runs).
+static uint64_t png_chunk_bytes() {
+    static const uint64_t v = [] {
+        const char* e = getenv("IK_PNG_CHUNK_KB");
+        const long kb = e ? atol(e) : 0;
+        if (kb >= 4 && kb <= 4096) return (uint64_t)kb << 10;
+        return png_wave_decoder() ? (uint64_t)kPngWaveChunkBytes : kPngChunkBytes;
+    }();
+    return v;
+}
+
 int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, PngUpload& up) {
     static const bool timing = getenv("IK_TIMING") != nullptr;
     auto st = std::make_shared<PngBatchState>();
@@ -614,8 +642,8 @@ int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Png
         const uint32_t tail = (uint32_t)((((j.zlen + 3) & ~size_t(3)) + kPad) - j.zlen);
         png_gather_plan(j.raw_off, j.idat, raw + j.z_off, tail, (uint32_t)k, pieces, chunks);
     }
-    // the block search's chunks: 16 KiB of stream each (chunk 0 starts at the first block)
-    const uint64_t cbits = kPngChunkBytes * 8;
+    // the block search's chunks (chunk 0 starts at the first block): png_chunk_bytes() of stream each
+    const uint64_t cbits = png_chunk_bytes() * 8;
     int nchunks = 0;
     for (PngJob* j : S.J) {
         j->nbits = (uint64_t)j->zlen * 8;
@@ -709,7 +737,7 @@ int png_upload_begin(const uint8_t* const* bytes, const size_t* lens, int n, Png
 static void png_find_launch(PngBatchState& S, hipStream_t s) {
     if (S.find_launched || S.rc || !S.area || S.J.empty()) return;
     UploadArea* A = S.area;
-    const uint64_t cbits = kPngChunkBytes * 8;
+    const uint64_t cbits = png_chunk_bytes() * 8;
     hipError_t e = A->ev[2] ? hipStreamWaitEvent(s, A->ev[2], 0) : hipSuccess;
     if (e == hipSuccess && A->ev[4]) e = hipEventRecord(A->ev[4], s);
     const int* ft = reinterpret_cast<const int*>(A->dev + S.o_ftab);
@@ -771,18 +799,6 @@ static bool order_lanes(const std::vector<PngLaneDev>& hl, const std::vector<Png
         order[r < nlong ? r : n - 1 - (r - nlong)] = (uint32_t)t;
     }
     return true;
-}
-
-// The decode pass: the wave decoder (ik_png_wave.h, k_png_wave: a wave per lane,
-// 64 self-synchronising sub-lanes over shared lookup tables) by default;
-// IK_PNG_DECODE=lane selects round 4's one-thread-per-lane canonical decoder
-// (k_png_decode, token streams with literal tables) for A/B runs.
-static bool png_wave_decoder() {
-    static const bool v = [] {
-        const char* e = getenv("IK_PNG_DECODE");
-        return !(e && !strcmp(e, "lane"));
-    }();
-    return v;
 }
 
 // token region of a lane of `bits` compressed bits (its capacity in tokens)
@@ -851,7 +867,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             for (PngJob* j : J) pieces_total += wave::pieces_capacity(j->nbits) + 64ull * (uint64_t)j->nchunks;
             pieces_total += pieces_total / 2 + 4096;
         }
-        const size_t pieces_bytes = up256(sizeof(uint2) * pieces_total);
+        const size_t pieces_bytes = up256(sizeof(uint2) * pieces_total);  // (twice: pieces, unit records)
         size_t dyn = up256(sizeof(PngLaneDev) * max_lanes) + up256(sizeof(infl::LaneResult) * max_lanes) +
                      up256(sizeof(int64_t) * max_lanes) + up256(2 * sizeof(int) * max_lanes) +
                      up256(sizeof(uint32_t) * max_lanes) + up256(sizeof(PngImgDev) * m);
@@ -866,7 +882,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         // progress counter per band and one ticket per class (zeroed)
         const size_t unf_tab = up256(sizeof(int2) * ngroups) + up256(sizeof(int) * m);
         const size_t unf_zero = up256(sizeof(unsigned) * (nbands + 8));
-        dyn += up256(sizeof(int2) * nrows) + up256(sizeof(int) * npages) + unf_tab + unf_zero + pieces_bytes +
+        dyn += up256(sizeof(int2) * nrows) + up256(sizeof(int) * npages) + unf_tab + unf_zero + 2 * pieces_bytes +
                up256(2 * tok_total);
         uint8_t* dev = scratch_slot(2, o_dyn + dyn);
         if (!dev) rc = fail(IK_ERR_DEVICE, "cannot allocate the PNG batch work area (%zu bytes)", o_dyn + dyn);
@@ -880,6 +896,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         int* d_pages = nullptr;
         uint8_t* d_unf = nullptr;
         uint2* d_pieces = nullptr;
+        uint2* d_units = nullptr;  // the wave decoder's expand-unit records (slots parallel to d_pieces)
         uint16_t* d_tok = nullptr;
         if (!rc) {
             size_t o = o_dyn;
@@ -902,6 +919,8 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             d_unf = dev + o;
             o += unf_tab + unf_zero;
             d_pieces = pieces_bytes ? reinterpret_cast<uint2*>(dev + o) : nullptr;
+            o += pieces_bytes;
+            d_units = pieces_bytes ? reinterpret_cast<uint2*>(dev + o) : nullptr;
             o += pieces_bytes;
             d_tok = reinterpret_cast<uint16_t*>(dev + o);
         }
@@ -1121,7 +1140,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             if (!mk[0]) mk[0] = now_ms();  // plan built, lanes uploaded (first round)
             rec(2, s);
             hipError_t e2 = wavedec ? launch_png_wave(d_imgs, d_lanes, ordered ? d_order : nullptr, (int)hl.size(), d_tok,
-                                                      d_pieces, d_res, s)
+                                                      d_pieces, d_units, d_res, s)
                                     : launch_png_decode(d_imgs, d_lanes, ordered ? d_order : nullptr, (int)hl.size(), d_tok,
                                                         d_res, s);
             rec(3, s);
@@ -1186,6 +1205,10 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         hl.clear();
         size_t npg = 0;                        // page-table entries so far
         std::vector<std::pair<int, size_t>> pj;  // (job, its first entry in hob) of every verified job
+        // the wave decoder's expand units (ik_png_wave.h unit_starts): numbered lane by
+        // lane; an image's units are contiguous from uimg[k]
+        uint32_t nunits = 0;
+        std::vector<uint32_t> uimg(m, 0);
         for (int k = 0; k < m && !rc; ++k) {
             PngJob& j = *J[k];
             if (j.state != 1) continue;
@@ -1193,6 +1216,11 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             uint64_t tot = 0;
             pngplan::offsets(j.lanes, ob, &tot);
             if (tot != j.raw_total) { reject(j, "image data length"); continue; }  // png's error
+            if (wavedec) {
+                bool units_ok = true;
+                for (size_t i = 0; i < ob.size(); ++i) units_ok = units_ok && j.lanes.res[i].units > 0;
+                if (!units_ok) { reject(j, "expand units"); continue; }
+            }
             if (j.expand) {  // unfiltered rows in a row image, then k_png_px into the output image
                 if (alloc_image((uint32_t)j.rowbytes, j.h, 1, &j.rows) ||
                 alloc_image(j.w, j.h, (uint32_t)j.out_c, &j.img, j.depth == 16 ? 2 : 1)) {
@@ -1203,9 +1231,10 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                 reject(j, "image allocation");
                 continue;
             }
-            hd[k].obase = d_obase + hob.size();
+            hd[k].obase = d_obase + hob.size();  // (the wave decoder's: its unit table, set below)
             hd[k].page_lane = d_pages + npg;  // (the page table itself is built while expand runs)
             hd[k].nlanes = (int)ob.size();
+            uimg[k] = nunits;
             pj.emplace_back(k, hob.size());
             npg += (j.raw_total >> kPngPageShift) + 1;
             hd[k].dst = j.expand ? j.rows->d : j.img->d;
@@ -1219,14 +1248,36 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                 L.ntok = j.lanes.res[i].ntok;
                 L.img = (uint32_t)k;
                 L.first = i == 0;
-                if (wavedec) {  // the tokens are the lane's pieces (piece table at its slot)
+                if (wavedec) {  // the tokens are the lane's pieces (piece table at its slot), expanded by units
                     L.pbase = (uint64_t)j.lanes.pslot[i];
                     L.npieces = j.lanes.res[i].pieces;
+                    L.ubase = nunits;
+                    L.uimg = uimg[k];
+                    L.nunits = j.lanes.res[i].units;
+                    nunits += L.nunits;
                 }
                 hl.push_back(L);
             }
+            if (wavedec) hd[k].nlanes = (int)(nunits - uimg[k]);
             hob.insert(hob.end(), ob.begin(), ob.end());
         }
+        // the units' tables: offsets (resolve's lane_obase), unit -> lane, expand status
+        int64_t* d_uob = nullptr;
+        uint32_t* d_ulane = nullptr;
+        int* d_uxst = nullptr;
+        if (!rc && wavedec && nunits) {
+            const size_t b0 = up256(sizeof(int64_t) * nunits), b1 = up256(sizeof(uint32_t) * nunits);
+            uint8_t* ua = scratch_slot(5, b0 + b1 + up256(2 * sizeof(int) * nunits));
+            if (!ua) {
+                rc = fail(IK_ERR_DEVICE, "cannot allocate the PNG expand-unit tables (%u units)", nunits);
+            } else {
+                d_uob = reinterpret_cast<int64_t*>(ua);
+                d_ulane = reinterpret_cast<uint32_t*>(ua + b0);
+                d_uxst = reinterpret_cast<int*>(ua + b0 + b1);
+                for (const auto& q : pj) hd[q.first].obase = d_uob + uimg[q.first];
+            }
+        }
+        const size_t nexp = wavedec ? (size_t)nunits : hl.size();  // expand waves: units, or lanes
         mk[1] = now_ms();  // offsets, images, page tables, lane table built
         std::vector<int2>& hrows = ht.rows;
         std::vector<int>& hxst = ht.xst;
@@ -1242,7 +1293,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             if (ue == hipSuccess) ue = X.h2d(dev + o_imgs, hd.data(), sizeof(PngImgDev) * m);
             if (ue == hipSuccess) ue = hipMemsetAsync(dev + o_err, 0, sizeof(int) * m, s);
             if (ue != hipSuccess) rc = hip_fail(ue, "PNG expand tables");
-            hxst.resize(2 * hl.size());
+            hxst.resize(2 * nexp);
             mk[2] = now_ms();  // lane tables uploaded
             // the next batch's block search (VALU-bound) beside this batch's expand,
             // resolve and unfilter, which run at a raised wave priority (ik_png.hip
@@ -1254,21 +1305,30 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             if (!rc) {
                 hipError_t e3 = hipSuccess;
                 rec(4, s);
-                if (e3 == hipSuccess)
-                    e3 = launch_png_expand(d_imgs, d_lanes, (int)hl.size(), d_tok, d_xst, s, wavedec ? d_pieces : nullptr);
+                if (wavedec) {
+                    // the units' tables and page tables (k_png_units), then one wave per unit
+                    if (e3 == hipSuccess) e3 = launch_png_units(d_imgs, d_lanes, (int)hl.size(), d_units, d_ulane, s);
+                    if (e3 == hipSuccess)
+                        e3 = launch_png_expand(d_imgs, d_lanes, (int)nunits, d_tok, d_uxst, s, d_pieces, d_units, d_ulane);
+                } else if (e3 == hipSuccess) {
+                    e3 = launch_png_expand(d_imgs, d_lanes, (int)hl.size(), d_tok, d_xst, s);
+                }
                 rec(5, s);
-                // page -> decoder that holds the page's first byte (resolve's lane lookup)
+                // page -> decoder that holds the page's first byte (resolve's lane lookup;
+                // the wave decoder's units: k_png_units built it)
                 for (const auto& q : pj) {
                     const PngJob& j = *J[q.first];
-                    const int64_t* ob = hob.data() + q.second;
-                    const size_t nl = (size_t)hd[q.first].nlanes;
-                    for (uint64_t pg = 0, ln = 0; pg <= (j.raw_total >> kPngPageShift); ++pg) {
-                        while (ln + 1 < nl && (uint64_t)ob[ln + 1] <= (pg << kPngPageShift)) ++ln;
-                        hpages.push_back((int)ln);
+                    if (!wavedec) {
+                        const int64_t* ob = hob.data() + q.second;
+                        const size_t nl = (size_t)hd[q.first].nlanes;
+                        for (uint64_t pg = 0, ln = 0; pg <= (j.raw_total >> kPngPageShift); ++pg) {
+                            while (ln + 1 < nl && (uint64_t)ob[ln + 1] <= (pg << kPngPageShift)) ++ln;
+                            hpages.push_back((int)ln);
+                        }
                     }
                     for (uint32_t y = 0; y < j.h; ++y) hrows.push_back(make_int2(q.first, (int)y));
                 }
-                if (e3 == hipSuccess) e3 = X.h2d(d_pages, hpages.data(), sizeof(int) * hpages.size());
+                if (e3 == hipSuccess && !wavedec) e3 = X.h2d(d_pages, hpages.data(), sizeof(int) * hpages.size());
                 if (e3 == hipSuccess) e3 = X.h2d(d_rows, hrows.data(), sizeof(int2) * hrows.size());
                 if (e3 == hipSuccess) e3 = launch_png_resolve(d_imgs, d_rows, (int)hrows.size(),
                                                               reinterpret_cast<int*>(dev + o_err), s);
@@ -1339,7 +1399,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                                 (double)pf[2] / pf[7], (double)pf[3] / pf[7], (double)pf[4] / pf[7], ev_ms(6, 7));
                 }
 #endif
-                if (e3 == hipSuccess) e3 = X.d2h(hxst.data(), d_xst, 2 * sizeof(int) * hl.size());
+                if (e3 == hipSuccess) e3 = X.d2h(hxst.data(), wavedec ? d_uxst : d_xst, 2 * sizeof(int) * nexp);
                 if (e3 == hipSuccess) e3 = X.d2h(herr.data(), dev + o_err, sizeof(int) * m);
                 mk[3] = now_ms();  // expand .. unfilter done
                 if (e3 != hipSuccess) rc = hip_fail(e3, "PNG inflate (expand) / unfilter");
@@ -1356,15 +1416,18 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                     if (j.state != 1) continue;
                     const bool rows_ok = herr[k] == 0;
                     bool lanes_ok = true;
-                    for (size_t i = 0; i < j.lanes.start.size(); ++i, ++t) {
-                        lanes_ok = lanes_ok && hxst[2 * t] == 0;
-                        if (timing && hxst[2 * t] != 0) {
-                            const infl::LaneResult& q = j.lanes.res[i];
-                            fprintf(stderr, "[png] stream %d lane %zu/%zu: expand failed (start %llu stop %llu end %llu out %llu "
-                                    "tokens %u pieces %u blocks %u status %d)\n", j.idx, i, j.lanes.start.size(),
-                                    (unsigned long long)j.lanes.start[i], (unsigned long long)j.lanes.stop[i],
-                                    (unsigned long long)q.end_bit, (unsigned long long)q.out_len, q.ntok, q.pieces, q.blocks,
-                                    q.status);
+                    for (size_t i = 0; i < j.lanes.start.size(); ++i) {
+                        const uint32_t nu = wavedec ? j.lanes.res[i].units : 1u;  // expand waves of this lane
+                        for (uint32_t u = 0; u < nu; ++u, ++t) {
+                            lanes_ok = lanes_ok && hxst[2 * t] == 0;
+                            if (timing && hxst[2 * t] != 0) {
+                                const infl::LaneResult& q = j.lanes.res[i];
+                                fprintf(stderr, "[png] stream %d lane %zu/%zu unit %u/%u: expand failed (start %llu stop %llu "
+                                        "end %llu out %llu tokens %u pieces %u blocks %u status %d)\n", j.idx, i,
+                                        j.lanes.start.size(), u, nu, (unsigned long long)j.lanes.start[i],
+                                        (unsigned long long)j.lanes.stop[i], (unsigned long long)q.end_bit,
+                                        (unsigned long long)q.out_len, q.ntok, q.pieces, q.blocks, q.status);
+                            }
                         }
                     }
                     if (!rows_ok || !lanes_ok) reject(j, !lanes_ok ? "expand status" : "row filter bytes");

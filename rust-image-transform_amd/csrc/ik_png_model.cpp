@@ -206,13 +206,18 @@ int ikm_inflate_chunked(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8
 // The same stream through the wave decoder's algorithm (ik_png_wave.h: one lane
 // = whole blocks decoded by up to 64 self-synchronising sub-lanes with shared
 // lookup tables, its tokens in pieces), then the unchanged expand / resolve.
-// warm_bits: overrides kWarmBits when > 0 (the model's sweep).  stats (16 x u64):
-// chunks, candidates, lanes, rounds, overflows, windows, sub-lane passes, redo
-// passes, fix rounds, most fix rounds of one window, blocks, decoded symbol bits,
-// chain-check status, token-region tokens used, markers
+// stats (20 x u64): chunks, candidates, lanes, rounds, overflows, windows, sub-lane
+// passes, redo passes, fix rounds, most fix rounds of one window, blocks, decoded
+// symbol bits, chain-check status, token-region tokens used, markers, sub-lane steps,
+// wave steps (the passes' longest sub-lanes), expand units.  IKM_WARM / IKM_EST:
+// warm-up and block-end estimate overrides (the model's sweeps).
 int ikm_inflate_wave(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8_t* out, size_t out_cap,
                      uint64_t* out_len, uint64_t* stats) {
-    for (int i = 0; i < 16; ++i) stats[i] = 0;
+    for (int i = 0; i < 20; ++i) stats[i] = 0;
+    if (const char* e = getenv("IKM_EST")) {  // model experiments: mul/1024, add, min tail (bits)
+        long a = 1024, b = 4096, c = 16384;
+        if (sscanf(e, "%ld,%ld,%ld", &a, &b, &c) == 3) { wave::g_est_mul = a; wave::g_est_add = b; wave::g_min_tail = c; }
+    }
     if (zlen < 2) return -1;
     if ((z[0] & 15) != 8 || ((z[0] << 8) | z[1]) % 31 || (z[1] & 0x20)) return -1;
     const uint64_t nbits = (uint64_t)zlen * 8;
@@ -239,6 +244,7 @@ int ikm_inflate_wave(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8_t*
     // tokens and pieces by lane start (the chain check drops and splits lanes)
     std::map<uint64_t, std::vector<uint16_t>> tok;
     std::map<uint64_t, std::vector<std::pair<uint32_t, uint32_t>>> pieces;  // (base, vstart)
+    std::map<uint64_t, std::vector<std::pair<uint32_t, uint32_t>>> units;   // (first piece, output before it)
     wave::Stats ws;
     int st, overflows = 0;
     for (;;) {
@@ -250,7 +256,7 @@ int ikm_inflate_wave(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8_t*
             t.assign(cap, 0);
             static const uint64_t warm = getenv("IKM_WARM") ? strtoull(getenv("IKM_WARM"), nullptr, 10) : wave::kWarmBits;
             wave::lane_host(win, nbits, L.start[i], L.stop[i], L.big[i] != 0, t.data(), cap, L.res[i],
-                            pieces[L.start[i]], &ws, warm);
+                            pieces[L.start[i]], units[L.start[i]], &ws, warm);
             if (L.res[i].status == infl::kLaneOverflow) {
                 ++overflows;
                 if (L.big[i]) {
@@ -287,44 +293,46 @@ int ikm_inflate_wave(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8_t*
     stats[11] = ws.symbols_bits;
     stats[12] = (uint64_t)(int64_t)st;
     stats[15] = ws.steps;
+    stats[16] = ws.wave_steps;
     if (st) return -2;
     std::vector<int64_t> obase;
     uint64_t total;
     pngplan::offsets(L, obase, &total);
     if (total > out_cap) return -3;
     std::vector<uint16_t> u16(total + 16);
+    // the expand units (ik_png_wave.h kUnitMinTok): each unit's pieces in order, as
+    // the GPU expand pass reads them, expanded at the unit's output offset (window
+    // markers for copies before the unit); the resolve tables are per unit
+    std::vector<int64_t> uob;
     for (size_t i = 0; i < L.start.size(); ++i) {
-        // the pieces in order, as the GPU expand pass reads them
-        std::vector<uint16_t> cat;
         const std::vector<std::pair<uint32_t, uint32_t>>& pt = pieces[L.start[i]];
+        const std::vector<std::pair<uint32_t, uint32_t>>& ut = units[L.start[i]];
         const std::vector<uint16_t>& t = tok[L.start[i]];
-        for (size_t k = 0; k < pt.size(); ++k) {
-            const uint32_t n = (k + 1 < pt.size() ? pt[k + 1].second : L.res[i].ntok) - pt[k].second;
-            cat.insert(cat.end(), t.begin() + pt[k].first, t.begin() + pt[k].first + n);
-        }
-        stats[13] += cat.size();
-        cat.resize(cat.size() + 16, (uint16_t)infl::kTokPad);
-        infl::TokInHost tin{cat.data()};
-        if (infl::expand_lane(tin, (uint32_t)(cat.size() - 16), infl::U16Out{u16.data()}, obase[i], L.res[i].out_len)) {
-            if (getenv("IKM_DEBUG")) {
-                // where the tokens stop making sense: count the output they describe
-                uint64_t n = 0, bad = 0;
-                for (size_t q = 0; q + 16 < cat.size(); ++q) {
-                    const uint32_t v = cat[q];
-                    if (v == infl::kTokPad) continue;
-                    if ((v & 0xFF00u) == infl::kTokRaw) { ++n; continue; }
-                    if ((v & 0xFF00u) == infl::kTokMatch) { n += (v & 255u) + 3; ++q; continue; }
-                    if (!bad) fprintf(stderr, "lane %zu: bad token 0x%04x at %zu (out so far %llu)\n", i, v, q,
-                                      (unsigned long long)n);
-                    ++bad;
-                }
-                fprintf(stderr, "lane %zu expand failed: tokens %zu describe %llu bytes (out_len %llu), %llu bad\n", i,
-                        cat.size() - 16, (unsigned long long)n, (unsigned long long)L.res[i].out_len,
-                        (unsigned long long)bad);
+        if (ut.empty() && L.res[i].out_len) return -4;
+        for (size_t u = 0; u < ut.size(); ++u) {
+            const uint32_t p0 = ut[u].first, p1 = u + 1 < ut.size() ? ut[u + 1].first : (uint32_t)pt.size();
+            const uint64_t o0 = ut[u].second, o1 = u + 1 < ut.size() ? ut[u + 1].second : L.res[i].out_len;
+            if (p0 > p1 || p1 > pt.size() || o0 > o1) return -4;
+            std::vector<uint16_t> cat;
+            for (uint32_t k = p0; k < p1; ++k) {
+                const uint32_t n = (k + 1 < pt.size() ? pt[k + 1].second : L.res[i].ntok) - pt[k].second;
+                cat.insert(cat.end(), t.begin() + pt[k].first, t.begin() + pt[k].first + n);
             }
-            return -4;
+            stats[13] += cat.size();
+            stats[17] += 1;
+            cat.resize(cat.size() + 16, (uint16_t)infl::kTokPad);
+            infl::TokInHost tin{cat.data()};
+            const int64_t ob = obase[i] + (int64_t)o0;
+            uob.push_back(ob);
+            if (infl::expand_lane(tin, (uint32_t)(cat.size() - 16), infl::U16Out{u16.data()}, ob, o1 - o0)) {
+                if (getenv("IKM_DEBUG"))
+                    fprintf(stderr, "lane %zu unit %zu/%zu expand failed: tokens %zu, out %llu\n", i, u, ut.size(),
+                            cat.size() - 16, (unsigned long long)(o1 - o0));
+                return -4;
+            }
         }
     }
+    obase.swap(uob);
     const int shift = 12;
     std::vector<int> pages((total >> shift) + 1);
     for (size_t pg = 0, ln = 0; pg < pages.size(); ++pg) {

@@ -353,15 +353,32 @@ IK_HD Split split_range(uint64_t bp, uint64_t re, bool big) {
     return s;
 }
 // The end of a block window from bp: the staging limit, the lane's stop, and --
-// for a block after the lane's first -- about the previous block's length (a
-// block's end is found only by decoding it: sub-lanes past it decode for nothing,
-// so a lane of many short blocks sizes each block's range by the last one's; a
-// block longer than that takes another window from where the first stopped)
-IK_HD uint64_t window_end(uint64_t bp, uint64_t stop_eff, uint64_t prev_bits) {
+// for a block after the lane's first -- the block's estimated end (a block's end is
+// found only by decoding it: sub-lanes past it decode for nothing).  zlib ends a
+// block when its symbol buffer fills, so consecutive blocks of an image hold about
+// as many bits: the estimate is the previous block's length + 4 Kbit, for every
+// window of the block (a block longer than that takes one more window of at least
+// 16 Kbit; the model's sweep on bench frames: shorter estimates cost more in extra
+// windows than they save).
+#if !defined(__HIP_DEVICE_COMPILE__)
+inline int64_t g_est_mul = 1024, g_est_add = 4096, g_min_tail = 16384;  // (model experiments)
+#endif
+IK_HD uint64_t block_end_estimate(uint64_t body, uint64_t prev_bits) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+    return prev_bits ? body + prev_bits * (uint64_t)g_est_mul / 1024 + (uint64_t)g_est_add : 0;
+#else
+    return prev_bits ? body + prev_bits + 4096 : 0;
+#endif
+}
+IK_HD uint64_t window_end(uint64_t bp, uint64_t stop_eff, uint64_t est_end) {
     uint64_t re = bp + kWindowBits < stop_eff ? bp + kWindowBits : stop_eff;
-    if (prev_bits) {
-        const uint64_t est = bp + prev_bits + prev_bits / 4 + 4096;
-        if (est < re) re = est;
+    if (est_end) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+        const uint64_t e = est_end > bp + (uint64_t)g_min_tail ? est_end : bp + (uint64_t)g_min_tail;
+#else
+        const uint64_t e = est_end > bp + 16384 ? est_end : bp + 16384;
+#endif
+        if (e < re) re = e;
     }
     return re;
 }
@@ -379,7 +396,19 @@ IK_HD uint64_t region_capacity(uint64_t bits, bool big) {
 struct Stats {
     uint64_t windows = 0, sub_passes = 0, redo_passes = 0, fix_rounds = 0, max_rounds = 0;
     uint64_t symbols_bits = 0, blocks = 0, slow = 0, steps = 0;
+    uint64_t wave_steps = 0;  // the wave's latency: per pass, its longest sub-lane's steps
 };
+
+// Expand units: the expand pass runs one wave per unit -- a run of a lane's whole
+// blocks -- rather than per lane, so that a lane of many blocks (64 KiB of stream)
+// expands with the parallelism of one-block lanes.  A block starts a new unit unless
+// the lane's current unit holds fewer than kUnitMinTok tokens (short blocks share a
+// unit).  Unit record k of a lane, at the lane's piece-table slot k (a lane has no
+// more units than pieces): (its first piece, the lane's output bytes before it).
+constexpr uint32_t kUnitMinTok = 16384;
+IK_HD bool unit_starts(uint32_t nunits, uint64_t written, uint64_t unit_v0) {
+    return nunits == 0 || written - unit_v0 >= kUnitMinTok;
+}
 
 #if !defined(__HIP_DEVICE_COMPILE__)
 // The lane algorithm on the host (the CPU model; ik_png.hip k_png_wave runs the
@@ -388,7 +417,8 @@ struct Stats {
 // out_len, status, final_block, blocks) and pt.
 template <class WinFn, class Pieces>
 inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, bool big, uint16_t* region,
-                      uint64_t cap, infl::LaneResult& r, Pieces& pt, Stats* stats, uint64_t warm = kWarmBits) {
+                      uint64_t cap, infl::LaneResult& r, Pieces& pt, Pieces& units, Stats* stats,
+                      uint64_t warm = kWarmBits) {
     const uint32_t pcap = pieces_capacity((stop == ~0ull ? nbits : stop) - start);
     const uint64_t stop_eff = stop == ~0ull ? nbits : stop;
     uint64_t p = start, used = 0, total = 0, written = 0;
@@ -398,6 +428,8 @@ inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, 
     r.blocks = 0;
     r.iters = 0;
     pt.clear();
+    units.clear();
+    uint64_t unit_v0 = 0;  // the current unit's first token (virtual index)
     uint32_t lit[1u << kLB], dist[1u << kDB];
     uint16_t lsyms[288], dsyms[32];
     Code LC, DC;
@@ -409,7 +441,12 @@ inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, 
         if (p + 3 > nbits) break;
         // this block's start: a split goes back to it
         const uint64_t blk_start = p, blk_total = total, blk_used = used, blk_written = written;
-        const uint32_t blk_pieces = (uint32_t)pt.size();
+        const uint32_t blk_pieces = (uint32_t)pt.size(), blk_units = (uint32_t)units.size();
+        const uint64_t blk_v0 = unit_v0;
+        if (unit_starts((uint32_t)units.size(), written, unit_v0)) {  // (undone with the block on a split)
+            units.push_back({(uint32_t)pt.size(), (uint32_t)total});
+            unit_v0 = written;
+        }
         const uint64_t h = win(p);
         const int bfinal = (int)(h & 1u), btype = (int)((h >> 1) & 3u);
         ++r.blocks;
@@ -429,7 +466,11 @@ inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, 
             }
             const uint32_t n8 = (len + 7u) & ~7u;
             if (used + n8 > cap) { r.status = infl::kLaneOverflow; break; }
-            if (pt.size() >= pcap) { r.status = p > start ? (int)infl::kLaneSplit : (int)infl::kLaneOverflow; break; }
+            if (pt.size() >= pcap) {
+                units.resize(blk_units);  // (the split lane ends before this block)
+                r.status = p > start ? (int)infl::kLaneSplit : (int)infl::kLaneOverflow;
+                break;
+            }
             for (uint32_t i = 0; i < n8; ++i)
                 region[used + i] = i < len ? (uint16_t)(infl::kTokRaw | ((uint32_t)win(q + 8ull * i) & 255u))
                                            : (uint16_t)infl::kTokPad;
@@ -463,7 +504,7 @@ inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, 
             for (uint32_t e = 0; e < (1u << kDB); ++e) dist[e] = dist_table_entry(e, DC, dsyms);
             // the body, window by window (LDS holds kWindowBits of stream on the GPU)
             uint64_t bp = body;
-            bool first_window = true;
+            const uint64_t est_end = block_end_estimate(body, prev_bits);
             int done = 0;  // 1: block ended (p updated), 2: lane ends (status set), 3: corrupt / overflow
             while (!done) {
                 if (bp >= stop_eff) {  // the block runs past the lane's stop
@@ -471,8 +512,7 @@ inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, 
                     done = 2;
                     break;
                 }
-                const uint64_t re = window_end(bp, stop_eff, first_window ? prev_bits : 0);
-                first_window = false;
+                const uint64_t re = window_end(bp, stop_eff, est_end);
                 const Split sp = split_range(bp, re, big);
                 if (used + (uint64_t)sp.nsub * sp.cap > cap) { r.status = infl::kLaneOverflow; done = 3; break; }
                 if (stats) ++stats->windows;
@@ -486,13 +526,16 @@ inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, 
                 uint32_t lo[kSub + 1];
                 for (int j = 0; j < sp.nsub; ++j) lo[j] = 32u * sp.lw * (uint32_t)j;
                 lo[sp.nsub] = (uint32_t)(re - bp);
+                uint32_t pass_max = 0;
                 for (int j = 0; j < sp.nsub; ++j) {
                     SubOutHost o{region + used + (uint64_t)j * sp.cap, sp.cap};
                     const uint32_t p0 = j == 0 ? 0u : (lo[j] >= warm ? lo[j] - (uint32_t)warm : 0u);
                     sub_decode(rwin, p0, lo[j], lo[j + 1], lit, dist, LC, lsyms, DC, dsyms, o, sr[j]);
                     o.finish();
                     if (stats) { ++stats->sub_passes; stats->steps += sr[j].steps; }
+                    pass_max = sr[j].steps > pass_max ? sr[j].steps : pass_max;
                 }
+                if (stats) stats->wave_steps += pass_max;
                 // fix rounds: a sub-lane whose start is not its predecessor's exit decodes
                 // again from that exit (all such at once), until the chain holds
                 int v = 0, rounds = 0;
@@ -507,13 +550,16 @@ inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, 
                         ex[j] = sr[j].exit;
                         redo[j] = j > v && !sr[j - 1].eob && !sr[j - 1].bad && sr[j].start != sr[j - 1].exit;
                     }
+                    uint32_t redo_max = 0;
                     for (int j = v + 1; j < sp.nsub; ++j) {
                         if (!redo[j]) continue;
                         SubOutHost o{region + used + (uint64_t)j * sp.cap, sp.cap};
                         sub_decode(rwin, ex[j - 1], lo[j], lo[j + 1], lit, dist, LC, lsyms, DC, dsyms, o, sr[j]);
                         o.finish();
-                        if (stats) ++stats->redo_passes;
+                        if (stats) { ++stats->redo_passes; stats->steps += sr[j].steps; }
+                        redo_max = sr[j].steps > redo_max ? sr[j].steps : redo_max;
                     }
+                    if (stats) stats->wave_steps += redo_max;
                 }
                 if (stats) {
                     stats->fix_rounds += (uint64_t)rounds;
@@ -568,6 +614,8 @@ inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, 
             }
             if (done == 4) {  // split: undo this block (its earlier windows' pieces and output)
                 pt.resize(blk_pieces);
+                units.resize(blk_units);
+                unit_v0 = blk_v0;
                 total = blk_total;
                 used = blk_used;
                 written = blk_written;

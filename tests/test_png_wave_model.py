@@ -23,7 +23,7 @@ from test_png_model import CASES, _idat, filtered
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MODEL = os.path.join(ROOT, "rust-image-transform_amd", "lib", "libik_pngmodel.so")
 NAMES = ("chunks cand lanes rounds overflows windows sub_passes redo_passes fix_rounds max_rounds blocks "
-         "symbol_bits status tokens markers steps").split()
+         "symbol_bits status tokens markers steps wave_steps units").split()
 
 
 @pytest.fixture(scope="module")
@@ -41,13 +41,13 @@ def model():
 def inflate(model, z, raw_len, chunk):
     out = np.zeros(raw_len + 16, np.uint8)
     n = ctypes.c_uint64()
-    st = (ctypes.c_uint64 * 16)()
+    st = (ctypes.c_uint64 * 20)()
     rc = model.ikm_inflate_wave(z, len(z), chunk, out.ctypes.data, raw_len, ctypes.byref(n), st)
     return rc, bytes(out[:n.value]), dict(zip(NAMES, list(st)))
 
 
 @pytest.mark.parametrize("w,h,c,pat,level,strategy", CASES)
-@pytest.mark.parametrize("chunk", [4096, 16384])
+@pytest.mark.parametrize("chunk", [4096, 16384, 65536])
 def test_wave_inflate_equals_zlib(model, w, h, c, pat, level, strategy, chunk):
     raw = filtered(ikutil.synth(w, h, c, seed=w + h, pattern=pat))
     co = zlib.compressobj(level, zlib.DEFLATED, 15, 8, strategy)
@@ -109,7 +109,8 @@ def test_pillow_png_streams(model, mode, c):
 
 
 @pytest.mark.parametrize("size,seed", [(1024, 8), (640, 480), (1500, 3)])
-def test_pillow_rgba_frames(model, size, seed):
+@pytest.mark.parametrize("chunk", [16384, 65536])
+def test_pillow_rgba_frames(model, size, seed, chunk):
     """Pillow's own encoder on bench-pattern RGBA frames: sub-lane pieces that fill
     their token capacity exactly (the padded last group must fit too -- a GPU
     test caught a piece whose last group was not stored)."""
@@ -119,7 +120,7 @@ def test_pillow_rgba_frames(model, size, seed):
     Image.fromarray(img, "RGBA").save(b, format="PNG")
     z = _idat(b.getvalue())
     raw = zlib.decompress(z)
-    rc, out, st = inflate(model, z, len(raw), 16384)
+    rc, out, st = inflate(model, z, len(raw), chunk)
     assert rc == 0 and out == raw, st
 
 
