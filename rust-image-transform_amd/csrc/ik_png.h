@@ -112,6 +112,9 @@ hipError_t launch_copy_words(const uint32_t* src, uint32_t* dst, size_t n, hipSt
 #ifdef IK_UNF_PROF
 hipError_t png_unf_prof_read(unsigned long long* out);  // dev build: k_png_unfilter's segment clock sums (reset)
 #endif
+#ifdef IK_WAVE_PROF
+hipError_t png_wave_prof_read(unsigned long long* out);  // dev build: k_png_wave's phase clock sums (reset)
+#endif
 #ifdef IK_FIND_PROF
 hipError_t png_find_prof_read(unsigned long long* out);  // dev build: k_png_find's phase clock sums (reset)
 #endif

@@ -415,14 +415,40 @@ constexpr uint32_t kWaveWinWords = (uint32_t)(wave::kWindowBits / 32) + 16;  // 
 
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 
-// the 64 stream bits from bit o of the staged window (relative positions: w[0]'s bit 0 = 0)
-struct WaveLdsWin {
+// The 64 stream bits at a sub-lane's position in the staged window (relative
+// positions: w[0]'s bit 0 = 0), as a cursor: words wi .. wi+3 in registers, and
+// wi+4, wi+5 read from LDS one step ahead -- a step consumes at most 48 bits (two
+// words), so the step's bits never wait on an LDS read; only its table lookups do.
+struct WaveLdsCursor {
     const lds_u32* w;
-    __device__ uint64_t operator()(uint32_t o) const {
-        const uint32_t wi = o >> 5, sh = o & 31u;
-        const uint32_t a = w[wi], b = w[wi + 1], c = w[wi + 2];
-        const uint32_t lo = __builtin_amdgcn_alignbit(b, a, sh), hi = __builtin_amdgcn_alignbit(c, b, sh);
-        return ((uint64_t)hi << 32) | lo;
+    uint32_t wi = 0, b0 = 0, b1 = 0, b2 = 0, b3 = 0, p0 = 0, p1 = 0;
+    __device__ void init(uint32_t pos) {
+        wi = pos >> 5;
+        b0 = w[wi];
+        b1 = w[wi + 1];
+        b2 = w[wi + 2];
+        b3 = w[wi + 3];
+        p0 = w[wi + 4];
+        p1 = w[wi + 5];
+    }
+    __device__ uint64_t operator()(uint32_t pos) {
+        const uint32_t d = (pos >> 5) - wi;  // 0, 1 or 2
+        // (opaque to the optimizer: a select between two of these loaded fields would
+        // otherwise become a load through a selected address, and the cursor scratch memory)
+        asm("" : "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3), "+v"(p0), "+v"(p1));
+        const uint32_t n0 = d == 0 ? b0 : d == 1 ? b1 : b2;
+        const uint32_t n1 = d == 0 ? b1 : d == 1 ? b2 : b3;
+        const uint32_t n2 = d == 0 ? b2 : d == 1 ? b3 : p0;
+        const uint32_t n3 = d == 0 ? b3 : d == 1 ? p0 : p1;
+        b0 = n0;
+        b1 = n1;
+        b2 = n2;
+        b3 = n3;
+        wi += d;
+        p0 = w[wi + 4];  // the next step's (in flight during this one)
+        p1 = w[wi + 5];
+        const uint32_t sh = pos & 31u;
+        return ((uint64_t)__builtin_amdgcn_alignbit(b2, b1, sh) << 32) | __builtin_amdgcn_alignbit(b1, b0, sh);
     }
 };
 // the same straight from the stream in memory (block headers, stored blocks)
@@ -437,45 +463,52 @@ struct WaveGlobalWin {
     }
 };
 
-// A sub-lane's token output on the GPU: the open group of 8 tokens sits in LDS
-// (a 16-token ring per lane, lane-minor: token slot q of lane l at 16-bit half q & 1
-// of dword 64 (q >> 1) + l, so no two lanes share a bank), each completed group
-// goes to the sub-lane's piece with one 16-byte store.  (may_alias: the slots are
-// written as u16 and read back as dwords.)
-typedef __attribute__((address_space(3), may_alias)) uint16_t lds_u16a;
-typedef __attribute__((address_space(3), may_alias)) uint32_t lds_u32a;
+// A sub-lane's token output on the GPU: the open group of 8 tokens sits in two
+// 64-bit registers (token slot i at bits 16 i of g0:g1), each completed group goes
+// to the sub-lane's piece with one 16-byte store -- no LDS traffic per token.
 struct WaveOut {
     IK_GLOBAL uint16_t* p;
     uint32_t cap;        // tokens (a multiple of 8)
-    uint32_t n;          // tokens put
-    lds_u32a* ring;      // this lane's dword 0 (s_ring + lane)
-    __device__ void reset() { n = 0; }
-    __device__ void slot(uint32_t q, uint32_t t) const {
-        ((lds_u16a*)(ring + 64u * ((q & 15u) >> 1)))[q & 1u] = (uint16_t)t;
-    }
-    __device__ void flush(uint32_t g) const {  // the group of tokens [g, g + 8) (g a multiple of 8)
+    uint32_t n = 0;      // tokens put
+    uint64_t g0 = 0, g1 = 0;
+    __device__ void reset() { n = 0; g0 = 0; g1 = 0; }
+    __device__ void mark(uint32_t, uint32_t) const {}  // (the CPU model's step profile)
+    __device__ void store(uint32_t g) const {  // the group of tokens [g, g + 8) (g a multiple of 8)
         if (g + 8u > cap) return;
-        const uint32_t r0 = (g & 15u) >> 1;
         typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-        const u4 q = {ring[64u * r0], ring[64u * (r0 + 1u)], ring[64u * (r0 + 2u)], ring[64u * (r0 + 3u)]};
+        const u4 q = {(uint32_t)g0, (uint32_t)(g0 >> 32), (uint32_t)g1, (uint32_t)(g1 >> 32)};
         *reinterpret_cast<IK_GLOBAL u4*>(p + g) = q;
     }
-    // all four slots are written whatever k is: a slot past the k tokens is a free
-    // slot of the open group or the next, which a later token overwrites before the
-    // group is stored (and it is never in the group this call completes)
+    // the first k of the four tokens at slot n & 7 (the part past slot 7 opens the next group)
     __device__ void put4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
-        slot(n, a);
-        slot(n + 1u, b);
-        slot(n + 2u, c);
-        slot(n + 3u, d);
+        uint64_t T = (uint64_t)(a & 0xFFFFu) | ((uint64_t)(b & 0xFFFFu) << 16) | ((uint64_t)(c & 0xFFFFu) << 32) |
+                     ((uint64_t)d << 48);
+        T &= k >= 4u ? ~0ull : (1ull << (16u * k)) - 1ull;
+        // (selects of shifts, no branches: the 128-bit group g0:g1 |= T << off, the part
+        // past bit 128 is the next group's start)
+        const uint32_t off = 16u * (n & 7u);  // 0 .. 112
+        const uint64_t lo_part = T << (off & 63u), hi_part = (T >> 1) >> (63u - (off & 63u));
+        g0 |= off < 64u ? lo_part : 0ull;
+        g1 |= off < 64u ? hi_part : lo_part;  // (off 0: hi_part is 0)
+        const uint64_t carry = off > 64u ? hi_part : 0ull;
         const uint32_t n2 = n + k;
-        if ((n2 ^ n) & ~7u) flush((n2 & ~7u) - 8u);  // a group completed
+        const bool done = ((n2 ^ n) & ~7u) != 0u;  // a group completed
+        if (done) store(n & ~7u);
+        g0 = done ? carry : g0;
+        g1 = done ? 0ull : g1;
         n = n2;
     }
     __device__ void finish() {  // pad the open group and store it
         if (n & 7u) {
-            for (uint32_t q = n; q & 7u; ++q) slot(q, infl::kTokPad);
-            flush(n & ~7u);
+            constexpr uint64_t P = 0xFFFEFFFEFFFEFFFEull;
+            const uint32_t off = 16u * (n & 7u);  // 16 .. 112
+            if (off < 64u) {
+                g0 |= P << off;
+                g1 |= P;
+            } else {
+                g1 |= P << (off - 64u);
+            }
+            store(n & ~7u);
         }
     }
 };
@@ -561,16 +594,19 @@ __device__ bool wave_code_build(const uint8_t* lens, int n, bool is_dist, bool f
 }
 
 // The block's codes by the wave: a dynamic header's code-length code (lanes 0..18
-// take one length each) and its 7-bit decode table (cl, LDS), the literal/length
-// and distance code lengths (lane 0, serial: the repeat codes chain them) from the
-// header's bits staged in hw (LDS words from stream bit hb0), then both codes
-// (wave_code_build).  Checks as infl::parse_dynamic (zlib).  *body = the first
-// bit of the block's data.
-__device__ bool wave_block_codes(const IK_GLOBAL uint32_t* W, uint64_t nbits, uint64_t p, int btype, uint32_t* hw,
-                                 uint8_t* cl, uint8_t* lens, wave::Code* code, uint16_t* lsym, uint16_t* dsym,
-                                 int* shared_ok, uint64_t* body) {
+// take one length each) and its 7-bit decode table, then the literal/length and
+// distance code lengths, then both codes (wave_code_build).  Checks as
+// infl::parse_dynamic (zlib).  *body = the first bit of the block's data.
+// The header's 160 words (17 + 57 + 316 * 14 bits at most) stay in registers, lane
+// l holding words l, 64 + l, 128 + l, and so does the 128-entry decode table (lane l:
+// entries l and 64 + l): the code-length symbols -- a serial chain, each one's
+// length places the next -- are decoded by the whole wave in step, every value
+// wave-uniform (scalar ALU, v_readlane lookups), with no memory latency in the
+// chain; a repeat run is written by as many lanes at once.
+__device__ bool wave_block_codes(const IK_GLOBAL uint32_t* W, uint64_t nbits, uint64_t p, int btype,
+                                 uint8_t* lens, wave::Code* code, uint16_t* lsym, uint16_t* dsym, uint64_t* body) {
     const int lane = threadIdx.x;
-    __syncthreads();  // the previous block's readers of hw (the staged window) and of the tables are done
+    __syncthreads();  // the previous block's readers of the tables are done
     if (btype == 1) {
         for (int i = lane; i < 288 + 32; i += 64) lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < 288 ? 8 : 5;
         __syncthreads();
@@ -580,23 +616,24 @@ __device__ bool wave_block_codes(const IK_GLOBAL uint32_t* W, uint64_t nbits, ui
         __syncthreads();
         return a && b;
     }
-    // stage the header: 17 + 57 + 316 * 14 bits at most -- 160 words from p's word
     const uint64_t hb0 = (p >> 5) << 5;
     const uint64_t wmax = (nbits >> 5) + 64;  // (the stream's zero padding: 128 words)
-    for (int k = lane; k < 160; k += 64) hw[k] = (p >> 5) + (uint64_t)k < wmax ? W[(p >> 5) + (uint64_t)k] : 0u;
-    __syncthreads();
-    auto bits = [&](uint32_t o) -> uint64_t {  // 64 bits from relative bit o
-        const uint32_t wi = o >> 5, sh = o & 31u;
-        const uint32_t a = hw[wi], b = hw[wi + 1], c = hw[wi + 2];
-        return ((uint64_t)__builtin_amdgcn_alignbit(c, b, sh) << 32) | __builtin_amdgcn_alignbit(b, a, sh);
+    auto hload = [&](int k) -> uint32_t { return k < 160 && (p >> 5) + (uint64_t)k < wmax ? W[(p >> 5) + (uint64_t)k] : 0u; };
+    const uint32_t hv0 = hload(lane), hv1 = hload(lane + 64), hv2 = hload(lane + 128);
+    auto word = [&](uint32_t k) -> uint32_t {  // header word k (wave-uniform k < 192)
+        const uint32_t src = k < 64u ? hv0 : k < 128u ? hv1 : hv2;
+        return (uint32_t)__builtin_amdgcn_readlane((int)src, (int)(k & 63u));
+    };
+    auto bits32 = [&](uint32_t o) -> uint32_t {  // 32 bits from relative bit o
+        return __builtin_amdgcn_alignbit(word((o >> 5) + 1u), word(o >> 5), o & 31u);
     };
     const uint32_t o0 = (uint32_t)(p - hb0) + 3;
-    const uint64_t h = bits(o0);
+    const uint32_t h = bits32(o0);
     const int nlen = (int)(h & 31u) + 257, ndist = (int)((h >> 5) & 31u) + 1, ncode = (int)((h >> 10) & 15u) + 4;
     if (nlen > 286 || ndist > 30) return false;
-    // the code-length code: lane s holds symbol s's length
+    // the code-length code: lane s holds symbol s's length (57 bits from o0 + 14)
     constexpr uint8_t inv_order[19] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};
-    const uint64_t clb = bits(o0 + 14);
+    const uint64_t clb = (uint64_t)bits32(o0 + 14) | ((uint64_t)bits32(o0 + 46) << 32);
     uint32_t myl = 0;
     if (lane < 19) {
         const int i = inv_order[lane];
@@ -609,6 +646,8 @@ __device__ bool wave_block_codes(const IK_GLOBAL uint32_t* W, uint64_t nbits, ui
 #pragma unroll
     for (int L = 1; L <= 7; ++L) kraft += cnt[L] << (7 - L);
     if (kraft != 128u) return false;  // the code-length code must be complete
+    // the decode table: entry e (the next 7 bits, first bit lowest) = symbol | length << 5
+    uint32_t tab = 0;  // this lane's entries lane (byte 0) and 64 + lane (byte 1)
     {
         uint32_t code_l = 0, first[8];
 #pragma unroll
@@ -616,66 +655,79 @@ __device__ bool wave_block_codes(const IK_GLOBAL uint32_t* W, uint64_t nbits, ui
             code_l = (code_l + (L > 1 ? cnt[L - 1] : 0u)) << 1;
             first[L] = code_l;
         }
-        uint32_t mycode = 0;
+        uint32_t mine = 0;  // (bit-reversed code | length << 8) of this lane's symbol
 #pragma unroll
         for (int L = 1; L <= 7; ++L) {
             const unsigned long long m = __ballot(myl == (uint32_t)L);
-            if (myl == (uint32_t)L) mycode = first[L] + lane_rank(m);
+            if (myl == (uint32_t)L) mine = (__builtin_bitreverse32(first[L] + lane_rank(m)) >> (32 - L)) | ((uint32_t)L << 8);
         }
-        if (myl) {
-            const uint32_t r = __builtin_bitreverse32(mycode) >> (32 - myl);
-            for (uint32_t e = r; e < 128u; e += 1u << myl) cl[e] = (uint8_t)(lane | (myl << 5));
+        for (int sy = 0; sy < 19; ++sy) {
+            const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)mine, sy);
+            const uint32_t Ls = q >> 8;
+            if (!Ls) continue;
+            const uint32_t r = q & 127u, msk = (1u << Ls) - 1u, ent = (uint32_t)sy | (Ls << 5);
+            if (((uint32_t)lane & msk) == r) tab |= ent;
+            if (((uint32_t)(lane + 64) & msk) == r) tab |= ent << 8;
         }
     }
-    __syncthreads();
-    if (lane == 0) {
-        uint32_t o = o0 + 14 + 3 * (uint32_t)ncode;
-        const int total = nlen + ndist;
-        int i = 0, ok = 1, prev = -1;
-        while (i < total) {
-            const uint64_t v = bits(o);
-            const uint32_t e = cl[(uint32_t)v & 127u];
-            const uint32_t L = e >> 5, sym = e & 31u;
-            int rep = 1, val = (int)sym;
-            uint32_t xb = 0;
-            if (sym == 16) {
-                if (prev < 0) { ok = 0; break; }
-                val = prev;  // (the previous length: the literal/length code's last one for the first distance)
-                xb = 2;
-                rep = 3 + (int)((uint32_t)(v >> L) & 3u);
-            } else if (sym == 17) {
-                val = 0;
-                xb = 3;
-                rep = 3 + (int)((uint32_t)(v >> L) & 7u);
-            } else if (sym == 18) {
-                val = 0;
-                xb = 7;
-                rep = 11 + (int)((uint32_t)(v >> L) & 127u);
-            }
-            if (i + rep > total) { ok = 0; break; }
-            for (int k = 0; k < rep; ++k) {
-                // the distance lengths go to lens[288 ..] directly
-                const int d = i + k;
-                lens[d < nlen ? d : 288 + (d - nlen)] = (uint8_t)val;
-            }
-            i += rep;
-            prev = val;
-            o += L + xb;
-            if (o > 160 * 32 - 96) { ok = 0; break; }  // past any valid header
+    // the literal/length and distance code lengths (the distance lengths to lens[288 ..])
+    uint32_t o = o0 + 14 + 3 * (uint32_t)ncode;
+    const int total = nlen + ndist;
+    int i = 0, prev = -1;
+    bool ok = true;
+    while (i < total) {
+        const uint32_t v = bits32(o);
+        const uint32_t e7 = v & 127u;
+        const uint32_t ent = ((uint32_t)__builtin_amdgcn_readlane((int)tab, (int)(e7 & 63u)) >> (8u * (e7 >> 6))) & 255u;
+        const uint32_t L = ent >> 5, sym = ent & 31u;
+        int rep = 1, val = (int)sym;
+        uint32_t xb = 0;
+        if (sym == 16) {
+            if (prev < 0) { ok = false; break; }
+            val = prev;  // (the previous length: the literal/length code's last one for the first distance)
+            xb = 2;
+            rep = 3 + (int)((v >> L) & 3u);
+        } else if (sym == 17) {
+            val = 0;
+            xb = 3;
+            rep = 3 + (int)((v >> L) & 7u);
+        } else if (sym == 18) {
+            val = 0;
+            xb = 7;
+            rep = 11 + (int)((v >> L) & 127u);
         }
-        if (ok && lens[256] == 0) ok = 0;  // no end-of-block code
-        shared_ok[0] = ok;
-        shared_ok[1] = (int)o;
+        if (i + rep > total) { ok = false; break; }
+        for (int k0 = 0; k0 < rep; k0 += 64) {
+            const int d = i + k0 + lane;
+            if (k0 + lane < rep) lens[d < nlen ? d : 288 + (d - nlen)] = (uint8_t)val;
+        }
+        i += rep;
+        prev = val;
+        o += L + xb;
+        if (o > 160 * 32 - 96) { ok = false; break; }  // past any valid header
     }
-    __syncthreads();
-    if (!shared_ok[0]) return false;
-    *body = hb0 + (uint32_t)shared_ok[1];
+    __syncthreads();  // the lengths are in LDS
+    if (!ok || lens[256] == 0) return false;  // (no end-of-block code: invalid)
+    *body = hb0 + o;
     if (*body > nbits) return false;
     const bool a = wave_code_build(lens, nlen, false, false, code[0], lsym);
     const bool b = wave_code_build(lens + 288, ndist, true, false, code[1], dsym);
     __syncthreads();
     return a && b;
 }
+
+#ifdef IK_WAVE_PROF  // dev build: k_png_wave's phase clock sums (tools/dev_png experiments)
+__device__ unsigned long long g_wave_prof[8];
+hipError_t png_wave_prof_read(unsigned long long* out) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_prof), sizeof(g_wave_prof));
+    unsigned long long z[8] = {};
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_wave_prof), z, sizeof(z));
+    return e;
+}
+#define IK_WP(k, t0) (wprof[k] += clock64() - (t0))
+#else
+#define IK_WP(k, t0) ((void)0)
+#endif
 
 __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const PngLaneDev* lanes, const uint32_t* order,
                                                  int nlanes, uint16_t* tok, uint2* pieces, uint2* units,
@@ -686,10 +738,7 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
     __shared__ uint16_t s_lsym[288];
     __shared__ uint16_t s_dsym[32];
     __shared__ uint8_t s_lens[288 + 32];
-    __shared__ uint8_t s_cl[128];  // the code-length code's decode table (symbol | length << 5)
-    __shared__ uint32_t s_ring[8 * 64];  // the sub-lanes' open token groups (WaveOut)
     __shared__ wave::Code s_code[2];
-    __shared__ int s_hdr[4];  // lane 0's header parse: status, body position (lo, hi)
     const int slot = blockIdx.x;
     if (slot >= nlanes) return;
     const int t = order ? (int)order[slot] : slot;
@@ -707,6 +756,9 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
     const uint32_t pcap = L.npieces;  // piece-table entries of this lane (wave::pieces_capacity)
     const bool big = L.big != 0;
     const uint64_t c0 = clock64();
+#ifdef IK_WAVE_PROF
+    uint64_t wprof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     uint64_t p = start, used = 0, total = 0;
     uint32_t npieces = 0, nblocks = 0, steps = 0, nunits = 0;
     uint64_t written = 0;  // tokens in the pieces (padding included)
@@ -769,11 +821,29 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
             // ---- the block's codes, by the wave ----
             uint64_t body = 0;
             const uint64_t ck0 = clock64();
-            if (!wave_block_codes(W, nbits, p, btype, s_win, s_cl, s_lens, s_code, s_lsym, s_dsym, s_hdr, &body)) break;
+            if (!wave_block_codes(W, nbits, p, btype, s_lens, s_code, s_lsym, s_dsym, &body)) break;
+            IK_WP(1, ck0);
             // ---- the lookup tables, all lanes ----
-            for (uint32_t e = (uint32_t)lane; e < (1u << wave::kLB); e += 64) s_lit[e] = wave::lit_table_entry(e, s_code[0], lsym);
-            for (uint32_t e = (uint32_t)lane; e < (1u << wave::kDB); e += 64) s_dist[e] = wave::dist_table_entry(e, s_code[1], dsym);
+            [[maybe_unused]] const uint64_t ckt = clock64();
+            {
+                // the codes' limits in registers (wave-uniform), their per-length info read from LDS
+                struct CodeRegs {
+                    uint32_t pk[8];
+                    const lds_u32* info;
+                };
+                CodeRegs lc, dc;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    lc.pk[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_code[0].pk[k]);
+                    dc.pk[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_code[1].pk[k]);
+                }
+                lc.info = (const lds_u32*)s_code[0].info;
+                dc.info = (const lds_u32*)s_code[1].info;
+                for (uint32_t e = (uint32_t)lane; e < (1u << wave::kLB); e += 64) s_lit[e] = wave::lit_table_entry(e, lc, lsym);
+                for (uint32_t e = (uint32_t)lane; e < (1u << wave::kDB); e += 64) s_dist[e] = wave::dist_table_entry(e, dc, dsym);
+            }
             __syncthreads();
+            IK_WP(2, ckt);
             ck_setup += clock64() - ck0;
             // ---- the body, window by window ----
             uint64_t bp = body;
@@ -798,26 +868,44 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
                     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
                     const IK_GLOBAL u4* src = (const IK_GLOBAL u4*)(W + w0);
                     __syncthreads();  // the previous window's readers are done
-                    for (uint32_t k = (uint32_t)lane; k < nq; k += 64) *(u4*)(s_win + 4 * k) = src[k];
+                    // 7 loads in flight per lane (a 12 KiB window is 13 per lane): two memory
+                    // latencies per window, not one per load
+                    for (uint32_t k0 = (uint32_t)lane; k0 < nq; k0 += 7 * 64) {
+                        u4 v[7];
+#pragma unroll
+                        for (int i = 0; i < 7; ++i)
+                            if (k0 + 64u * i < nq) v[i] = src[k0 + 64u * i];
+#pragma unroll
+                        for (int i = 0; i < 7; ++i)
+                            if (k0 + 64u * i < nq) *(u4*)(s_win + 4 * (k0 + 64u * i)) = v[i];
+                    }
                     __syncthreads();
+                    IK_WP(3, ck1);
                     ck_setup += clock64() - ck1;
                 }
-                const WaveLdsWin win{(const lds_u32*)s_win};
+                WaveLdsCursor win{(const lds_u32*)s_win};
                 const int j = lane;
                 const bool act = j < sp.nsub;
                 // positions relative to the staged window's first bit (w0 << 5)
                 const uint32_t rb = (uint32_t)(bp - (w0 << 5));
                 const uint32_t lo = rb + 32u * sp.lw * (uint32_t)j;
                 const uint32_t hi = j + 1 < sp.nsub ? lo + 32u * sp.lw : (uint32_t)(re - (w0 << 5));
-                WaveOut o{region + used + (uint64_t)j * sp.cap, sp.cap, 0u, (lds_u32a*)s_ring + lane};
+                WaveOut o{region + used + (uint64_t)j * sp.cap, sp.cap};
                 wave::SubRes r{};
                 r.start = r.exit = ~0u;
+#ifdef IK_WAVE_PROF
+                const uint64_t ckp = clock64();
+#endif
                 if (act) {
                     const uint32_t p0 = j == 0 ? rb : (lo >= rb + wave::kWarmBits ? lo - (uint32_t)wave::kWarmBits : rb);
                     wave::sub_decode(win, p0, lo, hi, lit, dist, s_code[0], lsym, s_code[1], dsym, o, r);
                     o.finish();
                     steps += r.steps;
                 }
+                IK_WP(4, ckp);
+#ifdef IK_WAVE_PROF
+                const uint64_t ckf = clock64();
+#endif
                 // fix rounds (all lanes in the shuffles; the redone sub-lanes diverge)
                 int v = 0;
                 for (;;) {
@@ -834,6 +922,7 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
                         steps += r.steps;
                     }
                 }
+                IK_WP(5, ckf);
                 const bool in = j <= v;
                 if (__ballot(in && r.over)) { status = infl::kLaneOverflow; done = 3; break; }
                 if (npieces + (uint32_t)(v + 1) > pcap) {
@@ -897,6 +986,11 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
         r.kc_setup = (uint32_t)(ck_setup >> 10);
         r.units = nunits;
         res[t] = r;
+#ifdef IK_WAVE_PROF
+        wprof[0] = clock64() - c0;
+        wprof[7] = 1;
+        for (int k = 0; k < 8; ++k) atomicAdd(&g_wave_prof[k], (unsigned long long)wprof[k]);
+#endif
     }
 }
 

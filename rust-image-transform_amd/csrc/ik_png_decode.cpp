@@ -1157,6 +1157,17 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             if (e2 == hipSuccess) e2 = X.d2h_finish(hres.data(), d_res, rbytes, roff, ev.ok ? ev.e[10] : nullptr);
             if (e2 != hipSuccess) { rc = hip_fail(e2, "PNG inflate (decode)"); break; }
             count_dev += ev_ms(2, 3);
+#ifdef IK_WAVE_PROF
+            if (wavedec) {
+                unsigned long long pf[8] = {};
+                if (png_wave_prof_read(pf) == hipSuccess && pf[7])
+                    fprintf(stderr, "[wave-prof] lanes %llu: kcycles/lane total %.0f, codes %.0f, tables %.0f, staging %.0f, "
+                            "first passes %.0f, fix rounds %.0f, rest %.0f\n", pf[7], pf[0] / 1024.0 / pf[7],
+                            pf[1] / 1024.0 / pf[7], pf[2] / 1024.0 / pf[7], pf[3] / 1024.0 / pf[7], pf[4] / 1024.0 / pf[7],
+                            pf[5] / 1024.0 / pf[7],
+                            ((double)pf[0] - pf[1] - pf[2] - pf[3] - pf[4] - pf[5]) / 1024.0 / pf[7]);
+            }
+#endif
             ++rounds;
             std::vector<char> again(m, 0);  // a job with overflowed lanes: those first, then the check
             for (size_t t = 0; t < hl.size(); ++t) {

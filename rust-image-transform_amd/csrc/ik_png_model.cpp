@@ -294,6 +294,11 @@ int ikm_inflate_wave(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8_t*
     stats[12] = (uint64_t)(int64_t)st;
     stats[15] = ws.steps;
     stats[16] = ws.wave_steps;
+    if (getenv("IKM_PROF"))
+        fprintf(stderr, "[model] first-pass wave steps %llu: any slow literal %.1f%%, slow distance %.1f%%, group store "
+                "%.1f%%, match %.1f%%, warm-up %.1f%%\n", (unsigned long long)ws.prof[7],
+                100.0 * ws.prof[0] / ws.prof[7], 100.0 * ws.prof[1] / ws.prof[7], 100.0 * ws.prof[2] / ws.prof[7],
+                100.0 * ws.prof[3] / ws.prof[7], 100.0 * ws.prof[4] / ws.prof[7]);
     if (st) return -2;
     std::vector<int64_t> obase;
     uint64_t total;

@@ -38,6 +38,16 @@
 namespace ik {
 namespace wave {
 
+// IK_KEEP(x, y): on the GPU, x and y are computed on every path here (an empty
+// volatile asm uses them), so the selects after it stay selects -- the compiler
+// would otherwise sink an arm's arithmetic into a branch of its own, and a wave
+// whose sub-lanes take both arms runs both with exec-mask bookkeeping around them.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define IK_KEEP(x, y) asm volatile("" ::"v"(x), "v"(y))
+#else
+#define IK_KEEP(x, y) ((void)0)
+#endif
+
 constexpr int kLB = 10;                 // literal/length table bits
 constexpr int kDB = 8;                  // distance table bits
 constexpr uint32_t kLM = (1u << kLB) - 1u, kDM = (1u << kDB) - 1u;
@@ -139,8 +149,8 @@ IK_HD int code_build(const Lens& lens, int n, bool is_dist, Code& C, Syms syms, 
 
 // canonical decode of the next 15 stream bits (v: bit 0 = the next bit): symbol and
 // code length L, or L > 15 for no code
-template <class Syms>
-IK_HD int canon_sym(uint32_t v15, const Code& C, const Syms& syms, int& L) {
+template <class CodeT, class Syms>
+IK_HD int canon_sym(uint32_t v15, const CodeT& C, const Syms& syms, int& L) {
     const uint32_t c15 = infl::rev32(v15) >> 17;
     L = infl::canon_len(c15, C.pk);
     if (L > 15) return -1;
@@ -165,8 +175,8 @@ IK_HD uint32_t dist_symbol_entry(int sym, uint32_t D) {
 }
 
 // table entry e (the next kLB stream bits, bit 0 first)
-template <class Syms>
-IK_HD uint32_t lit_table_entry(uint32_t e, const Code& C, const Syms& syms) {
+template <class CodeT, class Syms>
+IK_HD uint32_t lit_table_entry(uint32_t e, const CodeT& C, const Syms& syms) {
     int L;
     const int s = canon_sym(e, C, syms, L);  // (bits past kLB read as zero: a code longer than kLB shows L > kLB)
     if (L > kLB || s < 0) return kSlowEntry;
@@ -179,8 +189,8 @@ IK_HD uint32_t lit_table_entry(uint32_t e, const Code& C, const Syms& syms) {
     }
     return lit_symbol_entry(s, (uint32_t)L);
 }
-template <class Syms>
-IK_HD uint32_t dist_table_entry(uint32_t e, const Code& C, const Syms& syms) {
+template <class CodeT, class Syms>
+IK_HD uint32_t dist_table_entry(uint32_t e, const CodeT& C, const Syms& syms) {
     int D;
     const int s = canon_sym(e, C, syms, D);
     if (D > kDB || s < 0) return kSlowDist;
@@ -212,7 +222,12 @@ struct SubOutHost {
     uint16_t* p;
     uint32_t cap;        // tokens (a multiple of 8)
     uint32_t n = 0;      // tokens put
+    uint8_t* marks = nullptr;  // the model's step profile: flags per step (sub_decode's out.mark)
+    uint32_t nmarks = 0;
     IK_HD void reset() { n = 0; }
+    IK_HD void mark(uint32_t step, uint32_t f) {
+        if (marks && step - 1 < nmarks) marks[step - 1] |= (uint8_t)f;
+    }
     IK_HD void put4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
         const uint32_t t[4] = {a, b, c, d};
         for (uint32_t i = 0; i < k; ++i) {
@@ -243,7 +258,8 @@ struct SubRes {
 // one when p0 >= lo), symbols before `lo` are the warm-up (no output; invalid codes skip a
 // bit, end-of-block codes are stepped over); from the first boundary >= lo (START)
 // tokens go out until the first boundary >= hi (EXIT) or an end-of-block code.
-// win(pos) = the 64 stream bits from pos; lit / dist = the shared tables; C / syms
+// win(pos) = the 64 stream bits from pos (positions only grow, by at most 48 bits a
+// step, after win.init(p0)); lit / dist = the shared tables; C / syms
 // = the codes (the slow path).  One step decodes up to four literals (two table
 // entries of one or two each) or one match; both are computed and selected, so
 // the lanes of a wave stay together except on the rare slow codes.
@@ -252,36 +268,38 @@ IK_HD void sub_decode(Win& win, uint32_t p0, uint32_t lo, uint32_t hi, const Lit
                       const Code& LC, const LSyms& lsyms, const Code& DC, const DSyms& dsyms, Out& out,
                       SubRes& r) {
     uint32_t pos = p0;
-    bool started = p0 >= lo;
-    r.start = started ? p0 : 0;
+    win.init(p0);  // (the GPU's cursor keeps the stream bits around pos in registers)
+    // START is the first boundary at or past lo: positions only grow, so a step is
+    // past START iff pos >= lo.  The step's control is bitwise (no short-circuit
+    // branches: on the GPU a wave's 64 sub-lanes take one path); the loop's only
+    // exits are the range end and a verified end-of-block / invalid code.
+    r.start = p0 >= lo ? p0 : ~0u;
     r.eob = 0;
     r.bad = 0;
     out.reset();
     uint32_t cnt = 0;
     uint32_t steps = 0;
-    for (;;) {
+    bool stop = pos >= hi;
+    while (!stop) {
         ++steps;
-        uint32_t limit = started ? hi : lo;
-        if (pos >= limit) {
-            if (started) break;
-            started = true;  // START: the first boundary at or past lo
-            r.start = pos;
-            limit = hi;
-            if (pos >= limit) break;
-        }
+        const bool started = pos >= lo;
+        r.start = (started & (r.start == ~0u)) ? pos : r.start;
+        const uint32_t limit = started ? hi : lo;
         const uint64_t v = win(pos);
         uint32_t e1 = lit[(uint32_t)v & kLM];
-        if (e_kind(e1) == kKSlow) e1 = lit_slow(v, LC, lsyms);
+        const bool slow1 = e_kind(e1) == kKSlow;
+        if (slow1) e1 = lit_slow(v, LC, lsyms);
         const uint32_t k1 = e_kind(e1), n1 = e_bits(e1), L1 = e_len1(e1);
         // literals: e1's one or two, then the next entry's (each taken only while
         // it starts before the limit)
         const bool isl = k1 == kKLit;
-        const bool two1 = e_two(e1) && pos + L1 < limit;
+        const bool two1 = e_two(e1) & (pos + L1 < limit);
         const uint32_t c1 = two1 ? n1 : L1;
         const uint32_t e2 = lit[(uint32_t)(v >> c1) & kLM];
-        const bool lit2 = isl && (two1 || !e_two(e1)) && pos + c1 < limit && e_kind(e2) == kKLit;
+        const bool lit2 = ((uint32_t)isl & ((uint32_t)two1 | (uint32_t)!e_two(e1)) & (uint32_t)(pos + c1 < limit) &
+                           (uint32_t)(e_kind(e2) == kKLit)) != 0u;
         const uint32_t L2 = e_len1(e2);
-        const bool two2 = lit2 && e_two(e2) && pos + c1 + L2 < limit;
+        const bool two2 = lit2 & e_two(e2) & (pos + c1 + L2 < limit);
         const uint32_t c2 = lit2 ? (two2 ? e_bits(e2) : L2) : 0u;
         // a match (computed for every symbol, used for a length code)
         const uint32_t le = e_lextra(e1);
@@ -289,28 +307,38 @@ IK_HD void sub_decode(Win& win, uint32_t p0, uint32_t lo, uint32_t hi, const Lit
         const uint64_t vd = v >> (n1 + le);
         uint32_t d = dist[(uint32_t)vd & kDM];
         const bool isn = k1 == kKLen;
-        if (isn && d_slow(d)) d = dist_slow(vd, DC, dsyms);
-        const bool bad = k1 == kKSlow || (isn && d_slow(d));
+        const bool slow2 = isn & d_slow(d);
+        if (slow2) d = dist_slow(vd, DC, dsyms);
+        const bool bad = (k1 == kKSlow) | (isn & d_slow(d));
         const uint32_t D = d_len(d), de = d_extra(d);
         const uint32_t dd = d_base(d) + ((uint32_t)(vd >> D) & ((1u << de) - 1u));
+        IK_KEEP(ll, dd);
         const bool eob = k1 == kKEob;
-        if (started && (bad || eob)) {
-            if (eob) pos += n1;
-            r.eob = eob;
-            r.bad = bad;
-            break;
-        }
+        const bool fin = started & (bad | eob);  // the pass ends here (no tokens)
         // tokens: literals a b c d (two1 / lit2 / two2 say which), or the match's two
         const uint32_t t1 = isl ? infl::kTokRaw | e_lit1(e1) : infl::kTokMatch | (ll - 3u);
-        const uint32_t t2 = isl ? infl::kTokRaw | (two1 ? e_lit2(e1) : e_lit1(e2)) : dd - 1u;
+        const uint32_t t2l = infl::kTokRaw | (two1 ? e_lit2(e1) : e_lit1(e2)), t2m = dd - 1u;
+        IK_KEEP(t2l, t2m);
+        const uint32_t t2 = isl ? t2l : t2m;
         const uint32_t t3 = infl::kTokRaw | (two1 ? e_lit1(e2) : e_lit2(e2));
         const uint32_t t4 = infl::kTokRaw | e_lit2(e2);
         const uint32_t nl = 1u + (two1 ? 1u : 0u) + (lit2 ? 1u : 0u) + (two2 ? 1u : 0u);
-        const uint32_t k = !started ? 0u : isl ? nl : isn ? 2u : 0u;
+        const bool emit = started & !fin;
+        const uint32_t k = !emit ? 0u : isl ? nl : isn ? 2u : 0u;
+        out.mark(steps, (slow1 ? 1u : 0u) | (slow2 ? 2u : 0u) | (((out.n + k) ^ out.n) & ~7u ? 4u : 0u) |
+                            (isn ? 8u : 0u) | (!started ? 16u : 0u));
         out.put4(t1, t2, t3, t4, k);
-        cnt += !started ? 0u : isl ? nl : isn ? ll : 0u;
-        pos += isl ? c1 + c2 : isn ? n1 + le + D + de : eob ? n1 : 1u;  // (warm-up: an invalid code skips a bit)
+        cnt += !emit ? 0u : isl ? nl : isn ? ll : 0u;
+        // (warm-up: an invalid code skips a bit; a verified invalid code stays put)
+        const uint32_t adv_l = c1 + c2, adv_n = n1 + le + D + de;
+        IK_KEEP(adv_l, adv_n);
+        const uint32_t adv = isl ? adv_l : isn ? adv_n : eob ? n1 : 1u;
+        pos += (fin & bad) ? 0u : adv;
+        r.eob = fin & eob;
+        r.bad = fin & bad;
+        stop = fin | (pos >= hi);
     }
+    if (r.start == ~0u) r.start = pos;  // (the range was crossed in one step: START = EXIT)
     r.exit = pos;
     r.out = cnt;
     r.ntok = out.n;
@@ -397,6 +425,8 @@ struct Stats {
     uint64_t windows = 0, sub_passes = 0, redo_passes = 0, fix_rounds = 0, max_rounds = 0;
     uint64_t symbols_bits = 0, blocks = 0, slow = 0, steps = 0;
     uint64_t wave_steps = 0;  // the wave's latency: per pass, its longest sub-lane's steps
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // first passes' wave steps with any sub-lane: slow literal,
+                                                  // slow distance, group store, match, warm-up; all steps
 };
 
 // Expand units: the expand pass runs one wave per unit -- a run of a lane's whole
@@ -521,21 +551,32 @@ inline void lane_host(WinFn win, uint64_t nbits, uint64_t start, uint64_t stop, 
                 struct RelWin {
                     WinFn& w;
                     uint64_t base;
+                    void init(uint32_t) {}
                     uint64_t operator()(uint32_t rel) const { return w(base + rel); }
                 } rwin{win, bp};
                 uint32_t lo[kSub + 1];
                 for (int j = 0; j < sp.nsub; ++j) lo[j] = 32u * sp.lw * (uint32_t)j;
                 lo[sp.nsub] = (uint32_t)(re - bp);
                 uint32_t pass_max = 0;
+                std::vector<uint8_t> wmarks(stats ? 4096 : 0, 0);
                 for (int j = 0; j < sp.nsub; ++j) {
                     SubOutHost o{region + used + (uint64_t)j * sp.cap, sp.cap};
+                    std::vector<uint8_t> sm(wmarks.size(), 0);
+                    o.marks = sm.data();
+                    o.nmarks = (uint32_t)sm.size();
                     const uint32_t p0 = j == 0 ? 0u : (lo[j] >= warm ? lo[j] - (uint32_t)warm : 0u);
                     sub_decode(rwin, p0, lo[j], lo[j + 1], lit, dist, LC, lsyms, DC, dsyms, o, sr[j]);
                     o.finish();
                     if (stats) { ++stats->sub_passes; stats->steps += sr[j].steps; }
                     pass_max = sr[j].steps > pass_max ? sr[j].steps : pass_max;
+                    for (size_t q = 0; q < sm.size(); ++q) wmarks[q] |= sm[q];
                 }
-                if (stats) stats->wave_steps += pass_max;
+                if (stats) {
+                    stats->wave_steps += pass_max;
+                    for (uint32_t q = 0; q < pass_max && q < wmarks.size(); ++q)
+                        for (int b = 0; b < 5; ++b) stats->prof[b] += (wmarks[q] >> b) & 1u;
+                    stats->prof[7] += pass_max;
+                }
                 // fix rounds: a sub-lane whose start is not its predecessor's exit decodes
                 // again from that exit (all such at once), until the chain holds
                 int v = 0, rounds = 0;
