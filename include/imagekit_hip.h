@@ -72,6 +72,13 @@ uint64_t ik_request_cost(const uint8_t *bytes, size_t len, int64_t w, int64_t h,
  * assign[i]; largest request first to the least-loaded device */
 void ik_schedule_plan(const uint64_t *costs, uint32_t n, uint32_t ndev, const uint64_t *outstanding,
                       uint32_t *assign);
+/* a batch submit's split over ndev logical devices on its own (no device work):
+ * min(ndev, n / min_batch) contiguous parts (at least one) -- part q is requests
+ * [part_lo[q], part_lo[q+1]) (part_lo: ndev + 1 entries) -- each placed in turn on
+ * the least-loaded device (part_dev[q]); returns the part count.  submit uses it
+ * with min_batch = IK_MIN_DEVICE_BATCH (64). */
+uint32_t ik_schedule_split(const uint64_t *costs, uint32_t n, uint32_t ndev, const uint64_t *outstanding,
+                           uint32_t min_batch, uint32_t *part_lo, uint32_t *part_dev);
 /* Orderly teardown: waits for every submitted batch, ends
  * the library's stage threads and worker pools (each releases its HIP streams
  * and arenas), then frees the pooled images, upload areas, resize plans and

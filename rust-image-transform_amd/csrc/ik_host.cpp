@@ -747,6 +747,14 @@ void ik_schedule_plan(const uint64_t* costs, uint32_t n, uint32_t ndev, const ui
     sched_plan(costs, n, ndev, outstanding, assign);
 }
 
+uint32_t ik_schedule_split(const uint64_t* costs, uint32_t n, uint32_t ndev, const uint64_t* outstanding,
+                           uint32_t min_batch, uint32_t* part_lo, uint32_t* part_dev) {
+    if (!costs || !part_lo || !part_dev || !ndev) return 0;
+    std::vector<uint64_t> out(ndev, 0);
+    if (outstanding) std::copy(outstanding, outstanding + ndev, out.begin());
+    return sched_split(costs, n, ndev, min_batch, out.data(), part_lo, part_dev);
+}
+
 int ik_image_from_host(const uint8_t* pixels, uint32_t width, uint32_t height, uint32_t channels,
                        ik_image** out) {
     IK_API_ENTER();
@@ -1939,12 +1947,16 @@ int submit_parts(const std::shared_ptr<Ticket>& t, const uint8_t* const* bytes, 
         if (p->logical < 0) return fail(IK_ERR_INVALID, "the inputs are on device %d, which serves no logical device", phys);
         parts.push_back(p);
     } else {
-        // whole parts of >= IK_MIN_DEVICE_BATCH requests, each to the least-loaded device
-        const int nd = sched_count();
-        const uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)nd, n / (uint32_t)min_device_batch()));
+        // whole parts of >= IK_MIN_DEVICE_BATCH requests (sched_split's bounds), each to the
+        // least-loaded device by the live counters
+        const uint32_t nd = (uint32_t)sched_count();
+        std::vector<uint64_t> costs(n), out(nd, 0);
+        for (uint32_t i = 0; i < n; ++i) costs[i] = cost_of(i);
+        std::vector<uint32_t> lo(nd + 1), dev(nd);
+        const uint32_t P = sched_split(costs.data(), n, nd, (uint32_t)min_device_batch(), out.data(), lo.data(), dev.data());
         for (uint32_t q = 0; q < P; ++q) {
-            auto p = make_part((uint32_t)((uint64_t)n * q / P), (uint32_t)((uint64_t)n * (q + 1) / P));
-            for (uint32_t i : p->hp.idx) p->cost += cost_of(i);
+            auto p = make_part(lo[q], lo[q + 1]);
+            for (uint32_t i : p->hp.idx) p->cost += costs[i];
             p->logical = sched_acquire(p->cost);
             parts.push_back(p);
         }

@@ -355,6 +355,27 @@ void sched_release(int ld, uint64_t cost) {
     L.cost_done += cost;
 }
 
+// A batch's split over nd logical devices: P = min(nd, n / min_batch) (at least 1)
+// contiguous parts of n/P requests (lo[0..P] their bounds), each placed in turn on
+// the device with the least outstanding cost (outstanding: nd entries, updated),
+// as submit_parts does with the live counters
+uint32_t sched_split(const uint64_t* costs, uint32_t n, uint32_t nd, uint32_t min_batch, uint64_t* outstanding,
+                     uint32_t* lo, uint32_t* dev) {
+    if (!nd || !n) return 0;
+    const uint32_t P = std::max<uint32_t>(1, std::min<uint32_t>(nd, n / std::max<uint32_t>(1, min_batch)));
+    for (uint32_t q = 0; q <= P; ++q) lo[q] = (uint32_t)((uint64_t)n * q / P);
+    for (uint32_t q = 0; q < P; ++q) {
+        uint64_t c = 0;
+        for (uint32_t i = lo[q]; i < lo[q + 1]; ++i) c += costs[i];
+        uint32_t best = 0;
+        for (uint32_t d = 1; d < nd; ++d)
+            if (outstanding[d] < outstanding[best]) best = d;
+        dev[q] = best;
+        outstanding[best] += c;
+    }
+    return P;
+}
+
 void sched_plan(const uint64_t* costs, uint32_t n, uint32_t ndev, const uint64_t* outstanding, uint32_t* assign) {
     // longest processing time first: the largest request goes to the least-loaded device
     std::vector<uint64_t> load(ndev, 0);

@@ -176,6 +176,8 @@ int sched_acquire_on(int phys, uint64_t cost);
 void sched_release(int logical, uint64_t cost);
 void sched_acquire_batch(const uint64_t* costs, uint32_t n, uint32_t* assign);
 void sched_plan(const uint64_t* costs, uint32_t n, uint32_t ndev, const uint64_t* outstanding, uint32_t* assign);
+uint32_t sched_split(const uint64_t* costs, uint32_t n, uint32_t nd, uint32_t min_batch, uint64_t* outstanding,
+                     uint32_t* lo, uint32_t* dev);
 int sched_stats(uint32_t logical, uint64_t* jobs, uint64_t* cost_done, uint64_t* outstanding);
 // header-only dimension sniff (PNG IHDR, JPEG SOFn, WebP VP8/VP8L/VP8X); c = bytes per pixel
 bool sniff_dims(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& c);

@@ -32,6 +32,7 @@ SIGNATURES = [
     ("ik_logical_device_stats", ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     ("ik_request_cost", ctypes.c_uint64, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int64, ctypes.c_int]),
     ("ik_schedule_plan", None, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
+    ("ik_schedule_split", ctypes.c_uint32, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     ("ik_last_error", ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_size_t]),
     ("ik_version", ctypes.c_char_p, []),
     ("ik_host_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),

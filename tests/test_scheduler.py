@@ -91,3 +91,40 @@ def test_every_request_is_placed_once(ndev):
 
 def test_multi_device_off_by_default():
     assert _lib.load().ik_logical_device_count() == 0
+
+
+def split(costs, ndev, min_batch=64, outstanding=None):
+    lib = _lib.load()
+    n = len(costs)
+    c = (ctypes.c_uint64 * n)(*costs)
+    o = (ctypes.c_uint64 * ndev)(*outstanding) if outstanding else None
+    lo = (ctypes.c_uint32 * (ndev + 1))()
+    dev = (ctypes.c_uint32 * ndev)()
+    P = lib.ik_schedule_split(c, n, ndev, o, min_batch, lo, dev)
+    return [(lo[q], lo[q + 1], dev[q]) for q in range(P)]
+
+
+def test_512_request_submit_spreads_over_8_devices():
+    """A 512-request submit (the driver's 8-GPU bench batch) goes to 8 logical
+    devices in parts of 64, one part each (ik_transform_batch_submit's split)."""
+    parts = split([1000] * 512, 8)
+    assert len(parts) == 8
+    assert [hi - lo for lo, hi, _ in parts] == [64] * 8
+    assert sorted(d for _, _, d in parts) == list(range(8))
+    assert parts[0][0] == 0 and parts[-1][1] == 512
+    assert all(parts[q][1] == parts[q + 1][0] for q in range(7))
+
+
+@pytest.mark.parametrize("n,ndev,want", [(100, 8, [100]), (130, 8, [65, 65]), (64, 8, [64]), (1000, 8, [125] * 8),
+                                         (63, 4, [63]), (512, 3, [170, 171, 171])])
+def test_parts_are_at_least_the_minimum(n, ndev, want):
+    parts = split([1] * n, ndev)
+    assert [hi - lo for lo, hi, _ in parts] == want
+    assert all(hi - lo >= min(64, n) for lo, hi, _ in parts)
+    assert len(set(d for _, _, d in parts)) == len(parts)  # idle devices first
+
+
+def test_split_respects_outstanding_work():
+    # devices 0..3 busy: the 4 parts of a 256-request submit go to devices 4..7
+    parts = split([10] * 256, 8, outstanding=[10**6] * 4 + [0] * 4)
+    assert sorted(d for _, _, d in parts) == [4, 5, 6, 7]
