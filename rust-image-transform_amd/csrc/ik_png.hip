@@ -1212,60 +1212,6 @@ __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const
             }
         unsigned long long m1 = __ballot(nm >= 1);
         const unsigned long long m2 = __ballot(nm >= 2);
-        // a match whose sources all lie before the batch (o - d + min(len, d) <= 0: in
-        // the ring, in memory, or before the lane) reads nothing this batch writes:
-        // those go first, eight at a time with all their loads in flight, and only the
-        // rest -- sources inside the batch -- one after another in token order
-        auto indep = [](uint32_t A, uint32_t d) {
-            const uint32_t o = A & 0xFFFFu, ln = A >> 16;
-            return ln != 0u && o + (ln < d ? ln : d) <= d;
-        };
-        const unsigned long long q0 = __ballot(nm >= 1 && indep(ma0, md0));
-        const unsigned long long q1 = __ballot(nm >= 2 && indep(ma1, md1));
-        // source value of position j of an independent match (A, d)
-        auto fetch = [&](uint32_t A, uint32_t d, uint32_t j) -> uint16_t {
-            const uint32_t o = A & 0xFFFFu;
-            const uint32_t jj = j < d ? j : j % d;  // (overlapping: the source repeats with period d)
-            const int32_t sr = (int32_t)o - (int32_t)d + (int32_t)jj;  // < 0: before the batch
-            const int64_t ab = cnt + sr;
-            const uint16_t vr = s_ring[(gb + (uint32_t)sr) & M];
-            const uint16_t vg = U[ob + (ab > 0 ? ab : 0)];
-            if (ab < -(int64_t)infl::kWindow) bad = true;
-            return ab < 0 ? (uint16_t)(0x8000u | (uint32_t)(infl::kWindow + ab)) : sr >= -kXNear ? vr : vg;
-        };
-        {
-            unsigned long long r0 = q0, r1 = q1;
-            while (r0 | r1) {
-                constexpr int G = 8;
-                uint32_t gA[G], gD[G];
-#pragma unroll
-                for (int k = 0; k < G; ++k) {
-                    gA[k] = 0;
-                    gD[k] = 1;
-                    if (r0) {
-                        const int l = __builtin_ctzll(r0);
-                        r0 &= r0 - 1ull;
-                        gA[k] = (uint32_t)__builtin_amdgcn_readlane((int)ma0, l);
-                        gD[k] = (uint32_t)__builtin_amdgcn_readlane((int)md0, l);
-                    } else if (r1) {
-                        const int l = __builtin_ctzll(r1);
-                        r1 &= r1 - 1ull;
-                        gA[k] = (uint32_t)__builtin_amdgcn_readlane((int)ma1, l);
-                        gD[k] = (uint32_t)__builtin_amdgcn_readlane((int)md1, l);
-                    }
-                }
-                uint16_t gv[G];
-#pragma unroll
-                for (int k = 0; k < G; ++k) gv[k] = (uint32_t)x < (gA[k] >> 16) ? fetch(gA[k], gD[k], (uint32_t)x) : 0;
-#pragma unroll
-                for (int k = 0; k < G; ++k)
-                    if ((uint32_t)x < (gA[k] >> 16)) s_ring[(gb + (gA[k] & 0xFFFFu) + (uint32_t)x) & M] = gv[k];
-#pragma unroll
-                for (int k = 0; k < G; ++k)
-                    for (uint32_t j = (uint32_t)x + 64u; j < (gA[k] >> 16); j += 64)  // (matches longer than 64)
-                        s_ring[(gb + (gA[k] & 0xFFFFu) + j) & M] = fetch(gA[k], gD[k], j);
-            }
-        }
         auto copy = [&](uint32_t A, uint32_t d) {
             const uint32_t o = A & 0xFFFFu, ln = A >> 16;
             const bool wrap = d < ln;  // overlapping: the source repeats with period d
@@ -1293,13 +1239,11 @@ __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const
                 s_ring[(gb + o + j) & M] = v;
             }
         };
-        m1 &= ~q0 | m2;  // (a lane whose both matches are independent has nothing left)
         while (m1) {
             const int l = __builtin_ctzll(m1);
             m1 &= m1 - 1ull;
-            if (!((q0 >> l) & 1ull))
-                copy((uint32_t)__builtin_amdgcn_readlane((int)ma0, l), (uint32_t)__builtin_amdgcn_readlane((int)md0, l));
-            if (((m2 & ~q1) >> l) & 1ull)
+            copy((uint32_t)__builtin_amdgcn_readlane((int)ma0, l), (uint32_t)__builtin_amdgcn_readlane((int)md0, l));
+            if ((m2 >> l) & 1ull)
                 copy((uint32_t)__builtin_amdgcn_readlane((int)ma1, l), (uint32_t)__builtin_amdgcn_readlane((int)md1, l));
         }
         // 3. ring -> memory, aligned groups of 4 positions
