@@ -38,6 +38,7 @@ struct PngImgDev {
     uint8_t* ft;             // filter type of every row
     uint8_t* dst;            // the image (pitched); filtered rows, then pixels in place
     size_t pitch;
+    const int* flags;        // the image's resolve flags: 1 bad filter type, 2 bad marker, 4 Average/Paeth rows
 };
 
 struct PngLaneDev {
@@ -112,6 +113,9 @@ hipError_t launch_copy_words(const uint32_t* src, uint32_t* dst, size_t n, hipSt
 #ifdef IK_UNF_PROF
 hipError_t png_unf_prof_read(unsigned long long* out);  // dev build: k_png_unfilter's segment clock sums (reset)
 #endif
+#ifdef IK_EXP_PROF
+hipError_t png_exp_prof_read(unsigned long long* out);  // dev build: k_png_expand8's phase clock sums (reset)
+#endif
 #ifdef IK_WAVE_PROF
 hipError_t png_wave_prof_read(unsigned long long* out);  // dev build: k_png_wave's phase clock sums (reset)
 #endif
@@ -144,6 +148,18 @@ hipError_t launch_png_units(const PngImgDev* imgs, const PngLaneDev* lanes, int 
 hipError_t launch_png_resolve(const PngImgDev* imgs, const int2* rows, int nrows, int* err, hipStream_t s);
 // groups[t] = (image, band group) of the workgroup holding ticket t; prog: one
 // zeroed counter per band (the image's at prog_base[image]); ticket: zeroed
+// The unfilter's scan path (k_png_unfilter_su): an RGBA8 image without Average /
+// Paeth rows (flags bit 4 clear) and at most kSuThreads * 4 chunks of 16 bytes a row
+// (4,096 pixels) is unfiltered by segments -- a None / Sub row and the Up rows under
+// it -- instead of the diagonal wavefront (the Up rows' only dependency is the row
+// above, byte for byte; a Sub row's is a prefix sum along the row).  k_png_unfilter
+// skips those images.
+constexpr int kSuThreads = 256, kSuChunks = 4, kSuRanges = 16;
+IK_HD bool png_unfilter_scan_path(int bpp, int rowbytes, int flags) {
+    return bpp == 4 && (rowbytes + 15) / 16 <= kSuThreads * kSuChunks && !(flags & 7);
+}
+// nimg images of one class (bpp 4): kSuRanges workgroups each
+hipError_t launch_png_unfilter_su(const PngImgDev* imgs, int nimg, hipStream_t s);
 hipError_t launch_png_unfilter(const PngImgDev* imgs, const int2* groups, int ngroups, const int* prog_base,
                                unsigned* prog, unsigned* ticket, int bpp, hipStream_t s);
 

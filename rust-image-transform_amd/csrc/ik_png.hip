@@ -9,10 +9,15 @@
 //                   the next lane's start -> the lane's token stream and output
 //                   length.  Code tables in LDS per thread (192 B), input through
 //                   an LDS ring filled by LDS-DMA (128 B per thread)
-//   k_png_expand4   one wave per verified lane: tokens -> u16 symbols (bytes,
-//                   window markers) at the lane's output offset, 256 tokens per
-//                   step, literals by a wave prefix sum, copies in token order;
-//                   status and clock ticks / 1024 per lane (status[2 t], [2 t + 1])
+//   k_png_wave      one wave per decoder lane of the wave decoder (ik_png_wave.h):
+//                   64 self-synchronising sub-lanes per block window -> token
+//                   pieces, their piece table and the lane's expand-unit records
+//   k_png_units     the expand units' offset, unit -> lane and page tables
+//   k_png_expand8   one wave per expand unit (or per lane of the lane decoder):
+//                   tokens -> u16 symbols (bytes, window markers) at the unit's
+//                   output offset, 512 tokens per step, literals by a wave prefix
+//                   sum, copies in token order; status and clock ticks / 1024 per
+//                   unit (status[2 t], [2 t + 1])
 //   k_png_resolve   u16 symbols -> the filtered bytes of every row, 16 per thread,
 //                   markers followed to their source; rows land 16-B aligned in
 //                   the destination image (pitched) and filter types in ft[]
@@ -1008,10 +1013,13 @@ using infl::kTokRaw;
 using infl::kTokTable;
 using infl::kTokTableLen;
 
-// Four tokens per thread (256 per batch) and the copies done in token order: on
-// image data ~96 % of the tokens are literals and a match is ~1 in 25 tokens,
-// so the batch costs a load, a prefix sum (DPP) and one LDS write per literal,
-// ~20 instructions per match, and a coalesced ring -> memory copy.
+// Eight tokens per thread (512 per batch: the batch's fixed costs -- ballots, the
+// prefix sum, the ring copy, the barrier -- over twice the tokens of four) and the
+// copies done in token order: on the bench frames 98.7 % of the tokens are
+// literals and a match (~6 bytes, 97 % of them more than kXNear back) is ~1 in
+// 75 tokens, so the batch costs a 16-byte load per thread, a prefix sum (DPP), a
+// branch-free classification and one LDS write per literal, ~20 instructions and
+// one load per match, and a coalesced ring -> memory copy.
 //   1. the literals of the batch go to the LDS ring (indexed by absolute symbol
 //      position) at their offsets;
 //   2. the matches, in token order, each by the whole wave: a position of the
@@ -1023,17 +1031,32 @@ using infl::kTokTableLen;
 //      (8-byte stores; a group's 1-3 positions before the batch are rewritten
 //      with the same values, its positions after the batch -- stale ring data --
 //      are rewritten by the next batch; groups are clipped to the lane's output).
-constexpr uint32_t kX4Tok = 256;
+constexpr uint32_t kX8Tok = 512;  // tokens per batch: 8 per thread
 constexpr int kXPieces = 192;  // piece-table entries staged in LDS (a unit of one 18 KiB block has ~130)
 
-__global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const PngLaneDev* lanes, int nlanes,
+#ifdef IK_EXP_PROF  // dev build: k_png_expand8's phase clock sums (tools/dev_png experiments)
+__device__ unsigned long long g_exp_prof[8];
+hipError_t png_exp_prof_read(unsigned long long* out) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp_prof), sizeof(g_exp_prof));
+    unsigned long long z[8] = {};
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_exp_prof), z, sizeof(z));
+    return e;
+}
+#define IK_XP(k) do { const uint64_t _t = clock64(); xprof[k] += _t - xt; xt = _t; } while (0)
+#else
+#define IK_XP(k) ((void)0)
+#endif
+
+template <bool TAB>
+__global__ __launch_bounds__(64) void k_png_expand8(const PngImgDev* imgs, const PngLaneDev* lanes, int nlanes,
                                                     const uint16_t* tok, int* status, const uint2* pieces,
                                                     const uint2* units, const uint32_t* ulane) {
     raise_priority();
     __shared__ __attribute__((aligned(16))) uint16_t s_ring[kXRing];  // recent output, by absolute position
-    __shared__ uint32_t s_tab[64];                                      // the block's literal table
+    __shared__ uint32_t s_tab[TAB ? 64 : 1];                            // the block's literal table (TAB)
     __shared__ uint32_t s_pb[kXPieces], s_ps[kXPieces];                 // wave decoder lanes: piece table
     constexpr uint32_t M = kXRing - 1;
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     const int li = blockIdx.x;  // lane, or expand unit
     if (li >= nlanes) return;
     const int x = threadIdx.x;
@@ -1066,7 +1089,7 @@ __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const
         oe = L.obase + (int64_t)r1.y;
     }
     // the unit's first kXPieces entries staged in LDS; past them, memory.  Each thread
-    // keeps the piece of its last token (its index only grows: a window is 256
+    // keeps the piece of its last token (its index only grows: a window is 512
     // tokens, a piece tens to hundreds), so a load walks a step or two at most
     if (np) {
         for (uint32_t k = (uint32_t)x; pf + k < np && k < (uint32_t)kXPieces; k += 64) {
@@ -1085,133 +1108,147 @@ __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const
     uint32_t t = t0;
     int64_t cnt = 0;
     bool have_tab = false, bad = false;
-    // this thread's 4 tokens of the batch window at a (a multiple of 4; the region
-    // is 16-byte aligned and padded past ntok to a multiple of 8 tokens)
-    auto load4 = [&](uint32_t a) -> uint64_t {
-        const uint32_t i = a + 4u * (uint32_t)x;
-        if (i >= ntok) return 0xFFFEFFFEFFFEFFFEull;
-        if (!np) return *(const IK_GLOBAL uint64_t*)(T + i);
+    // this thread's 8 tokens of the batch window at a (a multiple of 8, so one
+    // 16-byte load that never straddles two pieces; the region is 16-byte aligned
+    // and padded past ntok to a multiple of 8 tokens)
+    auto load8 = [&](uint32_t a) -> u4 {
+        const uint32_t i = a + 8u * (uint32_t)x;
+        if (i >= ntok) return u4{0xFFFEFFFEu, 0xFFFEFFFEu, 0xFFFEFFFEu, 0xFFFEFFFEu};
+        if (!np) return *(const IK_GLOBAL u4*)(T + i);
         while (i >= pn_start) {
             ++kc;
             pc_base = piece_base(kc);
             pc_start = pn_start;
             pn_start = kc + 1 < np ? piece_start(kc + 1) : 0xFFFFFFFFu;
         }
-        return *(const IK_GLOBAL uint64_t*)(T + pc_base + (i - pc_start));
+        return *(const IK_GLOBAL u4*)(T + pc_base + (i - pc_start));
     };
-    uint64_t w = load4(t0);
+    u4 w = load8(t0 & ~7u);
+#ifdef IK_EXP_PROF
+    uint64_t xprof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, xt = clock64();
+#endif
     while (t < ntok) {
-        const uint32_t a = t & ~3u, i0 = a + 4u * (uint32_t)x;
-        uint32_t u[4];
+        IK_XP(5);
+        const uint32_t a = t & ~7u, i0 = a + 8u * (uint32_t)x;
+        uint32_t u[8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) u[k] = (uint32_t)(w >> (16 * k)) & 0xFFFFu;
-        // the first table record at or after t in the window
-        int ft = 4;
+        for (int k = 0; k < 4; ++k) {
+            u[2 * k] = w[k] & 0xFFFFu;
+            u[2 * k + 1] = w[k] >> 16;
+        }
+        IK_XP(6);
+        uint32_t end = a + kX8Tok < ntok ? a + kX8Tok : ntok;
+        if constexpr (TAB) {
+            // the first table record at or after t in the window
+            int ft = 8;
 #pragma unroll
-        for (int k = 3; k >= 0; --k)
-            if (i0 + k >= t && i0 + k < ntok && u[k] == kTokTable) ft = k;
-        const unsigned long long tl = __ballot(ft < 4);
-        uint32_t end = a + kX4Tok < ntok ? a + kX4Tok : ntok;
-        if (tl) {
-            const int l = __builtin_ctzll(tl);
-            const uint32_t e = a + 4u * (uint32_t)l + (uint32_t)__builtin_amdgcn_readlane(ft, l);
-            if (e == t) {  // the table: the literal table -> LDS
-                const uint32_t tt = (t + 8) & ~7u;
-                if (tt + kTokTableLen > ntok) { bad = true; break; }
-                s_tab[x] = ((const IK_GLOBAL uint32_t*)(T + tt))[x];
-                have_tab = true;
-                t = tt + kTokTableLen;
-                w = load4(t & ~3u);
-                __syncthreads();
-                continue;
+            for (int k = 7; k >= 0; --k)
+                if (i0 + k >= t && i0 + k < ntok && u[k] == kTokTable) ft = k;
+            const unsigned long long tl = __ballot(ft < 8);
+            if (tl) {
+                const int l = __builtin_ctzll(tl);
+                const uint32_t e = a + 8u * (uint32_t)l + (uint32_t)__builtin_amdgcn_readlane(ft, l);
+                if (e == t) {  // the table: the literal table -> LDS
+                    const uint32_t tt = (t + 8) & ~7u;
+                    if (tt + kTokTableLen > ntok) { bad = true; break; }
+                    s_tab[x] = ((const IK_GLOBAL uint32_t*)(T + tt))[x];
+                    have_tab = true;
+                    t = tt + kTokTableLen;
+                    w = load8(t & ~7u);
+                    __syncthreads();
+                    continue;
+                }
+                end = e;
             }
-            end = e;
         }
         // a match's first token last: its distance is in the next window
         {
             const uint32_t q = end - 1u;
-            const bool mine = q >= t && (q >> 2) == (i0 >> 2);
-            const uint32_t uq = (uint32_t)(w >> (16 * (q & 3u))) & 0xFFFFu;
+            const bool mine = q >= t && (q >> 3) == (i0 >> 3);
+            const uint32_t wq = w[(q >> 1) & 3u];
+            const uint32_t uq = (q & 1u) ? wq >> 16 : wq & 0xFFFFu;
             if (__ballot(mine && (uq & 0xFF00u) == kTokMatch)) --end;
         }
         if (end <= t) { bad = true; break; }
         // the token after each slot (a match's distance) and before slot 0
         const uint32_t nx = (uint32_t)__shfl_down((int)u[0], 1, 64);
-        const uint32_t pv = (uint32_t)__shfl_up((int)u[3], 1, 64);
-        uint32_t len[4], val[4];
-        bool lit[4];
+        const uint32_t pv = (uint32_t)__shfl_up((int)u[7], 1, 64);
+        // classify (no branches): a literal, a match's length token (its distance is
+        // the next token), the distance token itself, padding; bad: anything else
+        uint32_t len[8], val[8], lit = 0;  // lit: bit k = slot k is a literal
+        uint32_t bd = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < 8; ++k) {
             const uint32_t idx = i0 + k;
-            const uint32_t prev = k ? u[k - 1] : pv;
-            const bool valid = idx >= t && idx < end;
-            const bool dist_tok = idx > t && (prev & 0xFF00u) == kTokMatch;
-            const bool start = valid && !dist_tok;
+            const uint32_t prev = k ? u[k - 1] : pv, nxt = k < 7 ? u[k + 1] : nx;
             const uint32_t v = u[k];
-            len[k] = 0;
-            val[k] = 0;
-            lit[k] = false;
-            if (start) {
-                if (v < 256u) {
-                    if (!have_tab) bad = true;
-                    len[k] = 1;
-                    lit[k] = true;
-                    val[k] = (s_tab[v >> 2] >> (8 * (v & 3u))) & 0xFFu;
-                } else if ((v & 0xFF00u) == kTokRaw) {
-                    len[k] = 1;
-                    lit[k] = true;
-                    val[k] = v & 0xFFu;
-                } else if ((v & 0xFF00u) == kTokMatch) {
-                    len[k] = (v & 0xFFu) + 3u;
-                    val[k] = (k < 3 ? u[k + 1] : nx) + 1u;  // the distance
-                } else if (v != kTokPad) {  // (padding of a wave decoder's piece: no symbol)
-                    bad = true;
-                }
+            const bool start = (idx >= t) & (idx < end) & !((idx > t) & ((prev & 0xFF00u) == kTokMatch));
+            const bool raw = (v & 0xFF00u) == kTokRaw, mt = (v & 0xFF00u) == kTokMatch, pad = v == kTokPad;
+            const bool rk = TAB && v < 256u;  // (the lane decoder's Huffman-literal rank)
+            const bool isl = raw | rk;
+            len[k] = !start ? 0u : isl ? 1u : mt ? (v & 0xFFu) + 3u : 0u;
+            uint32_t lv = v & 0xFFu;
+            if constexpr (TAB) {
+                if (start & rk) lv = (s_tab[v >> 2] >> (8 * (v & 3u))) & 0xFFu;
+                bd |= (uint32_t)(start & rk & !have_tab);
             }
+            val[k] = isl ? lv : nxt + 1u;  // a literal's byte, or the match's distance
+            lit |= (uint32_t)isl << k;
+            bd |= (uint32_t)(start & !(isl | mt | pad));
         }
-        if (__ballot(bad)) { bad = true; break; }
-        uint32_t off[4], tot;
+        if (__ballot(bd != 0u)) { bad = true; break; }
+        uint32_t off[8], tot;
         for (;;) {
-            const uint32_t sum = len[0] + len[1] + len[2] + len[3];
+            uint32_t sum = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) sum += len[k];
             const uint32_t incl = wave_incl_scan_dpp(sum);
             tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
             off[0] = incl - sum;
-            off[1] = off[0] + len[0];
-            off[2] = off[1] + len[1];
-            off[3] = off[2] + len[2];
+#pragma unroll
+            for (int k = 1; k < 8; ++k) off[k] = off[k - 1] + len[k - 1];
             if (tot <= (uint32_t)kXCap) break;
             // cut the batch before the first symbol that does not fit (one always does)
-            int fk = 4;
+            int fk = 8;
 #pragma unroll
-            for (int k = 3; k >= 0; --k)
+            for (int k = 7; k >= 0; --k)
                 if (len[k] && off[k] + len[k] > (uint32_t)kXCap) fk = k;
-            const unsigned long long ov = __ballot(fk < 4);
+            const unsigned long long ov = __ballot(fk < 8);
             const int l = __builtin_ctzll(ov);
-            end = a + 4u * (uint32_t)l + (uint32_t)__builtin_amdgcn_readlane(fk, l);
+            end = a + 8u * (uint32_t)l + (uint32_t)__builtin_amdgcn_readlane(fk, l);
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
+            for (int k = 0; k < 8; ++k)
                 if (i0 + k >= end) len[k] = 0;
         }
+        IK_XP(1);
         // the next window's tokens, in flight while this batch is written
         const uint32_t t2 = end;
-        const uint64_t wn = t2 < ntok ? load4(t2 & ~3u) : 0ull;
+        const u4 wn = t2 < ntok ? load8(t2 & ~7u) : u4{0, 0, 0, 0};
         const uint32_t gb = (uint32_t)(ob + cnt);  // ring index base (absolute position, low bits)
         // 1. literals
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (len[k] && lit[k]) s_ring[(gb + off[k]) & M] = (uint16_t)val[k];
-        // 2. matches in token order (a thread holds at most two)
-        uint32_t ma0 = 0, ma1 = 0, md0 = 0, md1 = 0;
-        int nm = 0;
+        for (int k = 0; k < 8; ++k)
+            if (len[k] && ((lit >> k) & 1u)) s_ring[(gb + off[k]) & M] = (uint16_t)val[k];
+        // 2. matches in token order (a thread holds at most four), by selects
+        uint32_t ma[4] = {0, 0, 0, 0}, md[4] = {0, 0, 0, 0};
+        uint32_t nm = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (len[k] && !lit[k]) {
-                if (nm == 0) { ma0 = off[k] | (len[k] << 16); md0 = val[k]; }
-                else { ma1 = off[k] | (len[k] << 16); md1 = val[k]; }
-                ++nm;
+        for (int k = 0; k < 8; ++k) {
+            const bool m = len[k] && !((lit >> k) & 1u);
+            const uint32_t A = off[k] | (len[k] << 16);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                ma[q] = m && nm == (uint32_t)q ? A : ma[q];
+                md[q] = m && nm == (uint32_t)q ? val[k] : md[q];
             }
+            nm += m ? 1u : 0u;
+        }
+        IK_XP(2);
+#ifdef IK_EXP_PROF
+        xprof[7] += 1;
+#endif
         unsigned long long m1 = __ballot(nm >= 1);
-        const unsigned long long m2 = __ballot(nm >= 2);
+        const unsigned long long m2 = __ballot(nm >= 2), m3 = __ballot(nm >= 3), m4 = __ballot(nm >= 4);
         auto copy = [&](uint32_t A, uint32_t d) {
             const uint32_t o = A & 0xFFFFu, ln = A >> 16;
             const bool wrap = d < ln;  // overlapping: the source repeats with period d
@@ -1242,10 +1279,15 @@ __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const
         while (m1) {
             const int l = __builtin_ctzll(m1);
             m1 &= m1 - 1ull;
-            copy((uint32_t)__builtin_amdgcn_readlane((int)ma0, l), (uint32_t)__builtin_amdgcn_readlane((int)md0, l));
+            copy((uint32_t)__builtin_amdgcn_readlane((int)ma[0], l), (uint32_t)__builtin_amdgcn_readlane((int)md[0], l));
             if ((m2 >> l) & 1ull)
-                copy((uint32_t)__builtin_amdgcn_readlane((int)ma1, l), (uint32_t)__builtin_amdgcn_readlane((int)md1, l));
+                copy((uint32_t)__builtin_amdgcn_readlane((int)ma[1], l), (uint32_t)__builtin_amdgcn_readlane((int)md[1], l));
+            if ((m3 >> l) & 1ull)
+                copy((uint32_t)__builtin_amdgcn_readlane((int)ma[2], l), (uint32_t)__builtin_amdgcn_readlane((int)md[2], l));
+            if ((m4 >> l) & 1ull)
+                copy((uint32_t)__builtin_amdgcn_readlane((int)ma[3], l), (uint32_t)__builtin_amdgcn_readlane((int)md[3], l));
         }
+        IK_XP(3);
         // 3. ring -> memory, aligned groups of 4 positions
         {
             const int64_t s0 = ob + cnt, s1 = s0 + tot, cb = s0 & ~3ll;
@@ -1263,6 +1305,7 @@ __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const
             }
         }
         __syncthreads();
+        IK_XP(4);
         cnt += tot;
         t = t2;
         w = wn;
@@ -1271,6 +1314,10 @@ __global__ __launch_bounds__(64) void k_png_expand4(const PngImgDev* imgs, const
     if (x == 0) {
         status[2 * li] = (!bad && cnt == oe - ob) ? 0 : -1;
         status[2 * li + 1] = (int)((clock64() - c0) >> 10);  // profile: clock ticks / 1024
+#ifdef IK_EXP_PROF
+        xprof[0] = clock64() - c0;
+        for (int k = 0; k < 8; ++k) atomicAdd(&g_exp_prof[k], (unsigned long long)xprof[k]);
+#endif
     }
 }
 
@@ -1325,6 +1372,7 @@ __global__ __launch_bounds__(256) void k_png_resolve(const PngImgDev* imgs, cons
         const int v = infl::resolve_at(I.u16, I.obase, I.nlanes, I.page_lane, kPngPageShift, rs);
         I.ft[y] = (uint8_t)(v < 0 ? 255 : v);
         if (v < 0 || v > 4) atomicOr(err + ir.x, 1);
+        else if (v >= 3) atomicOr(err + ir.x, 4);  // (Average / Paeth: the unfilter's diagonal path)
     }
     // (global address space: global_* ops, counted in vmcnt only, not flat_*)
     IK_GLOBAL uint8_t* const drow = (IK_GLOBAL uint8_t*)(I.dst + (size_t)y * I.pitch);
@@ -1490,6 +1538,7 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngI
     __syncthreads();
     const int2 gk = groups[s_t];  // (image, workgroup of the image)
     const PngImgDev I = imgs[gk.x];
+    if (png_unfilter_scan_path(BPP, I.rowbytes, *(const volatile int*)I.flags)) return;  // (k_png_unfilter_su's)
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int nch = (I.rowbytes + 15) >> 4;
     const int nbands = (I.H + 63) >> 6;
@@ -1612,6 +1661,91 @@ __global__ __launch_bounds__(kPngUnfilterThreads) void k_png_unfilter(const PngI
         atomicAdd(&g_unf_prof[7], 1ull);
     }
 #endif
+}
+
+// ---- unfilter, scan path ----------------------------------------------------------
+// RGBA8 images of None / Sub / Up rows only (png_unfilter_scan_path): a segment is a
+// None or Sub row (or row 0) and the Up rows under it; segments are independent.
+// kSuRanges workgroups per image, workgroup j taking the segments that start in its
+// slice of rows (and following each to its end, past the slice if need be).  A
+// thread owns 4 consecutive 16-byte chunks (16 pixels) of the row: an Up row adds
+// the row above byte-wise (kept in registers), a Sub row is a byte-wise prefix sum
+// per channel -- 4-byte pixels, so one SWAR word per pixel: in the thread, across
+// the wave (DPP), across the workgroup's 4 waves (LDS).
+__device__ __forceinline__ uint32_t add_bytes(uint32_t a, uint32_t b) {  // four independent mod-256 sums
+    return ((a & 0x7F7F7F7Fu) + (b & 0x7F7F7F7Fu)) ^ ((a ^ b) & 0x80808080u);
+}
+__device__ __forceinline__ uint32_t wave_scan_bytes(uint32_t v) {  // inclusive, add_bytes
+    v = add_bytes(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true));  // row_shr:1
+    v = add_bytes(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true));  // row_shr:2
+    v = add_bytes(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true));  // row_shr:4
+    v = add_bytes(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true));  // row_shr:8
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+    const uint32_t r1 = add_bytes(r0, (uint32_t)__builtin_amdgcn_readlane((int)v, 31));
+    const uint32_t r2 = add_bytes(r1, (uint32_t)__builtin_amdgcn_readlane((int)v, 47));
+    const int row = (int)(threadIdx.x & 63) >> 4;
+    return add_bytes(v, row == 0 ? 0u : row == 1 ? r0 : row == 2 ? r1 : r2);
+}
+
+__global__ __launch_bounds__(kSuThreads) void k_png_unfilter_su(const PngImgDev* imgs, int nimg) {
+    raise_priority();
+    __shared__ uint32_t s_w[kSuThreads / 64];
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const int im = (int)blockIdx.x / kSuRanges, jr = (int)blockIdx.x % kSuRanges;
+    if (im >= nimg) return;
+    const PngImgDev I = imgs[im];
+    if (!png_unfilter_scan_path(4, I.rowbytes, *(const volatile int*)I.flags)) return;
+    const int H = I.H, nch = (I.rowbytes + 15) >> 4;
+    const int tid = threadIdx.x, wv = tid >> 6;
+    const int c0 = tid * kSuChunks;  // this thread's first chunk
+    const int y1 = (int)((int64_t)H * (jr + 1) / kSuRanges);
+    int y = (int)((int64_t)H * jr / kSuRanges);
+    const IK_GLOBAL uint8_t* ft = (const IK_GLOBAL uint8_t*)I.ft;
+    while (y < y1 && y != 0 && ft[y] > 1) ++y;  // (rows of a segment that started above belong to its workgroup)
+    while (y < y1) {
+        uint32_t prev[4 * kSuChunks];
+#pragma unroll
+        for (int k = 0; k < 4 * kSuChunks; ++k) prev[k] = 0;
+        int r = y;
+        do {
+            const uint32_t f = ft[r];
+            IK_GLOBAL uint8_t* row = (IK_GLOBAL uint8_t*)(I.dst + (size_t)r * I.pitch);
+            uint32_t w[4 * kSuChunks];
+#pragma unroll
+            for (int i = 0; i < kSuChunks; ++i) {
+                const u4 v = c0 + i < nch ? *(const IK_GLOBAL u4*)(row + 16 * (c0 + i)) : u4{0, 0, 0, 0};
+                w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+            }
+            if (f == 2) {
+#pragma unroll
+                for (int k = 0; k < 4 * kSuChunks; ++k) w[k] = add_bytes(w[k], prev[k]);
+            } else if (f == 1) {  // (uniform: the whole workgroup reads the same filter type)
+#pragma unroll
+                for (int k = 1; k < 4 * kSuChunks; ++k) w[k] = add_bytes(w[k], w[k - 1]);
+                const uint32_t incl = wave_scan_bytes(w[4 * kSuChunks - 1]);
+                uint32_t carry = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x138, 0xF, 0xF, true);  // wave_shr:1
+                if ((tid & 63) == 63) s_w[wv] = incl;
+                __syncthreads();
+                for (int q = 0; q < wv; ++q) carry = add_bytes(carry, s_w[q]);
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < 4 * kSuChunks; ++k) w[k] = add_bytes(w[k], carry);
+            }
+#pragma unroll
+            for (int i = 0; i < kSuChunks; ++i)
+                if (c0 + i < nch) *(IK_GLOBAL u4*)(row + 16 * (c0 + i)) = u4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+#pragma unroll
+            for (int k = 0; k < 4 * kSuChunks; ++k) prev[k] = w[k];
+            ++r;
+        } while (r < H && ft[r] == 2);
+        y = r;
+    }
+}
+
+hipError_t launch_png_unfilter_su(const PngImgDev* imgs, int nimg, hipStream_t s) {
+    if (nimg <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_png_unfilter_su, dim3(nimg * kSuRanges), dim3(kSuThreads), 0, s, imgs, nimg);
+    return hipGetLastError();
 }
 
 // ---- small transfers through the compute queue ---------------------------------------
@@ -1934,7 +2068,11 @@ hipError_t launch_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int
                              hipStream_t s, const uint2* pieces, const uint2* units, const uint32_t* ulane) {
     if (n <= 0) return hipSuccess;
     if ((units != nullptr) != (ulane != nullptr) || (units && !pieces)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_png_expand4, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status, pieces, units, ulane);
+    // (the lane decoder's tokens may carry literal tables; the wave decoder's never do)
+    if (pieces)
+        hipLaunchKernelGGL(k_png_expand8<false>, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status, pieces, units, ulane);
+    else
+        hipLaunchKernelGGL(k_png_expand8<true>, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status, pieces, units, ulane);
     return hipGetLastError();
 }
 

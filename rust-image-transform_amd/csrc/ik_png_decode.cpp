@@ -1250,6 +1250,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             npg += (j.raw_total >> kPngPageShift) + 1;
             hd[k].dst = j.expand ? j.rows->d : j.img->d;
             hd[k].pitch = j.expand ? j.rows->pitch : j.img->pitch;
+            hd[k].flags = reinterpret_cast<const int*>(dev + o_err) + k;
             for (size_t i = 0; i < ob.size(); ++i) tim[12] += (double)j.lanes.res[i].ntok;
             for (size_t i = 0; i < ob.size(); ++i) {
                 PngLaneDev L{};
@@ -1387,6 +1388,9 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                         const int g0 = ranges[r].grp0, i0 = ranges[r].img0;
                         e3 = launch_png_unfilter(d_cls + i0, d_groups + g0, g1 - g0, d_pbase + i0, d_prog,
                                                  d_ticket + r, ranges[r].bpp, s);
+                        // (RGBA8 images of None / Sub / Up rows: the scan path; each kernel skips the other's)
+                        const int i1 = r + 1 < ranges.size() ? ranges[r + 1].img0 : (int)cls.size();
+                        if (e3 == hipSuccess && ranges[r].bpp == 4) e3 = launch_png_unfilter_su(d_cls + i0, i1 - i0, s);
                     }
                 }
                 // png's EXPAND for the palette / low-bit / tRNS images
@@ -1400,6 +1404,17 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                     e3 = launch_png_px(j.px, s);
                 }
                 rec(7, s);
+#ifdef IK_EXP_PROF
+                {
+                    (void)hipStreamSynchronize(s);
+                    unsigned long long pf[8] = {};
+                    if (png_exp_prof_read(pf) == hipSuccess && pf[0])
+                        fprintf(stderr, "[exp-prof] waves %zu: kcycles/wave %.0f: token wait %.0f, scan %.0f, literals %.0f, "
+                                "matches %.0f, stores+sync %.0f, loop %.0f; batches/wave %.1f\n", nexp,
+                                pf[0] / 1024.0 / nexp, pf[6] / 1024.0 / nexp, pf[1] / 1024.0 / nexp, pf[2] / 1024.0 / nexp,
+                                pf[3] / 1024.0 / nexp, pf[4] / 1024.0 / nexp, pf[5] / 1024.0 / nexp, (double)pf[7] / nexp);
+                }
+#endif
 #ifdef IK_UNF_PROF
                 {
                     (void)hipStreamSynchronize(s);
@@ -1425,7 +1440,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                 for (int k = 0; k < m; ++k) {
                     PngJob& j = *J[k];
                     if (j.state != 1) continue;
-                    const bool rows_ok = herr[k] == 0;
+                    const bool rows_ok = (herr[k] & 3) == 0;  // (bit 4: Average / Paeth rows, not an error)
                     bool lanes_ok = true;
                     for (size_t i = 0; i < j.lanes.start.size(); ++i) {
                         const uint32_t nu = wavedec ? j.lanes.res[i].units : 1u;  // expand waves of this lane

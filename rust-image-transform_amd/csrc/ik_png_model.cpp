@@ -325,6 +325,24 @@ int ikm_inflate_wave(const uint8_t* z, size_t zlen, size_t chunk_bytes, uint8_t*
             }
             stats[13] += cat.size();
             stats[17] += 1;
+            for (size_t q = 0; q + 1 < cat.size(); ++q) {  // match profile: near (<= 1024 back) / far, their lengths
+                const uint32_t v = cat[q];
+                if ((v & 0xFF00u) != infl::kTokMatch) continue;
+                const uint32_t len = (v & 255u) + 3, d = (uint32_t)cat[q + 1] + 1;
+                stats[d <= 1024 ? 18 : 19] += 1;
+                if (getenv("IKM_PROF")) {
+                    static uint64_t hist[8] = {0};
+                    hist[d <= 4 ? 0 : d <= 64 ? 1 : d <= 1024 ? 2 : d <= 16384 ? 3 : d <= 16388 ? 4 : 5] += 1;
+                    hist[6] += len;
+                    hist[7] += 1;
+                    if ((hist[7] & ((1u << 16) - 1)) == 0)
+                        fprintf(stderr, "[model] matches %llu: d<=4 %llu, <=64 %llu, <=1024 %llu, <=16384 %llu, 16385-16388 %llu, "
+                                "farther %llu; mean length %.1f\n", (unsigned long long)hist[7], (unsigned long long)hist[0],
+                                (unsigned long long)hist[1], (unsigned long long)hist[2], (unsigned long long)hist[3],
+                                (unsigned long long)hist[4], (unsigned long long)hist[5], (double)hist[6] / hist[7]);
+                }
+                ++q;
+            }
             cat.resize(cat.size() + 16, (uint16_t)infl::kTokPad);
             infl::TokInHost tin{cat.data()};
             const int64_t ob = obase[i] + (int64_t)o0;

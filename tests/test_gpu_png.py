@@ -66,7 +66,7 @@ def own_png(img, level=6, strategy=zlib.Z_DEFAULT_STRATEGY, filters=None, idat_s
     prev = np.zeros(w * c, np.int32)
     for y in range(h):
         cur = img[y].reshape(-1).astype(np.int32)
-        ft = (y % 5) if filters is None else filters
+        ft = (y % 5) if filters is None else filters if isinstance(filters, int) else int(filters[y])
         a = np.concatenate([np.zeros(c, np.int32), cur[:-c]])
         b = prev
         cc = np.concatenate([np.zeros(c, np.int32), prev[:-c]])
@@ -162,6 +162,32 @@ def test_batch_tall_band_groups(on_gpu):
     shapes = [(300, 2500, 4), (517, 1100, 3), (64, 4100, 1), (1000, 1090, 4), (211, 3333, 2), (90, 2049, 4)]
     imgs = [ikutil.synth(w, h, c, seed=50 + k, pattern="N" if k % 2 else "S") for k, (w, h, c) in enumerate(shapes)]
     datas = [own_png(im, idat_size=65536) for im in imgs]
+    out = decode_image_batch(datas)
+    for (d, fmt), im in zip(out, imgs):
+        np.testing.assert_array_equal(d.to_array().reshape(im.shape), im)
+
+
+def test_unfilter_scan_path_batch(on_gpu):
+    """k_png_unfilter_su (RGBA8 images of None / Sub / Up rows: segments of a None
+    or Sub row and the Up rows under it) beside the diagonal kernel in one batch:
+    Up runs crossing the workgroups' row slices, an image that is one segment (Up
+    from row 0), Sub-only and None-only images, the widest scan-path row (4,096
+    pixels: 1,024 chunks) and one pixel wider (diagonal), and images with Average /
+    Paeth rows (diagonal)."""
+    rnd = np.random.default_rng(5)
+    cases = [
+        ((4096, 300, 4), rnd.choice([1, 2, 2, 2, 2, 2, 2, 0], 300)),
+        ((1000, 2000, 4), np.where(rnd.random(2000) < 0.02, 1, 2)),
+        ((777, 1500, 4), np.full(1500, 2)),
+        ((512, 700, 4), np.full(700, 1)),
+        ((333, 257, 4), np.full(257, 0)),
+        ((4097, 64, 4), rnd.choice([1, 2], 64)),
+        ((640, 900, 4), rnd.choice([1, 2, 3, 4], 900)),
+        ((901, 333, 3), rnd.choice([1, 2], 333)),
+        ((1234, 1111, 4), np.concatenate([np.full(1110, 2), [4]])),
+    ]
+    imgs = [ikutil.synth(w, h, c, seed=70 + k, pattern="N" if k % 2 else "S") for k, ((w, h, c), _) in enumerate(cases)]
+    datas = [own_png(im, filters=f, idat_size=65536) for im, (_, f) in zip(imgs, cases)]
     out = decode_image_batch(datas)
     for (d, fmt), im in zip(out, imgs):
         np.testing.assert_array_equal(d.to_array().reshape(im.shape), im)
