@@ -246,6 +246,10 @@ hipStream_t thread_stream() {
     return s;
 }
 
+// The upload stream (PCIe copies of whole batches: 2.25 GB on the bench, ~42 ms)
+// at the lowest stream priority: a stream of another priority never shares its
+// hardware queue, so no kernel of another stage waits in queue order behind a
+// batch's DMA (GPU_MAX_HW_QUEUES is 4: same-priority streams share queues).
 hipStream_t thread_copy_stream() {
     ThreadRes& r = tres();
     const int d = current_device();
@@ -253,7 +257,14 @@ hipStream_t thread_copy_stream() {
     if (it != r.copy_streams.end()) return it->second;
     (void)hipSetDevice(d);
     hipStream_t s = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
+    // (the priority other than the default one: the lowest if it is not the default)
+    const int prio = least != 0 ? least : greatest;
+    if (getenv("IK_TIMING")) fprintf(stderr, "[streams] priority range %d..%d: upload stream at %d\n", least, greatest, prio);
+    if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio) != hipSuccess &&
+        hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess)
+        return nullptr;
     r.copy_streams[d] = s;
     return s;
 }

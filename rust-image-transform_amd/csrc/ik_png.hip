@@ -1229,26 +1229,18 @@ __global__ __launch_bounds__(64) void k_png_expand8(const PngImgDev* imgs, const
 #pragma unroll
         for (int k = 0; k < 8; ++k)
             if (len[k] && ((lit >> k) & 1u)) s_ring[(gb + off[k]) & M] = (uint16_t)val[k];
-        // 2. matches in token order (a thread holds at most four), by selects
-        uint32_t ma[4] = {0, 0, 0, 0}, md[4] = {0, 0, 0, 0};
-        uint32_t nm = 0;
+        // 2. matches in token order: slot k of lane l is a match start iff bit l of
+        // mk[k]; lane by lane, its slots in order, each copy by the whole wave
+        unsigned long long mk[8], any = 0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const bool m = len[k] && !((lit >> k) & 1u);
-            const uint32_t A = off[k] | (len[k] << 16);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                ma[q] = m && nm == (uint32_t)q ? A : ma[q];
-                md[q] = m && nm == (uint32_t)q ? val[k] : md[q];
-            }
-            nm += m ? 1u : 0u;
+            mk[k] = __ballot(len[k] != 0u && !((lit >> k) & 1u));
+            any |= mk[k];
         }
         IK_XP(2);
 #ifdef IK_EXP_PROF
         xprof[7] += 1;
 #endif
-        unsigned long long m1 = __ballot(nm >= 1);
-        const unsigned long long m2 = __ballot(nm >= 2), m3 = __ballot(nm >= 3), m4 = __ballot(nm >= 4);
         auto copy = [&](uint32_t A, uint32_t d) {
             const uint32_t o = A & 0xFFFFu, ln = A >> 16;
             const bool wrap = d < ln;  // overlapping: the source repeats with period d
@@ -1276,16 +1268,14 @@ __global__ __launch_bounds__(64) void k_png_expand8(const PngImgDev* imgs, const
                 s_ring[(gb + o + j) & M] = v;
             }
         };
-        while (m1) {
-            const int l = __builtin_ctzll(m1);
-            m1 &= m1 - 1ull;
-            copy((uint32_t)__builtin_amdgcn_readlane((int)ma[0], l), (uint32_t)__builtin_amdgcn_readlane((int)md[0], l));
-            if ((m2 >> l) & 1ull)
-                copy((uint32_t)__builtin_amdgcn_readlane((int)ma[1], l), (uint32_t)__builtin_amdgcn_readlane((int)md[1], l));
-            if ((m3 >> l) & 1ull)
-                copy((uint32_t)__builtin_amdgcn_readlane((int)ma[2], l), (uint32_t)__builtin_amdgcn_readlane((int)md[2], l));
-            if ((m4 >> l) & 1ull)
-                copy((uint32_t)__builtin_amdgcn_readlane((int)ma[3], l), (uint32_t)__builtin_amdgcn_readlane((int)md[3], l));
+        while (any) {
+            const int l = __builtin_ctzll(any);
+            any &= any - 1ull;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if ((mk[k] >> l) & 1ull)
+                    copy((uint32_t)__builtin_amdgcn_readlane((int)(off[k] | (len[k] << 16)), l),
+                         (uint32_t)__builtin_amdgcn_readlane((int)val[k], l));
         }
         IK_XP(3);
         // 3. ring -> memory, aligned groups of 4 positions

@@ -273,6 +273,8 @@ struct Xfer {
     hipError_t h2d(void* dev, const void* host, size_t n) {
         if (!n) return hipSuccess;
         const size_t o = take(n + 4);
+        if (o == ~size_t(0) && getenv("IK_TIMING"))
+            fprintf(stderr, "[png] transfer area full: a %zu-byte copy takes the copy engine\n", n);
         if (o == ~size_t(0))  // (more decode rounds than the area was sized for) the copy engine
             return copy_h2d_2d(reinterpret_cast<uint8_t*>(dev), n, reinterpret_cast<const uint8_t*>(host), n, n, 1, s)
                        ? hipErrorUnknown : hipSuccess;
@@ -311,6 +313,8 @@ struct Xfer {
             if (e == hipSuccess) std::memcpy(host, pin + o, n & ~size_t(3));
             done = n & ~size_t(3);
         }
+        if (o == ~size_t(0) && getenv("IK_TIMING"))
+            fprintf(stderr, "[png] transfer area full: a %zu-byte copy takes the copy engine\n", n);
         if (e == hipSuccess && done < n) {  // a tail under one word, or no room: the copy engine
             e = hipMemcpyAsync(reinterpret_cast<uint8_t*>(host) + done, reinterpret_cast<const uint8_t*>(dev) + done,
                                n - done, hipMemcpyDeviceToHost, s);
@@ -925,9 +929,16 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             d_tok = reinterpret_cast<uint16_t*>(dev + o);
         }
         uint64_t tok_used = 0;
+        // the small transfers go through the pinned area by copy kernels on this stream:
+        // one that falls back to the copy engine queues behind the next batch's PCIe
+        // upload (2.25 GB on the bench) and stalls this kernel stage for its length.
+        // The expand units' status (2 ints each): a unit holds kUnitMinTok tokens or
+        // ends its lane
+        const size_t max_units = wavedec ? (size_t)(tok_total / wave::kUnitMinTok) + max_lanes + 16 : 0;
         Xfer X;
         if (!rc && !X.init(2 * sizeof(PngLaneDev) * max_lanes + sizeof(infl::LaneResult) * max_lanes +
                                sizeof(int64_t) * (max_lanes + nchunks) + 3 * sizeof(int) * max_lanes +
+                               2 * sizeof(int) * max_units +
                                sizeof(int2) * (nrows + ngroups) + sizeof(int) * (npages + 4 * m) +
                                3 * sizeof(PngImgDev) * m + 2 * sizeof(int) * nchunks + (64u << 10), s))
             rc = fail(IK_ERR_NOMEM, "cannot allocate pinned PNG transfer area");

@@ -435,7 +435,10 @@ struct Stats {
 // the lane's current unit holds fewer than kUnitMinTok tokens (short blocks share a
 // unit).  Unit record k of a lane, at the lane's piece-table slot k (a lane has no
 // more units than pieces): (its first piece, the lane's output bytes before it).
-constexpr uint32_t kUnitMinTok = 16384;
+#ifndef IK_UNIT_MIN_TOK
+#define IK_UNIT_MIN_TOK 16384
+#endif
+constexpr uint32_t kUnitMinTok = IK_UNIT_MIN_TOK;
 IK_HD bool unit_starts(uint32_t nunits, uint64_t written, uint64_t unit_v0) {
     return nunits == 0 || written - unit_v0 >= kUnitMinTok;
 }
