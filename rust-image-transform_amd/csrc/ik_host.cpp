@@ -1789,7 +1789,7 @@ private:
                 // hardware queue measured 63-69 vs 61-62 ms per step (the search took
                 // resolve from 3.6 to 13-19 ms; profiles/r03n_find_*.json).
                 if (!png_upload_landed(nx->up)) return;
-                hipStream_t fs = thread_stream();
+                hipStream_t fs = png_find_beside_decode() ? thread_copy_stream() : thread_stream();
                 if (after && hipStreamWaitEvent(fs, after, 0) != hipSuccess) return;
                 png_find_prelaunch(nx->up, fs);
             };

@@ -598,6 +598,19 @@ __device__ bool wave_code_build(const uint8_t* lens, int n, bool is_dist, bool f
     return true;
 }
 
+#ifdef IK_WAVE_PROF  // dev build: k_png_wave's phase clock sums (tools/dev_png experiments)
+__device__ unsigned long long g_wave_prof[8];
+hipError_t png_wave_prof_read(unsigned long long* out) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_prof), sizeof(g_wave_prof));
+    unsigned long long z[8] = {};
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_wave_prof), z, sizeof(z));
+    return e;
+}
+#define IK_WP(k, t0) (wprof[k] += clock64() - (t0))
+#else
+#define IK_WP(k, t0) ((void)0)
+#endif
+
 // The block's codes by the wave: a dynamic header's code-length code (lanes 0..18
 // take one length each) and its 7-bit decode table, then the literal/length and
 // distance code lengths, then both codes (wave_code_build).  Checks as
@@ -676,12 +689,26 @@ __device__ bool wave_block_codes(const IK_GLOBAL uint32_t* W, uint64_t nbits, ui
         }
     }
     // the literal/length and distance code lengths (the distance lengths to lens[288 ..])
+#ifdef IK_WAVE_PROF
+    const uint64_t tl0 = clock64();
+#endif
     uint32_t o = o0 + 14 + 3 * (uint32_t)ncode;
     const int total = nlen + ndist;
     int i = 0, prev = -1;
     bool ok = true;
+    // a wave-uniform 64-bit bit buffer (scalar registers): refilled a word at a time
+    // when under 32 bits remain (a symbol takes at most 7 + 7), so a symbol costs one
+    // table v_readlane and scalar arithmetic
+    uint32_t wn = (o >> 5) + 2u;
+    uint64_t buf = (((uint64_t)word((o >> 5) + 1u) << 32) | word(o >> 5)) >> (o & 31u);
+    uint32_t nb = 64u - (o & 31u);
     while (i < total) {
-        const uint32_t v = bits32(o);
+        if (nb < 32u) {
+            buf |= (uint64_t)word(wn) << nb;
+            nb += 32u;
+            ++wn;
+        }
+        const uint32_t v = (uint32_t)buf;
         const uint32_t e7 = v & 127u;
         const uint32_t ent = ((uint32_t)__builtin_amdgcn_readlane((int)tab, (int)(e7 & 63u)) >> (8u * (e7 >> 6))) & 255u;
         const uint32_t L = ent >> 5, sym = ent & 31u;
@@ -708,10 +735,15 @@ __device__ bool wave_block_codes(const IK_GLOBAL uint32_t* W, uint64_t nbits, ui
         }
         i += rep;
         prev = val;
+        buf >>= L + xb;
+        nb -= L + xb;
         o += L + xb;
         if (o > 160 * 32 - 96) { ok = false; break; }  // past any valid header
     }
     __syncthreads();  // the lengths are in LDS
+#ifdef IK_WAVE_PROF
+    if (lane == 0) atomicAdd(&g_wave_prof[6], (unsigned long long)(clock64() - tl0));
+#endif
     if (!ok || lens[256] == 0) return false;  // (no end-of-block code: invalid)
     *body = hb0 + o;
     if (*body > nbits) return false;
@@ -721,18 +753,6 @@ __device__ bool wave_block_codes(const IK_GLOBAL uint32_t* W, uint64_t nbits, ui
     return a && b;
 }
 
-#ifdef IK_WAVE_PROF  // dev build: k_png_wave's phase clock sums (tools/dev_png experiments)
-__device__ unsigned long long g_wave_prof[8];
-hipError_t png_wave_prof_read(unsigned long long* out) {
-    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_prof), sizeof(g_wave_prof));
-    unsigned long long z[8] = {};
-    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_wave_prof), z, sizeof(z));
-    return e;
-}
-#define IK_WP(k, t0) (wprof[k] += clock64() - (t0))
-#else
-#define IK_WP(k, t0) ((void)0)
-#endif
 
 __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const PngLaneDev* lanes, const uint32_t* order,
                                                  int nlanes, uint16_t* tok, uint2* pieces, uint2* units,
@@ -844,7 +864,11 @@ __global__ __launch_bounds__(64) void k_png_wave(const PngImgDev* imgs, const Pn
                 }
                 lc.info = (const lds_u32*)s_code[0].info;
                 dc.info = (const lds_u32*)s_code[1].info;
+                // (unrolled: the entries' dependent LDS reads -- per-length info, then the
+                // symbol -- of several entries in flight at once)
+#pragma unroll 4
                 for (uint32_t e = (uint32_t)lane; e < (1u << wave::kLB); e += 64) s_lit[e] = wave::lit_table_entry(e, lc, lsym);
+#pragma unroll
                 for (uint32_t e = (uint32_t)lane; e < (1u << wave::kDB); e += 64) s_dist[e] = wave::dist_table_entry(e, dc, dsym);
             }
             __syncthreads();
@@ -1356,9 +1380,14 @@ __global__ __launch_bounds__(256) void k_png_resolve(const PngImgDev* imgs, cons
     const PngImgDev I = imgs[ir.x];
     const int y = ir.y;
     const int64_t rs = (int64_t)y * (I.rowbytes + 1);  // filter byte of row y
+    __shared__ int64_t s_hlo, s_hhi;  // the output range of the unit holding the row's first symbol
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
     if (threadIdx.x == 0) {
+        int hl = I.page_lane[rs >> kPngPageShift];
+        while (hl + 1 < I.nlanes && I.obase[hl + 1] <= rs) ++hl;
+        s_hlo = I.obase[hl];
+        s_hhi = hl + 1 < I.nlanes ? I.obase[hl + 1] : INT64_MAX;
         const int v = infl::resolve_at(I.u16, I.obase, I.nlanes, I.page_lane, kPngPageShift, rs);
         I.ft[y] = (uint8_t)(v < 0 ? 255 : v);
         if (v < 0 || v > 4) atomicOr(err + ir.x, 1);
@@ -1413,9 +1442,20 @@ __global__ __launch_bounds__(256) void k_png_resolve(const PngImgDev* imgs, cons
     }
     __syncthreads();  // (also orders the chunk stores before the marker bytes below)
     const uint32_t cnt = s_cnt < (uint32_t)kResolveList ? s_cnt : (uint32_t)kResolveList;
+    const int64_t hlo = s_hlo, hhi = s_hhi;
     for (uint32_t m = threadIdx.x; m < cnt; m += 256) {
         const uint32_t x = s_pos[m];
-        const int rv = infl::resolve_at(I.u16, I.obase, I.nlanes, I.page_lane, kPngPageShift, rs + 1 + (int64_t)x);
+        // the first hop: a marker in the row's first unit resolves against its offset
+        // without the page-table walk (then the general walk, from the source)
+        const int64_t q = rs + 1 + (int64_t)x;
+        int rv;
+        if (q >= hlo && q < hhi) {
+            const uint32_t mv = I.u16[q];
+            const int64_t q2 = hlo - infl::kWindow + (int64_t)(mv & 0x7FFFu);
+            rv = (mv & 0x8000u) && q2 >= 0 ? infl::resolve_at(I.u16, I.obase, I.nlanes, I.page_lane, kPngPageShift, q2) : -1;
+        } else {
+            rv = infl::resolve_at(I.u16, I.obase, I.nlanes, I.page_lane, kPngPageShift, q);
+        }
         if (rv < 0) atomicOr(err + ir.x, 2);
         drow[x] = (uint8_t)rv;
     }

@@ -530,6 +530,11 @@ struct PngBatchState {
 // 64 self-synchronising sub-lanes over shared lookup tables) by default;
 // IK_PNG_DECODE=lane selects round 4's one-thread-per-lane canonical decoder
 // (k_png_decode, token streams with literal tables) for A/B runs.
+bool png_find_beside_decode() {
+    static const bool v = getenv("IK_FIND_BESIDE") != nullptr;
+    return v;
+}
+
 static bool png_wave_decoder() {
     static const bool v = [] {
         const char* e = getenv("IK_PNG_DECODE");
@@ -1150,6 +1155,12 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             hres.resize(hl.size());
             if (!mk[0]) mk[0] = now_ms();  // plan built, lanes uploaded (first round)
             rec(2, s);
+            // (IK_FIND_BESIDE: the next batch's block search beside this decode, on another queue)
+            if (!search_done && png_find_beside_decode() && up.on_next_search && ev.ok) {
+                (void)hipEventRecord(ev.e[11], s);
+                up.on_next_search(ev.e[11]);
+                search_done = true;
+            }
             hipError_t e2 = wavedec ? launch_png_wave(d_imgs, d_lanes, ordered ? d_order : nullptr, (int)hl.size(), d_tok,
                                                       d_pieces, d_units, d_res, s)
                                     : launch_png_decode(d_imgs, d_lanes, ordered ? d_order : nullptr, (int)hl.size(), d_tok,
@@ -1172,8 +1183,9 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             if (wavedec) {
                 unsigned long long pf[8] = {};
                 if (png_wave_prof_read(pf) == hipSuccess && pf[7])
-                    fprintf(stderr, "[wave-prof] lanes %llu: kcycles/lane total %.0f, codes %.0f, tables %.0f, staging %.0f, "
-                            "first passes %.0f, fix rounds %.0f, rest %.0f\n", pf[7], pf[0] / 1024.0 / pf[7],
+                    fprintf(stderr, "[wave-prof] lanes %llu: kcycles/lane total %.0f, codes %.0f (lengths %.0f), tables %.0f, "
+                            "staging %.0f, first passes %.0f, fix rounds %.0f, rest %.0f\n", pf[7], pf[0] / 1024.0 / pf[7],
+                            pf[6] / 1024.0 / pf[7],
                             pf[1] / 1024.0 / pf[7], pf[2] / 1024.0 / pf[7], pf[3] / 1024.0 / pf[7], pf[4] / 1024.0 / pf[7],
                             pf[5] / 1024.0 / pf[7],
                             ((double)pf[0] - pf[1] - pf[2] - pf[3] - pf[4] - pf[5]) / 1024.0 / pf[7]);

@@ -290,6 +290,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
 // the block search of an issued upload, on stream s (after the upload lands);
 // png_decode_finish then only waits for it.  Kernel-stage thread only.
 void png_find_prelaunch(PngUpload& up, hipStream_t s);
+bool png_find_beside_decode();  // IK_FIND_BESIDE: the next batch's block search beside the decode (experiment)
 bool png_upload_landed(const PngUpload& up);  // its upload + gather pass have completed (nothing to wait for)
 constexpr int kPngTimingFields = 17;  // ik_png_last_timing
 // caller-pinned host memory (ik_host_alloc / ik_host_register): [p, p + n) lies
