@@ -359,6 +359,16 @@ struct WinLds {
     // that store are done -- the ring's DMA from the last tick among them -- and
     // issue the block three ahead.  Between ticks the loop issues no memory
     // instruction, so the count in the wait is exact.
+    // Why these hand-counted waits are safe (round 3's unfilter bug was
+    // asm loads whose destination VGPRs the register allocator copied before the
+    // asm wait): a global_load_lds_dword has no destination VGPR -- the data goes
+    // to LDS at M0 -- so there is no register for the allocator to copy early, and
+    // the ring words are read only by ds_read after the wait.  The only vector-
+    // memory instructions between two ticks are this tick's st stores (issued
+    // after the DMAs, gfx9 counts stores in vmcnt and retires the counter in
+    // issue order), so vmcnt(st) leaves exactly them outstanding and every DMA of
+    // the previous tick complete.  The wave decoder (the default, k_png_wave)
+    // stages its windows with plain loads and LDS stores the compiler waits for.
     __device__ void tick(infl::TokOut& o) {
         if (++it % kRingTick) return;
         const int st = o.flush();  // 0, 1 or 2 stores for this lane; the wave issued as many as its max
@@ -1056,6 +1066,7 @@ using infl::kTokTableLen;
 //      with the same values, its positions after the batch -- stale ring data --
 //      are rewritten by the next batch; groups are clipped to the lane's output).
 constexpr uint32_t kX8Tok = 512;  // tokens per batch: 8 per thread
+constexpr int kXFar = 64;          // far matches a batch copies flattened (more: one by one)
 constexpr int kXPieces = 192;  // piece-table entries staged in LDS (a unit of one 18 KiB block has ~130)
 
 #ifdef IK_EXP_PROF  // dev build: k_png_expand8's phase clock sums (tools/dev_png experiments)
@@ -1079,6 +1090,7 @@ __global__ __launch_bounds__(64) void k_png_expand8(const PngImgDev* imgs, const
     __shared__ __attribute__((aligned(16))) uint16_t s_ring[kXRing];  // recent output, by absolute position
     __shared__ uint32_t s_tab[TAB ? 64 : 1];                            // the block's literal table (TAB)
     __shared__ uint32_t s_pb[kXPieces], s_ps[kXPieces];                 // wave decoder lanes: piece table
+    __shared__ uint32_t s_fo[kXFar], s_fd[kXFar], s_fc[kXFar];          // the batch's far matches (offset, distance, start)
     constexpr uint32_t M = kXRing - 1;
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     const int li = blockIdx.x;  // lane, or expand unit
@@ -1253,12 +1265,56 @@ __global__ __launch_bounds__(64) void k_png_expand8(const PngImgDev* imgs, const
 #pragma unroll
         for (int k = 0; k < 8; ++k)
             if (len[k] && ((lit >> k) & 1u)) s_ring[(gb + off[k]) & M] = (uint16_t)val[k];
-        // 2. matches in token order: slot k of lane l is a match start iff bit l of
-        // mk[k]; lane by lane, its slots in order, each copy by the whole wave
+        // 2. matches.  A far match (distance > kXNear, so more than the batch's 1,024
+        // positions: every source lies before the batch) reads nothing the batch
+        // writes: the far matches -- nearly all of them on image data (rows above) --
+        // are flattened into one list of positions and copied by all lanes at once, a
+        // position per lane (up to 64 of them, listed in LDS by a prefix sum over the
+        // lanes); the rest, in token order, each by the whole wave.  (One copy after
+        // another, the wave's per-match control -- lane and slot search, readlanes,
+        // the loop -- was ~400 scalar instructions per batch, and the CU's one scalar
+        // unit bounded the kernel.)
+        uint32_t fcnt = 0, flen = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const bool fk = len[k] != 0u && !((lit >> k) & 1u) && val[k] > (uint32_t)kXNear;
+            fcnt += fk ? 1u : 0u;
+            flen += fk ? len[k] : 0u;
+        }
+        const uint32_t fp = fcnt | (flen << 16), fincl = wave_incl_scan_dpp(fp);
+        const uint32_t ftot = (uint32_t)__builtin_amdgcn_readlane((int)fincl, 63);
+        const uint32_t F = ftot & 0xFFFFu, FT = ftot >> 16;  // far matches, their positions
+        const bool flat = F != 0u && F <= (uint32_t)kXFar;
+        if (flat) {
+            uint32_t ri = (fincl - fp) & 0xFFFFu, rc = (fincl - fp) >> 16;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const bool fk = len[k] != 0u && !((lit >> k) & 1u) && val[k] > (uint32_t)kXNear;
+                if (fk) {
+                    s_fo[ri] = off[k];
+                    s_fd[ri] = val[k];
+                    s_fc[ri] = rc;
+                    ++ri;
+                    rc += len[k];
+                }
+            }
+            __syncthreads();  // (one wave: orders the list's writes before its reads)
+            for (uint32_t j = (uint32_t)x; j < FT; j += 64) {
+                uint32_t m = 0;  // the match holding flattened position j: the last with start <= j
+                for (uint32_t q = 1; q < F; ++q) m = s_fc[q] <= j ? q : m;
+                const uint32_t o = s_fo[m], d = s_fd[m], jj = j - s_fc[m];
+                const int32_t sr = (int32_t)(o + jj) - (int32_t)d;  // < -kXNear + ...: before the batch
+                const int64_t ab = cnt + sr;
+                if (ab < -(int64_t)infl::kWindow) bad = true;
+                const uint16_t v = ab < 0 ? (uint16_t)(0x8000u | (uint32_t)(infl::kWindow + ab))
+                                          : sr >= -kXNear ? s_ring[(gb + (uint32_t)sr) & M] : U[ob + ab];
+                s_ring[(gb + o + jj) & M] = v;
+            }
+        }
         unsigned long long mk[8], any = 0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            mk[k] = __ballot(len[k] != 0u && !((lit >> k) & 1u));
+            mk[k] = __ballot(len[k] != 0u && !((lit >> k) & 1u) && !(flat && val[k] > (uint32_t)kXNear));
             any |= mk[k];
         }
         IK_XP(2);
