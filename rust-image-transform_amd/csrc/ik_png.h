@@ -127,12 +127,23 @@ hipError_t launch_png_find(const PngImgDev* imgs, const int* chunk_img, const in
 // order (nullable): launch slot -> lane index; lane t's result goes to res[t]
 hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, const uint32_t* order, int n,
                              uint16_t* tok, infl::LaneResult* res, hipStream_t s);
+// The direct-rows expand (the wave decoder's default): expand writes the image's
+// rows and filter types itself and lists the window markers (image << 40 | raw
+// position) here; k_png_marks resolves them, k_png_ftflags checks the filter types.
+// count > cap: the list overflowed -- the batch then takes k_png_resolve after all.
+constexpr uint32_t kMarkLists = 256;  // sub-lists (unit % kMarkLists), cap / kMarkLists entries each
+struct PngMarks {
+    uint64_t* list = nullptr;  // nullptr: expand writes only the u16 symbols (k_png_resolve's input)
+    uint32_t* count = nullptr; // kMarkLists counters
+    uint32_t cap = 0;          // entries over all sub-lists
+};
+hipError_t launch_png_marks(const PngImgDev* imgs, PngMarks mk, const int2* rows, int nrows, int* err, hipStream_t s);
 // expand: one wave per lane (units == nullptr; n lanes), or -- the wave decoder's
 // lanes -- one wave per expand unit (n units; unit u of lane ulane[u], its record at
 // units[lanes[l].pbase + u - lanes[l].ubase]); status: 2 ints per lane / unit
 hipError_t launch_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int n, const uint16_t* tok, int* status,
                              hipStream_t s, const uint2* pieces = nullptr, const uint2* units = nullptr,
-                             const uint32_t* ulane = nullptr);
+                             const uint32_t* ulane = nullptr, PngMarks mk = PngMarks());
 // the wave decoder (ik_png_wave.h): one wave per lane; pieces: (token base in the
 // lane's region, first index in its virtual token stream) per piece, a table of
 // lanes[t].npieces entries at lanes[t].pbase; units: the lane's expand-unit

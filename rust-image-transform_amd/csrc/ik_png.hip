@@ -1085,7 +1085,7 @@ hipError_t png_exp_prof_read(unsigned long long* out) {
 template <bool TAB>
 __global__ __launch_bounds__(64) void k_png_expand8(const PngImgDev* imgs, const PngLaneDev* lanes, int nlanes,
                                                     const uint16_t* tok, int* status, const uint2* pieces,
-                                                    const uint2* units, const uint32_t* ulane) {
+                                                    const uint2* units, const uint32_t* ulane, PngMarks mk_out) {
     raise_priority();
     __shared__ __attribute__((aligned(16))) uint16_t s_ring[kXRing];  // recent output, by absolute position
     __shared__ uint32_t s_tab[TAB ? 64 : 1];                            // the block's literal table (TAB)
@@ -1374,6 +1374,42 @@ __global__ __launch_bounds__(64) void k_png_expand8(const PngImgDev* imgs, const
                 }
             }
         }
+        // 3b. (mk_out.list: the rows directly) the batch's bytes into the image rows
+        // (position p of the raw stream is row p / RB, column p % RB: column 0 the
+        // filter byte -> ft[], the rest -> dst), its window markers onto the batch's
+        // marker list for k_png_marks -- so no pass reads the u16 symbols back whole
+        if (mk_out.list) {
+            const int64_t RB = (int64_t)I.rowbytes + 1, s0 = ob + cnt;
+            const int64_t y0 = s0 / RB;
+            int64_t y = y0, c = s0 - y0 * RB + x;
+            while (c >= RB) { c -= RB; ++y; }
+            uint32_t mm = 0;  // bit i: position s0 + x + 64 i holds a marker (or an invalid symbol)
+            for (uint32_t i = 0, q = (uint32_t)x; q < tot; ++i, q += 64) {
+                const uint32_t v = s_ring[(uint32_t)(s0 + q) & M];
+                if (v >= 256u) mm |= 1u << i;
+                else if (c == 0) I.ft[y] = (uint8_t)v;
+                else ((IK_GLOBAL uint8_t*)I.dst)[(size_t)y * I.pitch + (size_t)(c - 1)] = (uint8_t)v;
+                c += 64;
+                while (c >= RB) { c -= RB; ++y; }
+            }
+            const uint32_t nmk = (uint32_t)__builtin_popcount(mm), incl = wave_incl_scan_dpp(nmk);
+            const uint32_t tot_mk = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            if (tot_mk) {
+                // one of kMarkLists sub-lists by unit (one counter per list: a single
+                // counter for the whole batch serialised ~8 M atomics on one address)
+                const uint32_t sl = (uint32_t)li % kMarkLists, scap = mk_out.cap / kMarkLists;
+                uint32_t base = 0;
+                if (x == 63) base = atomicAdd(mk_out.count + sl, tot_mk);
+                base = (uint32_t)__builtin_amdgcn_readlane((int)base, 63) + incl - nmk;
+                IK_GLOBAL uint64_t* const out = (IK_GLOBAL uint64_t*)(mk_out.list + (size_t)sl * scap);
+                while (mm) {
+                    const uint32_t i = (uint32_t)__builtin_ctz(mm);
+                    mm &= mm - 1u;
+                    if (base < scap) out[base] = ((uint64_t)L.img << 40) | (uint64_t)(s0 + x + 64 * i);
+                    ++base;
+                }
+            }
+        }
         __syncthreads();
         IK_XP(4);
         cnt += tot;
@@ -1414,6 +1450,43 @@ __global__ __launch_bounds__(256) void k_png_units(const PngImgDev* imgs, const 
         for (int64_t pg = (o + P - 1) >> kPngPageShift; (pg << kPngPageShift) < oe; ++pg) pages[pg] = (int)(base + b);
         o = oe;
     }
+}
+
+// ---- window markers of the direct-rows expand -----------------------------------
+// One thread per listed marker (a grid-stride loop: the count is on the device):
+// its value followed through the earlier units (infl::resolve_at over the u16
+// symbols, which expand still writes), into the row or the filter type.  Then one
+// thread per row checks the filter types (png's error for > 4; bit 4: Average /
+// Paeth rows, the unfilter's diagonal path).
+__global__ __launch_bounds__(256) void k_png_marks(const PngImgDev* imgs, PngMarks mk, int* err) {
+    // workgroups in kMarkLists groups, group g taking sub-list g % kMarkLists
+    const uint32_t sl = blockIdx.x % kMarkLists, part = blockIdx.x / kMarkLists, parts = gridDim.x / kMarkLists;
+    const uint32_t scap = mk.cap / kMarkLists, c = mk.count[sl];
+    const uint32_t n = c < scap ? c : scap;
+    const uint64_t* list = mk.list + (size_t)sl * scap;
+    for (uint32_t i = part * 256 + threadIdx.x; i < n; i += parts * 256) {
+        const uint64_t e = list[i];
+        const int k = (int)(e >> 40);
+        const int64_t pos = (int64_t)(e & ((1ull << 40) - 1));
+        const PngImgDev I = imgs[k];
+        const int v = infl::resolve_at(I.u16, I.obase, I.nlanes, I.page_lane, kPngPageShift, pos);
+        if (v < 0) {
+            atomicOr(err + k, 2);
+            continue;
+        }
+        const int64_t RB = (int64_t)I.rowbytes + 1, y = pos / RB, c = pos - y * RB;
+        if (c == 0) I.ft[y] = (uint8_t)v;
+        else ((IK_GLOBAL uint8_t*)I.dst)[(size_t)y * I.pitch + (size_t)(c - 1)] = (uint8_t)v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_png_ftflags(const PngImgDev* imgs, const int2* rows, int nrows, int* err) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= nrows) return;
+    const int2 ir = rows[r];
+    const uint32_t v = imgs[ir.x].ft[ir.y];
+    if (v > 4) atomicOr(err + ir.x, 1);
+    else if (v >= 3) atomicOr(err + ir.x, 4);
 }
 
 // ---- resolve ------------------------------------------------------------------------
@@ -2150,15 +2223,22 @@ hipError_t launch_png_decode(const PngImgDev* imgs, const PngLaneDev* lanes, con
     return hipGetLastError();
 }
 
+hipError_t launch_png_marks(const PngImgDev* imgs, PngMarks mk, const int2* rows, int nrows, int* err, hipStream_t s) {
+    hipLaunchKernelGGL(k_png_marks, dim3(8 * kMarkLists), dim3(256), 0, s, imgs, mk, err);
+    if (nrows > 0) hipLaunchKernelGGL(k_png_ftflags, dim3((nrows + 255) / 256), dim3(256), 0, s, imgs, rows, nrows, err);
+    return hipGetLastError();
+}
+
 hipError_t launch_png_expand(const PngImgDev* imgs, const PngLaneDev* lanes, int n, const uint16_t* tok, int* status,
-                             hipStream_t s, const uint2* pieces, const uint2* units, const uint32_t* ulane) {
+                             hipStream_t s, const uint2* pieces, const uint2* units, const uint32_t* ulane, PngMarks mk) {
     if (n <= 0) return hipSuccess;
     if ((units != nullptr) != (ulane != nullptr) || (units && !pieces)) return hipErrorInvalidValue;
+    if (mk.list && !pieces) return hipErrorInvalidValue;  // (the direct rows: the wave decoder's tokens only)
     // (the lane decoder's tokens may carry literal tables; the wave decoder's never do)
     if (pieces)
-        hipLaunchKernelGGL(k_png_expand8<false>, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status, pieces, units, ulane);
+        hipLaunchKernelGGL(k_png_expand8<false>, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status, pieces, units, ulane, mk);
     else
-        hipLaunchKernelGGL(k_png_expand8<true>, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status, pieces, units, ulane);
+        hipLaunchKernelGGL(k_png_expand8<true>, dim3(n), dim3(64), 0, s, imgs, lanes, n, tok, status, pieces, units, ulane, mk);
     return hipGetLastError();
 }
 

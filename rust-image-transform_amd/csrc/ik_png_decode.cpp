@@ -530,6 +530,17 @@ struct PngBatchState {
 // 64 self-synchronising sub-lanes over shared lookup tables) by default;
 // IK_PNG_DECODE=lane selects round 4's one-thread-per-lane canonical decoder
 // (k_png_decode, token streams with literal tables) for A/B runs.
+// The direct-rows expand (IK_PNG_DIRECT=1: expand writes the rows and filter types
+// itself and lists the window markers for k_png_marks, so no pass reads the u16
+// symbols back whole).  Measured slower on the bench frames and not the default:
+// their 164 M markers per 64 frames (3.8 % of the bytes, near every unit start) cost
+// expand 3.9 ms of list writes and byte stores and k_png_marks 3.1 ms, against the
+// resolve pass's 4.3 ms (profiles/r05_ab_notes.md).
+static bool png_direct_rows() {
+    static const bool v = getenv("IK_PNG_DIRECT") != nullptr;
+    return v;
+}
+
 bool png_find_beside_decode() {
     static const bool v = getenv("IK_FIND_BESIDE") != nullptr;
     return v;
@@ -1300,9 +1311,18 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
         int64_t* d_uob = nullptr;
         uint32_t* d_ulane = nullptr;
         int* d_uxst = nullptr;
+        // and the direct-rows expand's marker list (png_direct_rows): a slot per 16 output bytes
+        PngMarks marks;
         if (!rc && wavedec && nunits) {
+            uint64_t raw_sum = 0;
+            for (const auto& q : pj) raw_sum += J[q.first]->raw_total;
+            // (at least 64 K entries per sub-list: a small batch's few units each take one)
+            const uint64_t mcap =
+                png_direct_rows() ? std::min<uint64_t>(std::max<uint64_t>(raw_sum / 16, 65536ull * kMarkLists), 0xFFFFFF00ull) : 0;
             const size_t b0 = up256(sizeof(int64_t) * nunits), b1 = up256(sizeof(uint32_t) * nunits);
-            uint8_t* ua = scratch_slot(5, b0 + b1 + up256(2 * sizeof(int) * nunits));
+            const size_t b2 = up256(2 * sizeof(int) * nunits),
+                         b3 = mcap ? up256(sizeof(uint32_t) * kMarkLists) + up256(sizeof(uint64_t) * mcap) : 0;
+            uint8_t* ua = scratch_slot(5, b0 + b1 + b2 + b3);
             if (!ua) {
                 rc = fail(IK_ERR_DEVICE, "cannot allocate the PNG expand-unit tables (%u units)", nunits);
             } else {
@@ -1310,6 +1330,11 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                 d_ulane = reinterpret_cast<uint32_t*>(ua + b0);
                 d_uxst = reinterpret_cast<int*>(ua + b0 + b1);
                 for (const auto& q : pj) hd[q.first].obase = d_uob + uimg[q.first];
+                if (mcap) {
+                    marks.count = reinterpret_cast<uint32_t*>(ua + b0 + b1 + b2);
+                    marks.list = reinterpret_cast<uint64_t*>(ua + b0 + b1 + b2 + up256(sizeof(uint32_t) * kMarkLists));
+                    marks.cap = (uint32_t)mcap;
+                }
             }
         }
         const size_t nexp = wavedec ? (size_t)nunits : hl.size();  // expand waves: units, or lanes
@@ -1327,6 +1352,7 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
             if (ue == hipSuccess) ue = X.h2d(d_obase, hob.data(), sizeof(int64_t) * hob.size());
             if (ue == hipSuccess) ue = X.h2d(dev + o_imgs, hd.data(), sizeof(PngImgDev) * m);
             if (ue == hipSuccess) ue = hipMemsetAsync(dev + o_err, 0, sizeof(int) * m, s);
+            if (ue == hipSuccess && marks.count) ue = hipMemsetAsync(marks.count, 0, sizeof(uint32_t) * kMarkLists, s);
             if (ue != hipSuccess) rc = hip_fail(ue, "PNG expand tables");
             hxst.resize(2 * nexp);
             mk[2] = now_ms();  // lane tables uploaded
@@ -1344,7 +1370,8 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                     // the units' tables and page tables (k_png_units), then one wave per unit
                     if (e3 == hipSuccess) e3 = launch_png_units(d_imgs, d_lanes, (int)hl.size(), d_units, d_ulane, s);
                     if (e3 == hipSuccess)
-                        e3 = launch_png_expand(d_imgs, d_lanes, (int)nunits, d_tok, d_uxst, s, d_pieces, d_units, d_ulane);
+                        e3 = launch_png_expand(d_imgs, d_lanes, (int)nunits, d_tok, d_uxst, s, d_pieces, d_units, d_ulane,
+                                               marks);
                 } else if (e3 == hipSuccess) {
                     e3 = launch_png_expand(d_imgs, d_lanes, (int)hl.size(), d_tok, d_xst, s);
                 }
@@ -1365,8 +1392,9 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                 }
                 if (e3 == hipSuccess && !wavedec) e3 = X.h2d(d_pages, hpages.data(), sizeof(int) * hpages.size());
                 if (e3 == hipSuccess) e3 = X.h2d(d_rows, hrows.data(), sizeof(int2) * hrows.size());
-                if (e3 == hipSuccess) e3 = launch_png_resolve(d_imgs, d_rows, (int)hrows.size(),
-                                                              reinterpret_cast<int*>(dev + o_err), s);
+                if (e3 == hipSuccess)
+                    e3 = marks.list ? launch_png_marks(d_imgs, marks, d_rows, (int)hrows.size(), reinterpret_cast<int*>(dev + o_err), s)
+                                    : launch_png_resolve(d_imgs, d_rows, (int)hrows.size(), reinterpret_cast<int*>(dev + o_err), s);
                 rec(6, s);
 #ifdef IK_PNG_DUMP  // dev experiment: every image's filtered rows and filter types before the unfilter
                 if (e3 == hipSuccess) {
@@ -1374,58 +1402,64 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                     png_dump_store(J, hd, m);
                 }
 #endif
-                // unfilter: one launch per bytes-per-pixel class, over that class's
-                // images; a workgroup per 16 bands, its (image, group) by ticket
-                if (e3 == hipSuccess) {
-                    std::vector<PngImgDev> cls;
-                    std::vector<int2> groups;
-                    std::vector<int> pbase;
-                    struct Range { int bpp, img0, grp0; };
-                    std::vector<Range> ranges;
-                    int band0 = 0;
-                    for (int bpp : {1, 2, 3, 4, 6, 8}) {
-                        const Range r{bpp, (int)cls.size(), (int)groups.size()};
-                        for (int k = 0; k < m; ++k)
-                            if (J[k]->state == 1 && hd[k].bpp == bpp) {
-                                for (int g = 0; g < png_unfilter_groups(hd[k].H); ++g)
-                                    groups.push_back(make_int2((int)cls.size() - r.img0, g));
-                                pbase.push_back(band0);
-                                band0 += (hd[k].H + 63) / 64;
-                                cls.push_back(hd[k]);
-                            }
-                        if ((int)cls.size() > r.img0) ranges.push_back(r);
+                // unfilter (+ png's EXPAND), as a step of its own: the direct-rows path whose
+                // marker list overflowed runs resolve and this again (below)
+                auto unfilter_all = [&](hipError_t e3) -> hipError_t {
+                    // unfilter: one launch per bytes-per-pixel class, over that class's
+                    // images; a workgroup per 16 bands, its (image, group) by ticket
+                    if (e3 == hipSuccess) {
+                        std::vector<PngImgDev> cls;
+                        std::vector<int2> groups;
+                        std::vector<int> pbase;
+                        struct Range { int bpp, img0, grp0; };
+                        std::vector<Range> ranges;
+                        int band0 = 0;
+                        for (int bpp : {1, 2, 3, 4, 6, 8}) {
+                            const Range r{bpp, (int)cls.size(), (int)groups.size()};
+                            for (int k = 0; k < m; ++k)
+                                if (J[k]->state == 1 && hd[k].bpp == bpp) {
+                                    for (int g = 0; g < png_unfilter_groups(hd[k].H); ++g)
+                                        groups.push_back(make_int2((int)cls.size() - r.img0, g));
+                                    pbase.push_back(band0);
+                                    band0 += (hd[k].H + 63) / 64;
+                                    cls.push_back(hd[k]);
+                                }
+                            if ((int)cls.size() > r.img0) ranges.push_back(r);
+                        }
+                        const size_t gb = up256(sizeof(int2) * ngroups);
+                        std::vector<uint8_t> tabs(unf_tab, 0);
+                        std::memcpy(tabs.data(), groups.data(), sizeof(int2) * groups.size());
+                        std::memcpy(tabs.data() + gb, pbase.data(), sizeof(int) * pbase.size());
+                        e3 = X.h2d(d_unf, tabs.data(), unf_tab);
+                        unsigned* d_prog = reinterpret_cast<unsigned*>(d_unf + unf_tab);
+                        unsigned* d_ticket = d_prog + nbands;
+                        if (e3 == hipSuccess) e3 = hipMemsetAsync(d_prog, 0, unf_zero, s);
+                        if (e3 == hipSuccess) e3 = X.h2d(d_cls, cls.data(), sizeof(PngImgDev) * cls.size());
+                        const int2* d_groups = reinterpret_cast<const int2*>(d_unf);
+                        const int* d_pbase = reinterpret_cast<const int*>(d_unf + gb);
+                        for (size_t r = 0; r < ranges.size() && e3 == hipSuccess; ++r) {
+                            const int g1 = r + 1 < ranges.size() ? ranges[r + 1].grp0 : (int)groups.size();
+                            const int g0 = ranges[r].grp0, i0 = ranges[r].img0;
+                            e3 = launch_png_unfilter(d_cls + i0, d_groups + g0, g1 - g0, d_pbase + i0, d_prog,
+                                                     d_ticket + r, ranges[r].bpp, s);
+                            // (RGBA8 images of None / Sub / Up rows: the scan path; each kernel skips the other's)
+                            const int i1 = r + 1 < ranges.size() ? ranges[r + 1].img0 : (int)cls.size();
+                            if (e3 == hipSuccess && ranges[r].bpp == 4) e3 = launch_png_unfilter_su(d_cls + i0, i1 - i0, s);
+                        }
                     }
-                    const size_t gb = up256(sizeof(int2) * ngroups);
-                    std::vector<uint8_t> tabs(unf_tab, 0);
-                    std::memcpy(tabs.data(), groups.data(), sizeof(int2) * groups.size());
-                    std::memcpy(tabs.data() + gb, pbase.data(), sizeof(int) * pbase.size());
-                    e3 = X.h2d(d_unf, tabs.data(), unf_tab);
-                    unsigned* d_prog = reinterpret_cast<unsigned*>(d_unf + unf_tab);
-                    unsigned* d_ticket = d_prog + nbands;
-                    if (e3 == hipSuccess) e3 = hipMemsetAsync(d_prog, 0, unf_zero, s);
-                    if (e3 == hipSuccess) e3 = X.h2d(d_cls, cls.data(), sizeof(PngImgDev) * cls.size());
-                    const int2* d_groups = reinterpret_cast<const int2*>(d_unf);
-                    const int* d_pbase = reinterpret_cast<const int*>(d_unf + gb);
-                    for (size_t r = 0; r < ranges.size() && e3 == hipSuccess; ++r) {
-                        const int g1 = r + 1 < ranges.size() ? ranges[r + 1].grp0 : (int)groups.size();
-                        const int g0 = ranges[r].grp0, i0 = ranges[r].img0;
-                        e3 = launch_png_unfilter(d_cls + i0, d_groups + g0, g1 - g0, d_pbase + i0, d_prog,
-                                                 d_ticket + r, ranges[r].bpp, s);
-                        // (RGBA8 images of None / Sub / Up rows: the scan path; each kernel skips the other's)
-                        const int i1 = r + 1 < ranges.size() ? ranges[r + 1].img0 : (int)cls.size();
-                        if (e3 == hipSuccess && ranges[r].bpp == 4) e3 = launch_png_unfilter_su(d_cls + i0, i1 - i0, s);
+                    // png's EXPAND for the palette / low-bit / tRNS images
+                    for (int k = 0; k < m && e3 == hipSuccess; ++k) {
+                        PngJob& j = *J[k];
+                        if (j.state != 1 || !j.expand || !j.rows) continue;
+                        j.px.src = j.rows->d;
+                        j.px.sp = j.rows->pitch;
+                        j.px.dst = j.img->d;
+                        j.px.dp = j.img->pitch;
+                        e3 = launch_png_px(j.px, s);
                     }
-                }
-                // png's EXPAND for the palette / low-bit / tRNS images
-                for (int k = 0; k < m && e3 == hipSuccess; ++k) {
-                    PngJob& j = *J[k];
-                    if (j.state != 1 || !j.expand || !j.rows) continue;
-                    j.px.src = j.rows->d;
-                    j.px.sp = j.rows->pitch;
-                    j.px.dst = j.img->d;
-                    j.px.dp = j.img->pitch;
-                    e3 = launch_png_px(j.px, s);
-                }
+                    return e3;
+                };
+                e3 = unfilter_all(e3);
                 rec(7, s);
 #ifdef IK_EXP_PROF
                 {
@@ -1448,6 +1482,25 @@ int png_decode_finish(PngUpload& up, ik_image** outs, int* status, std::string* 
                                 (double)pf[2] / pf[7], (double)pf[3] / pf[7], (double)pf[4] / pf[7], ev_ms(6, 7));
                 }
 #endif
+                uint32_t nmarks = 0, mcnt[kMarkLists];
+                bool mover = false;
+                if (e3 == hipSuccess && marks.count) {
+                    e3 = X.d2h(mcnt, marks.count, sizeof(mcnt));
+                    for (uint32_t q = 0; q < kMarkLists; ++q) {
+                        nmarks += mcnt[q];
+                        mover = mover || mcnt[q] > marks.cap / kMarkLists;
+                    }
+                }
+                if (e3 == hipSuccess && mover) {
+                    // the marker list overflowed (runs of copies across units, e.g. a flat
+                    // image): the rows from the u16 symbols after all, then the unfilter again
+                    if (timing) fprintf(stderr, "[png] %u window markers > list %u: resolve pass\n", nmarks, marks.cap);
+                    e3 = hipMemsetAsync(dev + o_err, 0, sizeof(int) * m, s);
+                    if (e3 == hipSuccess)
+                        e3 = launch_png_resolve(d_imgs, d_rows, (int)hrows.size(), reinterpret_cast<int*>(dev + o_err), s);
+                    e3 = unfilter_all(e3);
+                }
+                if (timing && marks.count) fprintf(stderr, "[png] window markers %u (list %u)\n", nmarks, marks.cap);
                 if (e3 == hipSuccess) e3 = X.d2h(hxst.data(), wavedec ? d_uxst : d_xst, 2 * sizeof(int) * nexp);
                 if (e3 == hipSuccess) e3 = X.d2h(herr.data(), dev + o_err, sizeof(int) * m);
                 mk[3] = now_ms();  // expand .. unfilter done

@@ -193,6 +193,21 @@ def test_unfilter_scan_path_batch(on_gpu):
         np.testing.assert_array_equal(d.to_array().reshape(im.shape), im)
 
 
+def test_flat_images_markers_through_every_unit(on_gpu):
+    """A flat image is runs of copies across every unit boundary: window markers fill
+    its rows (chains through every earlier unit) -- beside a normal frame.  (With
+    IK_PNG_DIRECT=1 the direct-rows expand's marker list overflows here and the batch
+    takes the resolve pass after all; tests/test_gpu_png_direct.py runs that.)"""
+    flat = np.zeros((2048, 2048, 4), np.uint8)
+    flat[..., 0] = 200
+    flat[..., 3] = 255
+    img = ikutil.synth(1024, 768, 4, seed=91, pattern="S")
+    datas = [own_png(flat, filters=0, idat_size=65536), pil_png(img), own_png(flat[:300], filters=2)]
+    out = decode_image_batch(datas)
+    for (d, fmt), im in zip(out, [flat, img, flat[:300]]):
+        np.testing.assert_array_equal(d.to_array().reshape(im.shape), im)
+
+
 def test_batch_mixed(on_gpu):
     imgs = [ikutil.synth(w, h, c, seed=k) for k, (w, h, c) in
             enumerate([(640, 480, 4), (1024, 768, 3), (333, 222, 1), (2048, 1024, 4), (100, 3000, 2)])]
