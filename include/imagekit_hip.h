@@ -336,6 +336,25 @@ int ik_webp_yuv420_device(const uint8_t *dev_src, uint32_t w, uint32_t h, uint32
  * writes); *out is allocated by the library (ik_buf_free) */
 int ik_webp_encode_gpu_device(const uint8_t *dev_yuv, uint32_t w, uint32_t h, int quality,
                               uint8_t **out, size_t *out_len);
+/* libwebp's method-4 segment analysis on the GPU -- the first stage of
+ * encode_image's WebP coder (src/transform.rs:129-137 -> libwebp VP8EncAnalyze +
+ * VP8SetSegmentParams), exact: the same segment map and segment header libwebp
+ * writes for these planes at this quality.  n images of w x h YUV420 planes in
+ * device memory (the ik_webp_yuv420_device layout), image i at dev_yuv +
+ * i*yuv_stride.  seg (host) receives n * mb_w * mb_h segment ids, raster order per
+ * image; hdr (host) n headers.  Runs on the calling thread's stream and waits. */
+typedef struct {
+    int32_t num_segments;  /* after libwebp's SimplifySegments (1..4) */
+    int32_t update_map;    /* the frame codes a segment map */
+    int32_t quant[4];      /* segment quantiser indices (the header's absolute values) */
+    int32_t fstrength[4];  /* initial filter levels (libwebp raises them after coding) */
+    int32_t base_quant;    /* y_ac_qi */
+    int32_t dq_uv_dc, dq_uv_ac;
+    int32_t probs[3];      /* segment-tree probabilities */
+    int32_t alpha, uv_alpha; /* frame susceptibilities (enc->alpha_, enc->uv_alpha_) */
+} ik_vp8_segment_header;
+int ik_vp8_analyze_device(const uint8_t *dev_yuv, size_t yuv_stride, uint32_t n, uint32_t w, uint32_t h,
+                          float quality, uint8_t *seg, ik_vp8_segment_header *hdr);
 /* the JPEG front end (to_rgb8 + RGB->YCbCr + FDCT + quantise) on the device:
  * int16 coefficients, MCU-major, Y/Cb/Cr, natural order */
 int ik_jpeg_coeffs_device(const uint8_t *dev_src, uint32_t w, uint32_t h, uint32_t C,

@@ -37,6 +37,18 @@ constexpr uint32_t kPackMagic = 0x4b503856u;  // "V8PK"
 constexpr int kMaxPackMBs = 4096;             // one image's MBs (scan in LDS): 1024x1024
 constexpr size_t kPackMaxMBBytes = 8 + 16 + 25 * (2 + 32);
 inline size_t vp8_pack_cap(size_t nmb) { return (kPackHeaderBytes + nmb * kPackMaxMBBytes + 15) & ~(size_t)15; }
+// libwebp's segment analysis (ik_vp8_analysis.hip): per image the k-means result
+struct SegRecord {
+    int32_t centers[4];
+    int32_t mid;  // AssignSegments' weighted_average
+    int32_t nmb;
+    unsigned long long alpha_sum, uv_alpha_sum;  // MBAnalyze's accumulators
+};
+// n images of w x h YUV420 planes (Vp8Args layout) -> alpha/uva per MB, seg per MB
+// (the k-means cluster, before SimplifySegments), rec per image
+hipError_t launch_vp8_analysis(const uint8_t* yuv, size_t yuv_stride, int n, int w, int h, uint8_t* alpha,
+                               uint16_t* uva, uint8_t* seg, SegRecord* rec, hipStream_t s);
+
 hipError_t launch_vp8_pack(const MBOut* mbs, int nmb, int n, uint8_t* scratch, uint8_t* host_dst, size_t cap_img,
                            hipStream_t s);
 

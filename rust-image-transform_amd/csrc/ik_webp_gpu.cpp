@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -135,6 +136,82 @@ int webp_encode_gpu(const uint8_t* d_yuv, int w, int h, int quality, std::vector
     return IK_OK;
 }
 
+// The host half of libwebp's segment set-up, from k_vp8_kmeans' record and
+// cluster map (ik_vp8_analysis.hip): SetSegmentAlphas (analysis_enc.c),
+// VP8SetSegmentParams with its pow() quality curve, SetupFilterStrength
+// (filter_enc.c, sharpness 0: kLevelsFromDelta[0] is the identity on 0..63),
+// SimplifySegments (quant_enc.c) and SetSegmentProbas (frame_enc.c).  libwebp's
+// WebPConfigInit defaults: segments 4, sns_strength 50, filter_strength 60.
+// seg: the image's k-means clusters in, final segment ids out.
+void vp8_segment_setup(const vp8::SegRecord& r, float quality, uint8_t* seg, ik_vp8_segment_header* hd) {
+    constexpr int nb = 4, sns = 50, filter_strength = 60;
+    auto clip = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
+    int mn = r.centers[0], mx = r.centers[0];
+    for (int k = 0; k < nb; ++k) {
+        mn = r.centers[k] < mn ? r.centers[k] : mn;
+        mx = r.centers[k] > mx ? r.centers[k] : mx;
+    }
+    if (mx == mn) mx = mn + 1;
+    int s_alpha[nb], s_beta[nb], quant[nb], fstr[nb];
+    for (int k = 0; k < nb; ++k) {
+        s_alpha[k] = clip(255 * (r.centers[k] - r.mid) / (mx - mn), -127, 127);
+        s_beta[k] = clip(255 * (r.centers[k] - mn) / (mx - mn), 0, 255);
+    }
+    const double amp = 0.9 * sns / 100. / 128.;  // SNS_TO_DQ
+    const double Q = quality / 100.;
+    const double linear_c = (Q < 0.75) ? Q * (2. / 3.) : 2. * Q - 1.;
+    const double c_base = pow(linear_c, 1 / 3.);
+    for (int k = 0; k < nb; ++k) {
+        const double expn = 1. - amp * s_alpha[k];
+        const double c = pow(c_base, expn);
+        quant[k] = clip((int)(127. * (1. - c)), 0, 127);
+    }
+    const int total = r.nmb > 0 ? r.nmb : 1;
+    const int uv_alpha = (int)(r.uv_alpha_sum / (unsigned long long)total);
+    // MID_ALPHA 64, MIN_ALPHA 30, MAX_ALPHA 100; MIN/MAX_DQ_UV -4 / 6
+    int dq_uv_ac = (uv_alpha - 64) * (6 - (-4)) / (100 - 30);
+    dq_uv_ac = clip(dq_uv_ac * sns / 100, -4, 6);
+    const int dq_uv_dc = clip(-4 * sns / 100, -15, 15);
+    const int level0 = 5 * filter_strength;
+    for (int k = 0; k < nb; ++k) {
+        const int qstep = vp8::kAcTable[clip(quant[k], 0, 127)] >> 2;
+        const int base = qstep < 63 ? qstep : 63;
+        const int f = base * level0 / (256 + s_beta[k]);
+        fstr[k] = f < 2 ? 0 : (f > 63 ? 63 : f);  // FSTRENGTH_CUTOFF 2
+    }
+    hd->base_quant = quant[0];
+    int map[nb] = {0, 1, 2, 3}, nfinal = 1;
+    for (int s1 = 1; s1 < nb; ++s1) {
+        int s2 = 0;
+        bool found = false;
+        for (; s2 < nfinal; ++s2)
+            if (quant[s1] == quant[s2] && fstr[s1] == fstr[s2]) { found = true; break; }
+        map[s1] = s2;
+        if (!found) {
+            if (nfinal != s1) { quant[nfinal] = quant[s1]; fstr[nfinal] = fstr[s1]; }
+            ++nfinal;
+        }
+    }
+    int cnt[nb] = {0, 0, 0, 0};
+    for (int i = 0; i < r.nmb; ++i) {
+        seg[i] = (uint8_t)(nfinal < nb ? map[seg[i]] : seg[i]);
+        ++cnt[seg[i]];
+    }
+    for (int k = nfinal; k < nb; ++k) { quant[k] = quant[nfinal - 1]; fstr[k] = fstr[nfinal - 1]; }
+    auto proba = [](int a, int b) { const int t = a + b; return t == 0 ? 255 : (255 * a + t / 2) / t; };
+    hd->probs[0] = proba(cnt[0] + cnt[1], cnt[2] + cnt[3]);
+    hd->probs[1] = proba(cnt[0], cnt[1]);
+    hd->probs[2] = proba(cnt[2], cnt[3]);
+    hd->num_segments = nfinal;
+    hd->update_map = nfinal > 1 && (hd->probs[0] != 255 || hd->probs[1] != 255 || hd->probs[2] != 255);
+    if (nfinal > 1 && !hd->update_map) std::memset(seg, 0, (size_t)r.nmb);  // ResetSegments
+    for (int k = 0; k < nb; ++k) { hd->quant[k] = quant[k]; hd->fstrength[k] = fstr[k]; }
+    hd->dq_uv_dc = dq_uv_dc;
+    hd->dq_uv_ac = dq_uv_ac;
+    hd->alpha = (int)(r.alpha_sum / (unsigned long long)total);
+    hd->uv_alpha = uv_alpha;
+}
+
 }  // namespace ik
 
 using namespace ik;
@@ -161,6 +238,36 @@ int ik_webp_encode_gpu_device(const uint8_t* dev_yuv, uint32_t w, uint32_t h, in
     if (!*out) return fail(IK_ERR_NOMEM, "out of host memory");
     std::memcpy(*out, bytes.data(), bytes.size());
     *out_len = bytes.size();
+    return IK_OK;
+}
+
+int ik_vp8_analyze_device(const uint8_t* dev_yuv, size_t yuv_stride, uint32_t n, uint32_t w, uint32_t h,
+                          float quality, uint8_t* seg, ik_vp8_segment_header* hdr) {
+    IK_API_ENTER();
+    if (!dev_yuv || !seg || !hdr) return fail(IK_ERR_INVALID, "null pointer");
+    if (n < 1 || n > 65535 || w < 1 || h < 1 || w > 16383 || h > 16383)
+        return fail(IK_ERR_INVALID, "bad VP8 analysis shape %ux%u x %u", w, h, n);
+    if (!(quality >= 0.f)) quality = 0.f;
+    if (quality > 100.f) quality = 100.f;
+    const size_t ysz = (size_t)w * h + 2 * (size_t)((w + 1) / 2) * ((h + 1) / 2);
+    if (n > 1 && yuv_stride < ysz) return fail(IK_ERR_INVALID, "image stride %zu under the planes' %zu bytes", yuv_stride, ysz);
+    const int nmb = (int)(((w + 15) >> 4) * ((h + 15) >> 4));
+    hipStream_t s = thread_stream();
+    if (!s) return fail(IK_ERR_DEVICE, "cannot create HIP stream");
+    const size_t per = (size_t)nmb * n;
+    uint8_t* d = nullptr;
+    const size_t o_uva = (per + 255) & ~(size_t)255, o_seg = o_uva + ((2 * per + 255) & ~(size_t)255);
+    const size_t o_rec = o_seg + ((per + 255) & ~(size_t)255), bytes = o_rec + sizeof(vp8::SegRecord) * n;
+    IK_HIP(hipMalloc((void**)&d, bytes));
+    std::vector<vp8::SegRecord> recs(n);
+    hipError_t e = vp8::launch_vp8_analysis(dev_yuv, yuv_stride, (int)n, (int)w, (int)h, d, (uint16_t*)(d + o_uva),
+                                            d + o_seg, (vp8::SegRecord*)(d + o_rec), s);
+    if (e == hipSuccess) e = hipMemcpyAsync(seg, d + o_seg, per, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(recs.data(), d + o_rec, sizeof(vp8::SegRecord) * n, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(IK_ERR_DEVICE, "VP8 analysis: %s", hipGetErrorString(e));
+    for (uint32_t i = 0; i < n; ++i) vp8_segment_setup(recs[i], quality, seg + (size_t)nmb * i, hdr + i);
     return IK_OK;
 }
 
