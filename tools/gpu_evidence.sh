@@ -12,6 +12,7 @@
 #   ltrst     the same with a restart marker per MCU row
 #   jtests    the JPEG GPU parity tests only (decode, zune reconstruction, the configs[2] parity case)
 #   ptime     the headline bench with IK_TIMING (host stage marks on stderr)
+#   c4        configs[4] (8192^2 PNG -> 1024^2 Lanczos3 -> AVIF q60) under rocprofv3, kernel stats
 #   pmc       PMC HBM traffic of the PNG kernels (tools/pmc_png_traffic.sh) -> ${TAG}_pmc_png.json
 #   gtest     the GPU tests named in $GTESTS
 # Outputs go to gpurun_out/${TAG}_*; copy what is judged into profiles/.
@@ -54,6 +55,12 @@ for s in $STEPS; do
       timeout -k 10 900 python -u bench.py --source jpeg --format jpeg --quality 85 --filter lanczos3 --batch 256 --steps 4 --warmup 1 --no-extras --no-cpu-baseline > ${O}_c2norst.json 2> ${O}_c2norst.err \
         || { echo "C2NORST FAILED"; tail -20 ${O}_c2norst.err; exit 1; }
       python tools/bench_summary.py ${O}_c2norst.json ;;
+    c4)
+      # configs[4]: 32 x 8192^2 RGBA PNG (HBM) -> 1024^2 Lanczos3 -> AVIF q60, under rocprofv3 (kernel stats)
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d ${O}_c4prof -o run -f csv -- python bench.py --size 8192 --out 1024 --filter lanczos3 --format avif --quality 60 --batch 32 --steps 3 --warmup 1 --no-extras --no-pcie-leg --cpu-seconds 10 > ${O}_c4.json 2> ${O}_c4.err \
+        || { echo "C4 FAILED"; tail -20 ${O}_c4.err; exit 1; }
+      python tools/bench_summary.py ${O}_c4.json
+      find ${O}_c4prof -name "*kernel_stats.csv" -exec cp {} ${O}_c4_kernel_stats.csv \; ;;
     lt)
       timeout -k 10 900 python -u tools/loadtest.py --requests 10000 --batch 64 --threads 16 --cpu-seconds 15 > ${O}_lt.json 2> ${O}_lt.err \
         || { echo "LOADTEST FAILED"; tail -20 ${O}_lt.err; exit 1; }
