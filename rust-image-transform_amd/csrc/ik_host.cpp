@@ -718,10 +718,34 @@ int ik_device_count(void) {
     return n;
 }
 
+// How host threads wait for the GPU.  HIP's default (hipDeviceScheduleAuto) spins
+// the waiting thread on the CPU; the batch paths have several threads waiting on
+// device work at once (stage threads, lane checks) while the host coders (libwebp)
+// need every core of the quota, so the library asks for blocking waits
+// (hipDeviceScheduleBlockingSync: the thread sleeps until the GPU signals).
+// IK_SYNC=spin keeps the spinning.  Applied once per visible device, process-wide.
+static void apply_sync_mode(int ndev) {
+    static std::once_flag once;
+    std::call_once(once, [ndev] {
+        const char* e = getenv("IK_SYNC");
+        if (e && !strcmp(e, "spin")) return;
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess) cur = 0;
+        for (int d = 0; d < ndev; ++d) {
+            if (hipSetDevice(d) != hipSuccess) continue;
+            const hipError_t r = hipSetDeviceFlags(hipDeviceScheduleBlockingSync);
+            if (r != hipSuccess && getenv("IK_TIMING"))
+                fprintf(stderr, "[init] device %d: blocking sync not set (%s)\n", d, hipGetErrorString(r));
+        }
+        (void)hipSetDevice(cur);
+    });
+}
+
 int ik_init(int device) {
     IK_API_ENTER();
     int n = 0;
     IK_HIP(hipGetDeviceCount(&n));
+    apply_sync_mode(n);
     if (device >= n) return fail(IK_ERR_INVALID, "device %d out of range (%d devices)", device, n);
     if (device < 0) {  // every visible GPU (or IK_DEVICES): one process, many devices
         if (int rc = sched_configure(nullptr, 0)) return rc;

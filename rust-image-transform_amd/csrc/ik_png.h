@@ -165,9 +165,9 @@ hipError_t launch_png_resolve(const PngImgDev* imgs, const int2* rows, int nrows
 // it -- instead of the diagonal wavefront (the Up rows' only dependency is the row
 // above, byte for byte; a Sub row's is a prefix sum along the row).  k_png_unfilter
 // skips those images.
-constexpr int kSuThreads = 256, kSuChunks = 4, kSuRanges = 16;
+constexpr int kSuThreads = 256, kSuChunks = 4, kSuChunksWide = 8, kSuRanges = 16;
 IK_HD bool png_unfilter_scan_path(int bpp, int rowbytes, int flags) {
-    return bpp == 4 && (rowbytes + 15) / 16 <= kSuThreads * kSuChunks && !(flags & 7);
+    return bpp == 4 && (rowbytes + 15) / 16 <= kSuThreads * kSuChunksWide && !(flags & 7);
 }
 // nimg images of one class (bpp 4): kSuRanges workgroups each
 hipError_t launch_png_unfilter_su(const PngImgDev* imgs, int nimg, hipStream_t s);

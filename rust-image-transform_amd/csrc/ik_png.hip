@@ -1846,8 +1846,12 @@ __device__ __forceinline__ uint32_t wave_scan_bytes(uint32_t v) {  // inclusive,
     return add_bytes(v, row == 0 ? 0u : row == 1 ? r0 : row == 2 ? r1 : r2);
 }
 
+// CH chunks per thread: kSuChunks for rows up to 4,096 pixels, kSuChunksWide for
+// rows up to 8,192 (each launch takes its own images of the batch).
+template <int CH>
 __global__ __launch_bounds__(kSuThreads) void k_png_unfilter_su(const PngImgDev* imgs, int nimg) {
     raise_priority();
+    constexpr int kSuChunks = CH;
     __shared__ uint32_t s_w[kSuThreads / 64];
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     const int im = (int)blockIdx.x / kSuRanges, jr = (int)blockIdx.x % kSuRanges;
@@ -1855,6 +1859,8 @@ __global__ __launch_bounds__(kSuThreads) void k_png_unfilter_su(const PngImgDev*
     const PngImgDev I = imgs[im];
     if (!png_unfilter_scan_path(4, I.rowbytes, *(const volatile int*)I.flags)) return;
     const int H = I.H, nch = (I.rowbytes + 15) >> 4;
+    // (wave-uniform) the narrow kernel takes rows of <= kSuThreads * 4 chunks, the wide one the rest
+    if ((nch <= kSuThreads * ::ik::kSuChunks) != (CH == ::ik::kSuChunks)) return;
     const int tid = threadIdx.x, wv = tid >> 6;
     const int c0 = tid * kSuChunks;  // this thread's first chunk
     const int y1 = (int)((int64_t)H * (jr + 1) / kSuRanges);
@@ -1903,7 +1909,8 @@ __global__ __launch_bounds__(kSuThreads) void k_png_unfilter_su(const PngImgDev*
 
 hipError_t launch_png_unfilter_su(const PngImgDev* imgs, int nimg, hipStream_t s) {
     if (nimg <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_png_unfilter_su, dim3(nimg * kSuRanges), dim3(kSuThreads), 0, s, imgs, nimg);
+    hipLaunchKernelGGL(k_png_unfilter_su<kSuChunks>, dim3(nimg * kSuRanges), dim3(kSuThreads), 0, s, imgs, nimg);
+    hipLaunchKernelGGL(k_png_unfilter_su<kSuChunksWide>, dim3(nimg * kSuRanges), dim3(kSuThreads), 0, s, imgs, nimg);
     return hipGetLastError();
 }
 

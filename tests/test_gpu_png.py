@@ -172,8 +172,9 @@ def test_unfilter_scan_path_batch(on_gpu):
     or Sub row and the Up rows under it) beside the diagonal kernel in one batch:
     Up runs crossing the workgroups' row slices, an image that is one segment (Up
     from row 0), Sub-only and None-only images, the widest scan-path row (4,096
-    pixels: 1,024 chunks) and one pixel wider (diagonal), and images with Average /
-    Paeth rows (diagonal)."""
+    pixels: 1,024 chunks) and one pixel wider, and images with Average /
+    Paeth rows (diagonal); rows of 4,097 ... 8,192 pixels take the wide scan kernel
+    (8 chunks per thread), 8,193 the diagonal one."""
     rnd = np.random.default_rng(5)
     cases = [
         ((4096, 300, 4), rnd.choice([1, 2, 2, 2, 2, 2, 2, 0], 300)),
@@ -185,6 +186,9 @@ def test_unfilter_scan_path_batch(on_gpu):
         ((640, 900, 4), rnd.choice([1, 2, 3, 4], 900)),
         ((901, 333, 3), rnd.choice([1, 2], 333)),
         ((1234, 1111, 4), np.concatenate([np.full(1110, 2), [4]])),
+        ((8192, 40, 4), rnd.choice([1, 2, 2, 2, 0], 40)),   # the wide scan-path kernel (2,048 chunks)
+        ((6000, 33, 4), np.where(np.arange(33) % 11 == 0, 1, 2)),
+        ((8193, 9, 4), rnd.choice([1, 2], 9)),               # one pixel wider: diagonal
     ]
     imgs = [ikutil.synth(w, h, c, seed=70 + k, pattern="N" if k % 2 else "S") for k, ((w, h, c), _) in enumerate(cases)]
     datas = [own_png(im, filters=f, idat_size=65536) for im, (_, f) in zip(imgs, cases)]
