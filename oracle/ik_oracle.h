@@ -87,6 +87,11 @@ int iko_jpeg_decode(const uint8_t *bytes, size_t n, int mode, uint8_t **out, int
 /* webp 0.3.1 Encoder::from_rgb(..).encode(q) == libwebp WebPEncodeRGB(rgb,w,h,3w,q)
  * through dlopen("libwebp.so.7").  Returns size, or -1 (library missing). */
 long iko_webp_encode_rgb(const uint8_t *rgb, int w, int h, int stride, float q, uint8_t **out);
+/* libwebp's method-4 macroblock decisions restated (vp8_modes.c): modes per MB and the
+ * final coefficient probabilities, from YUV420 planes + the segment set-up */
+int iko_vp8_modes(const uint8_t *y, const uint8_t *u, const uint8_t *v, int w, int h, float quality,
+                  const uint8_t *seg, const int *quant, int dq_uv_dc, int dq_uv_ac, uint8_t *ymode,
+                  uint8_t *bmodes, uint8_t *uvmode, uint8_t *probas);
 
 /* the reference CPU transform (resize_image + encode_image) on a decoded 8-bit
  * image: fmt 0=jpeg 1=webp.  Used as bench.py's cpu_baseline "port". */
