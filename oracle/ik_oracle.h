@@ -92,6 +92,10 @@ long iko_webp_encode_rgb(const uint8_t *rgb, int w, int h, int stride, float q, 
 int iko_vp8_modes(const uint8_t *y, const uint8_t *u, const uint8_t *v, int w, int h, float quality,
                   const uint8_t *seg, const int *quant, int dq_uv_dc, int dq_uv_ac, uint8_t *ymode,
                   uint8_t *bmodes, uint8_t *uvmode, uint8_t *probas);
+/* the whole WebP file libwebp writes, restated (vp8_modes.c); *out malloc'd (iko_free) */
+long iko_vp8_encode(const uint8_t *y, const uint8_t *u, const uint8_t *v, int w, int h, float quality,
+                    const uint8_t *seg, int num_segments, int update_map, const int *probs, const int *quant,
+                    const int *fstr, int dq_uv_dc, int dq_uv_ac, uint8_t **out);
 
 /* the reference CPU transform (resize_image + encode_image) on a decoded 8-bit
  * image: fmt 0=jpeg 1=webp.  Used as bench.py's cpu_baseline "port". */

@@ -14,7 +14,9 @@
  * non-zero-context bookkeeping).  Its cost tables come from libwebp's own read-only data
  * (vp8_enc_tables.h, tools/gen_vp8_tables.py).  The output -- every macroblock's luma
  * and chroma modes and the frame's final coefficient probabilities -- is pinned against
- * what libwebp writes into its bytes (tests/test_vp8_modes.py, via tests/vp8_parse.py).
+ * what libwebp writes into its bytes (tests/test_vp8_modes.py, via tests/vp8_parse.py), and
+ * iko_vp8_encode adds the bitstream (filter levels, partition 0, the token partition,
+ * RIFF) -- byte-identical to WebPEncodeRGB's output.
  * The segment map and segment quantisers are inputs (tests/oracle_vp8.py restates
  * that first stage).
  */
@@ -155,45 +157,102 @@ static int record_stats(int bit, uint32_t* s) {
     return bit;
 }
 
+/* the token sink (VP8TBuffer): bit 15 = the bit, bit 14 = a constant probability
+ * (bits 0-7), else bits 0-13 = the index of the coefficient probability it is coded
+ * with (TOKEN_ID + node); NULL while only the decisions are wanted */
+static uint32_t* g_tok;
+static size_t g_ntok, g_tcap;
+
+static void put_token(uint32_t t) {
+    if (!g_tok && !g_tcap) return;
+    if (g_ntok == g_tcap) {
+        g_tcap = g_tcap * 2 + 4096;
+        g_tok = realloc(g_tok, g_tcap * sizeof(*g_tok));
+    }
+    g_tok[g_ntok++] = t;
+}
+
+static int add_token(int bit, uint32_t id, uint32_t* s) {
+    put_token(((uint32_t)bit << 15) | id);
+    return record_stats(bit, s);
+}
+
+static void add_const(int bit, int prob) { put_token(((uint32_t)bit << 15) | (1u << 14) | (uint32_t)prob); }
+
+#define TOKEN_ID(t, b, ctx) (11u * ((ctx) + 3u * ((b) + 8u * (t))))
+static const uint8_t kCat3[] = {173, 148, 140, 0};
+static const uint8_t kCat4[] = {176, 155, 140, 135, 0};
+static const uint8_t kCat5[] = {180, 157, 141, 134, 130, 0};
+static const uint8_t kCat6[] = {254, 254, 243, 230, 196, 177, 153, 140, 133, 130, 129, 0};
+
 static int record_coeff_tokens(Proba* P, int ctx, const Residual* r) {
     const int16_t* coeffs = r->coeffs;
-    const int last = r->last;
+    const int t = r->type, last = r->last;
     int n = r->first;
-    uint32_t* s = P->stats[r->type][n][ctx];
-    if (!record_stats(last >= 0, s + 0)) return 0;
+    uint32_t base_id = TOKEN_ID(t, n, ctx);
+    uint32_t* s = P->stats[t][n][ctx];
+    if (!add_token(last >= 0, base_id + 0, s + 0)) return 0;
     while (n < 16) {
         const int c = coeffs[n++];
-        const uint32_t v = (uint32_t)(c < 0 ? -c : c);
-        if (!record_stats(v != 0, s + 1)) {
-            s = P->stats[r->type][kEncBands[n]][0];
+        const int sign = c < 0;
+        const uint32_t v = (uint32_t)(sign ? -c : c);
+        if (!add_token(v != 0, base_id + 1, s + 1)) {
+            base_id = TOKEN_ID(t, kEncBands[n], 0);
+            s = P->stats[t][kEncBands[n]][0];
             continue;
         }
-        if (!record_stats(v > 1, s + 2)) {
-            s = P->stats[r->type][kEncBands[n]][1];
+        if (!add_token(v > 1, base_id + 2, s + 2)) {
+            base_id = TOKEN_ID(t, kEncBands[n], 1);
+            s = P->stats[t][kEncBands[n]][1];
         } else {
-            if (!record_stats(v > 4, s + 3)) {
-                if (record_stats(v != 2, s + 4)) record_stats(v == 4, s + 5);
-            } else if (!record_stats(v > 10, s + 6)) {
-                record_stats(v > 6, s + 7);
-            } else {
-                const uint32_t residue = v - 3;
-                if (residue < (8 << 1)) {
-                    record_stats(0, s + 8);
-                    record_stats(0, s + 9);
-                } else if (residue < (8 << 2)) {
-                    record_stats(0, s + 8);
-                    record_stats(1, s + 9);
-                } else if (residue < (8 << 3)) {  /* (libwebp records cat 5/6's second bit at slot 9) */
-                    record_stats(1, s + 8);
-                    record_stats(0, s + 9);
+            if (!add_token(v > 4, base_id + 3, s + 3)) {
+                if (add_token(v != 2, base_id + 4, s + 4)) add_token(v == 4, base_id + 5, s + 5);
+            } else if (!add_token(v > 10, base_id + 6, s + 6)) {
+                if (!add_token(v > 6, base_id + 7, s + 7)) {
+                    add_const(v == 6, 159);
                 } else {
-                    record_stats(1, s + 8);
-                    record_stats(1, s + 9);
+                    add_const(v >= 9, 165);
+                    add_const(!(v & 1), 145);
+                }
+            } else {
+                int mask;
+                const uint8_t* tab;
+                uint32_t residue = v - 3;
+                if (residue < (8 << 1)) {
+                    add_token(0, base_id + 8, s + 8);
+                    add_token(0, base_id + 9, s + 9);
+                    residue -= (8 << 0);
+                    mask = 1 << 2;
+                    tab = kCat3;
+                } else if (residue < (8 << 2)) {
+                    add_token(0, base_id + 8, s + 8);
+                    add_token(1, base_id + 9, s + 9);
+                    residue -= (8 << 1);
+                    mask = 1 << 3;
+                    tab = kCat4;
+                } else if (residue < (8 << 3)) {  /* (libwebp records cat 5/6's node-10 bit at stats slot 9) */
+                    add_token(1, base_id + 8, s + 8);
+                    add_token(0, base_id + 10, s + 9);
+                    residue -= (8 << 2);
+                    mask = 1 << 4;
+                    tab = kCat5;
+                } else {
+                    add_token(1, base_id + 8, s + 8);
+                    add_token(1, base_id + 10, s + 9);
+                    residue -= (8 << 3);
+                    mask = 1 << 10;
+                    tab = kCat6;
+                }
+                while (mask) {
+                    add_const(!!(residue & (uint32_t)mask), *tab++);
+                    mask >>= 1;
                 }
             }
-            s = P->stats[r->type][kEncBands[n]][2];
+            base_id = TOKEN_ID(t, kEncBands[n], 2);
+            s = P->stats[t][kEncBands[n]][2];
         }
-        if (n == 16 || !record_stats(n <= last, s + 0)) return 1;
+        add_const(sign, 128);
+        if (n == 16 || !add_token(n <= last, base_id + 0, s + 0)) return 1;
     }
     return 1;
 }
@@ -670,7 +729,11 @@ typedef struct {
     uint8_t predc[4][BPS * 8];  /* chroma predictions, U at 0, V at 8 */
     uint8_t yuv_out[BPS * 16];  /* the chosen reconstruction */
     const SegQ* dqm;
+    int seg;
 } MB;
+
+static int g_y2q1[4];
+static int g_max_edge[4];  /* per segment: StoreMaxDelta's largest DC step of DC-only i16 MBs */
 
 static int reconstruct_i16(Frame* F, MB* m, ModeScore* rd, uint8_t* out, int mode) {
     const uint8_t* ref = m->pred16[mode];
@@ -766,6 +829,14 @@ static void pick_best_intra16(Frame* F, MB* m, ModeScore* rd) {
     }
     *rd = best;
     set_rd_score(dqm->lambda_mode, rd);
+    /* a blocky MB (only DCs non-zero) with fairly high distortion: record its largest
+     * DC step for the filter strength (StoreMaxDelta) */
+    if ((rd->nz & 0x100ffffu) == 0x1000000u && rd->D > 20 * dqm->y1.q[0]) {
+        const int v0 = abs(rd->y_dc_levels[1]), v1 = abs(rd->y_dc_levels[2]), v2 = abs(rd->y_dc_levels[4]);
+        int max_v = v1 > v0 ? v1 : v0;
+        max_v = v2 > max_v ? v2 : max_v;
+        if (max_v > g_max_edge[m->seg]) g_max_edge[m->seg] = max_v;
+    }
 }
 
 
@@ -1035,6 +1106,10 @@ int iko_vp8_modes(const uint8_t* y, const uint8_t* u, const uint8_t* v, int w, i
     F.P.dirty = 1;
     SegQ segq[4];
     for (int s = 0; s < 4; ++s) setup_matrices(&segq[s], quant[s], dq_uv_dc, dq_uv_ac, 50);
+    for (int s = 0; s < 4; ++s) {
+        g_max_edge[s] = 0;
+        g_y2q1[s] = segq[s].y2.q[1];
+    }
     calculate_level_costs(&F.P);
     int max_count = (mb_w * mb_h) >> 3;
     if (max_count < 96) max_count = 96;  /* MIN_COUNT */
@@ -1055,7 +1130,8 @@ int iko_vp8_modes(const uint8_t* y, const uint8_t* u, const uint8_t* v, int w, i
             g_mx = mx;
             m.mx = mx;
             m.my = my;
-            m.dqm = &segq[seg[my * mb_w + mx]];
+            m.seg = seg[my * mb_w + mx];
+            m.dqm = &segq[m.seg];
             for (int r = 0; r < 16; ++r) memcpy(m.yuv_in + r * BPS, Y + (size_t)(my * 16 + r) * W + mx * 16, 16);
             for (int r = 0; r < 8; ++r) {
                 memcpy(m.yuv_in + 16 + r * BPS, U + (size_t)(my * 8 + r) * (W / 2) + mx * 8, 8);
@@ -1122,4 +1198,237 @@ int iko_vp8_modes(const uint8_t* y, const uint8_t* u, const uint8_t* v, int w, i
     free(Y); free(U); free(V);
     free(F.y_top); free(F.uv_top); free(F.nz); free(F.top_derr); free(F.preds);
     return 0;
+}
+
+/* ---- the bitstream (libwebp utils/bit_writer_utils.c, enc/syntax_enc.c) ---- */
+typedef struct {
+    int32_t range, value;
+    int run, nb_bits;
+    uint8_t* buf;
+    size_t pos, cap;
+} BitWriter;
+
+static void bw_init(BitWriter* bw) {
+    memset(bw, 0, sizeof(*bw));
+    bw->range = 255 - 1;
+    bw->nb_bits = -8;
+}
+
+static void bw_byte(BitWriter* bw, uint8_t b) {
+    if (bw->pos == bw->cap) {
+        bw->cap = bw->cap * 2 + 1024;
+        bw->buf = realloc(bw->buf, bw->cap);
+    }
+    bw->buf[bw->pos++] = b;
+}
+
+static void bw_flush(BitWriter* bw) {
+    const int s = 8 + bw->nb_bits;
+    const int32_t bits = bw->value >> s;
+    bw->value -= bits << s;
+    bw->nb_bits -= 8;
+    if ((bits & 0xff) != 0xff) {
+        if (bits & 0x100) {  /* carry into the bytes written */
+            if (bw->pos > 0) bw->buf[bw->pos - 1]++;
+        }
+        for (; bw->run > 0; --bw->run) bw_byte(bw, (bits & 0x100) ? 0x00 : 0xff);
+        bw_byte(bw, (uint8_t)(bits & 0xff));
+    } else {
+        bw->run++;  /* delay 0xff bytes, a carry may still come */
+    }
+}
+
+static int norm_shift(int r) { int s = 0; while (((r + 1) << s) < 128) ++s; return s; }
+
+static int bw_put(BitWriter* bw, int bit, int prob) {
+    const int split = (bw->range * prob) >> 8;
+    if (bit) {
+        bw->value += split + 1;
+        bw->range -= split + 1;
+    } else {
+        bw->range = split;
+    }
+    if (bw->range < 127) {
+        const int shift = norm_shift(bw->range);
+        bw->range = ((bw->range + 1) << shift) - 1;
+        bw->value <<= shift;
+        bw->nb_bits += shift;
+        if (bw->nb_bits > 0) bw_flush(bw);
+    }
+    return bit;
+}
+
+static int bw_uniform(BitWriter* bw, int bit) {
+    const int split = bw->range >> 1;
+    if (bit) {
+        bw->value += split + 1;
+        bw->range -= split + 1;
+    } else {
+        bw->range = split;
+    }
+    if (bw->range < 127) {
+        bw->range = ((bw->range + 1) << 1) - 1;
+        bw->value <<= 1;
+        bw->nb_bits += 1;
+        if (bw->nb_bits > 0) bw_flush(bw);
+    }
+    return bit;
+}
+
+static void bw_bits(BitWriter* bw, uint32_t value, int nb) {
+    for (uint32_t mask = 1u << (nb - 1); mask; mask >>= 1) bw_uniform(bw, (value & mask) != 0);
+}
+
+static void bw_signed(BitWriter* bw, int value, int nb) {
+    if (!bw_uniform(bw, value != 0)) return;
+    if (value < 0) bw_bits(bw, ((uint32_t)(-value) << 1) | 1u, nb + 1);
+    else bw_bits(bw, (uint32_t)value << 1, nb + 1);
+}
+
+static void bw_finish(BitWriter* bw) {
+    bw_bits(bw, 0, 9 - bw->nb_bits);
+    bw->nb_bits = 0;
+    bw_flush(bw);
+}
+
+static void put_le32(uint8_t* p, uint32_t v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24); }
+
+/*
+ * The whole WebP file libwebp writes (WebPEncodeRGB, method 4, lossy, no alpha) from the
+ * YUV420 planes and the restated segment set-up (tests/oracle_vp8.py): seg (per MB),
+ * num_segments / update_map / probs[3] (segment map), quant[4], fstr[4] (filter levels
+ * before libwebp raises them after coding), dq_uv_dc / dq_uv_ac.  *out is malloc'd;
+ * returns its size.
+ */
+long iko_vp8_encode(const uint8_t* y, const uint8_t* u, const uint8_t* v, int w, int h, float quality,
+                    const uint8_t* seg, int num_segments, int update_map, const int* probs, const int* quant,
+                    const int* fstr, int dq_uv_dc, int dq_uv_ac, uint8_t** out) {
+    const int mb_w = (w + 15) / 16, mb_h = (h + 15) / 16, n = mb_w * mb_h;
+    uint8_t* ym = malloc((size_t)n);
+    uint8_t* bm = malloc((size_t)n * 16);
+    uint8_t* uvm = malloc((size_t)n);
+    uint8_t probas[1056];
+    g_ntok = 0;  /* the token sink on */
+    g_tcap = 4096;
+    g_tok = malloc(g_tcap * sizeof(*g_tok));
+    iko_vp8_modes(y, u, v, w, h, quality, seg, quant, dq_uv_dc, dq_uv_ac, ym, bm, uvm, probas);
+    /* VP8AdjustFilterStrength (no autofilter): each segment's level at least the one its
+     * largest DC step needs (kLevelsFromDelta[sharpness 0] is the identity on 0..63) */
+    int level[4], max_level = 0;
+    for (int s = 0; s < 4; ++s) {
+        const int delta = (g_max_edge[s] * g_y2q1[s]) >> 3;
+        const int lv = delta < 63 ? delta : 63;
+        level[s] = fstr[s] > lv ? fstr[s] : lv;
+        if (level[s] > max_level) max_level = level[s];
+    }
+    /* partition 0: header + modes (GeneratePartition0) */
+    BitWriter b0;
+    bw_init(&b0);
+    bw_uniform(&b0, 0);  /* colour space */
+    bw_uniform(&b0, 0);  /* clamping */
+    if (bw_uniform(&b0, num_segments > 1)) {
+        bw_uniform(&b0, update_map);
+        if (bw_uniform(&b0, 1)) {  /* segment data, absolute values */
+            bw_uniform(&b0, 1);
+            for (int s = 0; s < 4; ++s) bw_signed(&b0, quant[s], 7);
+            for (int s = 0; s < 4; ++s) bw_signed(&b0, level[s], 6);
+        }
+        if (update_map)
+            for (int s = 0; s < 3; ++s)
+                if (bw_uniform(&b0, probs[s] != 255)) bw_bits(&b0, (uint32_t)probs[s], 8);
+    }
+    bw_uniform(&b0, 0);          /* normal (not simple) loop filter */
+    bw_bits(&b0, (uint32_t)max_level, 6);
+    bw_bits(&b0, 0, 3);          /* sharpness */
+    bw_uniform(&b0, 0);          /* no lf deltas */
+    bw_bits(&b0, 0, 2);          /* one token partition */
+    bw_bits(&b0, (uint32_t)quant[0], 7);
+    bw_signed(&b0, 0, 4);
+    bw_signed(&b0, 0, 4);
+    bw_signed(&b0, 0, 4);
+    bw_signed(&b0, dq_uv_dc, 4);
+    bw_signed(&b0, dq_uv_ac, 4);
+    bw_uniform(&b0, 0);          /* no entropy refresh */
+    for (int i = 0; i < 1056; ++i)
+        if (bw_put(&b0, probas[i] != kCoeffsProba0[i], kCoeffsUpdateProba[i])) bw_bits(&b0, probas[i], 8);
+    bw_uniform(&b0, 0);          /* no skip probability */
+    {
+        const int pw = mb_w * 4;
+        uint8_t* pr = calloc((size_t)pw * mb_h * 4, 1);
+        for (int i = 0; i < n; ++i) {
+            const int mx = i % mb_w, my = i / mb_w;
+            for (int k = 0; k < 16; ++k) pr[(my * 4 + (k >> 2)) * pw + mx * 4 + (k & 3)] = bm[(size_t)i * 16 + k];
+        }
+        for (int i = 0; i < n; ++i) {
+            const int mx = i % mb_w, my = i / mb_w;
+            if (update_map) {
+                const int sg = seg[i];
+                if (bw_put(&b0, sg >= 2, probs[0])) bw_put(&b0, sg & 1, probs[2]);
+                else bw_put(&b0, sg & 1, probs[1]);
+            }
+            if (bw_put(&b0, ym[i] != 4, 145)) {
+                const int mode = ym[i];
+                if (bw_put(&b0, mode == 1 || mode == 3, 156)) bw_put(&b0, mode == 1, 128);
+                else bw_put(&b0, mode == 2, 163);
+            } else {
+                for (int k = 0; k < 16; ++k) {
+                    const int by = my * 4 + (k >> 2), bx = mx * 4 + (k & 3);
+                    const int top = by > 0 ? pr[(by - 1) * pw + bx] : 0, left = bx > 0 ? pr[by * pw + bx - 1] : 0;
+                    const uint8_t* p = kBModesProba + (top * 10 + left) * 9;
+                    const int mode = bm[(size_t)i * 16 + k];
+                    if (bw_put(&b0, mode != 0, p[0]))
+                        if (bw_put(&b0, mode != 1, p[1]))
+                            if (bw_put(&b0, mode != 2, p[2])) {
+                                if (!bw_put(&b0, mode >= 6, p[3])) {
+                                    if (bw_put(&b0, mode != 3, p[4])) bw_put(&b0, mode != 4, p[5]);
+                                } else if (bw_put(&b0, mode != 6, p[6])) {
+                                    if (bw_put(&b0, mode != 7, p[7])) bw_put(&b0, mode != 8, p[8]);
+                                }
+                            }
+                }
+            }
+            const int uvmd = uvm[i];
+            if (bw_put(&b0, uvmd != 0, 142))
+                if (bw_put(&b0, uvmd != 2, 114)) bw_put(&b0, uvmd != 3, 183);
+        }
+        free(pr);
+    }
+    bw_finish(&b0);
+    /* partition 1: the tokens with the final probabilities (VP8EmitTokens) */
+    BitWriter b1;
+    bw_init(&b1);
+    for (size_t i = 0; i < g_ntok; ++i) {
+        const uint32_t t = g_tok[i];
+        const int bit = (int)((t >> 15) & 1);
+        if (t & (1u << 14)) bw_put(&b1, bit, (int)(t & 0xffu));
+        else bw_put(&b1, bit, probas[t & 0x3fffu]);
+    }
+    bw_finish(&b1);
+    free(g_tok);
+    g_tok = NULL; g_ntok = 0; g_tcap = 0;
+    /* RIFF + VP8 chunk (PutWebPHeaders, PutVP8FrameHeader; profile 0: normal filter) */
+    size_t vp8_size = 10 + b0.pos + b1.pos;
+    const size_t pad = vp8_size & 1;
+    vp8_size += pad;
+    const size_t riff_size = 4 + 8 + vp8_size;
+    const size_t total = 8 + riff_size;
+    uint8_t* o = malloc(total);
+    memcpy(o, "RIFF", 4);
+    put_le32(o + 4, (uint32_t)riff_size);
+    memcpy(o + 8, "WEBPVP8 ", 8);
+    put_le32(o + 16, (uint32_t)vp8_size);
+    {
+        const uint32_t bits = 0u | (0u << 1) | (1u << 4) | ((uint32_t)b0.pos << 5);
+        uint8_t* f = o + 20;
+        f[0] = (uint8_t)bits; f[1] = (uint8_t)(bits >> 8); f[2] = (uint8_t)(bits >> 16);
+        f[3] = 0x9d; f[4] = 0x01; f[5] = 0x2a;
+        f[6] = (uint8_t)(w & 0xff); f[7] = (uint8_t)(w >> 8); f[8] = (uint8_t)(h & 0xff); f[9] = (uint8_t)(h >> 8);
+    }
+    memcpy(o + 30, b0.buf, b0.pos);
+    memcpy(o + 30 + b0.pos, b1.buf, b1.pos);
+    if (pad) o[30 + b0.pos + b1.pos] = 0;
+    free(b0.buf); free(b1.buf);
+    free(ym); free(bm); free(uvm);
+    *out = o;
+    return (long)total;
 }

@@ -8,7 +8,11 @@ token statistics of the whole frame, refreshed every mb_count/8 macroblocks duri
 pass), must equal what libwebp's first partition says (tests/vp8_parse.py) -- across
 sizes 1x1 ... 1000x600, smooth and noise content, and qualities 1 ... 100 (error
 diffusion on at <= 98, off above).  The segment set-up is the restated first stage
-(tests/oracle_vp8.py, itself pinned by tests/test_vp8_analysis.py)."""
+(tests/oracle_vp8.py, itself pinned by tests/test_vp8_analysis.py).
+
+The last tests close the loop: the restated filter levels, header, modes, token
+partition and RIFF container are the same *file* WebPEncodeRGB writes, byte for byte --
+the whole reference WebP coder restated, the model a GPU coder is checked against."""
 import ctypes
 import os
 import re
@@ -73,3 +77,45 @@ def test_modes_and_probabilities_equal_libwebp(orc, wh, pat, q):
     for name, g, e in zip(("luma mode", "sub-block modes", "chroma mode", "final probabilities"), got, want):
         bad = np.argwhere(np.asarray(g) != np.asarray(e))
         assert bad.size == 0, f"{w}x{h} {pat} q{q}: {name} differs first at {bad[0].tolist()} ({len(bad)} entries)"
+
+
+def restated_webp(orc, y, u, v, q):
+    """The whole file, restated: oracle_vp8's segment set-up + vp8_modes.c's decisions,
+    filter levels, token partition and RIFF container (iko_vp8_encode)."""
+    h, w = y.shape
+    a = oracle_vp8.analyze(y, u, v, q)
+    lib = orc.lib
+    lib.iko_vp8_encode.restype = ctypes.c_long
+    lib.iko_vp8_encode.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 2 + [ctypes.c_float] + [ctypes.c_void_p] + \
+        [ctypes.c_int] * 2 + [ctypes.c_void_p] * 3 + [ctypes.c_int] * 2 + [ctypes.c_void_p]
+    seg = np.ascontiguousarray(a["segments"].reshape(-1).astype(np.uint8))
+    arr = lambda x: np.ascontiguousarray(np.array(x, np.int32))  # noqa: E731
+    probs, quant, fstr = arr(a["probs"]), arr(a["quant"]), arr(a["fstrength_pre"])
+    y, u, v = (np.ascontiguousarray(t) for t in (y, u, v))
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    n = lib.iko_vp8_encode(y.ctypes.data, u.ctypes.data, v.ctypes.data, w, h, q, seg.ctypes.data, a["num_segments"],
+                           int(a["update_map"]), probs.ctypes.data, quant.ctypes.data, fstr.ctypes.data, a["uv_dc"],
+                           a["uv_ac"], ctypes.byref(out))
+    assert n > 0
+    b = ctypes.string_at(out, n)
+    lib.iko_free(out)
+    return b
+
+
+@pytest.mark.parametrize("wh", [(1, 1), (7, 5), (17, 31), (64, 48), (333, 222), (512, 512)])
+@pytest.mark.parametrize("pat", ["S", "N"])
+@pytest.mark.parametrize("q", [1.0, 50.0, 80.0, 100.0])
+def test_whole_file_equals_libwebp(orc, wh, pat, q):
+    # header (segment and filter levels raised after coding, quantisers, probability
+    # updates), every macroblock's modes, the token partition and the RIFF container
+    w, h = wh
+    rgb = ikutil.synth(w, h, 3, seed=5 * w + h, pattern=pat)
+    assert restated_webp(orc, *orc.libwebp_import_yuv(rgb), q) == orc.webp_encode_rgb(rgb, q)
+
+
+def test_golden_webp_bytes(orc):
+    g = np.load(os.path.join(ROOT, "tests", "golden", "codec_golden.npz"))
+    for name in ("a", "b", "c", "d"):
+        W, H, pat, seed, q = (int(x) for x in g[f"{name}_meta"])
+        rgb = ikutil.synth(W, H, 3, seed=seed, pattern="SN"[pat])
+        assert restated_webp(orc, *orc.libwebp_import_yuv(rgb), float(q)) == bytes(g[f"{name}_webp"]), name
