@@ -355,6 +355,13 @@ typedef struct {
 } ik_vp8_segment_header;
 int ik_vp8_analyze_device(const uint8_t *dev_yuv, size_t yuv_stride, uint32_t n, uint32_t w, uint32_t h,
                           float quality, uint8_t *seg, ik_vp8_segment_header *hdr);
+/* the exact WebP coder on the GPU: libwebp method 4's segment analysis and macroblock
+ * decisions on the device (a wavefront per probability-refresh epoch), the bitstream on
+ * the host -- the file WebPEncodeRGB writes for these planes at this quality.  n images
+ * of w x h device YUV420 planes (the ik_webp_yuv420_device layout) yuv_stride apart;
+ * outs[i] / out_lens[i] receive each file (library-allocated, ik_buf_free). */
+int ik_webp_encode_exact_device(const uint8_t *dev_yuv, size_t yuv_stride, uint32_t n, uint32_t w, uint32_t h,
+                                int quality, uint8_t **outs, size_t *out_lens);
 /* the JPEG front end (to_rgb8 + RGB->YCbCr + FDCT + quantise) on the device:
  * int16 coefficients, MCU-major, Y/Cb/Cr, natural order */
 int ik_jpeg_coeffs_device(const uint8_t *dev_src, uint32_t w, uint32_t h, uint32_t C,

@@ -1,0 +1,448 @@
+// ik_vp8x.hip -- the exact WebP coder's device half: libwebp method 4's macroblock
+// decisions (reference src/transform.rs:129-137 -> webp 0.3.1 -> libwebp; the arithmetic
+// is ik_vp8x.h, the same as oracle/vp8_modes.c, whose files equal WebPEncodeRGB's).
+//
+// Dependencies and how they are scheduled:
+//  - a macroblock predicts from the reconstruction of its left, top-left, top and
+//    top-right neighbours, and reads their non-zero contexts and chroma DC errors: all
+//    MBs with the same mb_x + 2 mb_y are independent (a diagonal);
+//  - libwebp's token loop refreshes the coefficient probabilities -- hence the level
+//    costs every decision uses -- from the statistics of all MBs before it, at MB
+//    indices M, 2M+1, 3M+2, ... (M = max(mb_count / 8, 96)): an epoch's MBs may only
+//    start when every earlier MB is decided and the statistics folded.
+// So per epoch: one k_vp8x_mb launch per diagonal (every image of the batch in the
+// launch, grid.y = image), then k_vp8x_stats (one wave per image) folds the epoch's
+// token statistics in raster order (libwebp halves a counter pair at 65534, so the
+// order matters) and refreshes probabilities and level costs.
+//
+// k_vp8x_mb: one wave64 per MB; the modes of each stage run on their own lanes --
+// i16: 4 lanes, intra-4: 10 lanes per sub-block (16 sub-blocks in order), chroma: 4
+// lanes -- and the winner is the lowest score, ties to the lowest mode (libwebp's
+// early-out in the intra-4 loop never changes that argmin: a skipped mode's partial
+// score already reaches the best full score).
+#include <hip/hip_runtime.h>
+
+#include "ik_vp8x.h"
+#include "ik_vp8x_gpu.h"
+
+namespace ik {
+namespace vp8x {
+
+namespace {
+
+constexpr int kTopLeftI4[16] = {17, 21, 25, 29, 13, 17, 21, 25, 9, 13, 17, 21, 5, 9, 13, 17};
+
+__device__ __forceinline__ int64_t rd_score(int64_t R, int64_t H, int64_t D, int64_t SD, int lambda) {
+    return (R + H) * lambda + 256 * (D + SD);
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__ list) {
+    const int l = threadIdx.x;
+    const int img = blockIdx.y;
+    const int mb = list[blockIdx.x];
+    const int mx = mb % a.mb_w, my = mb / a.mb_w;
+    const int nmb = a.mb_w * a.mb_h;
+    const int W = a.mb_w * 16, H = a.mb_h * 16;
+    const int uw = (a.w + 1) >> 1, uh = (a.h + 1) >> 1;
+    const uint8_t* Y = a.yuv + (size_t)img * a.yuv_stride;
+    const uint8_t* U = Y + (size_t)a.w * a.h;
+    const uint8_t* V = U + (size_t)uw * uh;
+    uint8_t* RY = a.rec + (size_t)img * a.rec_stride;
+    uint8_t* RU = RY + (size_t)W * H;
+    uint8_t* RV = RU + (size_t)(W / 2) * (H / 2);
+    XMB* mbs = a.mbs + (size_t)img * nmb;
+    uint32_t* nzs = a.nz + (size_t)img * nmb;
+    int8_t* derrs = a.derr + (size_t)img * nmb * 8;
+    const uint16_t* lc = a.lc + (size_t)img * kCostRows * kLevelTab;
+    const uint8_t* pr = a.pr + (size_t)img * 1056;
+    const int sg = a.seg[(size_t)img * nmb + mb];
+    const XSeg& Q = a.segs[img * 4 + sg];
+
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[BPS * 16];      // Y 0..15, U 16..23, V 24..31
+    __shared__ uint8_t s_yl[17], s_yt[20], s_ul[9], s_ut[8], s_vl[9], s_vt[8];
+    __shared__ int s_tnz[9], s_lnz[9];
+    __shared__ int8_t s_derr_t[2][2], s_derr_l[2][2];
+    __shared__ __attribute__((aligned(16))) uint8_t s_rec16[4][BPS * 16];
+    __shared__ int16_t s_lv16[4][17][16];
+    __shared__ int64_t s_sc[16], s_part[16][4];
+    __shared__ int s_flat[4], s_nz16[4];
+    __shared__ __attribute__((aligned(16))) uint8_t s_best4[BPS * 16];
+    __shared__ uint8_t s_bound[37];
+    __shared__ int16_t s_lv4[16][16];
+    __shared__ uint8_t s_modes4[16];
+    __shared__ __attribute__((aligned(16))) uint8_t s_blk[10][4 * BPS];
+    __shared__ int16_t s_blv[10][16];
+    __shared__ int s_i4nz[10];
+    __shared__ __attribute__((aligned(16))) uint8_t s_recuv[4][BPS * 8];
+    __shared__ int16_t s_lvuv[4][8][16];
+    __shared__ int8_t s_duv[4][2][3];
+    __shared__ int s_b16, s_buv, s_i4ok;
+    __shared__ int64_t s_s16;  // the i16 best's score at lambda_mode (the intra-4 bar)
+
+    // ---- load the source MB (ImportBlock: clamped coordinates) and the boundaries ----
+    for (int i = l; i < 256; i += 64) {
+        const int y = i >> 4, x = i & 15;
+        s_in[y * BPS + x] = Y[(size_t)min(16 * my + y, a.h - 1) * a.w + min(16 * mx + x, a.w - 1)];
+    }
+    for (int i = l; i < 128; i += 64) {
+        const int c = i >> 6, k = i & 63, y = k >> 3, x = k & 7;
+        const uint8_t* P = c ? V : U;
+        s_in[y * BPS + 16 + 8 * c + x] = P[(size_t)min(8 * my + y, uh - 1) * uw + min(8 * mx + x, uw - 1)];
+    }
+    if (l < 16) {
+        s_yl[1 + l] = mx ? RY[(size_t)(16 * my + l) * W + 16 * mx - 1] : 129;
+        s_yt[l] = my ? RY[(size_t)(16 * my - 1) * W + 16 * mx + l] : 127;
+    } else if (l < 20) {
+        const int k = l - 16;
+        s_yt[16 + k] = !my ? 127 : (mx < a.mb_w - 1 ? RY[(size_t)(16 * my - 1) * W + 16 * mx + 16 + k]
+                                                       : RY[(size_t)(16 * my - 1) * W + 16 * mx + 15]);
+    } else if (l < 28) {
+        const int k = l - 20;
+        s_ul[1 + k] = mx ? RU[(size_t)(8 * my + k) * (W / 2) + 8 * mx - 1] : 129;
+        s_vl[1 + k] = mx ? RV[(size_t)(8 * my + k) * (W / 2) + 8 * mx - 1] : 129;
+        s_ut[k] = my ? RU[(size_t)(8 * my - 1) * (W / 2) + 8 * mx + k] : 127;
+        s_vt[k] = my ? RV[(size_t)(8 * my - 1) * (W / 2) + 8 * mx + k] : 127;
+    } else if (l == 28) {
+        s_yl[0] = !mx ? (my ? 129 : 127) : (my ? RY[(size_t)(16 * my - 1) * W + 16 * mx - 1] : 127);
+        s_ul[0] = !mx ? (my ? 129 : 127) : (my ? RU[(size_t)(8 * my - 1) * (W / 2) + 8 * mx - 1] : 127);
+        s_vl[0] = !mx ? (my ? 129 : 127) : (my ? RV[(size_t)(8 * my - 1) * (W / 2) + 8 * mx - 1] : 127);
+    } else if (l == 29) {  // NzToBytes (+ the row's running left DC bit in bit 25)
+        const uint32_t tnz = my ? nzs[mb - a.mb_w] : 0u, lnz = mx ? nzs[mb - 1] : 0u;
+        const int tb[9] = {12, 13, 14, 15, 18, 19, 22, 23, 24}, lb[8] = {3, 7, 11, 15, 17, 19, 21, 23};
+        for (int i = 0; i < 9; ++i) s_tnz[i] = (int)((tnz >> tb[i]) & 1u);
+        for (int i = 0; i < 8; ++i) s_lnz[i] = (int)((lnz >> lb[i]) & 1u);
+        s_lnz[8] = (int)((lnz >> 25) & 1u);
+    } else if (l == 30) {
+        for (int c = 0; c < 2; ++c)
+            for (int k = 0; k < 2; ++k) {
+                s_derr_t[c][k] = (a.use_derr && my) ? derrs[(size_t)(mb - a.mb_w) * 8 + c * 2 + k] : 0;
+                s_derr_l[c][k] = (a.use_derr && mx) ? derrs[(size_t)(mb - 1) * 8 + 4 + c * 2 + k] : 0;
+            }
+    }
+    __syncthreads();
+
+    // ---- intra-16: lane = mode ----
+    if (l < 4) {
+        const int m = l;
+        uint8_t pred[BPS * 16];
+        pred_nxn(pred, m, mx ? s_yl + 1 : nullptr, my ? s_yt : nullptr, 16);
+        int16_t tmp[16][16], dc[16];
+        uint32_t nz = 0;
+        for (int n = 0; n < 16; ++n) {
+            const int off = (n & 3) * 4 + (n >> 2) * 4 * BPS;
+            ftransform(s_in + off, pred + off, tmp[n]);
+        }
+        ftransform_wht(tmp[0], dc);
+        nz |= (uint32_t)quantize_block(dc, s_lv16[m][0], Q.y2) << 24;
+        for (int n = 0; n < 16; ++n) {
+            tmp[n][0] = 0;
+            nz |= (uint32_t)quantize_block(tmp[n], s_lv16[m][1 + n], Q.y1) << n;
+        }
+        itransform_wht(dc, tmp[0]);
+        for (int n = 0; n < 16; ++n) {
+            const int off = (n & 3) * 4 + (n >> 2) * 4 * BPS;
+            itransform(pred + off, tmp[n], s_rec16[m] + off);
+        }
+        int64_t D = sse_wh(s_in, s_rec16[m], 16, 16), SD = 0;
+        if (Q.tlambda) {
+            int d = 0;
+            for (int y = 0; y < 16; y += 4)
+                for (int x = 0; x < 16; x += 4) d += disto4x4(s_in + x + y * BPS, s_rec16[m] + x + y * BPS);
+            SD = (Q.tlambda * d + 128) >> 8;
+        }
+        // rate (VP8GetCostLuma16 from the MB's incoming contexts)
+        int tnz[4], lnz[4];
+        for (int i = 0; i < 4; ++i) { tnz[i] = s_tnz[i]; lnz[i] = s_lnz[i]; }
+        int R = residual_cost(lc, pr, 1, 0, s_tnz[8] + s_lnz[8], s_lv16[m][0]);
+        for (int y = 0; y < 4; ++y)
+            for (int x = 0; x < 4; ++x) {
+                const int16_t* c = s_lv16[m][1 + x + 4 * y];
+                R += residual_cost(lc, pr, 0, 1, tnz[x] + lnz[y], c);
+                int any = 0;
+                for (int k = 1; k < 16; ++k) any |= c[k] != 0;
+                tnz[x] = lnz[y] = any;
+            }
+        s_flat[m] = is_flat(s_lv16[m][1], 16, 10);
+        s_nz16[m] = (int)nz;
+        s_part[m][0] = D;
+        s_part[m][1] = SD;
+        s_part[m][2] = R;
+        s_part[m][3] = kFixedCostsI16[m];
+    }
+    __syncthreads();
+    if (l == 0) {
+        // IsFlatSource16; the doubling chain of PickBestIntra16 (flat so far in mode order)
+        int flat = 1;
+        for (int i = 1; i < 256 && flat; ++i) flat = s_in[(i >> 4) * BPS + (i & 15)] == s_in[0];
+        int best = 0;
+        int64_t bs = 0, bD = 0, bSD = 0, bR = 0, bH = 0;
+        for (int m = 0; m < 4; ++m) {
+            int64_t D = s_part[m][0], SD = s_part[m][1];
+            if (flat) {
+                flat = s_flat[m];
+                if (flat) { D *= 2; SD *= 2; }
+            }
+            const int64_t sc = rd_score(s_part[m][2], s_part[m][3], D, SD, Q.lambda_i16);
+            if (m == 0 || sc < bs) { bs = sc; best = m; bD = D; bSD = SD; bR = s_part[m][2]; bH = s_part[m][3]; }
+        }
+        s_b16 = best;
+        s_s16 = rd_score(bR, bH, bD, bSD, Q.lambda_mode);  // the i16 score for the mode decision
+        // StoreMaxDelta: a DC-only MB of fairly high distortion
+        if (((uint32_t)s_nz16[best] & 0x100ffffu) == 0x1000000u && bD > Q.min_disto) {
+            const int16_t* d = s_lv16[best][0];
+            int mv = xabs(d[1]) > xabs(d[2]) ? xabs(d[1]) : xabs(d[2]);
+            mv = xabs(d[4]) > mv ? xabs(d[4]) : mv;
+            atomicMax(a.max_edge + img * 4 + sg, mv);
+        }
+        // VP8IteratorStartI4: the intra-4 boundary, contexts re-imported
+        for (int i = 0; i < 17; ++i) s_bound[i] = s_yl[16 - i];
+        for (int i = 0; i < 20; ++i) s_bound[17 + i] = s_yt[i];
+        s_i4ok = 1;
+    }
+    __syncthreads();
+
+    // ---- intra-4: 16 sub-blocks in order, lane = mode ----
+    {
+        int tnz4[4], lnz4[4];
+        for (int i = 0; i < 4; ++i) { tnz4[i] = s_tnz[i]; lnz4[i] = s_lnz[i]; }
+        int64_t aS = 211ll * Q.lambda_mode;  // rd_best: H = 211 = VP8BitCost(0, 145)
+        int header_bits = 0;
+        for (int i4 = 0; i4 < 16; ++i4) {
+            const int bx = i4 & 3, by = i4 >> 2;
+            const int off = bx * 4 + by * 4 * BPS;
+            if (l < 10) {
+                const int m = l;
+                const uint8_t* top = s_bound + kTopLeftI4[i4];
+                // mode costs from the neighbouring sub-blocks' modes (frame edge: B_DC)
+                const int left = bx ? s_modes4[i4 - 1] : (mx ? mbs[mb - 1].bmodes[by * 4 + 3] : 0);
+                const int topm = by ? s_modes4[i4 - 4] : (my ? mbs[mb - a.mb_w].bmodes[12 + bx] : 0);
+                uint8_t pred[4 * BPS];
+                pred4(pred, m, top);
+                int16_t tmp[16];
+                ftransform(s_in + off, pred, tmp);
+                s_i4nz[m] = quantize_block(tmp, s_blv[m], Q.y1);
+                itransform(pred, tmp, s_blk[m]);
+                int64_t D = 0;
+                for (int y = 0; y < 4; ++y)
+                    for (int x = 0; x < 4; ++x) {
+                        const int d = s_in[off + x + y * BPS] - s_blk[m][x + y * BPS];
+                        D += d * d;
+                    }
+                const int64_t SD = Q.tlambda ? ((Q.tlambda * disto4x4(s_in + off, s_blk[m]) + 128) >> 8) : 0;
+                const int64_t Hc = kFixedCostsI4[(topm * 10 + left) * 10 + m];
+                int64_t R = (m > 0 && is_flat(s_blv[m], 1, 3)) ? 140 : 0;
+                R += residual_cost(lc, pr, 3, 0, tnz4[bx] + lnz4[by], s_blv[m]);
+                s_sc[m] = rd_score(R, Hc, D, SD, Q.lambda_i4);
+                s_part[m][0] = D;
+                s_part[m][1] = SD;
+                s_part[m][2] = R;
+                s_part[m][3] = Hc;
+            }
+            __syncthreads();
+            int best = 0;
+            for (int m = 1; m < 10; ++m)
+                if (s_sc[m] < s_sc[best]) best = m;
+            const int64_t sD = s_part[best][0], sSD = s_part[best][1], sR = s_part[best][2], sH = s_part[best][3];
+            aS += rd_score(sR, sH, sD, sSD, Q.lambda_mode);
+            header_bits += (int)sH;
+            const bool stop = aS >= s_s16 || header_bits > 256 * 16 * 16;
+            if (l < 16) s_lv4[i4][l] = s_blv[best][l];
+            if (l < 16) s_best4[off + (l & 3) + (l >> 2) * BPS] = s_blk[best][(l & 3) + (l >> 2) * BPS];
+            const int nzb = s_i4nz[best];
+            __syncthreads();
+            if (stop) {
+                if (l == 0) s_i4ok = 0;
+                break;
+            }
+            tnz4[bx] = lnz4[by] = nzb;
+            if (l == 0) {
+                s_modes4[i4] = (uint8_t)best;
+                // VP8IteratorRotateI4
+                uint8_t* top = s_bound + kTopLeftI4[i4];
+                const uint8_t* blk = s_best4 + off;
+                for (int i = 0; i <= 3; ++i) top[-4 + i] = blk[i + 3 * BPS];
+                if ((i4 & 3) != 3) {
+                    for (int i = 0; i <= 2; ++i) top[i] = blk[3 + (2 - i) * BPS];
+                } else {
+                    for (int i = 0; i <= 3; ++i) top[i] = top[i + 4];
+                }
+            }
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+
+    // ---- chroma: lane = mode ----
+    if (l < 4) {
+        const int m = l;
+        uint8_t pred[BPS * 8];
+        pred_nxn(pred, m, mx ? s_ul + 1 : nullptr, my ? s_ut : nullptr, 8);
+        pred_nxn(pred + 8, m, mx ? s_vl + 1 : nullptr, my ? s_vt : nullptr, 8);
+        int16_t tmp[8][16];
+        for (int n = 0; n < 8; ++n) {
+            const int off = (n & 1) * 4 + ((n >> 1) & 1) * 4 * BPS + (n >> 2) * 8;
+            ftransform(s_in + 16 + off, pred + off, tmp[n]);
+        }
+        if (a.use_derr) {  // CorrectDCValues
+            for (int ch = 0; ch <= 1; ++ch) {
+                const int8_t* top = s_derr_t[ch];
+                const int8_t* left = s_derr_l[ch];
+                int16_t(*c)[16] = &tmp[ch * 4];
+                auto qs = [&](int16_t* v) {
+                    int Vv = *v;
+                    const int sign = Vv < 0;
+                    if (sign) Vv = -Vv;
+                    if (Vv > (int)Q.uv.zthresh[0]) {
+                        const int qV = (int)(((uint32_t)Vv * Q.uv.iq[0] + Q.uv.bias[0]) >> QFIX) * Q.uv.q[0];
+                        const int err = Vv - qV;
+                        *v = (int16_t)(sign ? -qV : qV);
+                        return (sign ? -err : err) >> 1;
+                    }
+                    *v = 0;
+                    return (sign ? -Vv : Vv) >> 1;
+                };
+                c[0][0] = (int16_t)(c[0][0] + ((7 * top[0] + 8 * left[0]) >> 3));
+                const int e0 = qs(&c[0][0]);
+                c[1][0] = (int16_t)(c[1][0] + ((7 * top[1] + 8 * e0) >> 3));
+                const int e1 = qs(&c[1][0]);
+                c[2][0] = (int16_t)(c[2][0] + ((7 * e0 + 8 * left[1]) >> 3));
+                const int e2 = qs(&c[2][0]);
+                c[3][0] = (int16_t)(c[3][0] + ((7 * e1 + 8 * e2) >> 3));
+                const int e3 = qs(&c[3][0]);
+                s_duv[m][ch][0] = (int8_t)e1;
+                s_duv[m][ch][1] = (int8_t)e2;
+                s_duv[m][ch][2] = (int8_t)e3;
+            }
+        }
+        for (int n = 0; n < 8; ++n) quantize_block(tmp[n], s_lvuv[m][n], Q.uv);
+        for (int n = 0; n < 8; ++n) {
+            const int off = (n & 1) * 4 + ((n >> 1) & 1) * 4 * BPS + (n >> 2) * 8;
+            itransform(pred + off, tmp[n], s_recuv[m] + off);
+        }
+        int64_t D = 0;
+        for (int y = 0; y < 8; ++y)
+            for (int x = 0; x < 16; ++x) {
+                const int d = s_in[16 + x + y * BPS] - s_recuv[m][x + y * BPS];
+                D += d * d;
+            }
+        int tnz[4], lnz[4];
+        for (int i = 0; i < 4; ++i) { tnz[i] = s_tnz[4 + i]; lnz[i] = s_lnz[4 + i]; }
+        int R = 0;
+        for (int ch = 0; ch <= 2; ch += 2)
+            for (int y = 0; y < 2; ++y)
+                for (int x = 0; x < 2; ++x) {
+                    const int16_t* c = s_lvuv[m][ch * 2 + x + y * 2];
+                    R += residual_cost(lc, pr, 2, 0, tnz[ch + x] + lnz[ch + y], c);
+                    int any = 0;
+                    for (int k = 0; k < 16; ++k) any |= c[k] != 0;
+                    tnz[ch + x] = lnz[ch + y] = any;
+                }
+        if (m > 0 && is_flat(s_lvuv[m][0], 8, 2)) R += 140 * 8;
+        s_sc[m] = rd_score(R, kFixedCostsUV[m], D, 0, Q.lambda_uv);
+    }
+    __syncthreads();
+    if (l == 0) {
+        int best = 0;
+        for (int m = 1; m < 4; ++m)
+            if (s_sc[m] < s_sc[best]) best = m;
+        s_buv = best;
+    }
+    __syncthreads();
+
+    // ---- outputs: reconstruction, the MB record, contexts, chroma errors ----
+    const bool i4 = s_i4ok != 0;
+    const int b16 = s_b16, buv = s_buv;
+    for (int i = l; i < 256; i += 64) {
+        const int y = i >> 4, x = i & 15;
+        RY[(size_t)(16 * my + y) * W + 16 * mx + x] = i4 ? s_best4[y * BPS + x] : s_rec16[b16][y * BPS + x];
+    }
+    for (int i = l; i < 128; i += 64) {
+        const int c = i >> 6, k = i & 63, y = k >> 3, x = k & 7;
+        (c ? RV : RU)[(size_t)(8 * my + y) * (W / 2) + 8 * mx + x] = s_recuv[buv][y * BPS + 8 * c + x];
+    }
+    XMB& o = mbs[mb];
+    for (int i = l; i < 16 * 16; i += 64) o.ac[i >> 4][i & 15] = i4 ? s_lv4[i >> 4][i & 15] : s_lv16[b16][1 + (i >> 4)][i & 15];
+    for (int i = l; i < 8 * 16; i += 64) o.uv[i >> 4][i & 15] = s_lvuv[buv][i >> 4][i & 15];
+    if (l < 16) {
+        o.dc[l] = i4 ? 0 : s_lv16[b16][0][l];
+        o.bmodes[l] = i4 ? s_modes4[l] : (uint8_t)b16;
+    }
+    if (l == 0) {
+        o.ymode = i4 ? 4 : (uint8_t)b16;
+        o.uvmode = (uint8_t)buv;
+        o.seg = (uint8_t)sg;
+        o.pad = 0;
+        // the contexts after this MB (RecordTokens' nz, packed as BytesToNz + bit 25 = left DC)
+        int tnz[9], lnz[9];
+        for (int i = 0; i < 9; ++i) { tnz[i] = s_tnz[i]; lnz[i] = s_lnz[i]; }
+        auto anynz = [](const int16_t* c) { int r = 0; for (int k = 0; k < 16; ++k) r |= c[k] != 0; return r; };
+        if (!i4) tnz[8] = lnz[8] = anynz(s_lv16[b16][0]);
+        for (int y = 0; y < 4; ++y)
+            for (int x = 0; x < 4; ++x) tnz[x] = lnz[y] = anynz(i4 ? s_lv4[x + 4 * y] : s_lv16[b16][1 + x + 4 * y]);
+        for (int ch = 0; ch <= 2; ch += 2)
+            for (int y = 0; y < 2; ++y)
+                for (int x = 0; x < 2; ++x) tnz[4 + ch + x] = lnz[4 + ch + y] = anynz(s_lvuv[buv][ch * 2 + x + y * 2]);
+        uint32_t nz = 0;
+        nz |= (uint32_t)((tnz[0] << 12) | (tnz[1] << 13) | (tnz[2] << 14) | (tnz[3] << 15));
+        nz |= (uint32_t)((tnz[4] << 18) | (tnz[5] << 19) | (tnz[6] << 22) | (tnz[7] << 23));
+        nz |= (uint32_t)(tnz[8] << 24);
+        nz |= (uint32_t)((lnz[0] << 3) | (lnz[1] << 7) | (lnz[2] << 11));
+        nz |= (uint32_t)((lnz[4] << 17) | (lnz[6] << 21));
+        nz |= (uint32_t)(lnz[8] << 25);
+        nzs[mb] = nz;
+        // StoreDiffusionErrors: [0..3] the top pair per channel (for the MB below), [4..7] the left pair
+        int8_t* d = derrs + (size_t)mb * 8;
+        for (int ch = 0; ch < 2; ++ch) {
+            const int8_t* e = s_duv[buv][ch];
+            const int8_t l1 = a.use_derr ? (int8_t)((3 * e[2]) >> 2) : 0;
+            d[4 + ch * 2 + 0] = a.use_derr ? e[0] : 0;
+            d[4 + ch * 2 + 1] = l1;
+            d[ch * 2 + 0] = a.use_derr ? e[1] : 0;
+            d[ch * 2 + 1] = a.use_derr ? (int8_t)(e[2] - l1) : 0;
+        }
+    }
+}
+
+// One wave per image: fold the epoch's token statistics in raster order, then refresh
+// the probabilities and the level costs the next epoch's decisions use.
+__global__ __launch_bounds__(64) void k_vp8x_stats(XArgs a, int k0, int k1) {
+    const int img = blockIdx.x, l = threadIdx.x;
+    const int nmb = a.mb_w * a.mb_h;
+    const XMB* mbs = a.mbs + (size_t)img * nmb;
+    const uint32_t* nzs = a.nz + (size_t)img * nmb;
+    uint32_t* stats = a.stats + (size_t)img * 1056;
+    uint8_t* pr = a.pr + (size_t)img * 1056;
+    uint16_t* lc = a.lc + (size_t)img * kCostRows * kLevelTab;
+    if (l == 0) {
+        for (int k = k0; k < k1; ++k) {
+            const int mx = k % a.mb_w, my = k / a.mb_w;
+            const uint32_t tnz = my ? nzs[k - a.mb_w] : 0u, lnz = mx ? nzs[k - 1] : 0u;
+            const int tb[9] = {12, 13, 14, 15, 18, 19, 22, 23, 24}, lb[8] = {3, 7, 11, 15, 17, 19, 21, 23};
+            int t[9], lf[9];
+            for (int i = 0; i < 9; ++i) t[i] = (int)((tnz >> tb[i]) & 1u);
+            for (int i = 0; i < 8; ++i) lf[i] = (int)((lnz >> lb[i]) & 1u);
+            lf[8] = (int)((lnz >> 25) & 1u);
+            record_mb(stats, mbs[k], t, lf, [](int, uint32_t) {});
+        }
+    }
+    __syncthreads();
+    for (int i = l; i < 1056; i += 64) pr[i] = (uint8_t)finalize_proba(stats[i], i);
+    __syncthreads();
+    for (int r = l; r < kCostRows; r += 64) level_cost_row(pr + r * 11, r % 3, lc + r * kLevelTab);
+}
+
+hipError_t launch_vp8x_mb(const XArgs& a, const int* list, int count, int n, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_vp8x_mb, dim3(count, n), dim3(64), 0, s, a, list);
+    return hipGetLastError();
+}
+
+hipError_t launch_vp8x_stats(const XArgs& a, int k0, int k1, int n, hipStream_t s) {
+    hipLaunchKernelGGL(k_vp8x_stats, dim3(n), dim3(64), 0, s, a, k0, k1);
+    return hipGetLastError();
+}
+
+}  // namespace vp8x
+}  // namespace ik

@@ -1,0 +1,366 @@
+// ik_vp8x_host.cpp -- the exact WebP coder's host half (encode_image's WebP branch,
+// reference src/transform.rs:129-137 -> webp 0.3.1 -> libwebp WebPEncodeRGB): libwebp's
+// segment analysis and macroblock decisions run on the GPU (ik_vp8_analysis.hip,
+// ik_vp8x.hip); here the epoch/diagonal schedule, the segment set-up, and the
+// bitstream: the tokens in RecordTokens order with the final probabilities, libwebp's
+// boolean coder, partition 0 (header, segment map, modes), the filter levels libwebp
+// raises after coding, and the RIFF container -- the same file WebPEncodeRGB writes
+// (tests/test_gpu_vp8x.py; the model is oracle/vp8_modes.c).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/imagekit_hip.h"
+#include "ik_runtime.h"
+#include "ik_vp8_gpu.h"
+#include "ik_vp8x_gpu.h"
+
+namespace ik {
+
+void vp8_segment_setup(const vp8::SegRecord& r, float quality, uint8_t* seg, ik_vp8_segment_header* hd);
+
+namespace {
+
+using namespace vp8x;
+
+// ---- libwebp's boolean coder (utils/bit_writer_utils.c) ----
+struct BitWriter {
+    int32_t range = 255 - 1, value = 0;
+    int run = 0, nb_bits = -8;
+    std::vector<uint8_t> buf;
+
+    void flush() {
+        const int s = 8 + nb_bits;
+        const int32_t bits = value >> s;
+        value -= bits << s;
+        nb_bits -= 8;
+        if ((bits & 0xff) != 0xff) {
+            if ((bits & 0x100) && !buf.empty()) buf.back()++;  // carry into the bytes written
+            for (; run > 0; --run) buf.push_back((bits & 0x100) ? 0x00 : 0xff);
+            buf.push_back((uint8_t)(bits & 0xff));
+        } else {
+            run++;  // 0xff bytes wait: a carry may still come
+        }
+    }
+    int put(int bit, int prob) {
+        const int split = (range * prob) >> 8;
+        if (bit) {
+            value += split + 1;
+            range -= split + 1;
+        } else {
+            range = split;
+        }
+        if (range < 127) {
+            int shift = 0;
+            while (((range + 1) << shift) < 128) ++shift;
+            range = ((range + 1) << shift) - 1;
+            value <<= shift;
+            nb_bits += shift;
+            if (nb_bits > 0) flush();
+        }
+        return bit;
+    }
+    int uniform(int bit) {
+        const int split = range >> 1;
+        if (bit) {
+            value += split + 1;
+            range -= split + 1;
+        } else {
+            range = split;
+        }
+        if (range < 127) {
+            range = ((range + 1) << 1) - 1;
+            value <<= 1;
+            nb_bits += 1;
+            if (nb_bits > 0) flush();
+        }
+        return bit;
+    }
+    void bits(uint32_t v, int nb) {
+        for (uint32_t mask = 1u << (nb - 1); mask; mask >>= 1) uniform((v & mask) != 0);
+    }
+    void sbits(int v, int nb) {
+        if (!uniform(v != 0)) return;
+        if (v < 0) bits(((uint32_t)(-v) << 1) | 1u, nb + 1);
+        else bits((uint32_t)v << 1, nb + 1);
+    }
+    void finish() {
+        bits(0, 9 - nb_bits);
+        nb_bits = 0;
+        flush();
+    }
+};
+
+void put_le32(uint8_t* p, uint32_t v) {
+    p[0] = (uint8_t)v;
+    p[1] = (uint8_t)(v >> 8);
+    p[2] = (uint8_t)(v >> 16);
+    p[3] = (uint8_t)(v >> 24);
+}
+
+// The WebP file of one image from the device's decisions.
+void write_file(int w, int h, const XMB* mbs, const uint8_t* probas, const ik_vp8_segment_header& hd,
+                const int* max_edge, const XSeg* segs, std::vector<uint8_t>& out) {
+    const int mb_w = (w + 15) / 16, mb_h = (h + 15) / 16;
+    // the token partition, in RecordTokens order, with the final probabilities
+    BitWriter b1;
+    {
+        std::vector<uint32_t> dummy(1056, 0);
+        std::vector<int> top((size_t)mb_w * 9, 0);
+        for (int my = 0; my < mb_h; ++my) {
+            int left[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+            for (int mx = 0; mx < mb_w; ++mx) {
+                record_mb(dummy.data(), mbs[my * mb_w + mx], &top[(size_t)mx * 9], left, [&](int bit, uint32_t id) {
+                    if (id & 0x4000u) b1.put(bit, (int)(id & 0xffu));
+                    else b1.put(bit, probas[id]);
+                });
+            }
+        }
+        b1.finish();
+    }
+    // VP8AdjustFilterStrength: each segment's level at least what its DC-only MBs' largest
+    // step needs (kLevelsFromDelta[sharpness 0] is the identity on 0..63)
+    int level[4], max_level = 0;
+    for (int s = 0; s < 4; ++s) {
+        const int delta = (max_edge[s] * segs[s].y2.q[1]) >> 3;
+        const int lv = delta < 63 ? delta : 63;
+        level[s] = hd.fstrength[s] > lv ? hd.fstrength[s] : lv;
+        if (level[s] > max_level) max_level = level[s];
+    }
+    // partition 0
+    BitWriter b0;
+    b0.uniform(0);  // colour space
+    b0.uniform(0);  // clamping
+    if (b0.uniform(hd.num_segments > 1)) {
+        b0.uniform(hd.update_map);
+        if (b0.uniform(1)) {
+            b0.uniform(1);  // absolute values
+            for (int s = 0; s < 4; ++s) b0.sbits(hd.quant[s], 7);
+            for (int s = 0; s < 4; ++s) b0.sbits(level[s], 6);
+        }
+        if (hd.update_map)
+            for (int s = 0; s < 3; ++s)
+                if (b0.uniform(hd.probs[s] != 255)) b0.bits((uint32_t)hd.probs[s], 8);
+    }
+    b0.uniform(0);  // normal loop filter
+    b0.bits((uint32_t)max_level, 6);
+    b0.bits(0, 3);  // sharpness
+    b0.uniform(0);  // no lf deltas
+    b0.bits(0, 2);  // one token partition
+    b0.bits((uint32_t)hd.quant[0], 7);
+    b0.sbits(0, 4);
+    b0.sbits(0, 4);
+    b0.sbits(0, 4);
+    b0.sbits(hd.dq_uv_dc, 4);
+    b0.sbits(hd.dq_uv_ac, 4);
+    b0.uniform(0);  // no entropy refresh
+    for (int i = 0; i < 1056; ++i)
+        if (b0.put(probas[i] != kCoeffProbs0[i], kCoeffUpdateProbs[i])) b0.bits(probas[i], 8);
+    b0.uniform(0);  // no skip probability
+    for (int i = 0; i < mb_w * mb_h; ++i) {
+        const int mx = i % mb_w, my = i / mb_w;
+        const XMB& m = mbs[i];
+        if (hd.update_map) {
+            if (b0.put(m.seg >= 2, hd.probs[0])) b0.put(m.seg & 1, hd.probs[2]);
+            else b0.put(m.seg & 1, hd.probs[1]);
+        }
+        if (b0.put(m.ymode != 4, 145)) {
+            const int mode = m.ymode;
+            if (b0.put(mode == 1 || mode == 3, 156)) b0.put(mode == 1, 128);
+            else b0.put(mode == 2, 163);
+        } else {
+            for (int k = 0; k < 16; ++k) {
+                const int bx = k & 3, by = k >> 2;
+                const int top = by ? m.bmodes[k - 4] : (my ? mbs[i - mb_w].bmodes[12 + bx] : 0);
+                const int left = bx ? m.bmodes[k - 1] : (mx ? mbs[i - 1].bmodes[by * 4 + 3] : 0);
+                const uint8_t* p = kBModeProbs + (top * 10 + left) * 9;
+                const int mode = m.bmodes[k];
+                if (b0.put(mode != 0, p[0]))
+                    if (b0.put(mode != 1, p[1]))
+                        if (b0.put(mode != 2, p[2])) {
+                            if (!b0.put(mode >= 6, p[3])) {
+                                if (b0.put(mode != 3, p[4])) b0.put(mode != 4, p[5]);
+                            } else if (b0.put(mode != 6, p[6])) {
+                                if (b0.put(mode != 7, p[7])) b0.put(mode != 8, p[8]);
+                            }
+                        }
+            }
+        }
+        if (b0.put(m.uvmode != 0, 142))
+            if (b0.put(m.uvmode != 2, 114)) b0.put(m.uvmode != 3, 183);
+    }
+    b0.finish();
+    // RIFF + VP8 chunk (profile 0: normal filter)
+    size_t vp8_size = 10 + b0.buf.size() + b1.buf.size();
+    const size_t pad = vp8_size & 1;
+    vp8_size += pad;
+    const size_t riff_size = 4 + 8 + vp8_size;
+    out.assign(8 + riff_size, 0);
+    uint8_t* o = out.data();
+    std::memcpy(o, "RIFF", 4);
+    put_le32(o + 4, (uint32_t)riff_size);
+    std::memcpy(o + 8, "WEBPVP8 ", 8);
+    put_le32(o + 16, (uint32_t)vp8_size);
+    const uint32_t bits = (1u << 4) | ((uint32_t)b0.buf.size() << 5);
+    o[20] = (uint8_t)bits;
+    o[21] = (uint8_t)(bits >> 8);
+    o[22] = (uint8_t)(bits >> 16);
+    o[23] = 0x9d;
+    o[24] = 0x01;
+    o[25] = 0x2a;
+    o[26] = (uint8_t)(w & 0xff);
+    o[27] = (uint8_t)(w >> 8);
+    o[28] = (uint8_t)(h & 0xff);
+    o[29] = (uint8_t)(h >> 8);
+    std::memcpy(o + 30, b0.buf.data(), b0.buf.size());
+    std::memcpy(o + 30 + b0.buf.size(), b1.buf.data(), b1.buf.size());
+}
+
+}  // namespace
+
+// n images of w x h YUV420 planes on the device (yuv_stride bytes apart) -> the WebP
+// files libwebp's WebPEncodeRGB writes at this quality.  Runs on the calling thread's
+// stream and waits.
+int webp_encode_exact(const uint8_t* d_yuv, size_t yuv_stride, int n, int w, int h, int quality,
+                      std::vector<std::vector<uint8_t>>& outs) {
+    if (n < 1 || n > 65535 || w < 1 || h < 1 || w > 16383 || h > 16383)
+        return fail(IK_ERR_INVALID, "bad WebP shape %dx%d x %d", w, h, n);
+    hipStream_t s = thread_stream();
+    if (!s) return fail(IK_ERR_DEVICE, "cannot create HIP stream");
+    const int mb_w = (w + 15) / 16, mb_h = (h + 15) / 16, nmb = mb_w * mb_h;
+    const size_t rec_stride = (size_t)mb_w * 16 * mb_h * 16 * 3 / 2;
+    const float q = (float)quality;
+    // device buffers (one allocation, 256-byte aligned parts)
+    size_t off = 0;
+    auto part = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+    const size_t o_alpha = part((size_t)nmb * n), o_uva = part((size_t)nmb * n * 2), o_kseg = part((size_t)nmb * n);
+    const size_t o_rec = part(sizeof(vp8::SegRecord) * n);
+    const size_t o_recon = part(rec_stride * n), o_mbs = part(sizeof(XMB) * nmb * n), o_nz = part(4ull * nmb * n);
+    const size_t o_derr = part(8ull * nmb * n), o_seg = part((size_t)nmb * n), o_segs = part(sizeof(XSeg) * 4 * n);
+    const size_t o_lc = part(2ull * kCostRows * kLevelTab * n), o_pr = part(1056ull * n), o_st = part(4ull * 1056 * n);
+    const size_t o_me = part(16ull * n);
+    // the wavefront schedule: epochs at libwebp's probability refreshes, diagonals inside
+    const int M = (nmb >> 3) < 96 ? 96 : (nmb >> 3);
+    std::vector<int> bounds{0};
+    for (int k = M; k < nmb; k += M + 1) bounds.push_back(k);
+    bounds.push_back(nmb);
+    std::vector<int> list;
+    struct Step { int off, count, epoch_end; };
+    std::vector<Step> steps;
+    for (size_t e = 0; e + 1 < bounds.size(); ++e) {
+        const int k0 = bounds[e], k1 = bounds[e + 1];
+        int dmin = 1 << 30, dmax = -1;
+        for (int k = k0; k < k1; ++k) {
+            const int d = k % mb_w + 2 * (k / mb_w);
+            dmin = d < dmin ? d : dmin;
+            dmax = d > dmax ? d : dmax;
+        }
+        for (int d = dmin; d <= dmax; ++d) {
+            const int o = (int)list.size();
+            for (int k = k0; k < k1; ++k)
+                if (k % mb_w + 2 * (k / mb_w) == d) list.push_back(k);
+            if ((int)list.size() > o) steps.push_back({o, (int)list.size() - o, -1});
+        }
+        steps.push_back({0, 0, k1});  // the epoch's statistics
+    }
+    const size_t o_list = part(4ull * list.size());
+    uint8_t* d = nullptr;
+    IK_HIP(hipMalloc((void**)&d, off));
+    struct Free { uint8_t* p; ~Free() { if (p) (void)hipFree(p); } } guard{d};
+    // 1. segment analysis (exact, ik_vp8_analysis.hip)
+    std::vector<vp8::SegRecord> recs(n);
+    std::vector<uint8_t> seg((size_t)nmb * n);
+    IK_HIP(vp8::launch_vp8_analysis(d_yuv, yuv_stride, n, w, h, d + o_alpha, (uint16_t*)(d + o_uva), d + o_kseg,
+                                    (vp8::SegRecord*)(d + o_rec), s));
+    IK_HIP(hipMemcpyAsync(seg.data(), d + o_kseg, seg.size(), hipMemcpyDeviceToHost, s));
+    IK_HIP(hipMemcpyAsync(recs.data(), d + o_rec, sizeof(vp8::SegRecord) * n, hipMemcpyDeviceToHost, s));
+    IK_HIP(hipStreamSynchronize(s));
+    std::vector<ik_vp8_segment_header> hdr(n);
+    std::vector<XSeg> segs((size_t)4 * n);
+    for (int i = 0; i < n; ++i) {
+        vp8_segment_setup(recs[i], q, seg.data() + (size_t)nmb * i, &hdr[i]);
+        for (int sg = 0; sg < 4; ++sg) segs[(size_t)i * 4 + sg] = setup_segment(hdr[i].quant[sg], hdr[i].dq_uv_dc, hdr[i].dq_uv_ac, 50);
+    }
+    // 2. initial state: default probabilities and their level costs, zero statistics
+    std::vector<uint8_t> pr0((size_t)1056 * n);
+    std::vector<uint16_t> lc0((size_t)kCostRows * kLevelTab * n);
+    for (int i = 0; i < n; ++i) {
+        std::memcpy(&pr0[(size_t)1056 * i], kCoeffProbs0, 1056);
+        for (int r = 0; r < kCostRows; ++r) level_cost_row(kCoeffProbs0 + r * 11, r % 3, &lc0[((size_t)i * kCostRows + r) * kLevelTab]);
+    }
+    IK_HIP(hipMemcpyAsync(d + o_seg, seg.data(), seg.size(), hipMemcpyHostToDevice, s));
+    IK_HIP(hipMemcpyAsync(d + o_segs, segs.data(), sizeof(XSeg) * segs.size(), hipMemcpyHostToDevice, s));
+    IK_HIP(hipMemcpyAsync(d + o_pr, pr0.data(), pr0.size(), hipMemcpyHostToDevice, s));
+    IK_HIP(hipMemcpyAsync(d + o_lc, lc0.data(), 2 * lc0.size(), hipMemcpyHostToDevice, s));
+    IK_HIP(hipMemcpyAsync(d + o_list, list.data(), 4 * list.size(), hipMemcpyHostToDevice, s));
+    IK_HIP(hipMemsetAsync(d + o_st, 0, 4ull * 1056 * n, s));
+    IK_HIP(hipMemsetAsync(d + o_me, 0, 16ull * n, s));
+    // 3. the decisions
+    XArgs a{};
+    a.yuv = d_yuv;
+    a.yuv_stride = yuv_stride;
+    a.w = w;
+    a.h = h;
+    a.mb_w = mb_w;
+    a.mb_h = mb_h;
+    a.rec = d + o_recon;
+    a.rec_stride = rec_stride;
+    a.mbs = (XMB*)(d + o_mbs);
+    a.nz = (uint32_t*)(d + o_nz);
+    a.derr = (int8_t*)(d + o_derr);
+    a.seg = d + o_seg;
+    a.segs = (const XSeg*)(d + o_segs);
+    a.lc = (uint16_t*)(d + o_lc);
+    a.pr = d + o_pr;
+    a.stats = (uint32_t*)(d + o_st);
+    a.max_edge = (int*)(d + o_me);
+    a.use_derr = q <= 98.f;  // ERROR_DIFFUSION_QUALITY
+    const int* dlist = (const int*)(d + o_list);
+    int k0 = 0;
+    for (const Step& st : steps) {
+        if (st.epoch_end >= 0) {
+            IK_HIP(launch_vp8x_stats(a, k0, st.epoch_end, n, s));
+            k0 = st.epoch_end;
+        } else {
+            IK_HIP(launch_vp8x_mb(a, dlist + st.off, st.count, n, s));
+        }
+    }
+    // 4. the records back; the files on the host
+    std::vector<XMB> mbs((size_t)nmb * n);
+    std::vector<uint8_t> pr((size_t)1056 * n);
+    std::vector<int> me((size_t)4 * n);
+    IK_HIP(hipMemcpyAsync(mbs.data(), d + o_mbs, sizeof(XMB) * mbs.size(), hipMemcpyDeviceToHost, s));
+    IK_HIP(hipMemcpyAsync(pr.data(), d + o_pr, pr.size(), hipMemcpyDeviceToHost, s));
+    IK_HIP(hipMemcpyAsync(me.data(), d + o_me, 4 * me.size(), hipMemcpyDeviceToHost, s));
+    IK_HIP(hipStreamSynchronize(s));
+    outs.resize(n);
+    for (int i = 0; i < n; ++i)
+        write_file(w, h, &mbs[(size_t)nmb * i], &pr[(size_t)1056 * i], hdr[i], &me[(size_t)4 * i], &segs[(size_t)4 * i],
+                   outs[i]);
+    return IK_OK;
+}
+
+}  // namespace ik
+
+using namespace ik;
+
+extern "C" int ik_webp_encode_exact_device(const uint8_t* dev_yuv, size_t yuv_stride, uint32_t n, uint32_t w,
+                                           uint32_t h, int quality, uint8_t** outs, size_t* out_lens) {
+    IK_API_ENTER();
+    if (!dev_yuv || !outs || !out_lens) return fail(IK_ERR_INVALID, "null pointer");
+    const int q = quality < 1 ? 1 : (quality > 100 ? 100 : quality);
+    const size_t ysz = (size_t)w * h + 2 * (size_t)((w + 1) / 2) * ((h + 1) / 2);
+    if (n > 1 && yuv_stride < ysz) return fail(IK_ERR_INVALID, "image stride %zu under the planes' %zu bytes", yuv_stride, ysz);
+    std::vector<std::vector<uint8_t>> files;
+    if (int rc = webp_encode_exact(dev_yuv, yuv_stride, (int)n, (int)w, (int)h, q, files)) return rc;
+    for (uint32_t i = 0; i < n; ++i) {
+        outs[i] = (uint8_t*)malloc(files[i].size() ? files[i].size() : 1);
+        if (!outs[i]) return fail(IK_ERR_NOMEM, "out of host memory");
+        std::memcpy(outs[i], files[i].data(), files[i].size());
+        out_lens[i] = files[i].size();
+    }
+    return IK_OK;
+}
