@@ -221,8 +221,11 @@ int ik_encode(const ik_image *img, int fmt, int quality, uint8_t **out, size_t *
  * IK_WEBP_GPU: the gfx950 VP8 macroblock encoder (RD mode search, transforms,
  *   quantisation on the GPU; boolean coding on the host) -- a different encoder
  *   with libwebp-level size and PSNR, not byte-identical to libwebp.
- * The process default comes from IK_WEBP_ENCODER=gpu|libwebp when first used. */
-typedef enum { IK_WEBP_LIBWEBP = 0, IK_WEBP_GPU = 1 } ik_webp_encoder;
+ * The process default comes from IK_WEBP_ENCODER=gpu|exact|libwebp when first used. */
+/* IK_WEBP_EXACT: libwebp's own method-4 decisions on the GPU (segment analysis, RD mode
+ *   search, token statistics; ik_webp_encode_exact_device) and its bitstream on the host
+ *   -- byte-identical to IK_WEBP_LIBWEBP's output, with the coding off the host cores. */
+typedef enum { IK_WEBP_LIBWEBP = 0, IK_WEBP_GPU = 1, IK_WEBP_EXACT = 2 } ik_webp_encoder;
 int ik_set_webp_encoder(int encoder); /* process-wide, for ik_encode / ik_transform */
 /* version of the libwebp that codes WebP (WebPGetEncoderVersion, e.g. 0x010600),
  * -1 when none could be loaded.  The codec libraries are explicit dependencies:

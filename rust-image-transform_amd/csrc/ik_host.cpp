@@ -509,13 +509,17 @@ int encode_device_front(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, 
         if (!dc) return fail(IK_ERR_DEVICE, "cannot upload WebP tables");
         const size_t uvw = (w + 1) / 2, uvh = (h + 1) / 2;
         const size_t bytes = (size_t)w * h + 2 * uvw * uvh;
-        if (default_webp_encoder() == IK_WEBP_GPU) {
+        if (default_webp_encoder() == IK_WEBP_GPU || default_webp_encoder() == IK_WEBP_EXACT) {
             uint8_t* dyuv = scratch(bytes);
             if (!dyuv) return fail(IK_ERR_DEVICE, "cannot allocate device scratch");
             hipError_t e = launch_webp_yuv420(dev, (int)w, (int)h, (int)c, pitch, 0, dyuv, 0, 1,
                                               dc->gamma_to_lin, dc->lin_to_gamma, s);
             if (e != hipSuccess) return hip_fail(e, "webp yuv420");
-            return webp_encode_gpu(dyuv, (int)w, (int)h, q, out);
+            if (default_webp_encoder() == IK_WEBP_GPU) return webp_encode_gpu(dyuv, (int)w, (int)h, q, out);
+            std::vector<std::vector<uint8_t>> files;
+            if (int rc = webp_encode_exact(dyuv, 0, 1, (int)w, (int)h, q, files)) return rc;
+            out.swap(files[0]);
+            return IK_OK;
         }
         // the colour kernel writes the planes straight into pinned host memory: no
         // copy-engine transfer, which would queue behind another batch's stream upload
@@ -1015,11 +1019,41 @@ static std::shared_ptr<uint8_t> pinned_block(size_t bytes) {
     });
 }
 
+// The exact coder for a same-geometry group (IK_WEBP_EXACT): one batched colour launch
+// into device memory, then the whole group through webp_encode_exact -- the files
+// are final, no host coder runs.
+static int webp_exact_group(const std::vector<ik_image*>& imgs, int quality, std::vector<std::vector<uint8_t>*>& outs) {
+    const size_t n = imgs.size();
+    const ik_image* i0 = imgs[0];
+    DeviceGuard g(i0->device);
+    const DeviceConsts* dc = device_consts(current_device());
+    if (!dc) return fail(IK_ERR_DEVICE, "cannot upload WebP tables");
+    const uint32_t w = i0->w, h = i0->h;
+    const size_t uvw = (w + 1) / 2, uvh = (h + 1) / 2, bytes = (size_t)w * h + 2 * uvw * uvh;
+    const size_t stride = (bytes + 255) & ~size_t(255);
+    hipStream_t s = thread_stream();
+    uint8_t* dyuv = scratch(stride * n + 16 * n + 256);
+    if (!dyuv) return fail(IK_ERR_DEVICE, "cannot allocate device scratch");
+    std::vector<uint64_t> htab(n);
+    for (size_t i = 0; i < n; ++i) htab[i] = (uint64_t)(uintptr_t)imgs[i]->d;
+    uint64_t* dtab = reinterpret_cast<uint64_t*>(dyuv + stride * n);
+    hipError_t e = hipMemcpyAsync(dtab, htab.data(), 8 * n, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = launch_webp_yuv420(nullptr, (int)w, (int)h, (int)i0->c, i0->pitch, 0, dyuv, stride, (int)n,
+                               dc->gamma_to_lin, dc->lin_to_gamma, s, dtab);
+    if (e != hipSuccess) return hip_fail(e, "webp yuv420 (exact group)");
+    std::vector<std::vector<uint8_t>> files;
+    const int q = quality < 1 ? 1 : (quality > 100 ? 100 : quality);
+    if (int rc = webp_encode_exact(dyuv, stride, (int)n, (int)w, (int)h, q, files)) return rc;
+    for (size_t i = 0; i < n; ++i) outs[i]->swap(files[i]);
+    return IK_OK;
+}
+
 int webp_front_group(const std::vector<ik_image*>& imgs, int quality, std::vector<EncodePrep*>& prep) {
     const size_t n = imgs.size();
     if (!n) return IK_OK;
     const ik_image* i0 = imgs[0];
-    if (default_webp_encoder() == IK_WEBP_GPU || i0->w > 16383 || i0->h > 16383 || i0->depth != 1)
+    if (default_webp_encoder() != IK_WEBP_LIBWEBP || i0->w > 16383 || i0->h > 16383 || i0->depth != 1)
         return IK_ERR_UNSUPPORTED;
     DeviceGuard g(i0->device);
     const DeviceConsts* dc = device_consts(current_device());
@@ -1589,6 +1623,18 @@ static void transform_post_phase(const int64_t* w, const int64_t* h, const int* 
                 std::vector<ik_image*> im;
                 std::vector<EncodePrep*> pp;
                 for (uint32_t k : qv.second) { im.push_back(rsz[k]); pp.push_back(&prep[k]); }
+                if (default_webp_encoder() == IK_WEBP_EXACT && im[0]->depth == 1 && im[0]->w <= 16383 &&
+                    im[0]->h <= 16383) {
+                    std::vector<std::vector<uint8_t>*> oo;
+                    for (uint32_t k : qv.second) oo.push_back(&bytes_out[k]);
+                    if (webp_exact_group(im, qv.first, oo) == IK_OK)
+                        for (uint32_t k : qv.second) {
+                            fronted[k] = 1;
+                            prep[k].fmt = IK_FORMAT_WEBP;
+                            prep[k].done = true;  // the files are final: no host coder
+                        }
+                    continue;
+                }
                 if (webp_front_group(im, qv.first, pp) == IK_OK)
                     for (uint32_t k : qv.second) fronted[k] = 1;
             }

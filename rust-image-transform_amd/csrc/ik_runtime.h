@@ -246,6 +246,9 @@ struct Vp8Work {
 };
 int default_webp_encoder();  // IK_WEBP_LIBWEBP unless ik_set_webp_encoder / IK_WEBP_ENCODER=gpu
 int webp_encode_gpu(const uint8_t* d_yuv, int w, int h, int quality, std::vector<uint8_t>& out);
+// the exact coder (ik_vp8x_host.cpp): libwebp's files from n device YUV420 images
+int webp_encode_exact(const uint8_t* d_yuv, size_t yuv_stride, int n, int w, int h, int quality,
+                      std::vector<std::vector<uint8_t>>& outs);
 
 // host decoders (ik_decode.cpp): tightly packed 8-bit pixels
 enum class Sniffed { Png, Jpeg, Gif, WebP, Tiff, Bmp, Ico, Hdr, Avif, OpenExr, Qoi, Farbfeld, Pnm, Dds, Unknown };

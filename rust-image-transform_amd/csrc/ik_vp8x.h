@@ -446,29 +446,28 @@ IK_HD int record_stats(int bit, uint32_t* s) {
     return bit;
 }
 
-// TOK(bit, id) is called for every token (id: TOKEN_ID + node, or 0x4000 | fixed probability)
-template <typename TOK>
-IK_HD int record_coeff(uint32_t* stats, int type, int first, int ctx, const int16_t* coeffs, TOK tok) {
+// ST(slot, bit) records one statistic (and returns bit); TOK(bit, id) sees every token
+// (id: TOKEN_ID + node, or 0x4000 | a fixed probability)
+template <typename ST, typename TOK>
+IK_HD int record_coeff(ST st, int type, int first, int ctx, const int16_t* coeffs, TOK tok) {
     int last = -1;
     for (int n = 15; n >= 0; --n)
         if (coeffs[n]) { last = n; break; }
     int n = first;
     uint32_t base = (uint32_t)(11 * (ctx + 3 * (n + 8 * type)));
-    uint32_t* s = stats + base;
-    auto add = [&](int bit, uint32_t id, uint32_t* st) { tok(bit, id); return record_stats(bit, st); };
+    uint32_t s = base;  // the statistics row (== base: ids and slots coincide but for node 10)
+    auto add = [&](int bit, uint32_t id, uint32_t slot) { tok(bit, id); return st(slot, bit); };
     if (!add(last >= 0, base + 0, s + 0)) return 0;
     while (n < 16) {
         const int c = coeffs[n++];
         const int sign = c < 0;
         const uint32_t v = (uint32_t)(sign ? -c : c);
         if (!add(v != 0, base + 1, s + 1)) {
-            base = (uint32_t)(11 * (0 + 3 * (kEncBands[n] + 8 * type)));
-            s = stats + base;
+            base = s = (uint32_t)(11 * (0 + 3 * (kEncBands[n] + 8 * type)));
             continue;
         }
         if (!add(v > 1, base + 2, s + 2)) {
-            base = (uint32_t)(11 * (1 + 3 * (kEncBands[n] + 8 * type)));
-            s = stats + base;
+            base = s = (uint32_t)(11 * (1 + 3 * (kEncBands[n] + 8 * type)));
         } else {
             if (!add(v > 4, base + 3, s + 3)) {
                 if (add(v != 2, base + 4, s + 4)) add(v == 4, base + 5, s + 5);
@@ -517,8 +516,7 @@ IK_HD int record_coeff(uint32_t* stats, int type, int first, int ctx, const int1
                     mask >>= 1;
                 }
             }
-            base = (uint32_t)(11 * (2 + 3 * (kEncBands[n] + 8 * type)));
-            s = stats + base;
+            base = s = (uint32_t)(11 * (2 + 3 * (kEncBands[n] + 8 * type)));
         }
         tok(sign, 0x4000u | 128);
         if (n == 16 || !add(n <= last, base + 0, s + 0)) return 1;
@@ -527,22 +525,22 @@ IK_HD int record_coeff(uint32_t* stats, int type, int first, int ctx, const int1
 }
 
 // one MB's tokens in RecordTokens order; tnz/lnz: the iterator's top_nz[9] / left_nz[9]
-template <typename TOK>
-IK_HD void record_mb(uint32_t* stats, const XMB& m, int* tnz, int* lnz, TOK tok) {
+template <typename ST, typename TOK>
+IK_HD void record_mb(ST st, const XMB& m, int* tnz, int* lnz, TOK tok) {
     int first = 0, type = 3;
     if (m.ymode != 4) {
         const int ctx = tnz[8] + lnz[8];
-        tnz[8] = lnz[8] = record_coeff(stats, 1, 0, ctx, m.dc, tok);
+        tnz[8] = lnz[8] = record_coeff(st, 1, 0, ctx, m.dc, tok);
         first = 1;
         type = 0;
     }
     for (int y = 0; y < 4; ++y)
-        for (int x = 0; x < 4; ++x) tnz[x] = lnz[y] = record_coeff(stats, type, first, tnz[x] + lnz[y], m.ac[x + 4 * y], tok);
+        for (int x = 0; x < 4; ++x) tnz[x] = lnz[y] = record_coeff(st, type, first, tnz[x] + lnz[y], m.ac[x + 4 * y], tok);
     for (int ch = 0; ch <= 2; ch += 2)
         for (int y = 0; y < 2; ++y)
             for (int x = 0; x < 2; ++x)
                 tnz[4 + ch + x] = lnz[4 + ch + y] =
-                    record_coeff(stats, 2, 0, tnz[4 + ch + x] + lnz[4 + ch + y], m.uv[ch * 2 + x + y * 2], tok);
+                    record_coeff(st, 2, 0, tnz[4 + ch + x] + lnz[4 + ch + y], m.uv[ch * 2 + x + y * 2], tok);
 }
 
 // FinalizeTokenProbas: the probabilities the stats say are worth their update cost

@@ -55,9 +55,17 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
     XMB* mbs = a.mbs + (size_t)img * nmb;
     uint32_t* nzs = a.nz + (size_t)img * nmb;
     int8_t* derrs = a.derr + (size_t)img * nmb * 8;
-    const uint16_t* lc = a.lc + (size_t)img * kCostRows * kLevelTab;
-    const uint8_t* pr = a.pr + (size_t)img * 1056;
     const int sg = a.seg[(size_t)img * nmb + mb];
+    // the image's level costs and probabilities, read at every coefficient of every
+    // candidate: staged in LDS (13.4 KB)
+    __shared__ __attribute__((aligned(16))) uint16_t lc[kCostRows * kLevelTab];
+    __shared__ __attribute__((aligned(16))) uint8_t pr[1056];
+    {
+        const uint4* g = (const uint4*)(a.lc + (size_t)img * kCostRows * kLevelTab);
+        for (int i = l; i < kCostRows * kLevelTab / 8; i += 64) ((uint4*)lc)[i] = g[i];
+        const uint4* gp = (const uint4*)(a.pr + (size_t)img * 1056);
+        for (int i = l; i < 1056 / 16; i += 64) ((uint4*)pr)[i] = gp[i];
+    }
     const XSeg& Q = a.segs[img * 4 + sg];
 
     __shared__ __attribute__((aligned(16))) uint8_t s_in[BPS * 16];      // Y 0..15, U 16..23, V 24..31
@@ -80,6 +88,12 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
     __shared__ int8_t s_duv[4][2][3];
     __shared__ int s_b16, s_buv, s_i4ok;
     __shared__ int64_t s_s16;  // the i16 best's score at lambda_mode (the intra-4 bar)
+    // per-lane work buffers in LDS (private arrays would live in scratch memory)
+    __shared__ __attribute__((aligned(16))) uint8_t s_pred16[4][BPS * 16];
+    __shared__ __attribute__((aligned(16))) int16_t s_tmp16[4][16][16];
+    __shared__ __attribute__((aligned(16))) uint8_t s_pred4[10][4 * BPS];
+    __shared__ __attribute__((aligned(16))) uint8_t s_predc[4][BPS * 8];
+    __shared__ __attribute__((aligned(16))) int16_t s_tmpc[4][8][16];
 
     // ---- load the source MB (ImportBlock: clamped coordinates) and the boundaries ----
     for (int i = l; i < 256; i += 64) {
@@ -126,9 +140,10 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
     // ---- intra-16: lane = mode ----
     if (l < 4) {
         const int m = l;
-        uint8_t pred[BPS * 16];
+        uint8_t* pred = s_pred16[m];
         pred_nxn(pred, m, mx ? s_yl + 1 : nullptr, my ? s_yt : nullptr, 16);
-        int16_t tmp[16][16], dc[16];
+        int16_t(*tmp)[16] = s_tmp16[m];
+        int16_t dc[16];
         uint32_t nz = 0;
         for (int n = 0; n < 16; ++n) {
             const int off = (n & 3) * 4 + (n >> 2) * 4 * BPS;
@@ -218,7 +233,7 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
                 // mode costs from the neighbouring sub-blocks' modes (frame edge: B_DC)
                 const int left = bx ? s_modes4[i4 - 1] : (mx ? mbs[mb - 1].bmodes[by * 4 + 3] : 0);
                 const int topm = by ? s_modes4[i4 - 4] : (my ? mbs[mb - a.mb_w].bmodes[12 + bx] : 0);
-                uint8_t pred[4 * BPS];
+                uint8_t* pred = s_pred4[m];
                 pred4(pred, m, top);
                 int16_t tmp[16];
                 ftransform(s_in + off, pred, tmp);
@@ -277,10 +292,10 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
     // ---- chroma: lane = mode ----
     if (l < 4) {
         const int m = l;
-        uint8_t pred[BPS * 8];
+        uint8_t* pred = s_predc[m];
         pred_nxn(pred, m, mx ? s_ul + 1 : nullptr, my ? s_ut : nullptr, 8);
         pred_nxn(pred + 8, m, mx ? s_vl + 1 : nullptr, my ? s_vt : nullptr, 8);
-        int16_t tmp[8][16];
+        int16_t(*tmp)[16] = s_tmpc[m];
         for (int n = 0; n < 8; ++n) {
             const int off = (n & 1) * 4 + ((n >> 1) & 1) * 4 * BPS + (n >> 2) * 8;
             ftransform(s_in + 16 + off, pred + off, tmp[n]);
@@ -415,20 +430,58 @@ __global__ __launch_bounds__(64) void k_vp8x_stats(XArgs a, int k0, int k1) {
     uint32_t* stats = a.stats + (size_t)img * 1056;
     uint8_t* pr = a.pr + (size_t)img * 1056;
     uint16_t* lc = a.lc + (size_t)img * kCostRows * kLevelTab;
-    if (l == 0) {
-        for (int k = k0; k < k1; ++k) {
-            const int mx = k % a.mb_w, my = k / a.mb_w;
-            const uint32_t tnz = my ? nzs[k - a.mb_w] : 0u, lnz = mx ? nzs[k - 1] : 0u;
-            const int tb[9] = {12, 13, 14, 15, 18, 19, 22, 23, 24}, lb[8] = {3, 7, 11, 15, 17, 19, 21, 23};
-            int t[9], lf[9];
-            for (int i = 0; i < 9; ++i) t[i] = (int)((tnz >> tb[i]) & 1u);
-            for (int i = 0; i < 8; ++i) lf[i] = (int)((lnz >> lb[i]) & 1u);
-            lf[8] = (int)((lnz >> 25) & 1u);
-            record_mb(stats, mbs[k], t, lf, [](int, uint32_t) {});
-        }
+    // the counters in LDS.  libwebp halves a counter pair when its total reaches 65534,
+    // which makes the fold order-dependent; an epoch adds at most 25 blocks x 16
+    // records per slot per MB, so when every total is below 65534 minus that bound no
+    // counter can reach the halving point and the MBs fold in parallel (LDS atomics);
+    // otherwise lane 0 walks them in raster order, staged in LDS.
+    __shared__ uint32_t s_st[1056];
+    __shared__ __attribute__((aligned(16))) XMB s_mb;
+    __shared__ int s_serial;
+    static_assert(sizeof(XMB) % 4 == 0, "XMB words");
+    if (l == 0) s_serial = 0;
+    __syncthreads();
+    const uint32_t bound = (uint32_t)(k1 - k0) * 25u * 16u;
+    for (int i = l; i < 1056; i += 64) {
+        s_st[i] = stats[i];
+        if ((s_st[i] >> 16) + bound >= 0xfffeu) s_serial = 1;
     }
     __syncthreads();
-    for (int i = l; i < 1056; i += 64) pr[i] = (uint8_t)finalize_proba(stats[i], i);
+    auto ctx_of = [&](int k, int* t, int* lf) {
+        const int mx = k % a.mb_w, my = k / a.mb_w;
+        const uint32_t tnz = my ? nzs[k - a.mb_w] : 0u, lnz = mx ? nzs[k - 1] : 0u;
+        const int tb[9] = {12, 13, 14, 15, 18, 19, 22, 23, 24}, lb[8] = {3, 7, 11, 15, 17, 19, 21, 23};
+        for (int i = 0; i < 9; ++i) t[i] = (int)((tnz >> tb[i]) & 1u);
+        for (int i = 0; i < 8; ++i) lf[i] = (int)((lnz >> lb[i]) & 1u);
+        lf[8] = (int)((lnz >> 25) & 1u);
+    };
+    if (!s_serial) {
+        uint32_t* st = s_st;
+        for (int k = k0 + l; k < k1; k += 64) {
+            int t[9], lf[9];
+            ctx_of(k, t, lf);
+            record_mb([st](uint32_t slot, int bit) { atomicAdd(st + slot, 0x00010000u + (uint32_t)bit); return bit; },
+                      mbs[k], t, lf, [](int, uint32_t) {});
+        }
+        __syncthreads();
+    } else {
+        for (int k = k0; k < k1; ++k) {
+            const uint32_t* src = (const uint32_t*)(mbs + k);
+            for (int i = l; i < (int)(sizeof(XMB) / 4); i += 64) ((uint32_t*)&s_mb)[i] = src[i];
+            __syncthreads();
+            if (l == 0) {
+                int t[9], lf[9];
+                ctx_of(k, t, lf);
+                record_mb([&](uint32_t slot, int bit) { return record_stats(bit, s_st + slot); }, s_mb, t, lf,
+                          [](int, uint32_t) {});
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = l; i < 1056; i += 64) {
+        stats[i] = s_st[i];
+        pr[i] = (uint8_t)finalize_proba(s_st[i], i);
+    }
     __syncthreads();
     for (int r = l; r < kCostRows; r += 64) level_cost_row(pr + r * 11, r % 3, lc + r * kLevelTab);
 }

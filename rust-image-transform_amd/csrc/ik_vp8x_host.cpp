@@ -108,12 +108,12 @@ void write_file(int w, int h, const XMB* mbs, const uint8_t* probas, const ik_vp
     // the token partition, in RecordTokens order, with the final probabilities
     BitWriter b1;
     {
-        std::vector<uint32_t> dummy(1056, 0);
         std::vector<int> top((size_t)mb_w * 9, 0);
         for (int my = 0; my < mb_h; ++my) {
             int left[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
             for (int mx = 0; mx < mb_w; ++mx) {
-                record_mb(dummy.data(), mbs[my * mb_w + mx], &top[(size_t)mx * 9], left, [&](int bit, uint32_t id) {
+                record_mb([](uint32_t, int bit) { return bit; }, mbs[my * mb_w + mx], &top[(size_t)mx * 9], left,
+                          [&](int bit, uint32_t id) {
                     if (id & 0x4000u) b1.put(bit, (int)(id & 0xffu));
                     else b1.put(bit, probas[id]);
                 });
@@ -267,9 +267,24 @@ int webp_encode_exact(const uint8_t* d_yuv, size_t yuv_stride, int n, int w, int
         steps.push_back({0, 0, k1});  // the epoch's statistics
     }
     const size_t o_list = part(4ull * list.size());
-    uint8_t* d = nullptr;
-    IK_HIP(hipMalloc((void**)&d, off));
-    struct Free { uint8_t* p; ~Free() { if (p) (void)hipFree(p); } } guard{d};
+    // a per-thread work area, grown as needed and kept (a hipFree would wait for the
+    // whole device, the next batch's decode kernels included)
+    struct Area {
+        uint8_t* p = nullptr;
+        size_t cap = 0;
+        int dev = -1;
+    };
+    static thread_local Area area;
+    const int dev = current_device();
+    if (area.cap < off || area.dev != dev) {
+        if (area.p) (void)hipFree(area.p);
+        area.p = nullptr;
+        area.cap = 0;
+        IK_HIP(hipMalloc((void**)&area.p, off));
+        area.cap = off;
+        area.dev = dev;
+    }
+    uint8_t* d = area.p;
     // 1. segment analysis (exact, ik_vp8_analysis.hip)
     std::vector<vp8::SegRecord> recs(n);
     std::vector<uint8_t> seg((size_t)nmb * n);
@@ -337,9 +352,10 @@ int webp_encode_exact(const uint8_t* d_yuv, size_t yuv_stride, int n, int w, int
     IK_HIP(hipMemcpyAsync(me.data(), d + o_me, 4 * me.size(), hipMemcpyDeviceToHost, s));
     IK_HIP(hipStreamSynchronize(s));
     outs.resize(n);
-    for (int i = 0; i < n; ++i)
+    parallel_for(n, n < 16 ? n : 16, [&](int i) {
         write_file(w, h, &mbs[(size_t)nmb * i], &pr[(size_t)1056 * i], hdr[i], &me[(size_t)4 * i], &segs[(size_t)4 * i],
                    outs[i]);
+    });
     return IK_OK;
 }
 

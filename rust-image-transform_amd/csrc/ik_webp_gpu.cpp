@@ -29,7 +29,8 @@ int default_webp_encoder() {
     int e = g_webp_encoder.load();
     if (e < 0) {
         const char* s = getenv("IK_WEBP_ENCODER");
-        e = (s && (!strcmp(s, "gpu") || !strcmp(s, "1"))) ? IK_WEBP_GPU : IK_WEBP_LIBWEBP;
+        e = (s && (!strcmp(s, "gpu") || !strcmp(s, "1"))) ? IK_WEBP_GPU
+            : (s && (!strcmp(s, "exact") || !strcmp(s, "2"))) ? IK_WEBP_EXACT : IK_WEBP_LIBWEBP;
         int expected = -1;
         g_webp_encoder.compare_exchange_strong(expected, e);
         e = g_webp_encoder.load();
@@ -219,7 +220,8 @@ using namespace ik;
 extern "C" {
 
 int ik_set_webp_encoder(int encoder) {
-    if (encoder != IK_WEBP_LIBWEBP && encoder != IK_WEBP_GPU) return fail(IK_ERR_INVALID, "bad WebP encoder %d", encoder);
+    if (encoder != IK_WEBP_LIBWEBP && encoder != IK_WEBP_GPU && encoder != IK_WEBP_EXACT)
+        return fail(IK_ERR_INVALID, "bad WebP encoder %d", encoder);
     (void)default_webp_encoder();
     g_webp_encoder.store(encoder);
     return IK_OK;

@@ -75,3 +75,29 @@ def test_bench_frames(ik, oracle):
         512, 512, FilterType.Triangle).to_array() for s in range(2)]
     for i, (got, img) in enumerate(zip(encode_exact(ik, smalls, 80), smalls)):
         assert got == oracle.webp_encode_rgb(oracle.to_rgb8(img), 80.0), f"bench frame {i}"
+
+
+def test_transform_batch_with_the_exact_coder(ik):
+    # encode_image's WebP branch through the batch path (same-geometry groups and a
+    # single request) with IK_WEBP_EXACT: the bytes equal the libwebp coder's (the
+    # default) for the same requests
+    import io
+    from PIL import Image
+    from imagekit import ImageFormat, transform_batch
+    datas = []
+    for s in range(3):
+        b = io.BytesIO()
+        Image.fromarray(ikutil.synth(1024, 768, 4, seed=s, pattern="S"), "RGBA").save(b, format="PNG")
+        datas.append(b.getvalue())
+    datas.append(datas[0])
+    sizes = [(512, None)] * 3 + [(300, 200)]
+    fmts = [ImageFormat.webp] * 4
+    qs = [80, 80, 80, 50]
+    assert ik.ik_set_webp_encoder(0) == 0
+    ref = transform_batch(datas, sizes, fmts, qs, FilterType.Triangle)
+    assert ik.ik_set_webp_encoder(2) == 0
+    try:
+        got = transform_batch(datas, sizes, fmts, qs, FilterType.Triangle)
+    finally:
+        ik.ik_set_webp_encoder(0)
+    assert got == ref
