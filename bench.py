@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--threads", type=int, default=32, help="host threads per GPU (stated budget)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of each cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--webp-encoder", default="libwebp", choices=["libwebp", "exact"],
+                    help="exact: libwebp's method-4 decisions on the GPU (IK_WEBP_EXACT, byte-identical files)")
     ap.add_argument("--no-extras", action="store_true", help="skip the hbm_resident / JPEG legs")
     ap.add_argument("--hbm-batch", type=int, default=64)
     ap.add_argument("--hbm-steps", type=int, default=6)
@@ -352,6 +354,8 @@ def main():
     lib = _lib.load()
     if lib.ik_init(-1 if args.inproc_devices > 0 else local) != 0:
         raise SystemExit(f"ik_init failed: {_lib.last_error()}")
+    if args.webp_encoder == "exact" and lib.ik_set_webp_encoder(2) != 0:
+        raise SystemExit(f"ik_set_webp_encoder failed: {_lib.last_error()}")
     dev = f"cuda:{local}"
     # request bodies in page-locked host memory (ik_host_alloc), as a server reads
     # them: the upload DMAs them in place (--pageable: ordinary Python bytes)
@@ -705,7 +709,9 @@ def main():
                  "jpeg": "JPEG q90 4:2:0 without restart markers, in page-locked host memory -> "
                          "ik_transform_batch_submit: decode_image (GPU self-synchronising entropy decoding, IDCT, "
                          "upsampling, colour)"}[args.source] if args.pipeline else "host memory -> ik_transform_batch")
-    coder = {"webp": "libwebp", "jpeg": "GPU FDCT + Huffman", "avif": "libavif/aom"}[args.format]
+    coder = {"webp": "libwebp" if args.webp_encoder == "libwebp" else
+             "libwebp method 4 on the GPU (IK_WEBP_EXACT, byte-identical)",
+             "jpeg": "GPU FDCT + Huffman", "avif": "libavif/aom"}[args.format]
     if rank == 0:
         line = {
             "metric": METRIC,

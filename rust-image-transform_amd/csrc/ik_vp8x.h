@@ -323,6 +323,37 @@ IK_HD void pred_nxn(uint8_t* dst, int m, const uint8_t* left, const uint8_t* top
     }
 }
 
+// the 4x4 block (bx, by) of pred_nxn(.., m, .., 16)
+IK_HD void pred16_block(uint8_t* dst, int m, const uint8_t* left, const uint8_t* top, int bx, int by) {
+    const int x0 = 4 * bx, y0 = 4 * by;
+    int v = 0;
+    if (m == 0) {
+        int DC = 0;
+        if (top) {
+            for (int j = 0; j < 16; ++j) DC += top[j];
+            if (left) for (int j = 0; j < 16; ++j) DC += left[j];
+            else DC += DC;
+            DC = (DC + 16) >> 5;
+        } else if (left) {
+            for (int j = 0; j < 16; ++j) DC += left[j];
+            DC += DC;
+            DC = (DC + 16) >> 5;
+        } else {
+            DC = 0x80;
+        }
+        v = DC;
+    }
+    for (int y = y0; y < y0 + 4; ++y)
+        for (int x = x0; x < x0 + 4; ++x) {
+            int p;
+            if (m == 0) p = v;
+            else if (m == 1) p = (left && top) ? xclip8(left[y] + top[x] - left[-1]) : left ? left[y] : top ? top[x] : 129;
+            else if (m == 2) p = top ? top[x] : 127;
+            else p = left ? left[y] : 129;
+            dst[x + y * BPS] = (uint8_t)p;
+        }
+}
+
 IK_HD uint8_t avg3(int a, int b, int c) { return (uint8_t)((a + 2 * b + c + 2) >> 2); }
 IK_HD uint8_t avg2(int a, int b) { return (uint8_t)((a + b + 1) >> 1); }
 

@@ -94,6 +94,8 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
     __shared__ __attribute__((aligned(16))) uint8_t s_pred4[10][4 * BPS];
     __shared__ __attribute__((aligned(16))) uint8_t s_predc[4][BPS * 8];
     __shared__ __attribute__((aligned(16))) int16_t s_tmpc[4][8][16];
+    __shared__ int16_t s_dc16[4][16];
+    __shared__ int s_bnz[4][16], s_cnz[4][8];
 
     // ---- load the source MB (ImportBlock: clamped coordinates) and the boundaries ----
     for (int i = l; i < 256; i += 64) {
@@ -137,54 +139,56 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
     }
     __syncthreads();
 
-    // ---- intra-16: lane = mode ----
-    if (l < 4) {
-        const int m = l;
+    // ---- intra-16: lane = (mode, 4x4 block), 4 x 16 lanes ----
+    {
+        const int m = l >> 4, n = l & 15, bx = n & 3, by = n >> 2;
+        const int off = bx * 4 + by * 4 * BPS;
         uint8_t* pred = s_pred16[m];
-        pred_nxn(pred, m, mx ? s_yl + 1 : nullptr, my ? s_yt : nullptr, 16);
-        int16_t(*tmp)[16] = s_tmp16[m];
-        int16_t dc[16];
-        uint32_t nz = 0;
-        for (int n = 0; n < 16; ++n) {
-            const int off = (n & 3) * 4 + (n >> 2) * 4 * BPS;
-            ftransform(s_in + off, pred + off, tmp[n]);
+        pred16_block(pred, m, mx ? s_yl + 1 : nullptr, my ? s_yt : nullptr, bx, by);
+        ftransform(s_in + off, pred + off, s_tmp16[m][n]);
+        __syncthreads();
+        if (n == 0) {  // the mode's Y2: WHT of the 16 DCs, quantised
+            ftransform_wht(s_tmp16[m][0], s_dc16[m]);
+            s_nz16[m] = quantize_block(s_dc16[m], s_lv16[m][0], Q.y2) << 24;
         }
-        ftransform_wht(tmp[0], dc);
-        nz |= (uint32_t)quantize_block(dc, s_lv16[m][0], Q.y2) << 24;
-        for (int n = 0; n < 16; ++n) {
-            tmp[n][0] = 0;
-            nz |= (uint32_t)quantize_block(tmp[n], s_lv16[m][1 + n], Q.y1) << n;
-        }
-        itransform_wht(dc, tmp[0]);
-        for (int n = 0; n < 16; ++n) {
-            const int off = (n & 3) * 4 + (n >> 2) * 4 * BPS;
-            itransform(pred + off, tmp[n], s_rec16[m] + off);
-        }
-        int64_t D = sse_wh(s_in, s_rec16[m], 16, 16), SD = 0;
-        if (Q.tlambda) {
-            int d = 0;
-            for (int y = 0; y < 16; y += 4)
-                for (int x = 0; x < 16; x += 4) d += disto4x4(s_in + x + y * BPS, s_rec16[m] + x + y * BPS);
-            SD = (Q.tlambda * d + 128) >> 8;
-        }
-        // rate (VP8GetCostLuma16 from the MB's incoming contexts)
-        int tnz[4], lnz[4];
-        for (int i = 0; i < 4; ++i) { tnz[i] = s_tnz[i]; lnz[i] = s_lnz[i]; }
-        int R = residual_cost(lc, pr, 1, 0, s_tnz[8] + s_lnz[8], s_lv16[m][0]);
+        __syncthreads();
+        s_tmp16[m][n][0] = 0;
+        const int bnz = quantize_block(s_tmp16[m][n], s_lv16[m][1 + n], Q.y1);
+        s_bnz[m][n] = bnz;
+        __syncthreads();
+        if (n == 0) itransform_wht(s_dc16[m], s_tmp16[m][0]);  // the DCs back into the blocks
+        __syncthreads();
+        itransform(pred + off, s_tmp16[m][n], s_rec16[m] + off);
+        // this block's distortion, rate (VP8GetCostLuma16's contexts: the block above and
+        // to the left in this mode, or the MB's incoming ones) and AC count
+        int D = 0;
         for (int y = 0; y < 4; ++y)
             for (int x = 0; x < 4; ++x) {
-                const int16_t* c = s_lv16[m][1 + x + 4 * y];
-                R += residual_cost(lc, pr, 0, 1, tnz[x] + lnz[y], c);
-                int any = 0;
-                for (int k = 1; k < 16; ++k) any |= c[k] != 0;
-                tnz[x] = lnz[y] = any;
+                const int d = s_in[off + x + y * BPS] - s_rec16[m][off + x + y * BPS];
+                D += d * d;
             }
-        s_flat[m] = is_flat(s_lv16[m][1], 16, 10);
-        s_nz16[m] = (int)nz;
-        s_part[m][0] = D;
-        s_part[m][1] = SD;
-        s_part[m][2] = R;
-        s_part[m][3] = kFixedCostsI16[m];
+        int dis = Q.tlambda ? disto4x4(s_in + off, s_rec16[m] + off) : 0;
+        const int ctx = (by ? s_bnz[m][n - 4] : s_tnz[bx]) + (bx ? s_bnz[m][n - 1] : s_lnz[by]);
+        int R = residual_cost(lc, pr, 0, 1, ctx, s_lv16[m][1 + n]);
+        if (n == 0) R += residual_cost(lc, pr, 1, 0, s_tnz[8] + s_lnz[8], s_lv16[m][0]);
+        int cnt = 0;
+        for (int k = 1; k < 16; ++k) cnt += s_lv16[m][1 + n][k] != 0;
+        int nzm = bnz << n;
+        for (int o = 8; o; o >>= 1) {  // sums over the mode's 16 lanes
+            D += __shfl_xor(D, o, 64);
+            dis += __shfl_xor(dis, o, 64);
+            R += __shfl_xor(R, o, 64);
+            cnt += __shfl_xor(cnt, o, 64);
+            nzm |= __shfl_xor(nzm, o, 64);
+        }
+        if (n == 0) {
+            s_flat[m] = cnt <= 10;  // IsFlat(levels, 16 blocks, FLATNESS_LIMIT_I16)
+            s_nz16[m] |= nzm;
+            s_part[m][0] = D;
+            s_part[m][1] = Q.tlambda ? ((Q.tlambda * dis + 128) >> 8) : 0;
+            s_part[m][2] = R;
+            s_part[m][3] = kFixedCostsI16[m];
+        }
     }
     __syncthreads();
     if (l == 0) {
@@ -289,73 +293,74 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
     }
     __syncthreads();
 
-    // ---- chroma: lane = mode ----
-    if (l < 4) {
-        const int m = l;
+    // ---- chroma: lane = (mode, 4x4 block), 4 x 8 lanes ----
+    {
+        const int m = (l >> 3) & 3, n = l & 7, ch = n >> 2, b = n & 3, bx = b & 1, by = b >> 1;
+        const int off = bx * 4 + by * 4 * BPS + ch * 8;  // VP8ScanUV
+        const bool act = l < 32;
         uint8_t* pred = s_predc[m];
-        pred_nxn(pred, m, mx ? s_ul + 1 : nullptr, my ? s_ut : nullptr, 8);
-        pred_nxn(pred + 8, m, mx ? s_vl + 1 : nullptr, my ? s_vt : nullptr, 8);
-        int16_t(*tmp)[16] = s_tmpc[m];
-        for (int n = 0; n < 8; ++n) {
-            const int off = (n & 1) * 4 + ((n >> 1) & 1) * 4 * BPS + (n >> 2) * 8;
-            ftransform(s_in + 16 + off, pred + off, tmp[n]);
+        if (act && n == 0) {
+            pred_nxn(pred, m, mx ? s_ul + 1 : nullptr, my ? s_ut : nullptr, 8);
+            pred_nxn(pred + 8, m, mx ? s_vl + 1 : nullptr, my ? s_vt : nullptr, 8);
         }
-        if (a.use_derr) {  // CorrectDCValues
-            for (int ch = 0; ch <= 1; ++ch) {
-                const int8_t* top = s_derr_t[ch];
-                const int8_t* left = s_derr_l[ch];
-                int16_t(*c)[16] = &tmp[ch * 4];
-                auto qs = [&](int16_t* v) {
-                    int Vv = *v;
-                    const int sign = Vv < 0;
-                    if (sign) Vv = -Vv;
-                    if (Vv > (int)Q.uv.zthresh[0]) {
-                        const int qV = (int)(((uint32_t)Vv * Q.uv.iq[0] + Q.uv.bias[0]) >> QFIX) * Q.uv.q[0];
-                        const int err = Vv - qV;
-                        *v = (int16_t)(sign ? -qV : qV);
-                        return (sign ? -err : err) >> 1;
-                    }
-                    *v = 0;
-                    return (sign ? -Vv : Vv) >> 1;
-                };
-                c[0][0] = (int16_t)(c[0][0] + ((7 * top[0] + 8 * left[0]) >> 3));
-                const int e0 = qs(&c[0][0]);
-                c[1][0] = (int16_t)(c[1][0] + ((7 * top[1] + 8 * e0) >> 3));
-                const int e1 = qs(&c[1][0]);
-                c[2][0] = (int16_t)(c[2][0] + ((7 * e0 + 8 * left[1]) >> 3));
-                const int e2 = qs(&c[2][0]);
-                c[3][0] = (int16_t)(c[3][0] + ((7 * e1 + 8 * e2) >> 3));
-                const int e3 = qs(&c[3][0]);
-                s_duv[m][ch][0] = (int8_t)e1;
-                s_duv[m][ch][1] = (int8_t)e2;
-                s_duv[m][ch][2] = (int8_t)e3;
-            }
-        }
-        for (int n = 0; n < 8; ++n) quantize_block(tmp[n], s_lvuv[m][n], Q.uv);
-        for (int n = 0; n < 8; ++n) {
-            const int off = (n & 1) * 4 + ((n >> 1) & 1) * 4 * BPS + (n >> 2) * 8;
-            itransform(pred + off, tmp[n], s_recuv[m] + off);
-        }
-        int64_t D = 0;
-        for (int y = 0; y < 8; ++y)
-            for (int x = 0; x < 16; ++x) {
-                const int d = s_in[16 + x + y * BPS] - s_recuv[m][x + y * BPS];
-                D += d * d;
-            }
-        int tnz[4], lnz[4];
-        for (int i = 0; i < 4; ++i) { tnz[i] = s_tnz[4 + i]; lnz[i] = s_lnz[4 + i]; }
-        int R = 0;
-        for (int ch = 0; ch <= 2; ch += 2)
-            for (int y = 0; y < 2; ++y)
-                for (int x = 0; x < 2; ++x) {
-                    const int16_t* c = s_lvuv[m][ch * 2 + x + y * 2];
-                    R += residual_cost(lc, pr, 2, 0, tnz[ch + x] + lnz[ch + y], c);
-                    int any = 0;
-                    for (int k = 0; k < 16; ++k) any |= c[k] != 0;
-                    tnz[ch + x] = lnz[ch + y] = any;
+        __syncthreads();
+        if (act) ftransform(s_in + 16 + off, pred + off, s_tmpc[m][n]);
+        __syncthreads();
+        if (act && a.use_derr && b == 0) {  // CorrectDCValues, one channel: its 4 DCs in order
+            const int8_t* top = s_derr_t[ch];
+            const int8_t* left = s_derr_l[ch];
+            int16_t(*c)[16] = &s_tmpc[m][ch * 4];
+            auto qs = [&](int16_t* v) {
+                int Vv = *v;
+                const int sign = Vv < 0;
+                if (sign) Vv = -Vv;
+                if (Vv > (int)Q.uv.zthresh[0]) {
+                    const int qV = (int)(((uint32_t)Vv * Q.uv.iq[0] + Q.uv.bias[0]) >> QFIX) * Q.uv.q[0];
+                    const int err = Vv - qV;
+                    *v = (int16_t)(sign ? -qV : qV);
+                    return (sign ? -err : err) >> 1;
                 }
-        if (m > 0 && is_flat(s_lvuv[m][0], 8, 2)) R += 140 * 8;
-        s_sc[m] = rd_score(R, kFixedCostsUV[m], D, 0, Q.lambda_uv);
+                *v = 0;
+                return (sign ? -Vv : Vv) >> 1;
+            };
+            c[0][0] = (int16_t)(c[0][0] + ((7 * top[0] + 8 * left[0]) >> 3));
+            const int e0 = qs(&c[0][0]);
+            c[1][0] = (int16_t)(c[1][0] + ((7 * top[1] + 8 * e0) >> 3));
+            const int e1 = qs(&c[1][0]);
+            c[2][0] = (int16_t)(c[2][0] + ((7 * e0 + 8 * left[1]) >> 3));
+            const int e2 = qs(&c[2][0]);
+            c[3][0] = (int16_t)(c[3][0] + ((7 * e1 + 8 * e2) >> 3));
+            const int e3 = qs(&c[3][0]);
+            s_duv[m][ch][0] = (int8_t)e1;
+            s_duv[m][ch][1] = (int8_t)e2;
+            s_duv[m][ch][2] = (int8_t)e3;
+        }
+        __syncthreads();
+        int D = 0, R = 0, cnt = 0;
+        if (act) {
+            s_cnz[m][n] = quantize_block(s_tmpc[m][n], s_lvuv[m][n], Q.uv);
+            itransform(pred + off, s_tmpc[m][n], s_recuv[m] + off);
+            for (int y = 0; y < 4; ++y)
+                for (int x = 0; x < 4; ++x) {
+                    const int d = s_in[16 + off + x + y * BPS] - s_recuv[m][off + x + y * BPS];
+                    D += d * d;
+                }
+            for (int k = 1; k < 16; ++k) cnt += s_lvuv[m][n][k] != 0;
+        }
+        __syncthreads();
+        if (act) {
+            const int ctx = (by ? s_cnz[m][n - 2] : s_tnz[4 + 2 * ch + bx]) + (bx ? s_cnz[m][n - 1] : s_lnz[4 + 2 * ch + by]);
+            R = residual_cost(lc, pr, 2, 0, ctx, s_lvuv[m][n]);
+        }
+        for (int o = 4; o; o >>= 1) {  // sums over the mode's 8 lanes
+            D += __shfl_xor(D, o, 64);
+            R += __shfl_xor(R, o, 64);
+            cnt += __shfl_xor(cnt, o, 64);
+        }
+        if (act && n == 0) {
+            if (m > 0 && cnt <= 2) R += 140 * 8;  // IsFlat(uv levels, 8, FLATNESS_LIMIT_UV)
+            s_sc[m] = rd_score(R, kFixedCostsUV[m], D, 0, Q.lambda_uv);
+        }
     }
     __syncthreads();
     if (l == 0) {
