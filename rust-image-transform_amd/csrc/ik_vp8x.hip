@@ -32,6 +32,31 @@ namespace {
 
 constexpr int kTopLeftI4[16] = {17, 21, 25, 29, 13, 17, 21, 25, 9, 13, 17, 21, 5, 9, 13, 17};
 
+// GetResidualCost with libwebp's fixed level costs and entropy costs staged in LDS
+// (the constant tables would be per-lane divergent global loads inside the serial
+// coefficient loop)
+__device__ __forceinline__ int rcost(const uint16_t* lc, const uint8_t* pr, const uint16_t* fixed, const uint16_t* ent,
+                                     const uint8_t* bands, int type, int first, int ctx0, const int16_t* c) {
+    int last = -1;
+    for (int n = 15; n >= 0; --n)
+        if (c[n]) { last = n; break; }
+    int n = first;
+    const int p0 = pr[((type * 8 + n) * 3 + ctx0) * 11];
+    if (last < 0) return ent[p0];
+    int cost = ctx0 == 0 ? ent[255 - p0] : 0;
+    const uint16_t* t = lc + ((type * 8 + bands[n]) * 3 + ctx0) * kLevelTab;
+    for (; n < last; ++n) {
+        const int v = c[n] < 0 ? -c[n] : c[n];
+        const int ctx = v >= 2 ? 2 : v;
+        cost += fixed[v] + t[v > kMaxVarLevel ? kMaxVarLevel : v];
+        t = lc + ((type * 8 + bands[n + 1]) * 3 + ctx) * kLevelTab;
+    }
+    const int v = c[n] < 0 ? -c[n] : c[n];
+    cost += fixed[v] + t[v > kMaxVarLevel ? kMaxVarLevel : v];
+    if (n < 15) cost += ent[pr[((type * 8 + bands[n + 1]) * 3 + (v == 1 ? 1 : 2)) * 11]];
+    return cost;
+}
+
 __device__ __forceinline__ int64_t rd_score(int64_t R, int64_t H, int64_t D, int64_t SD, int lambda) {
     return (R + H) * lambda + 256 * (D + SD);
 }
@@ -60,6 +85,14 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
     // candidate: staged in LDS (13.4 KB)
     __shared__ __attribute__((aligned(16))) uint16_t lc[kCostRows * kLevelTab];
     __shared__ __attribute__((aligned(16))) uint8_t pr[1056];
+    __shared__ __attribute__((aligned(16))) uint16_t s_fixed[2048];
+    __shared__ uint16_t s_ent[256];
+    __shared__ uint8_t s_bands[17];
+    __shared__ uint16_t s_fi4[1000];
+    for (int i = l; i < 1000; i += 64) s_fi4[i] = kFixedCostsI4[i];
+    for (int i = l; i < 2048; i += 64) s_fixed[i] = kLevelFixedCosts[i];
+    for (int i = l; i < 256; i += 64) s_ent[i] = kEntropyCost[i];
+    if (l < 17) s_bands[l] = kEncBands[l];
     {
         const uint4* g = (const uint4*)(a.lc + (size_t)img * kCostRows * kLevelTab);
         for (int i = l; i < kCostRows * kLevelTab / 8; i += 64) ((uint4*)lc)[i] = g[i];
@@ -169,8 +202,8 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
             }
         int dis = Q.tlambda ? disto4x4(s_in + off, s_rec16[m] + off) : 0;
         const int ctx = (by ? s_bnz[m][n - 4] : s_tnz[bx]) + (bx ? s_bnz[m][n - 1] : s_lnz[by]);
-        int R = residual_cost(lc, pr, 0, 1, ctx, s_lv16[m][1 + n]);
-        if (n == 0) R += residual_cost(lc, pr, 1, 0, s_tnz[8] + s_lnz[8], s_lv16[m][0]);
+        int R = rcost(lc, pr, s_fixed, s_ent, s_bands, 0, 1, ctx, s_lv16[m][1 + n]);
+        if (n == 0) R += rcost(lc, pr, s_fixed, s_ent, s_bands, 1, 0, s_tnz[8] + s_lnz[8], s_lv16[m][0]);
         int cnt = 0;
         for (int k = 1; k < 16; ++k) cnt += s_lv16[m][1 + n][k] != 0;
         int nzm = bnz << n;
@@ -250,9 +283,9 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
                         D += d * d;
                     }
                 const int64_t SD = Q.tlambda ? ((Q.tlambda * disto4x4(s_in + off, s_blk[m]) + 128) >> 8) : 0;
-                const int64_t Hc = kFixedCostsI4[(topm * 10 + left) * 10 + m];
+                const int64_t Hc = s_fi4[(topm * 10 + left) * 10 + m];
                 int64_t R = (m > 0 && is_flat(s_blv[m], 1, 3)) ? 140 : 0;
-                R += residual_cost(lc, pr, 3, 0, tnz4[bx] + lnz4[by], s_blv[m]);
+                R += rcost(lc, pr, s_fixed, s_ent, s_bands, 3, 0, tnz4[bx] + lnz4[by], s_blv[m]);
                 s_sc[m] = rd_score(R, Hc, D, SD, Q.lambda_i4);
                 s_part[m][0] = D;
                 s_part[m][1] = SD;
@@ -350,7 +383,7 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
         __syncthreads();
         if (act) {
             const int ctx = (by ? s_cnz[m][n - 2] : s_tnz[4 + 2 * ch + bx]) + (bx ? s_cnz[m][n - 1] : s_lnz[4 + 2 * ch + by]);
-            R = residual_cost(lc, pr, 2, 0, ctx, s_lvuv[m][n]);
+            R = rcost(lc, pr, s_fixed, s_ent, s_bands, 2, 0, ctx, s_lvuv[m][n]);
         }
         for (int o = 4; o; o >>= 1) {  // sums over the mode's 8 lanes
             D += __shfl_xor(D, o, 64);

@@ -228,8 +228,34 @@ int webp_encode_exact(const uint8_t* d_yuv, size_t yuv_stride, int n, int w, int
                       std::vector<std::vector<uint8_t>>& outs) {
     if (n < 1 || n > 65535 || w < 1 || h < 1 || w > 16383 || h > 16383)
         return fail(IK_ERR_INVALID, "bad WebP shape %dx%d x %d", w, h, n);
-    hipStream_t s = thread_stream();
-    if (!s) return fail(IK_ERR_DEVICE, "cannot create HIP stream");
+    hipStream_t ts = thread_stream();
+    if (!ts) return fail(IK_ERR_DEVICE, "cannot create HIP stream");
+    // the coder's ~300 small launches per batch go to a stream of their own at the
+    // highest priority: a hardware queue of their own, so they run beside another
+    // batch's decode kernels instead of queueing behind them; ordered after the
+    // caller's stream (which produced the planes) by an event
+    struct XStream {
+        hipStream_t s = nullptr;
+        hipEvent_t ev = nullptr;
+        int dev = -1;
+    };
+    static thread_local XStream xs;
+    if (xs.dev != current_device()) {
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
+        if (hipStreamCreateWithPriority(&xs.s, hipStreamNonBlocking, greatest) != hipSuccess) xs.s = ts;
+        if (hipEventCreateWithFlags(&xs.ev, hipEventDisableTiming) != hipSuccess) xs.ev = nullptr;
+        xs.dev = current_device();
+    }
+    hipStream_t s = xs.s;
+    if (s != ts) {
+        if (!xs.ev) {
+            s = ts;
+        } else {
+            IK_HIP(hipEventRecord(xs.ev, ts));
+            IK_HIP(hipStreamWaitEvent(s, xs.ev, 0));
+        }
+    }
     const int mb_w = (w + 15) / 16, mb_h = (h + 15) / 16, nmb = mb_w * mb_h;
     const size_t rec_stride = (size_t)mb_w * 16 * mb_h * 16 * 3 / 2;
     const float q = (float)quality;
