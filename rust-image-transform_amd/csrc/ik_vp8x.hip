@@ -129,6 +129,8 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
     __shared__ __attribute__((aligned(16))) int16_t s_tmpc[4][8][16];
     __shared__ int16_t s_dc16[4][16];
     __shared__ int s_bnz[4][16], s_cnz[4][8];
+    __shared__ int s_ft4[10][16], s_C4[10][16], s_tt4[10][2][16];
+    __shared__ int16_t s_cf4[10][16];
 
     // ---- load the source MB (ImportBlock: clamped coordinates) and the boundaries ----
     for (int i = l; i < 256; i += 64) {
@@ -264,28 +266,124 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
         for (int i4 = 0; i4 < 16; ++i4) {
             const int bx = i4 & 3, by = i4 >> 2;
             const int off = bx * 4 + by * 4 * BPS;
-            if (l < 10) {
-                const int m = l;
-                const uint8_t* top = s_bound + kTopLeftI4[i4];
+            // lanes = (mode, row): 10 x 4; each transform split into its row and column passes
+            const int m = l >> 2, r = l & 3;
+            const bool act = l < 40;
+            if (act && r == 0) pred4(s_pred4[m], m, s_bound + kTopLeftI4[i4]);
+            __syncthreads();
+            if (act) {  // FTransform, row r
+                const uint8_t* sr = s_in + off + r * BPS;
+                const uint8_t* pp = s_pred4[m] + r * BPS;
+                const int d0 = sr[0] - pp[0], d1 = sr[1] - pp[1], d2 = sr[2] - pp[2], d3 = sr[3] - pp[3];
+                const int a0 = d0 + d3, a1 = d1 + d2, a2 = d1 - d2, a3 = d0 - d3;
+                s_ft4[m][0 + 4 * r] = (a0 + a1) * 8;
+                s_ft4[m][1 + 4 * r] = (a2 * 2217 + a3 * 5352 + 1812) >> 9;
+                s_ft4[m][2 + 4 * r] = (a0 - a1) * 8;
+                s_ft4[m][3 + 4 * r] = (a3 * 2217 - a2 * 5352 + 937) >> 9;
+            }
+            __syncthreads();
+            if (act) {  // column r
+                const int* t = s_ft4[m];
+                const int i = r;
+                const int a0 = t[0 + i] + t[12 + i], a1 = t[4 + i] + t[8 + i];
+                const int a2 = t[4 + i] - t[8 + i], a3 = t[0 + i] - t[12 + i];
+                s_cf4[m][0 + i] = (int16_t)((a0 + a1 + 7) >> 4);
+                s_cf4[m][4 + i] = (int16_t)(((a2 * 2217 + a3 * 5352 + 12000) >> 16) + (a3 != 0));
+                s_cf4[m][8 + i] = (int16_t)((a0 - a1 + 7) >> 4);
+                s_cf4[m][12 + i] = (int16_t)((a3 * 2217 - a2 * 5352 + 51000) >> 16);
+            }
+            __syncthreads();
+            int nzl = 0, cnt = 0;
+            if (act) {  // QuantizeBlock: zigzag positions 4r .. 4r+3
+                for (int k = 0; k < 4; ++k) {
+                    const int n = 4 * r + k, j = zigzag(n);
+                    const int v = s_cf4[m][j];
+                    const int sign = v < 0;
+                    const uint32_t coeff = (uint32_t)((sign ? -v : v) + Q.y1.sharpen[j]);
+                    int level = 0;
+                    if (coeff > Q.y1.zthresh[j]) {
+                        level = (int)((coeff * Q.y1.iq[j] + Q.y1.bias[j]) >> QFIX);
+                        if (level > 2047) level = 2047;
+                        if (sign) level = -level;
+                    }
+                    s_cf4[m][j] = (int16_t)(level * (int)Q.y1.q[j]);
+                    s_blv[m][n] = (int16_t)level;
+                    nzl |= level != 0;
+                    cnt += n > 0 && level != 0;
+                }
+            }
+            __syncthreads();
+            if (act) {  // ITransform, column r
+                const int16_t* in = s_cf4[m];
+                const int i = r;
+                const int a = in[i] + in[8 + i], b = in[i] - in[8 + i];
+                const int c = ((in[4 + i] * 35468) >> 16) - (((in[12 + i] * 20091) >> 16) + in[12 + i]);
+                const int d = (((in[4 + i] * 20091) >> 16) + in[4 + i]) + ((in[12 + i] * 35468) >> 16);
+                s_C4[m][4 * i + 0] = a + d;
+                s_C4[m][4 * i + 1] = b + c;
+                s_C4[m][4 * i + 2] = b - c;
+                s_C4[m][4 * i + 3] = a - d;
+            }
+            __syncthreads();
+            int sse = 0;
+            if (act) {  // row r: the reconstruction, its SSE and the spectral rows of source and reconstruction
+                const int* C = s_C4[m];
+                const int i = r;
+                const int dc = C[i] + 4;
+                const int a = dc + C[8 + i], b = dc - C[8 + i];
+                const int c = ((C[4 + i] * 35468) >> 16) - (((C[12 + i] * 20091) >> 16) + C[12 + i]);
+                const int d = (((C[4 + i] * 20091) >> 16) + C[4 + i]) + ((C[12 + i] * 35468) >> 16);
+                const uint8_t* pp = s_pred4[m] + i * BPS;
+                uint8_t* o = s_blk[m] + i * BPS;
+                o[0] = xclip8(pp[0] + ((a + d) >> 3));
+                o[1] = xclip8(pp[1] + ((b + c) >> 3));
+                o[2] = xclip8(pp[2] + ((b - c) >> 3));
+                o[3] = xclip8(pp[3] + ((a - d) >> 3));
+                const uint8_t* sr = s_in + off + i * BPS;
+                for (int x = 0; x < 4; ++x) {
+                    const int e = sr[x] - o[x];
+                    sse += e * e;
+                }
+                for (int q = 0; q < 2; ++q) {
+                    const uint8_t* in = q ? o : sr;
+                    const int a0 = in[0] + in[2], a1 = in[1] + in[3], a2 = in[1] - in[3], a3 = in[0] - in[2];
+                    s_tt4[m][q][0 + 4 * i] = a0 + a1;
+                    s_tt4[m][q][1 + 4 * i] = a3 + a2;
+                    s_tt4[m][q][2 + 4 * i] = a3 - a2;
+                    s_tt4[m][q][3 + 4 * i] = a0 - a1;
+                }
+            }
+            __syncthreads();
+            int tA = 0, tB = 0;
+            if (act) {  // the spectral columns, weighted
+                const int i = r;
+                for (int q = 0; q < 2; ++q) {
+                    const int* t = s_tt4[m][q];
+                    const int a0 = t[0 + i] + t[8 + i], a1 = t[4 + i] + t[12 + i];
+                    const int a2 = t[4 + i] - t[12 + i], a3 = t[0 + i] - t[8 + i];
+                    const int v = kWeightY[i] * xabs(a0 + a1) + kWeightY[4 + i] * xabs(a3 + a2) +
+                                  kWeightY[8 + i] * xabs(a3 - a2) + kWeightY[12 + i] * xabs(a0 - a1);
+                    if (q) tB = v;
+                    else tA = v;
+                }
+            }
+            for (int o = 1; o <= 2; o <<= 1) {  // over the mode's 4 lanes
+                sse += __shfl_xor(sse, o, 64);
+                tA += __shfl_xor(tA, o, 64);
+                tB += __shfl_xor(tB, o, 64);
+                cnt += __shfl_xor(cnt, o, 64);
+                nzl |= __shfl_xor(nzl, o, 64);
+            }
+            if (act && r == 0) {
                 // mode costs from the neighbouring sub-blocks' modes (frame edge: B_DC)
                 const int left = bx ? s_modes4[i4 - 1] : (mx ? mbs[mb - 1].bmodes[by * 4 + 3] : 0);
                 const int topm = by ? s_modes4[i4 - 4] : (my ? mbs[mb - a.mb_w].bmodes[12 + bx] : 0);
-                uint8_t* pred = s_pred4[m];
-                pred4(pred, m, top);
-                int16_t tmp[16];
-                ftransform(s_in + off, pred, tmp);
-                s_i4nz[m] = quantize_block(tmp, s_blv[m], Q.y1);
-                itransform(pred, tmp, s_blk[m]);
-                int64_t D = 0;
-                for (int y = 0; y < 4; ++y)
-                    for (int x = 0; x < 4; ++x) {
-                        const int d = s_in[off + x + y * BPS] - s_blk[m][x + y * BPS];
-                        D += d * d;
-                    }
-                const int64_t SD = Q.tlambda ? ((Q.tlambda * disto4x4(s_in + off, s_blk[m]) + 128) >> 8) : 0;
+                const int64_t D = sse;
+                const int64_t SD = Q.tlambda ? ((Q.tlambda * (xabs(tB - tA) >> 5) + 128) >> 8) : 0;
                 const int64_t Hc = s_fi4[(topm * 10 + left) * 10 + m];
-                int64_t R = (m > 0 && is_flat(s_blv[m], 1, 3)) ? 140 : 0;
+                int64_t R = (m > 0 && cnt <= 3) ? 140 : 0;  // IsFlat(levels, 1, FLATNESS_LIMIT_I4)
                 R += rcost(lc, pr, s_fixed, s_ent, s_bands, 3, 0, tnz4[bx] + lnz4[by], s_blv[m]);
+                s_i4nz[m] = nzl;
                 s_sc[m] = rd_score(R, Hc, D, SD, Q.lambda_i4);
                 s_part[m][0] = D;
                 s_part[m][1] = SD;
