@@ -263,7 +263,12 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
         for (int i = 0; i < 4; ++i) { tnz4[i] = s_tnz[i]; lnz4[i] = s_lnz[i]; }
         int64_t aS = 211ll * Q.lambda_mode;  // rd_best: H = 211 = VP8BitCost(0, 145)
         int header_bits = 0;
+#ifdef IK_VP8X_NO_I4
+        if (l == 0) s_i4ok = 0;
+        for (int i4 = 0; i4 < 0; ++i4) {
+#else
         for (int i4 = 0; i4 < 16; ++i4) {
+#endif
             const int bx = i4 & 3, by = i4 >> 2;
             const int off = bx * 4 + by * 4 * BPS;
             // lanes = (mode, row): 10 x 4; each transform split into its row and column passes

@@ -369,17 +369,31 @@ int webp_encode_exact(const uint8_t* d_yuv, size_t yuv_stride, int n, int w, int
             IK_HIP(launch_vp8x_mb(a, dlist + st.off, st.count, n, s));
         }
     }
-    // 4. the records back; the files on the host
-    std::vector<XMB> mbs((size_t)nmb * n);
-    std::vector<uint8_t> pr((size_t)1056 * n);
-    std::vector<int> me((size_t)4 * n);
-    IK_HIP(hipMemcpyAsync(mbs.data(), d + o_mbs, sizeof(XMB) * mbs.size(), hipMemcpyDeviceToHost, s));
-    IK_HIP(hipMemcpyAsync(pr.data(), d + o_pr, pr.size(), hipMemcpyDeviceToHost, s));
-    IK_HIP(hipMemcpyAsync(me.data(), d + o_me, 4 * me.size(), hipMemcpyDeviceToHost, s));
+    // 4. the records back (into a page-locked area kept per thread: ~820 B per MB); the
+    // files on the host
+    const size_t rec_bytes = sizeof(XMB) * (size_t)nmb * n, tail = 1056ull * n + 16ull * n;
+    struct Pinned {
+        uint8_t* p = nullptr;
+        size_t cap = 0;
+    };
+    static thread_local Pinned hpin;
+    if (hpin.cap < rec_bytes + tail) {
+        if (hpin.p) (void)hipHostFree(hpin.p);
+        hpin.p = nullptr;
+        hpin.cap = 0;
+        IK_HIP(hipHostMalloc((void**)&hpin.p, rec_bytes + tail, hipHostMallocDefault));
+        hpin.cap = rec_bytes + tail;
+    }
+    const XMB* mbs = reinterpret_cast<const XMB*>(hpin.p);
+    const uint8_t* pr = hpin.p + rec_bytes;
+    const int* me = reinterpret_cast<const int*>(hpin.p + rec_bytes + 1056ull * n);
+    IK_HIP(hipMemcpyAsync(hpin.p, d + o_mbs, rec_bytes, hipMemcpyDeviceToHost, s));
+    IK_HIP(hipMemcpyAsync(hpin.p + rec_bytes, d + o_pr, 1056ull * n, hipMemcpyDeviceToHost, s));
+    IK_HIP(hipMemcpyAsync(hpin.p + rec_bytes + 1056ull * n, d + o_me, 16ull * n, hipMemcpyDeviceToHost, s));
     IK_HIP(hipStreamSynchronize(s));
     outs.resize(n);
     parallel_for(n, n < 16 ? n : 16, [&](int i) {
-        write_file(w, h, &mbs[(size_t)nmb * i], &pr[(size_t)1056 * i], hdr[i], &me[(size_t)4 * i], &segs[(size_t)4 * i],
+        write_file(w, h, mbs + (size_t)nmb * i, pr + (size_t)1056 * i, hdr[i], me + (size_t)4 * i, &segs[(size_t)4 * i],
                    outs[i]);
     });
     return IK_OK;

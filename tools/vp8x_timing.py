@@ -20,6 +20,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=64)
 ap.add_argument("--iters", type=int, default=3)
 ap.add_argument("--threads", type=int, default=16)
+ap.add_argument("--no-check", action="store_true", help="dev builds that change the output: skip the byte check")
 args = ap.parse_args()
 ik = _lib.load()
 assert ik.ik_init(0) == 0
@@ -42,7 +43,7 @@ for it in range(args.iters + 1):
         ik.ik_buf_free(outs[i])
 orc = ikutil.Oracle()
 ref = [orc.webp_encode_rgb(orc.to_rgb8(base[i]), 80.0) for i in range(4)]
-assert all(files[i] == ref[i % 4] for i in range(args.n)), "bytes differ from libwebp"
+assert args.no_check or all(files[i] == ref[i % 4] for i in range(args.n)), "bytes differ from libwebp"
 # libwebp on the host, the same frames, args.threads threads
 rgb = [np.ascontiguousarray(orc.to_rgb8(base[i % 4])) for i in range(args.n)]
 t = time.perf_counter()
