@@ -83,7 +83,11 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
     const int sg = a.seg[(size_t)img * nmb + mb];
     // the image's level costs and probabilities, read at every coefficient of every
     // candidate: staged in LDS (13.4 KB)
+#ifdef IK_VP8X_LC_GLOBAL
+    const uint16_t* lc = a.lc + (size_t)img * kCostRows * kLevelTab;
+#else
     __shared__ __attribute__((aligned(16))) uint16_t lc[kCostRows * kLevelTab];
+#endif
     __shared__ __attribute__((aligned(16))) uint8_t pr[1056];
     __shared__ __attribute__((aligned(16))) uint16_t s_fixed[2048];
     __shared__ uint16_t s_ent[256];
@@ -94,8 +98,10 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
     for (int i = l; i < 256; i += 64) s_ent[i] = kEntropyCost[i];
     if (l < 17) s_bands[l] = kEncBands[l];
     {
+#ifndef IK_VP8X_LC_GLOBAL
         const uint4* g = (const uint4*)(a.lc + (size_t)img * kCostRows * kLevelTab);
         for (int i = l; i < kCostRows * kLevelTab / 8; i += 64) ((uint4*)lc)[i] = g[i];
+#endif
         const uint4* gp = (const uint4*)(a.pr + (size_t)img * 1056);
         for (int i = l; i < 1056 / 16; i += 64) ((uint4*)pr)[i] = gp[i];
     }
