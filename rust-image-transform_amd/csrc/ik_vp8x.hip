@@ -34,26 +34,52 @@ constexpr int kTopLeftI4[16] = {17, 21, 25, 29, 13, 17, 21, 25, 9, 13, 17, 21, 5
 
 // GetResidualCost with libwebp's fixed level costs and entropy costs staged in LDS
 // (the constant tables would be per-lane divergent global loads inside the serial
-// coefficient loop)
+// coefficient loop).  Every coefficient's context is known from its predecessor's
+// level, so the 16 terms are independent: the block comes in with two 16-byte LDS
+// reads, and all 32 table reads are issued together (unrolled; a position outside
+// [first, last] reads a valid entry and adds 0) instead of a chain of dependent
+// reads per coefficient.  Same integer sum as residual_cost (ik_vp8x.h): the last
+// position is max(last non-zero, first), as in libwebp's loop.
 __device__ __forceinline__ int rcost(const uint16_t* lc, const uint8_t* pr, const uint16_t* fixed, const uint16_t* ent,
                                      const uint8_t* bands, int type, int first, int ctx0, const int16_t* c) {
-    int last = -1;
-    for (int n = 15; n >= 0; --n)
-        if (c[n]) { last = n; break; }
-    int n = first;
-    const int p0 = pr[((type * 8 + n) * 3 + ctx0) * 11];
-    if (last < 0) return ent[p0];
-    int cost = ctx0 == 0 ? ent[255 - p0] : 0;
-    const uint16_t* t = lc + ((type * 8 + bands[n]) * 3 + ctx0) * kLevelTab;
-    for (; n < last; ++n) {
-        const int v = c[n] < 0 ? -c[n] : c[n];
-        const int ctx = v >= 2 ? 2 : v;
-        cost += fixed[v] + t[v > kMaxVarLevel ? kMaxVarLevel : v];
-        t = lc + ((type * 8 + bands[n + 1]) * 3 + ctx) * kLevelTab;
+    int v[16];
+    {
+        const uint4 q0 = reinterpret_cast<const uint4*>(c)[0], q1 = reinterpret_cast<const uint4*>(c)[1];
+        const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int lo = (int16_t)(w[i] & 0xffffu), hi = (int16_t)(w[i] >> 16);
+            v[2 * i] = lo < 0 ? -lo : lo;
+            v[2 * i + 1] = hi < 0 ? -hi : hi;
+        }
     }
-    const int v = c[n] < 0 ? -c[n] : c[n];
-    cost += fixed[v] + t[v > kMaxVarLevel ? kMaxVarLevel : v];
-    if (n < 15) cost += ent[pr[((type * 8 + bands[n + 1]) * 3 + (v == 1 ? 1 : 2)) * 11]];
+    int last = -1;
+#pragma unroll
+    for (int n = 0; n < 16; ++n)
+        if (v[n]) last = n;
+    const int p0 = pr[((type * 8 + kEncBands[first]) * 3 + ctx0) * 11];
+    if (last < 0) return ent[p0];
+    if (last < first) last = first;
+    int cost = ctx0 == 0 ? ent[255 - p0] : 0;
+    const int rowbase = type * 8 * 3;
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+        const int ctx = n == 0 ? ctx0 : (n == first ? ctx0 : (v[n - 1] >= 2 ? 2 : v[n - 1]));
+        const int vv = v[n];
+        const int term = fixed[vv] + lc[(rowbase + kEncBands[n] * 3 + ctx) * kLevelTab + (vv > kMaxVarLevel ? kMaxVarLevel : vv)];
+        cost += (n >= first && n <= last) ? term : 0;
+    }
+    int vl = 0;
+#pragma unroll
+    for (int n = 0; n < 16; ++n)
+        if (n == last) vl = v[n];
+    if (last < 15) {
+        int bl = 0;
+#pragma unroll
+        for (int n = 0; n < 15; ++n)
+            if (n == last) bl = kEncBands[n + 1];
+        cost += ent[pr[((type * 8 + bl) * 3 + (vl == 1 ? 1 : 2)) * 11]];
+    }
     return cost;
 }
 
@@ -112,18 +138,19 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
     __shared__ int s_tnz[9], s_lnz[9];
     __shared__ int8_t s_derr_t[2][2], s_derr_l[2][2];
     __shared__ __attribute__((aligned(16))) uint8_t s_rec16[4][BPS * 16];
-    __shared__ int16_t s_lv16[4][17][16];
+    __shared__ __attribute__((aligned(16))) int16_t s_lv16[4][17][16];
     __shared__ int64_t s_sc[16], s_part[16][4];
     __shared__ int s_flat[4], s_nz16[4];
     __shared__ __attribute__((aligned(16))) uint8_t s_best4[BPS * 16];
     __shared__ uint8_t s_bound[37];
     __shared__ int16_t s_lv4[16][16];
     __shared__ uint8_t s_modes4[16];
+    __shared__ uint8_t s_nbm[8];  // the left MB's right column of sub-block modes, the top MB's bottom row
     __shared__ __attribute__((aligned(16))) uint8_t s_blk[10][4 * BPS];
-    __shared__ int16_t s_blv[10][16];
+    __shared__ __attribute__((aligned(16))) int16_t s_blv[10][16];
     __shared__ int s_i4nz[10];
     __shared__ __attribute__((aligned(16))) uint8_t s_recuv[4][BPS * 8];
-    __shared__ int16_t s_lvuv[4][8][16];
+    __shared__ __attribute__((aligned(16))) int16_t s_lvuv[4][8][16];
     __shared__ int8_t s_duv[4][2][3];
     __shared__ int s_b16, s_buv, s_i4ok;
     __shared__ int64_t s_s16;  // the i16 best's score at lambda_mode (the intra-4 bar)
@@ -171,6 +198,9 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
         for (int i = 0; i < 9; ++i) s_tnz[i] = (int)((tnz >> tb[i]) & 1u);
         for (int i = 0; i < 8; ++i) s_lnz[i] = (int)((lnz >> lb[i]) & 1u);
         s_lnz[8] = (int)((lnz >> 25) & 1u);
+    } else if (l >= 32 && l < 40) {
+        const int k = l - 32;
+        s_nbm[k] = k < 4 ? (mx ? mbs[mb - 1].bmodes[k * 4 + 3] : 0) : (my ? mbs[mb - a.mb_w].bmodes[12 + k - 4] : 0);
     } else if (l == 30) {
         for (int c = 0; c < 2; ++c)
             for (int k = 0; k < 2; ++k) {
@@ -387,8 +417,8 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
             }
             if (act && r == 0) {
                 // mode costs from the neighbouring sub-blocks' modes (frame edge: B_DC)
-                const int left = bx ? s_modes4[i4 - 1] : (mx ? mbs[mb - 1].bmodes[by * 4 + 3] : 0);
-                const int topm = by ? s_modes4[i4 - 4] : (my ? mbs[mb - a.mb_w].bmodes[12 + bx] : 0);
+                const int left = bx ? s_modes4[i4 - 1] : s_nbm[by];
+                const int topm = by ? s_modes4[i4 - 4] : s_nbm[4 + bx];
                 const int64_t D = sse;
                 const int64_t SD = Q.tlambda ? ((Q.tlambda * (xabs(tB - tA) >> 5) + 128) >> 8) : 0;
                 const int64_t Hc = s_fi4[(topm * 10 + left) * 10 + m];
