@@ -358,22 +358,25 @@ IK_HD uint8_t avg3(int a, int b, int c) { return (uint8_t)((a + 2 * b + c + 2) >
 IK_HD uint8_t avg2(int a, int b) { return (uint8_t)((a + b + 1) >> 1); }
 
 // intra-4 predictor from top[] (top[-1] corner, top[-2..-5] the left column, top[0..7]
-// above and above-right)
+// above and above-right); row stride S (the device builds it in registers with S = 4)
+template <int S = BPS>
 IK_HD void pred4(uint8_t* dst, int mode, const uint8_t* top) {
     const int X = top[-1], I = top[-2], J = top[-3], K = top[-4], L = top[-5];
     const int A = top[0], B = top[1], C = top[2], D = top[3], E = top[4], F = top[5], G = top[6], H = top[7];
-#define DST(x, y) dst[(x) + (y) * BPS]
+#define DST(x, y) dst[(x) + (y) * S]
     switch (mode) {
     case 0: {
-        uint32_t dc = 4;
-        for (int i = 0; i < 4; ++i) dc += top[i] + top[-5 + i];
-        fill(dst, (int)(dc >> 3), 4);
+        const int dc = (4 + A + B + C + D + I + J + K + L) >> 3;
+        for (int y = 0; y < 4; ++y)
+            for (int x = 0; x < 4; ++x) DST(x, y) = (uint8_t)dc;
         break;
     }
-    case 1:
+    case 1: {
+        const int lf[4] = {I, J, K, L}, tp[4] = {A, B, C, D};
         for (int y = 0; y < 4; ++y)
-            for (int x = 0; x < 4; ++x) DST(x, y) = xclip8(top[-2 - y] + top[x] - X);
+            for (int x = 0; x < 4; ++x) DST(x, y) = xclip8(lf[y] + tp[x] - X);
         break;
+    }
     case 2:
         for (int y = 0; y < 4; ++y) {
             DST(0, y) = avg3(X, A, B);

@@ -83,16 +83,82 @@ __device__ __forceinline__ int rcost(const uint16_t* lc, const uint8_t* pr, cons
     return cost;
 }
 
+// row y of pred_nxn(dst, m, left, top, 8) (ik_vp8x.h), built in registers and stored as
+// two words: the chroma predictors on 8 lanes per mode instead of one
+__device__ __forceinline__ void pred8_row(uint8_t* dst, int m, const uint8_t* left, const uint8_t* top, int y) {
+    uint8_t o[8];
+    if (m == 0) {
+        int DC = 0;
+        if (top) {
+            for (int j = 0; j < 8; ++j) DC += top[j];
+            if (left) for (int j = 0; j < 8; ++j) DC += left[j];
+            else DC += DC;
+            DC = (DC + 8) >> 4;
+        } else if (left) {
+            for (int j = 0; j < 8; ++j) DC += left[j];
+            DC += DC;
+            DC = (DC + 8) >> 4;
+        } else {
+            DC = 0x80;
+        }
+#pragma unroll
+        for (int x = 0; x < 8; ++x) o[x] = (uint8_t)DC;
+    } else if (m == 1 && left && top) {
+        const int ly = left[y], c = left[-1];
+#pragma unroll
+        for (int x = 0; x < 8; ++x) o[x] = xclip8(ly + top[x] - c);
+    } else if ((m == 1 && top) || m == 2) {  // TM without left, V: the row above (127 at the top edge)
+#pragma unroll
+        for (int x = 0; x < 8; ++x) o[x] = top ? top[x] : (m == 1 ? 129 : 127);
+    } else {  // TM without top, H: the left sample (129 at the left edge; TM with neither: 129)
+        const uint8_t v = left ? left[y] : 129;
+#pragma unroll
+        for (int x = 0; x < 8; ++x) o[x] = v;
+    }
+    uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+        w0 |= (uint32_t)o[x] << (8 * x);
+        w1 |= (uint32_t)o[4 + x] << (8 * x);
+    }
+    *reinterpret_cast<uint2*>(dst + y * BPS) = make_uint2(w0, w1);
+}
+
+__device__ __forceinline__ int64_t rdlane64(int64_t v, int lane) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), lane);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ int64_t rd_score(int64_t R, int64_t H, int64_t D, int64_t SD, int lambda) {
     return (R + H) * lambda + 256 * (D + SD);
 }
 
 }  // namespace
 
+// dev switch IK_VP8X_STAMPS: per-phase shader-clock sums over image 0's MBs
+// (tools/vp8x_timing.py --stamps reads them through ik_vp8x_stamps)
+#ifdef IK_VP8X_STAMPS
+__device__ unsigned long long g_vp8x_stamps[32];
+#define IK_STAMP(i)                                                         \
+    do {                                                                    \
+        if (l == 0 && img == 0) {                                           \
+            const unsigned long long t_ = clock64();                        \
+            atomicAdd(&g_vp8x_stamps[i], t_ - t_prev);                      \
+            t_prev = t_;                                                    \
+        }                                                                   \
+    } while (0)
+#else
+#define IK_STAMP(i) do {} while (0)
+#endif
+
 __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__ list) {
     const int l = threadIdx.x;
     const int img = blockIdx.y;
     const int mb = list[blockIdx.x];
+#ifdef IK_VP8X_STAMPS
+    unsigned long long t_prev = clock64();
+#endif
     const int mx = mb % a.mb_w, my = mb / a.mb_w;
     const int nmb = a.mb_w * a.mb_h;
     const int W = a.mb_w * 16, H = a.mb_h * 16;
@@ -119,19 +185,48 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
     __shared__ uint16_t s_ent[256];
     __shared__ uint8_t s_bands[17];
     __shared__ uint16_t s_fi4[1000];
-    for (int i = l; i < 1000; i += 64) s_fi4[i] = kFixedCostsI4[i];
-    for (int i = l; i < 2048; i += 64) s_fixed[i] = kLevelFixedCosts[i];
-    for (int i = l; i < 256; i += 64) s_ent[i] = kEntropyCost[i];
-    if (l < 17) s_bands[l] = kEncBands[l];
+    // staging: every lane issues all of its global reads first (one memory latency for
+    // the whole prologue), then writes them to LDS
     {
-#ifndef IK_VP8X_LC_GLOBAL
-        const uint4* g = (const uint4*)(a.lc + (size_t)img * kCostRows * kLevelTab);
-        for (int i = l; i < kCostRows * kLevelTab / 8; i += 64) ((uint4*)lc)[i] = g[i];
-#endif
+        constexpr int kFi4 = (1000 + 63) / 64, kFix = 2048 / 64, kEnt = 256 / 64;
+        constexpr int kPr = (1056 / 16 + 63) / 64;
+        uint16_t rf4[kFi4], rfx[kFix], ren[kEnt];
+#pragma unroll
+        for (int j = 0; j < kFi4; ++j) rf4[j] = kFixedCostsI4[min(l + 64 * j, 999)];
+#pragma unroll
+        for (int j = 0; j < kFix; ++j) rfx[j] = kLevelFixedCosts[l + 64 * j];
+#pragma unroll
+        for (int j = 0; j < kEnt; ++j) ren[j] = kEntropyCost[l + 64 * j];
         const uint4* gp = (const uint4*)(a.pr + (size_t)img * 1056);
-        for (int i = l; i < 1056 / 16; i += 64) ((uint4*)pr)[i] = gp[i];
+        uint4 rpr[kPr];
+#pragma unroll
+        for (int j = 0; j < kPr; ++j) rpr[j] = gp[min(l + 64 * j, 1056 / 16 - 1)];
+#pragma unroll
+        for (int j = 0; j < kFi4; ++j)
+            if (l + 64 * j < 1000) s_fi4[l + 64 * j] = rf4[j];
+#pragma unroll
+        for (int j = 0; j < kFix; ++j) s_fixed[l + 64 * j] = rfx[j];
+#pragma unroll
+        for (int j = 0; j < kEnt; ++j) s_ent[l + 64 * j] = ren[j];
+#ifndef IK_VP8X_LC_GLOBAL
+        {  // 13 x 16 B per lane (a register array this size would go to scratch)
+            const uint4* g = (const uint4*)(a.lc + (size_t)img * kCostRows * kLevelTab);
+            for (int i = l; i < kCostRows * kLevelTab / 8; i += 64) ((uint4*)lc)[i] = g[i];
+        }
+#endif
+#pragma unroll
+        for (int j = 0; j < kPr; ++j)
+            if (l + 64 * j < 1056 / 16) ((uint4*)pr)[l + 64 * j] = rpr[j];
     }
-    const XSeg& Q = a.segs[img * 4 + sg];
+    if (l < 17) s_bands[l] = kEncBands[l];
+    // the segment's matrices and lambdas, read per lane in every quantisation: LDS
+    __shared__ __attribute__((aligned(16))) XSeg s_Q;
+    {
+        static_assert(sizeof(XSeg) % 4 == 0, "XSeg copied as words");
+        const uint32_t* gq = reinterpret_cast<const uint32_t*>(a.segs + img * 4 + sg);
+        for (int i = l; i < (int)(sizeof(XSeg) / 4); i += 64) reinterpret_cast<uint32_t*>(&s_Q)[i] = gq[i];
+    }
+    const XSeg& Q = s_Q;
 
     __shared__ __attribute__((aligned(16))) uint8_t s_in[BPS * 16];      // Y 0..15, U 16..23, V 24..31
     __shared__ uint8_t s_yl[17], s_yt[20], s_ul[9], s_ut[8], s_vl[9], s_vt[8];
@@ -148,7 +243,6 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
     __shared__ uint8_t s_nbm[8];  // the left MB's right column of sub-block modes, the top MB's bottom row
     __shared__ __attribute__((aligned(16))) uint8_t s_blk[10][4 * BPS];
     __shared__ __attribute__((aligned(16))) int16_t s_blv[10][16];
-    __shared__ int s_i4nz[10];
     __shared__ __attribute__((aligned(16))) uint8_t s_recuv[4][BPS * 8];
     __shared__ __attribute__((aligned(16))) int16_t s_lvuv[4][8][16];
     __shared__ int8_t s_duv[4][2][3];
@@ -209,6 +303,7 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
             }
     }
     __syncthreads();
+    IK_STAMP(0);
 
     // ---- intra-16: lane = (mode, 4x4 block), 4 x 16 lanes ----
     {
@@ -262,6 +357,7 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
         }
     }
     __syncthreads();
+    IK_STAMP(1);
     if (l == 0) {
         // IsFlatSource16; the doubling chain of PickBestIntra16 (flat so far in mode order)
         int flat = 1;
@@ -292,6 +388,7 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
         s_i4ok = 1;
     }
     __syncthreads();
+    IK_STAMP(2);
 
     // ---- intra-4: 16 sub-blocks in order, lane = mode ----
     {
@@ -310,8 +407,18 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
             // lanes = (mode, row): 10 x 4; each transform split into its row and column passes
             const int m = l >> 2, r = l & 3;
             const bool act = l < 40;
-            if (act && r == 0) pred4(s_pred4[m], m, s_bound + kTopLeftI4[i4]);
+            if (act) {  // the mode's block in registers, row r stored by lane r
+                uint8_t d[16];
+                pred4<4>(d, m, s_bound + kTopLeftI4[i4]);
+                uint32_t rw[4];
+#pragma unroll
+                for (int y = 0; y < 4; ++y)
+                    rw[y] = (uint32_t)d[4 * y] | ((uint32_t)d[4 * y + 1] << 8) | ((uint32_t)d[4 * y + 2] << 16) |
+                            ((uint32_t)d[4 * y + 3] << 24);
+                *reinterpret_cast<uint32_t*>(s_pred4[m] + r * BPS) = r == 0 ? rw[0] : r == 1 ? rw[1] : r == 2 ? rw[2] : rw[3];
+            }
             __syncthreads();
+            IK_STAMP(10);
             if (act) {  // FTransform, row r
                 const uint8_t* sr = s_in + off + r * BPS;
                 const uint8_t* pp = s_pred4[m] + r * BPS;
@@ -323,6 +430,7 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
                 s_ft4[m][3 + 4 * r] = (a3 * 2217 - a2 * 5352 + 937) >> 9;
             }
             __syncthreads();
+            IK_STAMP(11);
             if (act) {  // column r
                 const int* t = s_ft4[m];
                 const int i = r;
@@ -334,6 +442,7 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
                 s_cf4[m][12 + i] = (int16_t)((a3 * 2217 - a2 * 5352 + 51000) >> 16);
             }
             __syncthreads();
+            IK_STAMP(12);
             int nzl = 0, cnt = 0;
             if (act) {  // QuantizeBlock: zigzag positions 4r .. 4r+3
                 for (int k = 0; k < 4; ++k) {
@@ -354,6 +463,7 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
                 }
             }
             __syncthreads();
+            IK_STAMP(13);
             if (act) {  // ITransform, column r
                 const int16_t* in = s_cf4[m];
                 const int i = r;
@@ -366,6 +476,7 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
                 s_C4[m][4 * i + 3] = a - d;
             }
             __syncthreads();
+            IK_STAMP(14);
             int sse = 0;
             if (act) {  // row r: the reconstruction, its SSE and the spectral rows of source and reconstruction
                 const int* C = s_C4[m];
@@ -395,6 +506,7 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
                 }
             }
             __syncthreads();
+            IK_STAMP(15);
             int tA = 0, tB = 0;
             if (act) {  // the spectral columns, weighted
                 const int i = r;
@@ -415,55 +527,60 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
                 cnt += __shfl_xor(cnt, o, 64);
                 nzl |= __shfl_xor(nzl, o, 64);
             }
+            // the mode's score and terms on its lane r == 0 (4m)
+            int64_t myS = INT64_MAX, myD = 0, mySD = 0, myR = 0, myH = 0;
             if (act && r == 0) {
                 // mode costs from the neighbouring sub-blocks' modes (frame edge: B_DC)
                 const int left = bx ? s_modes4[i4 - 1] : s_nbm[by];
                 const int topm = by ? s_modes4[i4 - 4] : s_nbm[4 + bx];
-                const int64_t D = sse;
-                const int64_t SD = Q.tlambda ? ((Q.tlambda * (xabs(tB - tA) >> 5) + 128) >> 8) : 0;
-                const int64_t Hc = s_fi4[(topm * 10 + left) * 10 + m];
-                int64_t R = (m > 0 && cnt <= 3) ? 140 : 0;  // IsFlat(levels, 1, FLATNESS_LIMIT_I4)
-                R += rcost(lc, pr, s_fixed, s_ent, s_bands, 3, 0, tnz4[bx] + lnz4[by], s_blv[m]);
-                s_i4nz[m] = nzl;
-                s_sc[m] = rd_score(R, Hc, D, SD, Q.lambda_i4);
-                s_part[m][0] = D;
-                s_part[m][1] = SD;
-                s_part[m][2] = R;
-                s_part[m][3] = Hc;
+                myD = sse;
+                mySD = Q.tlambda ? ((Q.tlambda * (xabs(tB - tA) >> 5) + 128) >> 8) : 0;
+                myH = s_fi4[(topm * 10 + left) * 10 + m];
+                myR = (m > 0 && cnt <= 3) ? 140 : 0;  // IsFlat(levels, 1, FLATNESS_LIMIT_I4)
+                myR += rcost(lc, pr, s_fixed, s_ent, s_bands, 3, 0, tnz4[bx] + lnz4[by], s_blv[m]);
+                myS = rd_score(myR, myH, myD, mySD, Q.lambda_i4);
             }
-            __syncthreads();
+            // lane 4m holds mode m's score: read the ten with v_readlane (wave-uniform
+            // results, no LDS), strict "<" in mode order = ties to the lowest mode
+            int64_t bsc = INT64_MAX;
             int best = 0;
-            for (int m = 1; m < 10; ++m)
-                if (s_sc[m] < s_sc[best]) best = m;
-            const int64_t sD = s_part[best][0], sSD = s_part[best][1], sR = s_part[best][2], sH = s_part[best][3];
+#pragma unroll
+            for (int mm = 0; mm < 10; ++mm) {
+                const int64_t sc = rdlane64(myS, 4 * mm);
+                if (sc < bsc) { bsc = sc; best = mm; }
+            }
+            const int64_t sD = rdlane64(myD, 4 * best), sSD = rdlane64(mySD, 4 * best), sR = rdlane64(myR, 4 * best),
+                          sH = rdlane64(myH, 4 * best);
+            const int nzb = __builtin_amdgcn_readlane(nzl, 4 * best);
             aS += rd_score(sR, sH, sD, sSD, Q.lambda_mode);
             header_bits += (int)sH;
             const bool stop = aS >= s_s16 || header_bits > 256 * 16 * 16;
             if (l < 16) s_lv4[i4][l] = s_blv[best][l];
             if (l < 16) s_best4[off + (l & 3) + (l >> 2) * BPS] = s_blk[best][(l & 3) + (l >> 2) * BPS];
-            const int nzb = s_i4nz[best];
             __syncthreads();
+            IK_STAMP(16);
             if (stop) {
                 if (l == 0) s_i4ok = 0;
                 break;
             }
             tnz4[bx] = lnz4[by] = nzb;
-            if (l == 0) {
-                s_modes4[i4] = (uint8_t)best;
-                // VP8IteratorRotateI4
+            if (l == 0) s_modes4[i4] = (uint8_t)best;
+            if (l < 4) {
+                // VP8IteratorRotateI4, one position per lane (the writes [-4, 4) never
+                // overlap another lane's reads: [4, 8) or the block)
                 uint8_t* top = s_bound + kTopLeftI4[i4];
                 const uint8_t* blk = s_best4 + off;
-                for (int i = 0; i <= 3; ++i) top[-4 + i] = blk[i + 3 * BPS];
-                if ((i4 & 3) != 3) {
-                    for (int i = 0; i <= 2; ++i) top[i] = blk[3 + (2 - i) * BPS];
-                } else {
-                    for (int i = 0; i <= 3; ++i) top[i] = top[i + 4];
-                }
+                const uint8_t b0 = blk[l + 3 * BPS];
+                const uint8_t b1 = (i4 & 3) != 3 ? (l < 3 ? blk[3 + (2 - l) * BPS] : top[3]) : top[l + 4];
+                top[-4 + l] = b0;
+                top[l] = b1;
             }
             __syncthreads();
+            IK_STAMP(17);
         }
     }
     __syncthreads();
+    IK_STAMP(3);
 
     // ---- chroma: lane = (mode, 4x4 block), 4 x 8 lanes ----
     {
@@ -471,9 +588,9 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
         const int off = bx * 4 + by * 4 * BPS + ch * 8;  // VP8ScanUV
         const bool act = l < 32;
         uint8_t* pred = s_predc[m];
-        if (act && n == 0) {
-            pred_nxn(pred, m, mx ? s_ul + 1 : nullptr, my ? s_ut : nullptr, 8);
-            pred_nxn(pred + 8, m, mx ? s_vl + 1 : nullptr, my ? s_vt : nullptr, 8);
+        if (act) {  // lane (m, n): row n of both channels
+            pred8_row(pred, m, mx ? s_ul + 1 : nullptr, my ? s_ut : nullptr, n);
+            pred8_row(pred + 8, m, mx ? s_vl + 1 : nullptr, my ? s_vt : nullptr, n);
         }
         __syncthreads();
         if (act) ftransform(s_in + 16 + off, pred + off, s_tmpc[m][n]);
@@ -542,6 +659,7 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
         s_buv = best;
     }
     __syncthreads();
+    IK_STAMP(4);
 
     // ---- outputs: reconstruction, the MB record, contexts, chroma errors ----
     const bool i4 = s_i4ok != 0;
@@ -595,6 +713,7 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
             d[ch * 2 + 1] = a.use_derr ? (int8_t)(e[2] - l1) : 0;
         }
     }
+    IK_STAMP(5);
 }
 
 // One wave per image: fold the epoch's token statistics in raster order, then refresh
@@ -676,3 +795,13 @@ hipError_t launch_vp8x_stats(const XArgs& a, int k0, int k1, int n, hipStream_t 
 
 }  // namespace vp8x
 }  // namespace ik
+
+#ifdef IK_VP8X_STAMPS
+extern "C" int ik_vp8x_stamps(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ik::vp8x::g_vp8x_stamps), sizeof(unsigned long long) * 32) != hipSuccess)
+        return -1;
+    unsigned long long z[32] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(ik::vp8x::g_vp8x_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -21,6 +21,7 @@ ap.add_argument("--n", type=int, default=64)
 ap.add_argument("--iters", type=int, default=3)
 ap.add_argument("--threads", type=int, default=16)
 ap.add_argument("--no-check", action="store_true", help="dev builds that change the output: skip the byte check")
+ap.add_argument("--stamps", action="store_true", help="IK_VP8X_STAMPS builds: per-phase clock sums of image 0's MBs")
 args = ap.parse_args()
 ik = _lib.load()
 assert ik.ik_init(0) == 0
@@ -33,6 +34,9 @@ dy, stride = _device_yuv_batch(ik, imgs)
 outs = (_lib.u8p * args.n)()
 lens = (ctypes.c_size_t * args.n)()
 times = []
+if args.stamps:
+    stamps = (ctypes.c_ulonglong * 32)()
+    ik.ik_vp8x_stamps(stamps)  # reset
 for it in range(args.iters + 1):
     t = time.perf_counter()
     assert ik.ik_webp_encode_exact_device(dy, stride, args.n, 512, 512, 80, ctypes.cast(outs, ctypes.c_void_p),
@@ -41,6 +45,15 @@ for it in range(args.iters + 1):
     files = [ctypes.string_at(outs[i], lens[i]) for i in range(args.n)]
     for i in range(args.n):
         ik.ik_buf_free(outs[i])
+if args.stamps:
+    ik.ik_vp8x_stamps(stamps)
+    names = {0: "prologue", 1: "i16", 2: "i16 select", 10: "i4 pred", 11: "i4 fwd rows", 12: "i4 fwd cols",
+             13: "i4 quant", 14: "i4 inv cols", 15: "i4 recon+spectral rows", 16: "i4 score+argmin+copy",
+             17: "i4 rotate", 3: "i4 tail", 4: "chroma", 5: "outputs"}
+    calls = (args.iters + 1) * 1024  # image 0's MBs per batch (512^2: 32 x 32)
+    tot = sum(stamps[i] for i in names)
+    for i, nm in names.items():
+        print(f"stamp {i:2d} {nm:24s} {stamps[i] / calls:10.0f} cycles/MB  {100.0 * stamps[i] / max(tot, 1):5.1f} %")
 orc = ikutil.Oracle()
 ref = [orc.webp_encode_rgb(orc.to_rgb8(base[i]), 80.0) for i in range(4)]
 assert args.no_check or all(files[i] == ref[i % 4] for i in range(args.n)), "bytes differ from libwebp"
