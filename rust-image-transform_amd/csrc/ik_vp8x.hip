@@ -408,14 +408,29 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
             const int m = l >> 2, r = l & 3;
             const bool act = l < 40;
             if (act) {  // the mode's block in registers, row r stored by lane r
-                uint8_t d[16];
-                pred4<4>(d, m, s_bound + kTopLeftI4[i4]);
-                uint32_t rw[4];
+                // the 13 boundary samples are the same for every lane: read them once and
+                // make them wave-uniform (SGPRs), so the ten divergent mode paths below are
+                // pure ALU instead of ten rounds of LDS reads
+                const uint8_t* tp = s_bound + kTopLeftI4[i4];
+                uint8_t e[13];
 #pragma unroll
-                for (int y = 0; y < 4; ++y)
-                    rw[y] = (uint32_t)d[4 * y] | ((uint32_t)d[4 * y + 1] << 8) | ((uint32_t)d[4 * y + 2] << 16) |
-                            ((uint32_t)d[4 * y + 3] << 24);
-                *reinterpret_cast<uint32_t*>(s_pred4[m] + r * BPS) = r == 0 ? rw[0] : r == 1 ? rw[1] : r == 2 ? rw[2] : rw[3];
+                for (int k = 0; k < 13; ++k) e[k] = (uint8_t)__builtin_amdgcn_readfirstlane((int)tp[k - 5]);
+                // every mode's block from the uniform samples (scalar ALU, no divergent
+                // paths); lane (m, r) keeps its mode's row r by selects
+                uint32_t mine = 0;
+#pragma unroll
+                for (int mm = 0; mm < 10; ++mm) {
+                    uint8_t d[16];
+                    pred4<4>(d, mm, e + 5);
+                    uint32_t rw[4];
+#pragma unroll
+                    for (int y = 0; y < 4; ++y)
+                        rw[y] = (uint32_t)d[4 * y] | ((uint32_t)d[4 * y + 1] << 8) | ((uint32_t)d[4 * y + 2] << 16) |
+                                ((uint32_t)d[4 * y + 3] << 24);
+                    const uint32_t row = r == 0 ? rw[0] : r == 1 ? rw[1] : r == 2 ? rw[2] : rw[3];
+                    mine = m == mm ? row : mine;
+                }
+                *reinterpret_cast<uint32_t*>(s_pred4[m] + r * BPS) = mine;
             }
             __syncthreads();
             IK_STAMP(10);
