@@ -459,10 +459,17 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
             __syncthreads();
             IK_STAMP(12);
             int nzl = 0, cnt = 0;
-            if (act) {  // QuantizeBlock: zigzag positions 4r .. 4r+3
+            if (act) {  // QuantizeBlock: zigzag positions 4r .. 4r+3 (all reads first, then the
+                        // stores: the reads of one position no longer wait for the last one's store)
+                int jj[4], vv[4], lv[4];
+#pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const int n = 4 * r + k, j = zigzag(n);
-                    const int v = s_cf4[m][j];
+                    jj[k] = zigzag(4 * r + k);
+                    vv[k] = s_cf4[m][jj[k]];
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int j = jj[k], v = vv[k];
                     const int sign = v < 0;
                     const uint32_t coeff = (uint32_t)((sign ? -v : v) + Q.y1.sharpen[j]);
                     int level = 0;
@@ -471,10 +478,14 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
                         if (level > 2047) level = 2047;
                         if (sign) level = -level;
                     }
-                    s_cf4[m][j] = (int16_t)(level * (int)Q.y1.q[j]);
-                    s_blv[m][n] = (int16_t)level;
+                    lv[k] = level;
                     nzl |= level != 0;
-                    cnt += n > 0 && level != 0;
+                    cnt += (4 * r + k) > 0 && level != 0;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    s_cf4[m][jj[k]] = (int16_t)(lv[k] * (int)Q.y1.q[jj[k]]);
+                    s_blv[m][4 * r + k] = (int16_t)lv[k];
                 }
             }
             __syncthreads();
