@@ -80,12 +80,14 @@ struct Arena {
     int device = 0;
 };
 struct ThreadRes {
-    std::map<int, hipStream_t> streams, copy_streams;
+    std::map<int, hipStream_t> streams, copy_streams, prio_streams;
+    std::map<int, hipEvent_t> prio_events;
     std::map<std::pair<int, int>, Arena> dev;  // (device, slot)
-    Arena pinned[8];
+    Arena pinned[10];
     void release() {
         for (auto& kv : streams) (void)hipStreamSynchronize(kv.second);
         for (auto& kv : copy_streams) (void)hipStreamSynchronize(kv.second);
+        for (auto& kv : prio_streams) (void)hipStreamSynchronize(kv.second);
         for (auto& kv : dev) {
             if (!kv.second.p) continue;
             (void)hipSetDevice(kv.second.device);
@@ -99,8 +101,12 @@ struct ThreadRes {
             }
         for (auto& kv : streams) (void)hipStreamDestroy(kv.second);
         for (auto& kv : copy_streams) (void)hipStreamDestroy(kv.second);
+        for (auto& kv : prio_streams) (void)hipStreamDestroy(kv.second);
+        for (auto& kv : prio_events) (void)hipEventDestroy(kv.second);
         streams.clear();
         copy_streams.clear();
+        prio_streams.clear();
+        prio_events.clear();
         dev.clear();
         for (Arena& a : pinned) a = Arena();
     }
@@ -269,6 +275,29 @@ hipStream_t thread_copy_stream() {
     return s;
 }
 
+bool thread_prio_stream(hipStream_t* out, hipEvent_t* ev) {
+    ThreadRes& r = tres();
+    const int d = current_device();
+    auto it = r.prio_streams.find(d);
+    if (it == r.prio_streams.end()) {
+        (void)hipSetDevice(d);
+        hipStream_t s = nullptr;
+        hipEvent_t e = nullptr;
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
+        if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest) != hipSuccess) return false;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            (void)hipStreamDestroy(s);
+            return false;
+        }
+        it = r.prio_streams.emplace(d, s).first;
+        r.prio_events[d] = e;
+    }
+    *out = it->second;
+    *ev = r.prio_events[d];
+    return true;
+}
+
 uint8_t* pinned_slot(int slot, size_t bytes) {
     Arena& a = tres().pinned[slot];
     if (bytes <= a.cap) return a.p;
@@ -276,6 +305,8 @@ uint8_t* pinned_slot(int slot, size_t bytes) {
         (void)hipStreamSynchronize(thread_stream());  // no copy may still read the old buffer
         auto cs = tres().copy_streams.find(current_device());
         if (cs != tres().copy_streams.end()) (void)hipStreamSynchronize(cs->second);
+        auto ps = tres().prio_streams.find(current_device());
+        if (ps != tres().prio_streams.end()) (void)hipStreamSynchronize(ps->second);
         (void)hipHostFree(a.p);
         mem_stat(kMemArenaPinned, -(int64_t)a.cap);
     }
@@ -356,6 +387,8 @@ uint8_t* scratch_slot(int slot, size_t bytes) {
     if (bytes <= a.cap) return a.p;
     if (a.p) {
         (void)hipStreamSynchronize(thread_stream());
+        auto ps = tres().prio_streams.find(d);
+        if (ps != tres().prio_streams.end()) (void)hipStreamSynchronize(ps->second);
         (void)hipFree(a.p);
         mem_stat(kMemArenaDev, -(int64_t)a.cap);
     }

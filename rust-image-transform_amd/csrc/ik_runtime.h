@@ -185,12 +185,17 @@ uint64_t request_cost(const uint8_t* b, size_t n, int64_t w, int64_t h, int fmt)
 
 hipStream_t thread_stream();  // per-thread, per-device non-blocking stream
 hipStream_t thread_copy_stream();  // a second one, for uploads that overlap the first's kernels
+// a third, at the highest priority, and an event to order it after the first (the
+// exact WebP coder's launches); false if it cannot be made
+bool thread_prio_stream(hipStream_t* s, hipEvent_t* ev);
 size_t pitch_for(uint32_t w, uint32_t c);
 uint8_t* scratch(size_t bytes);  // per-thread device scratch, valid until the next call
 // per-thread, per-device grow-only device arenas for batch work (slot 1: JPEG
 // batch decode, slot 2: PNG batch decode); valid until the next call with that slot
 uint8_t* scratch_slot(int slot, size_t bytes);
-uint8_t* pinned_slot(int slot, size_t bytes);  // per-thread grow-only pinned host arenas
+uint8_t* pinned_slot(int slot, size_t bytes);  // per-thread grow-only pinned host arenas (slots 0..9)
+// the exact WebP coder's arenas: its device work area; its constants in, its records out
+constexpr int kScratchExact = 8, kPinnedExactIn = 8, kPinnedExactOut = 9;
 int copy_h2d_2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,
                 size_t height, hipStream_t s);
 int copy_d2h_2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,

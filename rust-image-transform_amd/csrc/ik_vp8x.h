@@ -34,8 +34,8 @@ IK_HD int xabs(int v) { return v < 0 ? -v : v; }
 IK_HD uint8_t xclip8(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
 IK_HD int bit_cost(int bit, int p) { return !bit ? kEntropyCost[p] : kEntropyCost[255 - p]; }
 
-// ---- set-up (quant_enc.c SetupMatrices), host ----
-inline int expand_matrix(XMatrix& m, int type) {
+// ---- set-up (quant_enc.c SetupMatrices) ----
+IK_HD int expand_matrix(XMatrix& m, int type) {
     constexpr int kBias[3][2] = {{96, 110}, {96, 108}, {110, 115}};
     int sum = 0;
     for (int i = 0; i < 2; ++i) {
@@ -56,7 +56,7 @@ inline int expand_matrix(XMatrix& m, int type) {
     return (sum + 8) >> 4;
 }
 
-inline XSeg setup_segment(int q, int dq_uv_dc, int dq_uv_ac, int sns) {
+IK_HD XSeg setup_segment(int q, int dq_uv_dc, int dq_uv_ac, int sns) {
     auto clip = [](int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; };
     XSeg s{};
     s.y1.q[0] = kDcTable[clip(q, 0, 127)];
@@ -459,7 +459,7 @@ IK_HD void pred4(uint8_t* dst, int mode, const uint8_t* top) {
 }
 
 // ---- per-MB record the device hands to the host bitstream writer ----
-struct XMB {
+struct alignas(16) XMB {
     uint8_t ymode;      // 0..3 i16 DC/TM/V/H, 4 = intra-4
     uint8_t uvmode;
     uint8_t seg;
@@ -468,7 +468,9 @@ struct XMB {
     int16_t dc[16];     // i16: the Y2 levels (zigzag)
     int16_t ac[16][16]; // luma levels per block (raster block order), zigzag
     int16_t uv[8][16];  // U blocks 0..3, V 4..7
+    uint8_t pad2[12];   // a whole number of 16-byte stores
 };
+static_assert(sizeof(XMB) == 832, "XMB is stored as 52 16-byte words");
 
 // The token statistics of one MB (frame_enc.c RecordTokens, token_enc.c
 // VP8RecordCoeffTokens' statistics side); nz contexts in/out like the iterator's.

@@ -2,24 +2,37 @@
 // decisions (reference src/transform.rs:129-137 -> webp 0.3.1 -> libwebp; the arithmetic
 // is ik_vp8x.h, the same as oracle/vp8_modes.c, whose files equal WebPEncodeRGB's).
 //
-// Dependencies and how they are scheduled:
+// Dependencies:
 //  - a macroblock predicts from the reconstruction of its left, top-left, top and
-//    top-right neighbours, and reads their non-zero contexts and chroma DC errors: all
-//    MBs with the same mb_x + 2 mb_y are independent (a diagonal);
+//    top-right neighbours, and reads their non-zero contexts and chroma DC errors;
 //  - libwebp's token loop refreshes the coefficient probabilities -- hence the level
 //    costs every decision uses -- from the statistics of all MBs before it, at MB
 //    indices M, 2M+1, 3M+2, ... (M = max(mb_count / 8, 96)): an epoch's MBs may only
 //    start when every earlier MB is decided and the statistics folded.
-// So per epoch: one k_vp8x_mb launch per diagonal (every image of the batch in the
-// launch, grid.y = image), then k_vp8x_stats (one wave per image) folds the epoch's
-// token statistics in raster order (libwebp halves a counter pair at 65534, so the
-// order matters) and refreshes probabilities and level costs.
 //
-// k_vp8x_mb: one wave64 per MB; the modes of each stage run on their own lanes --
-// i16: 4 lanes, intra-4: 10 lanes per sub-block (16 sub-blocks in order), chroma: 4
-// lanes -- and the winner is the lowest score, ties to the lowest mode (libwebp's
-// early-out in the intra-4 loop never changes that argmin: a skipped mode's partial
-// score already reaches the best full score).
+// k_vp8x_run is ONE persistent launch per call.  Its workgroups (one wave each) take
+// tasks by ticket from a global counter: the MBs of every image in (epoch, diagonal
+// mb_x + 2 mb_y, image) order, each epoch's per-image statistics fold after the
+// epoch's MBs.  A task waits only for what it reads -- an MB for its left and
+// top-right neighbours (which imply the top-left and top) and its epoch's level
+// costs, a fold for its epoch's MB count -- by polling hand-off words, so image 0's
+// next diagonal starts as soon as its own MBs are done, not when the slowest MB of
+// the whole batch is; no launch per diagonal, no host round trip.  Every dependency
+// holds a smaller ticket, so the lowest unfinished ticket can always run and the grid
+// drains whatever the residency; every wait is bounded (a timeout sets the error word
+// and the grid drains).
+//
+// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility, recipe R1): the payload
+// -- an MB's edge record (XEdge) and decision record (XMB), a fold's statistics,
+// probabilities and level costs -- is stored write-through (sc1, 16-byte stores),
+// drained (s_waitcnt vmcnt(0)), then one lane sets the flag (agent-scope atomic);
+// the consumer polls the flag, takes an agent-scope acquire, and loads plainly.
+//
+// An MB task: one wave64; the modes of each stage run on their own lanes -- i16: 4
+// lanes, intra-4: 10 lanes per sub-block (16 sub-blocks in order), chroma: 4 lanes --
+// and the winner is the lowest score, ties to the lowest mode (libwebp's early-out in
+// the intra-4 loop never changes that argmin: a skipped mode's partial score already
+// reaches the best full score).
 #include <hip/hip_runtime.h>
 
 #include "ik_vp8x.h"
@@ -138,6 +151,87 @@ __device__ __forceinline__ int64_t rd_score(int64_t R, int64_t H, int64_t D, int
 
 // dev switch IK_VP8X_STAMPS: per-phase shader-clock sums over image 0's MBs
 // (tools/vp8x_timing.py --stamps reads them through ik_vp8x_stamps)
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+// buffer intrinsics' cache-policy operand: sc1 (gfx940+ CPol::SC1) -- write-through stores
+constexpr int kCpolSc1 = 16;
+
+// a wave-uniform 64-bit value in SGPRs
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// lanes [0, nbytes / 16) store their 16 bytes of `src` (LDS) to `dst` (wave-uniform)
+// write-through; the other lanes' offsets are out of range (dropped)
+__device__ __forceinline__ void store_wt(void* dst, const void* src, uint32_t nbytes, int l) {
+    const uint64_t base = uniform_u64((uint64_t)(uintptr_t)dst);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)nbytes, 0x00020000);
+    const bool act = (uint32_t)l < nbytes / 16;
+    const u32x4 v = act ? reinterpret_cast<const u32x4*>(src)[l] : u32x4{0, 0, 0, 0};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, act ? 16 * l : 0x7ffffff0, 0, kCpolSc1);
+}
+
+// the MB task's LDS (the fold's overlays it)
+struct MbLds {
+    alignas(16) uint16_t lc[kCostRows * kLevelTab];  // the image's level costs (13 KB), read at every coefficient
+    alignas(16) uint8_t pr[1056];
+    alignas(16) uint16_t fixed[2048];
+    uint16_t ent[256];
+    uint16_t fi4[1000];
+    uint8_t bands[17];
+    alignas(16) XSeg Q;  // the segment's matrices and lambdas, read per lane in every quantisation
+    alignas(16) uint8_t in[BPS * 16];  // Y 0..15, U 16..23, V 24..31
+    uint8_t yl[17], yt[20], ul[9], ut[8], vl[9], vt[8];
+    int tnz[9], lnz[9];
+    int8_t derr_t[2][2], derr_l[2][2];
+    alignas(16) uint8_t rec16[4][BPS * 16];
+    alignas(16) int16_t lv16[4][17][16];
+    int64_t sc[16], part[16][4];
+    int flat[4], nz16[4];
+    alignas(16) uint8_t best4[BPS * 16];
+    uint8_t bound[37];
+    int16_t lv4[16][16];
+    uint8_t modes4[16];
+    uint8_t nbm[8];  // the left MB's right column of sub-block modes, the top MB's bottom row
+    alignas(16) uint8_t blk[10][4 * BPS];
+    alignas(16) int16_t blv[10][16];
+    alignas(16) uint8_t recuv[4][BPS * 8];
+    alignas(16) int16_t lvuv[4][8][16];
+    int8_t duv[4][2][3];
+    int b16, buv, i4ok;
+    int64_t s16;  // the i16 best's score at lambda_mode (the intra-4 bar)
+    // per-lane work buffers (private arrays would live in scratch memory); the
+    // neighbours' edge records overlay pred16 (prologue only), the outgoing records
+    // tmp16 and pred4 (dead by the outputs)
+    alignas(16) uint8_t pred16[4][BPS * 16];
+    alignas(16) int16_t tmp16[4][16][16];
+    alignas(16) uint8_t pred4[10][4 * BPS];
+    alignas(16) uint8_t predc[4][BPS * 8];
+    alignas(16) int16_t tmpc[4][8][16];
+    int16_t dc16[4][16];
+    int bnz[4][16], cnz[4][8];
+    int ft4[10][16], C4[10][16], tt4[10][2][16];
+    int16_t cf4[10][16];
+};
+static_assert(sizeof(((MbLds*)0)->pred16) >= 4 * sizeof(XEdge), "neighbour records overlay pred16");
+static_assert(sizeof(((MbLds*)0)->tmp16) >= sizeof(XMB), "the MB record overlays tmp16");
+static_assert(sizeof(((MbLds*)0)->pred4) >= sizeof(XEdge), "the edge record overlays pred4");
+
+// the statistics fold's LDS
+struct FoldLds {
+    alignas(16) uint32_t st[1056];
+    alignas(16) uint8_t pr[1056];
+    alignas(16) uint16_t lc[kCostRows * kLevelTab];
+    alignas(16) XMB mb;
+    int serial;
+};
+
+union XLds {
+    MbLds m;
+    FoldLds f;
+};
+
 #ifdef IK_VP8X_STAMPS
 __device__ unsigned long long g_vp8x_stamps[32];
 #define IK_STAMP(i)                                                         \
@@ -152,41 +246,75 @@ __device__ unsigned long long g_vp8x_stamps[32];
 #define IK_STAMP(i) do {} while (0)
 #endif
 
-__global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__ list) {
-    const int l = threadIdx.x;
-    const int img = blockIdx.y;
-    const int mb = list[blockIdx.x];
+// One MB: libwebp's VP8Decimate (i16, intra-4, chroma; RD by the image's current level
+// costs), then the MB's decision record and edge record, stored write-through.
+__device__ __forceinline__ void mb_body(const XArgs& a, int img, int mb, MbLds& S, int l) {
 #ifdef IK_VP8X_STAMPS
     unsigned long long t_prev = clock64();
 #endif
     const int mx = mb % a.mb_w, my = mb / a.mb_w;
     const int nmb = a.mb_w * a.mb_h;
-    const int W = a.mb_w * 16, H = a.mb_h * 16;
     const int uw = (a.w + 1) >> 1, uh = (a.h + 1) >> 1;
     const uint8_t* Y = a.yuv + (size_t)img * a.yuv_stride;
     const uint8_t* U = Y + (size_t)a.w * a.h;
     const uint8_t* V = U + (size_t)uw * uh;
-    uint8_t* RY = a.rec + (size_t)img * a.rec_stride;
-    uint8_t* RU = RY + (size_t)W * H;
-    uint8_t* RV = RU + (size_t)(W / 2) * (H / 2);
-    XMB* mbs = a.mbs + (size_t)img * nmb;
-    uint32_t* nzs = a.nz + (size_t)img * nmb;
-    int8_t* derrs = a.derr + (size_t)img * nmb * 8;
+    const XEdge* edges = a.edges + (size_t)img * nmb;
     const int sg = a.seg[(size_t)img * nmb + mb];
-    // the image's level costs and probabilities, read at every coefficient of every
-    // candidate: staged in LDS (13.4 KB)
-#ifdef IK_VP8X_LC_GLOBAL
-    const uint16_t* lc = a.lc + (size_t)img * kCostRows * kLevelTab;
-#else
-    __shared__ __attribute__((aligned(16))) uint16_t lc[kCostRows * kLevelTab];
-#endif
-    __shared__ __attribute__((aligned(16))) uint8_t pr[1056];
-    __shared__ __attribute__((aligned(16))) uint16_t s_fixed[2048];
-    __shared__ uint16_t s_ent[256];
-    __shared__ uint8_t s_bands[17];
-    __shared__ uint16_t s_fi4[1000];
+    auto& lc = S.lc;
+    auto& pr = S.pr;
+    auto& s_fixed = S.fixed;
+    auto& s_ent = S.ent;
+    auto& s_bands = S.bands;
+    auto& s_fi4 = S.fi4;
+    auto& s_in = S.in;
+    auto& s_yl = S.yl;
+    auto& s_yt = S.yt;
+    auto& s_ul = S.ul;
+    auto& s_ut = S.ut;
+    auto& s_vl = S.vl;
+    auto& s_vt = S.vt;
+    auto& s_tnz = S.tnz;
+    auto& s_lnz = S.lnz;
+    auto& s_derr_t = S.derr_t;
+    auto& s_derr_l = S.derr_l;
+    auto& s_rec16 = S.rec16;
+    auto& s_lv16 = S.lv16;
+    auto& s_sc = S.sc;
+    auto& s_part = S.part;
+    auto& s_flat = S.flat;
+    auto& s_nz16 = S.nz16;
+    auto& s_best4 = S.best4;
+    auto& s_bound = S.bound;
+    auto& s_lv4 = S.lv4;
+    auto& s_modes4 = S.modes4;
+    auto& s_nbm = S.nbm;
+    auto& s_blk = S.blk;
+    auto& s_blv = S.blv;
+    auto& s_recuv = S.recuv;
+    auto& s_lvuv = S.lvuv;
+    auto& s_duv = S.duv;
+    auto& s_b16 = S.b16;
+    auto& s_buv = S.buv;
+    auto& s_i4ok = S.i4ok;
+    auto& s_s16 = S.s16;
+    auto& s_pred16 = S.pred16;
+    auto& s_tmp16 = S.tmp16;
+    auto& s_pred4 = S.pred4;
+    auto& s_predc = S.predc;
+    auto& s_tmpc = S.tmpc;
+    auto& s_dc16 = S.dc16;
+    auto& s_bnz = S.bnz;
+    auto& s_cnz = S.cnz;
+    auto& s_ft4 = S.ft4;
+    auto& s_C4 = S.C4;
+    auto& s_tt4 = S.tt4;
+    auto& s_cf4 = S.cf4;
+    uint8_t (*s_nb)[sizeof(XEdge)] = reinterpret_cast<uint8_t (*)[sizeof(XEdge)]>(&S.pred16[0][0]);
     // staging: every lane issues all of its global reads first (one memory latency for
-    // the whole prologue), then writes them to LDS
+    // the whole prologue), then writes them to LDS: libwebp's fixed cost tables, the
+    // image's probabilities and level costs, the segment's matrices, the source MB
+    // (ImportBlock: clamped coordinates) and the neighbours' edge records (left, top,
+    // top-right, top-left; 16 bytes per lane)
     {
         constexpr int kFi4 = (1000 + 63) / 64, kFix = 2048 / 64, kEnt = 256 / 64;
         constexpr int kPr = (1056 / 16 + 63) / 64;
@@ -201,6 +329,30 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
         uint4 rpr[kPr];
 #pragma unroll
         for (int j = 0; j < kPr; ++j) rpr[j] = gp[min(l + 64 * j, 1056 / 16 - 1)];
+        const int q = l >> 3;
+        int nb = -1;
+        if (l < 32) {
+            if (q == 0 && mx) nb = mb - 1;
+            else if (q == 1 && my) nb = mb - a.mb_w;
+            else if (q == 2 && my && mx < a.mb_w - 1) nb = mb - a.mb_w + 1;
+            else if (q == 3 && mx && my) nb = mb - a.mb_w - 1;
+        }
+        const uint4 rnb = nb >= 0 ? reinterpret_cast<const uint4*>(edges + nb)[l & 7] : uint4{0, 0, 0, 0};
+        uint8_t rin[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = l + 64 * k;
+            const int y = i >> 4, x = i & 15;
+            rin[k] = Y[(size_t)min(16 * my + y, a.h - 1) * a.w + min(16 * mx + x, a.w - 1)];
+        }
+        uint8_t ruv[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int i = l + 64 * k;
+            const int c = i >> 6, kk = i & 63, y = kk >> 3, x = kk & 7;
+            const uint8_t* P = c ? V : U;
+            ruv[k] = P[(size_t)min(8 * my + y, uh - 1) * uw + min(8 * mx + x, uw - 1)];
+        }
 #pragma unroll
         for (int j = 0; j < kFi4; ++j)
             if (l + 64 * j < 1000) s_fi4[l + 64 * j] = rf4[j];
@@ -208,99 +360,72 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
         for (int j = 0; j < kFix; ++j) s_fixed[l + 64 * j] = rfx[j];
 #pragma unroll
         for (int j = 0; j < kEnt; ++j) s_ent[l + 64 * j] = ren[j];
-#ifndef IK_VP8X_LC_GLOBAL
         {  // 13 x 16 B per lane (a register array this size would go to scratch)
             const uint4* g = (const uint4*)(a.lc + (size_t)img * kCostRows * kLevelTab);
             for (int i = l; i < kCostRows * kLevelTab / 8; i += 64) ((uint4*)lc)[i] = g[i];
         }
-#endif
 #pragma unroll
         for (int j = 0; j < kPr; ++j)
             if (l + 64 * j < 1056 / 16) ((uint4*)pr)[l + 64 * j] = rpr[j];
+        if (nb >= 0) reinterpret_cast<uint4*>(s_nb[q])[l & 7] = rnb;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = l + 64 * k;
+            s_in[(i >> 4) * BPS + (i & 15)] = rin[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int i = l + 64 * k;
+            const int c = i >> 6, kk = i & 63;
+            s_in[(kk >> 3) * BPS + 16 + 8 * c + (kk & 7)] = ruv[k];
+        }
     }
     if (l < 17) s_bands[l] = kEncBands[l];
-    // the segment's matrices and lambdas, read per lane in every quantisation: LDS
-    __shared__ __attribute__((aligned(16))) XSeg s_Q;
     {
         static_assert(sizeof(XSeg) % 4 == 0, "XSeg copied as words");
         const uint32_t* gq = reinterpret_cast<const uint32_t*>(a.segs + img * 4 + sg);
-        for (int i = l; i < (int)(sizeof(XSeg) / 4); i += 64) reinterpret_cast<uint32_t*>(&s_Q)[i] = gq[i];
+        for (int i = l; i < (int)(sizeof(XSeg) / 4); i += 64) reinterpret_cast<uint32_t*>(&S.Q)[i] = gq[i];
     }
-    const XSeg& Q = s_Q;
-
-    __shared__ __attribute__((aligned(16))) uint8_t s_in[BPS * 16];      // Y 0..15, U 16..23, V 24..31
-    __shared__ uint8_t s_yl[17], s_yt[20], s_ul[9], s_ut[8], s_vl[9], s_vt[8];
-    __shared__ int s_tnz[9], s_lnz[9];
-    __shared__ int8_t s_derr_t[2][2], s_derr_l[2][2];
-    __shared__ __attribute__((aligned(16))) uint8_t s_rec16[4][BPS * 16];
-    __shared__ __attribute__((aligned(16))) int16_t s_lv16[4][17][16];
-    __shared__ int64_t s_sc[16], s_part[16][4];
-    __shared__ int s_flat[4], s_nz16[4];
-    __shared__ __attribute__((aligned(16))) uint8_t s_best4[BPS * 16];
-    __shared__ uint8_t s_bound[37];
-    __shared__ int16_t s_lv4[16][16];
-    __shared__ uint8_t s_modes4[16];
-    __shared__ uint8_t s_nbm[8];  // the left MB's right column of sub-block modes, the top MB's bottom row
-    __shared__ __attribute__((aligned(16))) uint8_t s_blk[10][4 * BPS];
-    __shared__ __attribute__((aligned(16))) int16_t s_blv[10][16];
-    __shared__ __attribute__((aligned(16))) uint8_t s_recuv[4][BPS * 8];
-    __shared__ __attribute__((aligned(16))) int16_t s_lvuv[4][8][16];
-    __shared__ int8_t s_duv[4][2][3];
-    __shared__ int s_b16, s_buv, s_i4ok;
-    __shared__ int64_t s_s16;  // the i16 best's score at lambda_mode (the intra-4 bar)
-    // per-lane work buffers in LDS (private arrays would live in scratch memory)
-    __shared__ __attribute__((aligned(16))) uint8_t s_pred16[4][BPS * 16];
-    __shared__ __attribute__((aligned(16))) int16_t s_tmp16[4][16][16];
-    __shared__ __attribute__((aligned(16))) uint8_t s_pred4[10][4 * BPS];
-    __shared__ __attribute__((aligned(16))) uint8_t s_predc[4][BPS * 8];
-    __shared__ __attribute__((aligned(16))) int16_t s_tmpc[4][8][16];
-    __shared__ int16_t s_dc16[4][16];
-    __shared__ int s_bnz[4][16], s_cnz[4][8];
-    __shared__ int s_ft4[10][16], s_C4[10][16], s_tt4[10][2][16];
-    __shared__ int16_t s_cf4[10][16];
-
-    // ---- load the source MB (ImportBlock: clamped coordinates) and the boundaries ----
-    for (int i = l; i < 256; i += 64) {
-        const int y = i >> 4, x = i & 15;
-        s_in[y * BPS + x] = Y[(size_t)min(16 * my + y, a.h - 1) * a.w + min(16 * mx + x, a.w - 1)];
-    }
-    for (int i = l; i < 128; i += 64) {
-        const int c = i >> 6, k = i & 63, y = k >> 3, x = k & 7;
-        const uint8_t* P = c ? V : U;
-        s_in[y * BPS + 16 + 8 * c + x] = P[(size_t)min(8 * my + y, uh - 1) * uw + min(8 * mx + x, uw - 1)];
-    }
-    if (l < 16) {
-        s_yl[1 + l] = mx ? RY[(size_t)(16 * my + l) * W + 16 * mx - 1] : 129;
-        s_yt[l] = my ? RY[(size_t)(16 * my - 1) * W + 16 * mx + l] : 127;
-    } else if (l < 20) {
-        const int k = l - 16;
-        s_yt[16 + k] = !my ? 127 : (mx < a.mb_w - 1 ? RY[(size_t)(16 * my - 1) * W + 16 * mx + 16 + k]
-                                                       : RY[(size_t)(16 * my - 1) * W + 16 * mx + 15]);
-    } else if (l < 28) {
-        const int k = l - 20;
-        s_ul[1 + k] = mx ? RU[(size_t)(8 * my + k) * (W / 2) + 8 * mx - 1] : 129;
-        s_vl[1 + k] = mx ? RV[(size_t)(8 * my + k) * (W / 2) + 8 * mx - 1] : 129;
-        s_ut[k] = my ? RU[(size_t)(8 * my - 1) * (W / 2) + 8 * mx + k] : 127;
-        s_vt[k] = my ? RV[(size_t)(8 * my - 1) * (W / 2) + 8 * mx + k] : 127;
-    } else if (l == 28) {
-        s_yl[0] = !mx ? (my ? 129 : 127) : (my ? RY[(size_t)(16 * my - 1) * W + 16 * mx - 1] : 127);
-        s_ul[0] = !mx ? (my ? 129 : 127) : (my ? RU[(size_t)(8 * my - 1) * (W / 2) + 8 * mx - 1] : 127);
-        s_vl[0] = !mx ? (my ? 129 : 127) : (my ? RV[(size_t)(8 * my - 1) * (W / 2) + 8 * mx - 1] : 127);
-    } else if (l == 29) {  // NzToBytes (+ the row's running left DC bit in bit 25)
-        const uint32_t tnz = my ? nzs[mb - a.mb_w] : 0u, lnz = mx ? nzs[mb - 1] : 0u;
-        const int tb[9] = {12, 13, 14, 15, 18, 19, 22, 23, 24}, lb[8] = {3, 7, 11, 15, 17, 19, 21, 23};
-        for (int i = 0; i < 9; ++i) s_tnz[i] = (int)((tnz >> tb[i]) & 1u);
-        for (int i = 0; i < 8; ++i) s_lnz[i] = (int)((lnz >> lb[i]) & 1u);
-        s_lnz[8] = (int)((lnz >> 25) & 1u);
-    } else if (l >= 32 && l < 40) {
-        const int k = l - 32;
-        s_nbm[k] = k < 4 ? (mx ? mbs[mb - 1].bmodes[k * 4 + 3] : 0) : (my ? mbs[mb - a.mb_w].bmodes[12 + k - 4] : 0);
-    } else if (l == 30) {
-        for (int c = 0; c < 2; ++c)
-            for (int k = 0; k < 2; ++k) {
-                s_derr_t[c][k] = (a.use_derr && my) ? derrs[(size_t)(mb - a.mb_w) * 8 + c * 2 + k] : 0;
-                s_derr_l[c][k] = (a.use_derr && mx) ? derrs[(size_t)(mb - 1) * 8 + 4 + c * 2 + k] : 0;
-            }
+    const XSeg& Q = S.Q;
+    __syncthreads();
+    // ---- the boundaries (libwebp's 127 / 129 edge rules) from the neighbours' records ----
+    {
+        const XEdge& EL = *reinterpret_cast<const XEdge*>(s_nb[0]);
+        const XEdge& ET = *reinterpret_cast<const XEdge*>(s_nb[1]);
+        const XEdge& ETR = *reinterpret_cast<const XEdge*>(s_nb[2]);
+        const XEdge& ETL = *reinterpret_cast<const XEdge*>(s_nb[3]);
+        if (l < 16) {
+            s_yl[1 + l] = mx ? EL.yright[l] : 129;
+            s_yt[l] = my ? ET.ybot[l] : 127;
+        } else if (l < 20) {
+            const int k = l - 16;
+            s_yt[16 + k] = !my ? 127 : (mx < a.mb_w - 1 ? ETR.ybot[k] : ET.ybot[15]);
+        } else if (l < 28) {
+            const int k = l - 20;
+            s_ul[1 + k] = mx ? EL.uright[k] : 129;
+            s_vl[1 + k] = mx ? EL.vright[k] : 129;
+            s_ut[k] = my ? ET.ubot[k] : 127;
+            s_vt[k] = my ? ET.vbot[k] : 127;
+        } else if (l == 28) {
+            s_yl[0] = !mx ? (my ? 129 : 127) : (my ? ETL.ybot[15] : 127);
+            s_ul[0] = !mx ? (my ? 129 : 127) : (my ? ETL.ubot[7] : 127);
+            s_vl[0] = !mx ? (my ? 129 : 127) : (my ? ETL.vbot[7] : 127);
+        } else if (l == 29) {  // NzToBytes (+ the row's running left DC bit in bit 25)
+            const uint32_t tnz = my ? ET.nz : 0u, lnz = mx ? EL.nz : 0u;
+            const int tb[9] = {12, 13, 14, 15, 18, 19, 22, 23, 24}, lb[8] = {3, 7, 11, 15, 17, 19, 21, 23};
+            for (int i = 0; i < 9; ++i) s_tnz[i] = (int)((tnz >> tb[i]) & 1u);
+            for (int i = 0; i < 8; ++i) s_lnz[i] = (int)((lnz >> lb[i]) & 1u);
+            s_lnz[8] = (int)((lnz >> 25) & 1u);
+        } else if (l >= 32 && l < 40) {
+            const int k = l - 32;
+            s_nbm[k] = k < 4 ? (mx ? EL.bmr[k] : 0) : (my ? ET.bmb[k - 4] : 0);
+        } else if (l == 30) {
+            for (int c = 0; c < 2; ++c)
+                for (int k = 0; k < 2; ++k) {
+                    s_derr_t[c][k] = (a.use_derr && my) ? ET.derr[c * 2 + k] : 0;
+                    s_derr_l[c][k] = (a.use_derr && mx) ? EL.derr[4 + c * 2 + k] : 0;
+                }
+        }
     }
     __syncthreads();
     IK_STAMP(0);
@@ -687,23 +812,33 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
     __syncthreads();
     IK_STAMP(4);
 
-    // ---- outputs: reconstruction, the MB record, contexts, chroma errors ----
+    // ---- outputs: the MB record, the edge record (reconstruction edges, contexts,
+    // chroma errors, edge sub-block modes), built in LDS and stored write-through ----
     const bool i4 = s_i4ok != 0;
     const int b16 = s_b16, buv = s_buv;
-    for (int i = l; i < 256; i += 64) {
-        const int y = i >> 4, x = i & 15;
-        RY[(size_t)(16 * my + y) * W + 16 * mx + x] = i4 ? s_best4[y * BPS + x] : s_rec16[b16][y * BPS + x];
-    }
-    for (int i = l; i < 128; i += 64) {
-        const int c = i >> 6, k = i & 63, y = k >> 3, x = k & 7;
-        (c ? RV : RU)[(size_t)(8 * my + y) * (W / 2) + 8 * mx + x] = s_recuv[buv][y * BPS + 8 * c + x];
-    }
-    XMB& o = mbs[mb];
+    XMB& o = *reinterpret_cast<XMB*>(&s_tmp16[0][0][0]);
+    XEdge& E = *reinterpret_cast<XEdge*>(&s_pred4[0][0]);
+    const uint8_t* ry = i4 ? s_best4 : s_rec16[b16];
+    const uint8_t* ruv = s_recuv[buv];
     for (int i = l; i < 16 * 16; i += 64) o.ac[i >> 4][i & 15] = i4 ? s_lv4[i >> 4][i & 15] : s_lv16[b16][1 + (i >> 4)][i & 15];
     for (int i = l; i < 8 * 16; i += 64) o.uv[i >> 4][i & 15] = s_lvuv[buv][i >> 4][i & 15];
     if (l < 16) {
         o.dc[l] = i4 ? 0 : s_lv16[b16][0][l];
         o.bmodes[l] = i4 ? s_modes4[l] : (uint8_t)b16;
+        E.ybot[l] = ry[15 * BPS + l];
+        E.yright[l] = ry[l * BPS + 15];
+    } else if (l < 24) {
+        const int k = l - 16;
+        E.ubot[k] = ruv[7 * BPS + k];
+        E.vbot[k] = ruv[7 * BPS + 8 + k];
+        E.uright[k] = ruv[k * BPS + 7];
+        E.vright[k] = ruv[k * BPS + 15];
+    } else if (l < 28) {
+        const int k = l - 24;
+        E.bmr[k] = i4 ? s_modes4[4 * k + 3] : (uint8_t)b16;
+        E.bmb[k] = i4 ? s_modes4[12 + k] : (uint8_t)b16;
+    } else if (l < 40) {
+        o.pad2[l - 28] = 0;
     }
     if (l == 0) {
         o.ymode = i4 ? 4 : (uint8_t)b16;
@@ -727,58 +862,54 @@ __global__ __launch_bounds__(64) void k_vp8x_mb(XArgs a, const int* __restrict__
         nz |= (uint32_t)((lnz[0] << 3) | (lnz[1] << 7) | (lnz[2] << 11));
         nz |= (uint32_t)((lnz[4] << 17) | (lnz[6] << 21));
         nz |= (uint32_t)(lnz[8] << 25);
-        nzs[mb] = nz;
+        E.nz = nz;
         // StoreDiffusionErrors: [0..3] the top pair per channel (for the MB below), [4..7] the left pair
-        int8_t* d = derrs + (size_t)mb * 8;
         for (int ch = 0; ch < 2; ++ch) {
             const int8_t* e = s_duv[buv][ch];
             const int8_t l1 = a.use_derr ? (int8_t)((3 * e[2]) >> 2) : 0;
-            d[4 + ch * 2 + 0] = a.use_derr ? e[0] : 0;
-            d[4 + ch * 2 + 1] = l1;
-            d[ch * 2 + 0] = a.use_derr ? e[1] : 0;
-            d[ch * 2 + 1] = a.use_derr ? (int8_t)(e[2] - l1) : 0;
+            E.derr[4 + ch * 2 + 0] = a.use_derr ? e[0] : 0;
+            E.derr[4 + ch * 2 + 1] = l1;
+            E.derr[ch * 2 + 0] = a.use_derr ? e[1] : 0;
+            E.derr[ch * 2 + 1] = a.use_derr ? (int8_t)(e[2] - l1) : 0;
         }
     }
+    __syncthreads();
+    store_wt(a.mbs + (size_t)img * nmb + mb, &o, sizeof(XMB), l);
+    store_wt(a.edges + (size_t)img * nmb + mb, &E, sizeof(XEdge), l);
     IK_STAMP(5);
 }
 
-// One wave per image: fold the epoch's token statistics in raster order, then refresh
-// the probabilities and the level costs the next epoch's decisions use.
-__global__ __launch_bounds__(64) void k_vp8x_stats(XArgs a, int k0, int k1) {
-    const int img = blockIdx.x, l = threadIdx.x;
+// One image's statistics fold after epoch [k0, k1): the epoch's token statistics in
+// raster order, then the probabilities and level costs the next epoch's decisions use
+// (and, after the last epoch, the file's probabilities), stored write-through.
+__device__ __forceinline__ void fold_body(const XArgs& a, int img, int k0, int k1, FoldLds& F, int l) {
     const int nmb = a.mb_w * a.mb_h;
     const XMB* mbs = a.mbs + (size_t)img * nmb;
-    const uint32_t* nzs = a.nz + (size_t)img * nmb;
-    uint32_t* stats = a.stats + (size_t)img * 1056;
-    uint8_t* pr = a.pr + (size_t)img * 1056;
-    uint16_t* lc = a.lc + (size_t)img * kCostRows * kLevelTab;
+    const XEdge* edges = a.edges + (size_t)img * nmb;
+    const uint32_t* stats = a.stats + (size_t)img * 1056;
     // the counters in LDS.  libwebp halves a counter pair when its total reaches 65534,
     // which makes the fold order-dependent; an epoch adds at most 25 blocks x 16
     // records per slot per MB, so when every total is below 65534 minus that bound no
     // counter can reach the halving point and the MBs fold in parallel (LDS atomics);
     // otherwise lane 0 walks them in raster order, staged in LDS.
-    __shared__ uint32_t s_st[1056];
-    __shared__ __attribute__((aligned(16))) XMB s_mb;
-    __shared__ int s_serial;
-    static_assert(sizeof(XMB) % 4 == 0, "XMB words");
-    if (l == 0) s_serial = 0;
+    if (l == 0) F.serial = 0;
     __syncthreads();
     const uint32_t bound = (uint32_t)(k1 - k0) * 25u * 16u;
     for (int i = l; i < 1056; i += 64) {
-        s_st[i] = stats[i];
-        if ((s_st[i] >> 16) + bound >= 0xfffeu) s_serial = 1;
+        F.st[i] = stats[i];
+        if ((F.st[i] >> 16) + bound >= 0xfffeu) F.serial = 1;
     }
     __syncthreads();
     auto ctx_of = [&](int k, int* t, int* lf) {
         const int mx = k % a.mb_w, my = k / a.mb_w;
-        const uint32_t tnz = my ? nzs[k - a.mb_w] : 0u, lnz = mx ? nzs[k - 1] : 0u;
+        const uint32_t tnz = my ? edges[k - a.mb_w].nz : 0u, lnz = mx ? edges[k - 1].nz : 0u;
         const int tb[9] = {12, 13, 14, 15, 18, 19, 22, 23, 24}, lb[8] = {3, 7, 11, 15, 17, 19, 21, 23};
         for (int i = 0; i < 9; ++i) t[i] = (int)((tnz >> tb[i]) & 1u);
         for (int i = 0; i < 8; ++i) lf[i] = (int)((lnz >> lb[i]) & 1u);
         lf[8] = (int)((lnz >> 25) & 1u);
     };
-    if (!s_serial) {
-        uint32_t* st = s_st;
+    if (!F.serial) {
+        uint32_t* st = F.st;
         for (int k = k0 + l; k < k1; k += 64) {
             int t[9], lf[9];
             ctx_of(k, t, lf);
@@ -788,34 +919,210 @@ __global__ __launch_bounds__(64) void k_vp8x_stats(XArgs a, int k0, int k1) {
         __syncthreads();
     } else {
         for (int k = k0; k < k1; ++k) {
-            const uint32_t* src = (const uint32_t*)(mbs + k);
-            for (int i = l; i < (int)(sizeof(XMB) / 4); i += 64) ((uint32_t*)&s_mb)[i] = src[i];
+            const uint4* src = reinterpret_cast<const uint4*>(mbs + k);
+            for (int i = l; i < (int)(sizeof(XMB) / 16); i += 64) reinterpret_cast<uint4*>(&F.mb)[i] = src[i];
             __syncthreads();
             if (l == 0) {
                 int t[9], lf[9];
                 ctx_of(k, t, lf);
-                record_mb([&](uint32_t slot, int bit) { return record_stats(bit, s_st + slot); }, s_mb, t, lf,
+                record_mb([&](uint32_t slot, int bit) { return record_stats(bit, F.st + slot); }, F.mb, t, lf,
                           [](int, uint32_t) {});
             }
             __syncthreads();
         }
     }
-    for (int i = l; i < 1056; i += 64) {
-        stats[i] = s_st[i];
-        pr[i] = (uint8_t)finalize_proba(s_st[i], i);
-    }
+    for (int i = l; i < 1056; i += 64) F.pr[i] = (uint8_t)finalize_proba(F.st[i], i);
     __syncthreads();
-    for (int r = l; r < kCostRows; r += 64) level_cost_row(pr + r * 11, r % 3, lc + r * kLevelTab);
+    for (int r = l; r < kCostRows; r += 64) level_cost_row(F.pr + r * 11, r % 3, F.lc + r * kLevelTab);
+    __syncthreads();
+    for (int c = 0; c < 1056 * 4 / 16; c += 64)
+        store_wt(a.stats + (size_t)img * 1056 + 4 * c, F.st + 4 * c, min(1056 * 4 / 16 - c, 64) * 16, l);
+    store_wt(a.pr + (size_t)img * 1056, F.pr, 1056, l);  // 66 words: lanes 0..63 ...
+    store_wt(a.pr + (size_t)img * 1056 + 1024, F.pr + 1024, 32, l);  // ... and the last two
+    constexpr int kLcWords = kCostRows * kLevelTab * 2 / 16;
+    for (int c = 0; c < kLcWords; c += 64)
+        store_wt(a.lc + (size_t)img * kCostRows * kLevelTab + 8 * c, F.lc + 8 * c, min(kLcWords - c, 64) * 16, l);
 }
 
-hipError_t launch_vp8x_mb(const XArgs& a, const int* list, int count, int n, hipStream_t s) {
-    if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_vp8x_mb, dim3(count, n), dim3(64), 0, s, a, list);
+// lane 0: wait until *f >= want; false on a timeout (which sets the error word) or
+// when another wait has failed
+__device__ bool poll_ge(const uint32_t* f, uint32_t want, uint32_t* err, uint64_t t_end) {
+    for (;;) {
+        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) return true;
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+        if (__builtin_amdgcn_s_memrealtime() > t_end) {
+            __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+// The whole call's decisions and statistics folds, one launch (see the file header).
+__global__ __launch_bounds__(64) void k_vp8x_run(XArgs a, XRun r) {
+    __shared__ XLds S;
+    __shared__ uint64_t s_task;
+    __shared__ int s_ok;
+    const int l = threadIdx.x;
+    const int nmb = a.mb_w * a.mb_h;
+    uint32_t* err = r.sync + 1;
+    for (;;) {
+        if (l == 0) {
+            uint64_t task = ~0ull;
+            bool ok = true;
+            const uint32_t t = __hip_atomic_fetch_add(r.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t < r.ntasks) {
+                task = r.tasks[t];
+                const int img = (int)((task >> 32) & 0xffffu), e = (int)((task >> 48) & 0xffu);
+                const int mb = (int)(uint32_t)task;
+                // 4 s per wait (s_memrealtime counts at 100 MHz); a call takes tens of ms
+                const uint64_t t_end = __builtin_amdgcn_s_memrealtime() + 400000000ull;
+                if (task >> 63) {  // the fold of epoch e: its MBs decided, the previous fold's statistics in place
+                    ok = poll_ge(r.cnt + (size_t)img * r.nep + e, (uint32_t)(r.bounds[e + 1] - r.bounds[e]), err, t_end);
+                    if (ok && e > 0) ok = poll_ge(r.ready + (size_t)img * r.nep + e, 1u, err, t_end);
+                } else {  // an MB: its epoch's level costs, its left and top-right (or top) neighbours
+                    const int mx = mb % a.mb_w, my = mb / a.mb_w;
+                    const uint32_t* done = r.done + (size_t)img * nmb;
+                    if (e > 0) ok = poll_ge(r.ready + (size_t)img * r.nep + e, 1u, err, t_end);
+                    if (ok && mx > 0) ok = poll_ge(done + mb - 1, 1u, err, t_end);
+                    if (ok && my > 0) ok = poll_ge(done + mb - a.mb_w + (mx < a.mb_w - 1 ? 1 : 0), 1u, err, t_end);
+                }
+            }
+            s_task = task;
+            s_ok = ok;
+        }
+        __syncthreads();
+        const uint64_t task = uniform_u64(s_task);
+        const int ok = __builtin_amdgcn_readfirstlane(s_ok);
+        if (task == ~0ull || !ok) return;
+        // the hand-off's acquire: this CU's L1 holds nothing older than the flags seen
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const int img = (int)((task >> 32) & 0xffffu), e = (int)((task >> 48) & 0xffu);
+        // the lane index made opaque per task: otherwise the compiler hoists every
+        // lane-derived address of the MB body out of the task loop (255 VGPRs, not 98)
+        int lt = threadIdx.x;
+        asm volatile("" : "+v"(lt));
+        if (task >> 63) fold_body(a, img, r.bounds[e], r.bounds[e + 1], S.f, lt);
+        else mb_body(a, img, (int)(uint32_t)task, S.m, lt);
+        // the payload's write-through stores have completed before the flag
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (l == 0) {
+            if (task >> 63) {
+                if (e + 1 < (int)r.nep)
+                    __hip_atomic_store(r.ready + (size_t)img * r.nep + e + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                __hip_atomic_store(r.done + (size_t)img * nmb + (uint32_t)task, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(r.cnt + (size_t)img * r.nep + e, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// The segment set-up (libwebp VP8SetSegmentParams + SimplifySegments + the segment
+// map's tree probabilities; restated from the host's vp8_segment_setup) and the
+// initial coding state of every image: one wave per image.  qtab[s_alpha + 127] is
+// the segment quantiser for a segment alpha at this quality (libwebp's pow(), computed
+// on the host with the same libm).
+__global__ __launch_bounds__(64) void k_vp8x_setup(XArgs a, const vp8::SegRecord* recs, const uint8_t* kseg,
+                                                   const int* qtab, ik_vp8_segment_header* hdrs) {
+    constexpr int nb = 4, sns = 50, filter_strength = 60;
+    const int img = blockIdx.x, l = threadIdx.x;
+    const int nmb = a.mb_w * a.mb_h;
+    __shared__ int s_map[nb], s_cnt[nb], s_nfinal, s_reset;
+    __shared__ ik_vp8_segment_header s_hd;
+    auto clip = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
+    const vp8::SegRecord& r = recs[img];
+    if (l == 0) {
+        int mn = r.centers[0], mx = r.centers[0];
+        for (int k = 0; k < nb; ++k) {
+            mn = r.centers[k] < mn ? r.centers[k] : mn;
+            mx = r.centers[k] > mx ? r.centers[k] : mx;
+        }
+        if (mx == mn) mx = mn + 1;
+        int quant[nb], fstr[nb];
+        for (int k = 0; k < nb; ++k) {
+            const int s_alpha = clip(255 * (r.centers[k] - r.mid) / (mx - mn), -127, 127);
+            const int s_beta = clip(255 * (r.centers[k] - mn) / (mx - mn), 0, 255);
+            quant[k] = qtab[s_alpha + 127];
+            const int qstep = vp8::kAcTable[clip(quant[k], 0, 127)] >> 2;
+            const int base = qstep < 63 ? qstep : 63;
+            const int f = base * (5 * filter_strength) / (256 + s_beta);
+            fstr[k] = f < 2 ? 0 : (f > 63 ? 63 : f);  // FSTRENGTH_CUTOFF 2
+        }
+        const int total = r.nmb > 0 ? r.nmb : 1;
+        const int uv_alpha = (int)(r.uv_alpha_sum / (unsigned long long)total);
+        // MID_ALPHA 64, MIN_ALPHA 30, MAX_ALPHA 100; MIN/MAX_DQ_UV -4 / 6
+        int dq_uv_ac = (uv_alpha - 64) * (6 - (-4)) / (100 - 30);
+        dq_uv_ac = clip(dq_uv_ac * sns / 100, -4, 6);
+        s_hd.base_quant = quant[0];
+        int nfinal = 1;
+        s_map[0] = 0;
+        for (int s1 = 1; s1 < nb; ++s1) {
+            int s2 = 0;
+            bool found = false;
+            for (; s2 < nfinal; ++s2)
+                if (quant[s1] == quant[s2] && fstr[s1] == fstr[s2]) { found = true; break; }
+            s_map[s1] = s2;
+            if (!found) {
+                if (nfinal != s1) { quant[nfinal] = quant[s1]; fstr[nfinal] = fstr[s1]; }
+                ++nfinal;
+            }
+        }
+        for (int k = nfinal; k < nb; ++k) { quant[k] = quant[nfinal - 1]; fstr[k] = fstr[nfinal - 1]; }
+        for (int k = 0; k < nb; ++k) { s_hd.quant[k] = quant[k]; s_hd.fstrength[k] = fstr[k]; s_cnt[k] = 0; }
+        s_hd.dq_uv_dc = clip(-4 * sns / 100, -15, 15);
+        s_hd.dq_uv_ac = dq_uv_ac;
+        s_hd.alpha = (int)(r.alpha_sum / (unsigned long long)total);
+        s_hd.uv_alpha = uv_alpha;
+        s_nfinal = nfinal;
+    }
+    __syncthreads();
+    const int nfinal = s_nfinal;
+    uint8_t* seg = a.seg + (size_t)img * nmb;
+    const uint8_t* ks = kseg + (size_t)img * nmb;
+    for (int i = l; i < nmb; i += 64) {
+        const int v = nfinal < nb ? s_map[ks[i]] : ks[i];
+        seg[i] = (uint8_t)v;
+        atomicAdd(&s_cnt[v], 1);
+    }
+    __syncthreads();
+    if (l == 0) {
+        auto proba = [](int x, int y) { const int t = x + y; return t == 0 ? 255 : (255 * x + t / 2) / t; };
+        s_hd.probs[0] = proba(s_cnt[0] + s_cnt[1], s_cnt[2] + s_cnt[3]);
+        s_hd.probs[1] = proba(s_cnt[0], s_cnt[1]);
+        s_hd.probs[2] = proba(s_cnt[2], s_cnt[3]);
+        s_hd.num_segments = nfinal;
+        s_hd.update_map = nfinal > 1 && (s_hd.probs[0] != 255 || s_hd.probs[1] != 255 || s_hd.probs[2] != 255);
+        s_reset = nfinal > 1 && !s_hd.update_map;  // ResetSegments
+        hdrs[img] = s_hd;
+    }
+    __syncthreads();
+    if (s_reset)
+        for (int i = l; i < nmb; i += 64) seg[i] = 0;
+    if (l < nb) a.segs[(size_t)img * nb + l] = setup_segment(s_hd.quant[l], s_hd.dq_uv_dc, s_hd.dq_uv_ac, sns);
+    // the initial coding state: default probabilities, their level costs, no statistics
+    for (int i = l; i < 1056; i += 64) {
+        a.pr[(size_t)img * 1056 + i] = kCoeffProbs0[i];
+        a.stats[(size_t)img * 1056 + i] = 0;
+    }
+    for (int rr = l; rr < kCostRows; rr += 64)
+        level_cost_row(kCoeffProbs0 + rr * 11, rr % 3, a.lc + ((size_t)img * kCostRows + rr) * kLevelTab);
+    if (l < nb) a.max_edge[img * nb + l] = 0;
+}
+
+hipError_t launch_vp8x_setup(const XArgs& a, const vp8::SegRecord* rec, const uint8_t* kseg, const int* qtab,
+                             ik_vp8_segment_header* hdr, int n, hipStream_t s) {
+    hipLaunchKernelGGL(k_vp8x_setup, dim3(n), dim3(64), 0, s, a, rec, kseg, qtab, hdr);
     return hipGetLastError();
 }
 
-hipError_t launch_vp8x_stats(const XArgs& a, int k0, int k1, int n, hipStream_t s) {
-    hipLaunchKernelGGL(k_vp8x_stats, dim3(n), dim3(64), 0, s, a, k0, k1);
+hipError_t launch_vp8x_run(const XArgs& a, const XRun& r, int grid, hipStream_t s) {
+    if (grid <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_vp8x_run, dim3(grid), dim3(64), 0, s, a, r);
     return hipGetLastError();
 }
 

@@ -10,6 +10,8 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -19,8 +21,6 @@
 #include "ik_vp8x_gpu.h"
 
 namespace ik {
-
-void vp8_segment_setup(const vp8::SegRecord& r, float quality, uint8_t* seg, ik_vp8_segment_header* hd);
 
 namespace {
 
@@ -219,127 +219,125 @@ void write_file(int w, int h, const XMB* mbs, const uint8_t* probas, const ik_vp
     std::memcpy(o + 30 + b0.buf.size(), b1.buf.data(), b1.buf.size());
 }
 
+// The call's schedule, cached per thread for its geometry: epochs at libwebp's
+// probability refreshes; tickets in (epoch, diagonal, image) order, each epoch's folds
+// after its MBs.  Diagonals are found by one counting pass per epoch.
+struct XSchedule {
+    int w = 0, h = 0, n = 0;
+    std::vector<int> bounds;
+    std::vector<uint64_t> tasks;
+    int grid = 0;
+};
+
+const XSchedule& exact_schedule(int w, int h, int n) {
+    static thread_local XSchedule sc;
+    if (sc.w == w && sc.h == h && sc.n == n) return sc;
+    const int mb_w = (w + 15) / 16, mb_h = (h + 15) / 16, nmb = mb_w * mb_h;
+    const int M = (nmb >> 3) < 96 ? 96 : (nmb >> 3);
+    sc.bounds.assign(1, 0);
+    for (int k = M; k < nmb; k += M + 1) sc.bounds.push_back(k);
+    sc.bounds.push_back(nmb);
+    sc.tasks.clear();
+    sc.tasks.reserve((size_t)n * (nmb + sc.bounds.size()));
+    int widest = 1;
+    std::vector<int> first, list;
+    for (size_t e = 0; e + 1 < sc.bounds.size(); ++e) {
+        const int k0 = sc.bounds[e], k1 = sc.bounds[e + 1];
+        // (an epoch that starts mid-row holds MBs of smaller diagonals in its next row)
+        int d0 = 1 << 30, d1 = -1;
+        for (int k = k0; k < k1; ++k) {
+            d0 = std::min(d0, k % mb_w + 2 * (k / mb_w));
+            d1 = std::max(d1, k % mb_w + 2 * (k / mb_w));
+        }
+        first.assign((size_t)(d1 - d0 + 2), 0);  // counting sort of the epoch's MBs by diagonal
+        for (int k = k0; k < k1; ++k) ++first[(size_t)(k % mb_w + 2 * (k / mb_w) - d0 + 1)];
+        for (size_t d = 1; d < first.size(); ++d) first[d] += first[d - 1];
+        list.assign((size_t)(k1 - k0), 0);
+        std::vector<int> at(first.begin(), first.end() - 1);
+        for (int k = k0; k < k1; ++k) list[(size_t)at[(size_t)(k % mb_w + 2 * (k / mb_w) - d0)]++] = k;
+        const uint64_t ep = (uint64_t)e << 48;
+        for (int d = 0; d <= d1 - d0; ++d) {
+            const int a = first[(size_t)d], b = first[(size_t)d + 1];
+            widest = std::max(widest, (b - a) * n);
+            for (int i = 0; i < n; ++i)
+                for (int j = a; j < b; ++j) sc.tasks.push_back(ep | ((uint64_t)i << 32) | (uint32_t)list[(size_t)j]);
+        }
+        for (int i = 0; i < n; ++i) sc.tasks.push_back((1ull << 63) | ep | ((uint64_t)i << 32));
+    }
+    // resident workgroups: twice the widest diagonal, so the next diagonal's MBs are
+    // waiting on their flags when the current one's finish
+    sc.grid = (int)std::min<size_t>(std::min(2 * widest, 2048), sc.tasks.size());
+    sc.w = w;
+    sc.h = h;
+    sc.n = n;
+    return sc;
+}
+
+// libwebp VP8SetSegmentParams' quantiser for a segment alpha (-127..127) at quality q:
+// the pow() is the host's (the same libm call libwebp makes)
+void segment_quant_table(float quality, int* qtab) {
+    const double amp = 0.9 * 50 / 100. / 128.;  // SNS_TO_DQ, sns 50
+    const double Q = quality / 100.;
+    const double linear_c = (Q < 0.75) ? Q * (2. / 3.) : 2. * Q - 1.;
+    const double c_base = pow(linear_c, 1 / 3.);
+    for (int s = -127; s <= 127; ++s) {
+        const int v = (int)(127. * (1. - pow(c_base, 1. - amp * s)));
+        qtab[s + 127] = v < 0 ? 0 : (v > 127 ? 127 : v);
+    }
+}
+
 }  // namespace
 
 // n images of w x h YUV420 planes on the device (yuv_stride bytes apart) -> the WebP
-// files libwebp's WebPEncodeRGB writes at this quality.  Runs on the calling thread's
-// stream and waits.
+// files libwebp's WebPEncodeRGB writes at this quality.  Device work on the thread's
+// coder stream (ordered after its main stream, which produced the planes): segment
+// analysis, set-up, ONE persistent launch for every decision and statistics fold,
+// the records back; then the files on the host.
 int webp_encode_exact(const uint8_t* d_yuv, size_t yuv_stride, int n, int w, int h, int quality,
                       std::vector<std::vector<uint8_t>>& outs) {
     if (n < 1 || n > 65535 || w < 1 || h < 1 || w > 16383 || h > 16383)
         return fail(IK_ERR_INVALID, "bad WebP shape %dx%d x %d", w, h, n);
     hipStream_t ts = thread_stream();
     if (!ts) return fail(IK_ERR_DEVICE, "cannot create HIP stream");
-    // the coder's ~300 small launches per batch go to a stream of their own at the
-    // highest priority: a hardware queue of their own, so they run beside another
-    // batch's decode kernels instead of queueing behind them; ordered after the
-    // caller's stream (which produced the planes) by an event
-    struct XStream {
-        hipStream_t s = nullptr;
-        hipEvent_t ev = nullptr;
-        int dev = -1;
-    };
-    static thread_local XStream xs;
-    if (xs.dev != current_device()) {
-        int least = 0, greatest = 0;
-        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
-        if (hipStreamCreateWithPriority(&xs.s, hipStreamNonBlocking, greatest) != hipSuccess) xs.s = ts;
-        if (hipEventCreateWithFlags(&xs.ev, hipEventDisableTiming) != hipSuccess) xs.ev = nullptr;
-        xs.dev = current_device();
-    }
-    hipStream_t s = xs.s;
-    if (s != ts) {
-        if (!xs.ev) {
-            s = ts;
-        } else {
-            IK_HIP(hipEventRecord(xs.ev, ts));
-            IK_HIP(hipStreamWaitEvent(s, xs.ev, 0));
-        }
+    // the coder's stream: the highest priority, so its launch is dispatched ahead of
+    // another batch's decode kernels; ordered after the caller's stream by an event
+    hipStream_t s = ts;
+    hipEvent_t ev = nullptr;
+    if (thread_prio_stream(&s, &ev) && s != ts) {
+        IK_HIP(hipEventRecord(ev, ts));
+        IK_HIP(hipStreamWaitEvent(s, ev, 0));
+    } else {
+        s = ts;
     }
     const int mb_w = (w + 15) / 16, mb_h = (h + 15) / 16, nmb = mb_w * mb_h;
-    const size_t rec_stride = (size_t)mb_w * 16 * mb_h * 16 * 3 / 2;
     const float q = (float)quality;
-    // device buffers (one allocation, 256-byte aligned parts)
+    const XSchedule& sc = exact_schedule(w, h, n);
+    const int nep = (int)sc.bounds.size() - 1;
+    // device buffers (one allocation, 256-byte aligned parts); the hand-off words first,
+    // zeroed by one memset per call
     size_t off = 0;
     auto part = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+    const size_t sync_words = 4 + (size_t)n * nmb + 2ull * n * nep;
+    const size_t o_sync = part(4 * sync_words);
+    const size_t sync_bytes = off;
     const size_t o_alpha = part((size_t)nmb * n), o_uva = part((size_t)nmb * n * 2), o_kseg = part((size_t)nmb * n);
-    const size_t o_rec = part(sizeof(vp8::SegRecord) * n);
-    const size_t o_recon = part(rec_stride * n), o_mbs = part(sizeof(XMB) * nmb * n), o_nz = part(4ull * nmb * n);
-    const size_t o_derr = part(8ull * nmb * n), o_seg = part((size_t)nmb * n), o_segs = part(sizeof(XSeg) * 4 * n);
+    const size_t o_rec = part(sizeof(vp8::SegRecord) * n), o_hdr = part(sizeof(ik_vp8_segment_header) * n);
+    const size_t o_mbs = part(sizeof(XMB) * nmb * n), o_edges = part(sizeof(XEdge) * nmb * n);
+    const size_t o_seg = part((size_t)nmb * n), o_segs = part(sizeof(XSeg) * 4 * n);
     const size_t o_lc = part(2ull * kCostRows * kLevelTab * n), o_pr = part(1056ull * n), o_st = part(4ull * 1056 * n);
     const size_t o_me = part(16ull * n);
-    // the wavefront schedule: epochs at libwebp's probability refreshes, diagonals inside
-    const int M = (nmb >> 3) < 96 ? 96 : (nmb >> 3);
-    std::vector<int> bounds{0};
-    for (int k = M; k < nmb; k += M + 1) bounds.push_back(k);
-    bounds.push_back(nmb);
-    std::vector<int> list;
-    struct Step { int off, count, epoch_end; };
-    std::vector<Step> steps;
-    for (size_t e = 0; e + 1 < bounds.size(); ++e) {
-        const int k0 = bounds[e], k1 = bounds[e + 1];
-        int dmin = 1 << 30, dmax = -1;
-        for (int k = k0; k < k1; ++k) {
-            const int d = k % mb_w + 2 * (k / mb_w);
-            dmin = d < dmin ? d : dmin;
-            dmax = d > dmax ? d : dmax;
-        }
-        for (int d = dmin; d <= dmax; ++d) {
-            const int o = (int)list.size();
-            for (int k = k0; k < k1; ++k)
-                if (k % mb_w + 2 * (k / mb_w) == d) list.push_back(k);
-            if ((int)list.size() > o) steps.push_back({o, (int)list.size() - o, -1});
-        }
-        steps.push_back({0, 0, k1});  // the epoch's statistics
-    }
-    const size_t o_list = part(4ull * list.size());
-    // a per-thread work area, grown as needed and kept (a hipFree would wait for the
-    // whole device, the next batch's decode kernels included)
-    struct Area {
-        uint8_t* p = nullptr;
-        size_t cap = 0;
-        int dev = -1;
-    };
-    static thread_local Area area;
-    const int dev = current_device();
-    if (area.cap < off || area.dev != dev) {
-        if (area.p) (void)hipFree(area.p);
-        area.p = nullptr;
-        area.cap = 0;
-        IK_HIP(hipMalloc((void**)&area.p, off));
-        area.cap = off;
-        area.dev = dev;
-    }
-    uint8_t* d = area.p;
-    // 1. segment analysis (exact, ik_vp8_analysis.hip)
-    std::vector<vp8::SegRecord> recs(n);
-    std::vector<uint8_t> seg((size_t)nmb * n);
-    IK_HIP(vp8::launch_vp8_analysis(d_yuv, yuv_stride, n, w, h, d + o_alpha, (uint16_t*)(d + o_uva), d + o_kseg,
-                                    (vp8::SegRecord*)(d + o_rec), s));
-    IK_HIP(hipMemcpyAsync(seg.data(), d + o_kseg, seg.size(), hipMemcpyDeviceToHost, s));
-    IK_HIP(hipMemcpyAsync(recs.data(), d + o_rec, sizeof(vp8::SegRecord) * n, hipMemcpyDeviceToHost, s));
-    IK_HIP(hipStreamSynchronize(s));
-    std::vector<ik_vp8_segment_header> hdr(n);
-    std::vector<XSeg> segs((size_t)4 * n);
-    for (int i = 0; i < n; ++i) {
-        vp8_segment_setup(recs[i], q, seg.data() + (size_t)nmb * i, &hdr[i]);
-        for (int sg = 0; sg < 4; ++sg) segs[(size_t)i * 4 + sg] = setup_segment(hdr[i].quant[sg], hdr[i].dq_uv_dc, hdr[i].dq_uv_ac, 50);
-    }
-    // 2. initial state: default probabilities and their level costs, zero statistics
-    std::vector<uint8_t> pr0((size_t)1056 * n);
-    std::vector<uint16_t> lc0((size_t)kCostRows * kLevelTab * n);
-    for (int i = 0; i < n; ++i) {
-        std::memcpy(&pr0[(size_t)1056 * i], kCoeffProbs0, 1056);
-        for (int r = 0; r < kCostRows; ++r) level_cost_row(kCoeffProbs0 + r * 11, r % 3, &lc0[((size_t)i * kCostRows + r) * kLevelTab]);
-    }
-    IK_HIP(hipMemcpyAsync(d + o_seg, seg.data(), seg.size(), hipMemcpyHostToDevice, s));
-    IK_HIP(hipMemcpyAsync(d + o_segs, segs.data(), sizeof(XSeg) * segs.size(), hipMemcpyHostToDevice, s));
-    IK_HIP(hipMemcpyAsync(d + o_pr, pr0.data(), pr0.size(), hipMemcpyHostToDevice, s));
-    IK_HIP(hipMemcpyAsync(d + o_lc, lc0.data(), 2 * lc0.size(), hipMemcpyHostToDevice, s));
-    IK_HIP(hipMemcpyAsync(d + o_list, list.data(), 4 * list.size(), hipMemcpyHostToDevice, s));
-    IK_HIP(hipMemsetAsync(d + o_st, 0, 4ull * 1056 * n, s));
-    IK_HIP(hipMemsetAsync(d + o_me, 0, 16ull * n, s));
-    // 3. the decisions
+    const size_t o_qtab = part(4 * 255), o_bounds = part(4 * sc.bounds.size()), o_tasks = part(8 * sc.tasks.size());
+    uint8_t* d = scratch_slot(kScratchExact, off);
+    if (!d) return fail(IK_ERR_DEVICE, "cannot allocate the exact coder's work area (%zu bytes)", off);
+    // the constants: quantiser table, epoch bounds, tickets (through pinned staging)
+    const size_t const_bytes = off - o_qtab;
+    uint8_t* hc = pinned_slot(kPinnedExactIn, const_bytes);
+    if (!hc) return IK_ERR_NOMEM;
+    segment_quant_table(q, reinterpret_cast<int*>(hc));
+    std::memcpy(hc + (o_bounds - o_qtab), sc.bounds.data(), 4 * sc.bounds.size());
+    std::memcpy(hc + (o_tasks - o_qtab), sc.tasks.data(), 8 * sc.tasks.size());
+    IK_HIP(hipMemcpyAsync(d + o_qtab, hc, const_bytes, hipMemcpyHostToDevice, s));
+    IK_HIP(hipMemsetAsync(d + o_sync, 0, sync_bytes, s));
     XArgs a{};
     a.yuv = d_yuv;
     a.yuv_stride = yuv_stride;
@@ -347,54 +345,55 @@ int webp_encode_exact(const uint8_t* d_yuv, size_t yuv_stride, int n, int w, int
     a.h = h;
     a.mb_w = mb_w;
     a.mb_h = mb_h;
-    a.rec = d + o_recon;
-    a.rec_stride = rec_stride;
     a.mbs = (XMB*)(d + o_mbs);
-    a.nz = (uint32_t*)(d + o_nz);
-    a.derr = (int8_t*)(d + o_derr);
+    a.edges = (XEdge*)(d + o_edges);
     a.seg = d + o_seg;
-    a.segs = (const XSeg*)(d + o_segs);
+    a.segs = (XSeg*)(d + o_segs);
     a.lc = (uint16_t*)(d + o_lc);
     a.pr = d + o_pr;
     a.stats = (uint32_t*)(d + o_st);
     a.max_edge = (int*)(d + o_me);
     a.use_derr = q <= 98.f;  // ERROR_DIFFUSION_QUALITY
-    const int* dlist = (const int*)(d + o_list);
-    int k0 = 0;
-    for (const Step& st : steps) {
-        if (st.epoch_end >= 0) {
-            IK_HIP(launch_vp8x_stats(a, k0, st.epoch_end, n, s));
-            k0 = st.epoch_end;
-        } else {
-            IK_HIP(launch_vp8x_mb(a, dlist + st.off, st.count, n, s));
-        }
-    }
-    // 4. the records back (into a page-locked area kept per thread: ~820 B per MB); the
-    // files on the host
-    const size_t rec_bytes = sizeof(XMB) * (size_t)nmb * n, tail = 1056ull * n + 16ull * n;
-    struct Pinned {
-        uint8_t* p = nullptr;
-        size_t cap = 0;
-    };
-    static thread_local Pinned hpin;
-    if (hpin.cap < rec_bytes + tail) {
-        if (hpin.p) (void)hipHostFree(hpin.p);
-        hpin.p = nullptr;
-        hpin.cap = 0;
-        IK_HIP(hipHostMalloc((void**)&hpin.p, rec_bytes + tail, hipHostMallocDefault));
-        hpin.cap = rec_bytes + tail;
-    }
-    const XMB* mbs = reinterpret_cast<const XMB*>(hpin.p);
-    const uint8_t* pr = hpin.p + rec_bytes;
-    const int* me = reinterpret_cast<const int*>(hpin.p + rec_bytes + 1056ull * n);
-    IK_HIP(hipMemcpyAsync(hpin.p, d + o_mbs, rec_bytes, hipMemcpyDeviceToHost, s));
-    IK_HIP(hipMemcpyAsync(hpin.p + rec_bytes, d + o_pr, 1056ull * n, hipMemcpyDeviceToHost, s));
-    IK_HIP(hipMemcpyAsync(hpin.p + rec_bytes + 1056ull * n, d + o_me, 16ull * n, hipMemcpyDeviceToHost, s));
+    XRun r{};
+    r.tasks = (const uint64_t*)(d + o_tasks);
+    r.ntasks = (uint32_t)sc.tasks.size();
+    r.nep = (uint32_t)nep;
+    r.bounds = (const int*)(d + o_bounds);
+    r.sync = (uint32_t*)(d + o_sync);
+    r.done = r.sync + 4;
+    r.cnt = r.done + (size_t)n * nmb;
+    r.ready = r.cnt + (size_t)n * nep;
+    // 1. segment analysis (ik_vp8_analysis.hip), 2. set-up, 3. every decision and fold
+    IK_HIP(vp8::launch_vp8_analysis(d_yuv, yuv_stride, n, w, h, d + o_alpha, (uint16_t*)(d + o_uva), d + o_kseg,
+                                    (vp8::SegRecord*)(d + o_rec), s));
+    IK_HIP(launch_vp8x_setup(a, (const vp8::SegRecord*)(d + o_rec), d + o_kseg, (const int*)(d + o_qtab),
+                             (ik_vp8_segment_header*)(d + o_hdr), n, s));
+    IK_HIP(launch_vp8x_run(a, r, sc.grid, s));
+    // 4. the records back (~830 B per MB), the final probabilities, the filter-edge
+    // maxima, the headers and the error word; the files on the host
+    const size_t rec_bytes = sizeof(XMB) * (size_t)nmb * n;
+    const size_t o_hpr = rec_bytes, o_hme = o_hpr + 1056ull * n, o_hhd = o_hme + 16ull * n;
+    const size_t o_herr = o_hhd + sizeof(ik_vp8_segment_header) * n, hbytes = o_herr + 16;
+    uint8_t* hp = pinned_slot(kPinnedExactOut, hbytes);
+    if (!hp) return IK_ERR_NOMEM;
+    IK_HIP(hipMemcpyAsync(hp, d + o_mbs, rec_bytes, hipMemcpyDeviceToHost, s));
+    IK_HIP(hipMemcpyAsync(hp + o_hpr, d + o_pr, 1056ull * n, hipMemcpyDeviceToHost, s));
+    IK_HIP(hipMemcpyAsync(hp + o_hme, d + o_me, 16ull * n, hipMemcpyDeviceToHost, s));
+    IK_HIP(hipMemcpyAsync(hp + o_hhd, d + o_hdr, sizeof(ik_vp8_segment_header) * n, hipMemcpyDeviceToHost, s));
+    IK_HIP(hipMemcpyAsync(hp + o_herr, d + o_sync, 8, hipMemcpyDeviceToHost, s));
     IK_HIP(hipStreamSynchronize(s));
+    uint32_t err_word = 0;
+    std::memcpy(&err_word, hp + o_herr + 4, 4);
+    if (err_word) return fail(IK_ERR_DEVICE, "exact WebP coder: a dependency wait timed out on the device");
+    const XMB* mbs = reinterpret_cast<const XMB*>(hp);
+    const uint8_t* pr = hp + o_hpr;
+    const int* me = reinterpret_cast<const int*>(hp + o_hme);
+    const ik_vp8_segment_header* hdr = reinterpret_cast<const ik_vp8_segment_header*>(hp + o_hhd);
     outs.resize(n);
     parallel_for(n, n < 16 ? n : 16, [&](int i) {
-        write_file(w, h, mbs + (size_t)nmb * i, pr + (size_t)1056 * i, hdr[i], me + (size_t)4 * i, &segs[(size_t)4 * i],
-                   outs[i]);
+        XSeg segs[4];
+        for (int sg = 0; sg < 4; ++sg) segs[sg] = setup_segment(hdr[i].quant[sg], hdr[i].dq_uv_dc, hdr[i].dq_uv_ac, 50);
+        write_file(w, h, mbs + (size_t)nmb * i, pr + (size_t)1056 * i, hdr[i], me + (size_t)4 * i, segs, outs[i]);
     });
     return IK_OK;
 }
@@ -414,7 +413,14 @@ extern "C" int ik_webp_encode_exact_device(const uint8_t* dev_yuv, size_t yuv_st
     if (int rc = webp_encode_exact(dev_yuv, yuv_stride, (int)n, (int)w, (int)h, q, files)) return rc;
     for (uint32_t i = 0; i < n; ++i) {
         outs[i] = (uint8_t*)malloc(files[i].size() ? files[i].size() : 1);
-        if (!outs[i]) return fail(IK_ERR_NOMEM, "out of host memory");
+        if (!outs[i]) {
+            for (uint32_t j = 0; j < i; ++j) {
+                free(outs[j]);
+                outs[j] = nullptr;
+                out_lens[j] = 0;
+            }
+            return fail(IK_ERR_NOMEM, "out of host memory");
+        }
         std::memcpy(outs[i], files[i].data(), files[i].size());
         out_lens[i] = files[i].size();
     }

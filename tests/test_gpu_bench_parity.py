@@ -48,8 +48,20 @@ def bench_frames():
     return [ikutil.synth(4096, 4096, 4, seed=sd, pattern="S") for sd in bench.shard_seeds(0, 4)]
 
 
-def test_bench_headline_batch_equals_oracle(ik, oracle, bench_frames):
+@pytest.mark.parametrize("encoder", ["libwebp", "exact"])
+def test_bench_headline_batch_equals_oracle(ik, oracle, bench_frames, encoder):
+    # both WebP coders: libwebp on the host, and the exact GPU coder (IK_WEBP_EXACT:
+    # ik_vp8x.hip's persistent launch per same-geometry group), each byte-identical
     B = 64
+    prev = ik.ik_get_webp_encoder()
+    assert ik.ik_set_webp_encoder({"libwebp": 0, "exact": 2}[encoder]) == 0
+    try:
+        _headline_batches(ik, oracle, bench_frames, B)
+    finally:
+        ik.ik_set_webp_encoder(prev)
+
+
+def _headline_batches(ik, oracle, bench_frames, B):
     pngs = bench.make_pngs(bench_frames)
     noise = ikutil.synth(4096, 4096, 4, seed=4, pattern="N")
     npng = bench.make_pngs([noise])[0]

@@ -64,6 +64,40 @@ def test_equals_webpencodergb(ik, oracle, wh, pat, q):
     assert got == want, f"{w}x{h} {pat} q{q}: differs at byte {first_diff(got, want)} ({len(got)} vs {len(want)})"
 
 
+# frames above 1,024 MBs: epochs of more than 96 MBs (M = mb_count / 8), many diagonals
+# per epoch, and statistics folds in raster order (an epoch over 163 MBs can reach
+# libwebp's 65,534 halving point, so k_vp8x_run folds it serially)
+@pytest.mark.parametrize("w,h,pat,q", [(799, 799, "S", 80), (1024, 1024, "S", 80), (1000, 600, "N", 80),
+                                       (1000, 600, "S", 95), (1920, 1080, "S", 80)])
+def test_large_frames(ik, oracle, w, h, pat, q):
+    img = ikutil.synth(w, h, 3, seed=w ^ h, pattern=pat)
+    got = encode_exact(ik, [img], q)[0]
+    want = oracle.webp_encode_rgb(img, float(q))
+    assert got == want, f"{w}x{h} {pat} q{q}: differs at byte {first_diff(got, want)} ({len(got)} vs {len(want)})"
+
+
+def test_counters_past_the_halving_point(ik, oracle):
+    # 1920x1080 noise at q95: 8,160 MBs of 25 coded blocks each -- a coefficient slot's
+    # record count passes 65,534 within the frame, so libwebp halves it mid-frame and
+    # the fold's raster order decides the probabilities
+    img = ikutil.synth(1920, 1080, 3, seed=7, pattern="N")
+    got = encode_exact(ik, [img], 95)[0]
+    want = oracle.webp_encode_rgb(img, 95.0)
+    assert got == want, f"differs at byte {first_diff(got, want)} ({len(got)} vs {len(want)})"
+
+
+def test_work_area_growth(ik, oracle):
+    # one thread's calls: small, large (the work area and pinned buffers grow), small
+    # again on the grown area, and a batch of two large frames
+    shapes = [(64, 48), (1280, 720), (96, 80)]
+    for k, (w, h) in enumerate(shapes):
+        img = ikutil.synth(w, h, 3, seed=11 + k, pattern="S")
+        assert encode_exact(ik, [img], 80)[0] == oracle.webp_encode_rgb(img, 80.0), f"{w}x{h}"
+    imgs = [ikutil.synth(1280, 720, 3, seed=s, pattern="SN"[s]) for s in range(2)]
+    for i, (got, img) in enumerate(zip(encode_exact(ik, imgs, 80), imgs)):
+        assert got == oracle.webp_encode_rgb(img, 80.0), f"batch image {i}"
+
+
 def test_batch(ik, oracle):
     imgs = [ikutil.synth(512, 512, 3, seed=s, pattern="SSNS"[s]) for s in range(4)]
     for i, (got, img) in enumerate(zip(encode_exact(ik, imgs, 80), imgs)):
