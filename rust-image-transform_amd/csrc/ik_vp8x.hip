@@ -45,6 +45,24 @@ namespace {
 
 constexpr int kTopLeftI4[16] = {17, 21, 25, 29, 13, 17, 21, 25, 9, 13, 17, 21, 5, 9, 13, 17};
 
+// libwebp's ten intra-4 predictors (pred4, ik_vp8x.h) as taps: per (mode, pixel y*4+x)
+// the samples e[i0], e[i1], e[i2] of e[] = L K J I X A B C D E F G H (bits 0-3, 4-7,
+// 8-11) and the op (bits 12-14): 0 avg3(i0, i1, i2) = (i0 + 2 i1 + i2 + 2) >> 2,
+// 1 avg2(i0, i1), 2 e[i0], 3 TM clip(e[i0] + e[i1] - e[i2]), 4 DC.  Made by
+// transcribing pred4's assignments (tools/gen_i4_taps.py); the byte tests hold it.
+constexpr uint16_t kI4Tap[10][16] = {
+    {0x4000, 0x4000, 0x4000, 0x4000, 0x4000, 0x4000, 0x4000, 0x4000, 0x4000, 0x4000, 0x4000, 0x4000, 0x4000, 0x4000, 0x4000, 0x4000},
+    {0x3453, 0x3463, 0x3473, 0x3483, 0x3452, 0x3462, 0x3472, 0x3482, 0x3451, 0x3461, 0x3471, 0x3481, 0x3450, 0x3460, 0x3470, 0x3480},
+    {0x0654, 0x0765, 0x0876, 0x0987, 0x0654, 0x0765, 0x0876, 0x0987, 0x0654, 0x0765, 0x0876, 0x0987, 0x0654, 0x0765, 0x0876, 0x0987},
+    {0x0234, 0x0234, 0x0234, 0x0234, 0x0123, 0x0123, 0x0123, 0x0123, 0x0012, 0x0012, 0x0012, 0x0012, 0x0001, 0x0001, 0x0001, 0x0001},
+    {0x0345, 0x0456, 0x0567, 0x0678, 0x0234, 0x0345, 0x0456, 0x0567, 0x0123, 0x0234, 0x0345, 0x0456, 0x0012, 0x0123, 0x0234, 0x0345},
+    {0x1054, 0x1065, 0x1076, 0x1087, 0x0543, 0x0654, 0x0765, 0x0876, 0x0432, 0x1054, 0x1065, 0x1076, 0x0321, 0x0543, 0x0654, 0x0765},
+    {0x0765, 0x0876, 0x0987, 0x0a98, 0x0876, 0x0987, 0x0a98, 0x0ba9, 0x0987, 0x0a98, 0x0ba9, 0x0cba, 0x0a98, 0x0ba9, 0x0cba, 0x0ccb},
+    {0x1065, 0x1076, 0x1087, 0x1098, 0x0765, 0x0876, 0x0987, 0x0a98, 0x1076, 0x1087, 0x1098, 0x0ba9, 0x0876, 0x0987, 0x0a98, 0x0cba},
+    {0x1043, 0x0543, 0x0654, 0x0765, 0x1032, 0x0432, 0x1043, 0x0543, 0x1021, 0x0321, 0x1032, 0x0432, 0x1010, 0x0210, 0x1021, 0x0321},
+    {0x1023, 0x0123, 0x1012, 0x0012, 0x1012, 0x0012, 0x1001, 0x0001, 0x1001, 0x0001, 0x2000, 0x2000, 0x2000, 0x2000, 0x2000, 0x2000},
+};
+
 // GetResidualCost with libwebp's fixed level costs and entropy costs staged in LDS
 // (the constant tables would be per-lane divergent global loads inside the serial
 // coefficient loop).  Every coefficient's context is known from its predecessor's
@@ -137,10 +155,14 @@ __device__ __forceinline__ void pred8_row(uint8_t* dst, int m, const uint8_t* le
     *reinterpret_cast<uint2*>(dst + y * BPS) = make_uint2(w0, w1);
 }
 
-__device__ __forceinline__ int64_t rdlane64(int64_t v, int lane) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), lane);
-    return (int64_t)(((uint64_t)hi << 32) | lo);
+
+// the other lanes of a quad (DPP quad_perm [1,0,3,2] and [2,3,0,1]): sums over a
+// mode's four lanes without LDS
+__device__ __forceinline__ int qx1(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ int qx2(int v) { return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false); }
+__device__ __forceinline__ int qsum(int v) {
+    v += qx1(v);
+    return v + qx2(v);
 }
 
 __device__ __forceinline__ int64_t rd_score(int64_t R, int64_t H, int64_t D, int64_t SD, int lambda) {
@@ -151,6 +173,10 @@ __device__ __forceinline__ int64_t rd_score(int64_t R, int64_t H, int64_t D, int
 
 // dev switch IK_VP8X_STAMPS: per-phase shader-clock sums over image 0's MBs
 // (tools/vp8x_timing.py --stamps reads them through ik_vp8x_stamps)
+#ifndef IK_VP8X_PRIO
+#define IK_VP8X_PRIO 2
+#endif
+
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // buffer intrinsics' cache-policy operand: sc1 (gfx940+ CPol::SC1) -- write-through stores
 constexpr int kCpolSc1 = 16;
@@ -172,13 +198,29 @@ __device__ __forceinline__ void store_wt(void* dst, const void* src, uint32_t nb
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, act ? 16 * l : 0x7ffffff0, 0, kCpolSc1);
 }
 
+// threads per task: an MB's intra-4 search runs on wave 0 while wave 1 runs intra-16
+// and chroma (the three are independent given the MB's context; libwebp's intra-4
+// early-out only ends a search whose result it then rejects, so the search runs to
+// the end and the decision compares the final sums)
+constexpr int kNT = 128;
+
+// a barrier for one wave's lanes: LDS operations of a wave complete in issue order;
+// this keeps the compiler from moving them across
+#define WSYNC()                                            \
+    do {                                                   \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); \
+        __builtin_amdgcn_wave_barrier();                   \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); \
+    } while (0)
+
 // the MB task's LDS (the fold's overlays it)
 struct MbLds {
-    alignas(16) uint16_t lc[kCostRows * kLevelTab];  // the image's level costs (13 KB), read at every coefficient
     alignas(16) uint8_t pr[1056];
+#ifndef IK_VP8X_TABLES_GLOBAL
     alignas(16) uint16_t fixed[2048];
     uint16_t ent[256];
     uint16_t fi4[1000];
+#endif
     uint8_t bands[17];
     alignas(16) XSeg Q;  // the segment's matrices and lambdas, read per lane in every quantisation
     alignas(16) uint8_t in[BPS * 16];  // Y 0..15, U 16..23, V 24..31
@@ -199,8 +241,9 @@ struct MbLds {
     alignas(16) uint8_t recuv[4][BPS * 8];
     alignas(16) int16_t lvuv[4][8][16];
     int8_t duv[4][2][3];
-    int b16, buv, i4ok;
+    int b16, buv, hb4;
     int64_t s16;  // the i16 best's score at lambda_mode (the intra-4 bar)
+    int64_t aS4;  // the intra-4 search's final score and header bits
     // per-lane work buffers (private arrays would live in scratch memory); the
     // neighbours' edge records overlay pred16 (prologue only), the outgoing records
     // tmp16 and pred4 (dead by the outputs)
@@ -260,12 +303,21 @@ __device__ __forceinline__ void mb_body(const XArgs& a, int img, int mb, MbLds& 
     const uint8_t* V = U + (size_t)uw * uh;
     const XEdge* edges = a.edges + (size_t)img * nmb;
     const int sg = a.seg[(size_t)img * nmb + mb];
-    auto& lc = S.lc;
+    // the image's level costs (13 KB), read at every coefficient of every candidate:
+    // from L1 / L2, not LDS -- as fast alone, and the LDS a resident coder task holds is
+    // what another batch's decode kernels beside it lose in occupancy
+    const uint16_t* lc = a.lc + (size_t)img * kCostRows * kLevelTab;
     auto& pr = S.pr;
+#ifdef IK_VP8X_TABLES_GLOBAL
+    const uint16_t* s_fixed = kLevelFixedCosts;
+    const uint16_t* s_ent = kEntropyCost;
+    const uint16_t* s_fi4 = kFixedCostsI4;
+#else
     auto& s_fixed = S.fixed;
     auto& s_ent = S.ent;
-    auto& s_bands = S.bands;
     auto& s_fi4 = S.fi4;
+#endif
+    auto& s_bands = S.bands;
     auto& s_in = S.in;
     auto& s_yl = S.yl;
     auto& s_yt = S.yt;
@@ -295,7 +347,6 @@ __device__ __forceinline__ void mb_body(const XArgs& a, int img, int mb, MbLds& 
     auto& s_duv = S.duv;
     auto& s_b16 = S.b16;
     auto& s_buv = S.buv;
-    auto& s_i4ok = S.i4ok;
     auto& s_s16 = S.s16;
     auto& s_pred16 = S.pred16;
     auto& s_tmp16 = S.tmp16;
@@ -308,14 +359,14 @@ __device__ __forceinline__ void mb_body(const XArgs& a, int img, int mb, MbLds& 
     auto& s_ft4 = S.ft4;
     auto& s_C4 = S.C4;
     auto& s_tt4 = S.tt4;
-    auto& s_cf4 = S.cf4;
+
     uint8_t (*s_nb)[sizeof(XEdge)] = reinterpret_cast<uint8_t (*)[sizeof(XEdge)]>(&S.pred16[0][0]);
     // staging: every lane issues all of its global reads first (one memory latency for
     // the whole prologue), then writes them to LDS: libwebp's fixed cost tables, the
     // image's probabilities and level costs, the segment's matrices, the source MB
     // (ImportBlock: clamped coordinates) and the neighbours' edge records (left, top,
     // top-right, top-left; 16 bytes per lane)
-    {
+    if (l < 64) {
         constexpr int kFi4 = (1000 + 63) / 64, kFix = 2048 / 64, kEnt = 256 / 64;
         constexpr int kPr = (1056 / 16 + 63) / 64;
         uint16_t rf4[kFi4], rfx[kFix], ren[kEnt];
@@ -329,62 +380,64 @@ __device__ __forceinline__ void mb_body(const XArgs& a, int img, int mb, MbLds& 
         uint4 rpr[kPr];
 #pragma unroll
         for (int j = 0; j < kPr; ++j) rpr[j] = gp[min(l + 64 * j, 1056 / 16 - 1)];
-        const int q = l >> 3;
+#ifndef IK_VP8X_TABLES_GLOBAL
+#pragma unroll
+        for (int j = 0; j < kFi4; ++j)
+            if (l + 64 * j < 1000) S.fi4[l + 64 * j] = rf4[j];
+#pragma unroll
+        for (int j = 0; j < kFix; ++j) S.fixed[l + 64 * j] = rfx[j];
+#pragma unroll
+        for (int j = 0; j < kEnt; ++j) S.ent[l + 64 * j] = ren[j];
+#else
+        (void)rf4;
+        (void)rfx;
+        (void)ren;
+#endif
+#pragma unroll
+        for (int j = 0; j < kPr; ++j)
+            if (l + 64 * j < 1056 / 16) ((uint4*)pr)[l + 64 * j] = rpr[j];
+        if (l < 17) s_bands[l] = kEncBands[l];
+    } else {
+        const int w = l - 64;
+        const int q = w >> 3;
         int nb = -1;
-        if (l < 32) {
+        if (w < 32) {
             if (q == 0 && mx) nb = mb - 1;
             else if (q == 1 && my) nb = mb - a.mb_w;
             else if (q == 2 && my && mx < a.mb_w - 1) nb = mb - a.mb_w + 1;
             else if (q == 3 && mx && my) nb = mb - a.mb_w - 1;
         }
-        const uint4 rnb = nb >= 0 ? reinterpret_cast<const uint4*>(edges + nb)[l & 7] : uint4{0, 0, 0, 0};
+        const uint4 rnb = nb >= 0 ? reinterpret_cast<const uint4*>(edges + nb)[w & 7] : uint4{0, 0, 0, 0};
         uint8_t rin[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int i = l + 64 * k;
+            const int i = w + 64 * k;
             const int y = i >> 4, x = i & 15;
             rin[k] = Y[(size_t)min(16 * my + y, a.h - 1) * a.w + min(16 * mx + x, a.w - 1)];
         }
         uint8_t ruv[2];
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-            const int i = l + 64 * k;
+            const int i = w + 64 * k;
             const int c = i >> 6, kk = i & 63, y = kk >> 3, x = kk & 7;
             const uint8_t* P = c ? V : U;
             ruv[k] = P[(size_t)min(8 * my + y, uh - 1) * uw + min(8 * mx + x, uw - 1)];
         }
-#pragma unroll
-        for (int j = 0; j < kFi4; ++j)
-            if (l + 64 * j < 1000) s_fi4[l + 64 * j] = rf4[j];
-#pragma unroll
-        for (int j = 0; j < kFix; ++j) s_fixed[l + 64 * j] = rfx[j];
-#pragma unroll
-        for (int j = 0; j < kEnt; ++j) s_ent[l + 64 * j] = ren[j];
-        {  // 13 x 16 B per lane (a register array this size would go to scratch)
-            const uint4* g = (const uint4*)(a.lc + (size_t)img * kCostRows * kLevelTab);
-            for (int i = l; i < kCostRows * kLevelTab / 8; i += 64) ((uint4*)lc)[i] = g[i];
-        }
-#pragma unroll
-        for (int j = 0; j < kPr; ++j)
-            if (l + 64 * j < 1056 / 16) ((uint4*)pr)[l + 64 * j] = rpr[j];
-        if (nb >= 0) reinterpret_cast<uint4*>(s_nb[q])[l & 7] = rnb;
+        static_assert(sizeof(XSeg) % 4 == 0, "XSeg copied as words");
+        const uint32_t* gq = reinterpret_cast<const uint32_t*>(a.segs + img * 4 + sg);
+        for (int i = w; i < (int)(sizeof(XSeg) / 4); i += 64) reinterpret_cast<uint32_t*>(&S.Q)[i] = gq[i];
+        if (nb >= 0) reinterpret_cast<uint4*>(s_nb[q])[w & 7] = rnb;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int i = l + 64 * k;
+            const int i = w + 64 * k;
             s_in[(i >> 4) * BPS + (i & 15)] = rin[k];
         }
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-            const int i = l + 64 * k;
+            const int i = w + 64 * k;
             const int c = i >> 6, kk = i & 63;
             s_in[(kk >> 3) * BPS + 16 + 8 * c + (kk & 7)] = ruv[k];
         }
-    }
-    if (l < 17) s_bands[l] = kEncBands[l];
-    {
-        static_assert(sizeof(XSeg) % 4 == 0, "XSeg copied as words");
-        const uint32_t* gq = reinterpret_cast<const uint32_t*>(a.segs + img * 4 + sg);
-        for (int i = l; i < (int)(sizeof(XSeg) / 4); i += 64) reinterpret_cast<uint32_t*>(&S.Q)[i] = gq[i];
     }
     const XSeg& Q = S.Q;
     __syncthreads();
@@ -430,6 +483,8 @@ __device__ __forceinline__ void mb_body(const XArgs& a, int img, int mb, MbLds& 
     __syncthreads();
     IK_STAMP(0);
 
+    // wave 1: intra-16, then chroma; wave 0: intra-4 (lane numbers per wave)
+    auto run_i16_uv = [&](const int l) {
     // ---- intra-16: lane = (mode, 4x4 block), 4 x 16 lanes ----
     {
         const int m = l >> 4, n = l & 15, bx = n & 3, by = n >> 2;
@@ -437,18 +492,18 @@ __device__ __forceinline__ void mb_body(const XArgs& a, int img, int mb, MbLds& 
         uint8_t* pred = s_pred16[m];
         pred16_block(pred, m, mx ? s_yl + 1 : nullptr, my ? s_yt : nullptr, bx, by);
         ftransform(s_in + off, pred + off, s_tmp16[m][n]);
-        __syncthreads();
+        WSYNC();
         if (n == 0) {  // the mode's Y2: WHT of the 16 DCs, quantised
             ftransform_wht(s_tmp16[m][0], s_dc16[m]);
             s_nz16[m] = quantize_block(s_dc16[m], s_lv16[m][0], Q.y2) << 24;
         }
-        __syncthreads();
+        WSYNC();
         s_tmp16[m][n][0] = 0;
         const int bnz = quantize_block(s_tmp16[m][n], s_lv16[m][1 + n], Q.y1);
         s_bnz[m][n] = bnz;
-        __syncthreads();
+        WSYNC();
         if (n == 0) itransform_wht(s_dc16[m], s_tmp16[m][0]);  // the DCs back into the blocks
-        __syncthreads();
+        WSYNC();
         itransform(pred + off, s_tmp16[m][n], s_rec16[m] + off);
         // this block's distortion, rate (VP8GetCostLuma16's contexts: the block above and
         // to the left in this mode, or the MB's incoming ones) and AC count
@@ -481,7 +536,7 @@ __device__ __forceinline__ void mb_body(const XArgs& a, int img, int mb, MbLds& 
             s_part[m][3] = kFixedCostsI16[m];
         }
     }
-    __syncthreads();
+    WSYNC();
     IK_STAMP(1);
     if (l == 0) {
         // IsFlatSource16; the doubling chain of PickBestIntra16 (flat so far in mode order)
@@ -507,231 +562,9 @@ __device__ __forceinline__ void mb_body(const XArgs& a, int img, int mb, MbLds& 
             mv = xabs(d[4]) > mv ? xabs(d[4]) : mv;
             atomicMax(a.max_edge + img * 4 + sg, mv);
         }
-        // VP8IteratorStartI4: the intra-4 boundary, contexts re-imported
-        for (int i = 0; i < 17; ++i) s_bound[i] = s_yl[16 - i];
-        for (int i = 0; i < 20; ++i) s_bound[17 + i] = s_yt[i];
-        s_i4ok = 1;
     }
-    __syncthreads();
+    WSYNC();
     IK_STAMP(2);
-
-    // ---- intra-4: 16 sub-blocks in order, lane = mode ----
-    {
-        int tnz4[4], lnz4[4];
-        for (int i = 0; i < 4; ++i) { tnz4[i] = s_tnz[i]; lnz4[i] = s_lnz[i]; }
-        int64_t aS = 211ll * Q.lambda_mode;  // rd_best: H = 211 = VP8BitCost(0, 145)
-        int header_bits = 0;
-#ifdef IK_VP8X_NO_I4
-        if (l == 0) s_i4ok = 0;
-        for (int i4 = 0; i4 < 0; ++i4) {
-#else
-        for (int i4 = 0; i4 < 16; ++i4) {
-#endif
-            const int bx = i4 & 3, by = i4 >> 2;
-            const int off = bx * 4 + by * 4 * BPS;
-            // lanes = (mode, row): 10 x 4; each transform split into its row and column passes
-            const int m = l >> 2, r = l & 3;
-            const bool act = l < 40;
-            if (act) {  // the mode's block in registers, row r stored by lane r
-                // the 13 boundary samples are the same for every lane: read them once and
-                // make them wave-uniform (SGPRs), so the ten divergent mode paths below are
-                // pure ALU instead of ten rounds of LDS reads
-                const uint8_t* tp = s_bound + kTopLeftI4[i4];
-                uint8_t e[13];
-#pragma unroll
-                for (int k = 0; k < 13; ++k) e[k] = (uint8_t)__builtin_amdgcn_readfirstlane((int)tp[k - 5]);
-                // every mode's block from the uniform samples (scalar ALU, no divergent
-                // paths); lane (m, r) keeps its mode's row r by selects
-                uint32_t mine = 0;
-#pragma unroll
-                for (int mm = 0; mm < 10; ++mm) {
-                    uint8_t d[16];
-                    pred4<4>(d, mm, e + 5);
-                    uint32_t rw[4];
-#pragma unroll
-                    for (int y = 0; y < 4; ++y)
-                        rw[y] = (uint32_t)d[4 * y] | ((uint32_t)d[4 * y + 1] << 8) | ((uint32_t)d[4 * y + 2] << 16) |
-                                ((uint32_t)d[4 * y + 3] << 24);
-                    const uint32_t row = r == 0 ? rw[0] : r == 1 ? rw[1] : r == 2 ? rw[2] : rw[3];
-                    mine = m == mm ? row : mine;
-                }
-                *reinterpret_cast<uint32_t*>(s_pred4[m] + r * BPS) = mine;
-            }
-            __syncthreads();
-            IK_STAMP(10);
-            if (act) {  // FTransform, row r
-                const uint8_t* sr = s_in + off + r * BPS;
-                const uint8_t* pp = s_pred4[m] + r * BPS;
-                const int d0 = sr[0] - pp[0], d1 = sr[1] - pp[1], d2 = sr[2] - pp[2], d3 = sr[3] - pp[3];
-                const int a0 = d0 + d3, a1 = d1 + d2, a2 = d1 - d2, a3 = d0 - d3;
-                s_ft4[m][0 + 4 * r] = (a0 + a1) * 8;
-                s_ft4[m][1 + 4 * r] = (a2 * 2217 + a3 * 5352 + 1812) >> 9;
-                s_ft4[m][2 + 4 * r] = (a0 - a1) * 8;
-                s_ft4[m][3 + 4 * r] = (a3 * 2217 - a2 * 5352 + 937) >> 9;
-            }
-            __syncthreads();
-            IK_STAMP(11);
-            if (act) {  // column r
-                const int* t = s_ft4[m];
-                const int i = r;
-                const int a0 = t[0 + i] + t[12 + i], a1 = t[4 + i] + t[8 + i];
-                const int a2 = t[4 + i] - t[8 + i], a3 = t[0 + i] - t[12 + i];
-                s_cf4[m][0 + i] = (int16_t)((a0 + a1 + 7) >> 4);
-                s_cf4[m][4 + i] = (int16_t)(((a2 * 2217 + a3 * 5352 + 12000) >> 16) + (a3 != 0));
-                s_cf4[m][8 + i] = (int16_t)((a0 - a1 + 7) >> 4);
-                s_cf4[m][12 + i] = (int16_t)((a3 * 2217 - a2 * 5352 + 51000) >> 16);
-            }
-            __syncthreads();
-            IK_STAMP(12);
-            int nzl = 0, cnt = 0;
-            if (act) {  // QuantizeBlock: zigzag positions 4r .. 4r+3 (all reads first, then the
-                        // stores: the reads of one position no longer wait for the last one's store)
-                int jj[4], vv[4], lv[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    jj[k] = zigzag(4 * r + k);
-                    vv[k] = s_cf4[m][jj[k]];
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const int j = jj[k], v = vv[k];
-                    const int sign = v < 0;
-                    const uint32_t coeff = (uint32_t)((sign ? -v : v) + Q.y1.sharpen[j]);
-                    int level = 0;
-                    if (coeff > Q.y1.zthresh[j]) {
-                        level = (int)((coeff * Q.y1.iq[j] + Q.y1.bias[j]) >> QFIX);
-                        if (level > 2047) level = 2047;
-                        if (sign) level = -level;
-                    }
-                    lv[k] = level;
-                    nzl |= level != 0;
-                    cnt += (4 * r + k) > 0 && level != 0;
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    s_cf4[m][jj[k]] = (int16_t)(lv[k] * (int)Q.y1.q[jj[k]]);
-                    s_blv[m][4 * r + k] = (int16_t)lv[k];
-                }
-            }
-            __syncthreads();
-            IK_STAMP(13);
-            if (act) {  // ITransform, column r
-                const int16_t* in = s_cf4[m];
-                const int i = r;
-                const int a = in[i] + in[8 + i], b = in[i] - in[8 + i];
-                const int c = ((in[4 + i] * 35468) >> 16) - (((in[12 + i] * 20091) >> 16) + in[12 + i]);
-                const int d = (((in[4 + i] * 20091) >> 16) + in[4 + i]) + ((in[12 + i] * 35468) >> 16);
-                s_C4[m][4 * i + 0] = a + d;
-                s_C4[m][4 * i + 1] = b + c;
-                s_C4[m][4 * i + 2] = b - c;
-                s_C4[m][4 * i + 3] = a - d;
-            }
-            __syncthreads();
-            IK_STAMP(14);
-            int sse = 0;
-            if (act) {  // row r: the reconstruction, its SSE and the spectral rows of source and reconstruction
-                const int* C = s_C4[m];
-                const int i = r;
-                const int dc = C[i] + 4;
-                const int a = dc + C[8 + i], b = dc - C[8 + i];
-                const int c = ((C[4 + i] * 35468) >> 16) - (((C[12 + i] * 20091) >> 16) + C[12 + i]);
-                const int d = (((C[4 + i] * 20091) >> 16) + C[4 + i]) + ((C[12 + i] * 35468) >> 16);
-                const uint8_t* pp = s_pred4[m] + i * BPS;
-                uint8_t* o = s_blk[m] + i * BPS;
-                o[0] = xclip8(pp[0] + ((a + d) >> 3));
-                o[1] = xclip8(pp[1] + ((b + c) >> 3));
-                o[2] = xclip8(pp[2] + ((b - c) >> 3));
-                o[3] = xclip8(pp[3] + ((a - d) >> 3));
-                const uint8_t* sr = s_in + off + i * BPS;
-                for (int x = 0; x < 4; ++x) {
-                    const int e = sr[x] - o[x];
-                    sse += e * e;
-                }
-                for (int q = 0; q < 2; ++q) {
-                    const uint8_t* in = q ? o : sr;
-                    const int a0 = in[0] + in[2], a1 = in[1] + in[3], a2 = in[1] - in[3], a3 = in[0] - in[2];
-                    s_tt4[m][q][0 + 4 * i] = a0 + a1;
-                    s_tt4[m][q][1 + 4 * i] = a3 + a2;
-                    s_tt4[m][q][2 + 4 * i] = a3 - a2;
-                    s_tt4[m][q][3 + 4 * i] = a0 - a1;
-                }
-            }
-            __syncthreads();
-            IK_STAMP(15);
-            int tA = 0, tB = 0;
-            if (act) {  // the spectral columns, weighted
-                const int i = r;
-                for (int q = 0; q < 2; ++q) {
-                    const int* t = s_tt4[m][q];
-                    const int a0 = t[0 + i] + t[8 + i], a1 = t[4 + i] + t[12 + i];
-                    const int a2 = t[4 + i] - t[12 + i], a3 = t[0 + i] - t[8 + i];
-                    const int v = kWeightY[i] * xabs(a0 + a1) + kWeightY[4 + i] * xabs(a3 + a2) +
-                                  kWeightY[8 + i] * xabs(a3 - a2) + kWeightY[12 + i] * xabs(a0 - a1);
-                    if (q) tB = v;
-                    else tA = v;
-                }
-            }
-            for (int o = 1; o <= 2; o <<= 1) {  // over the mode's 4 lanes
-                sse += __shfl_xor(sse, o, 64);
-                tA += __shfl_xor(tA, o, 64);
-                tB += __shfl_xor(tB, o, 64);
-                cnt += __shfl_xor(cnt, o, 64);
-                nzl |= __shfl_xor(nzl, o, 64);
-            }
-            // the mode's score and terms on its lane r == 0 (4m)
-            int64_t myS = INT64_MAX, myD = 0, mySD = 0, myR = 0, myH = 0;
-            if (act && r == 0) {
-                // mode costs from the neighbouring sub-blocks' modes (frame edge: B_DC)
-                const int left = bx ? s_modes4[i4 - 1] : s_nbm[by];
-                const int topm = by ? s_modes4[i4 - 4] : s_nbm[4 + bx];
-                myD = sse;
-                mySD = Q.tlambda ? ((Q.tlambda * (xabs(tB - tA) >> 5) + 128) >> 8) : 0;
-                myH = s_fi4[(topm * 10 + left) * 10 + m];
-                myR = (m > 0 && cnt <= 3) ? 140 : 0;  // IsFlat(levels, 1, FLATNESS_LIMIT_I4)
-                myR += rcost(lc, pr, s_fixed, s_ent, s_bands, 3, 0, tnz4[bx] + lnz4[by], s_blv[m]);
-                myS = rd_score(myR, myH, myD, mySD, Q.lambda_i4);
-            }
-            // lane 4m holds mode m's score: read the ten with v_readlane (wave-uniform
-            // results, no LDS), strict "<" in mode order = ties to the lowest mode
-            int64_t bsc = INT64_MAX;
-            int best = 0;
-#pragma unroll
-            for (int mm = 0; mm < 10; ++mm) {
-                const int64_t sc = rdlane64(myS, 4 * mm);
-                if (sc < bsc) { bsc = sc; best = mm; }
-            }
-            const int64_t sD = rdlane64(myD, 4 * best), sSD = rdlane64(mySD, 4 * best), sR = rdlane64(myR, 4 * best),
-                          sH = rdlane64(myH, 4 * best);
-            const int nzb = __builtin_amdgcn_readlane(nzl, 4 * best);
-            aS += rd_score(sR, sH, sD, sSD, Q.lambda_mode);
-            header_bits += (int)sH;
-            const bool stop = aS >= s_s16 || header_bits > 256 * 16 * 16;
-            if (l < 16) s_lv4[i4][l] = s_blv[best][l];
-            if (l < 16) s_best4[off + (l & 3) + (l >> 2) * BPS] = s_blk[best][(l & 3) + (l >> 2) * BPS];
-            __syncthreads();
-            IK_STAMP(16);
-            if (stop) {
-                if (l == 0) s_i4ok = 0;
-                break;
-            }
-            tnz4[bx] = lnz4[by] = nzb;
-            if (l == 0) s_modes4[i4] = (uint8_t)best;
-            if (l < 4) {
-                // VP8IteratorRotateI4, one position per lane (the writes [-4, 4) never
-                // overlap another lane's reads: [4, 8) or the block)
-                uint8_t* top = s_bound + kTopLeftI4[i4];
-                const uint8_t* blk = s_best4 + off;
-                const uint8_t b0 = blk[l + 3 * BPS];
-                const uint8_t b1 = (i4 & 3) != 3 ? (l < 3 ? blk[3 + (2 - l) * BPS] : top[3]) : top[l + 4];
-                top[-4 + l] = b0;
-                top[l] = b1;
-            }
-            __syncthreads();
-            IK_STAMP(17);
-        }
-    }
-    __syncthreads();
-    IK_STAMP(3);
 
     // ---- chroma: lane = (mode, 4x4 block), 4 x 8 lanes ----
     {
@@ -743,9 +576,9 @@ __device__ __forceinline__ void mb_body(const XArgs& a, int img, int mb, MbLds& 
             pred8_row(pred, m, mx ? s_ul + 1 : nullptr, my ? s_ut : nullptr, n);
             pred8_row(pred + 8, m, mx ? s_vl + 1 : nullptr, my ? s_vt : nullptr, n);
         }
-        __syncthreads();
+        WSYNC();
         if (act) ftransform(s_in + 16 + off, pred + off, s_tmpc[m][n]);
-        __syncthreads();
+        WSYNC();
         if (act && a.use_derr && b == 0) {  // CorrectDCValues, one channel: its 4 DCs in order
             const int8_t* top = s_derr_t[ch];
             const int8_t* left = s_derr_l[ch];
@@ -775,7 +608,7 @@ __device__ __forceinline__ void mb_body(const XArgs& a, int img, int mb, MbLds& 
             s_duv[m][ch][1] = (int8_t)e2;
             s_duv[m][ch][2] = (int8_t)e3;
         }
-        __syncthreads();
+        WSYNC();
         int D = 0, R = 0, cnt = 0;
         if (act) {
             s_cnz[m][n] = quantize_block(s_tmpc[m][n], s_lvuv[m][n], Q.uv);
@@ -787,7 +620,7 @@ __device__ __forceinline__ void mb_body(const XArgs& a, int img, int mb, MbLds& 
                 }
             for (int k = 1; k < 16; ++k) cnt += s_lvuv[m][n][k] != 0;
         }
-        __syncthreads();
+        WSYNC();
         if (act) {
             const int ctx = (by ? s_cnz[m][n - 2] : s_tnz[4 + 2 * ch + bx]) + (bx ? s_cnz[m][n - 1] : s_lnz[4 + 2 * ch + by]);
             R = rcost(lc, pr, s_fixed, s_ent, s_bands, 2, 0, ctx, s_lvuv[m][n]);
@@ -802,26 +635,289 @@ __device__ __forceinline__ void mb_body(const XArgs& a, int img, int mb, MbLds& 
             s_sc[m] = rd_score(R, kFixedCostsUV[m], D, 0, Q.lambda_uv);
         }
     }
-    __syncthreads();
+    WSYNC();
     if (l == 0) {
         int best = 0;
         for (int m = 1; m < 4; ++m)
             if (s_sc[m] < s_sc[best]) best = m;
         s_buv = best;
     }
-    __syncthreads();
+    WSYNC();
     IK_STAMP(4);
+    };
+
+    auto run_i4 = [&](const int l) {
+    // ---- intra-4: 16 sub-blocks in order; lane = (mode, row), 10 x 4 ----
+    // Per sub-block four phases between wave barriers, the rest in registers:
+    //  A: the lane's predictor row (mode m's row r, from the tap table) and source row;
+    //     FTransform's row pass;
+    //  B: column r: FTransform's column pass, QuantizeBlock of its four coefficients
+    //     (raster r, 4+r, 8+r, 12+r: quantisation is per coefficient), and
+    //     ITransform's column pass on the dequantised four;
+    //  C: row r: ITransform's row pass onto the predictor row, the SSE, the spectral
+    //     (TTransform) rows of source and reconstruction;
+    //  D: the spectral columns, the mode's rate and score, the winner, the rotation.
+    if (l == 0) {  // VP8IteratorStartI4: the intra-4 boundary, contexts re-imported
+        for (int i = 0; i < 17; ++i) s_bound[i] = s_yl[16 - i];
+        for (int i = 0; i < 20; ++i) s_bound[17 + i] = s_yt[i];
+    }
+    const int m = l >> 2, r = l & 3;
+    const bool act = l < 40;
+    // the lane's fixed terms: predictor taps, and the quantiser of its column (positions
+    // 1..15 share q / iq / bias / zero threshold: expand_matrix; sharpening per position)
+    uint32_t tap[4];
+    int shq[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+        tap[x] = kI4Tap[act ? m : 0][4 * r + x];
+        shq[x] = Q.y1.sharpen[r + 4 * x];
+    }
+    int bandrow[4];  // the level-cost row of zigzag position 4r + k, type 3: (3 * 8 + band) * 3
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bandrow[k] = (24 + kEncBands[4 * r + k]) * 3;
+    const uint32_t zt0 = Q.y1.zthresh[0], zt1 = Q.y1.zthresh[1], iq0 = Q.y1.iq[0], iq1 = Q.y1.iq[1];
+    const uint32_t bi0 = Q.y1.bias[0], bi1 = Q.y1.bias[1];
+    const int q0 = Q.y1.q[0], q1 = Q.y1.q[1];
+    WSYNC();
+    {
+        int tnz4[4], lnz4[4];
+        for (int i = 0; i < 4; ++i) { tnz4[i] = s_tnz[i]; lnz4[i] = s_lnz[i]; }
+        int64_t aS = 211ll * Q.lambda_mode;  // rd_best: H = 211 = VP8BitCost(0, 145)
+        int header_bits = 0;
+#ifdef IK_VP8X_NO_I4
+        header_bits = 1 << 30;
+        for (int i4 = 0; i4 < 0; ++i4) {
+#else
+        for (int i4 = 0; i4 < 16; ++i4) {
+#endif
+            const int bx = i4 & 3, by = i4 >> 2;
+            const int off = bx * 4 + by * 4 * BPS;
+            const uint8_t* tp = s_bound + kTopLeftI4[i4] - 5;  // e[0..12] = L K J I X A B C D E F G H
+            // ---- A ----
+            int p[4], sr[4];
+            {
+                int e0[4], e1[4], e2[4];
+#pragma unroll
+                for (int x = 0; x < 4; ++x) {
+                    e0[x] = tp[tap[x] & 15];
+                    e1[x] = tp[(tap[x] >> 4) & 15];
+                    e2[x] = tp[(tap[x] >> 8) & 15];
+                    sr[x] = s_in[off + r * BPS + x];
+                }
+                const int dc = (4 + tp[0] + tp[1] + tp[2] + tp[3] + tp[5] + tp[6] + tp[7] + tp[8]) >> 3;
+#pragma unroll
+                for (int x = 0; x < 4; ++x) {
+                    const uint32_t op = tap[x] >> 12;
+                    const int v3 = (e0[x] + 2 * e1[x] + e2[x] + 2) >> 2, v2 = (e0[x] + e1[x] + 1) >> 1;
+                    const int tm = xclip8(e0[x] + e1[x] - e2[x]);
+                    p[x] = op == 0 ? v3 : op == 1 ? v2 : op == 2 ? e0[x] : op == 3 ? tm : dc;
+                }
+            }
+            if (act) {  // FTransform, row r
+                const int d0 = sr[0] - p[0], d1 = sr[1] - p[1], d2 = sr[2] - p[2], d3 = sr[3] - p[3];
+                const int a0 = d0 + d3, a1 = d1 + d2, a2 = d1 - d2, a3 = d0 - d3;
+                *reinterpret_cast<int4*>(&s_ft4[m][4 * r]) =
+                    make_int4((a0 + a1) * 8, (a2 * 2217 + a3 * 5352 + 1812) >> 9, (a0 - a1) * 8,
+                              (a3 * 2217 - a2 * 5352 + 937) >> 9);
+            }
+            WSYNC();
+            IK_STAMP(10);
+            // ---- B ----
+            int nzl = 0, cnt = 0;
+            if (act) {
+                const int* t = s_ft4[m];
+                const int i = r;
+                const int a0 = t[0 + i] + t[12 + i], a1 = t[4 + i] + t[8 + i];
+                const int a2 = t[4 + i] - t[8 + i], a3 = t[0 + i] - t[12 + i];
+                int c[4];
+                c[0] = (int16_t)((a0 + a1 + 7) >> 4);
+                c[1] = (int16_t)(((a2 * 2217 + a3 * 5352 + 12000) >> 16) + (a3 != 0));
+                c[2] = (int16_t)((a0 - a1 + 7) >> 4);
+                c[3] = (int16_t)((a3 * 2217 - a2 * 5352 + 51000) >> 16);
+                int dq[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {  // QuantizeBlock of raster position j = r + 4k
+                    const int j = r + 4 * k;
+                    const int v = c[k];
+                    const int sign = v < 0;
+                    const uint32_t coeff = (uint32_t)((sign ? -v : v) + shq[k]);
+                    const bool z = j == 0;
+                    int level = 0;
+                    if (coeff > (z ? zt0 : zt1)) {
+                        level = (int)((coeff * (z ? iq0 : iq1) + (z ? bi0 : bi1)) >> QFIX);
+                        if (level > 2047) level = 2047;
+                        if (sign) level = -level;
+                    }
+                    s_blv[m][izigzag(j)] = (int16_t)level;
+                    dq[k] = (int16_t)(level * (z ? q0 : q1));
+                    nzl |= level != 0;
+                    cnt += j > 0 && level != 0;
+                }
+                // ITransform, column r
+                const int a = dq[0] + dq[2], b = dq[0] - dq[2];
+                const int cc = ((dq[1] * 35468) >> 16) - (((dq[3] * 20091) >> 16) + dq[3]);
+                const int d = (((dq[1] * 20091) >> 16) + dq[1]) + ((dq[3] * 35468) >> 16);
+                *reinterpret_cast<int4*>(&s_C4[m][4 * i]) = make_int4(a + d, b + cc, b - cc, a - d);
+            }
+            WSYNC();
+            IK_STAMP(13);
+            // ---- C ----
+            int sse = 0;
+            if (act) {
+                const int* C = s_C4[m];
+                const int i = r;
+                const int dc = C[i] + 4;
+                const int a = dc + C[8 + i], b = dc - C[8 + i];
+                const int c = ((C[4 + i] * 35468) >> 16) - (((C[12 + i] * 20091) >> 16) + C[12 + i]);
+                const int d = (((C[4 + i] * 20091) >> 16) + C[4 + i]) + ((C[12 + i] * 35468) >> 16);
+                int o[4];
+                o[0] = xclip8(p[0] + ((a + d) >> 3));
+                o[1] = xclip8(p[1] + ((b + c) >> 3));
+                o[2] = xclip8(p[2] + ((b - c) >> 3));
+                o[3] = xclip8(p[3] + ((a - d) >> 3));
+                *reinterpret_cast<uint32_t*>(s_blk[m] + i * BPS) =
+                    (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) | ((uint32_t)o[3] << 24);
+#pragma unroll
+                for (int x = 0; x < 4; ++x) {
+                    const int e = sr[x] - o[x];
+                    sse += e * e;
+                }
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int* in = q ? o : sr;
+                    const int a0 = in[0] + in[2], a1 = in[1] + in[3], a2 = in[1] - in[3], a3 = in[0] - in[2];
+                    *reinterpret_cast<int4*>(&s_tt4[m][q][4 * i]) = make_int4(a0 + a1, a3 + a2, a3 - a2, a0 - a1);
+                }
+            }
+            WSYNC();
+            IK_STAMP(15);
+            // ---- D ----
+            int tA = 0, tB = 0;
+            if (act) {  // the spectral columns, weighted
+                const int i = r;
+                for (int q = 0; q < 2; ++q) {
+                    const int* t = s_tt4[m][q];
+                    const int a0 = t[0 + i] + t[8 + i], a1 = t[4 + i] + t[12 + i];
+                    const int a2 = t[4 + i] - t[12 + i], a3 = t[0 + i] - t[8 + i];
+                    const int v = kWeightY[i] * xabs(a0 + a1) + kWeightY[4 + i] * xabs(a3 + a2) +
+                                  kWeightY[8 + i] * xabs(a3 - a2) + kWeightY[12 + i] * xabs(a0 - a1);
+                    if (q) tB = v;
+                    else tA = v;
+                }
+            }
+            // sums over the mode's 4 lanes
+            sse = qsum(sse);
+            tA = qsum(tA);
+            tB = qsum(tB);
+            cnt = qsum(cnt);
+            nzl |= qx1(nzl);
+            nzl |= qx2(nzl);
+            // the mode's rate, GetResidualCost (type 3, first 0) over its four lanes: lane r
+            // sums the terms of zigzag positions 4r .. 4r+3 (each position's context is its
+            // predecessor's level), the quad's last non-zero position bounds them
+            const int ctx0 = tnz4[bx] + lnz4[by];
+            int rate_terms = 0, last = -1;
+            {
+                const int16_t* lvm = s_blv[act ? m : 0];
+                const uint2 w2 = *reinterpret_cast<const uint2*>(lvm + 4 * r);
+                int v[4] = {(int16_t)(w2.x & 0xffffu), (int16_t)(w2.x >> 16), (int16_t)(w2.y & 0xffffu),
+                            (int16_t)(w2.y >> 16)};
+                int vp = r ? lvm[4 * r - 1] : 0;
+                vp = vp < 0 ? -vp : vp;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    v[k] = v[k] < 0 ? -v[k] : v[k];
+                    if (v[k]) last = 4 * r + k;
+                }
+                last = max(last, qx1(last));
+                last = max(last, qx2(last));
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int n = 4 * r + k;
+                    const int pv = k ? v[k - 1] : vp;
+                    const int ctx = n == 0 ? ctx0 : (pv >= 2 ? 2 : pv);
+                    const int term = s_fixed[v[k]] + lc[(bandrow[k] + ctx) * kLevelTab + (v[k] > kMaxVarLevel ? kMaxVarLevel : v[k])];
+                    rate_terms += n <= last ? term : 0;
+                }
+                rate_terms = qsum(rate_terms);
+            }
+            // the mode's score and terms on its lane r == 0 (4m)
+            int myS = INT32_MAX, myD = 0, mySD = 0, myR = 0, myH = 0;
+            if (act && r == 0) {
+                // mode costs from the neighbouring sub-blocks' modes (frame edge: B_DC)
+                const int left = bx ? s_modes4[i4 - 1] : s_nbm[by];
+                const int topm = by ? s_modes4[i4 - 4] : s_nbm[4 + bx];
+                myD = sse;
+                mySD = Q.tlambda ? ((Q.tlambda * (xabs(tB - tA) >> 5) + 128) >> 8) : 0;
+                myH = s_fi4[(topm * 10 + left) * 10 + m];
+                myR = (m > 0 && cnt <= 3) ? 140 : 0;  // IsFlat(levels, 1, FLATNESS_LIMIT_I4)
+                const int p0 = pr[(24 * 3 + ctx0) * 11];
+                if (last < 0) {
+                    myR += s_ent[p0];
+                } else {
+                    int vl = s_blv[m][last];
+                    vl = vl < 0 ? -vl : vl;
+                    myR += (ctx0 == 0 ? s_ent[255 - p0] : 0) + rate_terms;
+                    if (last < 15) myR += s_ent[pr[((24 + s_bands[last + 1]) * 3 + (vl == 1 ? 1 : 2)) * 11]];
+                }
+                // (the i4 terms fit 32 bits: D <= 16 * 255^2, rates and lambdas small)
+                myS = (myR + myH) * Q.lambda_i4 + 256 * (myD + mySD);
+            }
+            // lane 4m holds mode m's score: read the ten with v_readlane (wave-uniform
+            // results, no LDS), strict "<" in mode order = ties to the lowest mode
+            int bsc = INT32_MAX;
+            int best = 0;
+#pragma unroll
+            for (int mm = 0; mm < 10; ++mm) {
+                const int sc = __builtin_amdgcn_readlane(myS, 4 * mm);
+                if (sc < bsc) { bsc = sc; best = mm; }
+            }
+            const int64_t sD = __builtin_amdgcn_readlane(myD, 4 * best), sSD = __builtin_amdgcn_readlane(mySD, 4 * best),
+                          sR = __builtin_amdgcn_readlane(myR, 4 * best), sH = __builtin_amdgcn_readlane(myH, 4 * best);
+            const int nzb = __builtin_amdgcn_readlane(nzl, 4 * best);
+            aS += rd_score(sR, sH, sD, sSD, Q.lambda_mode);
+            header_bits += (int)sH;
+            if (l < 16) s_lv4[i4][l] = s_blv[best][l];
+            if (l < 16) s_best4[off + (l & 3) + (l >> 2) * BPS] = s_blk[best][(l & 3) + (l >> 2) * BPS];
+            IK_STAMP(16);
+            tnz4[bx] = lnz4[by] = nzb;
+            if (l == 0) s_modes4[i4] = (uint8_t)best;
+            if (l < 4) {
+                // VP8IteratorRotateI4, one position per lane (the writes [-4, 4) never
+                // overlap another lane's reads: [4, 8) or the winner's block)
+                uint8_t* top = s_bound + kTopLeftI4[i4];
+                const uint8_t* blk = s_blk[best];
+                const uint8_t b0 = blk[l + 3 * BPS];
+                const uint8_t b1 = (i4 & 3) != 3 ? (l < 3 ? blk[3 + (2 - l) * BPS] : top[3]) : top[l + 4];
+                top[-4 + l] = b0;
+                top[l] = b1;
+            }
+            WSYNC();
+            IK_STAMP(17);
+        }
+        if (l == 0) {
+            S.aS4 = aS;
+            S.hb4 = header_bits;
+        }
+    }
+    IK_STAMP(3);
+    };
+    if (__builtin_amdgcn_readfirstlane(l >> 6)) run_i16_uv(l - 64);
+    else run_i4(l);
+    __syncthreads();
 
     // ---- outputs: the MB record, the edge record (reconstruction edges, contexts,
     // chroma errors, edge sub-block modes), built in LDS and stored write-through ----
-    const bool i4 = s_i4ok != 0;
+    // intra-4 wins iff its running score never reached the i16 score nor its header
+    // bits the limit (both only grow): libwebp's loop would not have stopped
+    const bool i4 = S.aS4 < s_s16 && S.hb4 <= 256 * 16 * 16;
     const int b16 = s_b16, buv = s_buv;
     XMB& o = *reinterpret_cast<XMB*>(&s_tmp16[0][0][0]);
     XEdge& E = *reinterpret_cast<XEdge*>(&s_pred4[0][0]);
     const uint8_t* ry = i4 ? s_best4 : s_rec16[b16];
     const uint8_t* ruv = s_recuv[buv];
-    for (int i = l; i < 16 * 16; i += 64) o.ac[i >> 4][i & 15] = i4 ? s_lv4[i >> 4][i & 15] : s_lv16[b16][1 + (i >> 4)][i & 15];
-    for (int i = l; i < 8 * 16; i += 64) o.uv[i >> 4][i & 15] = s_lvuv[buv][i >> 4][i & 15];
+    for (int i = l; i < 16 * 16; i += kNT) o.ac[i >> 4][i & 15] = i4 ? s_lv4[i >> 4][i & 15] : s_lv16[b16][1 + (i >> 4)][i & 15];
+    if (l < 8 * 16) o.uv[l >> 4][l & 15] = s_lvuv[buv][l >> 4][l & 15];
     if (l < 16) {
         o.dc[l] = i4 ? 0 : s_lv16[b16][0][l];
         o.bmodes[l] = i4 ? s_modes4[l] : (uint8_t)b16;
@@ -895,7 +991,7 @@ __device__ __forceinline__ void fold_body(const XArgs& a, int img, int k0, int k
     if (l == 0) F.serial = 0;
     __syncthreads();
     const uint32_t bound = (uint32_t)(k1 - k0) * 25u * 16u;
-    for (int i = l; i < 1056; i += 64) {
+    for (int i = l; i < 1056; i += kNT) {
         F.st[i] = stats[i];
         if ((F.st[i] >> 16) + bound >= 0xfffeu) F.serial = 1;
     }
@@ -910,7 +1006,7 @@ __device__ __forceinline__ void fold_body(const XArgs& a, int img, int k0, int k
     };
     if (!F.serial) {
         uint32_t* st = F.st;
-        for (int k = k0 + l; k < k1; k += 64) {
+        for (int k = k0 + l; k < k1; k += kNT) {
             int t[9], lf[9];
             ctx_of(k, t, lf);
             record_mb([st](uint32_t slot, int bit) { atomicAdd(st + slot, 0x00010000u + (uint32_t)bit); return bit; },
@@ -920,7 +1016,7 @@ __device__ __forceinline__ void fold_body(const XArgs& a, int img, int k0, int k
     } else {
         for (int k = k0; k < k1; ++k) {
             const uint4* src = reinterpret_cast<const uint4*>(mbs + k);
-            for (int i = l; i < (int)(sizeof(XMB) / 16); i += 64) reinterpret_cast<uint4*>(&F.mb)[i] = src[i];
+            for (int i = l; i < (int)(sizeof(XMB) / 16); i += kNT) reinterpret_cast<uint4*>(&F.mb)[i] = src[i];
             __syncthreads();
             if (l == 0) {
                 int t[9], lf[9];
@@ -931,17 +1027,16 @@ __device__ __forceinline__ void fold_body(const XArgs& a, int img, int k0, int k
             __syncthreads();
         }
     }
-    for (int i = l; i < 1056; i += 64) F.pr[i] = (uint8_t)finalize_proba(F.st[i], i);
+    for (int i = l; i < 1056; i += kNT) F.pr[i] = (uint8_t)finalize_proba(F.st[i], i);
     __syncthreads();
-    for (int r = l; r < kCostRows; r += 64) level_cost_row(F.pr + r * 11, r % 3, F.lc + r * kLevelTab);
+    for (int r = l; r < kCostRows; r += kNT) level_cost_row(F.pr + r * 11, r % 3, F.lc + r * kLevelTab);
     __syncthreads();
-    for (int c = 0; c < 1056 * 4 / 16; c += 64)
-        store_wt(a.stats + (size_t)img * 1056 + 4 * c, F.st + 4 * c, min(1056 * 4 / 16 - c, 64) * 16, l);
-    store_wt(a.pr + (size_t)img * 1056, F.pr, 1056, l);  // 66 words: lanes 0..63 ...
-    store_wt(a.pr + (size_t)img * 1056 + 1024, F.pr + 1024, 32, l);  // ... and the last two
+    for (int c = 0; c < 1056 * 4 / 16; c += kNT)
+        store_wt(a.stats + (size_t)img * 1056 + 4 * c, F.st + 4 * c, min(1056 * 4 / 16 - c, kNT) * 16, l);
+    store_wt(a.pr + (size_t)img * 1056, F.pr, 1056, l);
     constexpr int kLcWords = kCostRows * kLevelTab * 2 / 16;
-    for (int c = 0; c < kLcWords; c += 64)
-        store_wt(a.lc + (size_t)img * kCostRows * kLevelTab + 8 * c, F.lc + 8 * c, min(kLcWords - c, 64) * 16, l);
+    for (int c = 0; c < kLcWords; c += kNT)
+        store_wt(a.lc + (size_t)img * kCostRows * kLevelTab + 8 * c, F.lc + 8 * c, min(kLcWords - c, kNT) * 16, l);
 }
 
 // lane 0: wait until *f >= want; false on a timeout (which sets the error word) or
@@ -959,13 +1054,19 @@ __device__ bool poll_ge(const uint32_t* f, uint32_t want, uint32_t* err, uint64_
 }
 
 // The whole call's decisions and statistics folds, one launch (see the file header).
-__global__ __launch_bounds__(64) void k_vp8x_run(XArgs a, XRun r) {
+__global__ __launch_bounds__(kNT) void k_vp8x_run(XArgs a, XRun r) {
     __shared__ XLds S;
     __shared__ uint64_t s_task;
     __shared__ int s_ok;
     const int l = threadIdx.x;
     const int nmb = a.mb_w * a.mb_h;
     uint32_t* err = r.sync + 1;
+    // the coder's waves win instruction issue on a SIMD they share with another batch's
+    // decode waves: its MB chain is latency-bound, the decode throughput-bound
+    __builtin_amdgcn_s_setprio(IK_VP8X_PRIO);
+#ifdef IK_VP8X_STAMPS
+    unsigned long long t_loop = clock64();
+#endif
     for (;;) {
         if (l == 0) {
             uint64_t task = ~0ull;
@@ -1000,6 +1101,12 @@ __global__ __launch_bounds__(64) void k_vp8x_run(XArgs a, XRun r) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         const int img = (int)((task >> 32) & 0xffffu), e = (int)((task >> 48) & 0xffu);
+#ifdef IK_VP8X_STAMPS
+        if (l == 0 && img == 0 && !(task >> 63)) {  // stamp 20: ticket + dependency wait + acquire
+            const unsigned long long t_ = clock64();
+            atomicAdd(&g_vp8x_stamps[20], t_ - t_loop);
+        }
+#endif
         // the lane index made opaque per task: otherwise the compiler hoists every
         // lane-derived address of the MB body out of the task loop (255 VGPRs, not 98)
         int lt = threadIdx.x;
@@ -1019,6 +1126,13 @@ __global__ __launch_bounds__(64) void k_vp8x_run(XArgs a, XRun r) {
             }
         }
         __syncthreads();
+#ifdef IK_VP8X_STAMPS
+        if (l == 0) {
+            const unsigned long long t_ = clock64();
+            if (img == 0 && !(task >> 63)) atomicAdd(&g_vp8x_stamps[21], t_ - t_loop);  // stamp 21: the whole task
+            t_loop = t_;
+        }
+#endif
     }
 }
 
@@ -1122,7 +1236,7 @@ hipError_t launch_vp8x_setup(const XArgs& a, const vp8::SegRecord* rec, const ui
 
 hipError_t launch_vp8x_run(const XArgs& a, const XRun& r, int grid, hipStream_t s) {
     if (grid <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_vp8x_run, dim3(grid), dim3(64), 0, s, a, r);
+    hipLaunchKernelGGL(k_vp8x_run, dim3(grid), dim3(kNT), 0, s, a, r);
     return hipGetLastError();
 }
 

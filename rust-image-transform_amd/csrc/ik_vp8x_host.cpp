@@ -264,9 +264,10 @@ const XSchedule& exact_schedule(int w, int h, int n) {
         }
         for (int i = 0; i < n; ++i) sc.tasks.push_back((1ull << 63) | ep | ((uint64_t)i << 32));
     }
-    // resident workgroups: twice the widest diagonal, so the next diagonal's MBs are
-    // waiting on their flags when the current one's finish
-    sc.grid = (int)std::min<size_t>(std::min(2 * widest, 2048), sc.tasks.size());
+    // resident workgroups: the widest diagonal's MBs (every workgroup more would hold
+    // LDS and registers that another batch's decode kernels beside the coder lose)
+    static const int mul = getenv("IK_VP8X_GRID_MUL") ? atoi(getenv("IK_VP8X_GRID_MUL")) : 1;
+    sc.grid = (int)std::min<size_t>(std::min(std::max(mul, 1) * widest, 2048), sc.tasks.size());
     sc.w = w;
     sc.h = h;
     sc.n = n;

@@ -50,10 +50,13 @@ if args.stamps:
     names = {0: "prologue", 1: "i16", 2: "i16 select", 10: "i4 pred", 11: "i4 fwd rows", 12: "i4 fwd cols",
              13: "i4 quant", 14: "i4 inv cols", 15: "i4 recon+spectral rows", 16: "i4 score+argmin+copy",
              17: "i4 rotate", 3: "i4 tail", 4: "chroma", 5: "outputs"}
+    task = {20: "task: ticket+wait+acquire", 21: "task: whole (loop top to loop top)"}
     calls = (args.iters + 1) * 1024  # image 0's MBs per batch (512^2: 32 x 32)
     tot = sum(stamps[i] for i in names)
     for i, nm in names.items():
         print(f"stamp {i:2d} {nm:24s} {stamps[i] / calls:10.0f} cycles/MB  {100.0 * stamps[i] / max(tot, 1):5.1f} %")
+    for i, nm in task.items():
+        print(f"stamp {i:2d} {nm:36s} {stamps[i] / calls:10.0f} cycles/MB")
 orc = ikutil.Oracle()
 ref = [orc.webp_encode_rgb(orc.to_rgb8(base[i]), 80.0) for i in range(4)]
 assert args.no_check or all(files[i] == ref[i % 4] for i in range(args.n)), "bytes differ from libwebp"
