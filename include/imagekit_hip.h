@@ -215,17 +215,15 @@ int ik_resize_exact(const ik_image *img, uint32_t nw, uint32_t nh, int filter, i
  * *out is allocated by the library; release with ik_buf_free. */
 int ik_encode(const ik_image *img, int fmt, int quality, uint8_t **out, size_t *out_len);
 
-/* WebP encoder behind encode_image (src/transform.rs:129-137).
- * IK_WEBP_LIBWEBP (default): libwebp's VP8 coder on the host over device-made
- *   YUV420 planes -- bytes identical to the reference's webp 0.3.1 / libwebp.
- * IK_WEBP_GPU: the gfx950 VP8 macroblock encoder (RD mode search, transforms,
- *   quantisation on the GPU; boolean coding on the host) -- a different encoder
- *   with libwebp-level size and PSNR, not byte-identical to libwebp.
- * The process default comes from IK_WEBP_ENCODER=gpu|exact|libwebp when first used. */
-/* IK_WEBP_EXACT: libwebp's own method-4 decisions on the GPU (segment analysis, RD mode
- *   search, token statistics; ik_webp_encode_exact_device) and its bitstream on the host
- *   -- byte-identical to IK_WEBP_LIBWEBP's output, with the coding off the host cores. */
-typedef enum { IK_WEBP_LIBWEBP = 0, IK_WEBP_GPU = 1, IK_WEBP_EXACT = 2 } ik_webp_encoder;
+/* WebP coder behind encode_image (src/transform.rs:129-137); both write the bytes of
+ * the reference's webp 0.3.1 -> libwebp WebPEncodeRGB.
+ * IK_WEBP_LIBWEBP: libwebp's VP8 coder on host threads over device-made YUV420 planes.
+ * IK_WEBP_EXACT: libwebp's own method-4 decisions on the GPU (segment analysis, RD mode
+ *   search, token statistics: ik_webp_encode_exact_device) and its bitstream on the
+ *   host -- the same files, with the coding off the host cores.
+ * The process default comes from IK_WEBP_ENCODER=exact|libwebp when first used.
+ * (Value 1, a non-exact GPU VP8 encoder of earlier rounds, is retired: refused.) */
+typedef enum { IK_WEBP_LIBWEBP = 0, IK_WEBP_EXACT = 2 } ik_webp_encoder;
 int ik_set_webp_encoder(int encoder); /* process-wide, for ik_encode / ik_transform */
 /* version of the libwebp that codes WebP (WebPGetEncoderVersion, e.g. 0x010600),
  * -1 when none could be loaded.  The codec libraries are explicit dependencies:
@@ -335,10 +333,6 @@ int ik_resize_batch_device(const uint8_t *dev_src, uint32_t W, uint32_t H, uint3
  * dev_yuv receives the Y (w*h), U and V ((w+1)/2 * (h+1)/2) planes back to back */
 int ik_webp_yuv420_device(const uint8_t *dev_src, uint32_t w, uint32_t h, uint32_t C,
                           size_t pitch, uint8_t *dev_yuv, void *hip_stream);
-/* the GPU WebP encoder on device YUV420 planes (the layout ik_webp_yuv420_device
- * writes); *out is allocated by the library (ik_buf_free) */
-int ik_webp_encode_gpu_device(const uint8_t *dev_yuv, uint32_t w, uint32_t h, int quality,
-                              uint8_t **out, size_t *out_len);
 /* libwebp's method-4 segment analysis on the GPU -- the first stage of
  * encode_image's WebP coder (src/transform.rs:129-137 -> libwebp VP8EncAnalyze +
  * VP8SetSegmentParams), exact: the same segment map and segment header libwebp

@@ -542,13 +542,12 @@ int encode_device_front(const uint8_t* dev, uint32_t w, uint32_t h, uint32_t c, 
         if (!dc) return fail(IK_ERR_DEVICE, "cannot upload WebP tables");
         const size_t uvw = (w + 1) / 2, uvh = (h + 1) / 2;
         const size_t bytes = (size_t)w * h + 2 * uvw * uvh;
-        if (default_webp_encoder() == IK_WEBP_GPU || default_webp_encoder() == IK_WEBP_EXACT) {
+        if (default_webp_encoder() == IK_WEBP_EXACT) {  // (read once: a concurrent switch cannot mix paths)
             uint8_t* dyuv = scratch(bytes);
             if (!dyuv) return fail(IK_ERR_DEVICE, "cannot allocate device scratch");
             hipError_t e = launch_webp_yuv420(dev, (int)w, (int)h, (int)c, pitch, 0, dyuv, 0, 1,
                                               dc->gamma_to_lin, dc->lin_to_gamma, s);
             if (e != hipSuccess) return hip_fail(e, "webp yuv420");
-            if (default_webp_encoder() == IK_WEBP_GPU) return webp_encode_gpu(dyuv, (int)w, (int)h, q, out);
             std::vector<std::vector<uint8_t>> files;
             if (int rc = webp_encode_exact(dyuv, 0, 1, (int)w, (int)h, q, files)) return rc;
             out.swap(files[0]);
@@ -1086,7 +1085,7 @@ int webp_front_group(const std::vector<ik_image*>& imgs, int quality, std::vecto
     const size_t n = imgs.size();
     if (!n) return IK_OK;
     const ik_image* i0 = imgs[0];
-    if (default_webp_encoder() != IK_WEBP_LIBWEBP || i0->w > 16383 || i0->h > 16383 || i0->depth != 1)
+    if (i0->w > 16383 || i0->h > 16383 || i0->depth != 1)  // (the caller chose the libwebp coder)
         return IK_ERR_UNSUPPORTED;
     DeviceGuard g(i0->device);
     const DeviceConsts* dc = device_consts(current_device());
@@ -1651,12 +1650,13 @@ static void transform_post_phase(const int64_t* w, const int64_t* h, const int* 
                 if (fmt[idx[k]] == IK_FORMAT_WEBP) byq[quality[idx[k]]].push_back(k);
                 if (fmt[idx[k]] == IK_FORMAT_JPEG) jbyq[quality[idx[k]]].push_back(k);
             }
+            const int webp_enc = default_webp_encoder();  // read once for the batch's groups
             for (auto& qv : byq) {
                 if (qv.second.size() < 2) continue;
                 std::vector<ik_image*> im;
                 std::vector<EncodePrep*> pp;
                 for (uint32_t k : qv.second) { im.push_back(rsz[k]); pp.push_back(&prep[k]); }
-                if (default_webp_encoder() == IK_WEBP_EXACT && im[0]->depth == 1 && im[0]->w <= 16383 &&
+                if (webp_enc == IK_WEBP_EXACT && im[0]->depth == 1 && im[0]->w <= 16383 &&
                     im[0]->h <= 16383) {
                     std::vector<std::vector<uint8_t>*> oo;
                     for (uint32_t k : qv.second) oo.push_back(&bytes_out[k]);

@@ -4,9 +4,9 @@
 //
 // Per batch: ONE resize launch over the whole batch (k_resize_fused, pixels HBM ->
 // LDS -> HBM), ONE colour-convert launch (WebP YUV420 planes or JPEG quantised
-// coefficients), with the GPU WebP encoder the VP8 wavefront (ik_vp8.hip), one
-// D2H copy of the small planes / MB records into pinned memory, then the host
-// entropy stage (libwebp VP8 / VP8 boolean coder / baseline Huffman) over a
+// coefficients), one D2H copy of the small planes into pinned memory, then the host
+// entropy stage (libwebp VP8 / AV1 / the JPEG segments the GPU Huffman coder wrote;
+// with the exact WebP coder, ik_vp8x.hip's one launch per batch) over a
 // persistent thread pool, one image per task -- the reference runs one
 // synchronous transform per tokio worker (src/main.rs:20), so per-image serial
 // entropy coding across cores is the same structure.  submit / collect keep two
@@ -97,7 +97,7 @@ private:
 struct ik_pipeline {
     int device = 0;
     hipStream_t stream = nullptr;   // resize + colour convert (+ host copies)
-    hipStream_t stream2 = nullptr;  // GPU VP8 wavefront + packer: overlaps the next batch's resize
+    hipStream_t stream2 = nullptr;  // (spare stream, kept for the ABI's event layout)
     uint32_t W = 0, H = 0, C = 0, nw = 0, nh = 0, max_batch = 0;
     int filter = 4, fmt = 1, quality = 80;
     uint8_t* d_resized = nullptr;
@@ -107,29 +107,26 @@ struct ik_pipeline {
     uint8_t* d_qt = nullptr;
     uint8_t qt[128];
     float* d_tmp = nullptr;      // naive resize path only
-    int webp_enc = IK_WEBP_LIBWEBP;  // IK_WEBP_GPU: k_vp8_diag wavefront + host bitstream
+    int webp_enc = IK_WEBP_LIBWEBP;  // IK_WEBP_EXACT: the exact GPU coder in the collect stage
     uint8_t* d_jwork = nullptr;      // JPEG: k_jpeg_huff_enc work (2 * jcap per image)
     size_t jcap = 0;
     std::vector<uint8_t> jpeg_hdr;   // SOI .. SOS for this geometry and quality
-    ik::Vp8Work vp8;
     // Two slots: the device stage of batch k+1 (enqueued by submit) runs while
     // the host entropy stage of batch k (collect) works from its slot.  The
     // resized images are shared (stream order); each slot has its own stage
-    // planes on the device, so with the GPU VP8 encoder the resize of batch k+1
-    // (stream) runs beside the wavefront of batch k (stream2).
+    // planes on the device, so the exact WebP coder of batch k (collect) reads its
+    // slot's planes while the resize of batch k+1 runs.
     struct Slot {
         uint8_t* h_stage = nullptr;       // pinned planes / coefficients
-        ik::vp8::MBOut* h_mbs = nullptr;  // pinned MB records (GPU VP8, frames too big to pack)
-        uint8_t* h_pack = nullptr;        // pinned compact MB streams (GPU VP8, k_vp8_pack)
         uint8_t* h_jpeg = nullptr;        // pinned entropy-coded JPEG segments (k_jpeg_huff_enc), jcap apart
         uint32_t* h_jlen = nullptr;       // their lengths
         int* d_aflag = nullptr;           // AVIF: per image, 1 when any alpha < 255 (k_avif_yuv444)
         int* h_aflag = nullptr;           // their pinned copies
-        // resize start / end, colour end, vp8 end, copies end, vp8 start (stream2)
+        // resize start / end, colour end, stage end, copies end, stage start
         hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
         uint8_t* d_stage = nullptr;       // this slot's part of ik_pipeline::d_stage
         uint32_t n = 0;
-        bool gpu_vp8 = false, packed = false;
+        bool exact = false;  // WebP: the exact GPU coder codes this slot's planes in collect
     } slot[2];
     int head = 0, inflight = 0;
     double ms[4] = {0, 0, 0, 0};
@@ -161,15 +158,14 @@ int enqueue(ik_pipeline* p, ik_pipeline::Slot& s, const uint8_t* dev_src, size_t
     ResizePlan* plan = get_resize_plan(p->device, (int)p->W, (int)p->H, (int)p->C, (int)p->nw, (int)p->nh,
                                        p->filter, (int)p->max_batch);
     if (!plan) return fail(IK_ERR_DEVICE, "cannot build resize plan");
-    s.gpu_vp8 = p->fmt == IK_FORMAT_WEBP && p->webp_enc == IK_WEBP_GPU;
+    s.exact = p->fmt == IK_FORMAT_WEBP && p->webp_enc == IK_WEBP_EXACT;
     s.n = n;
     IK_HIP(hipEventRecord(s.ev[0], p->stream));
     IK_HIP(launch_resize(*plan, dev_src, src_pitch, src_image_stride, p->d_resized, p->r_pitch,
                          p->r_img_stride, (int)n, p->d_tmp, p->stream));
     IK_HIP(hipEventRecord(s.ev[1], p->stream));
-    // the slot's stage planes were last read by the wavefront of the batch two
-    // back (stream2): its end event is still in s.ev[3] (a no-op wait if never recorded)
-    IK_HIP(hipStreamWaitEvent(p->stream, s.ev[3], 0));
+    // the slot's stage planes were last read two batches back (collected before
+    // this submit: the host stage waited for them)
     if (p->fmt == IK_FORMAT_AVIF) {
         IK_HIP(launch_avif_yuv444(p->d_resized, (int)p->nw, (int)p->nh, (int)p->C, p->r_pitch, p->r_img_stride,
                                   s.d_stage, p->stage_bytes, s.d_aflag, (int)n, p->stream));
@@ -184,20 +180,7 @@ int enqueue(ik_pipeline* p, ik_pipeline::Slot& s, const uint8_t* dev_src, size_t
                                   p->stage_bytes / sizeof(int16_t), (int)n, p->stream));
     }
     IK_HIP(hipEventRecord(s.ev[2], p->stream));
-    s.packed = false;
-    if (s.gpu_vp8) {
-        IK_HIP(hipStreamWaitEvent(p->stream2, s.ev[2], 0));
-        IK_HIP(hipEventRecord(s.ev[5], p->stream2));
-        if (int rc = p->vp8.launch(s.d_stage, p->stage_bytes, (int)n, p->quality, p->stream2)) return rc;
-        IK_HIP(hipEventRecord(s.ev[3], p->stream2));
-        if (copy_out && p->vp8.packable()) {
-            if (int rc = p->vp8.pack_to(s.h_pack, (int)n, p->stream2)) return rc;
-            s.packed = true;
-        } else if (copy_out) {
-            if (int rc = p->vp8.fetch_to(s.h_mbs, (int)n, p->stream2)) return rc;
-        }
-        IK_HIP(hipEventRecord(s.ev[4], p->stream2));
-    } else {
+    {
         IK_HIP(hipEventRecord(s.ev[5], p->stream));
         if (copy_out && p->fmt == IK_FORMAT_JPEG) {  // Huffman coding on the GPU, straight into pinned memory
             JpegEncArgs ja{};
@@ -215,7 +198,7 @@ int enqueue(ik_pipeline* p, ik_pipeline::Slot& s, const uint8_t* dev_src, size_t
             IK_HIP(launch_jpeg_huff_enc(ja, (int)n, p->stream));
         }
         IK_HIP(hipEventRecord(s.ev[3], p->stream));
-        if (copy_out && p->fmt != IK_FORMAT_JPEG)
+        if (copy_out && p->fmt != IK_FORMAT_JPEG && !s.exact)
             IK_HIP(hipMemcpyAsync(s.h_stage, s.d_stage, p->stage_bytes * n, hipMemcpyDeviceToHost, p->stream));
         if (copy_out && p->fmt == IK_FORMAT_AVIF)
             IK_HIP(hipMemcpyAsync(s.h_aflag, s.d_aflag, sizeof(int) * n, hipMemcpyDeviceToHost, p->stream));
@@ -232,7 +215,8 @@ int finish_device(ik_pipeline* p, ik_pipeline::Slot& s) {
     IK_HIP(hipEventElapsedTime(&c, s.ev[5], s.ev[3]));
     p->ms[0] = a;
     p->ms[1] = b;
-    p->ms[2] = s.gpu_vp8 ? c : 0.0;
+    p->ms[2] = 0.0;
+    (void)c;
     p->last_n = s.n;
     return IK_OK;
 }
@@ -244,18 +228,14 @@ int host_stage(ik_pipeline* p, const ik_pipeline::Slot& s, uint8_t* out, size_t 
     p->outs.resize(n);
     p->status.assign(n, 0);
     std::vector<std::string> errs(n);
-    p->pool->run((int)n, [&](int i) {
+    if (s.exact) {  // libwebp's decisions on the GPU for the whole batch, the files on the host
+        DeviceGuard g(p->device);
+        if (int rc = webp_encode_exact(s.d_stage, p->stage_bytes, (int)n, (int)p->nw, (int)p->nh, p->quality, p->outs))
+            return rc;
+    }
+    p->pool->run(s.exact ? 0 : (int)n, [&](int i) {
         const uint8_t* st = s.h_stage + p->stage_bytes * (size_t)i;
-        if (s.packed) {
-            p->status[i] = p->vp8.write_packed(s.h_pack + p->vp8.pack_cap() * (size_t)i, p->quality, p->outs[i]);
-            if (p->status[i]) {
-                char buf[256];
-                ik_last_error(buf, sizeof(buf));
-                errs[i] = buf;
-            }
-        } else if (s.gpu_vp8) {
-            p->vp8.write_from(s.h_mbs, i, p->quality, p->outs[i]);
-        } else if (p->fmt == IK_FORMAT_AVIF) {
+        if (p->fmt == IK_FORMAT_AVIF) {
             // image 0.25.8 AvifEncoder::new_with_speed_quality(out, 4, q) (src/transform.rs:140-145)
             p->status[i] = avif_encode_yuv444(st, s.h_aflag[i] != 0, (int)p->nw, (int)p->nh, p->quality, 4,
                                               p->outs[i]);
@@ -328,7 +308,7 @@ int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t
         return rc;
     }
     *out = p;
-    if (fmt == IK_FORMAT_WEBP && default_webp_encoder() == IK_WEBP_GPU) return ik_pipeline_set_webp_encoder(p, IK_WEBP_GPU);
+    if (fmt == IK_FORMAT_WEBP && default_webp_encoder() == IK_WEBP_EXACT) return ik_pipeline_set_webp_encoder(p, IK_WEBP_EXACT);
     return IK_OK;
 }
 
@@ -396,21 +376,11 @@ extern "C" {
 int ik_pipeline_set_webp_encoder(ik_pipeline* p, int encoder) {
     IK_API_ENTER();
     if (!p) return fail(IK_ERR_INVALID, "null pipeline");
-    if (encoder != IK_WEBP_LIBWEBP && encoder != IK_WEBP_GPU) return fail(IK_ERR_INVALID, "bad WebP encoder %d", encoder);
+    if (encoder != IK_WEBP_LIBWEBP && encoder != IK_WEBP_EXACT) return fail(IK_ERR_INVALID, "bad WebP encoder %d", encoder);
     if (p->fmt != IK_FORMAT_WEBP) return fail(IK_ERR_INVALID, "not a WebP pipeline");
     if (p->inflight) return fail(IK_ERR_INVALID, "batches in flight: collect them first");
-    IK_HIP(hipSetDevice(p->device));
-    if (encoder == IK_WEBP_GPU) {
-        if (p->nw > 16383 || p->nh > 16383) return fail(IK_ERR_TRANSFORM, "WebP dimensions exceed 16383");
-        if (int rc = p->vp8.reserve((int)p->nw, (int)p->nh, (int)p->max_batch, false)) return rc;
-        for (auto& sl : p->slot) {
-            if (p->vp8.packable()) {
-                if (!sl.h_pack) IK_HIP(hipHostMalloc(&sl.h_pack, p->vp8.pack_cap() * p->max_batch, hipHostMallocDefault));
-            } else if (!sl.h_mbs) {
-                IK_HIP(hipHostMalloc(&sl.h_mbs, p->vp8.record_bytes((int)p->max_batch), hipHostMallocDefault));
-            }
-        }
-    }
+    if (encoder == IK_WEBP_EXACT && (p->nw > 16383 || p->nh > 16383))
+        return fail(IK_ERR_TRANSFORM, "WebP dimensions exceed 16383");
     p->webp_enc = encoder;
     return IK_OK;
 }
@@ -475,7 +445,6 @@ void ik_pipeline_destroy(ik_pipeline* p) {
     if (p->stream) (void)hipStreamSynchronize(p->stream);
     if (p->stream2) (void)hipStreamSynchronize(p->stream2);
     delete p->pool;
-    p->vp8.release();
     if (p->d_resized) (void)hipFree(p->d_resized);
     if (p->d_stage) (void)hipFree(p->d_stage);
     if (p->d_qt) (void)hipFree(p->d_qt);
@@ -483,8 +452,6 @@ void ik_pipeline_destroy(ik_pipeline* p) {
     if (p->d_jwork) (void)hipFree(p->d_jwork);
     for (auto& sl : p->slot) {
         if (sl.h_stage) (void)hipHostFree(sl.h_stage);
-        if (sl.h_mbs) (void)hipHostFree(sl.h_mbs);
-        if (sl.h_pack) (void)hipHostFree(sl.h_pack);
         if (sl.h_jpeg) (void)hipHostFree(sl.h_jpeg);
         if (sl.h_jlen) (void)hipHostFree(sl.h_jlen);
         if (sl.d_aflag) (void)hipFree(sl.d_aflag);

@@ -221,39 +221,17 @@ void jpeg_write(const int16_t* coef, int w, int h, const uint8_t qt[128], std::v
 void jpeg_header(int w, int h, const uint8_t qt[128], std::vector<uint8_t>& out);  // SOI .. SOS
 void jpeg_huff_u32(uint32_t t[4 * 256]);  // ldc, lac, cdc, cac: code << 8 | size
 
-// GPU WebP encoder (ik_webp_gpu.cpp + ik_vp8.hip): reusable device / pinned
-// buffers for n images of one geometry
-namespace vp8 { struct MBOut; }
-struct Vp8Work {
-    int w = 0, h = 0, cap_n = 0;
-    uint8_t* d_rec = nullptr;        // reconstruction planes (prediction context)
-    vp8::MBOut* d_mbs = nullptr;     // per-MB decisions + levels
-    uint8_t* d_nz = nullptr;         // per-MB outgoing non-zero contexts
-    vp8::MBOut* h_mbs = nullptr;     // pinned mirror of d_mbs (host_buffers, frames too big to pack)
-    uint8_t* d_pack = nullptr;       // k_vp8_pack scratch (pack_cap() bytes per image)
-    uint8_t* h_pack = nullptr;       // pinned compact streams (single-image path)
-    int reserve(int w, int h, int n, bool host_buffers);
-    void release();
-    size_t mb_count() const;
-    size_t record_bytes(int n) const;  // MB records of n images
-    // the wavefront launches for n images (YUV420 planes yuv_stride apart), async on s
-    int launch(const uint8_t* d_yuv, size_t yuv_stride, int n, int quality, hipStream_t s);
-    int fetch(int n, hipStream_t s) { return fetch_to(h_mbs, n, s); }  // async D2H of the MB records
-    int fetch_to(vp8::MBOut* dst, int n, hipStream_t s);
-    void write(int i, int quality, std::vector<uint8_t>& out) const { write_from(h_mbs, i, quality, out); }
-    void write_from(const vp8::MBOut* recs, int i, int quality, std::vector<uint8_t>& out) const;  // host bitstream
-    // compact records (k_vp8_pack) of n images straight into pinned host memory,
-    // pack_cap() bytes apart; packable() = the frame fits the packer
-    bool packable() const;
-    size_t pack_cap() const;
-    int pack_to(uint8_t* host_dst, int n, hipStream_t s);
-    int write_packed(const uint8_t* pack_img, int quality, std::vector<uint8_t>& out) const;
-};
-int default_webp_encoder();  // IK_WEBP_LIBWEBP unless ik_set_webp_encoder / IK_WEBP_ENCODER=gpu
-int webp_encode_gpu(const uint8_t* d_yuv, int w, int h, int quality, std::vector<uint8_t>& out);
+// the WebP coder encode_image uses unless ik_set_webp_encoder / IK_WEBP_ENCODER says
+// otherwise (ik_webp_gpu.cpp)
+constexpr int kDefaultWebpEncoder = IK_WEBP_LIBWEBP;
+int default_webp_encoder();
 // the exact coder (ik_vp8x_host.cpp): libwebp's files from n device YUV420 images
 int webp_encode_exact(const uint8_t* d_yuv, size_t yuv_stride, int n, int w, int h, int quality,
                       std::vector<std::vector<uint8_t>>& outs);
+// its first stages alone (ik_vp8_analyze_device): segment analysis and set-up on the
+// device, the segment map and headers into host memory
+int vp8_analyze_setup(const uint8_t* d_yuv, size_t yuv_stride, int n, int w, int h, float quality, uint8_t* seg,
+                      ik_vp8_segment_header* hdr);
 
 // host decoders (ik_decode.cpp): tightly packed 8-bit pixels
 enum class Sniffed { Png, Jpeg, Gif, WebP, Tiff, Bmp, Ico, Hdr, Avif, OpenExr, Qoi, Farbfeld, Pnm, Dds, Unknown };

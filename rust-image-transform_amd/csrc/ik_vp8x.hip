@@ -281,7 +281,7 @@ __device__ unsigned long long g_vp8x_stamps[32];
     do {                                                                    \
         if (l == 0 && img == 0) {                                           \
             const unsigned long long t_ = clock64();                        \
-            atomicAdd(&g_vp8x_stamps[i], t_ - t_prev);                      \
+            atomicAdd(&stm[i], t_ - t_prev); /* LDS: no vmcnt wait */       \
             t_prev = t_;                                                    \
         }                                                                   \
     } while (0)
@@ -291,7 +291,7 @@ __device__ unsigned long long g_vp8x_stamps[32];
 
 // One MB: libwebp's VP8Decimate (i16, intra-4, chroma; RD by the image's current level
 // costs), then the MB's decision record and edge record, stored write-through.
-__device__ __forceinline__ void mb_body(const XArgs& a, int img, int mb, MbLds& S, int l) {
+__device__ __forceinline__ void mb_body(const XArgs& a, int img, int mb, MbLds& S, int l, unsigned long long* stm) {
 #ifdef IK_VP8X_STAMPS
     unsigned long long t_prev = clock64();
 #endif
@@ -1066,6 +1066,11 @@ __global__ __launch_bounds__(kNT) void k_vp8x_run(XArgs a, XRun r) {
     __builtin_amdgcn_s_setprio(IK_VP8X_PRIO);
 #ifdef IK_VP8X_STAMPS
     unsigned long long t_loop = clock64();
+    __shared__ unsigned long long stm[32];
+    if (l < 32) stm[l] = 0;
+    __syncthreads();
+#else
+    unsigned long long* stm = nullptr;
 #endif
     for (;;) {
         if (l == 0) {
@@ -1095,7 +1100,12 @@ __global__ __launch_bounds__(kNT) void k_vp8x_run(XArgs a, XRun r) {
         __syncthreads();
         const uint64_t task = uniform_u64(s_task);
         const int ok = __builtin_amdgcn_readfirstlane(s_ok);
-        if (task == ~0ull || !ok) return;
+        if (task == ~0ull || !ok) {
+#ifdef IK_VP8X_STAMPS
+            if (l < 32) atomicAdd(&g_vp8x_stamps[l], stm[l]);
+#endif
+            return;
+        }
         // the hand-off's acquire: this CU's L1 holds nothing older than the flags seen
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1104,7 +1114,7 @@ __global__ __launch_bounds__(kNT) void k_vp8x_run(XArgs a, XRun r) {
 #ifdef IK_VP8X_STAMPS
         if (l == 0 && img == 0 && !(task >> 63)) {  // stamp 20: ticket + dependency wait + acquire
             const unsigned long long t_ = clock64();
-            atomicAdd(&g_vp8x_stamps[20], t_ - t_loop);
+            atomicAdd(&stm[20], t_ - t_loop);
         }
 #endif
         // the lane index made opaque per task: otherwise the compiler hoists every
@@ -1112,7 +1122,7 @@ __global__ __launch_bounds__(kNT) void k_vp8x_run(XArgs a, XRun r) {
         int lt = threadIdx.x;
         asm volatile("" : "+v"(lt));
         if (task >> 63) fold_body(a, img, r.bounds[e], r.bounds[e + 1], S.f, lt);
-        else mb_body(a, img, (int)(uint32_t)task, S.m, lt);
+        else mb_body(a, img, (int)(uint32_t)task, S.m, lt, stm);
         // the payload's write-through stores have completed before the flag
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -1129,7 +1139,7 @@ __global__ __launch_bounds__(kNT) void k_vp8x_run(XArgs a, XRun r) {
 #ifdef IK_VP8X_STAMPS
         if (l == 0) {
             const unsigned long long t_ = clock64();
-            if (img == 0 && !(task >> 63)) atomicAdd(&g_vp8x_stamps[21], t_ - t_loop);  // stamp 21: the whole task
+            if (img == 0 && !(task >> 63)) atomicAdd(&stm[21], t_ - t_loop);  // stamp 21: the whole task
             t_loop = t_;
         }
 #endif

@@ -399,6 +399,51 @@ int webp_encode_exact(const uint8_t* d_yuv, size_t yuv_stride, int n, int w, int
     return IK_OK;
 }
 
+
+// The exact coder's first two stages alone (ik_vp8_analyze_device): libwebp's segment
+// analysis and the segment set-up on the device, the final segment map and headers
+// into host memory; on the calling thread's stream, waits.
+int vp8_analyze_setup(const uint8_t* d_yuv, size_t yuv_stride, int n, int w, int h, float quality, uint8_t* seg,
+                      ik_vp8_segment_header* hdr) {
+    hipStream_t s = thread_stream();
+    if (!s) return fail(IK_ERR_DEVICE, "cannot create HIP stream");
+    const int mb_w = (w + 15) / 16, mb_h = (h + 15) / 16, nmb = mb_w * mb_h;
+    size_t off = 0;
+    auto part = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~(size_t)255; return o; };
+    const size_t o_alpha = part((size_t)nmb * n), o_uva = part((size_t)nmb * n * 2), o_kseg = part((size_t)nmb * n);
+    const size_t o_rec = part(sizeof(vp8::SegRecord) * n), o_hdr = part(sizeof(ik_vp8_segment_header) * n);
+    const size_t o_seg = part((size_t)nmb * n), o_segs = part(sizeof(XSeg) * 4 * n);
+    const size_t o_lc = part(2ull * kCostRows * kLevelTab * n), o_pr = part(1056ull * n), o_st = part(4ull * 1056 * n);
+    const size_t o_me = part(16ull * n), o_qtab = part(4 * 255);
+    uint8_t* d = scratch_slot(kScratchExact, off);
+    if (!d) return fail(IK_ERR_DEVICE, "cannot allocate the segment analysis' work area (%zu bytes)", off);
+    uint8_t* hc = pinned_slot(kPinnedExactIn, 4 * 255);
+    if (!hc) return IK_ERR_NOMEM;
+    segment_quant_table(quality, reinterpret_cast<int*>(hc));
+    IK_HIP(hipMemcpyAsync(d + o_qtab, hc, 4 * 255, hipMemcpyHostToDevice, s));
+    XArgs a{};
+    a.yuv = d_yuv;
+    a.yuv_stride = yuv_stride;
+    a.w = w;
+    a.h = h;
+    a.mb_w = mb_w;
+    a.mb_h = mb_h;
+    a.seg = d + o_seg;
+    a.segs = (XSeg*)(d + o_segs);
+    a.lc = (uint16_t*)(d + o_lc);
+    a.pr = d + o_pr;
+    a.stats = (uint32_t*)(d + o_st);
+    a.max_edge = (int*)(d + o_me);
+    IK_HIP(vp8::launch_vp8_analysis(d_yuv, yuv_stride, n, w, h, d + o_alpha, (uint16_t*)(d + o_uva), d + o_kseg,
+                                    (vp8::SegRecord*)(d + o_rec), s));
+    IK_HIP(launch_vp8x_setup(a, (const vp8::SegRecord*)(d + o_rec), d + o_kseg, (const int*)(d + o_qtab),
+                             (ik_vp8_segment_header*)(d + o_hdr), n, s));
+    IK_HIP(hipMemcpyAsync(seg, d + o_seg, (size_t)nmb * n, hipMemcpyDeviceToHost, s));
+    IK_HIP(hipMemcpyAsync(hdr, d + o_hdr, sizeof(ik_vp8_segment_header) * n, hipMemcpyDeviceToHost, s));
+    IK_HIP(hipStreamSynchronize(s));
+    return IK_OK;
+}
+
 }  // namespace ik
 
 using namespace ik;

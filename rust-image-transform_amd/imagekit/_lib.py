@@ -57,7 +57,6 @@ SIGNATURES = [
     ("ik_codec_library", ctypes.c_size_t, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
     ("ik_get_webp_encoder", ctypes.c_int, []),
     ("ik_pipeline_set_webp_encoder", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
-    ("ik_webp_encode_gpu_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]),
     ("ik_webp_encode_exact_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     ("ik_vp8_analyze_device", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p]),
     ("ik_pipeline_create", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),

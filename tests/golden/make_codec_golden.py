@@ -7,9 +7,6 @@ encode_image branches (TEST INFRASTRUCTURE).
   the libwebp vendored by libwebp-sys 0.9.6 cannot be checked offline.
 - jpeg_*: the oracle restatement of image 0.25.8's JpegEncoder (oracle/jpeg_enc.c),
   checked to decode in libjpeg-turbo (Pillow) within 30 dB of its input.
-- vp8_*: this project's scalar VP8 encoder (tools/vp8_cpu_check.cpp, the GPU
-  encoder's restatement), checked to decode in libwebp -- a regression pin, not
-  a reference output.
 Inputs are deterministic SplitMix64 images (tests/ikutil.synth); only outputs and
 the input recipe are stored.  No reference code is executed or copied.
 
@@ -23,7 +20,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
-sys.path[:0] = [os.path.dirname(HERE), os.path.join(ROOT, "tools")]
+sys.path[:0] = [os.path.dirname(HERE)]
 import ikutil  # noqa: E402
 
 CASES = [  # (name, W, H, pattern, seed, q)
@@ -38,22 +35,17 @@ def psnr(a, b):
 
 def main():
     from PIL import Image
-    import vp8_cpu_check as vp8
     orc = ikutil.Oracle()
     out = {}
     for name, W, H, pat, seed, q in CASES:
         rgb = ikutil.synth(W, H, 3, seed=seed, pattern=pat)
         w = orc.webp_encode_rgb(rgb, float(q))
         j = orc.jpeg_encode_rgb(rgb, q)
-        Y, U, V = orc.webp_yuv420(rgb)
-        v, _ = vp8.encode(Y, U, V, float(q), -1)
         assert np.asarray(Image.open(io.BytesIO(w))).shape == (H, W, 3)
         assert psnr(np.asarray(Image.open(io.BytesIO(j)).convert("RGB")), rgb) > (30 if pat == "S" and q >= 80 else 5)
-        assert vp8.decode_yuv(v) is not None
         out[f"{name}_meta"] = np.array([W, H, 0 if pat == "S" else 1, seed, q], np.int64)
         out[f"{name}_webp"] = np.frombuffer(w, np.uint8)
         out[f"{name}_jpeg"] = np.frombuffer(j, np.uint8)
-        out[f"{name}_vp8"] = np.frombuffer(v, np.uint8)
     np.savez_compressed(os.path.join(HERE, "codec_golden.npz"), **out)
     print(f"wrote {len(CASES)} cases")
 

@@ -2,10 +2,9 @@
 tests/golden/make_codec_golden.py).
 
 CPU: the oracle reproduces them (libwebp 1.2.2 WebPEncodeRGB proxy; the JPEG
-restatement; the scalar VP8 restatement).  GPU (marked): encode_image / the GPU
-VP8 encoder reproduce the same bytes."""
+restatement).  GPU (marked): encode_image reproduces the same bytes with both WebP
+coders (libwebp, and the exact GPU coder)."""
 import os
-import sys
 
 import numpy as np
 import pytest
@@ -29,15 +28,6 @@ def test_oracle_reproduces_codec_golden(oracle, name):
     assert oracle.jpeg_encode_rgb(rgb, q) == G[f"{name}_jpeg"].tobytes()
 
 
-@pytest.mark.parametrize("name", NAMES)
-def test_scalar_vp8_reproduces_golden(oracle, name):
-    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tools"))
-    vp8 = pytest.importorskip("vp8_cpu_check")
-    rgb, q = _case(name)
-    Y, U, V = oracle.webp_yuv420(rgb)
-    assert vp8.encode(Y, U, V, float(q), -1)[0] == G[f"{name}_vp8"].tobytes()
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", NAMES)
 def test_gpu_encoders_reproduce_codec_golden(ik, oracle, name):
@@ -47,9 +37,11 @@ def test_gpu_encoders_reproduce_codec_golden(ik, oracle, name):
     d = DynamicImage.from_array(rgb)
     assert encode_image(d, ImageFormat.webp, q) == G[f"{name}_webp"].tobytes()
     assert encode_image(d, ImageFormat.jpeg, q) == G[f"{name}_jpeg"].tobytes()
-    assert ik.ik_set_webp_encoder(1) == 0
+    prev = ik.ik_get_webp_encoder()
+    assert ik.ik_set_webp_encoder(2 - prev) == 0  # the other coder
     try:
         got = encode_image(d, ImageFormat.webp, q)
     finally:
-        assert ik.ik_set_webp_encoder(0) == 0
-    assert got == G[f"{name}_vp8"].tobytes()
+        assert ik.ik_set_webp_encoder(prev) == 0
+    assert got == G[f"{name}_webp"].tobytes()
+    assert ik.ik_set_webp_encoder(1) != 0  # the retired non-exact encoder is refused

@@ -2,7 +2,7 @@
 batched form of the /img handler's decode -> resize_image -> encode_image chain
 (reference src/lib.rs:175-191, src/transform.rs:62-150) with two batches in
 flight.  Bar: every batch's bytes identical to ik_pipeline_run on the same
-frames (itself pinned against the oracle in test_gpu_pipeline / test_gpu_vp8),
+frames (itself pinned against the oracle in test_gpu_pipeline; the exact WebP coder in test_gpu_vp8x),
 for every encoder, with batches of different sizes and sources interleaved."""
 import ctypes
 
@@ -41,7 +41,7 @@ def _unpack(out, sizes, n):
     return res
 
 
-@pytest.mark.parametrize("fmt,enc", [(IK_WEBP, 0), (IK_WEBP, 1), (IK_JPEG, 0)])
+@pytest.mark.parametrize("fmt,enc", [(IK_WEBP, 0), (IK_WEBP, 2), (IK_JPEG, 0)])
 def test_submit_collect_equals_run(ik, fmt, enc):
     max_b = 4
     batches = [(_frames(100, 4), 4), (_frames(200, 3), 3), (_frames(300, 4), 1), (_frames(400, 2), 2)]
@@ -78,7 +78,7 @@ def test_submit_collect_equals_run(ik, fmt, enc):
         assert ik.ik_pipeline_submit(p, devs[2].p, pitch, H * pitch, 4) != 0  # a third is refused
         assert ik.ik_pipeline_run(p, devs[2].p, pitch, H * pitch, 4, None, 0, None) != 0
         if fmt == IK_WEBP:
-            assert ik.ik_pipeline_set_webp_encoder(p, 1 - enc) != 0
+            assert ik.ik_pipeline_set_webp_encoder(p, 2 - enc) != 0
         collect()
         submit(2)
         collect()

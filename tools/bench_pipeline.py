@@ -47,7 +47,7 @@ ikutil.use_pillow_codecs()  # codec libraries named explicitly (IK_LIBWEBP / IK_
 METRIC = "transform MPix/s (decode+resize+encode) 4096²→512² WebP q80; 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FILTERS = {"nearest": 0, "triangle": 1, "catmullrom": 2, "gaussian": 3, "lanczos3": 4}
-ENCODERS = {"libwebp": 0, "gpu": 1}
+ENCODERS = {"libwebp": 0, "exact": 2}
 CPU_CODER = {"webp": "libwebp", "jpeg": "image-crate JPEG", "avif": "libavif/aom speed 4 (Pillow, rav1e absent)"}
 FORMATS = {"jpeg": 0, "webp": 1, "avif": 2}
 
@@ -71,7 +71,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline sample wall-time budget (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--device-only", action="store_true", help="time resize+colour kernels only")
-    ap.add_argument("--webp-encoder", default="libwebp", choices=["libwebp", "gpu"],
+    ap.add_argument("--webp-encoder", default="libwebp", choices=["libwebp", "exact"],
                     help="libwebp: host VP8 coder, bytes identical to the reference; gpu: gfx950 VP8 encoder")
     ap.add_argument("--sync", action="store_true", help="one batch in flight (ik_pipeline_run per step)")
     ap.add_argument("--no-alt-encoder", action="store_true", help="skip timing the other WebP encoder")
@@ -363,7 +363,7 @@ def main():
     # images per launch)
     alt_enc = {}
     if not args.device_only and not args.no_alt_encoder and fmt == 1:
-        other = "gpu" if args.webp_encoder == "libwebp" else "libwebp"
+        other = "exact" if args.webp_encoder == "libwebp" else "libwebp"
         AB = args.alt_batch
         p3 = ctypes.c_void_p()
         if lib.ik_pipeline_create(S, S, 4, O, O, f, 1, args.quality, AB, args.threads, ctypes.byref(p3)) == 0:

@@ -47,9 +47,9 @@ for it in range(args.iters + 1):
         ik.ik_buf_free(outs[i])
 if args.stamps:
     ik.ik_vp8x_stamps(stamps)
-    names = {0: "prologue", 1: "i16", 2: "i16 select", 10: "i4 pred", 11: "i4 fwd rows", 12: "i4 fwd cols",
-             13: "i4 quant", 14: "i4 inv cols", 15: "i4 recon+spectral rows", 16: "i4 score+argmin+copy",
-             17: "i4 rotate", 3: "i4 tail", 4: "chroma", 5: "outputs"}
+    names = {0: "prologue", 1: "i16", 2: "i16 select", 10: "i4 A: pred+fwd rows",
+             13: "i4 B: fwd cols+quant+inv cols", 15: "i4 C: recon+sse+spectral rows",
+             16: "i4 D: spectral cols+rate+argmin+copy", 17: "i4 rotate", 3: "i4 tail", 4: "chroma", 5: "outputs"}
     task = {20: "task: ticket+wait+acquire", 21: "task: whole (loop top to loop top)"}
     calls = (args.iters + 1) * 1024  # image 0's MBs per batch (512^2: 32 x 32)
     tot = sum(stamps[i] for i in names)
