@@ -83,8 +83,12 @@ def parse():
     ap.add_argument("--threads", type=int, default=32, help="host threads per GPU (stated budget)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of each cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--webp-encoder", default="libwebp", choices=["libwebp", "exact"],
-                    help="exact: libwebp's method-4 decisions on the GPU (IK_WEBP_EXACT, byte-identical files)")
+    ap.add_argument("--webp-encoder", default="auto", choices=["auto", "libwebp", "exact"],
+                    help="auto (the library default, IK_WEBP_AUTO): a batch's same-geometry groups on the exact GPU "
+                         "coder (libwebp's method-4 decisions on the GPU, byte-identical files); exact: every image "
+                         "on it; libwebp: libwebp on host threads")
+    ap.add_argument("--alt-steps", type=int, default=6,
+                    help="steps of the extra leg with the other WebP coder (0 = skip)")
     ap.add_argument("--no-extras", action="store_true", help="skip the hbm_resident / JPEG legs")
     ap.add_argument("--hbm-batch", type=int, default=64)
     ap.add_argument("--hbm-steps", type=int, default=6)
@@ -354,7 +358,8 @@ def main():
     lib = _lib.load()
     if lib.ik_init(-1 if args.inproc_devices > 0 else local) != 0:
         raise SystemExit(f"ik_init failed: {_lib.last_error()}")
-    if args.webp_encoder == "exact" and lib.ik_set_webp_encoder(2) != 0:
+    WEBP_ENC = {"libwebp": 0, "exact": 2, "auto": 3}
+    if lib.ik_set_webp_encoder(WEBP_ENC[args.webp_encoder]) != 0:
         raise SystemExit(f"ik_set_webp_encoder failed: {_lib.last_error()}")
     dev = f"cuda:{local}"
     # request bodies in page-locked host memory (ik_host_alloc), as a server reads
@@ -473,13 +478,15 @@ def main():
     raw = (S * 4 + 1) * S          # filtered image bytes per frame (filter byte + RGBA row)
     nd = max(1, int(st[9]))        # frames in the timed decode launch
     tok = float(st[12])            # u16 tokens its decode pass wrote
+    # the decoder that ran: the wave decoder (default) or round 4's lane decoder
+    dec_kernel = "k_png_decode" if os.environ.get("IK_PNG_DECODE") == "lane" else "k_png_wave"
     kern = {
         # the files read, the assembled streams (+ padding) written
         "k_png_gather": (png_stages["gather_crc"], nd * 2 * in_bytes),
         # the compressed streams read (every bit offset is examined)
         "k_png_find": (png_stages["find"], nd * in_bytes),
         # compressed stream read, tokens written
-        "k_png_decode": (png_stages["decode"], nd * in_bytes + 2 * tok),
+        dec_kernel: (png_stages["decode"], nd * in_bytes + 2 * tok),
         # tokens read, u16 symbols written
         "k_png_expand": (png_stages["expand"], 2 * tok + nd * 2 * raw),
         "k_png_resolve": (png_stages["resolve"], nd * (2 * raw + 4 * S * S)),
@@ -560,6 +567,8 @@ def main():
             "bytes_basis": (f"SURVEY D-5 per frame: encoded input {in_bytes} + {C}*W*H + {C}*w*h + encoded output "
                             f"{out_bytes} = {d5_frame} B, x {nd if args.source == 'png' else int(bt[3])} frames"),
             "traffic_basis": traffic_basis,
+            # PMC bytes over the launch's algorithmic bytes: > 1 = re-reads and partial lines
+            "traffic_over_bytes": round(traffic_png / dbytes, 3) if traffic_png else None,
             "kernel_stream": {"bytes_per_launch": int(kbytes), "achieved": round(kbytes / (dms * 1e-3) / 1e9, 1),
                               "frac": round(kbytes / (dms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)},
             "note": note}
@@ -578,6 +587,32 @@ def main():
         te = reduce_max(time.perf_counter() - t1, dist, dev)
         pageable = {"value": round(aggregate_mpix(world, B * args.pageable_steps, S, te), 2), "unit": "MPix/s",
                     "steps": args.pageable_steps, "ms_per_step": round(te / args.pageable_steps * 1e3, 3)}
+
+    # the same headline workload with the other WebP coder (byte-identical files): its
+    # rate and the host cores it keeps busy, so both coders are measured in one run
+    alt_coder = {}
+    if args.format == "webp" and args.alt_steps > 0 and args.pipeline:
+        other = "libwebp" if args.webp_encoder != "libwebp" else "exact"
+        lib.ik_set_webp_encoder(WEBP_ENC[other])
+        run_pipelined(args.warmup, rq=dreqs)
+        barrier()
+        ra0 = resource.getrusage(resource.RUSAGE_SELF)
+        t1 = time.perf_counter()
+        ra = run_pipelined(args.alt_steps, rq=dreqs)
+        torch.cuda.synchronize()
+        te = time.perf_counter() - t1
+        ra1 = resource.getrusage(resource.RUSAGE_SELF)
+        cpu_a = (ra1.ru_utime - ra0.ru_utime) + (ra1.ru_stime - ra0.ru_stime)
+        te_max = reduce_max(te, dist, dev)
+        barrier()
+        lib.ik_set_webp_encoder(WEBP_ENC[args.webp_encoder])
+        stage_ms.clear()
+        batch_ms.clear()
+        assert ra is not None and all(magic(r) for r in ra) and ra == res, "the coders' bytes differ"
+        alt_coder = {"webp_encoder": other, "value": round(aggregate_mpix(world, B * args.alt_steps, S, te_max), 2),
+                     "unit": "MPix/s", "steps": args.alt_steps, "ms_per_step": round(te_max / args.alt_steps * 1e3, 3),
+                     "rank0_cores_busy": round(cpu_a / max(te, 1e-9), 2),
+                     "bytes_equal_to_value_leg": True}
 
     # ---- extras: HBM-resident pipeline (old headline) and JPEG-source leg ----
     hbm = {}
@@ -709,8 +744,9 @@ def main():
                  "jpeg": "JPEG q90 4:2:0 without restart markers, in page-locked host memory -> "
                          "ik_transform_batch_submit: decode_image (GPU self-synchronising entropy decoding, IDCT, "
                          "upsampling, colour)"}[args.source] if args.pipeline else "host memory -> ik_transform_batch")
-    coder = {"webp": "libwebp" if args.webp_encoder == "libwebp" else
-             "libwebp method 4 on the GPU (IK_WEBP_EXACT, byte-identical)",
+    coder = {"webp": "libwebp on host threads" if args.webp_encoder == "libwebp" else
+             "libwebp method 4's decisions on the GPU, the exact coder (IK_WEBP_%s, byte-identical)" %
+             args.webp_encoder.upper(),
              "jpeg": "GPU FDCT + Huffman", "avif": "libavif/aom"}[args.format]
     if rank == 0:
         line = {
@@ -738,6 +774,7 @@ def main():
                                 "memory figure is pcie_inclusive.value" if args.pipeline and args.source == "png"
                                 else "encoded inputs in host memory -> encoded outputs in host memory (SURVEY D-1)"),
                 "inproc_devices": args.inproc_devices, "filter": args.filter, "format": args.format, "quality": args.quality,
+                "webp_encoder": args.webp_encoder if args.format == "webp" else None,
                 "host_threads_per_gpu": args.threads, "png_bytes_per_image": in_bytes,
                 "webp_bytes_per_image": out_bytes,
                 "libwebp": "%d.%d.%d" % (lib.ik_libwebp_version() >> 16, (lib.ik_libwebp_version() >> 8) & 255,
@@ -758,6 +795,7 @@ def main():
             "kernels": kernels,
             "pcie_inclusive": pcie,
             "pageable_input": pageable,
+            "webp_coder_alt": alt_coder,
             "hbm_resident": hbm,
             "decode_inclusive_jpeg": jpg,
             "cpu_baseline": cpu,

@@ -215,15 +215,19 @@ int ik_resize_exact(const ik_image *img, uint32_t nw, uint32_t nh, int filter, i
  * *out is allocated by the library; release with ik_buf_free. */
 int ik_encode(const ik_image *img, int fmt, int quality, uint8_t **out, size_t *out_len);
 
-/* WebP coder behind encode_image (src/transform.rs:129-137); both write the bytes of
- * the reference's webp 0.3.1 -> libwebp WebPEncodeRGB.
+/* WebP coder behind encode_image (src/transform.rs:129-137); every choice writes the
+ * bytes of the reference's webp 0.3.1 -> libwebp WebPEncodeRGB.
  * IK_WEBP_LIBWEBP: libwebp's VP8 coder on host threads over device-made YUV420 planes.
  * IK_WEBP_EXACT: libwebp's own method-4 decisions on the GPU (segment analysis, RD mode
  *   search, token statistics: ik_webp_encode_exact_device) and its bitstream on the
  *   host -- the same files, with the coding off the host cores.
- * The process default comes from IK_WEBP_ENCODER=exact|libwebp when first used.
+ * IK_WEBP_AUTO (the default): the exact GPU coder for a batch's same-geometry groups
+ *   and the pipeline API (its chain of macroblock launches costs about as much for 64
+ *   images as for one), libwebp for a lone image (one host core codes a 512^2 image
+ *   in ~8 ms, the GPU chain takes ~18).
+ * The process default comes from IK_WEBP_ENCODER=auto|exact|libwebp when first used.
  * (Value 1, a non-exact GPU VP8 encoder of earlier rounds, is retired: refused.) */
-typedef enum { IK_WEBP_LIBWEBP = 0, IK_WEBP_EXACT = 2 } ik_webp_encoder;
+typedef enum { IK_WEBP_LIBWEBP = 0, IK_WEBP_EXACT = 2, IK_WEBP_AUTO = 3 } ik_webp_encoder;
 int ik_set_webp_encoder(int encoder); /* process-wide, for ik_encode / ik_transform */
 /* version of the libwebp that codes WebP (WebPGetEncoderVersion, e.g. 0x010600),
  * -1 when none could be loaded.  The codec libraries are explicit dependencies:

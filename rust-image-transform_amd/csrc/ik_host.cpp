@@ -1650,13 +1650,13 @@ static void transform_post_phase(const int64_t* w, const int64_t* h, const int* 
                 if (fmt[idx[k]] == IK_FORMAT_WEBP) byq[quality[idx[k]]].push_back(k);
                 if (fmt[idx[k]] == IK_FORMAT_JPEG) jbyq[quality[idx[k]]].push_back(k);
             }
-            const int webp_enc = default_webp_encoder();  // read once for the batch's groups
+            const int webp_enc = default_webp_encoder();  // read once for the batch's groups (AUTO: exact)
             for (auto& qv : byq) {
                 if (qv.second.size() < 2) continue;
                 std::vector<ik_image*> im;
                 std::vector<EncodePrep*> pp;
                 for (uint32_t k : qv.second) { im.push_back(rsz[k]); pp.push_back(&prep[k]); }
-                if (webp_enc == IK_WEBP_EXACT && im[0]->depth == 1 && im[0]->w <= 16383 &&
+                if (webp_enc != IK_WEBP_LIBWEBP && im[0]->depth == 1 && im[0]->w <= 16383 &&
                     im[0]->h <= 16383) {
                     std::vector<std::vector<uint8_t>*> oo;
                     for (uint32_t k : qv.second) oo.push_back(&bytes_out[k]);

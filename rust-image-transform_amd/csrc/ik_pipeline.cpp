@@ -308,7 +308,8 @@ int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t
         return rc;
     }
     *out = p;
-    if (fmt == IK_FORMAT_WEBP && default_webp_encoder() == IK_WEBP_EXACT) return ik_pipeline_set_webp_encoder(p, IK_WEBP_EXACT);
+    if (fmt == IK_FORMAT_WEBP && default_webp_encoder() != IK_WEBP_LIBWEBP)  // (EXACT or AUTO: a batch)
+        return ik_pipeline_set_webp_encoder(p, IK_WEBP_EXACT);
     return IK_OK;
 }
 

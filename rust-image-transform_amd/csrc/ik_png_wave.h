@@ -57,10 +57,7 @@ constexpr int kMinSubBits = 512;        // fewer sub-lanes for shorter ranges
 // stream bits of one window of a block's body (LDS staging): 12 KiB keeps the
 // wave's LDS at ~20 KB (8 waves per CU) at ~8 % more sub-lane steps than a
 // window holding a whole ~18 KB block
-#ifndef IK_PNG_WAVE_WIN_BYTES
-#define IK_PNG_WAVE_WIN_BYTES 12288
-#endif
-constexpr uint64_t kWindowBits = 8ull * IK_PNG_WAVE_WIN_BYTES;
+constexpr uint64_t kWindowBits = 8ull * 12288;
 
 // literal/length entry (u32):
 //   bits 0..4   bits consumed by the entry's symbols (0: slow / invalid)

@@ -223,7 +223,7 @@ void jpeg_huff_u32(uint32_t t[4 * 256]);  // ldc, lac, cdc, cac: code << 8 | siz
 
 // the WebP coder encode_image uses unless ik_set_webp_encoder / IK_WEBP_ENCODER says
 // otherwise (ik_webp_gpu.cpp)
-constexpr int kDefaultWebpEncoder = IK_WEBP_LIBWEBP;
+constexpr int kDefaultWebpEncoder = IK_WEBP_AUTO;
 int default_webp_encoder();
 // the exact coder (ik_vp8x_host.cpp): libwebp's files from n device YUV420 images
 int webp_encode_exact(const uint8_t* d_yuv, size_t yuv_stride, int n, int w, int h, int quality,

@@ -25,7 +25,8 @@ int default_webp_encoder() {
     if (e < 0) {
         const char* s = getenv("IK_WEBP_ENCODER");
         e = (s && (!strcmp(s, "libwebp") || !strcmp(s, "0"))) ? IK_WEBP_LIBWEBP
-            : (s && (!strcmp(s, "exact") || !strcmp(s, "2"))) ? IK_WEBP_EXACT : kDefaultWebpEncoder;
+            : (s && (!strcmp(s, "exact") || !strcmp(s, "2"))) ? IK_WEBP_EXACT
+            : (s && (!strcmp(s, "auto") || !strcmp(s, "3"))) ? IK_WEBP_AUTO : kDefaultWebpEncoder;
         int expected = -1;
         g_webp_encoder.compare_exchange_strong(expected, e);
         e = g_webp_encoder.load();
@@ -40,7 +41,8 @@ using namespace ik;
 extern "C" {
 
 int ik_set_webp_encoder(int encoder) {
-    if (encoder != IK_WEBP_LIBWEBP && encoder != IK_WEBP_EXACT) return fail(IK_ERR_INVALID, "bad WebP encoder %d", encoder);
+    if (encoder != IK_WEBP_LIBWEBP && encoder != IK_WEBP_EXACT && encoder != IK_WEBP_AUTO)
+        return fail(IK_ERR_INVALID, "bad WebP encoder %d", encoder);
     (void)default_webp_encoder();
     g_webp_encoder.store(encoder);
     return IK_OK;

@@ -38,10 +38,12 @@ def test_gpu_encoders_reproduce_codec_golden(ik, oracle, name):
     assert encode_image(d, ImageFormat.webp, q) == G[f"{name}_webp"].tobytes()
     assert encode_image(d, ImageFormat.jpeg, q) == G[f"{name}_jpeg"].tobytes()
     prev = ik.ik_get_webp_encoder()
-    assert ik.ik_set_webp_encoder(2 - prev) == 0  # the other coder
+    got = {}
     try:
-        got = encode_image(d, ImageFormat.webp, q)
+        for enc in (0, 2):  # libwebp, the exact GPU coder (the default AUTO picks libwebp for one image)
+            assert ik.ik_set_webp_encoder(enc) == 0
+            got[enc] = encode_image(d, ImageFormat.webp, q)
     finally:
         assert ik.ik_set_webp_encoder(prev) == 0
-    assert got == G[f"{name}_webp"].tobytes()
+    assert got[0] == G[f"{name}_webp"].tobytes() and got[2] == G[f"{name}_webp"].tobytes()
     assert ik.ik_set_webp_encoder(1) != 0  # the retired non-exact encoder is refused

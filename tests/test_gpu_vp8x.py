@@ -127,11 +127,12 @@ def test_transform_batch_with_the_exact_coder(ik):
     sizes = [(512, None)] * 3 + [(300, 200)]
     fmts = [ImageFormat.webp] * 4
     qs = [80, 80, 80, 50]
-    assert ik.ik_set_webp_encoder(0) == 0
-    ref = transform_batch(datas, sizes, fmts, qs, FilterType.Triangle)
-    assert ik.ik_set_webp_encoder(2) == 0
+    prev = ik.ik_get_webp_encoder()
     try:
+        assert ik.ik_set_webp_encoder(0) == 0
+        ref = transform_batch(datas, sizes, fmts, qs, FilterType.Triangle)
+        assert ik.ik_set_webp_encoder(2) == 0
         got = transform_batch(datas, sizes, fmts, qs, FilterType.Triangle)
     finally:
-        ik.ik_set_webp_encoder(0)
+        ik.ik_set_webp_encoder(prev)
     assert got == ref
