@@ -352,12 +352,13 @@ def test_config1_jpeg_to_webp(ik, oracle):
     assert encode_image(out, ImageFormat.webp, 80) == want
 
 
-# ---- GPU entropy decoding (k_jpeg_huff): baseline scans with restart intervals ----
+# ---- GPU entropy decoding (the self-synchronising ik_jsync.hip path): baseline scans with restart intervals ----
 @pytest.mark.parametrize("wh", [(16, 16), (300, 200), (1023, 767), (17, 9)])
 @pytest.mark.parametrize("sub", [0, 1, 2])
 @pytest.mark.parametrize("rst", [("rows", 1), ("rows", 3), ("blocks", 1), ("blocks", 7)])
 def test_jpeg_restart_intervals_gpu_entropy(ik, wh, sub, rst):
-    """One GPU lane per restart interval; pixels equal libjpeg-turbo's."""
+    """Restart-marked baseline scans through the self-synchronising GPU decoder (ik_jsync.hip: lanes of
+    1,024 bits, interval starts from the unstuffing pass); pixels equal libjpeg-turbo's."""
     w, h = wh
     kw = {"restart_marker_rows" if rst[0] == "rows" else "restart_marker_blocks": rst[1]}
     pat = "N" if (w * h) % 2 else "S"
