@@ -83,7 +83,7 @@ struct ThreadRes {
     std::map<int, hipStream_t> streams, copy_streams, prio_streams;
     std::map<int, hipEvent_t> prio_events;
     std::map<std::pair<int, int>, Arena> dev;  // (device, slot)
-    Arena pinned[10];
+    Arena pinned[11];
     void release() {
         for (auto& kv : streams) (void)hipStreamSynchronize(kv.second);
         for (auto& kv : copy_streams) (void)hipStreamSynchronize(kv.second);
@@ -1341,7 +1341,14 @@ static int decode_one(const uint8_t* bytes, size_t len, ik_image** out, int* fmt
         break;
     }
     case Sniffed::Jpeg: st = decode_jpeg_device(bytes, len, &img); break;
-    case Sniffed::WebP: st = decode_webp(bytes, len, w, h, c, px); break;
+    case Sniffed::WebP:  // lossy on the GPU when it covers the file, else libwebp on the host
+        st = decode_webp_device(bytes, len, &img);
+        if (st == kVp8dHost) {
+            if (webp_decode_mode() == 2)
+                return fail(IK_ERR_TRANSFORM, "IK_WEBP_DECODE=gpu: the GPU WebP decoder leaves this file to libwebp");
+            st = decode_webp(bytes, len, w, h, c, px);
+        }
+        break;
     default:
         return fail(IK_ERR_TRANSFORM, "The image format %s is not supported", format_name(f));
     }

@@ -193,9 +193,11 @@ uint8_t* scratch(size_t bytes);  // per-thread device scratch, valid until the n
 // per-thread, per-device grow-only device arenas for batch work (slot 1: JPEG
 // batch decode, slot 2: PNG batch decode); valid until the next call with that slot
 uint8_t* scratch_slot(int slot, size_t bytes);
-uint8_t* pinned_slot(int slot, size_t bytes);  // per-thread grow-only pinned host arenas (slots 0..9)
+uint8_t* pinned_slot(int slot, size_t bytes);  // per-thread grow-only pinned host arenas (slots 0..10)
 // the exact WebP coder's arenas: its device work area; its constants in, its records out
 constexpr int kScratchExact = 8, kPinnedExactIn = 8, kPinnedExactOut = 9;
+// the WebP (VP8) decoder's: its device work area and its staged file + headers
+constexpr int kScratchVp8d = 9, kPinnedVp8d = 10;
 int copy_h2d_2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,
                 size_t height, hipStream_t s);
 int copy_d2h_2d(uint8_t* dst, size_t dpitch, const uint8_t* src, size_t spitch, size_t width,
@@ -284,6 +286,16 @@ constexpr int kPngTimingFields = 17;  // ik_png_last_timing
 bool host_pinned(const void* p, size_t n);
 bool png_gpu_enabled(size_t raw_bytes);  // IK_PNG_GPU / IK_PNG_GPU_MIN policy
 int decode_webp(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& c, std::vector<uint8_t>& px);
+// WebP lossy ("VP8 ", no alpha, no animation) on the GPU (ik_vp8d_host.cpp + ik_vp8d.hip):
+// the host parses the headers and partition 0, the device decodes the tokens,
+// reconstructs, loop-filters and converts to RGB straight into a new device image.
+// Returns kVp8dHost (nothing recorded) for files it leaves to decode_webp: other
+// WebP kinds, anything its parser finds unusual, data that runs out.
+constexpr int kVp8dHost = -1000;
+int decode_webp_device(const uint8_t* b, size_t n, ik_image** out);
+// IK_WEBP_DECODE (read per call): 0 "host" (libwebp only), 2 "gpu" (a file the GPU
+// path leaves to the host is an error instead: the tests' proof that it ran), 1 otherwise
+int webp_decode_mode();
 
 // JPEG: host entropy decode + GPU reconstruction straight into a new device image
 // (ik_jpeg_decode.cpp + ik_jpeg.hip)
