@@ -293,8 +293,9 @@ int decode_webp(const uint8_t* b, size_t n, uint32_t& w, uint32_t& h, uint32_t& 
 // WebP kinds, anything its parser finds unusual, data that runs out.
 constexpr int kVp8dHost = -1000;
 int decode_webp_device(const uint8_t* b, size_t n, ik_image** out);
-// IK_WEBP_DECODE (read per call): 0 "host" (libwebp only), 2 "gpu" (a file the GPU
-// path leaves to the host is an error instead: the tests' proof that it ran), 1 otherwise
+// IK_WEBP_DECODE (read per call): 0 "host" (libwebp only), 2 "gpu" (every size; a file
+// the GPU path leaves to the host is an error instead: the tests' proof that it ran),
+// 1 otherwise (auto: the GPU path from 3 MPix, where it is faster than libwebp)
 int webp_decode_mode();
 
 // JPEG: host entropy decode + GPU reconstruction straight into a new device image

@@ -1,5 +1,6 @@
 // ik_vp8d_gpu.h -- launchers of the WebP (VP8) decoder's device half (ik_vp8d.hip); the
-// host half (container, frame header, partition 0, driver) is ik_vp8d_host.cpp.
+// host half (container, frame header, partition 0, the token partitions, driver) is
+// ik_vp8d_host.cpp.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -14,21 +15,22 @@ namespace vp8d {
 struct alignas(16) DImg {
     const DFrame* fr;
     const DMB* mbs;
-    const uint8_t* file;  // the file bytes (16-byte aligned, 16 bytes of slack after)
-    int16_t* coef;        // per MB 384 dequantised coefficients (Y 16x16, U 4x16, V 4x16)
-    uint8_t* flags;       // per MB: 1 = some coefficient is non-zero (libwebp !skip)
+    const uint32_t* coef;    // the frame's non-zero coefficients: (value << 16) | position in
+                             // the MB's 384 (Y 16x16, U 4x16, V 4x16; dequantised, Y2 applied)
+    const uint32_t* coef_at; // per MB its first entry; [mb_w * mb_h] = the total
+    const uint8_t* flags;    // per MB: 1 = some coefficient is non-zero (libwebp !skip)
     uint8_t *y, *u, *v;
     uint8_t* top;
-    uint8_t* out;         // the ik_image's pixels (RGB)
-    uint32_t ys, uvs;     // plane pitches
+    uint8_t* out;            // the ik_image's pixels (RGB)
+    uint32_t ys, uvs;        // plane pitches
     uint32_t out_pitch;
-    uint32_t* err;        // set to 1 when a token partition runs out of data
+    uint32_t row0, rows;     // the launch's tickets of this image's MB rows: [row0, row0 + rows)
+    uint32_t* prog;          // per MB row: MBs done (zeroed per launch)
+    uint32_t* err;           // set when a row's wait times out (zeroed per launch)
 };
 
-constexpr int kReconWaves = 8;  // MB rows in flight per image
-
-hipError_t launch_vp8d_tokens(const DImg* imgs, int n, hipStream_t s);
-hipError_t launch_vp8d_recon(const DImg* imgs, int n, hipStream_t s);
+// ticket: zeroed per launch; total_rows: the images' MB rows together
+hipError_t launch_vp8d_recon(const DImg* imgs, int n, uint32_t total_rows, uint32_t* ticket, hipStream_t s);
 hipError_t launch_vp8d_rgb(const DImg* imgs, int n, int max_h, hipStream_t s);
 
 }  // namespace vp8d

@@ -177,3 +177,12 @@ def test_transform_batch_webp_inputs(ik, gpu_only):
     got = transform_batch(datas, sizes, fmts, qs, FilterType.Triangle)
     for i, d in enumerate(datas):
         assert got[i] == transform(d, 320, None, ImageFormat.jpeg, 85, FilterType.Triangle), i
+
+
+def test_auto_policy(ik, monkeypatch):
+    # default (auto): frames from 3 MPix on take the device path, smaller ones libwebp;
+    # either way the pixels are WebPDecodeRGB's
+    monkeypatch.delenv("IK_WEBP_DECODE", raising=False)
+    for w, h in [(2048, 1536), (640, 480)]:
+        img = ikutil.synth(w, h, 3, seed=w, pattern="S")
+        check(wt.encode(img, 80), f"auto {w}x{h}")

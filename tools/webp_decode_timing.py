@@ -24,12 +24,12 @@ def timed(fn, reps):
 
 
 def main():
-    cases = [(512, 512, 80), (1920, 1080, 80), (4096, 4096, 80)]
+    cases = [(512, 512, 80), (1920, 1080, 80), (2560, 1440, 80), (3000, 2000, 80), (4096, 4096, 80)]
     for w, h, q in cases:
         data = wt.encode(ikutil.synth(w, h, 3, seed=1, pattern="S"), q)
         reps = 20 if w * h <= 1 << 21 else 5
         res = {"case": f"{w}x{h} q{q}", "bytes": len(data)}
-        for mode in ("gpu", "host"):
+        for mode in ("gpu", "host", "auto"):
             os.environ["IK_WEBP_DECODE"] = mode
             res[f"{mode}_ms"] = round(timed(lambda: decode_image(data), reps), 3)
         batch = [wt.encode(ikutil.synth(w, h, 3, seed=s, pattern="S"), q) for s in range(16)] if w * h <= 1 << 21 else None
