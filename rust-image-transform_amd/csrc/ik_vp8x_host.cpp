@@ -266,8 +266,10 @@ const XSchedule& exact_schedule(int w, int h, int n) {
     }
     // resident workgroups: the widest diagonal's MBs (every workgroup more would hold
     // LDS and registers that another batch's decode kernels beside the coder lose)
-    static const int mul = getenv("IK_VP8X_GRID_MUL") ? atoi(getenv("IK_VP8X_GRID_MUL")) : 1;
-    sc.grid = (int)std::min<size_t>(std::min(std::max(mul, 1) * widest, 2048), sc.tasks.size());
+    // (IK_VP8X_GRID: a multiple of that, e.g. 0.5 -- dev A/B)
+    static const double mul = getenv("IK_VP8X_GRID") ? atof(getenv("IK_VP8X_GRID")) : 1.0;
+    const int want = std::max(1, (int)(std::max(mul, 0.05) * widest));
+    sc.grid = (int)std::min<size_t>(std::min(want, 2048), sc.tasks.size());
     sc.w = w;
     sc.h = h;
     sc.n = n;
