@@ -113,7 +113,9 @@ __device__ __forceinline__ int idct_pixel(const int16_t* q, int r, int c) {
 // its stores of each MB; the row below starts MB x once the row above has done x + 2.
 __global__ __launch_bounds__(64) void k_vp8d_recon(const DImg* __restrict__ imgs, int n, uint32_t* __restrict__ ticket) {
     __shared__ WaveLds L;
+    __shared__ uint16_t s_tap[10 * 16];  // the predictor taps (a divergent index into them: LDS, not memory)
     const int lane = threadIdx.x;
+    for (int i = lane; i < 10 * 16; i += 64) s_tap[i] = kTap[i >> 4][i & 15];
     uint8_t* const Ry = L.ry + 36;
     uint8_t* const Ru = L.ru + 36;
     uint8_t* const Rv = L.rv + 36;
@@ -152,12 +154,14 @@ __global__ __launch_bounds__(64) void k_vp8d_recon(const DImg* __restrict__ imgs
         const int has_top = mb_y > 0;
         const uint32_t tbase_in = (uint32_t)((mb_y - 1) & 1) * mb_w * 32, tbase_out = (uint32_t)(mb_y & 1) * mb_w * 32;
         uint32_t seen = 0;  // the row above's progress last read
+        // the next MB's first 64 coefficient words, loaded a step ahead (after this
+        // step's publish, so the drain before the flag does not wait for them)
+        uint32_t c0 = coef_at[mb_y * mb_w], c1 = coef_at[mb_y * mb_w + 1];
+        uint32_t e0 = c0 + lane < c1 ? coef[c0 + lane] : ~0u;
         for (int mb_x = 0; mb_x < mb_w; ++mb_x) {
             const int mb = mb_y * mb_w + mb_x;
             const int has_left = mb_x > 0;
             // the MB's coefficients: the first 64 entries load now, under the wait
-            const uint32_t c0 = coef_at[mb], c1 = coef_at[mb + 1];
-            const uint32_t e0 = c0 + lane < c1 ? coef[c0 + lane] : ~0u;
             if (lane < 48) reinterpret_cast<uint4*>(L.coef)[lane] = make_uint4(0, 0, 0, 0);
             const cptr<uint32_t> m = mbw + 6 * mb;
             const uint32_t m0 = m[0], bm0 = m[2], bm1 = m[3], bm2 = m[4], bm3 = m[5];
@@ -253,7 +257,7 @@ __global__ __launch_bounds__(64) void k_vp8d_recon(const DImg* __restrict__ imgs
                         const int nb = 4 * by + bx;
                         const uint8_t* blk = Ry + by * 4 * 32 + bx * 4;
                         const uint32_t bw = (nb >> 2) == 0 ? bm0 : (nb >> 2) == 1 ? bm1 : (nb >> 2) == 2 ? bm2 : bm3;
-                        const uint32_t tap = kTap[(bw >> (8 * (nb & 3))) & 255][px];
+                        const uint32_t tap = s_tap[((bw >> (8 * (nb & 3))) & 255) * 16 + px];
                         const int op = tap >> 12;
                         int p;
                         if (op == 4) {
@@ -330,27 +334,22 @@ __global__ __launch_bounds__(64) void k_vp8d_recon(const DImg* __restrict__ imgs
                         uint8_t* p = lane < 16 ? Fy + lane * 32 : fc + cl * 16;
                         filter_line(p, 1, t_mb, ilevel, hev_t, true);
                     }
+                    // (luma lanes 0-15 and chroma lanes 16-31 on one code path: pointer, pitch and
+                    // edge count per lane, so a phase is not run twice under two masks)
+                    const bool lu = lane < 16;
+                    uint8_t* const rowp = lu ? Fy + lane * 32 : fc + cl * 16;  // this lane's row
+                    uint8_t* const colp = lu ? Fy + lane : fc + cl;             // this lane's column
+                    const int pitch = lu ? 32 : 16, nin = lu ? 4 : 2;           // inner edges: 3 luma, 1 chroma
                     WSYNC();
-                    if (inner && lane < 32) {
-                        if (lane < 16) {
-                            for (int k = 1; k < 4; ++k) filter_line(Fy + lane * 32 + 4 * k, 1, t_in, ilevel, hev_t, false);
-                        } else {
-                            filter_line(fc + cl * 16 + 4, 1, t_in, ilevel, hev_t, false);
-                        }
-                    }
+                    if (inner && lane < 32)
+                        for (int k = 1; k < 4; ++k)
+                            if (k < nin) filter_line(rowp + 4 * k, 1, t_in, ilevel, hev_t, false);
                     WSYNC();
-                    if (has_top && lane < 32) {
-                        if (lane < 16) filter_line(Fy + lane, 32, t_mb, ilevel, hev_t, true);
-                        else filter_line(fc + cl, 16, t_mb, ilevel, hev_t, true);
-                    }
+                    if (has_top && lane < 32) filter_line(colp, pitch, t_mb, ilevel, hev_t, true);
                     WSYNC();
-                    if (inner && lane < 32) {
-                        if (lane < 16) {
-                            for (int k = 1; k < 4; ++k) filter_line(Fy + 4 * k * 32 + lane, 32, t_in, ilevel, hev_t, false);
-                        } else {
-                            filter_line(fc + 4 * 16 + cl, 16, t_in, ilevel, hev_t, false);
-                        }
-                    }
+                    if (inner && lane < 32)
+                        for (int k = 1; k < 4; ++k)
+                            if (k < nin) filter_line(colp + 4 * k * pitch, pitch, t_in, ilevel, hev_t, false);
                 }
                 WSYNC();
                 if (has_top) {  // the MB above's filtered bottom rows
@@ -400,6 +399,11 @@ __global__ __launch_bounds__(64) void k_vp8d_recon(const DImg* __restrict__ imgs
             // publish: every store of this MB step has left (sc1), then the flag
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) __hip_atomic_store(prog + mb_y, (uint32_t)mb_x + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (mb_x + 1 < mb_w) {
+                c0 = c1;
+                c1 = coef_at[mb + 2];
+                e0 = c0 + lane < c1 ? coef[c0 + lane] : ~0u;
+            }
             WSYNC();
         }
     }
