@@ -52,6 +52,11 @@ struct ResizeArgs {
     const unsigned long long* step_mask;  // [nsteps] bit j*A+d: row start+j feeds acc[d]
     const float* step_w;        // [nsteps][R][A] the matching weights (0 elsewhere)
     const int* band_step;       // [NB+1] first step of each band
+    // periodic sweep (k_resize_periodic): step t brings in source rows
+    // R*t + per_base .. +R-1, and output row y takes its taps from steps y .. y+A-1
+    const float* per_w;      // [steps][A*R]: per_w[t][e*R + j] = weight of row j of step t in output t-e
+    const int* per_bands;    // [NBp*2] (oy0, oy1)
+    int per_base, NBp;
     int max_strip_cols;      // max output columns of a strip (LDS table size)
     int max_strip_weights;   // max nox*Tx of a strip (LDS weights size when in LDS)
     float* tmp;        // naive path only: f32 vertical intermediate [n][nh][row_bytes]
@@ -69,6 +74,7 @@ struct ResizePlan {
     bool weights_in_lds = false;
     int flush = 3;        // completed vertical rows staged in LDS per horizontal pass
     int NS = 0, NB = 0;
+    int per_A = 0, per_R = 0;  // periodic geometry (k_resize_periodic); 0 = not periodic
     size_t table_bytes = 0;
     void* dev_tables = nullptr;
     ResizeArgs args{};    // pointers into dev_tables; src/dst/tmp filled per launch
@@ -91,6 +97,10 @@ hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_
                          const uint64_t* src_tab = nullptr, const uint64_t* dst_tab = nullptr);
 // dynamic LDS bytes of the fused kernel
 size_t resize_lds_bytes(const ResizeArgs& a, bool wl, int flush);
+// k_resize_periodic (ik_kernels.hip): whether (A accumulators, R rows per step) has
+// an instance; its band plan aims at kPerTargetWG workgroups, bands >= kPerMinBand rows
+bool periodic_instance(int A, int R);
+constexpr int kPerTargetWG = 4096, kPerMinBand = 32;
 hipError_t launch_webp_yuv420(const uint8_t* src, int w, int h, int C, size_t pitch,
                               size_t img_stride, uint8_t* yuv /* Y, U, V planes per image */,
                               size_t yuv_img_stride, int n, const uint16_t* gamma_to_lin,

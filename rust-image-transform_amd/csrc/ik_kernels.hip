@@ -16,6 +16,8 @@
 // correctly rounded division, Rust round-half-away-from-zero.
 #include "ik_internal.h"
 
+#include <utility>
+
 #pragma clang fp contract(off)
 
 namespace ik {
@@ -138,7 +140,13 @@ __device__ __forceinline__ void horizontal_rows(const ResizeArgs& a, const float
 
 // waves per SIMD to ask the register allocator for (A=8 fits 168 VGPRs at 3)
 template <int A>
-struct FusedOcc { static constexpr int value = A <= 4 ? 4 : (A <= 8 ? 3 : 1); };
+struct FusedOcc {
+#ifdef IK_AB_OCC
+    static constexpr int value = A <= 4 ? 4 : (A <= 8 ? IK_AB_OCC : 1);
+#else
+    static constexpr int value = A <= 4 ? 4 : (A <= 8 ? 3 : 1);
+#endif
+};
 
 // Fused resampler.  Workgroup = (column strip, band of output rows, image).
 // Each lane owns kBytesPerLane consecutive bytes of the strip (the vertical pass
@@ -269,8 +277,13 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
                             if constexpr (FMA) {
                                 acc[d][q] = __builtin_fmaf(p[q], wt, acc[d][q]);
                             } else {
+#ifdef IK_ABL_NOVMATH  // dev ablation: the loads and conversions only
+                                if (d == 0) acc[0][q] = acc[0][q] + p[q];
+                                (void)wt;
+#else
                                 const float prod = p[q] * wt;
                                 acc[d][q] = acc[d][q] + prod;
+#endif
                             }
                         }
                     }
@@ -291,9 +304,15 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
             for (int q = 0; q < kBytesPerLane; ++q) acc[A - 1][q] = 0.0f;
             const int nrows = (next - oy0) % F + 1;
             if (nrows == F || next == oy1 - 1) {
+#ifndef IK_ABL_NOBAR  // dev ablations: without the barriers / the horizontal pass (wrong pixels)
                 __syncthreads();
+#endif
+#ifndef IK_ABL_NOHORZ
                 horizontal_rows<FMA>(a, lds, hw, s_off, next - nrows + 1, nrows, ox0, nox, hq, hox, dst);
+#endif
+#ifndef IK_ABL_NOBAR
                 __syncthreads();
+#endif
             }
             ++next;
         }
@@ -305,6 +324,152 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
         body(k, buf0);
         body(k + 1, buf1);
     }
+}
+
+// Periodic resampler (integer ratio R, every output window inside A steps of R
+// rows; ik_plan.cpp): the vertical pass of k_resize_fused without its step tables.
+// Step t brings in rows R*t + per_base .. +R-1; output row y takes tap e*R + j from
+// row j of step y + e, so each step feeds A open output rows and completes one.
+// The loop is unrolled over G steps (G = A, or 2A for odd A, so that the two-step
+// prefetch ring keeps its parity), which fixes every accumulator's role at compile
+// time: the output that starts at phase u sits in acc[u], and the one that
+// completes at phase u is acc[(u + 1) % A].  No masks, no shifts, no branches in the
+// tap loop; a step's A*R weights come in with a few wide scalar loads.  Bands sweep
+// a whole number of groups (ik_plan.cpp); steps past the band's last row and the
+// first A-1 steps' rows of the band above accumulate rows that are never emitted.
+// The horizontal pass, LDS layout and tile mapping are k_resize_fused's.
+template <typename Fn, int... U>
+__device__ __forceinline__ void unroll_seq(Fn&& f, std::integer_sequence<int, U...>) {
+    (f(std::integral_constant<int, U>()), ...);
+}
+
+template <int A, int R, int F, bool WL>
+__global__ __launch_bounds__(kThreads) void k_resize_periodic(ResizeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int G = A % 2 ? 2 * A : A;
+    const int Gd = (int)gridDim.x;
+    const int h = (int)blockIdx.x;
+    const int per = Gd >> 3, rem = Gd & 7, x = h & 7;
+    const int L = x * per + (x < rem ? x : rem) + (h >> 3);
+    const int tiles = a.NS * a.NBp;
+    const int img = L / tiles;
+    const int tile = L - img * tiles;
+    const int strip = tile % a.NS;
+    const int band = tile / a.NS;
+    const cptr<int> strips = as_const(a.strips);
+    const cptr<int> bands = as_const(a.per_bands);
+    const cptr<float> pw = as_const(a.per_w);
+    const int ox0 = strips[3 * strip], ox1 = strips[3 * strip + 1], sb = strips[3 * strip + 2];
+    const int nox = ox1 - ox0;
+    const int oy0 = bands[2 * band], oy1 = bands[2 * band + 1];
+    const uint8_t* __restrict__ src =
+        a.src_tab ? reinterpret_cast<const uint8_t*>(as_const(a.src_tab)[img]) : a.src + (size_t)img * a.src_img_stride;
+    g_u8* __restrict__ dst = (g_u8*)(a.dst_tab ? reinterpret_cast<uint8_t*>(as_const(a.dst_tab)[img])
+                                               : a.dst + (size_t)img * a.dst_img_stride);
+
+    float* __restrict__ s_w = lds + F * kRowWords;
+    int* __restrict__ s_off = reinterpret_cast<int*>(s_w + (WL ? a.max_strip_weights : 0));
+    for (int t = threadIdx.x; t < nox; t += kThreads) s_off[t] = a.lx[ox0 + t] * a.C - sb;
+    for (int t = threadIdx.x; t < F * kRowWords / 4; t += kThreads)
+        reinterpret_cast<float4*>(lds)[t] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const int hq = (int)threadIdx.x / nox, hox = (int)threadIdx.x - hq * nox;
+    if (WL) {
+        const float* __restrict__ gw = a.wx + (size_t)ox0 * a.Tx;
+        for (int t = threadIdx.x; t < nox * a.Tx; t += kThreads) s_w[t] = gw[t];
+    }
+    const float* __restrict__ hw = WL ? s_w : a.wx + (size_t)ox0 * a.Tx;
+
+    const int mybyte = sb + kBytesPerLane * (int)threadIdx.x;
+    const int voff = mybyte < a.row_bytes ? mybyte : 0;
+    const unsigned long long base = (unsigned long long)src;
+    const unsigned blo = __builtin_amdgcn_readfirstlane((unsigned)base);
+    const unsigned bhi = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((unsigned long long)bhi << 32) | blo), (short)0, (int)(a.src_pitch * a.H), 0x00020000);
+    float* __restrict__ my_lds = lds + lds_idx(kBytesPerLane * (int)threadIdx.x);
+    const int Hm1 = a.H - 1;
+    const int pitch = (int)a.src_pitch;
+    const int rb = a.per_base;
+    auto ld = [&](int row) -> uint2 {
+        row = row < 0 ? 0 : (row < Hm1 ? row : Hm1);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, voff, row * pitch, 0);
+        return make_uint2(v[0], v[1]);
+    };
+
+    float acc[A][kBytesPerLane];
+#pragma unroll
+    for (int d = 0; d < A; ++d)
+#pragma unroll
+        for (int j = 0; j < kBytesPerLane; ++j) acc[d][j] = 0.0f;
+    const int t0 = oy0;
+    const int t1 = t0 + ((oy1 - oy0 + A - 1 + G - 1) / G) * G;
+    uint2 buf0[R], buf1[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) buf0[j] = ld(R * t0 + rb + j);
+#pragma unroll
+    for (int j = 0; j < R; ++j) buf1[j] = ld(R * (t0 + 1) + rb + j);
+    __syncthreads();  // s_w / s_off ready
+
+    auto step = [&](auto UC, int t, uint2 (&cur)[R]) {
+        constexpr int U = decltype(UC)::value % A;
+        // one step's weights live at a time: without this the scheduler pulls the
+        // whole group's scalar loads up front and spills them
+        __builtin_amdgcn_sched_barrier(0);
+        const cptr<float> w = pw + (size_t)t * (A * R);
+        float wv[A * R];
+#pragma unroll
+        for (int i = 0; i < A * R; ++i) wv[i] = w[i];
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const uint2 raw = cur[j];
+            float p[kBytesPerLane];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                p[q] = (float)((raw.x >> (8 * q)) & 0xffu);
+                p[4 + q] = (float)((raw.y >> (8 * q)) & 0xffu);
+            }
+#pragma unroll
+            for (int e = 0; e < A; ++e) {
+                const int slot = (U - e + A) % A;  // the output that started e steps ago
+                const float wt = wv[e * R + j];
+#pragma unroll
+                for (int q = 0; q < kBytesPerLane; ++q) {
+                    const float prod = p[q] * wt;
+                    if (e == 0 && j == 0) acc[slot][q] = prod;  // its first tap
+                    else acc[slot][q] = acc[slot][q] + prod;
+                }
+            }
+            cur[j] = ld(R * (t + 2) + rb + j);  // refill: row j of step t+2
+        }
+        // the step's taps all land before the emit test: otherwise the compiler sinks
+        // part of them into both sides of it and keeps the converted rows live across
+        // (A=2, R=8: 167 VGPRs instead of ~70)
+#pragma unroll
+        for (int d = 0; d < A; ++d)
+            asm volatile("" : "+v"(acc[d][0]), "+v"(acc[d][1]), "+v"(acc[d][2]), "+v"(acc[d][3]), "+v"(acc[d][4]),
+                              "+v"(acc[d][5]), "+v"(acc[d][6]), "+v"(acc[d][7]));
+        const int y = t - (A - 1);  // completed by this step
+        if (y >= oy0 && y < oy1) {
+            constexpr int done = (U + 1) % A;
+            float* o = my_lds + ((y - oy0) % F) * kRowWords;
+            *reinterpret_cast<float4*>(o) = make_float4(acc[done][0], acc[done][1], acc[done][2], acc[done][3]);
+            *reinterpret_cast<float4*>(o + 4) = make_float4(acc[done][4], acc[done][5], acc[done][6], acc[done][7]);
+            const int nrows = (y - oy0) % F + 1;
+            if (nrows == F || y == oy1 - 1) {
+                __syncthreads();
+#ifndef IK_ABL_NOHORZ
+                horizontal_rows<false>(a, lds, hw, s_off, y - nrows + 1, nrows, ox0, nox, hq, hox, dst);
+#endif
+                __syncthreads();
+            }
+        }
+    };
+    for (int t = t0; t < t1; t += G)
+        unroll_seq([&](auto UC) {
+            constexpr int u = decltype(UC)::value;
+            if constexpr (u & 1) step(UC, t + u, buf1);
+            else step(UC, t + u, buf0);
+        }, std::make_integer_sequence<int, G>());
 }
 
 // Fallback vertical pass: one thread per (byte column, output row, image).
@@ -413,6 +578,21 @@ hipError_t launch_u16_to_u8(const uint8_t* src, size_t sp, uint8_t* dst, size_t 
     return hipGetLastError();
 }
 
+#define IK_PERIODIC_INSTANCES(X) X(2, 2) X(2, 4) X(2, 8) X(4, 2) X(4, 4) X(4, 8) X(6, 2) X(6, 4) X(6, 8)
+
+bool periodic_instance(int A, int R) {
+#define IK_PER_HAS(A_, R_) if (A == A_ && R == R_) return true;
+    IK_PERIODIC_INSTANCES(IK_PER_HAS)
+#undef IK_PER_HAS
+    return false;
+}
+
+// IK_RESIZE_PERIODIC=0: periodic geometries on k_resize_fused too (A/B, tests)
+static bool periodic_enabled() {
+    const char* e = getenv("IK_RESIZE_PERIODIC");
+    return !(e && e[0] == '0');
+}
+
 size_t resize_lds_bytes(const ResizeArgs& a, bool wl, int flush) {
     return sizeof(float) * ((size_t)flush * kRowWords + (wl ? (size_t)a.max_strip_weights : 0) +
                             (size_t)a.max_strip_cols);
@@ -424,7 +604,12 @@ size_t resize_lds_bytes(const ResizeArgs& a, bool wl, int flush) {
     X(2, 4, 2) X(2, 4, 3) X(2, 4, 4) X(2, 8, 2) X(2, 8, 3) X(2, 8, 4)       \
     X(4, 4, 2) X(4, 4, 3) X(4, 4, 4) X(4, 8, 2) X(4, 8, 3) X(4, 8, 4)       \
     X(8, 4, 2) X(8, 4, 3) X(8, 4, 4) X(8, 8, 2) X(8, 8, 3) X(8, 8, 4)       \
-    X(16, 4, 2) X(16, 4, 3) X(16, 4, 4)
+    X(16, 4, 2) X(16, 4, 3) X(16, 4, 4) IK_AB_INSTANCES(X)
+#ifdef IK_AB_SLOTS6  // dev A/B builds only
+#define IK_AB_INSTANCES(X) X(6, 8, 2) X(6, 8, 3) X(6, 4, 2) X(6, 4, 3)
+#else
+#define IK_AB_INSTANCES(X)
+#endif
 
 hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_pitch,
                          size_t src_img_stride, uint8_t* dst, size_t dst_pitch,
@@ -441,6 +626,17 @@ hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_
         const bool wl = plan.weights_in_lds;
         const size_t lds = resize_lds_bytes(a, wl, plan.flush);
         const bool fma = resize_mode() == IK_RESIZE_FMA;
+        if (plan.per_A && !fma && plan.flush == 3 && periodic_enabled()) {
+            dim3 pgrid(plan.NS * a.NBp * n);
+#define IK_PLAUNCH(A_, R_)                                                                                    \
+    if (plan.per_A == A_ && plan.per_R == R_) {                                                               \
+        if (wl) hipLaunchKernelGGL((k_resize_periodic<A_, R_, 3, true>), pgrid, dim3(kThreads), lds, s, a);   \
+        else hipLaunchKernelGGL((k_resize_periodic<A_, R_, 3, false>), pgrid, dim3(kThreads), lds, s, a);     \
+        return hipGetLastError();                                                                             \
+    }
+            IK_PERIODIC_INSTANCES(IK_PLAUNCH)
+#undef IK_PLAUNCH
+        }
 #define IK_LAUNCH(A_, R_, F_)                                                                                 \
     if (plan.slots == A_ && plan.rows == R_ && plan.flush == F_) {                                            \
         if (fma) {                                                                                            \

@@ -164,6 +164,9 @@ ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, i
     const int Ty = axis_weights(H, nh, filter, ly, cy, wy);
     int A = required_slots(ly, cy);
     int slots = A <= 2 ? 2 : A <= 4 ? 4 : A <= 8 ? 8 : A <= 16 ? 16 : 0;
+#ifdef IK_AB_SLOTS6  // dev A/B builds only
+    if (A > 4 && A <= 6) slots = 6;
+#endif
 
     // prefetch depth: source rows consumed per output row after the first
     int maxblk = 1;
@@ -176,6 +179,9 @@ ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, i
     // take the kernel's chunked path)
     if (slots <= 8 && rows > 8) rows = 8;
     if (slots == 16) rows = 4;
+#ifdef IK_AB_R4
+    if (slots <= 8) rows = 4;
+#endif
     // column strips: as many output columns as fit kStripBytes source bytes (and,
     // when possible, kMaxStripWeights horizontal weights in LDS)
     bool wl = (long)Tx <= kMaxStripWeights;
@@ -231,7 +237,11 @@ ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, i
     // best on MI355X for both triangle and lanczos3 8x downscales (deeper costs
     // resident workgroups, shallower runs the barrier-bound horizontal pass more
     // often; tools/sweep_resize.py FLUSH=2,3,4)
+#ifdef IK_AB_FLUSH
+    const int flush = IK_AB_FLUSH;
+#else
     const int flush = 3;
+#endif
     const auto key = std::make_tuple(device, W, H, C, nw, nh, filter, band_h, flush);
     std::lock_guard<std::mutex> lk(g_plan_mu);
     auto it = g_plans.find(key);
@@ -287,7 +297,54 @@ ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, i
         band_step.push_back((int)smask.size());
     }
 
+    // Periodic geometry (integer ratio R, every output window inside steps y .. y+A-1
+    // of R rows each, step t starting at source row R*t + base): k_resize_periodic
+    // sweeps it with A accumulators whose roles rotate at compile time -- no step
+    // masks, no accumulator shifts.  Taps outside an output's own window carry weight
+    // 0 (+0 added to the sum, so the f32 sequence of the reference is unchanged; the
+    // first tap is assigned, not added to 0, which can differ only in the sign of a
+    // zero sum and so never in an output byte).
+    int per_A = 0, per_R = 0, per_base = 0;
+    std::vector<float> per_w;
+    std::vector<int> per_bands;
+    if (slots && nh > 0 && H % nh == 0) {
+        const int R = H / nh;
+        int lo = 1 << 30, hi = -(1 << 30);
+        for (int y = 0; y < nh; ++y) {
+            lo = std::min(lo, ly[y] - R * y);
+            hi = std::max(hi, ly[y] + cy[y] - R * y);
+        }
+        const int A = (hi - lo + R - 1) / R;
+        if (periodic_instance(A, R)) {
+            per_A = A; per_R = R; per_base = lo;
+        }
+    }
+    if (per_A) {
+        const int A = per_A, R = per_R, G = A % 2 ? 2 * A : A;  // steps per unrolled group
+        // bands: ~kPerTarget workgroups; a band of h rows sweeps h + A - 1 steps,
+        // rounded up to whole groups (the extra steps emit nothing)
+        long per_img = (kPerTargetWG + n - 1) / n;
+        long nb = std::max(1L, (per_img + NS - 1) / NS);
+        int h = (int)((nh + nb - 1) / nb);
+        h = std::max(h, std::min(nh, kPerMinBand));
+        h = ((h + A - 1 + G - 1) / G) * G - (A - 1);  // h + A - 1 a whole number of groups
+        if (h < 1) h = std::min(nh, G);
+        for (int y = 0; y < nh; y += h) { per_bands.push_back(y); per_bands.push_back(std::min(nh, y + h)); }
+        const int nsteps = nh + A - 1 + G;  // the last band's rounding included
+        per_w.assign((size_t)nsteps * A * R, 0.0f);
+        for (int t = 0; t < nsteps; ++t)
+            for (int e = 0; e < A; ++e) {
+                const int y = t - e;
+                if (y < 0 || y >= nh) continue;
+                for (int j = 0; j < R; ++j) {
+                    const int kk = R * t + per_base + j - ly[y];
+                    if (kk >= 0 && kk < cy[y]) per_w[((size_t)t * A + e) * R + j] = wy[(size_t)y * Ty + kk];
+                }
+            }
+    }
+
     std::vector<char> blob;
+    const size_t o_pw = put(blob, per_w), o_pb = put(blob, per_bands);
     const size_t o_ly = put(blob, ly), o_cy = put(blob, cy), o_wy = put(blob, wy);
     const size_t o_lx = put(blob, lx), o_cx = put(blob, cx), o_wx = put(blob, wx);
     const size_t o_st = put(blob, strips), o_bd = put(blob, bands);
@@ -301,6 +358,8 @@ ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, i
     p->flush = flush;
     p->NS = NS;
     p->NB = (int)bands.size() / 2;
+    p->per_A = per_A;
+    p->per_R = per_R;
     p->table_bytes = blob.size();
     // upload on this thread's stream, synchronised there (copy_h2d_2d): done
     // before any stream launches with the plan, without a device-wide sync
@@ -329,6 +388,10 @@ ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, i
     a.step_mask = (const unsigned long long*)(d + o_sm);
     a.step_w = (const float*)(d + o_sw);
     a.band_step = (const int*)(d + o_bst);
+    a.per_w = (const float*)(d + o_pw);
+    a.per_bands = (const int*)(d + o_pb);
+    a.per_base = per_base;
+    a.NBp = (int)per_bands.size() / 2;
     g_plans[key] = p;
     return p;
 }

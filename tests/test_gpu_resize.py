@@ -100,3 +100,50 @@ def test_resize_image_dims_and_pixels(ik, oracle, wh):
     assert out.dimensions() == (ow, oh)
     want = src if (ow, oh) == (800, 600) else oracle.resize(src, ow, oh, LANCZOS3)
     np.testing.assert_array_equal(out.to_array(), want)
+
+
+# Integer vertical ratios take the periodic kernel (k_resize_periodic: A rotating
+# accumulators, zero-weight taps outside each output's window); the rest of the
+# geometries above keep k_resize_fused.  Both must be bit-exact.
+PERIODIC = [((2048, 1024), (256, 128)), ((1024, 1024), (256, 256)), ((640, 480), (160, 120)),
+            ((96, 64), (48, 32)), ((512, 4096), (64, 512)), ((3000, 2000), (375, 250)),
+            ((37, 64), (37, 8)), ((4096, 256), (512, 32)), ((300, 900), (7, 450)), ((64, 2048), (64, 256))]
+
+
+@pytest.mark.parametrize("geom", PERIODIC, ids=lambda g: f"{g[0][0]}x{g[0][1]}-{g[1][0]}x{g[1][1]}")
+@pytest.mark.parametrize("c", [1, 3, 4])
+@pytest.mark.parametrize("f", FILTERS, ids=lambda f: f.name)
+def test_resize_exact_periodic(ik, oracle, geom, c, f):
+    (W, H), (nw, nh) = geom
+    src = ikutil.synth(W, H, c, seed=W + 3 * H + c, pattern="N" if (W + c) % 2 else "S")
+    got = DynamicImage.from_array(src).resize(nw, nh, f).to_array()
+    np.testing.assert_array_equal(got, oracle.resize(src, nw, nh, int(f)))
+
+
+@pytest.mark.parametrize("periodic", ["1", "0"])
+def test_resize_batch_device_periodic(ik, oracle, monkeypatch, periodic):
+    """A batched launch at an 8x vertical ratio, on the periodic kernel and with it
+    switched off (IK_RESIZE_PERIODIC=0): both bit-exact."""
+    monkeypatch.setenv("IK_RESIZE_PERIODIC", periodic)
+    W, H, C, n, nw, nh = 1000, 704, 4, 3, 125, 88
+    imgs = [ikutil.synth(W, H, C, seed=20 + s, pattern="N" if s % 2 else "S") for s in range(n)]
+    pitch, opitch = 4096, 512
+    src = np.zeros((n, H, pitch), np.uint8)
+    for i, im in enumerate(imgs):
+        src[i, :, :W * C] = im.reshape(H, W * C)
+    d_src, d_dst = ctypes.c_void_p(), ctypes.c_void_p()
+    assert ik.ik_dev_alloc(src.nbytes, ctypes.byref(d_src)) == 0
+    assert ik.ik_dev_alloc(n * nh * opitch, ctypes.byref(d_dst)) == 0
+    try:
+        assert ik.ik_memcpy_h2d(d_src, src.ctypes.data, src.nbytes) == 0
+        for f in (FilterType.Lanczos3, FilterType.Triangle, FilterType.CatmullRom):
+            assert ik.ik_resize_batch_device(d_src, W, H, C, pitch, H * pitch, n, nw, nh, int(f), d_dst, opitch,
+                                             nh * opitch, None) == 0
+            assert ik.ik_dev_synchronize() == 0
+            out = np.zeros((n, nh, opitch), np.uint8)
+            assert ik.ik_memcpy_d2h(out.ctypes.data, d_dst, out.nbytes) == 0
+            for i, im in enumerate(imgs):
+                np.testing.assert_array_equal(out[i, :, :nw * C].reshape(nh, nw, C), oracle.resize(im, nw, nh, int(f)))
+    finally:
+        ik.ik_dev_free(d_src)
+        ik.ik_dev_free(d_dst)
