@@ -44,6 +44,48 @@ __device__ __forceinline__ uint8_t float_nearest_u8(float t) {
     return (uint8_t)roundf(t);
 }
 
+// LDS row layout of the vertical results.  C != 3: strip byte b at word lds_idx(b)
+// (4 pad words per 32).  C == 3: x = b + phi (phi = sb % 3, so x = 0 starts a pixel)
+// at word x + x / 24 -- one pad word per 8 pixels, never inside a pixel, so the
+// horizontal pass reads a pixel's three channels at one address with immediate
+// offsets, and 8-pixel lanes (25 words apart) hit distinct banks.
+struct RowPut {
+    int lo, hi;  // C == 3: word of the lane's first byte; +1 from the pad crossing on
+    int phi;     // C == 3: sb % 3 (wave-uniform); -1: the 4-per-32 layout (lo = lds_idx)
+};
+
+__device__ __forceinline__ RowPut row_put_init(int C, int sb) {
+    RowPut r;
+    const int b0 = kBytesPerLane * (int)threadIdx.x;
+    if (C == 3) {
+        r.phi = sb % 3;
+        const int x0 = b0 + r.phi;
+        r.lo = x0 + ((x0 * 2731) >> 16);  // x0 / 24 for x0 < 2200
+        // only a lane whose bytes start at 16 + phi (mod 24) crosses a pad, at byte 8 - phi
+        r.hi = r.lo + (((b0 % 24) == 16 && r.phi > 0) ? 1 : 0);
+    } else {
+        r.phi = -1;
+        r.lo = r.hi = lds_idx(b0);
+    }
+    return r;
+}
+
+__device__ __forceinline__ void row_put(float* __restrict__ row, const RowPut& r, const float (&v)[kBytesPerLane]) {
+    if (r.phi < 0) {
+        *reinterpret_cast<float4*>(row + r.lo) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(row + r.lo + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else if (r.phi == 0) {
+#pragma unroll
+        for (int i = 0; i < kBytesPerLane; ++i) row[r.lo + i] = v[i];
+    } else if (r.phi == 1) {
+#pragma unroll
+        for (int i = 0; i < kBytesPerLane; ++i) row[(i < 7 ? r.lo : r.hi) + i] = v[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < kBytesPerLane; ++i) row[(i < 6 ? r.lo : r.hi) + i] = v[i];
+    }
+}
+
 // Horizontal pass over `nrows` (<= F) completed vertical rows staged
 // in LDS.  Lane = (row, output column) of the strip, all C channels per lane:
 // one LDS read of C consecutive f32 per tap (ds_read_b128 for RGBA; the 4-per-32
@@ -90,10 +132,13 @@ __device__ __forceinline__ void horizontal_rows_c(const ResizeArgs& a, const flo
                 } else if constexpr (C == 2) {
                     const float2 t2 = *reinterpret_cast<const float2*>(row + lds_idx(idx));
                     t[u][0] = t2.x; t[u][1] = t2.y;
+                } else if constexpr (C == 3) {
+                    // base counts pixels here (row_put's RGB layout: pixel p at 3p + p/8)
+                    const int px = base + k + u;
+                    const float* __restrict__ pp = row + 3 * px + (px >> 3);
+                    t[u][0] = pp[0]; t[u][1] = pp[1]; t[u][2] = pp[2];
                 } else {
-                    // C = 3 / 1: channels may straddle a 32-word pad boundary
-#pragma unroll
-                    for (int c = 0; c < C; ++c) t[u][c] = row[lds_idx(idx + c)];
+                    t[u][0] = row[lds_idx(idx)];
                 }
             }
 #pragma unroll
@@ -197,7 +242,8 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
 
     float* __restrict__ s_w = lds + F * kRowWords;
     int* __restrict__ s_off = reinterpret_cast<int*>(s_w + (WL ? a.max_strip_weights : 0));
-    for (int t = threadIdx.x; t < nox; t += kThreads) s_off[t] = a.lx[ox0 + t] * a.C - sb;
+    for (int t = threadIdx.x; t < nox; t += kThreads)  // byte in the strip (C == 3: pixel, see row_put)
+        s_off[t] = a.C == 3 ? a.lx[ox0 + t] - sb / 3 : a.lx[ox0 + t] * a.C - sb;
     for (int t = threadIdx.x; t < F * kRowWords / 4; t += kThreads)
         reinterpret_cast<float4*>(lds)[t] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const int hq = (int)threadIdx.x / nox, hox = (int)threadIdx.x - hq * nox;
@@ -216,7 +262,7 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
     const unsigned bhi = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(((unsigned long long)bhi << 32) | blo), (short)0, (int)(a.src_pitch * a.H), 0x00020000);
-    float* __restrict__ my_lds = lds + lds_idx(kBytesPerLane * (int)threadIdx.x);
+    const RowPut rput = row_put_init(a.C, sb);
     const int Hm1 = a.H - 1;
     const int pitch = (int)a.src_pitch;
     auto ld = [&](int row) -> uint2 {
@@ -293,9 +339,7 @@ __global__ __launch_bounds__(kThreads, FusedOcc<A>::value) void k_resize_fused(R
         }
         if (hemit) {
             // row `next` complete -> LDS slot, shift the accumulators down
-            float* o = my_lds + ((next - oy0) % F) * kRowWords;
-            *reinterpret_cast<float4*>(o) = make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
-            *reinterpret_cast<float4*>(o + 4) = make_float4(acc[0][4], acc[0][5], acc[0][6], acc[0][7]);
+            row_put(lds + ((next - oy0) % F) * kRowWords, rput, acc[0]);
 #pragma unroll
             for (int d = 0; d + 1 < A; ++d)
 #pragma unroll
@@ -369,7 +413,8 @@ __global__ __launch_bounds__(kThreads) void k_resize_periodic(ResizeArgs a) {
 
     float* __restrict__ s_w = lds + F * kRowWords;
     int* __restrict__ s_off = reinterpret_cast<int*>(s_w + (WL ? a.max_strip_weights : 0));
-    for (int t = threadIdx.x; t < nox; t += kThreads) s_off[t] = a.lx[ox0 + t] * a.C - sb;
+    for (int t = threadIdx.x; t < nox; t += kThreads)  // byte in the strip (C == 3: pixel, see row_put)
+        s_off[t] = a.C == 3 ? a.lx[ox0 + t] - sb / 3 : a.lx[ox0 + t] * a.C - sb;
     for (int t = threadIdx.x; t < F * kRowWords / 4; t += kThreads)
         reinterpret_cast<float4*>(lds)[t] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const int hq = (int)threadIdx.x / nox, hox = (int)threadIdx.x - hq * nox;
@@ -386,7 +431,7 @@ __global__ __launch_bounds__(kThreads) void k_resize_periodic(ResizeArgs a) {
     const unsigned bhi = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(((unsigned long long)bhi << 32) | blo), (short)0, (int)(a.src_pitch * a.H), 0x00020000);
-    float* __restrict__ my_lds = lds + lds_idx(kBytesPerLane * (int)threadIdx.x);
+    const RowPut rput = row_put_init(a.C, sb);
     const int Hm1 = a.H - 1;
     const int pitch = (int)a.src_pitch;
     const int rb = a.per_base;
@@ -451,9 +496,7 @@ __global__ __launch_bounds__(kThreads) void k_resize_periodic(ResizeArgs a) {
         const int y = t - (A - 1);  // completed by this step
         if (y >= oy0 && y < oy1) {
             constexpr int done = (U + 1) % A;
-            float* o = my_lds + ((y - oy0) % F) * kRowWords;
-            *reinterpret_cast<float4*>(o) = make_float4(acc[done][0], acc[done][1], acc[done][2], acc[done][3]);
-            *reinterpret_cast<float4*>(o + 4) = make_float4(acc[done][4], acc[done][5], acc[done][6], acc[done][7]);
+            row_put(lds + ((y - oy0) % F) * kRowWords, rput, acc[done]);
             const int nrows = (y - oy0) % F + 1;
             if (nrows == F || y == oy1 - 1) {
                 __syncthreads();
