@@ -185,13 +185,7 @@ __device__ __forceinline__ void horizontal_rows(const ResizeArgs& a, const float
 
 // waves per SIMD to ask the register allocator for (A=8 fits 168 VGPRs at 3)
 template <int A>
-struct FusedOcc {
-#ifdef IK_AB_OCC
-    static constexpr int value = A <= 4 ? 4 : (A <= 8 ? IK_AB_OCC : 1);
-#else
-    static constexpr int value = A <= 4 ? 4 : (A <= 8 ? 3 : 1);
-#endif
-};
+struct FusedOcc { static constexpr int value = A <= 4 ? 4 : (A <= 8 ? 3 : 1); };
 
 // Fused resampler.  Workgroup = (column strip, band of output rows, image).
 // Each lane owns kBytesPerLane consecutive bytes of the strip (the vertical pass
@@ -499,11 +493,15 @@ __global__ __launch_bounds__(kThreads) void k_resize_periodic(ResizeArgs a) {
             row_put(lds + ((y - oy0) % F) * kRowWords, rput, acc[done]);
             const int nrows = (y - oy0) % F + 1;
             if (nrows == F || y == oy1 - 1) {
+#ifndef IK_ABL_NOBAR  // dev ablations, as in k_resize_fused
                 __syncthreads();
+#endif
 #ifndef IK_ABL_NOHORZ
                 horizontal_rows<false>(a, lds, hw, s_off, y - nrows + 1, nrows, ox0, nox, hq, hox, dst);
 #endif
+#ifndef IK_ABL_NOBAR
                 __syncthreads();
+#endif
             }
         }
     };
@@ -647,12 +645,7 @@ size_t resize_lds_bytes(const ResizeArgs& a, bool wl, int flush) {
     X(2, 4, 2) X(2, 4, 3) X(2, 4, 4) X(2, 8, 2) X(2, 8, 3) X(2, 8, 4)       \
     X(4, 4, 2) X(4, 4, 3) X(4, 4, 4) X(4, 8, 2) X(4, 8, 3) X(4, 8, 4)       \
     X(8, 4, 2) X(8, 4, 3) X(8, 4, 4) X(8, 8, 2) X(8, 8, 3) X(8, 8, 4)       \
-    X(16, 4, 2) X(16, 4, 3) X(16, 4, 4) IK_AB_INSTANCES(X)
-#ifdef IK_AB_SLOTS6  // dev A/B builds only
-#define IK_AB_INSTANCES(X) X(6, 8, 2) X(6, 8, 3) X(6, 4, 2) X(6, 4, 3)
-#else
-#define IK_AB_INSTANCES(X)
-#endif
+    X(16, 4, 2) X(16, 4, 3) X(16, 4, 4)
 
 hipError_t launch_resize(const ResizePlan& plan, const uint8_t* src, size_t src_pitch,
                          size_t src_img_stride, uint8_t* dst, size_t dst_pitch,

@@ -164,9 +164,6 @@ ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, i
     const int Ty = axis_weights(H, nh, filter, ly, cy, wy);
     int A = required_slots(ly, cy);
     int slots = A <= 2 ? 2 : A <= 4 ? 4 : A <= 8 ? 8 : A <= 16 ? 16 : 0;
-#ifdef IK_AB_SLOTS6  // dev A/B builds only
-    if (A > 4 && A <= 6) slots = 6;
-#endif
 
     // prefetch depth: source rows consumed per output row after the first
     int maxblk = 1;
@@ -179,9 +176,6 @@ ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, i
     // take the kernel's chunked path)
     if (slots <= 8 && rows > 8) rows = 8;
     if (slots == 16) rows = 4;
-#ifdef IK_AB_R4
-    if (slots <= 8) rows = 4;
-#endif
     // column strips: as many output columns as fit kStripBytes source bytes (and,
     // when possible, kMaxStripWeights horizontal weights in LDS)
     bool wl = (long)Tx <= kMaxStripWeights;
@@ -237,11 +231,7 @@ ResizePlan* build_resize_plan(int device, int W, int H, int C, int nw, int nh, i
     // best on MI355X for both triangle and lanczos3 8x downscales (deeper costs
     // resident workgroups, shallower runs the barrier-bound horizontal pass more
     // often; tools/sweep_resize.py FLUSH=2,3,4)
-#ifdef IK_AB_FLUSH
-    const int flush = IK_AB_FLUSH;
-#else
     const int flush = 3;
-#endif
     const auto key = std::make_tuple(device, W, H, C, nw, nh, filter, band_h, flush);
     std::lock_guard<std::mutex> lk(g_plan_mu);
     auto it = g_plans.find(key);
