@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 #pragma clang fp contract(off)
 
 constexpr int S = 4096, RB = S * 4, OH = 512, NSTRIP = 9, STRIPB = 2048;
@@ -108,7 +109,14 @@ int main(int argc, char** argv) {
     uint8_t* src;
     float *wt, *out;
     if (hipMalloc(&src, (size_t)nimg * S * RB) != hipSuccess) return 1;
-    (void)hipMemset(src, 0x5a, (size_t)nimg * S * RB);
+    if (argc > 1) {  // random bytes (one frame's worth, copied to every frame)
+        std::vector<uint8_t> h((size_t)S * RB);
+        unsigned x = 12345;
+        for (auto& b : h) { x = x * 1664525u + 1013904223u; b = (uint8_t)(x >> 24); }
+        for (int i = 0; i < nimg; ++i) (void)hipMemcpy(src + (size_t)i * S * RB, h.data(), h.size(), hipMemcpyHostToDevice);
+    } else {
+        (void)hipMemset(src, 0x5a, (size_t)nimg * S * RB);
+    }
     float hw[48];
     for (int i = 0; i < 48; ++i) hw[i] = 0.01f * (i % 7) - 0.013f;
     (void)hipMalloc(&wt, sizeof(hw));
