@@ -380,6 +380,10 @@ def main():
 
     f = FILTERS[args.filter]
 
+    def resize_kernel(C: int) -> str:  # the resampler this geometry takes (k_resize_periodic / _fused / naive)
+        k = lib.ik_resize_kernel_name(S, S, C, O, O, f)
+        return k.decode() if k else "unknown"
+
     # ---- headline: PNG bytes in host memory -> WebP bytes in host memory ----
     stage_ms = []
     NT = 17  # ik_png_last_timing fields
@@ -507,7 +511,7 @@ def main():
     if bt[5] > 0:
         resize_batch = {"bound": "hbm", "achieved": round(bt[6] / (bt[5] * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
                         "unit": "GB/s", "frac": round(bt[6] / (bt[5] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                        "traffic": None, "kernel": "k_resize_fused", "kernel_ms": round(float(bt[5]), 4),
+                        "traffic": None, "kernel": resize_kernel(C), "kernel_ms": round(float(bt[5]), 4),
                         "bytes_per_launch": int(bt[6]), "batch": int(bt[7]),
                         "note": "the grouped resize launch of the measured batches themselves (HIP events on the "
                                 "post stage's stream, beside the next batch's decode kernels); bytes = C*W*H in + "
@@ -674,11 +678,13 @@ def main():
             try:
                 d = json.load(open(pmc))
                 key = f"{args.filter}_{S}_{O}_b{HB}"
-                traffic = d[key]["hbm_bytes_per_launch"] if key in d else None
+                # quoted only when collected on the kernel this geometry takes now
+                if key in d and d[key].get("kernel", "k_resize_fused") == resize_kernel(4):
+                    traffic = d[key]["hbm_bytes_per_launch"]
             except Exception:
                 traffic = None
         roof_resize = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                       "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "kernel": "k_resize_fused",
+                       "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "kernel": resize_kernel(4),
                        "kernel_ms": round(float(kmm[0]), 4), "bytes_per_launch": rb, "batch": HB}
         del src
         torch.cuda.empty_cache()
@@ -730,7 +736,7 @@ def main():
         rb = B * C * (S * S + O * O)
         roof_resize = {"bound": "hbm", "achieved": round(rb / (rms_med * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
                        "unit": "GB/s", "frac": round(rb / (rms_med * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
-                       "kernel": "k_resize_fused", "kernel_ms": round(rms_med, 4), "bytes_per_launch": rb, "batch": B,
+                       "kernel": resize_kernel(C), "kernel_ms": round(rms_med, 4), "bytes_per_launch": rb, "batch": B,
                        "note": f"the resize kernel alone (ik_resize_batch_device, {C} channels, the batch's "
                                f"geometry and filter), HIP events on its stream, median of 3 launches"}
         del src, dstt

@@ -196,6 +196,11 @@ int ik_resize(ik_image *img, int64_t w, int64_t h, int filter, ik_image **out);
 typedef enum { IK_RESIZE_EXACT = 0, IK_RESIZE_FMA = 1 } ik_resize_mode;
 int ik_set_resize_mode(int mode);
 int ik_get_resize_mode(void);
+/* The resampler kernel a launch of this geometry takes under the current modes
+ * (for profiles and benchmarks): "k_resize_periodic" (integer vertical ratios),
+ * "k_resize_fused", or "k_vert_naive" (the two-pass fallback); NULL on bad
+ * arguments or without a device. */
+const char *ik_resize_kernel_name(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t nh, int filter);
 
 /* JPEG reconstruction behind decode_image (src/transform.rs:31 -> image 0.25.8
  * -> zune-jpeg 0.4.21, Cargo.lock:3106).  IK_JPEG_RECON_ZUNE (default): zune-jpeg's

@@ -2309,6 +2309,12 @@ int ik_resize_batch_device(const uint8_t* dev_src, uint32_t W, uint32_t H, uint3
     return IK_OK;
 }
 
+const char* ik_resize_kernel_name(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t nh, int filter) {
+    if (C < 1 || C > 4 || !W || !H || !nw || !nh || filter < 0 || filter > 4) return nullptr;
+    ResizePlan* plan = get_resize_plan(current_device(), (int)W, (int)H, (int)C, (int)nw, (int)nh, filter, 1);
+    return plan ? resize_kernel_name(*plan, (size_t)W * C) : nullptr;
+}
+
 int ik_webp_yuv420_device(const uint8_t* dev_src, uint32_t w, uint32_t h, uint32_t C, size_t pitch,
                           uint8_t* dev_yuv, void* hip_stream) {
     IK_API_ENTER();

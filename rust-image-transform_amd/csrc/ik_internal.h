@@ -100,6 +100,8 @@ size_t resize_lds_bytes(const ResizeArgs& a, bool wl, int flush);
 // k_resize_periodic (ik_kernels.hip): whether (A accumulators, R rows per step) has
 // an instance; its band plan aims at kPerTargetWG workgroups, bands >= kPerMinBand rows
 bool periodic_instance(int A, int R);
+// the kernel launch_resize picks for this plan (ik_resize_kernel_name)
+const char* resize_kernel_name(const ResizePlan& plan, size_t src_pitch);
 constexpr int kPerTargetWG = 4096, kPerMinBand = 32;
 hipError_t launch_webp_yuv420(const uint8_t* src, int w, int h, int C, size_t pitch,
                               size_t img_stride, uint8_t* yuv /* Y, U, V planes per image */,

@@ -634,6 +634,14 @@ static bool periodic_enabled() {
     return !(e && e[0] == '0');
 }
 
+const char* resize_kernel_name(const ResizePlan& plan, size_t src_pitch) {
+    if (!(plan.slots > 0 && resize_fused_fits(src_pitch, (size_t)plan.H))) return "k_vert_naive";
+    if (plan.per_A && resize_mode() != IK_RESIZE_FMA && plan.flush == 3 && periodic_enabled() &&
+        periodic_instance(plan.per_A, plan.per_R))
+        return "k_resize_periodic";
+    return "k_resize_fused";
+}
+
 size_t resize_lds_bytes(const ResizeArgs& a, bool wl, int flush) {
     return sizeof(float) * ((size_t)flush * kRowWords + (wl ? (size_t)a.max_strip_weights : 0) +
                             (size_t)a.max_strip_cols);

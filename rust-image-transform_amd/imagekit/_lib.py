@@ -73,6 +73,7 @@ SIGNATURES = [
     ("ik_png_counters", ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
     ("ik_jpeg_counters", ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong)]),
     ("ik_get_resize_mode", ctypes.c_int, []),
+    ("ik_resize_kernel_name", ctypes.c_char_p, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]),
     ("ik_set_jpeg_reconstruction", ctypes.c_int, [ctypes.c_int]),
     ("ik_get_jpeg_reconstruction", ctypes.c_int, []),
     ("ik_pipeline_submit", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint32]),

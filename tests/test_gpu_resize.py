@@ -147,3 +147,15 @@ def test_resize_batch_device_periodic(ik, oracle, monkeypatch, periodic):
     finally:
         ik.ik_dev_free(d_src)
         ik.ik_dev_free(d_dst)
+
+
+def test_resize_kernel_name(ik, monkeypatch):
+    """ik_resize_kernel_name reports the kernel launch_resize picks."""
+    name = lambda *g: ik.ik_resize_kernel_name(*g).decode()  # noqa: E731
+    assert name(4096, 4096, 4, 512, 512, LANCZOS3) == "k_resize_periodic"
+    assert name(4096, 4096, 3, 512, 512, int(FilterType.Triangle)) == "k_resize_periodic"
+    assert name(2000, 2000, 3, 431, 431, LANCZOS3) == "k_resize_fused"
+    assert name(4096, 4096, 4, 512, 512, int(FilterType.Nearest)) == "k_resize_fused"
+    monkeypatch.setenv("IK_RESIZE_PERIODIC", "0")
+    assert name(4096, 4096, 4, 512, 512, LANCZOS3) == "k_resize_fused"
+    assert ik.ik_resize_kernel_name(0, 1, 4, 1, 1, 1) is None

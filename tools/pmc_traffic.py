@@ -5,7 +5,8 @@ count) as MI355X_MICROARCH.md's HBM section prescribes.
 
 usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR CALIB_DIR KEY BATCH S O [FIRST COUNT]
 (FIRST/COUNT select the dispatches of one configuration, e.g. bench.py's main filter
- = the first warmup+steps launches, its alt filter = the rest)
+ = the first warmup+steps launches, its alt filter = the rest).  IK_PMC_KERNEL names the
+kernel (default k_resize_fused; k_resize_periodic for integer ratios); it is recorded.
 """
 import csv, json, os, sys
 
@@ -22,8 +23,9 @@ def main():
     fdir, wdir, cdir, key, B, S, O = sys.argv[1:8]
     first, count = (int(sys.argv[8]), int(sys.argv[9])) if len(sys.argv) > 9 else (0, None)
     B, S, O = int(B), int(S), int(O)
-    fetch_kb, nf = per_dispatch(fdir, "FETCH_SIZE", "k_resize_fused", first, count)
-    write_kb, nw = per_dispatch(wdir, "WRITE_SIZE", "k_resize_fused", first, count)
+    kname = os.environ.get("IK_PMC_KERNEL", "k_resize_fused")
+    fetch_kb, nf = per_dispatch(fdir, "FETCH_SIZE", kname, first, count)
+    write_kb, nw = per_dispatch(wdir, "WRITE_SIZE", kname, first, count)
     cal_kb, nc = per_dispatch(cdir, "FETCH_SIZE", "k_strip")
     known = 32 * 4096 * 4096 * 4  # tools/bw_probe.py: 32 images of 4096^2 RGBA8 (fixed), each byte read once
     calib = known / (cal_kb * 1024.0)
@@ -34,6 +36,7 @@ def main():
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_resize.json")
     d = json.load(open(out_path)) if os.path.exists(out_path) else {}
     d[key] = {
+        "kernel": kname,
         "hbm_bytes_per_launch": int(fetch + write),
         "fetch_bytes_corrected": int(fetch), "write_bytes": int(write),
         "fetch_size_kb_raw": fetch_kb, "write_size_kb_raw": write_kb,
