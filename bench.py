@@ -511,7 +511,7 @@ def main():
     if bt[5] > 0:
         resize_batch = {"bound": "hbm", "achieved": round(bt[6] / (bt[5] * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
                         "unit": "GB/s", "frac": round(bt[6] / (bt[5] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                        "traffic": None, "kernel": resize_kernel(C), "kernel_ms": round(float(bt[5]), 4),
+                        "traffic": None, "kernel": resize_kernel(3 if args.source != "png" else 4), "kernel_ms": round(float(bt[5]), 4),
                         "bytes_per_launch": int(bt[6]), "batch": int(bt[7]),
                         "note": "the grouped resize launch of the measured batches themselves (HIP events on the "
                                 "post stage's stream, beside the next batch's decode kernels); bytes = C*W*H in + "
