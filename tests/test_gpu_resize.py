@@ -107,7 +107,8 @@ def test_resize_image_dims_and_pixels(ik, oracle, wh):
 # geometries above keep k_resize_fused.  Both must be bit-exact.
 PERIODIC = [((2048, 1024), (256, 128)), ((1024, 1024), (256, 256)), ((640, 480), (160, 120)),
             ((96, 64), (48, 32)), ((512, 4096), (64, 512)), ((3000, 2000), (375, 250)),
-            ((37, 64), (37, 8)), ((4096, 256), (512, 32)), ((300, 900), (7, 450)), ((64, 2048), (64, 256))]
+            ((37, 64), (37, 8)), ((4096, 256), (512, 32)), ((300, 900), (7, 450)), ((64, 2048), (64, 256)),
+            ((8, 8), (4, 4)), ((3, 16), (3, 2)), ((5, 12), (5, 3)), ((10, 6), (5, 3)), ((7, 64), (9, 16))]
 
 
 @pytest.mark.parametrize("geom", PERIODIC, ids=lambda g: f"{g[0][0]}x{g[0][1]}-{g[1][0]}x{g[1][1]}")
