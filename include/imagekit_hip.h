@@ -227,9 +227,9 @@ int ik_encode(const ik_image *img, int fmt, int quality, uint8_t **out, size_t *
  *   search, token statistics: ik_webp_encode_exact_device) and its bitstream on the
  *   host -- the same files, with the coding off the host cores.
  * IK_WEBP_AUTO (the default): the exact GPU coder for a batch's same-geometry groups
- *   and the pipeline API (its chain of macroblock launches costs about as much for 64
- *   images as for one), libwebp for a lone image (one host core codes a 512^2 image
- *   in ~8 ms, the GPU chain takes ~18).
+ *   of 32 or more images and the pipeline API (its chain of macroblock steps costs
+ *   about as much for 64 images as for one), libwebp for smaller groups and lone
+ *   images (one host core codes a 512^2 image in ~8 ms, the GPU chain takes ~18).
  * The process default comes from IK_WEBP_ENCODER=auto|exact|libwebp when first used.
  * (Value 1, a non-exact GPU VP8 encoder of earlier rounds, is retired: refused.) */
 typedef enum { IK_WEBP_LIBWEBP = 0, IK_WEBP_EXACT = 2, IK_WEBP_AUTO = 3 } ik_webp_encoder;

@@ -1604,6 +1604,9 @@ static void transform_decode_phase(const uint8_t* const* bytes, const size_t* le
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tg1).count());
 }
 
+// IK_WEBP_AUTO: smallest same-geometry group that the exact GPU coder takes
+constexpr size_t kAutoExactMinGroup = 32;
+
 // Device half, post stage: resize, the encoders' device front ends (under the
 // post gate, so a batch's resize runs beside the next batch's decode kernels);
 // request i's status / message land in st[i] / errs[i]
@@ -1663,8 +1666,13 @@ static void transform_post_phase(const int64_t* w, const int64_t* h, const int* 
                 std::vector<ik_image*> im;
                 std::vector<EncodePrep*> pp;
                 for (uint32_t k : qv.second) { im.push_back(rsz[k]); pp.push_back(&prep[k]); }
-                if (webp_enc != IK_WEBP_LIBWEBP && im[0]->depth == 1 && im[0]->w <= 16383 &&
-                    im[0]->h <= 16383) {
+                // AUTO: the GPU coder from kAutoExactMinGroup frames of one geometry on (its
+                // chain of macroblock steps costs about the same for 2 frames as for 64; a
+                // mixed-size stream's small groups code faster on the host threads:
+                // configs[3]'s loadtest 2,106 vs 1,224 requests/s)
+                const bool exact = webp_enc == IK_WEBP_EXACT ||
+                                   (webp_enc == IK_WEBP_AUTO && qv.second.size() >= kAutoExactMinGroup);
+                if (exact && im[0]->depth == 1 && im[0]->w <= 16383 && im[0]->h <= 16383) {
                     std::vector<std::vector<uint8_t>*> oo;
                     for (uint32_t k : qv.second) oo.push_back(&bytes_out[k]);
                     if (webp_exact_group(im, qv.first, oo) == IK_OK)
