@@ -227,7 +227,7 @@ int ik_encode(const ik_image *img, int fmt, int quality, uint8_t **out, size_t *
  *   search, token statistics: ik_webp_encode_exact_device) and its bitstream on the
  *   host -- the same files, with the coding off the host cores.
  * IK_WEBP_AUTO (the default): the exact GPU coder for a batch's same-geometry groups
- *   of 32 or more images and the pipeline API (its chain of macroblock steps costs
+ *   of 32 or more images and pipelines of max_batch >= 32 (its chain of macroblock steps costs
  *   about as much for 64 images as for one), libwebp for smaller groups and lone
  *   images (one host core codes a 512^2 image in ~8 ms, the GPU chain takes ~18).
  * The process default comes from IK_WEBP_ENCODER=auto|exact|libwebp when first used.

@@ -308,7 +308,10 @@ int ik_pipeline_create(uint32_t W, uint32_t H, uint32_t C, uint32_t nw, uint32_t
         return rc;
     }
     *out = p;
-    if (fmt == IK_FORMAT_WEBP && default_webp_encoder() != IK_WEBP_LIBWEBP)  // (EXACT or AUTO: a batch)
+    // EXACT, or AUTO with batches of 32+ frames (the rule of a batch's same-geometry
+    // groups, ik_host.cpp kAutoExactMinGroup)
+    const int enc = default_webp_encoder();
+    if (fmt == IK_FORMAT_WEBP && (enc == IK_WEBP_EXACT || (enc == IK_WEBP_AUTO && max_batch >= 32)))
         return ik_pipeline_set_webp_encoder(p, IK_WEBP_EXACT);
     return IK_OK;
 }
